@@ -1,0 +1,1835 @@
+/*
+ * ymerge_oracle.c -- CPU restatement of yjs's binary update layer.  TEST INFRASTRUCTURE ONLY: this file
+ * is the parity checker and the cpu_baseline "port"; it is never linked into the product library.
+ *
+ * Follows, function by function (citations into /root/reference = gaberogan/yjs@v0 = yjs 13.4.9, and
+ * into the yjs 13.5.16 JupyterLab bundle 3502.fbe0c610be82ba1360db.js "@offset", lib0 0.2.42 bundle
+ * 8086.1dfabaac37d971e2cc4c.js "lib0@offset"):
+ *   lib0 readVarUint/readVarInt/readVarString/readAny ........ lib0@2950-4300 (module 64485 U,T,E,B)
+ *   lib0 writeVarUint/writeVarInt/writeVarString/writeAny .... lib0@7400-9300 (module 29194 x,I,j,G)
+ *   lib0 Rle/UintOptRle/IntDiffOptRle/String en-/decoders .... lib0@4300-5600, 9300-10300
+ *   UpdateDecoderV1/V2, DSDecoderV1/V2 ....................... src/utils/UpdateDecoder.js:127-392
+ *   UpdateEncoderV1/V2, DSEncoderV1/V2 ....................... src/utils/UpdateEncoder.js:110-408
+ *   Item.write / GC.write / Content*.write / read*  .......... src/structs/Item.js:625-683, GC.js:45-48,
+ *                                                              Content{String,Deleted,JSON,Binary,Any,
+ *                                                              Embed,Format,Type,Doc}.js; 13.5.16 @78000+
+ *   ContentString.splice (U+FFFD rule) ....................... src/structs/ContentString.js:51-66
+ *   readDeleteSet / writeDeleteSet / mergeDeleteSets ......... src/utils/DeleteSet.js:141-256; 13.5.16
+ *                                                              le@10242 he@10482 fe@11101 ge@11342
+ *   LazyStructReader (ts/es) ................................. 13.5.16 @36560, @37148
+ *   sliceStruct (as) ......................................... 13.5.16 @38661
+ *   mergeUpdatesV2 (ds) ...................................... 13.5.16 @39007
+ *   diffUpdateV2 (us) ........................................ 13.5.16 @40707
+ *   LazyStructWriter write/flush/finish (ps/gs/ws) ........... 13.5.16 @41236-41700
+ *   encodeStateVectorFromUpdateV2 (os) ....................... 13.5.16 @37724
+ *   decodeStateVector (Fe/Ve) ................................ src/utils/encoding.js:536-565
+ * The per-iteration reader sort of mergeUpdates emulates V8's Array.prototype.sort (TimSort: run
+ * detection + binary insertion for < 64 readers); for >= 64 readers a stable merge sort is used, which
+ * is exact whenever the comparator is consistent (it is not when a GC and an Item tie on (client,clock);
+ * such inputs with >= 64 readers report YMO_ERR_UNSUPPORTED).
+ * JS values: numbers are IEEE doubles, strings are UTF-16 code-unit arrays, object property order
+ * follows OrdinaryOwnPropertyKeys (array-index keys ascending, then insertion order).
+ */
+#define _GNU_SOURCE
+#include "ymerge_oracle.h"
+#include <math.h>
+#include <pthread.h>
+#include <setjmp.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------------------------------ */
+/* arena + error context                                                                           */
+/* ------------------------------------------------------------------------------------------------ */
+typedef struct Chunk { struct Chunk *next; size_t cap, used; } Chunk;
+typedef struct Ctx {
+  jmp_buf jb;
+  Chunk *chunks;
+  int v2;
+  int inconsistent_cmp; /* a GC/Item tie was compared during a reader sort */
+  int big_inconsistent; /* ... during a sort of >= 64 readers (emulated by a merge sort) */
+} Ctx;
+
+static void ctx_free(Ctx *c) {
+  Chunk *k = c->chunks;
+  while (k) { Chunk *n = k->next; free(k); k = n; }
+  c->chunks = NULL;
+}
+
+static void __attribute__((noreturn)) fail(Ctx *c, int code) { longjmp(c->jb, code); }
+
+static void *aalloc(Ctx *c, size_t n) {
+  n = (n + 15) & ~(size_t)15;
+  Chunk *k = c->chunks;
+  if (!k || k->cap - k->used < n) {
+    size_t cap = n + sizeof(Chunk) + 15 > (1u << 20) ? n + sizeof(Chunk) + 16 : (1u << 20);
+    Chunk *nk = (Chunk *)malloc(cap);
+    if (!nk) fail(c, YMO_ERR_UNSUPPORTED);
+    nk->cap = cap;
+    nk->used = (sizeof(Chunk) + 15) & ~(size_t)15;
+    nk->next = c->chunks;
+    c->chunks = nk;
+    k = nk;
+  }
+  void *p = (char *)k + k->used;
+  k->used += n;
+  return p;
+}
+
+/* growable byte buffer (lib0 Encoder) */
+typedef struct { uint8_t *p; size_t n, cap; } Buf;
+static Buf *buf_new(Ctx *c) {
+  Buf *b = (Buf *)aalloc(c, sizeof(Buf));
+  b->cap = 64; b->n = 0; b->p = (uint8_t *)aalloc(c, b->cap);
+  return b;
+}
+static void buf_reserve(Ctx *c, Buf *b, size_t extra) {
+  if (b->n + extra <= b->cap) return;
+  size_t cap = b->cap * 2;
+  while (cap < b->n + extra) cap *= 2;
+  uint8_t *np = (uint8_t *)aalloc(c, cap);
+  memcpy(np, b->p, b->n);
+  b->p = np; b->cap = cap;
+}
+static void put8(Ctx *c, Buf *b, unsigned v) { buf_reserve(c, b, 1); b->p[b->n++] = (uint8_t)v; }
+static void putraw(Ctx *c, Buf *b, const uint8_t *p, size_t n) {
+  if (!n) return;
+  buf_reserve(c, b, n); memcpy(b->p + b->n, p, n); b->n += n;
+}
+
+/* JS strings: UTF-16 code units */
+typedef struct { const uint16_t *u; size_t n; } Str;
+static int str_eq(Str a, Str b) { return a.n == b.n && (a.n == 0 || memcmp(a.u, b.u, a.n * 2) == 0); }
+static Str str_slice(Str s, int64_t a, int64_t b) { /* String.prototype.slice with non-negative args */
+  if (a > (int64_t)s.n) a = (int64_t)s.n;
+  if (b > (int64_t)s.n) b = (int64_t)s.n;
+  if (b < a) b = a;
+  Str r = {s.u + a, (size_t)(b - a)};
+  return r;
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* JS number helpers                                                                               */
+/* ------------------------------------------------------------------------------------------------ */
+static uint32_t js_touint32(double v) {
+  if (!isfinite(v) || v == 0) return 0;
+  double t = trunc(v);
+  double m = fmod(t, 4294967296.0);
+  if (m < 0) m += 4294967296.0;
+  return (uint32_t)m;
+}
+static int32_t js_toint32(double v) { return (int32_t)js_touint32(v); }
+static int js_is_negzero_or_neg(double v) { return v != 0 ? v < 0 : signbit(v) != 0; } /* math.isNegativeZero */
+
+/* ------------------------------------------------------------------------------------------------ */
+/* UTF-8 <-> UTF-16 (decodeURIComponent(escape(..)) / unescape(encodeURIComponent(..)))             */
+/* ------------------------------------------------------------------------------------------------ */
+static Str utf8_decode_strict(Ctx *c, const uint8_t *p, size_t n) {
+  uint16_t *u = (uint16_t *)aalloc(c, n * 2 + 2);
+  size_t k = 0, i = 0;
+  while (i < n) {
+    uint32_t b = p[i];
+    if (b < 0x80) { u[k++] = (uint16_t)b; i++; continue; }
+    int len;
+    uint32_t cp, min;
+    if ((b & 0xE0) == 0xC0) { len = 2; cp = b & 0x1F; min = 0x80; }
+    else if ((b & 0xF0) == 0xE0) { len = 3; cp = b & 0x0F; min = 0x800; }
+    else if ((b & 0xF8) == 0xF0) { len = 4; cp = b & 0x07; min = 0x10000; }
+    else fail(c, YMO_ERR_URI);
+    if (i + len > n) fail(c, YMO_ERR_URI);
+    for (int j = 1; j < len; j++) {
+      uint32_t cb = p[i + j];
+      if ((cb & 0xC0) != 0x80) fail(c, YMO_ERR_URI);
+      cp = (cp << 6) | (cb & 0x3F);
+    }
+    if (cp < min || cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF)) fail(c, YMO_ERR_URI);
+    if (cp >= 0x10000) {
+      cp -= 0x10000;
+      u[k++] = (uint16_t)(0xD800 + (cp >> 10));
+      u[k++] = (uint16_t)(0xDC00 + (cp & 0x3FF));
+    } else {
+      u[k++] = (uint16_t)cp;
+    }
+    i += len;
+  }
+  Str r = {u, k};
+  return r;
+}
+
+/* UTF-16 -> UTF-8 into b; URIError on lone surrogates */
+static void utf8_encode(Ctx *c, Buf *b, Str s) {
+  buf_reserve(c, b, s.n * 3 + 4);
+  for (size_t i = 0; i < s.n; i++) {
+    uint32_t cu = s.u[i];
+    if (cu < 0x80) { b->p[b->n++] = (uint8_t)cu; continue; }
+    if (cu < 0x800) { b->p[b->n++] = (uint8_t)(0xC0 | (cu >> 6)); b->p[b->n++] = (uint8_t)(0x80 | (cu & 0x3F)); continue; }
+    if (cu >= 0xD800 && cu <= 0xDBFF) {
+      if (i + 1 >= s.n || s.u[i + 1] < 0xDC00 || s.u[i + 1] > 0xDFFF) fail(c, YMO_ERR_URI);
+      uint32_t cp = 0x10000 + ((cu - 0xD800) << 10) + (s.u[i + 1] - 0xDC00);
+      i++;
+      buf_reserve(c, b, 4 + (s.n - i) * 3);
+      b->p[b->n++] = (uint8_t)(0xF0 | (cp >> 18));
+      b->p[b->n++] = (uint8_t)(0x80 | ((cp >> 12) & 0x3F));
+      b->p[b->n++] = (uint8_t)(0x80 | ((cp >> 6) & 0x3F));
+      b->p[b->n++] = (uint8_t)(0x80 | (cp & 0x3F));
+      continue;
+    }
+    if (cu >= 0xDC00 && cu <= 0xDFFF) fail(c, YMO_ERR_URI);
+    b->p[b->n++] = (uint8_t)(0xE0 | (cu >> 12));
+    b->p[b->n++] = (uint8_t)(0x80 | ((cu >> 6) & 0x3F));
+    b->p[b->n++] = (uint8_t)(0x80 | (cu & 0x3F));
+  }
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* lib0 decoding (module 64485)                                                                    */
+/* ------------------------------------------------------------------------------------------------ */
+typedef struct { const uint8_t *a; size_t len; size_t pos; } Dec;
+/* readUint8: t.arr[t.pos++]; -1 stands for `undefined` past the end */
+static inline int dbyte(Dec *d) { size_t p = d->pos++; return p < d->len ? d->a[p] : -1; }
+static inline int dhas(Dec *d) { return d->pos != d->len; } /* hasContent */
+
+static uint32_t rd_vu(Ctx *c, Dec *d) { /* readVarUint (U) */
+  uint32_t s = 0;
+  unsigned n = 0;
+  for (;;) {
+    int e = dbyte(d);
+    uint32_t bits = e < 0 ? 0u : (uint32_t)(e & 127);
+    s |= bits << (n & 31);
+    n += 7;
+    if (e >= 0 && e < 128) return s;
+    if (n > 35) fail(c, YMO_ERR_INT_RANGE);
+  }
+}
+
+static double rd_vi(Ctx *c, Dec *d) { /* readVarInt (T), returns a JS number incl. -0 */
+  int s = dbyte(d);
+  uint32_t sb = s < 0 ? 0u : (uint32_t)s;
+  uint32_t n = sb & 63;
+  unsigned e = 6;
+  double sign = (sb & 64) ? -1.0 : 1.0;
+  if ((sb & 128) == 0) return sign * (double)n;
+  for (;;) {
+    s = dbyte(d);
+    sb = s < 0 ? 0u : (uint32_t)s;
+    n |= (sb & 127) << (e & 31);
+    e += 7;
+    if (s >= 0 && s < 128) return sign * (double)n;
+    if (e > 41) fail(c, YMO_ERR_INT_RANGE);
+  }
+}
+
+static Str rd_vstr(Ctx *c, Dec *d) { /* readVarString (E) */
+  uint32_t L = rd_vu(c, d);
+  Str empty = {NULL, 0};
+  if (L == 0) return empty;
+  size_t avail = d->pos < d->len ? d->len - d->pos : 0;
+  uint8_t *tmp = (uint8_t *)aalloc(c, ((size_t)L < avail ? (size_t)L : avail) + 2);
+  size_t k = 0;
+  int b = dbyte(d);
+  if (b < 0) fail(c, YMO_ERR_RANGE); /* String.fromCodePoint(undefined) */
+  tmp[k++] = (uint8_t)b;
+  uint32_t s = L - 1;
+  if (s < 100) {
+    while (s--) {
+      b = dbyte(d);
+      if (b < 0) fail(c, YMO_ERR_RANGE);
+      tmp[k++] = (uint8_t)b;
+    }
+  } else {
+    while (s > 0) {
+      uint32_t e = s < 10000 ? s : 10000;
+      size_t a0 = d->pos, a1 = d->pos + e;
+      if (a0 > d->len) a0 = d->len;
+      if (a1 > d->len) a1 = d->len;
+      if (a1 > a0) { memcpy(tmp + k, d->a + a0, a1 - a0); k += a1 - a0; }
+      d->pos += e;
+      s -= e;
+    }
+  }
+  return utf8_decode_strict(c, tmp, k);
+}
+
+typedef struct { const uint8_t *p; size_t n; } Span;
+static Span rd_vbytes(Ctx *c, Dec *d) { /* readVarUint8Array: new Uint8Array(buffer, pos, len) */
+  uint32_t L = rd_vu(c, d);
+  if (d->pos > d->len || (size_t)L > d->len - d->pos) fail(c, YMO_ERR_RANGE);
+  Span s = {d->a + d->pos, L};
+  d->pos += L;
+  return s;
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* JS values produced by readAny / JSON.parse                                                      */
+/* ------------------------------------------------------------------------------------------------ */
+enum { V_UNDEF, V_NULL, V_BOOL, V_NUM, V_BIGINT, V_STR, V_ARR, V_OBJ, V_BYTES };
+typedef struct Val {
+  int t;
+  int b;
+  double num;
+  uint8_t big[8];
+  Str s;
+  struct Val **items; /* ARR / OBJ values */
+  Str *keys;          /* OBJ keys */
+  size_t n, cap;
+  Span bytes;
+} Val;
+
+static Val *val_new(Ctx *c, int t) {
+  Val *v = (Val *)aalloc(c, sizeof(Val));
+  memset(v, 0, sizeof(Val));
+  v->t = t;
+  return v;
+}
+/* canonical array index ("0" .. "4294967294"); returns 1 and the index */
+static int key_array_index(Str k, uint32_t *idx) {
+  if (k.n == 0 || k.n > 10) return 0;
+  if (k.n > 1 && k.u[0] == '0') return 0;
+  uint64_t v = 0;
+  for (size_t i = 0; i < k.n; i++) {
+    if (k.u[i] < '0' || k.u[i] > '9') return 0;
+    v = v * 10 + (k.u[i] - '0');
+  }
+  if (v >= 4294967295ull) return 0;
+  *idx = (uint32_t)v;
+  return 1;
+}
+/* [[Set]] / CreateDataProperty on a plain object, keeping OrdinaryOwnPropertyKeys order.
+ * is_json: JSON.parse semantics (__proto__ is an ordinary key); else assignment semantics (readAny). */
+static void obj_set(Ctx *c, Val *o, Str k, Val *v, int is_json) {
+  for (size_t i = 0; i < o->n; i++)
+    if (str_eq(o->keys[i], k)) { o->items[i] = v; return; }
+  static const uint16_t proto[] = {'_', '_', 'p', 'r', 'o', 't', 'o', '_', '_'};
+  Str ps = {proto, 9};
+  if (!is_json && str_eq(k, ps)) return; /* sets [[Prototype]] (object/null) or is ignored: no own key */
+  if (o->n == o->cap) {
+    size_t cap = o->cap ? o->cap * 2 : 4;
+    Val **ni = (Val **)aalloc(c, cap * sizeof(Val *));
+    Str *nk = (Str *)aalloc(c, cap * sizeof(Str));
+    if (o->n) { memcpy(ni, o->items, o->n * sizeof(Val *)); memcpy(nk, o->keys, o->n * sizeof(Str)); }
+    o->items = ni; o->keys = nk; o->cap = cap;
+  }
+  /* position: array-index keys ascending before all string keys */
+  uint32_t idx;
+  size_t pos = o->n;
+  if (key_array_index(k, &idx)) {
+    pos = 0;
+    while (pos < o->n) {
+      uint32_t j;
+      if (!key_array_index(o->keys[pos], &j) || j > idx) break;
+      pos++;
+    }
+  }
+  memmove(o->items + pos + 1, o->items + pos, (o->n - pos) * sizeof(Val *));
+  memmove(o->keys + pos + 1, o->keys + pos, (o->n - pos) * sizeof(Str));
+  o->items[pos] = v; o->keys[pos] = k; o->n++;
+}
+static void arr_push(Ctx *c, Val *a, Val *v) {
+  if (a->n == a->cap) {
+    size_t cap = a->cap ? a->cap * 2 : 4;
+    Val **ni = (Val **)aalloc(c, cap * sizeof(Val *));
+    if (a->n) memcpy(ni, a->items, a->n * sizeof(Val *));
+    a->items = ni; a->cap = cap;
+  }
+  a->items[a->n++] = v;
+}
+
+static double rd_be_f32(const uint8_t *p) {
+  uint32_t u = ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+  float f; memcpy(&f, &u, 4); return (double)f;
+}
+static double rd_be_f64(const uint8_t *p) {
+  uint64_t u = 0;
+  for (int i = 0; i < 8; i++) u = (u << 8) | p[i];
+  double f; memcpy(&f, &u, 8); return f;
+}
+
+static Val *rd_any(Ctx *c, Dec *d) { /* readAny (B) */
+  int tag = dbyte(d);
+  if (tag < 116 || tag > 127) fail(c, YMO_ERR_TYPE); /* k[127 - tag] is not a function */
+  Val *v;
+  switch (tag) {
+    case 127: return val_new(c, V_UNDEF);
+    case 126: return val_new(c, V_NULL);
+    case 125: v = val_new(c, V_NUM); v->num = rd_vi(c, d); return v;
+    case 124:
+      if (d->pos > d->len || d->len - d->pos < 4) fail(c, YMO_ERR_RANGE);
+      v = val_new(c, V_NUM); v->num = rd_be_f32(d->a + d->pos); d->pos += 4; return v;
+    case 123:
+      if (d->pos > d->len || d->len - d->pos < 8) fail(c, YMO_ERR_RANGE);
+      v = val_new(c, V_NUM); v->num = rd_be_f64(d->a + d->pos); d->pos += 8; return v;
+    case 122:
+      if (d->pos > d->len || d->len - d->pos < 8) fail(c, YMO_ERR_RANGE);
+      v = val_new(c, V_BIGINT); memcpy(v->big, d->a + d->pos, 8); d->pos += 8; return v;
+    case 121: v = val_new(c, V_BOOL); v->b = 0; return v;
+    case 120: v = val_new(c, V_BOOL); v->b = 1; return v;
+    case 119: v = val_new(c, V_STR); v->s = rd_vstr(c, d); return v;
+    case 118: {
+      uint32_t n = rd_vu(c, d);
+      v = val_new(c, V_OBJ);
+      for (uint32_t i = 0; i < n; i++) {
+        Str k = rd_vstr(c, d);
+        Val *x = rd_any(c, d);
+        obj_set(c, v, k, x, 0);
+      }
+      return v;
+    }
+    case 117: {
+      uint32_t n = rd_vu(c, d);
+      v = val_new(c, V_ARR);
+      for (uint32_t i = 0; i < n; i++) arr_push(c, v, rd_any(c, d));
+      return v;
+    }
+    default: /* 116 */
+      v = val_new(c, V_BYTES); v->bytes = rd_vbytes(c, d); return v;
+  }
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* lib0 encoding (module 29194)                                                                    */
+/* ------------------------------------------------------------------------------------------------ */
+/* writeVarUint on a JS integer (int64 domain): `while (num > 127) { .. num >>>= 7 }` */
+static void wr_vu(Ctx *c, Buf *b, int64_t num) {
+  while (num > 127) {
+    put8(c, b, 0x80 | (unsigned)(num & 127));
+    num = (int64_t)((uint32_t)num >> 7);
+  }
+  put8(c, b, (unsigned)(num & 127));
+}
+/* writeVarInt on a JS number (integral, possibly -0) */
+static void wr_vi(Ctx *c, Buf *b, double num) {
+  int neg = js_is_negzero_or_neg(num);
+  if (neg) num = -num;
+  put8(c, b, (num > 63 ? 0x80 : 0) | (neg ? 0x40 : 0) | (unsigned)(js_toint32(num) & 63));
+  uint32_t s = js_touint32(num) >> 6;
+  while (s > 0) {
+    put8(c, b, (s > 127 ? 0x80 : 0) | (s & 127));
+    s >>= 7;
+  }
+}
+static void wr_vstr(Ctx *c, Buf *b, Str s) { /* writeVarString */
+  Buf *t = buf_new(c);
+  utf8_encode(c, t, s);
+  wr_vu(c, b, (int64_t)t->n);
+  putraw(c, b, t->p, t->n);
+}
+static void wr_vbytes(Ctx *c, Buf *b, const uint8_t *p, size_t n) { wr_vu(c, b, (int64_t)n); putraw(c, b, p, n); }
+
+static int js_is_integer(double v) { return isfinite(v) && floor(v) == v; }
+static int js_f32_exact(double v) { return (double)(float)v == v; } /* setFloat32 / getFloat32 === v */
+
+static void wr_any(Ctx *c, Buf *b, const Val *v) { /* writeAny (G) */
+  switch (v->t) {
+    case V_UNDEF: put8(c, b, 127); return;
+    case V_NULL: put8(c, b, 126); return;
+    case V_BOOL: put8(c, b, v->b ? 120 : 121); return;
+    case V_NUM: {
+      double x = v->num;
+      if (js_is_integer(x) && x <= 2147483647.0) { put8(c, b, 125); wr_vi(c, b, x); }
+      else if (js_f32_exact(x)) {
+        float f = (float)x; uint32_t u; memcpy(&u, &f, 4);
+        put8(c, b, 124); put8(c, b, u >> 24); put8(c, b, (u >> 16) & 255); put8(c, b, (u >> 8) & 255); put8(c, b, u & 255);
+      } else {
+        uint64_t u; memcpy(&u, &x, 8);
+        put8(c, b, 123);
+        for (int i = 7; i >= 0; i--) put8(c, b, (unsigned)((u >> (8 * i)) & 255));
+      }
+      return;
+    }
+    case V_BIGINT: put8(c, b, 122); putraw(c, b, v->big, 8); return;
+    case V_STR: put8(c, b, 119); wr_vstr(c, b, v->s); return;
+    case V_ARR:
+      put8(c, b, 117); wr_vu(c, b, (int64_t)v->n);
+      for (size_t i = 0; i < v->n; i++) wr_any(c, b, v->items[i]);
+      return;
+    case V_BYTES: put8(c, b, 116); wr_vbytes(c, b, v->bytes.p, v->bytes.n); return;
+    default:
+      put8(c, b, 118); wr_vu(c, b, (int64_t)v->n);
+      for (size_t i = 0; i < v->n; i++) { wr_vstr(c, b, v->keys[i]); wr_any(c, b, v->items[i]); }
+      return;
+  }
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* JSON.parse / JSON.stringify (V1 writeJSON/readJSON, ContentJSON in both formats)                */
+/* ------------------------------------------------------------------------------------------------ */
+typedef struct { const uint16_t *u; size_t n, i; } JP;
+static void jws(JP *p) { while (p->i < p->n && (p->u[p->i] == ' ' || p->u[p->i] == '\t' || p->u[p->i] == '\n' || p->u[p->i] == '\r')) p->i++; }
+static int jhex(int ch) {
+  if (ch >= '0' && ch <= '9') return ch - '0';
+  if (ch >= 'a' && ch <= 'f') return ch - 'a' + 10;
+  if (ch >= 'A' && ch <= 'F') return ch - 'A' + 10;
+  return -1;
+}
+static Str jstr(Ctx *c, JP *p) {
+  p->i++; /* opening quote */
+  uint16_t *out = (uint16_t *)aalloc(c, (p->n - p->i) * 2 + 2);
+  size_t k = 0;
+  for (;;) {
+    if (p->i >= p->n) fail(c, YMO_ERR_SYNTAX);
+    uint16_t ch = p->u[p->i++];
+    if (ch == '"') break;
+    if (ch < 0x20) fail(c, YMO_ERR_SYNTAX);
+    if (ch != '\\') { out[k++] = ch; continue; }
+    if (p->i >= p->n) fail(c, YMO_ERR_SYNTAX);
+    ch = p->u[p->i++];
+    switch (ch) {
+      case '"': out[k++] = '"'; break;
+      case '\\': out[k++] = '\\'; break;
+      case '/': out[k++] = '/'; break;
+      case 'b': out[k++] = 8; break;
+      case 'f': out[k++] = 12; break;
+      case 'n': out[k++] = 10; break;
+      case 'r': out[k++] = 13; break;
+      case 't': out[k++] = 9; break;
+      case 'u': {
+        if (p->i + 4 > p->n) fail(c, YMO_ERR_SYNTAX);
+        unsigned v = 0;
+        for (int j = 0; j < 4; j++) {
+          int h = jhex(p->u[p->i + j]);
+          if (h < 0) fail(c, YMO_ERR_SYNTAX);
+          v = v * 16 + (unsigned)h;
+        }
+        p->i += 4;
+        out[k++] = (uint16_t)v;
+        break;
+      }
+      default: fail(c, YMO_ERR_SYNTAX);
+    }
+  }
+  Str r = {out, k};
+  return r;
+}
+static Val *jval(Ctx *c, JP *p, int depth) {
+  if (depth > 10000) fail(c, YMO_ERR_RANGE);
+  jws(p);
+  if (p->i >= p->n) fail(c, YMO_ERR_SYNTAX);
+  uint16_t ch = p->u[p->i];
+  if (ch == '{') {
+    p->i++;
+    Val *o = val_new(c, V_OBJ);
+    jws(p);
+    if (p->i < p->n && p->u[p->i] == '}') { p->i++; return o; }
+    for (;;) {
+      jws(p);
+      if (p->i >= p->n || p->u[p->i] != '"') fail(c, YMO_ERR_SYNTAX);
+      Str k = jstr(c, p);
+      jws(p);
+      if (p->i >= p->n || p->u[p->i] != ':') fail(c, YMO_ERR_SYNTAX);
+      p->i++;
+      Val *v = jval(c, p, depth + 1);
+      obj_set(c, o, k, v, 1);
+      jws(p);
+      if (p->i >= p->n) fail(c, YMO_ERR_SYNTAX);
+      if (p->u[p->i] == ',') { p->i++; continue; }
+      if (p->u[p->i] == '}') { p->i++; return o; }
+      fail(c, YMO_ERR_SYNTAX);
+    }
+  }
+  if (ch == '[') {
+    p->i++;
+    Val *a = val_new(c, V_ARR);
+    jws(p);
+    if (p->i < p->n && p->u[p->i] == ']') { p->i++; return a; }
+    for (;;) {
+      arr_push(c, a, jval(c, p, depth + 1));
+      jws(p);
+      if (p->i >= p->n) fail(c, YMO_ERR_SYNTAX);
+      if (p->u[p->i] == ',') { p->i++; continue; }
+      if (p->u[p->i] == ']') { p->i++; return a; }
+      fail(c, YMO_ERR_SYNTAX);
+    }
+  }
+  if (ch == '"') { Val *v = val_new(c, V_STR); v->s = jstr(c, p); return v; }
+  static const char *lits[3] = {"true", "false", "null"};
+  for (int l = 0; l < 3; l++) {
+    size_t ln = strlen(lits[l]);
+    if (p->i + ln <= p->n) {
+      int ok = 1;
+      for (size_t j = 0; j < ln; j++) if (p->u[p->i + j] != (uint16_t)lits[l][j]) { ok = 0; break; }
+      if (ok) {
+        p->i += ln;
+        if (l == 2) return val_new(c, V_NULL);
+        Val *v = val_new(c, V_BOOL); v->b = (l == 0); return v;
+      }
+    }
+  }
+  /* number: -?(0|[1-9]\d*)(\.\d+)?([eE][+-]?\d+)? */
+  size_t st = p->i;
+  if (p->i < p->n && p->u[p->i] == '-') p->i++;
+  if (p->i >= p->n) fail(c, YMO_ERR_SYNTAX);
+  if (p->u[p->i] == '0') p->i++;
+  else if (p->u[p->i] >= '1' && p->u[p->i] <= '9') { while (p->i < p->n && p->u[p->i] >= '0' && p->u[p->i] <= '9') p->i++; }
+  else fail(c, YMO_ERR_SYNTAX);
+  if (p->i < p->n && p->u[p->i] == '.') {
+    p->i++;
+    if (p->i >= p->n || p->u[p->i] < '0' || p->u[p->i] > '9') fail(c, YMO_ERR_SYNTAX);
+    while (p->i < p->n && p->u[p->i] >= '0' && p->u[p->i] <= '9') p->i++;
+  }
+  if (p->i < p->n && (p->u[p->i] == 'e' || p->u[p->i] == 'E')) {
+    p->i++;
+    if (p->i < p->n && (p->u[p->i] == '+' || p->u[p->i] == '-')) p->i++;
+    if (p->i >= p->n || p->u[p->i] < '0' || p->u[p->i] > '9') fail(c, YMO_ERR_SYNTAX);
+    while (p->i < p->n && p->u[p->i] >= '0' && p->u[p->i] <= '9') p->i++;
+  }
+  size_t ln = p->i - st;
+  char *tmp = (char *)aalloc(c, ln + 1);
+  for (size_t j = 0; j < ln; j++) tmp[j] = (char)p->u[st + j];
+  tmp[ln] = 0;
+  Val *v = val_new(c, V_NUM);
+  v->num = strtod(tmp, NULL);
+  return v;
+}
+static Val *json_parse(Ctx *c, Str s) {
+  JP p = {s.u, s.n, 0};
+  Val *v = jval(c, &p, 0);
+  jws(&p);
+  if (p.i != p.n) fail(c, YMO_ERR_SYNTAX);
+  return v;
+}
+
+/* Number::toString(x) for finite x (ECMA-262 7.1.12.1), shortest round-trip digits */
+static void js_num_to_string(double x, char *out) {
+  if (x == 0) { strcpy(out, "0"); return; }
+  if (isnan(x)) { strcpy(out, "NaN"); return; }
+  char *o = out;
+  if (x < 0) { *o++ = '-'; x = -x; }
+  if (isinf(x)) { strcpy(o, "Infinity"); return; }
+  char buf[64];
+  int p;
+  for (p = 1; p <= 17; p++) {
+    snprintf(buf, sizeof buf, "%.*e", p - 1, x);
+    if (strtod(buf, NULL) == x) break;
+  }
+  char digits[32];
+  int k = 0;
+  char *e = strchr(buf, 'e');
+  for (char *q = buf; q < e; q++) if (*q >= '0' && *q <= '9') digits[k++] = *q;
+  while (k > 1 && digits[k - 1] == '0') k--;
+  digits[k] = 0;
+  int n = atoi(e + 1) + 1;
+  if (k <= n && n <= 21) {
+    memcpy(o, digits, k); o += k;
+    for (int i = 0; i < n - k; i++) *o++ = '0';
+    *o = 0;
+  } else if (0 < n && n <= 21) {
+    memcpy(o, digits, n); o += n; *o++ = '.';
+    memcpy(o, digits + n, k - n); o += k - n; *o = 0;
+  } else if (-6 < n && n <= 0) {
+    *o++ = '0'; *o++ = '.';
+    for (int i = 0; i < -n; i++) *o++ = '0';
+    memcpy(o, digits, k); o += k; *o = 0;
+  } else {
+    *o++ = digits[0];
+    if (k > 1) { *o++ = '.'; memcpy(o, digits + 1, k - 1); o += k - 1; }
+    sprintf(o, "e%c%d", n - 1 >= 0 ? '+' : '-', abs(n - 1));
+  }
+}
+
+typedef struct { uint16_t *u; size_t n, cap; } WStr;
+static void ws_put(Ctx *c, WStr *w, uint16_t ch) {
+  if (w->n == w->cap) {
+    size_t cap = w->cap ? w->cap * 2 : 32;
+    uint16_t *nu = (uint16_t *)aalloc(c, cap * 2);
+    if (w->n) memcpy(nu, w->u, w->n * 2);
+    w->u = nu; w->cap = cap;
+  }
+  w->u[w->n++] = ch;
+}
+static void ws_ascii(Ctx *c, WStr *w, const char *s) { while (*s) ws_put(c, w, (uint8_t)*s++); }
+static void json_quote(Ctx *c, WStr *w, Str s) {
+  static const char *hexd = "0123456789abcdef";
+  ws_put(c, w, '"');
+  for (size_t i = 0; i < s.n; i++) {
+    uint16_t ch = s.u[i];
+    switch (ch) {
+      case 8: ws_ascii(c, w, "\\b"); continue;
+      case 9: ws_ascii(c, w, "\\t"); continue;
+      case 10: ws_ascii(c, w, "\\n"); continue;
+      case 12: ws_ascii(c, w, "\\f"); continue;
+      case 13: ws_ascii(c, w, "\\r"); continue;
+      case '"': ws_ascii(c, w, "\\\""); continue;
+      case '\\': ws_ascii(c, w, "\\\\"); continue;
+    }
+    int lone = 0;
+    if (ch >= 0xD800 && ch <= 0xDBFF) {
+      if (i + 1 < s.n && s.u[i + 1] >= 0xDC00 && s.u[i + 1] <= 0xDFFF) { ws_put(c, w, ch); ws_put(c, w, s.u[++i]); continue; }
+      lone = 1;
+    } else if (ch >= 0xDC00 && ch <= 0xDFFF) lone = 1;
+    if (ch < 0x20 || lone) {
+      ws_ascii(c, w, "\\u");
+      ws_put(c, w, hexd[(ch >> 12) & 15]); ws_put(c, w, hexd[(ch >> 8) & 15]);
+      ws_put(c, w, hexd[(ch >> 4) & 15]); ws_put(c, w, hexd[ch & 15]);
+      continue;
+    }
+    ws_put(c, w, ch);
+  }
+  ws_put(c, w, '"');
+}
+static void json_stringify_into(Ctx *c, WStr *w, const Val *v) {
+  switch (v->t) {
+    case V_NULL: case V_UNDEF: ws_ascii(c, w, "null"); return;
+    case V_BOOL: ws_ascii(c, w, v->b ? "true" : "false"); return;
+    case V_NUM: {
+      if (!isfinite(v->num)) { ws_ascii(c, w, "null"); return; }
+      char buf[64]; js_num_to_string(v->num, buf); ws_ascii(c, w, buf); return;
+    }
+    case V_STR: json_quote(c, w, v->s); return;
+    case V_ARR:
+      ws_put(c, w, '[');
+      for (size_t i = 0; i < v->n; i++) { if (i) ws_put(c, w, ','); json_stringify_into(c, w, v->items[i]); }
+      ws_put(c, w, ']');
+      return;
+    case V_OBJ:
+      ws_put(c, w, '{');
+      for (size_t i = 0; i < v->n; i++) {
+        if (i) ws_put(c, w, ',');
+        json_quote(c, w, v->keys[i]); ws_put(c, w, ':'); json_stringify_into(c, w, v->items[i]);
+      }
+      ws_put(c, w, '}');
+      return;
+    default: fail(c, YMO_ERR_UNSUPPORTED); /* not producible by JSON.parse */
+  }
+}
+static Str json_stringify(Ctx *c, const Val *v) {
+  WStr w = {NULL, 0, 0};
+  json_stringify_into(c, &w, v);
+  Str r = {w.u, w.n};
+  return r;
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* lib0 RLE column decoders (V2)                                                                   */
+/* ------------------------------------------------------------------------------------------------ */
+typedef struct { Dec d; int s; int64_t count; } RleDec;            /* RleDecoder<readUint8> (N) */
+typedef struct { Dec d; double s; int64_t count; } UintOptDec;     /* UintOptRleDecoder (P)     */
+typedef struct { Dec d; int64_t s; int64_t count; int64_t diff; } IntDiffDec; /* (G)          */
+typedef struct { UintOptDec lens; Str str; int64_t spos; } StrDec; /* StringDecoder ($)         */
+
+static int rle_read(Ctx *c, RleDec *r) {
+  if (r->count == 0) {
+    r->s = dbyte(&r->d);
+    if (dhas(&r->d)) r->count = (int64_t)rd_vu(c, &r->d) + 1;
+    else r->count = -1;
+  }
+  r->count--;
+  return r->s;
+}
+static int64_t uopt_read(Ctx *c, UintOptDec *r) {
+  if (r->count == 0) {
+    r->s = rd_vi(c, &r->d);
+    int neg = js_is_negzero_or_neg(r->s);
+    r->count = 1;
+    if (neg) { r->s = -r->s; r->count = (int64_t)rd_vu(c, &r->d) + 2; }
+  }
+  r->count--;
+  return (int64_t)r->s;
+}
+static int64_t idiff_read(Ctx *c, IntDiffDec *r) {
+  if (r->count == 0) {
+    double t = rd_vi(c, &r->d);
+    int32_t ti = js_toint32(t);
+    int sb = ti & 1;
+    r->diff = ti >> 1;
+    r->count = 1;
+    if (sb) r->count = (int64_t)rd_vu(c, &r->d) + 2;
+  }
+  r->s += r->diff;
+  r->count--;
+  return r->s;
+}
+static Str sdec_read(Ctx *c, StrDec *r) {
+  int64_t t = r->spos + uopt_read(c, &r->lens);
+  Str s = str_slice(r->str, r->spos, t);
+  r->spos = t;
+  return s;
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* lib0 RLE column encoders (V2)                                                                   */
+/* ------------------------------------------------------------------------------------------------ */
+typedef struct { Buf *b; int s; int64_t count; } RleEnc;             /* RleEncoder<writeUint8> ($) */
+typedef struct { Buf *b; double s; int64_t count; } UintOptEnc;      /* UintOptRleEncoder (K)       */
+typedef struct { Buf *b; int64_t s, count, diff; } IntDiffEnc;        /* IntDiffOptRleEncoder (H)    */
+typedef struct { WStr s; UintOptEnc lens; } StrEnc;                   /* StringEncoder (W)           */
+
+static void rle_write(Ctx *c, RleEnc *e, int v) {
+  if (e->s == v) { e->count++; return; }
+  if (e->count > 0) wr_vu(c, e->b, e->count - 1);
+  e->count = 1;
+  put8(c, e->b, (unsigned)v & 255);
+  e->s = v;
+}
+static void uopt_flush(Ctx *c, UintOptEnc *e) {
+  if (e->count > 0) {
+    wr_vi(c, e->b, e->count == 1 ? e->s : -e->s);
+    if (e->count > 1) wr_vu(c, e->b, e->count - 2);
+  }
+}
+static void uopt_write(Ctx *c, UintOptEnc *e, double v) {
+  if (e->s == v) { e->count++; return; } /* JS ===: 0 === -0 */
+  uopt_flush(c, e);
+  e->count = 1;
+  e->s = v;
+}
+static void idiff_flush(Ctx *c, IntDiffEnc *e) {
+  if (e->count > 0) {
+    int32_t d = (int32_t)((uint32_t)js_toint32((double)e->diff) << 1) | (e->count == 1 ? 0 : 1);
+    wr_vi(c, e->b, (double)d);
+    if (e->count > 1) wr_vu(c, e->b, e->count - 2);
+  }
+}
+static void idiff_write(Ctx *c, IntDiffEnc *e, int64_t v) {
+  if (e->diff == v - e->s) { e->s = v; e->count++; return; }
+  idiff_flush(c, e);
+  e->count = 1;
+  e->diff = v - e->s;
+  e->s = v;
+}
+static void senc_write(Ctx *c, StrEnc *e, Str s) {
+  for (size_t i = 0; i < s.n; i++) ws_put(c, &e->s, s.u[i]);
+  uopt_write(c, &e->lens, (double)s.n);
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* UpdateDecoderV1 / UpdateDecoderV2 (src/utils/UpdateDecoder.js:154-243, 270-392)                 */
+/* ------------------------------------------------------------------------------------------------ */
+typedef struct {
+  int v2;
+  Dec rest;
+  IntDiffDec keyClock, leftClock, rightClock;
+  UintOptDec client, typeRef, len;
+  RleDec info, parentInfo;
+  StrDec str;
+  Str *keys;
+  size_t nkeys, capkeys;
+  int64_t dsCurr;
+} UDec;
+
+static Dec col_dec(Ctx *c, Dec *rest) {
+  Span s = rd_vbytes(c, rest);
+  Dec d = {s.p, s.n, 0};
+  return d;
+}
+static void udec_init(Ctx *c, UDec *u, const uint8_t *p, size_t n, int v2) {
+  memset(u, 0, sizeof(*u));
+  u->v2 = v2;
+  u->rest.a = p; u->rest.len = n; u->rest.pos = 0;
+  if (!v2) return;
+  rd_vu(c, &u->rest); /* feature flag (13.5.16 reads it with readVarUint) */
+  u->keyClock.d = col_dec(c, &u->rest);
+  u->client.d = col_dec(c, &u->rest);
+  u->leftClock.d = col_dec(c, &u->rest);
+  u->rightClock.d = col_dec(c, &u->rest);
+  u->info.d = col_dec(c, &u->rest);
+  u->str.lens.d = col_dec(c, &u->rest);
+  u->str.str = rd_vstr(c, &u->str.lens.d); /* StringDecoder decodes the whole column up front */
+  u->parentInfo.d = col_dec(c, &u->rest);
+  u->typeRef.d = col_dec(c, &u->rest);
+  u->len.d = col_dec(c, &u->rest);
+}
+typedef struct { int64_t client, clock; } JID;
+static JID ud_left(Ctx *c, UDec *u) {
+  JID r;
+  if (u->v2) { r.client = uopt_read(c, &u->client); r.clock = idiff_read(c, &u->leftClock); }
+  else { r.client = rd_vu(c, &u->rest); r.clock = rd_vu(c, &u->rest); }
+  return r;
+}
+static JID ud_right(Ctx *c, UDec *u) {
+  JID r;
+  if (u->v2) { r.client = uopt_read(c, &u->client); r.clock = idiff_read(c, &u->rightClock); }
+  else { r.client = rd_vu(c, &u->rest); r.clock = rd_vu(c, &u->rest); }
+  return r;
+}
+static int64_t ud_client(Ctx *c, UDec *u) { return u->v2 ? uopt_read(c, &u->client) : (int64_t)rd_vu(c, &u->rest); }
+static int ud_info(Ctx *c, UDec *u) { return u->v2 ? rle_read(c, &u->info) : dbyte(&u->rest); }
+static Str ud_string(Ctx *c, UDec *u) { return u->v2 ? sdec_read(c, &u->str) : rd_vstr(c, &u->rest); }
+static int ud_parent_info(Ctx *c, UDec *u) { return u->v2 ? rle_read(c, &u->parentInfo) == 1 : rd_vu(c, &u->rest) == 1; }
+static int64_t ud_typeref(Ctx *c, UDec *u) { return u->v2 ? uopt_read(c, &u->typeRef) : (int64_t)rd_vu(c, &u->rest); }
+static int64_t ud_len(Ctx *c, UDec *u) { return u->v2 ? uopt_read(c, &u->len) : (int64_t)rd_vu(c, &u->rest); }
+static Str ud_key(Ctx *c, UDec *u) {
+  if (!u->v2) return rd_vstr(c, &u->rest);
+  int64_t kc = idiff_read(c, &u->keyClock);
+  if (kc >= 0 && (size_t)kc < u->nkeys) return u->keys[kc];
+  Str s = sdec_read(c, &u->str);
+  if (u->nkeys == u->capkeys) {
+    size_t cap = u->capkeys ? u->capkeys * 2 : 8;
+    Str *nk = (Str *)aalloc(c, cap * sizeof(Str));
+    if (u->nkeys) memcpy(nk, u->keys, u->nkeys * sizeof(Str));
+    u->keys = nk; u->capkeys = cap;
+  }
+  u->keys[u->nkeys++] = s;
+  return s;
+}
+static void ud_reset_ds(UDec *u) { u->dsCurr = 0; }
+static int64_t ud_ds_clock(Ctx *c, UDec *u) {
+  if (!u->v2) return rd_vu(c, &u->rest);
+  u->dsCurr += rd_vu(c, &u->rest);
+  return u->dsCurr;
+}
+static int64_t ud_ds_len(Ctx *c, UDec *u) {
+  if (!u->v2) return rd_vu(c, &u->rest);
+  int64_t d = (int64_t)rd_vu(c, &u->rest) + 1;
+  u->dsCurr += d;
+  return d;
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* UpdateEncoderV1 / UpdateEncoderV2 (src/utils/UpdateEncoder.js:138-227, 264-408)                  */
+/* ------------------------------------------------------------------------------------------------ */
+typedef struct {
+  int v2;
+  Buf *rest;
+  IntDiffEnc keyClock, leftClock, rightClock;
+  UintOptEnc client, typeRef, len;
+  RleEnc info, parentInfo;
+  StrEnc str;
+  int64_t keyClockCounter;
+  int64_t dsCurr;
+} UEnc;
+
+static void uenc_init(Ctx *c, UEnc *e, int v2) {
+  memset(e, 0, sizeof(*e));
+  e->v2 = v2;
+  e->rest = buf_new(c);
+  if (!v2) return;
+  e->keyClock.b = buf_new(c); e->leftClock.b = buf_new(c); e->rightClock.b = buf_new(c);
+  e->client.b = buf_new(c); e->typeRef.b = buf_new(c); e->len.b = buf_new(c);
+  e->info.b = buf_new(c); e->info.s = -1000; /* RleEncoder starts with s = null */
+  e->parentInfo.b = buf_new(c); e->parentInfo.s = -1000;
+  e->str.lens.b = buf_new(c);
+}
+static void ue_left(Ctx *c, UEnc *e, JID id) {
+  if (e->v2) { uopt_write(c, &e->client, (double)id.client); idiff_write(c, &e->leftClock, id.clock); }
+  else { wr_vu(c, e->rest, id.client); wr_vu(c, e->rest, id.clock); }
+}
+static void ue_right(Ctx *c, UEnc *e, JID id) {
+  if (e->v2) { uopt_write(c, &e->client, (double)id.client); idiff_write(c, &e->rightClock, id.clock); }
+  else { wr_vu(c, e->rest, id.client); wr_vu(c, e->rest, id.clock); }
+}
+static void ue_client(Ctx *c, UEnc *e, int64_t client) {
+  if (e->v2) uopt_write(c, &e->client, (double)client);
+  else wr_vu(c, e->rest, client);
+}
+static void ue_info(Ctx *c, UEnc *e, int info) {
+  if (e->v2) rle_write(c, &e->info, info);
+  else put8(c, e->rest, (unsigned)info & 255);
+}
+static void ue_string(Ctx *c, UEnc *e, Str s) {
+  if (e->v2) senc_write(c, &e->str, s);
+  else wr_vstr(c, e->rest, s);
+}
+static void ue_parent_info(Ctx *c, UEnc *e, int isykey) {
+  if (e->v2) rle_write(c, &e->parentInfo, isykey ? 1 : 0);
+  else wr_vu(c, e->rest, isykey ? 1 : 0);
+}
+static void ue_typeref(Ctx *c, UEnc *e, int64_t t) {
+  if (e->v2) uopt_write(c, &e->typeRef, (double)t);
+  else wr_vu(c, e->rest, t);
+}
+static void ue_len(Ctx *c, UEnc *e, int64_t l) {
+  if (e->v2) uopt_write(c, &e->len, (double)l);
+  else wr_vu(c, e->rest, l);
+}
+static void ue_key(Ctx *c, UEnc *e, Str k) {
+  if (e->v2) { idiff_write(c, &e->keyClock, e->keyClockCounter++); senc_write(c, &e->str, k); }
+  else wr_vstr(c, e->rest, k);
+}
+static void ue_reset_ds(UEnc *e) { e->dsCurr = 0; }
+static void ue_ds_clock(Ctx *c, UEnc *e, int64_t clock) {
+  if (!e->v2) { wr_vu(c, e->rest, clock); return; }
+  int64_t d = clock - e->dsCurr;
+  e->dsCurr = clock;
+  wr_vu(c, e->rest, d);
+}
+static void ue_ds_len(Ctx *c, UEnc *e, int64_t len) {
+  if (!e->v2) { wr_vu(c, e->rest, len); return; }
+  if (len == 0) fail(c, YMO_ERR_UNEXPECTED);
+  wr_vu(c, e->rest, len - 1);
+  e->dsCurr += len;
+}
+static Buf *uenc_finish(Ctx *c, UEnc *e) {
+  if (!e->v2) return e->rest;
+  Buf *o = buf_new(c);
+  wr_vu(c, o, 0); /* feature flag */
+  idiff_flush(c, &e->keyClock); wr_vbytes(c, o, e->keyClock.b->p, e->keyClock.b->n);
+  uopt_flush(c, &e->client); wr_vbytes(c, o, e->client.b->p, e->client.b->n);
+  idiff_flush(c, &e->leftClock); wr_vbytes(c, o, e->leftClock.b->p, e->leftClock.b->n);
+  idiff_flush(c, &e->rightClock); wr_vbytes(c, o, e->rightClock.b->p, e->rightClock.b->n);
+  wr_vbytes(c, o, e->info.b->p, e->info.b->n);
+  {
+    Buf *sb = buf_new(c);
+    Str all = {e->str.s.u, e->str.s.n};
+    wr_vstr(c, sb, all);
+    uopt_flush(c, &e->str.lens);
+    putraw(c, sb, e->str.lens.b->p, e->str.lens.b->n);
+    wr_vbytes(c, o, sb->p, sb->n);
+  }
+  wr_vbytes(c, o, e->parentInfo.b->p, e->parentInfo.b->n);
+  uopt_flush(c, &e->typeRef); wr_vbytes(c, o, e->typeRef.b->p, e->typeRef.b->n);
+  uopt_flush(c, &e->len); wr_vbytes(c, o, e->len.b->p, e->len.b->n);
+  putraw(c, o, e->rest->p, e->rest->n);
+  return o;
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* Structs and contents                                                                            */
+/* ------------------------------------------------------------------------------------------------ */
+enum { K_GC = 0, K_SKIP = 1, K_ITEM = 2 };
+typedef struct {
+  int ref;      /* 1..9 */
+  int64_t dlen; /* ContentDeleted */
+  Str str;      /* ContentString */
+  Span bin;     /* ContentBinary */
+  /* JSON (ref 2): elements are canonical JSON texts, `undef` marks the literal 'undefined' */
+  Str *jstrs; uint8_t *jundef;
+  /* Any (ref 8): values */
+  Val **anys;
+  size_t n;     /* JSON / Any element count */
+  /* Embed (5) / Format value (6): V1 canonical JSON text; V2 any value */
+  Str jtext; Val *jval;
+  Str key;      /* Format key */
+  int64_t typeRef; Str typeName; /* ContentType */
+  Str guid; Val *docOpts;        /* ContentDoc */
+} Content;
+
+typedef struct Struct {
+  int kind;
+  int64_t client, clock, len;
+  int has_origin, has_right;
+  JID origin, right;
+  int parent_kind; /* 0 none, 1 ykey, 2 ID */
+  Str pkey; JID pid;
+  int has_psub; Str psub;
+  Content *content;
+} Struct;
+
+static int js_truthy(const Val *v) {
+  switch (v->t) {
+    case V_UNDEF: case V_NULL: return 0;
+    case V_BOOL: return v->b;
+    case V_NUM: return !(v->num == 0 || isnan(v->num));
+    case V_STR: return v->s.n != 0;
+    case V_BIGINT: { for (int i = 0; i < 8; i++) if (v->big[i]) return 1; return 0; }
+    default: return 1;
+  }
+}
+
+/* ContentDoc (13.5.16 Pr/Rr; ContentDoc.js:116-135): new Doc({guid, ...opts}) then opts re-derived */
+static void content_doc_canon(Ctx *c, Content *ct, Str guid, Val *o) {
+  static const uint16_t kg[] = {'g', 'u', 'i', 'd'}, kgc[] = {'g', 'c'},
+                        kal[] = {'a', 'u', 't', 'o', 'L', 'o', 'a', 'd'}, km[] = {'m', 'e', 't', 'a'};
+  Str sg = {kg, 4}, sgc = {kgc, 2}, sal = {kal, 8}, sm = {km, 4};
+  Val *vguid = NULL, *vgc = NULL, *val = NULL, *vmeta = NULL;
+  if (o->t == V_OBJ) {
+    for (size_t i = 0; i < o->n; i++) {
+      if (str_eq(o->keys[i], sg)) vguid = o->items[i];
+      else if (str_eq(o->keys[i], sgc)) vgc = o->items[i];
+      else if (str_eq(o->keys[i], sal)) val = o->items[i];
+      else if (str_eq(o->keys[i], sm)) vmeta = o->items[i];
+    }
+  }
+  if (vguid) {
+    if (vguid->t == V_UNDEF || vguid->t != V_STR) fail(c, YMO_ERR_UNSUPPORTED); /* random / non-string guid */
+    guid = vguid->s;
+  }
+  Val *opts = val_new(c, V_OBJ);
+  int gc = (vgc == NULL || vgc->t == V_UNDEF) ? 1 : js_truthy(vgc);
+  int autoload = (val == NULL || val->t == V_UNDEF) ? 0 : js_truthy(val);
+  Val *meta = (vmeta == NULL || vmeta->t == V_UNDEF) ? NULL : vmeta;
+  if (!gc) { Val *f = val_new(c, V_BOOL); f->b = 0; obj_set(c, opts, sgc, f, 1); }
+  if (autoload) { Val *t = val_new(c, V_BOOL); t->b = 1; obj_set(c, opts, sal, t, 1); }
+  if (meta && meta->t != V_NULL) obj_set(c, opts, sm, meta, 1);
+  ct->guid = guid;
+  ct->docOpts = opts;
+}
+
+static int64_t content_len(const Content *ct) {
+  switch (ct->ref) {
+    case 1: return ct->dlen;
+    case 2: case 8: return (int64_t)ct->n;
+    case 4: return (int64_t)ct->str.n;
+    default: return 1;
+  }
+}
+
+static Content *read_content(Ctx *c, UDec *u, int info) { /* readItemContent / contentRefs (Item.js:665-683) */
+  int ref = info & 31;
+  Content *ct = (Content *)aalloc(c, sizeof(Content));
+  memset(ct, 0, sizeof(*ct));
+  ct->ref = ref;
+  switch (ref) {
+    case 1: ct->dlen = ud_len(c, u); break;
+    case 2: {
+      int64_t n = ud_len(c, u);
+      static const uint16_t und[] = {'u', 'n', 'd', 'e', 'f', 'i', 'n', 'e', 'd'};
+      Str us = {und, 9};
+      size_t cap = 0;
+      for (int64_t i = 0; i < n; i++) {
+        Str s = ud_string(c, u);
+        if (ct->n == cap) {
+          cap = cap ? cap * 2 : 4;
+          Str *nj = (Str *)aalloc(c, cap * sizeof(Str));
+          uint8_t *nu = (uint8_t *)aalloc(c, cap);
+          if (ct->n) { memcpy(nj, ct->jstrs, ct->n * sizeof(Str)); memcpy(nu, ct->jundef, ct->n); }
+          ct->jstrs = nj; ct->jundef = nu;
+        }
+        if (str_eq(s, us)) { ct->jundef[ct->n] = 1; ct->jstrs[ct->n] = us; }
+        else { ct->jundef[ct->n] = 0; ct->jstrs[ct->n] = json_stringify(c, json_parse(c, s)); }
+        ct->n++;
+      }
+      break;
+    }
+    case 3: {
+      Span s = rd_vbytes(c, &u->rest);
+      ct->bin = s;
+      break;
+    }
+    case 4: ct->str = ud_string(c, u); break;
+    case 5:
+      if (u->v2) ct->jval = rd_any(c, &u->rest);
+      else ct->jtext = json_stringify(c, json_parse(c, rd_vstr(c, &u->rest)));
+      break;
+    case 6:
+      ct->key = ud_string(c, u);
+      if (u->v2) ct->jval = rd_any(c, &u->rest);
+      else ct->jtext = json_stringify(c, json_parse(c, rd_vstr(c, &u->rest)));
+      break;
+    case 7: {
+      int64_t tr = ud_typeref(c, u);
+      if (tr < 0 || tr > 6) fail(c, YMO_ERR_TYPE);
+      ct->typeRef = tr;
+      if (tr == 3 || tr == 5) ct->typeName = ud_key(c, u);
+      break;
+    }
+    case 8: {
+      int64_t n = ud_len(c, u);
+      size_t cap = 0;
+      for (int64_t i = 0; i < n; i++) {
+        Val *v = rd_any(c, &u->rest);
+        if (ct->n == cap) {
+          cap = cap ? cap * 2 : 4;
+          Val **na = (Val **)aalloc(c, cap * sizeof(Val *));
+          if (ct->n) memcpy(na, ct->anys, ct->n * sizeof(Val *));
+          ct->anys = na;
+        }
+        ct->anys[ct->n++] = v;
+      }
+      break;
+    }
+    case 9: {
+      Str guid = ud_string(c, u);
+      Val *o = rd_any(c, &u->rest);
+      content_doc_canon(c, ct, guid, o);
+      break;
+    }
+    case 0: case 10: fail(c, YMO_ERR_UNEXPECTED);
+    default: fail(c, YMO_ERR_TYPE);
+  }
+  return ct;
+}
+
+/* ContentX.splice(offset): returns the right part (13.5.16 @70000-75900) */
+static Content *content_splice(Ctx *c, const Content *src, int64_t off) {
+  Content *r = (Content *)aalloc(c, sizeof(Content));
+  *r = *src;
+  switch (src->ref) {
+    case 1: r->dlen = src->dlen - off; break;
+    case 2:
+      r->n = off < (int64_t)src->n ? src->n - (size_t)off : 0;
+      r->jstrs = src->jstrs + (off < (int64_t)src->n ? off : (int64_t)src->n);
+      r->jundef = src->jundef + (off < (int64_t)src->n ? off : (int64_t)src->n);
+      break;
+    case 8:
+      r->n = off < (int64_t)src->n ? src->n - (size_t)off : 0;
+      r->anys = src->anys + (off < (int64_t)src->n ? off : (int64_t)src->n);
+      break;
+    case 4: {
+      Str right = str_slice(src->str, off, (int64_t)src->str.n);
+      if (off >= 1 && off <= (int64_t)src->str.n) { /* charCodeAt(t - 1) of the left part */
+        uint16_t ch = src->str.u[off - 1];
+        if (ch >= 0xD800 && ch <= 0xDBFF) { /* ContentString.js:55-64: replace both halves by U+FFFD */
+          uint16_t *nu = (uint16_t *)aalloc(c, (right.n + 1) * 2);
+          nu[0] = 0xFFFD;
+          if (right.n > 1) memcpy(nu + 1, right.u + 1, (right.n - 1) * 2);
+          Str ns = {nu, right.n ? right.n : 1};
+          right = ns;
+        }
+      }
+      r->str = right;
+      break;
+    }
+    default: fail(c, YMO_ERR_METHOD);
+  }
+  return r;
+}
+
+static void content_write(Ctx *c, UEnc *e, const Content *ct, int64_t off) {
+  switch (ct->ref) {
+    case 1: ue_len(c, e, ct->dlen - off); break;
+    case 2:
+      ue_len(c, e, (int64_t)ct->n - off);
+      for (int64_t i = off; i < (int64_t)ct->n; i++) ue_string(c, e, ct->jstrs[i]);
+      break;
+    case 3: wr_vbytes(c, e->rest, ct->bin.p, ct->bin.n); break;
+    case 4: ue_string(c, e, off == 0 ? ct->str : str_slice(ct->str, off, (int64_t)ct->str.n)); break;
+    case 5:
+      if (e->v2) wr_any(c, e->rest, ct->jval);
+      else wr_vstr(c, e->rest, ct->jtext);
+      break;
+    case 6:
+      ue_key(c, e, ct->key);
+      if (e->v2) wr_any(c, e->rest, ct->jval);
+      else wr_vstr(c, e->rest, ct->jtext);
+      break;
+    case 7:
+      ue_typeref(c, e, ct->typeRef);
+      if (ct->typeRef == 3 || ct->typeRef == 5) ue_key(c, e, ct->typeName);
+      break;
+    case 8:
+      ue_len(c, e, (int64_t)ct->n - off);
+      for (int64_t i = off; i < (int64_t)ct->n; i++) wr_any(c, e->rest, ct->anys[i]);
+      break;
+    case 9: ue_string(c, e, ct->guid); wr_any(c, e->rest, ct->docOpts); break;
+    default: fail(c, YMO_ERR_UNEXPECTED);
+  }
+}
+
+/* Item.write / GC.write / Skip.write with offset (Item.js:625-658, GC.js:45-48, 13.5.16 ui.write) */
+static void struct_write(Ctx *c, UEnc *e, const Struct *s, int64_t off) {
+  if (s->kind == K_GC) { ue_info(c, e, 0); ue_len(c, e, s->len - off); return; }
+  if (s->kind == K_SKIP) { ue_info(c, e, 10); wr_vu(c, e->rest, s->len - off); return; }
+  int has_origin = off > 0 ? 1 : s->has_origin;
+  JID origin = s->origin;
+  if (off > 0) { origin.client = s->client; origin.clock = s->clock + off - 1; }
+  int info = (s->content->ref & 31) | (has_origin ? 0x80 : 0) | (s->has_right ? 0x40 : 0) | (s->has_psub ? 0x20 : 0);
+  ue_info(c, e, info);
+  if (has_origin) ue_left(c, e, origin);
+  if (s->has_right) ue_right(c, e, s->right);
+  if (!has_origin && !s->has_right) {
+    if (s->parent_kind == 1) { ue_parent_info(c, e, 1); ue_string(c, e, s->pkey); }
+    else if (s->parent_kind == 2) { ue_parent_info(c, e, 0); ue_left(c, e, s->pid); }
+    else fail(c, YMO_ERR_UNEXPECTED);
+    if (s->has_psub) ue_string(c, e, s->psub);
+  }
+  content_write(c, e, s->content, off);
+}
+
+/* sliceStruct (13.5.16 as@38661) */
+static Struct *slice_struct(Ctx *c, const Struct *s, int64_t diff) {
+  Struct *r = (Struct *)aalloc(c, sizeof(Struct));
+  *r = *s;
+  r->clock = s->clock + diff;
+  r->len = s->len - diff;
+  if (s->kind == K_ITEM) {
+    r->has_origin = 1;
+    r->origin.client = s->client; r->origin.clock = s->clock + diff - 1;
+    r->content = content_splice(c, s->content, diff);
+    r->len = content_len(r->content);
+  }
+  return r;
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* LazyStructReader (13.5.16 ts@36560 generator + es@37148)                                         */
+/* ------------------------------------------------------------------------------------------------ */
+typedef struct {
+  UDec *u;
+  int filter_skips;
+  int64_t nclients, ci;  /* outer loop */
+  int64_t nstructs, si;  /* inner loop */
+  int64_t client, clock;
+  int started, done;
+  Struct *curr;
+} LReader;
+
+static Struct *gen_next(Ctx *c, LReader *r) {
+  UDec *u = r->u;
+  if (r->done) return NULL;
+  if (!r->started) {
+    r->started = 1;
+    r->nclients = rd_vu(c, &u->rest);
+    r->ci = 0;
+    r->si = 0; r->nstructs = 0;
+  }
+  for (;;) {
+    if (r->si < r->nstructs) break;
+    if (r->ci >= r->nclients) { r->done = 1; return NULL; }
+    r->ci++;
+    r->nstructs = rd_vu(c, &u->rest);
+    r->client = ud_client(c, u);
+    r->clock = rd_vu(c, &u->rest);
+    r->si = 0;
+  }
+  r->si++;
+  Struct *s = (Struct *)aalloc(c, sizeof(Struct));
+  memset(s, 0, sizeof(*s));
+  s->client = r->client;
+  s->clock = r->clock;
+  int info = ud_info(c, u);
+  if (info == 10) {
+    s->kind = K_SKIP;
+    s->len = rd_vu(c, &u->rest);
+  } else if (info >= 0 && (info & 31) != 0) {
+    s->kind = K_ITEM;
+    int noorig = (info & (0x40 | 0x80)) == 0;
+    if (info & 0x80) { s->has_origin = 1; s->origin = ud_left(c, u); }
+    if (info & 0x40) { s->has_right = 1; s->right = ud_right(c, u); }
+    if (noorig) {
+      if (ud_parent_info(c, u)) { s->parent_kind = 1; s->pkey = ud_string(c, u); }
+      else { s->parent_kind = 2; s->pid = ud_left(c, u); }
+      if (info & 0x20) { s->has_psub = 1; s->psub = ud_string(c, u); }
+    }
+    s->content = read_content(c, u, info);
+    s->len = content_len(s->content);
+  } else {
+    s->kind = K_GC;
+    s->len = ud_len(c, u);
+  }
+  r->clock += s->len;
+  return s;
+}
+static Struct *lr_next(Ctx *c, LReader *r) {
+  do { r->curr = gen_next(c, r); } while (r->filter_skips && r->curr && r->curr->kind == K_SKIP);
+  return r->curr;
+}
+static void lr_init(Ctx *c, LReader *r, UDec *u, int filter_skips) {
+  memset(r, 0, sizeof(*r));
+  r->u = u;
+  r->filter_skips = filter_skips;
+  lr_next(c, r);
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* LazyStructWriter (13.5.16 rs / ps / gs / ws)                                                     */
+/* ------------------------------------------------------------------------------------------------ */
+typedef struct { int64_t written; Buf *rest; } Part;
+typedef struct {
+  int64_t currClient, written;
+  UEnc *enc;
+  Part *parts;
+  size_t nparts, cap;
+} LWriter;
+
+static void lw_flush(Ctx *c, LWriter *w) {
+  if (w->written > 0) {
+    if (w->nparts == w->cap) {
+      size_t cap = w->cap ? w->cap * 2 : 16;
+      Part *np = (Part *)aalloc(c, cap * sizeof(Part));
+      if (w->nparts) memcpy(np, w->parts, w->nparts * sizeof(Part));
+      w->parts = np; w->cap = cap;
+    }
+    w->parts[w->nparts].written = w->written;
+    w->parts[w->nparts].rest = w->enc->rest;
+    w->nparts++;
+    w->enc->rest = buf_new(c);
+    w->written = 0;
+  }
+}
+static void lw_write(Ctx *c, LWriter *w, const Struct *s, int64_t off) {
+  if (w->written > 0 && w->currClient != s->client) lw_flush(c, w);
+  if (w->written == 0) {
+    w->currClient = s->client;
+    ue_client(c, w->enc, s->client);
+    wr_vu(c, w->enc->rest, s->clock + off);
+  }
+  struct_write(c, w->enc, s, off);
+  w->written++;
+}
+static void lw_finish(Ctx *c, LWriter *w) {
+  lw_flush(c, w);
+  Buf *r = w->enc->rest;
+  wr_vu(c, r, (int64_t)w->nparts);
+  for (size_t i = 0; i < w->nparts; i++) {
+    wr_vu(c, r, w->parts[i].written);
+    putraw(c, r, w->parts[i].rest->p, w->parts[i].rest->n);
+  }
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* DeleteSet (DeleteSet.js:113-256; 13.5.16 le/he/fe/ge)                                            */
+/* ------------------------------------------------------------------------------------------------ */
+typedef struct { int64_t clock, len; } DItem;
+typedef struct { int64_t client; DItem *items; size_t n, cap; } DClient;
+typedef struct { DClient *cl; size_t n, cap; } DSet;
+
+static DClient *ds_get_or_add(Ctx *c, DSet *ds, int64_t client) {
+  for (size_t i = 0; i < ds->n; i++) if (ds->cl[i].client == client) return &ds->cl[i];
+  if (ds->n == ds->cap) {
+    size_t cap = ds->cap ? ds->cap * 2 : 8;
+    DClient *nc = (DClient *)aalloc(c, cap * sizeof(DClient));
+    if (ds->n) memcpy(nc, ds->cl, ds->n * sizeof(DClient));
+    ds->cl = nc; ds->cap = cap;
+  }
+  DClient *d = &ds->cl[ds->n++];
+  memset(d, 0, sizeof(*d));
+  d->client = client;
+  return d;
+}
+static void dc_push(Ctx *c, DClient *d, int64_t clock, int64_t len) {
+  if (d->n == d->cap) {
+    size_t cap = d->cap ? d->cap * 2 : 8;
+    DItem *ni = (DItem *)aalloc(c, cap * sizeof(DItem));
+    if (d->n) memcpy(ni, d->items, d->n * sizeof(DItem));
+    d->items = ni; d->cap = cap;
+  }
+  d->items[d->n].clock = clock; d->items[d->n].len = len; d->n++;
+}
+static void ds_read(Ctx *c, UDec *u, DSet *ds) { /* readDeleteSet (ge) */
+  memset(ds, 0, sizeof(*ds));
+  uint32_t n = rd_vu(c, &u->rest);
+  for (uint32_t i = 0; i < n; i++) {
+    ud_reset_ds(u);
+    int64_t client = rd_vu(c, &u->rest);
+    uint32_t m = rd_vu(c, &u->rest);
+    if (m > 0) {
+      DClient *d = ds_get_or_add(c, ds, client);
+      for (uint32_t j = 0; j < m; j++) {
+        int64_t clock = ud_ds_clock(c, u);
+        int64_t len = ud_ds_len(c, u);
+        dc_push(c, d, clock, len);
+      }
+    }
+  }
+}
+static void ds_write(Ctx *c, UEnc *e, const DSet *ds) { /* writeDeleteSet (fe) */
+  wr_vu(c, e->rest, (int64_t)ds->n);
+  for (size_t i = 0; i < ds->n; i++) {
+    ue_reset_ds(e);
+    wr_vu(c, e->rest, ds->cl[i].client);
+    wr_vu(c, e->rest, (int64_t)ds->cl[i].n);
+    for (size_t j = 0; j < ds->cl[i].n; j++) {
+      ue_ds_clock(c, e, ds->cl[i].items[j].clock);
+      ue_ds_len(c, e, ds->cl[i].items[j].len);
+    }
+  }
+}
+static void ditem_msort(DItem *a, DItem *tmp, size_t n) { /* stable by clock */
+  if (n < 2) return;
+  size_t h = n / 2;
+  ditem_msort(a, tmp, h);
+  ditem_msort(a + h, tmp, n - h);
+  size_t i = 0, j = h, k = 0;
+  while (i < h && j < n) tmp[k++] = (a[j].clock < a[i].clock) ? a[j++] : a[i++];
+  while (i < h) tmp[k++] = a[i++];
+  while (j < n) tmp[k++] = a[j++];
+  memcpy(a, tmp, n * sizeof(DItem));
+}
+static void ds_sort_and_merge(Ctx *c, DSet *ds) { /* sortAndMergeDeleteSet (le) */
+  for (size_t ci = 0; ci < ds->n; ci++) {
+    DClient *d = &ds->cl[ci];
+    if (d->n > 1) {
+      DItem *tmp = (DItem *)aalloc(c, d->n * sizeof(DItem));
+      ditem_msort(d->items, tmp, d->n);
+    }
+    size_t i, j;
+    for (i = 1, j = 1; i < d->n; i++) {
+      DItem *left = &d->items[j - 1];
+      DItem right = d->items[i];
+      if (left->clock + left->len >= right.clock) {
+        int64_t m = right.clock + right.len - left->clock;
+        if (m > left->len) left->len = m;
+      } else {
+        if (j < i) d->items[j] = right;
+        j++;
+      }
+    }
+    if (d->n > 0) d->n = j;
+  }
+}
+static void ds_merge(Ctx *c, DSet *dss, size_t k, DSet *out) { /* mergeDeleteSets (he) */
+  memset(out, 0, sizeof(*out));
+  for (size_t i = 0; i < k; i++) {
+    for (size_t ci = 0; ci < dss[i].n; ci++) {
+      int64_t client = dss[i].cl[ci].client;
+      int have = 0;
+      for (size_t q = 0; q < out->n; q++) if (out->cl[q].client == client) { have = 1; break; }
+      if (have) continue;
+      DClient *d = ds_get_or_add(c, out, client);
+      for (size_t j = i; j < k; j++) {
+        for (size_t cj = 0; cj < dss[j].n; cj++) {
+          if (dss[j].cl[cj].client != client) continue;
+          for (size_t t = 0; t < dss[j].cl[cj].n; t++) dc_push(c, d, dss[j].cl[cj].items[t].clock, dss[j].cl[cj].items[t].len);
+        }
+      }
+    }
+  }
+  ds_sort_and_merge(c, out);
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* mergeUpdatesV2 (13.5.16 ds@39007)                                                                */
+/* ------------------------------------------------------------------------------------------------ */
+/* reader comparator (dec1, dec2) */
+static int reader_cmp(Ctx *c, const LReader *a, const LReader *b) {
+  const Struct *x = a->curr, *y = b->curr;
+  if (x->client == y->client) {
+    int64_t d = x->clock - y->clock;
+    if (d == 0) {
+      int cx = x->kind, cy = y->kind;
+      if (cx == cy) return 0;
+      if (cx != K_SKIP && cy != K_SKIP) c->inconsistent_cmp = 1;
+      return cx == K_SKIP ? 1 : -1;
+    }
+    return d < 0 ? -1 : 1;
+  }
+  return y->client - x->client < 0 ? -1 : 1;
+}
+
+/* V8 TimSort for n < 64: CountAndMakeRun + BinaryInsertionSort (third_party/v8/builtins/array-sort.tq) */
+static void v8_sort(Ctx *c, LReader **a, size_t n, LReader **tmp) {
+  if (n < 2) return;
+  if (n < 64) {
+    size_t run = 2;
+    int order = reader_cmp(c, a[1], a[0]);
+    int desc = order < 0;
+    LReader *prev = a[1];
+    for (size_t i = 2; i < n; i++) {
+      order = reader_cmp(c, a[i], prev);
+      if (desc) { if (order >= 0) break; }
+      else if (order < 0) break;
+      prev = a[i];
+      run++;
+    }
+    if (desc) for (size_t i = 0, j = run - 1; i < j; i++, j--) { LReader *t = a[i]; a[i] = a[j]; a[j] = t; }
+    for (size_t start = run; start < n; start++) {
+      LReader *pivot = a[start];
+      size_t left = 0, right = start;
+      while (left < right) {
+        size_t mid = left + ((right - left) >> 1);
+        if (reader_cmp(c, pivot, a[mid]) < 0) right = mid; else left = mid + 1;
+      }
+      for (size_t p = start; p > left; p--) a[p] = a[p - 1];
+      a[left] = pivot;
+    }
+    return;
+  }
+  /* stable merge sort (exact for a consistent comparator) */
+  int saved = c->inconsistent_cmp;
+  c->inconsistent_cmp = 0;
+  size_t h = n / 2;
+  v8_sort(c, a, h, tmp);
+  v8_sort(c, a + h, n - h, tmp);
+  size_t i = 0, j = h, k = 0;
+  while (i < h && j < n) tmp[k++] = (reader_cmp(c, a[j], a[i]) < 0) ? a[j++] : a[i++];
+  while (i < h) tmp[k++] = a[i++];
+  while (j < n) tmp[k++] = a[j++];
+  memcpy(a, tmp, n * sizeof(LReader *));
+  if (c->inconsistent_cmp) c->big_inconsistent = 1;
+  c->inconsistent_cmp = saved;
+}
+
+static int struct_merge_with(Struct *cur, const Struct *s) { /* GC/Skip.mergeWith; Item never merges */
+  if (cur->kind == K_ITEM) return 0;
+  if (cur->kind != s->kind) return 0;
+  cur->len += s->len;
+  return 1;
+}
+
+static Buf *merge_impl(Ctx *c, const uint8_t *const *upds, const size_t *lens, size_t n, int v2) {
+  UDec *decs = (UDec *)aalloc(c, (n + 1) * sizeof(UDec));
+  for (size_t i = 0; i < n; i++) udec_init(c, &decs[i], upds[i], lens[i], v2);
+  LReader *rs = (LReader *)aalloc(c, (n + 1) * sizeof(LReader));
+  for (size_t i = 0; i < n; i++) lr_init(c, &rs[i], &decs[i], 1);
+  LReader **arr = (LReader **)aalloc(c, (n + 1) * sizeof(LReader *));
+  LReader **tmp = (LReader **)aalloc(c, (n + 1) * sizeof(LReader *));
+  size_t na = n;
+  for (size_t i = 0; i < n; i++) arr[i] = &rs[i];
+  UEnc enc;
+  uenc_init(c, &enc, v2);
+  LWriter w;
+  memset(&w, 0, sizeof(w));
+  w.enc = &enc;
+  Struct *cur = NULL;
+  for (;;) {
+    size_t k = 0;
+    for (size_t i = 0; i < na; i++) if (arr[i]->curr) arr[k++] = arr[i];
+    na = k;
+    v8_sort(c, arr, na, tmp);
+    if (na == 0) break;
+    LReader *R = arr[0];
+    int64_t first_client = R->curr->client;
+    if (cur) {
+      Struct *s = R->curr;
+      int iterated = 0;
+      while (s && s->clock + s->len <= cur->clock + cur->len && s->client >= cur->client) {
+        s = lr_next(c, R);
+        iterated = 1;
+      }
+      if (!s || s->client != first_client || (iterated && s->clock > cur->clock + cur->len)) continue;
+      if (first_client != cur->client) {
+        lw_write(c, &w, cur, 0);
+        cur = s;
+        lr_next(c, R);
+      } else if (cur->clock + cur->len < s->clock) {
+        if (cur->kind == K_SKIP) {
+          cur->len = s->clock + s->len - cur->clock;
+        } else {
+          lw_write(c, &w, cur, 0);
+          int64_t diff = s->clock - cur->clock - cur->len;
+          Struct *sk = (Struct *)aalloc(c, sizeof(Struct));
+          memset(sk, 0, sizeof(*sk));
+          sk->kind = K_SKIP; sk->client = first_client; sk->clock = cur->clock + cur->len; sk->len = diff;
+          cur = sk;
+        }
+      } else {
+        int64_t d = cur->clock + cur->len - s->clock;
+        if (d > 0) {
+          if (cur->kind == K_SKIP) cur->len -= d;
+          else s = slice_struct(c, s, d);
+        }
+        if (!struct_merge_with(cur, s)) {
+          lw_write(c, &w, cur, 0);
+          cur = s;
+          lr_next(c, R);
+        }
+      }
+    } else {
+      cur = R->curr;
+      lr_next(c, R);
+    }
+    for (Struct *nx = R->curr; nx && nx->client == first_client && nx->clock == cur->clock + cur->len && nx->kind != K_SKIP;
+         nx = lr_next(c, R)) {
+      lw_write(c, &w, cur, 0);
+      cur = nx;
+    }
+  }
+  if (cur) lw_write(c, &w, cur, 0);
+  lw_finish(c, &w);
+  if (c->big_inconsistent) fail(c, YMO_ERR_UNSUPPORTED);
+  DSet *dss = (DSet *)aalloc(c, (n + 1) * sizeof(DSet));
+  for (size_t i = 0; i < n; i++) ds_read(c, &decs[i], &dss[i]);
+  DSet merged;
+  ds_merge(c, dss, n, &merged);
+  ds_write(c, &enc, &merged);
+  return uenc_finish(c, &enc);
+}
+
+/* decodeStateVector (encoding.js:536-565; 13.5.16 Fe/Ve) */
+typedef struct { int64_t client, clock; } SVE;
+typedef struct { SVE *e; size_t n; } SV;
+static void sv_decode(Ctx *c, const uint8_t *p, size_t n, SV *sv) {
+  Dec d = {p, n, 0};
+  uint32_t cnt = rd_vu(c, &d);
+  sv->e = (SVE *)aalloc(c, ((size_t)(cnt < 1u << 20 ? cnt : 1u << 20) + 1) * sizeof(SVE));
+  sv->n = 0;
+  size_t cap = (cnt < 1u << 20 ? cnt : 1u << 20) + 1;
+  for (uint32_t i = 0; i < cnt; i++) {
+    int64_t client = rd_vu(c, &d);
+    int64_t clock = rd_vu(c, &d);
+    size_t j;
+    for (j = 0; j < sv->n; j++) if (sv->e[j].client == client) break;
+    if (j == sv->n) {
+      if (sv->n == cap) {
+        SVE *ne = (SVE *)aalloc(c, cap * 2 * sizeof(SVE));
+        memcpy(ne, sv->e, sv->n * sizeof(SVE));
+        sv->e = ne; cap *= 2;
+      }
+      sv->e[sv->n].client = client; sv->n++;
+    }
+    sv->e[j].clock = clock;
+  }
+}
+static int64_t sv_get(const SV *sv, int64_t client) {
+  for (size_t j = 0; j < sv->n; j++) if (sv->e[j].client == client) return sv->e[j].clock;
+  return 0;
+}
+
+/* diffUpdateV2 (13.5.16 us@40707) */
+static Buf *diff_impl(Ctx *c, const uint8_t *upd, size_t len, const uint8_t *svb, size_t svlen, int v2) {
+  SV sv;
+  sv_decode(c, svb, svlen, &sv);
+  UEnc enc;
+  uenc_init(c, &enc, v2);
+  LWriter w;
+  memset(&w, 0, sizeof(w));
+  w.enc = &enc;
+  UDec dec;
+  udec_init(c, &dec, upd, len, v2);
+  LReader r;
+  lr_init(c, &r, &dec, 0);
+  while (r.curr) {
+    Struct *t = r.curr;
+    int64_t client = t->client;
+    int64_t k = sv_get(&sv, client);
+    if (t->kind == K_SKIP) { lr_next(c, &r); continue; }
+    if (t->clock + t->len > k) {
+      int64_t off = k - t->clock;
+      if (off < 0) off = 0;
+      lw_write(c, &w, t, off);
+      lr_next(c, &r);
+      while (r.curr && r.curr->client == client) { lw_write(c, &w, r.curr, 0); lr_next(c, &r); }
+    } else {
+      while (r.curr && r.curr->client == client && r.curr->clock + r.curr->len <= k) lr_next(c, &r);
+    }
+  }
+  lw_finish(c, &w);
+  DSet ds;
+  ds_read(c, &dec, &ds);
+  ds_write(c, &enc, &ds);
+  return uenc_finish(c, &enc);
+}
+
+/* encodeStateVectorFromUpdateV2 (13.5.16 os@37724) */
+static Buf *sv_impl(Ctx *c, const uint8_t *upd, size_t len, int v2) {
+  Buf *rest = buf_new(c);
+  UDec dec;
+  udec_init(c, &dec, upd, len, v2);
+  LReader r;
+  lr_init(c, &r, &dec, 0);
+  Struct *i = r.curr;
+  Buf *out = buf_new(c);
+  if (i) {
+    int64_t cnt = 0;
+    int64_t client = i->client;
+    int stop = i->clock != 0;
+    int64_t clock = stop ? 0 : i->clock + i->len;
+    for (; i; i = lr_next(c, &r)) {
+      if (client != i->client) {
+        if (clock != 0) { cnt++; wr_vu(c, rest, client); wr_vu(c, rest, clock); }
+        client = i->client;
+        clock = 0;
+        stop = i->clock != 0;
+      }
+      if (i->kind == K_SKIP) stop = 1;
+      if (!stop) clock = i->clock + i->len;
+    }
+    if (clock != 0) { cnt++; wr_vu(c, rest, client); wr_vu(c, rest, clock); }
+    wr_vu(c, out, cnt);
+    putraw(c, out, rest->p, rest->n);
+  } else {
+    wr_vu(c, out, 0);
+  }
+  return out;
+}
+
+/* ------------------------------------------------------------------------------------------------ */
+/* public API                                                                                      */
+/* ------------------------------------------------------------------------------------------------ */
+static int finish_out(Ctx *c, Buf *b, uint8_t **out, size_t *out_len) {
+  *out = (uint8_t *)malloc(b->n ? b->n : 1);
+  if (!*out) return YMO_ERR_UNSUPPORTED;
+  memcpy(*out, b->p, b->n);
+  *out_len = b->n;
+  (void)c;
+  return YMO_OK;
+}
+
+int ymo_merge(const uint8_t *const *upds, const size_t *lens, size_t n, int fmt, uint8_t **out, size_t *out_len) {
+  *out = NULL; *out_len = 0;
+  if (n == 1) { /* identity: `if (updates.length === 1) return updates[0]` */
+    *out = (uint8_t *)malloc(lens[0] ? lens[0] : 1);
+    memcpy(*out, upds[0], lens[0]);
+    *out_len = lens[0];
+    return YMO_OK;
+  }
+  Ctx c;
+  memset(&c, 0, sizeof(c));
+  int code = setjmp(c.jb);
+  if (code) { ctx_free(&c); return code; }
+  Buf *b = merge_impl(&c, upds, lens, n, fmt == 2);
+  int rc = finish_out(&c, b, out, out_len);
+  ctx_free(&c);
+  return rc;
+}
+
+int ymo_diff(const uint8_t *upd, size_t len, const uint8_t *sv, size_t sv_len, int fmt, uint8_t **out, size_t *out_len) {
+  *out = NULL; *out_len = 0;
+  Ctx c;
+  memset(&c, 0, sizeof(c));
+  int code = setjmp(c.jb);
+  if (code) { ctx_free(&c); return code; }
+  Buf *b = diff_impl(&c, upd, len, sv, sv_len, fmt == 2);
+  int rc = finish_out(&c, b, out, out_len);
+  ctx_free(&c);
+  return rc;
+}
+
+int ymo_sv_from_update(const uint8_t *upd, size_t len, int fmt, uint8_t **out, size_t *out_len) {
+  *out = NULL; *out_len = 0;
+  Ctx c;
+  memset(&c, 0, sizeof(c));
+  int code = setjmp(c.jb);
+  if (code) { ctx_free(&c); return code; }
+  Buf *b = sv_impl(&c, upd, len, fmt == 2);
+  int rc = finish_out(&c, b, out, out_len);
+  ctx_free(&c);
+  return rc;
+}
+
+void ymo_free(void *p) { free(p); }
+
+/* ------------------------------------------------------------------------------------------------ */
+/* batched host baseline (one worker thread per core, docs dealt round-robin)                       */
+/* ------------------------------------------------------------------------------------------------ */
+typedef struct {
+  int op, fmt;
+  const uint8_t *arena; const uint64_t *upd_off; const uint32_t *doc_upd; uint32_t n_docs;
+  const uint8_t *sv_arena; const uint64_t *sv_off;
+  uint8_t *out_arena; const uint64_t *out_cap_off; uint64_t *out_len; int32_t *status;
+  int tid, nthreads;
+  int nerr;
+} BatchJob;
+
+static void *batch_worker(void *arg) {
+  BatchJob *j = (BatchJob *)arg;
+  size_t cap_ptrs = 64;
+  const uint8_t **ptrs = (const uint8_t **)malloc(cap_ptrs * sizeof(*ptrs));
+  size_t *lens = (size_t *)malloc(cap_ptrs * sizeof(*lens));
+  for (uint32_t d = (uint32_t)j->tid; d < j->n_docs; d += (uint32_t)j->nthreads) {
+    uint32_t u0 = j->doc_upd[d], u1 = j->doc_upd[d + 1];
+    size_t n = u1 - u0;
+    if (n > cap_ptrs) {
+      cap_ptrs = n * 2;
+      ptrs = (const uint8_t **)realloc(ptrs, cap_ptrs * sizeof(*ptrs));
+      lens = (size_t *)realloc(lens, cap_ptrs * sizeof(*lens));
+    }
+    for (size_t i = 0; i < n; i++) {
+      ptrs[i] = j->arena + j->upd_off[u0 + i];
+      lens[i] = (size_t)(j->upd_off[u0 + i + 1] - j->upd_off[u0 + i]);
+    }
+    uint8_t *out = NULL;
+    size_t olen = 0;
+    int st;
+    if (j->op == 0) st = ymo_merge(ptrs, lens, n, j->fmt, &out, &olen);
+    else if (j->op == 1) {
+      const uint8_t *sv = j->sv_arena + j->sv_off[d];
+      size_t svl = (size_t)(j->sv_off[d + 1] - j->sv_off[d]);
+      st = n >= 1 ? ymo_diff(ptrs[0], lens[0], sv, svl, j->fmt, &out, &olen) : YMO_ERR_UNEXPECTED;
+    } else st = n >= 1 ? ymo_sv_from_update(ptrs[0], lens[0], j->fmt, &out, &olen) : YMO_ERR_UNEXPECTED;
+    if (st == YMO_OK && j->out_arena) {
+      uint64_t cap = j->out_cap_off[d + 1] - j->out_cap_off[d];
+      if (olen > cap) st = YMO_ERR_CAPACITY;
+      else memcpy(j->out_arena + j->out_cap_off[d], out, olen);
+    }
+    free(out);
+    j->out_len[d] = olen;
+    j->status[d] = st;
+    if (st) j->nerr++;
+  }
+  free(ptrs);
+  free(lens);
+  return NULL;
+}
+
+int ymo_batch(int op, int fmt, const uint8_t *arena, const uint64_t *upd_off, const uint32_t *doc_upd,
+              uint32_t n_docs, const uint8_t *sv_arena, const uint64_t *sv_off, int nthreads,
+              uint8_t *out_arena, const uint64_t *out_cap_off, uint64_t *out_len, int32_t *status) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  BatchJob jobs[256];
+  pthread_t th[256];
+  for (int t = 0; t < nthreads; t++) {
+    BatchJob b = {op, fmt, arena, upd_off, doc_upd, n_docs, sv_arena, sv_off, out_arena, out_cap_off, out_len, status, t, nthreads, 0};
+    jobs[t] = b;
+  }
+  if (nthreads == 1) batch_worker(&jobs[0]);
+  else {
+    for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, batch_worker, &jobs[t]);
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+  }
+  int nerr = 0;
+  for (int t = 0; t < nthreads; t++) nerr += jobs[t].nerr;
+  return nerr;
+}
