@@ -1,0 +1,94 @@
+/*
+ * ymerge.h -- C ABI of libymerge.so, the MI355X-native batched Yjs update engine.
+ *
+ * Drop-in boundary for the yjs binary update layer.  Each entry point is the batched form of one
+ * yjs function; the per-document semantics (bytes in, bytes out, errors) are those of yjs 13.5.16,
+ * whose wire format is gaberogan/yjs@v0's (src/utils/UpdateEncoder.js, UpdateDecoder.js):
+ *
+ *   ym_merge(fmt=1)  <- Y.mergeUpdates(updates)            (yjs 13.5.16 `is`; public API beside
+ *   ym_merge(fmt=2)  <- Y.mergeUpdatesV2(updates)           /root/reference/src/index.js:53-67)
+ *   ym_diff(fmt=1)   <- Y.diffUpdate(update, stateVector)   (13.5.16 `fs`; reference composition:
+ *   ym_diff(fmt=2)   <- Y.diffUpdateV2(update, sv)            src/utils/encoding.js:462-526)
+ *   ym_sv(fmt=1|2)   <- Y.encodeStateVectorFromUpdate[V2]    (13.5.16 `cs`/`os`; reference composition:
+ *                                                             src/utils/encoding.js:587-611)
+ *
+ * All pointers are plain byte/offset arrays; no framework types cross this boundary.  `mem` says
+ * where every array of a batch lives: YM_MEM_HOST (the library stages it through pinned memory) or
+ * YM_MEM_DEVICE (already resident in HBM on the selected device -- the throughput path).
+ *
+ * Batch layout: document d owns updates doc_upd[d] .. doc_upd[d+1]-1; update u is the byte range
+ * arena[upd_off[u] .. upd_off[u+1]).  For ym_diff, doc d's state vector is
+ * sv_arena[sv_off[d] .. sv_off[d+1]) and doc d must own exactly one update.
+ *
+ * Results: out_off[d] / out_len[d] locate doc d's output inside out_arena (outputs are densely
+ * packed but not necessarily in document order); status[d] is a YM_* code.  A doc whose status is
+ * not YM_OK has out_len[d] = 0.  Errors are per document; the batch always completes.
+ */
+#ifndef YMERGE_H
+#define YMERGE_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* per-document status codes (the JS wrapper rethrows the matching yjs exception) */
+enum {
+  YM_OK = 0,
+  YM_ERR_INT_RANGE = 1,   /* Error('Integer out of range!')  (lib0 readVarUint / truncated input)  */
+  YM_ERR_UNEXPECTED = 2,  /* Error('Unexpected case')                                            */
+  YM_ERR_URI = 3,         /* URIError('URI malformed')       (invalid UTF-8 / split surrogate)    */
+  YM_ERR_TYPE = 4,        /* TypeError                       (unknown content ref, typeRef, tag)  */
+  YM_ERR_RANGE = 5,       /* RangeError                      (truncated string / typed array)     */
+  YM_ERR_SYNTAX = 6,      /* SyntaxError                     (JSON.parse of a V1 JSON field)      */
+  YM_ERR_UNSUPPORTED = 7, /* valid input needing a canonicalisation the engine does not implement */
+  YM_ERR_METHOD = 8,      /* Error('Method unimplemented')                                       */
+  YM_ERR_CAPACITY = 9,    /* output arena too small: call again with a larger cap                */
+};
+
+enum { YM_MEM_HOST = 0, YM_MEM_DEVICE = 1 };
+enum { YM_V1 = 1, YM_V2 = 2 };
+
+typedef struct ym_batch {
+  const uint8_t *arena;    /* concatenated update bytes                                   */
+  const uint64_t *upd_off; /* n_upd + 1 byte offsets into arena                           */
+  const uint32_t *doc_upd; /* n_docs + 1 update-index ranges                              */
+  uint32_t n_docs;
+  uint32_t n_upd;
+  int32_t format;          /* YM_V1 | YM_V2                                               */
+  int32_t mem;             /* YM_MEM_HOST | YM_MEM_DEVICE (applies to every array here)   */
+  const uint8_t *sv_arena; /* ym_diff only: concatenated encoded state vectors            */
+  const uint64_t *sv_off;  /* ym_diff only: n_docs + 1                                    */
+} ym_batch;
+
+typedef struct ym_out {
+  uint8_t *arena;    /* output bytes, capacity `cap` (same memory kind as the batch)      */
+  uint64_t cap;
+  uint64_t *out_off; /* n_docs                                                            */
+  uint64_t *out_len; /* n_docs                                                            */
+  int32_t *status;   /* n_docs                                                            */
+  uint64_t used;     /* filled in: bytes of `arena` used (if > cap, retry with cap=used)  */
+} ym_out;
+
+/* per-call statistics (also reduced across ranks by the benchmark over RCCL) */
+typedef struct ym_stats {
+  uint64_t docs, docs_fast, docs_general, docs_error;
+  uint64_t bytes_in, bytes_out;
+  double device_ms; /* device time of the call (HIP events on the call's stream) */
+} ym_stats;
+
+int ym_init(int device);           /* select the HIP device for this thread; 0 on success */
+int ym_shutdown(void);
+const char *ym_strerror(int code); /* message of a status / return code */
+uint64_t ym_out_bound(const ym_batch *b); /* a capacity that is normally sufficient for ym_* */
+
+/* stream: a hipStream_t (NULL = the library's stream for the device).  Return value: 0, or
+ * YM_ERR_CAPACITY when out->used > out->cap (nothing useful was written), or a negative HIP error. */
+int ym_merge(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
+int ym_diff(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
+int ym_sv(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

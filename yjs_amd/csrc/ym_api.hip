@@ -1,0 +1,339 @@
+// ym_api.hip -- host side of libymerge.so: the C ABI of include/ymerge.h.
+//
+// Per call: (1) the LDS fast path (ym_fast.hip) takes every document it can prove simple and writes
+// its output; (2) the remaining documents are compacted into a list and run through the general
+// path (ym_general.hip) with an HBM workspace sized by an exclusive scan; (3) outputs are bump-
+// allocated in the caller's arena.  Host-memory batches are staged through device buffers.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <mutex>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+
+#include "../../include/ymerge.h"
+#include "ym_kernels.h"
+
+namespace ymk {
+__global__ void k_general_ws(GeneralJob j, uint64_t *ws_size);
+__global__ void k_general(GeneralJob j, int pass);
+int fast_launch(uint32_t op, const GeneralJob &j, hipStream_t st);  // ym_fast.hip
+}  // namespace ymk
+
+using namespace ymk;
+
+namespace {
+
+#define HIPCHK(x)                                   \
+  do {                                              \
+    hipError_t e_ = (x);                            \
+    if (e_ != hipSuccess) return -(int)e_ - 1000;   \
+  } while (0)
+
+struct DBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t n) {
+    if (n <= cap) return 0;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = n + n / 4 + 4096;
+    if (hipMalloc(&p, want) != hipSuccess) return -1;
+    cap = want;
+    return 0;
+  }
+  template <class T> T *as() const { return (T *)p; }
+};
+
+struct DevState {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  DBuf ws, ws_size, ws_off, layout, counters, scan_tmp, list_a, list_b, flags;
+  DBuf in_arena, in_off, in_doc, in_sv, in_svoff, out_arena, out_off, out_len, status;  // host staging
+  uint64_t *pinned = nullptr;
+};
+
+thread_local DevState *g_state = nullptr;
+std::mutex g_mu;
+
+DevState *state() {
+  if (!g_state) {
+    g_state = new DevState();
+    int dev = 0;
+    const char *env = getenv("YMERGE_DEVICE");
+    if (env) dev = atoi(env);
+    else hipGetDevice(&dev);
+    g_state->device = dev;
+  }
+  if (!g_state->stream) {
+    hipSetDevice(g_state->device);
+    hipStreamCreateWithFlags(&g_state->stream, hipStreamNonBlocking);
+    hipEventCreate(&g_state->ev0);
+    hipEventCreate(&g_state->ev1);
+    hipHostMalloc((void **)&g_state->pinned, 64 * sizeof(uint64_t), hipHostMallocDefault);
+  }
+  return g_state;
+}
+
+__global__ void k_status_flags(const uint32_t *list, uint32_t n, const int32_t *status, int want, uint8_t *flags) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t d = list ? list[i] : i;
+  flags[i] = status[d] == want;
+}
+
+__global__ void k_stats(const int32_t *status, const uint64_t *out_len, uint32_t n, uint64_t *acc) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t err = 0, bytes = 0;
+  if (i < n) {
+    err = status[i] != 0;
+    bytes = status[i] == 0 ? out_len[i] : 0;
+  }
+  // wave reduction then one atomic per wave
+  for (int o = 32; o > 0; o >>= 1) {
+    err += __shfl_down(err, o, 64);
+    bytes += __shfl_down(bytes, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd((unsigned long long *)&acc[0], (unsigned long long)err);
+    atomicAdd((unsigned long long *)&acc[1], (unsigned long long)bytes);
+  }
+}
+
+__global__ void k_in_bytes(const uint64_t *upd_off, uint32_t n_upd, uint64_t *acc) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) acc[2] = upd_off[n_upd] - upd_off[0];
+}
+
+// Compacts the ids of listed docs whose status == want into `dst`; returns the count.
+int select_docs(DevState *S, hipStream_t st, const uint32_t *list, uint32_t n, const int32_t *status, int want,
+                uint32_t *dst, uint32_t *count_out) {
+  if (S->flags.ensure(n + 1)) return -1;
+  k_status_flags<<<(n + 255) / 256, 256, 0, st>>>(list, n, status, want, S->flags.as<uint8_t>());
+  uint32_t *d_num = S->counters.as<uint32_t>() + 8;
+  size_t tmp = 0;
+  if (list) hipcub::DeviceSelect::Flagged(nullptr, tmp, list, S->flags.as<uint8_t>(), dst, d_num, n, st);
+  else hipcub::DeviceSelect::Flagged(nullptr, tmp, hipcub::CountingInputIterator<uint32_t>(0), S->flags.as<uint8_t>(), dst, d_num, n, st);
+  if (S->scan_tmp.ensure(tmp + 16)) return -1;
+  if (list) hipcub::DeviceSelect::Flagged(S->scan_tmp.p, tmp, list, S->flags.as<uint8_t>(), dst, d_num, n, st);
+  else hipcub::DeviceSelect::Flagged(S->scan_tmp.p, tmp, hipcub::CountingInputIterator<uint32_t>(0), S->flags.as<uint8_t>(), dst, d_num, n, st);
+  HIPCHK(hipMemcpyAsync(S->pinned, d_num, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  *count_out = (uint32_t)(S->pinned[0] & 0xffffffffu);
+  return 0;
+}
+
+// Runs the general path over `list` (n docs); retries docs whose part table overflowed.
+int run_general(DevState *S, hipStream_t st, GeneralJob j, uint32_t *list, uint32_t n) {
+  uint32_t parts_mul = 1;
+  for (int round = 0; n > 0; round++) {
+    j.list = list;
+    j.n = n;
+    j.parts_mul = parts_mul;
+    if (S->ws_size.ensure((size_t)(n + 1) * 8) || S->ws_off.ensure((size_t)(n + 1) * 8)) return -1;
+    k_general_ws<<<(n + 255) / 256, 256, 0, st>>>(j, S->ws_size.as<uint64_t>());
+    size_t tmp = 0;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, S->ws_size.as<uint64_t>(), S->ws_off.as<uint64_t>(), n, st);
+    if (S->scan_tmp.ensure(tmp + 16)) return -1;
+    hipcub::DeviceScan::ExclusiveSum(S->scan_tmp.p, tmp, S->ws_size.as<uint64_t>(), S->ws_off.as<uint64_t>(), n, st);
+    HIPCHK(hipMemcpyAsync(S->pinned, S->ws_off.as<uint64_t>() + (n - 1), 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(S->pinned + 1, S->ws_size.as<uint64_t>() + (n - 1), 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    uint64_t ws_total = S->pinned[0] + S->pinned[1];
+    if (S->ws.ensure(ws_total + 64)) return -2;
+    j.ws = S->ws.as<uint8_t>();
+    j.ws_off = S->ws_off.as<uint64_t>();
+    HIPCHK(hipMemsetAsync(j.counter_retry, 0, 4, st));
+    uint32_t blocks = (n + 63) / 64;
+    k_general<<<blocks, 64, 0, st>>>(j, 1);
+    k_general<<<blocks, 64, 0, st>>>(j, 2);
+    HIPCHK(hipMemcpyAsync(S->pinned, j.counter_retry, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    uint32_t nretry = (uint32_t)(S->pinned[0] & 0xffffffffu);
+    if (nretry == 0 || round >= 6) break;
+    uint32_t *next = list == S->list_a.as<uint32_t>() ? S->list_b.as<uint32_t>() : S->list_a.as<uint32_t>();
+    uint32_t cnt = 0;
+    if (select_docs(S, st, list, n, j.status, ym::ST_RETRY, next, &cnt)) return -1;
+    list = next;
+    n = cnt;
+    parts_mul *= 8;
+  }
+  return 0;
+}
+
+int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) {
+  if (!b || !out) return -1;
+  DevState *S = state();
+  hipStream_t st = stream ? (hipStream_t)stream : S->stream;
+  uint32_t nd = b->n_docs;
+  if (stats) memset(stats, 0, sizeof(*stats));
+  if (nd == 0) { out->used = 0; return 0; }
+  const uint8_t *A = b->arena;
+  const uint64_t *upd_off = b->upd_off;
+  const uint32_t *doc_upd = b->doc_upd;
+  const uint8_t *svp = b->sv_arena;
+  const uint64_t *sv_off = b->sv_off;
+  uint8_t *o_arena = out->arena;
+  uint64_t *o_off = out->out_off, *o_len = out->out_len;
+  int32_t *o_status = out->status;
+  bool host = b->mem == YM_MEM_HOST;
+  if (host) {  // stage inputs
+    uint64_t abytes = upd_off[b->n_upd];
+    if (S->in_arena.ensure(abytes + 16) || S->in_off.ensure((b->n_upd + 1) * 8ull) || S->in_doc.ensure((nd + 1) * 4ull)) return -2;
+    HIPCHK(hipMemcpyAsync(S->in_arena.p, A, abytes, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(S->in_off.p, upd_off, (b->n_upd + 1) * 8ull, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(S->in_doc.p, doc_upd, (nd + 1) * 4ull, hipMemcpyHostToDevice, st));
+    A = S->in_arena.as<uint8_t>();
+    upd_off = S->in_off.as<uint64_t>();
+    doc_upd = S->in_doc.as<uint32_t>();
+    if (op == OP_DIFF) {
+      uint64_t sb = sv_off[nd];
+      if (S->in_sv.ensure(sb + 16) || S->in_svoff.ensure((nd + 1) * 8ull)) return -2;
+      HIPCHK(hipMemcpyAsync(S->in_sv.p, svp, sb, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(S->in_svoff.p, sv_off, (nd + 1) * 8ull, hipMemcpyHostToDevice, st));
+      svp = S->in_sv.as<uint8_t>();
+      sv_off = S->in_svoff.as<uint64_t>();
+    }
+    if (S->out_arena.ensure(out->cap + 16) || S->out_off.ensure(nd * 8ull) || S->out_len.ensure(nd * 8ull) ||
+        S->status.ensure(nd * 4ull))
+      return -2;
+    o_arena = S->out_arena.as<uint8_t>();
+    o_off = S->out_off.as<uint64_t>();
+    o_len = S->out_len.as<uint64_t>();
+    o_status = S->status.as<int32_t>();
+  }
+  if (S->layout.ensure(nd * sizeof(ym::Layout) + 16) || S->counters.ensure(256) || S->list_a.ensure((nd + 1) * 4ull) ||
+      S->list_b.ensure((nd + 1) * 4ull))
+    return -2;
+  uint64_t *counters = S->counters.as<uint64_t>();
+  HIPCHK(hipMemsetAsync(counters, 0, 256, st));
+  HIPCHK(hipEventRecord(S->ev0, st));
+
+  GeneralJob j;
+  memset(&j, 0, sizeof(j));
+  j.A = A;
+  j.upd_off = upd_off;
+  j.doc_upd = doc_upd;
+  j.sv = svp;
+  j.sv_off = sv_off;
+  j.op = op;
+  j.v2 = b->format == YM_V2;
+  j.layout = S->layout.as<ym::Layout>();
+  j.status = o_status;
+  j.out = o_arena;
+  j.cap = out->cap;
+  j.out_off = o_off;
+  j.out_len = o_len;
+  j.used = counters + 0;
+  j.counter_retry = (uint32_t *)(counters + 1);
+  j.n = nd;
+
+  // (1) fast path over every document; leaves status ST_PENDING where it declines
+  int fr = fast_launch(op, j, st);
+  if (fr < 0) return fr;
+  uint32_t ngen = nd;
+  uint32_t *list = nullptr;
+  if (fr == 1) {  // the fast path ran: select the declined docs
+    if (select_docs(S, st, nullptr, nd, o_status, ST_PENDING, S->list_a.as<uint32_t>(), &ngen)) return -1;
+    list = S->list_a.as<uint32_t>();
+  }
+  // (2) general path over the rest
+  if (ngen > 0) {
+    int r = run_general(S, st, j, list, ngen);
+    if (r) return r;
+  }
+  HIPCHK(hipEventRecord(S->ev1, st));
+  // (3) bookkeeping
+  if (stats) {
+    k_stats<<<(nd + 255) / 256, 256, 0, st>>>(o_status, o_len, nd, counters + 4);
+    k_in_bytes<<<1, 1, 0, st>>>(upd_off, b->n_upd, counters + 4);
+    HIPCHK(hipMemcpyAsync(S->pinned + 8, counters + 4, 24, hipMemcpyDeviceToHost, st));
+  }
+  HIPCHK(hipMemcpyAsync(S->pinned, counters, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  uint64_t used = S->pinned[0];
+  out->used = used;
+  if (stats) {
+    float ms = 0;
+    hipEventElapsedTime(&ms, S->ev0, S->ev1);
+    stats->device_ms = ms;
+    stats->docs = nd;
+    stats->docs_general = ngen;
+    stats->docs_fast = nd - ngen;
+    stats->docs_error = S->pinned[8];
+    stats->bytes_out = S->pinned[9];
+    stats->bytes_in = S->pinned[10];
+  }
+  if (used > out->cap) return YM_ERR_CAPACITY;
+  if (host) {
+    HIPCHK(hipMemcpyAsync(out->arena, o_arena, used, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(out->out_off, o_off, nd * 8ull, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(out->out_len, o_len, nd * 8ull, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(out->status, o_status, nd * 4ull, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ym_init(int device) {
+  std::lock_guard<std::mutex> g(g_mu);
+  if (hipSetDevice(device) != hipSuccess) return -1;
+  if (g_state && g_state->device != device) { g_state = nullptr; }
+  if (!g_state) { g_state = new DevState(); g_state->device = device; }
+  state();
+  return 0;
+}
+
+int ym_shutdown(void) {
+  if (!g_state) return 0;
+  DevState *S = g_state;
+  hipStreamSynchronize(S->stream);
+  DBuf *bufs[] = {&S->ws, &S->ws_size, &S->ws_off, &S->layout, &S->counters, &S->scan_tmp, &S->list_a, &S->list_b,
+                  &S->flags, &S->in_arena, &S->in_off, &S->in_doc, &S->in_sv, &S->in_svoff, &S->out_arena,
+                  &S->out_off, &S->out_len, &S->status};
+  for (DBuf *b : bufs) if (b->p) hipFree(b->p);
+  if (S->pinned) hipHostFree(S->pinned);
+  if (S->ev0) hipEventDestroy(S->ev0);
+  if (S->ev1) hipEventDestroy(S->ev1);
+  if (S->stream) hipStreamDestroy(S->stream);
+  delete S;
+  g_state = nullptr;
+  return 0;
+}
+
+const char *ym_strerror(int code) {
+  switch (code) {
+    case YM_OK: return "ok";
+    case YM_ERR_INT_RANGE: return "Integer out of range!";
+    case YM_ERR_UNEXPECTED: return "Unexpected case";
+    case YM_ERR_URI: return "URI malformed";
+    case YM_ERR_TYPE: return "TypeError: unknown content, type or value tag";
+    case YM_ERR_RANGE: return "RangeError: read past the end of the update";
+    case YM_ERR_SYNTAX: return "SyntaxError: invalid JSON";
+    case YM_ERR_UNSUPPORTED: return "input needs a canonicalisation the engine does not implement";
+    case YM_ERR_METHOD: return "Method unimplemented";
+    case YM_ERR_CAPACITY: return "output arena too small";
+    default: return code < 0 ? "HIP runtime error" : "unknown status";
+  }
+}
+
+uint64_t ym_out_bound(const ym_batch *b) {
+  // merge/diff outputs re-encode their inputs: a generous multiple of the input plus headers
+  uint64_t in = 0;
+  if (b->mem == YM_MEM_HOST && b->upd_off) in = b->upd_off[b->n_upd] - b->upd_off[0];
+  else in = (uint64_t)b->n_upd * 64;
+  return 2 * in + 64ull * b->n_docs + 4096;
+}
+
+int ym_merge(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_MERGE, b, out, stream, stats); }
+int ym_diff(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_DIFF, b, out, stream, stats); }
+int ym_sv(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_SV, b, out, stream, stats); }
+
+}  // extern "C"

@@ -1,0 +1,56 @@
+// ym_kernels.h -- launch descriptors shared by the host API (ym_api.hip) and the kernels.
+#pragma once
+#include <stdint.h>
+
+#include "ym_core.h"
+
+namespace ymk {
+
+enum : uint32_t { OP_MERGE = 0, OP_DIFF = 1, OP_SV = 2 };
+
+// internal status: document not taken by the fast path, routed to the general path
+constexpr int ST_PENDING = 101;
+
+struct GeneralJob {
+  const uint8_t *A;          // update arena
+  const uint64_t *upd_off;
+  const uint32_t *doc_upd;
+  const uint8_t *sv;         // diff: state-vector arena
+  const uint64_t *sv_off;
+  uint32_t n;                // documents in this launch
+  const uint32_t *list;      // document ids (nullptr: 0..n-1)
+  uint32_t op, v2;
+  uint32_t parts_mul;        // part-table capacity multiplier (grown on ST_RETRY)
+  uint8_t *ws;               // workspace
+  const uint64_t *ws_off;    // per listed slot
+  ym::Layout *layout;        // per doc
+  int32_t *status;           // per doc
+  uint8_t *out;              // output arena
+  uint64_t cap;
+  uint64_t *out_off, *out_len;  // per doc
+  uint64_t *used;            // bump allocator over `out`
+  uint32_t *counter_retry;
+};
+
+struct GeneralWsSize {
+  uint64_t rs, arr, parts, ds, dsg, sv, total;
+  uint32_t parts_cap, sv_cap;
+  uint64_t ds_cap;
+};
+__host__ __device__ inline uint64_t al16(uint64_t x) { return (x + 15) & ~(uint64_t)15; }
+__host__ __device__ inline GeneralWsSize general_ws_size(uint32_t k, uint64_t bytes, uint32_t parts_mul, uint64_t svbytes) {
+  GeneralWsSize z;
+  z.rs = al16((uint64_t)(k ? k : 1) * sizeof(ym::Reader));
+  z.arr = al16((uint64_t)(k + 1) * 4);
+  z.parts_cap = (uint32_t)((2ull * k + 16) * parts_mul);
+  z.parts = al16((uint64_t)z.parts_cap * sizeof(ym::PartRec));
+  z.ds_cap = bytes / 2 + 2;  // every delete-set entry occupies >= 2 input bytes
+  z.ds = al16(z.ds_cap * sizeof(ym::DSE));
+  z.dsg = al16(z.ds_cap * sizeof(ym::DSG));
+  z.sv_cap = (uint32_t)(svbytes / 2 + 2);
+  z.sv = al16((uint64_t)z.sv_cap * 16);
+  z.total = z.rs + 2 * z.arr + z.parts + z.ds + z.dsg + z.sv;
+  return z;
+}
+
+}  // namespace ymk

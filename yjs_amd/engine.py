@@ -1,0 +1,258 @@
+"""ctypes binding of libymerge.so (include/ymerge.h) and the yjs-shaped API on top of it.
+
+Function names, argument meaning and error behaviour mirror yjs 13.5.16's update API
+(Y.mergeUpdates / Y.diffUpdate / Y.encodeStateVectorFromUpdate and their V2 forms, which sit beside
+gaberogan/yjs@v0's public API in src/index.js:53-67): a malformed update raises the error class the
+JS function throws (Error('Integer out of range!'), URIError, TypeError, RangeError, SyntaxError).
+The *Batch variants take many documents at once -- the engine's reason to exist.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def lib_path():
+    return os.path.join(_HERE, "libymerge.so")
+
+
+class YjsError(Exception):
+    """Error('...') thrown by lib0/yjs (e.g. 'Integer out of range!', 'Unexpected case')."""
+
+
+class YjsURIError(YjsError):
+    """URIError('URI malformed'): invalid UTF-8 or a split surrogate pair."""
+
+
+class YjsTypeError(YjsError):
+    """TypeError: unknown content ref / type ref / any tag."""
+
+
+class YjsRangeError(YjsError):
+    """RangeError: read past the end of the update."""
+
+
+class YjsSyntaxError(YjsError):
+    """SyntaxError: JSON.parse of a V1 JSON field."""
+
+
+class UnsupportedInput(YjsError):
+    """Valid input that needs a canonicalisation the engine does not implement."""
+
+
+_STATUS_EXC = {
+    1: (YjsError, "Integer out of range!"),
+    2: (YjsError, "Unexpected case"),
+    3: (YjsURIError, "URI malformed"),
+    4: (YjsTypeError, "unknown content ref, type ref or any tag"),
+    5: (YjsRangeError, "read past the end of the update"),
+    6: (YjsSyntaxError, "invalid JSON"),
+    7: (UnsupportedInput, "input needs a canonicalisation the engine does not implement"),
+    8: (YjsError, "Method unimplemented"),
+    9: (YjsError, "output arena too small"),
+}
+
+
+def raise_for_status(st):
+    if st:
+        exc, msg = _STATUS_EXC.get(int(st), (YjsError, f"status {st}"))
+        raise exc(msg)
+
+
+class _Batch(ctypes.Structure):
+    _fields_ = [("arena", ctypes.c_void_p), ("upd_off", ctypes.c_void_p), ("doc_upd", ctypes.c_void_p),
+                ("n_docs", ctypes.c_uint32), ("n_upd", ctypes.c_uint32), ("format", ctypes.c_int32),
+                ("mem", ctypes.c_int32), ("sv_arena", ctypes.c_void_p), ("sv_off", ctypes.c_void_p)]
+
+
+class _Out(ctypes.Structure):
+    _fields_ = [("arena", ctypes.c_void_p), ("cap", ctypes.c_uint64), ("out_off", ctypes.c_void_p),
+                ("out_len", ctypes.c_void_p), ("status", ctypes.c_void_p), ("used", ctypes.c_uint64)]
+
+
+class _Stats(ctypes.Structure):
+    _fields_ = [("docs", ctypes.c_uint64), ("docs_fast", ctypes.c_uint64), ("docs_general", ctypes.c_uint64),
+                ("docs_error", ctypes.c_uint64), ("bytes_in", ctypes.c_uint64), ("bytes_out", ctypes.c_uint64),
+                ("device_ms", ctypes.c_double)]
+
+
+EXPORTS = ("ym_init", "ym_shutdown", "ym_strerror", "ym_out_bound", "ym_merge", "ym_diff", "ym_sv")
+
+
+def load_library(path=None):
+    path = path or lib_path()
+    if not os.path.exists(path):
+        raise RuntimeError(f"libymerge.so not built ({path}); run __graft_entry__.build()")
+    L = ctypes.CDLL(path)
+    L.ym_init.argtypes = [ctypes.c_int]
+    L.ym_strerror.restype = ctypes.c_char_p
+    L.ym_out_bound.restype = ctypes.c_uint64
+    for fn in (L.ym_merge, L.ym_diff, L.ym_sv):
+        fn.argtypes = [ctypes.POINTER(_Batch), ctypes.POINTER(_Out), ctypes.c_void_p, ctypes.POINTER(_Stats)]
+        fn.restype = ctypes.c_int
+    return L
+
+
+def pack_docs(docs):
+    """[[bytes, ...], ...] -> (arena u8, upd_off u64, doc_upd u32)."""
+    blobs = []
+    doc_upd = [0]
+    for d in docs:
+        blobs.extend(d)
+        doc_upd.append(doc_upd[-1] + len(d))
+    lens = np.fromiter((len(b) for b in blobs), dtype=np.uint64, count=len(blobs))
+    upd_off = np.zeros(len(blobs) + 1, np.uint64)
+    np.cumsum(lens, out=upd_off[1:])
+    arena = np.frombuffer(b"".join(blobs), np.uint8) if blobs else np.zeros(0, np.uint8)
+    return arena, upd_off, np.array(doc_upd, np.uint32)
+
+
+class Engine:
+    """One engine per process/GPU (the library keeps one HIP stream and workspace per thread)."""
+
+    def __init__(self, device=0, path=None):
+        self.lib = load_library(path)
+        rc = self.lib.ym_init(device)
+        if rc != 0:
+            raise RuntimeError(f"ym_init({device}) failed: no usable MI355X/HIP device")
+        self.device = device
+        self.last_stats = _Stats()
+
+    # ---- host-memory batches ------------------------------------------------------------------
+    def run_host(self, op, fmt, arena, upd_off, doc_upd, sv_arena=None, sv_off=None):
+        """Runs op ('merge'|'diff'|'sv') over a packed host batch.
+        Returns (out_arena u8, out_off u64, out_len u64, status i32)."""
+        arena = np.ascontiguousarray(arena, np.uint8)
+        upd_off = np.ascontiguousarray(upd_off, np.uint64)
+        doc_upd = np.ascontiguousarray(doc_upd, np.uint32)
+        n_docs = len(doc_upd) - 1
+        n_upd = len(upd_off) - 1
+        keep = [arena, upd_off, doc_upd]
+        b = _Batch()
+        b.arena = arena.ctypes.data if arena.size else None
+        b.upd_off = upd_off.ctypes.data
+        b.doc_upd = doc_upd.ctypes.data
+        b.n_docs = n_docs
+        b.n_upd = n_upd
+        b.format = fmt
+        b.mem = 0
+        if op == "diff":
+            sv_arena = np.ascontiguousarray(sv_arena, np.uint8)
+            sv_off = np.ascontiguousarray(sv_off, np.uint64)
+            keep += [sv_arena, sv_off]
+            b.sv_arena = sv_arena.ctypes.data if sv_arena.size else None
+            b.sv_off = sv_off.ctypes.data
+        cap = int(self.lib.ym_out_bound(ctypes.byref(b)))
+        fn = {"merge": self.lib.ym_merge, "diff": self.lib.ym_diff, "sv": self.lib.ym_sv}[op]
+        for _ in range(4):
+            out_arena = np.zeros(max(cap, 1), np.uint8)
+            out_off = np.zeros(max(n_docs, 1), np.uint64)
+            out_len = np.zeros(max(n_docs, 1), np.uint64)
+            status = np.zeros(max(n_docs, 1), np.int32)
+            o = _Out(out_arena.ctypes.data, cap, out_off.ctypes.data, out_len.ctypes.data, status.ctypes.data, 0)
+            rc = fn(ctypes.byref(b), ctypes.byref(o), None, ctypes.byref(self.last_stats))
+            if rc == 9:  # YM_ERR_CAPACITY
+                cap = int(o.used) + 4096
+                continue
+            if rc != 0:
+                raise RuntimeError(f"libymerge call failed: {rc} ({self.lib.ym_strerror(rc).decode()})")
+            del keep
+            return out_arena, out_off[:n_docs], out_len[:n_docs], status[:n_docs]
+        raise RuntimeError("output capacity negotiation failed")
+
+    # ---- device-resident batches (torch tensors on cuda) ---------------------------------------
+    def run_device(self, op, fmt, arena, upd_off, doc_upd, out_arena, out_off, out_len, status,
+                   sv_arena=None, sv_off=None, stream=None):
+        """All arguments are torch CUDA tensors (uint8 / int64 / int32 views of the ABI arrays).
+        Returns (rc, used_bytes).  stream: a torch.cuda.Stream or None (library stream)."""
+        b = _Batch()
+        b.arena = arena.data_ptr()
+        b.upd_off = upd_off.data_ptr()
+        b.doc_upd = doc_upd.data_ptr()
+        b.n_docs = doc_upd.numel() - 1
+        b.n_upd = upd_off.numel() - 1
+        b.format = fmt
+        b.mem = 1
+        if op == "diff":
+            b.sv_arena = sv_arena.data_ptr()
+            b.sv_off = sv_off.data_ptr()
+        o = _Out(out_arena.data_ptr(), out_arena.numel(), out_off.data_ptr(), out_len.data_ptr(), status.data_ptr(), 0)
+        fn = {"merge": self.lib.ym_merge, "diff": self.lib.ym_diff, "sv": self.lib.ym_sv}[op]
+        s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+        rc = fn(ctypes.byref(b), ctypes.byref(o), s, ctypes.byref(self.last_stats))
+        return rc, int(o.used)
+
+    @property
+    def stats(self):
+        s = self.last_stats
+        return {k: getattr(s, k) for k, _ in _Stats._fields_}
+
+
+_ENGINE = None
+
+
+def _engine():
+    global _ENGINE
+    if _ENGINE is None:
+        _ENGINE = Engine(int(os.environ.get("YMERGE_DEVICE", "0")))
+    return _ENGINE
+
+
+def _unpack(out_arena, out_off, out_len, status, raise_errors):
+    res = []
+    for d in range(len(status)):
+        if status[d]:
+            if raise_errors:
+                raise_for_status(status[d])
+            res.append(int(status[d]))
+        else:
+            o = int(out_off[d])
+            res.append(out_arena[o:o + int(out_len[d])].tobytes())
+    return res
+
+
+def mergeUpdatesBatch(docs, fmt=1, raise_errors=False):
+    """docs: list of lists of update bytes. Returns one merged update per doc (or the status code)."""
+    arena, upd_off, doc_upd = pack_docs(docs)
+    return _unpack(*_engine().run_host("merge", fmt, arena, upd_off, doc_upd), raise_errors)
+
+
+def diffUpdateBatch(updates, state_vectors, fmt=1, raise_errors=False):
+    arena, upd_off, doc_upd = pack_docs([[u] for u in updates])
+    sva, svo, _ = pack_docs([[s] for s in state_vectors])
+    return _unpack(*_engine().run_host("diff", fmt, arena, upd_off, doc_upd, sva, svo), raise_errors)
+
+
+def encodeStateVectorFromUpdateBatch(updates, fmt=1, raise_errors=False):
+    arena, upd_off, doc_upd = pack_docs([[u] for u in updates])
+    return _unpack(*_engine().run_host("sv", fmt, arena, upd_off, doc_upd), raise_errors)
+
+
+def mergeUpdates(updates):
+    if len(updates) == 1:  # yjs returns the very same object
+        return updates[0]
+    return mergeUpdatesBatch([list(updates)], 1, True)[0]
+
+
+def mergeUpdatesV2(updates):
+    if len(updates) == 1:
+        return updates[0]
+    return mergeUpdatesBatch([list(updates)], 2, True)[0]
+
+
+def diffUpdate(update, sv):
+    return diffUpdateBatch([update], [sv], 1, True)[0]
+
+
+def diffUpdateV2(update, sv):
+    return diffUpdateBatch([update], [sv], 2, True)[0]
+
+
+def encodeStateVectorFromUpdate(update):
+    return encodeStateVectorFromUpdateBatch([update], 1, True)[0]
+
+
+def encodeStateVectorFromUpdateV2(update):
+    return encodeStateVectorFromUpdateBatch([update], 2, True)[0]
