@@ -74,7 +74,9 @@ typedef struct ym_out {
 typedef struct ym_stats {
   uint64_t docs, docs_fast, docs_general, docs_error;
   uint64_t bytes_in, bytes_out;
-  double device_ms; /* device time of the call (HIP events on the call's stream) */
+  double device_ms;  /* device time of the call (HIP events on the call's stream)          */
+  double fast_ms;    /* ... of the LDS fast-path kernel alone                              */
+  double general_ms; /* ... of the general path (workspace sizing + both passes)           */
 } ym_stats;
 
 int ym_init(int device);           /* select the HIP device for this thread; 0 on success */

@@ -1,0 +1,140 @@
+// Benchmark workload templates (container-only recipe; the outputs are data committed under bench_data/).
+//
+// Builds the BASELINE.json configs with yjs 13.5.16's own Doc API, per SURVEY.md §8(d):
+//   C1  1 doc, client 7, Y.Text, 10,000 ops in 1,000 transactions of 10 (60% insert [a-z]{1,5},
+//       40% delete 1-3), seed 12345.  mergeUpdates of all 1,000 updates.
+//   C2  docs of 4 clients x 100 transactions (60% insert word, 20% of them {bold:true}; 40% delete
+//       1-3; 30% one-way sync after each tx), seed = doc+1; local updates only.  TEMPLATES docs are
+//       generated and bench.py replicates them to 10,000 docs (doc i = template i % TEMPLATES).
+//   C3  B4-like single-client trace (259,778 single-char ops: 2% random jump, 29.7% backspace, else
+//       type), final state V1/V2; bench replicates it with random state vectors.
+//   C4  Y.Map docs, 64 clients, 128 broadcast transactions, keys k0..k7, delete p=0.6 when present.
+// File format (.ymb, little endian): "YMB1" u32 n_docs u32 n_upd | u32 doc_upd[n_docs+1] |
+// u64 upd_off[n_upd+1] | arena bytes; gzip-compressed.
+'use strict'
+const fs = require('fs')
+const path = require('path')
+const zlib = require('zlib')
+const { Y } = require('./yjs_bundle.cjs')
+
+const OUT = process.argv[2] || path.join(__dirname, '../../bench_data')
+const which = (process.argv[3] || 'c1,c2,c3,c4').split(',')
+
+function rng (seed) {
+  let s = (seed >>> 0) || 1
+  const next = () => { s ^= s << 13; s >>>= 0; s ^= s >>> 17; s ^= s << 5; s >>>= 0; return s }
+  return {
+    u32: next,
+    int: (lo, hi) => lo + (next() % (hi - lo + 1)),
+    real: () => next() / 4294967296,
+    word: (lo, hi) => { const n = lo + (next() % (hi - lo + 1)); let w = ''; for (let i = 0; i < n; i++) w += String.fromCharCode(97 + next() % 26); return w }
+  }
+}
+
+function writeYmb (file, docs) {
+  const nDocs = docs.length
+  let nUpd = 0; let bytes = 0
+  for (const d of docs) { nUpd += d.length; for (const u of d) bytes += u.length }
+  const head = Buffer.alloc(12 + 4 * (nDocs + 1) + 8 * (nUpd + 1))
+  head.write('YMB1', 0, 'latin1')
+  head.writeUInt32LE(nDocs, 4); head.writeUInt32LE(nUpd, 8)
+  let o = 12; let u = 0
+  for (let i = 0; i <= nDocs; i++) { head.writeUInt32LE(u, o); o += 4; if (i < nDocs) u += docs[i].length }
+  let off = 0
+  head.writeBigUInt64LE(BigInt(0), o); o += 8
+  const arena = Buffer.alloc(bytes)
+  for (const d of docs) for (const x of d) { arena.set(x, off); off += x.length; head.writeBigUInt64LE(BigInt(off), o); o += 8 }
+  fs.writeFileSync(file, zlib.gzipSync(Buffer.concat([head, arena]), { level: 9 }))
+  console.log(file, nDocs, 'docs', nUpd, 'updates', bytes, 'bytes')
+}
+
+function genText (seed, nClients, nTx, opsPerTx, bold, syncP, ids) {
+  const r = rng(seed)
+  const v1 = []; const v2 = []
+  const docs = []
+  for (let c = 0; c < nClients; c++) {
+    const d = new Y.Doc(); d.clientID = ids[c]
+    d.on('update', (u, origin) => { if (origin !== 'remote') v1.push(u) })
+    d.on('updateV2', (u, origin) => { if (origin !== 'remote') v2.push(u) })
+    docs.push(d)
+  }
+  for (let t = 0; t < nTx; t++) {
+    const d = docs[r.u32() % docs.length]
+    const text = d.getText('text')
+    d.transact(() => {
+      for (let o = 0; o < opsPerTx; o++) {
+        const len = text.length
+        if (len === 0 || r.real() < 0.6) {
+          const pos = r.int(0, len); const w = r.word(1, 5)
+          if (bold && r.real() < 0.2) text.insert(pos, w, { bold: true }); else text.insert(pos, w)
+        } else {
+          const pos = r.int(0, len - 1)
+          text.delete(pos, Math.min(r.int(1, 3), len - pos))
+        }
+      }
+    })
+    if (nClients > 1 && r.real() < syncP) {
+      const a = docs[r.u32() % docs.length]; const b = docs[r.u32() % docs.length]
+      if (a !== b) Y.applyUpdate(b, Y.encodeStateAsUpdate(a, Y.encodeStateVector(b)), 'remote')
+    }
+  }
+  return { v1, v2 }
+}
+
+function genMap (seed, nClients, nTx, nKeys) {
+  const r = rng(seed)
+  const v1 = []; const v2 = []
+  const docs = []
+  for (let c = 0; c < nClients; c++) { const d = new Y.Doc(); d.clientID = 500 + 31 * c; docs.push(d) }
+  for (const d of docs) {
+    d.on('update', (u, origin) => { if (origin === 'remote') return; v1.push(u); for (const o of docs) if (o !== d) Y.applyUpdate(o, u, 'remote') })
+    d.on('updateV2', (u, origin) => { if (origin !== 'remote') v2.push(u) })
+  }
+  for (let t = 0; t < nTx; t++) {
+    const d = docs[r.u32() % docs.length]
+    const m = d.getMap('map')
+    const key = 'k' + (r.u32() % nKeys)
+    if (m.has(key) && r.real() < 0.6) m.delete(key)
+    else m.set(key, r.real() < 0.5 ? r.int(0, 1000000) : r.word(1, 6))
+  }
+  return { v1, v2 }
+}
+
+fs.mkdirSync(OUT, { recursive: true })
+if (which.includes('c1')) {
+  const { v1, v2 } = genText(12345, 1, 1000, 10, false, 0, [7])
+  writeYmb(path.join(OUT, 'c1_v1.ymb.gz'), [v1])
+  writeYmb(path.join(OUT, 'c1_v2.ymb.gz'), [v2])
+}
+if (which.includes('c2')) {
+  const T = Number(process.env.C2_TEMPLATES || 1024)
+  const d1 = []; const d2 = []
+  for (let doc = 0; doc < T; doc++) {
+    const { v1, v2 } = genText(doc + 1, 4, 100, 1, true, 0.3, [1000, 8919, 16838, 24757])
+    d1.push(v1); d2.push(v2)
+  }
+  writeYmb(path.join(OUT, 'c2_v1.ymb.gz'), d1)
+  writeYmb(path.join(OUT, 'c2_v2.ymb.gz'), d2)
+}
+if (which.includes('c3')) {
+  const r = rng(4242)
+  const d = new Y.Doc(); d.clientID = 1
+  const text = d.getText('text')
+  let cursor = 0
+  for (let i = 0; i < 259778; i++) {
+    if (r.real() < 0.02) cursor = r.int(0, text.length)
+    if (cursor > 0 && r.real() < 0.297) { text.delete(cursor - 1, 1); cursor-- } else { text.insert(cursor, String.fromCharCode(97 + r.u32() % 26)); cursor++ }
+  }
+  writeYmb(path.join(OUT, 'c3_v1.ymb.gz'), [[Y.encodeStateAsUpdate(d)]])
+  writeYmb(path.join(OUT, 'c3_v2.ymb.gz'), [[Y.encodeStateAsUpdateV2(d)]])
+}
+if (which.includes('c4')) {
+  const T = Number(process.env.C4_TEMPLATES || 256)
+  const d1 = []; const d2 = []
+  for (let doc = 0; doc < T; doc++) {
+    const { v1, v2 } = genMap(doc + 1, 64, 128, 8)
+    d1.push(v1); d2.push(v2)
+  }
+  writeYmb(path.join(OUT, 'c4_v1.ymb.gz'), d1)
+  writeYmb(path.join(OUT, 'c4_v2.ymb.gz'), d2)
+}

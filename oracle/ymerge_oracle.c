@@ -63,7 +63,7 @@ static void *aalloc(Ctx *c, size_t n) {
   n = (n + 15) & ~(size_t)15;
   Chunk *k = c->chunks;
   if (!k || k->cap - k->used < n) {
-    size_t cap = n + sizeof(Chunk) + 15 > (1u << 20) ? n + sizeof(Chunk) + 16 : (1u << 20);
+    size_t cap = n + sizeof(Chunk) + 15 > (1u << 16) ? n + sizeof(Chunk) + 16 : (1u << 16);
     Chunk *nk = (Chunk *)malloc(cap);
     if (!nk) fail(c, YMO_ERR_UNSUPPORTED);
     nk->cap = cap;

@@ -51,7 +51,7 @@ struct DBuf {
 struct DevState {
   int device = -1;
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, evf0 = nullptr, evf1 = nullptr, evg1 = nullptr;
   DBuf ws, ws_size, ws_off, layout, counters, scan_tmp, list_a, list_b, flags;
   DBuf in_arena, in_off, in_doc, in_sv, in_svoff, out_arena, out_off, out_len, status;  // host staging
   uint64_t *pinned = nullptr;
@@ -74,6 +74,9 @@ DevState *state() {
     hipStreamCreateWithFlags(&g_state->stream, hipStreamNonBlocking);
     hipEventCreate(&g_state->ev0);
     hipEventCreate(&g_state->ev1);
+    hipEventCreate(&g_state->evf0);
+    hipEventCreate(&g_state->evf1);
+    hipEventCreate(&g_state->evg1);
     hipHostMalloc((void **)&g_state->pinned, 64 * sizeof(uint64_t), hipHostMallocDefault);
   }
   return g_state;
@@ -232,8 +235,10 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   j.n = nd;
 
   // (1) fast path over every document; leaves status ST_PENDING where it declines
+  HIPCHK(hipEventRecord(S->evf0, st));
   int fr = fast_launch(op, j, st);
   if (fr < 0) return fr;
+  HIPCHK(hipEventRecord(S->evf1, st));
   uint32_t ngen = nd;
   uint32_t *list = nullptr;
   if (fr == 1) {  // the fast path ran: select the declined docs
@@ -245,6 +250,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
     int r = run_general(S, st, j, list, ngen);
     if (r) return r;
   }
+  HIPCHK(hipEventRecord(S->evg1, st));
   HIPCHK(hipEventRecord(S->ev1, st));
   // (3) bookkeeping
   if (stats) {
@@ -257,9 +263,13 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   uint64_t used = S->pinned[0];
   out->used = used;
   if (stats) {
-    float ms = 0;
+    float ms = 0, fms = 0, gms = 0;
     hipEventElapsedTime(&ms, S->ev0, S->ev1);
+    hipEventElapsedTime(&fms, S->evf0, S->evf1);
+    hipEventElapsedTime(&gms, S->evf1, S->evg1);
     stats->device_ms = ms;
+    stats->fast_ms = fr == 1 ? fms : 0.0;
+    stats->general_ms = ngen > 0 ? gms : 0.0;
     stats->docs = nd;
     stats->docs_general = ngen;
     stats->docs_fast = nd - ngen;
@@ -302,6 +312,9 @@ int ym_shutdown(void) {
   if (S->pinned) hipHostFree(S->pinned);
   if (S->ev0) hipEventDestroy(S->ev0);
   if (S->ev1) hipEventDestroy(S->ev1);
+  if (S->evf0) hipEventDestroy(S->evf0);
+  if (S->evf1) hipEventDestroy(S->evf1);
+  if (S->evg1) hipEventDestroy(S->evg1);
   if (S->stream) hipStreamDestroy(S->stream);
   delete S;
   g_state = nullptr;
