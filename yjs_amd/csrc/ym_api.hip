@@ -19,7 +19,7 @@
 namespace ymk {
 __global__ void k_general_ws(GeneralJob j, uint64_t *ws_size);
 __global__ void k_general(GeneralJob j, int pass);
-int fast_launch(uint32_t op, const GeneralJob &j, hipStream_t st);  // ym_fast.hip
+int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st);  // ym_fast.hip
 }  // namespace ymk
 
 using namespace ymk;
@@ -236,7 +236,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
 
   // (1) fast path over every document; leaves status ST_PENDING where it declines
   HIPCHK(hipEventRecord(S->evf0, st));
-  int fr = fast_launch(op, j, st);
+  int fr = fast_launch(op, j, b->n_upd, st);
   if (fr < 0) return fr;
   HIPCHK(hipEventRecord(S->evf1, st));
   uint32_t ngen = nd;
@@ -338,11 +338,13 @@ const char *ym_strerror(int code) {
 }
 
 uint64_t ym_out_bound(const ym_batch *b) {
-  // merge/diff outputs re-encode their inputs: a generous multiple of the input plus headers
+  // fast-path slot region (2 * in + 64 per doc) followed by room for general-path outputs
   uint64_t in = 0;
   if (b->mem == YM_MEM_HOST && b->upd_off) in = b->upd_off[b->n_upd] - b->upd_off[0];
   else in = (uint64_t)b->n_upd * 64;
-  return 2 * in + 64ull * b->n_docs + 4096;
+  uint64_t sv = 0;
+  if (b->mem == YM_MEM_HOST && b->sv_off) sv = b->sv_off[b->n_docs] - b->sv_off[0];
+  return 4 * in + 2 * sv + 128ull * b->n_docs + 8192;
 }
 
 int ym_merge(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_MERGE, b, out, stream, stats); }
