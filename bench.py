@@ -145,15 +145,11 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
-    # max over ranks of elapsed; sums of work
-    red = torch.tensor([elapsed, 0.0], dtype=torch.float64, device=dev)
-    tot = torch.tensor([float(in_bytes), float(out_bytes), float(n_docs), float(errors),
-                        float(st0["docs_fast"]), float(st0["docs_general"])], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(red, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-    elapsed = float(red[0].item())
-    in_all, out_all, docs_all, err_all, fast_all, gen_all = [float(x) for x in tot.tolist()]
+    # the only collectives: max of the timed region, sum of per-rank counters (RCCL over xGMI)
+    from yjs_amd.distributed import reduce_run
+    elapsed, (in_all, out_all, docs_all, err_all, fast_all, gen_all) = reduce_run(
+        dist if world > 1 else None, elapsed,
+        [in_bytes, out_bytes, n_docs, errors, st0["docs_fast"], st0["docs_general"]], device=dev)
 
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3

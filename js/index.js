@@ -1,0 +1,100 @@
+// yjs-compatible batched update API on the MI355X (libymerge.so via the N-API addon).
+//
+// Drop-in for yjs 13.5's update functions -- same names, same arguments, same results and the same
+// exception classes -- plus *Batch variants that process many documents in one GPU call:
+//   mergeUpdates(updates) / mergeUpdatesV2            (yjs: Y.mergeUpdates[V2])
+//   diffUpdate(update, sv) / diffUpdateV2              (yjs: Y.diffUpdate[V2])
+//   encodeStateVectorFromUpdate(update) / ...V2        (yjs: Y.encodeStateVectorFromUpdate[V2])
+//   mergeUpdatesBatch(docs, {format}), diffUpdateBatch(updates, svs, {format}),
+//   encodeStateVectorFromUpdateBatch(updates, {format})
+// There is no CPU fallback: a missing addon or GPU throws.
+'use strict'
+const path = require('path')
+const addon = require(path.join(__dirname, 'build', 'ymerge_napi.node'))
+
+let initialised = false
+function init () {
+  if (!initialised) {
+    const rc = addon.init(Number(process.env.YMERGE_DEVICE || 0))
+    if (rc !== 0) throw new Error('ymerge: no usable MI355X/HIP device')
+    initialised = true
+  }
+}
+
+const OP = { merge: 0, diff: 1, sv: 2 }
+const fmtOf = o => (o && (o.format === 'v2' || o.format === 2)) ? 2 : 1
+
+// status -> the exception yjs itself throws for that input
+function toError (st) {
+  switch (st) {
+    case 1: return new Error('Integer out of range!')
+    case 2: return new Error('Unexpected case')
+    case 3: return new URIError('URI malformed')
+    case 4: return new TypeError('unknown content, type or value tag')
+    case 5: return new RangeError('read past the end of the update')
+    case 6: return new SyntaxError('invalid JSON in update')
+    case 7: { const e = new Error('ymerge: input needs a canonicalisation the engine does not implement'); e.code = 'YM_UNSUPPORTED'; return e }
+    case 8: return new Error('Method unimplemented')
+    default: return new Error('ymerge status ' + st)
+  }
+}
+
+function pack (docs) {
+  let n = 0; let bytes = 0
+  for (const d of docs) { n += d.length; for (const u of d) bytes += u.length }
+  const arena = new Uint8Array(bytes)
+  const updOff = new Float64Array(n + 1)
+  const docUpd = new Uint32Array(docs.length + 1)
+  let o = 0; let u = 0
+  docs.forEach((d, i) => {
+    docUpd[i] = u
+    for (const x of d) { arena.set(x, o); updOff[u] = o; o += x.length; u++ }
+  })
+  docUpd[docs.length] = u
+  updOff[n] = o
+  return { arena, updOff, docUpd }
+}
+
+function unpack (res, throwErrors) {
+  const out = new Array(res.status.length)
+  for (let d = 0; d < res.status.length; d++) {
+    if (res.status[d] !== 0) {
+      const e = toError(res.status[d])
+      if (throwErrors) throw e
+      out[d] = e
+    } else {
+      out[d] = res.arena.slice(res.offsets[d], res.offsets[d] + res.lengths[d])
+    }
+  }
+  return out
+}
+
+function mergeUpdatesBatch (docs, opts, throwErrors = false) {
+  init()
+  const p = pack(docs)
+  return unpack(addon.run(OP.merge, fmtOf(opts), p.arena, p.updOff, p.docUpd), throwErrors)
+}
+function diffUpdateBatch (updates, svs, opts, throwErrors = false) {
+  init()
+  const p = pack(updates.map(u => [u]))
+  const s = pack(svs.map(x => [x]))
+  return unpack(addon.run(OP.diff, fmtOf(opts), p.arena, p.updOff, p.docUpd, s.arena, s.updOff), throwErrors)
+}
+function encodeStateVectorFromUpdateBatch (updates, opts, throwErrors = false) {
+  init()
+  const p = pack(updates.map(u => [u]))
+  return unpack(addon.run(OP.sv, fmtOf(opts), p.arena, p.updOff, p.docUpd), throwErrors)
+}
+
+// single-document yjs signatures (mergeUpdates([u]) returns the same object, like yjs)
+const mergeUpdates = updates => updates.length === 1 ? updates[0] : mergeUpdatesBatch([updates], { format: 'v1' }, true)[0]
+const mergeUpdatesV2 = updates => updates.length === 1 ? updates[0] : mergeUpdatesBatch([updates], { format: 'v2' }, true)[0]
+const diffUpdate = (update, sv) => diffUpdateBatch([update], [sv], { format: 'v1' }, true)[0]
+const diffUpdateV2 = (update, sv) => diffUpdateBatch([update], [sv], { format: 'v2' }, true)[0]
+const encodeStateVectorFromUpdate = u => encodeStateVectorFromUpdateBatch([u], { format: 'v1' }, true)[0]
+const encodeStateVectorFromUpdateV2 = u => encodeStateVectorFromUpdateBatch([u], { format: 'v2' }, true)[0]
+
+module.exports = {
+  mergeUpdates, mergeUpdatesV2, diffUpdate, diffUpdateV2, encodeStateVectorFromUpdate, encodeStateVectorFromUpdateV2,
+  mergeUpdatesBatch, diffUpdateBatch, encodeStateVectorFromUpdateBatch
+}

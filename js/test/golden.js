@@ -1,0 +1,30 @@
+// Runs the golden vectors (tests/golden/*.json) through the JS API on the GPU; prints a JSON summary.
+'use strict'
+const fs = require('fs')
+const path = require('path')
+const Y = require('..')
+const dir = path.join(__dirname, '..', '..', 'tests', 'golden')
+const errName = { URIError: 'URIError', TypeError: 'TypeError', RangeError: 'RangeError', SyntaxError: 'SyntaxError', Error: 'Error' }
+let ok = 0; let bad = []; let unsupported = 0
+for (const f of fs.readdirSync(dir).filter(f => f.endsWith('.json')).sort()) {
+  const cases = JSON.parse(fs.readFileSync(path.join(dir, f))).cases
+  for (const c of cases) {
+    const inputs = c.inputs.map(b => new Uint8Array(Buffer.from(b, 'base64')))
+    if (c.op === 'merge' && inputs.length === 0) continue
+    let out; let err
+    try {
+      if (c.op === 'merge') out = (c.fmt === 1 ? Y.mergeUpdates : Y.mergeUpdatesV2)(inputs)
+      else if (c.op === 'diff') out = (c.fmt === 1 ? Y.diffUpdate : Y.diffUpdateV2)(inputs[0], new Uint8Array(Buffer.from(c.sv, 'base64')))
+      else out = (c.fmt === 1 ? Y.encodeStateVectorFromUpdate : Y.encodeStateVectorFromUpdateV2)(inputs[0])
+    } catch (e) { err = e }
+    const id = `${f}/${c.name}/v${c.fmt}/${c.op}`
+    if (err && err.code === 'YM_UNSUPPORTED') { unsupported++; continue }
+    if (c.error) {
+      if (!err || err.constructor.name !== errName[c.error] || (c.error === 'Error' && err.message !== c.message)) bad.push([id, 'error', err && err.message])
+      else ok++
+    } else if (err || Buffer.compare(Buffer.from(out), Buffer.from(c.expect, 'base64')) !== 0) bad.push([id, 'bytes', err && err.message])
+    else ok++
+  }
+}
+console.log(JSON.stringify({ ok, bad: bad.length, unsupported, first: bad.slice(0, 10) }))
+process.exit(bad.length ? 1 : 0)

@@ -1,0 +1,21 @@
+"""The Node.js drop-in (js/index.js -> N-API addon -> libymerge.so -> MI355X) reproduces every golden
+vector with yjs's own function names and exception classes."""
+import json
+import os
+import shutil
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.skipif(shutil.which("node") is None, reason="node not installed on this box")
+def test_js_api_golden():
+    r = subprocess.run(["node", os.path.join(ROOT, "js", "test", "golden.js")], capture_output=True, text=True, timeout=600)
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert line, r.stderr[-3000:]
+    res = json.loads(line[-1])
+    assert r.returncode == 0 and res["bad"] == 0, res
+    assert res["ok"] >= 650 and res["unsupported"] <= 5, res

@@ -1,0 +1,67 @@
+"""World-size-2 rehearsal of the multi-GPU path on CPU (gloo): ranks take disjoint document shards,
+process them independently (here with the CPU oracle standing in for the device), and the only
+collectives are the max-time / sum-of-counters reductions.  The union of the shards' outputs must equal
+a single-process run."""
+import os
+import socket
+
+import numpy as np
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch.distributed as dist
+    import oracle_ref
+    from yjs_amd.distributed import reduce_run, shard_batch, shard_ranges
+    from yjs_amd.workloads import load_ymb
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    a, o, d = load_ymb("c2_v1")
+    n = 96
+    s, e = shard_ranges(n, world)[rank]
+    sa, so, sd = shard_batch(a, o, d, s, e)
+    outs, st, ol = oracle_ref.batch("merge", 1, sa, so, sd)
+    tmax, (docs, bytes_out, errs) = reduce_run(dist, 0.5 + rank, [e - s, float(np.sum(ol)), float((st != 0).sum())])
+    q.put((rank, s, outs, tmax, docs, bytes_out, errs))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_sharding_matches_single_process():
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ref
+    from yjs_amd.distributed import shard_batch
+    from yjs_amd.workloads import load_ymb
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in procs])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    a, o, d = load_ymb("c2_v1")
+    ref, st, ol = oracle_ref.batch("merge", 1, *shard_batch(a, o, d, 0, 96))
+    merged = [x for r in res for x in r[2]]
+    assert merged == ref
+    for r in res:
+        assert r[3] == 1.5                      # max over ranks
+        assert r[4] == 96                       # docs summed over ranks
+        assert r[5] == float(np.sum(ol))        # bytes summed over ranks
+        assert r[6] == 0
