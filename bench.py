@@ -110,7 +110,7 @@ def main():
     g_arena = torch.from_numpy(arena).to(dev)
     g_off = torch.from_numpy(upd_off.view(np.int64)).to(dev)
     g_doc = torch.from_numpy(doc_upd.view(np.int32)).to(dev)
-    cap = 2 * in_bytes + 64 * n_docs + 4096
+    cap = 4 * in_bytes + 128 * n_docs + 8192  # fast-path slots (2*in + 64 per doc) + general-path room
     o_arena = torch.empty(cap, dtype=torch.uint8, device=dev)
     o_off = torch.empty(n_docs, dtype=torch.int64, device=dev)
     o_len = torch.empty(n_docs, dtype=torch.int64, device=dev)
