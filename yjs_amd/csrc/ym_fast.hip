@@ -1,19 +1,26 @@
-// ym_fast.hip -- LDS fast path: one 64-lane wave per document, the whole document staged in LDS.
+// ym_fast.hip -- LDS fast path for batched mergeUpdates (V1): one 64-lane wave per document.
 //
-// Takes mergeUpdates (V1) documents whose inputs are "simple": every update's structs increase in
-// (client desc, clock asc), no two structs overlap, no GC/Skip structs, canonical encodings, payloads
-// of the kinds yjs writes (strings, formats/embeds with literal JSON, scalar `any` values).  For such
-// documents yjs 13.5.16's k-way merge (bundle ds@39007) reduces to: all structs sorted by
-// (client desc, clock asc), a Skip before every clock gap, consecutive same-client structs grouped
-// into one part (SURVEY.md App. B "Consequences for the GPU design"); the delete set is the per-client
-// union of all inputs' ranges with clients in first-appearance order (DeleteSet.js:113-161, 13.5.16
-// le@10242 / he@10482).  Everything else is declined (status ST_PENDING) and handled exactly by the
-// general path (ym_general.hip).
+// Takes documents whose inputs are "simple": every update's structs increase in (client desc,
+// clock asc), no two structs overlap, no GC/Skip structs, canonical encodings, payloads of the kinds
+// yjs writes (strings, formats/embeds with literal JSON, scalar `any` values).  For such documents
+// yjs 13.5.16's k-way merge (bundle ds@39007) reduces to: all structs sorted by
+// (client desc, clock asc), a Skip (info 10, 13.5.16 ui.write) before every clock gap, consecutive
+// same-client structs grouped into one part (encoding.js:94-116 writeClientsStructs layout); the
+// delete set is the per-client union of all inputs' ranges (13.5.16 le@10242: `>=` touching rule,
+// max end) with clients in first-appearance order (DeleteSet.js:141-161 mergeDeleteSets, 13.5.16
+// he@10482).  Anything else is declined (status ST_PENDING) and handled exactly by the general path
+// (ym_general.hip) -- never approximated.
 //
-// Per document (one wave, ~10 KB of LDS, no scratch):
-//   16-B loads of the update bytes into LDS -> lanes walk updates (count pass, wave scan, emit pass)
-//   -> bitonic sort of (client, clock) keys -> struct sizes + part headers by wave scans -> delete-set
-//   union, one lane per client -> output staged in LDS -> 16-B stores into the doc's slot.
+// Per document, all in LDS (~7.6 KB, no scratch), every phase data-parallel across the wave:
+//   1. 16-B loads of the document's bytes into LDS.
+//   2. one lane per update walks its V1 bytes (branch-free varints from one unaligned 8-byte LDS
+//      read, SWAR ASCII/JSON checks) and appends struct / delete-range records via LDS atomics.
+//   3. rank sort of the struct keys (each lane counts the keys <= its own: broadcast reads, no
+//      barriers inside), scatter, duplicate check.
+//   4. struct layout by DPP wave scans: Skips at clock gaps, part headers, byte offsets.
+//   5. delete set: rank sort of (client, clock), segmented running-max scan = interval union,
+//      groups ranked by first appearance, byte offsets by scans.
+//   6. emit into LDS (aliasing the dead record arrays), 16-B stores into the doc's output slot.
 // Output slot of doc d: 2 * (input bytes before d) + 64 * d, 16-aligned (a bound the kernel checks),
 // so the fast path needs no global atomics; the general path appends after that region.
 #include <hip/hip_runtime.h>
@@ -22,180 +29,213 @@
 #include "ym_kernels.h"
 
 namespace ymk {
+namespace fastv1 {
 
-template <int IN, int UPD, int REC, int DS, int OUT>
-struct FastCfg {
-  static constexpr int kIn = IN, kUpd = UPD, kRec = REC, kDs = DS, kOut = OUT;
-};
+constexpr uint32_t IN = 2560;    // max document bytes
+constexpr uint32_t UPD = 128;    // max updates per document
+constexpr uint32_t E = 2;        // records per lane
+constexpr uint32_t REC = 64 * E; // max structs per document
+constexpr uint32_t DSN = 64 * E; // max delete ranges per document (before the union)
+constexpr uint32_t OUT = 2048;   // max output bytes
 
-// LDS layout (byte offsets into the dynamic LDS block), every array 16-aligned
-template <class C>
-struct Lay {
-  static constexpr int a16(int x) { return (x + 15) & ~15; }
-  static constexpr int rkey = 0;                                 // u64[REC] (client desc, clock)
-  static constexpr int dkey = a16(rkey + 8 * C::kRec);           // u64[DS]  (client, clock)
-  static constexpr int rlen = a16(dkey + 8 * C::kDs);            // u32[REC] struct length
-  static constexpr int dlen = a16(rlen + 4 * C::kRec);           // u32[DS]  range length (by idx)
-  static constexpr int dend = a16(dlen + 4 * C::kDs);            // u32[DS]  union end at interval start
-  static constexpr int rpos = a16(dend + 4 * C::kDs);            // u16[REC] inclusive struct-count prefix
-  static constexpr int rstart = a16(rpos + 2 * C::kRec);         // u16[REC] struct start in `in`
-  static constexpr int rblen = a16(rstart + 2 * C::kRec);        // u16[REC] struct bytes incl. info
-  static constexpr int ridx = a16(rblen + 2 * C::kRec);          // u16[REC] sort payload
-  static constexpr int didx = a16(ridx + 2 * C::kRec);           // u16[DS]  sort payload = appearance
-  static constexpr int dseq = a16(didx + 2 * C::kDs);            // u16[DS]  (update << 8 | position) by slot
-  static constexpr int dflag = a16(dseq + 2 * C::kDs);           // u8[DS]   interval start flags
-  static constexpr int rinfo = a16(dflag + C::kDs);              // u8[REC]
-  static constexpr int uoff = a16(rinfo + C::kRec);              // u16[UPD+1]
-  static constexpr int ubase = a16(uoff + 2 * (C::kUpd + 1));    // u16[UPD]
-  static constexpr int dbase = a16(ubase + 2 * C::kUpd);         // u16[UPD]
-  static constexpr int gstart = a16(dbase + 2 * C::kUpd);        // u16[DS+1] group start entry
-  static constexpr int gmin = a16(gstart + 2 * (C::kDs + 1));    // u16[DS]  group first appearance
-  static constexpr int gsz = a16(gmin + 2 * C::kDs);             // u16[DS]  group bytes
-  static constexpr int gcnt = a16(gsz + 2 * C::kDs);             // u16[DS]  group interval count
-  static constexpr int grank = a16(gcnt + 2 * C::kDs);           // u16[DS]  group -> rank
-  static constexpr int roff = a16(grank + 2 * C::kDs);           // u16[DS]  rank -> byte offset
-  static constexpr int misc = a16(roff + 2 * C::kDs);            // u32[16]
-  static constexpr int in = a16(misc + 64);                      // u8[IN + 16]
-  static constexpr int out = a16(in + C::kIn + 16);              // u8[OUT]
-  static constexpr int total = a16(out + C::kOut);
-};
+// ---- LDS map (byte offsets; every array 16-aligned) ----------------------------------------------
+constexpr uint32_t L_IN = 0;                    // u8[IN + 16]   document bytes (+ slack for 8-B reads)
+constexpr uint32_t L_UOFF = IN + 16;            // u16[UPD + 1]  update start (absolute LDS offsets)
+constexpr uint32_t L_MISC = L_UOFF + 272;       // u32[16]       counters
+constexpr uint32_t R = L_MISC + 64;             // phase region
+// phase 2-4: struct records (walk order, then rank order in place)
+constexpr uint32_t L_RKEY = R;                  // u64[REC]  (~client << 32 | clock)
+constexpr uint32_t L_RLEN = L_RKEY + 8 * REC;   // u32[REC]
+constexpr uint32_t L_RSRC = L_RLEN + 4 * REC;   // u16[REC]  LDS offset of the info byte
+constexpr uint32_t L_RBLEN = L_RSRC + 2 * REC;  // u16[REC]  struct bytes incl. info
+constexpr uint32_t L_RINFO = L_RBLEN + 2 * REC; // u8[REC]
+constexpr uint32_t L_RSLOT = L_RINFO + REC;     // u8[REC]   rank -> walk slot (duplicate check)
+// phase 2, 5: delete ranges
+constexpr uint32_t L_DKEY = L_RSLOT + REC;      // u64[DSN]  (client << 32 | clock)
+constexpr uint32_t L_DLEN = L_DKEY + 8 * DSN;   // u32[DSN]
+constexpr uint32_t L_DSEQ = L_DLEN + 4 * DSN;   // u16[DSN]  update << 8 | position (first appearance)
+constexpr uint32_t L_DSLOT = L_DSEQ + 2 * DSN;  // u8[DSN]
+constexpr uint32_t L_PFIRST = L_DSLOT + DSN;    // u16[REC]  part -> units before it
+constexpr uint32_t L_PLAST = L_PFIRST + 2 * REC;// u16[REC]  part -> units through it
+constexpr uint32_t L_END = L_PLAST + 2 * REC;
+// phase 5 (after the struct records are held in registers): merged ranges and groups, over R
+constexpr uint32_t L_QCLK = R;                  // u32[DSN]  merged range start
+constexpr uint32_t L_QEND = L_QCLK + 4 * DSN;   // u32[DSN]  merged range end
+constexpr uint32_t L_QGRP = L_QEND + 4 * DSN;   // u8[DSN]   merged range -> group
+constexpr uint32_t L_QPRE = L_QGRP + DSN;       // u16[DSN + 1] exclusive byte prefix over ranges
+constexpr uint32_t L_GFIRST = L_QPRE + 272;     // u16[DSN + 1] group -> first range
+constexpr uint32_t L_GCLI = L_GFIRST + 272;     // u32[DSN]  group client
+constexpr uint32_t L_P5END = L_GCLI + 4 * DSN;
+constexpr uint32_t L_GBYR = L_QCLK;             // u16[DSN]  bytes by rank, then offsets by rank (QCLK is dead by then)
+constexpr uint32_t L_GMIN = L_PFIRST;           // u32[DSN]  group first appearance, then group base (parts are dead)
+static_assert(L_P5END <= L_DKEY, "phase-5 arrays must not overlap the sorted delete ranges");
+static_assert(L_GMIN + 4 * DSN <= L_END, "group array fits");
+// phase 6: output staging over R
+constexpr uint32_t L_OUT = R;
+static_assert(L_OUT + OUT <= L_END, "output staging fits the phase region");
+constexpr uint32_t LDS_BYTES = L_END;
 
-extern __shared__ __attribute__((aligned(16))) uint8_t g_smem[];
-
+extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
 template <class T>
-__device__ __forceinline__ T *lds(int off) { return reinterpret_cast<T *>(g_smem + off); }
+__device__ __forceinline__ T &at(uint32_t off) { return *reinterpret_cast<T *>(sm + off); }
+// unaligned LDS accesses (gfx950 runs them in hardware: tools/probe/lds_unaligned.hip)
+__device__ __forceinline__ uint64_t ld8(uint32_t p) { uint64_t x; __builtin_memcpy(&x, sm + p, 8); return x; }
+__device__ __forceinline__ uint32_t ld4(uint32_t p) { uint32_t x; __builtin_memcpy(&x, sm + p, 4); return x; }
+__device__ __forceinline__ void st4(uint32_t p, uint32_t x) { __builtin_memcpy(sm + p, &x, 4); }
 
-// ---- wave primitives ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t *total) {
-  const uint32_t lane = threadIdx.x & 63;
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= (uint32_t)o) x += y;
-  }
-  *total = __shfl(x, 63, 64);
-  return x - v;
+// ---- wave primitives (DPP row shifts + row broadcasts: no LDS traffic) ---------------------------
+#define YM_DPP(x, ctl, rm) (uint32_t) __builtin_amdgcn_update_dpp(0, (int)(x), ctl, rm, 0xf, false)
+// inclusive prefix sum over the 64 lanes
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
+  x += YM_DPP(x, 0x111, 0xf);  // row_shr:1
+  x += YM_DPP(x, 0x112, 0xf);  // row_shr:2
+  x += YM_DPP(x, 0x114, 0xf);  // row_shr:4
+  x += YM_DPP(x, 0x118, 0xf);  // row_shr:8
+  x += YM_DPP(x, 0x142, 0xa);  // row_bcast:15 -> rows 1, 3
+  x += YM_DPP(x, 0x143, 0xc);  // row_bcast:31 -> rows 2, 3
+  return x;
 }
+__device__ __forceinline__ uint32_t lane_read(uint32_t x, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, l); }
+// inclusive prefix max over the 64 lanes, u64
+template <int CTL, int RM>
+__device__ __forceinline__ uint64_t max_step(uint64_t x) {
+  const uint32_t lo = YM_DPP((uint32_t)x, CTL, RM), hi = YM_DPP((uint32_t)(x >> 32), CTL, RM);
+  const uint64_t y = ((uint64_t)hi << 32) | lo;
+  return y > x ? y : x;
+}
+__device__ __forceinline__ uint64_t wave_incl_max64(uint64_t x) {
+  x = max_step<0x111, 0xf>(x);
+  x = max_step<0x112, 0xf>(x);
+  x = max_step<0x114, 0xf>(x);
+  x = max_step<0x118, 0xf>(x);
+  x = max_step<0x142, 0xa>(x);
+  x = max_step<0x143, 0xc>(x);
+  return x;
+}
+__device__ __forceinline__ uint64_t lane_read64(uint64_t x, int l) {
+  return ((uint64_t)lane_read((uint32_t)(x >> 32), l) << 32) | lane_read((uint32_t)x, l);
+}
+// value of lane-1 (0 for lane 0) / lane+1 (0 for lane 63): DPP wave_shr:1 / wave_shl:1
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, false); }
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, false); }
 
 __device__ __forceinline__ uint32_t vsz(uint64_t v) {
-  uint32_t n = 1;
-  while (v > 127) { v >>= 7; n++; }
-  return n;
+  return 1 + (v >= (1ull << 7)) + (v >= (1ull << 14)) + (v >= (1ull << 21)) + (v >= (1ull << 28)) +
+         (v >= (1ull << 35)) + (v >= (1ull << 42)) + (v >= (1ull << 49));
 }
-__device__ __forceinline__ uint32_t put_vu(uint8_t *o, uint32_t p, uint64_t v) {
-  while (v > 127) { o[p++] = (uint8_t)(0x80 | (v & 127)); v >>= 7; }
-  o[p++] = (uint8_t)v;
+__device__ __forceinline__ uint32_t put_vu(uint32_t p, uint64_t v) {
+  while (v > 127) { sm[p++] = (uint8_t)(0x80 | (v & 127)); v >>= 7; }
+  sm[p++] = (uint8_t)v;
   return p;
 }
 
-// ---- lean V1 walker over LDS bytes -------------------------------------------------------------
+// ---- V1 walker over LDS bytes ---------------------------------------------------------------------
 // Any anomaly (truncation, non-canonical varint, invalid UTF-8, a payload kind this path does not
 // verify) sets `bad`; the general path then reproduces yjs's exact result or error.
 struct Cur {
-  uint32_t p, end;  // byte offsets into the dynamic LDS block
+  uint32_t p, e;
   bool bad;
 };
-__device__ __forceinline__ uint32_t lb(uint32_t off) { return g_smem[off]; }
-__device__ __forceinline__ uint32_t rdb(Cur &c) {
-  if (c.p >= c.end) { c.bad = true; return 0; }
-  return g_smem[c.p++];
-}
-// unaligned 8-byte little-endian window at LDS offset p (two aligned dword reads + funnel shift);
-// the staging buffer has >= 8 bytes of slack past every document
-__device__ __forceinline__ uint64_t win8(uint32_t p) {
-  const uint32_t a = p & ~3u;
-  const uint32_t w0 = *reinterpret_cast<const uint32_t *>(g_smem + a);
-  const uint32_t w1 = *reinterpret_cast<const uint32_t *>(g_smem + a + 4);
-  const uint32_t w2 = *reinterpret_cast<const uint32_t *>(g_smem + a + 8);
-  const uint32_t sh = (p & 3u) * 8u;
-  const uint64_t lo = ((uint64_t)w1 << 32) | w0;
-  return sh ? (lo >> sh) | ((uint64_t)w2 << (64 - sh)) : lo;
-}
-// lib0 readVarUint, canonical encodings only, branch-free over a 5-byte window
+// lib0 readVarUint (u32, canonical encodings only) from one unaligned 8-byte window
 __device__ __forceinline__ uint32_t rvu(Cur &c) {
-  const uint64_t x = win8(c.p);
-  const uint64_t stop = ~x & 0x8080808080ull;
-  if (stop == 0) { c.bad = true; return 0; }
-  const uint32_t nb = (uint32_t)(__builtin_ctzll(stop) >> 3) + 1;
-  uint64_t v = (x & 0x7full) | ((x >> 1) & (0x7full << 7)) | ((x >> 2) & (0x7full << 14)) |
-               ((x >> 3) & (0x7full << 21)) | ((x >> 4) & (0x7full << 28));
-  v &= (1ull << (7 * nb)) - 1;
-  const uint32_t last = (uint32_t)(x >> (8 * (nb - 1))) & 0xff;
-  if ((nb > 1 && last == 0) || v > 0xffffffffull || nb > c.end - c.p) c.bad = true;
+  const uint64_t x = ld8(c.p);
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const uint32_t stop = ~lo & 0x80808080u;
+  const uint32_t nb = stop ? (__builtin_ctz(stop) >> 3) + 1 : ((hi & 0x80u) ? 0u : 5u);
+  uint32_t v = (lo & 0x7fu) | ((lo >> 1) & 0x3f80u) | ((lo >> 2) & 0x1fc000u) | ((lo >> 3) & 0xfe00000u) | (hi << 28);
+  if (nb < 5) v &= (1u << (7 * nb)) - 1u;
+  const bool noncanon = nb > 1 && v < (1u << (7 * nb - 7));
+  c.bad |= nb == 0 || c.p + nb > c.e || noncanon || (nb == 5 && (hi & 0x70u));
   c.p += nb;
-  return (uint32_t)v;
+  return v;
 }
-// strict UTF-8 (decodeURIComponent(escape(..))) over the next n bytes; returns the UTF-16 length
-__device__ __forceinline__ uint32_t utf8_len16(Cur &c, uint32_t n) {
-  if (n > c.end - c.p) { c.bad = true; return 0; }
-  {  // ASCII fast path: 8 bytes per window
-    uint64_t hi = 0;
-    for (uint32_t o = 0; o < n; o += 8) {
-      uint64_t x = win8(c.p + o);
-      if (n - o < 8) x &= (1ull << (8 * (n - o))) - 1;
-      hi |= x;
-    }
-    if ((hi & 0x8080808080808080ull) == 0) { c.p += n; return n; }
-  }
-  uint32_t i = c.p, u = 0;
-  const uint32_t e = c.p + n;
+__device__ __forceinline__ uint32_t rdb(Cur &c) {
+  c.bad |= c.p >= c.e;
+  return sm[c.p++];
+}
+__device__ __forceinline__ bool room(const Cur &c, uint32_t n) { return c.p <= c.e && n <= c.e - c.p; }
+// strict UTF-8 (lib0: decodeURIComponent(escape(..))) over the next n bytes; returns the UTF-16 length
+__device__ __forceinline__ uint32_t utf8_slow(uint32_t i, uint32_t e, bool &bad) {
+  uint32_t u = 0;
   while (i < e) {
-    const uint32_t b = lb(i);
+    const uint32_t b = sm[i];
     if (b < 0x80) { u++; i++; continue; }
     uint32_t len, cp, mn;
     if ((b & 0xE0) == 0xC0) { len = 2; cp = b & 0x1F; mn = 0x80; }
     else if ((b & 0xF0) == 0xE0) { len = 3; cp = b & 0x0F; mn = 0x800; }
     else if ((b & 0xF8) == 0xF0) { len = 4; cp = b & 0x07; mn = 0x10000; }
-    else { c.bad = true; return 0; }
-    if (i + len > e) { c.bad = true; return 0; }
+    else { bad = true; return 0; }
+    if (i + len > e) { bad = true; return 0; }
     for (uint32_t q = 1; q < len; q++) {
-      const uint32_t cb = lb(i + q);
-      if ((cb & 0xC0) != 0x80) { c.bad = true; return 0; }
+      const uint32_t cb = sm[i + q];
+      if ((cb & 0xC0) != 0x80) { bad = true; return 0; }
       cp = (cp << 6) | (cb & 0x3F);
     }
-    if (cp < mn || cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF)) { c.bad = true; return 0; }
+    if (cp < mn || cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF)) { bad = true; return 0; }
     u += cp >= 0x10000 ? 2 : 1;
     i += len;
   }
-  c.p = e;
   return u;
 }
-__device__ __forceinline__ uint32_t rstr(Cur &c) {  // varString -> UTF-16 length
+__device__ __forceinline__ uint64_t mask_bytes(uint64_t x, uint32_t n) { return n >= 8 ? x : x & ((1ull << (8 * n)) - 1); }
+__device__ __forceinline__ uint32_t utf16_len(Cur &c, uint32_t n) {
+  if (!room(c, n)) { c.bad = true; return 0; }
+  uint64_t hi = 0;
+  for (uint32_t o = 0; o < n; o += 8) hi |= mask_bytes(ld8(c.p + o), n - o);
+  uint32_t u = n;
+  if (hi & 0x8080808080808080ull) u = utf8_slow(c.p, c.p + n, c.bad);
+  c.p += n;
+  return u;
+}
+__device__ __forceinline__ uint32_t rstr(Cur &c) {
   const uint32_t n = rvu(c);
-  if (c.bad) return 0;
-  return utf8_len16(c, n);
+  return c.bad ? 0 : utf16_len(c, n);
+}
+// SWAR: bytes of x equal to b / below 0x20 (exact per byte for the masked-in bytes)
+__device__ __forceinline__ uint64_t has_byte(uint64_t x, uint64_t b) {
+  const uint64_t y = x ^ (0x0101010101010101ull * b);
+  return (y - 0x0101010101010101ull) & ~y & 0x8080808080808080ull;
+}
+__device__ __forceinline__ uint64_t has_ctl(uint64_t x) {
+  return (x - 0x2020202020202020ull) & ~x & 0x8080808080808080ull;
 }
 // JSON text as yjs writes it for formats / embeds: true | false | null | "string without escapes"
 __device__ __forceinline__ void json_lit(Cur &c) {
   const uint32_t n = rvu(c);
-  if (c.bad || n > c.end - c.p) { c.bad = true; return; }
-  const uint8_t *t = g_smem + c.p;
-  bool ok = false;
-  if (n == 4 && t[0] == 't' && t[1] == 'r' && t[2] == 'u' && t[3] == 'e') ok = true;
-  else if (n == 4 && t[0] == 'n' && t[1] == 'u' && t[2] == 'l' && t[3] == 'l') ok = true;
-  else if (n == 5 && t[0] == 'f' && t[1] == 'a' && t[2] == 'l' && t[3] == 's' && t[4] == 'e') ok = true;
-  else if (n >= 2 && t[0] == '"' && t[n - 1] == '"') {
-    ok = true;
-    for (uint32_t i = 1; i + 1 < n; i++)
-      if (t[i] < 0x20 || t[i] == '"' || t[i] == '\\') ok = false;
+  if (c.bad || !room(c, n)) { c.bad = true; return; }
+  const uint64_t w = ld8(c.p);
+  bool ok;
+  if (n == 4) ok = (uint32_t)w == 0x65757274u || (uint32_t)w == 0x6c6c756eu;  // "true" / "null"
+  else if (n == 5) ok = (w & 0xffffffffffull) == 0x65736c6166ull;            // "false"
+  else ok = false;
+  if (!ok && n >= 2 && (w & 0xff) == '"' && sm[c.p + n - 1] == '"') {
+    // interior bytes [1, n-1): no control characters, quotes or backslashes.  Bytes >= 0x80 are
+    // masked out of the control test (multi-byte UTF-8 is checked by utf16_len below).
+    uint64_t bad = 0;
+    for (uint32_t o = 1; o + 1 < n; o += 8) {
+      uint64_t x = mask_bytes(ld8(c.p + o), n - 1 - o);
+      const uint64_t pad = (n - 1 - o) >= 8 ? 0 : ~0ull << (8 * (n - 1 - o));
+      const uint64_t xs = x | (pad & 0x4040404040404040ull);  // padding bytes look like '@'
+      bad |= has_byte(xs, '"') | has_byte(xs, '\\') | (has_ctl(xs) & ~xs);
+    }
+    ok = bad == 0;
   }
   if (!ok) { c.bad = true; return; }
-  utf8_len16(c, n);
+  utf16_len(c, n);
 }
 // one scalar `any` value in the canonical form lib0 writeAny emits (objects/arrays: general path)
 __device__ __forceinline__ void any_scalar(Cur &c) {
   const uint32_t tag = rdb(c);
   switch (tag) {
-    case 127: case 126: case 121: case 120: return;
+    case 127: case 126: case 121: case 120: return;  // undefined, null, false, true
     case 125: {  // varInt: minimal, and <= 2^31-1 when positive (larger is written as a float)
       uint32_t b = rdb(c);
       uint64_t mag = b & 63;
       const bool neg = b & 64;
       int s = 6, nb = 1;
-      while (b & 128) {
+      while ((b & 128) && !c.bad) {
         b = rdb(c);
-        if (c.bad || s > 34) { c.bad = true; return; }
+        if (s > 34) { c.bad = true; return; }
         mag |= (uint64_t)(b & 127) << s;
         s += 7;
         nb++;
@@ -204,17 +244,16 @@ __device__ __forceinline__ void any_scalar(Cur &c) {
       return;
     }
     case 124: {  // float32, not an integer <= 2^31-1 (those are written as varInt), not NaN
-      if (c.end - c.p < 4) { c.bad = true; return; }
-      const uint32_t u = (lb(c.p) << 24) | (lb(c.p + 1) << 16) | (lb(c.p + 2) << 8) | lb(c.p + 3);
+      if (!room(c, 4)) { c.bad = true; return; }
+      const uint32_t u = __builtin_bswap32(ld4(c.p));
       const float f = __uint_as_float(u);
       if (f != f || (truncf(f) == f && (double)f <= 2147483647.0)) c.bad = true;
       c.p += 4;
       return;
     }
     case 123: {  // float64 that is neither a small integer nor float32-exact
-      if (c.end - c.p < 8) { c.bad = true; return; }
-      uint64_t u = 0;
-      for (int i = 0; i < 8; i++) u = (u << 8) | lb(c.p + i);
+      if (!room(c, 8)) { c.bad = true; return; }
+      const uint64_t u = __builtin_bswap64(ld8(c.p));
       const double x = __longlong_as_double((long long)u);
       if (x == x && ((trunc(x) == x && x <= 2147483647.0) || (double)(float)x == x)) c.bad = true;
       c.p += 8;
@@ -225,27 +264,22 @@ __device__ __forceinline__ void any_scalar(Cur &c) {
   }
 }
 
-// Walks update u (LDS bytes [base+uoff[u], base+uoff[u+1])) and appends its structs and delete-set
-// entries to the document's record arrays through LDS atomic slot counters (misc[2], misc[3]); the
-// records are sorted afterwards, and a delete entry's payload (update << 8 | position) keeps yjs's
+// Walks update u and appends its structs and delete ranges to the record arrays (slots from LDS
+// atomic counters misc[0] / misc[1]).  A delete range's payload (u << 8 | position) keeps yjs's
 // first-appearance order.  Returns false to decline the document.
-template <class C>
-__device__ __attribute__((noinline)) bool walk_v1(uint32_t base, uint32_t u) {
-  using L = Lay<C>;
-  const uint16_t *uoff = lds<uint16_t>(L::uoff);
-  uint32_t *misc = lds<uint32_t>(L::misc);
-  Cur c = {(uint32_t)L::in + base + uoff[u], (uint32_t)L::in + base + uoff[u + 1], false};
+__device__ __forceinline__ bool walk_update(uint32_t u) {
+  Cur c = {at<uint16_t>(L_UOFF + 2 * u), at<uint16_t>(L_UOFF + 2 * u + 2), false};
   const uint32_t nclients = rvu(c);
   uint64_t prev = 0;
   bool have_prev = false;
   for (uint32_t ci = 0; ci < nclients && !c.bad; ci++) {
     const uint32_t nstructs = rvu(c);
     const uint32_t client = rvu(c);
-    uint64_t clock = rvu(c);
+    uint32_t clock = rvu(c);
     for (uint32_t si = 0; si < nstructs && !c.bad; si++) {
       const uint32_t s0 = c.p;
       const uint32_t info = rdb(c);
-      if (c.bad || info == 10 || (info & 31) == 0) return false;  // Skip / GC -> general path
+      if (info == 10 || (info & 31) == 0) return false;  // Skip / GC -> general path
       if (info & 0x80) { rvu(c); rvu(c); }
       if (info & 0x40) { rvu(c); rvu(c); }
       if ((info & 0xC0) == 0) {
@@ -255,41 +289,39 @@ __device__ __attribute__((noinline)) bool walk_v1(uint32_t base, uint32_t u) {
         else { rvu(c); rvu(c); }
         if (info & 0x20) rstr(c);
       }
-      uint64_t len = 1;
+      uint32_t len = 1;
       switch (info & 31) {
-        case 1: len = rvu(c); break;                                           // ContentDeleted
-        case 3: { const uint32_t n = rvu(c); if (n > c.end - c.p) c.bad = true; else c.p += n; break; }  // Binary
-        case 4: len = rstr(c); break;                                          // ContentString
-        case 5: json_lit(c); break;                                            // ContentEmbed
-        case 6: rstr(c); json_lit(c); break;                                   // ContentFormat
-        case 7: {                                                              // ContentType
+        case 1: len = rvu(c); break;                                      // ContentDeleted
+        case 3: { const uint32_t n = rvu(c); if (!room(c, n)) c.bad = true; else c.p += n; break; }  // Binary
+        case 4: len = rstr(c); break;                                     // ContentString
+        case 5: json_lit(c); break;                                       // ContentEmbed
+        case 6: rstr(c); json_lit(c); break;                              // ContentFormat
+        case 7: {                                                         // ContentType
           const uint32_t t = rvu(c);
           if (t > 6) return false;
           if (t == 3 || t == 5) rstr(c);
           break;
         }
-        case 8:                                                                // ContentAny
+        case 8:                                                           // ContentAny
           len = rvu(c);
-          for (uint64_t i = 0; i < len && !c.bad; i++) any_scalar(c);
+          for (uint32_t i = 0; i < len && !c.bad; i++) any_scalar(c);
           break;
         default: return false;  // ContentJSON, ContentDoc, invalid refs
       }
       if (c.bad || len == 0) return false;
-      const uint64_t end = clock + len;
-      if (end > 0xffffffffull) return false;
+      if ((uint64_t)clock + len > 0xffffffffull) return false;
       const uint64_t key = ((uint64_t)(~client) << 32) | clock;
       if (have_prev && key <= prev) return false;  // each update must already be in merge order
       prev = key + len - 1;
       have_prev = true;
-      const uint32_t q = atomicAdd(&misc[2], 1u);
-      if (q >= (uint32_t)C::kRec) return false;
-      lds<uint64_t>(L::rkey)[q] = key;
-      lds<uint32_t>(L::rlen)[q] = (uint32_t)len;
-      lds<uint16_t>(L::rstart)[q] = (uint16_t)(s0 - L::in);
-      lds<uint16_t>(L::rblen)[q] = (uint16_t)(c.p - s0);
-      lds<uint8_t>(L::rinfo)[q] = (uint8_t)info;
-      lds<uint16_t>(L::ridx)[q] = (uint16_t)q;
-      clock = end;
+      const uint32_t q = atomicAdd(&at<uint32_t>(L_MISC), 1u);
+      if (q >= REC) return false;
+      at<uint64_t>(L_RKEY + 8 * q) = key;
+      at<uint32_t>(L_RLEN + 4 * q) = len;
+      at<uint16_t>(L_RSRC + 2 * q) = (uint16_t)s0;
+      at<uint16_t>(L_RBLEN + 2 * q) = (uint16_t)(c.p - s0);
+      at<uint8_t>(L_RINFO + q) = (uint8_t)info;
+      clock += len;
     }
   }
   if (c.bad) return false;
@@ -302,314 +334,473 @@ __device__ __attribute__((noinline)) bool walk_v1(uint32_t base, uint32_t u) {
       const uint32_t clock = rvu(c);
       const uint32_t len = rvu(c);
       if (c.bad || pos > 255) return false;
-      const uint32_t x = atomicAdd(&misc[3], 1u);
-      if (x >= (uint32_t)C::kDs) return false;
-      lds<uint64_t>(L::dkey)[x] = ((uint64_t)client << 32) | clock;
-      lds<uint32_t>(L::dlen)[x] = len;
-      lds<uint16_t>(L::didx)[x] = (uint16_t)x;
-      lds<uint16_t>(L::dseq)[x] = (uint16_t)((u << 8) | pos);
+      const uint32_t x = atomicAdd(&at<uint32_t>(L_MISC + 4), 1u);
+      if (x >= DSN) return false;
+      at<uint64_t>(L_DKEY + 8 * x) = ((uint64_t)client << 32) | clock;
+      at<uint32_t>(L_DLEN + 4 * x) = len;
+      at<uint16_t>(L_DSEQ + 2 * x) = (uint16_t)((u << 8) | pos);
     }
   }
   return !c.bad;
 }
 
-__device__ __forceinline__ void bitonic(uint64_t *key, uint16_t *idx, uint32_t n) {
-  const uint32_t lane = threadIdx.x;
-  for (uint32_t size = 2; size <= n; size <<= 1) {
-    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-      __syncthreads();
-      for (uint32_t t = lane; t < n / 2; t += 64) {
-        const uint32_t i = 2 * t - (t & (stride - 1));
-        const uint32_t q = i + stride;
-        const bool up = (i & size) == 0;
-        const uint64_t a = key[i], b = key[q];
-        if ((a > b) == up) {
-          key[i] = b;
-          key[q] = a;
-          const uint16_t x = idx[i];
-          idx[i] = idx[q];
-          idx[q] = x;
-        }
-      }
-    }
+// rank of each of the lane's keys among keys[0..n): #keys <= own (own included) - 1.  Keys past n
+// are ~0 (padding) and never count.  Equal keys collide; callers detect that.
+__device__ __forceinline__ void rank_le(uint32_t keys, uint32_t n, const uint64_t (&k)[E], uint32_t (&rank)[E]) {
+  uint32_t cnt[E];
+#pragma unroll
+  for (uint32_t s = 0; s < E; s++) cnt[s] = 0;
+  for (uint32_t jj = 0; jj < n; jj += 2) {
+    const uint64_t a = at<uint64_t>(keys + 8 * jj), b = at<uint64_t>(keys + 8 * jj + 8);
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++) cnt[s] += (uint32_t)(a <= k[s]) + (uint32_t)(b <= k[s]);
   }
-  __syncthreads();
+#pragma unroll
+  for (uint32_t s = 0; s < E; s++) rank[s] = cnt[s] - 1;
+}
+// exact ranks with ties broken by slot index (used only when equal keys exist)
+__device__ __forceinline__ void rank_exact(uint32_t keys, uint32_t n, const uint64_t (&k)[E], uint32_t (&rank)[E]) {
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t s = 0; s < E; s++) {
+    const uint32_t i = lane + 64 * s;
+    uint32_t cnt = 0;
+    for (uint32_t jj = 0; jj < n; jj++) {
+      const uint64_t a = at<uint64_t>(keys + 8 * jj);
+      cnt += (a < k[s]) || (a == k[s] && jj < i);
+    }
+    rank[s] = cnt;
+  }
 }
 
-// STOP > 0 builds a timing-only variant that ends every document after phase STOP (profiling the
-// phases by ablation, cdna_hip_programming.md §7); outputs of such builds are not meaningful.
-#define YM_STOP(n)                                          \
-  if (STOP == (n)) {                                        \
-    if (lane == 0) { j.status[d] = ym::ST_OK; j.out_len[d] = 0; } \
-    __syncthreads();                                        \
-    continue;                                               \
+#define YM_DECLINE()                                 \
+  {                                                  \
+    if (lane == 0) j.status[d] = ST_PENDING;         \
+    __syncthreads();                                 \
+    continue;                                        \
   }
-template <class C, int STOP>
-__global__ void __launch_bounds__(64) k_fast_merge_v1(GeneralJob j) {
-  using L = Lay<C>;
-  const uint32_t lane = threadIdx.x;
-  uint32_t *misc = lds<uint32_t>(L::misc);
-  uint8_t *in = lds<uint8_t>(L::in);
-  uint8_t *out = lds<uint8_t>(L::out);
-  uint64_t *rkey = lds<uint64_t>(L::rkey);
-  uint64_t *dkey = lds<uint64_t>(L::dkey);
-  uint32_t *rlen = lds<uint32_t>(L::rlen);
-  uint32_t *dlen = lds<uint32_t>(L::dlen);
-  uint32_t *dend = lds<uint32_t>(L::dend);
-  uint16_t *rpos = lds<uint16_t>(L::rpos);
-  uint16_t *rstart = lds<uint16_t>(L::rstart);
-  uint16_t *rblen = lds<uint16_t>(L::rblen);
-  uint16_t *ridx = lds<uint16_t>(L::ridx);
-  uint16_t *didx = lds<uint16_t>(L::didx);
-  uint16_t *dseq = lds<uint16_t>(L::dseq);
-  uint8_t *dflag = lds<uint8_t>(L::dflag);
-  uint8_t *rinfo = lds<uint8_t>(L::rinfo);
-  uint16_t *uoff = lds<uint16_t>(L::uoff);
-  uint16_t *ubase = lds<uint16_t>(L::ubase);
-  uint16_t *dbase = lds<uint16_t>(L::dbase);
-  uint16_t *gstart = lds<uint16_t>(L::gstart);
-  uint16_t *gmin = lds<uint16_t>(L::gmin);
-  uint16_t *gsz = lds<uint16_t>(L::gsz);
-  uint16_t *gcnt = lds<uint16_t>(L::gcnt);
-  uint16_t *grank = lds<uint16_t>(L::grank);
-  uint16_t *roff = lds<uint16_t>(L::roff);
-  constexpr int ROUNDS = (C::kUpd + 63) / 64;
-  const uint64_t arena0 = j.upd_off[0];
+// STOP > 0 builds a timing-only variant that ends every document after phase STOP (profiling the
+// phases by ablation); outputs of such builds are not meaningful.
+#define YM_STOP(n)                                                      \
+  if (STOP == (n)) {                                                    \
+    if (lane == 0) { j.status[d] = ym::ST_OK; j.out_len[d] = 0; }       \
+    __syncthreads();                                                    \
+    continue;                                                           \
+  }
 
+template <int STOP>
+__global__ void __launch_bounds__(64) k_fast_merge_v1(GeneralJob j) {
+  const uint32_t lane = threadIdx.x;
+  const uint64_t arena0 = j.upd_off[0];
   for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
     const uint32_t u0 = j.doc_upd[d], k = j.doc_upd[d + 1] - u0;
     const uint64_t b0 = j.upd_off[u0], bytes = j.upd_off[u0 + k] - b0;
-    if (k <= 1 || k > (uint32_t)C::kUpd || bytes > (uint64_t)C::kIn) {
+    if (k <= 1 || k > UPD || bytes > IN) {
       if (lane == 0) j.status[d] = ST_PENDING;
       continue;
     }
-    // 1. stage with 16-B loads covering [b0, b0 + bytes); `base` = b0 & 15
+    // ---- 1. stage with 16-B loads covering [b0, b0 + bytes); byte b0 lands at LDS offset `base`
     const uint32_t base = (uint32_t)(b0 & 15);
     {
       const uint4 *src = reinterpret_cast<const uint4 *>(j.A + (b0 - base));
       const uint32_t nvec = (uint32_t)((base + bytes + 15) >> 4);
-      for (uint32_t v = lane; v < nvec; v += 64) reinterpret_cast<uint4 *>(in)[v] = src[v];
+      for (uint32_t v = lane; v < nvec; v += 64) at<uint4>(L_IN + 16 * v) = src[v];
     }
-    for (uint32_t i = lane; i <= k; i += 64) uoff[i] = (uint16_t)(j.upd_off[u0 + i] - b0);
+    for (uint32_t i = lane; i <= k; i += 64) at<uint16_t>(L_UOFF + 2 * i) = (uint16_t)(j.upd_off[u0 + i] - b0 + base);
+    if (lane < 2) at<uint32_t>(L_MISC + 4 * lane) = 0;
     __syncthreads();
     YM_STOP(1)
-    // 2. one pass over the updates, one lane per update; records appended through LDS atomics
-    if (lane == 0) { misc[2] = 0; misc[3] = 0; }
-    __syncthreads();
+    // ---- 2. walk: one lane per update
     bool ok = true;
 #pragma unroll 1
-    for (uint32_t u = lane; u < k; u += 64) ok &= walk_v1<C>(base, u);
-    if (__any(!ok)) {
-      if (lane == 0) j.status[d] = ST_PENDING;
-      __syncthreads();
-      continue;
+    for (uint32_t u = lane; u < k; u += 64) ok &= walk_update(u);
+    if (__any(!ok)) YM_DECLINE()
+    __syncthreads();
+    const uint32_t nrec = at<uint32_t>(L_MISC), nds = at<uint32_t>(L_MISC + 4);
+    if (nrec == 0 || nrec > REC || nds > DSN) YM_DECLINE()
+    if (lane == 0) {  // pad the key arrays to even length (rank loops read pairs)
+      if (nrec & 1) at<uint64_t>(L_RKEY + 8 * nrec) = ~0ull;
+      if (nds & 1) at<uint64_t>(L_DKEY + 8 * nds) = ~0ull;
     }
     __syncthreads();
-    const uint32_t nrec = misc[2], nds = misc[3];
-    if (nrec == 0 || nrec > (uint32_t)C::kRec || nds > (uint32_t)C::kDs) {
-      if (lane == 0) j.status[d] = ST_PENDING;
-      __syncthreads();
-      continue;
+    YM_STOP(2)
+    // ---- 3. struct rank sort
+    uint64_t rk[E];
+    uint32_t rl[E], rsrc[E], rbl[E], rinf[E], rr[E];
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++) {
+      const uint32_t i = lane + 64 * s;
+      const bool v = i < nrec;
+      rk[s] = v ? at<uint64_t>(L_RKEY + 8 * i) : ~0ull;
+      rl[s] = v ? at<uint32_t>(L_RLEN + 4 * i) : 0;
+      rsrc[s] = v ? at<uint16_t>(L_RSRC + 2 * i) : 0;
+      rbl[s] = v ? at<uint16_t>(L_RBLEN + 2 * i) : 0;
+      rinf[s] = v ? at<uint8_t>(L_RINFO + i) : 0;
+    }
+    rank_le(L_RKEY, nrec, rk, rr);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++) {
+      const uint32_t i = lane + 64 * s;
+      if (i < nrec) {
+        const uint32_t r = rr[s];
+        at<uint64_t>(L_RKEY + 8 * r) = rk[s];
+        at<uint32_t>(L_RLEN + 4 * r) = rl[s];
+        at<uint16_t>(L_RSRC + 2 * r) = (uint16_t)rsrc[s];
+        at<uint16_t>(L_RBLEN + 2 * r) = (uint16_t)rbl[s];
+        at<uint8_t>(L_RINFO + r) = (uint8_t)rinf[s];
+        at<uint8_t>(L_RSLOT + r) = (uint8_t)i;
+      }
+    }
+    __syncthreads();
+    {
+      bool dup = false;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint32_t i = lane + 64 * s;
+        if (i < nrec) dup |= at<uint8_t>(L_RSLOT + rr[s]) != i;
+      }
+      if (__any(dup)) YM_DECLINE()  // equal (client, clock): overlapping inputs
     }
     YM_STOP(3)
-    uint32_t np2 = 64;
-    while (np2 < nrec) np2 <<= 1;
-    for (uint32_t i = nrec + lane; i < np2; i += 64) { rkey[i] = ~0ull; ridx[i] = 0; }
-    uint32_t dp2 = 64;
-    while (dp2 < nds) dp2 <<= 1;
-    for (uint32_t i = nds + lane; i < dp2; i += 64) { dkey[i] = ~0ull; didx[i] = 0; }
-    // 4. sorts: structs by (client desc, clock asc); delete ranges by (client, clock)
-    bitonic(rkey, ridx, np2);
-    if (nds > 1) bitonic(dkey, didx, dp2);
-    YM_STOP(4)
-    // 5. struct section; lane owns sorted records [lo, hi)
-    const uint32_t per = (nrec + 63) >> 6;
-    const uint32_t lo = lane * per < nrec ? lane * per : nrec;
-    const uint32_t hi = lo + per < nrec ? lo + per : nrec;
+    // ---- 4. struct layout over rank order; lane owns positions r = E*lane + s
+    uint64_t sk[E];
+    uint32_t sl[E], ssrc[E], sbl[E], sinf[E], units[E], pstart[E], plastf[E], gapv[E];
     bool bad = false;
-    uint32_t units = 0;
-    for (uint32_t i = lo; i < hi; i++) {
-      uint32_t un = 1;
-      if (i > 0 && (rkey[i - 1] >> 32) == (rkey[i] >> 32)) {
-        const uint64_t pend = (rkey[i - 1] & 0xffffffffull) + rlen[ridx[i - 1]];
-        const uint64_t cl = rkey[i] & 0xffffffffull;
-        if (pend > cl) bad = true;       // overlapping inputs: general path
-        else if (pend < cl) un = 2;      // a Skip fills the gap
-      }
-      units += un;
-    }
-    if (__any(bad)) {
-      if (lane == 0) j.status[d] = ST_PENDING;
-      __syncthreads();
-      continue;
-    }
     {
-      uint32_t tot_units;
-      uint32_t acc = wave_excl_scan(units, &tot_units);
-      for (uint32_t i = lo; i < hi; i++) {
-        uint32_t un = 1;
-        if (i > 0 && (rkey[i - 1] >> 32) == (rkey[i] >> 32) &&
-            (rkey[i - 1] & 0xffffffffull) + rlen[ridx[i - 1]] < (rkey[i] & 0xffffffffull))
-          un = 2;
-        acc += un;
-        rpos[i] = (uint16_t)acc;  // inclusive prefix of output structs (incl. Skips)
+      const uint32_t r0 = E * lane;
+      uint64_t kp = r0 > 0 && r0 - 1 < nrec ? at<uint64_t>(L_RKEY + 8 * (r0 - 1)) : ~0ull;
+      uint32_t lp = r0 > 0 && r0 - 1 < nrec ? at<uint32_t>(L_RLEN + 4 * (r0 - 1)) : 0;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint32_t r = r0 + s;
+        const bool v = r < nrec;
+        sk[s] = v ? at<uint64_t>(L_RKEY + 8 * r) : ~0ull;
+        sl[s] = v ? at<uint32_t>(L_RLEN + 4 * r) : 0;
+        ssrc[s] = v ? at<uint16_t>(L_RSRC + 2 * r) : 0;
+        sbl[s] = v ? at<uint16_t>(L_RBLEN + 2 * r) : 0;
+        sinf[s] = v ? at<uint8_t>(L_RINFO + r) : 0;
+        const uint64_t kn = r + 1 < nrec ? at<uint64_t>(L_RKEY + 8 * (r + 1)) : ~0ull;
+        const bool same = v && r > 0 && (kp >> 32) == (sk[s] >> 32);
+        const uint64_t pend = (kp & 0xffffffffull) + lp;
+        const uint64_t cl = sk[s] & 0xffffffffull;
+        bad |= same && pend > cl;  // overlapping inputs: general path
+        gapv[s] = same && pend < cl ? (uint32_t)(cl - pend) : 0;
+        units[s] = v ? 1 + (gapv[s] != 0) : 0;
+        pstart[s] = v && !same;
+        plastf[s] = v && (r + 1 >= nrec || (kn >> 32) != (sk[s] >> 32));
+        kp = sk[s];
+        lp = sl[s];
+      }
+    }
+    if (__any(bad)) YM_DECLINE()
+    // one scan for (parts << 16 | units)
+    uint32_t pu[E], pu_lane = 0, nparts;
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++) pu_lane += (pstart[s] << 16) | units[s];
+    {
+      const uint32_t incl = wave_incl_add(pu_lane);
+      nparts = lane_read(incl, 63) >> 16;
+      uint32_t run = incl - pu_lane;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        pu[s] = run;  // exclusive (parts, units) before position r
+        run += (pstart[s] << 16) | units[s];
+        const uint32_t pid = (run >> 16) - 1;
+        if (pstart[s]) at<uint16_t>(L_PFIRST + 2 * pid) = (uint16_t)(pu[s] & 0xffff);
+        if (plastf[s]) at<uint16_t>(L_PLAST + 2 * pid) = (uint16_t)(run & 0xffff);
       }
     }
     __syncthreads();
-    uint32_t bytes_l = 0, parts_l = 0;
-    for (uint32_t i = lo; i < hi; i++) {
-      const uint64_t key = rkey[i];
-      bytes_l += rblen[ridx[i]];
-      if (i == 0 || (rkey[i - 1] >> 32) != (key >> 32)) {  // part header: vu(#structs) vu(client) vu(clock)
-        uint32_t e = i + 1;
-        while (e < nrec && (rkey[e] >> 32) == (key >> 32)) e++;
-        const uint32_t run_units = rpos[e - 1] - (i ? rpos[i - 1] : 0);
-        bytes_l += vsz(run_units) + vsz(~(uint32_t)(key >> 32)) + vsz(key & 0xffffffffull);
-        parts_l++;
-      } else {
-        const uint64_t pend = (rkey[i - 1] & 0xffffffffull) + rlen[ridx[i - 1]];
-        if (pend < (key & 0xffffffffull)) bytes_l += 1 + vsz((key & 0xffffffffull) - pend);
+    uint32_t runu[E], soff[E], sbytes_lane = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++) {
+      runu[s] = 0;
+      uint32_t b = sbl[s];
+      if (pstart[s]) {
+        const uint32_t pid = pu[s] >> 16;
+        runu[s] = at<uint16_t>(L_PLAST + 2 * pid) - at<uint16_t>(L_PFIRST + 2 * pid);
+        b += vsz(runu[s]) + vsz(~(uint32_t)(sk[s] >> 32)) + vsz(sk[s] & 0xffffffffull);
       }
+      if (gapv[s]) b += 1 + vsz(gapv[s]);
+      soff[s] = b;
+      sbytes_lane += b;
     }
-    uint32_t struct_bytes, nparts;
-    const uint32_t b_excl = wave_excl_scan(bytes_l, &struct_bytes);
-    wave_excl_scan(parts_l, &nparts);
+    uint32_t struct_bytes;
+    {
+      const uint32_t incl = wave_incl_add(sbytes_lane);
+      struct_bytes = lane_read(incl, 63);
+      uint32_t run = incl - sbytes_lane;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) { const uint32_t b = soff[s]; soff[s] = run; run += b; }
+    }
     const uint32_t hdr = vsz(nparts);
-    YM_STOP(5)
-    // 6. delete set.  Groups = clients (runs of equal client in the sorted entries).
-    const uint32_t dper = (nds + 63) >> 6;
-    const uint32_t dlo = lane * dper < nds ? lane * dper : nds;
-    const uint32_t dhi = dlo + dper < nds ? dlo + dper : nds;
-    uint32_t gs_l = 0;
-    for (uint32_t i = dlo; i < dhi; i++) gs_l += (i == 0 || (dkey[i] >> 32) != (dkey[i - 1] >> 32));
-    uint32_t ngroups;
-    uint32_t g = wave_excl_scan(gs_l, &ngroups);
-    for (uint32_t i = dlo; i < dhi; i++)
-      if (i == 0 || (dkey[i] >> 32) != (dkey[i - 1] >> 32)) gstart[g++] = (uint16_t)i;
-    if (lane == 0) gstart[ngroups] = (uint16_t)nds;
+    YM_STOP(4)
+    // ---- 5. delete set
+    uint64_t dk[E];
+    uint32_t dl[E], dq[E], dr[E];
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++) {
+      const uint32_t i = lane + 64 * s;
+      const bool v = i < nds;
+      dk[s] = v ? at<uint64_t>(L_DKEY + 8 * i) : ~0ull;
+      dl[s] = v ? at<uint32_t>(L_DLEN + 4 * i) : 0;
+      dq[s] = v ? at<uint16_t>(L_DSEQ + 2 * i) : 0;
+    }
+    rank_le(L_DKEY, nds, dk, dr);
     __syncthreads();
-    // one lane per group: in-place union (>= merges touching ranges), count, bytes, first appearance
-    for (uint32_t gg = lane; gg < ngroups; gg += 64) {
-      const uint32_t s = gstart[gg], e = gstart[gg + 1];
-      uint32_t mn = 0xffff, cnt = 0, sz = 0, open = s;
-      uint64_t cure = 0;
-      for (uint32_t i = s; i < e; i++) {
-        const uint32_t id = didx[i];
-        if (dseq[id] < mn) mn = dseq[id];
-        const uint64_t c0 = dkey[i] & 0xffffffffull;
-        const uint64_t en = c0 + dlen[id];
-        if (i == s || c0 > cure) {
-          if (i != s) { dend[open] = (uint32_t)cure; sz += vsz(dkey[open] & 0xffffffffull) + vsz(cure - (dkey[open] & 0xffffffffull)); }
-          open = i;
-          cure = en;
-          dflag[i] = 1;
-          cnt++;
-        } else {
-          dflag[i] = 0;
-          if (en > cure) cure = en;
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++) {
+      const uint32_t i = lane + 64 * s;
+      if (i < nds) at<uint8_t>(L_DSLOT + dr[s]) = (uint8_t)i;
+    }
+    __syncthreads();
+    {
+      bool dup = false;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint32_t i = lane + 64 * s;
+        if (i < nds) dup |= at<uint8_t>(L_DSLOT + dr[s]) != i;
+      }
+      if (__any(dup)) rank_exact(L_DKEY, nds, dk, dr);  // equal (client, clock) in several inputs
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++) {
+      if (lane + 64 * s < nds) {
+        const uint32_t r = dr[s];
+        at<uint64_t>(L_DKEY + 8 * r) = dk[s];
+        at<uint32_t>(L_DLEN + 4 * r) = dl[s];
+        at<uint16_t>(L_DSEQ + 2 * r) = (uint16_t)dq[s];
+      }
+    }
+    if (lane == 0) at<uint32_t>(L_MISC + 8) = 0;
+    __syncthreads();
+    // sorted positions r = E*lane + s: segments (clients), running max end, merged ranges
+    uint64_t ek[E], eend[E];
+    uint32_t eseq[E], segst[E], newr[E];
+    uint32_t seg_lane = 0;
+    {
+      const uint32_t r0 = E * lane;
+      uint64_t kp = r0 > 0 && r0 - 1 < nds ? at<uint64_t>(L_DKEY + 8 * (r0 - 1)) : ~0ull;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint32_t r = r0 + s;
+        const bool v = r < nds;
+        ek[s] = v ? at<uint64_t>(L_DKEY + 8 * r) : 0;
+        eend[s] = v ? (ek[s] & 0xffffffffull) + at<uint32_t>(L_DLEN + 4 * r) : 0;
+        eseq[s] = v ? at<uint16_t>(L_DSEQ + 2 * r) : 0xffff;
+        segst[s] = v && (r == 0 || (kp >> 32) != (ek[s] >> 32));
+        seg_lane += segst[s];
+        kp = ek[s];
+      }
+    }
+    uint32_t segid[E], ngroups;
+    {
+      const uint32_t incl = wave_incl_add(seg_lane);
+      ngroups = lane_read(incl, 63);
+      uint32_t run = incl - seg_lane;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) { run += segst[s]; segid[s] = run - 1; }
+    }
+    // running max of (segment << 33 | end): within a segment it is the max end so far
+    uint64_t rmax[E];
+    {
+      uint64_t m = 0;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint64_t x = E * lane + s < nds ? ((uint64_t)segid[s] << 33) | eend[s] : 0;
+        m = x > m ? x : m;
+        rmax[s] = m;
+      }
+      const uint64_t incl = wave_incl_max64(m);
+      uint64_t ex = ((uint64_t)from_prev_lane((uint32_t)(incl >> 32)) << 32) | from_prev_lane((uint32_t)incl);
+      uint32_t nr_lane = 0;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint64_t before = ex;  // running max through position r - 1
+        rmax[s] = rmax[s] > ex ? rmax[s] : ex;
+        ex = rmax[s];
+        const bool v = E * lane + s < nds;
+        const uint64_t cl = ek[s] & 0xffffffffull;
+        newr[s] = v && (segst[s] || cl > (before & 0x1ffffffffull));
+        nr_lane += newr[s];
+      }
+      // merged-range ids
+      const uint32_t incl_r = wave_incl_add(nr_lane);
+      const uint32_t nranges_ = lane_read(incl_r, 63);
+      uint32_t run = incl_r - nr_lane;
+      const uint32_t next_first = from_next_lane(newr[0]);  // newr of position E*(lane+1)
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint32_t r = E * lane + s;
+        if (r >= nds) break;
+        run += newr[s];
+        const uint32_t rid = run - 1;
+        if (newr[s]) {
+          at<uint32_t>(L_QCLK + 4 * rid) = (uint32_t)(ek[s] & 0xffffffffull);
+          at<uint8_t>(L_QGRP + rid) = (uint8_t)segid[s];
+        }
+        const bool nxt_new = s + 1 < E ? newr[s + 1] != 0 : next_first != 0;
+        if (r + 1 >= nds || nxt_new) {
+          const uint64_t en = rmax[s] & 0x1ffffffffull;
+          if (en > 0xffffffffull) bad = true;
+          at<uint32_t>(L_QEND + 4 * rid) = (uint32_t)en;
+        }
+        if (segst[s]) {
+          at<uint16_t>(L_GFIRST + 2 * segid[s]) = (uint16_t)rid;
+          at<uint32_t>(L_GCLI + 4 * segid[s]) = (uint32_t)(ek[s] >> 32);
+          at<uint32_t>(L_GMIN + 4 * segid[s]) = 0xffffffffu;
         }
       }
-      dend[open] = (uint32_t)cure;
-      sz += vsz(dkey[open] & 0xffffffffull) + vsz(cure - (dkey[open] & 0xffffffffull));
-      sz += vsz(dkey[s] >> 32) + vsz(cnt);
-      gmin[gg] = (uint16_t)mn;
-      gsz[gg] = (uint16_t)sz;
-      gcnt[gg] = (uint16_t)cnt;
+      if (lane == 0) {
+        at<uint16_t>(L_GFIRST + 2 * ngroups) = (uint16_t)nranges_;
+        at<uint32_t>(L_MISC + 8) = nranges_;
+      }
     }
+    if (__any(bad)) YM_DECLINE()
     __syncthreads();
-    // rank groups by first appearance; lay out their bytes in rank order
-    for (uint32_t gg = lane; gg < ngroups; gg += 64) {
-      uint32_t r = 0;
-      const uint32_t m = gmin[gg];
-      for (uint32_t h = 0; h < ngroups; h++) r += gmin[h] < m;
-      grank[gg] = (uint16_t)r;
-      roff[r] = gsz[gg];
+    // first appearance of each client (min over its entries' update << 8 | position)
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++)
+      if (E * lane + s < nds) atomicMin(&at<uint32_t>(L_GMIN + 4 * segid[s]), eseq[s]);
+    const uint32_t nranges = at<uint32_t>(L_MISC + 8);
+    // merged ranges q = E*lane + s: bytes, exclusive prefix over range ids
+    uint32_t qclk[E], qlen[E], qgrp[E], qoff[E], qb_lane = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++) {
+      const uint32_t q = E * lane + s;
+      const bool v = q < nranges;
+      qclk[s] = v ? at<uint32_t>(L_QCLK + 4 * q) : 0;
+      qlen[s] = v ? at<uint32_t>(L_QEND + 4 * q) - qclk[s] : 0;
+      qgrp[s] = v ? at<uint8_t>(L_QGRP + q) : 0;
+      qoff[s] = v ? vsz(qclk[s]) + vsz(qlen[s]) : 0;
+      qb_lane += qoff[s];
     }
-    __syncthreads();
     {
-      const uint32_t gper = (ngroups + 63) >> 6;
-      const uint32_t glo = lane * gper < ngroups ? lane * gper : ngroups;
-      const uint32_t ghi = glo + gper < ngroups ? glo + gper : ngroups;
-      uint32_t s = 0;
-      for (uint32_t r = glo; r < ghi; r++) s += roff[r];
-      uint32_t tot;
-      uint32_t ex = wave_excl_scan(s, &tot);
-      for (uint32_t r = glo; r < ghi; r++) { const uint32_t v = roff[r]; roff[r] = (uint16_t)ex; ex += v; }
-      if (lane == 0) misc[1] = tot;
+      const uint32_t incl = wave_incl_add(qb_lane);
+      uint32_t run = incl - qb_lane;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint32_t q = E * lane + s;
+        const uint32_t b = qoff[s];
+        qoff[s] = run;
+        if (q < nranges) at<uint16_t>(L_QPRE + 2 * q) = (uint16_t)run;
+        run += b;
+      }
+      if (lane == 63) at<uint16_t>(L_QPRE + 2 * nranges) = (uint16_t)incl;
     }
     __syncthreads();
-    const uint32_t ds_bytes = vsz(ngroups) + misc[1];
-    const uint32_t total = hdr + struct_bytes + ds_bytes;
+    // groups g = lane + 64 s: header, bytes, rank by first appearance
+    uint32_t gcli[E], gcnt[E], grk[E], gbytes[E], gq0[E];
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++) {
+      const uint32_t g = lane + 64 * s;
+      const bool v = g < ngroups;
+      const uint32_t f0 = v ? at<uint16_t>(L_GFIRST + 2 * g) : 0, f1 = v ? at<uint16_t>(L_GFIRST + 2 * g + 2) : 0;
+      gcli[s] = v ? at<uint32_t>(L_GCLI + 4 * g) : 0;
+      gcnt[s] = f1 - f0;
+      gq0[s] = v ? at<uint16_t>(L_QPRE + 2 * f0) : 0;
+      gbytes[s] = v ? vsz(gcli[s]) + vsz(gcnt[s]) + at<uint16_t>(L_QPRE + 2 * f1) - gq0[s] : 0;
+      const uint32_t mine = v ? at<uint32_t>(L_GMIN + 4 * g) : 0;
+      uint32_t rk_ = 0;
+      for (uint32_t h = 0; h < ngroups; h++) rk_ += at<uint32_t>(L_GMIN + 4 * h) < mine;
+      grk[s] = rk_;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++)
+      if (lane + 64 * s < ngroups) at<uint16_t>(L_GBYR + 2 * grk[s]) = (uint16_t)gbytes[s];
+    __syncthreads();
+    uint32_t ds_groups_bytes;
+    {  // exclusive prefix over ranks (ranks E*lane + s), in place
+      uint32_t v[E], t = 0;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) { const uint32_t r = E * lane + s; v[s] = r < ngroups ? at<uint16_t>(L_GBYR + 2 * r) : 0; t += v[s]; }
+      const uint32_t incl = wave_incl_add(t);
+      ds_groups_bytes = lane_read(incl, 63);
+      uint32_t run = incl - t;
+      __syncthreads();
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint32_t r = E * lane + s;
+        if (r < ngroups) at<uint16_t>(L_GBYR + 2 * r) = (uint16_t)run;
+        run += v[s];
+      }
+    }
+    __syncthreads();
+    const uint32_t ds_hdr = vsz(ngroups);
+    const uint32_t dsb = hdr + struct_bytes;
+    uint32_t goff[E];
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++) goff[s] = lane + 64 * s < ngroups ? dsb + ds_hdr + at<uint16_t>(L_GBYR + 2 * grk[s]) : 0;
+    // merged range q's output offset: its group's offset + group header + prefix within the group.
+    // Per-group base (offset + header - prefix of its first range) by group id, through LDS.
+    __syncthreads();
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++)
+      if (lane + 64 * s < ngroups)
+        at<uint32_t>(L_GMIN + 4 * (lane + 64 * s)) = goff[s] + vsz(gcli[s]) + vsz(gcnt[s]) - gq0[s];
+    __syncthreads();
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++)
+      if (E * lane + s < nranges) qoff[s] += at<uint32_t>(L_GMIN + 4 * qgrp[s]);
+    const uint32_t total = dsb + ds_hdr + ds_groups_bytes;
     // output slot: 16-aligned inside the bound 2 * in + 64 per doc
     const uint64_t slot = 2 * (b0 - arena0) + 64ull * d;
     const uint64_t slot_al = (slot + 15) & ~15ull;
-    if (total > (uint32_t)C::kOut || slot_al + total > slot + 2 * bytes + 64) {
-      if (lane == 0) j.status[d] = ST_PENDING;
-      __syncthreads();
-      continue;
-    }
+    if (total > OUT || slot_al + total > slot + 2 * bytes + 64) YM_DECLINE()
     if (slot_al + total > j.cap) {  // caller's arena is smaller than the fast region
       if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }
       __syncthreads();
       continue;
     }
-    YM_STOP(6)
-    // 7. struct section into LDS staging
-    if (lane == 0) put_vu(out, 0, nparts);
-    {
-      uint32_t p = hdr + b_excl;
-      for (uint32_t i = lo; i < hi; i++) {
-        const uint32_t id = ridx[i];
-        const uint64_t key = rkey[i];
-        const uint64_t clock = key & 0xffffffffull;
-        if (i == 0 || (rkey[i - 1] >> 32) != (key >> 32)) {
-          uint32_t e = i + 1;
-          while (e < nrec && (rkey[e] >> 32) == (key >> 32)) e++;
-          const uint32_t run_units = rpos[e - 1] - (i ? rpos[i - 1] : 0);
-          p = put_vu(out, p, run_units);
-          p = put_vu(out, p, ~(uint32_t)(key >> 32));
-          p = put_vu(out, p, clock);
-        } else {
-          const uint64_t pend = (rkey[i - 1] & 0xffffffffull) + rlen[ridx[i - 1]];
-          if (pend < clock) {  // Skip: info 10 + varuint length (13.5.16 ui.write)
-            out[p++] = 10;
-            p = put_vu(out, p, clock - pend);
-          }
-        }
-        uint32_t info = rinfo[id];
-        if (info & 0xC0) info &= ~0x20u;  // parentSub is only read / re-written without origins
-        out[p++] = (uint8_t)info;
-        const uint32_t s0 = rstart[id] + 1, n = rblen[id] - 1;
-        for (uint32_t b = 0; b < n; b++) out[p + b] = in[s0 + b];
-        p += n;
+    YM_STOP(5)
+    __syncthreads();  // every record / range array is dead: L_OUT aliases them
+    // ---- 6. emit
+    if (lane == 0) put_vu(L_OUT, nparts);
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++) {
+      if (E * lane + s >= nrec) break;
+      uint32_t p = L_OUT + hdr + soff[s];
+      if (pstart[s]) {  // part header: vu(#structs incl. skips) vu(client) vu(clock)
+        p = put_vu(p, runu[s]);
+        p = put_vu(p, ~(uint32_t)(sk[s] >> 32));
+        p = put_vu(p, sk[s] & 0xffffffffull);
       }
+      if (gapv[s]) {  // Skip: info 10 + varuint length (13.5.16 ui.write)
+        sm[p++] = 10;
+        p = put_vu(p, gapv[s]);
+      }
+      uint32_t info = sinf[s];
+      if (info & 0xC0) info &= ~0x20u;  // parentSub is only read / re-written without origins (E8)
+      sm[p++] = (uint8_t)info;
+      const uint32_t n = sbl[s] - 1, src = ssrc[s] + 1;
+      uint32_t o = 0;
+      for (; o + 4 <= n; o += 4) st4(p + o, ld4(src + o));
+      for (; o < n; o++) sm[p + o] = sm[src + o];
     }
-    // 8. delete set: vu(ngroups) | per client (first-appearance order): client, count, ranges
-    {
-      const uint32_t dsb = hdr + struct_bytes;
-      if (lane == 0) put_vu(out, dsb, ngroups);
-      const uint32_t gbase = dsb + vsz(ngroups);
-      for (uint32_t gg = lane; gg < ngroups; gg += 64) {
-        const uint32_t s = gstart[gg], e = gstart[gg + 1];
-        uint32_t p = gbase + roff[grank[gg]];
-        p = put_vu(out, p, dkey[s] >> 32);
-        p = put_vu(out, p, gcnt[gg]);
-        for (uint32_t q = s; q < e; q++) {
-          if (!dflag[q]) continue;
-          const uint32_t c0 = (uint32_t)(dkey[q] & 0xffffffffull);
-          p = put_vu(out, p, c0);
-          p = put_vu(out, p, dend[q] - c0);
-        }
+    if (lane == 0) put_vu(L_OUT + dsb, ngroups);
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++) {
+      if (lane + 64 * s < ngroups) {
+        uint32_t p = L_OUT + goff[s];
+        p = put_vu(p, gcli[s]);
+        put_vu(p, gcnt[s]);
+      }
+      if (E * lane + s < nranges) {
+        uint32_t p = L_OUT + qoff[s];
+        p = put_vu(p, qclk[s]);
+        put_vu(p, qlen[s]);
       }
     }
     __syncthreads();
-    YM_STOP(8)
-    // 9. 16-B stores into the doc's slot
+    YM_STOP(6)
+    // ---- 7. 16-B stores into the doc's slot
     {
       uint8_t *dst = j.out + slot_al;
       const uint32_t nvec = total >> 4;
-      for (uint32_t v = lane; v < nvec; v += 64) reinterpret_cast<uint4 *>(dst)[v] = reinterpret_cast<const uint4 *>(out)[v];
-      for (uint32_t b = (nvec << 4) + lane; b < total; b += 64) dst[b] = out[b];
+      for (uint32_t v = lane; v < nvec; v += 64) reinterpret_cast<uint4 *>(dst)[v] = at<uint4>(L_OUT + 16 * v);
+      for (uint32_t b = (nvec << 4) + lane; b < total; b += 64) dst[b] = sm[L_OUT + b];
     }
     if (lane == 0) {
       j.out_off[d] = slot_al;
@@ -620,7 +811,7 @@ __global__ void __launch_bounds__(64) k_fast_merge_v1(GeneralJob j) {
   }
 }
 
-using SmallCfg = FastCfg<2560, 128, 128, 128, 2048>;
+}  // namespace fastv1
 
 // the general path's bump allocator starts after the fast path's slot region
 __global__ void k_fast_region(GeneralJob j, uint32_t n_upd) {
@@ -628,21 +819,20 @@ __global__ void k_fast_region(GeneralJob j, uint32_t n_upd) {
 }
 
 int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st) {
+  using namespace fastv1;
   if (op != OP_MERGE || j.v2) return 0;  // fast path: V1 merges (the C2/C4 headline configs)
   k_fast_region<<<1, 64, 0, st>>>(j, n_upd);
   const uint32_t grid = j.n < 131072 ? j.n : 131072;
   static int stop = -1;
   if (stop < 0) { const char *e = getenv("YMERGE_FAST_STOP"); stop = e ? atoi(e) : 0; }
-  const size_t lds = Lay<SmallCfg>::total;
   switch (stop) {
-    case 1: k_fast_merge_v1<SmallCfg, 1><<<grid, 64, lds, st>>>(j); break;
-    case 2: k_fast_merge_v1<SmallCfg, 2><<<grid, 64, lds, st>>>(j); break;
-    case 3: k_fast_merge_v1<SmallCfg, 3><<<grid, 64, lds, st>>>(j); break;
-    case 4: k_fast_merge_v1<SmallCfg, 4><<<grid, 64, lds, st>>>(j); break;
-    case 5: k_fast_merge_v1<SmallCfg, 5><<<grid, 64, lds, st>>>(j); break;
-    case 6: k_fast_merge_v1<SmallCfg, 6><<<grid, 64, lds, st>>>(j); break;
-    case 8: k_fast_merge_v1<SmallCfg, 8><<<grid, 64, lds, st>>>(j); break;
-    default: k_fast_merge_v1<SmallCfg, 0><<<grid, 64, lds, st>>>(j); break;
+    case 1: k_fast_merge_v1<1><<<grid, 64, LDS_BYTES, st>>>(j); break;
+    case 2: k_fast_merge_v1<2><<<grid, 64, LDS_BYTES, st>>>(j); break;
+    case 3: k_fast_merge_v1<3><<<grid, 64, LDS_BYTES, st>>>(j); break;
+    case 4: k_fast_merge_v1<4><<<grid, 64, LDS_BYTES, st>>>(j); break;
+    case 5: k_fast_merge_v1<5><<<grid, 64, LDS_BYTES, st>>>(j); break;
+    case 6: k_fast_merge_v1<6><<<grid, 64, LDS_BYTES, st>>>(j); break;
+    default: k_fast_merge_v1<0><<<grid, 64, LDS_BYTES, st>>>(j); break;
   }
   return 1;
 }
