@@ -11,7 +11,7 @@
 // he@10482).  Anything else is declined (status ST_PENDING) and handled exactly by the general path
 // (ym_general.hip) -- never approximated.
 //
-// Per document, all in LDS (~7.6 KB, no scratch), every phase data-parallel across the wave:
+// Per document, all in LDS (~9.7 KB, no scratch), every phase data-parallel across the wave:
 //   1. 16-B loads of the document's bytes into LDS.
 //   2. one lane per update walks its V1 bytes (branch-free varints from one unaligned 8-byte LDS
 //      read, SWAR ASCII/JSON checks) and appends struct / delete-range records via LDS atomics.
@@ -20,7 +20,7 @@
 //   4. struct layout by DPP wave scans: Skips at clock gaps, part headers, byte offsets.
 //   5. delete set: rank sort of (client, clock), segmented running-max scan = interval union,
 //      groups ranked by first appearance, byte offsets by scans.
-//   6. emit into LDS (aliasing the dead record arrays), 16-B stores into the doc's output slot.
+//   6. emit into LDS staging (struct section right after step 4), 16-B stores into the doc's slot.
 // Output slot of doc d: 2 * (input bytes before d) + 64 * d, 16-aligned (a bound the kernel checks),
 // so the fast path needs no global atomics; the general path appends after that region.
 #include <hip/hip_runtime.h>
@@ -42,7 +42,9 @@ constexpr uint32_t OUT = 2048;   // max output bytes
 constexpr uint32_t L_IN = 0;                    // u8[IN + 16]   document bytes (+ slack for 8-B reads)
 constexpr uint32_t L_UOFF = IN + 16;            // u16[UPD + 1]  update start (absolute LDS offsets)
 constexpr uint32_t L_MISC = L_UOFF + 272;       // u32[16]       counters
-constexpr uint32_t R = L_MISC + 64;             // phase region
+constexpr uint32_t L_HIST = L_MISC + 64;        // u32[16]       update-length histogram -> bucket offsets
+constexpr uint32_t L_UORD = L_HIST + 64;        // u8[UPD]       walk order (updates by length bucket)
+constexpr uint32_t R = L_UORD + UPD;            // phase region
 // phase 2-4: struct records (walk order, then rank order in place)
 constexpr uint32_t L_RKEY = R;                  // u64[REC]  (~client << 32 | clock)
 constexpr uint32_t L_RLEN = L_RKEY + 8 * REC;   // u32[REC]
@@ -70,10 +72,9 @@ constexpr uint32_t L_GBYR = L_QCLK;             // u16[DSN]  bytes by rank, then
 constexpr uint32_t L_GMIN = L_PFIRST;           // u32[DSN]  group first appearance, then group base (parts are dead)
 static_assert(L_P5END <= L_DKEY, "phase-5 arrays must not overlap the sorted delete ranges");
 static_assert(L_GMIN + 4 * DSN <= L_END, "group array fits");
-// phase 6: output staging over R
-constexpr uint32_t L_OUT = R;
-static_assert(L_OUT + OUT <= L_END, "output staging fits the phase region");
-constexpr uint32_t LDS_BYTES = L_END;
+// output staging (struct section written after phase 4, delete set after phase 5)
+constexpr uint32_t L_OUT = L_END;
+constexpr uint32_t LDS_BYTES = L_OUT + OUT;
 
 extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
 template <class T>
@@ -407,12 +408,38 @@ __global__ void __launch_bounds__(64) k_fast_merge_v1(GeneralJob j) {
     }
     for (uint32_t i = lane; i <= k; i += 64) at<uint16_t>(L_UOFF + 2 * i) = (uint16_t)(j.upd_off[u0 + i] - b0 + base);
     if (lane < 2) at<uint32_t>(L_MISC + 4 * lane) = 0;
+    if (lane < 16) at<uint32_t>(L_HIST + 4 * lane) = 0;
     __syncthreads();
     YM_STOP(1)
-    // ---- 2. walk: one lane per update
+    // ---- 2. walk: one lane per update, updates ordered by length bucket so that the lanes of one
+    // round take updates of similar shape (fewer divergent loop trips)
+    {
+      uint32_t ub[UPD / 64], up[UPD / 64];
+#pragma unroll
+      for (uint32_t s = 0; s < UPD / 64; s++) {
+        const uint32_t u = lane + 64 * s;
+        if (u < k) {
+          const uint32_t len = at<uint16_t>(L_UOFF + 2 * u + 2) - at<uint16_t>(L_UOFF + 2 * u);
+          ub[s] = len >> 3 < 15 ? len >> 3 : 15;
+          up[s] = atomicAdd(&at<uint32_t>(L_HIST + 4 * ub[s]), 1u);
+        }
+      }
+      __syncthreads();
+      const uint32_t h = lane < 16 ? at<uint32_t>(L_HIST + 4 * lane) : 0;
+      const uint32_t ex = wave_incl_add(h) - h;
+      __syncthreads();
+      if (lane < 16) at<uint32_t>(L_HIST + 4 * lane) = ex;
+      __syncthreads();
+#pragma unroll
+      for (uint32_t s = 0; s < UPD / 64; s++) {
+        const uint32_t u = lane + 64 * s;
+        if (u < k) at<uint8_t>(L_UORD + at<uint32_t>(L_HIST + 4 * ub[s]) + up[s]) = (uint8_t)u;
+      }
+      __syncthreads();
+    }
     bool ok = true;
 #pragma unroll 1
-    for (uint32_t u = lane; u < k; u += 64) ok &= walk_update(u);
+    for (uint32_t i = lane; i < k; i += 64) ok &= walk_update(at<uint8_t>(L_UORD + i));
     if (__any(!ok)) YM_DECLINE()
     __syncthreads();
     const uint32_t nrec = at<uint32_t>(L_MISC), nds = at<uint32_t>(L_MISC + 4);
@@ -534,7 +561,31 @@ __global__ void __launch_bounds__(64) k_fast_merge_v1(GeneralJob j) {
       for (uint32_t s = 0; s < E; s++) { const uint32_t b = soff[s]; soff[s] = run; run += b; }
     }
     const uint32_t hdr = vsz(nparts);
+    if (hdr + struct_bytes > OUT) YM_DECLINE()
     YM_STOP(4)
+    // ---- 4b. emit the struct section (frees the records' registers before the delete set)
+    if (lane == 0) put_vu(L_OUT, nparts);
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++) {
+      if (E * lane + s >= nrec) break;
+      uint32_t p = L_OUT + hdr + soff[s];
+      if (pstart[s]) {  // part header: vu(#structs incl. skips) vu(client) vu(clock)
+        p = put_vu(p, runu[s]);
+        p = put_vu(p, ~(uint32_t)(sk[s] >> 32));
+        p = put_vu(p, sk[s] & 0xffffffffull);
+      }
+      if (gapv[s]) {  // Skip: info 10 + varuint length (13.5.16 ui.write)
+        sm[p++] = 10;
+        p = put_vu(p, gapv[s]);
+      }
+      uint32_t info = sinf[s];
+      if (info & 0xC0) info &= ~0x20u;  // parentSub is only read / re-written without origins (E8)
+      sm[p++] = (uint8_t)info;
+      const uint32_t n = sbl[s] - 1, src = ssrc[s] + 1;
+      uint32_t o = 0;
+      for (; o + 4 <= n; o += 4) st4(p + o, ld4(src + o));
+      for (; o < n; o++) sm[p + o] = sm[src + o];
+    }
     // ---- 5. delete set
     uint64_t dk[E];
     uint32_t dl[E], dq[E], dr[E];
@@ -755,30 +806,7 @@ __global__ void __launch_bounds__(64) k_fast_merge_v1(GeneralJob j) {
       continue;
     }
     YM_STOP(5)
-    __syncthreads();  // every record / range array is dead: L_OUT aliases them
-    // ---- 6. emit
-    if (lane == 0) put_vu(L_OUT, nparts);
-#pragma unroll
-    for (uint32_t s = 0; s < E; s++) {
-      if (E * lane + s >= nrec) break;
-      uint32_t p = L_OUT + hdr + soff[s];
-      if (pstart[s]) {  // part header: vu(#structs incl. skips) vu(client) vu(clock)
-        p = put_vu(p, runu[s]);
-        p = put_vu(p, ~(uint32_t)(sk[s] >> 32));
-        p = put_vu(p, sk[s] & 0xffffffffull);
-      }
-      if (gapv[s]) {  // Skip: info 10 + varuint length (13.5.16 ui.write)
-        sm[p++] = 10;
-        p = put_vu(p, gapv[s]);
-      }
-      uint32_t info = sinf[s];
-      if (info & 0xC0) info &= ~0x20u;  // parentSub is only read / re-written without origins (E8)
-      sm[p++] = (uint8_t)info;
-      const uint32_t n = sbl[s] - 1, src = ssrc[s] + 1;
-      uint32_t o = 0;
-      for (; o + 4 <= n; o += 4) st4(p + o, ld4(src + o));
-      for (; o < n; o++) sm[p + o] = sm[src + o];
-    }
+    // ---- 6. emit the delete set
     if (lane == 0) put_vu(L_OUT + dsb, ngroups);
 #pragma unroll
     for (uint32_t s = 0; s < E; s++) {
