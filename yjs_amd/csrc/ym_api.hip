@@ -212,9 +212,8 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
       S->list_b.ensure((nd + 1) * 4ull))
     return -2;
   uint64_t *counters = S->counters.as<uint64_t>();
-  HIPCHK(hipMemsetAsync(counters, 0, 256, st));
-  HIPCHK(hipEventRecord(S->ev0, st));
-
+  // counters: [0] used (bump allocator), [1] retry count, [2] fast-path declined count (u32),
+  //           [4..6] stats (errors, bytes out, bytes in)
   GeneralJob j;
   memset(&j, 0, sizeof(j));
   j.A = A;
@@ -232,50 +231,65 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   j.out_len = o_len;
   j.used = counters + 0;
   j.counter_retry = (uint32_t *)(counters + 1);
+  j.pend_count = (uint32_t *)(counters + 2);
+  j.pend_list = S->list_a.as<uint32_t>();
   j.n = nd;
 
-  // (1) fast path over every document; leaves status ST_PENDING where it declines
+  auto stats_launch = [&]() {
+    k_stats<<<(nd + 255) / 256, 256, 0, st>>>(o_status, o_len, nd, counters + 4);
+    k_in_bytes<<<1, 1, 0, st>>>(upd_off, b->n_upd, counters + 4);
+  };
+  HIPCHK(hipEventRecord(S->ev0, st));
+  // (1) fast path over every document; appends the ones it declines to list_a
   HIPCHK(hipEventRecord(S->evf0, st));
   int fr = fast_launch(op, j, b->n_upd, st);
   if (fr < 0) return fr;
   HIPCHK(hipEventRecord(S->evf1, st));
   uint32_t ngen = nd;
   uint32_t *list = nullptr;
-  if (fr == 1) {  // the fast path ran: select the declined docs
-    if (select_docs(S, st, nullptr, nd, o_status, ST_PENDING, S->list_a.as<uint32_t>(), &ngen)) return -1;
+  if (fr == 1) {
+    // one round trip: used, the declined count and (speculatively) the stats of the fast-only case
+    if (stats) {
+      HIPCHK(hipMemsetAsync(counters + 4, 0, 24, st));
+      stats_launch();
+    }
+    HIPCHK(hipEventRecord(S->ev1, st));
+    HIPCHK(hipMemcpyAsync(S->pinned, counters, stats ? 56 : 24, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    ngen = (uint32_t)(S->pinned[2] & 0xffffffffu);
     list = S->list_a.as<uint32_t>();
+  } else {
+    HIPCHK(hipMemsetAsync(counters, 0, 256, st));
   }
   // (2) general path over the rest
   if (ngen > 0) {
     int r = run_general(S, st, j, list, ngen);
     if (r) return r;
+    HIPCHK(hipEventRecord(S->evg1, st));
+    if (stats) {
+      HIPCHK(hipMemsetAsync(counters + 4, 0, 24, st));
+      stats_launch();
+    }
+    HIPCHK(hipEventRecord(S->ev1, st));
+    HIPCHK(hipMemcpyAsync(S->pinned, counters, stats ? 56 : 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
   }
-  HIPCHK(hipEventRecord(S->evg1, st));
-  HIPCHK(hipEventRecord(S->ev1, st));
-  // (3) bookkeeping
-  if (stats) {
-    k_stats<<<(nd + 255) / 256, 256, 0, st>>>(o_status, o_len, nd, counters + 4);
-    k_in_bytes<<<1, 1, 0, st>>>(upd_off, b->n_upd, counters + 4);
-    HIPCHK(hipMemcpyAsync(S->pinned + 8, counters + 4, 24, hipMemcpyDeviceToHost, st));
-  }
-  HIPCHK(hipMemcpyAsync(S->pinned, counters, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
   uint64_t used = S->pinned[0];
   out->used = used;
   if (stats) {
     float ms = 0, fms = 0, gms = 0;
     hipEventElapsedTime(&ms, S->ev0, S->ev1);
     hipEventElapsedTime(&fms, S->evf0, S->evf1);
-    hipEventElapsedTime(&gms, S->evf1, S->evg1);
+    if (ngen > 0) hipEventElapsedTime(&gms, S->evf1, S->evg1);
     stats->device_ms = ms;
     stats->fast_ms = fr == 1 ? fms : 0.0;
     stats->general_ms = ngen > 0 ? gms : 0.0;
     stats->docs = nd;
     stats->docs_general = ngen;
     stats->docs_fast = nd - ngen;
-    stats->docs_error = S->pinned[8];
-    stats->bytes_out = S->pinned[9];
-    stats->bytes_in = S->pinned[10];
+    stats->docs_error = S->pinned[4];
+    stats->bytes_out = S->pinned[5];
+    stats->bytes_in = S->pinned[6];
   }
   if (used > out->cap) return YM_ERR_CAPACITY;
   if (host) {

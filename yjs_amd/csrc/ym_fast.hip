@@ -373,9 +373,14 @@ __device__ __forceinline__ void rank_exact(uint32_t keys, uint32_t n, const uint
   }
 }
 
+// a declined document is appended to the general path's work list
+__device__ __forceinline__ void decline(const GeneralJob &j, uint32_t d) {
+  j.status[d] = ST_PENDING;
+  j.pend_list[atomicAdd(j.pend_count, 1u)] = d;
+}
 #define YM_DECLINE()                                 \
   {                                                  \
-    if (lane == 0) j.status[d] = ST_PENDING;         \
+    if (lane == 0) decline(j, d);                    \
     __syncthreads();                                 \
     continue;                                        \
   }
@@ -396,7 +401,7 @@ __global__ void __launch_bounds__(64) k_fast_merge_v1(GeneralJob j) {
     const uint32_t u0 = j.doc_upd[d], k = j.doc_upd[d + 1] - u0;
     const uint64_t b0 = j.upd_off[u0], bytes = j.upd_off[u0 + k] - b0;
     if (k <= 1 || k > UPD || bytes > IN) {
-      if (lane == 0) j.status[d] = ST_PENDING;
+      if (lane == 0) decline(j, d);
       continue;
     }
     // ---- 1. stage with 16-B loads covering [b0, b0 + bytes); byte b0 lands at LDS offset `base`
@@ -841,9 +846,12 @@ __global__ void __launch_bounds__(64) k_fast_merge_v1(GeneralJob j) {
 
 }  // namespace fastv1
 
-// the general path's bump allocator starts after the fast path's slot region
+// the general path's bump allocator starts after the fast path's slot region; empty work list
 __global__ void k_fast_region(GeneralJob j, uint32_t n_upd) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) *j.used = 2 * (j.upd_off[n_upd] - j.upd_off[0]) + 64ull * j.n + 64;
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    *j.used = 2 * (j.upd_off[n_upd] - j.upd_off[0]) + 64ull * j.n + 64;
+    *j.pend_count = 0;
+  }
 }
 
 int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st) {

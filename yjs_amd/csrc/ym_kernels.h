@@ -30,6 +30,8 @@ struct GeneralJob {
   uint64_t *out_off, *out_len;  // per doc
   uint64_t *used;            // bump allocator over `out`
   uint32_t *counter_retry;
+  uint32_t *pend_list;       // fast path: ids of the documents it declines (appended) ...
+  uint32_t *pend_count;      // ... and their number
 };
 
 struct GeneralWsSize {
