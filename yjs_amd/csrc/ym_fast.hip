@@ -11,7 +11,7 @@
 // he@10482).  Anything else is declined (status ST_PENDING) and handled exactly by the general path
 // (ym_general.hip) -- never approximated.
 //
-// Per document, all in LDS (~9.7 KB, no scratch), every phase data-parallel across the wave:
+// Per document, all in LDS (~7.8 KB, no scratch), every phase data-parallel across the wave:
 //   1. 16-B loads of the document's bytes into LDS.
 //   2. one lane per update walks its V1 bytes (branch-free varints from one unaligned 8-byte LDS
 //      read, SWAR ASCII/JSON checks) and appends struct / delete-range records via LDS atomics.
@@ -20,7 +20,7 @@
 //   4. struct layout by DPP wave scans: Skips at clock gaps, part headers, byte offsets.
 //   5. delete set: rank sort of (client, clock), segmented running-max scan = interval union,
 //      groups ranked by first appearance, byte offsets by scans.
-//   6. emit into LDS staging (struct section right after step 4), 16-B stores into the doc's slot.
+//   6. struct section written right after step 4, delete set after step 5, straight into the slot.
 // Output slot of doc d: 2 * (input bytes before d) + 64 * d, 16-aligned (a bound the kernel checks),
 // so the fast path needs no global atomics; the general path appends after that region.
 #include <hip/hip_runtime.h>
@@ -36,15 +36,16 @@ constexpr uint32_t UPD = 128;    // max updates per document
 constexpr uint32_t E = 2;        // records per lane
 constexpr uint32_t REC = 64 * E; // max structs per document
 constexpr uint32_t DSN = 64 * E; // max delete ranges per document (before the union)
-constexpr uint32_t OUT = 2048;   // max output bytes
 
 // ---- LDS map (byte offsets; every array 16-aligned) ----------------------------------------------
 constexpr uint32_t L_IN = 0;                    // u8[IN + 16]   document bytes (+ slack for 8-B reads)
 constexpr uint32_t L_UOFF = IN + 16;            // u16[UPD + 1]  update start (absolute LDS offsets)
 constexpr uint32_t L_MISC = L_UOFF + 272;       // u32[16]       counters
 constexpr uint32_t L_HIST = L_MISC + 64;        // u32[16]       update-length histogram -> bucket offsets
-constexpr uint32_t L_UORD = L_HIST + 64;        // u8[UPD]       walk order (updates by length bucket)
-constexpr uint32_t R = L_UORD + UPD;            // phase region
+constexpr uint32_t L_UORD = L_HIST + 64;        // u8[UPD]       struct walk list (updates with structs, by length)
+constexpr uint32_t L_UORD2 = L_UORD + UPD;      // u8[UPD]       delete-set walk list (updates with deletes)
+constexpr uint32_t L_UDS = L_UORD2 + UPD;       // u16[UPD]      LDS offset of each update's delete set
+constexpr uint32_t R = L_UDS + 2 * UPD;         // phase region
 // phase 2-4: struct records (walk order, then rank order in place)
 constexpr uint32_t L_RKEY = R;                  // u64[REC]  (~client << 32 | clock)
 constexpr uint32_t L_RLEN = L_RKEY + 8 * REC;   // u32[REC]
@@ -68,13 +69,12 @@ constexpr uint32_t L_QPRE = L_QGRP + DSN;       // u16[DSN + 1] exclusive byte p
 constexpr uint32_t L_GFIRST = L_QPRE + 272;     // u16[DSN + 1] group -> first range
 constexpr uint32_t L_GCLI = L_GFIRST + 272;     // u32[DSN]  group client
 constexpr uint32_t L_P5END = L_GCLI + 4 * DSN;
-constexpr uint32_t L_GBYR = L_QCLK;             // u16[DSN]  bytes by rank, then offsets by rank (QCLK is dead by then)
+constexpr uint32_t L_GBYR = L_DKEY;             // u16[DSN]  bytes by rank, then offsets by rank (sorted keys are dead)
+constexpr uint32_t L_GB2 = L_DKEY + 512;        // u32[DSN]  group -> base offset of its ranges
 constexpr uint32_t L_GMIN = L_PFIRST;           // u32[DSN]  group first appearance, then group base (parts are dead)
 static_assert(L_P5END <= L_DKEY, "phase-5 arrays must not overlap the sorted delete ranges");
 static_assert(L_GMIN + 4 * DSN <= L_END, "group array fits");
-// output staging (struct section written after phase 4, delete set after phase 5)
-constexpr uint32_t L_OUT = L_END;
-constexpr uint32_t LDS_BYTES = L_OUT + OUT;
+constexpr uint32_t LDS_BYTES = L_END;
 
 extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
 template <class T>
@@ -124,9 +124,22 @@ __device__ __forceinline__ uint32_t vsz(uint64_t v) {
   return 1 + (v >= (1ull << 7)) + (v >= (1ull << 14)) + (v >= (1ull << 21)) + (v >= (1ull << 28)) +
          (v >= (1ull << 35)) + (v >= (1ull << 42)) + (v >= (1ull << 49));
 }
-__device__ __forceinline__ uint32_t put_vu(uint32_t p, uint64_t v) {
-  while (v > 127) { sm[p++] = (uint8_t)(0x80 | (v & 127)); v >>= 7; }
-  sm[p++] = (uint8_t)v;
+// The document's output slot as a buffer resource: 32-bit offsets (no 64-bit address math per
+// store) and a hardware bound (stores past the slot are dropped).
+typedef __amdgpu_buffer_rsrc_t Slot;
+__device__ __forceinline__ Slot make_slot(uint8_t *base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void ob8(Slot o, uint32_t p, uint32_t v) {
+  __builtin_amdgcn_raw_buffer_store_b8((int8_t)v, o, (int)p, 0, 0);
+}
+__device__ __forceinline__ void ob32(Slot o, uint32_t p, uint32_t v) {
+  __builtin_amdgcn_raw_buffer_store_b32((int)v, o, (int)p, 0, 0);
+}
+// lib0 writeVarUint straight into the output slot
+__device__ __forceinline__ uint32_t put_vu(Slot o, uint32_t p, uint64_t v) {
+  while (v > 127) { ob8(o, p++, 0x80 | (uint32_t)(v & 127)); v >>= 7; }
+  ob8(o, p++, (uint32_t)v);
   return p;
 }
 
@@ -137,18 +150,38 @@ struct Cur {
   uint32_t p, e;
   bool bad;
 };
+// Length of the lib0 varuint at the start of an 8-byte window (1..5; 6 = no terminator within 5 bytes).
+// Branch-free: v_ffbl on the stop bits with a sentinel.
+__device__ __forceinline__ uint32_t vu_nb(uint32_t lo, uint32_t hi) {
+  const uint32_t s_lo = ~lo & 0x80808080u;
+  const uint32_t s_hi = (~hi & 0x80u) | 0x8000u;
+  const uint32_t t = __builtin_ctzg(s_lo, 32 + __builtin_ctz(s_hi));
+  return (t >> 3) + 1;
+}
+// validity of a varuint of nb bytes: terminated within 5 bytes, inside the update, canonical (no
+// zero final group), and < 2^32 (lib0 readVarUint is u32)
+__device__ __forceinline__ bool vu_bad(uint32_t lo, uint32_t hi, uint32_t nb, uint32_t p, uint32_t e) {
+  const uint32_t last = nb <= 4 ? (lo >> (8 * nb - 8)) & 0xffu : hi & 0xffu;
+  return (nb > 5) | (p + nb > e) | ((nb > 1) & (last == 0)) | ((nb == 5) & ((hi & 0x70u) != 0));
+}
 // lib0 readVarUint (u32, canonical encodings only) from one unaligned 8-byte window
 __device__ __forceinline__ uint32_t rvu(Cur &c) {
   const uint64_t x = ld8(c.p);
   const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-  const uint32_t stop = ~lo & 0x80808080u;
-  const uint32_t nb = stop ? (__builtin_ctz(stop) >> 3) + 1 : ((hi & 0x80u) ? 0u : 5u);
-  uint32_t v = (lo & 0x7fu) | ((lo >> 1) & 0x3f80u) | ((lo >> 2) & 0x1fc000u) | ((lo >> 3) & 0xfe00000u) | (hi << 28);
-  if (nb < 5) v &= (1u << (7 * nb)) - 1u;
-  const bool noncanon = nb > 1 && v < (1u << (7 * nb - 7));
-  c.bad |= nb == 0 || c.p + nb > c.e || noncanon || (nb == 5 && (hi & 0x70u));
-  c.p += nb;
-  return v;
+  const uint32_t nb = vu_nb(lo, hi);
+  const uint32_t v = (lo & 0x7fu) | ((lo >> 1) & 0x3f80u) | ((lo >> 2) & 0x1fc000u) | ((lo >> 3) & 0xfe00000u) | (hi << 28);
+  const uint32_t m = (uint32_t)((1ull << (7 * (nb < 5 ? nb : 5))) - 1);
+  c.bad |= vu_bad(lo, hi, nb, c.p, c.e);
+  c.p += nb < 6 ? nb : 0;
+  return v & m;
+}
+// skips a varuint whose value is not needed (origins, parent ids), with the same validity checks
+__device__ __forceinline__ void skvu(Cur &c) {
+  const uint64_t x = ld8(c.p);
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const uint32_t nb = vu_nb(lo, hi);
+  c.bad |= vu_bad(lo, hi, nb, c.p, c.e);
+  c.p += nb < 6 ? nb : 0;
 }
 __device__ __forceinline__ uint32_t rdb(Cur &c) {
   c.bad |= c.p >= c.e;
@@ -265,10 +298,9 @@ __device__ __forceinline__ void any_scalar(Cur &c) {
   }
 }
 
-// Walks update u and appends its structs and delete ranges to the record arrays (slots from LDS
-// atomic counters misc[0] / misc[1]).  A delete range's payload (u << 8 | position) keeps yjs's
-// first-appearance order.  Returns false to decline the document.
-__device__ __forceinline__ bool walk_update(uint32_t u) {
+// Walks the struct section of update u and appends its structs to the record arrays (slots from an
+// LDS atomic counter, misc[0]); records where its delete set starts.  Returns false to decline.
+__device__ __forceinline__ bool walk_structs(uint32_t u) {
   Cur c = {at<uint16_t>(L_UOFF + 2 * u), at<uint16_t>(L_UOFF + 2 * u + 2), false};
   const uint32_t nclients = rvu(c);
   uint64_t prev = 0;
@@ -281,13 +313,13 @@ __device__ __forceinline__ bool walk_update(uint32_t u) {
       const uint32_t s0 = c.p;
       const uint32_t info = rdb(c);
       if (info == 10 || (info & 31) == 0) return false;  // Skip / GC -> general path
-      if (info & 0x80) { rvu(c); rvu(c); }
-      if (info & 0x40) { rvu(c); rvu(c); }
+      if (info & 0x80) { skvu(c); skvu(c); }
+      if (info & 0x40) { skvu(c); skvu(c); }
       if ((info & 0xC0) == 0) {
         const uint32_t pi = rvu(c);
         if (pi > 1) return false;  // parentInfo re-encodes as 0/1
         if (pi == 1) rstr(c);
-        else { rvu(c); rvu(c); }
+        else { skvu(c); skvu(c); }
         if (info & 0x20) rstr(c);
       }
       uint32_t len = 1;
@@ -325,8 +357,14 @@ __device__ __forceinline__ bool walk_update(uint32_t u) {
       clock += len;
     }
   }
-  if (c.bad) return false;
-  const uint32_t ndc = rvu(c);  // delete set (DeleteSet.js:219-256)
+  at<uint16_t>(L_UDS + 2 * u) = (uint16_t)c.p;
+  return !c.bad;
+}
+// Walks the delete set of update u (DeleteSet.js:219-256) and appends its ranges (slots from misc[1]);
+// a range's payload (u << 8 | position) keeps yjs's first-appearance order.
+__device__ __forceinline__ bool walk_ds(uint32_t u) {
+  Cur c = {at<uint16_t>(L_UDS + 2 * u), at<uint16_t>(L_UOFF + 2 * u + 2), false};
+  const uint32_t ndc = rvu(c);
   uint32_t pos = 0;
   for (uint32_t i = 0; i < ndc && !c.bad; i++) {
     const uint32_t client = rvu(c);
@@ -393,8 +431,8 @@ __device__ __forceinline__ void decline(const GeneralJob &j, uint32_t d) {
     continue;                                                           \
   }
 
-template <int STOP>
-__global__ void __launch_bounds__(64) k_fast_merge_v1(GeneralJob j) {
+template <int STOP, int OCC>
+__global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
   const uint32_t lane = threadIdx.x;
   const uint64_t arena0 = j.upd_off[0];
   for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
@@ -416,36 +454,63 @@ __global__ void __launch_bounds__(64) k_fast_merge_v1(GeneralJob j) {
     if (lane < 16) at<uint32_t>(L_HIST + 4 * lane) = 0;
     __syncthreads();
     YM_STOP(1)
-    // ---- 2. walk: one lane per update, updates ordered by length bucket so that the lanes of one
-    // round take updates of similar shape (fewer divergent loop trips)
+    // ---- 2. walk.  W1: one lane per update that has structs, updates ordered by length bucket so
+    // that the lanes of one round take updates of similar shape; W2: one lane per update whose delete
+    // set is not empty.  Splitting the two keeps every lane of a round busy with the same kind of work.
     {
       uint32_t ub[UPD / 64], up[UPD / 64];
+      bool empty = false;
 #pragma unroll
       for (uint32_t s = 0; s < UPD / 64; s++) {
         const uint32_t u = lane + 64 * s;
+        ub[s] = 16;
         if (u < k) {
-          const uint32_t len = at<uint16_t>(L_UOFF + 2 * u + 2) - at<uint16_t>(L_UOFF + 2 * u);
-          ub[s] = len >> 3 < 15 ? len >> 3 : 15;
-          up[s] = atomicAdd(&at<uint32_t>(L_HIST + 4 * ub[s]), 1u);
+          const uint32_t u0_ = at<uint16_t>(L_UOFF + 2 * u), len = at<uint16_t>(L_UOFF + 2 * u + 2) - u0_;
+          empty |= len == 0;
+          if (len > 0 && sm[u0_] == 0) {
+            at<uint16_t>(L_UDS + 2 * u) = (uint16_t)(u0_ + 1);  // no structs: the delete set follows
+          } else {
+            ub[s] = len >> 3 < 15 ? len >> 3 : 15;
+            up[s] = atomicAdd(&at<uint32_t>(L_HIST + 4 * ub[s]), 1u);
+          }
         }
       }
+      if (__any(empty)) YM_DECLINE()
       __syncthreads();
       const uint32_t h = lane < 16 ? at<uint32_t>(L_HIST + 4 * lane) : 0;
-      const uint32_t ex = wave_incl_add(h) - h;
+      const uint32_t hincl = wave_incl_add(h);
+      const uint32_t n1 = lane_read(hincl, 15);
       __syncthreads();
-      if (lane < 16) at<uint32_t>(L_HIST + 4 * lane) = ex;
+      if (lane < 16) at<uint32_t>(L_HIST + 4 * lane) = hincl - h;
       __syncthreads();
+#pragma unroll
+      for (uint32_t s = 0; s < UPD / 64; s++)
+        if (ub[s] < 16) at<uint8_t>(L_UORD + at<uint32_t>(L_HIST + 4 * ub[s]) + up[s]) = (uint8_t)(lane + 64 * s);
+      __syncthreads();
+      bool ok = true;
+#pragma unroll 1
+      for (uint32_t i = lane; i < n1; i += 64) ok &= walk_structs(at<uint8_t>(L_UORD + i));
+      if (__any(!ok)) YM_DECLINE()
+      __syncthreads();
+      // W2 list: updates whose delete set has clients (first byte != 0), compacted by ballots
+      uint32_t n2 = 0;
 #pragma unroll
       for (uint32_t s = 0; s < UPD / 64; s++) {
         const uint32_t u = lane + 64 * s;
-        if (u < k) at<uint8_t>(L_UORD + at<uint32_t>(L_HIST + 4 * ub[s]) + up[s]) = (uint8_t)u;
+        bool has = false;
+        if (u < k) {
+          const uint32_t p = at<uint16_t>(L_UDS + 2 * u);
+          has = p >= at<uint16_t>(L_UOFF + 2 * u + 2) || sm[p] != 0;  // (a missing delete set: W2 declines)
+        }
+        const uint64_t m = __ballot(has);
+        if (has) at<uint8_t>(L_UORD2 + n2 + __popcll(m & ((1ull << lane) - 1))) = (uint8_t)u;
+        n2 += __popcll(m);
       }
       __syncthreads();
-    }
-    bool ok = true;
 #pragma unroll 1
-    for (uint32_t i = lane; i < k; i += 64) ok &= walk_update(at<uint8_t>(L_UORD + i));
-    if (__any(!ok)) YM_DECLINE()
+      for (uint32_t i = lane; i < n2; i += 64) ok &= walk_ds(at<uint8_t>(L_UORD2 + i));
+      if (__any(!ok)) YM_DECLINE()
+    }
     __syncthreads();
     const uint32_t nrec = at<uint32_t>(L_MISC), nds = at<uint32_t>(L_MISC + 4);
     if (nrec == 0 || nrec > REC || nds > DSN) YM_DECLINE()
@@ -566,51 +631,61 @@ __global__ void __launch_bounds__(64) k_fast_merge_v1(GeneralJob j) {
       for (uint32_t s = 0; s < E; s++) { const uint32_t b = soff[s]; soff[s] = run; run += b; }
     }
     const uint32_t hdr = vsz(nparts);
-    if (hdr + struct_bytes > OUT) YM_DECLINE()
+    // output slot: 16-aligned inside the bound 2 * in + 64 per doc (no global atomics)
+    const uint64_t slot = 2 * (b0 - arena0) + 64ull * d;
+    const uint64_t slot_al = (slot + 15) & ~15ull;
+    const uint64_t slot_end = slot + 2 * bytes + 64 < j.cap ? slot + 2 * bytes + 64 : j.cap;
+    if (slot_al + hdr + struct_bytes > slot_end) {
+      if (slot_al + hdr + struct_bytes > slot + 2 * bytes + 64) YM_DECLINE()
+      if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }  // caller's arena too small
+      __syncthreads();
+      continue;
+    }
     YM_STOP(4)
-    // ---- 4b. emit the struct section (frees the records' registers before the delete set)
-    if (lane == 0) put_vu(L_OUT, nparts);
+    // ---- 4b. write the struct section (frees the records' registers before the delete set)
+    const Slot dst = make_slot(j.out + slot_al, (uint32_t)(slot_end - slot_al));
+    if (lane == 0) put_vu(dst, 0, nparts);
 #pragma unroll
     for (uint32_t s = 0; s < E; s++) {
       if (E * lane + s >= nrec) break;
-      uint32_t p = L_OUT + hdr + soff[s];
+      uint32_t p = hdr + soff[s];
       if (pstart[s]) {  // part header: vu(#structs incl. skips) vu(client) vu(clock)
-        p = put_vu(p, runu[s]);
-        p = put_vu(p, ~(uint32_t)(sk[s] >> 32));
-        p = put_vu(p, sk[s] & 0xffffffffull);
+        p = put_vu(dst, p, runu[s]);
+        p = put_vu(dst, p, ~(uint32_t)(sk[s] >> 32));
+        p = put_vu(dst, p, sk[s] & 0xffffffffull);
       }
       if (gapv[s]) {  // Skip: info 10 + varuint length (13.5.16 ui.write)
-        sm[p++] = 10;
-        p = put_vu(p, gapv[s]);
+        ob8(dst, p++, 10);
+        p = put_vu(dst, p, gapv[s]);
       }
       uint32_t info = sinf[s];
       if (info & 0xC0) info &= ~0x20u;  // parentSub is only read / re-written without origins (E8)
-      sm[p++] = (uint8_t)info;
-      const uint32_t n = sbl[s] - 1, src = ssrc[s] + 1;
+      ob8(dst, p++, info);
+      const uint32_t n = sbl[s] - 1, src = ssrc[s] + 1;  // body bytes, copied verbatim
       uint32_t o = 0;
-      for (; o + 4 <= n; o += 4) st4(p + o, ld4(src + o));
-      for (; o < n; o++) sm[p + o] = sm[src + o];
+      for (; o + 4 <= n; o += 4) ob32(dst, p + o, ld4(src + o));
+      for (; o < n; o++) ob8(dst, p + o, sm[src + o]);
     }
     // ---- 5. delete set
-    uint64_t dk[E];
-    uint32_t dl[E], dq[E], dr[E];
-#pragma unroll
-    for (uint32_t s = 0; s < E; s++) {
-      const uint32_t i = lane + 64 * s;
-      const bool v = i < nds;
-      dk[s] = v ? at<uint64_t>(L_DKEY + 8 * i) : ~0ull;
-      dl[s] = v ? at<uint32_t>(L_DLEN + 4 * i) : 0;
-      dq[s] = v ? at<uint16_t>(L_DSEQ + 2 * i) : 0;
-    }
-    rank_le(L_DKEY, nds, dk, dr);
-    __syncthreads();
-#pragma unroll
-    for (uint32_t s = 0; s < E; s++) {
-      const uint32_t i = lane + 64 * s;
-      if (i < nds) at<uint8_t>(L_DSLOT + dr[s]) = (uint8_t)i;
-    }
-    __syncthreads();
     {
+      uint64_t dk[E];
+      uint32_t dl[E], dq[E], dr[E];
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint32_t i = lane + 64 * s;
+        const bool v = i < nds;
+        dk[s] = v ? at<uint64_t>(L_DKEY + 8 * i) : ~0ull;
+        dl[s] = v ? at<uint32_t>(L_DLEN + 4 * i) : 0;
+        dq[s] = v ? at<uint16_t>(L_DSEQ + 2 * i) : 0;
+      }
+      rank_le(L_DKEY, nds, dk, dr);
+      __syncthreads();
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint32_t i = lane + 64 * s;
+        if (i < nds) at<uint8_t>(L_DSLOT + dr[s]) = (uint8_t)i;
+      }
+      __syncthreads();
       bool dup = false;
 #pragma unroll
       for (uint32_t s = 0; s < E; s++) {
@@ -618,157 +693,145 @@ __global__ void __launch_bounds__(64) k_fast_merge_v1(GeneralJob j) {
         if (i < nds) dup |= at<uint8_t>(L_DSLOT + dr[s]) != i;
       }
       if (__any(dup)) rank_exact(L_DKEY, nds, dk, dr);  // equal (client, clock) in several inputs
-    }
-    __syncthreads();
+      __syncthreads();
 #pragma unroll
-    for (uint32_t s = 0; s < E; s++) {
-      if (lane + 64 * s < nds) {
-        const uint32_t r = dr[s];
-        at<uint64_t>(L_DKEY + 8 * r) = dk[s];
-        at<uint32_t>(L_DLEN + 4 * r) = dl[s];
-        at<uint16_t>(L_DSEQ + 2 * r) = (uint16_t)dq[s];
+      for (uint32_t s = 0; s < E; s++) {
+        if (lane + 64 * s < nds) {
+          const uint32_t r = dr[s];
+          at<uint64_t>(L_DKEY + 8 * r) = dk[s];
+          at<uint32_t>(L_DLEN + 4 * r) = dl[s];
+          at<uint16_t>(L_DSEQ + 2 * r) = (uint16_t)dq[s];
+        }
       }
+      __syncthreads();
     }
-    if (lane == 0) at<uint32_t>(L_MISC + 8) = 0;
-    __syncthreads();
-    // sorted positions r = E*lane + s: segments (clients), running max end, merged ranges
-    uint64_t ek[E], eend[E];
-    uint32_t eseq[E], segst[E], newr[E];
-    uint32_t seg_lane = 0;
+    // sorted positions r = E*lane + s: client segments (= groups), running max end of the union,
+    // merged ranges.  Per position only its key, end, segment flag and id stay in registers.
+    uint32_t ngroups, nranges;
     {
+      uint32_t ecl[E], ecli[E], segst[E], segid[E], eseq[E];
+      uint64_t eend[E];
+      uint32_t seg_lane = 0;
       const uint32_t r0 = E * lane;
-      uint64_t kp = r0 > 0 && r0 - 1 < nds ? at<uint64_t>(L_DKEY + 8 * (r0 - 1)) : ~0ull;
+      uint32_t cprev = r0 > 0 && r0 - 1 < nds ? (uint32_t)(at<uint64_t>(L_DKEY + 8 * (r0 - 1)) >> 32) : 0;
 #pragma unroll
       for (uint32_t s = 0; s < E; s++) {
         const uint32_t r = r0 + s;
         const bool v = r < nds;
-        ek[s] = v ? at<uint64_t>(L_DKEY + 8 * r) : 0;
-        eend[s] = v ? (ek[s] & 0xffffffffull) + at<uint32_t>(L_DLEN + 4 * r) : 0;
+        const uint64_t k = v ? at<uint64_t>(L_DKEY + 8 * r) : 0;
+        ecl[s] = (uint32_t)k;
+        ecli[s] = (uint32_t)(k >> 32);
+        eend[s] = v ? (uint64_t)ecl[s] + at<uint32_t>(L_DLEN + 4 * r) : 0;
         eseq[s] = v ? at<uint16_t>(L_DSEQ + 2 * r) : 0xffff;
-        segst[s] = v && (r == 0 || (kp >> 32) != (ek[s] >> 32));
+        segst[s] = v && (r == 0 || cprev != ecli[s]);
         seg_lane += segst[s];
-        kp = ek[s];
+        cprev = ecli[s];
       }
-    }
-    uint32_t segid[E], ngroups;
-    {
-      const uint32_t incl = wave_incl_add(seg_lane);
-      ngroups = lane_read(incl, 63);
-      uint32_t run = incl - seg_lane;
+      {
+        const uint32_t incl = wave_incl_add(seg_lane);
+        ngroups = lane_read(incl, 63);
+        uint32_t run = incl - seg_lane;
 #pragma unroll
-      for (uint32_t s = 0; s < E; s++) { run += segst[s]; segid[s] = run - 1; }
-    }
-    // running max of (segment << 33 | end): within a segment it is the max end so far
-    uint64_t rmax[E];
-    {
-      uint64_t m = 0;
+        for (uint32_t s = 0; s < E; s++) { run += segst[s]; segid[s] = run - 1; }
+      }
+      // running max of (segment << 33 | end): within a segment it is the max end so far
+      uint64_t m = 0, rmax[E];
 #pragma unroll
       for (uint32_t s = 0; s < E; s++) {
-        const uint64_t x = E * lane + s < nds ? ((uint64_t)segid[s] << 33) | eend[s] : 0;
+        const uint64_t x = r0 + s < nds ? ((uint64_t)segid[s] << 33) | eend[s] : 0;
         m = x > m ? x : m;
         rmax[s] = m;
       }
       const uint64_t incl = wave_incl_max64(m);
       uint64_t ex = ((uint64_t)from_prev_lane((uint32_t)(incl >> 32)) << 32) | from_prev_lane((uint32_t)incl);
-      uint32_t nr_lane = 0;
+      uint32_t newr[E], nr_lane = 0;
 #pragma unroll
       for (uint32_t s = 0; s < E; s++) {
         const uint64_t before = ex;  // running max through position r - 1
         rmax[s] = rmax[s] > ex ? rmax[s] : ex;
         ex = rmax[s];
-        const bool v = E * lane + s < nds;
-        const uint64_t cl = ek[s] & 0xffffffffull;
-        newr[s] = v && (segst[s] || cl > (before & 0x1ffffffffull));
+        newr[s] = r0 + s < nds && (segst[s] || ecl[s] > (before & 0x1ffffffffull));
         nr_lane += newr[s];
       }
-      // merged-range ids
       const uint32_t incl_r = wave_incl_add(nr_lane);
-      const uint32_t nranges_ = lane_read(incl_r, 63);
+      nranges = lane_read(incl_r, 63);
       uint32_t run = incl_r - nr_lane;
       const uint32_t next_first = from_next_lane(newr[0]);  // newr of position E*(lane+1)
+      __syncthreads();  // the sorted delete ranges are in registers: the phase-5 arrays reuse R
 #pragma unroll
       for (uint32_t s = 0; s < E; s++) {
-        const uint32_t r = E * lane + s;
+        const uint32_t r = r0 + s;
         if (r >= nds) break;
         run += newr[s];
         const uint32_t rid = run - 1;
         if (newr[s]) {
-          at<uint32_t>(L_QCLK + 4 * rid) = (uint32_t)(ek[s] & 0xffffffffull);
+          at<uint32_t>(L_QCLK + 4 * rid) = ecl[s];
           at<uint8_t>(L_QGRP + rid) = (uint8_t)segid[s];
         }
         const bool nxt_new = s + 1 < E ? newr[s + 1] != 0 : next_first != 0;
         if (r + 1 >= nds || nxt_new) {
           const uint64_t en = rmax[s] & 0x1ffffffffull;
-          if (en > 0xffffffffull) bad = true;
+          bad |= en > 0xffffffffull;
           at<uint32_t>(L_QEND + 4 * rid) = (uint32_t)en;
         }
         if (segst[s]) {
           at<uint16_t>(L_GFIRST + 2 * segid[s]) = (uint16_t)rid;
-          at<uint32_t>(L_GCLI + 4 * segid[s]) = (uint32_t)(ek[s] >> 32);
+          at<uint32_t>(L_GCLI + 4 * segid[s]) = ecli[s];
           at<uint32_t>(L_GMIN + 4 * segid[s]) = 0xffffffffu;
         }
       }
-      if (lane == 0) {
-        at<uint16_t>(L_GFIRST + 2 * ngroups) = (uint16_t)nranges_;
-        at<uint32_t>(L_MISC + 8) = nranges_;
-      }
-    }
-    if (__any(bad)) YM_DECLINE()
-    __syncthreads();
-    // first appearance of each client (min over its entries' update << 8 | position)
+      if (lane == 0) at<uint16_t>(L_GFIRST + 2 * ngroups) = (uint16_t)nranges;
+      if (__any(bad)) YM_DECLINE()
+      __syncthreads();
+      // first appearance of each client: min over its entries' (update << 8 | position)
 #pragma unroll
-    for (uint32_t s = 0; s < E; s++)
-      if (E * lane + s < nds) atomicMin(&at<uint32_t>(L_GMIN + 4 * segid[s]), eseq[s]);
-    const uint32_t nranges = at<uint32_t>(L_MISC + 8);
-    // merged ranges q = E*lane + s: bytes, exclusive prefix over range ids
-    uint32_t qclk[E], qlen[E], qgrp[E], qoff[E], qb_lane = 0;
-#pragma unroll
-    for (uint32_t s = 0; s < E; s++) {
-      const uint32_t q = E * lane + s;
-      const bool v = q < nranges;
-      qclk[s] = v ? at<uint32_t>(L_QCLK + 4 * q) : 0;
-      qlen[s] = v ? at<uint32_t>(L_QEND + 4 * q) - qclk[s] : 0;
-      qgrp[s] = v ? at<uint8_t>(L_QGRP + q) : 0;
-      qoff[s] = v ? vsz(qclk[s]) + vsz(qlen[s]) : 0;
-      qb_lane += qoff[s];
+      for (uint32_t s = 0; s < E; s++)
+        if (r0 + s < nds) atomicMin(&at<uint32_t>(L_GMIN + 4 * segid[s]), eseq[s]);
     }
+    // merged ranges q = E*lane + s: exclusive byte prefix over range ids
     {
-      const uint32_t incl = wave_incl_add(qb_lane);
-      uint32_t run = incl - qb_lane;
+      uint32_t qb[E], t = 0;
 #pragma unroll
       for (uint32_t s = 0; s < E; s++) {
         const uint32_t q = E * lane + s;
-        const uint32_t b = qoff[s];
-        qoff[s] = run;
+        const uint32_t c0 = q < nranges ? at<uint32_t>(L_QCLK + 4 * q) : 0;
+        qb[s] = q < nranges ? vsz(c0) + vsz(at<uint32_t>(L_QEND + 4 * q) - c0) : 0;
+        t += qb[s];
+      }
+      const uint32_t incl = wave_incl_add(t);
+      uint32_t run = incl - t;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint32_t q = E * lane + s;
         if (q < nranges) at<uint16_t>(L_QPRE + 2 * q) = (uint16_t)run;
-        run += b;
+        run += qb[s];
       }
       if (lane == 63) at<uint16_t>(L_QPRE + 2 * nranges) = (uint16_t)incl;
     }
     __syncthreads();
-    // groups g = lane + 64 s: header, bytes, rank by first appearance
-    uint32_t gcli[E], gcnt[E], grk[E], gbytes[E], gq0[E];
+    // groups g = lane + 64 s: bytes and rank by first appearance
+    uint32_t grk[E], gbytes[E];
 #pragma unroll
     for (uint32_t s = 0; s < E; s++) {
       const uint32_t g = lane + 64 * s;
       const bool v = g < ngroups;
       const uint32_t f0 = v ? at<uint16_t>(L_GFIRST + 2 * g) : 0, f1 = v ? at<uint16_t>(L_GFIRST + 2 * g + 2) : 0;
-      gcli[s] = v ? at<uint32_t>(L_GCLI + 4 * g) : 0;
-      gcnt[s] = f1 - f0;
-      gq0[s] = v ? at<uint16_t>(L_QPRE + 2 * f0) : 0;
-      gbytes[s] = v ? vsz(gcli[s]) + vsz(gcnt[s]) + at<uint16_t>(L_QPRE + 2 * f1) - gq0[s] : 0;
+      gbytes[s] = v ? vsz(at<uint32_t>(L_GCLI + 4 * g)) + vsz(f1 - f0) + at<uint16_t>(L_QPRE + 2 * f1) -
+                          at<uint16_t>(L_QPRE + 2 * f0)
+                    : 0;
       const uint32_t mine = v ? at<uint32_t>(L_GMIN + 4 * g) : 0;
       uint32_t rk_ = 0;
       for (uint32_t h = 0; h < ngroups; h++) rk_ += at<uint32_t>(L_GMIN + 4 * h) < mine;
       grk[s] = rk_;
     }
-    __syncthreads();
 #pragma unroll
     for (uint32_t s = 0; s < E; s++)
       if (lane + 64 * s < ngroups) at<uint16_t>(L_GBYR + 2 * grk[s]) = (uint16_t)gbytes[s];
     __syncthreads();
+    const uint32_t ds_hdr = vsz(ngroups);
+    const uint32_t dsb = hdr + struct_bytes;
     uint32_t ds_groups_bytes;
-    {  // exclusive prefix over ranks (ranks E*lane + s), in place
+    {  // exclusive prefix over ranks (ranks E*lane + s)
       uint32_t v[E], t = 0;
 #pragma unroll
       for (uint32_t s = 0; s < E; s++) { const uint32_t r = E * lane + s; v[s] = r < ngroups ? at<uint16_t>(L_GBYR + 2 * r) : 0; t += v[s]; }
@@ -784,56 +847,40 @@ __global__ void __launch_bounds__(64) k_fast_merge_v1(GeneralJob j) {
       }
     }
     __syncthreads();
-    const uint32_t ds_hdr = vsz(ngroups);
-    const uint32_t dsb = hdr + struct_bytes;
-    uint32_t goff[E];
+    // group g's output offset; its ranges' base = offset + header - prefix of its first range
 #pragma unroll
-    for (uint32_t s = 0; s < E; s++) goff[s] = lane + 64 * s < ngroups ? dsb + ds_hdr + at<uint16_t>(L_GBYR + 2 * grk[s]) : 0;
-    // merged range q's output offset: its group's offset + group header + prefix within the group.
-    // Per-group base (offset + header - prefix of its first range) by group id, through LDS.
+    for (uint32_t s = 0; s < E; s++) {
+      const uint32_t g = lane + 64 * s;
+      if (g < ngroups) {
+        const uint32_t f0 = at<uint16_t>(L_GFIRST + 2 * g), f1 = at<uint16_t>(L_GFIRST + 2 * g + 2);
+        const uint32_t off = dsb + ds_hdr + at<uint16_t>(L_GBYR + 2 * grk[s]);
+        at<uint32_t>(L_GMIN + 4 * g) = off;  // first appearance is no longer needed
+        at<uint32_t>(L_GB2 + 4 * g) = off + vsz(at<uint32_t>(L_GCLI + 4 * g)) + vsz(f1 - f0) - at<uint16_t>(L_QPRE + 2 * f0);
+      }
+    }
     __syncthreads();
-#pragma unroll
-    for (uint32_t s = 0; s < E; s++)
-      if (lane + 64 * s < ngroups)
-        at<uint32_t>(L_GMIN + 4 * (lane + 64 * s)) = goff[s] + vsz(gcli[s]) + vsz(gcnt[s]) - gq0[s];
-    __syncthreads();
-#pragma unroll
-    for (uint32_t s = 0; s < E; s++)
-      if (E * lane + s < nranges) qoff[s] += at<uint32_t>(L_GMIN + 4 * qgrp[s]);
     const uint32_t total = dsb + ds_hdr + ds_groups_bytes;
-    // output slot: 16-aligned inside the bound 2 * in + 64 per doc
-    const uint64_t slot = 2 * (b0 - arena0) + 64ull * d;
-    const uint64_t slot_al = (slot + 15) & ~15ull;
-    if (total > OUT || slot_al + total > slot + 2 * bytes + 64) YM_DECLINE()
-    if (slot_al + total > j.cap) {  // caller's arena is smaller than the fast region
+    if (slot_al + total > slot_end) {
+      if (slot_al + total > slot + 2 * bytes + 64) YM_DECLINE()
       if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }
       __syncthreads();
       continue;
     }
     YM_STOP(5)
-    // ---- 6. emit the delete set
-    if (lane == 0) put_vu(L_OUT + dsb, ngroups);
+    // ---- 6. write the delete set: vu(#clients) | per client (first-appearance order): client, count, ranges
+    if (lane == 0) put_vu(dst, dsb, ngroups);
 #pragma unroll
     for (uint32_t s = 0; s < E; s++) {
-      if (lane + 64 * s < ngroups) {
-        uint32_t p = L_OUT + goff[s];
-        p = put_vu(p, gcli[s]);
-        put_vu(p, gcnt[s]);
+      const uint32_t g = lane + 64 * s;
+      if (g < ngroups)
+        put_vu(dst, put_vu(dst, at<uint32_t>(L_GMIN + 4 * g), at<uint32_t>(L_GCLI + 4 * g)),
+               at<uint16_t>(L_GFIRST + 2 * g + 2) - at<uint16_t>(L_GFIRST + 2 * g));
+      const uint32_t q = E * lane + s;
+      if (q < nranges) {
+        const uint32_t c0 = at<uint32_t>(L_QCLK + 4 * q);
+        const uint32_t off = at<uint32_t>(L_GB2 + 4 * at<uint8_t>(L_QGRP + q)) + at<uint16_t>(L_QPRE + 2 * q);
+        put_vu(dst, put_vu(dst, off, c0), at<uint32_t>(L_QEND + 4 * q) - c0);
       }
-      if (E * lane + s < nranges) {
-        uint32_t p = L_OUT + qoff[s];
-        p = put_vu(p, qclk[s]);
-        put_vu(p, qlen[s]);
-      }
-    }
-    __syncthreads();
-    YM_STOP(6)
-    // ---- 7. 16-B stores into the doc's slot
-    {
-      uint8_t *dst = j.out + slot_al;
-      const uint32_t nvec = total >> 4;
-      for (uint32_t v = lane; v < nvec; v += 64) reinterpret_cast<uint4 *>(dst)[v] = at<uint4>(L_OUT + 16 * v);
-      for (uint32_t b = (nvec << 4) + lane; b < total; b += 64) dst[b] = sm[L_OUT + b];
     }
     if (lane == 0) {
       j.out_off[d] = slot_al;
@@ -859,17 +906,32 @@ int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st
   if (op != OP_MERGE || j.v2) return 0;  // fast path: V1 merges (the C2/C4 headline configs)
   k_fast_region<<<1, 64, 0, st>>>(j, n_upd);
   const uint32_t grid = j.n < 131072 ? j.n : 131072;
-  static int stop = -1;
-  if (stop < 0) { const char *e = getenv("YMERGE_FAST_STOP"); stop = e ? atoi(e) : 0; }
-  switch (stop) {
-    case 1: k_fast_merge_v1<1><<<grid, 64, LDS_BYTES, st>>>(j); break;
-    case 2: k_fast_merge_v1<2><<<grid, 64, LDS_BYTES, st>>>(j); break;
-    case 3: k_fast_merge_v1<3><<<grid, 64, LDS_BYTES, st>>>(j); break;
-    case 4: k_fast_merge_v1<4><<<grid, 64, LDS_BYTES, st>>>(j); break;
-    case 5: k_fast_merge_v1<5><<<grid, 64, LDS_BYTES, st>>>(j); break;
-    case 6: k_fast_merge_v1<6><<<grid, 64, LDS_BYTES, st>>>(j); break;
-    default: k_fast_merge_v1<0><<<grid, 64, LDS_BYTES, st>>>(j); break;
+  static int stop = -1, pad = 0;
+  if (stop < 0) {
+    const char *e = getenv("YMERGE_FAST_STOP");
+    stop = e ? atoi(e) : 0;
+    e = getenv("YMERGE_FAST_LDS_PAD");  // occupancy experiments: extra dynamic LDS per wave
+    pad = e ? atoi(e) : 0;
   }
+  const uint32_t LDS_BYTES = fastv1::LDS_BYTES + pad;
+  static int occ = -1;
+  if (occ < 0) { const char *e = getenv("YMERGE_FAST_OCC"); occ = e ? atoi(e) : 5; }
+#define YM_LAUNCH(S, O) k_fast_merge_v1<S, O><<<grid, 64, LDS_BYTES, st>>>(j)
+  if (occ == 4) {
+    YM_LAUNCH(0, 4);
+  } else if (occ == 6) {
+    YM_LAUNCH(0, 6);
+  } else {
+    switch (stop) {
+      case 1: YM_LAUNCH(1, 5); break;
+      case 2: YM_LAUNCH(2, 5); break;
+      case 3: YM_LAUNCH(3, 5); break;
+      case 4: YM_LAUNCH(4, 5); break;
+      case 5: YM_LAUNCH(5, 5); break;
+      default: YM_LAUNCH(0, 5); break;
+    }
+  }
+#undef YM_LAUNCH
   return 1;
 }
 
