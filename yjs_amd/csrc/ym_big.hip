@@ -1,0 +1,434 @@
+// ym_big.hip -- V1 diffUpdate / encodeStateVectorFromUpdate over single updates of any size: one wave
+// per document, the update streamed through an LDS window, the struct walk run by the whole wave in
+// lockstep (uniform control flow, no divergence), output assembled from small LDS pieces plus
+// verbatim input spans copied by all 64 lanes.
+//
+// Semantics are yjs 13.5.16's:
+//   diffUpdate (bundle fs / us@40707): per client section, structs whose end <= sv[client] are dropped,
+//     Skips before the cut are dropped, the first struct past the cut is written with offset
+//     max(sv - clock, 0) (Item.write with offset: origin := (client, clock + offset - 1), content
+//     sliced -- ContentString.js:94-96, ContentDeleted.js:83-85, ContentAny.js:80-87, GC.js:45-48),
+//     every following struct of the section is written as is (LazyStructWriter, rs/gs/ps/ws), the
+//     delete set is re-written unchanged (readDeleteSet + writeDeleteSet, DeleteSet.js:219-256).
+//   encodeStateVectorFromUpdate (cs / os@37724): per client, the end of its last struct while its
+//     first struct starts at 0 and no Skip has been seen; clients with clock 0 are omitted.
+// "As is" = the input bytes with the info byte normalised (0x20 cleared when an origin is present,
+// GC info := 0), which the kernel applies as patches after the bulk copy.  Inputs this path does not
+// verify (JSON/Doc content, non-canonical encodings, repeated clients, oversized structs, ...) are
+// declined to the exact general path (ym_general.hip), as in ym_fast.hip.
+#include <hip/hip_runtime.h>
+
+#include "ym_fast_common.h"
+#include "ym_kernels.h"
+
+namespace ymk {
+namespace big {
+using namespace fastc;
+
+constexpr uint32_t BW = 8192;   // LDS window over the update
+constexpr uint32_t BM = 2048;   // refill when fewer bytes remain ahead of the cursor (max struct size)
+constexpr uint32_t NSEC = 64;   // client sections per update
+constexpr uint32_t NSV = 256;   // state-vector entries
+constexpr uint32_t NPATCH = 512;
+constexpr uint32_t PRE = 48;    // sliced-struct prefix bytes per section
+
+constexpr uint32_t SECW = 12;   // u32 fields per section record
+constexpr uint32_t L_WIN = 0;                        // u8[BW + 16]
+constexpr uint32_t L_SEC = BW + 16;                  // u32[NSEC][SECW] section records
+constexpr uint32_t L_PRE = L_SEC + NSEC * 4 * SECW;  // u8[NSEC][PRE] sliced-struct head (re-encoded)
+constexpr uint32_t L_SV = L_PRE + NSEC * PRE;        // u32[NSV][2] state vector (client, clock)
+constexpr uint32_t L_PPOS = L_SV + NSV * 8;          // u32[NPATCH] patch positions (update-relative)
+constexpr uint32_t L_PVAL = L_PPOS + 4 * NPATCH;     // u8[NPATCH]  patched info bytes
+constexpr uint32_t L_DSC = L_PVAL + NPATCH;          // u32[64]     delete-set clients seen
+constexpr uint32_t LDS_BYTES = L_DSC + 256;
+// section record fields: head bytes (or NONE: nothing written), span A (content tail of a sliced
+// struct), span B (the following structs, as is), part header (written, client, first clock), and
+// the output position of update byte 0 within span B (for the patches)
+enum { S_PRELEN = 0, S_A0, S_A1, S_B0, S_B1, S_WRITTEN, S_CLIENT, S_FCLOCK, S_OUTB };
+constexpr uint32_t NONE = 0xffffffffu;
+__device__ __forceinline__ uint32_t &sec(uint32_t ci, uint32_t f) { return at<uint32_t>(L_SEC + 4 * (SECW * ci + f)); }
+
+// window over the update [0, len) at absolute arena offset b0; LDS byte i <-> arena byte wa + i
+struct Win {
+  uint64_t wa;     // absolute arena offset of LDS byte 0 (16-aligned)
+  uint64_t b0;     // absolute offset of the update
+  uint32_t len;    // update bytes
+  uint32_t wend;   // LDS offset one past the last usable byte
+};
+__device__ __forceinline__ uint32_t rel(const Win &w, uint32_t p) { return (uint32_t)(w.wa + p - w.b0); }
+
+// (re)load the window so that update byte `r` is near its start; all lanes participate
+__device__ __forceinline__ void win_load(Win &w, const uint8_t *A, uint32_t r) {
+  __syncthreads();
+  const uint64_t abs = w.b0 + r;
+  w.wa = abs & ~15ull;
+  const uint64_t end = w.b0 + w.len;  // exclusive
+  const uint64_t wend_abs = w.wa + BW < end ? w.wa + BW : end;
+  w.wend = (uint32_t)(wend_abs - w.wa);
+  const uint32_t nvec = (w.wend + 15) >> 4;
+  const uint4 *src = reinterpret_cast<const uint4 *>(A + w.wa);
+  for (uint32_t v = threadIdx.x; v < nvec; v += 64) at<uint4>(L_WIN + 16 * v) = src[v];
+  __syncthreads();
+}
+// keeps at least BM bytes (or the rest of the update) ahead of cursor c in the window
+__device__ __forceinline__ void win_ensure(Win &w, Cur &c, const uint8_t *A) {
+  if (c.p + BM > w.wend && w.wa + w.wend < w.b0 + w.len) {
+    const uint32_t r = rel(w, c.p), re = rel(w, c.e);
+    win_load(w, A, r);
+    c.p = (uint32_t)(w.b0 + r - w.wa);
+    c.e = w.wend;  // the update's end when it lies inside the window, else the window's end
+    (void)re;
+  }
+}
+__device__ __forceinline__ uint32_t put_vu_lds(uint32_t p, uint32_t v) {
+  while (v > 127) { sm[p++] = (uint8_t)(0x80 | (v & 127)); v >>= 7; }
+  sm[p++] = (uint8_t)v;
+  return p;
+}
+
+#define YB_DECLINE()                                        \
+  {                                                         \
+    if (threadIdx.x == 0) {                                 \
+      j.status[d] = ST_PENDING;                             \
+      j.pend_list[atomicAdd(j.pend_count, 1u)] = d;         \
+    }                                                       \
+    __syncthreads();                                        \
+    continue;                                               \
+  }
+
+// OP = OP_DIFF or OP_SV (V1 only)
+template <int OP>
+__global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
+    const uint32_t u0 = j.doc_upd[d];
+    if (j.doc_upd[d + 1] - u0 != 1) YB_DECLINE()
+    Win w;
+    w.b0 = j.upd_off[u0];
+    const uint64_t len64 = j.upd_off[u0 + 1] - w.b0;
+    if (len64 == 0 || len64 > 0xfffffff0ull) YB_DECLINE()
+    w.len = (uint32_t)len64;
+    // ---- state vector (diff): decodeStateVector, later entries win (encoding.js:536-545)
+    uint32_t nsv = 0;
+    bool bad = false;
+    if (OP == OP_DIFF) {
+      const uint64_t s0 = j.sv_off[d], s1 = j.sv_off[d + 1];
+      if (s1 - s0 > 4 * NSV * 5 + 8) YB_DECLINE()
+      // the state vector is tiny: stage it through the window
+      {
+        const uint64_t a = s0 & ~15ull;
+        const uint32_t nvec = (uint32_t)((s1 - a + 15) >> 4);
+        const uint4 *src = reinterpret_cast<const uint4 *>(j.sv + a);
+        for (uint32_t v = lane; v < nvec; v += 64) at<uint4>(L_WIN + 16 * v) = src[v];
+        __syncthreads();
+        Cur c = {(uint32_t)(s0 - a), (uint32_t)(s1 - a), false};
+        const uint32_t n = rvu(c);
+        for (uint32_t i = 0; i < n && !c.bad; i++) {
+          const uint32_t cl = rvu(c), ck = rvu(c);
+          if (nsv >= NSV) { c.bad = true; break; }
+          if (lane == 0) { at<uint32_t>(L_SV + 8 * nsv) = cl; at<uint32_t>(L_SV + 8 * nsv + 4) = ck; }
+          nsv++;
+        }
+        bad = c.bad;
+      }
+      if (bad) YB_DECLINE()
+    }
+    // ---- struct section (encoding.js:127-198 layout; 13.5.16 LazyStructReader)
+    win_load(w, j.A, 0);
+    Cur c = {(uint32_t)(w.b0 - w.wa), w.wend, false};
+    const uint32_t nclients = rvu(c);
+    if (nclients > NSEC) YB_DECLINE()
+    uint32_t nparts = 0, npatch = 0, body_bytes = 0;
+    // state-vector op state (os@37724), carried across sections
+    uint32_t sv_client = 0, sv_clock = 0, sv_n = 0;
+    bool sv_stop = false, sv_any = false;
+    uint32_t prev_client = 0;
+    bool declined = false;
+    for (uint32_t ci = 0; ci < nclients && !c.bad && !declined; ci++) {
+      win_ensure(w, c, j.A);
+      const uint32_t nstructs = rvu(c);
+      const uint32_t client = rvu(c);
+      uint64_t clock = rvu(c);
+      if (ci > 0 && client == prev_client) { declined = true; break; }  // writer would not start a part
+      prev_client = client;
+      uint32_t k = 0;
+      if (OP == OP_DIFF)
+        for (uint32_t i = 0; i < nsv; i++)
+          if (at<uint32_t>(L_SV + 8 * i) == client) k = at<uint32_t>(L_SV + 8 * i + 4);
+      if (OP == OP_SV && nstructs > 0 && sv_any && client != sv_client) {  // client change (os@37724)
+        if (sv_clock != 0) {
+          if (sv_n >= NSV) { declined = true; break; }
+          if (lane == 0) { at<uint32_t>(L_SV + 8 * sv_n) = sv_client; at<uint32_t>(L_SV + 8 * sv_n + 4) = sv_clock; }
+          sv_n++;
+        }
+        sv_client = client; sv_clock = 0; sv_stop = clock != 0;
+      }
+      bool copying = false;
+      uint32_t written = 0, b0r = 0;
+      for (uint32_t si = 0; si < nstructs && !c.bad; si++) {
+        win_ensure(w, c, j.A);
+        const uint32_t s0 = c.p;
+        const uint32_t info = rdb(c);
+        uint32_t len;
+        const bool skip = info == 10, gc = !skip && (info & 31) == 0;
+        if (skip || gc) len = rvu(c);
+        else if (!item_body(c, info, len)) { declined = true; break; }
+        if (c.bad || c.p > w.wend) { declined = true; break; }
+        if (clock + len > 0xffffffffull) { declined = true; break; }
+        if (OP == OP_SV) {
+          if (!sv_any) {  // the update's first struct initialises the state
+            sv_any = true;
+            sv_client = client;
+            sv_stop = clock != 0;
+            sv_clock = sv_stop ? 0 : (uint32_t)(clock + len);
+          }
+          if (skip) sv_stop = true;
+          if (!sv_stop) sv_clock = (uint32_t)(clock + len);
+        } else if (!copying) {
+          if (!skip && clock + len > k) {  // the cut: first struct that ends past sv[client]
+            copying = true;
+            written = 1;
+            const uint32_t off = k > clock ? (uint32_t)(k - clock) : 0;
+            const uint32_t pre = L_PRE + ci * PRE;
+            uint32_t q = pre, a0 = 0, a1 = 0;
+            if (off == 0) {
+              b0r = rel(w, s0);
+              const uint32_t ni = gc ? 0 : ((info & 0xC0) ? info & ~0x20u : info);
+              if (ni != info) {
+                if (npatch >= NPATCH) { declined = true; break; }
+                if (lane == 0) { at<uint32_t>(L_PPOS + 4 * npatch) = b0r; sm[L_PVAL + npatch] = (uint8_t)ni; }
+                npatch++;
+              }
+            } else {
+              // Item.write / GC.write with offset: re-encode the head, copy the content's tail
+              Cur e = {s0 + 1, c.p, false};
+              const uint32_t ref = info & 31;
+              if (gc) {
+                if (lane == 0) { sm[q] = 0; put_vu_lds(q + 1, len - off); }
+                q += 1 + vsz(len - off);
+              } else {
+                if (ref != 1 && ref != 4 && ref != 8) { declined = true; break; }
+                // parentSub was read iff there were no origins; Item.write keeps its info bit even
+                // though the new origin suppresses writing it (E9)
+                const uint32_t ni = ref | 0x80 | (info & 0x40) | ((info & 0xC0) == 0 ? (info & 0x20) : 0);
+                if (info & 0x80) { skvu(e); skvu(e); }
+                uint32_t ro0 = 0, ro1 = 0;
+                if (info & 0x40) { ro0 = e.p; skvu(e); skvu(e); ro1 = e.p; }
+                if ((info & 0xC0) == 0) {
+                  const uint32_t pi = rvu(e);
+                  if (pi == 1) { const uint32_t n = rvu(e); e.p += n; }
+                  else { skvu(e); skvu(e); }
+                  if (info & 0x20) { const uint32_t n = rvu(e); e.p += n; }
+                }
+                if (lane == 0) {
+                  sm[q] = (uint8_t)ni;
+                  uint32_t t = put_vu_lds(q + 1, client);
+                  t = put_vu_lds(t, (uint32_t)(clock + off - 1));
+                  for (uint32_t b = ro0; b < ro1; b++) sm[t++] = sm[b];
+                }
+                q += 1 + vsz(client) + vsz((uint32_t)(clock + off - 1)) + (ro1 - ro0);
+                if (ref == 1) {
+                  rvu(e);
+                  if (lane == 0) put_vu_lds(q, len - off);
+                  q += vsz(len - off);
+                } else if (ref == 8) {
+                  rvu(e);
+                  for (uint32_t i = 0; i < off; i++) any_scalar(e);  // ContentAny.splice: drop `off` values
+                  if (lane == 0) put_vu_lds(q, len - off);
+                  q += vsz(len - off);
+                  a0 = rel(w, e.p);
+                  a1 = rel(w, c.p);
+                } else {  // ContentString: str.slice(off) in UTF-16 units; a split surrogate throws in yjs
+                  const uint32_t n = rvu(e);
+                  uint32_t bi = 0, u = 0;
+                  while (u < off && bi < n) {
+                    const uint32_t b = sm[e.p + bi];
+                    const uint32_t l = b < 0x80 ? 1 : b < 0xE0 ? 2 : b < 0xF0 ? 3 : 4;
+                    u += l == 4 ? 2 : 1;
+                    bi += l;
+                  }
+                  if (u != off) { declined = true; break; }  // cut inside a surrogate pair: URIError path
+                  if (lane == 0) put_vu_lds(q, n - bi);
+                  q += vsz(n - bi);
+                  a0 = rel(w, e.p + bi);
+                  a1 = rel(w, e.p + n);
+                }
+                if (e.bad) { declined = true; break; }
+              }
+              b0r = rel(w, c.p);
+              if (q - pre > PRE) { declined = true; break; }
+            }
+            if (lane == 0) {
+              sec(ci, S_PRELEN) = q - pre;
+              sec(ci, S_A0) = a0;
+              sec(ci, S_A1) = a1;
+              sec(ci, S_B0) = b0r;
+              sec(ci, S_FCLOCK) = (uint32_t)(clock + off);
+              sec(ci, S_CLIENT) = client;
+            }
+          }
+        } else {
+          written++;
+          const uint32_t ni = skip ? info : gc ? 0 : ((info & 0xC0) ? info & ~0x20u : info);
+          if (ni != info) {
+            if (npatch >= NPATCH) { declined = true; break; }
+            if (lane == 0) { at<uint32_t>(L_PPOS + 4 * npatch) = rel(w, s0); sm[L_PVAL + npatch] = (uint8_t)ni; }
+            npatch++;
+          }
+        }
+        clock += len;
+      }
+      if (declined || c.bad) break;
+      if (OP == OP_DIFF) {
+        if (lane == 0) {
+          sec(ci, S_B1) = copying ? rel(w, c.p) : 0;
+          sec(ci, S_WRITTEN) = written;
+          if (!copying) sec(ci, S_PRELEN) = NONE;
+        }
+        nparts += copying;
+      }
+    }
+    if (declined || c.bad) YB_DECLINE()
+    __syncthreads();
+    if (OP == OP_SV) {
+      if (sv_any && sv_clock != 0) {
+        if (lane == 0) { at<uint32_t>(L_SV + 8 * sv_n) = sv_client; at<uint32_t>(L_SV + 8 * sv_n + 4) = sv_clock; }
+        sv_n++;
+      }
+      __syncthreads();
+      uint32_t total = vsz(sv_n);
+      for (uint32_t i = 0; i < sv_n; i++) total += vsz(at<uint32_t>(L_SV + 8 * i)) + vsz(at<uint32_t>(L_SV + 8 * i + 4));
+      uint64_t base = 0;
+      if (lane == 0) base = atomicAdd((unsigned long long *)j.used, (unsigned long long)total);
+      base = ((uint64_t)lane_read((uint32_t)(base >> 32), 0) << 32) | lane_read((uint32_t)base, 0);
+      if (base + total > j.cap) {
+        if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }
+        __syncthreads();
+        continue;
+      }
+      if (lane == 0) {
+        uint8_t *o = j.out + base;
+        uint32_t p = 0;
+        auto put = [&](uint32_t v) { while (v > 127) { o[p++] = (uint8_t)(0x80 | (v & 127)); v >>= 7; } o[p++] = (uint8_t)v; };
+        put(sv_n);
+        for (uint32_t i = 0; i < sv_n; i++) { put(at<uint32_t>(L_SV + 8 * i)); put(at<uint32_t>(L_SV + 8 * i + 4)); }
+        j.out_off[d] = base;
+        j.out_len[d] = total;
+        j.status[d] = ym::ST_OK;
+      }
+      __syncthreads();
+      continue;
+    }
+    // ---- delete set: validated, then copied verbatim (readDeleteSet + writeDeleteSet round trip)
+    win_ensure(w, c, j.A);
+    const uint32_t ds0 = rel(w, c.p);
+    {
+      const uint32_t ndc = rvu(c);
+      for (uint32_t i = 0; i < ndc && !c.bad && !declined; i++) {
+        win_ensure(w, c, j.A);
+        const uint32_t client = rvu(c);
+        const uint32_t m = rvu(c);
+        // readDeleteSet drops clients without ranges and merges a repeated client into its first
+        // occurrence: either makes the re-written set differ from the input bytes
+        if (m == 0 || i >= 64) { declined = true; break; }
+        for (uint32_t h = 0; h < i; h++) declined |= at<uint32_t>(L_DSC + 4 * h) == client;
+        if (lane == 0) at<uint32_t>(L_DSC + 4 * i) = client;
+        for (uint32_t q = 0; q < m && !c.bad; q++) {
+          win_ensure(w, c, j.A);
+          rvu(c);
+          rvu(c);
+        }
+      }
+    }
+    if (declined || c.bad) YB_DECLINE()
+    const uint32_t ds1 = rel(w, c.p);
+    __syncthreads();
+    // ---- sizes, allocation
+    uint32_t total = vsz(nparts) + (ds1 - ds0);
+    for (uint32_t ci = 0; ci < nclients; ci++) {
+      const uint32_t pl = sec(ci, S_PRELEN);
+      if (pl == NONE) continue;
+      total += vsz(sec(ci, S_WRITTEN)) + vsz(sec(ci, S_CLIENT)) + vsz(sec(ci, S_FCLOCK)) + pl +
+               (sec(ci, S_A1) - sec(ci, S_A0)) + (sec(ci, S_B1) - sec(ci, S_B0));
+    }
+    uint64_t base = 0;
+    if (lane == 0) base = atomicAdd((unsigned long long *)j.used, (unsigned long long)total);
+    base = ((uint64_t)lane_read((uint32_t)(base >> 32), 0) << 32) | lane_read((uint32_t)base, 0);
+    if (base + total > j.cap) {
+      if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }
+      __syncthreads();
+      continue;
+    }
+    // ---- write: small pieces by lane 0, spans by the wave, then the info patches
+    uint8_t *const o = j.out + base;
+    const uint8_t *const src = j.A + w.b0;
+    auto copy_span = [&](uint32_t dst, uint32_t s0_, uint32_t s1_) {
+      for (uint32_t i = s0_ + lane; i < s1_; i += 64) o[dst + i - s0_] = src[i];
+    };
+    uint32_t p = 0;
+    if (lane == 0) {
+      uint32_t t = 0;
+      uint32_t v = nparts;
+      while (v > 127) { o[t++] = (uint8_t)(0x80 | (v & 127)); v >>= 7; }
+      o[t++] = (uint8_t)v;
+    }
+    p = vsz(nparts);
+    for (uint32_t ci = 0; ci < nclients; ci++) {
+      const uint32_t pl = sec(ci, S_PRELEN);
+      if (pl == NONE) continue;
+      const uint32_t written = sec(ci, S_WRITTEN), client = sec(ci, S_CLIENT), fclock = sec(ci, S_FCLOCK);
+      if (lane == 0) {  // part header (LazyStructWriter: written, client, first clock) + sliced head
+        uint32_t t = p;
+        for (uint32_t v : {written, client, fclock}) {
+          while (v > 127) { o[t++] = (uint8_t)(0x80 | (v & 127)); v >>= 7; }
+          o[t++] = (uint8_t)v;
+        }
+        for (uint32_t b = 0; b < pl; b++) o[t + b] = sm[L_PRE + ci * PRE + b];
+      }
+      p += vsz(written) + vsz(client) + vsz(fclock) + pl;
+      const uint32_t a0 = sec(ci, S_A0), a1 = sec(ci, S_A1);
+      copy_span(p, a0, a1);
+      p += a1 - a0;
+      const uint32_t b0r = sec(ci, S_B0), b1r = sec(ci, S_B1);
+      copy_span(p, b0r, b1r);
+      if (lane == 0) sec(ci, S_OUTB) = p - b0r;  // output position = update position + S_OUTB
+      p += b1r - b0r;
+    }
+    copy_span(p, ds0, ds1);
+    __threadfence_block();
+    __syncthreads();
+    // patches: each lies in the B span of exactly one section (sections are disjoint, in order)
+    for (uint32_t i = lane; i < npatch; i += 64) {
+      const uint32_t pos = at<uint32_t>(L_PPOS + 4 * i);
+      for (uint32_t ci = 0; ci < nclients; ci++)
+        if (sec(ci, S_PRELEN) != NONE && pos >= sec(ci, S_B0) && pos < sec(ci, S_B1)) o[sec(ci, S_OUTB) + pos] = sm[L_PVAL + i];
+    }
+    if (lane == 0) {
+      j.out_off[d] = base;
+      j.out_len[d] = total;
+      j.status[d] = ym::ST_OK;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace big
+
+// the general path's bump allocator starts at 0; empty work list
+__global__ void k_big_init(GeneralJob j) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    *j.used = 0;
+    *j.pend_count = 0;
+  }
+}
+
+int big_launch(uint32_t op, const GeneralJob &j, hipStream_t st) {
+  if (j.v2 || (op != OP_DIFF && op != OP_SV)) return 0;
+  k_big_init<<<1, 64, 0, st>>>(j);
+  const uint32_t grid = j.n < 65536 ? j.n : 65536;
+  if (op == OP_DIFF) big::k_big_v1<OP_DIFF><<<grid, 64, big::LDS_BYTES, st>>>(j);
+  else big::k_big_v1<OP_SV><<<grid, 64, big::LDS_BYTES, st>>>(j);
+  return 1;
+}
+
+}  // namespace ymk

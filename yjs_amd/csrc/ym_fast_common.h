@@ -1,0 +1,271 @@
+// ym_fast_common.h -- device helpers shared by the LDS kernels (ym_fast.hip: batched V1 merge;
+// ym_big.hip: V1 diff / state vector over single large updates): LDS accessors, DPP wave scans,
+// lib0 varuint / varString / any readers with the canonical-form checks the verbatim copy relies on.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ymk {
+namespace fastc {
+
+extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
+template <class T>
+__device__ __forceinline__ T &at(uint32_t off) { return *reinterpret_cast<T *>(sm + off); }
+// unaligned LDS accesses (gfx950 runs them in hardware: tools/probe/lds_unaligned.hip)
+__device__ __forceinline__ uint64_t ld8(uint32_t p) { uint64_t x; __builtin_memcpy(&x, sm + p, 8); return x; }
+__device__ __forceinline__ uint32_t ld4(uint32_t p) { uint32_t x; __builtin_memcpy(&x, sm + p, 4); return x; }
+__device__ __forceinline__ void st4(uint32_t p, uint32_t x) { __builtin_memcpy(sm + p, &x, 4); }
+
+// ---- wave primitives (DPP row shifts + row broadcasts: no LDS traffic) ---------------------------
+#define YM_DPP(x, ctl, rm) (uint32_t) __builtin_amdgcn_update_dpp(0, (int)(x), ctl, rm, 0xf, false)
+// inclusive prefix sum over the 64 lanes
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
+  x += YM_DPP(x, 0x111, 0xf);  // row_shr:1
+  x += YM_DPP(x, 0x112, 0xf);  // row_shr:2
+  x += YM_DPP(x, 0x114, 0xf);  // row_shr:4
+  x += YM_DPP(x, 0x118, 0xf);  // row_shr:8
+  x += YM_DPP(x, 0x142, 0xa);  // row_bcast:15 -> rows 1, 3
+  x += YM_DPP(x, 0x143, 0xc);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+__device__ __forceinline__ uint32_t lane_read(uint32_t x, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, l); }
+// inclusive prefix max over the 64 lanes, u64
+template <int CTL, int RM>
+__device__ __forceinline__ uint64_t max_step(uint64_t x) {
+  const uint32_t lo = YM_DPP((uint32_t)x, CTL, RM), hi = YM_DPP((uint32_t)(x >> 32), CTL, RM);
+  const uint64_t y = ((uint64_t)hi << 32) | lo;
+  return y > x ? y : x;
+}
+__device__ __forceinline__ uint64_t wave_incl_max64(uint64_t x) {
+  x = max_step<0x111, 0xf>(x);
+  x = max_step<0x112, 0xf>(x);
+  x = max_step<0x114, 0xf>(x);
+  x = max_step<0x118, 0xf>(x);
+  x = max_step<0x142, 0xa>(x);
+  x = max_step<0x143, 0xc>(x);
+  return x;
+}
+__device__ __forceinline__ uint64_t lane_read64(uint64_t x, int l) {
+  return ((uint64_t)lane_read((uint32_t)(x >> 32), l) << 32) | lane_read((uint32_t)x, l);
+}
+// value of lane-1 (0 for lane 0) / lane+1 (0 for lane 63): DPP wave_shr:1 / wave_shl:1
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, false); }
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t x) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, false); }
+
+// bytes of lib0 writeVarUint(v) for a u32: ceil(significant bits / 7), at least 1 (x * 37 >> 8 == x / 7
+// for x <= 38)
+__device__ __forceinline__ uint32_t vsz(uint32_t v) {
+  const uint32_t bits = 32 - __builtin_clzg(v, 32);
+  return ((bits > 0 ? bits : 1) + 6) * 37 >> 8;
+}
+// The document's output slot as a buffer resource: 32-bit offsets (no 64-bit address math per
+// store) and a hardware bound (stores past the slot are dropped).
+typedef __amdgpu_buffer_rsrc_t Slot;
+__device__ __forceinline__ Slot make_slot(uint8_t *base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void ob8(Slot o, uint32_t p, uint32_t v) {
+  __builtin_amdgcn_raw_buffer_store_b8((int8_t)v, o, (int)p, 0, 0);
+}
+__device__ __forceinline__ void ob32(Slot o, uint32_t p, uint32_t v) {
+  __builtin_amdgcn_raw_buffer_store_b32((int)v, o, (int)p, 0, 0);
+}
+// lib0 writeVarUint straight into the output slot
+__device__ __forceinline__ uint32_t put_vu(Slot o, uint32_t p, uint64_t v) {
+  while (v > 127) { ob8(o, p++, 0x80 | (uint32_t)(v & 127)); v >>= 7; }
+  ob8(o, p++, (uint32_t)v);
+  return p;
+}
+
+// ---- V1 walker over LDS bytes ---------------------------------------------------------------------
+// Any anomaly (truncation, non-canonical varint, invalid UTF-8, a payload kind this path does not
+// verify) sets `bad`; the general path then reproduces yjs's exact result or error.
+struct Cur {
+  uint32_t p, e;
+  bool bad;
+};
+// Length of the lib0 varuint at the start of an 8-byte window (1..5; 6 = no terminator within 5 bytes).
+// Branch-free: v_ffbl on the stop bits with a sentinel.
+__device__ __forceinline__ uint32_t vu_nb(uint32_t lo, uint32_t hi) {
+  const uint32_t s_lo = ~lo & 0x80808080u;
+  const uint32_t s_hi = (~hi & 0x80u) | 0x8000u;
+  const uint32_t t = __builtin_ctzg(s_lo, 32 + __builtin_ctz(s_hi));
+  return (t >> 3) + 1;
+}
+// validity of a varuint of nb bytes: terminated within 5 bytes, inside the update, canonical (no
+// zero final group), and < 2^32 (lib0 readVarUint is u32)
+__device__ __forceinline__ bool vu_bad(uint32_t lo, uint32_t hi, uint32_t nb, uint32_t p, uint32_t e) {
+  const uint32_t last = nb <= 4 ? (lo >> (8 * nb - 8)) & 0xffu : hi & 0xffu;
+  return (nb > 5) | (p + nb > e) | ((nb > 1) & (last == 0)) | ((nb == 5) & ((hi & 0x70u) != 0));
+}
+// lib0 readVarUint (u32, canonical encodings only) from one unaligned 8-byte window
+__device__ __forceinline__ uint32_t rvu(Cur &c) {
+  const uint64_t x = ld8(c.p);
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const uint32_t nb = vu_nb(lo, hi);
+  const uint32_t v = (lo & 0x7fu) | ((lo >> 1) & 0x3f80u) | ((lo >> 2) & 0x1fc000u) | ((lo >> 3) & 0xfe00000u) | (hi << 28);
+  const uint32_t m = (uint32_t)((1ull << (7 * (nb < 5 ? nb : 5))) - 1);
+  c.bad |= vu_bad(lo, hi, nb, c.p, c.e);
+  c.p += nb < 6 ? nb : 0;
+  return v & m;
+}
+// skips a varuint whose value is not needed (origins, parent ids), with the same validity checks
+__device__ __forceinline__ void skvu(Cur &c) {
+  const uint64_t x = ld8(c.p);
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const uint32_t nb = vu_nb(lo, hi);
+  c.bad |= vu_bad(lo, hi, nb, c.p, c.e);
+  c.p += nb < 6 ? nb : 0;
+}
+__device__ __forceinline__ uint32_t rdb(Cur &c) {
+  c.bad |= c.p >= c.e;
+  return sm[c.p++];
+}
+__device__ __forceinline__ bool room(const Cur &c, uint32_t n) { return c.p <= c.e && n <= c.e - c.p; }
+// strict UTF-8 (lib0: decodeURIComponent(escape(..))) over the next n bytes; returns the UTF-16 length
+__device__ __forceinline__ uint32_t utf8_slow(uint32_t i, uint32_t e, bool &bad) {
+  uint32_t u = 0;
+  while (i < e) {
+    const uint32_t b = sm[i];
+    if (b < 0x80) { u++; i++; continue; }
+    uint32_t len, cp, mn;
+    if ((b & 0xE0) == 0xC0) { len = 2; cp = b & 0x1F; mn = 0x80; }
+    else if ((b & 0xF0) == 0xE0) { len = 3; cp = b & 0x0F; mn = 0x800; }
+    else if ((b & 0xF8) == 0xF0) { len = 4; cp = b & 0x07; mn = 0x10000; }
+    else { bad = true; return 0; }
+    if (i + len > e) { bad = true; return 0; }
+    for (uint32_t q = 1; q < len; q++) {
+      const uint32_t cb = sm[i + q];
+      if ((cb & 0xC0) != 0x80) { bad = true; return 0; }
+      cp = (cp << 6) | (cb & 0x3F);
+    }
+    if (cp < mn || cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF)) { bad = true; return 0; }
+    u += cp >= 0x10000 ? 2 : 1;
+    i += len;
+  }
+  return u;
+}
+__device__ __forceinline__ uint64_t mask_bytes(uint64_t x, uint32_t n) { return n >= 8 ? x : x & ((1ull << (8 * n)) - 1); }
+__device__ __forceinline__ uint32_t utf16_len(Cur &c, uint32_t n) {
+  if (!room(c, n)) { c.bad = true; return 0; }
+  uint64_t hi = 0;
+  for (uint32_t o = 0; o < n; o += 8) hi |= mask_bytes(ld8(c.p + o), n - o);
+  uint32_t u = n;
+  if (hi & 0x8080808080808080ull) u = utf8_slow(c.p, c.p + n, c.bad);
+  c.p += n;
+  return u;
+}
+__device__ __forceinline__ uint32_t rstr(Cur &c) {
+  const uint32_t n = rvu(c);
+  return c.bad ? 0 : utf16_len(c, n);
+}
+// SWAR: bytes of x equal to b / below 0x20 (exact per byte for the masked-in bytes)
+__device__ __forceinline__ uint64_t has_byte(uint64_t x, uint64_t b) {
+  const uint64_t y = x ^ (0x0101010101010101ull * b);
+  return (y - 0x0101010101010101ull) & ~y & 0x8080808080808080ull;
+}
+__device__ __forceinline__ uint64_t has_ctl(uint64_t x) {
+  return (x - 0x2020202020202020ull) & ~x & 0x8080808080808080ull;
+}
+// JSON text as yjs writes it for formats / embeds: true | false | null | "string without escapes"
+__device__ __forceinline__ void json_lit(Cur &c) {
+  const uint32_t n = rvu(c);
+  if (c.bad || !room(c, n)) { c.bad = true; return; }
+  const uint64_t w = ld8(c.p);
+  bool ok;
+  if (n == 4) ok = (uint32_t)w == 0x65757274u || (uint32_t)w == 0x6c6c756eu;  // "true" / "null"
+  else if (n == 5) ok = (w & 0xffffffffffull) == 0x65736c6166ull;            // "false"
+  else ok = false;
+  if (!ok && n >= 2 && (w & 0xff) == '"' && sm[c.p + n - 1] == '"') {
+    // interior bytes [1, n-1): no control characters, quotes or backslashes.  Bytes >= 0x80 are
+    // masked out of the control test (multi-byte UTF-8 is checked by utf16_len below).
+    uint64_t bad = 0;
+    for (uint32_t o = 1; o + 1 < n; o += 8) {
+      uint64_t x = mask_bytes(ld8(c.p + o), n - 1 - o);
+      const uint64_t pad = (n - 1 - o) >= 8 ? 0 : ~0ull << (8 * (n - 1 - o));
+      const uint64_t xs = x | (pad & 0x4040404040404040ull);  // padding bytes look like '@'
+      bad |= has_byte(xs, '"') | has_byte(xs, '\\') | (has_ctl(xs) & ~xs);
+    }
+    ok = bad == 0;
+  }
+  if (!ok) { c.bad = true; return; }
+  utf16_len(c, n);
+}
+// one scalar `any` value in the canonical form lib0 writeAny emits (objects/arrays: general path)
+__device__ __forceinline__ void any_scalar(Cur &c) {
+  const uint32_t tag = rdb(c);
+  switch (tag) {
+    case 127: case 126: case 121: case 120: return;  // undefined, null, false, true
+    case 125: {  // varInt: minimal, and <= 2^31-1 when positive (larger is written as a float)
+      uint32_t b = rdb(c);
+      uint64_t mag = b & 63;
+      const bool neg = b & 64;
+      int s = 6, nb = 1;
+      while ((b & 128) && !c.bad) {
+        b = rdb(c);
+        if (s > 34) { c.bad = true; return; }
+        mag |= (uint64_t)(b & 127) << s;
+        s += 7;
+        nb++;
+      }
+      if ((nb > 1 && b == 0) || (!neg && mag > 2147483647ull) || mag > 0xffffffffull) c.bad = true;
+      return;
+    }
+    case 124: {  // float32, not an integer <= 2^31-1 (those are written as varInt), not NaN
+      if (!room(c, 4)) { c.bad = true; return; }
+      const uint32_t u = __builtin_bswap32(ld4(c.p));
+      const float f = __uint_as_float(u);
+      if (f != f || (truncf(f) == f && (double)f <= 2147483647.0)) c.bad = true;
+      c.p += 4;
+      return;
+    }
+    case 123: {  // float64 that is neither a small integer nor float32-exact
+      if (!room(c, 8)) { c.bad = true; return; }
+      const uint64_t u = __builtin_bswap64(ld8(c.p));
+      const double x = __longlong_as_double((long long)u);
+      if (x == x && ((trunc(x) == x && x <= 2147483647.0) || (double)(float)x == x)) c.bad = true;
+      c.p += 8;
+      return;
+    }
+    case 119: rstr(c); return;
+    default: c.bad = true; return;
+  }
+}
+
+// The fields and content of one V1 Item after its info byte (UpdateDecoder.js:127-243 field readers,
+// Item.js:665-683 content refs; lazy reader of 13.5.16: parent kept raw, parentSub only without
+// origins).  Returns false (decline) for kinds this path does not verify; `len` = the Item's length.
+__device__ __forceinline__ bool item_body(Cur &c, uint32_t info, uint32_t &len) {
+  if (info & 0x80) { skvu(c); skvu(c); }
+  if (info & 0x40) { skvu(c); skvu(c); }
+  if ((info & 0xC0) == 0) {
+    const uint32_t pi = rvu(c);
+    if (pi > 1) return false;  // parentInfo re-encodes as 0/1
+    if (pi == 1) rstr(c);
+    else { skvu(c); skvu(c); }
+    if (info & 0x20) rstr(c);
+  }
+  len = 1;
+  switch (info & 31) {
+    case 1: len = rvu(c); break;                                      // ContentDeleted
+    case 3: { const uint32_t n = rvu(c); if (!room(c, n)) c.bad = true; else c.p += n; break; }  // Binary
+    case 4: len = rstr(c); break;                                     // ContentString
+    case 5: json_lit(c); break;                                       // ContentEmbed
+    case 6: rstr(c); json_lit(c); break;                              // ContentFormat
+    case 7: {                                                         // ContentType
+      const uint32_t t = rvu(c);
+      if (t > 6) return false;
+      if (t == 3 || t == 5) rstr(c);
+      break;
+    }
+    case 8:                                                           // ContentAny
+      len = rvu(c);
+      for (uint32_t i = 0; i < len && !c.bad; i++) any_scalar(c);
+      break;
+    default: return false;  // ContentJSON, ContentDoc, invalid refs
+  }
+  return !c.bad && len != 0;
+}
+
+}  // namespace fastc
+}  // namespace ymk
