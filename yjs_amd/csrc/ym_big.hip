@@ -395,7 +395,7 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
       p += b1r - b0r;
     }
     copy_span(p, ds0, ds1);
-    __threadfence_block();
+    __threadfence();  // the patches below overwrite bytes other lanes stored
     __syncthreads();
     // patches: each lies in the B span of exactly one section (sections are disjoint, in order)
     for (uint32_t i = lane; i < npatch; i += 64) {
