@@ -39,8 +39,8 @@ def test_merge_workload_matches_oracle(engine, name):
     bad = _compare(res, outs, status)
     assert not bad, bad[:10]
     st = engine.stats
-    if name in ("c2_v1", "c4_v1"):
-        assert st["docs_fast"] == st["docs"], st  # every C2/C4 V1 doc takes the LDS fast path
+    if name in ("c2_v1", "c4_v1", "c2_v2", "c4_v2"):
+        assert st["docs_fast"] == st["docs"], st  # every C2/C4 doc takes the LDS fast path (V1 and V2)
 
 
 @pytest.mark.parametrize("fmt", [1, 2])
@@ -53,6 +53,7 @@ def test_sv_and_diff_workload_matches_oracle(engine, fmt):
     outs, st, _ = O.batch("sv", fmt, a2, o2, d2, nthreads=8)
     bad = _compare(engine.run_host("sv", fmt, a2, o2, d2), outs, st)
     assert not bad, bad[:10]
+    assert engine.stats["docs_fast"] == engine.stats["docs"], engine.stats  # streamed wave walker
     svs = []
     for i, m in enumerate(merged):
         svs.extend(random_state_vectors(outs[i], 1, seed=i))
@@ -60,6 +61,19 @@ def test_sv_and_diff_workload_matches_oracle(engine, fmt):
     outs2, st2, _ = O.batch("diff", fmt, a2, o2, d2, sva, svo, nthreads=8)
     bad = _compare(engine.run_host("diff", fmt, a2, o2, d2, sva, svo), outs2, st2)
     assert not bad, bad[:10]
+    assert engine.stats["docs_fast"] == engine.stats["docs"], engine.stats
+
+
+@pytest.mark.parametrize("fmt", [1, 2])
+def test_c3_sv_matches_oracle(engine, fmt):
+    arena, upd_off, doc_upd = load_ymb(f"c3_v{fmt}")
+    from yjs_amd import pack_docs
+    upd = arena.tobytes()
+    a2, o2, d2 = pack_docs([[upd] for _ in range(4)])
+    outs, st, _ = O.batch("sv", fmt, a2, o2, d2)
+    bad = _compare(engine.run_host("sv", fmt, a2, o2, d2), outs, st)
+    assert not bad, bad[:10]
+    assert engine.stats["docs_fast"] == engine.stats["docs"], engine.stats
 
 
 @pytest.mark.parametrize("fmt", [1, 2])
@@ -75,3 +89,4 @@ def test_c3_diff_random_svs(engine, fmt):
     outs, st, _ = O.batch("diff", fmt, a2, o2, d2, sva, svo, nthreads=8)
     bad = _compare(engine.run_host("diff", fmt, a2, o2, d2, sva, svo), outs, st)
     assert not bad, bad[:10]
+    assert engine.stats["docs_fast"] == engine.stats["docs"], engine.stats

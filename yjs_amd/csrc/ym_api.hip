@@ -20,6 +20,7 @@ namespace ymk {
 __global__ void k_general_ws(GeneralJob j, uint64_t *ws_size);
 __global__ void k_general(GeneralJob j, int pass);
 int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st);  // ym_fast.hip
+int fast2_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st); // ym_fast2.hip
 int big_launch(uint32_t op, const GeneralJob &j, hipStream_t st);                    // ym_big.hip
 int big2_launch(uint32_t op, const GeneralJob &j, hipStream_t st);                   // ym_big2.hip
 }  // namespace ymk
@@ -245,6 +246,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   // (1) fast path over every document; appends the ones it declines to list_a
   HIPCHK(hipEventRecord(S->evf0, st));
   int fr = fast_launch(op, j, b->n_upd, st);     // V1 merge: LDS fast path
+  if (fr == 0) fr = fast2_launch(op, j, b->n_upd, st);  // V2 merge: LDS fast path
   if (fr == 0) fr = big_launch(op, j, st);         // V1 diff / state vector: streamed wave walker
   if (fr == 0) fr = big2_launch(op, j, st);        // V2 diff / state vector: streamed wave walker
   if (fr < 0) return fr;

@@ -1,0 +1,912 @@
+// ym_fast2.hip -- LDS fast path for batched mergeUpdatesV2: one 64-lane wave per document.
+//
+// The V1 fast path (ym_fast.hip) over the V2 layout (UpdateDecoder.js:245-392, UpdateEncoder.js:229-408).
+// It takes the same "simple" documents (every update's structs increasing in (client desc, clock asc),
+// no overlap, no GC/Skip inputs, canonical payloads) plus: ASCII string columns.  For them 13.5.16's
+// mergeUpdatesV2 (ds@39007) = all structs sorted by (client desc, clock asc), Skips at clock gaps,
+// parts per client run, each struct re-encoded into the nine columns; delete sets united per client,
+// clients in first-appearance order.
+//
+// Per document (one wave, ~12.4 KB of LDS):
+//   1. stage the bytes;  2. one lane per update: V2 header, per-lane lib0 RLE column decoders, struct
+//   records (values, not bytes) + delete ranges into LDS;  3. rank sort;  4. layout by DPP scans;
+//   5. every struct's column entries are scattered into per-column value arrays (counts scanned per
+//   column), then each column is RLE-encoded wave-parallel: run starts/ends by neighbour compares,
+//   run lengths by a running-max scan of start positions, run bytes by a prefix sum (UintOptRle,
+//   IntDiffOptRle, Rle<u8>, StringEncoder);  6. rest stream (part headers, Skip lengths, verbatim
+//   any/binary payloads) and the V2 delete set (clock deltas, len - 1).
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+
+#include "ym_fast_common.h"
+#include "ym_kernels.h"
+
+namespace ymk {
+namespace fastv2 {
+using namespace fastc;
+
+constexpr uint32_t IN = 3584, UPD = 128, E = 2, REC = 64 * E, DSN = 64 * E;
+
+constexpr uint32_t L_IN = 0;                       // u8[IN + 16]
+constexpr uint32_t L_UOFF = IN + 16;               // u16[UPD + 1]
+constexpr uint32_t L_MISC = L_UOFF + 272;          // u32[16]
+constexpr uint32_t R = L_MISC + 64;
+// struct records (walk slots, then rank order in place)
+constexpr uint32_t L_RKEY = R;                     // u64 (~client << 32 | clock)
+constexpr uint32_t L_RLEN = L_RKEY + 8 * REC;      // u32
+constexpr uint32_t L_RAUX = L_RLEN + 4 * REC;      // u32 info | pi << 8 | typeRef << 16
+constexpr uint32_t L_RF = L_RAUX + 4 * REC;        // u32[4]: origin (or parent id) client, clock; right origin client, clock
+constexpr uint32_t L_RS = L_RF + 16 * REC;         // u32[3]: strings (LDS offset | n << 16): ykey, parentSub, content/key/name
+constexpr uint32_t L_RSP = L_RS + 12 * REC;        // u32 rest span (LDS offset | n << 16)
+constexpr uint32_t L_RSLOT = L_RSP + 4 * REC;      // u8
+constexpr uint32_t L_RCEND = L_RSLOT + REC;
+// delete ranges
+constexpr uint32_t L_DKEY = L_RCEND;               // u64 (client << 32 | clock)
+constexpr uint32_t L_DLEN = L_DKEY + 8 * DSN;      // u32
+constexpr uint32_t L_DSEQ = L_DLEN + 4 * DSN;      // u16
+constexpr uint32_t L_DSLOT = L_DSEQ + 2 * DSN;     // u8
+constexpr uint32_t L_PFIRST = L_DSLOT + DSN;       // u16[REC]
+constexpr uint32_t L_PLAST = L_PFIRST + 2 * REC;   // u16[REC]
+constexpr uint32_t L_END = L_PLAST + 2 * REC;
+constexpr uint32_t LDS_BYTES = L_END;
+// phase 5: per-column value arrays over the record region (the records are held in registers)
+constexpr uint32_t V_CL = R;                       // u32[3 * REC]
+constexpr uint32_t V_LC = V_CL + 12 * REC;         // u32[REC]
+constexpr uint32_t V_RC = V_LC + 4 * REC;          // u32[REC]
+constexpr uint32_t V_LN = V_RC + 4 * REC;          // u32[REC]
+constexpr uint32_t V_ST = V_LN + 4 * REC;          // u32[3 * REC] (offset | n << 16)
+constexpr uint32_t V_TR = V_ST + 12 * REC;         // u8[REC]
+constexpr uint32_t V_IN = V_TR + REC;              // u8[2 * REC]
+constexpr uint32_t V_PI = V_IN + 2 * REC;          // u8[REC]
+constexpr uint32_t V_END = V_PI + REC;
+static_assert(V_END <= L_RCEND, "column arrays fit the record region");
+// phase 6 (delete set) over the record region again
+constexpr uint32_t L_QCLK = R, L_QEND = L_QCLK + 4 * DSN, L_QGRP = L_QEND + 4 * DSN, L_QPRE = L_QGRP + DSN;
+constexpr uint32_t L_GFIRST = L_QPRE + 272, L_GCLI = L_GFIRST + 272, L_GB2 = L_GCLI + 4 * DSN, L_GBYR = L_GB2 + 4 * DSN;
+constexpr uint32_t L_GMIN = L_PFIRST;
+static_assert(L_GBYR + 2 * DSN <= L_RCEND, "delete-set arrays fit the record region");
+
+// ---- per-lane lib0 decoders over LDS (canonical inputs only; anything else declines) -------------
+// readVarInt: sign (incl. -0) + u32 magnitude, at most 5 bytes
+__device__ __forceinline__ uint32_t rvi(Cur &c, bool &neg) {
+  const uint64_t x = ld8(c.p);
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const uint32_t nb = vu_nb(lo, hi);
+  neg = (lo & 0x40) != 0;
+  uint32_t m = (lo & 0x3fu) | ((lo >> 2) & 0x1fc0u) | ((lo >> 3) & 0xfe000u) | ((lo >> 4) & 0x7f00000u) | ((hi & 0x7fu) << 27);
+  const uint32_t bits = 6 + 7 * (nb - 1);
+  if (nb < 5) m &= (1u << bits) - 1u;
+  c.bad |= (nb > 5) | (c.p + nb > c.e) | ((nb == 5) & ((hi & 0x7fu) > 0x1fu));
+  c.p += nb < 6 ? nb : 0;
+  return m;
+}
+struct RleD { Cur c; uint32_t s, n; };              // RleDecoder<u8>
+struct UoptD { Cur c; uint32_t s, n; };             // UintOptRleDecoder
+struct IdifD { Cur c; uint32_t s, n; int32_t d; };  // IntDiffOptRleDecoder
+__device__ __forceinline__ uint32_t rd_rle(RleD &r) {
+  if (r.n == 0) {
+    r.s = rdb(r.c);
+    r.n = r.c.p < r.c.e ? rvu(r.c) + 1 : 0xffffffffu;  // the final run never ends
+  }
+  if (r.n != 0xffffffffu) r.n--;
+  return r.s;
+}
+__device__ __forceinline__ uint32_t rd_uopt(UoptD &r) {
+  if (r.n == 0) {
+    bool neg;
+    r.s = rvi(r.c, neg);
+    r.n = neg ? rvu(r.c) + 2 : 1;
+  }
+  r.n--;
+  return r.s;
+}
+__device__ __forceinline__ uint32_t rd_idif(IdifD &r) {
+  if (r.n == 0) {
+    bool neg;
+    const uint32_t m = rvi(r.c, neg);
+    const int32_t t = (int32_t)(neg ? 0u - m : m);  // ToInt32(sign * mag)
+    r.d = t >> 1;
+    r.n = (t & 1) ? rvu(r.c) + 2 : 1;
+  }
+  const int64_t v = (int64_t)r.s + r.d;
+  r.c.bad |= v < 0 || v > 0xffffffffll;  // clocks: this path keeps them u32
+  r.s = (uint32_t)v;
+  r.n--;
+  return r.s;
+}
+
+__device__ __forceinline__ void decline(const GeneralJob &j, uint32_t d) {
+  j.status[d] = ST_PENDING;
+  j.pend_list[atomicAdd(j.pend_count, 1u)] = d;
+}
+
+// Walks one V2 update (lane-private decoders) and appends struct records and delete ranges.
+__device__ bool walk_v2(uint32_t u) {
+  const uint32_t p0 = at<uint16_t>(L_UOFF + 2 * u), p1 = at<uint16_t>(L_UOFF + 2 * u + 2);
+  Cur h = {p0, p1, false};
+  rvu(h);  // feature flag
+  Cur col[9];
+#pragma unroll
+  for (uint32_t k = 0; k < 9; k++) {
+    const uint32_t n = rvu(h);
+    if (!room(h, n)) return false;
+    col[k] = Cur{h.p, h.p + n, false};
+    h.p += n;
+  }
+  if (h.bad) return false;
+  // StringDecoder: varString(body) then the UintOptRle of UTF-16 lengths; ASCII bodies only
+  const uint32_t sn = rvu(col[5]);
+  if (col[5].bad || !room(col[5], sn)) return false;
+  const uint32_t sb = col[5].p;
+  {
+    uint64_t hi = 0;
+    for (uint32_t o = 0; o < sn; o += 8) hi |= mask_bytes(ld8(sb + o), sn - o);
+    if (hi & 0x8080808080808080ull) return false;
+  }
+  col[5].p += sn;
+  IdifD kc = {col[0], 0, 0, 0};
+  UoptD cl = {col[1], 0, 0};
+  IdifD lc = {col[2], 0, 0, 0}, rc = {col[3], 0, 0, 0};
+  RleD in = {col[4], 0, 0};
+  UoptD sl = {col[5], 0, 0};
+  RleD pi_ = {col[6], 0, 0};
+  UoptD tr = {col[7], 0, 0}, ln = {col[8], 0, 0};
+  uint32_t spos = 0, keys = 0;
+  Cur c = h;  // rest stream
+  bool bad = false;
+  auto rstr = [&]() -> uint32_t {  // StringDecoder.read(): (LDS offset | n << 16)
+    const uint32_t n = rd_uopt(sl);
+    bad |= spos + n > sn || n > 0xffff;
+    const uint32_t v = (sb + spos) | (n << 16);
+    spos += n;
+    return v;
+  };
+  const uint32_t nclients = rvu(c);
+  uint64_t prev = 0;
+  bool have_prev = false;
+  for (uint32_t ci = 0; ci < nclients && !c.bad && !bad; ci++) {
+    const uint32_t nstructs = rvu(c);
+    const uint32_t client = rd_uopt(cl);
+    uint32_t clock = rvu(c);
+    for (uint32_t si = 0; si < nstructs && !c.bad && !bad; si++) {
+      const uint32_t info = rd_rle(in);
+      if (info == 10 || (info & 31) == 0 || info > 255) return false;  // Skip / GC inputs: general path
+      uint32_t f0 = 0, f1 = 0, f2 = 0, f3 = 0, s0 = 0, s1 = 0, s2 = 0, sp = 0, pi = 0, t = 0;
+      if (info & 0x80) { f0 = rd_uopt(cl); f1 = rd_idif(lc); }
+      if (info & 0x40) { f2 = rd_uopt(cl); f3 = rd_idif(rc); }
+      if ((info & 0xC0) == 0) {
+        pi = rd_rle(pi_) == 1 ? 1 : 0;  // readParentInfo() === 1
+        if (pi) s0 = rstr();
+        else { f0 = rd_uopt(cl); f1 = rd_idif(lc); }
+        if (info & 0x20) s1 = rstr();
+      }
+      uint32_t len = 1;
+      switch (info & 31) {
+        case 1: len = rd_uopt(ln); break;                                  // ContentDeleted
+        case 3: {                                                          // ContentBinary (rest)
+          const uint32_t a = c.p, n = rvu(c);
+          if (!room(c, n)) return false;
+          c.p += n;
+          sp = a | ((c.p - a) << 16);
+          break;
+        }
+        case 4: s2 = rstr(); len = s2 >> 16; break;                        // ContentString
+        case 5: case 6: {                                                  // Embed / Format (+ key)
+          if ((info & 31) == 6) s2 = rstr();
+          const uint32_t a = c.p;
+          any_scalar(c);
+          sp = a | ((c.p - a) << 16);
+          break;
+        }
+        case 7:                                                            // ContentType
+          t = rd_uopt(tr);
+          if (t > 6) return false;
+          if (t == 3 || t == 5) {  // readKey: a cached key (keyClock < keys read) reads no string
+            if (rd_idif(kc) < keys) return false;
+            keys++;
+            s2 = rstr();
+          }
+          break;
+        case 8: {                                                          // ContentAny
+          len = rd_uopt(ln);
+          const uint32_t a = c.p;
+          for (uint32_t i = 0; i < len && !c.bad; i++) any_scalar(c);
+          sp = a | ((c.p - a) << 16);
+          break;
+        }
+        default: return false;  // ContentJSON, ContentDoc, invalid refs
+      }
+      if (c.bad || bad || len == 0 || (sp >> 16) > 0x7fff) return false;
+      if ((uint64_t)clock + len > 0xffffffffull) return false;
+      const uint64_t key = ((uint64_t)(~client) << 32) | clock;
+      if (have_prev && key <= prev) return false;  // each update must already be in merge order
+      prev = key + len - 1;
+      have_prev = true;
+      const uint32_t q = atomicAdd(&at<uint32_t>(L_MISC), 1u);
+      if (q >= REC) return false;
+      at<uint64_t>(L_RKEY + 8 * q) = key;
+      at<uint32_t>(L_RLEN + 4 * q) = len;
+      at<uint32_t>(L_RAUX + 4 * q) = info | (pi << 8) | (t << 16);
+      at<uint4>(L_RF + 16 * q) = make_uint4(f0, f1, f2, f3);
+      at<uint32_t>(L_RS + 12 * q) = s0;
+      at<uint32_t>(L_RS + 12 * q + 4) = s1;
+      at<uint32_t>(L_RS + 12 * q + 8) = s2;
+      at<uint32_t>(L_RSP + 4 * q) = sp;
+      clock += len;
+    }
+  }
+  bad |= c.bad | cl.c.bad | lc.c.bad | rc.c.bad | in.c.bad | sl.c.bad | pi_.c.bad | tr.c.bad | ln.c.bad | kc.c.bad;
+  if (bad) return false;
+  // V2 delete set (rest): per client, clock deltas against dsCurr and len - 1 (UpdateDecoder.js:258-267)
+  const uint32_t ndc = rvu(c);
+  uint32_t pos = 0;
+  for (uint32_t i = 0; i < ndc && !c.bad; i++) {
+    const uint32_t client = rvu(c);
+    const uint32_t m = rvu(c);
+    uint64_t cur = 0;
+    for (uint32_t q = 0; q < m && !c.bad; q++, pos++) {
+      const uint64_t clock = cur + rvu(c);
+      const uint64_t len = (uint64_t)rvu(c) + 1;
+      cur = clock + len;
+      if (c.bad || pos > 255 || cur > 0xffffffffull) return false;
+      const uint32_t x = atomicAdd(&at<uint32_t>(L_MISC + 4), 1u);
+      if (x >= DSN) return false;
+      at<uint64_t>(L_DKEY + 8 * x) = ((uint64_t)client << 32) | clock;
+      at<uint32_t>(L_DLEN + 4 * x) = (uint32_t)len;
+      at<uint16_t>(L_DSEQ + 2 * x) = (uint16_t)((u << 8) | pos);
+    }
+  }
+  return !c.bad;
+}
+
+// ---- wave-parallel RLE column encoders ------------------------------------------------------------
+// lib0 writeVarInt size for a magnitude (sign lives in the first byte)
+__device__ __forceinline__ uint32_t vszi(uint32_t m) { return m < 64 ? 1 : 1 + vsz(m >> 6); }
+__device__ __forceinline__ uint32_t put_vi(Slot o, uint32_t p, bool neg, uint32_t m) {
+  ob8(o, p++, (m > 63 ? 0x80 : 0) | (neg ? 0x40 : 0) | (m & 63));
+  m >>= 6;
+  while (m > 0) { ob8(o, p++, (m > 127 ? 0x80 : 0) | (m & 127)); m >>= 7; }
+  return p;
+}
+// inclusive running max over lanes (u32)
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+  uint32_t y;
+  y = YM_DPP(x, 0x111, 0xf); x = y > x ? y : x;
+  y = YM_DPP(x, 0x112, 0xf); x = y > x ? y : x;
+  y = YM_DPP(x, 0x114, 0xf); x = y > x ? y : x;
+  y = YM_DPP(x, 0x118, 0xf); x = y > x ? y : x;
+  y = YM_DPP(x, 0x142, 0xa); x = y > x ? y : x;
+  y = YM_DPP(x, 0x143, 0xc); x = y > x ? y : x;
+  return x;
+}
+enum { K_UOPT = 0, K_IDIF = 1, K_RLE = 2 };
+constexpr uint32_t CPL = 6;  // column elements per lane (3 * REC / 64)
+// Encodes the n values get(i) (i < n <= 64 * CPL) with the lib0 encoder of kind K.  Returns the byte
+// size; writes the bytes at o[base ..] when `wr`.  Runs are found from neighbour compares (diffs for
+// IntDiffOptRle), run lengths from a running max of run-start positions, run bytes by a prefix sum
+// over run ends (each run end writes its run).  `bad` is set for diffs outside (-2^30, 2^30).
+template <int K, class Get>
+__device__ uint32_t col_encode(Get get, uint32_t n, bool wr, Slot o, uint32_t base, bool &bad) {
+  const uint32_t lane = threadIdx.x;
+  const uint32_t i0 = lane * CPL;
+  int64_t val[CPL + 2];  // values (or diffs) of elements i0 - 1 .. i0 + CPL
+#pragma unroll
+  for (uint32_t t = 0; t < CPL + 2; t++) {
+    const int64_t i = (int64_t)i0 + t - 1;
+    int64_t v = 0;
+    if (i >= 0 && i < (int64_t)n) {
+      v = (int64_t)get((uint32_t)i);
+      if (K == K_IDIF) v -= i > 0 ? (int64_t)get((uint32_t)i - 1) : 0;
+    }
+    val[t] = v;
+  }
+  uint32_t sp_local = 0, last_sp = 0;
+  uint32_t bytes_lane = 0;
+  uint32_t rb[CPL];
+  // pass 1: start positions (running max), run ends, run bytes
+  bool st[CPL];
+#pragma unroll
+  for (uint32_t t = 0; t < CPL; t++) {
+    const uint32_t i = i0 + t;
+    st[t] = i < n && (i == 0 || val[t + 1] != val[t]);
+    if (st[t]) last_sp = i;
+  }
+  const uint32_t carry = YM_DPP(wave_incl_max(last_sp), 0x138, 0xf);  // wave_shr:1 -> exclusive
+  sp_local = carry;
+#pragma unroll
+  for (uint32_t t = 0; t < CPL; t++) {
+    const uint32_t i = i0 + t;
+    rb[t] = 0;
+    if (i >= n) continue;
+    if (st[t]) sp_local = i;
+    const bool end = i + 1 == n || val[t + 2] != val[t + 1];
+    if (!end) continue;
+    const uint32_t cnt = i - sp_local + 1;
+    const int64_t v = val[t + 1];
+    if (K == K_UOPT) {
+      rb[t] = vszi((uint32_t)v) + (cnt > 1 ? vsz(cnt - 2) : 0);
+    } else if (K == K_IDIF) {
+      bad |= v <= -(1ll << 30) || v >= (1ll << 30);
+      const int32_t x = (int32_t)((uint32_t)(int32_t)v << 1) | (cnt > 1 ? 1 : 0);
+      rb[t] = vszi(x < 0 ? 0u - (uint32_t)x : (uint32_t)x) + (cnt > 1 ? vsz(cnt - 2) : 0);
+    } else {
+      rb[t] = 1 + (i + 1 == n ? 0 : vsz(cnt - 1));  // Rle<u8>: the final run's count is never written
+    }
+    bytes_lane += rb[t];
+  }
+  const uint32_t incl = wave_incl_add(bytes_lane);
+  const uint32_t total = lane_read(incl, 63);
+  if (wr) {
+    uint32_t p = base + incl - bytes_lane;
+    uint32_t sp2 = carry;
+#pragma unroll
+    for (uint32_t t = 0; t < CPL; t++) {
+      const uint32_t i = i0 + t;
+      if (i >= n) continue;
+      if (st[t]) sp2 = i;
+      if (rb[t] == 0) continue;
+      const uint32_t cnt = i - sp2 + 1;
+      const int64_t v = val[t + 1];
+      uint32_t q = p;
+      if (K == K_UOPT) {
+        q = put_vi(o, q, cnt > 1, (uint32_t)v);  // count==1 ? v : -v (-0 for v == 0)
+        if (cnt > 1) q = put_vu(o, q, cnt - 2);
+      } else if (K == K_IDIF) {
+        const int32_t x = (int32_t)((uint32_t)(int32_t)v << 1) | (cnt > 1 ? 1 : 0);
+        q = put_vi(o, q, x < 0, x < 0 ? 0u - (uint32_t)x : (uint32_t)x);
+        if (cnt > 1) q = put_vu(o, q, cnt - 2);
+      } else {
+        ob8(o, q++, (uint32_t)v);
+        if (i + 1 != n) q = put_vu(o, q, cnt - 1);
+      }
+      p += rb[t];
+    }
+  }
+  return total;
+}
+
+#define YM2_DECLINE()                    \
+  {                                      \
+    if (lane == 0) decline(j, d);        \
+    __syncthreads();                     \
+    continue;                            \
+  }
+
+__global__ void __launch_bounds__(64) k_fast_merge_v2(GeneralJob j) {
+  const uint32_t lane = threadIdx.x;
+  const uint64_t arena0 = j.upd_off[0];
+  for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
+    const uint32_t u0 = j.doc_upd[d], k = j.doc_upd[d + 1] - u0;
+    const uint64_t b0 = j.upd_off[u0], bytes = j.upd_off[u0 + k] - b0;
+    if (k <= 1 || k > UPD || bytes > IN) {
+      if (lane == 0) decline(j, d);
+      continue;
+    }
+    // ---- 1. stage
+    const uint32_t base = (uint32_t)(b0 & 15);
+    {
+      const uint4 *src = reinterpret_cast<const uint4 *>(j.A + (b0 - base));
+      const uint32_t nvec = (uint32_t)((base + bytes + 15) >> 4);
+      for (uint32_t v = lane; v < nvec; v += 64) at<uint4>(L_IN + 16 * v) = src[v];
+    }
+    for (uint32_t i = lane; i <= k; i += 64) at<uint16_t>(L_UOFF + 2 * i) = (uint16_t)(j.upd_off[u0 + i] - b0 + base);
+    if (lane < 2) at<uint32_t>(L_MISC + 4 * lane) = 0;
+    __syncthreads();
+    // ---- 2. walk
+    bool ok = true;
+#pragma unroll 1
+    for (uint32_t u = lane; u < k; u += 64) ok &= walk_v2(u);
+    if (__any(!ok)) YM2_DECLINE()
+    __syncthreads();
+    const uint32_t nrec = at<uint32_t>(L_MISC), nds = at<uint32_t>(L_MISC + 4);
+    if (nrec == 0 || nrec > REC || nds > DSN) YM2_DECLINE()
+    if (lane == 0) {
+      if (nrec & 1) at<uint64_t>(L_RKEY + 8 * nrec) = ~0ull;
+      if (nds & 1) at<uint64_t>(L_DKEY + 8 * nds) = ~0ull;
+    }
+    __syncthreads();
+    // ---- 3. struct rank sort (records move to rank order; the slot array detects duplicates)
+    {
+      uint64_t rk[E];
+      uint32_t rr[E];
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) rk[s] = lane + 64 * s < nrec ? at<uint64_t>(L_RKEY + 8 * (lane + 64 * s)) : ~0ull;
+      rank_le(L_RKEY, nrec, rk, rr);
+      uint32_t rl[E], ra[E], s0[E], s1[E], s2[E], sp[E];
+      uint4 rf[E];
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint32_t i = lane + 64 * s;
+        const bool v = i < nrec;
+        rl[s] = v ? at<uint32_t>(L_RLEN + 4 * i) : 0;
+        ra[s] = v ? at<uint32_t>(L_RAUX + 4 * i) : 0;
+        rf[s] = v ? at<uint4>(L_RF + 16 * i) : make_uint4(0, 0, 0, 0);
+        s0[s] = v ? at<uint32_t>(L_RS + 12 * i) : 0;
+        s1[s] = v ? at<uint32_t>(L_RS + 12 * i + 4) : 0;
+        s2[s] = v ? at<uint32_t>(L_RS + 12 * i + 8) : 0;
+        sp[s] = v ? at<uint32_t>(L_RSP + 4 * i) : 0;
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint32_t i = lane + 64 * s;
+        if (i < nrec) {
+          const uint32_t r = rr[s];
+          at<uint64_t>(L_RKEY + 8 * r) = rk[s];
+          at<uint32_t>(L_RLEN + 4 * r) = rl[s];
+          at<uint32_t>(L_RAUX + 4 * r) = ra[s];
+          at<uint4>(L_RF + 16 * r) = rf[s];
+          at<uint32_t>(L_RS + 12 * r) = s0[s];
+          at<uint32_t>(L_RS + 12 * r + 4) = s1[s];
+          at<uint32_t>(L_RS + 12 * r + 8) = s2[s];
+          at<uint32_t>(L_RSP + 4 * r) = sp[s];
+          at<uint8_t>(L_RSLOT + r) = (uint8_t)i;
+        }
+      }
+      __syncthreads();
+      bool dup = false;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint32_t i = lane + 64 * s;
+        if (i < nrec) dup |= at<uint8_t>(L_RSLOT + rr[s]) != i;
+      }
+      if (__any(dup)) YM2_DECLINE()
+    }
+    // ---- 4. layout over rank order; lane owns positions r = E*lane + s
+    uint64_t sk[E];
+    uint32_t sl_[E], sa[E], s0[E], s1[E], s2[E], ssp[E], pstart[E], gapv[E], runu[E];
+    uint4 sf[E];
+    uint32_t pu[E], nparts;
+    {
+      bool bad = false;
+      uint32_t plastf[E], units[E];
+      const uint32_t r0 = E * lane;
+      uint64_t kp = r0 > 0 && r0 - 1 < nrec ? at<uint64_t>(L_RKEY + 8 * (r0 - 1)) : ~0ull;
+      uint32_t lp = r0 > 0 && r0 - 1 < nrec ? at<uint32_t>(L_RLEN + 4 * (r0 - 1)) : 0;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint32_t r = r0 + s;
+        const bool v = r < nrec;
+        sk[s] = v ? at<uint64_t>(L_RKEY + 8 * r) : ~0ull;
+        sl_[s] = v ? at<uint32_t>(L_RLEN + 4 * r) : 0;
+        sa[s] = v ? at<uint32_t>(L_RAUX + 4 * r) : 0;
+        sf[s] = v ? at<uint4>(L_RF + 16 * r) : make_uint4(0, 0, 0, 0);
+        s0[s] = v ? at<uint32_t>(L_RS + 12 * r) : 0;
+        s1[s] = v ? at<uint32_t>(L_RS + 12 * r + 4) : 0;
+        s2[s] = v ? at<uint32_t>(L_RS + 12 * r + 8) : 0;
+        ssp[s] = v ? at<uint32_t>(L_RSP + 4 * r) : 0;
+        const uint64_t kn = r + 1 < nrec ? at<uint64_t>(L_RKEY + 8 * (r + 1)) : ~0ull;
+        const bool same = v && r > 0 && (kp >> 32) == (sk[s] >> 32);
+        const uint64_t pend = (kp & 0xffffffffull) + lp;
+        const uint64_t cl = sk[s] & 0xffffffffull;
+        bad |= same && pend > cl;
+        gapv[s] = same && pend < cl ? (uint32_t)(cl - pend) : 0;
+        units[s] = v ? 1 + (gapv[s] != 0) : 0;
+        pstart[s] = v && !same;
+        plastf[s] = v && (r + 1 >= nrec || (kn >> 32) != (sk[s] >> 32));
+        kp = sk[s];
+        lp = sl_[s];
+      }
+      if (__any(bad)) YM2_DECLINE()
+      uint32_t pu_lane = 0;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) pu_lane += (pstart[s] << 16) | units[s];
+      const uint32_t incl = wave_incl_add(pu_lane);
+      nparts = lane_read(incl, 63) >> 16;
+      uint32_t run = incl - pu_lane;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        pu[s] = run;
+        run += (pstart[s] << 16) | units[s];
+        const uint32_t pid = (run >> 16) - 1;
+        if (pstart[s]) at<uint16_t>(L_PFIRST + 2 * pid) = (uint16_t)(pu[s] & 0xffff);
+        if (plastf[s]) at<uint16_t>(L_PLAST + 2 * pid) = (uint16_t)(run & 0xffff);
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++)
+        runu[s] = pstart[s] ? at<uint16_t>(L_PLAST + 2 * (pu[s] >> 16)) - at<uint16_t>(L_PFIRST + 2 * (pu[s] >> 16)) : 0;
+    }
+    // ---- 5. columns.  Entry counts per struct (Item.write / LazyStructWriter routing, V2)
+    uint32_t cA[E], cB[E], cC[E];  // (cl | lc << 10 | rc << 20), (in | pi << 10 | st << 20), (kc | tr << 10 | ln << 20)
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++) {
+      const bool v = E * lane + s < nrec;
+      const uint32_t info = sa[s] & 0xff, pi = (sa[s] >> 8) & 0xff, t = sa[s] >> 16, ref = info & 31;
+      const bool ho = info & 0x80, hr = info & 0x40, noo = (info & 0xC0) == 0;
+      const bool key = ref == 6 || (ref == 7 && (t == 3 || t == 5));
+      const uint32_t ncl = pstart[s] + ho + hr + (noo && !pi);
+      const uint32_t nlc = ho || (noo && !pi);
+      const uint32_t nin = 1 + (gapv[s] != 0);
+      const uint32_t nst = (noo && pi) + (noo && (info & 0x20)) + (ref == 4 || key);
+      cA[s] = v ? ncl | (nlc << 10) | ((uint32_t)hr << 20) : 0;
+      cB[s] = v ? nin | ((uint32_t)noo << 10) | (nst << 20) : 0;
+      cC[s] = v ? (uint32_t)key | ((uint32_t)(ref == 7) << 10) | ((uint32_t)(ref == 1 || ref == 8) << 20) : 0;
+    }
+    uint32_t oA[E], oB[E], oC[E], nA, nB, nC;
+    {
+      uint32_t ta = cA[0] + cA[1], tb = cB[0] + cB[1], tc = cC[0] + cC[1];
+      const uint32_t ia = wave_incl_add(ta), ib = wave_incl_add(tb), ic = wave_incl_add(tc);
+      nA = lane_read(ia, 63); nB = lane_read(ib, 63); nC = lane_read(ic, 63);
+      oA[0] = ia - ta; oB[0] = ib - tb; oC[0] = ic - tc;
+      oA[1] = oA[0] + cA[0]; oB[1] = oB[0] + cB[0]; oC[1] = oC[0] + cC[0];
+    }
+    __syncthreads();  // the record arrays are dead (everything is in registers): the value arrays reuse R
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++) {
+      if (E * lane + s >= nrec) break;
+      const uint32_t info = sa[s] & 0xff, pi = (sa[s] >> 8) & 0xff, t = sa[s] >> 16, ref = info & 31;
+      const bool ho = info & 0x80, hr = info & 0x40, noo = (info & 0xC0) == 0;
+      uint32_t icl = oA[s] & 0x3ff, ilc = (oA[s] >> 10) & 0x3ff, irc = oA[s] >> 20;
+      uint32_t iin = oB[s] & 0x3ff, ipi = (oB[s] >> 10) & 0x3ff, ist = oB[s] >> 20;
+      uint32_t ikc = oC[s] & 0x3ff, itr = (oC[s] >> 10) & 0x3ff, iln = oC[s] >> 20;
+      if (pstart[s]) at<uint32_t>(V_CL + 4 * icl++) = ~(uint32_t)(sk[s] >> 32);  // writeClient at a part start
+      if (gapv[s]) at<uint8_t>(V_IN + iin++) = 10;                               // Skip
+      at<uint8_t>(V_IN + iin) = (uint8_t)(ho || hr ? info & ~0x20u : info);       // 0x20 only without origins
+      if (ho) { at<uint32_t>(V_CL + 4 * icl++) = sf[s].x; at<uint32_t>(V_LC + 4 * ilc) = sf[s].y; }
+      if (hr) { at<uint32_t>(V_CL + 4 * icl++) = sf[s].z; at<uint32_t>(V_RC + 4 * irc) = sf[s].w; }
+      if (noo) {
+        at<uint8_t>(V_PI + ipi) = (uint8_t)pi;
+        if (pi) at<uint32_t>(V_ST + 4 * ist++) = s0[s];
+        else { at<uint32_t>(V_CL + 4 * icl++) = sf[s].x; at<uint32_t>(V_LC + 4 * ilc) = sf[s].y; }
+        if (info & 0x20) at<uint32_t>(V_ST + 4 * ist++) = s1[s];
+      }
+      if (ref == 4 || ref == 6 || (ref == 7 && (t == 3 || t == 5))) at<uint32_t>(V_ST + 4 * ist) = s2[s];
+      if (ref == 6 || (ref == 7 && (t == 3 || t == 5))) (void)ikc;  // keyClock values are the entry index
+      if (ref == 7) at<uint8_t>(V_TR + itr) = (uint8_t)t;
+      if (ref == 1 || ref == 8) at<uint32_t>(V_LN + 4 * iln) = sl_[s];
+    }
+    __syncthreads();
+    const uint32_t ncl = nA & 0x3ff, nlc = (nA >> 10) & 0x3ff, nrc = nA >> 20;
+    const uint32_t nin = nB & 0x3ff, npi = (nB >> 10) & 0x3ff, nst = nB >> 20;
+    const uint32_t nkc = nC & 0x3ff, ntr = (nC >> 10) & 0x3ff, nln = nC >> 20;
+    auto g_cl = [](uint32_t i) { return at<uint32_t>(V_CL + 4 * i); };
+    auto g_lc = [](uint32_t i) { return at<uint32_t>(V_LC + 4 * i); };
+    auto g_rc = [](uint32_t i) { return at<uint32_t>(V_RC + 4 * i); };
+    auto g_ln = [](uint32_t i) { return at<uint32_t>(V_LN + 4 * i); };
+    auto g_tr = [](uint32_t i) { return (uint32_t)at<uint8_t>(V_TR + i); };
+    auto g_in = [](uint32_t i) { return (uint32_t)at<uint8_t>(V_IN + i); };
+    auto g_pi = [](uint32_t i) { return (uint32_t)at<uint8_t>(V_PI + i); };
+    auto g_kc = [](uint32_t i) { return i; };
+    auto g_sl = [](uint32_t i) { return at<uint32_t>(V_ST + 4 * i) >> 16; };
+    // string body bytes and per-entry offsets
+    uint32_t sbody, sboff[CPL];
+    {
+      uint32_t t = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < CPL; q++) {
+        const uint32_t i = lane * CPL + q;
+        sboff[q] = t;
+        t += i < nst ? at<uint32_t>(V_ST + 4 * i) >> 16 : 0;
+      }
+      const uint32_t incl = wave_incl_add(t);
+      sbody = lane_read(incl, 63);
+#pragma unroll
+      for (uint32_t q = 0; q < CPL; q++) sboff[q] += incl - t;
+    }
+    bool cbad = false;
+    const Slot none = make_slot(j.out, 0);
+    uint32_t csz[9];
+    csz[0] = col_encode<K_IDIF>(g_kc, nkc, false, none, 0, cbad);
+    csz[1] = col_encode<K_UOPT>(g_cl, ncl, false, none, 0, cbad);
+    csz[2] = col_encode<K_IDIF>(g_lc, nlc, false, none, 0, cbad);
+    csz[3] = col_encode<K_IDIF>(g_rc, nrc, false, none, 0, cbad);
+    csz[4] = col_encode<K_RLE>(g_in, nin, false, none, 0, cbad);
+    const uint32_t slsz = col_encode<K_UOPT>(g_sl, nst, false, none, 0, cbad);
+    csz[5] = vsz(sbody) + sbody + slsz;
+    csz[6] = col_encode<K_RLE>(g_pi, npi, false, none, 0, cbad);
+    csz[7] = col_encode<K_UOPT>(g_tr, ntr, false, none, 0, cbad);
+    csz[8] = col_encode<K_UOPT>(g_ln, nln, false, none, 0, cbad);
+    if (__any(cbad)) YM2_DECLINE()
+    uint32_t colbytes = 1;
+#pragma unroll
+    for (uint32_t c = 0; c < 9; c++) colbytes += vsz(csz[c]) + csz[c];
+    // rest part bytes per struct: part header (written, first clock), Skip length, payload span
+    uint32_t rb[E], rest_lane = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++) {
+      rb[s] = 0;
+      if (E * lane + s >= nrec) continue;
+      if (pstart[s]) rb[s] += vsz(runu[s]) + vsz((uint32_t)sk[s]);
+      if (gapv[s]) rb[s] += vsz(gapv[s]);
+      rb[s] += ssp[s] >> 16;
+      rest_lane += rb[s];
+    }
+    uint32_t rest_bytes, roff0;
+    {
+      const uint32_t incl = wave_incl_add(rest_lane);
+      rest_bytes = lane_read(incl, 63);
+      roff0 = incl - rest_lane;
+    }
+    const uint32_t rest_base = colbytes + vsz(nparts);
+    // output slot (as the V1 fast path): 16-aligned inside 2 * in + 64 per doc
+    const uint64_t slot = 2 * (b0 - arena0) + 64ull * d;
+    const uint64_t slot_al = (slot + 15) & ~15ull;
+    const uint64_t slot_end = slot + 2 * bytes + 64 < j.cap ? slot + 2 * bytes + 64 : j.cap;
+    if (slot_al + rest_base + rest_bytes > slot_end) {
+      if (slot_al + rest_base + rest_bytes > slot + 2 * bytes + 64) YM2_DECLINE()
+      if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }
+      __syncthreads();
+      continue;
+    }
+    const Slot dst = make_slot(j.out + slot_al, (uint32_t)(slot_end - slot_al));
+    // ---- write the columns: vu(0) | 9 x (vu(size) | bytes)
+    {
+      uint32_t p = 0;
+      if (lane == 0) ob8(dst, 0, 0);
+      p = 1;
+      uint32_t cb[9];
+#pragma unroll
+      for (uint32_t c = 0; c < 9; c++) {
+        if (lane == 0) put_vu(dst, p, csz[c]);
+        p += vsz(csz[c]);
+        cb[c] = p;
+        p += csz[c];
+      }
+      col_encode<K_IDIF>(g_kc, nkc, true, dst, cb[0], cbad);
+      col_encode<K_UOPT>(g_cl, ncl, true, dst, cb[1], cbad);
+      col_encode<K_IDIF>(g_lc, nlc, true, dst, cb[2], cbad);
+      col_encode<K_IDIF>(g_rc, nrc, true, dst, cb[3], cbad);
+      col_encode<K_RLE>(g_in, nin, true, dst, cb[4], cbad);
+      if (lane == 0) put_vu(dst, cb[5], sbody);
+      const uint32_t sbase = cb[5] + vsz(sbody);
+#pragma unroll
+      for (uint32_t q = 0; q < CPL; q++) {  // string bodies: copied from the update's string column
+        const uint32_t i = lane * CPL + q;
+        if (i >= nst) break;
+        const uint32_t e = at<uint32_t>(V_ST + 4 * i), a = e & 0xffff, n = e >> 16;
+        for (uint32_t b = 0; b < n; b++) ob8(dst, sbase + sboff[q] + b, sm[a + b]);
+      }
+      col_encode<K_UOPT>(g_sl, nst, true, dst, sbase + sbody, cbad);
+      col_encode<K_RLE>(g_pi, npi, true, dst, cb[6], cbad);
+      col_encode<K_UOPT>(g_tr, ntr, true, dst, cb[7], cbad);
+      col_encode<K_UOPT>(g_ln, nln, true, dst, cb[8], cbad);
+    }
+    // ---- rest: vu(#parts) | per struct: part header, Skip length, payload
+    if (lane == 0) put_vu(dst, colbytes, nparts);
+    {
+      uint32_t p = rest_base + roff0;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        if (E * lane + s >= nrec) break;
+        uint32_t q = p;
+        if (pstart[s]) { q = put_vu(dst, q, runu[s]); q = put_vu(dst, q, (uint32_t)sk[s]); }
+        if (gapv[s]) q = put_vu(dst, q, gapv[s]);
+        const uint32_t a = ssp[s] & 0xffff, n = ssp[s] >> 16;
+        for (uint32_t b = 0; b < n; b++) ob8(dst, q + b, sm[a + b]);
+        p += rb[s];
+      }
+    }
+    const uint32_t dsb = rest_base + rest_bytes;
+    // ---- 6. delete set (as ym_fast.hip step 5, V2 encoding: clock - previous end, len - 1)
+    {
+      uint64_t dk[E];
+      uint32_t dl[E], dq[E], dr[E];
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint32_t i = lane + 64 * s;
+        const bool v = i < nds;
+        dk[s] = v ? at<uint64_t>(L_DKEY + 8 * i) : ~0ull;
+        dl[s] = v ? at<uint32_t>(L_DLEN + 4 * i) : 0;
+        dq[s] = v ? at<uint16_t>(L_DSEQ + 2 * i) : 0;
+      }
+      rank_le(L_DKEY, nds, dk, dr);
+      __syncthreads();
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++)
+        if (lane + 64 * s < nds) at<uint8_t>(L_DSLOT + dr[s]) = (uint8_t)(lane + 64 * s);
+      __syncthreads();
+      bool dup = false;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++)
+        if (lane + 64 * s < nds) dup |= at<uint8_t>(L_DSLOT + dr[s]) != lane + 64 * s;
+      if (__any(dup)) rank_exact(L_DKEY, nds, dk, dr);
+      __syncthreads();
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        if (lane + 64 * s < nds) {
+          const uint32_t r = dr[s];
+          at<uint64_t>(L_DKEY + 8 * r) = dk[s];
+          at<uint32_t>(L_DLEN + 4 * r) = dl[s];
+          at<uint16_t>(L_DSEQ + 2 * r) = (uint16_t)dq[s];
+        }
+      }
+      __syncthreads();
+    }
+    uint32_t ngroups, nranges;
+    bool dbad = false;
+    {
+      uint32_t ecl[E], ecli[E], segst[E], segid[E], eseq[E];
+      uint64_t eend[E];
+      uint32_t seg_lane = 0;
+      const uint32_t r0 = E * lane;
+      uint32_t cprev = r0 > 0 && r0 - 1 < nds ? (uint32_t)(at<uint64_t>(L_DKEY + 8 * (r0 - 1)) >> 32) : 0;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint32_t r = r0 + s;
+        const bool v = r < nds;
+        const uint64_t kk = v ? at<uint64_t>(L_DKEY + 8 * r) : 0;
+        ecl[s] = (uint32_t)kk;
+        ecli[s] = (uint32_t)(kk >> 32);
+        eend[s] = v ? (uint64_t)ecl[s] + at<uint32_t>(L_DLEN + 4 * r) : 0;
+        eseq[s] = v ? at<uint16_t>(L_DSEQ + 2 * r) : 0xffff;
+        segst[s] = v && (r == 0 || cprev != ecli[s]);
+        seg_lane += segst[s];
+        cprev = ecli[s];
+      }
+      {
+        const uint32_t incl = wave_incl_add(seg_lane);
+        ngroups = lane_read(incl, 63);
+        uint32_t run = incl - seg_lane;
+#pragma unroll
+        for (uint32_t s = 0; s < E; s++) { run += segst[s]; segid[s] = run - 1; }
+      }
+      uint64_t m = 0, rmax[E];
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint64_t x = r0 + s < nds ? ((uint64_t)segid[s] << 33) | eend[s] : 0;
+        m = x > m ? x : m;
+        rmax[s] = m;
+      }
+      const uint64_t incl = wave_incl_max64(m);
+      uint64_t ex = ((uint64_t)from_prev_lane((uint32_t)(incl >> 32)) << 32) | from_prev_lane((uint32_t)incl);
+      uint32_t newr[E], nr_lane = 0;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint64_t before = ex;
+        rmax[s] = rmax[s] > ex ? rmax[s] : ex;
+        ex = rmax[s];
+        newr[s] = r0 + s < nds && (segst[s] || ecl[s] > (before & 0x1ffffffffull));
+        nr_lane += newr[s];
+      }
+      const uint32_t incl_r = wave_incl_add(nr_lane);
+      nranges = lane_read(incl_r, 63);
+      uint32_t run = incl_r - nr_lane;
+      const uint32_t next_first = from_next_lane(newr[0]);
+      __syncthreads();  // the rank-ordered delete ranges are in registers: phase arrays reuse R
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint32_t r = r0 + s;
+        if (r >= nds) break;
+        run += newr[s];
+        const uint32_t rid = run - 1;
+        if (newr[s]) {
+          at<uint32_t>(L_QCLK + 4 * rid) = ecl[s];
+          at<uint8_t>(L_QGRP + rid) = (uint8_t)segid[s];
+        }
+        const bool nxt_new = s + 1 < E ? newr[s + 1] != 0 : next_first != 0;
+        if (r + 1 >= nds || nxt_new) {
+          const uint64_t en = rmax[s] & 0x1ffffffffull;
+          dbad |= en > 0xffffffffull;
+          at<uint32_t>(L_QEND + 4 * rid) = (uint32_t)en;
+        }
+        if (segst[s]) {
+          at<uint16_t>(L_GFIRST + 2 * segid[s]) = (uint16_t)rid;
+          at<uint32_t>(L_GCLI + 4 * segid[s]) = ecli[s];
+          at<uint32_t>(L_GMIN + 4 * segid[s]) = 0xffffffffu;
+        }
+      }
+      if (lane == 0) at<uint16_t>(L_GFIRST + 2 * ngroups) = (uint16_t)nranges;
+      if (__any(dbad)) YM2_DECLINE()
+      __syncthreads();
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++)
+        if (r0 + s < nds) atomicMin(&at<uint32_t>(L_GMIN + 4 * segid[s]), eseq[s]);
+    }
+    __syncthreads();
+    // merged ranges q: V2 bytes = vu(clock - end of the previous range of the client) + vu(len - 1)
+    {
+      uint32_t qb[E], t = 0;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint32_t q = E * lane + s;
+        qb[s] = 0;
+        if (q < nranges) {
+          const uint32_t c0 = at<uint32_t>(L_QCLK + 4 * q), e0 = at<uint32_t>(L_QEND + 4 * q);
+          const uint32_t g = at<uint8_t>(L_QGRP + q);
+          const uint32_t pe = q > at<uint16_t>(L_GFIRST + 2 * g) ? at<uint32_t>(L_QEND + 4 * (q - 1)) : 0;
+          qb[s] = vsz(c0 - pe) + vsz(e0 - c0 - 1);
+        }
+        t += qb[s];
+      }
+      const uint32_t incl = wave_incl_add(t);
+      uint32_t run = incl - t;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint32_t q = E * lane + s;
+        if (q < nranges) at<uint16_t>(L_QPRE + 2 * q) = (uint16_t)run;
+        run += qb[s];
+      }
+      if (lane == 63) at<uint16_t>(L_QPRE + 2 * nranges) = (uint16_t)incl;
+    }
+    __syncthreads();
+    uint32_t grk[E], gbytes[E];
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++) {
+      const uint32_t g = lane + 64 * s;
+      const bool v = g < ngroups;
+      const uint32_t f0 = v ? at<uint16_t>(L_GFIRST + 2 * g) : 0, f1 = v ? at<uint16_t>(L_GFIRST + 2 * g + 2) : 0;
+      gbytes[s] = v ? vsz(at<uint32_t>(L_GCLI + 4 * g)) + vsz(f1 - f0) + at<uint16_t>(L_QPRE + 2 * f1) - at<uint16_t>(L_QPRE + 2 * f0) : 0;
+      const uint32_t mine = v ? at<uint32_t>(L_GMIN + 4 * g) : 0;
+      uint32_t rk_ = 0;
+      for (uint32_t h = 0; h < ngroups; h++) rk_ += at<uint32_t>(L_GMIN + 4 * h) < mine;
+      grk[s] = rk_;
+    }
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++)
+      if (lane + 64 * s < ngroups) at<uint16_t>(L_GBYR + 2 * grk[s]) = (uint16_t)gbytes[s];
+    __syncthreads();
+    const uint32_t ds_hdr = vsz(ngroups);
+    uint32_t ds_groups_bytes;
+    {
+      uint32_t v[E], t = 0;
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) { const uint32_t r = E * lane + s; v[s] = r < ngroups ? at<uint16_t>(L_GBYR + 2 * r) : 0; t += v[s]; }
+      const uint32_t incl = wave_incl_add(t);
+      ds_groups_bytes = lane_read(incl, 63);
+      uint32_t run = incl - t;
+      __syncthreads();
+#pragma unroll
+      for (uint32_t s = 0; s < E; s++) {
+        const uint32_t r = E * lane + s;
+        if (r < ngroups) at<uint16_t>(L_GBYR + 2 * r) = (uint16_t)run;
+        run += v[s];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++) {
+      const uint32_t g = lane + 64 * s;
+      if (g < ngroups) {
+        const uint32_t f0 = at<uint16_t>(L_GFIRST + 2 * g), f1 = at<uint16_t>(L_GFIRST + 2 * g + 2);
+        const uint32_t off = dsb + ds_hdr + at<uint16_t>(L_GBYR + 2 * grk[s]);
+        at<uint32_t>(L_GMIN + 4 * g) = off;
+        at<uint32_t>(L_GB2 + 4 * g) = off + vsz(at<uint32_t>(L_GCLI + 4 * g)) + vsz(f1 - f0) - at<uint16_t>(L_QPRE + 2 * f0);
+      }
+    }
+    __syncthreads();
+    const uint32_t total = dsb + ds_hdr + ds_groups_bytes;
+    if (slot_al + total > slot_end) {
+      if (slot_al + total > slot + 2 * bytes + 64) YM2_DECLINE()
+      if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }
+      __syncthreads();
+      continue;
+    }
+    if (lane == 0) put_vu(dst, dsb, ngroups);
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++) {
+      const uint32_t g = lane + 64 * s;
+      if (g < ngroups)
+        put_vu(dst, put_vu(dst, at<uint32_t>(L_GMIN + 4 * g), at<uint32_t>(L_GCLI + 4 * g)),
+               at<uint16_t>(L_GFIRST + 2 * g + 2) - at<uint16_t>(L_GFIRST + 2 * g));
+      const uint32_t q = E * lane + s;
+      if (q < nranges) {
+        const uint32_t c0 = at<uint32_t>(L_QCLK + 4 * q), e0 = at<uint32_t>(L_QEND + 4 * q);
+        const uint32_t g2 = at<uint8_t>(L_QGRP + q);
+        const uint32_t pe = q > at<uint16_t>(L_GFIRST + 2 * g2) ? at<uint32_t>(L_QEND + 4 * (q - 1)) : 0;
+        const uint32_t off = at<uint32_t>(L_GB2 + 4 * g2) + at<uint16_t>(L_QPRE + 2 * q);
+        put_vu(dst, put_vu(dst, off, c0 - pe), e0 - c0 - 1);
+      }
+    }
+    if (lane == 0) {
+      j.out_off[d] = slot_al;
+      j.out_len[d] = total;
+      j.status[d] = ym::ST_OK;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace fastv2
+
+__global__ void k_fast_region(GeneralJob j, uint32_t n_upd);  // ym_fast.hip
+
+int fast2_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st) {
+  if (op != OP_MERGE || !j.v2) return 0;
+  k_fast_region<<<1, 64, 0, st>>>(j, n_upd);
+  const uint32_t grid = j.n < 131072 ? j.n : 131072;
+  fastv2::k_fast_merge_v2<<<grid, 64, fastv2::LDS_BYTES, st>>>(j);
+  return 1;
+}
+
+}  // namespace ymk

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "ym_kernels.h"
+
 namespace ymk {
 namespace fastc {
 
@@ -267,5 +269,40 @@ __device__ __forceinline__ bool item_body(Cur &c, uint32_t info, uint32_t &len) 
   return !c.bad && len != 0;
 }
 
+// rank of each of the lane's keys among keys[0..n): #keys <= own (own included) - 1.  Keys past n
+// are ~0 (padding) and never count.  Equal keys collide; callers detect that.
+template <uint32_t E>
+__device__ __forceinline__ void rank_le(uint32_t keys, uint32_t n, const uint64_t (&k)[E], uint32_t (&rank)[E]) {
+  uint32_t cnt[E];
+#pragma unroll
+  for (uint32_t s = 0; s < E; s++) cnt[s] = 0;
+  for (uint32_t jj = 0; jj < n; jj += 2) {
+    const uint64_t a = at<uint64_t>(keys + 8 * jj), b = at<uint64_t>(keys + 8 * jj + 8);
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++) cnt[s] += (uint32_t)(a <= k[s]) + (uint32_t)(b <= k[s]);
+  }
+#pragma unroll
+  for (uint32_t s = 0; s < E; s++) rank[s] = cnt[s] - 1;
+}
+// exact ranks with ties broken by slot index (used only when equal keys exist)
+template <uint32_t E>
+__device__ __forceinline__ void rank_exact(uint32_t keys, uint32_t n, const uint64_t (&k)[E], uint32_t (&rank)[E]) {
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t s = 0; s < E; s++) {
+    const uint32_t i = lane + 64 * s;
+    uint32_t cnt = 0;
+    for (uint32_t jj = 0; jj < n; jj++) {
+      const uint64_t a = at<uint64_t>(keys + 8 * jj);
+      cnt += (a < k[s]) || (a == k[s] && jj < i);
+    }
+    rank[s] = cnt;
+  }
+}
+
+// a declined document is appended to the general path's work list
+__device__ __forceinline__ void decline(const GeneralJob &j, uint32_t d) {
+  j.status[d] = ST_PENDING;
+  j.pend_list[atomicAdd(j.pend_count, 1u)] = d;
+}
 }  // namespace fastc
 }  // namespace ymk
