@@ -44,6 +44,8 @@ def parse():
     p.add_argument("--docs-per-gpu", type=int, default=10000)
     p.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-secondary", action="store_true",
+                   help="skip the secondary workload lines (C4/C2-V2/C4-V2 merges, C3 diff/sv)")
     return p.parse_args()
 
 
@@ -72,6 +74,69 @@ def cpu_baseline(arena, upd_off, doc_upd, fmt, seconds):
                   f"oracle/ymerge_oracle.c (literal yjs 13.5.16 mergeUpdates), {threads} threads",
         "errors": int((st != 0).sum()),
     }
+
+
+def secondary(dev, eng):
+    """Quick device-resident measurements of the other BASELINE.json workloads (1 GPU): C4 and V2
+    merges (10k docs), C3 diffUpdate / encodeStateVectorFromUpdate (configs[2]: 4,096 V1 docs of
+    0.9 MB; 1,024 V2 docs) against random state vectors.  Whole-call GB/s of input."""
+    import torch
+    from yjs_amd import pack_docs
+    from yjs_amd.workloads import load_ymb, replicate, random_state_vectors
+    res = {}
+    cases = [("merge_c4_v1", "merge", "c4_v1", 10000), ("merge_c2_v2", "merge", "c2_v2", 10000),
+             ("merge_c4_v2", "merge", "c4_v2", 10000), ("diff_c3_v1", "diff", "c3_v1", 4096),
+             ("sv_c3_v1", "sv", "c3_v1", 4096), ("diff_c3_v2", "diff", "c3_v2", 1024)]
+    for name, op, wl, n in cases:
+        fmt = 2 if wl.endswith("v2") else 1
+        a, o, d = load_ymb(wl)
+        sva = svo = None
+        if op == "merge":
+            a, o, d = replicate(a, o, d, n)
+        else:
+            upd = a.tobytes()
+            a, o, d = replicate(a, o, d, n)  # n copies of the single C3 update
+            if op == "diff":
+                # the update's own state vector (one client: the trace's), random cuts per document
+                full = _sv_of_single_client_update(upd, fmt)
+                svs = random_state_vectors(full, n, seed=7)
+                sva, svo, _ = pack_docs([[x] for x in svs])
+        nd = len(d) - 1
+        ga = torch.from_numpy(a).to(dev)
+        go = torch.from_numpy(o.view(np.int64)).to(dev)
+        gd = torch.from_numpy(d.view(np.int32)).to(dev)
+        gsa = torch.from_numpy(sva).to(dev) if sva is not None else None
+        gso = torch.from_numpy(svo.view(np.int64)).to(dev) if svo is not None else None
+        cap = 4 * len(a) + 128 * nd + 8192 + (2 * len(sva) if sva is not None else 0)
+        oa = torch.empty(cap, dtype=torch.uint8, device=dev)
+        oo = torch.empty(nd, dtype=torch.int64, device=dev)
+        ol = torch.empty(nd, dtype=torch.int64, device=dev)
+        st = torch.empty(nd, dtype=torch.int32, device=dev)
+        steps = 5 if op == "merge" else 2
+        eng.run_device(op, fmt, ga, go, gd, oa, oo, ol, st, gsa, gso)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        kms = []
+        for _ in range(steps):
+            rc, _ = eng.run_device(op, fmt, ga, go, gd, oa, oo, ol, st, gsa, gso)
+            assert rc == 0, rc
+            kms.append(eng.last_stats.fast_ms)
+        torch.cuda.synchronize(dev)
+        el = (time.perf_counter() - t0) / steps
+        sts = eng.stats
+        res[name] = {"docs": nd, "input_bytes": int(len(a)), "value_gbs": round(len(a) / el / 1e9, 3),
+                     "docs_per_s": round(nd / el, 1), "ms_per_step": round(el * 1e3, 3),
+                     "kernel_ms": round(float(np.mean(kms)), 3), "docs_fast": int(sts["docs_fast"]),
+                     "docs_general": int(sts["docs_general"]), "errors": int(sts["docs_error"])}
+        del ga, go, gd, gsa, gso, oa, oo, ol, st
+        torch.cuda.empty_cache()
+    return res
+
+
+def _sv_of_single_client_update(upd, fmt):
+    """encodeStateVectorFromUpdate of a C3 template computed on the GPU engine (one client)."""
+    from yjs_amd import encodeStateVectorFromUpdate, encodeStateVectorFromUpdateV2
+    return (encodeStateVectorFromUpdateV2 if fmt == 2 else encodeStateVectorFromUpdate)(upd)
 
 
 def main():
@@ -194,6 +259,8 @@ def main():
         }
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(arena, upd_off, doc_upd, fmt, args.cpu_baseline_seconds)
+        if not args.no_secondary and world == 1:
+            line["secondary"] = secondary(dev, eng)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

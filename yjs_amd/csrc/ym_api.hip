@@ -92,26 +92,30 @@ __global__ void k_status_flags(const uint32_t *list, uint32_t n, const int32_t *
   flags[i] = status[d] == want;
 }
 
-__global__ void k_stats(const int32_t *status, const uint64_t *out_len, uint32_t n, uint64_t *acc) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+// per-call counters in one single-block launch (no atomics, no memset): errors, bytes out, bytes in
+__global__ void __launch_bounds__(1024) k_stats(const int32_t *status, const uint64_t *out_len, uint32_t n,
+                                                const uint64_t *upd_off, uint32_t n_upd, uint64_t *acc) {
+  __shared__ unsigned long long red[2][16];
   uint64_t err = 0, bytes = 0;
-  if (i < n) {
-    err = status[i] != 0;
-    bytes = status[i] == 0 ? out_len[i] : 0;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const bool ok = status[i] == 0;
+    err += !ok;
+    bytes += ok ? out_len[i] : 0;
   }
-  // wave reduction then one atomic per wave
   for (int o = 32; o > 0; o >>= 1) {
     err += __shfl_down(err, o, 64);
     bytes += __shfl_down(bytes, o, 64);
   }
-  if ((threadIdx.x & 63) == 0) {
-    atomicAdd((unsigned long long *)&acc[0], (unsigned long long)err);
-    atomicAdd((unsigned long long *)&acc[1], (unsigned long long)bytes);
+  const uint32_t w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[0][w] = err; red[1][w] = bytes; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t e = 0, b = 0;
+    for (uint32_t k = 0; k < blockDim.x / 64; k++) { e += red[0][k]; b += red[1][k]; }
+    acc[0] = e;
+    acc[1] = b;
+    acc[2] = upd_off[n_upd] - upd_off[0];
   }
-}
-
-__global__ void k_in_bytes(const uint64_t *upd_off, uint32_t n_upd, uint64_t *acc) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) acc[2] = upd_off[n_upd] - upd_off[0];
 }
 
 // Compacts the ids of listed docs whose status == want into `dst`; returns the count.
@@ -238,10 +242,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   j.pend_list = S->list_a.as<uint32_t>();
   j.n = nd;
 
-  auto stats_launch = [&]() {
-    k_stats<<<(nd + 255) / 256, 256, 0, st>>>(o_status, o_len, nd, counters + 4);
-    k_in_bytes<<<1, 1, 0, st>>>(upd_off, b->n_upd, counters + 4);
-  };
+  auto stats_launch = [&]() { k_stats<<<1, 1024, 0, st>>>(o_status, o_len, nd, upd_off, b->n_upd, counters + 4); };
   HIPCHK(hipEventRecord(S->ev0, st));
   // (1) fast path over every document; appends the ones it declines to list_a
   HIPCHK(hipEventRecord(S->evf0, st));
@@ -255,10 +256,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   uint32_t *list = nullptr;
   if (fr == 1) {
     // one round trip: used, the declined count and (speculatively) the stats of the fast-only case
-    if (stats) {
-      HIPCHK(hipMemsetAsync(counters + 4, 0, 24, st));
-      stats_launch();
-    }
+    if (stats) stats_launch();
     HIPCHK(hipEventRecord(S->ev1, st));
     HIPCHK(hipMemcpyAsync(S->pinned, counters, stats ? 56 : 24, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -272,10 +270,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
     int r = run_general(S, st, j, list, ngen);
     if (r) return r;
     HIPCHK(hipEventRecord(S->evg1, st));
-    if (stats) {
-      HIPCHK(hipMemsetAsync(counters + 4, 0, 24, st));
-      stats_launch();
-    }
+    if (stats) stats_launch();
     HIPCHK(hipEventRecord(S->ev1, st));
     HIPCHK(hipMemcpyAsync(S->pinned, counters, stats ? 56 : 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
