@@ -78,6 +78,8 @@ typedef struct ym_stats {
   double device_ms;  /* device time of the call (HIP events on the call's stream)          */
   double fast_ms;    /* ... of the LDS fast-path kernel alone                              */
   double general_ms; /* ... of the general path (workspace sizing + both passes)           */
+  uint64_t docs_large; /* documents merged by the large-document pipeline (ym_large.hip)     */
+  double large_ms;   /* ... device time of that pipeline                                   */
 } ym_stats;
 
 int ym_init(int device);           /* select the HIP device for this thread; 0 on success */

@@ -9,6 +9,7 @@
 //   C3  B4-like single-client trace (259,778 single-char ops: 2% random jump, 29.7% backspace, else
 //       type), final state V1/V2; bench replicates it with random state vectors.
 //   C4  Y.Map docs, 64 clients, 128 broadcast transactions, keys k0..k7, delete p=0.6 when present.
+//   C5  Y.XmlFragment docs, 1,024 clients x 16 transactions each (V1 and V2), see genXml.
 // File format (.ymb, little endian): "YMB1" u32 n_docs u32 n_upd | u32 doc_upd[n_docs+1] |
 // u64 upd_off[n_upd+1] | arena bytes; gzip-compressed.
 'use strict'
@@ -100,6 +101,51 @@ function genMap (seed, nClients, nTx, nKeys) {
   return { v1, v2 }
 }
 
+
+// C5: Y.XmlFragment('xml'), nClients clients x nTx transactions (16 per client), 30% one-way sync
+// between random peers after each transaction; local updates only (SURVEY.md §8(d) C5).  40% insert an
+// XmlElement('p'|'h1') with a `class` attribute and a formatted XmlText; 35% formatted text insert
+// into an existing element; 25% delete an element.
+function genXml (seed, nClients, nTx) {
+  const r = rng(seed)
+  const v1 = []; const v2 = []
+  const docs = []
+  for (let c = 0; c < nClients; c++) {
+    const d = new Y.Doc(); d.clientID = 3000 + 17 * c
+    d.on('update', (u, origin) => { if (origin !== 'remote') v1.push(u) })
+    d.on('updateV2', (u, origin) => { if (origin !== 'remote') v2.push(u) })
+    docs.push(d)
+  }
+  for (let t = 0; t < nTx; t++) {
+    const d = docs[r.u32() % docs.length]
+    const frag = d.getXmlFragment('xml')
+    const p = r.real()
+    d.transact(() => {
+    if (p < 0.4 || frag.length === 0) {
+      const el = new Y.XmlElement(r.u32() % 2 ? 'p' : 'h1')
+      el.setAttribute('class', 'c' + (r.u32() % 5))
+      const tx = new Y.XmlText()
+      el.insert(0, [tx])
+      frag.insert(r.int(0, frag.length), [el])
+      tx.insert(0, r.word(1, 6), r.real() < 0.5 ? { bold: true } : {})
+    } else if (p < 0.75) {
+      const el = frag.get(r.int(0, frag.length - 1))
+      if (el instanceof Y.XmlElement && el.length > 0) {
+        const tx = el.get(0)
+        if (tx instanceof Y.XmlText) tx.insert(r.int(0, tx.length), r.word(1, 4), r.real() < 0.5 ? { italic: true } : {})
+      }
+    } else {
+      frag.delete(r.int(0, frag.length - 1), 1)
+    }
+    })
+    if (r.real() < 0.3) {
+      const a = docs[r.u32() % docs.length]; const b = docs[r.u32() % docs.length]
+      if (a !== b) Y.applyUpdate(b, Y.encodeStateAsUpdate(a, Y.encodeStateVector(b)), 'remote')
+    }
+  }
+  return { v1, v2 }
+}
+
 fs.mkdirSync(OUT, { recursive: true })
 if (which.includes('c1')) {
   const { v1, v2 } = genText(12345, 1, 1000, 10, false, 0, [7])
@@ -137,4 +183,15 @@ if (which.includes('c4')) {
   }
   writeYmb(path.join(OUT, 'c4_v1.ymb.gz'), d1)
   writeYmb(path.join(OUT, 'c4_v2.ymb.gz'), d2)
+}
+if (which.includes('c5')) {
+  const T = Number(process.env.C5_TEMPLATES || 8)
+  const NC = Number(process.env.C5_CLIENTS || 1024)
+  const d1 = []; const d2 = []
+  for (let doc = 0; doc < T; doc++) {
+    const { v1, v2 } = genXml(doc + 101, NC, 16 * NC)
+    d1.push(v1); d2.push(v2)
+  }
+  writeYmb(path.join(OUT, 'c5_v1.ymb.gz'), d1)
+  writeYmb(path.join(OUT, 'c5_v2.ymb.gz'), d2)
 }

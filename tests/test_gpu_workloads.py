@@ -90,3 +90,57 @@ def test_c3_diff_random_svs(engine, fmt):
     bad = _compare(engine.run_host("diff", fmt, a2, o2, d2, sva, svo), outs, st)
     assert not bad, bad[:10]
     assert engine.stats["docs_fast"] == engine.stats["docs"], engine.stats
+
+
+def _subset(arena, upd_off, doc_upd, docs, keep):
+    """Documents `docs` of a template file, each restricted to the updates u (local index) with keep(u)."""
+    from yjs_amd import pack_docs
+    out = []
+    for d in docs:
+        u0, u1 = int(doc_upd[d]), int(doc_upd[d + 1])
+        out.append([arena[int(upd_off[u]):int(upd_off[u + 1])].tobytes() for u in range(u0, u1) if keep(u - u0)])
+    return pack_docs(out)
+
+
+@pytest.mark.parametrize("fmt", [1, 2])
+def test_large_merge_c5_matches_oracle(engine, fmt):
+    """configs[4] C5 (1,024 clients, ~16 k updates per document): the large-document pipeline."""
+    arena, upd_off, doc_upd = load_ymb(f"c5_v{fmt}")
+    outs, status, _ = O.batch("merge", fmt, arena, upd_off, doc_upd, nthreads=8)
+    bad = _compare(engine.run_host("merge", fmt, arena, upd_off, doc_upd), outs, status)
+    assert not bad, bad[:10]
+    st = engine.stats
+    assert st["docs_large"] == st["docs"], st
+
+
+@pytest.mark.parametrize("fmt", [1, 2])
+def test_large_merge_gaps_matches_oracle(engine, fmt):
+    """Dropped updates leave clock gaps: Skips inside client parts, delete sets of absent structs."""
+    arena, upd_off, doc_upd = load_ymb(f"c5_v{fmt}")
+    a, o, d = _subset(arena, upd_off, doc_upd, range(4), lambda u: u % 5 != 3)
+    outs, status, _ = O.batch("merge", fmt, a, o, d, nthreads=8)
+    bad = _compare(engine.run_host("merge", fmt, a, o, d), outs, status)
+    assert not bad, bad[:10]
+    assert engine.stats["docs_large"] == 4, engine.stats
+
+
+@pytest.mark.parametrize("fmt", [1, 2])
+def test_large_merge_mixed_batch(engine, fmt):
+    """One batch of small (fast path), large (pipeline) and overlapping (general path) documents:
+    C2 docs, C5 docs cut to 3,000 updates, and two C2 docs concatenated (same clients: overlaps)."""
+    from yjs_amd import pack_docs
+    a2, o2, d2 = load_ymb(f"c2_v{fmt}")
+    a5, o5, d5 = load_ymb(f"c5_v{fmt}")
+    docs = []
+    upd = lambda a, o, u: a[int(o[u]):int(o[u + 1])].tobytes()
+    for i in range(6):
+        docs.append([upd(a2, o2, u) for u in range(int(d2[i]), int(d2[i + 1]))])
+        docs.append([upd(a5, o5, u) for u in range(int(d5[i % 8]), int(d5[i % 8]) + 3000)])
+    docs.append(docs[0] + docs[2])
+    docs.append([upd(a2, o2, u) for u in range(int(d2[7]), int(d2[9]))])
+    a, o, d = pack_docs(docs)
+    outs, status, _ = O.batch("merge", fmt, a, o, d, nthreads=8)
+    bad = _compare(engine.run_host("merge", fmt, a, o, d), outs, status)
+    assert not bad, bad[:10]
+    st = engine.stats
+    assert st["docs_fast"] == 6 and st["docs_large"] == 6, st

@@ -57,6 +57,8 @@ struct DevState {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evf0 = nullptr, evf1 = nullptr, evg1 = nullptr;
   DBuf ws, ws_size, ws_off, layout, counters, scan_tmp, list_a, list_b, flags;
   DBuf in_arena, in_off, in_doc, in_sv, in_svoff, out_arena, out_off, out_len, status;  // host staging
+  LargeBufs large;
+  hipEvent_t evl1 = nullptr;
   uint64_t *pinned = nullptr;
 };
 
@@ -80,6 +82,7 @@ DevState *state() {
     hipEventCreate(&g_state->evf0);
     hipEventCreate(&g_state->evf1);
     hipEventCreate(&g_state->evg1);
+    hipEventCreate(&g_state->evl1);
     hipHostMalloc((void **)&g_state->pinned, 64 * sizeof(uint64_t), hipHostMallocDefault);
   }
   return g_state;
@@ -265,7 +268,29 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   } else {
     HIPCHK(hipMemsetAsync(counters, 0, 256, st));
   }
-  // (2) general path over the rest
+  // (2) large-document merges (ym_large.hip) over the declined list; what it declines stays pending
+  uint32_t nlarge = 0;
+  bool large = false;
+  if (ngen > 0 && list && op == OP_MERGE) {
+    int lr = large_run(j, list, ngen, st, S->large);
+    if (lr < 0) return lr;
+    if (lr == 1) {
+      large = true;
+      HIPCHK(hipEventRecord(S->evl1, st));
+      uint32_t cnt = 0;
+      if (select_docs(S, st, list, ngen, o_status, ST_PENDING, S->list_b.as<uint32_t>(), &cnt)) return -1;
+      nlarge = ngen - cnt;
+      ngen = cnt;
+      list = S->list_b.as<uint32_t>();
+      if (ngen == 0) {
+        if (stats) stats_launch();
+        HIPCHK(hipEventRecord(S->ev1, st));
+        HIPCHK(hipMemcpyAsync(S->pinned, counters, stats ? 56 : 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+      }
+    }
+  }
+  // (3) general path over the rest
   if (ngen > 0) {
     int r = run_general(S, st, j, list, ngen);
     if (r) return r;
@@ -281,13 +306,17 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
     float ms = 0, fms = 0, gms = 0;
     hipEventElapsedTime(&ms, S->ev0, S->ev1);
     hipEventElapsedTime(&fms, S->evf0, S->evf1);
-    if (ngen > 0) hipEventElapsedTime(&gms, S->evf1, S->evg1);
+    float lms = 0;
+    if (large) hipEventElapsedTime(&lms, S->evf1, S->evl1);
+    if (ngen > 0) hipEventElapsedTime(&gms, large ? S->evl1 : S->evf1, S->evg1);
+    stats->docs_large = nlarge;
+    stats->large_ms = lms;
     stats->device_ms = ms;
     stats->fast_ms = fr == 1 ? fms : 0.0;
     stats->general_ms = ngen > 0 ? gms : 0.0;
     stats->docs = nd;
     stats->docs_general = ngen;
-    stats->docs_fast = nd - ngen;
+    stats->docs_fast = nd - ngen - nlarge;
     stats->docs_error = S->pinned[4];
     stats->bytes_out = S->pinned[5];
     stats->bytes_in = S->pinned[6];
@@ -330,6 +359,9 @@ int ym_shutdown(void) {
   if (S->evf0) hipEventDestroy(S->evf0);
   if (S->evf1) hipEventDestroy(S->evf1);
   if (S->evg1) hipEventDestroy(S->evg1);
+  if (S->evl1) hipEventDestroy(S->evl1);
+  for (int k = 0; k < 4; k++) if (S->large.p[k]) hipFree(S->large.p[k]);
+  if (S->large.pinned) hipHostFree(S->large.pinned);
   if (S->stream) hipStreamDestroy(S->stream);
   delete S;
   g_state = nullptr;

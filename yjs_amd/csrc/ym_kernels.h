@@ -1,5 +1,6 @@
 // ym_kernels.h -- launch descriptors shared by the host API (ym_api.hip) and the kernels.
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "ym_core.h"
@@ -33,6 +34,16 @@ struct GeneralJob {
   uint32_t *pend_list;       // fast path: ids of the documents it declines (appended) ...
   uint32_t *pend_count;      // ... and their number
 };
+
+// device buffers of the large-document merge pipeline (ym_large.hip), grown on demand, cached
+struct LargeBufs {
+  void *p[4] = {nullptr, nullptr, nullptr, nullptr};
+  size_t cap[4] = {0, 0, 0, 0};
+  uint64_t *pinned = nullptr;
+};
+// Large-document merge over `list` (n documents the fast path declined).  Documents it takes get
+// status OK; the rest keep ST_PENDING.  Returns 1 when launched, 0 when not applicable, < 0 on error.
+int large_run(const GeneralJob &j, const uint32_t *list, uint32_t n, hipStream_t st, LargeBufs &B);
 
 struct GeneralWsSize {
   uint64_t rs, arr, parts, ds, dsg, sv, total;

@@ -75,7 +75,8 @@ class _Out(ctypes.Structure):
 class _Stats(ctypes.Structure):
     _fields_ = [("docs", ctypes.c_uint64), ("docs_fast", ctypes.c_uint64), ("docs_general", ctypes.c_uint64),
                 ("docs_error", ctypes.c_uint64), ("bytes_in", ctypes.c_uint64), ("bytes_out", ctypes.c_uint64),
-                ("device_ms", ctypes.c_double), ("fast_ms", ctypes.c_double), ("general_ms", ctypes.c_double)]
+                ("device_ms", ctypes.c_double), ("fast_ms", ctypes.c_double), ("general_ms", ctypes.c_double),
+                ("docs_large", ctypes.c_uint64), ("large_ms", ctypes.c_double)]
 
 
 EXPORTS = ("ym_init", "ym_shutdown", "ym_strerror", "ym_out_bound", "ym_merge", "ym_diff", "ym_sv")
