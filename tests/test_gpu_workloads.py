@@ -144,3 +144,28 @@ def test_large_merge_mixed_batch(engine, fmt):
     assert not bad, bad[:10]
     st = engine.stats
     assert st["docs_fast"] == 6 and st["docs_large"] == 6, st
+
+
+@pytest.mark.parametrize("fmt", [1, 2])
+def test_c5_sv_and_diff_many_clients(engine, fmt):
+    """configs[4] diffUpdate[V2] / encodeStateVectorFromUpdate[V2] over merged C5 documents (one update
+    of ~1,000 client parts each) against random per-client state vectors: the streamed wave walkers
+    (section / state-vector / delete-set tables in per-block HBM scratch) must take every document."""
+    from yjs_amd import pack_docs
+    arena, upd_off, doc_upd = load_ymb(f"c5_v{fmt}")
+    merged, status, _ = O.batch("merge", fmt, arena, upd_off, doc_upd, nthreads=8)
+    assert (status == 0).all()
+    a2, o2, d2 = pack_docs([[m] for m in merged])
+    outs, st, _ = O.batch("sv", fmt, a2, o2, d2, nthreads=8)
+    bad = _compare(engine.run_host("sv", fmt, a2, o2, d2), outs, st)
+    assert not bad, bad[:10]
+    assert engine.stats["docs_fast"] == engine.stats["docs"], engine.stats
+    svs = []
+    for i in range(len(merged)):
+        svs.extend(random_state_vectors(outs[i], 2, seed=100 + i))
+    a3, o3, d3 = pack_docs([[merged[i // 2]] for i in range(len(svs))])
+    sva, svo, _ = pack_docs([[s] for s in svs])
+    outs2, st2, _ = O.batch("diff", fmt, a3, o3, d3, sva, svo, nthreads=8)
+    bad = _compare(engine.run_host("diff", fmt, a3, o3, d3, sva, svo), outs2, st2)
+    assert not bad, bad[:10]
+    assert engine.stats["docs_fast"] == engine.stats["docs"], engine.stats

@@ -22,11 +22,21 @@ for case in cases:
     a, o, d = load_ymb(wl)
     sva = svo = None
     if op == "merge":
-        a, o, d = replicate(a, o, d, int(os.environ.get("NDOCS", "10000")))
+        a, o, d = replicate(a, o, d, int(os.environ.get("NDOCS", "256" if wl.startswith("c5") else "10000")))
+    elif wl.startswith("c5"):
+        # diff / sv over merged C5 documents (1,024 clients each), random per-client state vectors
+        n = int(os.environ.get("NDOCS_BIG", "256"))
+        ma, mo, ml, mst = eng.run_host("merge", fmt, a, o, d)
+        ups = [ma[int(mo[i]):int(mo[i]) + int(ml[i])].tobytes() for i in range(len(d) - 1)]
+        svfn = eng.run_host
+        sa, so_, sl, _ = svfn("sv", fmt, *pack_docs([[u] for u in ups]))
+        fulls = [sa[int(so_[i]):int(so_[i]) + int(sl[i])].tobytes() for i in range(len(ups))]
+        svs = [random_state_vectors(fulls[i % len(ups)], 1, seed=i)[0] for i in range(n)]
+        a, o, d = pack_docs([[ups[i % len(ups)]] for i in range(n)])
+        sva, svo, _ = pack_docs([[s] for s in svs])
     else:
         n = int(os.environ.get("NDOCS_BIG", "256"))
         upd = a.tobytes()
-    if op != "merge":
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_ref as O
         full = O.sv_from_update(upd, fmt)[1]

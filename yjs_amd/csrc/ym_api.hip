@@ -55,7 +55,7 @@ struct DevState {
   int device = -1;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evf0 = nullptr, evf1 = nullptr, evg1 = nullptr;
-  DBuf ws, ws_size, ws_off, layout, counters, scan_tmp, list_a, list_b, flags;
+  DBuf ws, ws_size, ws_off, layout, counters, scan_tmp, list_a, list_b, flags, bscratch;
   DBuf in_arena, in_off, in_doc, in_sv, in_svoff, out_arena, out_off, out_len, status;  // host staging
   LargeBufs large;
   hipEvent_t evl1 = nullptr;
@@ -244,6 +244,10 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   j.pend_count = (uint32_t *)(counters + 2);
   j.pend_list = S->list_a.as<uint32_t>();
   j.n = nd;
+  if (op != OP_MERGE) {  // per-block scratch of the streamed diff / state-vector kernels
+    if (S->bscratch.ensure(BS_GRID * BS_BYTES)) return -2;
+    j.bscratch = S->bscratch.as<uint8_t>();
+  }
 
   auto stats_launch = [&]() { k_stats<<<1, 1024, 0, st>>>(o_status, o_len, nd, upd_off, b->n_upd, counters + 4); };
   HIPCHK(hipEventRecord(S->ev0, st));
@@ -350,7 +354,7 @@ int ym_shutdown(void) {
   DevState *S = g_state;
   hipStreamSynchronize(S->stream);
   DBuf *bufs[] = {&S->ws, &S->ws_size, &S->ws_off, &S->layout, &S->counters, &S->scan_tmp, &S->list_a, &S->list_b,
-                  &S->flags, &S->in_arena, &S->in_off, &S->in_doc, &S->in_sv, &S->in_svoff, &S->out_arena,
+                  &S->flags, &S->bscratch, &S->in_arena, &S->in_off, &S->in_doc, &S->in_sv, &S->in_svoff, &S->out_arena,
                   &S->out_off, &S->out_len, &S->status};
   for (DBuf *b : bufs) if (b->p) hipFree(b->p);
   if (S->pinned) hipHostFree(S->pinned);

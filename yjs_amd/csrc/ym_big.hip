@@ -27,26 +27,53 @@ using namespace fastc;
 
 constexpr uint32_t BW = 8192;   // LDS window over the update
 constexpr uint32_t BM = 2048;   // refill when fewer bytes remain ahead of the cursor (max struct size)
-constexpr uint32_t NSEC = 64;   // client sections per update
-constexpr uint32_t NSV = 256;   // state-vector entries
+constexpr uint32_t NSEC = BS_NSEC;  // client sections per update (HBM scratch, per block)
+constexpr uint32_t NSV = BS_NSV;    // state-vector entries (HBM scratch)
 constexpr uint32_t NPATCH = 512;
-constexpr uint32_t PRE = 48;    // sliced-struct prefix bytes per section
+constexpr uint32_t PRE = BS_PRE;    // sliced-struct prefix bytes per section
 
-constexpr uint32_t SECW = 12;   // u32 fields per section record
+constexpr uint32_t SECW = BS_SECW;  // u32 fields per section record
 constexpr uint32_t L_WIN = 0;                        // u8[BW + 16]
-constexpr uint32_t L_SEC = BW + 16;                  // u32[NSEC][SECW] section records
-constexpr uint32_t L_PRE = L_SEC + NSEC * 4 * SECW;  // u8[NSEC][PRE] sliced-struct head (re-encoded)
-constexpr uint32_t L_SV = L_PRE + NSEC * PRE;        // u32[NSV][2] state vector (client, clock)
-constexpr uint32_t L_PPOS = L_SV + NSV * 8;          // u32[NPATCH] patch positions (update-relative)
+constexpr uint32_t L_PRE = BW + 16;                  // u8[PRE] the current section's sliced-struct head
+constexpr uint32_t L_PPOS = L_PRE + PRE;             // u32[NPATCH] patch positions (update-relative)
 constexpr uint32_t L_PVAL = L_PPOS + 4 * NPATCH;     // u8[NPATCH]  patched info bytes
-constexpr uint32_t L_DSC = L_PVAL + NPATCH;          // u32[64]     delete-set clients seen
-constexpr uint32_t LDS_BYTES = L_DSC + 256;
+constexpr uint32_t L_PSEC = L_PVAL + NPATCH;         // u32[NPATCH] section of each patch
+constexpr uint32_t LDS_BYTES = L_PSEC + 4 * NPATCH;
 // section record fields: head bytes (or NONE: nothing written), span A (content tail of a sliced
 // struct), span B (the following structs, as is), part header (written, client, first clock), and
 // the output position of update byte 0 within span B (for the patches)
 enum { S_PRELEN = 0, S_A0, S_A1, S_B0, S_B1, S_WRITTEN, S_CLIENT, S_FCLOCK, S_OUTB };
 constexpr uint32_t NONE = 0xffffffffu;
-__device__ __forceinline__ uint32_t &sec(uint32_t ci, uint32_t f) { return at<uint32_t>(L_SEC + 4 * (SECW * ci + f)); }
+// per-block HBM scratch (ym_kernels.h BS_*): section records, their sliced heads, state vector,
+// delete-set clients
+struct Scr {
+  uint32_t *sec, *svt, *dsc;
+  uint8_t *pre;
+};
+__device__ __forceinline__ Scr scratch(const GeneralJob &j) {
+  uint8_t *b = j.bscratch + (uint64_t)blockIdx.x * BS_BYTES;
+  return Scr{(uint32_t *)(b + BS_SEC), (uint32_t *)(b + BS_SVT), (uint32_t *)(b + BS_DSC), b + BS_PREB};
+}
+#define sec(ci, f) X.sec[SECW * (ci) + (f)]
+// sv[client] (decodeStateVector: a later entry for the same client wins), wave-parallel
+__device__ __forceinline__ uint32_t sv_lookup(const uint32_t *svt, uint32_t nsv, uint32_t client) {
+  int best = -1;
+  for (uint32_t i0 = 0; i0 < nsv; i0 += 64) {
+    const uint32_t i = i0 + threadIdx.x;
+    const uint64_t m = __ballot(i < nsv && svt[2 * i] == client);
+    if (m) best = (int)(i0 + 63 - __builtin_clzll(m));
+  }
+  return best >= 0 ? svt[2 * best + 1] : 0;
+}
+// was `client` among the first n delete-set clients? (wave-parallel)
+__device__ __forceinline__ bool seen_before(const uint32_t *dsc, uint32_t n, uint32_t client) {
+  bool hit = false;
+  for (uint32_t h0 = 0; h0 < n; h0 += 64) {
+    const uint32_t h = h0 + threadIdx.x;
+    hit |= __any(h < n && dsc[h] == client);
+  }
+  return hit;
+}
 
 // window over the update [0, len) at absolute arena offset b0; LDS byte i <-> arena byte wa + i
 struct Win {
@@ -100,6 +127,7 @@ __device__ __forceinline__ uint32_t put_vu_lds(uint32_t p, uint32_t v) {
 template <int OP>
 __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
   const uint32_t lane = threadIdx.x;
+  const Scr X = scratch(j);
   for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
     const uint32_t u0 = j.doc_upd[d];
     if (j.doc_upd[d + 1] - u0 != 1) YB_DECLINE()
@@ -113,7 +141,7 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
     bool bad = false;
     if (OP == OP_DIFF) {
       const uint64_t s0 = j.sv_off[d], s1 = j.sv_off[d + 1];
-      if (s1 - s0 > 4 * NSV * 5 + 8) YB_DECLINE()
+      if (s1 - s0 > BW - 32) YB_DECLINE()
       // the state vector is tiny: stage it through the window
       {
         const uint64_t a = s0 & ~15ull;
@@ -126,11 +154,12 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
         for (uint32_t i = 0; i < n && !c.bad; i++) {
           const uint32_t cl = rvu(c), ck = rvu(c);
           if (nsv >= NSV) { c.bad = true; break; }
-          if (lane == 0) { at<uint32_t>(L_SV + 8 * nsv) = cl; at<uint32_t>(L_SV + 8 * nsv + 4) = ck; }
+          if (lane == 0) { X.svt[2 * nsv] = cl; X.svt[2 * nsv + 1] = ck; }
           nsv++;
         }
         bad = c.bad;
       }
+      __syncthreads();
       if (bad) YB_DECLINE()
     }
     // ---- struct section (encoding.js:127-198 layout; 13.5.16 LazyStructReader)
@@ -151,14 +180,11 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
       uint64_t clock = rvu(c);
       if (ci > 0 && client == prev_client) { declined = true; break; }  // writer would not start a part
       prev_client = client;
-      uint32_t k = 0;
-      if (OP == OP_DIFF)
-        for (uint32_t i = 0; i < nsv; i++)
-          if (at<uint32_t>(L_SV + 8 * i) == client) k = at<uint32_t>(L_SV + 8 * i + 4);
+      const uint32_t k = OP == OP_DIFF ? sv_lookup(X.svt, nsv, client) : 0;
       if (OP == OP_SV && nstructs > 0 && sv_any && client != sv_client) {  // client change (os@37724)
         if (sv_clock != 0) {
           if (sv_n >= NSV) { declined = true; break; }
-          if (lane == 0) { at<uint32_t>(L_SV + 8 * sv_n) = sv_client; at<uint32_t>(L_SV + 8 * sv_n + 4) = sv_clock; }
+          if (lane == 0) { X.svt[2 * sv_n] = sv_client; X.svt[2 * sv_n + 1] = sv_clock; }
           sv_n++;
         }
         sv_client = client; sv_clock = 0; sv_stop = clock != 0;
@@ -189,14 +215,14 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
             copying = true;
             written = 1;
             const uint32_t off = k > clock ? (uint32_t)(k - clock) : 0;
-            const uint32_t pre = L_PRE + ci * PRE;
+            const uint32_t pre = L_PRE;
             uint32_t q = pre, a0 = 0, a1 = 0;
             if (off == 0) {
               b0r = rel(w, s0);
               const uint32_t ni = gc ? 0 : ((info & 0xC0) ? info & ~0x20u : info);
               if (ni != info) {
                 if (npatch >= NPATCH) { declined = true; break; }
-                if (lane == 0) { at<uint32_t>(L_PPOS + 4 * npatch) = b0r; sm[L_PVAL + npatch] = (uint8_t)ni; }
+                if (lane == 0) { at<uint32_t>(L_PPOS + 4 * npatch) = b0r; sm[L_PVAL + npatch] = (uint8_t)ni; at<uint32_t>(L_PSEC + 4 * npatch) = ci; }
                 npatch++;
               }
             } else {
@@ -259,6 +285,7 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
               if (q - pre > PRE) { declined = true; break; }
             }
             if (lane == 0) {
+              for (uint32_t b = 0; b < q - pre; b++) X.pre[ci * PRE + b] = sm[pre + b];
               sec(ci, S_PRELEN) = q - pre;
               sec(ci, S_A0) = a0;
               sec(ci, S_A1) = a1;
@@ -272,7 +299,7 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
           const uint32_t ni = skip ? info : gc ? 0 : ((info & 0xC0) ? info & ~0x20u : info);
           if (ni != info) {
             if (npatch >= NPATCH) { declined = true; break; }
-            if (lane == 0) { at<uint32_t>(L_PPOS + 4 * npatch) = rel(w, s0); sm[L_PVAL + npatch] = (uint8_t)ni; }
+            if (lane == 0) { at<uint32_t>(L_PPOS + 4 * npatch) = rel(w, s0); sm[L_PVAL + npatch] = (uint8_t)ni; at<uint32_t>(L_PSEC + 4 * npatch) = ci; }
             npatch++;
           }
         }
@@ -292,12 +319,15 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
     __syncthreads();
     if (OP == OP_SV) {
       if (sv_any && sv_clock != 0) {
-        if (lane == 0) { at<uint32_t>(L_SV + 8 * sv_n) = sv_client; at<uint32_t>(L_SV + 8 * sv_n + 4) = sv_clock; }
+        if (sv_n >= NSV) YB_DECLINE()
+        if (lane == 0) { X.svt[2 * sv_n] = sv_client; X.svt[2 * sv_n + 1] = sv_clock; }
         sv_n++;
       }
+      __threadfence_block();
       __syncthreads();
-      uint32_t total = vsz(sv_n);
-      for (uint32_t i = 0; i < sv_n; i++) total += vsz(at<uint32_t>(L_SV + 8 * i)) + vsz(at<uint32_t>(L_SV + 8 * i + 4));
+      uint32_t tl = 0;
+      for (uint32_t i = lane; i < sv_n; i += 64) tl += vsz(X.svt[2 * i]) + vsz(X.svt[2 * i + 1]);
+      const uint32_t total = vsz(sv_n) + lane_read(wave_incl_add(tl), 63);
       uint64_t base = 0;
       if (lane == 0) base = atomicAdd((unsigned long long *)j.used, (unsigned long long)total);
       base = ((uint64_t)lane_read((uint32_t)(base >> 32), 0) << 32) | lane_read((uint32_t)base, 0);
@@ -311,7 +341,7 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
         uint32_t p = 0;
         auto put = [&](uint32_t v) { while (v > 127) { o[p++] = (uint8_t)(0x80 | (v & 127)); v >>= 7; } o[p++] = (uint8_t)v; };
         put(sv_n);
-        for (uint32_t i = 0; i < sv_n; i++) { put(at<uint32_t>(L_SV + 8 * i)); put(at<uint32_t>(L_SV + 8 * i + 4)); }
+        for (uint32_t i = 0; i < sv_n; i++) { put(X.svt[2 * i]); put(X.svt[2 * i + 1]); }
         j.out_off[d] = base;
         j.out_len[d] = total;
         j.status[d] = ym::ST_OK;
@@ -330,9 +360,10 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
         const uint32_t m = rvu(c);
         // readDeleteSet drops clients without ranges and merges a repeated client into its first
         // occurrence: either makes the re-written set differ from the input bytes
-        if (m == 0 || i >= 64) { declined = true; break; }
-        for (uint32_t h = 0; h < i; h++) declined |= at<uint32_t>(L_DSC + 4 * h) == client;
-        if (lane == 0) at<uint32_t>(L_DSC + 4 * i) = client;
+        if (m == 0 || i >= BS_NDSC) { declined = true; break; }
+        if (seen_before(X.dsc, i, client)) { declined = true; break; }
+        if (lane == 0) X.dsc[i] = client;
+        __threadfence_block();
         for (uint32_t q = 0; q < m && !c.bad; q++) {
           win_ensure(w, c, j.A);
           rvu(c);
@@ -344,13 +375,16 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
     const uint32_t ds1 = rel(w, c.p);
     __syncthreads();
     // ---- sizes, allocation
-    uint32_t total = vsz(nparts) + (ds1 - ds0);
-    for (uint32_t ci = 0; ci < nclients; ci++) {
+    __threadfence_block();
+    __syncthreads();
+    uint32_t tl = 0;
+    for (uint32_t ci = lane; ci < nclients; ci += 64) {
       const uint32_t pl = sec(ci, S_PRELEN);
       if (pl == NONE) continue;
-      total += vsz(sec(ci, S_WRITTEN)) + vsz(sec(ci, S_CLIENT)) + vsz(sec(ci, S_FCLOCK)) + pl +
-               (sec(ci, S_A1) - sec(ci, S_A0)) + (sec(ci, S_B1) - sec(ci, S_B0));
+      tl += vsz(sec(ci, S_WRITTEN)) + vsz(sec(ci, S_CLIENT)) + vsz(sec(ci, S_FCLOCK)) + pl +
+            (sec(ci, S_A1) - sec(ci, S_A0)) + (sec(ci, S_B1) - sec(ci, S_B0));
     }
+    const uint32_t total = vsz(nparts) + (ds1 - ds0) + lane_read(wave_incl_add(tl), 63);
     uint64_t base = 0;
     if (lane == 0) base = atomicAdd((unsigned long long *)j.used, (unsigned long long)total);
     base = ((uint64_t)lane_read((uint32_t)(base >> 32), 0) << 32) | lane_read((uint32_t)base, 0);
@@ -383,7 +417,7 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
           while (v > 127) { o[t++] = (uint8_t)(0x80 | (v & 127)); v >>= 7; }
           o[t++] = (uint8_t)v;
         }
-        for (uint32_t b = 0; b < pl; b++) o[t + b] = sm[L_PRE + ci * PRE + b];
+        for (uint32_t b = 0; b < pl; b++) o[t + b] = X.pre[ci * PRE + b];
       }
       p += vsz(written) + vsz(client) + vsz(fclock) + pl;
       const uint32_t a0 = sec(ci, S_A0), a1 = sec(ci, S_A1);
@@ -400,8 +434,8 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
     // patches: each lies in the B span of exactly one section (sections are disjoint, in order)
     for (uint32_t i = lane; i < npatch; i += 64) {
       const uint32_t pos = at<uint32_t>(L_PPOS + 4 * i);
-      for (uint32_t ci = 0; ci < nclients; ci++)
-        if (sec(ci, S_PRELEN) != NONE && pos >= sec(ci, S_B0) && pos < sec(ci, S_B1)) o[sec(ci, S_OUTB) + pos] = sm[L_PVAL + i];
+      const uint32_t ci = at<uint32_t>(L_PSEC + 4 * i);
+      if (pos >= sec(ci, S_B0) && pos < sec(ci, S_B1)) o[sec(ci, S_OUTB) + pos] = sm[L_PVAL + i];
     }
     if (lane == 0) {
       j.out_off[d] = base;
@@ -425,7 +459,7 @@ __global__ void k_big_init(GeneralJob j) {
 int big_launch(uint32_t op, const GeneralJob &j, hipStream_t st) {
   if (j.v2 || (op != OP_DIFF && op != OP_SV)) return 0;
   k_big_init<<<1, 64, 0, st>>>(j);
-  const uint32_t grid = j.n < 65536 ? j.n : 65536;
+  const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
   if (op == OP_DIFF) big::k_big_v1<OP_DIFF><<<grid, 64, big::LDS_BYTES, st>>>(j);
   else big::k_big_v1<OP_SV><<<grid, 64, big::LDS_BYTES, st>>>(j);
   return 1;

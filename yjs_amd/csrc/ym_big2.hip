@@ -28,7 +28,7 @@ enum { I_REST = 0, I_KC, I_CL, I_LC, I_RC, I_IN, I_SL, I_PI, I_TR, I_LN, NIN };
 enum { O_KC = 0, O_CL, O_LC, O_RC, O_IN, O_SB, O_SL, O_PI, O_TR, O_LN, O_REST, NOUT };
 constexpr uint32_t WREST = 4096, MREST = 1024;  // rest window / margin (any payloads live here)
 constexpr uint32_t WCOL = 256, MCOL = 24;       // column windows / margin (one varint or byte)
-constexpr uint32_t NSEC = 64, NSV = 256;
+constexpr uint32_t NSEC = BS_NSEC, NSV = BS_NSV;  // parts / state-vector entries (per-block HBM scratch)
 
 constexpr uint32_t L_WREST = 0;
 constexpr uint32_t L_WCOL = WREST + 16;                      // (NIN-1) x (WCOL + 16)
@@ -36,10 +36,7 @@ constexpr uint32_t L_IST = L_WCOL + (NIN - 1) * (WCOL + 16); // u32[NIN][4]: pos
 constexpr uint32_t L_DEC = L_IST + NIN * 16;                 // u32[NIN][4]: s, count, diff, (pad)  (RLE decoders)
 constexpr uint32_t L_OST = L_DEC + NIN * 16;                 // u32[NOUT][4]: base, cur, cap, (pad)
 constexpr uint32_t L_ENC = L_OST + NOUT * 16;                // u32[NOUT][4]: s, count, diff, started
-constexpr uint32_t L_SV = L_ENC + NOUT * 16;                 // u32[NSV][2]
-constexpr uint32_t L_PART = L_SV + NSV * 8;                  // u32[NSEC][4]: rest start, rest end, written
-constexpr uint32_t L_DSC = L_PART + NSEC * 16;               // u32[64] delete-set clients
-constexpr uint32_t L_MISC = L_DSC + 256;                     // u32[16]
+constexpr uint32_t L_MISC = L_ENC + NOUT * 16;               // u32[16]
 constexpr uint32_t LDS_BYTES = L_MISC + 64;
 
 __device__ __forceinline__ uint32_t &ist(uint32_t s, uint32_t f) { return at<uint32_t>(L_IST + 16 * s + 4 * f); }
@@ -52,6 +49,25 @@ __device__ __forceinline__ void set_bad() {
   if (threadIdx.x == 0) misc(M_BAD) = 1;
 }
 __device__ __forceinline__ bool is_bad() { return misc(M_BAD) != 0; }
+
+// per-block HBM scratch (ym_kernels.h BS_*): parts (rest start, rest end, written), state vector,
+// delete-set clients
+struct Scr {
+  uint32_t *part, *svt, *dsc;
+};
+__device__ __forceinline__ Scr scratch(const GeneralJob &j) {
+  uint8_t *b = j.bscratch + (uint64_t)blockIdx.x * BS_BYTES;
+  return Scr{(uint32_t *)(b + BS_SEC), (uint32_t *)(b + BS_SVT), (uint32_t *)(b + BS_DSC)};
+}
+__device__ __forceinline__ uint32_t sv_lookup(const uint32_t *svt, uint32_t nsv, uint32_t client) {
+  int best = -1;  // decodeStateVector: a later entry for the same client wins
+  for (uint32_t i0 = 0; i0 < nsv; i0 += 64) {
+    const uint32_t i = i0 + threadIdx.x;
+    const uint64_t m = __ballot(i < nsv && svt[2 * i] == client);
+    if (m) best = (int)(i0 + 63 - __builtin_clzll(m));
+  }
+  return best >= 0 ? svt[2 * best + 1] : 0;
+}
 
 struct Doc {
   const uint8_t *A;  // arena
@@ -402,6 +418,7 @@ __device__ void v2_write(const Doc &D, const Rec &r, uint32_t off, uint32_t clie
 template <int OP>
 __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
   const uint32_t lane = threadIdx.x;
+  const Scr X = scratch(j);
   for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
     const uint32_t u0 = j.doc_upd[d];
     if (j.doc_upd[d + 1] - u0 != 1) YB2_DECLINE()
@@ -418,7 +435,7 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
     uint32_t nsv = 0;
     if (OP == OP_DIFF) {
       const uint64_t s0 = j.sv_off[d], s1 = j.sv_off[d + 1];
-      if (s1 - s0 > 4 * NSV * 5 + 8) YB2_DECLINE()
+      if (s1 - s0 > WREST - 32) YB2_DECLINE()
       const uint64_t a = s0 & ~15ull;
       const uint4 *src = reinterpret_cast<const uint4 *>(j.sv + a);
       for (uint32_t v = lane; v < (uint32_t)((s1 - a + 15) >> 4); v += 64) at<uint4>(L_WREST + 16 * v) = src[v];
@@ -428,11 +445,12 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
       for (uint32_t i = 0; i < n && !c.bad; i++) {
         const uint32_t cl = rvu(c), ck = rvu(c);
         if (nsv >= NSV) { c.bad = true; break; }
-        if (lane == 0) { at<uint32_t>(L_SV + 8 * nsv) = cl; at<uint32_t>(L_SV + 8 * nsv + 4) = ck; }
+        if (lane == 0) { X.svt[2 * nsv] = cl; X.svt[2 * nsv + 1] = ck; }
         nsv++;
       }
-      if (c.bad) YB2_DECLINE()
+      __threadfence_block();
       __syncthreads();
+      if (c.bad) YB2_DECLINE()
     }
     // ---- header: feature flag, nine columns (UpdateDecoderV2 constructor, UpdateDecoder.js:274-293)
     if (lane == 0) { ist(I_REST, 0) = 0; ist(I_REST, 1) = D.len; }
@@ -506,14 +524,11 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
       uint64_t clock = s_vu(D, I_REST);
       if (ci > 0 && client == prev_client) { set_bad(); break; }
       prev_client = client;
-      uint32_t k = 0;
-      if (OP == OP_DIFF)
-        for (uint32_t i = 0; i < nsv; i++)
-          if (at<uint32_t>(L_SV + 8 * i) == client) k = at<uint32_t>(L_SV + 8 * i + 4);
+      const uint32_t k = OP == OP_DIFF ? sv_lookup(X.svt, nsv, client) : 0;
       if (OP == OP_SV && nstructs > 0 && sv_any && client != sv_client) {
         if (sv_clock != 0) {
           if (sv_n >= NSV) { set_bad(); break; }
-          if (lane == 0) { at<uint32_t>(L_SV + 8 * sv_n) = sv_client; at<uint32_t>(L_SV + 8 * sv_n + 4) = sv_clock; }
+          if (lane == 0) { X.svt[2 * sv_n] = sv_client; X.svt[2 * sv_n + 1] = sv_clock; }
           sv_n++;
         }
         sv_client = client; sv_clock = 0; sv_stop = clock != 0;
@@ -547,9 +562,9 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
       if (OP == OP_DIFF && copying) {
         if (nparts >= NSEC) { set_bad(); break; }
         if (lane == 0) {
-          at<uint32_t>(L_PART + 16 * nparts) = prest0;
-          at<uint32_t>(L_PART + 16 * nparts + 4) = ost(O_REST, 1);
-          at<uint32_t>(L_PART + 16 * nparts + 8) = written;
+          X.part[4 * nparts] = prest0;
+          X.part[4 * nparts + 1] = ost(O_REST, 1);
+          X.part[4 * nparts + 2] = written;
         }
         nparts++;
         __syncthreads();
@@ -558,12 +573,15 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
     if (is_bad()) YB2_DECLINE()
     if (OP == OP_SV) {
       if (sv_any && sv_clock != 0) {
-        if (lane == 0) { at<uint32_t>(L_SV + 8 * sv_n) = sv_client; at<uint32_t>(L_SV + 8 * sv_n + 4) = sv_clock; }
+        if (sv_n >= NSV) YB2_DECLINE()
+        if (lane == 0) { X.svt[2 * sv_n] = sv_client; X.svt[2 * sv_n + 1] = sv_clock; }
         sv_n++;
       }
+      __threadfence_block();
       __syncthreads();
-      uint32_t total = vsz(sv_n);
-      for (uint32_t i = 0; i < sv_n; i++) total += vsz(at<uint32_t>(L_SV + 8 * i)) + vsz(at<uint32_t>(L_SV + 8 * i + 4));
+      uint32_t tl = 0;
+      for (uint32_t i = lane; i < sv_n; i += 64) tl += vsz(X.svt[2 * i]) + vsz(X.svt[2 * i + 1]);
+      const uint32_t total = vsz(sv_n) + lane_read(wave_incl_add(tl), 63);
       uint64_t base = 0;
       if (lane == 0) base = atomicAdd((unsigned long long *)j.used, (unsigned long long)total);
       base = ((uint64_t)lane_read((uint32_t)(base >> 32), 0) << 32) | lane_read((uint32_t)base, 0);
@@ -577,7 +595,7 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
         uint32_t p = 0;
         auto put = [&](uint32_t v) { while (v > 127) { o[p++] = (uint8_t)(0x80 | (v & 127)); v >>= 7; } o[p++] = (uint8_t)v; };
         put(sv_n);
-        for (uint32_t i = 0; i < sv_n; i++) { put(at<uint32_t>(L_SV + 8 * i)); put(at<uint32_t>(L_SV + 8 * i + 4)); }
+        for (uint32_t i = 0; i < sv_n; i++) { put(X.svt[2 * i]); put(X.svt[2 * i + 1]); }
         j.out_off[d] = base;
         j.out_len[d] = total;
         j.status[d] = ym::ST_OK;
@@ -597,10 +615,13 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
         const uint32_t client = rvu(c);
         const uint32_t m = rvu(c);
         s_commit(I_REST, c);
-        if (m == 0 || i >= 64) { set_bad(); break; }
-        for (uint32_t h = 0; h < i; h++) if (at<uint32_t>(L_DSC + 4 * h) == client) set_bad();
+        if (m == 0 || i >= BS_NDSC) { set_bad(); break; }
+        bool hit = false;  // readDeleteSet merges a repeated client: the bytes would change
+        for (uint32_t h0 = 0; h0 < i; h0 += 64) hit |= __any(h0 + lane < i && X.dsc[h0 + lane] == client);
+        if (hit) set_bad();
         __syncthreads();
-        if (lane == 0) at<uint32_t>(L_DSC + 4 * i) = client;
+        if (lane == 0) X.dsc[i] = client;
+        __threadfence_block();
         for (uint32_t q = 0; q < m && !is_bad(); q++) {
           c = s_cur(D, I_REST, MREST);
           rvu(c);
@@ -629,8 +650,13 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
     uint32_t total = 1;
     for (uint32_t k = 0; k < 9; k++) total += vsz(coln[k]) + coln[k];
     total += vsz(nparts);
-    for (uint32_t pI = 0; pI < nparts; pI++)
-      total += vsz(at<uint32_t>(L_PART + 16 * pI + 8)) + at<uint32_t>(L_PART + 16 * pI + 4) - at<uint32_t>(L_PART + 16 * pI);
+    __threadfence_block();
+    __syncthreads();
+    {
+      uint32_t tl = 0;
+      for (uint32_t pI = lane; pI < nparts; pI += 64) tl += vsz(X.part[4 * pI + 2]) + X.part[4 * pI + 1] - X.part[4 * pI];
+      total += lane_read(wave_incl_add(tl), 63);
+    }
     total += ds1 - ds0;
     uint64_t base = 0;
     if (lane == 0) base = atomicAdd((unsigned long long *)j.used, (unsigned long long)total);
@@ -668,8 +694,8 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
     }
     p = put(p, nparts);
     for (uint32_t pI = 0; pI < nparts; pI++) {
-      const uint32_t r0 = at<uint32_t>(L_PART + 16 * pI), r1 = at<uint32_t>(L_PART + 16 * pI + 4);
-      p = put(p, at<uint32_t>(L_PART + 16 * pI + 8));
+      const uint32_t r0 = X.part[4 * pI], r1 = X.part[4 * pI + 1];
+      p = put(p, X.part[4 * pI + 2]);
       p = copy(p, sc + ost(O_REST, 0) + r0, r1 - r0);
     }
     p = copy(p, D.A + D.b0 + ds0, ds1 - ds0);
@@ -688,7 +714,7 @@ __global__ void k_big_init(GeneralJob j);  // ym_big.hip
 int big2_launch(uint32_t op, const GeneralJob &j, hipStream_t st) {
   if (!j.v2 || (op != OP_SV && op != OP_DIFF)) return 0;
   k_big_init<<<1, 64, 0, st>>>(j);
-  const uint32_t grid = j.n < 65536 ? j.n : 65536;
+  const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
   if (op == OP_DIFF) big2::k_big_v2<OP_DIFF><<<grid, 64, big2::LDS_BYTES, st>>>(j);
   else big2::k_big_v2<OP_SV><<<grid, 64, big2::LDS_BYTES, st>>>(j);
   return 1;

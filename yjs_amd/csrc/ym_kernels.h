@@ -33,7 +33,19 @@ struct GeneralJob {
   uint32_t *counter_retry;
   uint32_t *pend_list;       // fast path: ids of the documents it declines (appended) ...
   uint32_t *pend_count;      // ... and their number
+  uint8_t *bscratch;         // streamed single-update kernels: BS_BYTES per block (ym_big*.hip)
 };
+
+// Per-block HBM scratch of the streamed diff / state-vector kernels (ym_big.hip, ym_big2.hip): client
+// sections (or parts), the decoded state vector and the delete set's clients.  Grid = BS_GRID blocks
+// (grid-stride over documents), so the scratch is bounded whatever the batch size.
+constexpr uint32_t BS_NSEC = 2048, BS_NSV = 2048, BS_NDSC = 2048, BS_PRE = 48, BS_SECW = 12;
+constexpr uint64_t BS_SEC = 0;                                      // u32[BS_NSEC][BS_SECW]
+constexpr uint64_t BS_PREB = BS_SEC + 4ull * BS_NSEC * BS_SECW;     // u8[BS_NSEC][BS_PRE]
+constexpr uint64_t BS_SVT = BS_PREB + (uint64_t)BS_NSEC * BS_PRE;   // u32[BS_NSV][2]
+constexpr uint64_t BS_DSC = BS_SVT + 8ull * BS_NSV;                 // u32[BS_NDSC]
+constexpr uint64_t BS_BYTES = BS_DSC + 4ull * BS_NDSC;
+constexpr uint32_t BS_GRID = 2048;
 
 // device buffers of the large-document merge pipeline (ym_large.hip), grown on demand, cached
 struct LargeBufs {
