@@ -32,6 +32,8 @@ WORKLOADS = {
     "c2": ("c2_v1", 1, "C2: 10k docs x 100 Y.Text updates (4 clients), batched mergeUpdates V1"),
     "c2v2": ("c2_v2", 2, "C2 shape, batched mergeUpdatesV2"),
     "c4": ("c4_v1", 1, "C4: Y.Map docs, 64 clients, 128 broadcast tx, delete-heavy, mergeUpdates V1"),
+    "c5": ("c5_v1", 1, "C5: Y.XmlFragment docs, 1,024 clients x 16 tx (~16 k updates), mergeUpdates V1"),
+    "c5v2": ("c5_v2", 2, "C5: Y.XmlFragment docs, 1,024 clients x 16 tx (~16 k updates), mergeUpdatesV2"),
 }
 
 
@@ -79,20 +81,33 @@ def cpu_baseline(arena, upd_off, doc_upd, fmt, seconds):
 def secondary(dev, eng):
     """Quick device-resident measurements of the other BASELINE.json workloads (1 GPU): C4 and V2
     merges (10k docs), C3 diffUpdate / encodeStateVectorFromUpdate (configs[2]: 4,096 V1 docs of
-    0.9 MB; 1,024 V2 docs) against random state vectors.  Whole-call GB/s of input."""
+    0.9 MB; 1,024 V2 docs) against random state vectors, C5 (configs[4]: 256 docs of ~16 k updates
+    from 1,024 clients) mergeUpdates[V2] and diffUpdate[V2] of the merged documents against random
+    per-client state vectors.  Whole-call GB/s of input."""
     import torch
     from yjs_amd import pack_docs
     from yjs_amd.workloads import load_ymb, replicate, random_state_vectors
     res = {}
     cases = [("merge_c4_v1", "merge", "c4_v1", 10000), ("merge_c2_v2", "merge", "c2_v2", 10000),
              ("merge_c4_v2", "merge", "c4_v2", 10000), ("diff_c3_v1", "diff", "c3_v1", 4096),
-             ("sv_c3_v1", "sv", "c3_v1", 4096), ("diff_c3_v2", "diff", "c3_v2", 1024)]
+             ("sv_c3_v1", "sv", "c3_v1", 4096), ("diff_c3_v2", "diff", "c3_v2", 1024),
+             ("merge_c5_v1", "merge", "c5_v1", 256), ("merge_c5_v2", "merge", "c5_v2", 256),
+             ("diff_c5_v1", "diff", "c5_v1", 256), ("diff_c5_v2", "diff", "c5_v2", 256)]
     for name, op, wl, n in cases:
         fmt = 2 if wl.endswith("v2") else 1
         a, o, d = load_ymb(wl)
         sva = svo = None
         if op == "merge":
             a, o, d = replicate(a, o, d, n)
+        elif wl.startswith("c5"):
+            # the merged C5 documents (merged here by the engine), random per-client state vectors
+            ma, mo, ml, _ = eng.run_host("merge", fmt, a, o, d)
+            ups = [ma[int(mo[i]):int(mo[i]) + int(ml[i])].tobytes() for i in range(len(d) - 1)]
+            sa, so_, sl, _ = eng.run_host("sv", fmt, *pack_docs([[u] for u in ups]))
+            fulls = [sa[int(so_[i]):int(so_[i]) + int(sl[i])].tobytes() for i in range(len(ups))]
+            svs = [random_state_vectors(fulls[i % len(ups)], 1, seed=i)[0] for i in range(n)]
+            a, o, d = pack_docs([[ups[i % len(ups)]] for i in range(n)])
+            sva, svo, _ = pack_docs([[x] for x in svs])
         else:
             upd = a.tobytes()
             a, o, d = replicate(a, o, d, n)  # n copies of the single C3 update
@@ -120,14 +135,15 @@ def secondary(dev, eng):
         for _ in range(steps):
             rc, _ = eng.run_device(op, fmt, ga, go, gd, oa, oo, ol, st, gsa, gso)
             assert rc == 0, rc
-            kms.append(eng.last_stats.fast_ms)
+            kms.append(eng.last_stats.fast_ms + eng.last_stats.large_ms)
         torch.cuda.synchronize(dev)
         el = (time.perf_counter() - t0) / steps
         sts = eng.stats
         res[name] = {"docs": nd, "input_bytes": int(len(a)), "value_gbs": round(len(a) / el / 1e9, 3),
                      "docs_per_s": round(nd / el, 1), "ms_per_step": round(el * 1e3, 3),
                      "kernel_ms": round(float(np.mean(kms)), 3), "docs_fast": int(sts["docs_fast"]),
-                     "docs_general": int(sts["docs_general"]), "errors": int(sts["docs_error"])}
+                     "docs_large": int(sts["docs_large"]), "docs_general": int(sts["docs_general"]),
+                     "errors": int(sts["docs_error"])}
         del ga, go, gd, gsa, gso, oa, oo, ol, st
         torch.cuda.empty_cache()
     return res
@@ -203,7 +219,7 @@ def main():
     for _ in range(args.steps):
         step()
         s = eng.last_stats
-        fast_ms.append(s.fast_ms)
+        fast_ms.append(s.fast_ms + s.large_ms)  # LDS fast path, or the large-document pipeline (C5)
         dev_ms.append(s.device_ms)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -223,6 +239,9 @@ def main():
         # roofline of the dominant kernel (fast-path merge): algorithmic bytes per launch / avg launch time
         avg_fast = float(np.mean(fast_ms)) if fast_ms else 0.0
         alg_bytes = float(in_bytes + out_bytes)  # per launch on this rank (all docs take the fast path)
+        kernel_name = {1: "k_fast_merge_v1", 2: "k_fast_merge_v2"}[fmt]
+        if st0["docs_large"]:
+            kernel_name = "large-document pipeline (ym_large.hip: walk, segmented sorts, k_lm_doc)"
         achieved = alg_bytes / (avg_fast * 1e-3) / 1e9 if avg_fast > 0 else 0.0
         traffic = None
         pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
@@ -243,8 +262,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic: yjs 13.5.16-generated C2 document templates (bench_data/, seeds 1..1024) "
-                    "replicated to docs_per_gpu distinct copies per rank",
+            "data": f"synthetic: yjs 13.5.16-generated {tname} document templates (bench_data/, recipe "
+                    "oracle/gen/make_bench_data.cjs) replicated to docs_per_gpu distinct copies per rank",
             "config": {"workload": desc, "docs_per_gpu": n_docs, "updates_per_gpu": int(doc_upd[-1]),
                        "input_bytes_per_gpu": in_bytes, "output_bytes_per_gpu": out_bytes, "format": f"v{fmt}",
                        "parallelism": f"docs sharded over {world} GPU(s), no collective in the hot path"},
@@ -252,7 +271,7 @@ def main():
             "hbm_frac_in_plus_out": round((in_all + out_all) * args.steps / elapsed / 1e9 / (HBM_PEAK_GBS * world), 5),
             "docs_fast_path": int(fast_all), "docs_general_path": int(gen_all), "doc_errors": int(err_all),
             "device_ms_per_step": round(float(np.mean(dev_ms)), 4),
-            "roofline": {"kernel": "k_fast_merge_v1", "bound": "hbm", "achieved": round(achieved, 2),
+            "roofline": {"kernel": kernel_name, "bound": "hbm", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "avg_launch_ms": round(avg_fast, 5),
                          "algorithmic_bytes_per_launch": int(alg_bytes)},
