@@ -198,8 +198,10 @@ def main():
     o_st = torch.empty(n_docs, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
 
+    call = eng.prepare_device("merge", fmt, g_arena, g_off, g_doc, o_arena, o_off, o_len, o_st, stream=stream)
+
     def step():
-        rc, used = eng.run_device("merge", fmt, g_arena, g_off, g_doc, o_arena, o_off, o_len, o_st, stream=stream)
+        rc, used = call()
         if rc != 0:
             raise RuntimeError(f"ym_merge rc={rc}")
         return used

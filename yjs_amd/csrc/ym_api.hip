@@ -23,6 +23,7 @@ int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st
 int fast2_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st); // ym_fast2.hip
 int big_launch(uint32_t op, const GeneralJob &j, hipStream_t st);                    // ym_big.hip
 int big2_launch(uint32_t op, const GeneralJob &j, hipStream_t st);                   // ym_big2.hip
+__global__ void k_fast_region(GeneralJob j, uint32_t n_upd);                         // ym_fast.hip
 }  // namespace ymk
 
 using namespace ymk;
@@ -59,7 +60,9 @@ struct DevState {
   DBuf in_arena, in_off, in_doc, in_sv, in_svoff, out_arena, out_off, out_len, status;  // host staging
   LargeBufs large;
   hipEvent_t evl1 = nullptr;
-  uint64_t *pinned = nullptr;
+  uint64_t *pinned = nullptr;   // host memory the finishing kernel writes into (no copy op)
+  uint64_t *pinned_dev = nullptr;  // ... its device address
+  bool dirty = true;            // device counters not known to be reset (first call, failed call)
 };
 
 thread_local DevState *g_state = nullptr;
@@ -83,7 +86,9 @@ DevState *state() {
     hipEventCreate(&g_state->evf1);
     hipEventCreate(&g_state->evg1);
     hipEventCreate(&g_state->evl1);
-    hipHostMalloc((void **)&g_state->pinned, 64 * sizeof(uint64_t), hipHostMallocDefault);
+    // fine-grained (coherent) host memory: the finishing kernel's stores reach it directly
+    hipHostMalloc((void **)&g_state->pinned, 64 * sizeof(uint64_t), hipHostMallocCoherent | hipHostMallocMapped);
+    hipHostGetDevicePointer((void **)&g_state->pinned_dev, g_state->pinned, 0);
   }
   return g_state;
 }
@@ -95,12 +100,15 @@ __global__ void k_status_flags(const uint32_t *list, uint32_t n, const int32_t *
   flags[i] = status[d] == want;
 }
 
-// per-call counters in one single-block launch (no atomics, no memset): errors, bytes out, bytes in
-__global__ void __launch_bounds__(1024) k_stats(const int32_t *status, const uint64_t *out_len, uint32_t n,
-                                                const uint64_t *upd_off, uint32_t n_upd, uint64_t *acc) {
+// The last kernel of every host round trip (one single-block launch, no atomics, no copy op): writes
+// the bump-allocator position, the declined count and (stats) errors / bytes out / bytes in straight
+// into pinned host memory, and resets the declined-document counter for the next launch.
+__global__ void __launch_bounds__(1024) k_finish(const int32_t *status, const uint64_t *out_len, uint32_t n,
+                                                 const uint64_t *upd_off, uint32_t n_upd, uint64_t *counters,
+                                                 volatile uint64_t *host, int stats, int merge) {
   __shared__ unsigned long long red[2][16];
   uint64_t err = 0, bytes = 0;
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+  for (uint32_t i = threadIdx.x; stats && i < n; i += blockDim.x) {
     const bool ok = status[i] == 0;
     err += !ok;
     bytes += ok ? out_len[i] : 0;
@@ -115,9 +123,15 @@ __global__ void __launch_bounds__(1024) k_stats(const int32_t *status, const uin
   if (threadIdx.x == 0) {
     uint64_t e = 0, b = 0;
     for (uint32_t k = 0; k < blockDim.x / 64; k++) { e += red[0][k]; b += red[1][k]; }
-    acc[0] = e;
-    acc[1] = b;
-    acc[2] = upd_off[n_upd] - upd_off[0];
+    // used: the bump allocator; merges also own the fast / large paths' slot region [0, 2 in + 64 n + 64)
+    const uint64_t region = merge ? 2 * (upd_off[n_upd] - upd_off[0]) + 64ull * n + 64 : 0;
+    host[0] = counters[0] > region ? counters[0] : region;
+    host[2] = counters[2] & 0xffffffffull;       // declined documents (the work list length)
+    host[4] = e;
+    host[5] = b;
+    host[6] = upd_off[n_upd] - upd_off[0];
+    ((uint32_t *)counters)[4] = 0;               // pend_count (counters + 2) := 0 for the next launch
+    __threadfence_system();
   }
 }
 
@@ -249,7 +263,16 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
     j.bscratch = S->bscratch.as<uint8_t>();
   }
 
-  auto stats_launch = [&]() { k_stats<<<1, 1024, 0, st>>>(o_status, o_len, nd, upd_off, b->n_upd, counters + 4); };
+  if (S->dirty) HIPCHK(hipMemsetAsync(counters, 0, 256, st));
+  S->dirty = true;
+  // ends a round trip: counters and stats land in pinned host memory, then one stream sync
+  auto finish = [&]() -> int {
+    k_finish<<<1, 1024, 0, st>>>(o_status, o_len, nd, upd_off, b->n_upd, counters, S->pinned_dev, stats ? 1 : 0,
+                                   op == OP_MERGE ? 1 : 0);
+    HIPCHK(hipEventRecord(S->ev1, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return 0;
+  };
   HIPCHK(hipEventRecord(S->ev0, st));
   // (1) fast path over every document; appends the ones it declines to list_a
   HIPCHK(hipEventRecord(S->evf0, st));
@@ -263,14 +286,9 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   uint32_t *list = nullptr;
   if (fr == 1) {
     // one round trip: used, the declined count and (speculatively) the stats of the fast-only case
-    if (stats) stats_launch();
-    HIPCHK(hipEventRecord(S->ev1, st));
-    HIPCHK(hipMemcpyAsync(S->pinned, counters, stats ? 56 : 24, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    if (int r = finish()) return r;
     ngen = (uint32_t)(S->pinned[2] & 0xffffffffu);
     list = S->list_a.as<uint32_t>();
-  } else {
-    HIPCHK(hipMemsetAsync(counters, 0, 256, st));
   }
   // (2) large-document merges (ym_large.hip) over the declined list; what it declines stays pending
   uint32_t nlarge = 0;
@@ -286,24 +304,19 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
       nlarge = ngen - cnt;
       ngen = cnt;
       list = S->list_b.as<uint32_t>();
-      if (ngen == 0) {
-        if (stats) stats_launch();
-        HIPCHK(hipEventRecord(S->ev1, st));
-        HIPCHK(hipMemcpyAsync(S->pinned, counters, stats ? 56 : 8, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-      }
+      if (ngen == 0)
+        if (int r = finish()) return r;
     }
   }
   // (3) general path over the rest
   if (ngen > 0) {
+    if (op == OP_MERGE) k_fast_region<<<1, 64, 0, st>>>(j, b->n_upd);  // bump allocator after the slots
     int r = run_general(S, st, j, list, ngen);
     if (r) return r;
     HIPCHK(hipEventRecord(S->evg1, st));
-    if (stats) stats_launch();
-    HIPCHK(hipEventRecord(S->ev1, st));
-    HIPCHK(hipMemcpyAsync(S->pinned, counters, stats ? 56 : 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    if (int r2 = finish()) return r2;
   }
+  S->dirty = false;
   uint64_t used = S->pinned[0];
   out->used = used;
   if (stats) {

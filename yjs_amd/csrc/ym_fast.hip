@@ -614,18 +614,16 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
 
 }  // namespace fastv1
 
-// the general path's bump allocator starts after the fast path's slot region; empty work list
+// merges: the general path's bump allocator starts after the fast paths' slot region (launched by
+// the host only when documents were declined)
 __global__ void k_fast_region(GeneralJob j, uint32_t n_upd) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
-    *j.used = 2 * (j.upd_off[n_upd] - j.upd_off[0]) + 64ull * j.n + 64;
-    *j.pend_count = 0;
-  }
+  if (threadIdx.x == 0 && blockIdx.x == 0) *j.used = 2 * (j.upd_off[n_upd] - j.upd_off[0]) + 64ull * j.n + 64;
 }
 
 int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st) {
   using namespace fastv1;
   if (op != OP_MERGE || j.v2) return 0;  // fast path: V1 merges (the C2/C4 headline configs)
-  k_fast_region<<<1, 64, 0, st>>>(j, n_upd);
+  (void)n_upd;  // the work-list counter is zero on entry (ym_api.hip k_finish); `used` is set later
   const uint32_t grid = j.n < 131072 ? j.n : 131072;
   static int stop = -1, pad = 0;
   if (stop < 0) {

@@ -899,11 +899,10 @@ __global__ void __launch_bounds__(64) k_fast_merge_v2(GeneralJob j) {
 
 }  // namespace fastv2
 
-__global__ void k_fast_region(GeneralJob j, uint32_t n_upd);  // ym_fast.hip
 
 int fast2_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st) {
   if (op != OP_MERGE || !j.v2) return 0;
-  k_fast_region<<<1, 64, 0, st>>>(j, n_upd);
+  (void)n_upd;
   const uint32_t grid = j.n < 131072 ? j.n : 131072;
   fastv2::k_fast_merge_v2<<<grid, 64, fastv2::LDS_BYTES, st>>>(j);
   return 1;
