@@ -20,21 +20,19 @@
 
 #include "ym_fast_common.h"
 #include "ym_kernels.h"
+#include "ym_scalar.h"
 
 namespace ymk {
 namespace big {
 using namespace fastc;
-
-constexpr uint32_t BW = 8192;   // LDS window over the update
-constexpr uint32_t BM = 2048;   // refill when fewer bytes remain ahead of the cursor (max struct size)
+using sc::SCur;
 constexpr uint32_t NSEC = BS_NSEC;  // client sections per update (HBM scratch, per block)
 constexpr uint32_t NSV = BS_NSV;    // state-vector entries (HBM scratch)
 constexpr uint32_t NPATCH = 512;
 constexpr uint32_t PRE = BS_PRE;    // sliced-struct prefix bytes per section
 
 constexpr uint32_t SECW = BS_SECW;  // u32 fields per section record
-constexpr uint32_t L_WIN = 0;                        // u8[BW + 16]
-constexpr uint32_t L_PRE = BW + 16;                  // u8[PRE] the current section's sliced-struct head
+constexpr uint32_t L_PRE = 0;                        // u8[PRE] the current section's sliced-struct head
 constexpr uint32_t L_PPOS = L_PRE + PRE;             // u32[NPATCH] patch positions (update-relative)
 constexpr uint32_t L_PVAL = L_PPOS + 4 * NPATCH;     // u8[NPATCH]  patched info bytes
 constexpr uint32_t L_PSEC = L_PVAL + NPATCH;         // u32[NPATCH] section of each patch
@@ -75,37 +73,12 @@ __device__ __forceinline__ bool seen_before(const uint32_t *dsc, uint32_t n, uin
   return hit;
 }
 
-// window over the update [0, len) at absolute arena offset b0; LDS byte i <-> arena byte wa + i
-struct Win {
-  uint64_t wa;     // absolute arena offset of LDS byte 0 (16-aligned)
-  uint64_t b0;     // absolute offset of the update
-  uint32_t len;    // update bytes
-  uint32_t wend;   // LDS offset one past the last usable byte
-};
-__device__ __forceinline__ uint32_t rel(const Win &w, uint32_t p) { return (uint32_t)(w.wa + p - w.b0); }
-
-// (re)load the window so that update byte `r` is near its start; all lanes participate
-__device__ __forceinline__ void win_load(Win &w, const uint8_t *A, uint32_t r) {
-  __syncthreads();
-  const uint64_t abs = w.b0 + r;
-  w.wa = abs & ~15ull;
-  const uint64_t end = w.b0 + w.len;  // exclusive
-  const uint64_t wend_abs = w.wa + BW < end ? w.wa + BW : end;
-  w.wend = (uint32_t)(wend_abs - w.wa);
-  const uint32_t nvec = (w.wend + 15) >> 4;
-  const uint4 *src = reinterpret_cast<const uint4 *>(A + w.wa);
-  for (uint32_t v = threadIdx.x; v < nvec; v += 64) at<uint4>(L_WIN + 16 * v) = src[v];
-  __syncthreads();
-}
-// keeps at least BM bytes (or the rest of the update) ahead of cursor c in the window
-__device__ __forceinline__ void win_ensure(Win &w, Cur &c, const uint8_t *A) {
-  if (c.p + BM > w.wend && w.wa + w.wend < w.b0 + w.len) {
-    const uint32_t r = rel(w, c.p), re = rel(w, c.e);
-    win_load(w, A, r);
-    c.p = (uint32_t)(w.b0 + r - w.wa);
-    c.e = w.wend;  // the update's end when it lies inside the window, else the window's end
-    (void)re;
-  }
+// wave copy of n bytes (any alignment): 16-byte unaligned vector accesses, then the tail bytes
+typedef uint4 __attribute__((aligned(1))) u4u;
+__device__ __forceinline__ void copy_bytes(uint8_t *dst, const uint8_t *src, uint32_t n) {
+  const uint32_t nv = n >> 4;
+  for (uint32_t v = threadIdx.x; v < nv; v += 64) reinterpret_cast<u4u *>(dst)[v] = reinterpret_cast<const u4u *>(src)[v];
+  for (uint32_t i = (nv << 4) + threadIdx.x; i < n; i += 64) dst[i] = src[i];
 }
 __device__ __forceinline__ uint32_t put_vu_lds(uint32_t p, uint32_t v) {
   while (v > 127) { sm[p++] = (uint8_t)(0x80 | (v & 127)); v >>= 7; }
@@ -131,28 +104,24 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
   for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
     const uint32_t u0 = j.doc_upd[d];
     if (j.doc_upd[d + 1] - u0 != 1) YB_DECLINE()
-    Win w;
-    w.b0 = j.upd_off[u0];
-    const uint64_t len64 = j.upd_off[u0 + 1] - w.b0;
+    // the update, read by scalar loads (ym_scalar.h): byte offsets from a dword-aligned base
+    const uint64_t ub = j.upd_off[u0];
+    const uint64_t len64 = j.upd_off[u0 + 1] - ub;
     if (len64 == 0 || len64 > 0xfffffff0ull) YB_DECLINE()
-    w.len = (uint32_t)len64;
+    sc::cu32 *const B = sc::base_of(j.A + ub);
+    const uint32_t adj = (uint32_t)(ub & 3);
+    auto rel = [&](uint32_t x) { return x - adj; };  // base offset -> update-relative
     // ---- state vector (diff): decodeStateVector, later entries win (encoding.js:536-545)
     uint32_t nsv = 0;
     bool bad = false;
     if (OP == OP_DIFF) {
       const uint64_t s0 = j.sv_off[d], s1 = j.sv_off[d + 1];
-      if (s1 - s0 > BW - 32) YB_DECLINE()
-      // the state vector is tiny: stage it through the window
+      if (s1 - s0 > 16ull * NSV) YB_DECLINE()
       {
-        const uint64_t a = s0 & ~15ull;
-        const uint32_t nvec = (uint32_t)((s1 - a + 15) >> 4);
-        const uint4 *src = reinterpret_cast<const uint4 *>(j.sv + a);
-        for (uint32_t v = lane; v < nvec; v += 64) at<uint4>(L_WIN + 16 * v) = src[v];
-        __syncthreads();
-        Cur c = {(uint32_t)(s0 - a), (uint32_t)(s1 - a), false};
-        const uint32_t n = rvu(c);
+        SCur c = sc::make(sc::base_of(j.sv + s0), (uint32_t)(s0 & 3), (uint32_t)(s0 & 3) + (uint32_t)(s1 - s0));
+        const uint32_t n = sc::rvu(c);
         for (uint32_t i = 0; i < n && !c.bad; i++) {
-          const uint32_t cl = rvu(c), ck = rvu(c);
+          const uint32_t cl = sc::rvu(c), ck = sc::rvu(c);
           if (nsv >= NSV) { c.bad = true; break; }
           if (lane == 0) { X.svt[2 * nsv] = cl; X.svt[2 * nsv + 1] = ck; }
           nsv++;
@@ -163,8 +132,7 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
       if (bad) YB_DECLINE()
     }
     // ---- struct section (encoding.js:127-198 layout; 13.5.16 LazyStructReader)
-    win_load(w, j.A, 0);
-    Cur c = {(uint32_t)(w.b0 - w.wa), w.wend, false};
+    SCur c = sc::make(B, adj, adj + (uint32_t)len64);
     const uint32_t nclients = rvu(c);
     if (nclients > NSEC) YB_DECLINE()
     uint32_t nparts = 0, npatch = 0, body_bytes = 0;
@@ -174,7 +142,6 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
     uint32_t prev_client = 0;
     bool declined = false;
     for (uint32_t ci = 0; ci < nclients && !c.bad && !declined; ci++) {
-      win_ensure(w, c, j.A);
       const uint32_t nstructs = rvu(c);
       const uint32_t client = rvu(c);
       uint64_t clock = rvu(c);
@@ -192,14 +159,13 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
       bool copying = false;
       uint32_t written = 0, b0r = 0;
       for (uint32_t si = 0; si < nstructs && !c.bad; si++) {
-        win_ensure(w, c, j.A);
         const uint32_t s0 = c.p;
         const uint32_t info = rdb(c);
         uint32_t len;
         const bool skip = info == 10, gc = !skip && (info & 31) == 0;
         if (skip || gc) len = rvu(c);
         else if (!item_body(c, info, len)) { declined = true; break; }
-        if (c.bad || c.p > w.wend) { declined = true; break; }
+        if (c.bad || c.p > c.e) { declined = true; break; }
         if (clock + len > 0xffffffffull) { declined = true; break; }
         if (OP == OP_SV) {
           if (!sv_any) {  // the update's first struct initialises the state
@@ -218,7 +184,7 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
             const uint32_t pre = L_PRE;
             uint32_t q = pre, a0 = 0, a1 = 0;
             if (off == 0) {
-              b0r = rel(w, s0);
+              b0r = rel(s0);
               const uint32_t ni = gc ? 0 : ((info & 0xC0) ? info & ~0x20u : info);
               if (ni != info) {
                 if (npatch >= NPATCH) { declined = true; break; }
@@ -227,7 +193,7 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
               }
             } else {
               // Item.write / GC.write with offset: re-encode the head, copy the content's tail
-              Cur e = {s0 + 1, c.p, false};
+              SCur e = sc::make(B, s0 + 1, c.p);
               const uint32_t ref = info & 31;
               if (gc) {
                 if (lane == 0) { sm[q] = 0; put_vu_lds(q + 1, len - off); }
@@ -242,15 +208,15 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
                 if (info & 0x40) { ro0 = e.p; skvu(e); skvu(e); ro1 = e.p; }
                 if ((info & 0xC0) == 0) {
                   const uint32_t pi = rvu(e);
-                  if (pi == 1) { const uint32_t n = rvu(e); e.p += n; }
+                  if (pi == 1) { const uint32_t n = rvu(e); sc::skip(e, n); }
                   else { skvu(e); skvu(e); }
-                  if (info & 0x20) { const uint32_t n = rvu(e); e.p += n; }
+                  if (info & 0x20) { const uint32_t n = rvu(e); sc::skip(e, n); }
                 }
                 if (lane == 0) {
                   sm[q] = (uint8_t)ni;
                   uint32_t t = put_vu_lds(q + 1, client);
                   t = put_vu_lds(t, (uint32_t)(clock + off - 1));
-                  for (uint32_t b = ro0; b < ro1; b++) sm[t++] = sm[b];
+                  for (uint32_t b = ro0; b < ro1; b++) sm[t++] = (uint8_t)sc::byte(B, b);
                 }
                 q += 1 + vsz(client) + vsz((uint32_t)(clock + off - 1)) + (ro1 - ro0);
                 if (ref == 1) {
@@ -262,13 +228,13 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
                   for (uint32_t i = 0; i < off; i++) any_scalar(e);  // ContentAny.splice: drop `off` values
                   if (lane == 0) put_vu_lds(q, len - off);
                   q += vsz(len - off);
-                  a0 = rel(w, e.p);
-                  a1 = rel(w, c.p);
+                  a0 = rel(e.p);
+                  a1 = rel(c.p);
                 } else {  // ContentString: str.slice(off) in UTF-16 units; a split surrogate throws in yjs
                   const uint32_t n = rvu(e);
                   uint32_t bi = 0, u = 0;
                   while (u < off && bi < n) {
-                    const uint32_t b = sm[e.p + bi];
+                    const uint32_t b = sc::byte(B, e.p + bi);
                     const uint32_t l = b < 0x80 ? 1 : b < 0xE0 ? 2 : b < 0xF0 ? 3 : 4;
                     u += l == 4 ? 2 : 1;
                     bi += l;
@@ -276,12 +242,12 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
                   if (u != off) { declined = true; break; }  // cut inside a surrogate pair: URIError path
                   if (lane == 0) put_vu_lds(q, n - bi);
                   q += vsz(n - bi);
-                  a0 = rel(w, e.p + bi);
-                  a1 = rel(w, e.p + n);
+                  a0 = rel(e.p + bi);
+                  a1 = rel(e.p + n);
                 }
                 if (e.bad) { declined = true; break; }
               }
-              b0r = rel(w, c.p);
+              b0r = rel(c.p);
               if (q - pre > PRE) { declined = true; break; }
             }
             if (lane == 0) {
@@ -299,7 +265,7 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
           const uint32_t ni = skip ? info : gc ? 0 : ((info & 0xC0) ? info & ~0x20u : info);
           if (ni != info) {
             if (npatch >= NPATCH) { declined = true; break; }
-            if (lane == 0) { at<uint32_t>(L_PPOS + 4 * npatch) = rel(w, s0); sm[L_PVAL + npatch] = (uint8_t)ni; at<uint32_t>(L_PSEC + 4 * npatch) = ci; }
+            if (lane == 0) { at<uint32_t>(L_PPOS + 4 * npatch) = rel(s0); sm[L_PVAL + npatch] = (uint8_t)ni; at<uint32_t>(L_PSEC + 4 * npatch) = ci; }
             npatch++;
           }
         }
@@ -308,7 +274,7 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
       if (declined || c.bad) break;
       if (OP == OP_DIFF) {
         if (lane == 0) {
-          sec(ci, S_B1) = copying ? rel(w, c.p) : 0;
+          sec(ci, S_B1) = copying ? rel(c.p) : 0;
           sec(ci, S_WRITTEN) = written;
           if (!copying) sec(ci, S_PRELEN) = NONE;
         }
@@ -350,12 +316,10 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
       continue;
     }
     // ---- delete set: validated, then copied verbatim (readDeleteSet + writeDeleteSet round trip)
-    win_ensure(w, c, j.A);
-    const uint32_t ds0 = rel(w, c.p);
+    const uint32_t ds0 = rel(c.p);
     {
       const uint32_t ndc = rvu(c);
       for (uint32_t i = 0; i < ndc && !c.bad && !declined; i++) {
-        win_ensure(w, c, j.A);
         const uint32_t client = rvu(c);
         const uint32_t m = rvu(c);
         // readDeleteSet drops clients without ranges and merges a repeated client into its first
@@ -365,14 +329,13 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
         if (lane == 0) X.dsc[i] = client;
         __threadfence_block();
         for (uint32_t q = 0; q < m && !c.bad; q++) {
-          win_ensure(w, c, j.A);
           rvu(c);
           rvu(c);
         }
       }
     }
     if (declined || c.bad) YB_DECLINE()
-    const uint32_t ds1 = rel(w, c.p);
+    const uint32_t ds1 = rel(c.p);
     __syncthreads();
     // ---- sizes, allocation
     __threadfence_block();
@@ -395,10 +358,8 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
     }
     // ---- write: small pieces by lane 0, spans by the wave, then the info patches
     uint8_t *const o = j.out + base;
-    const uint8_t *const src = j.A + w.b0;
-    auto copy_span = [&](uint32_t dst, uint32_t s0_, uint32_t s1_) {
-      for (uint32_t i = s0_ + lane; i < s1_; i += 64) o[dst + i - s0_] = src[i];
-    };
+    const uint8_t *const src = j.A + ub;
+    auto copy_span = [&](uint32_t dst, uint32_t s0_, uint32_t s1_) { copy_bytes(o + dst, src + s0_, s1_ - s0_); };
     uint32_t p = 0;
     if (lane == 0) {
       uint32_t t = 0;
