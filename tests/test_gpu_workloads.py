@@ -169,3 +169,21 @@ def test_c5_sv_and_diff_many_clients(engine, fmt):
     bad = _compare(engine.run_host("diff", fmt, a3, o3, d3, sva, svo), outs2, st2)
     assert not bad, bad[:10]
     assert engine.stats["docs_fast"] == engine.stats["docs"], engine.stats
+
+
+def test_state_does_not_leak_between_calls(engine):
+    """A large diff (big bump allocation) followed by a tiny merge on the same engine: the second call's
+    allocator starts clean (regression: a stale device counter made the merge report CAPACITY)."""
+    from yjs_amd import pack_docs
+    arena, upd_off, doc_upd = load_ymb("c3_v1")
+    upd = arena.tobytes()
+    a2, o2, d2 = pack_docs([[upd] for _ in range(8)])
+    sva, svo, _ = pack_docs([[b"\x00"] for _ in range(8)])
+    _, _, _, st = engine.run_host("diff", 1, a2, o2, d2, sva, svo)
+    assert (st == 0).all()
+    a, o, d = load_ymb("c2_v1")
+    docs = [[a[int(o[u]):int(o[u + 1])].tobytes() for u in range(int(d[0]), int(d[1]))]]
+    a3, o3, d3 = pack_docs(docs)
+    outs, status, _ = O.batch("merge", 1, a3, o3, d3)
+    bad = _compare(engine.run_host("merge", 1, a3, o3, d3), outs, status)
+    assert not bad, bad

@@ -130,8 +130,8 @@ __global__ void __launch_bounds__(1024) k_finish(const int32_t *status, const ui
     host[4] = e;
     host[5] = b;
     host[6] = upd_off[n_upd] - upd_off[0];
-    ((uint32_t *)counters)[4] = 0;               // pend_count (counters + 2) := 0 for the next launch
-    __threadfence_system();
+    counters[0] = 0;                             // used := 0 and pend_count (counters + 2) := 0: the
+    ((uint32_t *)counters)[4] = 0;               // next launch starts clean (see run_op for the general path)
   }
 }
 
@@ -310,7 +310,14 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   }
   // (3) general path over the rest
   if (ngen > 0) {
-    if (op == OP_MERGE) k_fast_region<<<1, 64, 0, st>>>(j, b->n_upd);  // bump allocator after the slots
+    // the general path's bump allocator: merges start after the slot region; diff / sv continue after
+    // what the streamed kernels allocated (k_finish reset the device counter)
+    if (op == OP_MERGE) {
+      k_fast_region<<<1, 64, 0, st>>>(j, b->n_upd);
+    } else {
+      S->pinned[16] = S->pinned[0];
+      HIPCHK(hipMemcpyAsync(counters, S->pinned + 16, 8, hipMemcpyHostToDevice, st));
+    }
     int r = run_general(S, st, j, list, ngen);
     if (r) return r;
     HIPCHK(hipEventRecord(S->evg1, st));
