@@ -38,6 +38,9 @@ constexpr uint32_t L_UOFF = WIN + 16;          // u32[65]
 constexpr uint32_t WALK_LDS = L_UOFF + 4 * 72;
 constexpr uint32_t BT = 512, NW = BT / 64;     // document workgroup
 constexpr uint32_t GMAX = 4096;                // delete-set groups (clients) ranked in LDS
+// per-document info passed between k_lm_doc1 -> k_lm_col -> k_lm_doc2 -> k_lm_col<write>
+enum { DI_NPARTS = 0, DI_NCOL = 1, DI_SBODY = 10, DI_SECT, DI_NGROUPS, DI_NRANGES, DI_DSBYTES, DI_CSZ = 16,
+       DI_CBASE = 25, DI_SLOT = 34 /* u64 */, DI_N = 40 };
 
 struct LMJob {
   const uint8_t *A;
@@ -69,6 +72,7 @@ struct LMJob {
   uint32_t *c_cl, *c_lc, *c_rc, *c_ln, *c_sbo;                   // V2 column values
   uint8_t *c_in, *c_pi, *c_tr;
   uint64_t *c_st;
+  uint32_t *dinfo;            // [nb][DI_N] per-document sizes between the phase kernels
   // outputs
   int32_t *status;
   uint8_t *out;
@@ -516,63 +520,78 @@ __device__ __forceinline__ void copy_bytes(uint8_t *dst, const uint8_t *src, uin
 }
 
 enum { K_UOPT = 0, K_IDIF = 1, K_RLE = 2 };
-// lib0 RLE column encoder over n values get(i), tiled: returns the byte size; writes at dst when wr.
-// Runs from neighbour compares (of diffs for IntDiffOptRle), run lengths from a carried running max
-// of the run-start positions, run bytes placed by a carried exclusive scan.
+// lib0 RLE column encoder over n values get(i), tiled (IT consecutive entries per thread): returns the
+// byte size; writes at dst when wr.  Runs from neighbour compares (of diffs for IntDiffOptRle), run
+// lengths from a carried running max of the run-start positions, run bytes placed by a carried scan.
 template <int K, class Get>
 __device__ uint32_t col_rle(Shm &S, Get get, uint32_t n, bool wr, uint8_t *dst, bool &bad) {
+  constexpr uint32_t IT = 4, TILE = BT * IT;
   uint64_t carry_sp = 0;
   uint32_t carry_b = 0;
-  for (uint32_t t0 = 0; t0 < n; t0 += BT) {
-    const uint32_t i = t0 + threadIdx.x;
-    const bool v = i < n;
-    int64_t cur = 0, prv = 0, nxt = 0;
-    if (v) {
-      const int64_t a = get(i);
-      const int64_t p = i > 0 ? (int64_t)get(i - 1) : 0;
-      const int64_t q = i + 1 < n ? (int64_t)get(i + 1) : 0;
-      if (K == K_IDIF) {
-        const int64_t pp = i > 1 ? (int64_t)get(i - 2) : 0;
-        cur = a - p;
-        prv = p - pp;
-        nxt = q - a;
-      } else {
-        cur = a;
-        prv = p;
-        nxt = q;
-      }
+  for (uint32_t t0 = 0; t0 < n; t0 += TILE) {
+    const uint32_t i0 = t0 + threadIdx.x * IT;
+    int64_t val[IT + 3];  // values of entries i0 - 2 .. i0 + IT (0 outside [0, n): the IntDiff base)
+#pragma unroll
+    for (uint32_t k = 0; k < IT + 3; k++) {
+      const int64_t e = (int64_t)i0 + k - 2;
+      val[k] = e >= 0 && e < (int64_t)n ? (int64_t)get((uint32_t)e) : 0;
     }
-    const bool st = v && (i == 0 || cur != prv);
-    const bool end = v && (i + 1 == n || nxt != cur);
-    uint64_t tmax;
-    const uint64_t sp = bmax(S, st ? i : 0, carry_sp, tmax);
-    uint32_t rb = 0;
-    const uint32_t cntv = (uint32_t)(i - sp + 1);
-    if (end) {
+    int64_t cv[IT + 2];   // compared value (diff for IntDiffOptRle) of entries i0 - 1 .. i0 + IT
+#pragma unroll
+    for (uint32_t k = 0; k < IT + 2; k++) cv[k] = K == K_IDIF ? val[k + 1] - val[k] : val[k + 1];
+    bool st[IT], en[IT];
+    uint32_t last = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < IT; t++) {
+      const uint32_t e = i0 + t;
+      const bool v = e < n;
+      st[t] = v && (e == 0 || cv[t + 1] != cv[t]);
+      en[t] = v && (e + 1 == n || cv[t + 2] != cv[t + 1]);
+      if (st[t]) last = e;
+    }
+    uint64_t tmax, ex;
+    bmax(S, last, carry_sp, tmax, &ex);
+    uint32_t sp = (uint32_t)ex, rb[IT], cnt[IT], tb = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < IT; t++) {
+      const uint32_t e = i0 + t;
+      if (st[t]) sp = e;
+      cnt[t] = e - sp + 1;
+      rb[t] = 0;
+      if (!en[t]) continue;
+      const int64_t cur = cv[t + 1];
       if (K == K_UOPT) {
-        rb = vszi((uint32_t)cur) + (cntv > 1 ? gvsz(cntv - 2) : 0);
+        rb[t] = vszi((uint32_t)cur) + (cnt[t] > 1 ? gvsz(cnt[t] - 2) : 0);
       } else if (K == K_IDIF) {
         bad |= cur <= -(1ll << 30) || cur >= (1ll << 30);
-        const int32_t x = (int32_t)((uint32_t)(int32_t)cur << 1) | (cntv > 1 ? 1 : 0);
-        rb = vszi(x < 0 ? 0u - (uint32_t)x : (uint32_t)x) + (cntv > 1 ? gvsz(cntv - 2) : 0);
+        const int32_t x = (int32_t)((uint32_t)(int32_t)cur << 1) | (cnt[t] > 1 ? 1 : 0);
+        rb[t] = vszi(x < 0 ? 0u - (uint32_t)x : (uint32_t)x) + (cnt[t] > 1 ? gvsz(cnt[t] - 2) : 0);
       } else {
-        rb = 1 + (i + 1 == n ? 0 : gvsz(cntv - 1));
+        rb[t] = 1 + (e + 1 == n ? 0 : gvsz(cnt[t] - 1));
       }
+      tb += rb[t];
     }
-    uint32_t x1[1] = {rb}, t1[1];
+    uint32_t x1[1] = {tb}, t1[1];
     bscan<1>(S, x1, t1);
-    if (wr && end) {
+    if (wr) {
       uint32_t q = carry_b + x1[0];
-      if (K == K_UOPT) {
-        q = gput_vi(dst, q, cntv > 1, (uint32_t)cur);
-        if (cntv > 1) gput_vu(dst, q, cntv - 2);
-      } else if (K == K_IDIF) {
-        const int32_t x = (int32_t)((uint32_t)(int32_t)cur << 1) | (cntv > 1 ? 1 : 0);
-        q = gput_vi(dst, q, x < 0, x < 0 ? 0u - (uint32_t)x : (uint32_t)x);
-        if (cntv > 1) gput_vu(dst, q, cntv - 2);
-      } else {
-        dst[q++] = (uint8_t)cur;
-        if (i + 1 != n) gput_vu(dst, q, cntv - 1);
+#pragma unroll
+      for (uint32_t t = 0; t < IT; t++) {
+        if (!en[t]) continue;
+        const int64_t cur = cv[t + 1];
+        uint32_t o = q;
+        if (K == K_UOPT) {
+          o = gput_vi(dst, o, cnt[t] > 1, (uint32_t)cur);
+          if (cnt[t] > 1) gput_vu(dst, o, cnt[t] - 2);
+        } else if (K == K_IDIF) {
+          const int32_t x = (int32_t)((uint32_t)(int32_t)cur << 1) | (cnt[t] > 1 ? 1 : 0);
+          o = gput_vi(dst, o, x < 0, x < 0 ? 0u - (uint32_t)x : (uint32_t)x);
+          if (cnt[t] > 1) gput_vu(dst, o, cnt[t] - 2);
+        } else {
+          dst[o++] = (uint8_t)cur;
+          if (i0 + t + 1 != n) gput_vu(dst, o, cnt[t] - 1);
+        }
+        q += rb[t];
       }
     }
     carry_b += t1[0];
@@ -581,18 +600,78 @@ __device__ uint32_t col_rle(Shm &S, Get get, uint32_t n, bool wr, uint8_t *dst, 
   return carry_b;
 }
 
+// the document's bases in the record / run / range arrays
+struct DocB {
+  uint32_t d, rb, ns, runb, nr, dsb, nds;
+  uint64_t b0, bytes;
+};
+__device__ __forceinline__ DocB doc_bases(const LMJob &J, uint32_t i) {
+  DocB B;
+  B.d = J.bdoc[i];
+  const uint32_t u0 = J.doc_upd[B.d], k = J.doc_upd[B.d + 1] - u0;
+  B.b0 = J.upd_off[u0];
+  B.bytes = J.upd_off[u0 + k] - B.b0;
+  const uint32_t bu0 = J.bu_off[i], bu1 = J.bu_off[i + 1];
+  B.rb = J.u_off[bu0];
+  B.ns = J.u_off[bu1] - B.rb;
+  B.runb = J.u_off[J.stride + bu0];
+  B.nr = J.u_off[J.stride + bu1] - B.runb;
+  B.dsb = J.u_off[2 * J.stride + bu0];
+  B.nds = J.u_off[2 * J.stride + bu1] - B.dsb;
+  return B;
+}
+
+// ---- 3b. V2 columns: one workgroup per (document, column); WR = false sizes, WR = true writes ------
+template <bool WR>
+__global__ void __launch_bounds__(BT) k_lm_col(LMJob J) {
+  __shared__ Shm S;
+  const uint32_t i = blockIdx.x, c = blockIdx.y;
+  if (J.bad[i]) return;
+  const DocB D = doc_bases(J, i);
+  uint32_t *const info = J.dinfo + (uint64_t)DI_N * i;
+  const uint32_t rb = D.rb;
+  const uint64_t cb = 3ull * rb, ib = 2ull * rb;
+  const uint32_t n = info[DI_NCOL + c];
+  uint8_t *dst = nullptr;
+  if (WR) dst = J.out + *(const uint64_t *)(info + DI_SLOT) + info[DI_CBASE + c];
+  bool bad = false;
+  uint32_t sz = 0;
+  switch (c) {
+    case 0: sz = col_rle<K_IDIF>(S, [&](uint32_t x) { return x; }, n, WR, dst, bad); break;
+    case 1: sz = col_rle<K_UOPT>(S, [&](uint32_t x) { return J.c_cl[cb + x]; }, n, WR, dst, bad); break;
+    case 2: sz = col_rle<K_IDIF>(S, [&](uint32_t x) { return J.c_lc[rb + x]; }, n, WR, dst, bad); break;
+    case 3: sz = col_rle<K_IDIF>(S, [&](uint32_t x) { return J.c_rc[rb + x]; }, n, WR, dst, bad); break;
+    case 4: sz = col_rle<K_RLE>(S, [&](uint32_t x) { return (uint32_t)J.c_in[ib + x]; }, n, WR, dst, bad); break;
+    case 5: {  // StringEncoder: varString(bodies) | UintOptRle(lengths); ASCII, so lengths are bytes
+      const uint32_t sbody = info[DI_SBODY];
+      const uint32_t hb = gvsz(sbody);
+      if (WR) {
+        if (threadIdx.x == 0) gput_vu(dst, 0, sbody);
+        for (uint32_t e = threadIdx.x; e < n; e += BT) {
+          const uint64_t s = J.c_st[cb + e];
+          copy_bytes(dst + hb + J.c_sbo[cb + e], J.A + (s >> 24), (uint32_t)(s & 0xffffff));
+        }
+      }
+      sz = hb + sbody + col_rle<K_UOPT>(S, [&](uint32_t x) { return (uint32_t)(J.c_st[cb + x] & 0xffffff); }, n, WR,
+                                        WR ? dst + hb + sbody : nullptr, bad);
+      break;
+    }
+    case 6: sz = col_rle<K_RLE>(S, [&](uint32_t x) { return (uint32_t)J.c_pi[rb + x]; }, n, WR, dst, bad); break;
+    case 7: sz = col_rle<K_UOPT>(S, [&](uint32_t x) { return (uint32_t)J.c_tr[rb + x]; }, n, WR, dst, bad); break;
+    default: sz = col_rle<K_UOPT>(S, [&](uint32_t x) { return J.c_ln[rb + x]; }, n, WR, dst, bad); break;
+  }
+  if (!WR && threadIdx.x == 0) info[DI_CSZ + c] = sz;
+  if (!WR && bor(S, bad) && threadIdx.x == 0) J.bad[i] = 1;  // (diffs outside +-2^30: general path)
+}
+
+// ---- 3a. per document: runs, output order, struct sizes / column entries, delete set --------------
 template <bool V2>
-__global__ void __launch_bounds__(BT) k_lm_doc(LMJob J) {
+__global__ void __launch_bounds__(BT) k_lm_doc1(LMJob J) {
   __shared__ Shm S;
   const uint32_t i = blockIdx.x, tid = threadIdx.x;
   if (J.bad[i]) return;
-  const uint32_t d = J.bdoc[i];
-  const uint32_t u0 = J.doc_upd[d], k = J.doc_upd[d + 1] - u0;
-  const uint64_t b0 = J.upd_off[u0], bytes = J.upd_off[u0 + k] - b0;
-  const uint32_t bu0 = J.bu_off[i], bu1 = J.bu_off[i + 1];
-  const uint32_t rb = J.u_off[bu0], ns = J.u_off[bu1] - rb;
-  const uint32_t runb = J.u_off[J.stride + bu0], nr = J.u_off[J.stride + bu1] - runb;
-  const uint32_t dsb = J.u_off[2 * J.stride + bu0], nds = J.u_off[2 * J.stride + bu1] - dsb;
+  const DocB D = doc_bases(J, i);
+  const uint32_t rb = D.rb, ns = D.ns, runb = D.runb, nr = D.nr, dsb = D.dsb, nds = D.nds;
   auto decline = [&]() {
     if (tid == 0) J.bad[i] = 1;  // status stays ST_PENDING: the general path takes the document
   };
@@ -746,31 +825,6 @@ __global__ void __launch_bounds__(BT) k_lm_doc(LMJob J) {
     (void)bad;
   }
   __syncthreads();
-  // ---- D. V2 column sizes
-  const uint64_t cb = 3ull * rb, ib = 2ull * rb;
-  auto g_kc = [&](uint32_t x) { return x; };
-  auto g_cl = [&](uint32_t x) { return J.c_cl[cb + x]; };
-  auto g_lc = [&](uint32_t x) { return J.c_lc[rb + x]; };
-  auto g_rc = [&](uint32_t x) { return J.c_rc[rb + x]; };
-  auto g_in = [&](uint32_t x) { return (uint32_t)J.c_in[ib + x]; };
-  auto g_sl = [&](uint32_t x) { return (uint32_t)(J.c_st[cb + x] & 0xffffff); };
-  auto g_pi = [&](uint32_t x) { return (uint32_t)J.c_pi[rb + x]; };
-  auto g_tr = [&](uint32_t x) { return (uint32_t)J.c_tr[rb + x]; };
-  auto g_ln = [&](uint32_t x) { return J.c_ln[rb + x]; };
-  uint32_t csz[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  if (V2) {
-    bool cbad = false;
-    csz[0] = col_rle<K_IDIF>(S, g_kc, ncol[0], false, nullptr, cbad);
-    csz[1] = col_rle<K_UOPT>(S, g_cl, ncol[1], false, nullptr, cbad);
-    csz[2] = col_rle<K_IDIF>(S, g_lc, ncol[2], false, nullptr, cbad);
-    csz[3] = col_rle<K_IDIF>(S, g_rc, ncol[3], false, nullptr, cbad);
-    csz[4] = col_rle<K_RLE>(S, g_in, ncol[4], false, nullptr, cbad);
-    csz[5] = gvsz(sbody) + sbody + col_rle<K_UOPT>(S, g_sl, ncol[5], false, nullptr, cbad);
-    csz[6] = col_rle<K_RLE>(S, g_pi, ncol[6], false, nullptr, cbad);
-    csz[7] = col_rle<K_UOPT>(S, g_tr, ncol[7], false, nullptr, cbad);
-    csz[8] = col_rle<K_UOPT>(S, g_ln, ncol[8], false, nullptr, cbad);
-    if (bor(S, cbad)) { decline(); return; }
-  }
   // ---- E. delete set: union per client (>= touching rule, max end), groups by first appearance
   uint32_t ngroups = 0, nranges = 0, qtot = 0;
   {
@@ -879,7 +933,31 @@ __global__ void __launch_bounds__(BT) k_lm_doc(LMJob J) {
     J.g_woff[dsb + g] = off;
     J.g_min[dsb + g] = off + gvsz(J.g_cli[dsb + g]) + gvsz(f1 - f0) - qpre(f0);  // base of its ranges
   }
-  __syncthreads();
+  if (tid == 0) {
+    uint32_t *const info = J.dinfo + (uint64_t)DI_N * i;
+    info[DI_NPARTS] = nparts;
+    for (int z = 0; z < 9; z++) info[DI_NCOL + z] = ncol[z];
+    info[DI_SBODY] = sbody;
+    info[DI_SECT] = sect;
+    info[DI_NGROUPS] = ngroups;
+    info[DI_NRANGES] = nranges;
+    info[DI_DSBYTES] = ds_bytes;
+  }
+}
+
+// ---- 3c. per document: placement in its slot, header, rest / rows, delete set (V2 columns: k_lm_col)
+template <bool V2>
+__global__ void __launch_bounds__(BT) k_lm_doc2(LMJob J) {
+  const uint32_t i = blockIdx.x, tid = threadIdx.x;
+  if (J.bad[i]) return;
+  const DocB D = doc_bases(J, i);
+  const uint32_t d = D.d, rb = D.rb, ns = D.ns, dsb = D.dsb;
+  const uint64_t b0 = D.b0, bytes = D.bytes;
+  uint32_t *const info = J.dinfo + (uint64_t)DI_N * i;
+  const uint32_t nparts = info[DI_NPARTS], sect = info[DI_SECT], ngroups = info[DI_NGROUPS];
+  const uint32_t nranges = info[DI_NRANGES], ds_bytes = info[DI_DSBYTES];
+  uint32_t csz[9];
+  for (int z = 0; z < 9; z++) csz[z] = V2 ? info[DI_CSZ + z] : 0;
   // ---- F. placement: the document's slot (2 * input bytes before it + 64 * d, 16-aligned)
   uint32_t cbase[9], colbytes = 0;
   {
@@ -897,36 +975,25 @@ __global__ void __launch_bounds__(BT) k_lm_doc(LMJob J) {
   const uint64_t slot = 2 * (b0 - J.upd_off[0]) + 64ull * d;
   const uint64_t slot_al = (slot + 15) & ~15ull;
   const uint64_t lim = slot + 2 * bytes + 64;
-  if (slot_al + total > lim || slot_al + total > J.cap) { decline(); return; }
+  if (slot_al + total > lim || slot_al + total > J.cap) {
+    if (tid == 0) J.bad[i] = 1;  // status stays ST_PENDING: the general path takes the document
+    return;
+  }
   uint8_t *dst = J.out + slot_al;
-  // ---- G. struct section
+  if (tid == 0) {
+    *(uint64_t *)(info + DI_SLOT) = slot_al;
+    for (int c = 0; c < 9; c++) info[DI_CBASE + c] = cbase[c];
+  }
+  // ---- G. struct section (the V2 columns themselves: k_lm_col<true>)
   if (tid == 0) {
     if (V2) {
       dst[0] = 0;
       uint32_t p = 1;
       for (int c = 0; c < 9; c++) p = gput_vu(dst, p, csz[c]) + csz[c];
       gput_vu(dst, colbytes, nparts);
-      gput_vu(dst, cbase[5], sbody);
     } else {
       gput_vu(dst, 0, nparts);
     }
-  }
-  if (V2) {
-    bool cbad = false;
-    col_rle<K_IDIF>(S, g_kc, ncol[0], true, dst + cbase[0], cbad);
-    col_rle<K_UOPT>(S, g_cl, ncol[1], true, dst + cbase[1], cbad);
-    col_rle<K_IDIF>(S, g_lc, ncol[2], true, dst + cbase[2], cbad);
-    col_rle<K_IDIF>(S, g_rc, ncol[3], true, dst + cbase[3], cbad);
-    col_rle<K_RLE>(S, g_in, ncol[4], true, dst + cbase[4], cbad);
-    const uint32_t sbase = cbase[5] + gvsz(sbody);
-    for (uint32_t e = tid; e < ncol[5]; e += BT) {  // string bodies, copied from the inputs' string columns
-      const uint64_t s = J.c_st[cb + e];
-      copy_bytes(dst + sbase + J.c_sbo[cb + e], J.A + (s >> 24), (uint32_t)(s & 0xffffff));
-    }
-    col_rle<K_UOPT>(S, g_sl, ncol[5], true, dst + sbase + sbody, cbad);
-    col_rle<K_RLE>(S, g_pi, ncol[6], true, dst + cbase[6], cbad);
-    col_rle<K_UOPT>(S, g_tr, ncol[7], true, dst + cbase[7], cbad);
-    col_rle<K_UOPT>(S, g_ln, ncol[8], true, dst + cbase[8], cbad);
   }
   for (uint32_t p = tid; p < ns; p += BT) {
     const uint32_t q = J.ord[rb + p], gap = J.o_gap[rb + p], pw = J.o_pw[rb + p];
@@ -1020,7 +1087,8 @@ int large_run(const GeneralJob &j, const uint32_t *list, uint32_t nb, hipStream_
   J.out_len = j.out_len;
   // per-document arrays
   const uint64_t n1 = nb + 1;
-  if (ensure(B, 0, 4 * csize<uint32_t>(n1) + csize<uint32_t>(nb) + csize<uint32_t>(4ull * nb) + 256)) return -2;
+  if (ensure(B, 0, 4 * csize<uint32_t>(n1) + csize<uint32_t>(nb) + csize<uint32_t>(4ull * nb) + csize<uint32_t>((uint64_t)DI_N * nb) + 512))
+    return -2;
   uint8_t *p = (uint8_t *)B.p[0];
   J.bu_off = carve<uint32_t>(p, n1);
   J.ch_off = carve<uint32_t>(p, n1);
@@ -1029,6 +1097,7 @@ int large_run(const GeneralJob &j, const uint32_t *list, uint32_t nb, hipStream_
   J.bad = carve<uint32_t>(p, nb);
   uint32_t *seg = carve<uint32_t>(p, 4ull * nb);
   uint32_t *tot = carve<uint32_t>(p, 4);
+  J.dinfo = carve<uint32_t>(p, (uint64_t)DI_N * nb);
   k_lm_prep<<<(nb + 256) / 256, 256, 0, st>>>(J, list, kcnt, ccnt);
   size_t tmp = 0, t2 = 0;
   hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, kcnt, J.bu_off, n1, st);
@@ -1131,8 +1200,15 @@ int large_run(const GeneralJob &j, const uint32_t *list, uint32_t nb, hipStream_
   if (ND > 1)
     hipcub::DeviceSegmentedRadixSort::SortPairs(B.p[3], s2, J.dkey, J.sdkey, J.didx, J.sdidx, (int)(ND - 1), (int)nb,
                                                 seg + 2 * nb, seg + 3 * nb, 0, 64, st);
-  if (J.v2) k_lm_doc<true><<<nb, BT, 0, st>>>(J);
-  else k_lm_doc<false><<<nb, BT, 0, st>>>(J);
+  if (J.v2) {
+    k_lm_doc1<true><<<nb, BT, 0, st>>>(J);
+    k_lm_col<false><<<dim3(nb, 9), BT, 0, st>>>(J);
+    k_lm_doc2<true><<<nb, BT, 0, st>>>(J);
+    k_lm_col<true><<<dim3(nb, 9), BT, 0, st>>>(J);
+  } else {
+    k_lm_doc1<false><<<nb, BT, 0, st>>>(J);
+    k_lm_doc2<false><<<nb, BT, 0, st>>>(J);
+  }
   return 1;
 }
 
