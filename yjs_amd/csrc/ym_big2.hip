@@ -32,23 +32,19 @@ constexpr uint32_t NSEC = BS_NSEC, NSV = BS_NSV;  // parts / state-vector entrie
 
 constexpr uint32_t L_WREST = 0;
 constexpr uint32_t L_WCOL = WREST + 16;                      // (NIN-1) x (WCOL + 16)
-constexpr uint32_t L_IST = L_WCOL + (NIN - 1) * (WCOL + 16); // u32[NIN][4]: pos, end, wdelta, wlim
-constexpr uint32_t L_DEC = L_IST + NIN * 16;                 // u32[NIN][4]: s, count, diff, (pad)  (RLE decoders)
-constexpr uint32_t L_OST = L_DEC + NIN * 16;                 // u32[NOUT][4]: base, cur, cap, (pad)
-constexpr uint32_t L_ENC = L_OST + NOUT * 16;                // u32[NOUT][4]: s, count, diff, started
-constexpr uint32_t L_MISC = L_ENC + NOUT * 16;               // u32[16]
-constexpr uint32_t LDS_BYTES = L_MISC + 64;
+constexpr uint32_t LDS_BYTES = L_WCOL + (NIN - 1) * (WCOL + 16);
 
-__device__ __forceinline__ uint32_t &ist(uint32_t s, uint32_t f) { return at<uint32_t>(L_IST + 16 * s + 4 * f); }
-__device__ __forceinline__ uint32_t &dec(uint32_t s, uint32_t f) { return at<uint32_t>(L_DEC + 16 * s + 4 * f); }
-__device__ __forceinline__ uint32_t &ost(uint32_t s, uint32_t f) { return at<uint32_t>(L_OST + 16 * s + 4 * f); }
-__device__ __forceinline__ uint32_t &enc(uint32_t s, uint32_t f) { return at<uint32_t>(L_ENC + 16 * s + 4 * f); }
-__device__ __forceinline__ uint32_t &misc(uint32_t f) { return at<uint32_t>(L_MISC + 4 * f); }
+// The walk is wave-uniform: every lane computes the same stream cursors, decoder and encoder states,
+// so they live in registers (Doc::st_*), identical in all 64 lanes -- no LDS round trip and no barrier
+// per field.  Only the stream windows (LDS) and the output bytes (stored by lane 0) are shared.
 enum { M_BAD = 0, M_KEYS, M_KCLOCK, M_SPOS };
-__device__ __forceinline__ void set_bad() {
-  if (threadIdx.x == 0) misc(M_BAD) = 1;
-}
-__device__ __forceinline__ bool is_bad() { return misc(M_BAD) != 0; }
+#define ist(s, f) D.st_in[s][f]    // input streams: pos, end, wdelta, wlim
+#define dec(s, f) D.st_dec[s][f]   // RLE decoders: s, count, diff
+#define ost(s, f) D.st_out[s][f]   // output streams (scratch): base, cur, cap
+#define enc(s, f) D.st_enc[s][f]   // RLE encoders: s, count, diff, started
+#define misc(f) D.st_misc[f]
+#define set_bad() (D.st_misc[M_BAD] = 1)
+#define is_bad() (D.st_misc[M_BAD] != 0)
 
 // per-block HBM scratch (ym_kernels.h BS_*): parts (rest start, rest end, written), state vector,
 // delete-set clients
@@ -74,11 +70,12 @@ struct Doc {
   uint64_t b0;       // update start (absolute)
   uint32_t len;      // update bytes
   uint8_t *O;        // output arena
+  uint32_t st_in[NIN][4], st_dec[NIN][4], st_out[NOUT][4], st_enc[NOUT][4], st_misc[4];
 };
 
 __device__ __forceinline__ uint32_t win_lds(uint32_t s) { return s == I_REST ? L_WREST : L_WCOL + (s - 1) * (WCOL + 16); }
 // (re)loads stream s's window at its cursor; every lane takes part (the walk is wave-uniform)
-__device__ __forceinline__ void s_load(const Doc &D, uint32_t s) {
+__device__ __forceinline__ void s_load(Doc &D, uint32_t s) {
   const uint32_t W = s == I_REST ? WREST : WCOL;
   const uint32_t pos = ist(s, 0), end = ist(s, 1);
   __syncthreads();
@@ -89,14 +86,11 @@ __device__ __forceinline__ void s_load(const Doc &D, uint32_t s) {
   const uint32_t base = win_lds(s);
   for (uint32_t v = threadIdx.x; v < (n + 15) >> 4; v += 64) at<uint4>(base + 16 * v) = src[v];
   __syncthreads();
-  if (threadIdx.x == 0) {
-    ist(s, 2) = (uint32_t)(base - (wa - D.b0));  // LDS address = pos + wdelta
-    ist(s, 3) = (uint32_t)(wa - D.b0) + n;       // loaded through (update-relative)
-  }
-  __syncthreads();
+  ist(s, 2) = (uint32_t)(base - (wa - D.b0));  // LDS address = pos + wdelta
+  ist(s, 3) = (uint32_t)(wa - D.b0) + n;       // loaded through (update-relative)
 }
 // cursor of stream s as an LDS Cur with at least `need` bytes loaded (or the stream's end)
-__device__ __forceinline__ Cur s_cur(const Doc &D, uint32_t s, uint32_t need) {
+__device__ __forceinline__ Cur s_cur(Doc &D, uint32_t s, uint32_t need) {
   uint32_t pos = ist(s, 0), end = ist(s, 1), lim = ist(s, 3);
   if (pos + need > lim && lim < end) {
     s_load(D, s);
@@ -106,26 +100,24 @@ __device__ __forceinline__ Cur s_cur(const Doc &D, uint32_t s, uint32_t need) {
   Cur c = {pos + wd, (end < lim ? end : lim) + wd, false};
   return c;
 }
-__device__ __forceinline__ void s_commit(uint32_t s, const Cur &c) {
-  __syncthreads();
-  if (threadIdx.x == 0) ist(s, 0) = c.p - ist(s, 2);
+__device__ __forceinline__ void s_commit(Doc &D, uint32_t s, const Cur &c) {
+  ist(s, 0) = c.p - ist(s, 2);
   if (c.bad) set_bad();
-  __syncthreads();
 }
-__device__ __forceinline__ uint32_t s_vu(const Doc &D, uint32_t s) {
+__device__ __forceinline__ uint32_t s_vu(Doc &D, uint32_t s) {
   Cur c = s_cur(D, s, MCOL);
   const uint32_t v = rvu(c);
-  s_commit(s, c);
+  s_commit(D, s, c);
   return v;
 }
-__device__ __forceinline__ uint32_t s_u8(const Doc &D, uint32_t s) {
+__device__ __forceinline__ uint32_t s_u8(Doc &D, uint32_t s) {
   Cur c = s_cur(D, s, MCOL);
   const uint32_t v = rdb(c);
-  s_commit(s, c);
+  s_commit(D, s, c);
   return v;
 }
 // lib0 readVarInt (canonical, <= 5 bytes): sign flag incl. -0, u32 magnitude
-__device__ __forceinline__ uint32_t s_vi(const Doc &D, uint32_t s, bool &neg) {
+__device__ __forceinline__ uint32_t s_vi(Doc &D, uint32_t s, bool &neg) {
   Cur c = s_cur(D, s, MCOL);
   const uint64_t x = ld8(c.p);
   const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
@@ -137,38 +129,34 @@ __device__ __forceinline__ uint32_t s_vi(const Doc &D, uint32_t s, bool &neg) {
   const uint32_t last = nb <= 4 ? (lo >> (8 * nb - 8)) & 0xffu : hi & 0xffu;
   c.bad |= (nb > 5) | (c.p + nb > c.e) | ((nb > 1) & (last == 0)) | ((nb == 5) & ((hi & 0x7fu) > 0x1fu));
   c.p += nb < 6 ? nb : 0;
-  s_commit(s, c);
+  s_commit(D, s, c);
   return m;
 }
-__device__ __forceinline__ bool s_has(uint32_t s) { return ist(s, 0) < ist(s, 1); }
+__device__ __forceinline__ bool s_has(Doc &D, uint32_t s) { return ist(s, 0) < ist(s, 1); }
 
 // lib0 decoders (state in L_DEC): RleDecoder<u8>, UintOptRleDecoder, IntDiffOptRleDecoder
-__device__ __forceinline__ uint32_t rle_read(const Doc &D, uint32_t s) {
+__device__ __forceinline__ uint32_t rle_read(Doc &D, uint32_t s) {
   uint32_t v = dec(s, 0), n = dec(s, 1);
   if (n == 0) {
     v = s_u8(D, s);
-    n = s_has(s) ? s_vu(D, s) + 1 : 0xffffffffu;  // the final run never ends
+    n = s_has(D, s) ? s_vu(D, s) + 1 : 0xffffffffu;  // the final run never ends
   }
-  __syncthreads();
-  if (threadIdx.x == 0) { dec(s, 0) = v; dec(s, 1) = n == 0xffffffffu ? n : n - 1; }
-  __syncthreads();
+  dec(s, 0) = v; dec(s, 1) = n == 0xffffffffu ? n : n - 1;
   return v;
 }
-__device__ __forceinline__ uint32_t uopt_read(const Doc &D, uint32_t s) {
+__device__ __forceinline__ uint32_t uopt_read(Doc &D, uint32_t s) {
   uint32_t v = dec(s, 0), n = dec(s, 1);
   if (n == 0) {
     bool neg;
     v = s_vi(D, s, neg);
     n = neg ? s_vu(D, s) + 2 : 1;
   }
-  __syncthreads();
-  if (threadIdx.x == 0) { dec(s, 0) = v; dec(s, 1) = n - 1; }
-  __syncthreads();
+  dec(s, 0) = v; dec(s, 1) = n - 1;
   return v;
 }
 // IntDiffOptRleDecoder: diff = ToInt32(sign * mag) >> 1, count from its low bit; values must stay in
 // [0, 2^32) for this path (clocks)
-__device__ __forceinline__ uint32_t idiff_read(const Doc &D, uint32_t s) {
+__device__ __forceinline__ uint32_t idiff_read(Doc &D, uint32_t s) {
   int64_t v = (int64_t)dec(s, 0);
   uint32_t n = dec(s, 1);
   int32_t df = (int32_t)dec(s, 2);
@@ -181,60 +169,52 @@ __device__ __forceinline__ uint32_t idiff_read(const Doc &D, uint32_t s) {
   }
   v += df;
   if (v < 0 || v > 0xffffffffll) set_bad();
-  __syncthreads();
-  if (threadIdx.x == 0) { dec(s, 0) = (uint32_t)v; dec(s, 1) = n - 1; dec(s, 2) = (uint32_t)df; }
-  __syncthreads();
+  dec(s, 0) = (uint32_t)v; dec(s, 1) = n - 1; dec(s, 2) = (uint32_t)df;
   return (uint32_t)v;
 }
 
 // ---- output streams (scratch in the output arena) -----------------------------------------------
-__device__ __forceinline__ void o_byte(const Doc &D, uint32_t s, uint32_t v) {
+__device__ __forceinline__ void o_byte(Doc &D, uint32_t s, uint32_t v) {
   const uint32_t cur = ost(s, 1);
   if (cur >= ost(s, 2)) { set_bad(); return; }
-  if (threadIdx.x == 0) { D.O[(uint64_t)ost(s, 0) + cur] = (uint8_t)v; ost(s, 1) = cur + 1; }
-  __syncthreads();
+  if (threadIdx.x == 0) D.O[(uint64_t)ost(s, 0) + cur] = (uint8_t)v;
+  ost(s, 1) = cur + 1;
 }
-__device__ __forceinline__ void o_vu(const Doc &D, uint32_t s, uint32_t v) {
+__device__ __forceinline__ void o_vu(Doc &D, uint32_t s, uint32_t v) {
   while (v > 127) { o_byte(D, s, 0x80 | (v & 127)); v >>= 7; }
   o_byte(D, s, v);
 }
-__device__ __forceinline__ void o_vi(const Doc &D, uint32_t s, bool neg, uint32_t m) {  // lib0 writeVarInt
+__device__ __forceinline__ void o_vi(Doc &D, uint32_t s, bool neg, uint32_t m) {  // lib0 writeVarInt
   o_byte(D, s, (m > 63 ? 0x80 : 0) | (neg ? 0x40 : 0) | (m & 63));
   m >>= 6;
   while (m > 0) { o_byte(D, s, (m > 127 ? 0x80 : 0) | (m & 127)); m >>= 7; }
 }
 // copies update bytes [a, b) to the end of output stream s (all lanes)
-__device__ __forceinline__ void o_span(const Doc &D, uint32_t s, uint32_t a, uint32_t b) {
+__device__ __forceinline__ void o_span(Doc &D, uint32_t s, uint32_t a, uint32_t b) {
   const uint32_t cur = ost(s, 1);
   if (cur + (b - a) > ost(s, 2)) { set_bad(); return; }
   uint8_t *dst = D.O + ost(s, 0) + cur;
   const uint8_t *src = D.A + D.b0 + a;
   for (uint32_t i = threadIdx.x; i < b - a; i += 64) dst[i] = src[i];
-  __syncthreads();
-  if (threadIdx.x == 0) ost(s, 1) = cur + (b - a);
-  __syncthreads();
+  ost(s, 1) = cur + (b - a);
 }
 // lib0 encoders (state in L_ENC: s, count, diff, started)
-__device__ __forceinline__ void uopt_flush(const Doc &D, uint32_t s) {
+__device__ __forceinline__ void uopt_flush(Doc &D, uint32_t s) {
   const uint32_t v = enc(s, 0), n = enc(s, 1);
   if (n > 0) {
     o_vi(D, s, n != 1, v);  // count==1 ? v : -v  (-0 for v==0)
     if (n > 1) o_vu(D, s, n - 2);
   }
 }
-__device__ __forceinline__ void uopt_w(const Doc &D, uint32_t s, uint32_t v) {
+__device__ __forceinline__ void uopt_w(Doc &D, uint32_t s, uint32_t v) {
   if (enc(s, 0) == v) {
-    __syncthreads();
-    if (threadIdx.x == 0) enc(s, 1) += 1;
-    __syncthreads();
+    enc(s, 1) += 1;
     return;
   }
   uopt_flush(D, s);
-  __syncthreads();
-  if (threadIdx.x == 0) { enc(s, 0) = v; enc(s, 1) = 1; }
-  __syncthreads();
+  enc(s, 0) = v; enc(s, 1) = 1;
 }
-__device__ __forceinline__ void idiff_flush(const Doc &D, uint32_t s) {
+__device__ __forceinline__ void idiff_flush(Doc &D, uint32_t s) {
   const int32_t df = (int32_t)enc(s, 2);
   const uint32_t n = enc(s, 1);
   if (n > 0) {
@@ -243,34 +223,26 @@ __device__ __forceinline__ void idiff_flush(const Doc &D, uint32_t s) {
     if (n > 1) o_vu(D, s, n - 2);
   }
 }
-__device__ __forceinline__ void idiff_w(const Doc &D, uint32_t s, uint32_t v) {
+__device__ __forceinline__ void idiff_w(Doc &D, uint32_t s, uint32_t v) {
   const int64_t d = (int64_t)v - (int64_t)enc(s, 0);
   if (d < -(1ll << 30) || d >= (1ll << 30)) { set_bad(); return; }  // JS `diff << 1` wraps beyond
   if ((int32_t)enc(s, 2) == (int32_t)d) {
-    __syncthreads();
-    if (threadIdx.x == 0) { enc(s, 0) = v; enc(s, 1) += 1; }
-    __syncthreads();
+    enc(s, 0) = v; enc(s, 1) += 1;
     return;
   }
   idiff_flush(D, s);
-  __syncthreads();
-  if (threadIdx.x == 0) { enc(s, 0) = v; enc(s, 1) = 1; enc(s, 2) = (uint32_t)(int32_t)d; }
-  __syncthreads();
+  enc(s, 0) = v; enc(s, 1) = 1; enc(s, 2) = (uint32_t)(int32_t)d;
 }
-__device__ __forceinline__ void rle_w(const Doc &D, uint32_t s, uint32_t v) {
+__device__ __forceinline__ void rle_w(Doc &D, uint32_t s, uint32_t v) {
   if (enc(s, 3) && enc(s, 0) == v) {
-    __syncthreads();
-    if (threadIdx.x == 0) enc(s, 1) += 1;
-    __syncthreads();
+    enc(s, 1) += 1;
     return;
   }
   if (enc(s, 1) > 0) o_vu(D, s, enc(s, 1) - 1);
   o_byte(D, s, v);
-  __syncthreads();
-  if (threadIdx.x == 0) { enc(s, 0) = v; enc(s, 1) = 1; enc(s, 3) = 1; }
-  __syncthreads();
+  enc(s, 0) = v; enc(s, 1) = 1; enc(s, 3) = 1;
 }
-__device__ __forceinline__ void str_w(const Doc &D, uint32_t sb0, uint32_t a, uint32_t n) {  // ASCII string
+__device__ __forceinline__ void str_w(Doc &D, uint32_t sb0, uint32_t a, uint32_t n) {  // ASCII string
   o_span(D, O_SB, sb0 + a, sb0 + a + n);
   uopt_w(D, O_SL, n);
 }
@@ -281,16 +253,14 @@ __device__ __forceinline__ void str_w(const Doc &D, uint32_t sb0, uint32_t a, ui
 struct Rec {
   uint32_t info, len, oc, ok, rc, rk, pi, ya, yn, pa, pn, pc, pk, ca, cn, ka, kn, t, r0, r1;
 };
-__device__ __forceinline__ void rstr(const Doc &D, uint32_t sn, uint32_t &a, uint32_t &n) {
+__device__ __forceinline__ void rstr(Doc &D, uint32_t sn, uint32_t &a, uint32_t &n) {
   const uint32_t pos = misc(M_SPOS);  // StringDecoder.read: the next slice (bytes == UTF-16 units)
   n = uopt_read(D, I_SL);
   a = pos;
   if ((uint64_t)pos + n > sn) set_bad();  // a slice past the end would shorten the string
-  __syncthreads();
-  if (threadIdx.x == 0) misc(M_SPOS) = pos + n;
-  __syncthreads();
+  misc(M_SPOS) = pos + n;
 }
-__device__ bool v2_read(const Doc &D, uint32_t info, uint32_t sn, Rec &r) {
+__device__ __forceinline__ bool v2_read(Doc &D, uint32_t info, uint32_t sn, Rec &r) {
   r = Rec{};
   r.info = info;
   if (info == 10) { r.len = s_vu(D, I_REST); return !is_bad(); }           // Skip: len in rest
@@ -311,7 +281,7 @@ __device__ bool v2_read(const Doc &D, uint32_t info, uint32_t sn, Rec &r) {
       r.r0 = c.p - ist(I_REST, 2);
       const uint32_t n = rvu(c);
       if (!room(c, n)) c.bad = true; else c.p += n;
-      s_commit(I_REST, c);
+      s_commit(D, I_REST, c);
       r.r1 = ist(I_REST, 0);
       break;
     }
@@ -321,7 +291,7 @@ __device__ bool v2_read(const Doc &D, uint32_t info, uint32_t sn, Rec &r) {
       Cur c = s_cur(D, I_REST, MREST);
       r.r0 = c.p - ist(I_REST, 2);
       any_scalar(c);
-      s_commit(I_REST, c);
+      s_commit(D, I_REST, c);
       r.r1 = ist(I_REST, 0);
       break;
     }
@@ -331,9 +301,7 @@ __device__ bool v2_read(const Doc &D, uint32_t info, uint32_t sn, Rec &r) {
       if (r.t == 3 || r.t == 5) {  // readKey: a cached key (keyClock < keys read) consumes no string
         const uint32_t kcv = idiff_read(D, I_KC);
         if (kcv < misc(M_KEYS)) { set_bad(); return false; }
-        __syncthreads();
-        if (threadIdx.x == 0) misc(M_KEYS) += 1;
-        __syncthreads();
+        misc(M_KEYS) += 1;
         rstr(D, sn, r.ka, r.kn);
       }
       break;
@@ -342,7 +310,7 @@ __device__ bool v2_read(const Doc &D, uint32_t info, uint32_t sn, Rec &r) {
       Cur c = s_cur(D, I_REST, MREST);
       r.r0 = c.p - ist(I_REST, 2);
       for (uint32_t i = 0; i < r.len && !c.bad; i++) any_scalar(c);
-      s_commit(I_REST, c);
+      s_commit(D, I_REST, c);
       r.r1 = ist(I_REST, 0);
       break;
     }
@@ -351,15 +319,13 @@ __device__ bool v2_read(const Doc &D, uint32_t info, uint32_t sn, Rec &r) {
   if (r.len == 0) set_bad();
   return !is_bad();
 }
-__device__ __forceinline__ void next_key(const Doc &D) {  // writeKey: keyClock++ (never cached, E9)
+__device__ __forceinline__ void next_key(Doc &D) {  // writeKey: keyClock++ (never cached, E9)
   const uint32_t kc = misc(M_KCLOCK);
   idiff_w(D, O_KC, kc);
-  __syncthreads();
-  if (threadIdx.x == 0) misc(M_KCLOCK) = kc + 1;
-  __syncthreads();
+  misc(M_KCLOCK) = kc + 1;
 }
 // Item.write / GC.write / Skip.write (encoder, off) into the output streams, V2 routing
-__device__ void v2_write(const Doc &D, const Rec &r, uint32_t off, uint32_t client, uint32_t clock, uint32_t sb0) {
+__device__ __forceinline__ void v2_write(Doc &D, const Rec &r, uint32_t off, uint32_t client, uint32_t clock, uint32_t sb0) {
   const uint32_t info = r.info;
   if (info == 10) { rle_w(D, O_IN, 10); o_vu(D, O_REST, r.len - off); return; }
   if ((info & 31) == 0) { rle_w(D, O_IN, 0); uopt_w(D, O_LN, r.len - off); return; }
@@ -429,8 +395,16 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
     const uint64_t len64 = j.upd_off[u0 + 1] - D.b0;
     if (len64 == 0 || len64 > 0xfffffff0ull) YB2_DECLINE()
     D.len = (uint32_t)len64;
-    for (uint32_t i = lane; i < (L_MISC + 64 - L_IST) / 4; i += 64) at<uint32_t>(L_IST + 4 * i) = 0;
-    __syncthreads();
+#pragma unroll
+    for (uint32_t a = 0; a < NIN; a++)
+#pragma unroll
+      for (uint32_t b = 0; b < 4; b++) { D.st_in[a][b] = 0; D.st_dec[a][b] = 0; }
+#pragma unroll
+    for (uint32_t a = 0; a < NOUT; a++)
+#pragma unroll
+      for (uint32_t b = 0; b < 4; b++) { D.st_out[a][b] = 0; D.st_enc[a][b] = 0; }
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) D.st_misc[b] = 0;
     // ---- state vector (diff)
     uint32_t nsv = 0;
     if (OP == OP_DIFF) {
@@ -453,20 +427,21 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
       if (c.bad) YB2_DECLINE()
     }
     // ---- header: feature flag, nine columns (UpdateDecoderV2 constructor, UpdateDecoder.js:274-293)
-    if (lane == 0) { ist(I_REST, 0) = 0; ist(I_REST, 1) = D.len; }
-    __syncthreads();
+    ist(I_REST, 0) = 0;
+    ist(I_REST, 1) = D.len;
     s_load(D, I_REST);
     uint32_t sb0 = 0, sn = 0;
     {
       s_vu(D, I_REST);  // feature flag (unused)
       const uint32_t map[9] = {I_KC, I_CL, I_LC, I_RC, I_IN, I_SL, I_PI, I_TR, I_LN};
-      for (uint32_t k = 0; k < 9 && !is_bad(); k++) {  // readVarUint8Array x 9: column spans
+#pragma unroll
+      for (uint32_t k = 0; k < 9; k++) {  // readVarUint8Array x 9: column spans
         const uint32_t n = s_vu(D, I_REST);
         const uint32_t c0 = ist(I_REST, 0);
-        if ((uint64_t)c0 + n > D.len) { set_bad(); break; }
-        __syncthreads();
-        if (lane == 0) { ist(map[k], 0) = c0; ist(map[k], 1) = c0 + n; ist(I_REST, 0) = c0 + n; }
-        __syncthreads();
+        if ((uint64_t)c0 + n > D.len) set_bad();
+        ist(map[k], 0) = c0;
+        ist(map[k], 1) = c0 + n;
+        ist(I_REST, 0) = c0 + n;
       }
       if (is_bad()) YB2_DECLINE()
       // the string column = varString(body) | UintOptRle(lengths)
@@ -474,9 +449,8 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
       sn = s_vu(D, I_SL);
       sb0 = ist(I_SL, 0);
       if ((uint64_t)sb0 + sn > ist(I_SL, 1)) set_bad();
-      __syncthreads();
-      if (lane == 0) ist(I_SL, 0) = sb0 + sn;
-      __syncthreads();
+      ist(I_SL, 0) = sb0 + sn;
+#pragma unroll
       for (uint32_t k = 0; k < 9; k++) s_load(D, map[k]);
     }
     if (is_bad()) YB2_DECLINE()
@@ -498,6 +472,7 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
                                     ist(I_SL, 1) - ist(I_SL, 0), ist(I_PI, 1) - ist(I_PI, 0), ist(I_TR, 1) - ist(I_TR, 0),
                                     ist(I_LN, 1) - ist(I_LN, 0), D.len};
       uint32_t tot = 0;
+#pragma unroll
       for (uint32_t k = 0; k < NOUT; k++) tot += in_sz[k] + slack;
       if (lane == 0) scratch = atomicAdd((unsigned long long *)j.used, (unsigned long long)tot);
       scratch = ((uint64_t)lane_read((uint32_t)(scratch >> 32), 0) << 32) | lane_read((uint32_t)scratch, 0);
@@ -506,11 +481,11 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
         __syncthreads();
         continue;
       }
-      if (lane == 0) {
+      {
         uint32_t o = 0;
+#pragma unroll
         for (uint32_t k = 0; k < NOUT; k++) { ost(k, 0) = o; ost(k, 1) = 0; ost(k, 2) = in_sz[k] + slack; o += in_sz[k] + slack; }
       }
-      __syncthreads();
       D.O = j.out + scratch;
     }
     // ---- the walk (13.5.16 LazyStructReader over V2; diff = us@40707, sv = os@37724)
@@ -609,12 +584,12 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
       Cur c = s_cur(D, I_REST, MREST);
       ds0 = c.p - ist(I_REST, 2);
       const uint32_t ndc = rvu(c);
-      s_commit(I_REST, c);
+      s_commit(D, I_REST, c);
       for (uint32_t i = 0; i < ndc && !is_bad(); i++) {
         c = s_cur(D, I_REST, MREST);
         const uint32_t client = rvu(c);
         const uint32_t m = rvu(c);
-        s_commit(I_REST, c);
+        s_commit(D, I_REST, c);
         if (m == 0 || i >= BS_NDSC) { set_bad(); break; }
         bool hit = false;  // readDeleteSet merges a repeated client: the bytes would change
         for (uint32_t h0 = 0; h0 < i; h0 += 64) hit |= __any(h0 + lane < i && X.dsc[h0 + lane] == client);
@@ -626,7 +601,7 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
           c = s_cur(D, I_REST, MREST);
           rvu(c);
           rvu(c);
-          s_commit(I_REST, c);
+          s_commit(D, I_REST, c);
         }
       }
       ds1 = ist(I_REST, 0);
@@ -644,10 +619,12 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
     // ---- final layout: vu(0) | 9 x (vu(n) column) | vu(#parts) parts | delete set
     uint32_t coln[9];
     const uint32_t order[9] = {O_KC, O_CL, O_LC, O_RC, O_IN, O_SB, O_PI, O_TR, O_LN};
+#pragma unroll
     for (uint32_t k = 0; k < 9; k++) coln[k] = ost(order[k], 1);
     const uint32_t sbn = ost(O_SB, 1), sln = ost(O_SL, 1);
     coln[5] = vsz(sbn) + sbn + sln;
     uint32_t total = 1;
+#pragma unroll
     for (uint32_t k = 0; k < 9; k++) total += vsz(coln[k]) + coln[k];
     total += vsz(nparts);
     __threadfence_block();
@@ -682,6 +659,7 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
       return p + n;
     };
     uint32_t p = put(0, 0);
+#pragma unroll
     for (uint32_t k = 0; k < 9; k++) {
       p = put(p, coln[k]);
       if (k == 5) {
