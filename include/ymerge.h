@@ -92,6 +92,9 @@ uint64_t ym_out_bound(const ym_batch *b); /* a capacity that is normally suffici
 int ym_merge(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
 int ym_diff(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
 int ym_sv(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
+/* convertUpdateFormatV1ToV2 (b->format = YM_V1) / convertUpdateFormatV2ToV1 (b->format = YM_V2): one
+ * update per document, re-encoded in the other format (yjs 13.5.x convertUpdateFormat, bundle ms@41803) */
+int ym_convert(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
 
 #ifdef __cplusplus
 }

@@ -7,6 +7,8 @@
 //   encodeStateVectorFromUpdate(update) / ...V2        (yjs: Y.encodeStateVectorFromUpdate[V2])
 //   mergeUpdatesBatch(docs, {format}), diffUpdateBatch(updates, svs, {format}),
 //   encodeStateVectorFromUpdateBatch(updates, {format})
+//   convertUpdateFormatV1ToV2(update) / convertUpdateFormatV2ToV1(update), convertUpdateFormatBatch(updates, {format})
+//                                                      (yjs 13.5.x convertUpdateFormat; format = the input's)
 // There is no CPU fallback: a missing addon or GPU throws.
 'use strict'
 const path = require('path')
@@ -21,7 +23,7 @@ function init () {
   }
 }
 
-const OP = { merge: 0, diff: 1, sv: 2 }
+const OP = { merge: 0, diff: 1, sv: 2, conv: 3 }
 const fmtOf = o => (o && (o.format === 'v2' || o.format === 2)) ? 2 : 1
 
 // status -> the exception yjs itself throws for that input
@@ -86,6 +88,12 @@ function encodeStateVectorFromUpdateBatch (updates, opts, throwErrors = false) {
   return unpack(addon.run(OP.sv, fmtOf(opts), p.arena, p.updOff, p.docUpd), throwErrors)
 }
 
+function convertUpdateFormatBatch (updates, opts, throwErrors = false) {
+  init()
+  const p = pack(updates.map(u => [u]))
+  return unpack(addon.run(OP.conv, fmtOf(opts), p.arena, p.updOff, p.docUpd), throwErrors)
+}
+
 // single-document yjs signatures (mergeUpdates([u]) returns the same object, like yjs)
 const mergeUpdates = updates => updates.length === 1 ? updates[0] : mergeUpdatesBatch([updates], { format: 'v1' }, true)[0]
 const mergeUpdatesV2 = updates => updates.length === 1 ? updates[0] : mergeUpdatesBatch([updates], { format: 'v2' }, true)[0]
@@ -93,8 +101,11 @@ const diffUpdate = (update, sv) => diffUpdateBatch([update], [sv], { format: 'v1
 const diffUpdateV2 = (update, sv) => diffUpdateBatch([update], [sv], { format: 'v2' }, true)[0]
 const encodeStateVectorFromUpdate = u => encodeStateVectorFromUpdateBatch([u], { format: 'v1' }, true)[0]
 const encodeStateVectorFromUpdateV2 = u => encodeStateVectorFromUpdateBatch([u], { format: 'v2' }, true)[0]
+const convertUpdateFormatV1ToV2 = u => convertUpdateFormatBatch([u], { format: 'v1' }, true)[0]
+const convertUpdateFormatV2ToV1 = u => convertUpdateFormatBatch([u], { format: 'v2' }, true)[0]
 
 module.exports = {
   mergeUpdates, mergeUpdatesV2, diffUpdate, diffUpdateV2, encodeStateVectorFromUpdate, encodeStateVectorFromUpdateV2,
-  mergeUpdatesBatch, diffUpdateBatch, encodeStateVectorFromUpdateBatch
+  mergeUpdatesBatch, diffUpdateBatch, encodeStateVectorFromUpdateBatch,
+  convertUpdateFormatV1ToV2, convertUpdateFormatV2ToV1, convertUpdateFormatBatch
 }

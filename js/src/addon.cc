@@ -131,7 +131,10 @@ static napi_value Run(napi_env env, napi_callback_info info) {
   for (int attempt = 0; attempt < 4; attempt++) {
     out_arena.assign(cap ? cap : 1, 0);
     ym_out o = {out_arena.data(), cap, out_off.data(), out_len.data(), status.data(), 0};
-    rc = op == 0 ? ym_merge(&b, &o, nullptr, nullptr) : op == 1 ? ym_diff(&b, &o, nullptr, nullptr) : ym_sv(&b, &o, nullptr, nullptr);
+    rc = op == 0   ? ym_merge(&b, &o, nullptr, nullptr)
+         : op == 1 ? ym_diff(&b, &o, nullptr, nullptr)
+         : op == 3 ? ym_convert(&b, &o, nullptr, nullptr)
+                   : ym_sv(&b, &o, nullptr, nullptr);
     if (rc == YM_ERR_CAPACITY) { cap = o.used + 4096; continue; }
     break;
   }

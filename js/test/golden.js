@@ -15,6 +15,7 @@ for (const f of fs.readdirSync(dir).filter(f => f.endsWith('.json')).sort()) {
     try {
       if (c.op === 'merge') out = (c.fmt === 1 ? Y.mergeUpdates : Y.mergeUpdatesV2)(inputs)
       else if (c.op === 'diff') out = (c.fmt === 1 ? Y.diffUpdate : Y.diffUpdateV2)(inputs[0], new Uint8Array(Buffer.from(c.sv, 'base64')))
+      else if (c.op === 'conv') out = (c.fmt === 1 ? Y.convertUpdateFormatV1ToV2 : Y.convertUpdateFormatV2ToV1)(inputs[0])
       else out = (c.fmt === 1 ? Y.encodeStateVectorFromUpdate : Y.encodeStateVectorFromUpdateV2)(inputs[0])
     } catch (e) { err = e }
     const id = `${f}/${c.name}/v${c.fmt}/${c.op}`

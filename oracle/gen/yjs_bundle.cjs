@@ -22,7 +22,18 @@ Math.random = () => nextU32() / 4294967296
 const KEY = 'webpackChunk_jupyterlab_application_top'
 global.self = global
 global[KEY] = []
-for (const c of CHUNKS) vm.runInThisContext(fs.readFileSync(path.join(BUNDLE_DIR, c), 'utf8'), { filename: c })
+// yjs 13.5.16's convertUpdateFormat (ms@41803) is not exported by the bundle: the chunk text is evaluated
+// with one added statement that hands the function to the fixture generators (in memory only; the
+// files on disk are untouched).  V1ToV2 = ms(u, UpdateDecoderV1 `ye`, UpdateEncoderV2 `De`), V2ToV1 = ks.
+const CONVERT_ANCHOR = 'const ks=t=>ms(t,be,Se);'
+for (const c of CHUNKS) {
+  let src = fs.readFileSync(path.join(BUNDLE_DIR, c), 'utf8')
+  if (c.startsWith('3502.')) {
+    if (src.split(CONVERT_ANCHOR).length !== 2) throw new Error('convertUpdateFormat anchor not found once')
+    src = src.replace(CONVERT_ANCHOR, CONVERT_ANCHOR + 'globalThis.__ymConvert={v1ToV2:t=>ms(t,ye,De),v2ToV1:ks};')
+  }
+  vm.runInThisContext(src, { filename: c })
+}
 const factories = {}
 for (const entry of global[KEY]) Object.assign(factories, entry[1])
 const cache = {}
@@ -42,4 +53,5 @@ load.n = m => { const g = m && m.__esModule ? () => m.default : () => m; load.d(
 load.g = global
 
 const Y = load(73502)
-module.exports = { Y, load }
+const convert = global.__ymConvert  // set when module 73502 ran
+module.exports = { Y, load, convert }

@@ -698,6 +698,51 @@ static Str json_stringify(Ctx *c, const Val *v) {
   Str r = {w.u, w.n};
   return r;
 }
+/* JSON.stringify over any readAny value (V2 -> V1 conversion of embeds / formats): undefined members of
+   objects are omitted, undefined array elements become null, a Uint8Array is an object with index
+   keys, a bigint throws TypeError; a top-level undefined gives JS `undefined`, which writeVarString
+   encodes as the text "undefined" (encodeURIComponent(undefined)). */
+static void json_any_into(Ctx *c, WStr *w, const Val *v) {
+  switch (v->t) {
+    case V_BIGINT: fail(c, YMO_ERR_TYPE); return;
+    case V_BYTES: {
+      ws_put(c, w, '{');
+      for (size_t i = 0; i < v->bytes.n; i++) {
+        char buf[32];
+        if (i) ws_put(c, w, ',');
+        snprintf(buf, sizeof buf, "\"%zu\":%u", i, (unsigned)v->bytes.p[i]);
+        ws_ascii(c, w, buf);
+      }
+      ws_put(c, w, '}');
+      return;
+    }
+    case V_ARR:
+      ws_put(c, w, '[');
+      for (size_t i = 0; i < v->n; i++) { if (i) ws_put(c, w, ','); json_any_into(c, w, v->items[i]); }
+      ws_put(c, w, ']');
+      return;
+    case V_OBJ: {
+      ws_put(c, w, '{');
+      int first = 1;
+      for (size_t i = 0; i < v->n; i++) {
+        if (v->items[i]->t == V_UNDEF) continue;
+        if (!first) ws_put(c, w, ',');
+        first = 0;
+        json_quote(c, w, v->keys[i]); ws_put(c, w, ':'); json_any_into(c, w, v->items[i]);
+      }
+      ws_put(c, w, '}');
+      return;
+    }
+    default: json_stringify_into(c, w, v); return;
+  }
+}
+static Str json_text_of_any(Ctx *c, const Val *v) {
+  WStr w = {NULL, 0, 0};
+  if (v->t == V_UNDEF) ws_ascii(c, &w, "undefined");
+  else json_any_into(c, &w, v);
+  Str r = {w.u, w.n};
+  return r;
+}
 
 /* ------------------------------------------------------------------------------------------------ */
 /* lib0 RLE column decoders (V2)                                                                   */
@@ -1087,14 +1132,14 @@ static Content *read_content(Ctx *c, UDec *u, int info) { /* readItemContent / c
       break;
     }
     case 4: ct->str = ud_string(c, u); break;
-    case 5:
+    case 5:  /* readJSON: V1 JSON.parse(readVarString), V2 readAny; both forms kept for either writer */
       if (u->v2) ct->jval = rd_any(c, &u->rest);
-      else ct->jtext = json_stringify(c, json_parse(c, rd_vstr(c, &u->rest)));
+      else { ct->jval = json_parse(c, rd_vstr(c, &u->rest)); ct->jtext = json_stringify(c, ct->jval); }
       break;
     case 6:
       ct->key = ud_string(c, u);
       if (u->v2) ct->jval = rd_any(c, &u->rest);
-      else ct->jtext = json_stringify(c, json_parse(c, rd_vstr(c, &u->rest)));
+      else { ct->jval = json_parse(c, rd_vstr(c, &u->rest)); ct->jtext = json_stringify(c, ct->jval); }
       break;
     case 7: {
       int64_t tr = ud_typeref(c, u);
@@ -1176,12 +1221,12 @@ static void content_write(Ctx *c, UEnc *e, const Content *ct, int64_t off) {
     case 4: ue_string(c, e, off == 0 ? ct->str : str_slice(ct->str, off, (int64_t)ct->str.n)); break;
     case 5:
       if (e->v2) wr_any(c, e->rest, ct->jval);
-      else wr_vstr(c, e->rest, ct->jtext);
+      else wr_vstr(c, e->rest, ct->jtext.u ? ct->jtext : json_text_of_any(c, ct->jval));
       break;
     case 6:
       ue_key(c, e, ct->key);
       if (e->v2) wr_any(c, e->rest, ct->jval);
-      else wr_vstr(c, e->rest, ct->jtext);
+      else wr_vstr(c, e->rest, ct->jtext.u ? ct->jtext : json_text_of_any(c, ct->jval));
       break;
     case 7:
       ue_typeref(c, e, ct->typeRef);
@@ -1671,6 +1716,28 @@ static Buf *diff_impl(Ctx *c, const uint8_t *upd, size_t len, const uint8_t *svb
   return uenc_finish(c, &enc);
 }
 
+/* convertUpdateFormat (13.5.16 ms@41803; convertUpdateFormatV2ToV1 = ks@42002 = ms(u, UpdateDecoderV2,
+   UpdateEncoderV1), V1ToV2 = ms(u, UpdateDecoderV1, UpdateEncoderV2)): a LazyStructReader that keeps
+   Skips, every struct written with offset 0 through a LazyStructWriter of the other format, then
+   readDeleteSet + writeDeleteSet. */
+static Buf *conv_impl(Ctx *c, const uint8_t *upd, size_t len, int v2_in) {
+  UEnc enc;
+  uenc_init(c, &enc, !v2_in);
+  LWriter w;
+  memset(&w, 0, sizeof(w));
+  w.enc = &enc;
+  UDec dec;
+  udec_init(c, &dec, upd, len, v2_in);
+  LReader r;
+  lr_init(c, &r, &dec, 0);
+  for (; r.curr; lr_next(c, &r)) lw_write(c, &w, r.curr, 0);
+  lw_finish(c, &w);
+  DSet ds;
+  ds_read(c, &dec, &ds);
+  ds_write(c, &enc, &ds);
+  return uenc_finish(c, &enc);
+}
+
 /* encodeStateVectorFromUpdateV2 (13.5.16 os@37724) */
 static Buf *sv_impl(Ctx *c, const uint8_t *upd, size_t len, int v2) {
   Buf *rest = buf_new(c);
@@ -1746,6 +1813,18 @@ int ymo_diff(const uint8_t *upd, size_t len, const uint8_t *sv, size_t sv_len, i
   return rc;
 }
 
+int ymo_convert(const uint8_t *upd, size_t len, int fmt, uint8_t **out, size_t *out_len) {
+  *out = NULL; *out_len = 0;
+  Ctx c;
+  memset(&c, 0, sizeof(c));
+  int code = setjmp(c.jb);
+  if (code) { ctx_free(&c); return code; }
+  Buf *b = conv_impl(&c, upd, len, fmt == 2);
+  int rc = finish_out(&c, b, out, out_len);
+  ctx_free(&c);
+  return rc;
+}
+
 int ymo_sv_from_update(const uint8_t *upd, size_t len, int fmt, uint8_t **out, size_t *out_len) {
   *out = NULL; *out_len = 0;
   Ctx c;
@@ -1797,6 +1876,8 @@ static void *batch_worker(void *arg) {
       const uint8_t *sv = j->sv_arena + j->sv_off[d];
       size_t svl = (size_t)(j->sv_off[d + 1] - j->sv_off[d]);
       st = n >= 1 ? ymo_diff(ptrs[0], lens[0], sv, svl, j->fmt, &out, &olen) : YMO_ERR_UNEXPECTED;
+    } else if (j->op == 3) {
+      st = n >= 1 ? ymo_convert(ptrs[0], lens[0], j->fmt, &out, &olen) : YMO_ERR_UNEXPECTED;
     } else st = n >= 1 ? ymo_sv_from_update(ptrs[0], lens[0], j->fmt, &out, &olen) : YMO_ERR_UNEXPECTED;
     if (st == YMO_OK && j->out_arena) {
       uint64_t cap = j->out_cap_off[d + 1] - j->out_cap_off[d];

@@ -54,6 +54,7 @@ def lib():
                                ctypes.POINTER(ctypes.c_size_t)]
         L.ymo_sv_from_update.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(u8p),
                                          ctypes.POINTER(ctypes.c_size_t)]
+        L.ymo_convert.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t)]
         L.ymo_free.argtypes = [ctypes.c_void_p]
         vp = ctypes.c_void_p
         L.ymo_batch.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, vp, ctypes.c_uint32, vp, vp, ctypes.c_int,
@@ -109,11 +110,21 @@ def sv_from_update(update, fmt=1):
     return st, (_take(out, olen) if st == 0 else None)
 
 
+def convert(update, fmt=1):
+    """convertUpdateFormatV1ToV2 (fmt=1) / convertUpdateFormatV2ToV1 (fmt=2) -> (status, bytes)."""
+    L = lib()
+    u, ul = _buf(update)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    st = L.ymo_convert(ctypes.cast(u, ctypes.POINTER(ctypes.c_uint8)), ul, fmt, ctypes.byref(out), ctypes.byref(olen))
+    return st, (_take(out, olen) if st == 0 else None)
+
+
 def batch(op, fmt, arena, upd_off, doc_upd, sv_arena=None, sv_off=None, nthreads=1, want_output=True):
     """Batched oracle over the engine's arena layout (numpy arrays). op: 'merge'|'diff'|'sv'.
     Returns (out_bytes_list_or_None, status ndarray, out_len ndarray)."""
     L = lib()
-    opc = {"merge": 0, "diff": 1, "sv": 2}[op]
+    opc = {"merge": 0, "diff": 1, "sv": 2, "conv": 3}[op]
     arena = np.ascontiguousarray(arena, dtype=np.uint8)
     upd_off = np.ascontiguousarray(upd_off, dtype=np.uint64)
     doc_upd = np.ascontiguousarray(doc_upd, dtype=np.uint32)

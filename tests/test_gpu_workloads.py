@@ -187,3 +187,25 @@ def test_state_does_not_leak_between_calls(engine):
     outs, status, _ = O.batch("merge", 1, a3, o3, d3)
     bad = _compare(engine.run_host("merge", 1, a3, o3, d3), outs, status)
     assert not bad, bad
+
+
+@pytest.mark.parametrize("fmt", [1, 2])
+def test_convert_workloads_match_oracle(engine, fmt):
+    """convertUpdateFormatV1ToV2 / V2ToV1 (13.5.x convertUpdateFormat) over merged C2 and C5 documents
+    and over the raw C4 updates, against the oracle (pinned by tests/golden/conv.json)."""
+    from yjs_amd import pack_docs
+    ups = []
+    for wl in (f"c2_v{fmt}", f"c5_v{fmt}"):
+        a, o, d = load_ymb(wl)
+        if wl.startswith("c2"):
+            a, o, d = pack_docs([[a[int(o[u]):int(o[u + 1])].tobytes() for u in range(int(d[i]), int(d[i + 1]))]
+                                 for i in range(64)])
+        merged, st, _ = O.batch("merge", fmt, a, o, d, nthreads=8)
+        ups += [m for m, s in zip(merged, st) if s == 0]
+    a, o, d = load_ymb(f"c4_v{fmt}")
+    ups += [a[int(o[u]):int(o[u + 1])].tobytes() for u in range(0, 2000)]
+    a2, o2, d2 = pack_docs([[u] for u in ups])
+    outs, st, _ = O.batch("conv", fmt, a2, o2, d2, nthreads=8)
+    assert (st == 0).all()
+    bad = _compare(engine.run_host("conv", fmt, a2, o2, d2), outs, st)
+    assert not bad, bad[:10]

@@ -14,6 +14,8 @@ def run_case(c):
         return O.merge(c["inputs"], c["fmt"])
     if c["op"] == "diff":
         return O.diff(c["inputs"][0], c["sv"], c["fmt"])
+    if c["op"] == "conv":
+        return O.convert(c["inputs"][0], c["fmt"])
     return O.sv_from_update(c["inputs"][0], c["fmt"])
 
 
@@ -29,8 +31,8 @@ def test_oracle_matches_golden(case):
 
 def test_golden_coverage():
     groups = {c["group"] for c in CASES}
-    assert {"c1_text", "c2_text", "c4_map", "c5_xml", "content", "edge", "refgolden"} <= groups
-    for op in ("merge", "diff", "sv"):
+    assert {"c1_text", "c2_text", "c4_map", "c5_xml", "content", "edge", "refgolden", "conv"} <= groups
+    for op in ("merge", "diff", "sv", "conv"):
         for fmt in (1, 2):
             assert any(c["op"] == op and c["fmt"] == fmt and "expect" in c for c in CASES), (op, fmt)
     assert sum("error" in c for c in CASES) >= 20

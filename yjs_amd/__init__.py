@@ -9,5 +9,6 @@ from .engine import (  # noqa: F401
     mergeUpdates, mergeUpdatesV2, diffUpdate, diffUpdateV2,
     encodeStateVectorFromUpdate, encodeStateVectorFromUpdateV2,
     mergeUpdatesBatch, diffUpdateBatch, encodeStateVectorFromUpdateBatch,
+    convertUpdateFormatV1ToV2, convertUpdateFormatV2ToV1, convertUpdateFormatBatch,
     pack_docs, lib_path,
 )

@@ -258,7 +258,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   j.pend_count = (uint32_t *)(counters + 2);
   j.pend_list = S->list_a.as<uint32_t>();
   j.n = nd;
-  if (op != OP_MERGE) {  // per-block scratch of the streamed diff / state-vector kernels
+  if (op == OP_DIFF || op == OP_SV) {  // per-block scratch of the streamed diff / state-vector kernels
     if (S->bscratch.ensure(BS_GRID * BS_BYTES)) return -2;
     j.bscratch = S->bscratch.as<uint8_t>();
   }
@@ -314,10 +314,10 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
     // what the streamed kernels allocated (k_finish reset the device counter)
     if (op == OP_MERGE) {
       k_fast_region<<<1, 64, 0, st>>>(j, b->n_upd);
-    } else {
+    } else if (fr == 1) {
       S->pinned[16] = S->pinned[0];
       HIPCHK(hipMemcpyAsync(counters, S->pinned + 16, 8, hipMemcpyHostToDevice, st));
-    }
+    }  // else (no specialised kernel ran): the counters are zero (reset by the last k_finish / memset)
     int r = run_general(S, st, j, list, ngen);
     if (r) return r;
     HIPCHK(hipEventRecord(S->evg1, st));
@@ -421,5 +421,6 @@ uint64_t ym_out_bound(const ym_batch *b) {
 int ym_merge(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_MERGE, b, out, stream, stats); }
 int ym_diff(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_DIFF, b, out, stream, stats); }
 int ym_sv(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_SV, b, out, stream, stats); }
+int ym_convert(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_CONV, b, out, stream, stats); }
 
 }  // extern "C"

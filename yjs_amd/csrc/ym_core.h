@@ -876,6 +876,7 @@ YM_INL void ostr_bytes(Out &o, const Ctx &c, const Span &s) {
 // V2 encoder state (UpdateEncoderV2, UpdateEncoder.js:264-408) + V1 (rest only)
 struct Enc {
   uint32_t v2;
+  uint32_t xfmt;  // convertUpdateFormat: the structs were read in the other format (JSON text <-> any)
   Out rest;
   Out kc, cl, lc, rc, in, sb, sl, pi, tr, ln;  // columns; sb = string bytes, sl = string lengths
   int64_t kc_s, kc_n, lc_s, lc_n, rc_s, rc_n;
@@ -974,6 +975,98 @@ YM_INL void e_flush_columns(Enc &e) {
   uopt_flush(e.ln, e.ln_s, e.ln_n);
 }
 
+// convertUpdateFormat of an embed / format value (writeJSON of the value readJSON produced):
+//   V1 -> V2: JSON text (canonical, validated on read) -> writeAny(JSON.parse(text));
+//   V2 -> V1: any value -> writeVarString(JSON.stringify(value)).
+// Exact for literals, strings and integers below 2^31 in magnitude; other numbers, arrays, objects and
+// byte arrays report ST_UNSUPPORTED (the oracle converts them all), a bigint throws TypeError as in JS.
+YM_INL void json_quote_bytes(const Ctx &c, Out &o, uint64_t off, uint64_t n) {  // JSON.stringify(str)
+  o8(o, '"');
+  for (uint64_t i = 0; i < n; i++) {
+    const uint32_t ch = c.A[off + i];
+    if (ch == '"' || ch == '\\') { o8(o, '\\'); o8(o, ch); }
+    else if (ch >= 0x20) o8(o, ch);
+    else if (ch == 8) { o8(o, '\\'); o8(o, 'b'); }
+    else if (ch == 9) { o8(o, '\\'); o8(o, 't'); }
+    else if (ch == 10) { o8(o, '\\'); o8(o, 'n'); }
+    else if (ch == 12) { o8(o, '\\'); o8(o, 'f'); }
+    else if (ch == 13) { o8(o, '\\'); o8(o, 'r'); }
+    else { o8(o, '\\'); o8(o, 'u'); o8(o, '0'); o8(o, '0'); o8(o, '0' + (ch >> 4)); o8(o, "0123456789abcdef"[ch & 15]); }
+  }
+  o8(o, '"');
+}
+YM_INL void e_json_x(Ctx &c, Enc &e, const Span &s) {
+  const uint8_t *a = c.A + s.off;
+  if (e.v2) {  // V1 text -> any
+    if (s.n == 4 && a[0] == 't' && a[1] == 'r' && a[2] == 'u' && a[3] == 'e') { o8(e.rest, 120); return; }
+    if (s.n == 5 && a[0] == 'f' && a[1] == 'a' && a[2] == 'l' && a[3] == 's' && a[4] == 'e') { o8(e.rest, 121); return; }
+    if (s.n == 4 && a[0] == 'n' && a[1] == 'u' && a[2] == 'l' && a[3] == 'l') { o8(e.rest, 126); return; }
+    if (s.n >= 2 && a[0] == '"') {  // a string without escapes: the UTF-8 bytes between the quotes
+      for (uint64_t i = 1; i + 1 < s.n; i++)
+        if (a[i] == '\\') { seterr(c, ST_UNSUPPORTED); return; }
+      o8(e.rest, 119);
+      ovu(e.rest, (int64_t)(s.n - 2));
+      ocopy(e.rest, c, s.off + 1, s.n - 2);
+      return;
+    }
+    // a canonical integer: -?(0|[1-9][0-9]*), |v| < 2^31 (writeAny: varInt)
+    uint64_t i = 0;
+    const bool neg = s.n > 0 && a[0] == '-';
+    if (neg) i++;
+    uint64_t v = 0;
+    if (i >= s.n || s.n - i > 10) { seterr(c, ST_UNSUPPORTED); return; }
+    for (; i < s.n; i++) {
+      if (a[i] < '0' || a[i] > '9') { seterr(c, ST_UNSUPPORTED); return; }
+      v = v * 10 + (a[i] - '0');
+    }
+    if (v >= 0x80000000ull || (neg && v == 0)) { seterr(c, ST_UNSUPPORTED); return; }
+    o8(e.rest, 125);
+    ovi(e.rest, neg, (uint32_t)v);
+    return;
+  }
+  // V2 any -> V1 text
+  const uint32_t tag = a[0];
+  Out &o = e.rest;
+  switch (tag) {
+    case 120: ovu(o, 4); o8(o, 't'); o8(o, 'r'); o8(o, 'u'); o8(o, 'e'); return;
+    case 121: ovu(o, 5); o8(o, 'f'); o8(o, 'a'); o8(o, 'l'); o8(o, 's'); o8(o, 'e'); return;
+    case 126: ovu(o, 4); o8(o, 'n'); o8(o, 'u'); o8(o, 'l'); o8(o, 'l'); return;
+    case 127: ovu(o, 9); for (const char *t = "undefined"; *t; t++) o8(o, (uint32_t)*t); return;  // encodeURIComponent(undefined)
+    case 122: seterr(c, ST_TYPE); return;  // JSON.stringify(bigint)
+    case 125: {  // varInt (canonical, |v| < 2^32 -- rd_any_span validated it): decimal text, -0 -> "0"
+      uint64_t mag = a[1] & 63;
+      const bool neg = a[1] & 64;
+      uint32_t sh = 6;
+      for (uint64_t i = 1; i < s.n && (a[i] & 128); i++) { mag |= (uint64_t)(a[i + 1] & 127) << sh; sh += 7; }
+      char buf[24];
+      int n = 0;
+      do { buf[n++] = (char)('0' + mag % 10); mag /= 10; } while (mag);
+      const bool minus = neg && !(n == 1 && buf[0] == '0');
+      ovu(o, n + (minus ? 1 : 0));
+      if (minus) o8(o, '-');
+      while (n) o8(o, (uint32_t)buf[--n]);
+      return;
+    }
+    case 119: {  // string: JSON.stringify quoting of the UTF-8 bytes (valid UTF-8: no lone surrogates)
+      uint64_t p = 1;
+      uint64_t len = 0;
+      uint32_t sh = 0;
+      for (;;) {
+        const uint32_t b = a[p++];
+        len |= (uint64_t)(b & 127) << sh;
+        sh += 7;
+        if (!(b & 128)) break;
+      }
+      Out cnt = {nullptr, 0};
+      json_quote_bytes(c, cnt, s.off + p, len);
+      ovu(o, (int64_t)cnt.n);
+      json_quote_bytes(c, o, s.off + p, len);
+      return;
+    }
+    default: seterr(c, ST_UNSUPPORTED); return;  // floats, arrays, objects, byte arrays
+  }
+}
+
 // skip k JSON element strings of a ContentJSON starting at its first element (returns new start)
 YM_BIG Span json_elems_from(Ctx &c, const SStruct &s, int64_t k, UOptCol *lens_out) {
   Span out = s.a;
@@ -1058,12 +1151,14 @@ YM_BIG void content_write(Ctx &c, Enc &e, const SStruct &s, int64_t off) {
       break;
     }
     case 5:
-      if (e.v2) ocopy(e.rest, c, s.a.off, s.a.n);
+      if (e.xfmt) e_json_x(c, e, s.a);
+      else if (e.v2) ocopy(e.rest, c, s.a.off, s.a.n);
       else { ovu(e.rest, s.a.n); ocopy(e.rest, c, s.a.off, s.a.n); }
       break;
     case 6:
       e_key(e, c, s.a);
-      if (e.v2) ocopy(e.rest, c, s.b.off, s.b.n);
+      if (e.xfmt) e_json_x(c, e, s.b);
+      else if (e.v2) ocopy(e.rest, c, s.b.off, s.b.n);
       else { ovu(e.rest, s.b.n); ocopy(e.rest, c, s.b.off, s.b.n); }
       break;
     case 7:
@@ -1643,6 +1738,46 @@ YM_BIG void diff_doc(Ctx &c, DocWS &ws, uint64_t uoff, uint64_t ulen, const uint
     L.parts_bytes = w.parts_bytes;
     L.ds_bytes = e.rest.n - ds0;
     layout_finish(L, v2);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// convertUpdateFormat (13.5.16 ms@41803): every struct, Skips included, re-written with offset 0 by a
+// LazyStructWriter of the other format; readDeleteSet + writeDeleteSet.  v2 = the input format.
+// ------------------------------------------------------------------------------------------------
+YM_BIG void conv_doc(Ctx &c, DocWS &ws, uint64_t uoff, uint64_t ulen, uint32_t v2, int pass, Layout &L, uint8_t *out) {
+  Enc e;
+  enc_init(e, !v2);
+  e.xfmt = 1;
+  if (pass == 2) layout_bind(L, e, out);
+  LW w;
+  __builtin_memset(&w, 0, sizeof(LW));
+  w.pass = (uint32_t)pass;
+  w.parts = ws.parts;
+  w.cap = ws.parts_cap;
+  Reader &r = ws.rs[0];
+  reader_open(c, r, uoff, ulen, v2);
+  if (c.err) return;
+  reader_next(c, r);
+  while (!c.err && r.has_curr) {
+    lw_write(c, w, e, r.curr, 0);
+    reader_next(c, r);
+  }
+  if (c.err) return;
+  lw_flush(c, w, e);
+  uint64_t nds = 0;
+  ds_gather(c, r, ws.ds, ws.ds_cap, nds);
+  if (c.err) return;
+  uint64_t ds0 = e.rest.n;
+  ds_emit(c, e, ws.ds, nds, ws.dsg, false);
+  e_flush_columns(e);
+  if (pass == 1) {
+    L.col[C_KC] = e.kc.n; L.col[C_CL] = e.cl.n; L.col[C_LC] = e.lc.n; L.col[C_RC] = e.rc.n; L.col[C_IN] = e.in.n;
+    L.col[C_SB] = e.sb.n; L.col[C_SL] = e.sl.n; L.col[C_PI] = e.pi.n; L.col[C_TR] = e.tr.n; L.col[C_LN] = e.ln.n;
+    L.nparts = w.nparts;
+    L.parts_bytes = w.parts_bytes;
+    L.ds_bytes = e.rest.n - ds0;
+    layout_finish(L, !v2);
   }
 }
 

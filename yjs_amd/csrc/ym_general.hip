@@ -58,6 +58,9 @@ __global__ void __launch_bounds__(64) k_general(GeneralJob j, int pass) {
     if (k != 1) c.err = ST_UNEXPECTED;
     else diff_doc(c, w, j.upd_off[u0], j.upd_off[u0 + 1] - j.upd_off[u0], j.sv + j.sv_off[d], j.sv_off[d + 1] - j.sv_off[d],
                   j.v2, pass, L, out);
+  } else if (j.op == OP_CONV) {
+    if (k != 1) c.err = ST_UNEXPECTED;
+    else conv_doc(c, w, j.upd_off[u0], j.upd_off[u0 + 1] - j.upd_off[u0], j.v2, pass, L, out);
   } else {
     if (k != 1) c.err = ST_UNEXPECTED;
     else sv_doc(c, w, j.upd_off[u0], j.upd_off[u0 + 1] - j.upd_off[u0], j.v2, pass, L, out);

@@ -79,7 +79,7 @@ class _Stats(ctypes.Structure):
                 ("docs_large", ctypes.c_uint64), ("large_ms", ctypes.c_double)]
 
 
-EXPORTS = ("ym_init", "ym_shutdown", "ym_strerror", "ym_out_bound", "ym_merge", "ym_diff", "ym_sv")
+EXPORTS = ("ym_init", "ym_shutdown", "ym_strerror", "ym_out_bound", "ym_merge", "ym_diff", "ym_sv", "ym_convert")
 
 
 def load_library(path=None):
@@ -90,7 +90,7 @@ def load_library(path=None):
     L.ym_init.argtypes = [ctypes.c_int]
     L.ym_strerror.restype = ctypes.c_char_p
     L.ym_out_bound.restype = ctypes.c_uint64
-    for fn in (L.ym_merge, L.ym_diff, L.ym_sv):
+    for fn in (L.ym_merge, L.ym_diff, L.ym_sv, L.ym_convert):
         fn.argtypes = [ctypes.POINTER(_Batch), ctypes.POINTER(_Out), ctypes.c_void_p, ctypes.POINTER(_Stats)]
         fn.restype = ctypes.c_int
     return L
@@ -146,7 +146,7 @@ class Engine:
             b.sv_arena = sv_arena.ctypes.data if sv_arena.size else None
             b.sv_off = sv_off.ctypes.data
         cap = int(self.lib.ym_out_bound(ctypes.byref(b)))
-        fn = {"merge": self.lib.ym_merge, "diff": self.lib.ym_diff, "sv": self.lib.ym_sv}[op]
+        fn = {"merge": self.lib.ym_merge, "diff": self.lib.ym_diff, "sv": self.lib.ym_sv, "conv": self.lib.ym_convert}[op]
         for _ in range(4):
             out_arena = np.zeros(max(cap, 1), np.uint8)
             out_off = np.zeros(max(n_docs, 1), np.uint64)
@@ -180,7 +180,7 @@ class Engine:
             b.sv_arena = sv_arena.data_ptr()
             b.sv_off = sv_off.data_ptr()
         o = _Out(out_arena.data_ptr(), out_arena.numel(), out_off.data_ptr(), out_len.data_ptr(), status.data_ptr(), 0)
-        fn = {"merge": self.lib.ym_merge, "diff": self.lib.ym_diff, "sv": self.lib.ym_sv}[op]
+        fn = {"merge": self.lib.ym_merge, "diff": self.lib.ym_diff, "sv": self.lib.ym_sv, "conv": self.lib.ym_convert}[op]
         s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
         rc = fn(ctypes.byref(b), ctypes.byref(o), s, ctypes.byref(self.last_stats))
         return rc, int(o.used)
@@ -201,7 +201,7 @@ class Engine:
             b.sv_arena = sv_arena.data_ptr()
             b.sv_off = sv_off.data_ptr()
         o = _Out(out_arena.data_ptr(), out_arena.numel(), out_off.data_ptr(), out_len.data_ptr(), status.data_ptr(), 0)
-        fn = {"merge": self.lib.ym_merge, "diff": self.lib.ym_diff, "sv": self.lib.ym_sv}[op]
+        fn = {"merge": self.lib.ym_merge, "diff": self.lib.ym_diff, "sv": self.lib.ym_sv, "conv": self.lib.ym_convert}[op]
         s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
         pb, po, ps = ctypes.byref(b), ctypes.byref(o), ctypes.byref(self.last_stats)
         keep = (b, o)
@@ -284,3 +284,17 @@ def encodeStateVectorFromUpdate(update):
 
 def encodeStateVectorFromUpdateV2(update):
     return encodeStateVectorFromUpdateBatch([update], 2, True)[0]
+
+
+def convertUpdateFormatBatch(updates, fmt=1, raise_errors=False):
+    """yjs 13.5.x convertUpdateFormat over a batch: fmt = the input format (1: V1 -> V2, 2: V2 -> V1)."""
+    arena, upd_off, doc_upd = pack_docs([[u] for u in updates])
+    return _unpack(*_engine().run_host("conv", fmt, arena, upd_off, doc_upd), raise_errors)
+
+
+def convertUpdateFormatV1ToV2(update):
+    return convertUpdateFormatBatch([update], 1, True)[0]
+
+
+def convertUpdateFormatV2ToV1(update):
+    return convertUpdateFormatBatch([update], 2, True)[0]
