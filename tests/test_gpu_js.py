@@ -21,3 +21,9 @@ def test_js_api_golden():
     # unsupported: the 5 non-canonical JSON texts, their 2 conversions, 12 object-valued embeds / formats
     # in conversions
     assert res["ok"] >= 990 and res["unsupported"] <= 19, res
+
+
+@pytest.mark.skipif(shutil.which("node") is None, reason="node not installed on this box")
+def test_js_sync_round():
+    r = subprocess.run(["node", os.path.join(ROOT, "js", "test", "sync.js")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
