@@ -63,6 +63,7 @@ struct DevState {
   uint64_t *pinned = nullptr;   // host memory the finishing kernel writes into (no copy op)
   uint64_t *pinned_dev = nullptr;  // ... its device address
   bool dirty = true;            // device counters not known to be reset (first call, failed call)
+  uint64_t seq = 0;             // call sequence number: the fast paths' completion flag (pinned[7])
 };
 
 thread_local DevState *g_state = nullptr;
@@ -105,13 +106,24 @@ __global__ void k_status_flags(const uint32_t *list, uint32_t n, const int32_t *
 // into pinned host memory, and resets the declined-document counter for the next launch.
 __global__ void __launch_bounds__(1024) k_finish(const int32_t *status, const uint64_t *out_len, uint32_t n,
                                                  const uint64_t *upd_off, uint32_t n_upd, uint64_t *counters,
-                                                 volatile uint64_t *host, int stats, int merge) {
+                                                 volatile uint64_t *host, int stats, int merge, uint64_t seq) {
   __shared__ unsigned long long red[2][16];
   uint64_t err = 0, bytes = 0;
-  for (uint32_t i = threadIdx.x; stats && i < n; i += blockDim.x) {
-    const bool ok = status[i] == 0;
-    err += !ok;
-    bytes += ok ? out_len[i] : 0;
+  // batches of 16 independent loads per thread (latency of one HBM round trip per batch, not per doc)
+  for (uint32_t i0 = 0; stats && i0 < n; i0 += 16 * blockDim.x) {
+    int32_t sv[16];
+    uint64_t lv[16];
+#pragma unroll
+    for (uint32_t t = 0; t < 16; t++) {
+      const uint32_t i = i0 + t * blockDim.x + threadIdx.x;
+      sv[t] = i < n ? status[i] : 0;
+      lv[t] = i < n ? out_len[i] : 0;
+    }
+#pragma unroll
+    for (uint32_t t = 0; t < 16; t++) {
+      err += sv[t] != 0;
+      bytes += sv[t] == 0 ? lv[t] : 0;
+    }
   }
   for (int o = 32; o > 0; o >>= 1) {
     err += __shfl_down(err, o, 64);
@@ -132,6 +144,7 @@ __global__ void __launch_bounds__(1024) k_finish(const int32_t *status, const ui
     host[6] = upd_off[n_upd] - upd_off[0];
     counters[0] = 0;                             // used := 0 and pend_count (counters + 2) := 0: the
     ((uint32_t *)counters)[4] = 0;               // next launch starts clean (see run_op for the general path)
+    host[7] = seq;                               // completion word (the host spins on it)
   }
 }
 
@@ -232,7 +245,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
     o_len = S->out_len.as<uint64_t>();
     o_status = S->status.as<int32_t>();
   }
-  if (S->layout.ensure(nd * sizeof(ym::Layout) + 16) || S->counters.ensure(256) || S->list_a.ensure((nd + 1) * 4ull) ||
+  if (S->layout.ensure(nd * sizeof(ym::Layout) + 16) || S->counters.ensure(1024) || S->list_a.ensure((nd + 1) * 4ull) ||
       S->list_b.ensure((nd + 1) * 4ull))
     return -2;
   uint64_t *counters = S->counters.as<uint64_t>();
@@ -258,19 +271,26 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   j.pend_count = (uint32_t *)(counters + 2);
   j.pend_list = S->list_a.as<uint32_t>();
   j.n = nd;
+  const uint64_t seq = ++S->seq;
   if (op == OP_DIFF || op == OP_SV) {  // per-block scratch of the streamed diff / state-vector kernels
     if (S->bscratch.ensure(BS_GRID * BS_BYTES)) return -2;
     j.bscratch = S->bscratch.as<uint8_t>();
   }
 
-  if (S->dirty) HIPCHK(hipMemsetAsync(counters, 0, 256, st));
+  if (S->dirty) HIPCHK(hipMemsetAsync(counters, 0, 1024, st));
   S->dirty = true;
   // ends a round trip: counters and stats land in pinned host memory, then one stream sync
   auto finish = [&]() -> int {
     k_finish<<<1, 1024, 0, st>>>(o_status, o_len, nd, upd_off, b->n_upd, counters, S->pinned_dev, stats ? 1 : 0,
-                                   op == OP_MERGE ? 1 : 0);
+                                   op == OP_MERGE ? 1 : 0, seq);
     HIPCHK(hipEventRecord(S->ev1, st));
-    HIPCHK(hipStreamSynchronize(st));
+    // spin on the completion word k_finish writes last (no interrupt wake-up of a blocking wait), then
+    // the stream sync, which finds the stream drained: it is what orders every result for the host
+    volatile uint64_t *hp = S->pinned;
+    for (uint64_t it = 0; hp[7] != seq && it < (1ull << 26); it++) __builtin_ia32_pause();
+    hipError_t q;
+    for (int it = 0; (q = hipStreamQuery(st)) == hipErrorNotReady && it < 100000; it++) __builtin_ia32_pause();
+    if (q != hipSuccess) HIPCHK(hipStreamSynchronize(st));
     return 0;
   };
   HIPCHK(hipEventRecord(S->ev0, st));
