@@ -278,7 +278,7 @@ def main():
                          "traffic": traffic, "avg_launch_ms": round(avg_fast, 5),
                          "algorithmic_bytes_per_launch": int(alg_bytes)},
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the host baseline is reported at N = 1 only
             line["cpu_baseline"] = cpu_baseline(arena, upd_off, doc_upd, fmt, args.cpu_baseline_seconds)
         if not args.no_secondary and world == 1:
             line["secondary"] = secondary(dev, eng)
