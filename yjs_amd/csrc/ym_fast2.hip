@@ -71,8 +71,13 @@ static_assert(L_GBYR + 2 * DSN <= L_RCEND, "delete-set arrays fit the record reg
 __device__ __forceinline__ uint32_t rvi(Cur &c, bool &neg) {
   const uint64_t x = ld8(c.p);
   const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-  const uint32_t nb = vu_nb(lo, hi);
   neg = (lo & 0x40) != 0;
+  if (__all((lo & 0x80u) == 0)) {  // every active lane: a one-byte varInt
+    c.bad |= c.p >= c.e;
+    c.p += 1;
+    return lo & 0x3fu;
+  }
+  const uint32_t nb = vu_nb(lo, hi);
   uint32_t m = (lo & 0x3fu) | ((lo >> 2) & 0x1fc0u) | ((lo >> 3) & 0xfe000u) | ((lo >> 4) & 0x7f00000u) | ((hi & 0x7fu) << 27);
   const uint32_t bits = 6 + 7 * (nb - 1);
   if (nb < 5) m &= (1u << bits) - 1u;
