@@ -20,12 +20,12 @@ oo = torch.empty(n, dtype=torch.int64, device=dev); ol = torch.empty(n, dtype=to
 e = Engine(0)
 ms = []
 for i in range(25):
-    rc, used = e.run_device("merge", 1, ga, go, gd, oa, oo, ol, st)
+    rc, used = e.run_device("merge", 2 if os.environ.get("WL", "c2_v1").endswith("v2") else 1, ga, go, gd, oa, oo, ol, st)
     if i >= 5: ms.append(e.last_stats.fast_ms)
 print(json.dumps({"stop": int(os.environ.get("YMERGE_FAST_STOP", "0")), "fast_ms_mean": float(np.mean(ms)), "fast_ms_min": float(np.min(ms))}))
 ''' % ROOT
 
-for stop in [1, 2, 3, 4, 5, 6, 0]:
+for stop in ([1, 2, 3, 4, 5, 6, 7, 0] if os.environ.get("WL", "").endswith("v2") else [1, 2, 3, 4, 5, 6, 0]):
     env = dict(os.environ, YMERGE_FAST_STOP=str(stop))
     r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
     line = [l for l in r.stdout.splitlines() if l.startswith("{")]

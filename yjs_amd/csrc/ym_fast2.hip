@@ -377,6 +377,14 @@ __device__ uint32_t col_encode(Get get, uint32_t n, bool wr, Slot o, uint32_t ba
     continue;                            \
   }
 
+// STOP > 0: timing-only variant ending every document after phase STOP (tools/ablate_fast.py)
+#define YM2_STOP(n)                                                     \
+  if (STOP == (n)) {                                                    \
+    if (lane == 0) { j.status[d] = ym::ST_OK; j.out_len[d] = 0; }       \
+    __syncthreads();                                                    \
+    continue;                                                           \
+  }
+template <int STOP>
 __global__ void __launch_bounds__(64) k_fast_merge_v2(GeneralJob j) {
   const uint32_t lane = threadIdx.x;
   const uint64_t arena0 = j.upd_off[0];
@@ -397,6 +405,7 @@ __global__ void __launch_bounds__(64) k_fast_merge_v2(GeneralJob j) {
     for (uint32_t i = lane; i <= k; i += 64) at<uint16_t>(L_UOFF + 2 * i) = (uint16_t)(j.upd_off[u0 + i] - b0 + base);
     if (lane < 2) at<uint32_t>(L_MISC + 4 * lane) = 0;
     __syncthreads();
+    YM2_STOP(1)
     // ---- 2. walk
     bool ok = true;
 #pragma unroll 1
@@ -410,6 +419,7 @@ __global__ void __launch_bounds__(64) k_fast_merge_v2(GeneralJob j) {
       if (nds & 1) at<uint64_t>(L_DKEY + 8 * nds) = ~0ull;
     }
     __syncthreads();
+    YM2_STOP(2)
     // ---- 3. struct rank sort (records move to rank order; the slot array detects duplicates)
     {
       uint64_t rk[E];
@@ -457,6 +467,7 @@ __global__ void __launch_bounds__(64) k_fast_merge_v2(GeneralJob j) {
       }
       if (__any(dup)) YM2_DECLINE()
     }
+    YM2_STOP(3)
     // ---- 4. layout over rank order; lane owns positions r = E*lane + s
     uint64_t sk[E];
     uint32_t sl_[E], sa[E], s0[E], s1[E], s2[E], ssp[E], pstart[E], gapv[E], runu[E];
@@ -512,6 +523,7 @@ __global__ void __launch_bounds__(64) k_fast_merge_v2(GeneralJob j) {
       for (uint32_t s = 0; s < E; s++)
         runu[s] = pstart[s] ? at<uint16_t>(L_PLAST + 2 * (pu[s] >> 16)) - at<uint16_t>(L_PFIRST + 2 * (pu[s] >> 16)) : 0;
     }
+    YM2_STOP(4)
     // ---- 5. columns.  Entry counts per struct (Item.write / LazyStructWriter routing, V2)
     uint32_t cA[E], cB[E], cC[E];  // (cl | lc << 10 | rc << 20), (in | pi << 10 | st << 20), (kc | tr << 10 | ln << 20)
 #pragma unroll
@@ -603,6 +615,7 @@ __global__ void __launch_bounds__(64) k_fast_merge_v2(GeneralJob j) {
     csz[7] = col_encode<K_UOPT>(g_tr, ntr, false, none, 0, cbad);
     csz[8] = col_encode<K_UOPT>(g_ln, nln, false, none, 0, cbad);
     if (__any(cbad)) YM2_DECLINE()
+    YM2_STOP(5)
     uint32_t colbytes = 1;
 #pragma unroll
     for (uint32_t c = 0; c < 9; c++) colbytes += vsz(csz[c]) + csz[c];
@@ -667,6 +680,7 @@ __global__ void __launch_bounds__(64) k_fast_merge_v2(GeneralJob j) {
       col_encode<K_UOPT>(g_tr, ntr, true, dst, cb[7], cbad);
       col_encode<K_UOPT>(g_ln, nln, true, dst, cb[8], cbad);
     }
+    YM2_STOP(6)
     // ---- rest: vu(#parts) | per struct: part header, Skip length, payload
     if (lane == 0) put_vu(dst, colbytes, nparts);
     {
@@ -683,6 +697,7 @@ __global__ void __launch_bounds__(64) k_fast_merge_v2(GeneralJob j) {
       }
     }
     const uint32_t dsb = rest_base + rest_bytes;
+    YM2_STOP(7)
     // ---- 6. delete set (as ym_fast.hip step 5, V2 encoding: clock - previous end, len - 1)
     {
       uint64_t dk[E];
@@ -909,7 +924,14 @@ int fast2_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t s
   if (op != OP_MERGE || !j.v2) return 0;
   (void)n_upd;
   const uint32_t grid = j.n < 131072 ? j.n : 131072;
-  fastv2::k_fast_merge_v2<<<grid, 64, fastv2::LDS_BYTES, st>>>(j);
+  static int stop = -1;
+  if (stop < 0) { const char *e = getenv("YMERGE_FAST_STOP"); stop = e ? atoi(e) : 0; }
+  switch (stop) {
+#define YM2_L(S) case S: fastv2::k_fast_merge_v2<S><<<grid, 64, fastv2::LDS_BYTES, st>>>(j); break;
+    YM2_L(1) YM2_L(2) YM2_L(3) YM2_L(4) YM2_L(5) YM2_L(6) YM2_L(7)
+    default: fastv2::k_fast_merge_v2<0><<<grid, 64, fastv2::LDS_BYTES, st>>>(j); break;
+#undef YM2_L
+  }
   return 1;
 }
 
