@@ -48,7 +48,10 @@ constexpr uint32_t L_DSLOT = L_DSEQ + 2 * DSN;     // u8
 constexpr uint32_t L_PFIRST = L_DSLOT + DSN;       // u16[REC]
 constexpr uint32_t L_PLAST = L_PFIRST + 2 * REC;   // u16[REC]
 constexpr uint32_t L_END = L_PLAST + 2 * REC;
-constexpr uint32_t LDS_BYTES = L_END;
+// output staging (merged outputs are about the input size; larger ones decline to the general path)
+constexpr uint32_t L_OUT = (L_END + 15) & ~15u, OUTCAP = IN + 1024;
+constexpr uint32_t LDS_BYTES = L_OUT + OUTCAP;
+static_assert(8 * LDS_BYTES <= 160 * 1024, "staging keeps 2 waves per SIMD (the VGPR bound)");
 // phase 5: per-column value arrays over the record region (the records are held in registers)
 constexpr uint32_t V_CL = R;                       // u32[3 * REC]
 constexpr uint32_t V_LC = V_CL + 12 * REC;         // u32[REC]
@@ -126,7 +129,7 @@ __device__ __forceinline__ void decline(const GeneralJob &j, uint32_t d) {
 }
 
 // Walks one V2 update (lane-private decoders) and appends struct records and delete ranges.
-__device__ bool walk_v2(uint32_t u) {
+__device__ __forceinline__ bool walk_v2(uint32_t u) {
   const uint32_t p0 = at<uint16_t>(L_UOFF + 2 * u), p1 = at<uint16_t>(L_UOFF + 2 * u + 2);
   Cur h = {p0, p1, false};
   rvu(h);  // feature flag
@@ -267,7 +270,8 @@ __device__ bool walk_v2(uint32_t u) {
 // ---- wave-parallel RLE column encoders ------------------------------------------------------------
 // lib0 writeVarInt size for a magnitude (sign lives in the first byte)
 __device__ __forceinline__ uint32_t vszi(uint32_t m) { return m < 64 ? 1 : 1 + vsz(m >> 6); }
-__device__ __forceinline__ uint32_t put_vi(Slot o, uint32_t p, bool neg, uint32_t m) {
+template <class O>
+__device__ __forceinline__ uint32_t put_vi(O o, uint32_t p, bool neg, uint32_t m) {
   ob8(o, p++, (m > 63 ? 0x80 : 0) | (neg ? 0x40 : 0) | (m & 63));
   m >>= 6;
   while (m > 0) { ob8(o, p++, (m > 127 ? 0x80 : 0) | (m & 127)); m >>= 7; }
@@ -286,40 +290,45 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
 }
 enum { K_UOPT = 0, K_IDIF = 1, K_RLE = 2 };
 constexpr uint32_t CPL = 6;  // column elements per lane (3 * REC / 64)
-// Encodes the n values get(i) (i < n <= 64 * CPL) with the lib0 encoder of kind K.  Returns the byte
-// size; writes the bytes at o[base ..] when `wr`.  Runs are found from neighbour compares (diffs for
-// IntDiffOptRle), run lengths from a running max of run-start positions, run bytes by a prefix sum
-// over run ends (each run end writes its run).  `bad` is set for diffs outside (-2^30, 2^30).
-template <int K, class Get>
-__device__ uint32_t col_encode(Get get, uint32_t n, bool wr, Slot o, uint32_t base, bool &bad) {
+// Encodes the n values get(i) (i < n <= 64 * C) with the lib0 encoder of kind K, C consecutive
+// elements per lane.  Returns the byte size; writes the bytes at o[base ..] when `wr`.  Runs are found
+// from neighbour compares (diffs for IntDiffOptRle), run lengths from a running max of run-start
+// positions, run bytes by a prefix sum over run ends (each run end writes its run).  Values are u32;
+// diffs are computed in 32 bits and `bad` is set for values >= 2^31 or diffs outside (-2^30, 2^30).
+template <int K, uint32_t C, class Get, class O>
+__device__ __forceinline__ uint32_t col_enc(Get get, uint32_t n, bool wr, O o, uint32_t base, bool &bad) {
   const uint32_t lane = threadIdx.x;
-  const uint32_t i0 = lane * CPL;
-  int64_t val[CPL + 2];  // values (or diffs) of elements i0 - 1 .. i0 + CPL
+  const uint32_t i0 = lane * C;
+  uint32_t val[C + 2];  // values (or diffs) of elements i0 - 1 .. i0 + C
+  uint32_t prev = 0;
 #pragma unroll
-  for (uint32_t t = 0; t < CPL + 2; t++) {
-    const int64_t i = (int64_t)i0 + t - 1;
-    int64_t v = 0;
-    if (i >= 0 && i < (int64_t)n) {
-      v = (int64_t)get((uint32_t)i);
-      if (K == K_IDIF) v -= i > 0 ? (int64_t)get((uint32_t)i - 1) : 0;
+  for (uint32_t t = 0; t < C + 2; t++) {
+    const int32_t i = (int32_t)i0 + (int32_t)t - 1;
+    uint32_t v = 0;
+    if (i >= 0 && i < (int32_t)n) {
+      v = get((uint32_t)i);
+      if (K == K_IDIF) {
+        const uint32_t pv = t == 0 ? (i > 0 ? get((uint32_t)i - 1) : 0) : prev;
+        prev = v;
+        bad |= ((v | pv) >> 31) != 0;
+        v -= pv;
+      }
     }
     val[t] = v;
   }
-  uint32_t sp_local = 0, last_sp = 0;
-  uint32_t bytes_lane = 0;
-  uint32_t rb[CPL];
-  // pass 1: start positions (running max), run ends, run bytes
-  bool st[CPL];
+  uint32_t last_sp = 0, bytes_lane = 0;
+  uint32_t rb[C];
+  bool st[C];
 #pragma unroll
-  for (uint32_t t = 0; t < CPL; t++) {
+  for (uint32_t t = 0; t < C; t++) {
     const uint32_t i = i0 + t;
     st[t] = i < n && (i == 0 || val[t + 1] != val[t]);
     if (st[t]) last_sp = i;
   }
   const uint32_t carry = YM_DPP(wave_incl_max(last_sp), 0x138, 0xf);  // wave_shr:1 -> exclusive
-  sp_local = carry;
+  uint32_t sp_local = carry;
 #pragma unroll
-  for (uint32_t t = 0; t < CPL; t++) {
+  for (uint32_t t = 0; t < C; t++) {
     const uint32_t i = i0 + t;
     rb[t] = 0;
     if (i >= n) continue;
@@ -327,12 +336,13 @@ __device__ uint32_t col_encode(Get get, uint32_t n, bool wr, Slot o, uint32_t ba
     const bool end = i + 1 == n || val[t + 2] != val[t + 1];
     if (!end) continue;
     const uint32_t cnt = i - sp_local + 1;
-    const int64_t v = val[t + 1];
+    const uint32_t v = val[t + 1];
     if (K == K_UOPT) {
-      rb[t] = vszi((uint32_t)v) + (cnt > 1 ? vsz(cnt - 2) : 0);
+      rb[t] = vszi(v) + (cnt > 1 ? vsz(cnt - 2) : 0);
     } else if (K == K_IDIF) {
-      bad |= v <= -(1ll << 30) || v >= (1ll << 30);
-      const int32_t x = (int32_t)((uint32_t)(int32_t)v << 1) | (cnt > 1 ? 1 : 0);
+      const int32_t sv = (int32_t)v;
+      bad |= sv <= -(1 << 30) || sv >= (1 << 30);
+      const int32_t x = (int32_t)(v << 1) | (cnt > 1 ? 1 : 0);
       rb[t] = vszi(x < 0 ? 0u - (uint32_t)x : (uint32_t)x) + (cnt > 1 ? vsz(cnt - 2) : 0);
     } else {
       rb[t] = 1 + (i + 1 == n ? 0 : vsz(cnt - 1));  // Rle<u8>: the final run's count is never written
@@ -345,29 +355,36 @@ __device__ uint32_t col_encode(Get get, uint32_t n, bool wr, Slot o, uint32_t ba
     uint32_t p = base + incl - bytes_lane;
     uint32_t sp2 = carry;
 #pragma unroll
-    for (uint32_t t = 0; t < CPL; t++) {
+    for (uint32_t t = 0; t < C; t++) {
       const uint32_t i = i0 + t;
       if (i >= n) continue;
       if (st[t]) sp2 = i;
       if (rb[t] == 0) continue;
       const uint32_t cnt = i - sp2 + 1;
-      const int64_t v = val[t + 1];
+      const uint32_t v = val[t + 1];
       uint32_t q = p;
       if (K == K_UOPT) {
-        q = put_vi(o, q, cnt > 1, (uint32_t)v);  // count==1 ? v : -v (-0 for v == 0)
+        q = put_vi(o, q, cnt > 1, v);  // count==1 ? v : -v (-0 for v == 0)
         if (cnt > 1) q = put_vu(o, q, cnt - 2);
       } else if (K == K_IDIF) {
-        const int32_t x = (int32_t)((uint32_t)(int32_t)v << 1) | (cnt > 1 ? 1 : 0);
+        const int32_t x = (int32_t)(v << 1) | (cnt > 1 ? 1 : 0);
         q = put_vi(o, q, x < 0, x < 0 ? 0u - (uint32_t)x : (uint32_t)x);
         if (cnt > 1) q = put_vu(o, q, cnt - 2);
       } else {
-        ob8(o, q++, (uint32_t)v);
+        ob8(o, q++, v);
         if (i + 1 != n) q = put_vu(o, q, cnt - 1);
       }
       p += rb[t];
     }
   }
   return total;
+}
+// n is wave-uniform: short columns (the common case) run with one or two elements per lane.
+template <int K, class Get, class O>
+__device__ __forceinline__ uint32_t col_encode(Get get, uint32_t n, bool wr, O o, uint32_t base, bool &bad) {
+  if (n <= 64) return col_enc<K, 1>(get, n, wr, o, base, bad);
+  if (n <= 128) return col_enc<K, 2>(get, n, wr, o, base, bad);
+  return col_enc<K, CPL>(get, n, wr, o, base, bad);
 }
 
 #define YM2_DECLINE()                    \
@@ -647,7 +664,8 @@ __global__ void __launch_bounds__(64) k_fast_merge_v2(GeneralJob j) {
       __syncthreads();
       continue;
     }
-    const Slot dst = make_slot(j.out + slot_al, (uint32_t)(slot_end - slot_al));
+    if (rest_base + rest_bytes > OUTCAP) YM2_DECLINE()
+    const LSlot dst{L_OUT};
     // ---- write the columns: vu(0) | 9 x (vu(size) | bytes)
     {
       uint32_t p = 0;
@@ -673,7 +691,7 @@ __global__ void __launch_bounds__(64) k_fast_merge_v2(GeneralJob j) {
         const uint32_t i = lane * CPL + q;
         if (i >= nst) break;
         const uint32_t e = at<uint32_t>(V_ST + 4 * i), a = e & 0xffff, n = e >> 16;
-        for (uint32_t b = 0; b < n; b++) ob8(dst, sbase + sboff[q] + b, sm[a + b]);
+        lds_copy(dst.b + sbase + sboff[q], a, n);
       }
       col_encode<K_UOPT>(g_sl, nst, true, dst, sbase + sbody, cbad);
       col_encode<K_RLE>(g_pi, npi, true, dst, cb[6], cbad);
@@ -692,7 +710,7 @@ __global__ void __launch_bounds__(64) k_fast_merge_v2(GeneralJob j) {
         if (pstart[s]) { q = put_vu(dst, q, runu[s]); q = put_vu(dst, q, (uint32_t)sk[s]); }
         if (gapv[s]) q = put_vu(dst, q, gapv[s]);
         const uint32_t a = ssp[s] & 0xffff, n = ssp[s] >> 16;
-        for (uint32_t b = 0; b < n; b++) ob8(dst, q + b, sm[a + b]);
+        lds_copy(dst.b + q, a, n);
         p += rb[s];
       }
     }
@@ -892,6 +910,7 @@ __global__ void __launch_bounds__(64) k_fast_merge_v2(GeneralJob j) {
       __syncthreads();
       continue;
     }
+    if (total > OUTCAP) YM2_DECLINE()
     if (lane == 0) put_vu(dst, dsb, ngroups);
 #pragma unroll
     for (uint32_t s = 0; s < E; s++) {
@@ -908,6 +927,8 @@ __global__ void __launch_bounds__(64) k_fast_merge_v2(GeneralJob j) {
         put_vu(dst, put_vu(dst, off, c0 - pe), e0 - c0 - 1);
       }
     }
+    __syncthreads();
+    copy_out(j.out + slot_al, L_OUT, total, slot_end - slot_al);
     if (lane == 0) {
       j.out_off[d] = slot_al;
       j.out_len[d] = total;

@@ -72,11 +72,39 @@ __device__ __forceinline__ void ob8(Slot o, uint32_t p, uint32_t v) {
 __device__ __forceinline__ void ob32(Slot o, uint32_t p, uint32_t v) {
   __builtin_amdgcn_raw_buffer_store_b32((int)v, o, (int)p, 0, 0);
 }
+// The document's output staged in LDS at byte offset b (copied out with 16-byte stores afterwards:
+// byte-wise global stores cost a memory-pipeline slot each).
+struct LSlot {
+  uint32_t b;
+};
+__device__ __forceinline__ void ob8(LSlot o, uint32_t p, uint32_t v) { sm[o.b + p] = (uint8_t)v; }
 // lib0 writeVarUint straight into the output slot
-__device__ __forceinline__ uint32_t put_vu(Slot o, uint32_t p, uint64_t v) {
+template <class O>
+__device__ __forceinline__ uint32_t put_vu(O o, uint32_t p, uint64_t v) {
   while (v > 127) { ob8(o, p++, 0x80 | (uint32_t)(v & 127)); v >>= 7; }
   ob8(o, p++, (uint32_t)v);
   return p;
+}
+// Lane-serial LDS -> LDS byte copy (regions do not overlap): eight loads in flight per wait instead of one.
+__device__ __forceinline__ void lds_copy(uint32_t dst, uint32_t src, uint32_t n) {
+  uint32_t b = 0;
+  for (; b + 8 <= n; b += 8) {
+    uint8_t t[8];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) t[k] = sm[src + b + k];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) sm[dst + b + k] = t[k];
+  }
+  for (; b < n; b++) sm[dst + b] = sm[src + b];
+}
+// Copies n staged bytes from LDS offset src to g (16-aligned) with 16-byte stores; `room` bytes are
+// writable at g, so the last chunk is written whole when it fits and byte-wise otherwise.
+__device__ __forceinline__ void copy_out(uint8_t *g, uint32_t src, uint32_t n, uint64_t room) {
+  const uint32_t lane = threadIdx.x;
+  const uint32_t n16 = ((uint64_t)((n + 15) & ~15u) <= room ? n + 15 : n) >> 4;
+  for (uint32_t k = lane; k < n16; k += 64)
+    *reinterpret_cast<uint4 *>(g + 16 * k) = *reinterpret_cast<const uint4 *>(sm + src + 16 * k);
+  for (uint32_t i = 16 * n16 + lane; i < n; i += 64) g[i] = sm[src + i];
 }
 
 // ---- V1 walker over LDS bytes ---------------------------------------------------------------------
