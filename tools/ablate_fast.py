@@ -25,7 +25,7 @@ for i in range(25):
 print(json.dumps({"stop": int(os.environ.get("YMERGE_FAST_STOP", "0")), "fast_ms_mean": float(np.mean(ms)), "fast_ms_min": float(np.min(ms))}))
 ''' % ROOT
 
-for stop in ([1, 2, 3, 4, 5, 6, 7, 0] if os.environ.get("WL", "").endswith("v2") else [1, 2, 3, 4, 5, 6, 0]):
+for stop in ([1, 2, 3, 4, 5, 6, 7, 0] if os.environ.get("WL", "").endswith("v2") else [int(x) for x in os.environ.get('STOPS', '1 2 3 4 5 6 0').split()]):
     env = dict(os.environ, YMERGE_FAST_STOP=str(stop))
     r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
     line = [l for l in r.stdout.splitlines() if l.startswith("{")]

@@ -55,7 +55,7 @@ constexpr uint32_t L_RBLEN = L_RSRC + 2 * REC;  // u16[REC]  struct bytes incl. 
 constexpr uint32_t L_RINFO = L_RBLEN + 2 * REC; // u8[REC]
 constexpr uint32_t L_RSLOT = L_RINFO + REC;     // u8[REC]   rank -> walk slot (duplicate check)
 // phase 2, 5: delete ranges
-constexpr uint32_t L_DKEY = L_RSLOT + REC;      // u64[DSN]  (client << 32 | clock)
+constexpr uint32_t L_DKEY = L_RSLOT + REC;      // u64[DSN]  (client << 32 | clock << 7 | slot)
 constexpr uint32_t L_DLEN = L_DKEY + 8 * DSN;   // u32[DSN]
 constexpr uint32_t L_DSEQ = L_DLEN + 4 * DSN;   // u16[DSN]  update << 8 | position (first appearance)
 constexpr uint32_t L_DSLOT = L_DSEQ + 2 * DSN;  // u8[DSN]
@@ -128,8 +128,10 @@ __device__ __forceinline__ bool walk_ds(uint32_t u) {
       const uint32_t len = rvu(c);
       if (c.bad || pos > 255) return false;
       const uint32_t x = atomicAdd(&at<uint32_t>(L_MISC + 4), 1u);
-      if (x >= DSN) return false;
-      at<uint64_t>(L_DKEY + 8 * x) = ((uint64_t)client << 32) | clock;
+      if (x >= DSN || clock >= (1u << 25)) return false;
+      // the slot in the low bits makes every key distinct (ranks are a permutation without a
+      // tie-break pass: equal (client, clock) ranges from several inputs are the common case)
+      at<uint64_t>(L_DKEY + 8 * x) = ((uint64_t)client << 32) | (clock << 7) | x;
       at<uint32_t>(L_DLEN + 4 * x) = len;
       at<uint16_t>(L_DSEQ + 2 * x) = (uint16_t)((u << 8) | pos);
     }
@@ -213,6 +215,7 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
       for (uint32_t i = lane; i < n1; i += 64) ok &= walk_structs(at<uint8_t>(L_UORD + i));
       if (__any(!ok)) YM_DECLINE()
       __syncthreads();
+      YM_STOP(8)
       // W2 list: updates whose delete set has clients (first byte != 0), compacted by ballots
       uint32_t n2 = 0;
 #pragma unroll
@@ -387,6 +390,7 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
       for (; o + 4 <= n; o += 4) ob32(dst, p + o, ld4(src + o));
       for (; o < n; o++) ob8(dst, p + o, sm[src + o]);
     }
+    YM_STOP(7)
     // ---- 5. delete set
     {
       uint64_t dk[E];
@@ -399,21 +403,7 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
         dl[s] = v ? at<uint32_t>(L_DLEN + 4 * i) : 0;
         dq[s] = v ? at<uint16_t>(L_DSEQ + 2 * i) : 0;
       }
-      rank_le(L_DKEY, nds, dk, dr);
-      __syncthreads();
-#pragma unroll
-      for (uint32_t s = 0; s < E; s++) {
-        const uint32_t i = lane + 64 * s;
-        if (i < nds) at<uint8_t>(L_DSLOT + dr[s]) = (uint8_t)i;
-      }
-      __syncthreads();
-      bool dup = false;
-#pragma unroll
-      for (uint32_t s = 0; s < E; s++) {
-        const uint32_t i = lane + 64 * s;
-        if (i < nds) dup |= at<uint8_t>(L_DSLOT + dr[s]) != i;
-      }
-      if (__any(dup)) rank_exact(L_DKEY, nds, dk, dr);  // equal (client, clock) in several inputs
+      rank_le(L_DKEY, nds, dk, dr);  // distinct keys: a permutation
       __syncthreads();
 #pragma unroll
       for (uint32_t s = 0; s < E; s++) {
@@ -440,7 +430,7 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
         const uint32_t r = r0 + s;
         const bool v = r < nds;
         const uint64_t k = v ? at<uint64_t>(L_DKEY + 8 * r) : 0;
-        ecl[s] = (uint32_t)k;
+        ecl[s] = (uint32_t)k >> 7;
         ecli[s] = (uint32_t)(k >> 32);
         eend[s] = v ? (uint64_t)ecl[s] + at<uint32_t>(L_DLEN + 4 * r) : 0;
         eseq[s] = v ? at<uint16_t>(L_DSEQ + 2 * r) : 0xffff;
@@ -647,6 +637,8 @@ int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st
       case 3: YM_LAUNCH(3, 5); break;
       case 4: YM_LAUNCH(4, 5); break;
       case 5: YM_LAUNCH(5, 5); break;
+      case 7: YM_LAUNCH(7, 5); break;
+      case 8: YM_LAUNCH(8, 5); break;
       default: YM_LAUNCH(0, 5); break;
     }
   }

@@ -41,7 +41,7 @@ constexpr uint32_t L_RSP = L_RS + 12 * REC;        // u32 rest span (LDS offset 
 constexpr uint32_t L_RSLOT = L_RSP + 4 * REC;      // u8
 constexpr uint32_t L_RCEND = L_RSLOT + REC;
 // delete ranges
-constexpr uint32_t L_DKEY = L_RCEND;               // u64 (client << 32 | clock)
+constexpr uint32_t L_DKEY = L_RCEND;               // u64 (client << 32 | clock << 7 | slot)
 constexpr uint32_t L_DLEN = L_DKEY + 8 * DSN;      // u32
 constexpr uint32_t L_DSEQ = L_DLEN + 4 * DSN;      // u16
 constexpr uint32_t L_DSLOT = L_DSEQ + 2 * DSN;     // u8
@@ -258,8 +258,9 @@ __device__ __forceinline__ bool walk_v2(uint32_t u) {
       cur = clock + len;
       if (c.bad || pos > 255 || cur > 0xffffffffull) return false;
       const uint32_t x = atomicAdd(&at<uint32_t>(L_MISC + 4), 1u);
-      if (x >= DSN) return false;
-      at<uint64_t>(L_DKEY + 8 * x) = ((uint64_t)client << 32) | clock;
+      if (x >= DSN || clock >= (1u << 25)) return false;
+      // slot in the low bits: distinct keys, ranks are a permutation (duplicated ranges are common)
+      at<uint64_t>(L_DKEY + 8 * x) = ((uint64_t)client << 32) | ((uint32_t)clock << 7) | x;
       at<uint32_t>(L_DLEN + 4 * x) = (uint32_t)len;
       at<uint16_t>(L_DSEQ + 2 * x) = (uint16_t)((u << 8) | pos);
     }
@@ -728,17 +729,7 @@ __global__ void __launch_bounds__(64) k_fast_merge_v2(GeneralJob j) {
         dl[s] = v ? at<uint32_t>(L_DLEN + 4 * i) : 0;
         dq[s] = v ? at<uint16_t>(L_DSEQ + 2 * i) : 0;
       }
-      rank_le(L_DKEY, nds, dk, dr);
-      __syncthreads();
-#pragma unroll
-      for (uint32_t s = 0; s < E; s++)
-        if (lane + 64 * s < nds) at<uint8_t>(L_DSLOT + dr[s]) = (uint8_t)(lane + 64 * s);
-      __syncthreads();
-      bool dup = false;
-#pragma unroll
-      for (uint32_t s = 0; s < E; s++)
-        if (lane + 64 * s < nds) dup |= at<uint8_t>(L_DSLOT + dr[s]) != lane + 64 * s;
-      if (__any(dup)) rank_exact(L_DKEY, nds, dk, dr);
+      rank_le(L_DKEY, nds, dk, dr);  // distinct keys: a permutation
       __syncthreads();
 #pragma unroll
       for (uint32_t s = 0; s < E; s++) {
@@ -764,7 +755,7 @@ __global__ void __launch_bounds__(64) k_fast_merge_v2(GeneralJob j) {
         const uint32_t r = r0 + s;
         const bool v = r < nds;
         const uint64_t kk = v ? at<uint64_t>(L_DKEY + 8 * r) : 0;
-        ecl[s] = (uint32_t)kk;
+        ecl[s] = (uint32_t)kk >> 7;
         ecli[s] = (uint32_t)(kk >> 32);
         eend[s] = v ? (uint64_t)ecl[s] + at<uint32_t>(L_DLEN + 4 * r) : 0;
         eseq[s] = v ? at<uint16_t>(L_DSEQ + 2 * r) : 0xffff;
