@@ -101,21 +101,26 @@ __global__ void k_status_flags(const uint32_t *list, uint32_t n, const int32_t *
   flags[i] = status[d] == want;
 }
 
-// The last kernel of every host round trip (one single-block launch, no atomics, no copy op): writes
-// the bump-allocator position, the declined count and (stats) errors / bytes out / bytes in straight
-// into pinned host memory, and resets the declined-document counter for the next launch.
-__global__ void __launch_bounds__(1024) k_finish(const int32_t *status, const uint64_t *out_len, uint32_t n,
-                                                 const uint64_t *upd_off, uint32_t n_upd, uint64_t *counters,
-                                                 volatile uint64_t *host, int stats, int merge, uint64_t seq) {
-  __shared__ unsigned long long red[2][16];
+// The last kernel of every host round trip (no copy op): writes the bump-allocator position, the
+// declined count and (stats) errors / bytes out / bytes in straight into pinned host memory, and resets
+// the device counters for the next launch.  Stats: a few blocks, each summing 4,096 documents' status /
+// out_len with 16 independent loads per thread (one HBM round trip), partial sums by atomics, and the
+// block that finishes last writes the host words (a handful of same-address atomics, not one per doc).
+// Counters: [0] used, [2] declined (u32), [8] finished blocks (u32), [9] errors, [10] bytes out.
+constexpr uint32_t FIN_DOCS = 4096, FIN_THREADS = 256;
+__global__ void __launch_bounds__(FIN_THREADS) k_finish(const int32_t *status, const uint64_t *out_len, uint32_t n,
+                                                        const uint64_t *upd_off, uint32_t n_upd, uint64_t *counters,
+                                                        volatile uint64_t *host, int stats, int merge, uint64_t seq) {
+  __shared__ unsigned long long red[2][FIN_THREADS / 64];
+  unsigned long long *c = reinterpret_cast<unsigned long long *>(counters);
   uint64_t err = 0, bytes = 0;
-  // batches of 16 independent loads per thread (latency of one HBM round trip per batch, not per doc)
-  for (uint32_t i0 = 0; stats && i0 < n; i0 += 16 * blockDim.x) {
+  const uint32_t i0 = blockIdx.x * FIN_DOCS;
+  if (stats) {
     int32_t sv[16];
     uint64_t lv[16];
 #pragma unroll
     for (uint32_t t = 0; t < 16; t++) {
-      const uint32_t i = i0 + t * blockDim.x + threadIdx.x;
+      const uint32_t i = i0 + t * FIN_THREADS + threadIdx.x;
       sv[t] = i < n ? status[i] : 0;
       lv[t] = i < n ? out_len[i] : 0;
     }
@@ -132,20 +137,33 @@ __global__ void __launch_bounds__(1024) k_finish(const int32_t *status, const ui
   const uint32_t w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) { red[0][w] = err; red[1][w] = bytes; }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    uint64_t e = 0, b = 0;
-    for (uint32_t k = 0; k < blockDim.x / 64; k++) { e += red[0][k]; b += red[1][k]; }
-    // used: the bump allocator; merges also own the fast / large paths' slot region [0, 2 in + 64 n + 64)
-    const uint64_t region = merge ? 2 * (upd_off[n_upd] - upd_off[0]) + 64ull * n + 64 : 0;
-    host[0] = counters[0] > region ? counters[0] : region;
-    host[2] = counters[2] & 0xffffffffull;       // declined documents (the work list length)
-    host[4] = e;
-    host[5] = b;
-    host[6] = upd_off[n_upd] - upd_off[0];
-    counters[0] = 0;                             // used := 0 and pend_count (counters + 2) := 0: the
-    ((uint32_t *)counters)[4] = 0;               // next launch starts clean (see run_op for the general path)
-    host[7] = seq;                               // completion word (the host spins on it)
+  if (threadIdx.x != 0) return;
+  uint64_t e = 0, b = 0;
+  for (uint32_t k = 0; k < FIN_THREADS / 64; k++) { e += red[0][k]; b += red[1][k]; }
+  if (gridDim.x > 1) {
+    // device-scope atomics are performed when they return: consuming both results orders the
+    // finished-block increment after them (no fence: an agent-scope release writes back the L2)
+    const unsigned long long r1 = atomicAdd(&c[9], (unsigned long long)e);
+    const unsigned long long r2 = atomicAdd(&c[10], (unsigned long long)b);
+    asm volatile("" ::"v"(r1), "v"(r2));
+    if (atomicAdd(reinterpret_cast<uint32_t *>(&c[8]), 1u) != gridDim.x - 1) return;
+    e = atomicAdd(&c[9], 0ull);
+    b = atomicAdd(&c[10], 0ull);
   }
+  // used: the bump allocator; merges also own the fast / large paths' slot region [0, 2 in + 64 n + 64)
+  const uint64_t region = merge ? 2 * (upd_off[n_upd] - upd_off[0]) + 64ull * n + 64 : 0;
+  const uint64_t used = atomicAdd(&c[0], 0ull);
+  host[0] = used > region ? used : region;
+  host[2] = atomicAdd(reinterpret_cast<uint32_t *>(&c[2]), 0u);  // declined documents (the work list length)
+  host[4] = e;
+  host[5] = b;
+  host[6] = upd_off[n_upd] - upd_off[0];
+  c[0] = 0;                                     // used := 0, pend_count := 0 and the finish counters:
+  reinterpret_cast<uint32_t *>(c)[4] = 0;       // the next launch starts clean (see run_op for the
+  c[8] = 0;                                     // general path)
+  c[9] = 0;
+  c[10] = 0;
+  host[7] = seq;                                // completion word (the host spins on it)
 }
 
 // Compacts the ids of listed docs whose status == want into `dst`; returns the count.
@@ -281,8 +299,9 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   S->dirty = true;
   // ends a round trip: counters and stats land in pinned host memory, then one stream sync
   auto finish = [&]() -> int {
-    k_finish<<<1, 1024, 0, st>>>(o_status, o_len, nd, upd_off, b->n_upd, counters, S->pinned_dev, stats ? 1 : 0,
-                                   op == OP_MERGE ? 1 : 0, seq);
+    const uint32_t fin_blocks = stats ? (nd + FIN_DOCS - 1) / FIN_DOCS : 1;
+    k_finish<<<fin_blocks, FIN_THREADS, 0, st>>>(o_status, o_len, nd, upd_off, b->n_upd, counters, S->pinned_dev,
+                                                 stats ? 1 : 0, op == OP_MERGE ? 1 : 0, seq);
     HIPCHK(hipEventRecord(S->ev1, st));
     // spin on the completion word k_finish writes last (no interrupt wake-up of a blocking wait), then
     // the stream sync, which finds the stream drained: it is what orders every result for the host
