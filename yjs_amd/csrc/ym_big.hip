@@ -142,6 +142,7 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
     uint32_t prev_client = 0;
     bool declined = false;
     for (uint32_t ci = 0; ci < nclients && !c.bad && !declined; ci++) {
+      sc::uni(c);
       const uint32_t nstructs = rvu(c);
       const uint32_t client = rvu(c);
       uint64_t clock = rvu(c);
@@ -159,6 +160,8 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
       bool copying = false;
       uint32_t written = 0, b0r = 0;
       for (uint32_t si = 0; si < nstructs && !c.bad; si++) {
+        sc::uni(c);
+        clock = sc::rfl64(clock);
         const uint32_t s0 = c.p;
         const uint32_t info = rdb(c);
         uint32_t len;

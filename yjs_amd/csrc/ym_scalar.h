@@ -52,6 +52,21 @@ __device__ __forceinline__ void fill(SCur &c) {  // nv >= 8 afterwards
   }
   c.nv += 8;
 }
+// Wave-uniform by construction, but the compiler's divergence analysis does not always prove it (the
+// walk then runs on the VALU with exec-mask branches and vector loads): readfirstlane pins the cursor
+// to SGPRs at loop heads.
+__device__ __forceinline__ uint32_t rfl(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ uint64_t rfl64(uint64_t x) { return ((uint64_t)rfl((uint32_t)(x >> 32)) << 32) | rfl((uint32_t)x); }
+__device__ __forceinline__ cu32 *rflp(cu32 *b) { return (cu32 *)(uintptr_t)rfl64((uint64_t)(uintptr_t)b); }
+__device__ __forceinline__ void uni(SCur &c) {
+  c.b = rflp(c.b);
+  c.p = rfl(c.p);
+  c.e = rfl(c.e);
+  c.lo = rfl64(c.lo);
+  c.hi = rfl64(c.hi);
+  c.nv = rfl(c.nv);
+  c.bad = rfl(c.bad) != 0;
+}
 __device__ __forceinline__ SCur make(cu32 *b, uint32_t p, uint32_t e) {
   SCur c = {b, p, e, false, 0, 0, 0};
   fill(c);
