@@ -159,6 +159,26 @@ __device__ __forceinline__ void skvu(Cur &c) {
   c.bad |= vu_bad(lo, hi, nb, c.p, c.e);
   c.p += nb < 6 ? nb : 0;
 }
+// skips two consecutive varuints (an ID: client, clock) read from one 8-byte window when both end
+// inside it (the common case), with the checks of two skvu calls: terminated within 5 bytes each,
+// inside the update, canonical, < 2^32.  Otherwise (a lane whose pair does not fit) two skvu calls.
+__device__ __forceinline__ uint32_t ctz64(uint64_t x) { return __builtin_ctzg(x, 64); }
+__device__ __forceinline__ void skvu2(Cur &c) {
+  const uint64_t x = ld8(c.p);
+  const uint64_t st = ~x & 0x8080808080808080ull;  // stop bytes (high bit clear)
+  const uint64_t st2 = st & (st - 1);                // ... without the first
+  if (st2 == 0) {
+    skvu(c);
+    skvu(c);
+    return;
+  }
+  const uint32_t i1 = ctz64(st) >> 3, i2 = ctz64(st2) >> 3;  // indices of the two stop bytes
+  const uint32_t b1 = (uint32_t)(x >> (8 * i1)) & 0xffu, b2 = (uint32_t)(x >> (8 * i2)) & 0xffu;
+  const uint32_t n1 = i1 + 1, n2 = i2 - i1;
+  c.bad |= (n1 > 5) | (n2 > 5) | (c.p + i2 + 1 > c.e) | ((n1 > 1) & (b1 == 0)) | ((n2 > 1) & (b2 == 0)) |
+           ((n1 == 5) & ((b1 & 0x70u) != 0)) | ((n2 == 5) & ((b2 & 0x70u) != 0));
+  c.p += i2 + 1;
+}
 __device__ __forceinline__ uint32_t rdb(Cur &c) {
   c.bad |= c.p >= c.e;
   return sm[c.p++];
@@ -278,13 +298,13 @@ __device__ __forceinline__ void any_scalar(Cur &c) {
 // Item.js:665-683 content refs; lazy reader of 13.5.16: parent kept raw, parentSub only without
 // origins).  Returns false (decline) for kinds this path does not verify; `len` = the Item's length.
 __device__ __forceinline__ bool item_body(Cur &c, uint32_t info, uint32_t &len) {
-  if (info & 0x80) { skvu(c); skvu(c); }
-  if (info & 0x40) { skvu(c); skvu(c); }
+  if (info & 0x80) skvu2(c);
+  if (info & 0x40) skvu2(c);
   if ((info & 0xC0) == 0) {
     const uint32_t pi = rvu(c);
     if (pi > 1) return false;  // parentInfo re-encodes as 0/1
     if (pi == 1) rstr(c);
-    else { skvu(c); skvu(c); }
+    else skvu2(c);
     if (info & 0x20) rstr(c);
   }
   len = 1;
