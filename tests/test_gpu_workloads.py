@@ -209,3 +209,59 @@ def test_convert_workloads_match_oracle(engine, fmt):
     assert (st == 0).all()
     bad = _compare(engine.run_host("conv", fmt, a2, o2, d2), outs, st)
     assert not bad, bad[:10]
+
+
+def _vu(v):
+    out = bytearray()
+    while v > 127:
+        out.append(0x80 | (v & 127))
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def _ds_update(ranges):
+    """A V1 update with no structs and the delete set {client: [(clock, len), ...]} (DeleteSet.js:219-232)."""
+    b = bytearray(b"\x00")
+    b += _vu(len(ranges))
+    for client, rs in ranges.items():
+        b += _vu(client) + _vu(len(rs))
+        for clock, ln in rs:
+            b += _vu(clock) + _vu(ln)
+    return bytes(b)
+
+
+@pytest.mark.parametrize("fmt", [1, 2])
+def test_delete_set_merges_duplicates_and_large_clocks(engine, fmt):
+    """Delete-set-only updates with equal (client, clock) ranges across inputs (the common case the fast
+    path's slot-tagged keys handle) and documents with clocks >= 2^25 (declined to the general path):
+    bytes equal the oracle's and only the large-clock documents leave the fast path."""
+    from yjs_amd import pack_docs
+    rng = np.random.default_rng(5)
+    docs, big = [], []
+    for d in range(96):
+        large = d % 4 == 3
+        clients = [int(c) for c in rng.choice([7, 300, 123456, 2**31 + 5], size=2, replace=False)]
+        # disjoint ranges (V2 delta-codes clocks against the previous range's end); updates pick
+        # overlapping subsets of them, so equal (client, clock) keys recur across inputs
+        base = [(8 * int(k) + (2**25 if large else 0), int(rng.integers(1, 6)))
+                for k in rng.choice(12, size=6, replace=False)]
+        # one struct (Y.Text insert of "ab" by client 99, ykey "t"): the fast path takes documents with structs
+        ups = [bytes([1, 1, 99, 0, 0x04, 1, 1, ord("t"), 2, ord("a"), ord("b"), 0])]
+        for _ in range(int(rng.integers(2, 9))):
+            sel = {}
+            for c in clients:
+                picks = rng.choice(len(base), size=int(rng.integers(1, 4)), replace=False)
+                sel[c] = sorted(base[int(i)] for i in picks)
+            ups.append(_ds_update(sel))
+        if fmt == 2:
+            ups = [O.convert(u, 1)[1] for u in ups]
+        docs.append(ups)
+        big.append(large)
+    a, o, d = pack_docs(docs)
+    outs, status, _ = O.batch("merge", fmt, a, o, d)
+    assert (status == 0).all()
+    bad = _compare(engine.run_host("merge", fmt, a, o, d), outs, status)
+    assert not bad, bad[:10]
+    st = engine.stats
+    assert st["docs_fast"] == len(docs) - sum(big), st

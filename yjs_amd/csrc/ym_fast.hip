@@ -91,23 +91,27 @@ __device__ __forceinline__ bool walk_structs(uint32_t u) {
     const uint32_t client = rvu(c);
     uint32_t clock = rvu(c);
     for (uint32_t si = 0; si < nstructs && !c.bad; si++) {
+      // declines set c.bad (one exit edge per loop instead of one per check)
       const uint32_t s0 = c.p;
       const uint32_t info = rdb(c);
-      if (info == 10 || (info & 31) == 0) return false;  // Skip / GC -> general path
-      uint32_t len;
-      if (!item_body(c, info, len)) return false;
-      if ((uint64_t)clock + len > 0xffffffffull) return false;
+      c.bad |= info == 10 || (info & 31) == 0;  // Skip / GC -> general path
+      uint32_t len = 1;
+      if (!c.bad) c.bad |= !item_body(c, info, len);
       const uint64_t key = ((uint64_t)(~client) << 32) | clock;
-      if (have_prev && key <= prev) return false;  // each update must already be in merge order
-      prev = key + len - 1;
-      have_prev = true;
-      const uint32_t q = atomicAdd(&at<uint32_t>(L_MISC), 1u);
-      if (q >= REC) return false;
-      at<uint64_t>(L_RKEY + 8 * q) = key;
-      at<uint32_t>(L_RLEN + 4 * q) = len;
-      at<uint16_t>(L_RSRC + 2 * q) = (uint16_t)s0;
-      at<uint16_t>(L_RBLEN + 2 * q) = (uint16_t)(c.p - s0);
-      at<uint8_t>(L_RINFO + q) = (uint8_t)info;
+      c.bad |= ((uint64_t)clock + len > 0xffffffffull) | (have_prev && key <= prev);  // inputs in merge order
+      if (!c.bad) {
+        prev = key + len - 1;
+        have_prev = true;
+        const uint32_t q = atomicAdd(&at<uint32_t>(L_MISC), 1u);
+        c.bad |= q >= REC;
+        if (q < REC) {
+          at<uint64_t>(L_RKEY + 8 * q) = key;
+          at<uint32_t>(L_RLEN + 4 * q) = len;
+          at<uint16_t>(L_RSRC + 2 * q) = (uint16_t)s0;
+          at<uint16_t>(L_RBLEN + 2 * q) = (uint16_t)(c.p - s0);
+          at<uint8_t>(L_RINFO + q) = (uint8_t)info;
+        }
+      }
       clock += len;
     }
   }
@@ -126,14 +130,18 @@ __device__ __forceinline__ bool walk_ds(uint32_t u) {
     for (uint32_t q = 0; q < m && !c.bad; q++, pos++) {
       const uint32_t clock = rvu(c);
       const uint32_t len = rvu(c);
-      if (c.bad || pos > 255) return false;
-      const uint32_t x = atomicAdd(&at<uint32_t>(L_MISC + 4), 1u);
-      if (x >= DSN || clock >= (1u << 25)) return false;
-      // the slot in the low bits makes every key distinct (ranks are a permutation without a
-      // tie-break pass: equal (client, clock) ranges from several inputs are the common case)
-      at<uint64_t>(L_DKEY + 8 * x) = ((uint64_t)client << 32) | (clock << 7) | x;
-      at<uint32_t>(L_DLEN + 4 * x) = len;
-      at<uint16_t>(L_DSEQ + 2 * x) = (uint16_t)((u << 8) | pos);
+      c.bad |= (pos > 255) | (clock >= (1u << 25));
+      if (!c.bad) {
+        const uint32_t x = atomicAdd(&at<uint32_t>(L_MISC + 4), 1u);
+        c.bad |= x >= DSN;
+        // the slot in the low bits makes every key distinct (ranks are a permutation without a
+        // tie-break pass: equal (client, clock) ranges from several inputs are the common case)
+        if (x < DSN) {
+          at<uint64_t>(L_DKEY + 8 * x) = ((uint64_t)client << 32) | (clock << 7) | x;
+          at<uint32_t>(L_DLEN + 4 * x) = len;
+          at<uint16_t>(L_DSEQ + 2 * x) = (uint16_t)((u << 8) | pos);
+        }
+      }
     }
   }
   return !c.bad;

@@ -302,7 +302,7 @@ __device__ __forceinline__ bool item_body(Cur &c, uint32_t info, uint32_t &len) 
   if (info & 0x40) skvu2(c);
   if ((info & 0xC0) == 0) {
     const uint32_t pi = rvu(c);
-    if (pi > 1) return false;  // parentInfo re-encodes as 0/1
+    c.bad |= pi > 1;  // parentInfo re-encodes as 0/1
     if (pi == 1) rstr(c);
     else skvu2(c);
     if (info & 0x20) rstr(c);
@@ -316,7 +316,7 @@ __device__ __forceinline__ bool item_body(Cur &c, uint32_t info, uint32_t &len) 
     case 6: rstr(c); json_lit(c); break;                              // ContentFormat
     case 7: {                                                         // ContentType
       const uint32_t t = rvu(c);
-      if (t > 6) return false;
+      c.bad |= t > 6;
       if (t == 3 || t == 5) rstr(c);
       break;
     }
@@ -324,8 +324,9 @@ __device__ __forceinline__ bool item_body(Cur &c, uint32_t info, uint32_t &len) 
       len = rvu(c);
       for (uint32_t i = 0; i < len && !c.bad; i++) any_scalar(c);
       break;
-    default: return false;  // ContentJSON, ContentDoc, invalid refs
+    default: c.bad = true; break;  // ContentJSON, ContentDoc, invalid refs
   }
+  // (no early returns: every decline sets c.bad, so the lane's loops and exits stay single-edged)
   return !c.bad && len != 0;
 }
 
