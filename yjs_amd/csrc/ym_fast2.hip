@@ -178,7 +178,8 @@ __device__ __forceinline__ bool walk_v2(uint32_t u) {
     uint32_t clock = rvu(c);
     for (uint32_t si = 0; si < nstructs && !c.bad && !bad; si++) {
       const uint32_t info = rd_rle(in);
-      if (info == 10 || (info & 31) == 0 || info > 255) return false;  // Skip / GC inputs: general path
+      // declines set `bad` (one exit edge per loop instead of one per check)
+      bad |= info == 10 || (info & 31) == 0 || info > 255;  // Skip / GC inputs: general path
       uint32_t f0 = 0, f1 = 0, f2 = 0, f3 = 0, s0 = 0, s1 = 0, s2 = 0, sp = 0, pi = 0, t = 0;
       if (info & 0x80) { f0 = rd_uopt(cl); f1 = rd_idif(lc); }
       if (info & 0x40) { f2 = rd_uopt(cl); f3 = rd_idif(rc); }
@@ -193,8 +194,8 @@ __device__ __forceinline__ bool walk_v2(uint32_t u) {
         case 1: len = rd_uopt(ln); break;                                  // ContentDeleted
         case 3: {                                                          // ContentBinary (rest)
           const uint32_t a = c.p, n = rvu(c);
-          if (!room(c, n)) return false;
-          c.p += n;
+          if (!room(c, n)) bad = true;
+          else c.p += n;
           sp = a | ((c.p - a) << 16);
           break;
         }
@@ -208,9 +209,9 @@ __device__ __forceinline__ bool walk_v2(uint32_t u) {
         }
         case 7:                                                            // ContentType
           t = rd_uopt(tr);
-          if (t > 6) return false;
+          bad |= t > 6;
           if (t == 3 || t == 5) {  // readKey: a cached key (keyClock < keys read) reads no string
-            if (rd_idif(kc) < keys) return false;
+            bad |= rd_idif(kc) < keys;
             keys++;
             s2 = rstr();
           }
@@ -222,24 +223,27 @@ __device__ __forceinline__ bool walk_v2(uint32_t u) {
           sp = a | ((c.p - a) << 16);
           break;
         }
-        default: return false;  // ContentJSON, ContentDoc, invalid refs
+        default: bad = true; break;  // ContentJSON, ContentDoc, invalid refs
       }
-      if (c.bad || bad || len == 0 || (sp >> 16) > 0x7fff) return false;
-      if ((uint64_t)clock + len > 0xffffffffull) return false;
       const uint64_t key = ((uint64_t)(~client) << 32) | clock;
-      if (have_prev && key <= prev) return false;  // each update must already be in merge order
-      prev = key + len - 1;
-      have_prev = true;
-      const uint32_t q = atomicAdd(&at<uint32_t>(L_MISC), 1u);
-      if (q >= REC) return false;
-      at<uint64_t>(L_RKEY + 8 * q) = key;
-      at<uint32_t>(L_RLEN + 4 * q) = len;
-      at<uint32_t>(L_RAUX + 4 * q) = info | (pi << 8) | (t << 16);
-      at<uint4>(L_RF + 16 * q) = make_uint4(f0, f1, f2, f3);
-      at<uint32_t>(L_RS + 12 * q) = s0;
-      at<uint32_t>(L_RS + 12 * q + 4) = s1;
-      at<uint32_t>(L_RS + 12 * q + 8) = s2;
-      at<uint32_t>(L_RSP + 4 * q) = sp;
+      bad |= c.bad | (len == 0) | ((sp >> 16) > 0x7fff) | ((uint64_t)clock + len > 0xffffffffull) |
+             (have_prev && key <= prev);  // each update must already be in merge order
+      if (!bad) {
+        prev = key + len - 1;
+        have_prev = true;
+        const uint32_t q = atomicAdd(&at<uint32_t>(L_MISC), 1u);
+        bad |= q >= REC;
+        if (q < REC) {
+          at<uint64_t>(L_RKEY + 8 * q) = key;
+          at<uint32_t>(L_RLEN + 4 * q) = len;
+          at<uint32_t>(L_RAUX + 4 * q) = info | (pi << 8) | (t << 16);
+          at<uint4>(L_RF + 16 * q) = make_uint4(f0, f1, f2, f3);
+          at<uint32_t>(L_RS + 12 * q) = s0;
+          at<uint32_t>(L_RS + 12 * q + 4) = s1;
+          at<uint32_t>(L_RS + 12 * q + 8) = s2;
+          at<uint32_t>(L_RSP + 4 * q) = sp;
+        }
+      }
       clock += len;
     }
   }
@@ -256,13 +260,17 @@ __device__ __forceinline__ bool walk_v2(uint32_t u) {
       const uint64_t clock = cur + rvu(c);
       const uint64_t len = (uint64_t)rvu(c) + 1;
       cur = clock + len;
-      if (c.bad || pos > 255 || cur > 0xffffffffull) return false;
-      const uint32_t x = atomicAdd(&at<uint32_t>(L_MISC + 4), 1u);
-      if (x >= DSN || clock >= (1u << 25)) return false;
-      // slot in the low bits: distinct keys, ranks are a permutation (duplicated ranges are common)
-      at<uint64_t>(L_DKEY + 8 * x) = ((uint64_t)client << 32) | ((uint32_t)clock << 7) | x;
-      at<uint32_t>(L_DLEN + 4 * x) = (uint32_t)len;
-      at<uint16_t>(L_DSEQ + 2 * x) = (uint16_t)((u << 8) | pos);
+      c.bad |= (pos > 255) | (cur > 0xffffffffull) | (clock >= (1u << 25));
+      if (!c.bad) {
+        const uint32_t x = atomicAdd(&at<uint32_t>(L_MISC + 4), 1u);
+        c.bad |= x >= DSN;
+        // slot in the low bits: distinct keys, ranks are a permutation (duplicated ranges are common)
+        if (x < DSN) {
+          at<uint64_t>(L_DKEY + 8 * x) = ((uint64_t)client << 32) | ((uint32_t)clock << 7) | x;
+          at<uint32_t>(L_DLEN + 4 * x) = (uint32_t)len;
+          at<uint16_t>(L_DSEQ + 2 * x) = (uint16_t)((u << 8) | pos);
+        }
+      }
     }
   }
   return !c.bad;
