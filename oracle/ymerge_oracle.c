@@ -1771,6 +1771,71 @@ static Buf *sv_impl(Ctx *c, const uint8_t *upd, size_t len, int v2) {
   return out;
 }
 
+/* parseUpdateMetaV2 (13.5.16 parseUpdateMeta / parseUpdateMetaV2): a LazyStructReader that keeps Skips;
+   `from` gets a client's first clock when its section starts, `to` the end (clock + length) of its last
+   struct when the next section starts.  Both are JS Maps: a client met again keeps its first position and
+   takes the new value.  Output (the engine's encoding of the two Maps): from then to, each as an encoded
+   state vector, vu(count) | (client, clock)*, in Map order. */
+static void meta_set(Ctx *c, int64_t **kv, size_t *n, size_t *cap, int64_t client, int64_t clock) {
+  for (size_t i = 0; i < *n; i++) if ((*kv)[2 * i] == client) { (*kv)[2 * i + 1] = clock; return; }
+  if (*n == *cap) {
+    size_t nc = *cap ? *cap * 2 : 16;
+    int64_t *p = (int64_t *)aalloc(c, nc * 2 * sizeof(int64_t));
+    if (*n) memcpy(p, *kv, *n * 2 * sizeof(int64_t));
+    *kv = p; *cap = nc;
+  }
+  (*kv)[2 * *n] = client; (*kv)[2 * *n + 1] = clock; (*n)++;
+}
+static Buf *meta_impl(Ctx *c, const uint8_t *upd, size_t len, int v2) {
+  UDec dec;
+  udec_init(c, &dec, upd, len, v2);
+  LReader r;
+  lr_init(c, &r, &dec, 0);
+  int64_t *from = NULL, *to = NULL;
+  size_t nf = 0, cf = 0, nt = 0, ct = 0;
+  Struct *i = r.curr;
+  if (i) {
+    int64_t client = i->client, clock = i->clock;
+    meta_set(c, &from, &nf, &cf, client, clock);
+    for (; i; i = lr_next(c, &r)) {
+      if (client != i->client) {
+        meta_set(c, &to, &nt, &ct, client, clock);
+        meta_set(c, &from, &nf, &cf, i->client, i->clock);
+        client = i->client;
+      }
+      clock = i->clock + i->len;
+    }
+    meta_set(c, &to, &nt, &ct, client, clock);
+  }
+  Buf *out = buf_new(c);
+  wr_vu(c, out, (int64_t)nf);
+  for (size_t k = 0; k < nf; k++) { wr_vu(c, out, from[2 * k]); wr_vu(c, out, from[2 * k + 1]); }
+  wr_vu(c, out, (int64_t)nt);
+  for (size_t k = 0; k < nt; k++) { wr_vu(c, out, to[2 * k]); wr_vu(c, out, to[2 * k + 1]); }
+  return out;
+}
+
+/* PermanentUserData's delete-set merge (PermanentUserData.js:49-54): every encoded delete set is read
+   with readDeleteSet (DeleteSet.js:241-256; DSDecoderV1, or DSDecoderV2 for fmt 2), the k sets are
+   merged by mergeDeleteSets (13.5.16 he@10482 + le@10242 union) and written by writeDeleteSet
+   (DSEncoderV1 / DSEncoderV2 rest bytes, as encodeSnapshot[V2] writes them, Snapshot.js:84-101). */
+static Buf *dsmerge_impl(Ctx *c, const uint8_t *const *dss_in, const size_t *lens, size_t k, int v2) {
+  DSet *dss = (DSet *)aalloc(c, (k ? k : 1) * sizeof(DSet));
+  for (size_t i = 0; i < k; i++) {
+    UDec dec;
+    udec_init(c, &dec, dss_in[i], lens[i], 0);
+    dec.v2 = v2;
+    ds_read(c, &dec, &dss[i]);
+  }
+  DSet m;
+  ds_merge(c, dss, k, &m);
+  UEnc enc;
+  uenc_init(c, &enc, 0);
+  enc.v2 = v2;
+  ds_write(c, &enc, &m);
+  return enc.rest;
+}
+
 /* ------------------------------------------------------------------------------------------------ */
 /* public API                                                                                      */
 /* ------------------------------------------------------------------------------------------------ */
@@ -1837,6 +1902,30 @@ int ymo_sv_from_update(const uint8_t *upd, size_t len, int fmt, uint8_t **out, s
   return rc;
 }
 
+int ymo_meta(const uint8_t *upd, size_t len, int fmt, uint8_t **out, size_t *out_len) {
+  *out = NULL; *out_len = 0;
+  Ctx c;
+  memset(&c, 0, sizeof(c));
+  int code = setjmp(c.jb);
+  if (code) { ctx_free(&c); return code; }
+  Buf *b = meta_impl(&c, upd, len, fmt == 2);
+  int rc = finish_out(&c, b, out, out_len);
+  ctx_free(&c);
+  return rc;
+}
+
+int ymo_ds_merge(const uint8_t *const *dss, const size_t *lens, size_t n, int fmt, uint8_t **out, size_t *out_len) {
+  *out = NULL; *out_len = 0;
+  Ctx c;
+  memset(&c, 0, sizeof(c));
+  int code = setjmp(c.jb);
+  if (code) { ctx_free(&c); return code; }
+  Buf *b = dsmerge_impl(&c, dss, lens, n, fmt == 2);
+  int rc = finish_out(&c, b, out, out_len);
+  ctx_free(&c);
+  return rc;
+}
+
 void ymo_free(void *p) { free(p); }
 
 /* ------------------------------------------------------------------------------------------------ */
@@ -1878,6 +1967,10 @@ static void *batch_worker(void *arg) {
       st = n >= 1 ? ymo_diff(ptrs[0], lens[0], sv, svl, j->fmt, &out, &olen) : YMO_ERR_UNEXPECTED;
     } else if (j->op == 3) {
       st = n >= 1 ? ymo_convert(ptrs[0], lens[0], j->fmt, &out, &olen) : YMO_ERR_UNEXPECTED;
+    } else if (j->op == 4) {
+      st = n == 1 ? ymo_meta(ptrs[0], lens[0], j->fmt, &out, &olen) : YMO_ERR_UNEXPECTED;
+    } else if (j->op == 5) {
+      st = ymo_ds_merge(ptrs, lens, n, j->fmt, &out, &olen);
     } else st = n >= 1 ? ymo_sv_from_update(ptrs[0], lens[0], j->fmt, &out, &olen) : YMO_ERR_UNEXPECTED;
     if (st == YMO_OK && j->out_arena) {
       uint64_t cap = j->out_cap_off[d + 1] - j->out_cap_off[d];

@@ -55,6 +55,8 @@ def lib():
         L.ymo_sv_from_update.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(u8p),
                                          ctypes.POINTER(ctypes.c_size_t)]
         L.ymo_convert.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t)]
+        L.ymo_meta.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t)]
+        L.ymo_ds_merge.argtypes = L.ymo_merge.argtypes
         L.ymo_free.argtypes = [ctypes.c_void_p]
         vp = ctypes.c_void_p
         L.ymo_batch.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, vp, ctypes.c_uint32, vp, vp, ctypes.c_int,
@@ -120,11 +122,35 @@ def convert(update, fmt=1):
     return st, (_take(out, olen) if st == 0 else None)
 
 
+def meta(update, fmt=1):
+    """parseUpdateMeta / parseUpdateMetaV2 -> (status, bytes: from-map then to-map, each as an encoded
+    state vector in Map order)."""
+    L = lib()
+    u, ul = _buf(update)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    st = L.ymo_meta(ctypes.cast(u, ctypes.POINTER(ctypes.c_uint8)), ul, fmt, ctypes.byref(out), ctypes.byref(olen))
+    return st, (_take(out, olen) if st == 0 else None)
+
+
+def ds_merge(blobs, fmt=1):
+    """PermanentUserData's mergeDeleteSets over encoded delete sets -> (status, encoded delete set)."""
+    L = lib()
+    bufs = [_buf(u) for u in blobs]
+    n = len(bufs)
+    ptrs = (ctypes.POINTER(ctypes.c_uint8) * max(1, n))(*[ctypes.cast(b[0], ctypes.POINTER(ctypes.c_uint8)) for b in bufs])
+    lens = (ctypes.c_size_t * max(1, n))(*[b[1] for b in bufs])
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    st = L.ymo_ds_merge(ptrs, lens, n, fmt, ctypes.byref(out), ctypes.byref(olen))
+    return st, (_take(out, olen) if st == 0 else None)
+
+
 def batch(op, fmt, arena, upd_off, doc_upd, sv_arena=None, sv_off=None, nthreads=1, want_output=True):
-    """Batched oracle over the engine's arena layout (numpy arrays). op: 'merge'|'diff'|'sv'.
+    """Batched oracle over the engine's arena layout (numpy arrays). op: 'merge'|'diff'|'sv'|'conv'|'meta'|'dsmerge'.
     Returns (out_bytes_list_or_None, status ndarray, out_len ndarray)."""
     L = lib()
-    opc = {"merge": 0, "diff": 1, "sv": 2, "conv": 3}[op]
+    opc = {"merge": 0, "diff": 1, "sv": 2, "conv": 3, "meta": 4, "dsmerge": 5}[op]
     arena = np.ascontiguousarray(arena, dtype=np.uint8)
     upd_off = np.ascontiguousarray(upd_off, dtype=np.uint64)
     doc_upd = np.ascontiguousarray(doc_upd, dtype=np.uint32)

@@ -16,6 +16,10 @@ def run_case(c):
         return O.diff(c["inputs"][0], c["sv"], c["fmt"])
     if c["op"] == "conv":
         return O.convert(c["inputs"][0], c["fmt"])
+    if c["op"] == "meta":
+        return O.meta(c["inputs"][0], c["fmt"])
+    if c["op"] == "dsmerge":
+        return O.ds_merge(c["inputs"], c["fmt"])
     return O.sv_from_update(c["inputs"][0], c["fmt"])
 
 
@@ -31,8 +35,8 @@ def test_oracle_matches_golden(case):
 
 def test_golden_coverage():
     groups = {c["group"] for c in CASES}
-    assert {"c1_text", "c2_text", "c4_map", "c5_xml", "content", "edge", "refgolden", "conv"} <= groups
-    for op in ("merge", "diff", "sv", "conv"):
+    assert {"c1_text", "c2_text", "c4_map", "c5_xml", "content", "edge", "refgolden", "conv", "meta", "dsmerge"} <= groups
+    for op in ("merge", "diff", "sv", "conv", "meta", "dsmerge"):
         for fmt in (1, 2):
             assert any(c["op"] == op and c["fmt"] == fmt and "expect" in c for c in CASES), (op, fmt)
     assert sum("error" in c for c in CASES) >= 20
