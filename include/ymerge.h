@@ -95,6 +95,15 @@ int ym_sv(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
 /* convertUpdateFormatV1ToV2 (b->format = YM_V1) / convertUpdateFormatV2ToV1 (b->format = YM_V2): one
  * update per document, re-encoded in the other format (yjs 13.5.x convertUpdateFormat, bundle ms@41803) */
 int ym_convert(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
+/* parseUpdateMeta (b->format = YM_V1) / parseUpdateMetaV2 (YM_V2), yjs 13.5.16: one update per document.
+ * The two Maps it returns are written as from then to, each vu(size) | (client, clock)* in Map order
+ * (the encoding of encodeStateVector, reference src/utils/encoding.js:572-579). */
+int ym_meta(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
+/* PermanentUserData's delete-set merge (reference src/utils/PermanentUserData.js:49-54): the "updates" of
+ * document d are encoded delete sets (DSEncoderV1 bytes for YM_V1, DSEncoderV2 for YM_V2, as
+ * encodeSnapshot[V2] writes them, src/utils/Snapshot.js:84-101); the output is
+ * writeDeleteSet(mergeDeleteSets(readDeleteSet(each))) in the same encoding (13.5.16 union, he@10482). */
+int ym_ds_merge(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
 
 #ifdef __cplusplus
 }

@@ -9,6 +9,11 @@
 //   encodeStateVectorFromUpdateBatch(updates, {format})
 //   convertUpdateFormatV1ToV2(update) / convertUpdateFormatV2ToV1(update), convertUpdateFormatBatch(updates, {format})
 //                                                      (yjs 13.5.x convertUpdateFormat; format = the input's)
+//   parseUpdateMeta(update) / parseUpdateMetaV2 -> {from: Map, to: Map}, parseUpdateMetaBatch(updates, {format})
+//                                                      (yjs 13.5.16 parseUpdateMeta[V2])
+//   mergeDeleteSetsBatch(docs, {format}), mergeEncodedDeleteSets(encodedDss, {format})
+//                                                      (PermanentUserData.js:49-54: mergeDeleteSets over
+//                                                       encoded delete sets -> one encoded delete set)
 // There is no CPU fallback: a missing addon or GPU throws.
 'use strict'
 const path = require('path')
@@ -23,7 +28,7 @@ function init () {
   }
 }
 
-const OP = { merge: 0, diff: 1, sv: 2, conv: 3 }
+const OP = { merge: 0, diff: 1, sv: 2, conv: 3, meta: 4, dsmerge: 5 }
 const fmtOf = o => (o && (o.format === 'v2' || o.format === 2)) ? 2 : 1
 
 // status -> the exception yjs itself throws for that input
@@ -94,6 +99,29 @@ function convertUpdateFormatBatch (updates, opts, throwErrors = false) {
   return unpack(addon.run(OP.conv, fmtOf(opts), p.arena, p.updOff, p.docUpd), throwErrors)
 }
 
+// the engine writes parseUpdateMeta's two Maps as two encoded state vectors (from, then to)
+function decodeMeta (b) {
+  let pos = 0
+  const vu = () => { let v = 0; let m = 1; for (;;) { const x = b[pos++]; v += (x & 0x7f) * m; m *= 128; if (x < 0x80) return v } }
+  const res = {}
+  for (const key of ['from', 'to']) {
+    const m = new Map()
+    for (let n = vu(); n > 0; n--) { const client = vu(); m.set(client, vu()) }
+    res[key] = m
+  }
+  return res
+}
+function parseUpdateMetaBatch (updates, opts, throwErrors = false) {
+  init()
+  const p = pack(updates.map(u => [u]))
+  return unpack(addon.run(OP.meta, fmtOf(opts), p.arena, p.updOff, p.docUpd), throwErrors).map(r => r instanceof Error ? r : decodeMeta(r))
+}
+function mergeDeleteSetsBatch (docs, opts, throwErrors = false) {
+  init()
+  const p = pack(docs)
+  return unpack(addon.run(OP.dsmerge, fmtOf(opts), p.arena, p.updOff, p.docUpd), throwErrors)
+}
+
 // single-document yjs signatures (mergeUpdates([u]) returns the same object, like yjs)
 const mergeUpdates = updates => updates.length === 1 ? updates[0] : mergeUpdatesBatch([updates], { format: 'v1' }, true)[0]
 const mergeUpdatesV2 = updates => updates.length === 1 ? updates[0] : mergeUpdatesBatch([updates], { format: 'v2' }, true)[0]
@@ -103,9 +131,13 @@ const encodeStateVectorFromUpdate = u => encodeStateVectorFromUpdateBatch([u], {
 const encodeStateVectorFromUpdateV2 = u => encodeStateVectorFromUpdateBatch([u], { format: 'v2' }, true)[0]
 const convertUpdateFormatV1ToV2 = u => convertUpdateFormatBatch([u], { format: 'v1' }, true)[0]
 const convertUpdateFormatV2ToV1 = u => convertUpdateFormatBatch([u], { format: 'v2' }, true)[0]
+const parseUpdateMeta = u => parseUpdateMetaBatch([u], { format: 'v1' }, true)[0]
+const parseUpdateMetaV2 = u => parseUpdateMetaBatch([u], { format: 'v2' }, true)[0]
+const mergeEncodedDeleteSets = (dss, opts) => mergeDeleteSetsBatch([dss], opts, true)[0]
 
 module.exports = {
   mergeUpdates, mergeUpdatesV2, diffUpdate, diffUpdateV2, encodeStateVectorFromUpdate, encodeStateVectorFromUpdateV2,
   mergeUpdatesBatch, diffUpdateBatch, encodeStateVectorFromUpdateBatch,
-  convertUpdateFormatV1ToV2, convertUpdateFormatV2ToV1, convertUpdateFormatBatch
+  convertUpdateFormatV1ToV2, convertUpdateFormatV2ToV1, convertUpdateFormatBatch,
+  parseUpdateMeta, parseUpdateMetaV2, parseUpdateMetaBatch, mergeDeleteSetsBatch, mergeEncodedDeleteSets
 }

@@ -134,6 +134,8 @@ static napi_value Run(napi_env env, napi_callback_info info) {
     rc = op == 0   ? ym_merge(&b, &o, nullptr, nullptr)
          : op == 1 ? ym_diff(&b, &o, nullptr, nullptr)
          : op == 3 ? ym_convert(&b, &o, nullptr, nullptr)
+         : op == 4 ? ym_meta(&b, &o, nullptr, nullptr)
+         : op == 5 ? ym_ds_merge(&b, &o, nullptr, nullptr)
                    : ym_sv(&b, &o, nullptr, nullptr);
     if (rc == YM_ERR_CAPACITY) { cap = o.used + 4096; continue; }
     break;

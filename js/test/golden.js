@@ -6,6 +6,13 @@ const Y = require('..')
 const dir = path.join(__dirname, '..', '..', 'tests', 'golden')
 const errName = { URIError: 'URIError', TypeError: 'TypeError', RangeError: 'RangeError', SyntaxError: 'SyntaxError', Error: 'Error' }
 let ok = 0; let bad = []; let unsupported = 0
+// parseUpdateMeta's Maps re-encoded the way the golden vectors hold them (from, then to; vu pairs)
+function encodeMeta (m) {
+  const out = []
+  const vu = v => { while (v > 127) { out.push(128 | (v % 128)); v = Math.floor(v / 128) } out.push(v) }
+  for (const map of [m.from, m.to]) { vu(map.size); map.forEach((clock, client) => { vu(client); vu(clock) }) }
+  return Uint8Array.from(out)
+}
 for (const f of fs.readdirSync(dir).filter(f => f.endsWith('.json')).sort()) {
   const cases = JSON.parse(fs.readFileSync(path.join(dir, f))).cases
   for (const c of cases) {
@@ -15,6 +22,8 @@ for (const f of fs.readdirSync(dir).filter(f => f.endsWith('.json')).sort()) {
     try {
       if (c.op === 'merge') out = (c.fmt === 1 ? Y.mergeUpdates : Y.mergeUpdatesV2)(inputs)
       else if (c.op === 'diff') out = (c.fmt === 1 ? Y.diffUpdate : Y.diffUpdateV2)(inputs[0], new Uint8Array(Buffer.from(c.sv, 'base64')))
+      else if (c.op === 'meta') out = encodeMeta((c.fmt === 1 ? Y.parseUpdateMeta : Y.parseUpdateMetaV2)(inputs[0]))
+      else if (c.op === 'dsmerge') out = Y.mergeEncodedDeleteSets(inputs, { format: c.fmt })
       else if (c.op === 'conv') out = (c.fmt === 1 ? Y.convertUpdateFormatV1ToV2 : Y.convertUpdateFormatV2ToV1)(inputs[0])
       else out = (c.fmt === 1 ? Y.encodeStateVectorFromUpdate : Y.encodeStateVectorFromUpdateV2)(inputs[0])
     } catch (e) { err = e }

@@ -43,8 +43,12 @@ def test_library_is_gfx950_code():
 def test_python_mirror_names():
     import yjs_amd
     for n in ("mergeUpdates", "mergeUpdatesV2", "diffUpdate", "diffUpdateV2", "encodeStateVectorFromUpdate",
-              "encodeStateVectorFromUpdateV2", "mergeUpdatesBatch", "diffUpdateBatch", "encodeStateVectorFromUpdateBatch"):
+              "encodeStateVectorFromUpdateV2", "mergeUpdatesBatch", "diffUpdateBatch", "encodeStateVectorFromUpdateBatch",
+              "parseUpdateMeta", "parseUpdateMetaV2", "parseUpdateMetaBatch", "mergeDeleteSetsBatch",
+              "mergeEncodedDeleteSets"):
         assert callable(getattr(yjs_amd, n))
+    # the meta decoder is host logic: two encoded state vectors, Map order kept
+    assert yjs_amd.decode_meta(bytes([2, 9, 0, 3, 5, 2, 9, 4, 3, 130, 1])) == {"from": {9: 0, 3: 5}, "to": {9: 4, 3: 130}}
     # identity semantics need no device: mergeUpdates([u]) is u itself
     u = b"\x00\x00"
     assert yjs_amd.mergeUpdates([u]) is u
@@ -59,4 +63,5 @@ def test_node_addon_loads_and_exports():
     assert r.returncode == 0, r.stderr
     names = set(r.stdout.strip().split(","))
     assert {"mergeUpdates", "mergeUpdatesV2", "diffUpdate", "diffUpdateV2", "encodeStateVectorFromUpdate",
-            "encodeStateVectorFromUpdateV2", "mergeUpdatesBatch"} <= names
+            "encodeStateVectorFromUpdateV2", "mergeUpdatesBatch", "parseUpdateMeta", "parseUpdateMetaV2",
+            "mergeEncodedDeleteSets"} <= names

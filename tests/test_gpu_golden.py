@@ -37,14 +37,14 @@ def test_golden_batched_on_gpu(engine, key):
     from yjs_amd import pack_docs
     cases = _groups()[key]
     op, fmt = key
-    if op == "merge":
+    if op in ("merge", "dsmerge"):  # k inputs per document
         arena, upd_off, doc_upd = pack_docs([c["inputs"] for c in cases])
-        res = engine.run_host("merge", fmt, arena, upd_off, doc_upd)
+        res = engine.run_host(op, fmt, arena, upd_off, doc_upd)
     elif op == "diff":
         arena, upd_off, doc_upd = pack_docs([[c["inputs"][0]] for c in cases])
         sva, svo, _ = pack_docs([[c["sv"]] for c in cases])
         res = engine.run_host("diff", fmt, arena, upd_off, doc_upd, sva, svo)
-    else:  # sv, conv: one update per document
+    else:  # sv, conv, meta: one update per document
         arena, upd_off, doc_upd = pack_docs([[c["inputs"][0]] for c in cases])
         res = engine.run_host(op, fmt, arena, upd_off, doc_upd)
     out_arena, out_off, out_len, status = res

@@ -265,3 +265,79 @@ def test_delete_set_merges_duplicates_and_large_clocks(engine, fmt):
     assert not bad, bad[:10]
     st = engine.stats
     assert st["docs_fast"] == len(docs) - sum(big), st
+
+
+@pytest.mark.parametrize("fmt", [1, 2])
+def test_meta_workloads_match_oracle(engine, fmt):
+    """parseUpdateMeta[V2] over the raw C2 updates (~1 M single updates, each one client section or a
+    few) and over merged C2 / C5 documents (4 and ~1,000 client sections): engine == oracle per update."""
+    from yjs_amd import pack_docs
+    arena, upd_off, doc_upd = load_ymb(f"c2_v{fmt}")
+    n_upd = int(doc_upd[1000])  # the first 1,000 documents' updates, one per batch document
+    a1, o1 = arena[:int(upd_off[n_upd])], upd_off[:n_upd + 1]
+    d1 = np.arange(n_upd + 1, dtype=np.uint32)
+    outs, st, _ = O.batch("meta", fmt, a1, o1, d1, nthreads=8)
+    bad = _compare(engine.run_host("meta", fmt, a1, o1, d1), outs, st)
+    assert not bad, bad[:10]
+    for name in (f"c2_v{fmt}", f"c5_v{fmt}"):
+        arena, upd_off, doc_upd = load_ymb(name)
+        if name.startswith("c5"):  # merged by the engine (C5 merges are checked against the oracle above)
+            oa, oo, ol, ost = engine.run_host("merge", fmt, arena, upd_off, doc_upd)
+            assert (ost == 0).all()
+            merged = [oa[int(oo[d]):int(oo[d]) + int(ol[d])].tobytes() for d in range(len(ost))]
+        else:
+            merged, status, _ = O.batch("merge", fmt, arena, upd_off, doc_upd, nthreads=8)
+            assert (status == 0).all()
+        a2, o2, d2 = pack_docs([[m] for m in merged])
+        outs, st, _ = O.batch("meta", fmt, a2, o2, d2, nthreads=8)
+        assert (st == 0).all()
+        bad = _compare(engine.run_host("meta", fmt, a2, o2, d2), outs, st)
+        assert not bad, (name, bad[:10])
+
+
+def _encode_ds(clients, v2):
+    out = bytearray(_vu(len(clients)))
+    for client, items in clients:
+        out += _vu(client) + _vu(len(items))
+        cur = 0
+        for clock, ln in items:
+            if v2:
+                out += _vu(clock - cur) + _vu(ln - 1)
+                cur = clock + ln
+            else:
+                out += _vu(clock) + _vu(ln)
+    return bytes(out)
+
+
+@pytest.mark.parametrize("fmt", [1, 2])
+def test_ds_merge_batch_matches_oracle(engine, fmt):
+    """PermanentUserData's delete-set merge over 20,000 documents of 1..48 encoded delete sets each
+    (64 clients, overlapping / touching / duplicated intervals, clocks up to 2^32 - 1)."""
+    from yjs_amd import pack_docs
+    rng = np.random.default_rng(77 + fmt)
+    docs = []
+    for d in range(20000):
+        k = int(rng.integers(1, 49)) if d % 50 else int(rng.integers(0, 3))
+        blobs = []
+        for _ in range(k):
+            cl = []
+            for client in rng.choice(64, size=int(rng.integers(0, 5)), replace=False):
+                base = 4294967000 if client == 63 else 0
+                n = int(rng.integers(0, 6))
+                starts = np.sort(rng.integers(0, 200, size=n))
+                items, end = [], -1
+                for s in starts:
+                    s = int(s) + base
+                    if fmt == 2 and s < end:
+                        continue  # a DSEncoderV2 writes clocks in order (delta coded)
+                    ln = int(rng.integers(1, 8))
+                    items.append((s, ln))
+                    end = s + ln
+                cl.append((int(client) * 7919 + 1, items))
+            blobs.append(_encode_ds(cl, fmt == 2))
+        docs.append(blobs)
+    a, o, dd = pack_docs(docs)
+    outs, status, _ = O.batch("dsmerge", fmt, a, o, dd, nthreads=8)
+    assert (status == 0).all()
+    bad = _compare(engine.run_host("dsmerge", fmt, a, o, dd), outs, status)
+    assert not bad, bad[:10]

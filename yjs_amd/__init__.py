@@ -10,5 +10,7 @@ from .engine import (  # noqa: F401
     encodeStateVectorFromUpdate, encodeStateVectorFromUpdateV2,
     mergeUpdatesBatch, diffUpdateBatch, encodeStateVectorFromUpdateBatch,
     convertUpdateFormatV1ToV2, convertUpdateFormatV2ToV1, convertUpdateFormatBatch,
+    parseUpdateMeta, parseUpdateMetaV2, parseUpdateMetaBatch, decode_meta,
+    mergeDeleteSetsBatch, mergeEncodedDeleteSets,
     pack_docs, lib_path,
 )

@@ -461,5 +461,7 @@ int ym_merge(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { re
 int ym_diff(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_DIFF, b, out, stream, stats); }
 int ym_sv(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_SV, b, out, stream, stats); }
 int ym_convert(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_CONV, b, out, stream, stats); }
+int ym_meta(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_META, b, out, stream, stats); }
+int ym_ds_merge(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_DSMERGE, b, out, stream, stats); }
 
 }  // extern "C"

@@ -577,6 +577,7 @@ struct Reader {
   Rd rest;
   uint32_t v2;
   uint8_t started, done, filter, has_curr;
+  uint8_t lax;  // non-canonical JSON / any accepted (parseUpdateMeta never re-encodes content)
   uint32_t nclients, ci, nstructs, si;
   int64_t client, clock;
   // V2 columns
@@ -658,7 +659,7 @@ YM_INL Span rd_json_text(Ctx &c, Reader &r) {
   int nc = 0;
   int e = json_check(c, s.off, s.n, &nc);
   if (e) seterr(c, e);
-  else if (nc) seterr(c, ST_UNSUPPORTED);
+  else if (nc && !r.lax) seterr(c, ST_UNSUPPORTED);
   return s;
 }
 // one `any` value in rest, must be canonical
@@ -667,7 +668,7 @@ YM_INL Span rd_any_span(Ctx &c, Reader &r) {
   int nc = 0;
   any_skip(c, r.rest, &nc);
   Span s = {r.rest.start + p0, (uint32_t)(r.rest.pos - p0), 0, 0};
-  if (!c.err && nc) seterr(c, ST_UNSUPPORTED);
+  if (!c.err && nc && !r.lax) seterr(c, ST_UNSUPPORTED);
   return s;
 }
 
@@ -725,7 +726,7 @@ YM_BIG void read_content(Ctx &c, Reader &r, SStruct &s, int info) {
           int nc = 0;
           int e = json_check(c, t.off, t.n, &nc);
           if (e) seterr(c, e);
-          else if (nc) seterr(c, ST_UNSUPPORTED);
+          else if (nc && !r.lax) seterr(c, ST_UNSUPPORTED);
         }
       }
       uint64_t last = r.v2 ? r.str_off + r.spos_b : r.rest.start + r.rest.pos;
@@ -767,7 +768,7 @@ YM_BIG void read_content(Ctx &c, Reader &r, SStruct &s, int info) {
       for (int64_t i = 0; i < s.cnt && !c.err; i++) {
         int nc = 0;
         any_skip(c, r.rest, &nc);
-        if (!c.err && nc) seterr(c, ST_UNSUPPORTED);
+        if (!c.err && nc && !r.lax) seterr(c, ST_UNSUPPORTED);
       }
       s.a.off = r.rest.start + p0;
       s.a.n = (uint32_t)(r.rest.pos - p0);
@@ -777,7 +778,7 @@ YM_BIG void read_content(Ctx &c, Reader &r, SStruct &s, int info) {
     case 9:
       s.a = rd_string(c, r);
       s.b = rd_any_span(c, r);
-      if (!c.err) check_doc_opts(c, s.b);
+      if (!c.err && !r.lax) check_doc_opts(c, s.b);
       s.len = 1;
       break;
     case 0: case 10: seterr(c, ST_UNEXPECTED); break;
@@ -1814,6 +1815,89 @@ YM_BIG void sv_doc(Ctx &c, DocWS &ws, uint64_t uoff, uint64_t ulen, uint32_t v2,
     __builtin_memset(&L, 0, sizeof(Layout));
     L.svcount = cnt;
     L.total = vu_size(cnt) + o.n;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// parseUpdateMetaV2 (13.5.16 parseUpdateMeta / parseUpdateMetaV2): a LazyStructReader that keeps Skips;
+// `from` takes a client's first clock when its section starts, `to` the end of its last struct when the
+// next section starts (JS Maps: a client met again keeps its position and takes the new value).
+// Output: from then to, each vu(count) | (client, clock)* in Map order.  ws.sv holds (client, from, to)
+// triples.
+// ------------------------------------------------------------------------------------------------
+YM_INL void meta_put(Ctx &c, DocWS &ws, uint32_t &n, int64_t client, int64_t v, int slot) {
+  uint32_t cap = (uint32_t)((2ull * ws.sv_cap) / 3);
+  int64_t *t = ws.sv;
+  for (uint32_t i = n; i-- > 0;) {  // the most recent section's client is the usual hit
+    if (t[3 * i] == client) { t[3 * i + slot] = v; return; }
+  }
+  if (n >= cap) { seterr(c, ST_RETRY); return; }
+  t[3 * n] = client; t[3 * n + 1] = 0; t[3 * n + 2] = 0;
+  t[3 * n + slot] = v;
+  n++;
+}
+YM_BIG void meta_doc(Ctx &c, DocWS &ws, uint64_t uoff, uint64_t ulen, uint32_t v2, int pass, Layout &L, uint8_t *out) {
+  Reader &r = ws.rs[0];
+  reader_open(c, r, uoff, ulen, v2);
+  r.lax = 1;
+  if (c.err) return;
+  reader_next(c, r);
+  if (c.err) return;
+  uint32_t n = 0;
+  if (r.has_curr) {
+    int64_t client = r.curr.client, clock = r.curr.clock;
+    meta_put(c, ws, n, client, clock, 1);
+    for (bool have = true; have && !c.err; have = reader_next(c, r)) {
+      if (client != r.curr.client) {
+        meta_put(c, ws, n, client, clock, 2);
+        meta_put(c, ws, n, r.curr.client, r.curr.clock, 1);
+        client = r.curr.client;
+      }
+      clock = r.curr.clock + r.curr.len;
+    }
+    if (c.err) return;
+    meta_put(c, ws, n, client, clock, 2);
+    if (c.err) return;
+  }
+  Out o = {pass == 2 ? out : nullptr, 0};
+  for (int slot = 1; slot <= 2; slot++) {
+    ovu(o, (int64_t)n);
+    for (uint32_t i = 0; i < n; i++) { ovu(o, ws.sv[3 * i]); ovu(o, ws.sv[3 * i + slot]); }
+  }
+  if (pass == 1) {
+    __builtin_memset(&L, 0, sizeof(Layout));
+    L.svcount = n;
+    L.total = o.n;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// PermanentUserData's delete-set merge (PermanentUserData.js:49-54): k encoded delete sets (DSEncoderV1
+// / DSEncoderV2 rest bytes, as encodeSnapshot[V2] writes them, Snapshot.js:84-101) read by
+// readDeleteSet, merged by mergeDeleteSets (13.5.16 he@10482 + le@10242 union), written by
+// writeDeleteSet.  Input i of the document is the byte range [upd_off[u0+i], upd_off[u0+i+1]).
+// ------------------------------------------------------------------------------------------------
+YM_BIG void dsmerge_doc(Ctx &c, DocWS &ws, const uint64_t *upd_off, uint32_t u0, uint32_t k, uint32_t v2, int pass,
+                        Layout &L, uint8_t *out) {
+  uint64_t nds = 0;
+  for (uint32_t i = 0; i < k && !c.err; i++) {
+    Reader &r = ws.rs[0];
+    __builtin_memset(&r, 0, sizeof(Reader));
+    r.rest.start = upd_off[u0 + i];
+    r.rest.len = upd_off[u0 + i + 1] - upd_off[u0 + i];
+    r.v2 = v2;
+    ds_gather(c, r, ws.ds, ws.ds_cap, nds);
+  }
+  if (c.err) return;
+  Enc e;
+  enc_init(e, v2);
+  e.rest.p = pass == 2 ? out : nullptr;
+  ds_emit(c, e, ws.ds, nds, ws.dsg, true);
+  if (c.err) return;
+  if (pass == 1) {
+    __builtin_memset(&L, 0, sizeof(Layout));
+    L.ds_bytes = e.rest.n;
+    L.total = e.rest.n;
   }
 }
 

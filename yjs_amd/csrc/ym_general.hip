@@ -12,10 +12,18 @@ using namespace ym;
 
 __device__ __forceinline__ uint32_t job_doc(const GeneralJob &j, uint32_t i) { return j.list ? j.list[i] : i; }
 
+// the state-vector table: diff = the decoded state vector; meta = (client, from, to) triples, at most one
+// client per update byte
+__device__ __forceinline__ uint64_t ws_sv_bytes(const GeneralJob &j, uint32_t d, uint64_t bytes) {
+  if (j.op == OP_DIFF) return j.sv_off[d + 1] - j.sv_off[d];
+  if (j.op == OP_META) return 3 * bytes + 6;
+  return 0;
+}
+
 __device__ __forceinline__ void carve(const GeneralJob &j, uint32_t i, uint32_t d, DocWS &w) {
   uint32_t k = j.doc_upd[d + 1] - j.doc_upd[d];
   uint64_t bytes = j.upd_off[j.doc_upd[d + 1]] - j.upd_off[j.doc_upd[d]];
-  GeneralWsSize z = general_ws_size(k, bytes, j.parts_mul, j.op == OP_DIFF ? (j.sv_off[d + 1] - j.sv_off[d]) : 0);
+  GeneralWsSize z = general_ws_size(k, bytes, j.parts_mul, ws_sv_bytes(j, d, bytes));
   uint8_t *p = j.ws + j.ws_off[i];
   w.rs = (Reader *)p; p += z.rs;
   w.arr = (uint32_t *)p; p += z.arr;
@@ -32,7 +40,7 @@ __global__ void k_general_ws(GeneralJob j, uint64_t *ws_size) {
   uint32_t d = job_doc(j, i);
   uint32_t k = j.doc_upd[d + 1] - j.doc_upd[d];
   uint64_t bytes = j.upd_off[j.doc_upd[d + 1]] - j.upd_off[j.doc_upd[d]];
-  ws_size[i] = general_ws_size(k, bytes, j.parts_mul, j.op == OP_DIFF ? (j.sv_off[d + 1] - j.sv_off[d]) : 0).total;
+  ws_size[i] = general_ws_size(k, bytes, j.parts_mul, ws_sv_bytes(j, d, bytes)).total;
 }
 
 __global__ void __launch_bounds__(64) k_general(GeneralJob j, int pass) {
@@ -58,6 +66,11 @@ __global__ void __launch_bounds__(64) k_general(GeneralJob j, int pass) {
     if (k != 1) c.err = ST_UNEXPECTED;
     else diff_doc(c, w, j.upd_off[u0], j.upd_off[u0 + 1] - j.upd_off[u0], j.sv + j.sv_off[d], j.sv_off[d + 1] - j.sv_off[d],
                   j.v2, pass, L, out);
+  } else if (j.op == OP_DSMERGE) {
+    dsmerge_doc(c, w, j.upd_off, u0, k, j.v2, pass, L, out);
+  } else if (j.op == OP_META) {
+    if (k != 1) c.err = ST_UNEXPECTED;
+    else meta_doc(c, w, j.upd_off[u0], j.upd_off[u0 + 1] - j.upd_off[u0], j.v2, pass, L, out);
   } else if (j.op == OP_CONV) {
     if (k != 1) c.err = ST_UNEXPECTED;
     else conv_doc(c, w, j.upd_off[u0], j.upd_off[u0 + 1] - j.upd_off[u0], j.v2, pass, L, out);

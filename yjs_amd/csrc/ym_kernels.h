@@ -7,7 +7,7 @@
 
 namespace ymk {
 
-enum : uint32_t { OP_MERGE = 0, OP_DIFF = 1, OP_SV = 2, OP_CONV = 3 };
+enum : uint32_t { OP_MERGE = 0, OP_DIFF = 1, OP_SV = 2, OP_CONV = 3, OP_META = 4, OP_DSMERGE = 5 };
 
 // internal status: document not taken by the fast path, routed to the general path
 constexpr int ST_PENDING = 101;

@@ -79,7 +79,8 @@ class _Stats(ctypes.Structure):
                 ("docs_large", ctypes.c_uint64), ("large_ms", ctypes.c_double)]
 
 
-EXPORTS = ("ym_init", "ym_shutdown", "ym_strerror", "ym_out_bound", "ym_merge", "ym_diff", "ym_sv", "ym_convert")
+EXPORTS = ("ym_init", "ym_shutdown", "ym_strerror", "ym_out_bound", "ym_merge", "ym_diff", "ym_sv", "ym_convert",
+           "ym_meta", "ym_ds_merge")
 
 
 def load_library(path=None):
@@ -90,7 +91,7 @@ def load_library(path=None):
     L.ym_init.argtypes = [ctypes.c_int]
     L.ym_strerror.restype = ctypes.c_char_p
     L.ym_out_bound.restype = ctypes.c_uint64
-    for fn in (L.ym_merge, L.ym_diff, L.ym_sv, L.ym_convert):
+    for fn in (L.ym_merge, L.ym_diff, L.ym_sv, L.ym_convert, L.ym_meta, L.ym_ds_merge):
         fn.argtypes = [ctypes.POINTER(_Batch), ctypes.POINTER(_Out), ctypes.c_void_p, ctypes.POINTER(_Stats)]
         fn.restype = ctypes.c_int
     return L
@@ -121,9 +122,14 @@ class Engine:
         self.device = device
         self.last_stats = _Stats()
 
+    def _fn(self, op):
+        L = self.lib
+        return {"merge": L.ym_merge, "diff": L.ym_diff, "sv": L.ym_sv, "conv": L.ym_convert, "meta": L.ym_meta,
+                "dsmerge": L.ym_ds_merge}[op]
+
     # ---- host-memory batches ------------------------------------------------------------------
     def run_host(self, op, fmt, arena, upd_off, doc_upd, sv_arena=None, sv_off=None):
-        """Runs op ('merge'|'diff'|'sv') over a packed host batch.
+        """Runs op ('merge'|'diff'|'sv'|'conv'|'meta'|'dsmerge') over a packed host batch.
         Returns (out_arena u8, out_off u64, out_len u64, status i32)."""
         arena = np.ascontiguousarray(arena, np.uint8)
         upd_off = np.ascontiguousarray(upd_off, np.uint64)
@@ -146,7 +152,7 @@ class Engine:
             b.sv_arena = sv_arena.ctypes.data if sv_arena.size else None
             b.sv_off = sv_off.ctypes.data
         cap = int(self.lib.ym_out_bound(ctypes.byref(b)))
-        fn = {"merge": self.lib.ym_merge, "diff": self.lib.ym_diff, "sv": self.lib.ym_sv, "conv": self.lib.ym_convert}[op]
+        fn = self._fn(op)
         for _ in range(4):
             out_arena = np.zeros(max(cap, 1), np.uint8)
             out_off = np.zeros(max(n_docs, 1), np.uint64)
@@ -180,7 +186,7 @@ class Engine:
             b.sv_arena = sv_arena.data_ptr()
             b.sv_off = sv_off.data_ptr()
         o = _Out(out_arena.data_ptr(), out_arena.numel(), out_off.data_ptr(), out_len.data_ptr(), status.data_ptr(), 0)
-        fn = {"merge": self.lib.ym_merge, "diff": self.lib.ym_diff, "sv": self.lib.ym_sv, "conv": self.lib.ym_convert}[op]
+        fn = self._fn(op)
         s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
         rc = fn(ctypes.byref(b), ctypes.byref(o), s, ctypes.byref(self.last_stats))
         return rc, int(o.used)
@@ -201,7 +207,7 @@ class Engine:
             b.sv_arena = sv_arena.data_ptr()
             b.sv_off = sv_off.data_ptr()
         o = _Out(out_arena.data_ptr(), out_arena.numel(), out_off.data_ptr(), out_len.data_ptr(), status.data_ptr(), 0)
-        fn = {"merge": self.lib.ym_merge, "diff": self.lib.ym_diff, "sv": self.lib.ym_sv, "conv": self.lib.ym_convert}[op]
+        fn = self._fn(op)
         s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
         pb, po, ps = ctypes.byref(b), ctypes.byref(o), ctypes.byref(self.last_stats)
         keep = (b, o)
@@ -298,3 +304,57 @@ def convertUpdateFormatV1ToV2(update):
 
 def convertUpdateFormatV2ToV1(update):
     return convertUpdateFormatBatch([update], 2, True)[0]
+
+
+def _read_vu(b, pos):
+    v, shift = 0, 0
+    while True:
+        x = b[pos]
+        pos += 1
+        v |= (x & 0x7F) << shift
+        shift += 7
+        if x < 0x80:
+            return v, pos
+
+
+def decode_meta(b):
+    """The engine's parseUpdateMeta bytes -> {"from": {client: clock}, "to": {client: clock}} (dict order =
+    the JS Map order)."""
+    out, pos = {}, 0
+    for key in ("from", "to"):
+        n, pos = _read_vu(b, pos)
+        m = {}
+        for _ in range(n):
+            client, pos = _read_vu(b, pos)
+            clock, pos = _read_vu(b, pos)
+            m[client] = clock
+        out[key] = m
+    return out
+
+
+def parseUpdateMetaBatch(updates, fmt=1, raise_errors=False, decode=True):
+    """yjs 13.5.16 parseUpdateMeta[V2] over a batch: per update {"from": {...}, "to": {...}} (or, with
+    decode=False, the engine's encoding: two encoded state vectors back to back)."""
+    arena, upd_off, doc_upd = pack_docs([[u] for u in updates])
+    res = _unpack(*_engine().run_host("meta", fmt, arena, upd_off, doc_upd), raise_errors)
+    return [decode_meta(r) if decode and isinstance(r, bytes) else r for r in res]
+
+
+def parseUpdateMeta(update):
+    return parseUpdateMetaBatch([update], 1, True)[0]
+
+
+def parseUpdateMetaV2(update):
+    return parseUpdateMetaBatch([update], 2, True)[0]
+
+
+def mergeDeleteSetsBatch(docs, fmt=1, raise_errors=False):
+    """PermanentUserData's delete-set merge (reference src/utils/PermanentUserData.js:49-54) over a batch:
+    docs is a list of lists of encoded delete sets (DSEncoderV1 bytes, or DSEncoderV2 with fmt=2); returns
+    one encoded merged delete set per document."""
+    arena, upd_off, doc_upd = pack_docs(docs)
+    return _unpack(*_engine().run_host("dsmerge", fmt, arena, upd_off, doc_upd), raise_errors)
+
+
+def mergeEncodedDeleteSets(encoded_dss, fmt=1):
+    return mergeDeleteSetsBatch([list(encoded_dss)], fmt, True)[0]
