@@ -83,22 +83,50 @@ def secondary(dev, eng):
     merges (10k docs), C3 diffUpdate / encodeStateVectorFromUpdate (configs[2]: 4,096 V1 docs of
     0.9 MB; 1,024 V2 docs) against random state vectors, C5 (configs[4]: 256 docs of ~16 k updates
     from 1,024 clients) mergeUpdates[V2] and diffUpdate[V2] of the merged documents against random
-    per-client state vectors.  Whole-call GB/s of input."""
+    per-client state vectors, parseUpdateMeta over the ~1 M C2 updates, PermanentUserData's
+    delete-set merge over the C4 updates' delete sets.  Whole-call GB/s of input."""
     import torch
     from yjs_amd import pack_docs
     from yjs_amd.workloads import load_ymb, replicate, random_state_vectors
     res = {}
+    only = os.environ.get("YM_SECONDARY")  # comma-separated subset of the case names
     cases = [("merge_c4_v1", "merge", "c4_v1", 10000), ("merge_c2_v2", "merge", "c2_v2", 10000),
              ("merge_c4_v2", "merge", "c4_v2", 10000), ("diff_c3_v1", "diff", "c3_v1", 4096),
              ("sv_c3_v1", "sv", "c3_v1", 4096), ("diff_c3_v2", "diff", "c3_v2", 1024),
              ("merge_c5_v1", "merge", "c5_v1", 256), ("merge_c5_v2", "merge", "c5_v2", 256),
-             ("diff_c5_v1", "diff", "c5_v1", 256), ("diff_c5_v2", "diff", "c5_v2", 256)]
+             ("diff_c5_v1", "diff", "c5_v1", 256), ("diff_c5_v2", "diff", "c5_v2", 256),
+             ("meta_c2_v1", "meta", "c2_v1", 10000), ("meta_c2_v2", "meta", "c2_v2", 10000),
+             ("dsmerge_c4_v1", "dsmerge", "c4_v1", 10000)]
     for name, op, wl, n in cases:
+        if only and name not in only.split(","):
+            continue
         fmt = 2 if wl.endswith("v2") else 1
         a, o, d = load_ymb(wl)
         sva = svo = None
         if op == "merge":
             a, o, d = replicate(a, o, d, n)
+        elif op == "meta":
+            # parseUpdateMeta of every update of n C2 documents (~1 M single-update batch entries)
+            a, o, d = replicate(a, o, d, n)
+            d = np.arange(len(o), dtype=np.uint32)
+        elif op == "dsmerge":
+            # PermanentUserData-style: per document, the encoded delete sets of its C4 updates (the DS of
+            # update u is diffUpdate(u, parseUpdateMeta(u).to) minus its empty struct section, vu(0)),
+            # merged into one
+            from yjs_amd import decode_meta
+            from yjs_amd.workloads import encode_sv
+            nt = min(1000, len(d) - 1)  # 1,000 templates (128 k updates), replicated to n documents
+            a, o, d = a[:int(o[d[nt]])], o[:int(d[nt]) + 1], d[:nt + 1]
+            per = np.arange(len(o), dtype=np.uint32)
+            sa, so_, sl, sst = eng.run_host("meta", 1, a, o, per)
+            svs = [encode_sv(list(decode_meta(sa[int(so_[i]):int(so_[i]) + int(sl[i])].tobytes())["to"].items()))
+                   for i in range(len(sst))]
+            sva_, svo_, _ = pack_docs([[x] for x in svs])
+            da, do_, dl, dst = eng.run_host("diff", 1, a, o, per, sva_, svo_)
+            assert (sst == 0).all() and (dst == 0).all()
+            blobs = [da[int(do_[i]) + 1:int(do_[i]) + int(dl[i])].tobytes() for i in range(len(dst))]
+            docs = [[blobs[u] for u in range(int(d[t]), int(d[t + 1]))] for t in range(len(d) - 1)]
+            a, o, d = replicate(*pack_docs(docs), n)
         elif wl.startswith("c5"):
             # the merged C5 documents (merged here by the engine), random per-client state vectors
             ma, mo, ml, _ = eng.run_host("merge", fmt, a, o, d)
@@ -127,7 +155,7 @@ def secondary(dev, eng):
         oo = torch.empty(nd, dtype=torch.int64, device=dev)
         ol = torch.empty(nd, dtype=torch.int64, device=dev)
         st = torch.empty(nd, dtype=torch.int32, device=dev)
-        steps = 5 if op == "merge" else 2
+        steps = 5 if op in ("merge", "meta", "dsmerge") else 2
         eng.run_device(op, fmt, ga, go, gd, oa, oo, ol, st, gsa, gso)
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()

@@ -297,11 +297,12 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
 
   if (S->dirty) HIPCHK(hipMemsetAsync(counters, 0, 1024, st));
   S->dirty = true;
+  bool slots = false;  // the fast paths wrote their outputs into the slot region (merges, delete-set merges)
   // ends a round trip: counters and stats land in pinned host memory, then one stream sync
   auto finish = [&]() -> int {
     const uint32_t fin_blocks = stats ? (nd + FIN_DOCS - 1) / FIN_DOCS : 1;
     k_finish<<<fin_blocks, FIN_THREADS, 0, st>>>(o_status, o_len, nd, upd_off, b->n_upd, counters, S->pinned_dev,
-                                                 stats ? 1 : 0, op == OP_MERGE ? 1 : 0, seq);
+                                                 stats ? 1 : 0, slots ? 1 : 0, seq);
     HIPCHK(hipEventRecord(S->ev1, st));
     // spin on the completion word k_finish writes last (no interrupt wake-up of a blocking wait), then
     // the stream sync, which finds the stream drained: it is what orders every result for the host
@@ -320,6 +321,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   if (fr == 0) fr = big_launch(op, j, st);         // V1 diff / state vector: streamed wave walker
   if (fr == 0) fr = big2_launch(op, j, st);        // V2 diff / state vector: streamed wave walker
   if (fr < 0) return fr;
+  slots = op == OP_MERGE || (op == OP_DSMERGE && fr == 1);
   HIPCHK(hipEventRecord(S->evf1, st));
   uint32_t ngen = nd;
   uint32_t *list = nullptr;
@@ -351,7 +353,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   if (ngen > 0) {
     // the general path's bump allocator: merges start after the slot region; diff / sv continue after
     // what the streamed kernels allocated (k_finish reset the device counter)
-    if (op == OP_MERGE) {
+    if (slots) {
       k_fast_region<<<1, 64, 0, st>>>(j, b->n_upd);
     } else if (fr == 1) {
       S->pinned[16] = S->pinned[0];

@@ -162,14 +162,16 @@ __device__ __forceinline__ bool walk_ds(uint32_t u) {
     continue;                                                           \
   }
 
-template <int STOP, int OCC>
+// DSONLY: PermanentUserData's delete-set merge (ym_ds_merge, V1): every input is an encoded delete set
+// (no struct section); the walk is W2 only and the output is the merged delete set alone.
+template <int STOP, int OCC, bool DSONLY = false>
 __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
   const uint32_t lane = threadIdx.x;
   const uint64_t arena0 = j.upd_off[0];
   for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
     const uint32_t u0 = j.doc_upd[d], k = j.doc_upd[d + 1] - u0;
     const uint64_t b0 = j.upd_off[u0], bytes = j.upd_off[u0 + k] - b0;
-    if (k <= 1 || k > UPD || bytes > IN) {
+    if ((DSONLY ? k == 0 : k <= 1) || k > UPD || bytes > IN) {
       if (lane == 0) decline(j, d);
       continue;
     }
@@ -198,8 +200,9 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
         if (u < k) {
           const uint32_t u0_ = at<uint16_t>(L_UOFF + 2 * u), len = at<uint16_t>(L_UOFF + 2 * u + 2) - u0_;
           empty |= len == 0;
-          if (len > 0 && sm[u0_] == 0) {
-            at<uint16_t>(L_UDS + 2 * u) = (uint16_t)(u0_ + 1);  // no structs: the delete set follows
+          if (len > 0 && (DSONLY || sm[u0_] == 0)) {
+            // no structs: the delete set follows (DSONLY: the input is the delete set)
+            at<uint16_t>(L_UDS + 2 * u) = (uint16_t)(DSONLY ? u0_ : u0_ + 1);
           } else {
             ub[s] = len >> 3 < 15 ? len >> 3 : 15;
             up[s] = atomicAdd(&at<uint32_t>(L_HIST + 4 * ub[s]), 1u);
@@ -245,13 +248,21 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
     }
     __syncthreads();
     const uint32_t nrec = at<uint32_t>(L_MISC), nds = at<uint32_t>(L_MISC + 4);
-    if (nrec == 0 || nrec > REC || nds > DSN) YM_DECLINE()
+    if ((DSONLY ? nrec != 0 : nrec == 0) || nrec > REC || nds > DSN) YM_DECLINE()
     if (lane == 0) {  // pad the key arrays to even length (rank loops read pairs)
       if (nrec & 1) at<uint64_t>(L_RKEY + 8 * nrec) = ~0ull;
       if (nds & 1) at<uint64_t>(L_DKEY + 8 * nds) = ~0ull;
     }
     __syncthreads();
     YM_STOP(2)
+    // output slot: 16-aligned inside the bound 2 * in + 64 per doc (no global atomics)
+    const uint64_t slot = 2 * (b0 - arena0) + 64ull * d;
+    const uint64_t slot_al = (slot + 15) & ~15ull;
+    const uint64_t slot_end = slot + 2 * bytes + 64 < j.cap ? slot + 2 * bytes + 64 : j.cap;
+    const Slot dst = make_slot(j.out + slot_al, (uint32_t)(slot_end - slot_al));
+    uint32_t hdr = 0, struct_bytes = 0;
+    bool bad = false;
+    if constexpr (!DSONLY) {
     // ---- 3. struct rank sort
     uint64_t rk[E];
     uint32_t rl[E], rsrc[E], rbl[E], rinf[E], rr[E];
@@ -294,7 +305,6 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
     // ---- 4. struct layout over rank order; lane owns positions r = E*lane + s
     uint64_t sk[E];
     uint32_t sl[E], ssrc[E], sbl[E], sinf[E], units[E], pstart[E], plastf[E], gapv[E];
-    bool bad = false;
     {
       const uint32_t r0 = E * lane;
       uint64_t kp = r0 > 0 && r0 - 1 < nrec ? at<uint64_t>(L_RKEY + 8 * (r0 - 1)) : ~0ull;
@@ -354,7 +364,6 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
       soff[s] = b;
       sbytes_lane += b;
     }
-    uint32_t struct_bytes;
     {
       const uint32_t incl = wave_incl_add(sbytes_lane);
       struct_bytes = lane_read(incl, 63);
@@ -362,11 +371,7 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
 #pragma unroll
       for (uint32_t s = 0; s < E; s++) { const uint32_t b = soff[s]; soff[s] = run; run += b; }
     }
-    const uint32_t hdr = vsz(nparts);
-    // output slot: 16-aligned inside the bound 2 * in + 64 per doc (no global atomics)
-    const uint64_t slot = 2 * (b0 - arena0) + 64ull * d;
-    const uint64_t slot_al = (slot + 15) & ~15ull;
-    const uint64_t slot_end = slot + 2 * bytes + 64 < j.cap ? slot + 2 * bytes + 64 : j.cap;
+    hdr = vsz(nparts);
     if (slot_al + hdr + struct_bytes > slot_end) {
       if (slot_al + hdr + struct_bytes > slot + 2 * bytes + 64) YM_DECLINE()
       if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }  // caller's arena too small
@@ -375,7 +380,6 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
     }
     YM_STOP(4)
     // ---- 4b. write the struct section (frees the records' registers before the delete set)
-    const Slot dst = make_slot(j.out + slot_al, (uint32_t)(slot_end - slot_al));
     if (lane == 0) put_vu(dst, 0, nparts);
 #pragma unroll
     for (uint32_t s = 0; s < E; s++) {
@@ -398,6 +402,7 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
       for (; o + 4 <= n; o += 4) ob32(dst, p + o, ld4(src + o));
       for (; o < n; o++) ob8(dst, p + o, sm[src + o]);
     }
+    }  // !DSONLY
     YM_STOP(7)
     // ---- 5. delete set
     {
@@ -620,6 +625,11 @@ __global__ void k_fast_region(GeneralJob j, uint32_t n_upd) {
 
 int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st) {
   using namespace fastv1;
+  if (op == OP_DSMERGE && !j.v2) {  // V1 delete-set merges: the same kernel, delete sets only
+    const uint32_t grid = j.n < 131072 ? j.n : 131072;
+    k_fast_merge_v1<0, 5, true><<<grid, 64, fastv1::LDS_BYTES, st>>>(j);
+    return 1;
+  }
   if (op != OP_MERGE || j.v2) return 0;  // fast path: V1 merges (the C2/C4 headline configs)
   (void)n_upd;  // the work-list counter is zero on entry (ym_api.hip k_finish); `used` is set later
   const uint32_t grid = j.n < 131072 ? j.n : 131072;
