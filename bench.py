@@ -78,6 +78,41 @@ def cpu_baseline(arena, upd_off, doc_upd, fmt, seconds):
     }
 
 
+def _ds_v1_to_v2(b):
+    """An encoded delete set, DSEncoderV1 -> DSEncoderV2 bytes (delta-coded clocks, len - 1)."""
+    pos, out = 0, bytearray()
+
+    def rd():
+        nonlocal pos
+        v, sh = 0, 0
+        while True:
+            x = b[pos]
+            pos += 1
+            v |= (x & 127) << sh
+            sh += 7
+            if x < 128:
+                return v
+
+    def wr(v):
+        while v > 127:
+            out.append(0x80 | (v & 127))
+            v >>= 7
+        out.append(v)
+    n = rd()
+    wr(n)
+    for _ in range(n):
+        wr(rd())
+        m = rd()
+        wr(m)
+        cur = 0
+        for _ in range(m):
+            clock, ln = rd(), rd()
+            wr(clock - cur)
+            wr(ln - 1)
+            cur = clock + ln
+    return bytes(out)
+
+
 def secondary(dev, eng):
     """Quick device-resident measurements of the other BASELINE.json workloads (1 GPU): C4 and V2
     merges (10k docs), C3 diffUpdate / encodeStateVectorFromUpdate (configs[2]: 4,096 V1 docs of
@@ -96,7 +131,7 @@ def secondary(dev, eng):
              ("merge_c5_v1", "merge", "c5_v1", 256), ("merge_c5_v2", "merge", "c5_v2", 256),
              ("diff_c5_v1", "diff", "c5_v1", 256), ("diff_c5_v2", "diff", "c5_v2", 256),
              ("meta_c2_v1", "meta", "c2_v1", 10000), ("meta_c2_v2", "meta", "c2_v2", 10000),
-             ("dsmerge_c4_v1", "dsmerge", "c4_v1", 10000)]
+             ("dsmerge_c4_v1", "dsmerge", "c4_v1", 10000), ("dsmerge_c4_v2", "dsmerge", "c4_v1", 10000)]
     for name, op, wl, n in cases:
         if only and name not in only.split(","):
             continue
@@ -125,6 +160,9 @@ def secondary(dev, eng):
             da, do_, dl, dst = eng.run_host("diff", 1, a, o, per, sva_, svo_)
             assert (sst == 0).all() and (dst == 0).all()
             blobs = [da[int(do_[i]) + 1:int(do_[i]) + int(dl[i])].tobytes() for i in range(len(dst))]
+            if name.endswith("v2"):  # the same delete sets in the DSEncoderV2 format
+                blobs = [_ds_v1_to_v2(x) for x in blobs]
+                fmt = 2
             docs = [[blobs[u] for u in range(int(d[t]), int(d[t + 1]))] for t in range(len(d) - 1)]
             a, o, d = replicate(*pack_docs(docs), n)
         elif wl.startswith("c5"):

@@ -120,6 +120,9 @@ __device__ __forceinline__ bool walk_structs(uint32_t u) {
 }
 // Walks the delete set of update u (DeleteSet.js:219-256) and appends its ranges (slots from misc[1]);
 // a range's payload (u << 8 | position) keeps yjs's first-appearance order.
+// V2: DSDecoderV2 (UpdateDecoder.js:258-267): clock delta-coded against the running value, which each
+// client resets; length stored as len - 1.
+template <bool V2 = false>
 __device__ __forceinline__ bool walk_ds(uint32_t u) {
   Cur c = {at<uint16_t>(L_UDS + 2 * u), at<uint16_t>(L_UOFF + 2 * u + 2), false};
   const uint32_t ndc = rvu(c);
@@ -127,9 +130,20 @@ __device__ __forceinline__ bool walk_ds(uint32_t u) {
   for (uint32_t i = 0; i < ndc && !c.bad; i++) {
     const uint32_t client = rvu(c);
     const uint32_t m = rvu(c);
+    uint64_t cur = 0;
     for (uint32_t q = 0; q < m && !c.bad; q++, pos++) {
-      const uint32_t clock = rvu(c);
-      const uint32_t len = rvu(c);
+      uint32_t clock, len;
+      if constexpr (V2) {
+        const uint64_t c64 = cur + rvu(c);
+        const uint64_t l64 = (uint64_t)rvu(c) + 1;
+        cur = c64 + l64;
+        c.bad |= (c64 >= (1u << 25)) | (l64 > 0xffffffffull);
+        clock = (uint32_t)c64;
+        len = (uint32_t)l64;
+      } else {
+        clock = rvu(c);
+        len = rvu(c);
+      }
       c.bad |= (pos > 255) | (clock >= (1u << 25));
       if (!c.bad) {
         const uint32_t x = atomicAdd(&at<uint32_t>(L_MISC + 4), 1u);
@@ -162,9 +176,10 @@ __device__ __forceinline__ bool walk_ds(uint32_t u) {
     continue;                                                           \
   }
 
-// DSONLY: PermanentUserData's delete-set merge (ym_ds_merge, V1): every input is an encoded delete set
-// (no struct section); the walk is W2 only and the output is the merged delete set alone.
-template <int STOP, int OCC, bool DSONLY = false>
+// DSONLY: PermanentUserData's delete-set merge (ym_ds_merge): every input is an encoded delete set (no
+// struct section); the walk is W2 only and the output is the merged delete set alone, in the DSEncoderV1
+// format, or DSEncoderV2's (DSV2: clocks delta-coded within a client, lengths minus one).
+template <int STOP, int OCC, bool DSONLY = false, bool DSV2 = false>
 __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
   const uint32_t lane = threadIdx.x;
   const uint64_t arena0 = j.upd_off[0];
@@ -243,7 +258,7 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
       }
       __syncthreads();
 #pragma unroll 1
-      for (uint32_t i = lane; i < n2; i += 64) ok &= walk_ds(at<uint8_t>(L_UORD2 + i));
+      for (uint32_t i = lane; i < n2; i += 64) ok &= walk_ds<DSV2>(at<uint8_t>(L_UORD2 + i));
       if (__any(!ok)) YM_DECLINE()
     }
     __syncthreads();
@@ -519,7 +534,13 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
       for (uint32_t s = 0; s < E; s++) {
         const uint32_t q = E * lane + s;
         const uint32_t c0 = q < nranges ? at<uint32_t>(L_QCLK + 4 * q) : 0;
-        qb[s] = q < nranges ? vsz(c0) + vsz(at<uint32_t>(L_QEND + 4 * q) - c0) : 0;
+        if constexpr (DSV2) {
+          const bool first = q < nranges && at<uint16_t>(L_GFIRST + 2 * at<uint8_t>(L_QGRP + q)) == q;
+          const uint32_t pe = q < nranges && !first ? at<uint32_t>(L_QEND + 4 * (q - 1)) : 0;
+          qb[s] = q < nranges ? vsz(c0 - pe) + vsz(at<uint32_t>(L_QEND + 4 * q) - c0 - 1) : 0;
+        } else {
+          qb[s] = q < nranges ? vsz(c0) + vsz(at<uint32_t>(L_QEND + 4 * q) - c0) : 0;
+        }
         t += qb[s];
       }
       const uint32_t incl = wave_incl_add(t);
@@ -603,7 +624,13 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
       if (q < nranges) {
         const uint32_t c0 = at<uint32_t>(L_QCLK + 4 * q);
         const uint32_t off = at<uint32_t>(L_GB2 + 4 * at<uint8_t>(L_QGRP + q)) + at<uint16_t>(L_QPRE + 2 * q);
-        put_vu(dst, put_vu(dst, off, c0), at<uint32_t>(L_QEND + 4 * q) - c0);
+        if constexpr (DSV2) {
+          const bool first = at<uint16_t>(L_GFIRST + 2 * at<uint8_t>(L_QGRP + q)) == q;
+          const uint32_t pe = first ? 0 : at<uint32_t>(L_QEND + 4 * (q - 1));
+          put_vu(dst, put_vu(dst, off, c0 - pe), at<uint32_t>(L_QEND + 4 * q) - c0 - 1);
+        } else {
+          put_vu(dst, put_vu(dst, off, c0), at<uint32_t>(L_QEND + 4 * q) - c0);
+        }
       }
     }
     if (lane == 0) {
@@ -625,9 +652,10 @@ __global__ void k_fast_region(GeneralJob j, uint32_t n_upd) {
 
 int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st) {
   using namespace fastv1;
-  if (op == OP_DSMERGE && !j.v2) {  // V1 delete-set merges: the same kernel, delete sets only
+  if (op == OP_DSMERGE) {  // delete-set merges: the same kernel, delete sets only
     const uint32_t grid = j.n < 131072 ? j.n : 131072;
-    k_fast_merge_v1<0, 5, true><<<grid, 64, fastv1::LDS_BYTES, st>>>(j);
+    if (j.v2) k_fast_merge_v1<0, 5, true, true><<<grid, 64, fastv1::LDS_BYTES, st>>>(j);
+    else k_fast_merge_v1<0, 5, true, false><<<grid, 64, fastv1::LDS_BYTES, st>>>(j);
     return 1;
   }
   if (op != OP_MERGE || j.v2) return 0;  // fast path: V1 merges (the C2/C4 headline configs)
