@@ -96,7 +96,8 @@ __device__ __forceinline__ uint32_t put_vu_lds(uint32_t p, uint32_t v) {
     continue;                                               \
   }
 
-// OP = OP_DIFF or OP_SV (V1 only)
+// OP = OP_DIFF, OP_SV or OP_META (parseUpdateMeta: per client section with structs, the first clock
+// (`from`) and the end of its last struct, Skips included (`to`); V1 only)
 template <int OP>
 __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
   const uint32_t lane = threadIdx.x;
@@ -147,6 +148,10 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
       const uint32_t client = rvu(c);
       uint64_t clock = rvu(c);
       if (ci > 0 && client == prev_client) { declined = true; break; }  // writer would not start a part
+      // meta: a client met again would keep its first Map position -- taken only when every section's
+      // client is below the previous one (yjs writes clients in descending order), so none repeats
+      if (OP == OP_META && ci > 0 && client > prev_client) { declined = true; break; }
+      const uint32_t first_clock = (uint32_t)clock;
       prev_client = client;
       const uint32_t k = OP == OP_DIFF ? sv_lookup(X.svt, nsv, client) : 0;
       if (OP == OP_SV && nstructs > 0 && sv_any && client != sv_client) {  // client change (os@37724)
@@ -275,6 +280,11 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
         clock += len;
       }
       if (declined || c.bad) break;
+      if (OP == OP_META && nstructs > 0) {
+        if (sv_n >= NSV) { declined = true; break; }
+        if (lane == 0) { X.svt[2 * sv_n] = client; X.svt[2 * sv_n + 1] = first_clock; X.sec[sv_n] = (uint32_t)clock; }
+        sv_n++;
+      }
       if (OP == OP_DIFF) {
         if (lane == 0) {
           sec(ci, S_B1) = copying ? rel(c.p) : 0;
@@ -286,6 +296,35 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
     }
     if (declined || c.bad) YB_DECLINE()
     __syncthreads();
+    if (OP == OP_META) {  // from then to, each vu(n) | (client, clock)*
+      __threadfence_block();
+      __syncthreads();
+      uint32_t tl = 0;
+      for (uint32_t i = lane; i < sv_n; i += 64) tl += 2 * vsz(X.svt[2 * i]) + vsz(X.svt[2 * i + 1]) + vsz(X.sec[i]);
+      const uint32_t total = 2 * vsz(sv_n) + lane_read(wave_incl_add(tl), 63);
+      uint64_t base = 0;
+      if (lane == 0) base = atomicAdd((unsigned long long *)j.used, (unsigned long long)total);
+      base = ((uint64_t)lane_read((uint32_t)(base >> 32), 0) << 32) | lane_read((uint32_t)base, 0);
+      if (base + total > j.cap) {
+        if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }
+        __syncthreads();
+        continue;
+      }
+      if (lane == 0) {
+        uint8_t *o = j.out + base;
+        uint32_t p = 0;
+        auto put = [&](uint32_t v) { while (v > 127) { o[p++] = (uint8_t)(0x80 | (v & 127)); v >>= 7; } o[p++] = (uint8_t)v; };
+        put(sv_n);
+        for (uint32_t i = 0; i < sv_n; i++) { put(X.svt[2 * i]); put(X.svt[2 * i + 1]); }
+        put(sv_n);
+        for (uint32_t i = 0; i < sv_n; i++) { put(X.svt[2 * i]); put(X.sec[i]); }
+        j.out_off[d] = base;
+        j.out_len[d] = total;
+        j.status[d] = ym::ST_OK;
+      }
+      __syncthreads();
+      continue;
+    }
     if (OP == OP_SV) {
       if (sv_any && sv_clock != 0) {
         if (sv_n >= NSV) YB_DECLINE()
@@ -421,10 +460,14 @@ __global__ void k_big_init(GeneralJob j) {
 }
 
 int big_launch(uint32_t op, const GeneralJob &j, hipStream_t st) {
-  if (j.v2 || (op != OP_DIFF && op != OP_SV)) return 0;
+  if (j.v2 || (op != OP_DIFF && op != OP_SV && op != OP_META)) return 0;
+  // meta over many small updates (e.g. every update of a batch): one thread per update on the general
+  // path beats a grid of BS_GRID waves walking hundreds of tiny updates each (1 M C2 updates: 2.5 vs 12 ms)
+  if (op == OP_META && j.n > 8 * BS_GRID) return 0;
   k_big_init<<<1, 64, 0, st>>>(j);
   const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
   if (op == OP_DIFF) big::k_big_v1<OP_DIFF><<<grid, 64, big::LDS_BYTES, st>>>(j);
+  else if (op == OP_META) big::k_big_v1<OP_META><<<grid, 64, big::LDS_BYTES, st>>>(j);
   else big::k_big_v1<OP_SV><<<grid, 64, big::LDS_BYTES, st>>>(j);
   return 1;
 }
