@@ -116,7 +116,7 @@ def _ds_v1_to_v2(b):
 def secondary(dev, eng):
     """Quick device-resident measurements of the other BASELINE.json workloads (1 GPU): C4 and V2
     merges (10k docs), C3 diffUpdate / encodeStateVectorFromUpdate (configs[2]: 4,096 V1 docs of
-    0.9 MB; 1,024 V2 docs) against random state vectors, C5 (configs[4]: 256 docs of ~16 k updates
+    0.9 MB V1 and 0.47 MB V2) against random state vectors, C5 (configs[4]: 256 docs of ~16 k updates
     from 1,024 clients) mergeUpdates[V2] and diffUpdate[V2] of the merged documents against random
     per-client state vectors, parseUpdateMeta over the ~1 M C2 updates, PermanentUserData's
     delete-set merge over the C4 updates' delete sets.  Whole-call GB/s of input."""
@@ -127,7 +127,7 @@ def secondary(dev, eng):
     only = os.environ.get("YM_SECONDARY")  # comma-separated subset of the case names
     cases = [("merge_c4_v1", "merge", "c4_v1", 10000), ("merge_c2_v2", "merge", "c2_v2", 10000),
              ("merge_c4_v2", "merge", "c4_v2", 10000), ("diff_c3_v1", "diff", "c3_v1", 4096),
-             ("sv_c3_v1", "sv", "c3_v1", 4096), ("diff_c3_v2", "diff", "c3_v2", 1024),
+             ("sv_c3_v1", "sv", "c3_v1", 4096), ("diff_c3_v2", "diff", "c3_v2", 4096),
              ("merge_c5_v1", "merge", "c5_v1", 256), ("merge_c5_v2", "merge", "c5_v2", 256),
              ("diff_c5_v1", "diff", "c5_v1", 256), ("diff_c5_v2", "diff", "c5_v2", 256),
              ("meta_c2_v1", "meta", "c2_v1", 10000), ("meta_c2_v2", "meta", "c2_v2", 10000),

@@ -291,7 +291,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   j.n = nd;
   const uint64_t seq = ++S->seq;
   if (op == OP_DIFF || op == OP_SV || op == OP_META) {  // per-block scratch of the streamed walkers
-    if (S->bscratch.ensure(BS_GRID * BS_BYTES)) return -2;
+    if (S->bscratch.ensure((uint64_t)(nd < BS_GRID ? nd : BS_GRID) * BS_BYTES)) return -2;
     j.bscratch = S->bscratch.as<uint8_t>();
   }
 
