@@ -410,8 +410,8 @@ __device__ __forceinline__ uint32_t col_encode(Get get, uint32_t n, bool wr, O o
     __syncthreads();                                                    \
     continue;                                                           \
   }
-template <int STOP>
-__global__ void __launch_bounds__(64) k_fast_merge_v2(GeneralJob j) {
+template <int STOP, int OCC = 1>
+__global__ void __launch_bounds__(64, OCC) k_fast_merge_v2(GeneralJob j) {
   const uint32_t lane = threadIdx.x;
   const uint64_t arena0 = j.upd_off[0];
   for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
@@ -944,8 +944,15 @@ int fast2_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t s
   if (op != OP_MERGE || !j.v2) return 0;
   (void)n_upd;
   const uint32_t grid = j.n < 131072 ? j.n : 131072;
-  static int stop = -1;
+  static int stop = -1, occ = -1;
   if (stop < 0) { const char *e = getenv("YMERGE_FAST_STOP"); stop = e ? atoi(e) : 0; }
+  if (occ < 0) { const char *e = getenv("YMERGE_FAST2_OCC"); occ = e ? atoi(e) : 3; }  // min waves / SIMD (3: 168 VGPRs, no spills)
+  if (stop == 0 && occ >= 2) {
+    if (occ == 2) fastv2::k_fast_merge_v2<0, 2><<<grid, 64, fastv2::LDS_BYTES, st>>>(j);
+    else if (occ == 3) fastv2::k_fast_merge_v2<0, 3><<<grid, 64, fastv2::LDS_BYTES, st>>>(j);
+    else fastv2::k_fast_merge_v2<0, 4><<<grid, 64, fastv2::LDS_BYTES, st>>>(j);
+    return 1;
+  }
   switch (stop) {
 #define YM2_L(S) case S: fastv2::k_fast_merge_v2<S><<<grid, 64, fastv2::LDS_BYTES, st>>>(j); break;
     YM2_L(1) YM2_L(2) YM2_L(3) YM2_L(4) YM2_L(5) YM2_L(6) YM2_L(7)
