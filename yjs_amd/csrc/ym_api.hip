@@ -107,13 +107,16 @@ __global__ void k_status_flags(const uint32_t *list, uint32_t n, const int32_t *
 // out_len with 16 independent loads per thread (one HBM round trip), partial sums by atomics, and the
 // block that finishes last writes the host words (a handful of same-address atomics, not one per doc).
 // Counters: [0] used, [2] declined (u32), [8] finished blocks (u32), [9] errors, [10] bytes out.
-constexpr uint32_t FIN_DOCS = 4096, FIN_THREADS = 256;
+// FIN_THREADS threads per block, 16 documents per thread: one 1,024-thread block up to 16 k documents (no
+// cross-block atomics), 256-thread blocks of 4,096 documents above that
+template <uint32_t FIN_THREADS>
 __global__ void __launch_bounds__(FIN_THREADS) k_finish(const int32_t *status, const uint64_t *out_len, uint32_t n,
                                                         const uint64_t *upd_off, uint32_t n_upd, uint64_t *counters,
                                                         volatile uint64_t *host, int stats, int merge, uint64_t seq) {
   __shared__ unsigned long long red[2][FIN_THREADS / 64];
   unsigned long long *c = reinterpret_cast<unsigned long long *>(counters);
   uint64_t err = 0, bytes = 0;
+  constexpr uint32_t FIN_DOCS = 16 * FIN_THREADS;
   const uint32_t i0 = blockIdx.x * FIN_DOCS;
   if (stats) {
     int32_t sv[16];
@@ -300,8 +303,13 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   bool slots = false;  // the fast paths wrote their outputs into the slot region (merges, delete-set merges)
   // ends a round trip: counters and stats land in pinned host memory, then one stream sync
   auto finish = [&]() -> int {
-    const uint32_t fin_blocks = stats ? (nd + FIN_DOCS - 1) / FIN_DOCS : 1;
-    k_finish<<<fin_blocks, FIN_THREADS, 0, st>>>(o_status, o_len, nd, upd_off, b->n_upd, counters, S->pinned_dev,
+    const bool one = !stats || nd <= 16 * 1024;
+    const uint32_t fin_blocks = one ? 1 : (nd + 4095) / 4096;
+    if (one)
+      k_finish<1024><<<1, 1024, 0, st>>>(o_status, o_len, nd, upd_off, b->n_upd, counters, S->pinned_dev,
+                                        stats ? 1 : 0, slots ? 1 : 0, seq);
+    else
+      k_finish<256><<<fin_blocks, 256, 0, st>>>(o_status, o_len, nd, upd_off, b->n_upd, counters, S->pinned_dev,
                                                  stats ? 1 : 0, slots ? 1 : 0, seq);
     HIPCHK(hipEventRecord(S->ev1, st));
     // spin on the completion word k_finish writes last (no interrupt wake-up of a blocking wait), then
