@@ -131,7 +131,7 @@ def secondary(dev, eng):
              ("merge_c5_v1", "merge", "c5_v1", 256), ("merge_c5_v2", "merge", "c5_v2", 256),
              ("diff_c5_v1", "diff", "c5_v1", 256), ("diff_c5_v2", "diff", "c5_v2", 256),
              ("meta_c2_v1", "meta", "c2_v1", 10000), ("meta_c2_v2", "meta", "c2_v2", 10000),
-             ("meta_c3_v1", "meta", "c3_v1", 4096),
+             ("meta_c3_v1", "meta", "c3_v1", 4096), ("meta_c3_v2", "meta", "c3_v2", 4096),
              ("dsmerge_c4_v1", "dsmerge", "c4_v1", 10000), ("dsmerge_c4_v2", "dsmerge", "c4_v1", 10000)]
     for name, op, wl, n in cases:
         if only and name not in only.split(","):

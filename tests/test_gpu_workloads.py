@@ -293,8 +293,8 @@ def test_meta_workloads_match_oracle(engine, fmt):
         assert (st == 0).all()
         bad = _compare(engine.run_host("meta", fmt, a2, o2, d2), outs, st)
         assert not bad, (name, bad[:10])
-        if fmt == 1:  # the streamed V1 walker (ym_big.hip, meta mode) takes every merged document
-            assert engine.stats["docs_fast"] == engine.stats["docs"], engine.stats
+        # the streamed walkers (ym_big.hip / ym_big2.hip, meta mode) take every merged document
+        assert engine.stats["docs_fast"] == engine.stats["docs"], engine.stats
 
 
 def _encode_ds(clients, v2):

@@ -184,6 +184,8 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
           }
           if (skip) sv_stop = true;
           if (!sv_stop) sv_clock = (uint32_t)(clock + len);
+        } else if (OP == OP_META) {
+          // parseUpdateMeta only measures the section: nothing is cut or copied
         } else if (!copying) {
           if (!skip && clock + len > k) {  // the cut: first struct that ends past sv[client]
             copying = true;

@@ -498,7 +498,10 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
       const uint32_t client = uopt_read(D, I_CL);
       uint64_t clock = s_vu(D, I_REST);
       if (ci > 0 && client == prev_client) { set_bad(); break; }
+      // meta (parseUpdateMeta): clients strictly descending (as yjs writes them), so none repeats
+      if (OP == OP_META && ci > 0 && client > prev_client) { set_bad(); break; }
       prev_client = client;
+      const uint32_t first_clock = (uint32_t)clock;
       const uint32_t k = OP == OP_DIFF ? sv_lookup(X.svt, nsv, client) : 0;
       if (OP == OP_SV && nstructs > 0 && sv_any && client != sv_client) {
         if (sv_clock != 0) {
@@ -520,6 +523,8 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
           if (!sv_any) { sv_any = true; sv_client = client; sv_stop = clock != 0; sv_clock = sv_stop ? 0 : (uint32_t)(clock + len); }
           if (info == 10) sv_stop = true;
           if (!sv_stop) sv_clock = (uint32_t)(clock + len);
+        } else if (OP == OP_META) {
+          // parseUpdateMeta only measures the section: nothing is cut or written
         } else if (copying) {
           written++;
           v2_write(D, r, 0, client, (uint32_t)clock, sb0);
@@ -534,6 +539,11 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
         }
         clock += len;
       }
+      if (OP == OP_META && nstructs > 0 && !is_bad()) {  // from = first clock, to = end of the last struct
+        if (sv_n >= NSV) { set_bad(); break; }
+        if (lane == 0) { X.svt[2 * sv_n] = client; X.svt[2 * sv_n + 1] = first_clock; X.part[sv_n] = (uint32_t)clock; }
+        sv_n++;
+      }
       if (OP == OP_DIFF && copying) {
         if (nparts >= NSEC) { set_bad(); break; }
         if (lane == 0) {
@@ -546,6 +556,35 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
       }
     }
     if (is_bad()) YB2_DECLINE()
+    if (OP == OP_META) {  // from then to, each vu(n) | (client, clock)*
+      __threadfence_block();
+      __syncthreads();
+      uint32_t tl = 0;
+      for (uint32_t i = lane; i < sv_n; i += 64) tl += 2 * vsz(X.svt[2 * i]) + vsz(X.svt[2 * i + 1]) + vsz(X.part[i]);
+      const uint32_t total = 2 * vsz(sv_n) + lane_read(wave_incl_add(tl), 63);
+      uint64_t base = 0;
+      if (lane == 0) base = atomicAdd((unsigned long long *)j.used, (unsigned long long)total);
+      base = ((uint64_t)lane_read((uint32_t)(base >> 32), 0) << 32) | lane_read((uint32_t)base, 0);
+      if (base + total > j.cap) {
+        if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }
+        __syncthreads();
+        continue;
+      }
+      if (lane == 0) {
+        uint8_t *o = j.out + base;
+        uint32_t p = 0;
+        auto put = [&](uint32_t v) { while (v > 127) { o[p++] = (uint8_t)(0x80 | (v & 127)); v >>= 7; } o[p++] = (uint8_t)v; };
+        put(sv_n);
+        for (uint32_t i = 0; i < sv_n; i++) { put(X.svt[2 * i]); put(X.svt[2 * i + 1]); }
+        put(sv_n);
+        for (uint32_t i = 0; i < sv_n; i++) { put(X.svt[2 * i]); put(X.part[i]); }
+        j.out_off[d] = base;
+        j.out_len[d] = total;
+        j.status[d] = ym::ST_OK;
+      }
+      __syncthreads();
+      continue;
+    }
     if (OP == OP_SV) {
       if (sv_any && sv_clock != 0) {
         if (sv_n >= NSV) YB2_DECLINE()
@@ -690,10 +729,12 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
 
 __global__ void k_big_init(GeneralJob j);  // ym_big.hip
 int big2_launch(uint32_t op, const GeneralJob &j, hipStream_t st) {
-  if (!j.v2 || (op != OP_SV && op != OP_DIFF)) return 0;
+  if (!j.v2 || (op != OP_SV && op != OP_DIFF && op != OP_META)) return 0;
+  if (op == OP_META && j.n > 8 * BS_GRID) return 0;  // many small updates: one thread per update (general)
   k_big_init<<<1, 64, 0, st>>>(j);
   const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
   if (op == OP_DIFF) big2::k_big_v2<OP_DIFF><<<grid, 64, big2::LDS_BYTES, st>>>(j);
+  else if (op == OP_META) big2::k_big_v2<OP_META><<<grid, 64, big2::LDS_BYTES, st>>>(j);
   else big2::k_big_v2<OP_SV><<<grid, 64, big2::LDS_BYTES, st>>>(j);
   return 1;
 }
