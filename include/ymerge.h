@@ -20,9 +20,10 @@
  * arena[upd_off[u] .. upd_off[u+1]).  For ym_diff, doc d's state vector is
  * sv_arena[sv_off[d] .. sv_off[d+1]) and doc d must own exactly one update.
  *
- * Results: out_off[d] / out_len[d] locate doc d's output inside out_arena (16-byte aligned slots,
- * not necessarily contiguous or in document order); status[d] is a YM_* code.  A doc whose status
- * is not YM_OK has out_len[d] = 0.  Errors are per document; the batch always completes.
+ * Results: out_off[d] / out_len[d] locate doc d's output inside out_arena (device batches: 16-byte
+ * aligned slots, not necessarily contiguous or in document order; host batches: packed back to back in
+ * document order); status[d] is a YM_* code.  A doc whose status is not YM_OK has out_len[d] = 0.
+ * Errors are per document; the batch always completes.
  * ym_out_bound() gives a capacity that normally suffices; out->used reports what was needed.
  */
 #ifndef YMERGE_H

@@ -59,3 +59,12 @@ for _ in range(300):
     x.add_(1)
     torch.cuda.synchronize()
 print(f"torch tiny op + sync {(time.perf_counter() - t) / 300 * 1e6:8.1f} us", flush=True)
+# PCIe-inclusive rate: the same batch from host memory (ym_merge with YM_MEM_HOST: H2D of the arena and
+# offsets, the kernels, D2H of the outputs) through Engine.run_host
+for _ in range(3):
+    eng.run_host("merge", fmt, a, o, d)
+t = time.perf_counter()
+for _ in range(20):
+    eng.run_host("merge", fmt, a, o, d)
+el = (time.perf_counter() - t) / 20
+print(f"host batch (PCIe-inclusive) {el * 1e3:8.3f} ms/call = {int(o[-1]) / el / 1e9:6.2f} GB/s of input", flush=True)

@@ -58,6 +58,7 @@ struct DevState {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evf0 = nullptr, evf1 = nullptr, evg1 = nullptr;
   DBuf ws, ws_size, ws_off, layout, counters, scan_tmp, list_a, list_b, flags, bscratch;
   DBuf in_arena, in_off, in_doc, in_sv, in_svoff, out_arena, out_off, out_len, status;  // host staging
+  DBuf cmp_off, cmp_len, cmp_arena;  // host batches: outputs packed in document order before the D2H copy
   LargeBufs large;
   hipEvent_t evl1 = nullptr;
   uint64_t *pinned = nullptr;   // host memory the finishing kernel writes into (no copy op)
@@ -92,6 +93,24 @@ DevState *state() {
     hipHostGetDevicePointer((void **)&g_state->pinned_dev, g_state->pinned, 0);
   }
   return g_state;
+}
+
+// host batches: document d's output moves to the packed offset cmp_off[d] (exclusive scan of out_len),
+// so the device-to-host copy carries the outputs only, not the fast paths' sparse slot region
+__global__ void __launch_bounds__(64) k_pack(const uint8_t *src, const uint64_t *off, const uint64_t *len,
+                                             const uint64_t *cmp_off, uint8_t *dst, uint32_t n) {
+  for (uint32_t d = blockIdx.x; d < n; d += gridDim.x) {
+    const uint8_t *s = src + off[d];
+    uint8_t *o = dst + cmp_off[d];
+    const uint64_t m = len[d];
+    for (uint64_t b = threadIdx.x; b < m; b += 64) o[b] = s[b];
+  }
+}
+
+// packed lengths: a document that is not OK contributes nothing (its out_len is reported as 0)
+__global__ void k_mask_len(const int32_t *status, const uint64_t *len, uint64_t *mlen, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) mlen[i] = status[i] == 0 ? len[i] : 0;
 }
 
 __global__ void k_status_flags(const uint32_t *list, uint32_t n, const int32_t *status, int want, uint8_t *flags) {
@@ -241,8 +260,14 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   uint64_t *o_off = out->out_off, *o_len = out->out_len;
   int32_t *o_status = out->status;
   bool host = b->mem == YM_MEM_HOST;
+  // device output capacity: the caller's (device batches); for host batches the library's own staging,
+  // at least the internal bound (the caller's buffer only receives the packed outputs)
+  uint64_t dev_cap = out->cap;
   if (host) {  // stage inputs
     uint64_t abytes = upd_off[b->n_upd];
+    const uint64_t svb = op == OP_DIFF ? sv_off[nd] : 0;
+    const uint64_t bound = 4 * abytes + 2 * svb + 128ull * nd + 8192;
+    dev_cap = out->cap > bound ? out->cap : bound;
     if (S->in_arena.ensure(abytes + 16) || S->in_off.ensure((b->n_upd + 1) * 8ull) || S->in_doc.ensure((nd + 1) * 4ull)) return -2;
     HIPCHK(hipMemcpyAsync(S->in_arena.p, A, abytes, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(S->in_off.p, upd_off, (b->n_upd + 1) * 8ull, hipMemcpyHostToDevice, st));
@@ -258,7 +283,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
       svp = S->in_sv.as<uint8_t>();
       sv_off = S->in_svoff.as<uint64_t>();
     }
-    if (S->out_arena.ensure(out->cap + 16) || S->out_off.ensure(nd * 8ull) || S->out_len.ensure(nd * 8ull) ||
+    if (S->out_arena.ensure(dev_cap + 16) || S->out_off.ensure(nd * 8ull) || S->out_len.ensure(nd * 8ull) ||
         S->status.ensure(nd * 4ull))
       return -2;
     o_arena = S->out_arena.as<uint8_t>();
@@ -284,7 +309,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   j.layout = S->layout.as<ym::Layout>();
   j.status = o_status;
   j.out = o_arena;
-  j.cap = out->cap;
+  j.cap = dev_cap;
   j.out_off = o_off;
   j.out_len = o_len;
   j.used = counters + 0;
@@ -303,14 +328,15 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   bool slots = false;  // the fast paths wrote their outputs into the slot region (merges, delete-set merges)
   // ends a round trip: counters and stats land in pinned host memory, then one stream sync
   auto finish = [&]() -> int {
-    const bool one = !stats || nd <= 16 * 1024;
+    const bool want = stats || host;  // host batches need the bytes out (the packed size)
+    const bool one = !want || nd <= 16 * 1024;
     const uint32_t fin_blocks = one ? 1 : (nd + 4095) / 4096;
     if (one)
       k_finish<1024><<<1, 1024, 0, st>>>(o_status, o_len, nd, upd_off, b->n_upd, counters, S->pinned_dev,
-                                        stats ? 1 : 0, slots ? 1 : 0, seq);
+                                        want ? 1 : 0, slots ? 1 : 0, seq);
     else
       k_finish<256><<<fin_blocks, 256, 0, st>>>(o_status, o_len, nd, upd_off, b->n_upd, counters, S->pinned_dev,
-                                                 stats ? 1 : 0, slots ? 1 : 0, seq);
+                                                 want ? 1 : 0, slots ? 1 : 0, seq);
     HIPCHK(hipEventRecord(S->ev1, st));
     // spin on the completion word k_finish writes last (no interrupt wake-up of a blocking wait), then
     // the stream sync, which finds the stream drained: it is what orders every result for the host
@@ -393,14 +419,29 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
     stats->bytes_out = S->pinned[5];
     stats->bytes_in = S->pinned[6];
   }
-  if (used > out->cap) return YM_ERR_CAPACITY;
-  if (host) {
-    HIPCHK(hipMemcpyAsync(out->arena, o_arena, used, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(out->out_off, o_off, nd * 8ull, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(out->out_len, o_len, nd * 8ull, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(out->status, o_status, nd * 4ull, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+  if (!host) return used > out->cap ? YM_ERR_CAPACITY : 0;
+  // host batch: pack the outputs in document order (out_off[d] = bytes of the outputs before d), then
+  // copy only them back.  A staging overflow reports the staging need (the caller's retry grows both).
+  if (used > dev_cap) return YM_ERR_CAPACITY;
+  const uint64_t total = S->pinned[5];
+  out->used = total;
+  if (total > out->cap) return YM_ERR_CAPACITY;
+  {
+    size_t tmp = 0;
+    if (S->cmp_off.ensure(nd * 8ull + 8) || S->cmp_len.ensure(nd * 8ull + 8) || S->cmp_arena.ensure(total + 16)) return -2;
+    uint64_t *mlen = S->cmp_len.as<uint64_t>();
+    k_mask_len<<<(nd + 255) / 256, 256, 0, st>>>(o_status, o_len, mlen, nd);
+    hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, mlen, (uint64_t *)nullptr, nd, st);
+    if (S->scan_tmp.ensure(tmp + 16)) return -2;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(S->scan_tmp.p, tmp, mlen, S->cmp_off.as<uint64_t>(), nd, st));
+    const uint32_t grid = nd < 65536 ? nd : 65536;
+    k_pack<<<grid, 64, 0, st>>>(o_arena, o_off, mlen, S->cmp_off.as<uint64_t>(), S->cmp_arena.as<uint8_t>(), nd);
   }
+  if (total) HIPCHK(hipMemcpyAsync(out->arena, S->cmp_arena.p, total, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(out->out_off, S->cmp_off.p, nd * 8ull, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(out->out_len, S->cmp_len.p, nd * 8ull, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(out->status, o_status, nd * 4ull, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
   return 0;
 }
 
@@ -423,7 +464,7 @@ int ym_shutdown(void) {
   hipStreamSynchronize(S->stream);
   DBuf *bufs[] = {&S->ws, &S->ws_size, &S->ws_off, &S->layout, &S->counters, &S->scan_tmp, &S->list_a, &S->list_b,
                   &S->flags, &S->bscratch, &S->in_arena, &S->in_off, &S->in_doc, &S->in_sv, &S->in_svoff, &S->out_arena,
-                  &S->out_off, &S->out_len, &S->status};
+                  &S->out_off, &S->out_len, &S->status, &S->cmp_off, &S->cmp_len, &S->cmp_arena};
   for (DBuf *b : bufs) if (b->p) hipFree(b->p);
   if (S->pinned) hipHostFree(S->pinned);
   if (S->ev0) hipEventDestroy(S->ev0);
@@ -457,7 +498,13 @@ const char *ym_strerror(int code) {
 }
 
 uint64_t ym_out_bound(const ym_batch *b) {
-  // fast-path slot region (2 * in + 64 per doc) followed by room for general-path outputs
+  // device batches: the fast-path slot region (2 * in + 64 per doc) followed by room for general-path
+  // outputs; host batches: the packed outputs only (the library stages the slot region itself)
+  if (b->mem == YM_MEM_HOST && b->upd_off) {
+    const uint64_t in_h = b->upd_off[b->n_upd] - b->upd_off[0];
+    const uint64_t sv_h = b->sv_off ? b->sv_off[b->n_docs] - b->sv_off[0] : 0;
+    return 2 * in_h + 2 * sv_h + 64ull * b->n_docs + 8192;
+  }
   uint64_t in = 0;
   if (b->mem == YM_MEM_HOST && b->upd_off) in = b->upd_off[b->n_upd] - b->upd_off[0];
   else in = (uint64_t)b->n_upd * 64;
