@@ -345,6 +345,16 @@ def main():
                          "traffic": traffic, "avg_launch_ms": round(avg_fast, 5),
                          "algorithmic_bytes_per_launch": int(alg_bytes)},
         }
+        if world == 1:
+            # PCIe-inclusive rate of the same batch from pageable host memory (what the Node addon
+            # hands over): H2D of arena + offsets, the kernels, D2H of the packed outputs.  Not `value`.
+            eng.run_host("merge", fmt, arena, upd_off, doc_upd)
+            th = time.perf_counter()
+            for _ in range(5):
+                eng.run_host("merge", fmt, arena, upd_off, doc_upd)
+            th = (time.perf_counter() - th) / 5
+            line["pcie_inclusive"] = {"value": round(in_bytes / th / 1e9, 3), "unit": "GB/s",
+                                      "ms_per_call": round(th * 1e3, 3), "source": "pageable host buffers"}
         if not args.no_cpu_baseline and world == 1:  # the host baseline is reported at N = 1 only
             line["cpu_baseline"] = cpu_baseline(arena, upd_off, doc_upd, fmt, args.cpu_baseline_seconds)
         if not args.no_secondary and world == 1:
