@@ -137,6 +137,16 @@ __global__ void __launch_bounds__(FIN_THREADS) k_finish(const int32_t *status, c
   uint64_t err = 0, bytes = 0;
   constexpr uint32_t FIN_DOCS = 16 * FIN_THREADS;
   const uint32_t i0 = blockIdx.x * FIN_DOCS;
+  // the host words' inputs (written by earlier kernels, never by k_finish) are loaded first, so their
+  // HBM / L2 round trips overlap the stats loads instead of following the reduction one by one
+  uint64_t used = 0, in_lo = 0, in_hi = 0;
+  uint32_t declined = 0;
+  if (threadIdx.x == 0) {
+    used = __hip_atomic_load(&c[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    declined = __hip_atomic_load(reinterpret_cast<uint32_t *>(&c[2]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    in_lo = upd_off[0];
+    in_hi = upd_off[n_upd];
+  }
   if (stats) {
     int32_t sv[16];
     uint64_t lv[16];
@@ -173,13 +183,12 @@ __global__ void __launch_bounds__(FIN_THREADS) k_finish(const int32_t *status, c
     b = atomicAdd(&c[10], 0ull);
   }
   // used: the bump allocator; merges also own the fast / large paths' slot region [0, 2 in + 64 n + 64)
-  const uint64_t region = merge ? 2 * (upd_off[n_upd] - upd_off[0]) + 64ull * n + 64 : 0;
-  const uint64_t used = atomicAdd(&c[0], 0ull);
+  const uint64_t region = merge ? 2 * (in_hi - in_lo) + 64ull * n + 64 : 0;
   host[0] = used > region ? used : region;
-  host[2] = atomicAdd(reinterpret_cast<uint32_t *>(&c[2]), 0u);  // declined documents (the work list length)
+  host[2] = declined;  // declined documents (the work list length)
   host[4] = e;
   host[5] = b;
-  host[6] = upd_off[n_upd] - upd_off[0];
+  host[6] = in_hi - in_lo;
   c[0] = 0;                                     // used := 0, pend_count := 0 and the finish counters:
   reinterpret_cast<uint32_t *>(c)[4] = 0;       // the next launch starts clean (see run_op for the
   c[8] = 0;                                     // general path)
