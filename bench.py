@@ -35,6 +35,7 @@ WORKLOADS = {
     "c5": ("c5_v1", 1, "C5: Y.XmlFragment docs, 1,024 clients x 16 tx (~16 k updates), mergeUpdates V1"),
     "c5v2": ("c5_v2", 2, "C5: Y.XmlFragment docs, 1,024 clients x 16 tx (~16 k updates), mergeUpdatesV2"),
 }
+PARTITION = {"c2": "hash", "c2v2": "hash", "c4": "hash", "c5": "bytes", "c5v2": "bytes"}
 
 
 def parse():
@@ -46,6 +47,11 @@ def parse():
     p.add_argument("--docs-per-gpu", type=int, default=10000)
     p.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--partition", default="auto", choices=["auto", "hash", "bytes"],
+                   help="document -> rank assignment: hash32(docIndex) % N, or greedy byte balance "
+                        "(auto: hash for the small-document workloads, bytes for C3 / C5)")
+    p.add_argument("--cpu-stub", action="store_true",
+                   help="gloo on CPU with a copy standing in for the merge (tests of the launcher only)")
     p.add_argument("--no-secondary", action="store_true",
                    help="skip the secondary workload lines (C4/C2-V2/C4-V2 merges, C3 diff/sv)")
     return p.parse_args()
@@ -56,7 +62,7 @@ def cpu_baseline(arena, upd_off, doc_upd, fmt, seconds):
     this process's CPU share, repeated until `seconds` of wall time."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ref  # test infrastructure: only the cpu_baseline leg may load it
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_cores()
     n_docs = len(doc_upd) - 1
     reps, t0 = 0, time.perf_counter()
     while True:
@@ -71,6 +77,7 @@ def cpu_baseline(arena, upd_off, doc_upd, fmt, seconds):
         "unit": "GB/s",
         "docs_per_s": round(n_docs * reps / el, 1),
         "cores": threads,
+        "host_cpu_count": os.cpu_count(),
         "kind": "port",
         "sample": f"{reps} x {n_docs} docs ({bytes_in / reps / 1e6:.1f} MB input each) in {el:.1f} s, "
                   f"oracle/ymerge_oracle.c (literal yjs 13.5.16 mergeUpdates), {threads} threads",
@@ -222,39 +229,111 @@ def _sv_of_single_client_update(upd, fmt):
     return (encodeStateVectorFromUpdateV2 if fmt == 2 else encodeStateVectorFromUpdate)(upd)
 
 
+def host_cores():
+    """Cores this process may use: the CPU affinity set, capped by a cgroup CPU quota when one is set
+    (on the GPU box os.cpu_count() reports the whole machine, not this job's share)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(-(-int(q) // int(per)))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def launch(args):
+    """--gpus N without an external launcher: start N rank processes (this script, RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* in their environment) before anything here touches a GPU, wait for all of them
+    and return the first failing exit code.  Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in pending:  # one rank failed: the others would wait in a collective forever
+                    q.kill()
+        time.sleep(0.05)
+    return rc
+
+
+class StubEngine:
+    """--cpu-stub: the launcher / sharding / reduce path without a GPU (gloo on CPU tensors).  The "op"
+    copies each rank's arena into its output arena; it stands in for ym_merge only in the multi-rank CPU
+    test of this script's own plumbing (tests/test_bench_launch.py)."""
+
+    last_stats = type("S", (), {"fast_ms": 0.0, "large_ms": 0.0, "device_ms": 0.0})()
+    stats = {"docs_fast": 0, "docs_general": 0, "docs_large": 0}
+
+    def prepare_device(self, op, fmt, g_arena, g_off, g_doc, o_arena, o_off, o_len, o_st, stream=None):
+        n = g_arena.numel()
+        nd = g_doc.numel() - 1
+        lens = g_off[g_doc[1:].long()] - g_off[g_doc[:-1].long()]
+
+        def call():
+            o_arena[:n].copy_(g_arena)
+            o_len.copy_(lens)
+            o_st.zero_()
+            return 0, n
+        self.stats = {"docs_fast": nd, "docs_general": 0, "docs_large": 0}
+        return call
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+    stub = args.cpu_stub
+    if stub:
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+    else:
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        if world > 1:
+            dist.init_process_group("nccl", device_id=dev)
 
-    from yjs_amd import Engine
-    from yjs_amd.workloads import load_ymb, replicate
+    from yjs_amd.distributed import weak_scaling_shard
+    from yjs_amd.workloads import load_ymb
 
     tname, fmt, desc = WORKLOADS[args.workload]
+    how = args.partition if args.partition != "auto" else PARTITION[args.workload]
     t_arena, t_off, t_doc = load_ymb(tname)
-    T = len(t_doc) - 1
-    # rank r processes global docs [r*D, (r+1)*D), doc g = template g % T (rotated per rank)
-    rot = (rank * args.docs_per_gpu) % T
-    if rot:
-        order = list(range(rot, T)) + list(range(rot))
-        docs = [[bytes(t_arena[int(t_off[u]):int(t_off[u + 1])]) for u in range(int(t_doc[d]), int(t_doc[d + 1]))]
-                for d in order]
-        from yjs_amd import pack_docs
-        t_arena, t_off, t_doc = pack_docs(docs)
-    arena, upd_off, doc_upd = replicate(t_arena, t_off, t_doc, args.docs_per_gpu)
+    # the job: world * docs_per_gpu documents (weak scaling), global doc g = a distinct copy of template
+    # g % T, partitioned over the ranks by hash32(g) % world or greedy byte balance
+    arena, upd_off, doc_upd, doc_ids = weak_scaling_shard(t_arena, t_off, t_doc, args.docs_per_gpu, world, rank, how)
     n_docs = len(doc_upd) - 1
     in_bytes = int(upd_off[-1])
 
-    eng = Engine(local)
+    if stub:
+        eng = StubEngine()
+    else:
+        from yjs_amd import Engine
+        eng = Engine(local)
     g_arena = torch.from_numpy(arena).to(dev)
     g_off = torch.from_numpy(upd_off.view(np.int64)).to(dev)
     g_doc = torch.from_numpy(doc_upd.view(np.int32)).to(dev)
@@ -263,7 +342,11 @@ def main():
     o_off = torch.empty(n_docs, dtype=torch.int64, device=dev)
     o_len = torch.empty(n_docs, dtype=torch.int64, device=dev)
     o_st = torch.empty(n_docs, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    stream = None if stub else torch.cuda.current_stream(dev)
+
+    def sync():
+        if not stub:
+            torch.cuda.synchronize(dev)
 
     call = eng.prepare_device("merge", fmt, g_arena, g_off, g_doc, o_arena, o_off, o_len, o_st, stream=stream)
 
@@ -275,14 +358,14 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
+    sync()
     errors = int((o_st != 0).sum().item())
-    st0 = eng.stats
-    out_bytes = int(o_len.sum().item())
+    st0 = dict(eng.stats)
+    out_bytes = int(o_len[o_st == 0].sum().item())
 
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     fast_ms, dev_ms = [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -290,16 +373,16 @@ def main():
         s = eng.last_stats
         fast_ms.append(s.fast_ms + s.large_ms)  # LDS fast path, or the large-document pipeline (C5)
         dev_ms.append(s.device_ms)
-    torch.cuda.synchronize(dev)
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
     # the only collectives: max of the timed region, sum of per-rank counters (RCCL over xGMI)
     from yjs_amd.distributed import reduce_run
-    elapsed, (in_all, out_all, docs_all, err_all, fast_all, gen_all) = reduce_run(
+    elapsed, (in_all, out_all, docs_all, err_all, fast_all, gen_all, upd_all) = reduce_run(
         dist if world > 1 else None, elapsed,
-        [in_bytes, out_bytes, n_docs, errors, st0["docs_fast"], st0["docs_general"]], device=dev)
+        [in_bytes, out_bytes, n_docs, errors, st0["docs_fast"], st0["docs_general"], int(doc_upd[-1])], device=dev)
 
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
@@ -312,11 +395,12 @@ def main():
         if st0["docs_large"]:
             kernel_name = "large-document pipeline (ym_large.hip: walk, segmented sorts, k_lm_doc)"
         achieved = alg_bytes / (avg_fast * 1e-3) / 1e9 if avg_fast > 0 else 0.0
-        traffic = None
+        traffic, traffic_src = None, None
         pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
-        if os.path.exists(pmc):
+        if os.path.exists(pmc) and args.docs_per_gpu == 10000 and world == 1:
             try:
-                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+                j = json.load(open(pmc))
+                traffic, traffic_src = j.get("hbm_bytes_per_launch"), j.get("source")
             except Exception:
                 traffic = None
         line = {
@@ -333,19 +417,23 @@ def main():
             "dtype": "u8",
             "data": f"synthetic: yjs 13.5.16-generated {tname} document templates (bench_data/, recipe "
                     "oracle/gen/make_bench_data.cjs) replicated to docs_per_gpu distinct copies per rank",
-            "config": {"workload": desc, "docs_per_gpu": n_docs, "updates_per_gpu": int(doc_upd[-1]),
-                       "input_bytes_per_gpu": in_bytes, "output_bytes_per_gpu": out_bytes, "format": f"v{fmt}",
-                       "parallelism": f"docs sharded over {world} GPU(s), no collective in the hot path"},
+            "config": {"workload": desc, "docs_total": int(docs_all), "docs_per_gpu": args.docs_per_gpu,
+                       "docs_rank0": n_docs, "updates_total": int(upd_all), "input_bytes_total": int(in_all),
+                       "output_bytes_total": int(out_all), "format": f"v{fmt}",
+                       "parallelism": f"docs {how}-partitioned over {world} GPU(s) (one process each), "
+                                      "no collective in the hot path; max-time / sum-counters all-reduce"},
             "docs_per_s": round(docs_s, 1),
             "hbm_frac_in_plus_out": round((in_all + out_all) * args.steps / elapsed / 1e9 / (HBM_PEAK_GBS * world), 5),
             "docs_fast_path": int(fast_all), "docs_general_path": int(gen_all), "doc_errors": int(err_all),
             "device_ms_per_step": round(float(np.mean(dev_ms)), 4),
             "roofline": {"kernel": kernel_name, "bound": "hbm", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": traffic, "avg_launch_ms": round(avg_fast, 5),
+                         "traffic": traffic, "traffic_source": traffic_src, "avg_launch_ms": round(avg_fast, 5),
                          "algorithmic_bytes_per_launch": int(alg_bytes)},
         }
-        if world == 1:
+        if stub:
+            line["stub"] = "cpu-stub: launcher/sharding/reduce plumbing only, no merge computed"
+        if world == 1 and not stub:
             # PCIe-inclusive rate of the same batch from pageable host memory (what the Node addon
             # hands over): H2D of arena + offsets, the kernels, D2H of the packed outputs.  Not `value`.
             eng.run_host("merge", fmt, arena, upd_off, doc_upd)
@@ -355,9 +443,9 @@ def main():
             th = (time.perf_counter() - th) / 5
             line["pcie_inclusive"] = {"value": round(in_bytes / th / 1e9, 3), "unit": "GB/s",
                                       "ms_per_call": round(th * 1e3, 3), "source": "pageable host buffers"}
-        if not args.no_cpu_baseline and world == 1:  # the host baseline is reported at N = 1 only
+        if not args.no_cpu_baseline and world == 1 and not stub:  # the host baseline: N = 1 only
             line["cpu_baseline"] = cpu_baseline(arena, upd_off, doc_upd, fmt, args.cpu_baseline_seconds)
-        if not args.no_secondary and world == 1:
+        if not args.no_secondary and world == 1 and not stub:
             line["secondary"] = secondary(dev, eng)
         print(json.dumps(line), flush=True)
     if world > 1:

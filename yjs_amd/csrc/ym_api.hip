@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <atomic>
 #include <mutex>
 #include <stdio.h>
 #include <stdlib.h>
@@ -65,19 +66,30 @@ struct DevState {
   uint64_t *pinned_dev = nullptr;  // ... its device address
   bool dirty = true;            // device counters not known to be reset (first call, failed call)
   uint64_t seq = 0;             // call sequence number: the fast paths' completion flag (pinned[7])
+  uint64_t min_stage_cap = 0;   // host batches: staging capacity learnt from an overflowing call
 };
 
+// Device state is per (thread, device): a thread may drive several devices in turn (ym_init switches
+// its current one and keeps the others' streams and workspaces), and a thread that never called
+// ym_init starts on the device the last ym_init of the process selected (else YMERGE_DEVICE, else the
+// HIP current device).
+constexpr int kMaxDevices = 64;
+thread_local DevState *g_states[kMaxDevices] = {};
 thread_local DevState *g_state = nullptr;
+std::atomic<int> g_default_device{-1};
 std::mutex g_mu;
 
 DevState *state() {
   if (!g_state) {
-    g_state = new DevState();
-    int dev = 0;
-    const char *env = getenv("YMERGE_DEVICE");
-    if (env) dev = atoi(env);
-    else hipGetDevice(&dev);
-    g_state->device = dev;
+    int dev = g_default_device.load();
+    if (dev < 0) {
+      const char *env = getenv("YMERGE_DEVICE");
+      if (env) dev = atoi(env);
+      else hipGetDevice(&dev);
+    }
+    if (dev < 0 || dev >= kMaxDevices) dev = 0;
+    if (!g_states[dev]) { g_states[dev] = new DevState(); g_states[dev]->device = dev; }
+    g_state = g_states[dev];
   }
   if (!g_state->stream) {
     hipSetDevice(g_state->device);
@@ -95,15 +107,80 @@ DevState *state() {
   return g_state;
 }
 
-// host batches: document d's output moves to the packed offset cmp_off[d] (exclusive scan of out_len),
-// so the device-to-host copy carries the outputs only, not the fast paths' sparse slot region
-__global__ void __launch_bounds__(64) k_pack(const uint8_t *src, const uint64_t *off, const uint64_t *len,
-                                             const uint64_t *cmp_off, uint8_t *dst, uint32_t n) {
-  for (uint32_t d = blockIdx.x; d < n; d += gridDim.x) {
-    const uint8_t *s = src + off[d];
-    uint8_t *o = dst + cmp_off[d];
-    const uint64_t m = len[d];
-    for (uint64_t b = threadIdx.x; b < m; b += 64) o[b] = s[b];
+// host batches: document d's output moves to the packed offset cmp_off[d] (exclusive scan of the masked
+// lengths), so the device-to-host copy carries the outputs only, not the fast paths' sparse slot region.
+// The grid walks the PACKED output in 16 KB chunks (a large document gets many blocks, a chunk may hold
+// many small documents): each thread writes one aligned 16-byte word of the destination, assembled
+// from two aligned 16-byte source loads and a byte funnel shift (the source slot of a document is at
+// an arbitrary offset relative to its packed position); the one word per document boundary that spans
+// two documents is assembled byte by byte.  Reads may touch <= 15 bytes past a document's output
+// (inside the arena's 16-byte padding).
+constexpr uint32_t PACK_THREADS = 256, PACK_WORDS = 4, PACK_CHUNK = PACK_THREADS * PACK_WORDS * 16;
+
+__device__ inline uint32_t pack_doc_of(const uint64_t *cmp_off, uint32_t lo, uint32_t hi, uint64_t p) {
+  // largest d in [lo, hi] with cmp_off[d] <= p
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (cmp_off[mid] <= p) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__device__ inline uint4 pack_load16(const uint8_t *src, uint64_t s) {
+  const uint64_t a = s & ~15ull;
+  const uint32_t sh = (uint32_t)(s & 15);
+  const uint4 x = *reinterpret_cast<const uint4 *>(src + a);
+  if (sh == 0) return x;
+  const uint4 y = *reinterpret_cast<const uint4 *>(src + a + 16);
+  const uint32_t d[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+  const uint32_t dw = sh >> 2, bs = sh & 3;
+  uint32_t r[4];
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++) {
+    uint32_t l = d[k], h = d[k + 1];
+#pragma unroll
+    for (uint32_t t = 1; t < 4; t++) {
+      l = dw == t ? d[k + t] : l;
+      h = dw == t ? d[k + t + 1] : h;
+    }
+    r[k] = __builtin_amdgcn_alignbyte(h, l, bs);
+  }
+  return make_uint4(r[0], r[1], r[2], r[3]);
+}
+
+__global__ void __launch_bounds__(PACK_THREADS) k_pack(const uint8_t *src, const uint64_t *off, const uint64_t *mlen,
+                                                       const uint64_t *cmp_off, uint8_t *dst, uint32_t n, uint64_t total) {
+  __shared__ uint32_t s_rng[2];
+  for (uint64_t c0 = (uint64_t)blockIdx.x * PACK_CHUNK; c0 < total; c0 += (uint64_t)gridDim.x * PACK_CHUNK) {
+    __syncthreads();
+    if (threadIdx.x < 2) {
+      const uint64_t p = threadIdx.x == 0 ? c0 : (c0 + PACK_CHUNK < total ? c0 + PACK_CHUNK : total) - 1;
+      s_rng[threadIdx.x] = pack_doc_of(cmp_off, 0, n - 1, p);
+    }
+    __syncthreads();
+    const uint32_t lo = s_rng[0], hi = s_rng[1];
+#pragma unroll
+    for (uint32_t it = 0; it < PACK_WORDS; it++) {
+      const uint64_t p = c0 + (uint64_t)(it * PACK_THREADS + threadIdx.x) * 16;
+      if (p >= total) break;
+      uint32_t d = pack_doc_of(cmp_off, lo, hi, p);
+      uint64_t e = cmp_off[d] + mlen[d];
+      const uint64_t pe = p + 16 < total ? p + 16 : total;
+      if (pe <= e) {  // one document
+        const uint4 v = pack_load16(src, off[d] - cmp_off[d] + p);
+        if (pe - p == 16) {
+          *reinterpret_cast<uint4 *>(dst + p) = v;
+        } else {
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+          for (uint64_t q = p; q < pe; q++) dst[q] = (uint8_t)(w[(q - p) >> 2] >> (8 * ((q - p) & 3)));
+        }
+        continue;
+      }
+      for (uint64_t q = p; q < pe; q++) {  // spans a document boundary (empty documents are skipped)
+        while (q >= e) { d++; e = cmp_off[d] + mlen[d]; }
+        dst[q] = src[off[d] + (q - cmp_off[d])];
+      }
+    }
   }
 }
 
@@ -253,9 +330,10 @@ int run_general(DevState *S, hipStream_t st, GeneralJob j, uint32_t *list, uint3
   return 0;
 }
 
-int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) {
+int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *stats, int depth = 0) {
   if (!b || !out) return -1;
   DevState *S = state();
+  HIPCHK(hipSetDevice(S->device));  // the caller (e.g. torch) may have switched this thread's device
   hipStream_t st = stream ? (hipStream_t)stream : S->stream;
   uint32_t nd = b->n_docs;
   if (stats) memset(stats, 0, sizeof(*stats));
@@ -277,6 +355,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
     const uint64_t svb = op == OP_DIFF ? sv_off[nd] : 0;
     const uint64_t bound = 4 * abytes + 2 * svb + 128ull * nd + 8192;
     dev_cap = out->cap > bound ? out->cap : bound;
+    if (S->min_stage_cap > dev_cap) dev_cap = S->min_stage_cap;
     if (S->in_arena.ensure(abytes + 16) || S->in_off.ensure((b->n_upd + 1) * 8ull) || S->in_doc.ensure((nd + 1) * 4ull)) return -2;
     HIPCHK(hipMemcpyAsync(S->in_arena.p, A, abytes, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(S->in_off.p, upd_off, (b->n_upd + 1) * 8ull, hipMemcpyHostToDevice, st));
@@ -430,8 +509,13 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   }
   if (!host) return used > out->cap ? YM_ERR_CAPACITY : 0;
   // host batch: pack the outputs in document order (out_off[d] = bytes of the outputs before d), then
-  // copy only them back.  A staging overflow reports the staging need (the caller's retry grows both).
-  if (used > dev_cap) return YM_ERR_CAPACITY;
+  // copy only them back.  The staging arena is the library's own: an overflow grows it and runs the
+  // call again here (the caller only ever sees the packed size in out->used).
+  if (used > dev_cap) {
+    if (depth >= 2) return YM_ERR_CAPACITY;
+    S->min_stage_cap = used + used / 4 + 4096;
+    return run_op(op, b, out, stream, stats, depth + 1);
+  }
   const uint64_t total = S->pinned[5];
   out->used = total;
   if (total > out->cap) return YM_ERR_CAPACITY;
@@ -443,8 +527,12 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
     hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, mlen, (uint64_t *)nullptr, nd, st);
     if (S->scan_tmp.ensure(tmp + 16)) return -2;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(S->scan_tmp.p, tmp, mlen, S->cmp_off.as<uint64_t>(), nd, st));
-    const uint32_t grid = nd < 65536 ? nd : 65536;
-    k_pack<<<grid, 64, 0, st>>>(o_arena, o_off, mlen, S->cmp_off.as<uint64_t>(), S->cmp_arena.as<uint8_t>(), nd);
+    if (total) {
+      const uint64_t chunks = (total + PACK_CHUNK - 1) / PACK_CHUNK;
+      const uint32_t grid = chunks < 65536 ? (uint32_t)chunks : 65536;
+      k_pack<<<grid, PACK_THREADS, 0, st>>>(o_arena, o_off, mlen, S->cmp_off.as<uint64_t>(), S->cmp_arena.as<uint8_t>(),
+                                            nd, total);
+    }
   }
   if (total) HIPCHK(hipMemcpyAsync(out->arena, S->cmp_arena.p, total, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(out->out_off, S->cmp_off.p, nd * 8ull, hipMemcpyDeviceToHost, st));
@@ -460,17 +548,18 @@ extern "C" {
 
 int ym_init(int device) {
   std::lock_guard<std::mutex> g(g_mu);
+  if (device < 0 || device >= kMaxDevices) return -1;
   if (hipSetDevice(device) != hipSuccess) return -1;
-  if (g_state && g_state->device != device) { g_state = nullptr; }
-  if (!g_state) { g_state = new DevState(); g_state->device = device; }
+  if (!g_states[device]) { g_states[device] = new DevState(); g_states[device]->device = device; }
+  g_state = g_states[device];  // other devices' states of this thread stay alive for a later switch
+  g_default_device.store(device);
   state();
   return 0;
 }
 
-int ym_shutdown(void) {
-  if (!g_state) return 0;
-  DevState *S = g_state;
-  hipStreamSynchronize(S->stream);
+static void release_state(DevState *S) {
+  hipSetDevice(S->device);
+  if (S->stream) hipStreamSynchronize(S->stream);
   DBuf *bufs[] = {&S->ws, &S->ws_size, &S->ws_off, &S->layout, &S->counters, &S->scan_tmp, &S->list_a, &S->list_b,
                   &S->flags, &S->bscratch, &S->in_arena, &S->in_off, &S->in_doc, &S->in_sv, &S->in_svoff, &S->out_arena,
                   &S->out_off, &S->out_len, &S->status, &S->cmp_off, &S->cmp_len, &S->cmp_arena};
@@ -486,6 +575,12 @@ int ym_shutdown(void) {
   if (S->large.pinned) hipHostFree(S->large.pinned);
   if (S->stream) hipStreamDestroy(S->stream);
   delete S;
+}
+
+// releases every device state of the calling thread
+int ym_shutdown(void) {
+  for (int d = 0; d < kMaxDevices; d++)
+    if (g_states[d]) { release_state(g_states[d]); g_states[d] = nullptr; }
   g_state = nullptr;
   return 0;
 }
