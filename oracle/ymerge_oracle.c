@@ -274,6 +274,8 @@ typedef struct Val {
   Str *keys;          /* OBJ keys */
   size_t n, cap;
   Span bytes;
+  struct Val *proto;  /* OBJ built by readAny: NULL = Object.prototype, else the value assigned to
+                         "__proto__" (an object, array, Uint8Array or null) */
 } Val;
 
 static Val *val_new(Ctx *c, int t) {
@@ -295,14 +297,35 @@ static int key_array_index(Str k, uint32_t *idx) {
   *idx = (uint32_t)v;
   return 1;
 }
-/* [[Set]] / CreateDataProperty on a plain object, keeping OrdinaryOwnPropertyKeys order.
- * is_json: JSON.parse semantics (__proto__ is an ordinary key); else assignment semantics (readAny). */
-static void obj_set(Ctx *c, Val *o, Str k, Val *v, int is_json) {
-  for (size_t i = 0; i < o->n; i++)
-    if (str_eq(o->keys[i], k)) { o->items[i] = v; return; }
-  static const uint16_t proto[] = {'_', '_', 'p', 'r', 'o', 't', 'o', '_', '_'};
-  Str ps = {proto, 9};
-  if (!is_json && str_eq(k, ps)) return; /* sets [[Prototype]] (object/null) or is ignored: no own key */
+static int str_is(Str k, const char *t) {
+  size_t i = 0;
+  for (; t[i]; i++) if (i >= k.n || k.u[i] != (uint8_t)t[i]) return 0;
+  return i == k.n;
+}
+static void js_num_to_string(double x, char *out);
+/* CanonicalNumericIndexString (ES2019 7.1.16): 1 when numeric; *idx = integer index or -1 */
+static int key_canonical_numeric(Str k, int64_t *idx) {
+  char buf[64];
+  *idx = -1;
+  if (k.n == 0 || k.n >= sizeof buf) return 0;
+  for (size_t i = 0; i < k.n; i++) { if (k.u[i] > 127) return 0; buf[i] = (char)k.u[i]; }
+  buf[k.n] = 0;
+  if (!strcmp(buf, "-0")) return 1;
+  char *end;
+  double x = strtod(buf, &end);
+  if (!strcmp(buf, "NaN")) x = NAN;
+  else if (*end) return 0;
+  char t[64];
+  js_num_to_string(x, t);
+  if (strcmp(t, buf)) return 0;
+  if (isfinite(x) && floor(x) == x && x >= 0 && !signbit(x)) *idx = (int64_t)x;
+  return 1;
+}
+static int obj_find(const Val *o, Str k) {
+  for (size_t i = 0; i < o->n; i++) if (str_eq(o->keys[i], k)) return (int)i;
+  return -1;
+}
+static void obj_append(Ctx *c, Val *o, Str k, Val *v) {
   if (o->n == o->cap) {
     size_t cap = o->cap ? o->cap * 2 : 4;
     Val **ni = (Val **)aalloc(c, cap * sizeof(Val *));
@@ -324,6 +347,62 @@ static void obj_set(Ctx *c, Val *o, Str k, Val *v, int is_json) {
   memmove(o->items + pos + 1, o->items + pos, (o->n - pos) * sizeof(Val *));
   memmove(o->keys + pos + 1, o->keys + pos, (o->n - pos) * sizeof(Str));
   o->items[pos] = v; o->keys[pos] = k; o->n++;
+}
+/* [[Set]] / CreateDataProperty on a plain object, keeping OrdinaryOwnPropertyKeys order.
+ * is_json: JSON.parse (CreateDataProperty: "__proto__" is an ordinary key).  Else readAny's
+ * `obj[key] = v` in strict code: OrdinarySet walks the prototype chain -- Object.prototype's __proto__
+ * setter replaces the prototype with an object / array / Uint8Array / null (a primitive is ignored);
+ * a null prototype, or a prototype object owning the key as data, creates an own property; a Uint8Array
+ * in the chain throws TypeError on its getters (length, byteLength, byteOffset, buffer) and read-only
+ * BYTES_PER_ELEMENT and, in the reference's V8, creates a canonical numeric key only when it indexes
+ * the array (else ignores it). */
+static void obj_set(Ctx *c, Val *o, Str k, Val *v, int is_json) {
+  int at = obj_find(o, k);
+  if (at >= 0) { o->items[at] = v; return; }
+  if (!is_json) {
+    int dunder = str_is(k, "__proto__");
+    int setter = v->t == V_OBJ || v->t == V_ARR || v->t == V_BYTES || v->t == V_NULL;
+    for (Val *P = o->proto;; P = P->proto) {
+      if (!P) {  /* Object.prototype */
+        if (dunder) { if (setter) o->proto = v; return; }
+        break;
+      }
+      if (P->t == V_NULL) break;
+      if (P->t == V_ARR) {
+        if (dunder) { if (setter) o->proto = v; return; }
+        break;
+      }
+      if (P->t == V_BYTES) {
+        if (str_is(k, "length") || str_is(k, "byteLength") || str_is(k, "byteOffset") || str_is(k, "buffer") ||
+            str_is(k, "BYTES_PER_ELEMENT"))
+          fail(c, YMO_ERR_TYPE);
+        int64_t idx;
+        if (key_canonical_numeric(k, &idx)) {
+          if (idx < 0 || (size_t)idx >= P->bytes.n) return;  /* ignored */
+          break;
+        }
+        if (dunder) { if (setter) o->proto = v; return; }
+        break;
+      }
+      if (obj_find(P, k) >= 0) break;  /* an inherited writable data property: created on the receiver */
+    }
+  }
+  obj_append(c, o, k, v);
+}
+/* the end of a readAny object's prototype chain: V_ARR / V_BYTES / 0 (Object.prototype or null) */
+static int proto_end(const Val *o) {
+  for (const Val *P = o->proto; P; P = P->proto)
+    if (P->t != V_OBJ) return P->t == V_NULL ? 0 : P->t;
+  return 0;
+}
+/* [[Get]](o, k) along the chain of an object whose chain ends in an Array */
+static const Val *chain_get(const Val *o, Str k, const Val **arr) {
+  for (const Val *P = o; P; P = P->proto) {
+    if (P->t == V_ARR) { *arr = P; return NULL; }
+    int at = obj_find(P, k);
+    if (at >= 0) return P->items[at];
+  }
+  return NULL;
 }
 static void arr_push(Ctx *c, Val *a, Val *v) {
   if (a->n == a->cap) {
@@ -444,10 +523,33 @@ static void wr_any(Ctx *c, Buf *b, const Val *v) { /* writeAny (G) */
       for (size_t i = 0; i < v->n; i++) wr_any(c, b, v->items[i]);
       return;
     case V_BYTES: put8(c, b, 116); wr_vbytes(c, b, v->bytes.p, v->bytes.n); return;
-    default:
+    default: {
+      /* writeAny: `data instanceof Array` / `instanceof Uint8Array` see the prototype chain */
+      int end = proto_end(v);
+      if (end == V_BYTES) fail(c, YMO_ERR_TYPE); /* writeVarUint8Array reads byteLength: incompatible receiver */
+      if (end == V_ARR) {
+        static const uint16_t lk[] = {'l', 'e', 'n', 'g', 't', 'h'};
+        Str ls = {lk, 6};
+        const Val *arr = NULL;
+        if (chain_get(v, ls, &arr)) fail(c, YMO_ERR_UNSUPPORTED); /* an own "length" on the chain */
+        put8(c, b, 117); wr_vu(c, b, (int64_t)arr->n);
+        for (size_t i = 0; i < arr->n; i++) {
+          char nb[32];
+          snprintf(nb, sizeof nb, "%zu", i);
+          uint16_t ku[32];
+          size_t kn = strlen(nb);
+          for (size_t j = 0; j < kn; j++) ku[j] = (uint8_t)nb[j];
+          Str ks = {ku, kn};
+          const Val *a2 = NULL;
+          const Val *x = chain_get(v, ks, &a2);
+          wr_any(c, b, x ? x : arr->items[i]);
+        }
+        return;
+      }
       put8(c, b, 118); wr_vu(c, b, (int64_t)v->n);
       for (size_t i = 0; i < v->n; i++) { wr_vstr(c, b, v->keys[i]); wr_any(c, b, v->items[i]); }
       return;
+    }
   }
 }
 

@@ -1,0 +1,53 @@
+"""Runs batches through the TEST-ONLY host build of the device core (tests/native/core_host.cpp: the
+general path's general_doc() compiled for the CPU, optionally under ASan + UBSan).  Same batch layout as
+the C ABI; returns (outputs list (bytes or None), status ndarray)."""
+import os
+import struct
+import subprocess
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NATIVE = os.path.join(ROOT, "tests", "native")
+OPS = {"merge": 0, "diff": 1, "sv": 2, "conv": 3, "meta": 4, "dsmerge": 5}
+
+
+def binary(san=False):
+    exe = os.path.join(NATIVE, "_build", "core_host_san" if san else "core_host")
+    subprocess.check_call(["make", "-s", "-C", NATIVE, os.path.relpath(exe, NATIVE)])
+    return exe
+
+
+def run(op, fmt, arena, upd_off, doc_upd, sv_arena=None, sv_off=None, san=False):
+    arena = np.ascontiguousarray(arena, np.uint8)
+    upd_off = np.ascontiguousarray(upd_off, np.uint64)
+    doc_upd = np.ascontiguousarray(doc_upd, np.uint32)
+    nd = len(doc_upd) - 1
+    if sv_arena is None:
+        sv_arena = np.zeros(0, np.uint8)
+        sv_off = np.zeros(nd + 1, np.uint64)
+    sv_arena = np.ascontiguousarray(sv_arena, np.uint8)
+    sv_off = np.ascontiguousarray(sv_off, np.uint64)
+    exe = binary(san)
+    with tempfile.TemporaryDirectory() as td:
+        fin, fout = os.path.join(td, "in"), os.path.join(td, "out")
+        with open(fin, "wb") as f:
+            f.write(struct.pack("<IIIIQQ", OPS[op], fmt, nd, len(upd_off) - 1, len(arena), len(sv_arena)))
+            f.write(doc_upd.tobytes())
+            f.write(upd_off.tobytes())
+            f.write(arena.tobytes())
+            f.write(sv_off.tobytes())
+            f.write(sv_arena.tobytes())
+        env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1")
+        r = subprocess.run([exe, fin, fout], capture_output=True, text=True, env=env, timeout=600)
+        assert r.returncode == 0, r.stderr[-4000:]
+        raw = open(fout, "rb").read()
+    outs, st, pos = [], np.zeros(nd, np.int32), 0
+    for d in range(nd):
+        s, n = struct.unpack_from("<iQ", raw, pos)
+        pos += 12
+        st[d] = s
+        outs.append(raw[pos:pos + n] if s == 0 else None)
+        pos += n
+    return outs, st

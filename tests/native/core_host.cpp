@@ -1,0 +1,81 @@
+// TEST-ONLY host build of yjs_amd/csrc/ym_core.h: the general path's per-document entry (general_doc,
+// the function k_general runs on the MI355X, one thread per document) compiled for the CPU, so the
+// device core can be unit-tested in the GPU-less container and run under ASan / UBSan.
+// It is not part of the product: libymerge.so only runs this code as HIP kernels.
+//
+// Usage: core_host <batch.in> <result.out>
+//   batch.in : u32 op, u32 fmt, u32 n_docs, u32 n_upd, u64 arena_len, u64 sv_len,
+//              u32 doc_upd[n_docs+1], u64 upd_off[n_upd+1], u8 arena[arena_len],
+//              u64 sv_off[n_docs+1], u8 sv[sv_len]
+//   result.out: per document: i32 status, u64 len, u8 bytes[len]
+#define YM_HD
+#include "../../yjs_amd/csrc/ym_core.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+using namespace ym;
+
+template <class T> static void rd(FILE *f, T *p, size_t n) {
+  if (n && fread(p, sizeof(T), n, f) != n) { fprintf(stderr, "short read\n"); exit(2); }
+}
+
+int main(int argc, char **argv) {
+  if (argc != 3) { fprintf(stderr, "usage: core_host in out\n"); return 2; }
+  FILE *f = fopen(argv[1], "rb");
+  if (!f) return 2;
+  uint32_t hdr[4];
+  uint64_t lens[2];
+  rd(f, hdr, 4);
+  rd(f, lens, 2);
+  const uint32_t op = hdr[0], fmt = hdr[1], nd = hdr[2], nu = hdr[3];
+  std::vector<uint32_t> doc_upd(nd + 1);
+  std::vector<uint64_t> upd_off(nu + 1), sv_off(nd + 1);
+  // +64: the lib0 readers may look one word past a short update (bounds are checked, loads are not)
+  std::vector<uint8_t> arena(lens[0] + 64), sv(lens[1] + 64);
+  rd(f, doc_upd.data(), nd + 1);
+  rd(f, upd_off.data(), nu + 1);
+  rd(f, arena.data(), lens[0]);
+  rd(f, sv_off.data(), nd + 1);
+  rd(f, sv.data(), lens[1]);
+  fclose(f);
+  FILE *o = fopen(argv[2], "wb");
+  if (!o) return 2;
+  const uint32_t v2 = fmt == 2;
+  for (uint32_t d = 0; d < nd; d++) {
+    const uint32_t u0 = doc_upd[d], k = doc_upd[d + 1] - u0;
+    const uint64_t bytes = upd_off[doc_upd[d + 1]] - upd_off[u0];
+    const uint64_t svlen = op == OP_DIFF ? sv_off[d + 1] - sv_off[d] : 0;
+    const uint8_t *svp = op == OP_DIFF ? sv.data() + sv_off[d] : nullptr;
+    int st = ST_RETRY;
+    std::vector<uint8_t> out;
+    for (uint32_t mul = 1, round = 0; st == ST_RETRY && round < 7; mul *= 8, round++) {
+      const GeneralWsSize z = general_ws_size(k, bytes, mul, general_sv_bytes(op, svlen, bytes));
+      std::vector<uint8_t> ws(z.total + 16);
+      DocWS w;
+      general_carve(ws.data(), z, w);
+      Layout L;
+      memset(&L, 0, sizeof(L));
+      Ctx c = {0, arena.data()};
+      general_doc(c, w, op, v2, upd_off.data(), u0, k, svp, svlen, 1, L, nullptr);
+      st = c.err;
+      if (st) continue;
+      // pass 2 over the same workspace (the part table recorded by pass 1 is read back)
+      out.assign(L.total + 1, 0);
+      Ctx c2 = {0, arena.data()};
+      general_doc(c2, w, op, v2, upd_off.data(), u0, k, svp, svlen, 2, L, out.data());
+      st = c2.err ? (c2.err == ST_RETRY ? ST_UNEXPECTED : c2.err) : 0;
+      out.resize(L.total);
+    }
+    const int32_t s32 = st;
+    const uint64_t n = st ? 0 : out.size();
+    fwrite(&s32, 4, 1, o);
+    fwrite(&n, 8, 1, o);
+    if (n) fwrite(out.data(), 1, n, o);
+  }
+  fclose(o);
+  return 0;
+}

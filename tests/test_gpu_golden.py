@@ -1,6 +1,8 @@
 """GPU parity: every golden vector through libymerge.so (C ABI) on the MI355X, batched per
 (op, format) group so one launch covers hundreds of documents.  Expected bytes / errors come from
-yjs 13.5.16 itself (tests/golden, recipe oracle/gen/make_fixtures.cjs)."""
+yjs 13.5.16 itself (tests/golden, recipes oracle/gen/make_*fixtures.cjs), with no exceptions: every
+vector must come out byte-identical (or with the same error), including the payload re-encodings of
+tests/golden/canon.json."""
 import collections
 
 import pytest
@@ -11,12 +13,6 @@ import oracle_ref as O
 pytestmark = pytest.mark.gpu
 
 CASES = [c for c in golden_io.load_cases() if not (c["op"] == "merge" and len(c["inputs"]) == 0)]
-# documented canonicalisation gap: V1 JSON texts that JSON.stringify would rewrite
-NONCANONICAL_JSON = {"edge/json_merge/v1/merge"} | {f"edge/json_diff_{k}/v1/diff" for k in (0, 3, 6, 9)}
-# documented conversion gap: embeds / formats whose JSON value is an object, array or non-integer number
-# (V1 text <-> V2 any needs JSON.parse / Number::toString on the device) report UNSUPPORTED
-CONV_OBJECT_JSON = {f"conv/content.json/unicode_rich_{k}/merged/v{f}/conv" for k in range(1, 6) for f in (1, 2)} | {
-    "conv/refgolden.json/ref2_identity/merged/v1/conv", "conv/refgolden.json/ref2_v2_self/merged/v2/conv"}
 
 
 @pytest.fixture(scope="module")
@@ -51,11 +47,6 @@ def test_golden_batched_on_gpu(engine, key):
     bad = []
     for i, c in enumerate(cases):
         st = int(status[i])
-        if c["id"] in NONCANONICAL_JSON or c["id"] in CONV_OBJECT_JSON or (
-                op == "conv" and c["name"].startswith("edge.json/json_") and st == 7):
-            if st != 7:
-                bad.append((c["id"], "expected UNSUPPORTED", st))
-            continue
         if "error" in c:
             want = O.js_error_status(c["error"], c["message"])
             if st != want:

@@ -18,9 +18,7 @@ def test_js_api_golden():
     assert line, r.stderr[-3000:]
     res = json.loads(line[-1])
     assert r.returncode == 0 and res["bad"] == 0, res
-    # unsupported: the 5 non-canonical JSON texts, their 2 conversions, 12 object-valued embeds / formats
-    # in conversions
-    assert res["ok"] >= 990 and res["unsupported"] <= 19, res
+    assert res["ok"] >= 990 and res["unsupported"] == 0, res
 
 
 @pytest.mark.skipif(shutil.which("node") is None, reason="node not installed on this box")

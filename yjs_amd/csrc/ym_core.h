@@ -214,6 +214,12 @@ YM_INL bool key_is_proto(const Ctx &c, const Span &k) {
 YM_INL bool vu_minimal(const Ctx &c, uint64_t start, uint64_t end) {  // last byte of a multi-byte varuint != 0
   return end - start <= 1 || c.A[end - 1] != 0;
 }
+// is the varuint at d.pos minimally encoded (d is not advanced)
+YM_INL bool vu_prefix_minimal(Ctx &c, const Rd &d) {
+  Rd t = d;
+  rd_vu(c, t);
+  return vu_minimal(c, t.start + d.pos, t.start + (t.pos < t.len ? t.pos : t.len));
+}
 YM_INL uint32_t vu_size(uint64_t v) {
   uint32_t n = 1;
   while (v > 127) { v = (uint32_t)v >> 7; n++; }
@@ -293,21 +299,17 @@ YM_BIG void any_skip(Ctx &c, Rd &d, int *noncanon) {
         if (d.pos > d.len || d.len - d.pos < 8) { seterr(c, ST_RANGE); return; }
         d.pos += 8;
         break;
-      case 119: {
-        uint64_t s0 = d.pos;
-        rd_vstr(c, d);
-        if (c.err) return;
-        (void)s0;
-        break;
-      }
-      case 116: {
-        rd_vbytes(c, d);
+      case 119: case 116: {  // writeVarString / writeVarUint8Array re-encode the length prefix
+        if (!vu_prefix_minimal(c, d)) *noncanon = 1;
+        if (tag == 119) rd_vstr(c, d); else rd_vbytes(c, d);
         if (c.err) return;
         break;
       }
       default: {  // 118 object / 117 array
+        uint64_t s0 = d.pos;
         uint32_t n = rd_vu(c, d);
         if (c.err) return;
+        if (!vu_minimal(c, d.start + s0, d.start + d.pos)) *noncanon = 1;
         if (n > 0) {
           if (sp >= YM_ANY_DEPTH) { seterr(c, ST_UNSUPPORTED); return; }
           left[sp] = n;
@@ -326,6 +328,7 @@ YM_BIG void any_skip(Ctx &c, Rd &d, int *noncanon) {
       if (left[sp - 1] == 0) { nkeys = kbase[sp - 1]; sp--; continue; }
       left[sp - 1]--;
       if (isobj[sp - 1]) {
+        if (!vu_prefix_minimal(c, d)) *noncanon = 1;
         Span k = rd_vstr(c, d);
         if (c.err) return;
         int64_t ki = key_index(c, k);
@@ -516,6 +519,10 @@ YM_BIG int json_check(const Ctx &c, uint64_t off, uint64_t n, int *noncanon) {
   }
 }
 
+}  // namespace ym
+#include "ym_canon.h"
+namespace ym {
+
 // ------------------------------------------------------------------------------------------------
 // V2 RLE column decoders (lib0 RleDecoder / UintOptRleDecoder / IntDiffOptRleDecoder)
 // ------------------------------------------------------------------------------------------------
@@ -568,6 +575,7 @@ struct SStruct {
   UOptCol lsnap;   // V2 ContentJSON: string-length decoder snapshot at the first element
   uint64_t lsb;    // V2 ContentJSON: byte offset (absolute) of the first element
   uint8_t kind, ref, has_origin, has_right, parent_kind, has_psub;
+  uint8_t nca, ncb;  // payload a / b not in the form yjs re-encodes it to: written through ym_canon.h
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -652,35 +660,42 @@ YM_INL void rd_right(Ctx &c, Reader &r, int64_t &cl, int64_t &ck) {
 YM_INL Span rd_string(Ctx &c, Reader &r) { return r.v2 ? sdec_read(c, r) : rd_vstr(c, r.rest); }
 YM_INL int64_t rd_len(Ctx &c, Reader &r) { return r.v2 ? (int64_t)uopt_read(c, r.ln) : (int64_t)rd_vu(c, r.rest); }
 
-// V1 JSON field (readJSON = JSON.parse(readVarString)): keep the text, it must be canonical
-YM_INL Span rd_json_text(Ctx &c, Reader &r) {
+// V1 JSON field (readJSON = JSON.parse(readVarString)): the text, validated; *nc = 1 when
+// JSON.stringify(JSON.parse(text)) differs from it
+YM_INL Span rd_json_text(Ctx &c, Reader &r, uint8_t *nc) {
   Span s = rd_vstr(c, r.rest);
   if (c.err) return s;
-  int nc = 0;
-  int e = json_check(c, s.off, s.n, &nc);
+  int n = 0;
+  int e = json_check(c, s.off, s.n, &n);
   if (e) seterr(c, e);
-  else if (nc && !r.lax) seterr(c, ST_UNSUPPORTED);
+  else if (n && !r.lax) *nc = 1;
   return s;
 }
-// one `any` value in rest, must be canonical
-YM_INL Span rd_any_span(Ctx &c, Reader &r) {
+// one `any` value in rest, validated; *nc = 1 when writeAny(readAny(..)) differs from it
+YM_INL Span rd_any_span(Ctx &c, Reader &r, uint8_t *nc) {
   uint64_t p0 = r.rest.pos;
-  int nc = 0;
-  any_skip(c, r.rest, &nc);
+  int n = 0;
+  any_skip(c, r.rest, &n);
   Span s = {r.rest.start + p0, (uint32_t)(r.rest.pos - p0), 0, 0};
-  if (!c.err && nc && !r.lax) seterr(c, ST_UNSUPPORTED);
+  if (!c.err && n) {
+    const int e = any_read_check(c.A, s.off, s.off + s.n);  // readAny itself can throw (prototype keys)
+    if (e) seterr(c, e);
+    else if (!r.lax) *nc = 1;
+  }
   return s;
 }
 
-// ContentDoc options must already be in the form ContentDoc re-derives ({gc:false}?, {autoLoad:true}?, {meta}?)
-YM_BIG void check_doc_opts(Ctx &c, const Span &o) {
+// ContentDoc options already in the form ContentDoc re-derives ({gc:false}?, {autoLoad:true}?, {meta}?,
+// meta canonical)?  Otherwise they are re-derived on write (ym_canon.h doc_opts).
+YM_BIG bool doc_opts_canonical(Ctx &c, const Span &o) {
+  Ctx cc = {0, c.A};
   Rd d = {o.off, o.n, 0};
-  int tag = rbyte(c, d);
-  if (tag != 118) { seterr(c, ST_UNSUPPORTED); return; }
-  uint32_t n = rd_vu(c, d);
+  int tag = rbyte(cc, d);
+  if (tag != 118) return false;
+  uint32_t n = rd_vu(cc, d);
   int stage = 0;
-  for (uint32_t i = 0; i < n && !c.err; i++) {
-    Span k = rd_vstr(c, d);
+  for (uint32_t i = 0; i < n && !cc.err; i++) {
+    Span k = rd_vstr(cc, d);
     const char *want[3] = {"gc", "autoLoad", "meta"};
     int which = -1;
     for (int w = stage; w < 3; w++) {
@@ -691,18 +706,19 @@ YM_BIG void check_doc_opts(Ctx &c, const Span &o) {
         if (c.A[k.off + q] != (uint8_t)want[w][q]) eq = false;
       if (eq) { which = w; break; }
     }
-    if (which < 0) { seterr(c, ST_UNSUPPORTED); return; }
+    if (which < 0) return false;
     stage = which + 1;
     uint64_t v0 = d.pos;
-    int vt = rbyte(c, d);
+    int vt = rbyte(cc, d);
     d.pos = v0;
-    if (which == 0 && vt != 121) { seterr(c, ST_UNSUPPORTED); return; }
-    if (which == 1 && vt != 120) { seterr(c, ST_UNSUPPORTED); return; }
-    if (which == 2 && (vt == 126 || vt == 127)) { seterr(c, ST_UNSUPPORTED); return; }
+    if (which == 0 && vt != 121) return false;
+    if (which == 1 && vt != 120) return false;
+    if (which == 2 && (vt == 126 || vt == 127)) return false;
     int nc = 0;
-    any_skip(c, d, &nc);
-    if (nc) { seterr(c, ST_UNSUPPORTED); return; }
+    any_skip(cc, d, &nc);
+    if (nc) return false;
   }
+  return !cc.err;
 }
 
 // readItemContent (Item.js:665-683, 13.5.16 ai[] table)
@@ -726,7 +742,7 @@ YM_BIG void read_content(Ctx &c, Reader &r, SStruct &s, int info) {
           int nc = 0;
           int e = json_check(c, t.off, t.n, &nc);
           if (e) seterr(c, e);
-          else if (nc && !r.lax) seterr(c, ST_UNSUPPORTED);
+          else if (nc && !r.lax) s.nca = 1;
         }
       }
       uint64_t last = r.v2 ? r.str_off + r.spos_b : r.rest.start + r.rest.pos;
@@ -737,10 +753,10 @@ YM_BIG void read_content(Ctx &c, Reader &r, SStruct &s, int info) {
     }
     case 3: s.a = rd_vbytes(c, r.rest); s.len = 1; break;
     case 4: s.a = rd_string(c, r); s.len = s.a.n16; break;
-    case 5: s.a = r.v2 ? rd_any_span(c, r) : rd_json_text(c, r); s.len = 1; break;
+    case 5: s.a = r.v2 ? rd_any_span(c, r, &s.nca) : rd_json_text(c, r, &s.nca); s.len = 1; break;
     case 6:
       s.a = rd_string(c, r);
-      s.b = r.v2 ? rd_any_span(c, r) : rd_json_text(c, r);
+      s.b = r.v2 ? rd_any_span(c, r, &s.ncb) : rd_json_text(c, r, &s.ncb);
       s.len = 1;
       break;
     case 7: {
@@ -767,8 +783,13 @@ YM_BIG void read_content(Ctx &c, Reader &r, SStruct &s, int info) {
       uint64_t p0 = r.rest.pos;
       for (int64_t i = 0; i < s.cnt && !c.err; i++) {
         int nc = 0;
+        const uint64_t v0 = r.rest.pos;
         any_skip(c, r.rest, &nc);
-        if (!c.err && nc && !r.lax) seterr(c, ST_UNSUPPORTED);
+        if (!c.err && nc) {
+          const int e = any_read_check(c.A, r.rest.start + v0, r.rest.start + r.rest.pos);
+          if (e) seterr(c, e);
+          else if (!r.lax) s.nca = 1;
+        }
       }
       s.a.off = r.rest.start + p0;
       s.a.n = (uint32_t)(r.rest.pos - p0);
@@ -777,8 +798,8 @@ YM_BIG void read_content(Ctx &c, Reader &r, SStruct &s, int info) {
     }
     case 9:
       s.a = rd_string(c, r);
-      s.b = rd_any_span(c, r);
-      if (!c.err && !r.lax) check_doc_opts(c, s.b);
+      s.b = rd_any_span(c, r, &s.ncb);
+      if (!c.err && !r.lax && !doc_opts_canonical(c, s.b)) s.ncb = 1;
       s.len = 1;
       break;
     case 0: case 10: seterr(c, ST_UNEXPECTED); break;
@@ -976,96 +997,59 @@ YM_INL void e_flush_columns(Enc &e) {
   uopt_flush(e.ln, e.ln_s, e.ln_n);
 }
 
-// convertUpdateFormat of an embed / format value (writeJSON of the value readJSON produced):
-//   V1 -> V2: JSON text (canonical, validated on read) -> writeAny(JSON.parse(text));
-//   V2 -> V1: any value -> writeVarString(JSON.stringify(value)).
-// Exact for literals, strings and integers below 2^31 in magnitude; other numbers, arrays, objects and
-// byte arrays report ST_UNSUPPORTED (the oracle converts them all), a bigint throws TypeError as in JS.
-YM_INL void json_quote_bytes(const Ctx &c, Out &o, uint64_t off, uint64_t n) {  // JSON.stringify(str)
-  o8(o, '"');
-  for (uint64_t i = 0; i < n; i++) {
-    const uint32_t ch = c.A[off + i];
-    if (ch == '"' || ch == '\\') { o8(o, '\\'); o8(o, ch); }
-    else if (ch >= 0x20) o8(o, ch);
-    else if (ch == 8) { o8(o, '\\'); o8(o, 'b'); }
-    else if (ch == 9) { o8(o, '\\'); o8(o, 't'); }
-    else if (ch == 10) { o8(o, '\\'); o8(o, 'n'); }
-    else if (ch == 12) { o8(o, '\\'); o8(o, 'f'); }
-    else if (ch == 13) { o8(o, '\\'); o8(o, 'r'); }
-    else { o8(o, '\\'); o8(o, 'u'); o8(o, '0'); o8(o, '0'); o8(o, '0' + (ch >> 4)); o8(o, "0123456789abcdef"[ch & 15]); }
-  }
-  o8(o, '"');
+struct SinkOut {
+  Out *o;
+  YM_INL void put(uint32_t b) { o8(*o, b); }
+};
+// canonical form of a value into an Out (counting when o.p == nullptr)
+YM_INL void canon_out(Ctx &c, Out &o, const uint8_t *A, uint64_t p, uint64_t end, uint8_t g, uint8_t t) {
+  SinkOut s = {&o};
+  canon_value(c, s, A, p, end, g, t);
 }
-YM_INL void e_json_x(Ctx &c, Enc &e, const Span &s) {
-  const uint8_t *a = c.A + s.off;
-  if (e.v2) {  // V1 text -> any
-    if (s.n == 4 && a[0] == 't' && a[1] == 'r' && a[2] == 'u' && a[3] == 'e') { o8(e.rest, 120); return; }
-    if (s.n == 5 && a[0] == 'f' && a[1] == 'a' && a[2] == 'l' && a[3] == 's' && a[4] == 'e') { o8(e.rest, 121); return; }
-    if (s.n == 4 && a[0] == 'n' && a[1] == 'u' && a[2] == 'l' && a[3] == 'l') { o8(e.rest, 126); return; }
-    if (s.n >= 2 && a[0] == '"') {  // a string without escapes: the UTF-8 bytes between the quotes
-      for (uint64_t i = 1; i + 1 < s.n; i++)
-        if (a[i] == '\\') { seterr(c, ST_UNSUPPORTED); return; }
-      o8(e.rest, 119);
-      ovu(e.rest, (int64_t)(s.n - 2));
-      ocopy(e.rest, c, s.off + 1, s.n - 2);
-      return;
-    }
-    // a canonical integer: -?(0|[1-9][0-9]*), |v| < 2^31 (writeAny: varInt)
-    uint64_t i = 0;
-    const bool neg = s.n > 0 && a[0] == '-';
-    if (neg) i++;
-    uint64_t v = 0;
-    if (i >= s.n || s.n - i > 10) { seterr(c, ST_UNSUPPORTED); return; }
-    for (; i < s.n; i++) {
-      if (a[i] < '0' || a[i] > '9') { seterr(c, ST_UNSUPPORTED); return; }
-      v = v * 10 + (a[i] - '0');
-    }
-    if (v >= 0x80000000ull || (neg && v == 0)) { seterr(c, ST_UNSUPPORTED); return; }
-    o8(e.rest, 125);
-    ovi(e.rest, neg, (uint32_t)v);
+// byte / UTF-16 length of a canonical JSON text
+YM_INL SinkLen canon_len(Ctx &c, const uint8_t *A, uint64_t p, uint64_t end, uint8_t g, uint8_t t) {
+  SinkLen n = {0, 0};
+  canon_value(c, n, A, p, end, g, t);
+  return n;
+}
+
+// writeString of a canonical JSON text (ContentJSON element: JSON.stringify(JSON.parse(text)))
+YM_BIG void e_json_string(Ctx &c, Enc &e, uint64_t off, uint64_t n) {
+  const uint64_t p = js_ws(c.A, off, off + n);
+  const SinkLen L = canon_len(c, c.A, p, off + n, G_JSON, T_JSON);
+  if (c.err) return;
+  if (e.v2) {
+    canon_out(c, e.sb, c.A, p, off + n, G_JSON, T_JSON);
+    uopt_w(e.sl, e.sl_s, e.sl_n, (uint32_t)L.u16);
+  } else {
+    ovu(e.rest, (int64_t)L.bytes);
+    canon_out(c, e.rest, c.A, p, off + n, G_JSON, T_JSON);
+  }
+}
+// writeJSON / writeAny of an embed or format value read as span s (V1: JSON text, V2: any), canonical.
+// Same format: V1 writeVarString(JSON.stringify(JSON.parse(text))), V2 writeAny(readAny(..)).
+// convertUpdateFormat (e.xfmt): V1 -> V2 writeAny(JSON.parse(text)); V2 -> V1
+// writeVarString(JSON.stringify(readAny(..))) (undefined -> the text "undefined", encodeURIComponent).
+YM_BIG void e_json_value(Ctx &c, Enc &e, const Span &s) {
+  const bool src_json = e.xfmt ? e.v2 != 0 : !e.v2;
+  if (src_json) {
+    const uint64_t p = js_ws(c.A, s.off, s.off + s.n);
+    if (e.v2) { canon_out(c, e.rest, c.A, p, s.off + s.n, G_JSON, T_ANY); return; }
+    const SinkLen L = canon_len(c, c.A, p, s.off + s.n, G_JSON, T_JSON);
+    if (c.err) return;
+    ovu(e.rest, (int64_t)L.bytes);
+    canon_out(c, e.rest, c.A, p, s.off + s.n, G_JSON, T_JSON);
     return;
   }
-  // V2 any -> V1 text
-  const uint32_t tag = a[0];
-  Out &o = e.rest;
-  switch (tag) {
-    case 120: ovu(o, 4); o8(o, 't'); o8(o, 'r'); o8(o, 'u'); o8(o, 'e'); return;
-    case 121: ovu(o, 5); o8(o, 'f'); o8(o, 'a'); o8(o, 'l'); o8(o, 's'); o8(o, 'e'); return;
-    case 126: ovu(o, 4); o8(o, 'n'); o8(o, 'u'); o8(o, 'l'); o8(o, 'l'); return;
-    case 127: ovu(o, 9); for (const char *t = "undefined"; *t; t++) o8(o, (uint32_t)*t); return;  // encodeURIComponent(undefined)
-    case 122: seterr(c, ST_TYPE); return;  // JSON.stringify(bigint)
-    case 125: {  // varInt (canonical, |v| < 2^32 -- rd_any_span validated it): decimal text, -0 -> "0"
-      uint64_t mag = a[1] & 63;
-      const bool neg = a[1] & 64;
-      uint32_t sh = 6;
-      for (uint64_t i = 1; i < s.n && (a[i] & 128); i++) { mag |= (uint64_t)(a[i + 1] & 127) << sh; sh += 7; }
-      char buf[24];
-      int n = 0;
-      do { buf[n++] = (char)('0' + mag % 10); mag /= 10; } while (mag);
-      const bool minus = neg && !(n == 1 && buf[0] == '0');
-      ovu(o, n + (minus ? 1 : 0));
-      if (minus) o8(o, '-');
-      while (n) o8(o, (uint32_t)buf[--n]);
-      return;
-    }
-    case 119: {  // string: JSON.stringify quoting of the UTF-8 bytes (valid UTF-8: no lone surrogates)
-      uint64_t p = 1;
-      uint64_t len = 0;
-      uint32_t sh = 0;
-      for (;;) {
-        const uint32_t b = a[p++];
-        len |= (uint64_t)(b & 127) << sh;
-        sh += 7;
-        if (!(b & 128)) break;
-      }
-      Out cnt = {nullptr, 0};
-      json_quote_bytes(c, cnt, s.off + p, len);
-      ovu(o, (int64_t)cnt.n);
-      json_quote_bytes(c, o, s.off + p, len);
-      return;
-    }
-    default: seterr(c, ST_UNSUPPORTED); return;  // floats, arrays, objects, byte arrays
+  if (!e.v2) {  // V2 any -> V1 JSON text
+    if (c.A[s.off] == 127) { ovu(e.rest, 9); for (const char *t = "undefined"; *t; t++) o8(e.rest, (uint32_t)*t); return; }
+    const SinkLen L = canon_len(c, c.A, s.off, s.off + s.n, G_ANY, T_JSONANY);
+    if (c.err) return;
+    ovu(e.rest, (int64_t)L.bytes);
+    canon_out(c, e.rest, c.A, s.off, s.off + s.n, G_ANY, T_JSONANY);
+    return;
   }
+  canon_out(c, e.rest, c.A, s.off, s.off + s.n, G_ANY, T_ANY);
 }
 
 // skip k JSON element strings of a ContentJSON starting at its first element (returns new start)
@@ -1127,7 +1111,11 @@ YM_BIG void content_write(Ctx &c, Enc &e, const SStruct &s, int64_t off) {
           utf8_check(c, t.off, t.n, &n16);
           t.n16 = n16;
         }
-        e_string(e, c, t);
+        // JSON.stringify(JSON.parse(text)) unless the element is 'undefined' (ContentJSON.js:83-90)
+        const bool und = t.n == 9 && c.A[t.off] == 'u' && c.A[t.off + 1] == 'n' && c.A[t.off + 2] == 'd' &&
+                         c.A[t.off + 3] == 'e' && c.A[t.off + 8] == 'd';
+        if (s.nca && !und) e_json_string(c, e, t.off, t.n);
+        else e_string(e, c, t);
         p = t.off + t.n;
       }
       break;
@@ -1152,13 +1140,13 @@ YM_BIG void content_write(Ctx &c, Enc &e, const SStruct &s, int64_t off) {
       break;
     }
     case 5:
-      if (e.xfmt) e_json_x(c, e, s.a);
+      if (e.xfmt || s.nca) e_json_value(c, e, s.a);
       else if (e.v2) ocopy(e.rest, c, s.a.off, s.a.n);
       else { ovu(e.rest, s.a.n); ocopy(e.rest, c, s.a.off, s.a.n); }
       break;
     case 6:
       e_key(e, c, s.a);
-      if (e.xfmt) e_json_x(c, e, s.b);
+      if (e.xfmt || s.ncb) e_json_value(c, e, s.b);
       else if (e.v2) ocopy(e.rest, c, s.b.off, s.b.n);
       else { ovu(e.rest, s.b.n); ocopy(e.rest, c, s.b.off, s.b.n); }
       break;
@@ -1169,10 +1157,32 @@ YM_BIG void content_write(Ctx &c, Enc &e, const SStruct &s, int64_t off) {
     case 8: {
       e_len(e, s.cnt - off);
       uint64_t p = off ? any_skip_n(c, s.a.off, s.a.n, off) : s.a.off;
-      ocopy(e.rest, c, p, s.a.off + s.a.n - p);
+      if (!s.nca) { ocopy(e.rest, c, p, s.a.off + s.a.n - p); break; }
+      for (int64_t i = off; i < s.cnt && !c.err; i++) {  // writeAny(readAny(..)) element by element
+        canon_out(c, e.rest, c.A, p, s.a.off + s.a.n, G_ANY, T_ANY);
+        p = any_end(c.A, p);
+      }
       break;
     }
-    case 9: e_string(e, c, s.a); ocopy(e.rest, c, s.b.off, s.b.n); break;
+    case 9: {
+      if (!s.ncb) { e_string(e, c, s.a); ocopy(e.rest, c, s.b.off, s.b.n); break; }
+      // new ContentDoc(new Doc({guid, ...opts})): the options re-derived, an own string `guid` wins
+      const DocOpts d = doc_opts(c, c.A, s.b.off, s.b.off + s.b.n);
+      if (c.err) break;
+      Span g = s.a;
+      if (d.has_guid) {
+        uint64_t q = d.guid_val;
+        const uint32_t L = cv_vu(c.A, q);
+        g.off = q; g.n = L; g.fffd = 0;
+        uint32_t n16 = 0;
+        utf8_check(c, q, L, &n16);
+        g.n16 = n16;
+      }
+      e_string(e, c, g);
+      SinkOut so = {&e.rest};
+      s_doc_opts(c, so, c.A, d, s.b.off + s.b.n);
+      break;
+    }
     default: seterr(c, ST_UNEXPECTED); break;
   }
 }
@@ -1899,6 +1909,71 @@ YM_BIG void dsmerge_doc(Ctx &c, DocWS &ws, const uint64_t *upd_off, uint32_t u0,
     L.ds_bytes = e.rest.n;
     L.total = e.rest.n;
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// The general path's per-document entry (k_general in ym_general.hip; the test-only host build in
+// tests/native/core_host.cpp runs the very same function on the CPU)
+// ------------------------------------------------------------------------------------------------
+enum : uint32_t { OP_MERGE = 0, OP_DIFF = 1, OP_SV = 2, OP_CONV = 3, OP_META = 4, OP_DSMERGE = 5 };
+
+struct GeneralWsSize {
+  uint64_t rs, arr, parts, ds, dsg, sv, total;
+  uint32_t parts_cap, sv_cap;
+  uint64_t ds_cap;
+};
+YM_INL uint64_t al16(uint64_t x) { return (x + 15) & ~(uint64_t)15; }
+YM_INL GeneralWsSize general_ws_size(uint32_t k, uint64_t bytes, uint32_t parts_mul, uint64_t svbytes) {
+  GeneralWsSize z;
+  z.rs = al16((uint64_t)(k ? k : 1) * sizeof(Reader));
+  z.arr = al16((uint64_t)(k + 1) * 4);
+  z.parts_cap = (uint32_t)((2ull * k + 16) * parts_mul);
+  z.parts = al16((uint64_t)z.parts_cap * sizeof(PartRec));
+  z.ds_cap = bytes / 2 + 2;  // every delete-set entry occupies >= 2 input bytes
+  z.ds = al16(z.ds_cap * sizeof(DSE));
+  z.dsg = al16(z.ds_cap * sizeof(DSG));
+  z.sv_cap = (uint32_t)(svbytes / 2 + 2);
+  z.sv = al16((uint64_t)z.sv_cap * 16);
+  z.total = z.rs + 2 * z.arr + z.parts + z.ds + z.dsg + z.sv;
+  return z;
+}
+// the state-vector table: diff = the decoded state vector; meta = (client, from, to) triples, at most one
+// client per update byte
+YM_INL uint64_t general_sv_bytes(uint32_t op, uint64_t svlen, uint64_t bytes) {
+  if (op == OP_DIFF) return svlen;
+  if (op == OP_META) return 3 * bytes + 6;
+  return 0;
+}
+YM_INL void general_carve(uint8_t *p, const GeneralWsSize &z, DocWS &w) {
+  w.rs = (Reader *)p; p += z.rs;
+  w.arr = (uint32_t *)p; p += z.arr;
+  w.tmp = (uint32_t *)p; p += z.arr;
+  w.parts = (PartRec *)p; p += z.parts; w.parts_cap = z.parts_cap;
+  w.ds = (DSE *)p; p += z.ds; w.ds_cap = z.ds_cap;
+  w.dsg = (DSG *)p; p += z.dsg;
+  w.sv = (int64_t *)p; w.sv_cap = z.sv_cap;
+}
+// One document, pass 1 (sizes into L) or 2 (writes to out).  Document = updates u0 .. u0+k-1 of the
+// arena (upd_off absolute); sv = its encoded state vector (diff).  Status in c.err.
+YM_BIG void general_doc(Ctx &c, DocWS &w, uint32_t op, uint32_t v2, const uint64_t *upd_off, uint32_t u0, uint32_t k,
+                        const uint8_t *sv, uint64_t svlen, int pass, Layout &L, uint8_t *out) {
+  if (op == OP_MERGE) {
+    if (k == 1) {  // `if (updates.length === 1) return updates[0]`
+      uint64_t n = upd_off[u0 + 1] - upd_off[u0];
+      if (pass == 1) { __builtin_memset(&L, 0, sizeof(Layout)); L.total = n; }
+      else for (uint64_t b = 0; b < n; b++) out[b] = c.A[upd_off[u0] + b];
+    } else {
+      merge_doc(c, w, upd_off, u0, k, v2, pass, L, out);
+    }
+    return;
+  }
+  if (op == OP_DSMERGE) { dsmerge_doc(c, w, upd_off, u0, k, v2, pass, L, out); return; }
+  if (k != 1) { c.err = ST_UNEXPECTED; return; }
+  const uint64_t uoff = upd_off[u0], ulen = upd_off[u0 + 1] - upd_off[u0];
+  if (op == OP_DIFF) diff_doc(c, w, uoff, ulen, sv, svlen, v2, pass, L, out);
+  else if (op == OP_META) meta_doc(c, w, uoff, ulen, v2, pass, L, out);
+  else if (op == OP_CONV) conv_doc(c, w, uoff, ulen, v2, pass, L, out);
+  else sv_doc(c, w, uoff, ulen, v2, pass, L, out);
 }
 
 }  // namespace ym

@@ -7,7 +7,12 @@
 
 namespace ymk {
 
-enum : uint32_t { OP_MERGE = 0, OP_DIFF = 1, OP_SV = 2, OP_CONV = 3, OP_META = 4, OP_DSMERGE = 5 };
+using ym::OP_MERGE;
+using ym::OP_DIFF;
+using ym::OP_SV;
+using ym::OP_CONV;
+using ym::OP_META;
+using ym::OP_DSMERGE;
 
 // internal status: document not taken by the fast path, routed to the general path
 constexpr int ST_PENDING = 101;
@@ -57,25 +62,8 @@ struct LargeBufs {
 // status OK; the rest keep ST_PENDING.  Returns 1 when launched, 0 when not applicable, < 0 on error.
 int large_run(const GeneralJob &j, const uint32_t *list, uint32_t n, hipStream_t st, LargeBufs &B);
 
-struct GeneralWsSize {
-  uint64_t rs, arr, parts, ds, dsg, sv, total;
-  uint32_t parts_cap, sv_cap;
-  uint64_t ds_cap;
-};
-__host__ __device__ inline uint64_t al16(uint64_t x) { return (x + 15) & ~(uint64_t)15; }
-__host__ __device__ inline GeneralWsSize general_ws_size(uint32_t k, uint64_t bytes, uint32_t parts_mul, uint64_t svbytes) {
-  GeneralWsSize z;
-  z.rs = al16((uint64_t)(k ? k : 1) * sizeof(ym::Reader));
-  z.arr = al16((uint64_t)(k + 1) * 4);
-  z.parts_cap = (uint32_t)((2ull * k + 16) * parts_mul);
-  z.parts = al16((uint64_t)z.parts_cap * sizeof(ym::PartRec));
-  z.ds_cap = bytes / 2 + 2;  // every delete-set entry occupies >= 2 input bytes
-  z.ds = al16(z.ds_cap * sizeof(ym::DSE));
-  z.dsg = al16(z.ds_cap * sizeof(ym::DSG));
-  z.sv_cap = (uint32_t)(svbytes / 2 + 2);
-  z.sv = al16((uint64_t)z.sv_cap * 16);
-  z.total = z.rs + 2 * z.arr + z.parts + z.ds + z.dsg + z.sv;
-  return z;
-}
+using ym::GeneralWsSize;
+using ym::general_ws_size;
+using ym::al16;
 
 }  // namespace ymk
