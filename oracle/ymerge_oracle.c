@@ -23,10 +23,9 @@
  *   LazyStructWriter write/flush/finish (ps/gs/ws) ........... 13.5.16 @41236-41700
  *   encodeStateVectorFromUpdateV2 (os) ....................... 13.5.16 @37724
  *   decodeStateVector (Fe/Ve) ................................ src/utils/encoding.js:536-565
- * The per-iteration reader sort of mergeUpdates emulates V8's Array.prototype.sort (TimSort: run
- * detection + binary insertion for < 64 readers); for >= 64 readers a stable merge sort is used, which
- * is exact whenever the comparator is consistent (it is not when a GC and an Item tie on (client,clock);
- * such inputs with >= 64 readers report YMO_ERR_UNSUPPORTED).
+ * The per-iteration reader sort of mergeUpdates restates V8's Array.prototype.sort (TimSort with
+ * galloping merges) operation by operation: the comparator is inconsistent when a GC and an Item tie
+ * on (client, clock), so the output order depends on exactly which pairs V8 compares.
  * JS values: numbers are IEEE doubles, strings are UTF-16 code-unit arrays, object property order
  * follows OrdinaryOwnPropertyKeys (array-index keys ascending, then insertion order).
  */
@@ -48,7 +47,6 @@ typedef struct Ctx {
   Chunk *chunks;
   int v2;
   int inconsistent_cmp; /* a GC/Item tie was compared during a reader sort */
-  int big_inconsistent; /* ... during a sort of >= 64 readers (emulated by a merge sort) */
 } Ctx;
 
 static void ctx_free(Ctx *c) {
@@ -995,10 +993,14 @@ static Str ud_string(Ctx *c, UDec *u) { return u->v2 ? sdec_read(c, &u->str) : r
 static int ud_parent_info(Ctx *c, UDec *u) { return u->v2 ? rle_read(c, &u->parentInfo) == 1 : rd_vu(c, &u->rest) == 1; }
 static int64_t ud_typeref(Ctx *c, UDec *u) { return u->v2 ? uopt_read(c, &u->typeRef) : (int64_t)rd_vu(c, &u->rest); }
 static int64_t ud_len(Ctx *c, UDec *u) { return u->v2 ? uopt_read(c, &u->len) : (int64_t)rd_vu(c, &u->rest); }
+/* readKey (UpdateDecoder.js:382-391): `keyClock < this.keys.length ? this.keys[keyClock] : read` -- a
+   negative keyClock indexes nothing: the key is `undefined` (K_UNDEF_KEY) */
+static const uint16_t K_UNDEF_KEY[1] = {0};
 static Str ud_key(Ctx *c, UDec *u) {
   if (!u->v2) return rd_vstr(c, &u->rest);
   int64_t kc = idiff_read(c, &u->keyClock);
-  if (kc >= 0 && (size_t)kc < u->nkeys) return u->keys[kc];
+  if (kc < 0) { Str un = {K_UNDEF_KEY, 0}; return un; }
+  if ((size_t)kc < u->nkeys) return u->keys[kc];
   Str s = sdec_read(c, &u->str);
   if (u->nkeys == u->capkeys) {
     size_t cap = u->capkeys ? u->capkeys * 2 : 8;
@@ -1080,6 +1082,14 @@ static void ue_len(Ctx *c, UEnc *e, int64_t l) {
   else wr_vu(c, e->rest, l);
 }
 static void ue_key(Ctx *c, UEnc *e, Str k) {
+  if (k.u == K_UNDEF_KEY) {  /* writeKey(undefined): V2 StringEncoder reads undefined.length (TypeError);
+                                V1 writeVarString(undefined) writes encodeURIComponent(undefined) = "undefined" */
+    if (e->v2) fail(c, YMO_ERR_TYPE);
+    static const uint16_t und[] = {'u', 'n', 'd', 'e', 'f', 'i', 'n', 'e', 'd'};
+    Str us = {und, 9};
+    wr_vstr(c, e->rest, us);
+    return;
+  }
   if (e->v2) { idiff_write(c, &e->keyClock, e->keyClockCounter++); senc_write(c, &e->str, k); }
   else wr_vstr(c, e->rest, k);
 }
@@ -1247,7 +1257,14 @@ static Content *read_content(Ctx *c, UDec *u, int info) { /* readItemContent / c
       int64_t tr = ud_typeref(c, u);
       if (tr < 0 || tr > 6) fail(c, YMO_ERR_TYPE);
       ct->typeRef = tr;
-      if (tr == 3 || tr == 5) ct->typeName = ud_key(c, u);
+      if (tr == 3 || tr == 5) {
+        ct->typeName = ud_key(c, u);
+        if (tr == 3 && ct->typeName.u == K_UNDEF_KEY) { /* new YXmlElement(undefined): nodeName = 'UNDEFINED' */
+          static const uint16_t un[] = {'U', 'N', 'D', 'E', 'F', 'I', 'N', 'E', 'D'};
+          Str us = {un, 9};
+          ct->typeName = us;
+        }
+      }
       break;
     }
     case 8: {
@@ -1624,47 +1641,270 @@ static int reader_cmp(Ctx *c, const LReader *a, const LReader *b) {
   return y->client - x->client < 0 ? -1 : 1;
 }
 
-/* V8 TimSort for n < 64: CountAndMakeRun + BinaryInsertionSort (third_party/v8/builtins/array-sort.tq) */
+/* V8's Array.prototype.sort (TimSort, third_party/v8/builtins/array-sort.tq of the reference's Node):
+ * runs found by CountAndMakeRun and extended to minrun by BinaryInsertionSort, a pending-run stack
+ * collapsed by MergeCollapse, merges by MergeLow / MergeHigh with galloping (minGallop starts at 7).
+ * Restated operation by operation because the reader comparator is inconsistent for a GC / Item tie
+ * (compare(a, b) = compare(b, a) = -1): the order then depends on exactly which pairs are compared. */
+typedef struct {
+  Ctx *c;
+  LReader **a, **tmp;
+  size_t base[80], len[80];
+  int nruns;
+  long min_gallop;
+} TS;
+#define TS_CMP(x, y) reader_cmp(ts->c, (x), (y))
+static long ts_gallop_left(TS *ts, LReader **arr, LReader *key, long base, long length, long hint) {
+  long last = 0, ofs = 1;
+  if (TS_CMP(arr[base + hint], key) < 0) {
+    long maxo = length - hint;
+    while (ofs < maxo) {
+      if (TS_CMP(arr[base + hint + ofs], key) >= 0) break;
+      last = ofs;
+      ofs = (ofs << 1) + 1;
+      if (ofs <= 0) ofs = maxo;
+    }
+    if (ofs > maxo) ofs = maxo;
+    last += hint;
+    ofs += hint;
+  } else {
+    long maxo = hint + 1;
+    while (ofs < maxo) {
+      if (TS_CMP(arr[base + hint - ofs], key) < 0) break;
+      last = ofs;
+      ofs = (ofs << 1) + 1;
+      if (ofs <= 0) ofs = maxo;
+    }
+    if (ofs > maxo) ofs = maxo;
+    long t = last;
+    last = hint - ofs;
+    ofs = hint - t;
+  }
+  last++;
+  while (last < ofs) {
+    long m = last + ((ofs - last) >> 1);
+    if (TS_CMP(arr[base + m], key) < 0) last = m + 1; else ofs = m;
+  }
+  return ofs;
+}
+static long ts_gallop_right(TS *ts, LReader **arr, LReader *key, long base, long length, long hint) {
+  long last = 0, ofs = 1;
+  if (TS_CMP(key, arr[base + hint]) < 0) {
+    long maxo = hint + 1;
+    while (ofs < maxo) {
+      if (TS_CMP(key, arr[base + hint - ofs]) >= 0) break;
+      last = ofs;
+      ofs = (ofs << 1) + 1;
+      if (ofs <= 0) ofs = maxo;
+    }
+    if (ofs > maxo) ofs = maxo;
+    long t = last;
+    last = hint - ofs;
+    ofs = hint - t;
+  } else {
+    long maxo = length - hint;
+    while (ofs < maxo) {
+      if (TS_CMP(key, arr[base + hint + ofs]) < 0) break;
+      last = ofs;
+      ofs = (ofs << 1) + 1;
+      if (ofs <= 0) ofs = maxo;
+    }
+    if (ofs > maxo) ofs = maxo;
+    last += hint;
+    ofs += hint;
+  }
+  last++;
+  while (last < ofs) {
+    long m = last + ((ofs - last) >> 1);
+    if (TS_CMP(key, arr[base + m]) < 0) ofs = m; else last = m + 1;
+  }
+  return ofs;
+}
+static void ts_merge_low(TS *ts, long baseA, long lenA, long baseB, long lenB) {
+  LReader **a = ts->a, **t = ts->tmp;
+  memcpy(t, a + baseA, lenA * sizeof(LReader *));
+  long dest = baseA, ct = 0, cb = baseB;
+  a[dest++] = a[cb++];
+  if (--lenB == 0) goto succeed;
+  if (lenA == 1) goto copy_b;
+  for (;;) {
+    long wa = 0, wb = 0;
+    for (;;) {
+      if (TS_CMP(a[cb], t[ct]) < 0) {
+        a[dest++] = a[cb++]; wb++; lenB--; wa = 0;
+        if (lenB == 0) goto succeed;
+        if (wb >= ts->min_gallop) break;
+      } else {
+        a[dest++] = t[ct++]; wa++; lenA--; wb = 0;
+        if (lenA == 1) goto copy_b;
+        if (wa >= ts->min_gallop) break;
+      }
+    }
+    ts->min_gallop++;
+    int first = 1;
+    while (wa >= 7 || wb >= 7 || first) {
+      first = 0;
+      ts->min_gallop = ts->min_gallop - 1 > 1 ? ts->min_gallop - 1 : 1;
+      wa = ts_gallop_right(ts, t, a[cb], ct, lenA, 0);
+      if (wa > 0) {
+        memcpy(a + dest, t + ct, wa * sizeof(LReader *));
+        dest += wa; ct += wa; lenA -= wa;
+        if (lenA == 1) goto copy_b;
+        if (lenA == 0) goto succeed;
+      }
+      a[dest++] = a[cb++];
+      if (--lenB == 0) goto succeed;
+      wb = ts_gallop_left(ts, a, t[ct], cb, lenB, 0);
+      if (wb > 0) {
+        memmove(a + dest, a + cb, wb * sizeof(LReader *));
+        dest += wb; cb += wb; lenB -= wb;
+        if (lenB == 0) goto succeed;
+      }
+      a[dest++] = t[ct++];
+      if (--lenA == 1) goto copy_b;
+    }
+    ts->min_gallop++;
+  }
+succeed:
+  if (lenA > 0) memcpy(a + dest, t + ct, lenA * sizeof(LReader *));
+  return;
+copy_b:
+  memmove(a + dest, a + cb, lenB * sizeof(LReader *));
+  a[dest + lenB] = t[ct];
+}
+static void ts_merge_high(TS *ts, long baseA, long lenA, long baseB, long lenB) {
+  LReader **a = ts->a, **t = ts->tmp;
+  memcpy(t, a + baseB, lenB * sizeof(LReader *));
+  long dest = baseB + lenB - 1, ct = lenB - 1, ca = baseA + lenA - 1;
+  a[dest--] = a[ca--];
+  if (--lenA == 0) goto succeed;
+  if (lenB == 1) goto copy_a;
+  for (;;) {
+    long wa = 0, wb = 0;
+    for (;;) {
+      if (TS_CMP(t[ct], a[ca]) < 0) {
+        a[dest--] = a[ca--]; wa++; lenA--; wb = 0;
+        if (lenA == 0) goto succeed;
+        if (wa >= ts->min_gallop) break;
+      } else {
+        a[dest--] = t[ct--]; wb++; lenB--; wa = 0;
+        if (lenB == 1) goto copy_a;
+        if (wb >= ts->min_gallop) break;
+      }
+    }
+    ts->min_gallop++;
+    int first = 1;
+    while (wa >= 7 || wb >= 7 || first) {
+      first = 0;
+      ts->min_gallop = ts->min_gallop - 1 > 1 ? ts->min_gallop - 1 : 1;
+      long k = ts_gallop_right(ts, a, t[ct], baseA, lenA, lenA - 1);
+      wa = lenA - k;
+      if (wa > 0) {
+        dest -= wa; ca -= wa;
+        memmove(a + dest + 1, a + ca + 1, wa * sizeof(LReader *));
+        lenA -= wa;
+        if (lenA == 0) goto succeed;
+      }
+      a[dest--] = t[ct--];
+      if (--lenB == 1) goto copy_a;
+      k = ts_gallop_left(ts, t, a[ca], 0, lenB, lenB - 1);
+      wb = lenB - k;
+      if (wb > 0) {
+        dest -= wb; ct -= wb;
+        memcpy(a + dest + 1, t + ct + 1, wb * sizeof(LReader *));
+        lenB -= wb;
+        if (lenB == 1) goto copy_a;
+        if (lenB == 0) goto succeed;
+      }
+      a[dest--] = a[ca--];
+      if (--lenA == 0) goto succeed;
+    }
+    ts->min_gallop++;
+  }
+succeed:
+  if (lenB > 0) memcpy(a + dest - (lenB - 1), t, lenB * sizeof(LReader *));
+  return;
+copy_a:
+  dest -= lenA; ca -= lenA;
+  memmove(a + dest + 1, a + ca + 1, lenA * sizeof(LReader *));
+  a[dest] = t[ct];
+}
+static void ts_merge_at(TS *ts, int i) {
+  long baseA = (long)ts->base[i], lenA = (long)ts->len[i], baseB = (long)ts->base[i + 1], lenB = (long)ts->len[i + 1];
+  ts->len[i] = lenA + lenB;
+  if (i == ts->nruns - 3) { ts->base[i + 1] = ts->base[i + 2]; ts->len[i + 1] = ts->len[i + 2]; }
+  ts->nruns--;
+  long k = ts_gallop_right(ts, ts->a, ts->a[baseB], baseA, lenA, 0);
+  baseA += k;
+  lenA -= k;
+  if (lenA == 0) return;
+  lenB = ts_gallop_left(ts, ts->a, ts->a[baseA + lenA - 1], baseB, lenB, lenB - 1);
+  if (lenB == 0) return;
+  if (lenA <= lenB) ts_merge_low(ts, baseA, lenA, baseB, lenB);
+  else ts_merge_high(ts, baseA, lenA, baseB, lenB);
+}
+static int ts_inv(TS *ts, int n) { return n < 2 || ts->len[n - 2] > ts->len[n - 1] + ts->len[n]; }
 static void v8_sort(Ctx *c, LReader **a, size_t n, LReader **tmp) {
   if (n < 2) return;
-  if (n < 64) {
-    size_t run = 2;
-    int order = reader_cmp(c, a[1], a[0]);
-    int desc = order < 0;
-    LReader *prev = a[1];
-    for (size_t i = 2; i < n; i++) {
-      order = reader_cmp(c, a[i], prev);
-      if (desc) { if (order >= 0) break; }
-      else if (order < 0) break;
-      prev = a[i];
-      run++;
-    }
-    if (desc) for (size_t i = 0, j = run - 1; i < j; i++, j--) { LReader *t = a[i]; a[i] = a[j]; a[j] = t; }
-    for (size_t start = run; start < n; start++) {
-      LReader *pivot = a[start];
-      size_t left = 0, right = start;
-      while (left < right) {
-        size_t mid = left + ((right - left) >> 1);
-        if (reader_cmp(c, pivot, a[mid]) < 0) right = mid; else left = mid + 1;
+  TS ts_;
+  TS *ts = &ts_;
+  ts->c = c; ts->a = a; ts->tmp = tmp; ts->nruns = 0; ts->min_gallop = 7;
+  long remaining = (long)n, low = 0;
+  long minrun = remaining, r = 0;
+  while (minrun >= 64) { r |= minrun & 1; minrun >>= 1; }
+  minrun += r;
+  while (remaining != 0) {
+    /* CountAndMakeRun(low, low + remaining) */
+    long run;
+    if (remaining == 1) run = 1;
+    else {
+      run = 2;
+      int desc = TS_CMP(a[low + 1], a[low]) < 0;
+      LReader *prev = a[low + 1];
+      for (long i = low + 2; i < low + remaining; i++) {
+        int o = TS_CMP(a[i], prev);
+        if (desc ? o >= 0 : o < 0) break;
+        prev = a[i];
+        run++;
       }
-      for (size_t p = start; p > left; p--) a[p] = a[p - 1];
-      a[left] = pivot;
+      if (desc) for (long i = low, j = low + run - 1; i < j; i++, j--) { LReader *x = a[i]; a[i] = a[j]; a[j] = x; }
     }
-    return;
+    if (run < minrun) {
+      long forced = minrun < remaining ? minrun : remaining;
+      /* BinaryInsertionSort(low, low + run, low + forced) */
+      for (long start = low + run; start < low + forced; start++) {
+        LReader *pivot = a[start];
+        long left = low, right = start;
+        while (left < right) {
+          long mid = left + ((right - left) >> 1);
+          if (TS_CMP(pivot, a[mid]) < 0) right = mid; else left = mid + 1;
+        }
+        for (long p = start; p > left; p--) a[p] = a[p - 1];
+        a[left] = pivot;
+      }
+      run = forced;
+    }
+    ts->base[ts->nruns] = (size_t)low;
+    ts->len[ts->nruns] = (size_t)run;
+    ts->nruns++;
+    /* MergeCollapse */
+    while (ts->nruns > 1) {
+      int m = ts->nruns - 2;
+      if (!ts_inv(ts, m + 1) || !ts_inv(ts, m)) {
+        if (ts->len[m - 1] < ts->len[m + 1]) m--;
+        ts_merge_at(ts, m);
+      } else if (ts->len[m] <= ts->len[m + 1]) {
+        ts_merge_at(ts, m);
+      } else break;
+    }
+    low += run;
+    remaining -= run;
   }
-  /* stable merge sort (exact for a consistent comparator) */
-  int saved = c->inconsistent_cmp;
-  c->inconsistent_cmp = 0;
-  size_t h = n / 2;
-  v8_sort(c, a, h, tmp);
-  v8_sort(c, a + h, n - h, tmp);
-  size_t i = 0, j = h, k = 0;
-  while (i < h && j < n) tmp[k++] = (reader_cmp(c, a[j], a[i]) < 0) ? a[j++] : a[i++];
-  while (i < h) tmp[k++] = a[i++];
-  while (j < n) tmp[k++] = a[j++];
-  memcpy(a, tmp, n * sizeof(LReader *));
-  if (c->inconsistent_cmp) c->big_inconsistent = 1;
-  c->inconsistent_cmp = saved;
+  while (ts->nruns > 1) { /* MergeForceCollapse */
+    int m = ts->nruns - 2;
+    if (m > 0 && ts->len[m - 1] < ts->len[m + 1]) m--;
+    ts_merge_at(ts, m);
+  }
 }
 
 static int struct_merge_with(Struct *cur, const Struct *s) { /* GC/Skip.mergeWith; Item never merges */
@@ -1744,7 +1984,6 @@ static Buf *merge_impl(Ctx *c, const uint8_t *const *upds, const size_t *lens, s
   }
   if (cur) lw_write(c, &w, cur, 0);
   lw_finish(c, &w);
-  if (c->big_inconsistent) fail(c, YMO_ERR_UNSUPPORTED);
   DSet *dss = (DSet *)aalloc(c, (n + 1) * sizeof(DSet));
   for (size_t i = 0; i < n; i++) ds_read(c, &decs[i], &dss[i]);
   DSet merged;

@@ -53,7 +53,7 @@ int main(int argc, char **argv) {
     int st = ST_RETRY;
     std::vector<uint8_t> out;
     for (uint32_t mul = 1, round = 0; st == ST_RETRY && round < 7; mul *= 8, round++) {
-      const GeneralWsSize z = general_ws_size(k, bytes, mul, general_sv_bytes(op, svlen, bytes));
+      const GeneralWsSize z = general_ws_size(k, bytes, mul, general_sv_bytes(op, svlen, bytes), v2);
       std::vector<uint8_t> ws(z.total + 16);
       DocWS w;
       general_carve(ws.data(), z, w);

@@ -333,7 +333,10 @@ int run_general(DevState *S, hipStream_t st, GeneralJob j, uint32_t *list, uint3
 int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *stats, int depth = 0) {
   if (!b || !out) return -1;
   DevState *S = state();
-  HIPCHK(hipSetDevice(S->device));  // the caller (e.g. torch) may have switched this thread's device
+  {  // the caller (e.g. torch) may have switched this thread's device
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || cur != S->device) HIPCHK(hipSetDevice(S->device));
+  }
   hipStream_t st = stream ? (hipStream_t)stream : S->stream;
   uint32_t nd = b->n_docs;
   if (stats) memset(stats, 0, sizeof(*stats));

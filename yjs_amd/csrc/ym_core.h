@@ -94,13 +94,18 @@ YM_INL VI rd_vi(Ctx &c, Rd &d) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// strings: spans of UTF-8 bytes; fffd = a U+FFFD prefix synthesised by ContentString.splice
+// strings: spans of UTF-8 bytes; fffd = a U+FFFD prefix synthesised by ContentString.splice.  A V2
+// string column is one UTF-8 string sliced by UTF-16 lengths (StringDecoder), so a slice can start with
+// the low half (lo) or end with the high half (hi) of a surrogate pair whose 4 UTF-8 bytes sit just
+// before off / just after off + n; those halves are not part of the n bytes.
 // ------------------------------------------------------------------------------------------------
 struct Span {
   uint64_t off;   // absolute
-  uint32_t n;     // bytes (excluding the fffd prefix)
-  uint32_t n16;   // UTF-16 length (including the fffd prefix)
-  uint32_t fffd;  // 1: string starts with U+FFFD (3 extra UTF-8 bytes)
+  uint32_t n;     // bytes (excluding the fffd prefix and the lo / hi halves)
+  uint32_t n16;   // UTF-16 length (including the fffd prefix and the lo / hi halves)
+  uint8_t fffd;   // 1: string starts with U+FFFD (3 extra UTF-8 bytes)
+  uint8_t lo, hi; // starts with a lone low surrogate / ends with a lone high surrogate
+  uint8_t pad;
 };
 YM_INL uint32_t span_bytes(const Span &s) { return s.n + (s.fffd ? 3u : 0u); }
 
@@ -576,6 +581,7 @@ struct SStruct {
   uint64_t lsb;    // V2 ContentJSON: byte offset (absolute) of the first element
   uint8_t kind, ref, has_origin, has_right, parent_kind, has_psub;
   uint8_t nca, ncb;  // payload a / b not in the form yjs re-encodes it to: written through ym_canon.h
+  uint8_t keyundef;  // ContentType element / hook name read by readKey as `undefined` (negative keyClock)
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -594,9 +600,12 @@ struct Reader {
   RleCol in, pi;
   uint64_t str_off, str_n;  // decoded string column (UTF-8), absolute
   uint64_t spos_b;          // string decoder byte position (relative to str_off)
+  uint32_t mid;             // ... inside a surrogate pair (the high half was sliced off)
   int64_t spos16;           // ... in UTF-16 units
   uint64_t str_n16;
   uint32_t nkeys;
+  Span *keys;        // V2 readKey cache (the keys read so far), keys_cap entries of the doc's workspace
+  uint32_t keys_cap;
   int64_t dsCurr;
   SStruct curr;
 };
@@ -631,20 +640,26 @@ YM_BIG void reader_open(Ctx &c, Reader &r, uint64_t off, uint64_t len, uint32_t 
   r.ln.d = col_view(c, r.rest);
 }
 
-// V2 StringDecoder.read: slice the decoded column by the next UTF-16 length
+// V2 StringDecoder.read: `str.slice(spos, spos + len)` of the decoded column; a slice boundary may fall
+// inside a surrogate pair (r.mid: the column position is past the high half of the 4-byte character at
+// spos_b), giving strings that start / end with a lone surrogate (Span lo / hi)
 YM_BIG Span sdec_read(Ctx &c, Reader &r) {
   uint32_t L = uopt_read(c, r.sl);
-  Span s = {r.str_off + r.spos_b, 0, 0, 0};
+  Span s = {r.str_off + r.spos_b, 0, 0, 0, 0, 0, 0};
   if (c.err) return s;
   int64_t t = r.spos16 + (int64_t)L;
   if (r.spos16 >= (int64_t)r.str_n16) { r.spos16 = t; return s; }  // slice past the end: ""
   int64_t take = t > (int64_t)r.str_n16 ? (int64_t)r.str_n16 - r.spos16 : (int64_t)L;
+  int64_t units = take;
+  uint64_t pb = r.spos_b;
+  if (r.mid && units > 0) { s.lo = 1; pb += 4; units--; r.mid = 0; }
   int split = 0;
-  uint64_t nb = utf8_unit_offset(c, r.str_off + r.spos_b, r.str_n - r.spos_b, (uint64_t)take, &split);
-  if (split || (r.spos16 > 0 && r.spos_b == 0 && false)) { seterr(c, ST_UNSUPPORTED); return s; }  // slice inside a surrogate pair
+  uint64_t nb = utf8_unit_offset(c, r.str_off + pb, r.str_n - pb, (uint64_t)units, &split);
+  s.off = r.str_off + pb;
   s.n = (uint32_t)nb;
   s.n16 = (uint32_t)take;
-  r.spos_b += nb;
+  if (split) { s.hi = 1; r.mid = 1; }  // the character at pb + nb: its low half starts the next slice
+  r.spos_b = pb + nb;
   r.spos16 = t;
   return s;
 }
@@ -734,6 +749,7 @@ YM_BIG void read_content(Ctx &c, Reader &r, SStruct &s, int info) {
       for (int64_t i = 0; i < s.cnt && !c.err; i++) {
         Span t = rd_string(c, r);
         if (c.err) break;
+        if (t.lo || t.hi) { seterr(c, ST_SYNTAX); break; }  // a lone surrogate at either end: not JSON
         bool und = t.n == 9;
         const char *u = "undefined";
         for (uint32_t q = 0; und && q < 9; q++)
@@ -764,13 +780,17 @@ YM_BIG void read_content(Ctx &c, Reader &r, SStruct &s, int info) {
       if (c.err) break;
       if (t < 0 || t > 6) { seterr(c, ST_TYPE); break; }
       s.cnt = t;
-      if (t == 3 || t == 5) {  // readKey
+      s.len = 1;
+      if (t == 3 || t == 5) {  // readKey (UpdateDecoder.js:382-391)
         if (r.v2) {
           int64_t kc = idiff_read(c, r.kc);
           if (c.err) break;
-          if (kc >= 0 && (uint64_t)kc < r.nkeys) { seterr(c, ST_UNSUPPORTED); break; }  // cached key reference
+          if (kc < 0) { s.keyundef = 1; break; }  // keys[negative]: undefined
+          if ((uint64_t)kc < r.nkeys) { s.a = r.keys[kc]; break; }  // a cached key
           s.a = sdec_read(c, r);
-          r.nkeys++;
+          if (c.err) break;
+          if (r.nkeys >= r.keys_cap) { seterr(c, ST_RETRY); break; }
+          r.keys[r.nkeys++] = s.a;
         } else {
           s.a = rd_vstr(c, r.rest);
         }
@@ -909,6 +929,7 @@ struct Enc {
   int64_t in_n, pi_n;
   int64_t keyClock;
   int64_t dsCurr;
+  uint32_t pend_hi;  // V2 string column: a lone high surrogate ended the last string written (0: none)
 };
 YM_INL void enc_init(Enc &e, uint32_t v2) {
   __builtin_memset(&e, 0, sizeof(Enc));
@@ -966,8 +987,32 @@ YM_INL void e_info(Enc &e, int info) {
   if (e.v2) rle_w(e.in, e.in_s, e.in_n, info);
   else o8(e.rest, (uint32_t)info);
 }
-YM_INL void e_string(Enc &e, const Ctx &c, const Span &s) {
-  if (e.v2) { ostr_bytes(e.sb, c, s); uopt_w(e.sl, e.sl_s, e.sl_n, s.n16); }
+// the surrogate halves of the 4-byte UTF-8 character at A[o]
+YM_INL uint32_t sur_hi(const Ctx &c, uint64_t o) {
+  const uint32_t cp = ((c.A[o] & 7u) << 18) | ((c.A[o + 1] & 63u) << 12) | ((c.A[o + 2] & 63u) << 6) | (c.A[o + 3] & 63u);
+  return 0xD800 + ((cp - 0x10000) >> 10);
+}
+YM_INL uint32_t sur_lo(const Ctx &c, uint64_t o) {
+  const uint32_t cp = ((c.A[o] & 7u) << 18) | ((c.A[o + 1] & 63u) << 12) | ((c.A[o + 2] & 63u) << 6) | (c.A[o + 3] & 63u);
+  return 0xDC00 + ((cp - 0x10000) & 0x3FF);
+}
+// writeString: V1 writeVarString (a lone surrogate throws URIError); V2 StringEncoder.write: the column
+// is one string, so a string ending with a lone high surrogate pairs with the next one's leading lone
+// low surrogate (any other lone half makes toUint8Array's writeVarString throw URIError)
+YM_INL void e_str_bytes(Enc &e, Ctx &c, const Span &s) {
+  if (s.lo) {
+    if (!e.pend_hi) { seterr(c, ST_URI); return; }
+    const uint32_t cp = 0x10000 + ((e.pend_hi - 0xD800) << 10) + (sur_lo(c, s.off - 4) - 0xDC00);
+    o8(e.sb, 0xF0 | (cp >> 18)); o8(e.sb, 0x80 | ((cp >> 12) & 63)); o8(e.sb, 0x80 | ((cp >> 6) & 63)); o8(e.sb, 0x80 | (cp & 63));
+    e.pend_hi = 0;
+  }
+  if (e.pend_hi && (s.fffd || s.n || s.hi)) { seterr(c, ST_URI); return; }
+  ostr_bytes(e.sb, c, s);
+  if (s.hi) e.pend_hi = sur_hi(c, s.off + s.n);
+}
+YM_INL void e_string(Enc &e, Ctx &c, const Span &s) {
+  if (e.v2) { e_str_bytes(e, c, s); uopt_w(e.sl, e.sl_s, e.sl_n, s.n16); }
+  else if (s.lo || s.hi) seterr(c, ST_URI);
   else { ovu(e.rest, span_bytes(s)); ostr_bytes(e.rest, c, s); }
 }
 YM_INL void e_parent_info(Enc &e, int ykey) {
@@ -982,12 +1027,14 @@ YM_INL void e_len(Enc &e, int64_t l) {
   if (e.v2) uopt_w(e.ln, e.ln_s, e.ln_n, (uint32_t)l);
   else ovu(e.rest, l);
 }
-YM_INL void e_key(Enc &e, const Ctx &c, const Span &k) {
-  if (e.v2) { idiff_w(e.kc, e.kc_s, e.kc_n, e.kc_d, e.keyClock++); ostr_bytes(e.sb, c, k); uopt_w(e.sl, e.sl_s, e.sl_n, k.n16); }
+YM_INL void e_key(Enc &e, Ctx &c, const Span &k) {
+  if (e.v2) { idiff_w(e.kc, e.kc_s, e.kc_n, e.kc_d, e.keyClock++); e_str_bytes(e, c, k); uopt_w(e.sl, e.sl_s, e.sl_n, k.n16); }
+  else if (k.lo || k.hi) seterr(c, ST_URI);
   else { ovu(e.rest, span_bytes(k)); ostr_bytes(e.rest, c, k); }
 }
-YM_INL void e_flush_columns(Enc &e) {
+YM_INL void e_flush_columns(Ctx &c, Enc &e) {
   if (!e.v2) return;
+  if (e.pend_hi) seterr(c, ST_URI);  // the column ends with a lone high surrogate
   idiff_flush(e.kc, e.kc_d, e.kc_n);
   uopt_flush(e.cl, e.cl_s, e.cl_n);
   idiff_flush(e.lc, e.lc_d, e.lc_n);
@@ -1015,6 +1062,7 @@ YM_INL SinkLen canon_len(Ctx &c, const uint8_t *A, uint64_t p, uint64_t end, uin
 
 // writeString of a canonical JSON text (ContentJSON element: JSON.stringify(JSON.parse(text)))
 YM_BIG void e_json_string(Ctx &c, Enc &e, uint64_t off, uint64_t n) {
+  if (e.v2 && e.pend_hi) { seterr(c, ST_URI); return; }  // a pending lone high surrogate stays unpaired
   const uint64_t p = js_ws(c.A, off, off + n);
   const SinkLen L = canon_len(c, c.A, p, off + n, G_JSON, T_JSON);
   if (c.err) return;
@@ -1127,15 +1175,17 @@ YM_BIG void content_write(Ctx &c, Enc &e, const SStruct &s, int64_t off) {
       // surrogate that writeVarString / the V2 StringEncoder reject (URIError)
       Span t = s.a;
       int64_t k = off;
-      if (t.fffd) {
-        if (k >= 1) { t.fffd = 0; k--; t.n16--; }
-      }
+      if (t.fffd && k >= 1) { t.fffd = 0; k--; t.n16--; }
+      if (t.lo && k >= 1) { t.lo = 0; k--; t.n16--; }
       int split = 0;
       uint64_t b = utf8_unit_offset(c, t.off, t.n, (uint64_t)k, &split);
-      if (split) { seterr(c, ST_URI); break; }
+      t.n16 -= (uint32_t)k;
+      if (split) {  // the cut leaves the low half of the pair at byte b: a lone surrogate (e_string decides)
+        t.lo = 1;
+        b += 4;
+      }
       t.off += b;
       t.n -= (uint32_t)b;
-      t.n16 = (uint32_t)((int64_t)t.n16 - k);
       e_string(e, c, t);
       break;
     }
@@ -1152,7 +1202,23 @@ YM_BIG void content_write(Ctx &c, Enc &e, const SStruct &s, int64_t off) {
       break;
     case 7:
       e_typeref(e, s.cnt);
-      if (s.cnt == 3 || s.cnt == 5) e_key(e, c, s.a);
+      if (s.cnt == 3 || s.cnt == 5) {
+        if (!s.keyundef) { e_key(e, c, s.a); break; }
+        // an undefined name: YXmlElement's constructor defaults it to 'UNDEFINED' (YXmlElement.js:22);
+        // YXmlHook keeps undefined, so writeKey(undefined): the V2 StringEncoder reads undefined.length
+        // (TypeError), V1 writeVarString writes encodeURIComponent(undefined) = "undefined"
+        const char *lit = s.cnt == 3 ? "UNDEFINED" : "undefined";
+        if (e.v2) {
+          if (s.cnt == 5) { seterr(c, ST_TYPE); break; }
+          idiff_w(e.kc, e.kc_s, e.kc_n, e.kc_d, e.keyClock++);
+          if (e.pend_hi) { seterr(c, ST_URI); break; }
+          for (const char *t = lit; *t; t++) o8(e.sb, (uint32_t)*t);
+          uopt_w(e.sl, e.sl_s, e.sl_n, 9);
+        } else {
+          ovu(e.rest, 9);
+          for (const char *t = lit; *t; t++) o8(e.rest, (uint32_t)*t);
+        }
+      }
       break;
     case 8: {
       e_len(e, s.cnt - off);
@@ -1238,6 +1304,7 @@ YM_BIG void slice_struct(Ctx &c, SStruct &s, int64_t diff) {
       int64_t k = diff;
       if (k > (int64_t)t.n16) k = t.n16;
       if (t.fffd && k >= 1) { t.fffd = 0; k--; t.n16--; }
+      if (t.lo && k >= 1) { t.lo = 0; k--; t.n16--; }  // charCodeAt(0) is a low surrogate: no U+FFFD rule
       int split = 0;
       uint64_t b = utf8_unit_offset(c, t.off, t.n, (uint64_t)k, &split);
       if (split) {
@@ -1474,7 +1541,18 @@ struct DocWS {          // per-document workspace (global memory), carved by the
   PartRec *parts; uint32_t parts_cap;
   DSE *ds; DSG *dsg; uint64_t ds_cap;
   int64_t *sv;  uint32_t sv_cap;   // diff: decoded state vector (client, clock) pairs
+  Span *keys; uint64_t keys_cap;   // V2 readKey caches of all readers
+  uint32_t mul;                    // capacity multiplier of this attempt (grown on ST_RETRY)
 };
+// a V2 reader's readKey cache: (its bytes / 64 + 4) * mul entries carved from the doc's pool
+YM_INL void reader_keys(Ctx &c, Reader &r, DocWS &ws, uint64_t &used) {
+  if (!r.v2) return;
+  const uint64_t cap = (r.rest.len / 64 + 4) * ws.mul;
+  if (used + cap > ws.keys_cap) { seterr(c, ST_RETRY); return; }
+  r.keys = ws.keys + used;
+  r.keys_cap = (uint32_t)cap;
+  used += cap;
+}
 
 // reader comparator of the 13.5.16 sort; *inconsistent is set for a GC/Item tie
 YM_INL int rcmp(const Reader &a, const Reader &b, int *inconsistent) {
@@ -1494,33 +1572,277 @@ YM_INL bool rtie_bad(const Reader &a, const Reader &b) {  // GC/Item tie (compar
   return a.curr.client == b.curr.client && a.curr.clock == b.curr.clock && a.curr.kind != b.curr.kind &&
          a.curr.kind != K_SKIP && b.curr.kind != K_SKIP;
 }
-// V8 Array.prototype.sort for n < 64 (CountAndMakeRun + BinaryInsertionSort)
-YM_BIG void v8_small_sort(Reader *rs, uint32_t *a, uint32_t n) {
-  if (n < 2) return;
-  int inc = 0;
-  uint32_t run = 2;
-  bool desc = rcmp(rs[a[1]], rs[a[0]], &inc) < 0;
-  uint32_t prev = a[1];
-  for (uint32_t i = 2; i < n; i++) {
-    int o = rcmp(rs[a[i]], rs[prev], &inc);
-    if (desc ? o >= 0 : o < 0) break;
-    prev = a[i];
-    run++;
-  }
-  if (desc)
-    for (uint32_t i = 0, j = run - 1; i < j; i++, j--) { uint32_t t = a[i]; a[i] = a[j]; a[j] = t; }
-  for (uint32_t st = run; st < n; st++) {
-    uint32_t pivot = a[st];
-    uint32_t l = 0, r = st;
-    while (l < r) {
-      uint32_t mid = l + ((r - l) >> 1);
-      if (rcmp(rs[pivot], rs[a[mid]], &inc) < 0) r = mid; else l = mid + 1;
+// V8's Array.prototype.sort (TimSort of third_party/v8/builtins/array-sort.tq in the reference's Node),
+// restated operation by operation over reader indices: runs by CountAndMakeRun, extended to minrun by
+// BinaryInsertionSort, a pending-run stack collapsed by MergeCollapse, merges by MergeLow / MergeHigh
+// with galloping (minGallop starts at 7).  The reader comparator is inconsistent for a GC / Item tie
+// (compare(a, b) = compare(b, a) = -1), so the order 13.5.16's mergeUpdates produces depends on exactly
+// which pairs V8 compares; below 64 readers only the first two steps run.  tmp: n scratch slots.
+struct V8Sort {
+  Reader *rs;
+  uint32_t *a, *t;
+  uint32_t base[80], len[80];
+  int nruns;
+  int64_t min_gallop;
+  YM_INL int cmp(uint32_t x, uint32_t y) { int inc = 0; return rcmp(rs[x], rs[y], &inc); }
+};
+YM_BIG int64_t v8_gallop_left(V8Sort &S, const uint32_t *arr, uint32_t key, int64_t base, int64_t length, int64_t hint) {
+  int64_t last = 0, ofs = 1;
+  if (S.cmp(arr[base + hint], key) < 0) {
+    const int64_t maxo = length - hint;
+    while (ofs < maxo) {
+      if (S.cmp(arr[base + hint + ofs], key) >= 0) break;
+      last = ofs;
+      ofs = (ofs << 1) + 1;
+      if (ofs <= 0) ofs = maxo;
     }
-    for (uint32_t p = st; p > l; p--) a[p] = a[p - 1];
-    a[l] = pivot;
+    if (ofs > maxo) ofs = maxo;
+    last += hint;
+    ofs += hint;
+  } else {
+    const int64_t maxo = hint + 1;
+    while (ofs < maxo) {
+      if (S.cmp(arr[base + hint - ofs], key) < 0) break;
+      last = ofs;
+      ofs = (ofs << 1) + 1;
+      if (ofs <= 0) ofs = maxo;
+    }
+    if (ofs > maxo) ofs = maxo;
+    const int64_t t = last;
+    last = hint - ofs;
+    ofs = hint - t;
+  }
+  last++;
+  while (last < ofs) {
+    const int64_t m = last + ((ofs - last) >> 1);
+    if (S.cmp(arr[base + m], key) < 0) last = m + 1; else ofs = m;
+  }
+  return ofs;
+}
+YM_BIG int64_t v8_gallop_right(V8Sort &S, const uint32_t *arr, uint32_t key, int64_t base, int64_t length, int64_t hint) {
+  int64_t last = 0, ofs = 1;
+  if (S.cmp(key, arr[base + hint]) < 0) {
+    const int64_t maxo = hint + 1;
+    while (ofs < maxo) {
+      if (S.cmp(key, arr[base + hint - ofs]) >= 0) break;
+      last = ofs;
+      ofs = (ofs << 1) + 1;
+      if (ofs <= 0) ofs = maxo;
+    }
+    if (ofs > maxo) ofs = maxo;
+    const int64_t t = last;
+    last = hint - ofs;
+    ofs = hint - t;
+  } else {
+    const int64_t maxo = length - hint;
+    while (ofs < maxo) {
+      if (S.cmp(key, arr[base + hint + ofs]) < 0) break;
+      last = ofs;
+      ofs = (ofs << 1) + 1;
+      if (ofs <= 0) ofs = maxo;
+    }
+    if (ofs > maxo) ofs = maxo;
+    last += hint;
+    ofs += hint;
+  }
+  last++;
+  while (last < ofs) {
+    const int64_t m = last + ((ofs - last) >> 1);
+    if (S.cmp(key, arr[base + m]) < 0) ofs = m; else last = m + 1;
+  }
+  return ofs;
+}
+YM_INL void v8_copy(uint32_t *dst, const uint32_t *src, int64_t n) {  // memmove
+  if (dst < src) for (int64_t i = 0; i < n; i++) dst[i] = src[i];
+  else for (int64_t i = n - 1; i >= 0; i--) dst[i] = src[i];
+}
+YM_BIG void v8_merge_low(V8Sort &S, int64_t baseA, int64_t lenA, int64_t baseB, int64_t lenB) {
+  uint32_t *a = S.a, *t = S.t;
+  v8_copy(t, a + baseA, lenA);
+  int64_t dest = baseA, ct = 0, cb = baseB;
+  a[dest++] = a[cb++];
+  if (--lenB == 0) goto succeed;
+  if (lenA == 1) goto copy_b;
+  for (;;) {
+    int64_t wa = 0, wb = 0;
+    for (;;) {
+      if (S.cmp(a[cb], t[ct]) < 0) {
+        a[dest++] = a[cb++]; wb++; lenB--; wa = 0;
+        if (lenB == 0) goto succeed;
+        if (wb >= S.min_gallop) break;
+      } else {
+        a[dest++] = t[ct++]; wa++; lenA--; wb = 0;
+        if (lenA == 1) goto copy_b;
+        if (wa >= S.min_gallop) break;
+      }
+    }
+    S.min_gallop++;
+    bool first = true;
+    while (wa >= 7 || wb >= 7 || first) {
+      first = false;
+      S.min_gallop = S.min_gallop - 1 > 1 ? S.min_gallop - 1 : 1;
+      wa = v8_gallop_right(S, t, a[cb], ct, lenA, 0);
+      if (wa > 0) {
+        v8_copy(a + dest, t + ct, wa);
+        dest += wa; ct += wa; lenA -= wa;
+        if (lenA == 1) goto copy_b;
+        if (lenA == 0) goto succeed;  // impossible for a consistent comparator
+      }
+      a[dest++] = a[cb++];
+      if (--lenB == 0) goto succeed;
+      wb = v8_gallop_left(S, a, t[ct], cb, lenB, 0);
+      if (wb > 0) {
+        v8_copy(a + dest, a + cb, wb);
+        dest += wb; cb += wb; lenB -= wb;
+        if (lenB == 0) goto succeed;
+      }
+      a[dest++] = t[ct++];
+      if (--lenA == 1) goto copy_b;
+    }
+    S.min_gallop++;
+  }
+succeed:
+  if (lenA > 0) v8_copy(a + dest, t + ct, lenA);
+  return;
+copy_b:
+  v8_copy(a + dest, a + cb, lenB);
+  a[dest + lenB] = t[ct];
+}
+YM_BIG void v8_merge_high(V8Sort &S, int64_t baseA, int64_t lenA, int64_t baseB, int64_t lenB) {
+  uint32_t *a = S.a, *t = S.t;
+  v8_copy(t, a + baseB, lenB);
+  int64_t dest = baseB + lenB - 1, ct = lenB - 1, ca = baseA + lenA - 1;
+  a[dest--] = a[ca--];
+  if (--lenA == 0) goto succeed;
+  if (lenB == 1) goto copy_a;
+  for (;;) {
+    int64_t wa = 0, wb = 0;
+    for (;;) {
+      if (S.cmp(t[ct], a[ca]) < 0) {
+        a[dest--] = a[ca--]; wa++; lenA--; wb = 0;
+        if (lenA == 0) goto succeed;
+        if (wa >= S.min_gallop) break;
+      } else {
+        a[dest--] = t[ct--]; wb++; lenB--; wa = 0;
+        if (lenB == 1) goto copy_a;
+        if (wb >= S.min_gallop) break;
+      }
+    }
+    S.min_gallop++;
+    bool first = true;
+    while (wa >= 7 || wb >= 7 || first) {
+      first = false;
+      S.min_gallop = S.min_gallop - 1 > 1 ? S.min_gallop - 1 : 1;
+      int64_t k = v8_gallop_right(S, a, t[ct], baseA, lenA, lenA - 1);
+      wa = lenA - k;
+      if (wa > 0) {
+        dest -= wa; ca -= wa;
+        v8_copy(a + dest + 1, a + ca + 1, wa);
+        lenA -= wa;
+        if (lenA == 0) goto succeed;
+      }
+      a[dest--] = t[ct--];
+      if (--lenB == 1) goto copy_a;
+      k = v8_gallop_left(S, t, a[ca], 0, lenB, lenB - 1);
+      wb = lenB - k;
+      if (wb > 0) {
+        dest -= wb; ct -= wb;
+        v8_copy(a + dest + 1, t + ct + 1, wb);
+        lenB -= wb;
+        if (lenB == 1) goto copy_a;
+        if (lenB == 0) goto succeed;  // impossible for a consistent comparator
+      }
+      a[dest--] = a[ca--];
+      if (--lenA == 0) goto succeed;
+    }
+    S.min_gallop++;
+  }
+succeed:
+  if (lenB > 0) v8_copy(a + dest - (lenB - 1), t, lenB);
+  return;
+copy_a:
+  dest -= lenA; ca -= lenA;
+  v8_copy(a + dest + 1, a + ca + 1, lenA);
+  a[dest] = t[ct];
+}
+YM_BIG void v8_merge_at(V8Sort &S, int i) {
+  int64_t baseA = S.base[i], lenA = S.len[i], baseB = S.base[i + 1], lenB = S.len[i + 1];
+  S.len[i] = (uint32_t)(lenA + lenB);
+  if (i == S.nruns - 3) { S.base[i + 1] = S.base[i + 2]; S.len[i + 1] = S.len[i + 2]; }
+  S.nruns--;
+  const int64_t k = v8_gallop_right(S, S.a, S.a[baseB], baseA, lenA, 0);
+  baseA += k;
+  lenA -= k;
+  if (lenA == 0) return;
+  lenB = v8_gallop_left(S, S.a, S.a[baseA + lenA - 1], baseB, lenB, lenB - 1);
+  if (lenB == 0) return;
+  if (lenA <= lenB) v8_merge_low(S, baseA, lenA, baseB, lenB);
+  else v8_merge_high(S, baseA, lenA, baseB, lenB);
+}
+YM_INL bool v8_run_inv(const V8Sort &S, int n) { return n < 2 || S.len[n - 2] > S.len[n - 1] + S.len[n]; }
+YM_BIG void v8_sort(Reader *rs, uint32_t *a, uint32_t *tmp, uint32_t n) {
+  if (n < 2) return;
+  V8Sort S;
+  S.rs = rs; S.a = a; S.t = tmp; S.nruns = 0; S.min_gallop = 7;
+  int64_t remaining = n, low = 0;
+  int64_t minrun = remaining, r = 0;
+  while (minrun >= 64) { r |= minrun & 1; minrun >>= 1; }
+  minrun += r;
+  while (remaining != 0) {
+    int64_t run;  // CountAndMakeRun(low, low + remaining)
+    if (remaining == 1) {
+      run = 1;
+    } else {
+      run = 2;
+      const bool desc = S.cmp(a[low + 1], a[low]) < 0;
+      uint32_t prev = a[low + 1];
+      for (int64_t i = low + 2; i < low + remaining; i++) {
+        const int o = S.cmp(a[i], prev);
+        if (desc ? o >= 0 : o < 0) break;
+        prev = a[i];
+        run++;
+      }
+      if (desc)
+        for (int64_t i = low, j = low + run - 1; i < j; i++, j--) { uint32_t x = a[i]; a[i] = a[j]; a[j] = x; }
+    }
+    if (run < minrun) {  // BinaryInsertionSort(low, low + run, low + forced)
+      const int64_t forced = minrun < remaining ? minrun : remaining;
+      for (int64_t start = low + run; start < low + forced; start++) {
+        const uint32_t pivot = a[start];
+        int64_t left = low, right = start;
+        while (left < right) {
+          const int64_t mid = left + ((right - left) >> 1);
+          if (S.cmp(pivot, a[mid]) < 0) right = mid; else left = mid + 1;
+        }
+        for (int64_t p = start; p > left; p--) a[p] = a[p - 1];
+        a[left] = pivot;
+      }
+      run = forced;
+    }
+    S.base[S.nruns] = (uint32_t)low;
+    S.len[S.nruns] = (uint32_t)run;
+    S.nruns++;
+    while (S.nruns > 1) {  // MergeCollapse
+      int m = S.nruns - 2;
+      if (!v8_run_inv(S, m + 1) || !v8_run_inv(S, m)) {
+        if (S.len[m - 1] < S.len[m + 1]) m--;
+        v8_merge_at(S, m);
+      } else if (S.len[m] <= S.len[m + 1]) {
+        v8_merge_at(S, m);
+      } else {
+        break;
+      }
+    }
+    low += run;
+    remaining -= run;
+  }
+  while (S.nruns > 1) {  // MergeForceCollapse
+    int m = S.nruns - 2;
+    if (m > 0 && S.len[m - 1] < S.len[m + 1]) m--;
+    v8_merge_at(S, m);
   }
 }
-// stable merge sort (initial order), bottom-up
+// stable merge sort (initial order), bottom-up: V8's result whenever the comparator is consistent
 YM_BIG void stable_sort(Reader *rs, uint32_t *a, uint32_t *t, uint32_t n) {
   int inc = 0;
   for (uint32_t w = 1; w < n; w *= 2) {
@@ -1539,7 +1861,11 @@ YM_BIG void merge_doc(Ctx &c, DocWS &ws, const uint64_t *upd_off, uint32_t u0, u
                       Layout &L, uint8_t *out) {
   Reader *rs = ws.rs;
   uint32_t *arr = ws.arr;
-  for (uint32_t i = 0; i < k && !c.err; i++) reader_open(c, rs[i], upd_off[u0 + i], upd_off[u0 + i + 1] - upd_off[u0 + i], v2);
+  uint64_t kused = 0;
+  for (uint32_t i = 0; i < k && !c.err; i++) {
+    reader_open(c, rs[i], upd_off[u0 + i], upd_off[u0 + i + 1] - upd_off[u0 + i], v2);
+    reader_keys(c, rs[i], ws, kused);
+  }
   for (uint32_t i = 0; i < k && !c.err; i++) { rs[i].filter = 1; reader_next(c, rs[i]); }
   if (c.err) return;
   Enc e;
@@ -1555,12 +1881,17 @@ YM_BIG void merge_doc(Ctx &c, DocWS &ws, const uint64_t *upd_off, uint32_t u0, u
   // first sort: exact V8 emulation below 64 readers; otherwise a stable sort (identical whenever the
   // comparator is consistent); afterwards the array stays sorted and only the head reader moves.
   bool literal = false;
-  if (na < 64) { v8_small_sort(rs, arr, na); }
+  if (na < 64) { v8_sort(rs, arr, ws.tmp, na); }
   else stable_sort(rs, arr, ws.tmp, na);
   for (uint32_t i = 1; i < na; i++)
     if (rtie_bad(rs[arr[i - 1]], rs[arr[i]])) {
-      if (na >= 64) { seterr(c, ST_UNSUPPORTED); return; }
       literal = true;
+      if (na >= 64) {  // the stable sort is not V8's order here: sort the input order as V8 does
+        na = 0;
+        for (uint32_t q = 0; q < k; q++) if (rs[q].has_curr) arr[na++] = q;
+        v8_sort(rs, arr, ws.tmp, na);
+      }
+      break;
     }
   SStruct cur;
   bool has_cur = false;
@@ -1572,7 +1903,7 @@ YM_BIG void merge_doc(Ctx &c, DocWS &ws, const uint64_t *upd_off, uint32_t u0, u
         uint32_t m = 0;
         for (uint32_t i = 0; i < na; i++) if (rs[arr[i]].has_curr) arr[m++] = arr[i];
         na = m;
-        v8_small_sort(rs, arr, na);
+        v8_sort(rs, arr, ws.tmp, na);
       } else {
         uint32_t R = arr[0];
         if (!rs[R].has_curr) {
@@ -1588,9 +1919,8 @@ YM_BIG void merge_doc(Ctx &c, DocWS &ws, const uint64_t *upd_off, uint32_t u0, u
           }
           bool bad = (lo < na && rtie_bad(rs[R], rs[arr[lo]])) || (lo > 1 && rtie_bad(rs[R], rs[arr[lo - 1]]));
           if (bad) {
-            if (na >= 64) { seterr(c, ST_UNSUPPORTED); return; }
             literal = true;
-            v8_small_sort(rs, arr, na);  // na < 64 and every reader still has a struct here
+            v8_sort(rs, arr, ws.tmp, na);  // every reader still has a struct here
           } else {
             for (uint32_t i = 1; i < lo; i++) arr[i - 1] = arr[i];
             arr[lo - 1] = R;
@@ -1665,7 +1995,7 @@ YM_BIG void merge_doc(Ctx &c, DocWS &ws, const uint64_t *upd_off, uint32_t u0, u
   if (c.err) return;
   uint64_t ds0 = e.rest.n;
   ds_emit(c, e, ws.ds, nds, ws.dsg, true);
-  e_flush_columns(e);
+  e_flush_columns(c, e);
   if (pass == 1) {
     L.col[C_KC] = e.kc.n; L.col[C_CL] = e.cl.n; L.col[C_LC] = e.lc.n; L.col[C_RC] = e.rc.n; L.col[C_IN] = e.in.n;
     L.col[C_SB] = e.sb.n; L.col[C_SL] = e.sl.n; L.col[C_PI] = e.pi.n; L.col[C_TR] = e.tr.n; L.col[C_LN] = e.ln.n;
@@ -1711,6 +2041,7 @@ YM_BIG void diff_doc(Ctx &c, DocWS &ws, uint64_t uoff, uint64_t ulen, const uint
   w.cap = ws.parts_cap;
   Reader &r = ws.rs[0];
   reader_open(c, r, uoff, ulen, v2);
+  { uint64_t kused = 0; reader_keys(c, r, ws, kused); }
   if (c.err) return;
   reader_next(c, r);
   int64_t last_client = -1, last_k = 0;
@@ -1741,7 +2072,7 @@ YM_BIG void diff_doc(Ctx &c, DocWS &ws, uint64_t uoff, uint64_t ulen, const uint
   if (c.err) return;
   uint64_t ds0 = e.rest.n;
   ds_emit(c, e, ws.ds, nds, ws.dsg, false);
-  e_flush_columns(e);
+  e_flush_columns(c, e);
   if (pass == 1) {
     L.col[C_KC] = e.kc.n; L.col[C_CL] = e.cl.n; L.col[C_LC] = e.lc.n; L.col[C_RC] = e.rc.n; L.col[C_IN] = e.in.n;
     L.col[C_SB] = e.sb.n; L.col[C_SL] = e.sl.n; L.col[C_PI] = e.pi.n; L.col[C_TR] = e.tr.n; L.col[C_LN] = e.ln.n;
@@ -1768,6 +2099,7 @@ YM_BIG void conv_doc(Ctx &c, DocWS &ws, uint64_t uoff, uint64_t ulen, uint32_t v
   w.cap = ws.parts_cap;
   Reader &r = ws.rs[0];
   reader_open(c, r, uoff, ulen, v2);
+  { uint64_t kused = 0; reader_keys(c, r, ws, kused); }
   if (c.err) return;
   reader_next(c, r);
   while (!c.err && r.has_curr) {
@@ -1781,7 +2113,7 @@ YM_BIG void conv_doc(Ctx &c, DocWS &ws, uint64_t uoff, uint64_t ulen, uint32_t v
   if (c.err) return;
   uint64_t ds0 = e.rest.n;
   ds_emit(c, e, ws.ds, nds, ws.dsg, false);
-  e_flush_columns(e);
+  e_flush_columns(c, e);
   if (pass == 1) {
     L.col[C_KC] = e.kc.n; L.col[C_CL] = e.cl.n; L.col[C_LC] = e.lc.n; L.col[C_RC] = e.rc.n; L.col[C_IN] = e.in.n;
     L.col[C_SB] = e.sb.n; L.col[C_SL] = e.sl.n; L.col[C_PI] = e.pi.n; L.col[C_TR] = e.tr.n; L.col[C_LN] = e.ln.n;
@@ -1798,6 +2130,7 @@ YM_BIG void conv_doc(Ctx &c, DocWS &ws, uint64_t uoff, uint64_t ulen, uint32_t v
 YM_BIG void sv_doc(Ctx &c, DocWS &ws, uint64_t uoff, uint64_t ulen, uint32_t v2, int pass, Layout &L, uint8_t *out) {
   Reader &r = ws.rs[0];
   reader_open(c, r, uoff, ulen, v2);
+  { uint64_t kused = 0; reader_keys(c, r, ws, kused); }
   if (c.err) return;
   reader_next(c, r);
   if (c.err) return;
@@ -1849,6 +2182,7 @@ YM_INL void meta_put(Ctx &c, DocWS &ws, uint32_t &n, int64_t client, int64_t v, 
 YM_BIG void meta_doc(Ctx &c, DocWS &ws, uint64_t uoff, uint64_t ulen, uint32_t v2, int pass, Layout &L, uint8_t *out) {
   Reader &r = ws.rs[0];
   reader_open(c, r, uoff, ulen, v2);
+  { uint64_t kused = 0; reader_keys(c, r, ws, kused); }
   r.lax = 1;
   if (c.err) return;
   reader_next(c, r);
@@ -1918,12 +2252,14 @@ YM_BIG void dsmerge_doc(Ctx &c, DocWS &ws, const uint64_t *upd_off, uint32_t u0,
 enum : uint32_t { OP_MERGE = 0, OP_DIFF = 1, OP_SV = 2, OP_CONV = 3, OP_META = 4, OP_DSMERGE = 5 };
 
 struct GeneralWsSize {
-  uint64_t rs, arr, parts, ds, dsg, sv, total;
+  uint64_t rs, arr, parts, ds, dsg, sv, keys, total;
+  uint32_t mul;
+  uint64_t keys_cap;
   uint32_t parts_cap, sv_cap;
   uint64_t ds_cap;
 };
 YM_INL uint64_t al16(uint64_t x) { return (x + 15) & ~(uint64_t)15; }
-YM_INL GeneralWsSize general_ws_size(uint32_t k, uint64_t bytes, uint32_t parts_mul, uint64_t svbytes) {
+YM_INL GeneralWsSize general_ws_size(uint32_t k, uint64_t bytes, uint32_t parts_mul, uint64_t svbytes, uint32_t v2) {
   GeneralWsSize z;
   z.rs = al16((uint64_t)(k ? k : 1) * sizeof(Reader));
   z.arr = al16((uint64_t)(k + 1) * 4);
@@ -1934,7 +2270,11 @@ YM_INL GeneralWsSize general_ws_size(uint32_t k, uint64_t bytes, uint32_t parts_
   z.dsg = al16(z.ds_cap * sizeof(DSG));
   z.sv_cap = (uint32_t)(svbytes / 2 + 2);
   z.sv = al16((uint64_t)z.sv_cap * 16);
-  z.total = z.rs + 2 * z.arr + z.parts + z.ds + z.dsg + z.sv;
+  z.mul = parts_mul;
+  // readKey caches (V2 only): a small start, grown by the retry rounds for key-heavy documents
+  z.keys_cap = v2 ? (bytes / 64 + 4ull * (k ? k : 1)) * parts_mul : 0;
+  z.keys = al16(z.keys_cap * sizeof(Span));
+  z.total = z.rs + 2 * z.arr + z.parts + z.ds + z.dsg + z.sv + z.keys;
   return z;
 }
 // the state-vector table: diff = the decoded state vector; meta = (client, from, to) triples, at most one
@@ -1951,7 +2291,9 @@ YM_INL void general_carve(uint8_t *p, const GeneralWsSize &z, DocWS &w) {
   w.parts = (PartRec *)p; p += z.parts; w.parts_cap = z.parts_cap;
   w.ds = (DSE *)p; p += z.ds; w.ds_cap = z.ds_cap;
   w.dsg = (DSG *)p; p += z.dsg;
-  w.sv = (int64_t *)p; w.sv_cap = z.sv_cap;
+  w.sv = (int64_t *)p; p += z.sv; w.sv_cap = z.sv_cap;
+  w.keys = (Span *)p; w.keys_cap = z.keys_cap;
+  w.mul = z.mul;
 }
 // One document, pass 1 (sizes into L) or 2 (writes to out).  Document = updates u0 .. u0+k-1 of the
 // arena (upd_off absolute); sv = its encoded state vector (diff).  Status in c.err.

@@ -16,7 +16,7 @@ __device__ __forceinline__ void carve(const GeneralJob &j, uint32_t i, uint32_t 
   uint32_t k = j.doc_upd[d + 1] - j.doc_upd[d];
   uint64_t bytes = j.upd_off[j.doc_upd[d + 1]] - j.upd_off[j.doc_upd[d]];
   const uint64_t svlen = j.op == OP_DIFF ? j.sv_off[d + 1] - j.sv_off[d] : 0;
-  general_carve(j.ws + j.ws_off[i], general_ws_size(k, bytes, j.parts_mul, general_sv_bytes(j.op, svlen, bytes)), w);
+  general_carve(j.ws + j.ws_off[i], general_ws_size(k, bytes, j.parts_mul, general_sv_bytes(j.op, svlen, bytes), j.v2), w);
 }
 
 __global__ void k_general_ws(GeneralJob j, uint64_t *ws_size) {
@@ -26,7 +26,7 @@ __global__ void k_general_ws(GeneralJob j, uint64_t *ws_size) {
   uint32_t k = j.doc_upd[d + 1] - j.doc_upd[d];
   uint64_t bytes = j.upd_off[j.doc_upd[d + 1]] - j.upd_off[j.doc_upd[d]];
   const uint64_t svlen = j.op == OP_DIFF ? j.sv_off[d + 1] - j.sv_off[d] : 0;
-  ws_size[i] = general_ws_size(k, bytes, j.parts_mul, general_sv_bytes(j.op, svlen, bytes)).total;
+  ws_size[i] = general_ws_size(k, bytes, j.parts_mul, general_sv_bytes(j.op, svlen, bytes), j.v2).total;
 }
 
 __global__ void __launch_bounds__(64) k_general(GeneralJob j, int pass) {
