@@ -50,6 +50,10 @@ enum {
 
 enum { YM_MEM_HOST = 0, YM_MEM_DEVICE = 1 };
 enum { YM_V1 = 1, YM_V2 = 2 };
+/* ym_ds_merge only, or-ed into ym_batch.format: the reference's own sortAndMergeDeleteSet
+ * (gaberogan/yjs@v0 src/utils/DeleteSet.js:113-135: only exactly adjacent ranges coalesce) instead of
+ * yjs 13.5.16's (touching and overlapping ranges merge) */
+enum { YM_DS_REF = 0x100 };
 
 typedef struct ym_batch {
   const uint8_t *arena;    /* concatenated update bytes                                   */
@@ -103,7 +107,8 @@ int ym_meta(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
 /* PermanentUserData's delete-set merge (reference src/utils/PermanentUserData.js:49-54): the "updates" of
  * document d are encoded delete sets (DSEncoderV1 bytes for YM_V1, DSEncoderV2 for YM_V2, as
  * encodeSnapshot[V2] writes them, src/utils/Snapshot.js:84-101); the output is
- * writeDeleteSet(mergeDeleteSets(readDeleteSet(each))) in the same encoding (13.5.16 union, he@10482). */
+ * writeDeleteSet(mergeDeleteSets(readDeleteSet(each))) in the same encoding (13.5.16 union, he@10482;
+ * with YM_DS_REF in b->format the reference's adjacency-only coalescing, DeleteSet.js:113-161). */
 int ym_ds_merge(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
 
 #ifdef __cplusplus

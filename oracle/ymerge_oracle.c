@@ -1580,7 +1580,10 @@ static void ditem_msort(DItem *a, DItem *tmp, size_t n) { /* stable by clock */
   while (j < n) tmp[k++] = a[j++];
   memcpy(a, tmp, n * sizeof(DItem));
 }
-static void ds_sort_and_merge(Ctx *c, DSet *ds) { /* sortAndMergeDeleteSet (le) */
+/* sortAndMergeDeleteSet: 13.5.16 (le@10242) merges touching and overlapping ranges (>=, max of the ends);
+   ref = the reference's own (gaberogan/yjs@v0 src/utils/DeleteSet.js:113-135) merges only exactly
+   adjacent ranges (left.clock + left.len === right.clock, left.len += right.len) and keeps the rest */
+static void ds_sort_and_merge_mode(Ctx *c, DSet *ds, int ref) {
   for (size_t ci = 0; ci < ds->n; ci++) {
     DClient *d = &ds->cl[ci];
     if (d->n > 1) {
@@ -1591,9 +1594,12 @@ static void ds_sort_and_merge(Ctx *c, DSet *ds) { /* sortAndMergeDeleteSet (le) 
     for (i = 1, j = 1; i < d->n; i++) {
       DItem *left = &d->items[j - 1];
       DItem right = d->items[i];
-      if (left->clock + left->len >= right.clock) {
-        int64_t m = right.clock + right.len - left->clock;
-        if (m > left->len) left->len = m;
+      if (ref ? left->clock + left->len == right.clock : left->clock + left->len >= right.clock) {
+        if (ref) left->len += right.len;
+        else {
+          int64_t m = right.clock + right.len - left->clock;
+          if (m > left->len) left->len = m;
+        }
       } else {
         if (j < i) d->items[j] = right;
         j++;
@@ -1602,7 +1608,7 @@ static void ds_sort_and_merge(Ctx *c, DSet *ds) { /* sortAndMergeDeleteSet (le) 
     if (d->n > 0) d->n = j;
   }
 }
-static void ds_merge(Ctx *c, DSet *dss, size_t k, DSet *out) { /* mergeDeleteSets (he) */
+static void ds_merge_mode(Ctx *c, DSet *dss, size_t k, DSet *out, int ref) { /* mergeDeleteSets (he; DeleteSet.js:141-161) */
   memset(out, 0, sizeof(*out));
   for (size_t i = 0; i < k; i++) {
     for (size_t ci = 0; ci < dss[i].n; ci++) {
@@ -1619,8 +1625,9 @@ static void ds_merge(Ctx *c, DSet *dss, size_t k, DSet *out) { /* mergeDeleteSet
       }
     }
   }
-  ds_sort_and_merge(c, out);
+  ds_sort_and_merge_mode(c, out, ref);
 }
+static void ds_merge(Ctx *c, DSet *dss, size_t k, DSet *out) { ds_merge_mode(c, dss, k, out, 0); }
 
 /* ------------------------------------------------------------------------------------------------ */
 /* mergeUpdatesV2 (13.5.16 ds@39007)                                                                */
@@ -2160,7 +2167,7 @@ static Buf *meta_impl(Ctx *c, const uint8_t *upd, size_t len, int v2) {
    with readDeleteSet (DeleteSet.js:241-256; DSDecoderV1, or DSDecoderV2 for fmt 2), the k sets are
    merged by mergeDeleteSets (13.5.16 he@10482 + le@10242 union) and written by writeDeleteSet
    (DSEncoderV1 / DSEncoderV2 rest bytes, as encodeSnapshot[V2] writes them, Snapshot.js:84-101). */
-static Buf *dsmerge_impl(Ctx *c, const uint8_t *const *dss_in, const size_t *lens, size_t k, int v2) {
+static Buf *dsmerge_impl(Ctx *c, const uint8_t *const *dss_in, const size_t *lens, size_t k, int v2, int ref) {
   DSet *dss = (DSet *)aalloc(c, (k ? k : 1) * sizeof(DSet));
   for (size_t i = 0; i < k; i++) {
     UDec dec;
@@ -2169,7 +2176,7 @@ static Buf *dsmerge_impl(Ctx *c, const uint8_t *const *dss_in, const size_t *len
     ds_read(c, &dec, &dss[i]);
   }
   DSet m;
-  ds_merge(c, dss, k, &m);
+  ds_merge_mode(c, dss, k, &m, ref);
   UEnc enc;
   uenc_init(c, &enc, 0);
   enc.v2 = v2;
@@ -2261,7 +2268,8 @@ int ymo_ds_merge(const uint8_t *const *dss, const size_t *lens, size_t n, int fm
   memset(&c, 0, sizeof(c));
   int code = setjmp(c.jb);
   if (code) { ctx_free(&c); return code; }
-  Buf *b = dsmerge_impl(&c, dss, lens, n, fmt == 2);
+  /* fmt: 1 DSEncoderV1 / 2 DSEncoderV2 blobs; | 0x100: the reference's adjacency-only coalescing */
+  Buf *b = dsmerge_impl(&c, dss, lens, n, (fmt & 0xff) == 2, (fmt & 0x100) != 0);
   int rc = finish_out(&c, b, out, out_len);
   ctx_free(&c);
   return rc;

@@ -29,6 +29,8 @@ def run(op, fmt, arena, upd_off, doc_upd, sv_arena=None, sv_off=None, san=False)
         sv_off = np.zeros(nd + 1, np.uint64)
     sv_arena = np.ascontiguousarray(sv_arena, np.uint8)
     sv_off = np.ascontiguousarray(sv_off, np.uint64)
+    if op == "dsmerge_ref":  # ym_ds_merge with YM_DS_REF: the reference's adjacency-only coalescing
+        op, fmt = "dsmerge", fmt | 0x100
     exe = binary(san)
     with tempfile.TemporaryDirectory() as td:
         fin, fout = os.path.join(td, "in"), os.path.join(td, "out")

@@ -44,7 +44,8 @@ int main(int argc, char **argv) {
   fclose(f);
   FILE *o = fopen(argv[2], "wb");
   if (!o) return 2;
-  const uint32_t v2 = fmt == 2;
+  const uint32_t v2 = (fmt & 0xff) == 2;
+  const uint32_t v2f = v2 | (op == OP_DSMERGE && (fmt & 0x100) ? 0x100u : 0u);
   for (uint32_t d = 0; d < nd; d++) {
     const uint32_t u0 = doc_upd[d], k = doc_upd[d + 1] - u0;
     const uint64_t bytes = upd_off[doc_upd[d + 1]] - upd_off[u0];
@@ -60,13 +61,13 @@ int main(int argc, char **argv) {
       Layout L;
       memset(&L, 0, sizeof(L));
       Ctx c = {0, arena.data()};
-      general_doc(c, w, op, v2, upd_off.data(), u0, k, svp, svlen, 1, L, nullptr);
+      general_doc(c, w, op, v2f, upd_off.data(), u0, k, svp, svlen, 1, L, nullptr);
       st = c.err;
       if (st) continue;
       // pass 2 over the same workspace (the part table recorded by pass 1 is read back)
       out.assign(L.total + 1, 0);
       Ctx c2 = {0, arena.data()};
-      general_doc(c2, w, op, v2, upd_off.data(), u0, k, svp, svlen, 2, L, out.data());
+      general_doc(c2, w, op, v2f, upd_off.data(), u0, k, svp, svlen, 2, L, out.data());
       st = c2.err ? (c2.err == ST_RETRY ? ST_UNEXPECTED : c2.err) : 0;
       out.resize(L.total);
     }

@@ -150,6 +150,8 @@ def batch(op, fmt, arena, upd_off, doc_upd, sv_arena=None, sv_off=None, nthreads
     """Batched oracle over the engine's arena layout (numpy arrays). op: 'merge'|'diff'|'sv'|'conv'|'meta'|'dsmerge'.
     Returns (out_bytes_list_or_None, status ndarray, out_len ndarray)."""
     L = lib()
+    if op == "dsmerge_ref":  # the reference's adjacency-only coalescing (DeleteSet.js:113-135)
+        op, fmt = "dsmerge", fmt | 0x100
     opc = {"merge": 0, "diff": 1, "sv": 2, "conv": 3, "meta": 4, "dsmerge": 5}[op]
     arena = np.ascontiguousarray(arena, dtype=np.uint8)
     upd_off = np.ascontiguousarray(upd_off, dtype=np.uint64)

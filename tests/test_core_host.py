@@ -24,7 +24,7 @@ def _groups():
 
 
 def run_cases(cases, op, fmt, san):
-    if op in ("merge", "dsmerge"):
+    if op in ("merge", "dsmerge", "dsmerge_ref"):
         a, o, d = pack_docs([c["inputs"] for c in cases])
         return core_host.run(op, fmt, a, o, d, san=san)
     a, o, d = pack_docs([[c["inputs"][0]] for c in cases])

@@ -33,7 +33,7 @@ def test_golden_batched_on_gpu(engine, key):
     from yjs_amd import pack_docs
     cases = _groups()[key]
     op, fmt = key
-    if op in ("merge", "dsmerge"):  # k inputs per document
+    if op in ("merge", "dsmerge", "dsmerge_ref"):  # k inputs per document
         arena, upd_off, doc_upd = pack_docs([c["inputs"] for c in cases])
         res = engine.run_host(op, fmt, arena, upd_off, doc_upd)
     elif op == "diff":
@@ -56,3 +56,21 @@ def test_golden_batched_on_gpu(engine, key):
         if st != 0 or got != c["expect"]:
             bad.append((c["id"], "bytes", st, len(got or b""), len(c["expect"])))
     assert not bad, bad[:20]
+
+
+def test_pref_bytes_on_gpu(engine):
+    """The engine's bytes are the ones gaberogan/yjs@v0 itself was checked against (P-ref, tests/pref)."""
+    import hashlib
+    import json
+    import os
+    from yjs_amd import pack_docs
+    pref = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "pref", "pref.json")))
+    gold = {c["id"]: c for c in CASES}
+    for op in ("merge", "sv"):
+        for fmt in (1, 2):
+            sel = [c for c in pref["cases"] if c["op"] == op and c["fmt"] == fmt and c.get("applicable")]
+            docs = [gold[c["id"]]["inputs"] if op == "merge" else [gold[c["id"]]["inputs"][0]] for c in sel]
+            oa, oo, ol, st = engine.run_host(op, fmt, *pack_docs(docs))
+            for i, c in enumerate(sel):
+                got = oa[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes()
+                assert st[i] == 0 and hashlib.sha256(got).hexdigest() == c["checked_sha256"], c["id"]

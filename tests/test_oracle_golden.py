@@ -20,6 +20,8 @@ def run_case(c):
         return O.meta(c["inputs"][0], c["fmt"])
     if c["op"] == "dsmerge":
         return O.ds_merge(c["inputs"], c["fmt"])
+    if c["op"] == "dsmerge_ref":
+        return O.ds_merge(c["inputs"], c["fmt"] | 0x100)
     return O.sv_from_update(c["inputs"][0], c["fmt"])
 
 

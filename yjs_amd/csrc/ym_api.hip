@@ -396,7 +396,8 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   j.sv = svp;
   j.sv_off = sv_off;
   j.op = op;
-  j.v2 = b->format == YM_V2;
+  j.v2 = (b->format & 0xff) == YM_V2;
+  j.dsref = op == OP_DSMERGE && (b->format & YM_DS_REF) != 0;
   j.layout = S->layout.as<ym::Layout>();
   j.status = o_status;
   j.out = o_arena;

@@ -1482,9 +1482,13 @@ YM_BIG void ds_gather(Ctx &c, Reader &r, DSE *ds, uint64_t cap, uint64_t &n) {
 }
 
 // Writes the DS of n gathered entries: merge=1 -> mergeDeleteSets (sort by clock + union, le@10242),
-// merge=0 -> readDeleteSet + writeDeleteSet only (entries regrouped by first client appearance).
-YM_BIG void ds_emit(Ctx &c, Enc &e, DSE *ds, uint64_t n, DSG *g, bool merge) {
-  if (merge) heap_sort(ds, n, [](const DSE &x, const DSE &y) { return x.client != y.client ? x.client < y.client : x.clock < y.clock; });
+// merge=2 -> the reference's mergeDeleteSets (stable sort by clock, only exactly adjacent ranges
+// coalesce: DeleteSet.js:113-135), merge=0 -> readDeleteSet + writeDeleteSet only (entries regrouped by
+// first client appearance).
+YM_BIG void ds_emit(Ctx &c, Enc &e, DSE *ds, uint64_t n, DSG *g, int merge) {
+  if (merge) heap_sort(ds, n, [](const DSE &x, const DSE &y) {
+    return x.client != y.client ? x.client < y.client : x.clock != y.clock ? x.clock < y.clock : x.seq < y.seq;
+  });
   else heap_sort(ds, n, [](const DSE &x, const DSE &y) { return x.client != y.client ? x.client < y.client : x.seq < y.seq; });
   uint64_t ng = 0;
   for (uint64_t i = 0; i < n;) {
@@ -1506,9 +1510,12 @@ YM_BIG void ds_emit(Ctx &c, Enc &e, DSE *ds, uint64_t n, DSG *g, bool merge) {
       uint32_t j = 1;
       for (uint32_t i = 1; i < cnt; i++) {
         DSE &left = it[j - 1];
-        if (left.clock + left.len >= it[i].clock) {
-          int64_t m = it[i].clock + it[i].len - left.clock;
-          if (m > left.len) left.len = m;
+        if (merge == 2 ? left.clock + left.len == it[i].clock : left.clock + left.len >= it[i].clock) {
+          if (merge == 2) left.len += it[i].len;
+          else {
+            int64_t m = it[i].clock + it[i].len - left.clock;
+            if (m > left.len) left.len = m;
+          }
         } else {
           if (j < i) it[j] = it[i];
           j++;
@@ -1994,7 +2001,7 @@ YM_BIG void merge_doc(Ctx &c, DocWS &ws, const uint64_t *upd_off, uint32_t u0, u
   for (uint32_t i = 0; i < k && !c.err; i++) ds_gather(c, rs[i], ws.ds, ws.ds_cap, nds);
   if (c.err) return;
   uint64_t ds0 = e.rest.n;
-  ds_emit(c, e, ws.ds, nds, ws.dsg, true);
+  ds_emit(c, e, ws.ds, nds, ws.dsg, 1);
   e_flush_columns(c, e);
   if (pass == 1) {
     L.col[C_KC] = e.kc.n; L.col[C_CL] = e.cl.n; L.col[C_LC] = e.lc.n; L.col[C_RC] = e.rc.n; L.col[C_IN] = e.in.n;
@@ -2071,7 +2078,7 @@ YM_BIG void diff_doc(Ctx &c, DocWS &ws, uint64_t uoff, uint64_t ulen, const uint
   ds_gather(c, r, ws.ds, ws.ds_cap, nds);
   if (c.err) return;
   uint64_t ds0 = e.rest.n;
-  ds_emit(c, e, ws.ds, nds, ws.dsg, false);
+  ds_emit(c, e, ws.ds, nds, ws.dsg, 0);
   e_flush_columns(c, e);
   if (pass == 1) {
     L.col[C_KC] = e.kc.n; L.col[C_CL] = e.cl.n; L.col[C_LC] = e.lc.n; L.col[C_RC] = e.rc.n; L.col[C_IN] = e.in.n;
@@ -2112,7 +2119,7 @@ YM_BIG void conv_doc(Ctx &c, DocWS &ws, uint64_t uoff, uint64_t ulen, uint32_t v
   ds_gather(c, r, ws.ds, ws.ds_cap, nds);
   if (c.err) return;
   uint64_t ds0 = e.rest.n;
-  ds_emit(c, e, ws.ds, nds, ws.dsg, false);
+  ds_emit(c, e, ws.ds, nds, ws.dsg, 0);
   e_flush_columns(c, e);
   if (pass == 1) {
     L.col[C_KC] = e.kc.n; L.col[C_CL] = e.cl.n; L.col[C_LC] = e.lc.n; L.col[C_RC] = e.rc.n; L.col[C_IN] = e.in.n;
@@ -2222,7 +2229,7 @@ YM_BIG void meta_doc(Ctx &c, DocWS &ws, uint64_t uoff, uint64_t ulen, uint32_t v
 // writeDeleteSet.  Input i of the document is the byte range [upd_off[u0+i], upd_off[u0+i+1]).
 // ------------------------------------------------------------------------------------------------
 YM_BIG void dsmerge_doc(Ctx &c, DocWS &ws, const uint64_t *upd_off, uint32_t u0, uint32_t k, uint32_t v2, int pass,
-                        Layout &L, uint8_t *out) {
+                        Layout &L, uint8_t *out, bool ref) {
   uint64_t nds = 0;
   for (uint32_t i = 0; i < k && !c.err; i++) {
     Reader &r = ws.rs[0];
@@ -2236,7 +2243,7 @@ YM_BIG void dsmerge_doc(Ctx &c, DocWS &ws, const uint64_t *upd_off, uint32_t u0,
   Enc e;
   enc_init(e, v2);
   e.rest.p = pass == 2 ? out : nullptr;
-  ds_emit(c, e, ws.ds, nds, ws.dsg, true);
+  ds_emit(c, e, ws.ds, nds, ws.dsg, ref ? 2 : 1);
   if (c.err) return;
   if (pass == 1) {
     __builtin_memset(&L, 0, sizeof(Layout));
@@ -2297,8 +2304,10 @@ YM_INL void general_carve(uint8_t *p, const GeneralWsSize &z, DocWS &w) {
 }
 // One document, pass 1 (sizes into L) or 2 (writes to out).  Document = updates u0 .. u0+k-1 of the
 // arena (upd_off absolute); sv = its encoded state vector (diff).  Status in c.err.
-YM_BIG void general_doc(Ctx &c, DocWS &w, uint32_t op, uint32_t v2, const uint64_t *upd_off, uint32_t u0, uint32_t k,
+// v2: 1 = V2 encoding; bit 8 (ym_ds_merge): the reference's adjacency-only delete-set coalescing
+YM_BIG void general_doc(Ctx &c, DocWS &w, uint32_t op, uint32_t v2f, const uint64_t *upd_off, uint32_t u0, uint32_t k,
                         const uint8_t *sv, uint64_t svlen, int pass, Layout &L, uint8_t *out) {
+  const uint32_t v2 = v2f & 1;
   if (op == OP_MERGE) {
     if (k == 1) {  // `if (updates.length === 1) return updates[0]`
       uint64_t n = upd_off[u0 + 1] - upd_off[u0];
@@ -2309,7 +2318,7 @@ YM_BIG void general_doc(Ctx &c, DocWS &w, uint32_t op, uint32_t v2, const uint64
     }
     return;
   }
-  if (op == OP_DSMERGE) { dsmerge_doc(c, w, upd_off, u0, k, v2, pass, L, out); return; }
+  if (op == OP_DSMERGE) { dsmerge_doc(c, w, upd_off, u0, k, v2, pass, L, out, (v2f >> 8) & 1); return; }
   if (k != 1) { c.err = ST_UNEXPECTED; return; }
   const uint64_t uoff = upd_off[u0], ulen = upd_off[u0 + 1] - upd_off[u0];
   if (op == OP_DIFF) diff_doc(c, w, uoff, ulen, sv, svlen, v2, pass, L, out);

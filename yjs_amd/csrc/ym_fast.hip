@@ -653,6 +653,7 @@ __global__ void k_fast_region(GeneralJob j, uint32_t n_upd) {
 int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st) {
   using namespace fastv1;
   if (op == OP_DSMERGE) {  // delete-set merges: the same kernel, delete sets only
+    if (j.dsref) return 0;  // the reference's adjacency-only coalescing: general path
     const uint32_t grid = j.n < 131072 ? j.n : 131072;
     if (j.v2) k_fast_merge_v1<0, 5, true, true><<<grid, 64, fastv1::LDS_BYTES, st>>>(j);
     else k_fast_merge_v1<0, 5, true, false><<<grid, 64, fastv1::LDS_BYTES, st>>>(j);

@@ -26,6 +26,7 @@ struct GeneralJob {
   uint32_t n;                // documents in this launch
   const uint32_t *list;      // document ids (nullptr: 0..n-1)
   uint32_t op, v2;
+  uint32_t dsref;            // ym_ds_merge: the reference's adjacency-only coalescing (YM_DS_REF)
   uint32_t parts_mul;        // part-table capacity multiplier (grown on ST_RETRY)
   uint8_t *ws;               // workspace
   const uint64_t *ws_off;    // per listed slot

@@ -42,6 +42,8 @@ class UnsupportedInput(YjsError):
     """Valid input that needs a canonicalisation the engine does not implement."""
 
 
+YM_DS_REF = 0x100  # ym_ds_merge: the reference's adjacency-only coalescing (include/ymerge.h)
+
 _STATUS_EXC = {
     1: (YjsError, "Integer out of range!"),
     2: (YjsError, "Unexpected case"),
@@ -125,7 +127,11 @@ class Engine:
     def _fn(self, op):
         L = self.lib
         return {"merge": L.ym_merge, "diff": L.ym_diff, "sv": L.ym_sv, "conv": L.ym_convert, "meta": L.ym_meta,
-                "dsmerge": L.ym_ds_merge}[op]
+                "dsmerge": L.ym_ds_merge, "dsmerge_ref": L.ym_ds_merge}[op]
+
+    @staticmethod
+    def _format(op, fmt):
+        return fmt | YM_DS_REF if op == "dsmerge_ref" else fmt
 
     # ---- host-memory batches ------------------------------------------------------------------
     def run_host(self, op, fmt, arena, upd_off, doc_upd, sv_arena=None, sv_off=None):
@@ -143,7 +149,7 @@ class Engine:
         b.doc_upd = doc_upd.ctypes.data
         b.n_docs = n_docs
         b.n_upd = n_upd
-        b.format = fmt
+        b.format = self._format(op, fmt)
         b.mem = 0
         if op == "diff":
             sv_arena = np.ascontiguousarray(sv_arena, np.uint8)
@@ -180,7 +186,7 @@ class Engine:
         b.doc_upd = doc_upd.data_ptr()
         b.n_docs = doc_upd.numel() - 1
         b.n_upd = upd_off.numel() - 1
-        b.format = fmt
+        b.format = self._format(op, fmt)
         b.mem = 1
         if op == "diff":
             b.sv_arena = sv_arena.data_ptr()
@@ -201,7 +207,7 @@ class Engine:
         b.doc_upd = doc_upd.data_ptr()
         b.n_docs = doc_upd.numel() - 1
         b.n_upd = upd_off.numel() - 1
-        b.format = fmt
+        b.format = self._format(op, fmt)
         b.mem = 1
         if op == "diff":
             b.sv_arena = sv_arena.data_ptr()
@@ -348,13 +354,15 @@ def parseUpdateMetaV2(update):
     return parseUpdateMetaBatch([update], 2, True)[0]
 
 
-def mergeDeleteSetsBatch(docs, fmt=1, raise_errors=False):
+def mergeDeleteSetsBatch(docs, fmt=1, raise_errors=False, reference=False):
     """PermanentUserData's delete-set merge (reference src/utils/PermanentUserData.js:49-54) over a batch:
     docs is a list of lists of encoded delete sets (DSEncoderV1 bytes, or DSEncoderV2 with fmt=2); returns
-    one encoded merged delete set per document."""
+    one encoded merged delete set per document.  reference=True: gaberogan/yjs@v0's own coalescing (only
+    exactly adjacent ranges merge, DeleteSet.js:113-135); default: yjs 13.5.16's (overlaps merge too)."""
     arena, upd_off, doc_upd = pack_docs(docs)
-    return _unpack(*_engine().run_host("dsmerge", fmt, arena, upd_off, doc_upd), raise_errors)
+    return _unpack(*_engine().run_host("dsmerge_ref" if reference else "dsmerge", fmt, arena, upd_off, doc_upd),
+                   raise_errors)
 
 
-def mergeEncodedDeleteSets(encoded_dss, fmt=1):
-    return mergeDeleteSetsBatch([list(encoded_dss)], fmt, True)[0]
+def mergeEncodedDeleteSets(encoded_dss, fmt=1, reference=False):
+    return mergeDeleteSetsBatch([list(encoded_dss)], fmt, True, reference)[0]
