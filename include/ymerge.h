@@ -22,7 +22,10 @@
  *
  * Results: out_off[d] / out_len[d] locate doc d's output inside out_arena (device batches: 16-byte
  * aligned slots, not necessarily contiguous or in document order; host batches: packed back to back in
- * document order); status[d] is a YM_* code.  A doc whose status is not YM_OK has out_len[d] = 0.
+ * document order); status[d] is a status word: bits 0-7 the YM_* class (YM_STATUS_CLASS), bits 8-15
+ * which of the class's exceptions yjs throws and bits 16-30 its argument -- ym_strerror(status[d])
+ * renders the message yjs's exception carries under V8 (e.g. "Invalid typed array length: 7").
+ * A doc whose status is not YM_OK has out_len[d] = 0.
  * Errors are per document; the batch always completes.
  * ym_out_bound() gives a capacity that normally suffices; out->used reports what was needed.
  */
@@ -47,6 +50,8 @@ enum {
   YM_ERR_METHOD = 8,      /* Error('Method unimplemented')                                       */
   YM_ERR_CAPACITY = 9,    /* output arena too small: call again with a larger cap                */
 };
+
+#define YM_STATUS_CLASS(s) ((s) & 0xff)
 
 enum { YM_MEM_HOST = 0, YM_MEM_DEVICE = 1 };
 enum { YM_V1 = 1, YM_V2 = 2 };
@@ -89,7 +94,9 @@ typedef struct ym_stats {
 
 int ym_init(int device);           /* select the HIP device for this thread; 0 on success */
 int ym_shutdown(void);
-const char *ym_strerror(int code); /* message of a status / return code */
+/* message of a status word / return code: for a per-document exception the text yjs's exception
+ * carries (Node 12 / V8 7.x wording; thread-local buffer, valid until the thread's next call) */
+const char *ym_strerror(int code);
 uint64_t ym_out_bound(const ym_batch *b); /* a capacity that is normally sufficient for ym_* */
 
 /* stream: a hipStream_t (NULL = the library's stream for the device).  Return value: 0, or

@@ -11,9 +11,11 @@
 //                                                      (yjs 13.5.x convertUpdateFormat; format = the input's)
 //   parseUpdateMeta(update) / parseUpdateMetaV2 -> {from: Map, to: Map}, parseUpdateMetaBatch(updates, {format})
 //                                                      (yjs 13.5.16 parseUpdateMeta[V2])
-//   mergeDeleteSetsBatch(docs, {format}), mergeEncodedDeleteSets(encodedDss, {format})
+//   mergeDeleteSetsBatch(docs, {format, reference}), mergeEncodedDeleteSets(encodedDss, {format, reference})
 //                                                      (PermanentUserData.js:49-54: mergeDeleteSets over
 //                                                       encoded delete sets -> one encoded delete set)
+//   every *Batch function also as *BatchAsync(...) -> Promise (the GPU call off the event loop)
+// Exceptions carry yjs's class and message (V8 wording; include/ymerge.h status words).
 // There is no CPU fallback: a missing addon or GPU throws.
 'use strict'
 const path = require('path')
@@ -31,20 +33,21 @@ function init () {
 const OP = { merge: 0, diff: 1, sv: 2, conv: 3, meta: 4, dsmerge: 5 }
 const fmtOf = o => (o && (o.format === 'v2' || o.format === 2)) ? 2 : 1
 
-// status -> the exception yjs itself throws for that input
+// status word -> the exception yjs itself throws for that input: the class from bits 0-7, the message
+// (V8's wording, e.g. "Invalid typed array length: 7") rendered by the library (ym_strerror)
 function toError (st) {
-  switch (st) {
-    case 1: return new Error('Integer out of range!')
-    case 2: return new Error('Unexpected case')
-    case 3: return new URIError('URI malformed')
-    case 4: return new TypeError('unknown content, type or value tag')
-    case 5: return new RangeError('read past the end of the update')
-    case 6: return new SyntaxError('invalid JSON in update')
-    case 7: { const e = new Error('ymerge: input needs a canonicalisation the engine does not implement'); e.code = 'YM_UNSUPPORTED'; return e }
-    case 8: return new Error('Method unimplemented')
-    default: return new Error('ymerge status ' + st)
+  const msg = addon.strerror(st)
+  switch (st & 0xff) {
+    case 1: case 2: case 8: return new Error(msg)
+    case 3: return new URIError(msg)
+    case 4: return new TypeError(msg)
+    case 5: return new RangeError(msg)
+    case 6: return new SyntaxError(msg)
+    case 7: { const e = new Error('ymerge: ' + msg); e.code = 'YM_UNSUPPORTED'; return e }
+    default: return new Error('ymerge status ' + st + ': ' + msg)
   }
 }
+const YM_DS_REF = 0x100 // mergeDeleteSets with the reference's adjacency-only coalescing (include/ymerge.h)
 
 function pack (docs) {
   let n = 0; let bytes = 0
@@ -76,27 +79,30 @@ function unpack (res, throwErrors) {
   return out
 }
 
-function mergeUpdatesBatch (docs, opts, throwErrors = false) {
+// every batch call: run(...) synchronously, or runAsync(...) -> Promise (napi_async_work: the GPU call
+// runs on a libuv worker thread and the event loop stays free)
+function call (async, args, done) {
   init()
-  const p = pack(docs)
-  return unpack(addon.run(OP.merge, fmtOf(opts), p.arena, p.updOff, p.docUpd), throwErrors)
+  if (!async) return done(addon.run(...args))
+  return addon.runAsync(...args).then(done)
 }
-function diffUpdateBatch (updates, svs, opts, throwErrors = false) {
-  init()
+function mergeUpdatesBatch (docs, opts, throwErrors = false, async = false) {
+  const p = pack(docs)
+  return call(async, [OP.merge, fmtOf(opts), p.arena, p.updOff, p.docUpd], r => unpack(r, throwErrors))
+}
+function diffUpdateBatch (updates, svs, opts, throwErrors = false, async = false) {
   const p = pack(updates.map(u => [u]))
   const s = pack(svs.map(x => [x]))
-  return unpack(addon.run(OP.diff, fmtOf(opts), p.arena, p.updOff, p.docUpd, s.arena, s.updOff), throwErrors)
+  return call(async, [OP.diff, fmtOf(opts), p.arena, p.updOff, p.docUpd, s.arena, s.updOff], r => unpack(r, throwErrors))
 }
-function encodeStateVectorFromUpdateBatch (updates, opts, throwErrors = false) {
-  init()
+function encodeStateVectorFromUpdateBatch (updates, opts, throwErrors = false, async = false) {
   const p = pack(updates.map(u => [u]))
-  return unpack(addon.run(OP.sv, fmtOf(opts), p.arena, p.updOff, p.docUpd), throwErrors)
+  return call(async, [OP.sv, fmtOf(opts), p.arena, p.updOff, p.docUpd], r => unpack(r, throwErrors))
 }
 
-function convertUpdateFormatBatch (updates, opts, throwErrors = false) {
-  init()
+function convertUpdateFormatBatch (updates, opts, throwErrors = false, async = false) {
   const p = pack(updates.map(u => [u]))
-  return unpack(addon.run(OP.conv, fmtOf(opts), p.arena, p.updOff, p.docUpd), throwErrors)
+  return call(async, [OP.conv, fmtOf(opts), p.arena, p.updOff, p.docUpd], r => unpack(r, throwErrors))
 }
 
 // the engine writes parseUpdateMeta's two Maps as two encoded state vectors (from, then to)
@@ -111,16 +117,26 @@ function decodeMeta (b) {
   }
   return res
 }
-function parseUpdateMetaBatch (updates, opts, throwErrors = false) {
-  init()
+function parseUpdateMetaBatch (updates, opts, throwErrors = false, async = false) {
   const p = pack(updates.map(u => [u]))
-  return unpack(addon.run(OP.meta, fmtOf(opts), p.arena, p.updOff, p.docUpd), throwErrors).map(r => r instanceof Error ? r : decodeMeta(r))
+  return call(async, [OP.meta, fmtOf(opts), p.arena, p.updOff, p.docUpd],
+    r => unpack(r, throwErrors).map(x => x instanceof Error ? x : decodeMeta(x)))
 }
-function mergeDeleteSetsBatch (docs, opts, throwErrors = false) {
-  init()
+// opts.reference: the reference's own sortAndMergeDeleteSet (DeleteSet.js:113-135, only adjacent ranges
+// coalesce) instead of yjs 13.5.16's union
+function mergeDeleteSetsBatch (docs, opts, throwErrors = false, async = false) {
   const p = pack(docs)
-  return unpack(addon.run(OP.dsmerge, fmtOf(opts), p.arena, p.updOff, p.docUpd), throwErrors)
+  const fmt = fmtOf(opts) | (opts && opts.reference ? YM_DS_REF : 0)
+  return call(async, [OP.dsmerge, fmt, p.arena, p.updOff, p.docUpd], r => unpack(r, throwErrors))
 }
+// Promise-returning batch forms: reject on a device failure, resolve to per-document results (bytes
+// or the Error yjs would throw for that document)
+const mergeUpdatesBatchAsync = (docs, opts) => mergeUpdatesBatch(docs, opts, false, true)
+const diffUpdateBatchAsync = (updates, svs, opts) => diffUpdateBatch(updates, svs, opts, false, true)
+const encodeStateVectorFromUpdateBatchAsync = (updates, opts) => encodeStateVectorFromUpdateBatch(updates, opts, false, true)
+const convertUpdateFormatBatchAsync = (updates, opts) => convertUpdateFormatBatch(updates, opts, false, true)
+const parseUpdateMetaBatchAsync = (updates, opts) => parseUpdateMetaBatch(updates, opts, false, true)
+const mergeDeleteSetsBatchAsync = (docs, opts) => mergeDeleteSetsBatch(docs, opts, false, true)
 
 // single-document yjs signatures (mergeUpdates([u]) returns the same object, like yjs)
 const mergeUpdates = updates => updates.length === 1 ? updates[0] : mergeUpdatesBatch([updates], { format: 'v1' }, true)[0]
@@ -139,5 +155,7 @@ module.exports = {
   mergeUpdates, mergeUpdatesV2, diffUpdate, diffUpdateV2, encodeStateVectorFromUpdate, encodeStateVectorFromUpdateV2,
   mergeUpdatesBatch, diffUpdateBatch, encodeStateVectorFromUpdateBatch,
   convertUpdateFormatV1ToV2, convertUpdateFormatV2ToV1, convertUpdateFormatBatch,
-  parseUpdateMeta, parseUpdateMetaV2, parseUpdateMetaBatch, mergeDeleteSetsBatch, mergeEncodedDeleteSets
+  parseUpdateMeta, parseUpdateMetaV2, parseUpdateMetaBatch, mergeDeleteSetsBatch, mergeEncodedDeleteSets,
+  mergeUpdatesBatchAsync, diffUpdateBatchAsync, encodeStateVectorFromUpdateBatchAsync, convertUpdateFormatBatchAsync,
+  parseUpdateMetaBatchAsync, mergeDeleteSetsBatchAsync
 }

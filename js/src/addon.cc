@@ -2,11 +2,18 @@
 // Each call takes one packed batch (arena + offsets) in host memory and returns
 // { arena, offsets, lengths, status } -- the JS module (js/index.js) turns that into per-document
 // Uint8Arrays and yjs-shaped exceptions.
+//   run(op, format, arena, updOff, docUpd[, svArena, svOff])       synchronous
+//   runAsync(op, format, arena, updOff, docUpd[, svArena, svOff])  -> Promise (napi_async_work: the
+//        library call runs on a libuv worker thread; the inputs are pinned by references until it ends)
+//   strerror(status)                                              ym_strerror (yjs's exception text)
+// The output arena is allocated uninitialised (the library writes every byte it reports) and handed to
+// JS as an external ArrayBuffer: no zero-fill, no second copy.
 #include <node_api.h>
 
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+
 #include <vector>
 
 #include "../../include/ymerge.h"
@@ -33,8 +40,8 @@ static bool get_u8(napi_env env, napi_value v, const uint8_t **p, size_t *n) {
   return true;
 }
 
-// u64 offsets from a BigUint64Array or a Float64Array (exact below 2^53)
-static bool get_u64(napi_env env, napi_value v, std::vector<uint64_t> &out) {
+// u64 offsets from a BigUint64Array (used in place), a Float64Array (exact below 2^53) or a Uint32Array
+static bool get_u64(napi_env env, napi_value v, const uint64_t **p, size_t *n, std::vector<uint64_t> &conv) {
   bool is_ta = false;
   if (napi_is_typedarray(env, v, &is_ta) != napi_ok || !is_ta) return false;
   napi_typedarray_type t;
@@ -43,11 +50,13 @@ static bool get_u64(napi_env env, napi_value v, std::vector<uint64_t> &out) {
   napi_value ab;
   size_t off;
   if (napi_get_typedarray_info(env, v, &t, &len, &data, &ab, &off) != napi_ok) return false;
-  out.resize(len);
-  if (t == napi_biguint64_array) memcpy(out.data(), data, len * 8);
-  else if (t == napi_float64_array) for (size_t i = 0; i < len; i++) out[i] = (uint64_t)((double *)data)[i];
-  else if (t == napi_uint32_array) for (size_t i = 0; i < len; i++) out[i] = ((uint32_t *)data)[i];
+  *n = len;
+  if (t == napi_biguint64_array) { *p = (const uint64_t *)data; return true; }
+  conv.resize(len);
+  if (t == napi_float64_array) for (size_t i = 0; i < len; i++) conv[i] = (uint64_t)((double *)data)[i];
+  else if (t == napi_uint32_array) for (size_t i = 0; i < len; i++) conv[i] = ((uint32_t *)data)[i];
   else return false;
+  *p = conv.data();
   return true;
 }
 
@@ -65,14 +74,91 @@ static bool get_u32(napi_env env, napi_value v, const uint32_t **p, size_t *n) {
   return true;
 }
 
-static napi_value make_u8(napi_env env, const uint8_t *src, size_t n) {
-  void *data = nullptr;
-  napi_value ab, ta;
-  if (napi_create_arraybuffer(env, n, &data, &ab) != napi_ok) return nullptr;
-  if (n) memcpy(data, src, n);
-  if (napi_create_typedarray(env, napi_uint8_array, n, ab, 0, &ta) != napi_ok) return nullptr;
-  return ta;
+// One library call: inputs (borrowed from the JS typed arrays), outputs (owned until handed to JS).
+struct Job {
+  int32_t op = 0;
+  ym_batch b;
+  std::vector<uint64_t> upd_conv, sv_conv;
+  uint8_t *arena = nullptr;  // malloc'ed, uninitialised
+  uint64_t used = 0;
+  std::vector<uint64_t> out_off, out_len;
+  std::vector<int32_t> status;
+  int rc = 0;
+  // async only
+  napi_ref refs[7] = {};
+  size_t nrefs = 0;
+  napi_deferred deferred = nullptr;
+  napi_async_work work = nullptr;
+  ~Job() { free(arena); }
+};
+
+// parses run()'s arguments into job (throws and returns false on a bad argument)
+static bool parse(napi_env env, napi_callback_info info, Job &j, napi_value *argv, size_t &argc) {
+  argc = 7;
+  if (napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr) != napi_ok) return false;
+  if (argc < 5) { napi_throw_type_error(env, nullptr, "run(op, format, arena, updOff, docUpd[, svArena, svOff])"); return false; }
+  int32_t fmt = 1;
+  if (napi_get_value_int32(env, argv[0], &j.op) != napi_ok || napi_get_value_int32(env, argv[1], &fmt) != napi_ok) {
+    napi_throw_type_error(env, nullptr, "op and format must be integers");
+    return false;
+  }
+  const uint8_t *arena = nullptr, *sva = nullptr;
+  const uint64_t *upd_off = nullptr, *sv_off = nullptr;
+  size_t alen = 0, svlen = 0, ndocs1 = 0, nupd1 = 0, nsv1 = 0;
+  const uint32_t *doc_upd = nullptr;
+  if (!get_u8(env, argv[2], &arena, &alen) || !get_u64(env, argv[3], &upd_off, &nupd1, j.upd_conv) ||
+      !get_u32(env, argv[4], &doc_upd, &ndocs1) || nupd1 == 0 || ndocs1 == 0) {
+    napi_throw_type_error(env, nullptr, "arena must be a Uint8Array, updOff a BigUint64Array/Float64Array, docUpd a Uint32Array");
+    return false;
+  }
+  if (upd_off[nupd1 - 1] > alen || doc_upd[ndocs1 - 1] > nupd1 - 1) {
+    napi_throw_range_error(env, nullptr, "updOff / docUpd exceed the arena");
+    return false;
+  }
+  if (j.op == 1 && (argc < 7 || !get_u8(env, argv[5], &sva, &svlen) || !get_u64(env, argv[6], &sv_off, &nsv1, j.sv_conv) ||
+                    nsv1 != ndocs1 || sv_off[nsv1 - 1] > svlen)) {
+    napi_throw_type_error(env, nullptr, "diff needs svArena (Uint8Array) and svOff (one more entry than documents)");
+    return false;
+  }
+  memset(&j.b, 0, sizeof(j.b));
+  j.b.arena = arena;
+  j.b.upd_off = upd_off;
+  j.b.doc_upd = doc_upd;
+  j.b.n_docs = (uint32_t)(ndocs1 - 1);
+  j.b.n_upd = (uint32_t)(nupd1 - 1);
+  j.b.format = fmt;
+  j.b.mem = YM_MEM_HOST;
+  j.b.sv_arena = sva;
+  j.b.sv_off = j.op == 1 ? sv_off : nullptr;
+  return true;
 }
+
+// the library call (no N-API use: runs on the main thread or a worker)
+static void execute(Job &j) {
+  const size_t nd = j.b.n_docs ? j.b.n_docs : 1;
+  j.out_off.resize(nd);
+  j.out_len.resize(nd);
+  j.status.resize(nd);
+  uint64_t cap = ym_out_bound(&j.b);
+  for (int attempt = 0; attempt < 4; attempt++) {
+    free(j.arena);
+    j.arena = (uint8_t *)malloc(cap ? cap : 1);
+    if (!j.arena) { j.rc = YM_ERR_CAPACITY; return; }
+    ym_out o = {j.arena, cap, j.out_off.data(), j.out_len.data(), j.status.data(), 0};
+    j.rc = j.op == 0   ? ym_merge(&j.b, &o, nullptr, nullptr)
+           : j.op == 1 ? ym_diff(&j.b, &o, nullptr, nullptr)
+           : j.op == 3 ? ym_convert(&j.b, &o, nullptr, nullptr)
+           : j.op == 4 ? ym_meta(&j.b, &o, nullptr, nullptr)
+           : j.op == 5 ? ym_ds_merge(&j.b, &o, nullptr, nullptr)
+                       : ym_sv(&j.b, &o, nullptr, nullptr);
+    j.used = o.used;
+    if (j.rc == YM_ERR_CAPACITY) { cap = o.used + 4096; continue; }
+    break;
+  }
+}
+
+static void free_arena(napi_env, void *data, void *) { free(data); }
+
 static napi_value make_f64(napi_env env, const uint64_t *src, size_t n) {
   void *data = nullptr;
   napi_value ab, ta;
@@ -90,80 +176,111 @@ static napi_value make_i32(napi_env env, const int32_t *src, size_t n) {
   return ta;
 }
 
-// run(op, format, arena, updOff, docUpd[, svArena, svOff])
-static napi_value Run(napi_env env, napi_callback_info info) {
-  size_t argc = 7;
-  napi_value argv[7];
-  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
-  if (argc < 5) { napi_throw_type_error(env, nullptr, "run(op, format, arena, updOff, docUpd[, svArena, svOff])"); return nullptr; }
-  int32_t op = 0, fmt = 1;
-  NAPI_CALL(env, napi_get_value_int32(env, argv[0], &op));
-  NAPI_CALL(env, napi_get_value_int32(env, argv[1], &fmt));
-  const uint8_t *arena = nullptr, *sva = nullptr;
-  size_t alen = 0, svlen = 0, ndocs1 = 0;
-  const uint32_t *doc_upd = nullptr;
-  std::vector<uint64_t> upd_off, sv_off;
-  if (!get_u8(env, argv[2], &arena, &alen) || !get_u64(env, argv[3], upd_off) || !get_u32(env, argv[4], &doc_upd, &ndocs1) ||
-      upd_off.empty() || ndocs1 == 0) {
-    napi_throw_type_error(env, nullptr, "arena must be a Uint8Array, updOff a BigUint64Array/Float64Array, docUpd a Uint32Array");
+// the result object, or nullptr with *err set to the exception to throw / reject with
+static napi_value result(napi_env env, Job &j, napi_value *err) {
+  *err = nullptr;
+  if (j.rc != 0) {
+    napi_value code, msg;
+    napi_create_string_utf8(env, "YMERGE_DEVICE", NAPI_AUTO_LENGTH, &code);
+    napi_create_string_utf8(env, ym_strerror(j.rc), NAPI_AUTO_LENGTH, &msg);
+    napi_create_error(env, code, msg, err);
     return nullptr;
   }
-  if (op == 1 && (argc < 7 || !get_u8(env, argv[5], &sva, &svlen) || !get_u64(env, argv[6], sv_off))) {
-    napi_throw_type_error(env, nullptr, "diff needs svArena (Uint8Array) and svOff");
+  // host batches: the outputs are packed back to back, `used` bytes in all
+  const uint64_t n = j.used;
+  napi_value ab, ta, res;
+  if (n > 0) {
+    if (napi_create_external_arraybuffer(env, j.arena, n, free_arena, nullptr, &ab) != napi_ok) return nullptr;
+    j.arena = nullptr;  // owned by the ArrayBuffer now
+  } else if (napi_create_arraybuffer(env, 0, nullptr, &ab) != napi_ok) {
     return nullptr;
   }
-  ym_batch b;
-  memset(&b, 0, sizeof(b));
-  b.arena = arena;
-  b.upd_off = upd_off.data();
-  b.doc_upd = doc_upd;
-  b.n_docs = (uint32_t)(ndocs1 - 1);
-  b.n_upd = (uint32_t)(upd_off.size() - 1);
-  b.format = fmt;
-  b.mem = YM_MEM_HOST;
-  b.sv_arena = sva;
-  b.sv_off = op == 1 ? sv_off.data() : nullptr;
-  uint64_t cap = ym_out_bound(&b);
-  std::vector<uint8_t> out_arena;
-  std::vector<uint64_t> out_off(b.n_docs ? b.n_docs : 1), out_len(b.n_docs ? b.n_docs : 1);
-  std::vector<int32_t> status(b.n_docs ? b.n_docs : 1);
-  int rc = 0;
-  for (int attempt = 0; attempt < 4; attempt++) {
-    out_arena.assign(cap ? cap : 1, 0);
-    ym_out o = {out_arena.data(), cap, out_off.data(), out_len.data(), status.data(), 0};
-    rc = op == 0   ? ym_merge(&b, &o, nullptr, nullptr)
-         : op == 1 ? ym_diff(&b, &o, nullptr, nullptr)
-         : op == 3 ? ym_convert(&b, &o, nullptr, nullptr)
-         : op == 4 ? ym_meta(&b, &o, nullptr, nullptr)
-         : op == 5 ? ym_ds_merge(&b, &o, nullptr, nullptr)
-                   : ym_sv(&b, &o, nullptr, nullptr);
-    if (rc == YM_ERR_CAPACITY) { cap = o.used + 4096; continue; }
-    break;
-  }
-  if (rc != 0) {
-    napi_throw_error(env, "YMERGE_DEVICE", ym_strerror(rc));
-    return nullptr;
-  }
-  napi_value res;
-  NAPI_CALL(env, napi_create_object(env, &res));
-  NAPI_CALL(env, napi_set_named_property(env, res, "arena", make_u8(env, out_arena.data(), out_arena.size())));
-  NAPI_CALL(env, napi_set_named_property(env, res, "offsets", make_f64(env, out_off.data(), b.n_docs)));
-  NAPI_CALL(env, napi_set_named_property(env, res, "lengths", make_f64(env, out_len.data(), b.n_docs)));
-  NAPI_CALL(env, napi_set_named_property(env, res, "status", make_i32(env, status.data(), b.n_docs)));
+  if (napi_create_typedarray(env, napi_uint8_array, n, ab, 0, &ta) != napi_ok) return nullptr;
+  if (napi_create_object(env, &res) != napi_ok) return nullptr;
+  napi_set_named_property(env, res, "arena", ta);
+  napi_set_named_property(env, res, "offsets", make_f64(env, j.out_off.data(), j.b.n_docs));
+  napi_set_named_property(env, res, "lengths", make_f64(env, j.out_len.data(), j.b.n_docs));
+  napi_set_named_property(env, res, "status", make_i32(env, j.status.data(), j.b.n_docs));
   return res;
+}
+
+static napi_value Run(napi_env env, napi_callback_info info) {
+  Job j;
+  napi_value argv[7];
+  size_t argc;
+  if (!parse(env, info, j, argv, argc)) return nullptr;
+  execute(j);
+  napi_value err, res = result(env, j, &err);
+  if (err) napi_throw(env, err);
+  return res;
+}
+
+static void async_execute(napi_env, void *data) { execute(*static_cast<Job *>(data)); }
+static void async_complete(napi_env env, napi_status status, void *data) {
+  Job *j = static_cast<Job *>(data);
+  napi_value err = nullptr, res = nullptr;
+  if (status != napi_ok) {
+    napi_value msg;
+    napi_create_string_utf8(env, "ymerge: async work cancelled", NAPI_AUTO_LENGTH, &msg);
+    napi_create_error(env, nullptr, msg, &err);
+  } else {
+    res = result(env, *j, &err);
+    if (!res && !err) {
+      napi_value msg;
+      napi_create_string_utf8(env, "ymerge: could not build the result", NAPI_AUTO_LENGTH, &msg);
+      napi_create_error(env, nullptr, msg, &err);
+    }
+  }
+  if (err) napi_reject_deferred(env, j->deferred, err);
+  else napi_resolve_deferred(env, j->deferred, res);
+  for (size_t i = 0; i < j->nrefs; i++) napi_delete_reference(env, j->refs[i]);
+  napi_delete_async_work(env, j->work);
+  delete j;
+}
+
+static napi_value RunAsync(napi_env env, napi_callback_info info) {
+  Job *j = new Job();
+  napi_value argv[7];
+  size_t argc;
+  if (!parse(env, info, *j, argv, argc)) { delete j; return nullptr; }
+  // the typed arrays stay alive (and their memory in place) until the work completes
+  for (size_t i = 2; i < argc; i++) napi_create_reference(env, argv[i], 1, &j->refs[j->nrefs++]);
+  napi_value promise, name;
+  if (napi_create_promise(env, &j->deferred, &promise) != napi_ok) { delete j; return nullptr; }
+  napi_create_string_utf8(env, "ymerge", NAPI_AUTO_LENGTH, &name);
+  if (napi_create_async_work(env, nullptr, name, async_execute, async_complete, j, &j->work) != napi_ok ||
+      napi_queue_async_work(env, j->work) != napi_ok) {
+    napi_throw_error(env, "YMERGE_NAPI", "could not queue the async work");
+    return nullptr;
+  }
+  return promise;
+}
+
+static napi_value StrError(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  int32_t st = 0;
+  if (argc > 0) NAPI_CALL(env, napi_get_value_int32(env, argv[0], &st));
+  napi_value r;
+  NAPI_CALL(env, napi_create_string_utf8(env, ym_strerror(st), NAPI_AUTO_LENGTH, &r));
+  return r;
 }
 
 static napi_value Init(napi_env env, napi_value exports) {
   int32_t dev = 0;
   const char *e = getenv("YMERGE_DEVICE");
   if (e) dev = atoi(e);
-  napi_value fn;
-  if (napi_create_function(env, "run", NAPI_AUTO_LENGTH, Run, nullptr, &fn) != napi_ok) return nullptr;
-  napi_set_named_property(env, exports, "run", fn);
+  struct { const char *name; napi_callback cb; } fns[] = {{"run", Run}, {"runAsync", RunAsync}, {"strerror", StrError}};
+  for (auto &f : fns) {
+    napi_value fn;
+    if (napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &fn) != napi_ok) return nullptr;
+    napi_set_named_property(env, exports, f.name, fn);
+  }
   napi_value d;
   napi_create_int32(env, dev, &d);
   napi_set_named_property(env, exports, "device", d);
-  (void)ym_init;  // the library selects the device lazily (ym_init is called by the JS module on first use)
+  // the library selects the device lazily (ym_init is called by the JS module on first use)
   napi_value initfn;
   napi_create_function(env, "init", NAPI_AUTO_LENGTH, [](napi_env env, napi_callback_info info) -> napi_value {
     size_t argc = 1;

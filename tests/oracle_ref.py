@@ -38,6 +38,23 @@ def js_error_status(name, message):
     raise ValueError(f"unmapped JS error {name}: {message}")
 
 
+# yjs 13.5.16's bundle is minified: its unknown-content-ref TypeError names the minified callee; the
+# engine reports the reference's own source text (src/structs/Item.js readItemContent) instead
+_MINIFIED = {"ai[(e & b.kr)] is not a function": "contentRefs[(info & binary.BITS5)] is not a function"}
+
+
+def js_error_mismatch(status_word, name, message):
+    """None if status word `status_word` is the exception (class and message) yjs threw, else a reason."""
+    want = js_error_status(name, message)
+    if int(status_word) & 0xff != want:
+        return f"class {int(status_word) & 0xff} != {want}"
+    from yjs_amd import status_message
+    got = status_message(int(status_word))
+    if got != _MINIFIED.get(message, message):
+        return f"message {got!r} != {message!r}"
+    return None
+
+
 _lib = None
 
 

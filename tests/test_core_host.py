@@ -38,9 +38,9 @@ def check(cases, outs, st):
     bad = []
     for i, c in enumerate(cases):
         if "error" in c:
-            want = O.js_error_status(c["error"], c["message"])
-            if st[i] != want:
-                bad.append((c["id"], "error", int(st[i]), want))
+            why = O.js_error_mismatch(st[i], c["error"], c["message"])
+            if why:
+                bad.append((c["id"], "error", why))
         elif st[i] != 0 or outs[i] != c["expect"]:
             bad.append((c["id"], "bytes", int(st[i])))
     return bad

@@ -19,6 +19,7 @@ def test_js_api_golden():
     res = json.loads(line[-1])
     assert r.returncode == 0 and res["bad"] == 0, res
     assert res["ok"] >= 990 and res["unsupported"] == 0, res
+    assert res["async_ok"] >= 800, res  # mergeUpdatesBatchAsync (napi_async_work) over the golden merges
 
 
 @pytest.mark.skipif(shutil.which("node") is None, reason="node not installed on this box")

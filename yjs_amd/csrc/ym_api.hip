@@ -590,14 +590,39 @@ int ym_shutdown(void) {
 }
 
 const char *ym_strerror(int code) {
+  if (code > 0 && (code >> 8) != 0) {  // a per-document exception with its detail (ym_core.h D_*)
+    static thread_local char buf[160];
+    const int detail = (code >> 8) & 0xff, arg = (code >> 16) & 0x7fff;
+    static const char *getters[4] = {"length", "byteLength", "byteOffset", "buffer"};
+    switch (detail) {
+      case 1: return "contentRefs[(info & binary.BITS5)] is not a function";
+      case 2: return "typeRefs[decoder.readTypeRef(...)] is not a function";
+      case 3: return "readAnyLookupTable[(127 - readUint8(...))] is not a function";
+      case 4: return "Do not know how to serialize a BigInt";
+      case 5: return "Method get TypedArray.prototype.byteLength called on incompatible receiver [object Object]";
+      case 6:
+        snprintf(buf, sizeof buf, "Cannot set property %s of [object Object] which has only a getter", getters[arg & 3]);
+        return buf;
+      case 7: return "Cannot assign to read only property 'BYTES_PER_ELEMENT' of object '[object Object]'";
+      case 8: return "Cannot read property 'length' of undefined";
+      case 9: return "Invalid code point NaN";
+      case 10: return "Offset is outside the bounds of the DataView";
+      case 11:
+        if (arg == 0x7fff) return "Invalid typed array length";
+        snprintf(buf, sizeof buf, "Invalid typed array length: %d", arg);
+        return buf;
+      default: break;
+    }
+    code &= 0xff;
+  }
   switch (code) {
     case YM_OK: return "ok";
     case YM_ERR_INT_RANGE: return "Integer out of range!";
     case YM_ERR_UNEXPECTED: return "Unexpected case";
     case YM_ERR_URI: return "URI malformed";
-    case YM_ERR_TYPE: return "TypeError: unknown content, type or value tag";
-    case YM_ERR_RANGE: return "RangeError: read past the end of the update";
-    case YM_ERR_SYNTAX: return "SyntaxError: invalid JSON";
+    case YM_ERR_TYPE: return "unknown content, type or value tag";
+    case YM_ERR_RANGE: return "read past the end of the update";
+    case YM_ERR_SYNTAX: return "Unexpected token in JSON";
     case YM_ERR_UNSUPPORTED: return "input needs a canonicalisation the engine does not implement";
     case YM_ERR_METHOD: return "Method unimplemented";
     case YM_ERR_CAPACITY: return "output arena too small";

@@ -398,7 +398,7 @@ YM_INL U16 cv_key(const uint8_t *A, uint8_t g, const CvEntry &e) { return g == G
 // The simulation re-scans entries on demand (no workspace); prototype objects nest at most PROTO_DEPTH
 // levels (deeper: UNSUPPORTED).
 // ------------------------------------------------------------------------------------------------
-enum : int { SET_OWN = 0, SET_IGNORE = 1, SET_PROTO = 2, SET_TYPEERR = 3, SET_DEEP = 4 };
+enum : int { SET_OWN = 0, SET_IGNORE = 1, SET_PROTO = 2, SET_DEEP = 4, SET_TYPEERR = 8 };  // SET_TYPEERR + key index
 enum : uint8_t { PK_PLAIN = 0, PK_NULL = 1, PK_ARRAY = 2, PK_BYTES = 3 };
 constexpr int PROTO_DEPTH = 4;
 struct ObjSim { uint64_t proto; int err; int live; };  // proto: value position (0 = Object.prototype)
@@ -473,7 +473,8 @@ template <int D> YM_NUM_FN int set_kind(const uint8_t *A, uint64_t end, uint64_t
     if (t == 117) return dunder ? setter : SET_OWN;  // Array (writable data) -> Array.prototype -> Object.prototype
     if (t == 116) {
       const char *ro[5] = {"length", "byteLength", "byteOffset", "buffer", "BYTES_PER_ELEMENT"};
-      if (key_is_any(key, ro, 5)) return SET_TYPEERR;
+      for (int q = 0; q < 5; q++)
+        if (key_is_any(key, ro + q, 1)) return SET_TYPEERR + q;
       int64_t idx;
       if (key_numeric(key, &idx)) {
         uint64_t qq = P + 1;
@@ -514,7 +515,10 @@ template <int D> YM_NUM_FN ObjSim obj_sim(const uint8_t *A, uint64_t end, uint64
     } else if (r.proto != 0 || dunder) {  // on the default chain every other key is a plain own property
       const int sk = set_kind<D>(A, end, r.proto, k, A[e.val]);
       if (sk == SET_DEEP) { r.err = ST_UNSUPPORTED; return r; }
-      if (sk == SET_TYPEERR) { r.err = ST_TYPE; return r; }
+      if (sk >= SET_TYPEERR) {  // an accessor without a setter / a read-only property on the chain (strict mode)
+        r.err = sk == SET_TYPEERR + 4 ? st_d(ST_TYPE, D_SET_RO) : st_d(ST_TYPE, D_SET_GETTER, sk - SET_TYPEERR);
+        return r;
+      }
       if (sk == SET_PROTO) { r.proto = e.val; live = 0; }
       else if (sk == SET_IGNORE) live = 0;
       else if (dunder) own_dunder = true;
@@ -718,7 +722,7 @@ YM_BIG void canon_value(Ctx &c, S &s, const uint8_t *A, uint64_t p, uint64_t end
           break;
         }
         case 122:
-          if (json_out) { seterr(c, ST_TYPE); return; }  // JSON.stringify(bigint)
+          if (json_out) { seterr(c, st_d(ST_TYPE, D_BIGINT_JSON)); return; }  // JSON.stringify(bigint)
           for (int i = 0; i < 9; i++) s.put(A[p + i]);
           break;
         case 119: {
@@ -756,12 +760,12 @@ YM_BIG void canon_value(Ctx &c, S &s, const uint8_t *A, uint64_t p, uint64_t end
           if (f.sim) {
             const ObjSim os = obj_sim<PROTO_DEPTH>(A, end, p, 0xFFFFFFFFu);
             const int kind = os.err ? -1 : proto_kind<PROTO_DEPTH>(A, end, os.proto);
-            if (os.err == ST_TYPE) { seterr(c, ST_TYPE); return; }
+            if ((os.err & 0xff) == ST_TYPE) { seterr(c, os.err); return; }
             if (kind < 0) { seterr(c, ST_UNSUPPORTED); return; }
             // writeAny: `instanceof Uint8Array` reads byteLength off a plain object (TypeError);
             // `instanceof Array` writes length and elements read through the prototype chain.
             // JSON.stringify serialises own keys whatever the prototype.
-            if (kind == PK_BYTES && !json_out) { seterr(c, ST_TYPE); return; }
+            if (kind == PK_BYTES && !json_out) { seterr(c, st_d(ST_TYPE, D_BYTELENGTH)); return; }
             if (kind == PK_ARRAY && !json_out) {
               uint64_t arr = 0;
               const uint8_t lk[6] = {'l', 'e', 'n', 'g', 't', 'h'};

@@ -37,6 +37,24 @@ enum : int {
   ST_UNSUPPORTED = 7, ST_METHOD = 8, ST_CAPACITY = 9,
   ST_RETRY = 100,  // internal: workspace too small for this doc, run again with more
 };
+// Which message the exception carries (yjs under V8, include/ymerge.h): status = class | detail << 8 |
+// argument << 16 (argument 0x7fff: unknown).  Class tests use st & 0xff.
+enum : int {
+  D_CONTENT_REF = 1,    // TypeError  contentRefs[(info & binary.BITS5)] is not a function   (Item.js readItemContent)
+  D_TYPE_REF = 2,       // TypeError  typeRefs[decoder.readTypeRef(...)] is not a function   (ContentType.js)
+  D_ANY_TAG = 3,        // TypeError  readAnyLookupTable[(127 - readUint8(...))] is not a function (lib0 readAny)
+  D_BIGINT_JSON = 4,    // TypeError  Do not know how to serialize a BigInt                   (JSON.stringify)
+  D_BYTELENGTH = 5,     // TypeError  Method get TypedArray.prototype.byteLength called on incompatible receiver [object Object]
+  D_SET_GETTER = 6,     // TypeError  Cannot set property <arg: length|byteLength|byteOffset|buffer> of [object Object] which has only a getter
+  D_SET_RO = 7,         // TypeError  Cannot assign to read only property 'BYTES_PER_ELEMENT' of object '[object Object]'
+  D_KEY_UNDEF = 8,      // TypeError  Cannot read property 'length' of undefined              (V2 writeKey(undefined))
+  D_CODEPOINT_NAN = 9,  // RangeError Invalid code point NaN                                  (lib0 readVarString, short)
+  D_DATAVIEW = 10,      // RangeError Offset is outside the bounds of the DataView            (readFloat32/64, readBigInt64)
+  D_TA_LENGTH = 11,     // RangeError Invalid typed array length: <arg>                       (lib0 readUint8Array)
+};
+YM_INL int st_d(int cls, int detail, uint64_t arg = 0) {
+  return cls | (detail << 8) | (int)((arg < 0x7fff ? arg : 0x7fff) << 16);
+}
 
 struct Ctx {
   int err;
@@ -158,7 +176,7 @@ YM_INL Span rd_vstr(Ctx &c, Rd &d) {
   uint64_t p0 = d.pos;
   uint64_t take;
   if (L - 1 < 100) {
-    if (d.pos > d.len || (uint64_t)L > d.len - d.pos) { seterr(c, ST_RANGE); return s; }  // fromCodePoint(undefined)
+    if (d.pos > d.len || (uint64_t)L > d.len - d.pos) { seterr(c, st_d(ST_RANGE, D_CODEPOINT_NAN)); return s; }  // fromCodePoint(undefined)
     take = L;
   } else {
     take = d.pos >= d.len ? 0 : (d.len - d.pos < L ? d.len - d.pos : L);  // subarray clamps
@@ -176,7 +194,7 @@ YM_INL Span rd_vbytes(Ctx &c, Rd &d) {
   Span s = {0, 0, 0, 0};
   uint32_t L = rd_vu(c, d);
   if (c.err) return s;
-  if (d.pos > d.len || (uint64_t)L > d.len - d.pos) { seterr(c, ST_RANGE); return s; }
+  if (d.pos > d.len || (uint64_t)L > d.len - d.pos) { seterr(c, st_d(ST_RANGE, D_TA_LENGTH, L)); return s; }
   s.off = d.start + d.pos;
   s.n = L;
   d.pos += L;
@@ -273,7 +291,7 @@ YM_BIG void any_skip(Ctx &c, Rd &d, int *noncanon) {
   for (;;) {
     // parse one value
     int tag = rbyte(c, d);
-    if (tag < 116 || tag > 127) { seterr(c, ST_TYPE); return; }
+    if (tag < 116 || tag > 127) { seterr(c, st_d(ST_TYPE, D_ANY_TAG)); return; }
     switch (tag) {
       case 127: case 126: case 121: case 120: break;
       case 125: {
@@ -286,14 +304,14 @@ YM_BIG void any_skip(Ctx &c, Rd &d, int *noncanon) {
         break;
       }
       case 124: {
-        if (d.pos > d.len || d.len - d.pos < 4) { seterr(c, ST_RANGE); return; }
+        if (d.pos > d.len || d.len - d.pos < 4) { seterr(c, st_d(ST_RANGE, D_DATAVIEW)); return; }
         double x = be_f32(c, d.start + d.pos);
         if (x != x || (num_is_int(x) && x <= 2147483647.0)) *noncanon = 1;
         d.pos += 4;
         break;
       }
       case 123: {
-        if (d.pos > d.len || d.len - d.pos < 8) { seterr(c, ST_RANGE); return; }
+        if (d.pos > d.len || d.len - d.pos < 8) { seterr(c, st_d(ST_RANGE, D_DATAVIEW)); return; }
         double x = be_f64(c, d.start + d.pos);
         if (num_is_int(x) && x <= 2147483647.0) *noncanon = 1;
         else if (x == x && (double)(float)x == x) *noncanon = 1;
@@ -301,7 +319,7 @@ YM_BIG void any_skip(Ctx &c, Rd &d, int *noncanon) {
         break;
       }
       case 122:
-        if (d.pos > d.len || d.len - d.pos < 8) { seterr(c, ST_RANGE); return; }
+        if (d.pos > d.len || d.len - d.pos < 8) { seterr(c, st_d(ST_RANGE, D_DATAVIEW)); return; }
         d.pos += 8;
         break;
       case 119: case 116: {  // writeVarString / writeVarUint8Array re-encode the length prefix
@@ -778,7 +796,7 @@ YM_BIG void read_content(Ctx &c, Reader &r, SStruct &s, int info) {
     case 7: {
       int64_t t = r.v2 ? (int64_t)uopt_read(c, r.tr) : (int64_t)rd_vu(c, r.rest);
       if (c.err) break;
-      if (t < 0 || t > 6) { seterr(c, ST_TYPE); break; }
+      if (t < 0 || t > 6) { seterr(c, st_d(ST_TYPE, D_TYPE_REF)); break; }
       s.cnt = t;
       s.len = 1;
       if (t == 3 || t == 5) {  // readKey (UpdateDecoder.js:382-391)
@@ -823,7 +841,7 @@ YM_BIG void read_content(Ctx &c, Reader &r, SStruct &s, int info) {
       s.len = 1;
       break;
     case 0: case 10: seterr(c, ST_UNEXPECTED); break;
-    default: seterr(c, ST_TYPE); break;
+    default: seterr(c, st_d(ST_TYPE, D_CONTENT_REF)); break;
   }
 }
 
@@ -1209,7 +1227,7 @@ YM_BIG void content_write(Ctx &c, Enc &e, const SStruct &s, int64_t off) {
         // (TypeError), V1 writeVarString writes encodeURIComponent(undefined) = "undefined"
         const char *lit = s.cnt == 3 ? "UNDEFINED" : "undefined";
         if (e.v2) {
-          if (s.cnt == 5) { seterr(c, ST_TYPE); break; }
+          if (s.cnt == 5) { seterr(c, st_d(ST_TYPE, D_KEY_UNDEF)); break; }
           idiff_w(e.kc, e.kc_s, e.kc_n, e.kc_d, e.keyClock++);
           if (e.pend_hi) { seterr(c, ST_URI); break; }
           for (const char *t = lit; *t; t++) o8(e.sb, (uint32_t)*t);

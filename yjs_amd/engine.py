@@ -45,22 +45,24 @@ class UnsupportedInput(YjsError):
 YM_DS_REF = 0x100  # ym_ds_merge: the reference's adjacency-only coalescing (include/ymerge.h)
 
 _STATUS_EXC = {
-    1: (YjsError, "Integer out of range!"),
-    2: (YjsError, "Unexpected case"),
-    3: (YjsURIError, "URI malformed"),
-    4: (YjsTypeError, "unknown content ref, type ref or any tag"),
-    5: (YjsRangeError, "read past the end of the update"),
-    6: (YjsSyntaxError, "invalid JSON"),
-    7: (UnsupportedInput, "input needs a canonicalisation the engine does not implement"),
-    8: (YjsError, "Method unimplemented"),
-    9: (YjsError, "output arena too small"),
+    1: YjsError, 2: YjsError, 3: YjsURIError, 4: YjsTypeError, 5: YjsRangeError, 6: YjsSyntaxError,
+    7: UnsupportedInput, 8: YjsError, 9: YjsError,
 }
+
+
+def status_class(st):
+    """The YM_* class of a status word (bits 0-7; include/ymerge.h YM_STATUS_CLASS)."""
+    return int(st) & 0xff
+
+
+def status_message(st):
+    """The message yjs's exception carries for status word `st` (ym_strerror: V8 wording)."""
+    return _load_lib().ym_strerror(int(st)).decode()
 
 
 def raise_for_status(st):
     if st:
-        exc, msg = _STATUS_EXC.get(int(st), (YjsError, f"status {st}"))
-        raise exc(msg)
+        raise _STATUS_EXC.get(status_class(st), YjsError)(status_message(st))
 
 
 class _Batch(ctypes.Structure):
@@ -97,6 +99,16 @@ def load_library(path=None):
         fn.argtypes = [ctypes.POINTER(_Batch), ctypes.POINTER(_Out), ctypes.c_void_p, ctypes.POINTER(_Stats)]
         fn.restype = ctypes.c_int
     return L
+
+
+_LIB = None
+
+
+def _load_lib():
+    global _LIB
+    if _LIB is None:
+        _LIB = load_library()
+    return _LIB
 
 
 def pack_docs(docs):
