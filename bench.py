@@ -41,7 +41,7 @@ PARTITION = {"c2": "hash", "c2v2": "hash", "c4": "hash", "c5": "bytes", "c5v2": 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     p.add_argument("--docs-per-gpu", type=int, default=10000)
@@ -335,7 +335,9 @@ def main():
         from yjs_amd import Engine
         eng = Engine(local)
     g_arena = torch.from_numpy(arena).to(dev)
-    g_off = torch.from_numpy(upd_off.view(np.int64)).to(dev)
+    # u32 offsets (YM_OFF32) when the rank's arena is below 4 GiB: half the offset bytes per update
+    off32 = in_bytes < 2 ** 32
+    g_off = torch.from_numpy(upd_off.astype(np.uint32).view(np.int32) if off32 else upd_off.view(np.int64)).to(dev)
     g_doc = torch.from_numpy(doc_upd.view(np.int32)).to(dev)
     cap = 4 * in_bytes + 128 * n_docs + 8192  # fast-path slots (2*in + 64 per doc) + general-path room
     o_arena = torch.empty(cap, dtype=torch.uint8, device=dev)
@@ -420,6 +422,7 @@ def main():
             "config": {"workload": desc, "docs_total": int(docs_all), "docs_per_gpu": args.docs_per_gpu,
                        "docs_rank0": n_docs, "updates_total": int(upd_all), "input_bytes_total": int(in_all),
                        "output_bytes_total": int(out_all), "format": f"v{fmt}",
+                       "update_offsets": "u32 (YM_OFF32)" if off32 else "u64",
                        "parallelism": f"docs {how}-partitioned over {world} GPU(s) (one process each), "
                                       "no collective in the hot path; max-time / sum-counters all-reduce"},
             "docs_per_s": round(docs_s, 1),

@@ -59,10 +59,16 @@ enum { YM_V1 = 1, YM_V2 = 2 };
  * (gaberogan/yjs@v0 src/utils/DeleteSet.js:113-135: only exactly adjacent ranges coalesce) instead of
  * yjs 13.5.16's (touching and overlapping ranges merge) */
 enum { YM_DS_REF = 0x100 };
+/* or-ed into ym_batch.format: upd_off points to n_upd + 1 uint32_t offsets (an arena below 4 GiB)
+ * instead of uint64_t.  Device batches: the V1 merge fast kernel reads them as they are (half the
+ * offset bytes per update); other paths widen them on the device first. */
+enum { YM_OFF32 = 0x200 };
+/* ym_snapshot only, or-ed into ym_batch.format: the output encoding (default: the input's) */
+enum { YM_OUT_V1 = 0x1000, YM_OUT_V2 = 0x2000 };
 
 typedef struct ym_batch {
   const uint8_t *arena;    /* concatenated update bytes                                   */
-  const uint64_t *upd_off; /* n_upd + 1 byte offsets into arena                           */
+  const uint64_t *upd_off; /* n_upd + 1 byte offsets into arena (uint32_t with YM_OFF32)  */
   const uint32_t *doc_upd; /* n_docs + 1 update-index ranges                              */
   uint32_t n_docs;
   uint32_t n_upd;
@@ -117,6 +123,11 @@ int ym_meta(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
  * writeDeleteSet(mergeDeleteSets(readDeleteSet(each))) in the same encoding (13.5.16 union, he@10482;
  * with YM_DS_REF in b->format the reference's adjacency-only coalescing, DeleteSet.js:113-161). */
 int ym_ds_merge(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
+/* Snapshot codec (reference src/utils/Snapshot.js:84-124): one encoded snapshot per document (DSEncoderV1
+ * for YM_V1 input, DSEncoderV2 for YM_V2), written back as encodeSnapshot / encodeSnapshotV2 (YM_OUT_V1 /
+ * YM_OUT_V2 or-ed into b->format; default the input's encoding) of decodeSnapshot[V2](input): normalisation
+ * (repeated clients merged in Map order) and V1 <-> V2 conversion, with decodeSnapshot's exceptions. */
+int ym_snapshot(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
 
 #ifdef __cplusplus
 }

@@ -14,6 +14,8 @@
 //   mergeDeleteSetsBatch(docs, {format, reference}), mergeEncodedDeleteSets(encodedDss, {format, reference})
 //                                                      (PermanentUserData.js:49-54: mergeDeleteSets over
 //                                                       encoded delete sets -> one encoded delete set)
+//   encodeSnapshot[V2] / decodeSnapshot[V2], encodeSnapshotBatch / decodeSnapshotBatch,
+//   convertSnapshotBatch(bufs, {format, to})         (Snapshot.js:84-124 codec, V1 <-> V2)
 //   every *Batch function also as *BatchAsync(...) -> Promise (the GPU call off the event loop)
 // Exceptions carry yjs's class and message (V8 wording; include/ymerge.h status words).
 // There is no CPU fallback: a missing addon or GPU throws.
@@ -30,7 +32,7 @@ function init () {
   }
 }
 
-const OP = { merge: 0, diff: 1, sv: 2, conv: 3, meta: 4, dsmerge: 5 }
+const OP = { merge: 0, diff: 1, sv: 2, conv: 3, meta: 4, dsmerge: 5, snapshot: 6 }
 const fmtOf = o => (o && (o.format === 'v2' || o.format === 2)) ? 2 : 1
 
 // status word -> the exception yjs itself throws for that input: the class from bits 0-7, the message
@@ -48,6 +50,8 @@ function toError (st) {
   }
 }
 const YM_DS_REF = 0x100 // mergeDeleteSets with the reference's adjacency-only coalescing (include/ymerge.h)
+const YM_OUT_V1 = 0x1000 // ym_snapshot output encodings
+const YM_OUT_V2 = 0x2000
 
 function pack (docs) {
   let n = 0; let bytes = 0
@@ -129,6 +133,47 @@ function mergeDeleteSetsBatch (docs, opts, throwErrors = false, async = false) {
   const fmt = fmtOf(opts) | (opts && opts.reference ? YM_DS_REF : 0)
   return call(async, [OP.dsmerge, fmt, p.arena, p.updOff, p.docUpd], r => unpack(r, throwErrors))
 }
+// Snapshot codec (reference src/utils/Snapshot.js:84-124) on the GPU: encodeSnapshot[V2](decodeSnapshot[V2](buf))
+// per buffer -- normalisation and V1 <-> V2 conversion (opts.format: the input's, opts.to: the output's)
+function convertSnapshotBatch (bufs, opts, throwErrors = false, async = false) {
+  const p = pack(bufs.map(b => [b]))
+  const to = opts && (opts.to === 'v2' || opts.to === 2) ? YM_OUT_V2 : (opts && (opts.to === 'v1' || opts.to === 1) ? YM_OUT_V1 : 0)
+  return call(async, [OP.snapshot, fmtOf(opts) | to, p.arena, p.updOff, p.docUpd], r => unpack(r, throwErrors))
+}
+// the canonical V1 bytes the engine writes -> { ds: Map<client, [{clock, len}]>, sv: Map<client, clock> }
+// (the shape of the reference's Snapshot: DeleteSet.clients and the state map)
+function readSnapshotV1 (b) {
+  let pos = 0
+  const vu = () => { let v = 0; let m = 1; for (;;) { const x = b[pos++]; v += (x & 0x7f) * m; m *= 128; if (x < 0x80) return v } }
+  const clients = new Map()
+  for (let n = vu(); n > 0; n--) {
+    const client = vu(); const items = []
+    for (let m = vu(); m > 0; m--) { const clock = vu(); items.push({ clock, len: vu() }) }
+    clients.set(client, items)
+  }
+  const sv = new Map()
+  for (let n = vu(); n > 0; n--) { const client = vu(); sv.set(client, vu()) }
+  return { ds: { clients }, sv }
+}
+// a snapshot object laid out as V1 bytes (the host only packs the values; the engine encodes)
+function writeSnapshotV1 (s) {
+  const out = []
+  const vu = v => { while (v > 127) { out.push(128 | (v % 128)); v = Math.floor(v / 128) } out.push(v) }
+  vu(s.ds.clients.size)
+  s.ds.clients.forEach((items, client) => { vu(client); vu(items.length); for (const it of items) { vu(it.clock); vu(it.len) } })
+  vu(s.sv.size)
+  s.sv.forEach((clock, client) => { vu(client); vu(clock) })
+  return Uint8Array.from(out)
+}
+const decodeSnapshotBatch = (bufs, opts, throwErrors = false) =>
+  convertSnapshotBatch(bufs, { format: fmtOf(opts), to: 1 }, throwErrors).map(r => r instanceof Error ? r : readSnapshotV1(r))
+const encodeSnapshotBatch = (snapshots, opts, throwErrors = false) =>
+  convertSnapshotBatch(snapshots.map(writeSnapshotV1), { format: 1, to: fmtOf(opts) }, throwErrors)
+const decodeSnapshot = buf => decodeSnapshotBatch([buf], { format: 1 }, true)[0]
+const decodeSnapshotV2 = buf => decodeSnapshotBatch([buf], { format: 2 }, true)[0]
+const encodeSnapshot = s => encodeSnapshotBatch([s], { format: 1 }, true)[0]
+const encodeSnapshotV2 = s => encodeSnapshotBatch([s], { format: 2 }, true)[0]
+
 // Promise-returning batch forms: reject on a device failure, resolve to per-document results (bytes
 // or the Error yjs would throw for that document)
 const mergeUpdatesBatchAsync = (docs, opts) => mergeUpdatesBatch(docs, opts, false, true)
@@ -137,6 +182,7 @@ const encodeStateVectorFromUpdateBatchAsync = (updates, opts) => encodeStateVect
 const convertUpdateFormatBatchAsync = (updates, opts) => convertUpdateFormatBatch(updates, opts, false, true)
 const parseUpdateMetaBatchAsync = (updates, opts) => parseUpdateMetaBatch(updates, opts, false, true)
 const mergeDeleteSetsBatchAsync = (docs, opts) => mergeDeleteSetsBatch(docs, opts, false, true)
+const convertSnapshotBatchAsync = (bufs, opts) => convertSnapshotBatch(bufs, opts, false, true)
 
 // single-document yjs signatures (mergeUpdates([u]) returns the same object, like yjs)
 const mergeUpdates = updates => updates.length === 1 ? updates[0] : mergeUpdatesBatch([updates], { format: 'v1' }, true)[0]
@@ -157,5 +203,7 @@ module.exports = {
   convertUpdateFormatV1ToV2, convertUpdateFormatV2ToV1, convertUpdateFormatBatch,
   parseUpdateMeta, parseUpdateMetaV2, parseUpdateMetaBatch, mergeDeleteSetsBatch, mergeEncodedDeleteSets,
   mergeUpdatesBatchAsync, diffUpdateBatchAsync, encodeStateVectorFromUpdateBatchAsync, convertUpdateFormatBatchAsync,
-  parseUpdateMetaBatchAsync, mergeDeleteSetsBatchAsync
+  parseUpdateMetaBatchAsync, mergeDeleteSetsBatchAsync,
+  convertSnapshotBatch, convertSnapshotBatchAsync, decodeSnapshotBatch, encodeSnapshotBatch,
+  decodeSnapshot, decodeSnapshotV2, encodeSnapshot, encodeSnapshotV2
 }

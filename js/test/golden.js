@@ -28,6 +28,7 @@ for (const f of fs.readdirSync(dir).filter(f => f.endsWith('.json')).sort()) {
       else if (c.op === 'meta') out = encodeMeta((c.fmt === 1 ? Y.parseUpdateMeta : Y.parseUpdateMetaV2)(inputs[0]))
       else if (c.op === 'dsmerge') out = Y.mergeEncodedDeleteSets(inputs, { format: c.fmt })
       else if (c.op === 'dsmerge_ref') out = Y.mergeEncodedDeleteSets(inputs, { format: c.fmt, reference: true })
+      else if (c.op === 'snap_to_v1' || c.op === 'snap_to_v2') out = Y.convertSnapshotBatch([inputs[0]], { format: c.fmt, to: c.op === 'snap_to_v2' ? 2 : 1 }, true)[0]
       else if (c.op === 'conv') out = (c.fmt === 1 ? Y.convertUpdateFormatV1ToV2 : Y.convertUpdateFormatV2ToV1)(inputs[0])
       else out = (c.fmt === 1 ? Y.encodeStateVectorFromUpdate : Y.encodeStateVectorFromUpdateV2)(inputs[0])
     } catch (e) { err = e }

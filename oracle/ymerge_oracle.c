@@ -2184,6 +2184,45 @@ static Buf *dsmerge_impl(Ctx *c, const uint8_t *const *dss_in, const size_t *len
   return enc.rest;
 }
 
+/* Snapshot codec (gaberogan/yjs@v0 src/utils/Snapshot.js:84-124; 13.5.16 _n / En): the snapshot that
+   decodeSnapshot[V2] reads -- readDeleteSet (DeleteSet.js:241-256) then readStateVector (encoding.js:
+   536-545, a Map: a repeated client keeps its first position and takes the last clock) -- written back by
+   encodeSnapshot[V2]: writeDeleteSet (DeleteSet.js:219-232) then writeStateVector (encoding.js:572-579). */
+static Buf *snap_impl(Ctx *c, const uint8_t *p, size_t n, int v2in, int v2out) {
+  UDec dec;
+  udec_init(c, &dec, p, n, 0);
+  dec.v2 = v2in;
+  DSet ds;
+  ds_read(c, &dec, &ds);
+  uint32_t m = rd_vu(c, &dec.rest);
+  size_t nsv = 0, cap = 0;
+  int64_t *sv = NULL; /* (client, clock) pairs in Map order */
+  for (uint32_t i = 0; i < m; i++) {
+    int64_t client = rd_vu(c, &dec.rest);
+    int64_t clock = rd_vu(c, &dec.rest);
+    size_t k = 0;
+    while (k < nsv && sv[2 * k] != client) k++;
+    if (k == nsv) {
+      if (nsv == cap) {
+        cap = cap ? 2 * cap : 16;
+        int64_t *ns = (int64_t *)aalloc(c, cap * 2 * sizeof(int64_t));
+        if (nsv) memcpy(ns, sv, nsv * 2 * sizeof(int64_t));
+        sv = ns;
+      }
+      sv[2 * nsv] = client;
+      nsv++;
+    }
+    sv[2 * k + 1] = clock;
+  }
+  UEnc enc;
+  uenc_init(c, &enc, 0);
+  enc.v2 = v2out;
+  ds_write(c, &enc, &ds);
+  wr_vu(c, enc.rest, (int64_t)nsv);
+  for (size_t k = 0; k < nsv; k++) { wr_vu(c, enc.rest, sv[2 * k]); wr_vu(c, enc.rest, sv[2 * k + 1]); }
+  return enc.rest;
+}
+
 /* ------------------------------------------------------------------------------------------------ */
 /* public API                                                                                      */
 /* ------------------------------------------------------------------------------------------------ */
@@ -2275,6 +2314,21 @@ int ymo_ds_merge(const uint8_t *const *dss, const size_t *lens, size_t n, int fm
   return rc;
 }
 
+int ymo_snapshot(const uint8_t *buf, size_t len, int fmt, uint8_t **out, size_t *out_len) {
+  *out = NULL; *out_len = 0;
+  Ctx c;
+  memset(&c, 0, sizeof(c));
+  int code = setjmp(c.jb);
+  if (code) { ctx_free(&c); return code; }
+  /* fmt: 1 / 2 the input encoding; | 0x1000 V1 output, | 0x2000 V2 output (default: the input's) */
+  const int v2in = (fmt & 0xff) == 2;
+  const int v2out = (fmt & 0x2000) ? 1 : (fmt & 0x1000) ? 0 : v2in;
+  Buf *b = snap_impl(&c, buf, len, v2in, v2out);
+  int rc = finish_out(&c, b, out, out_len);
+  ctx_free(&c);
+  return rc;
+}
+
 void ymo_free(void *p) { free(p); }
 
 /* ------------------------------------------------------------------------------------------------ */
@@ -2320,6 +2374,8 @@ static void *batch_worker(void *arg) {
       st = n == 1 ? ymo_meta(ptrs[0], lens[0], j->fmt, &out, &olen) : YMO_ERR_UNEXPECTED;
     } else if (j->op == 5) {
       st = ymo_ds_merge(ptrs, lens, n, j->fmt, &out, &olen);
+    } else if (j->op == 6) {
+      st = n == 1 ? ymo_snapshot(ptrs[0], lens[0], j->fmt, &out, &olen) : YMO_ERR_UNEXPECTED;
     } else st = n >= 1 ? ymo_sv_from_update(ptrs[0], lens[0], j->fmt, &out, &olen) : YMO_ERR_UNEXPECTED;
     if (st == YMO_OK && j->out_arena) {
       uint64_t cap = j->out_cap_off[d + 1] - j->out_cap_off[d];

@@ -10,7 +10,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NATIVE = os.path.join(ROOT, "tests", "native")
-OPS = {"merge": 0, "diff": 1, "sv": 2, "conv": 3, "meta": 4, "dsmerge": 5}
+OPS = {"merge": 0, "diff": 1, "sv": 2, "conv": 3, "meta": 4, "dsmerge": 5, "snap": 6}
 
 
 def binary(san=False):
@@ -31,6 +31,8 @@ def run(op, fmt, arena, upd_off, doc_upd, sv_arena=None, sv_off=None, san=False)
     sv_off = np.ascontiguousarray(sv_off, np.uint64)
     if op == "dsmerge_ref":  # ym_ds_merge with YM_DS_REF: the reference's adjacency-only coalescing
         op, fmt = "dsmerge", fmt | 0x100
+    if op in ("snap_to_v1", "snap_to_v2"):  # ym_snapshot with YM_OUT_V1 / YM_OUT_V2
+        op, fmt = "snap", fmt | (0x2000 if op == "snap_to_v2" else 0x1000)
     exe = binary(san)
     with tempfile.TemporaryDirectory() as td:
         fin, fout = os.path.join(td, "in"), os.path.join(td, "out")

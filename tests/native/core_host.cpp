@@ -45,7 +45,9 @@ int main(int argc, char **argv) {
   FILE *o = fopen(argv[2], "wb");
   if (!o) return 2;
   const uint32_t v2 = (fmt & 0xff) == 2;
-  const uint32_t v2f = v2 | (op == OP_DSMERGE && (fmt & 0x100) ? 0x100u : 0u);
+  // v2f bit 8: YM_DS_REF (ym_ds_merge); bit 9: V2 output (ym_snapshot: YM_OUT_V2, or a V2 input without YM_OUT_V1)
+  const uint32_t v2out = op == OP_SNAP && ((fmt & 0x2000) || (v2 && !(fmt & 0x1000)));
+  const uint32_t v2f = v2 | (op == OP_DSMERGE && (fmt & 0x100) ? 0x100u : 0u) | (v2out ? 0x200u : 0u);
   for (uint32_t d = 0; d < nd; d++) {
     const uint32_t u0 = doc_upd[d], k = doc_upd[d + 1] - u0;
     const uint64_t bytes = upd_off[doc_upd[d + 1]] - upd_off[u0];

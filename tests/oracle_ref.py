@@ -74,6 +74,7 @@ def lib():
         L.ymo_convert.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t)]
         L.ymo_meta.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t)]
         L.ymo_ds_merge.argtypes = L.ymo_merge.argtypes
+        L.ymo_snapshot.argtypes = L.ymo_convert.argtypes
         L.ymo_free.argtypes = [ctypes.c_void_p]
         vp = ctypes.c_void_p
         L.ymo_batch.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, vp, ctypes.c_uint32, vp, vp, ctypes.c_int,
@@ -150,6 +151,16 @@ def meta(update, fmt=1):
     return st, (_take(out, olen) if st == 0 else None)
 
 
+def snapshot(buf, fmt=1, to_fmt=1):
+    """encodeSnapshot[V2](decodeSnapshot[V2](buf)) -> (status, bytes) (Snapshot.js:84-124)."""
+    L = lib()
+    p, n = _buf(buf)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    st = L.ymo_snapshot(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint8)), n, fmt | (0x2000 if to_fmt == 2 else 0x1000), ctypes.byref(out), ctypes.byref(olen))
+    return st, (_take(out, olen) if st == 0 else None)
+
+
 def ds_merge(blobs, fmt=1):
     """PermanentUserData's mergeDeleteSets over encoded delete sets -> (status, encoded delete set)."""
     L = lib()
@@ -169,7 +180,9 @@ def batch(op, fmt, arena, upd_off, doc_upd, sv_arena=None, sv_off=None, nthreads
     L = lib()
     if op == "dsmerge_ref":  # the reference's adjacency-only coalescing (DeleteSet.js:113-135)
         op, fmt = "dsmerge", fmt | 0x100
-    opc = {"merge": 0, "diff": 1, "sv": 2, "conv": 3, "meta": 4, "dsmerge": 5}[op]
+    if op in ("snap_to_v1", "snap_to_v2"):  # snapshot codec, output encoding YM_OUT_V1 / YM_OUT_V2
+        op, fmt = "snap", fmt | (0x2000 if op == "snap_to_v2" else 0x1000)
+    opc = {"merge": 0, "diff": 1, "sv": 2, "conv": 3, "meta": 4, "dsmerge": 5, "snap": 6}[op]
     arena = np.ascontiguousarray(arena, dtype=np.uint8)
     upd_off = np.ascontiguousarray(upd_off, dtype=np.uint64)
     doc_upd = np.ascontiguousarray(doc_upd, dtype=np.uint32)

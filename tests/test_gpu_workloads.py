@@ -346,3 +346,49 @@ def test_ds_merge_batch_matches_oracle(engine, fmt):
     st = engine.stats
     # the fast kernel (delete-set-only mode) takes the documents that fit its LDS tables
     assert st["docs_fast"] > 0.3 * st["docs"], st  # (the rest: > 128 ranges or clocks >= 2^25)
+
+
+def _run_device_u32(engine, op, fmt, arena, upd_off, doc_upd):
+    """run_device with the batch resident on cuda:0 and the update offsets as u32 (YM_OFF32)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    nd = len(doc_upd) - 1
+    ga = torch.from_numpy(np.ascontiguousarray(arena)).to(dev)
+    go = torch.from_numpy(upd_off.astype(np.uint32).view(np.int32)).to(dev)
+    gd = torch.from_numpy(doc_upd.view(np.int32)).to(dev)
+    oa = torch.empty(4 * len(arena) + 128 * nd + 8192, dtype=torch.uint8, device=dev)
+    oo = torch.empty(nd, dtype=torch.int64, device=dev)
+    ol = torch.empty(nd, dtype=torch.int64, device=dev)
+    st = torch.empty(nd, dtype=torch.int32, device=dev)
+    rc, _ = engine.run_device(op, fmt, ga, go, gd, oa, oo, ol, st)
+    assert rc == 0, rc
+    return oa.cpu().numpy(), oo.cpu().numpy(), ol.cpu().numpy(), st.cpu().numpy()
+
+
+@pytest.mark.parametrize("name", ["c2_v1", "c4_v1", "c2_v2", "c5_v1"])
+def test_device_batch_u32_offsets(engine, name):
+    """Device-resident batches with u32 update offsets (YM_OFF32): the V1 fast kernel reads them directly,
+    every other path (V2 fast kernel, large-document pipeline) after the on-device widening."""
+    arena, upd_off, doc_upd = load_ymb(name)
+    fmt = 2 if name.endswith("v2") else 1
+    outs, status, _ = O.batch("merge", fmt, arena, upd_off, doc_upd, nthreads=8)
+    bad = _compare(_run_device_u32(engine, "merge", fmt, arena, upd_off, doc_upd), outs, status)
+    assert not bad, bad[:10]
+
+
+def test_device_u32_offsets_mixed_paths(engine):
+    """YM_OFF32 with documents the fast kernel declines (general path after widening): golden merges."""
+    import golden_io
+    cases = [c for c in golden_io.load_cases() if c["op"] == "merge" and c["fmt"] == 1 and len(c["inputs"]) > 0]
+    from yjs_amd import pack_docs
+    a, o, d = pack_docs([c["inputs"] for c in cases])
+    oa, oo, ol, st = _run_device_u32(engine, "merge", 1, a, o, d)
+    bad = []
+    for i, c in enumerate(cases):
+        if "error" in c:
+            if O.js_error_mismatch(st[i], c["error"], c["message"]):
+                bad.append(c["id"])
+        elif st[i] != 0 or oa[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() != c["expect"]:
+            bad.append(c["id"])
+    assert not bad, bad[:10]
+    assert engine.stats["docs_general"] > 0, engine.stats

@@ -22,6 +22,8 @@ def run_case(c):
         return O.ds_merge(c["inputs"], c["fmt"])
     if c["op"] == "dsmerge_ref":
         return O.ds_merge(c["inputs"], c["fmt"] | 0x100)
+    if c["op"] in ("snap_to_v1", "snap_to_v2"):
+        return O.snapshot(c["inputs"][0], c["fmt"], 2 if c["op"] == "snap_to_v2" else 1)
     return O.sv_from_update(c["inputs"][0], c["fmt"])
 
 
@@ -38,7 +40,7 @@ def test_oracle_matches_golden(case):
 def test_golden_coverage():
     groups = {c["group"] for c in CASES}
     assert {"c1_text", "c2_text", "c4_map", "c5_xml", "content", "edge", "refgolden", "conv", "meta", "dsmerge"} <= groups
-    for op in ("merge", "diff", "sv", "conv", "meta", "dsmerge"):
+    for op in ("merge", "diff", "sv", "conv", "meta", "dsmerge", "snap_to_v1", "snap_to_v2"):
         for fmt in (1, 2):
             assert any(c["op"] == op and c["fmt"] == fmt and "expect" in c for c in CASES), (op, fmt)
     assert sum("error" in c for c in CASES) >= 20

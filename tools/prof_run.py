@@ -17,7 +17,7 @@ fmt = 2 if wl.endswith("v2") else 1
 a, o, d = replicate(*load_ymb(wl), int(os.environ.get("NDOCS", "10000")))
 dev = torch.device("cuda", 0)
 ga = torch.from_numpy(a).to(dev)
-go = torch.from_numpy(o.view(np.int64)).to(dev)
+go = torch.from_numpy(o.astype(np.uint32).view(np.int32) if os.environ.get("OFF64") is None else o.view(np.int64)).to(dev)  # u32 offsets (YM_OFF32), as bench.py
 gd = torch.from_numpy(d.view(np.int32)).to(dev)
 n = len(d) - 1
 oa = torch.empty(4 * len(a) + 128 * n + 8192, dtype=torch.uint8, device=dev)

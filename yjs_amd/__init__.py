@@ -12,5 +12,7 @@ from .engine import (  # noqa: F401
     convertUpdateFormatV1ToV2, convertUpdateFormatV2ToV1, convertUpdateFormatBatch,
     parseUpdateMeta, parseUpdateMetaV2, parseUpdateMetaBatch, decode_meta,
     mergeDeleteSetsBatch, mergeEncodedDeleteSets,
+    Snapshot, convertSnapshotBatch, decodeSnapshotBatch, encodeSnapshotBatch,
+    decodeSnapshot, decodeSnapshotV2, encodeSnapshot, encodeSnapshotV2,
     pack_docs, lib_path, status_class, status_message,
 )

@@ -184,6 +184,12 @@ __global__ void __launch_bounds__(PACK_THREADS) k_pack(const uint8_t *src, const
   }
 }
 
+// YM_OFF32 offsets widened to u64 for the kernels that read u64 offsets
+__global__ void k_widen(const uint32_t *src, uint64_t *dst, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[i];
+}
+
 // packed lengths: a document that is not OK contributes nothing (its out_len is reported as 0)
 __global__ void k_mask_len(const int32_t *status, const uint64_t *len, uint64_t *mlen, uint32_t n) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -207,7 +213,8 @@ __global__ void k_status_flags(const uint32_t *list, uint32_t n, const int32_t *
 // cross-block atomics), 256-thread blocks of 4,096 documents above that
 template <uint32_t FIN_THREADS>
 __global__ void __launch_bounds__(FIN_THREADS) k_finish(const int32_t *status, const uint64_t *out_len, uint32_t n,
-                                                        const uint64_t *upd_off, uint32_t n_upd, uint64_t *counters,
+                                                        const uint64_t *upd_off, const uint32_t *upd_off32,
+                                                        uint32_t n_upd, uint64_t *counters,
                                                         volatile uint64_t *host, int stats, int merge, uint64_t seq) {
   __shared__ unsigned long long red[2][FIN_THREADS / 64];
   unsigned long long *c = reinterpret_cast<unsigned long long *>(counters);
@@ -221,8 +228,8 @@ __global__ void __launch_bounds__(FIN_THREADS) k_finish(const int32_t *status, c
   if (threadIdx.x == 0) {
     used = __hip_atomic_load(&c[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     declined = __hip_atomic_load(reinterpret_cast<uint32_t *>(&c[2]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    in_lo = upd_off[0];
-    in_hi = upd_off[n_upd];
+    in_lo = upd_off32 ? upd_off32[0] : upd_off[0];
+    in_hi = upd_off32 ? upd_off32[n_upd] : upd_off[n_upd];
   }
   if (stats) {
     int32_t sv[16];
@@ -342,7 +349,14 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   if (stats) memset(stats, 0, sizeof(*stats));
   if (nd == 0) { out->used = 0; return 0; }
   const uint8_t *A = b->arena;
-  const uint64_t *upd_off = b->upd_off;
+  const bool off32 = (b->format & YM_OFF32) != 0;
+  const uint64_t *upd_off = off32 ? nullptr : b->upd_off;
+  std::vector<uint64_t> host_off;
+  if (off32 && b->mem == YM_MEM_HOST) {  // host batches: widened here, staged as u64
+    const uint32_t *o32 = reinterpret_cast<const uint32_t *>(b->upd_off);
+    host_off.assign(o32, o32 + b->n_upd + 1);
+    upd_off = host_off.data();
+  }
   const uint32_t *doc_upd = b->doc_upd;
   const uint8_t *svp = b->sv_arena;
   const uint64_t *sv_off = b->sv_off;
@@ -392,12 +406,24 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   memset(&j, 0, sizeof(j));
   j.A = A;
   j.upd_off = upd_off;
+  if (off32 && !host) j.upd_off32 = reinterpret_cast<const uint32_t *>(b->upd_off);
+  // device u32 offsets: the V1 fast kernel reads them as they are; every other kernel reads u64
+  // offsets, widened here on first need
+  auto widen = [&]() -> int {
+    if (j.upd_off) return 0;
+    if (S->in_off.ensure((b->n_upd + 1) * 8ull)) return -2;
+    k_widen<<<(b->n_upd + 256) / 256, 256, 0, st>>>(j.upd_off32, S->in_off.as<uint64_t>(), b->n_upd + 1);
+    j.upd_off = upd_off = S->in_off.as<uint64_t>();
+    return 0;
+  };
   j.doc_upd = doc_upd;
   j.sv = svp;
   j.sv_off = sv_off;
   j.op = op;
   j.v2 = (b->format & 0xff) == YM_V2;
   j.dsref = op == OP_DSMERGE && (b->format & YM_DS_REF) != 0;
+  // ym_snapshot: the output encoding (YM_OUT_V1 / YM_OUT_V2; default: the input's)
+  j.v2out = op == OP_SNAP && ((b->format & YM_OUT_V2) != 0 || (j.v2 && (b->format & YM_OUT_V1) == 0));
   j.layout = S->layout.as<ym::Layout>();
   j.status = o_status;
   j.out = o_arena;
@@ -424,10 +450,10 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
     const bool one = !want || nd <= 16 * 1024;
     const uint32_t fin_blocks = one ? 1 : (nd + 4095) / 4096;
     if (one)
-      k_finish<1024><<<1, 1024, 0, st>>>(o_status, o_len, nd, upd_off, b->n_upd, counters, S->pinned_dev,
+      k_finish<1024><<<1, 1024, 0, st>>>(o_status, o_len, nd, j.upd_off, j.upd_off ? nullptr : j.upd_off32, b->n_upd, counters, S->pinned_dev,
                                         want ? 1 : 0, slots ? 1 : 0, seq);
     else
-      k_finish<256><<<fin_blocks, 256, 0, st>>>(o_status, o_len, nd, upd_off, b->n_upd, counters, S->pinned_dev,
+      k_finish<256><<<fin_blocks, 256, 0, st>>>(o_status, o_len, nd, j.upd_off, j.upd_off ? nullptr : j.upd_off32, b->n_upd, counters, S->pinned_dev,
                                                  want ? 1 : 0, slots ? 1 : 0, seq);
     HIPCHK(hipEventRecord(S->ev1, st));
     // spin on the completion word k_finish writes last (no interrupt wake-up of a blocking wait), then
@@ -439,6 +465,8 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
     if (q != hipSuccess) HIPCHK(hipStreamSynchronize(st));
     return 0;
   };
+  if (!((op == OP_MERGE && !j.v2) || (op == OP_DSMERGE && !j.dsref)))
+    if (int r = widen()) return r;
   HIPCHK(hipEventRecord(S->ev0, st));
   // (1) fast path over every document; appends the ones it declines to list_a
   int fr = fast_launch(op, j, b->n_upd, st);     // V1 merge: LDS fast path
@@ -456,6 +484,8 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
     ngen = (uint32_t)(S->pinned[2] & 0xffffffffu);
     list = S->list_a.as<uint32_t>();
   }
+  if (ngen > 0)
+    if (int r = widen()) return r;
   // (2) large-document merges (ym_large.hip) over the declined list; what it declines stays pending
   uint32_t nlarge = 0;
   bool large = false;
@@ -634,7 +664,8 @@ uint64_t ym_out_bound(const ym_batch *b) {
   // device batches: the fast-path slot region (2 * in + 64 per doc) followed by room for general-path
   // outputs; host batches: the packed outputs only (the library stages the slot region itself)
   if (b->mem == YM_MEM_HOST && b->upd_off) {
-    const uint64_t in_h = b->upd_off[b->n_upd] - b->upd_off[0];
+    const uint32_t *o32 = reinterpret_cast<const uint32_t *>(b->upd_off);
+    const uint64_t in_h = (b->format & YM_OFF32) ? (uint64_t)o32[b->n_upd] - o32[0] : b->upd_off[b->n_upd] - b->upd_off[0];
     const uint64_t sv_h = b->sv_off ? b->sv_off[b->n_docs] - b->sv_off[0] : 0;
     return 2 * in_h + 2 * sv_h + 64ull * b->n_docs + 8192;
   }
@@ -652,5 +683,6 @@ int ym_sv(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { retur
 int ym_convert(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_CONV, b, out, stream, stats); }
 int ym_meta(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_META, b, out, stream, stats); }
 int ym_ds_merge(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_DSMERGE, b, out, stream, stats); }
+int ym_snapshot(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_SNAP, b, out, stream, stats); }
 
 }  // extern "C"

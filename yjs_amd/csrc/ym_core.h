@@ -2271,10 +2271,127 @@ YM_BIG void dsmerge_doc(Ctx &c, DocWS &ws, const uint64_t *upd_off, uint32_t u0,
 }
 
 // ------------------------------------------------------------------------------------------------
+// Snapshot codec (Snapshot.js:84-124): encodeSnapshot[V2](decodeSnapshot[V2](bytes)) -- normalisation and
+// V1 <-> V2 conversion of encoded snapshots.  decode: readDeleteSet (DeleteSet.js:241-256: a client's
+// entries are appended to its first appearance, a client with no entries is not added; V2 clocks are
+// delta-coded per entry run, lengths stored minus one, UpdateDecoder.js DSDecoderV2) then readStateVector
+// (encoding.js:536-545: Map.set, a repeated client keeps its first position and takes the last clock).
+// encode: writeDeleteSet (DeleteSet.js:219-232, Map order; DSEncoderV2.writeDsLen(0) throws
+// 'Unexpected case', UpdateEncoder.js:255-261) then writeStateVector (encoding.js:572-579).  V2 clock
+// deltas of out-of-order entries are negative and go through lib0 writeVarUint as JS numbers (ovu).
+// Workspace: the delete set's client runs in ws.ds (client, entries, byte position), the state vector's
+// pairs in ws.sv.
+// ------------------------------------------------------------------------------------------------
+YM_INL void snap_items(Ctx &c, Out &o, uint64_t uoff, uint64_t ulen, uint64_t pos, uint32_t count, uint32_t v2in,
+                       uint32_t v2out, int64_t &cur_out) {
+  Rd d = {uoff, ulen, pos};
+  int64_t cur_in = 0;  // DSDecoderV2.dsCurrVal, reset per client run (readDeleteSet)
+  for (uint32_t q = 0; q < count && !c.err; q++) {
+    int64_t clock, len;
+    if (v2in) {
+      cur_in += rd_vu(c, d);
+      clock = cur_in;
+      len = (int64_t)rd_vu(c, d) + 1;
+      cur_in += len;
+    } else {
+      clock = rd_vu(c, d);
+      len = rd_vu(c, d);
+    }
+    if (c.err) return;
+    if (v2out) {
+      ovu(o, clock - cur_out);
+      cur_out = clock;
+      if (len == 0) { seterr(c, ST_UNEXPECTED); return; }
+      ovu(o, len - 1);
+      cur_out += len;
+    } else {
+      ovu(o, clock);
+      ovu(o, len);
+    }
+  }
+}
+YM_BIG void snap_doc(Ctx &c, DocWS &ws, uint64_t uoff, uint64_t ulen, uint32_t v2in, uint32_t v2out, int pass, Layout &L,
+                     uint8_t *out) {
+  Rd d = {uoff, ulen, 0};
+  const uint32_t ncl = rd_vu(c, d);
+  uint64_t nrun = 0;
+  for (uint32_t i = 0; i < ncl && !c.err; i++) {
+    const uint32_t client = rd_vu(c, d);
+    const uint32_t m = rd_vu(c, d);
+    if (c.err) return;
+    if (m > 0) {
+      if (nrun >= ws.ds_cap) { seterr(c, ST_RETRY); return; }
+      DSE &e = ws.ds[nrun++];
+      e.client = client;
+      e.seq = m;
+      e.clock = (int64_t)d.pos;
+    }
+    for (uint32_t q = 0; q < m && !c.err; q++) { rd_vu(c, d); rd_vu(c, d); }
+  }
+  if (c.err) return;
+  const uint32_t nsv = rd_vu(c, d);
+  uint32_t npair = 0;
+  for (uint32_t i = 0; i < nsv && !c.err; i++) {
+    const uint32_t client = rd_vu(c, d);
+    const uint32_t clock = rd_vu(c, d);
+    if (c.err) return;
+    if (npair >= ws.sv_cap) { seterr(c, ST_RETRY); return; }
+    ws.sv[2 * npair] = client;
+    ws.sv[2 * npair + 1] = clock;
+    npair++;
+  }
+  if (c.err) return;
+  Out o = {pass == 2 ? out : nullptr, 0};
+  // writeDeleteSet: clients in first-appearance order, each with the entries of all its runs
+  uint64_t ndist = 0;
+  for (uint64_t r = 0; r < nrun; r++) {
+    bool first = true;
+    for (uint64_t t = 0; t < r && first; t++) first = ws.ds[t].client != ws.ds[r].client;
+    ndist += first;
+  }
+  ovu(o, (int64_t)ndist);
+  for (uint64_t r = 0; r < nrun && !c.err; r++) {
+    bool first = true;
+    for (uint64_t t = 0; t < r && first; t++) first = ws.ds[t].client != ws.ds[r].client;
+    if (!first) continue;
+    int64_t total = 0;
+    for (uint64_t t = r; t < nrun; t++) if (ws.ds[t].client == ws.ds[r].client) total += ws.ds[t].seq;
+    ovu(o, ws.ds[r].client);
+    ovu(o, total);
+    int64_t cur_out = 0;  // DSEncoderV2.resetDsCurVal per client
+    for (uint64_t t = r; t < nrun && !c.err; t++)
+      if (ws.ds[t].client == ws.ds[r].client)
+        snap_items(c, o, uoff, ulen, (uint64_t)ws.ds[t].clock, ws.ds[t].seq, v2in, v2out, cur_out);
+  }
+  if (c.err) return;
+  // writeStateVector: Map order, the last clock of each client
+  uint32_t nd = 0;
+  for (uint32_t i = 0; i < npair; i++) {
+    bool first = true;
+    for (uint32_t t = 0; t < i && first; t++) first = ws.sv[2 * t] != ws.sv[2 * i];
+    nd += first;
+  }
+  ovu(o, nd);
+  for (uint32_t i = 0; i < npair; i++) {
+    bool first = true;
+    for (uint32_t t = 0; t < i && first; t++) first = ws.sv[2 * t] != ws.sv[2 * i];
+    if (!first) continue;
+    int64_t clock = ws.sv[2 * i + 1];
+    for (uint32_t t = i + 1; t < npair; t++) if (ws.sv[2 * t] == ws.sv[2 * i]) clock = ws.sv[2 * t + 1];
+    ovu(o, ws.sv[2 * i]);
+    ovu(o, clock);
+  }
+  if (pass == 1) {
+    __builtin_memset(&L, 0, sizeof(Layout));
+    L.total = o.n;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // The general path's per-document entry (k_general in ym_general.hip; the test-only host build in
 // tests/native/core_host.cpp runs the very same function on the CPU)
 // ------------------------------------------------------------------------------------------------
-enum : uint32_t { OP_MERGE = 0, OP_DIFF = 1, OP_SV = 2, OP_CONV = 3, OP_META = 4, OP_DSMERGE = 5 };
+enum : uint32_t { OP_MERGE = 0, OP_DIFF = 1, OP_SV = 2, OP_CONV = 3, OP_META = 4, OP_DSMERGE = 5, OP_SNAP = 6 };
 
 struct GeneralWsSize {
   uint64_t rs, arr, parts, ds, dsg, sv, keys, total;
@@ -2307,6 +2424,7 @@ YM_INL GeneralWsSize general_ws_size(uint32_t k, uint64_t bytes, uint32_t parts_
 YM_INL uint64_t general_sv_bytes(uint32_t op, uint64_t svlen, uint64_t bytes) {
   if (op == OP_DIFF) return svlen;
   if (op == OP_META) return 3 * bytes + 6;
+  if (op == OP_SNAP) return bytes + 4;  // state-vector pairs: >= 2 bytes each
   return 0;
 }
 YM_INL void general_carve(uint8_t *p, const GeneralWsSize &z, DocWS &w) {
@@ -2322,7 +2440,8 @@ YM_INL void general_carve(uint8_t *p, const GeneralWsSize &z, DocWS &w) {
 }
 // One document, pass 1 (sizes into L) or 2 (writes to out).  Document = updates u0 .. u0+k-1 of the
 // arena (upd_off absolute); sv = its encoded state vector (diff).  Status in c.err.
-// v2: 1 = V2 encoding; bit 8 (ym_ds_merge): the reference's adjacency-only delete-set coalescing
+// v2: 1 = V2 encoding; bit 8 (ym_ds_merge): the reference's adjacency-only delete-set coalescing;
+// bit 9 (ym_snapshot): V2 output encoding
 YM_BIG void general_doc(Ctx &c, DocWS &w, uint32_t op, uint32_t v2f, const uint64_t *upd_off, uint32_t u0, uint32_t k,
                         const uint8_t *sv, uint64_t svlen, int pass, Layout &L, uint8_t *out) {
   const uint32_t v2 = v2f & 1;
@@ -2342,6 +2461,7 @@ YM_BIG void general_doc(Ctx &c, DocWS &w, uint32_t op, uint32_t v2f, const uint6
   if (op == OP_DIFF) diff_doc(c, w, uoff, ulen, sv, svlen, v2, pass, L, out);
   else if (op == OP_META) meta_doc(c, w, uoff, ulen, v2, pass, L, out);
   else if (op == OP_CONV) conv_doc(c, w, uoff, ulen, v2, pass, L, out);
+  else if (op == OP_SNAP) snap_doc(c, w, uoff, ulen, v2, (v2f >> 9) & 1, pass, L, out);
   else sv_doc(c, w, uoff, ulen, v2, pass, L, out);
 }
 

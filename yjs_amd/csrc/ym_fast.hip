@@ -1,28 +1,35 @@
 // ym_fast.hip -- LDS fast path for batched mergeUpdates (V1): one 64-lane wave per document.
 //
-// Takes documents whose inputs are "simple": every update's structs increase in (client desc,
-// clock asc), no two structs overlap, no GC/Skip structs, canonical encodings, payloads of the kinds
+// Takes documents whose inputs are "simple": every update's client sections increase in (client desc,
+// clock asc), no two sections overlap, no GC/Skip structs, canonical encodings, payloads of the kinds
 // yjs writes (strings, formats/embeds with literal JSON, scalar `any` values).  For such documents
-// yjs 13.5.16's k-way merge (bundle ds@39007) reduces to: all structs sorted by
-// (client desc, clock asc), a Skip (info 10, 13.5.16 ui.write) before every clock gap, consecutive
-// same-client structs grouped into one part (encoding.js:94-116 writeClientsStructs layout); the
-// delete set is the per-client union of all inputs' ranges (13.5.16 le@10242: `>=` touching rule,
-// max end) with clients in first-appearance order (DeleteSet.js:141-161 mergeDeleteSets, 13.5.16
-// he@10482).  Anything else is declined (status ST_PENDING) and handled exactly by the general path
-// (ym_general.hip) -- never approximated.
+// yjs 13.5.16's k-way merge (bundle ds@39007) reduces to: the client sections of all
+// updates sorted by (client desc, clock asc), a Skip (info 10, 13.5.16 ui.write) before every clock
+// gap, consecutive same-client sections grouped into one part (encoding.js:94-116 writeClientsStructs
+// layout); the delete set is the per-client union of all inputs' ranges (13.5.16 le@10242: `>=`
+// touching rule, max end) with clients in first-appearance order (DeleteSet.js:141-161
+// mergeDeleteSets, 13.5.16 he@10482).  Anything else is declined (status ST_PENDING) and handled
+// exactly by the general path (ym_general.hip) -- never approximated.
 //
-// Per document, all in LDS (~7.8 KB, no scratch), every phase data-parallel across the wave:
-//   1. 16-B loads of the document's bytes into LDS.
-//   2. one lane per update walks its V1 bytes (branch-free varints from one unaligned 8-byte LDS
-//      read, SWAR ASCII/JSON checks) and appends struct / delete-range records via LDS atomics.
-//   3. rank sort of the struct keys (each lane counts the keys <= its own: broadcast reads, no
-//      barriers inside), scatter, duplicate check.
-//   4. struct layout by DPP wave scans: Skips at clock gaps, part headers, byte offsets.
-//   5. delete set: rank sort of (client, clock), segmented running-max scan = interval union,
-//      groups ranked by first appearance, byte offsets by scans.
-//   6. struct section written right after step 4, delete set after step 5, straight into the slot.
-// Output slot of doc d: 2 * (input bytes before d) + 64 * d, 16-aligned (a bound the kernel checks),
-// so the fast path needs no global atomics; the general path appends after that region.
+// The unit of work is the CLIENT SECTION (the structs of one client inside one update: contiguous
+// clocks, contiguous bytes), not the struct: a section is copied to the output as one byte range, so
+// sorting, layout and emission scale with the ~1 section per update of real traffic.  Per document,
+// all in LDS (~7.9 KB, no scratch), every phase data-parallel across the wave:
+//   1. 16-B loads of the document's bytes into LDS (update offsets u64, or u32 with YM_OFF32).
+//   2. W1: one lane per update walks its V1 struct section (varints from one unaligned 8-byte LDS read,
+//      SWAR ASCII/JSON checks), appends one record per client section via an LDS atomic and clears the
+//      parentSub bit of Items with an origin in place (13.5.16 drops it on re-write, E8).  W2: one lane
+//      per update with a non-empty delete set appends its ranges.
+//   3. rank sort of the section keys (each lane counts the keys <= its own: broadcast reads, no barriers
+//      inside), scatter, duplicate check.
+//   4. layout by DPP wave scans: Skips at clock gaps, part headers, byte offsets; each lane then writes
+//      its sections (part header, Skip, the section's bytes with 8-byte stores) straight into the slot.
+//   5. delete set: rank sort of (client, clock), segmented running-max scan = interval union, groups
+//      ranked by first appearance, byte offsets by scans, written after the struct section.
+// Output slot of doc d: 2 * (input bytes before d) + 64 * d, rounded up to 64 bytes (a bound the kernel
+// checks), so the fast path needs no global atomics; the general path appends after that region.
+// Documents are mapped to blocks XCD-contiguously (block b runs on XCD b % 8): neighbouring documents
+// share their boundary cache lines (input bytes, offsets, per-document results) inside one L2.
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
@@ -35,7 +42,7 @@ namespace fastv1 {
 constexpr uint32_t IN = 2560;    // max document bytes
 constexpr uint32_t UPD = 128;    // max updates per document
 constexpr uint32_t E = 2;        // records per lane
-constexpr uint32_t REC = 64 * E; // max structs per document
+constexpr uint32_t SEC = 64 * E; // max client sections per document
 constexpr uint32_t DSN = 64 * E; // max delete ranges per document (before the union)
 
 // ---- LDS map (byte offsets; every array 16-aligned) ----------------------------------------------
@@ -46,23 +53,22 @@ constexpr uint32_t L_HIST = L_MISC + 64;        // u32[16]       update-length h
 constexpr uint32_t L_UORD = L_HIST + 64;        // u8[UPD]       struct walk list (updates with structs, by length)
 constexpr uint32_t L_UORD2 = L_UORD + UPD;      // u8[UPD]       delete-set walk list (updates with deletes)
 constexpr uint32_t L_UDS = L_UORD2 + UPD;       // u16[UPD]      LDS offset of each update's delete set
+constexpr uint32_t L_SSLOT = L_UORD;            // u8[SEC]       rank -> walk slot (duplicate check; walk lists are dead)
 constexpr uint32_t R = L_UDS + 2 * UPD;         // phase region
-// phase 2-4: struct records (walk order, then rank order in place)
-constexpr uint32_t L_RKEY = R;                  // u64[REC]  (~client << 32 | clock)
-constexpr uint32_t L_RLEN = L_RKEY + 8 * REC;   // u32[REC]
-constexpr uint32_t L_RSRC = L_RLEN + 4 * REC;   // u16[REC]  LDS offset of the info byte
-constexpr uint32_t L_RBLEN = L_RSRC + 2 * REC;  // u16[REC]  struct bytes incl. info
-constexpr uint32_t L_RINFO = L_RBLEN + 2 * REC; // u8[REC]
-constexpr uint32_t L_RSLOT = L_RINFO + REC;     // u8[REC]   rank -> walk slot (duplicate check)
+// phase 2-4: client sections (walk order, then rank order in place)
+constexpr uint32_t L_SKEY = R;                  // u64[SEC]  (~client << 32 | clock)
+constexpr uint32_t L_SLEN = L_SKEY + 8 * SEC;   // u32[SEC]  clock length of the section
+constexpr uint32_t L_SNS = L_SLEN + 4 * SEC;    // u16[SEC]  structs in the section
+constexpr uint32_t L_SB = L_SNS + 2 * SEC;      // u16[SEC]  LDS offset of its first struct
+constexpr uint32_t L_SE = L_SB + 2 * SEC;       // u16[SEC]  ... and of its end
 // phase 2, 5: delete ranges
-constexpr uint32_t L_DKEY = L_RSLOT + REC;      // u64[DSN]  (client << 32 | clock << 7 | slot)
+constexpr uint32_t L_DKEY = L_SE + 2 * SEC;     // u64[DSN]  (client << 32 | clock << 7 | slot)
 constexpr uint32_t L_DLEN = L_DKEY + 8 * DSN;   // u32[DSN]
 constexpr uint32_t L_DSEQ = L_DLEN + 4 * DSN;   // u16[DSN]  update << 8 | position (first appearance)
-constexpr uint32_t L_DSLOT = L_DSEQ + 2 * DSN;  // u8[DSN]
-constexpr uint32_t L_PFIRST = L_DSLOT + DSN;    // u16[REC]  part -> units before it
-constexpr uint32_t L_PLAST = L_PFIRST + 2 * REC;// u16[REC]  part -> units through it
-constexpr uint32_t L_END = L_PLAST + 2 * REC;
-// phase 5 (after the struct records are held in registers): merged ranges and groups, over R
+constexpr uint32_t L_PFIRST = L_DSEQ + 2 * DSN; // u16[SEC]  part -> units before it
+constexpr uint32_t L_PLAST = L_PFIRST + 2 * SEC;// u16[SEC]  part -> units through it
+constexpr uint32_t L_END = L_PLAST + 2 * SEC;
+// phase 5 (after the struct section is written): merged ranges and groups, over R
 constexpr uint32_t L_QCLK = R;                  // u32[DSN]  merged range start
 constexpr uint32_t L_QEND = L_QCLK + 4 * DSN;   // u32[DSN]  merged range end
 constexpr uint32_t L_QGRP = L_QEND + 4 * DSN;   // u8[DSN]   merged range -> group
@@ -75,44 +81,60 @@ constexpr uint32_t L_GB2 = L_DKEY + 512;        // u32[DSN]  group -> base offse
 constexpr uint32_t L_GMIN = L_PFIRST;           // u32[DSN]  group first appearance, then group base (parts are dead)
 static_assert(L_P5END <= L_DKEY, "phase-5 arrays must not overlap the sorted delete ranges");
 static_assert(L_GMIN + 4 * DSN <= L_END, "group array fits");
+static_assert(SEC <= UPD, "the duplicate-check array reuses the walk list");
 constexpr uint32_t LDS_BYTES = L_END;
+static_assert(LDS_BYTES <= 8192, "5 one-wave workgroups per SIMD (160 KB LDS per CU)");
 
 using namespace fastc;
 
-// Walks the struct section of update u and appends its structs to the record arrays (slots from an
-// LDS atomic counter, misc[0]); records where its delete set starts.  Returns false to decline.
-__device__ __forceinline__ bool walk_structs(uint32_t u) {
+// update offset i of the batch (u64, or u32 with YM_OFF32)
+__device__ __forceinline__ uint64_t uoff_g(const GeneralJob &j, uint64_t i) {
+  return j.upd_off32 ? (uint64_t)j.upd_off32[i] : j.upd_off[i];
+}
+__device__ __forceinline__ void put_u64(Slot o, uint32_t p, uint64_t v) {
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 w = {(unsigned int)v, (unsigned int)(v >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b64(w, o, (int)p, 0, 0);
+}
+
+// Walks the struct section of update u and appends one record per client section (slot from an LDS
+// atomic counter, misc[0]); records where its delete set starts.  Item info bytes with an origin and
+// the parentSub bit get the bit cleared in place (13.5.16's lazy reader reads parentSub only without
+// origins and writes the info byte back without it, E8), so sections copy verbatim afterwards.
+// Returns false to decline.
+__device__ __forceinline__ bool walk_sections(uint32_t u) {
   Cur c = {at<uint16_t>(L_UOFF + 2 * u), at<uint16_t>(L_UOFF + 2 * u + 2), false};
   const uint32_t nclients = rvu(c);
-  uint64_t prev = 0;
-  bool have_prev = false;
+  uint64_t next_min = 0;  // sections of one update in merge order: each key > the previous one's last unit
   for (uint32_t ci = 0; ci < nclients && !c.bad; ci++) {
     const uint32_t nstructs = rvu(c);
     const uint32_t client = rvu(c);
-    uint32_t clock = rvu(c);
+    const uint32_t clock = rvu(c);
+    const uint32_t b = c.p;
+    uint64_t len = 0;
     for (uint32_t si = 0; si < nstructs && !c.bad; si++) {
       // declines set c.bad (one exit edge per loop instead of one per check)
       const uint32_t s0 = c.p;
       const uint32_t info = rdb(c);
       c.bad |= info == 10 || (info & 31) == 0;  // Skip / GC -> general path
-      uint32_t len = 1;
-      if (!c.bad) c.bad |= !item_body(c, info, len);
-      const uint64_t key = ((uint64_t)(~client) << 32) | clock;
-      c.bad |= ((uint64_t)clock + len > 0xffffffffull) | (have_prev && key <= prev);  // inputs in merge order
-      if (!c.bad) {
-        prev = key + len - 1;
-        have_prev = true;
-        const uint32_t q = atomicAdd(&at<uint32_t>(L_MISC), 1u);
-        c.bad |= q >= REC;
-        if (q < REC) {
-          at<uint64_t>(L_RKEY + 8 * q) = key;
-          at<uint32_t>(L_RLEN + 4 * q) = len;
-          at<uint16_t>(L_RSRC + 2 * q) = (uint16_t)s0;
-          at<uint16_t>(L_RBLEN + 2 * q) = (uint16_t)(c.p - s0);
-          at<uint8_t>(L_RINFO + q) = (uint8_t)info;
-        }
+      uint32_t l = 1;
+      if (!c.bad) c.bad |= !item_body(c, info, l);
+      if ((info & 0xC0) != 0 && (info & 0x20) != 0) sm[s0] = (uint8_t)(info & ~0x20u);
+      len += l;
+    }
+    const uint64_t key = ((uint64_t)(~client) << 32) | clock;
+    c.bad |= (nstructs == 0) | ((uint64_t)clock + len > 0xffffffffull) | (key < next_min);
+    next_min = key + len;
+    if (!c.bad) {
+      const uint32_t q = atomicAdd(&at<uint32_t>(L_MISC), 1u);
+      c.bad |= q >= SEC;
+      if (q < SEC) {
+        at<uint64_t>(L_SKEY + 8 * q) = key;
+        at<uint32_t>(L_SLEN + 4 * q) = (uint32_t)len;
+        at<uint16_t>(L_SNS + 2 * q) = (uint16_t)nstructs;
+        at<uint16_t>(L_SB + 2 * q) = (uint16_t)b;
+        at<uint16_t>(L_SE + 2 * q) = (uint16_t)c.p;
       }
-      clock += len;
     }
   }
   at<uint16_t>(L_UDS + 2 * u) = (uint16_t)c.p;
@@ -179,13 +201,15 @@ __device__ __forceinline__ bool walk_ds(uint32_t u) {
 // DSONLY: PermanentUserData's delete-set merge (ym_ds_merge): every input is an encoded delete set (no
 // struct section); the walk is W2 only and the output is the merged delete set alone, in the DSEncoderV1
 // format, or DSEncoderV2's (DSV2: clocks delta-coded within a client, lengths minus one).
+// Grid: a multiple of 8 blocks; block b takes documents (b % 8) * G/8 + b / 8 + k * G.
 template <int STOP, int OCC, bool DSONLY = false, bool DSV2 = false>
 __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
   const uint32_t lane = threadIdx.x;
-  const uint64_t arena0 = j.upd_off[0];
-  for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
+  const uint64_t arena0 = uoff_g(j, 0);
+  const uint32_t d0 = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  for (uint32_t d = d0; d < j.n; d += gridDim.x) {
     const uint32_t u0 = j.doc_upd[d], k = j.doc_upd[d + 1] - u0;
-    const uint64_t b0 = j.upd_off[u0], bytes = j.upd_off[u0 + k] - b0;
+    const uint64_t b0 = uoff_g(j, u0), bytes = uoff_g(j, u0 + k) - b0;
     if ((DSONLY ? k == 0 : k <= 1) || k > UPD || bytes > IN) {
       if (lane == 0) decline(j, d);
       continue;
@@ -197,7 +221,7 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
       const uint32_t nvec = (uint32_t)((base + bytes + 15) >> 4);
       for (uint32_t v = lane; v < nvec; v += 64) at<uint4>(L_IN + 16 * v) = src[v];
     }
-    for (uint32_t i = lane; i <= k; i += 64) at<uint16_t>(L_UOFF + 2 * i) = (uint16_t)(j.upd_off[u0 + i] - b0 + base);
+    for (uint32_t i = lane; i <= k; i += 64) at<uint16_t>(L_UOFF + 2 * i) = (uint16_t)(uoff_g(j, u0 + i) - b0 + base);
     if (lane < 2) at<uint32_t>(L_MISC + 4 * lane) = 0;
     if (lane < 16) at<uint32_t>(L_HIST + 4 * lane) = 0;
     __syncthreads();
@@ -238,7 +262,7 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
       __syncthreads();
       bool ok = true;
 #pragma unroll 1
-      for (uint32_t i = lane; i < n1; i += 64) ok &= walk_structs(at<uint8_t>(L_UORD + i));
+      for (uint32_t i = lane; i < n1; i += 64) ok &= walk_sections(at<uint8_t>(L_UORD + i));
       if (__any(!ok)) YM_DECLINE()
       __syncthreads();
       YM_STOP(8)
@@ -262,48 +286,49 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
       if (__any(!ok)) YM_DECLINE()
     }
     __syncthreads();
-    const uint32_t nrec = at<uint32_t>(L_MISC), nds = at<uint32_t>(L_MISC + 4);
-    if ((DSONLY ? nrec != 0 : nrec == 0) || nrec > REC || nds > DSN) YM_DECLINE()
+    const uint32_t nsec = at<uint32_t>(L_MISC), nds = at<uint32_t>(L_MISC + 4);
+    if ((DSONLY ? nsec != 0 : nsec == 0) || nsec > SEC || nds > DSN) YM_DECLINE()
     if (lane == 0) {  // pad the key arrays to even length (rank loops read pairs)
-      if (nrec & 1) at<uint64_t>(L_RKEY + 8 * nrec) = ~0ull;
+      if (nsec & 1) at<uint64_t>(L_SKEY + 8 * nsec) = ~0ull;
       if (nds & 1) at<uint64_t>(L_DKEY + 8 * nds) = ~0ull;
     }
     __syncthreads();
     YM_STOP(2)
-    // output slot: 16-aligned inside the bound 2 * in + 64 per doc (no global atomics)
+    // output slot: 64-aligned inside the bound 2 * in + 64 per doc (no global atomics)
     const uint64_t slot = 2 * (b0 - arena0) + 64ull * d;
-    const uint64_t slot_al = (slot + 15) & ~15ull;
+    const uint64_t slot_al = (slot + 63) & ~63ull;
     const uint64_t slot_end = slot + 2 * bytes + 64 < j.cap ? slot + 2 * bytes + 64 : j.cap;
+    if (slot_al >= slot_end) YM_DECLINE()
     const Slot dst = make_slot(j.out + slot_al, (uint32_t)(slot_end - slot_al));
     uint32_t hdr = 0, struct_bytes = 0;
     bool bad = false;
     if constexpr (!DSONLY) {
-    // ---- 3. struct rank sort
+    // ---- 3. section rank sort
     uint64_t rk[E];
-    uint32_t rl[E], rsrc[E], rbl[E], rinf[E], rr[E];
+    uint32_t rl[E], rns[E], rb[E], re[E], rr[E];
 #pragma unroll
     for (uint32_t s = 0; s < E; s++) {
       const uint32_t i = lane + 64 * s;
-      const bool v = i < nrec;
-      rk[s] = v ? at<uint64_t>(L_RKEY + 8 * i) : ~0ull;
-      rl[s] = v ? at<uint32_t>(L_RLEN + 4 * i) : 0;
-      rsrc[s] = v ? at<uint16_t>(L_RSRC + 2 * i) : 0;
-      rbl[s] = v ? at<uint16_t>(L_RBLEN + 2 * i) : 0;
-      rinf[s] = v ? at<uint8_t>(L_RINFO + i) : 0;
+      const bool v = i < nsec;
+      rk[s] = v ? at<uint64_t>(L_SKEY + 8 * i) : ~0ull;
+      rl[s] = v ? at<uint32_t>(L_SLEN + 4 * i) : 0;
+      rns[s] = v ? at<uint16_t>(L_SNS + 2 * i) : 0;
+      rb[s] = v ? at<uint16_t>(L_SB + 2 * i) : 0;
+      re[s] = v ? at<uint16_t>(L_SE + 2 * i) : 0;
     }
-    rank_le(L_RKEY, nrec, rk, rr);
+    rank_le(L_SKEY, nsec, rk, rr);
     __syncthreads();
 #pragma unroll
     for (uint32_t s = 0; s < E; s++) {
       const uint32_t i = lane + 64 * s;
-      if (i < nrec) {
+      if (i < nsec) {
         const uint32_t r = rr[s];
-        at<uint64_t>(L_RKEY + 8 * r) = rk[s];
-        at<uint32_t>(L_RLEN + 4 * r) = rl[s];
-        at<uint16_t>(L_RSRC + 2 * r) = (uint16_t)rsrc[s];
-        at<uint16_t>(L_RBLEN + 2 * r) = (uint16_t)rbl[s];
-        at<uint8_t>(L_RINFO + r) = (uint8_t)rinf[s];
-        at<uint8_t>(L_RSLOT + r) = (uint8_t)i;
+        at<uint64_t>(L_SKEY + 8 * r) = rk[s];
+        at<uint32_t>(L_SLEN + 4 * r) = rl[s];
+        at<uint16_t>(L_SNS + 2 * r) = (uint16_t)rns[s];
+        at<uint16_t>(L_SB + 2 * r) = (uint16_t)rb[s];
+        at<uint16_t>(L_SE + 2 * r) = (uint16_t)re[s];
+        at<uint8_t>(L_SSLOT + r) = (uint8_t)i;
       }
     }
     __syncthreads();
@@ -312,36 +337,36 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
 #pragma unroll
       for (uint32_t s = 0; s < E; s++) {
         const uint32_t i = lane + 64 * s;
-        if (i < nrec) dup |= at<uint8_t>(L_RSLOT + rr[s]) != i;
+        if (i < nsec) dup |= at<uint8_t>(L_SSLOT + rr[s]) != i;
       }
       if (__any(dup)) YM_DECLINE()  // equal (client, clock): overlapping inputs
     }
     YM_STOP(3)
-    // ---- 4. struct layout over rank order; lane owns positions r = E*lane + s
+    // ---- 4. layout over rank order; lane owns positions r = E*lane + s
     uint64_t sk[E];
-    uint32_t sl[E], ssrc[E], sbl[E], sinf[E], units[E], pstart[E], plastf[E], gapv[E];
+    uint32_t sl[E], sns[E], sb[E], se[E], units[E], pstart[E], plastf[E], gapv[E];
     {
       const uint32_t r0 = E * lane;
-      uint64_t kp = r0 > 0 && r0 - 1 < nrec ? at<uint64_t>(L_RKEY + 8 * (r0 - 1)) : ~0ull;
-      uint32_t lp = r0 > 0 && r0 - 1 < nrec ? at<uint32_t>(L_RLEN + 4 * (r0 - 1)) : 0;
+      uint64_t kp = r0 > 0 && r0 - 1 < nsec ? at<uint64_t>(L_SKEY + 8 * (r0 - 1)) : ~0ull;
+      uint32_t lp = r0 > 0 && r0 - 1 < nsec ? at<uint32_t>(L_SLEN + 4 * (r0 - 1)) : 0;
 #pragma unroll
       for (uint32_t s = 0; s < E; s++) {
         const uint32_t r = r0 + s;
-        const bool v = r < nrec;
-        sk[s] = v ? at<uint64_t>(L_RKEY + 8 * r) : ~0ull;
-        sl[s] = v ? at<uint32_t>(L_RLEN + 4 * r) : 0;
-        ssrc[s] = v ? at<uint16_t>(L_RSRC + 2 * r) : 0;
-        sbl[s] = v ? at<uint16_t>(L_RBLEN + 2 * r) : 0;
-        sinf[s] = v ? at<uint8_t>(L_RINFO + r) : 0;
-        const uint64_t kn = r + 1 < nrec ? at<uint64_t>(L_RKEY + 8 * (r + 1)) : ~0ull;
+        const bool v = r < nsec;
+        sk[s] = v ? at<uint64_t>(L_SKEY + 8 * r) : ~0ull;
+        sl[s] = v ? at<uint32_t>(L_SLEN + 4 * r) : 0;
+        sns[s] = v ? at<uint16_t>(L_SNS + 2 * r) : 0;
+        sb[s] = v ? at<uint16_t>(L_SB + 2 * r) : 0;
+        se[s] = v ? at<uint16_t>(L_SE + 2 * r) : 0;
+        const uint64_t kn = r + 1 < nsec ? at<uint64_t>(L_SKEY + 8 * (r + 1)) : ~0ull;
         const bool same = v && r > 0 && (kp >> 32) == (sk[s] >> 32);
         const uint64_t pend = (kp & 0xffffffffull) + lp;
         const uint64_t cl = sk[s] & 0xffffffffull;
         bad |= same && pend > cl;  // overlapping inputs: general path
         gapv[s] = same && pend < cl ? (uint32_t)(cl - pend) : 0;
-        units[s] = v ? 1 + (gapv[s] != 0) : 0;
+        units[s] = v ? sns[s] + (gapv[s] != 0) : 0;
         pstart[s] = v && !same;
-        plastf[s] = v && (r + 1 >= nrec || (kn >> 32) != (sk[s] >> 32));
+        plastf[s] = v && (r + 1 >= nsec || (kn >> 32) != (sk[s] >> 32));
         kp = sk[s];
         lp = sl[s];
       }
@@ -369,7 +394,7 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
 #pragma unroll
     for (uint32_t s = 0; s < E; s++) {
       runu[s] = 0;
-      uint32_t b = sbl[s];
+      uint32_t b = se[s] - sb[s];
       if (pstart[s]) {
         const uint32_t pid = pu[s] >> 16;
         runu[s] = at<uint16_t>(L_PLAST + 2 * pid) - at<uint16_t>(L_PFIRST + 2 * pid);
@@ -394,11 +419,11 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
       continue;
     }
     YM_STOP(4)
-    // ---- 4b. write the struct section (frees the records' registers before the delete set)
+    // ---- 4b. write the struct section: per section its part header, its Skip, then its bytes verbatim
     if (lane == 0) put_vu(dst, 0, nparts);
 #pragma unroll
     for (uint32_t s = 0; s < E; s++) {
-      if (E * lane + s >= nrec) break;
+      if (E * lane + s >= nsec) break;
       uint32_t p = hdr + soff[s];
       if (pstart[s]) {  // part header: vu(#structs incl. skips) vu(client) vu(clock)
         p = put_vu(dst, p, runu[s]);
@@ -409,12 +434,10 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
         ob8(dst, p++, 10);
         p = put_vu(dst, p, gapv[s]);
       }
-      uint32_t info = sinf[s];
-      if (info & 0xC0) info &= ~0x20u;  // parentSub is only read / re-written without origins (E8)
-      ob8(dst, p++, info);
-      const uint32_t n = sbl[s] - 1, src = ssrc[s] + 1;  // body bytes, copied verbatim
+      const uint32_t n = se[s] - sb[s], src = sb[s];
       uint32_t o = 0;
-      for (; o + 4 <= n; o += 4) ob32(dst, p + o, ld4(src + o));
+      for (; o + 8 <= n; o += 8) put_u64(dst, p + o, ld8(src + o));
+      if (o + 4 <= n) { ob32(dst, p + o, ld4(src + o)); o += 4; }
       for (; o < n; o++) ob8(dst, p + o, sm[src + o]);
     }
     }  // !DSONLY
@@ -650,18 +673,21 @@ __global__ void k_fast_region(GeneralJob j, uint32_t n_upd) {
   if (threadIdx.x == 0 && blockIdx.x == 0) *j.used = 2 * (j.upd_off[n_upd] - j.upd_off[0]) + 64ull * j.n + 64;
 }
 
+// grid: a multiple of 8 one-wave blocks (the kernel's XCD-contiguous document mapping)
+static uint32_t fast_grid(uint32_t n) { return ((n < 131072 ? n : 131072) + 7) & ~7u; }
+
 int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st) {
   using namespace fastv1;
   if (op == OP_DSMERGE) {  // delete-set merges: the same kernel, delete sets only
     if (j.dsref) return 0;  // the reference's adjacency-only coalescing: general path
-    const uint32_t grid = j.n < 131072 ? j.n : 131072;
+    const uint32_t grid = fast_grid(j.n);
     if (j.v2) k_fast_merge_v1<0, 5, true, true><<<grid, 64, fastv1::LDS_BYTES, st>>>(j);
     else k_fast_merge_v1<0, 5, true, false><<<grid, 64, fastv1::LDS_BYTES, st>>>(j);
     return 1;
   }
   if (op != OP_MERGE || j.v2) return 0;  // fast path: V1 merges (the C2/C4 headline configs)
   (void)n_upd;  // the work-list counter is zero on entry (ym_api.hip k_finish); `used` is set later
-  const uint32_t grid = j.n < 131072 ? j.n : 131072;
+  const uint32_t grid = fast_grid(j.n);
   static int stop = -1, pad = 0;
   if (stop < 0) {
     const char *e = getenv("YMERGE_FAST_STOP");

@@ -42,7 +42,7 @@ __global__ void __launch_bounds__(64) k_general(GeneralJob j, int pass) {
   uint8_t *out = pass == 2 ? j.out + j.out_off[d] : nullptr;
   const uint8_t *sv = j.op == OP_DIFF ? j.sv + j.sv_off[d] : nullptr;
   const uint64_t svlen = j.op == OP_DIFF ? j.sv_off[d + 1] - j.sv_off[d] : 0;
-  general_doc(c, w, j.op, j.v2 | (j.dsref << 8), j.upd_off, u0, k, sv, svlen, pass, L, out);
+  general_doc(c, w, j.op, j.v2 | (j.dsref << 8) | (j.v2out << 9), j.upd_off, u0, k, sv, svlen, pass, L, out);
   if (pass == 1) {
     j.status[d] = c.err;
     if (c.err == ST_RETRY) atomicAdd(j.counter_retry, 1u);

@@ -13,6 +13,7 @@ using ym::OP_SV;
 using ym::OP_CONV;
 using ym::OP_META;
 using ym::OP_DSMERGE;
+using ym::OP_SNAP;
 
 // internal status: document not taken by the fast path, routed to the general path
 constexpr int ST_PENDING = 101;
@@ -20,6 +21,8 @@ constexpr int ST_PENDING = 101;
 struct GeneralJob {
   const uint8_t *A;          // update arena
   const uint64_t *upd_off;
+  const uint32_t *upd_off32; // YM_OFF32 device batches: u32 offsets (read by the V1 fast kernel; the
+                             // other kernels get widened u64 offsets in upd_off)
   const uint32_t *doc_upd;
   const uint8_t *sv;         // diff: state-vector arena
   const uint64_t *sv_off;
@@ -27,6 +30,7 @@ struct GeneralJob {
   const uint32_t *list;      // document ids (nullptr: 0..n-1)
   uint32_t op, v2;
   uint32_t dsref;            // ym_ds_merge: the reference's adjacency-only coalescing (YM_DS_REF)
+  uint32_t v2out;            // ym_snapshot: V2 output encoding
   uint32_t parts_mul;        // part-table capacity multiplier (grown on ST_RETRY)
   uint8_t *ws;               // workspace
   const uint64_t *ws_off;    // per listed slot

@@ -43,6 +43,13 @@ class UnsupportedInput(YjsError):
 
 
 YM_DS_REF = 0x100  # ym_ds_merge: the reference's adjacency-only coalescing (include/ymerge.h)
+YM_OFF32 = 0x200   # upd_off holds uint32_t offsets (include/ymerge.h)
+YM_OUT_V1, YM_OUT_V2 = 0x1000, 0x2000  # ym_snapshot: output encoding
+
+
+def _off_flag(upd_off):
+    """YM_OFF32 for a 4-byte offsets tensor (int32 / uint32 view of u32 offsets), else 0."""
+    return YM_OFF32 if upd_off.element_size() == 4 else 0
 
 _STATUS_EXC = {
     1: YjsError, 2: YjsError, 3: YjsURIError, 4: YjsTypeError, 5: YjsRangeError, 6: YjsSyntaxError,
@@ -84,7 +91,7 @@ class _Stats(ctypes.Structure):
 
 
 EXPORTS = ("ym_init", "ym_shutdown", "ym_strerror", "ym_out_bound", "ym_merge", "ym_diff", "ym_sv", "ym_convert",
-           "ym_meta", "ym_ds_merge")
+           "ym_meta", "ym_ds_merge", "ym_snapshot")
 
 
 def load_library(path=None):
@@ -95,7 +102,7 @@ def load_library(path=None):
     L.ym_init.argtypes = [ctypes.c_int]
     L.ym_strerror.restype = ctypes.c_char_p
     L.ym_out_bound.restype = ctypes.c_uint64
-    for fn in (L.ym_merge, L.ym_diff, L.ym_sv, L.ym_convert, L.ym_meta, L.ym_ds_merge):
+    for fn in (L.ym_merge, L.ym_diff, L.ym_sv, L.ym_convert, L.ym_meta, L.ym_ds_merge, L.ym_snapshot):
         fn.argtypes = [ctypes.POINTER(_Batch), ctypes.POINTER(_Out), ctypes.c_void_p, ctypes.POINTER(_Stats)]
         fn.restype = ctypes.c_int
     return L
@@ -139,11 +146,13 @@ class Engine:
     def _fn(self, op):
         L = self.lib
         return {"merge": L.ym_merge, "diff": L.ym_diff, "sv": L.ym_sv, "conv": L.ym_convert, "meta": L.ym_meta,
-                "dsmerge": L.ym_ds_merge, "dsmerge_ref": L.ym_ds_merge}[op]
+                "dsmerge": L.ym_ds_merge, "dsmerge_ref": L.ym_ds_merge,
+                "snap_to_v1": L.ym_snapshot, "snap_to_v2": L.ym_snapshot}[op]
 
     @staticmethod
     def _format(op, fmt):
-        return fmt | YM_DS_REF if op == "dsmerge_ref" else fmt
+        extra = {"dsmerge_ref": YM_DS_REF, "snap_to_v1": YM_OUT_V1, "snap_to_v2": YM_OUT_V2}
+        return fmt | extra.get(op, 0)
 
     # ---- host-memory batches ------------------------------------------------------------------
     def run_host(self, op, fmt, arena, upd_off, doc_upd, sv_arena=None, sv_off=None):
@@ -190,15 +199,16 @@ class Engine:
     # ---- device-resident batches (torch tensors on cuda) ---------------------------------------
     def run_device(self, op, fmt, arena, upd_off, doc_upd, out_arena, out_off, out_len, status,
                    sv_arena=None, sv_off=None, stream=None):
-        """All arguments are torch CUDA tensors (uint8 / int64 / int32 views of the ABI arrays).
-        Returns (rc, used_bytes).  stream: a torch.cuda.Stream or None (library stream)."""
+        """All arguments are torch CUDA tensors (uint8 / int64 / int32 views of the ABI arrays; upd_off
+        may be a 4-byte tensor of u32 offsets: YM_OFF32).  Returns (rc, used_bytes).  stream: a
+        torch.cuda.Stream or None (library stream)."""
         b = _Batch()
         b.arena = arena.data_ptr()
         b.upd_off = upd_off.data_ptr()
         b.doc_upd = doc_upd.data_ptr()
         b.n_docs = doc_upd.numel() - 1
         b.n_upd = upd_off.numel() - 1
-        b.format = self._format(op, fmt)
+        b.format = self._format(op, fmt) | _off_flag(upd_off)
         b.mem = 1
         if op == "diff":
             b.sv_arena = sv_arena.data_ptr()
@@ -219,7 +229,7 @@ class Engine:
         b.doc_upd = doc_upd.data_ptr()
         b.n_docs = doc_upd.numel() - 1
         b.n_upd = upd_off.numel() - 1
-        b.format = self._format(op, fmt)
+        b.format = self._format(op, fmt) | _off_flag(upd_off)
         b.mem = 1
         if op == "diff":
             b.sv_arena = sv_arena.data_ptr()
@@ -378,3 +388,99 @@ def mergeDeleteSetsBatch(docs, fmt=1, raise_errors=False, reference=False):
 
 def mergeEncodedDeleteSets(encoded_dss, fmt=1, reference=False):
     return mergeDeleteSetsBatch([list(encoded_dss)], fmt, True, reference)[0]
+
+
+# ---- snapshots (reference src/utils/Snapshot.js:84-124) -----------------------------------------------
+class Snapshot:
+    """decodeSnapshot's result: ds = {client: [(clock, len), ...]} and sv = {client: clock}, dict order =
+    the JS Map order (DeleteSet.clients / the state map)."""
+
+    def __init__(self, ds, sv):
+        self.ds = ds
+        self.sv = sv
+
+    def __eq__(self, other):  # equalSnapshots (Snapshot.js:48-78) on plain values
+        return isinstance(other, Snapshot) and self.ds == other.ds and self.sv == other.sv
+
+    def __repr__(self):
+        return f"Snapshot(ds={self.ds!r}, sv={self.sv!r})"
+
+
+def _vu(v):
+    out = bytearray()
+    while v > 127:
+        out.append(0x80 | (v & 127))
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def _snapshot_v1_bytes(snap):
+    """A Snapshot object as DSEncoderV1 bytes: the host side only lays the values out; the engine
+    re-encodes them (and raises what encodeSnapshot[V2] raises)."""
+    b = bytearray(_vu(len(snap.ds)))
+    for client, items in snap.ds.items():
+        b += _vu(client) + _vu(len(items))
+        for clock, ln in items:
+            b += _vu(clock) + _vu(ln)
+    b += _vu(len(snap.sv))
+    for client, clock in snap.sv.items():
+        b += _vu(client) + _vu(clock)
+    return bytes(b)
+
+
+def _parse_snapshot_v1(b):
+    pos = 0
+    n, pos = _read_vu(b, pos)
+    ds = {}
+    for _ in range(n):
+        client, pos = _read_vu(b, pos)
+        m, pos = _read_vu(b, pos)
+        items = ds.setdefault(client, [])
+        for _ in range(m):
+            clock, pos = _read_vu(b, pos)
+            ln, pos = _read_vu(b, pos)
+            items.append((clock, ln))
+    n, pos = _read_vu(b, pos)
+    sv = {}
+    for _ in range(n):
+        client, pos = _read_vu(b, pos)
+        clock, pos = _read_vu(b, pos)
+        sv[client] = clock
+    return Snapshot(ds, sv)
+
+
+def convertSnapshotBatch(bufs, from_fmt=1, to_fmt=1, raise_errors=False):
+    """encodeSnapshot[V2](decodeSnapshot[V2](buf)) for every buf on the GPU (ym_snapshot): normalisation
+    (repeated clients merged in Map order) and V1 <-> V2 conversion."""
+    arena, upd_off, doc_upd = pack_docs([[b] for b in bufs])
+    op = "snap_to_v2" if to_fmt == 2 else "snap_to_v1"
+    return _unpack(*_engine().run_host(op, from_fmt, arena, upd_off, doc_upd), raise_errors)
+
+
+def decodeSnapshotBatch(bufs, fmt=1, raise_errors=False):
+    """decodeSnapshot[V2] over a batch: the engine validates and normalises (V1), the host reads the
+    canonical bytes into Snapshot objects."""
+    res = convertSnapshotBatch(bufs, fmt, 1, raise_errors)
+    return [_parse_snapshot_v1(r) if isinstance(r, bytes) else r for r in res]
+
+
+def encodeSnapshotBatch(snapshots, fmt=1, raise_errors=False):
+    """encodeSnapshot / encodeSnapshotV2 (fmt=2) of Snapshot objects over a batch."""
+    return convertSnapshotBatch([_snapshot_v1_bytes(s) for s in snapshots], 1, fmt, raise_errors)
+
+
+def decodeSnapshot(buf):
+    return decodeSnapshotBatch([buf], 1, True)[0]
+
+
+def decodeSnapshotV2(buf):
+    return decodeSnapshotBatch([buf], 2, True)[0]
+
+
+def encodeSnapshot(snapshot):
+    return encodeSnapshotBatch([snapshot], 1, True)[0]
+
+
+def encodeSnapshotV2(snapshot):
+    return encodeSnapshotBatch([snapshot], 2, True)[0]
