@@ -82,6 +82,11 @@ def cpu_baseline(arena, upd_off, doc_upd, fmt, seconds):
         "sample": f"{reps} x {n_docs} docs ({bytes_in / reps / 1e6:.1f} MB input each) in {el:.1f} s, "
                   f"oracle/ymerge_oracle.c (literal yjs 13.5.16 mergeUpdates), {threads} threads",
         "errors": int((st != 0).sum()),
+        # the port is faster than the JS it restates: per-thread ratios measured on identical C2 / C4
+        # documents in the build container (oracle/gen/time_js_baselines.cjs)
+        "calibration": {"port_over_yjs_13_5_16_js": {"c2": 5.25, "c4": 5.87},
+                        "port_over_reference_13_4_9_doc_roundtrip": {"c2": 11.2, "c4": 15.8},
+                        "source": "BASELINE.md section 2"},
     }
 
 
@@ -139,7 +144,9 @@ def secondary(dev, eng):
              ("diff_c5_v1", "diff", "c5_v1", 256), ("diff_c5_v2", "diff", "c5_v2", 256),
              ("meta_c2_v1", "meta", "c2_v1", 10000), ("meta_c2_v2", "meta", "c2_v2", 10000),
              ("meta_c3_v1", "meta", "c3_v1", 4096), ("meta_c3_v2", "meta", "c3_v2", 4096),
-             ("dsmerge_c4_v1", "dsmerge", "c4_v1", 10000), ("dsmerge_c4_v2", "dsmerge", "c4_v1", 10000)]
+             ("dsmerge_c4_v1", "dsmerge", "c4_v1", 10000), ("dsmerge_c4_v2", "dsmerge", "c4_v1", 10000),
+             # configs[3] at its per-GPU shard: 1 M docs over 8 GPUs = 125 k docs, 4,096 distinct templates
+             ("merge_c4_v1_125k", "merge", "c4_v1", 125000)]
     for name, op, wl, n in cases:
         if only and name not in only.split(","):
             continue
@@ -192,7 +199,9 @@ def secondary(dev, eng):
                 sva, svo, _ = pack_docs([[x] for x in svs])
         nd = len(d) - 1
         ga = torch.from_numpy(a).to(dev)
-        go = torch.from_numpy(o.view(np.int64)).to(dev)
+        # u32 update offsets (YM_OFF32) for the merges, as the headline line
+        off32 = op in ("merge", "dsmerge") and len(a) < 2 ** 32
+        go = torch.from_numpy(o.astype(np.uint32).view(np.int32) if off32 else o.view(np.int64)).to(dev)
         gd = torch.from_numpy(d.view(np.int32)).to(dev)
         gsa = torch.from_numpy(sva).to(dev) if sva is not None else None
         gso = torch.from_numpy(svo.view(np.int64)).to(dev) if svo is not None else None
@@ -213,11 +222,17 @@ def secondary(dev, eng):
         torch.cuda.synchronize(dev)
         el = (time.perf_counter() - t0) / steps
         sts = eng.stats
-        res[name] = {"docs": nd, "input_bytes": int(len(a)), "value_gbs": round(len(a) / el / 1e9, 3),
+        out_b = int(ol[st == 0].sum().item())
+        kms_mean = float(np.mean(kms))
+        # roofline of the call's dominant kernel(s): algorithmic bytes (inputs + outputs) / their device time
+        kgbs = (len(a) + out_b) / (kms_mean * 1e-3) / 1e9 if kms_mean > 0 else 0.0
+        res[name] = {"docs": nd, "input_bytes": int(len(a)), "output_bytes": out_b,
+                     "value_gbs": round(len(a) / el / 1e9, 3),
                      "docs_per_s": round(nd / el, 1), "ms_per_step": round(el * 1e3, 3),
-                     "kernel_ms": round(float(np.mean(kms)), 3), "docs_fast": int(sts["docs_fast"]),
+                     "kernel_ms": round(kms_mean, 3), "kernel_in_plus_out_gbs": round(kgbs, 2),
+                     "roofline_frac": round(kgbs / HBM_PEAK_GBS, 5), "docs_fast": int(sts["docs_fast"]),
                      "docs_large": int(sts["docs_large"]), "docs_general": int(sts["docs_general"]),
-                     "errors": int(sts["docs_error"])}
+                     "errors": int(sts["docs_error"]), "update_offsets": "u32" if off32 else "u64"}
         del ga, go, gd, gsa, gso, oa, oo, ol, st
         torch.cuda.empty_cache()
     return res

@@ -8,7 +8,8 @@
 //       generated and bench.py replicates them to 10,000 docs (doc i = template i % TEMPLATES).
 //   C3  B4-like single-client trace (259,778 single-char ops: 2% random jump, 29.7% backspace, else
 //       type), final state V1/V2; bench replicates it with random state vectors.
-//   C4  Y.Map docs, 64 clients, 128 broadcast transactions, keys k0..k7, delete p=0.6 when present.
+//   C4  Y.Map docs, 64 clients, 128 broadcast transactions, keys k0..k7, delete p=0.6 when present;
+//       4,096 templates (SURVEY.md §8(d)).
 //   C5  Y.XmlFragment docs, 1,024 clients x 16 transactions each (V1 and V2), see genXml.
 // File format (.ymb, little endian): "YMB1" u32 n_docs u32 n_upd | u32 doc_upd[n_docs+1] |
 // u64 upd_off[n_upd+1] | arena bytes; gzip-compressed.
@@ -101,6 +102,28 @@ function genMap (seed, nClients, nTx, nKeys) {
   return { v1, v2 }
 }
 
+// genMap with the 64 always-synced peers folded into one Doc: every transaction is followed by a broadcast
+// to all peers, so every peer holds the same state and a transaction of peer c is that state edited under
+// clientID c.  One Doc whose clientID is switched per transaction emits the very same update bytes (same
+// origins, clocks and delete sets; checked against genMap by `node make_bench_data.cjs <dir> c4check`) at
+// 1/64 of the cost.
+function genMapShared (seed, nClients, nTx, nKeys) {
+  const r = rng(seed)
+  const v1 = []; const v2 = []
+  const ids = []
+  for (let c = 0; c < nClients; c++) ids.push(500 + 31 * c)
+  const d = new Y.Doc(); d.clientID = ids[0]
+  d.on('update', u => v1.push(u))
+  d.on('updateV2', u => v2.push(u))
+  for (let t = 0; t < nTx; t++) {
+    d.clientID = ids[r.u32() % nClients]
+    const m = d.getMap('map')
+    const key = 'k' + (r.u32() % nKeys)
+    if (m.has(key) && r.real() < 0.6) m.delete(key)
+    else m.set(key, r.real() < 0.5 ? r.int(0, 1000000) : r.word(1, 6))
+  }
+  return { v1, v2 }
+}
 
 // C5: Y.XmlFragment('xml'), nClients clients x nTx transactions (16 per client), 30% one-way sync
 // between random peers after each transaction; local updates only (SURVEY.md §8(d) C5).  40% insert an
@@ -174,11 +197,18 @@ if (which.includes('c3')) {
   writeYmb(path.join(OUT, 'c3_v1.ymb.gz'), [[Y.encodeStateAsUpdate(d)]])
   writeYmb(path.join(OUT, 'c3_v2.ymb.gz'), [[Y.encodeStateAsUpdateV2(d)]])
 }
-if (which.includes('c4')) {
-  const T = Number(process.env.C4_TEMPLATES || 256)
+if (which.includes('c4check')) {  // genMapShared == genMap, byte for byte
+  for (let doc = 0; doc < 16; doc++) {
+    const a = genMap(doc + 1, 64, 128, 8); const b = genMapShared(doc + 1, 64, 128, 8)
+    const same = (x, y) => x.length === y.length && x.every((u, i) => Buffer.compare(Buffer.from(u), Buffer.from(y[i])) === 0)
+    if (!same(a.v1, b.v1) || !same(a.v2, b.v2)) throw new Error('genMapShared differs from genMap for template ' + doc)
+  }
+  console.log('genMapShared == genMap on 16 templates')
+} else if (which.includes('c4')) {
+  const T = Number(process.env.C4_TEMPLATES || 4096)
   const d1 = []; const d2 = []
   for (let doc = 0; doc < T; doc++) {
-    const { v1, v2 } = genMap(doc + 1, 64, 128, 8)
+    const { v1, v2 } = genMapShared(doc + 1, 64, 128, 8)
     d1.push(v1); d2.push(v2)
   }
   writeYmb(path.join(OUT, 'c4_v1.ymb.gz'), d1)

@@ -11,6 +11,6 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_
            "SQC_ICACHE_HITS SQC_ICACHE_MISSES GRBM_GUI_ACTIVE" \
            "FETCH_SIZE" "WRITE_SIZE" ${EXTRA_PMC}; do
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/$TAG/p$i -o run -- python3 tools/prof_run.py 5 > gpurun_out/$TAG/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/$TAG/p$i.log; exit 1; }
+  timeout -s KILL 150 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/$TAG/p$i -o run -- python3 ${RUNNER:-tools/prof_run.py} 5 > gpurun_out/$TAG/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/$TAG/p$i.log; exit 1; }
 done
 python3 tools/summarize_pmc.py gpurun_out/$TAG > gpurun_out/$TAG/summary.txt && cat gpurun_out/$TAG/summary.txt

@@ -82,6 +82,13 @@ constexpr uint32_t L_GMIN = L_PFIRST;           // u32[DSN]  group first appeara
 static_assert(L_P5END <= L_DKEY, "phase-5 arrays must not overlap the sorted delete ranges");
 static_assert(L_GMIN + 4 * DSN <= L_END, "group array fits");
 static_assert(SEC <= UPD, "the duplicate-check array reuses the walk list");
+// W1 struct records (skeleton walk -> validation pass -> section lengths), over the delete-range arrays
+// (W2 fills those only afterwards)
+constexpr uint32_t MAXS = 192;                  // max structs per document
+constexpr uint32_t L_TOFF = L_DKEY;             // u16[MAXS] LDS offset of the struct's info byte
+constexpr uint32_t L_TEND = L_TOFF + 2 * MAXS;  // u16[MAXS] ... of its end
+constexpr uint32_t L_TLEN = L_TEND + 2 * MAXS;  // u32[MAXS] its clock length
+static_assert(L_TLEN + 4 * MAXS <= L_PFIRST, "struct records fit over the delete ranges");
 constexpr uint32_t LDS_BYTES = L_END;
 static_assert(LDS_BYTES <= 8192, "5 one-wave workgroups per SIMD (160 KB LDS per CU)");
 
@@ -97,47 +104,119 @@ __device__ __forceinline__ void put_u64(Slot o, uint32_t p, uint64_t v) {
   __builtin_amdgcn_raw_buffer_store_b64(w, o, (int)p, 0, 0);
 }
 
-// Walks the struct section of update u and appends one record per client section (slot from an LDS
-// atomic counter, misc[0]); records where its delete set starts.  Item info bytes with an origin and
-// the parentSub bit get the bit cleared in place (13.5.16's lazy reader reads parentSub only without
-// origins and writes the info byte back without it, E8), so sections copy verbatim afterwards.
-// Returns false to decline.
-__device__ __forceinline__ bool walk_sections(uint32_t u) {
+// ---- W1a: skeleton walk (struct boundaries only; every field is re-read with all checks by W1b) -------
+constexpr uint32_t PLIM = IN + 8;  // skeleton positions are clamped here: 8-byte LDS reads stay in L_IN's slack
+// bytes of the varuint in window x (1..8; an unterminated window counts 8: W1b rejects it)
+__device__ __forceinline__ uint32_t vlen(uint64_t x) {
+  const uint64_t st = ~x & 0x8080808080808080ull;
+  return st ? (ctz64(st) >> 3) + 1 : 8;
+}
+// its value, clamped to 16 bits (lengths: anything larger runs past the document)
+__device__ __forceinline__ uint32_t vval16(uint64_t x, uint32_t nb) {
+  const uint32_t lo = (uint32_t)x;
+  const uint32_t v = (lo & 0x7fu) | ((lo >> 1) & 0x3f80u) | ((lo >> 2) & 0x1fc000u);
+  return nb > 2 ? (v > 0xffffu || nb > 3 ? 0xffffu : v) : v & ((1u << (7 * nb)) - 1);
+}
+__device__ __forceinline__ uint32_t skip_vu(uint32_t p) { return p + vlen(ld8(p)); }
+__device__ __forceinline__ uint32_t skip_vu2(uint32_t p) {  // an ID: two varuints, usually in one window
+  const uint64_t x = ld8(p);
+  const uint64_t st = ~x & 0x8080808080808080ull, st2 = st & (st - 1);
+  return st2 ? p + (ctz64(st2) >> 3) + 1 : skip_vu(skip_vu(p));
+}
+__device__ __forceinline__ uint32_t skip_str(uint32_t p) {  // varString / varUint8Array: length, bytes
+  const uint64_t x = ld8(p);
+  const uint32_t nb = vlen(x);
+  const uint32_t q = p + nb + vval16(x, nb);
+  return q < PLIM ? q : PLIM;
+}
+// One V1 Item (fields: UpdateDecoder.js:127-243, content refs: Item.js:665-683) skipped; kinds the fast path
+// does not take (GC, Skip, JSON, Doc, object / array / bigint / bytes `any` values, bad refs) set bad.
+__device__ __forceinline__ uint32_t skel_item(uint32_t p, uint32_t &bad) {
+  const uint32_t info = sm[p];
+  p++;
+  if (info & 0x80) p = skip_vu2(p);
+  if (info & 0x40) p = skip_vu2(p);
+  if ((info & 0xC0) == 0) {
+    p = sm[p] == 1 ? skip_str(p + 1) : skip_vu2(p + 1);  // parentInfo: ykey string / parent ID
+    if (info & 0x20) p = skip_str(p);                    // parentSub
+  }
+  switch (info & 31) {
+    case 1: p = skip_vu(p); break;                                        // ContentDeleted
+    case 3: case 4: case 5: p = skip_str(p); break;                       // Binary, String, Embed
+    case 6: p = skip_str(skip_str(p)); break;                             // Format: key, JSON value
+    case 7: {                                                             // Type: typeRef [, key]
+      const uint32_t t = sm[p];
+      p = t == 3 || t == 5 ? skip_str(p + 1) : p + 1;
+      break;
+    }
+    case 8: {                                                             // Any: count, scalar values
+      const uint64_t x = ld8(p);
+      const uint32_t nb = vlen(x), n = vval16(x, nb);
+      p += nb;
+      for (uint32_t i = 0; i < n && p < PLIM; i++) {
+        const uint32_t tag = sm[p++];
+        if (tag == 125) p = skip_vu(p);
+        else if (tag == 124) p += 4;
+        else if (tag == 123) p += 8;
+        else if (tag == 119) p = skip_str(p);
+        else if (tag < 120) { bad = 1; break; }
+      }
+      break;
+    }
+    default: bad = 1; break;
+  }
+  return p < PLIM ? p : PLIM;
+}
+// Update u's struct section: section headers read (and checked) here, one record per client section
+// (slots for all of the update's sections at once: misc[0]; struct slots per section: misc[2]), each
+// struct's byte range recorded for W1b.  Records where the delete set starts.  Returns false to decline.
+__device__ __forceinline__ bool walk_skeleton(uint32_t u) {
   Cur c = {at<uint16_t>(L_UOFF + 2 * u), at<uint16_t>(L_UOFF + 2 * u + 2), false};
   const uint32_t nclients = rvu(c);
-  uint64_t next_min = 0;  // sections of one update in merge order: each key > the previous one's last unit
-  for (uint32_t ci = 0; ci < nclients && !c.bad; ci++) {
+  uint32_t bad = c.bad | (nclients > SEC);
+  const uint32_t s0 = bad ? 0 : atomicAdd(&at<uint32_t>(L_MISC), nclients);
+  bad |= s0 + nclients > SEC;
+  for (uint32_t ci = 0; ci < nclients && !bad; ci++) {
     const uint32_t nstructs = rvu(c);
     const uint32_t client = rvu(c);
     const uint32_t clock = rvu(c);
-    const uint32_t b = c.p;
-    uint64_t len = 0;
-    for (uint32_t si = 0; si < nstructs && !c.bad; si++) {
-      // declines set c.bad (one exit edge per loop instead of one per check)
-      const uint32_t s0 = c.p;
-      const uint32_t info = rdb(c);
-      c.bad |= info == 10 || (info & 31) == 0;  // Skip / GC -> general path
-      uint32_t l = 1;
-      if (!c.bad) c.bad |= !item_body(c, info, l);
-      if ((info & 0xC0) != 0 && (info & 0x20) != 0) sm[s0] = (uint8_t)(info & ~0x20u);
-      len += l;
+    bad |= c.bad | (nstructs == 0) | (nstructs > MAXS);
+    if (bad) break;
+    const uint32_t t0 = atomicAdd(&at<uint32_t>(L_MISC + 8), nstructs);
+    bad |= t0 + nstructs > MAXS;
+    if (bad) break;
+    const uint32_t q = s0 + ci;
+    at<uint64_t>(L_SKEY + 8 * q) = ((uint64_t)(~client) << 32) | clock;
+    at<uint16_t>(L_SNS + 2 * q) = (uint16_t)(nstructs | (ci == 0 ? 0x8000u : 0u));  // first section of its update
+    at<uint16_t>(L_SB + 2 * q) = (uint16_t)c.p;
+    at<uint16_t>(L_SE + 2 * q) = (uint16_t)t0;  // first struct slot (the section end once lengths are known)
+    uint32_t p = c.p;
+    for (uint32_t si = 0; si < nstructs; si++) {
+      at<uint16_t>(L_TOFF + 2 * (t0 + si)) = (uint16_t)p;
+      p = skel_item(p, bad);
+      at<uint16_t>(L_TEND + 2 * (t0 + si)) = (uint16_t)p;
+      if (bad | (p > c.e)) break;
     }
-    const uint64_t key = ((uint64_t)(~client) << 32) | clock;
-    c.bad |= (nstructs == 0) | ((uint64_t)clock + len > 0xffffffffull) | (key < next_min);
-    next_min = key + len;
-    if (!c.bad) {
-      const uint32_t q = atomicAdd(&at<uint32_t>(L_MISC), 1u);
-      c.bad |= q >= SEC;
-      if (q < SEC) {
-        at<uint64_t>(L_SKEY + 8 * q) = key;
-        at<uint32_t>(L_SLEN + 4 * q) = (uint32_t)len;
-        at<uint16_t>(L_SNS + 2 * q) = (uint16_t)nstructs;
-        at<uint16_t>(L_SB + 2 * q) = (uint16_t)b;
-        at<uint16_t>(L_SE + 2 * q) = (uint16_t)c.p;
-      }
-    }
+    bad |= p > c.e;
+    c.p = p;
   }
   at<uint16_t>(L_UDS + 2 * u) = (uint16_t)c.p;
+  return !bad;
+}
+// W1b: struct t re-read with every check (item_body: canonical varints, strict UTF-8, JSON literals,
+// canonical `any` scalars), its clock length recorded; it must end exactly where the skeleton says.  Items
+// with an origin lose the parentSub bit in place (13.5.16's lazy reader reads parentSub only without
+// origins and writes the info byte back without it, E8), so sections copy verbatim afterwards.
+__device__ __forceinline__ bool check_struct(uint32_t t) {
+  const uint32_t s0 = at<uint16_t>(L_TOFF + 2 * t);
+  Cur c = {s0, at<uint16_t>(L_TEND + 2 * t), false};
+  const uint32_t info = rdb(c);
+  c.bad |= info == 10 || (info & 31) == 0;
+  uint32_t l = 1;
+  if (!c.bad) c.bad |= !item_body(c, info, l);
+  c.bad |= c.p != c.e;
+  if ((info & 0xC0) != 0 && (info & 0x20) != 0) sm[s0] = (uint8_t)(info & ~0x20u);
+  at<uint32_t>(L_TLEN + 4 * t) = l;
   return !c.bad;
 }
 // Walks the delete set of update u (DeleteSet.js:219-256) and appends its ranges (slots from misc[1]);
@@ -198,6 +277,234 @@ __device__ __forceinline__ bool walk_ds(uint32_t u) {
     continue;                                                           \
   }
 
+// ---- 5/6. delete set of document d (EE delete ranges per lane: 1 when they fit one wave) --------------
+enum : int { DS_DONE = 0, DS_DECLINE = 1, DS_STOP = 2 };
+template <uint32_t EE, int STOP, bool DSV2>
+__device__ __forceinline__ int ds_phase(const GeneralJob &j, uint32_t d, uint32_t nds, uint32_t hdr, uint32_t struct_bytes,
+                                        uint64_t slot, uint64_t slot_al, uint64_t slot_end, uint64_t bytes, Slot dst) {
+  const uint32_t lane = threadIdx.x;
+  bool bad = false;
+    // ---- 5. delete set
+    {
+      uint64_t dk[EE];
+      uint32_t dl[EE], dq[EE], dr[EE];
+#pragma unroll
+      for (uint32_t s = 0; s < EE; s++) {
+        const uint32_t i = lane + 64 * s;
+        const bool v = i < nds;
+        dk[s] = v ? at<uint64_t>(L_DKEY + 8 * i) : ~0ull;
+        dl[s] = v ? at<uint32_t>(L_DLEN + 4 * i) : 0;
+        dq[s] = v ? at<uint16_t>(L_DSEQ + 2 * i) : 0;
+      }
+      rank_le(L_DKEY, nds, dk, dr);  // distinct keys: a permutation
+      __syncthreads();
+#pragma unroll
+      for (uint32_t s = 0; s < EE; s++) {
+        if (lane + 64 * s < nds) {
+          const uint32_t r = dr[s];
+          at<uint64_t>(L_DKEY + 8 * r) = dk[s];
+          at<uint32_t>(L_DLEN + 4 * r) = dl[s];
+          at<uint16_t>(L_DSEQ + 2 * r) = (uint16_t)dq[s];
+        }
+      }
+      __syncthreads();
+    }
+    // sorted positions r = E*lane + s: client segments (= groups), running max end of the union,
+    // merged ranges.  Per position only its key, end, segment flag and id stay in registers.
+    uint32_t ngroups, nranges;
+    {
+      uint32_t ecl[EE], ecli[EE], segst[EE], segid[EE], eseq[EE];
+      uint64_t eend[EE];
+      uint32_t seg_lane = 0;
+      const uint32_t r0 = EE * lane;
+      uint32_t cprev = r0 > 0 && r0 - 1 < nds ? (uint32_t)(at<uint64_t>(L_DKEY + 8 * (r0 - 1)) >> 32) : 0;
+#pragma unroll
+      for (uint32_t s = 0; s < EE; s++) {
+        const uint32_t r = r0 + s;
+        const bool v = r < nds;
+        const uint64_t k = v ? at<uint64_t>(L_DKEY + 8 * r) : 0;
+        ecl[s] = (uint32_t)k >> 7;
+        ecli[s] = (uint32_t)(k >> 32);
+        eend[s] = v ? (uint64_t)ecl[s] + at<uint32_t>(L_DLEN + 4 * r) : 0;
+        eseq[s] = v ? at<uint16_t>(L_DSEQ + 2 * r) : 0xffff;
+        segst[s] = v && (r == 0 || cprev != ecli[s]);
+        seg_lane += segst[s];
+        cprev = ecli[s];
+      }
+      {
+        const uint32_t incl = wave_incl_add(seg_lane);
+        ngroups = lane_read(incl, 63);
+        uint32_t run = incl - seg_lane;
+#pragma unroll
+        for (uint32_t s = 0; s < EE; s++) { run += segst[s]; segid[s] = run - 1; }
+      }
+      // running max of (segment << 33 | end): within a segment it is the max end so far
+      uint64_t m = 0, rmax[EE];
+#pragma unroll
+      for (uint32_t s = 0; s < EE; s++) {
+        const uint64_t x = r0 + s < nds ? ((uint64_t)segid[s] << 33) | eend[s] : 0;
+        m = x > m ? x : m;
+        rmax[s] = m;
+      }
+      const uint64_t incl = wave_incl_max64(m);
+      uint64_t ex = ((uint64_t)from_prev_lane((uint32_t)(incl >> 32)) << 32) | from_prev_lane((uint32_t)incl);
+      uint32_t newr[EE], nr_lane = 0;
+#pragma unroll
+      for (uint32_t s = 0; s < EE; s++) {
+        const uint64_t before = ex;  // running max through position r - 1
+        rmax[s] = rmax[s] > ex ? rmax[s] : ex;
+        ex = rmax[s];
+        newr[s] = r0 + s < nds && (segst[s] || ecl[s] > (before & 0x1ffffffffull));
+        nr_lane += newr[s];
+      }
+      const uint32_t incl_r = wave_incl_add(nr_lane);
+      nranges = lane_read(incl_r, 63);
+      uint32_t run = incl_r - nr_lane;
+      const uint32_t next_first = from_next_lane(newr[0]);  // newr of position E*(lane+1)
+      __syncthreads();  // the sorted delete ranges are in registers: the phase-5 arrays reuse R
+#pragma unroll
+      for (uint32_t s = 0; s < EE; s++) {
+        const uint32_t r = r0 + s;
+        if (r >= nds) break;
+        run += newr[s];
+        const uint32_t rid = run - 1;
+        if (newr[s]) {
+          at<uint32_t>(L_QCLK + 4 * rid) = ecl[s];
+          at<uint8_t>(L_QGRP + rid) = (uint8_t)segid[s];
+        }
+        const bool nxt_new = s + 1 < EE ? newr[s + 1] != 0 : next_first != 0;
+        if (r + 1 >= nds || nxt_new) {
+          const uint64_t en = rmax[s] & 0x1ffffffffull;
+          bad |= en > 0xffffffffull;
+          at<uint32_t>(L_QEND + 4 * rid) = (uint32_t)en;
+        }
+        if (segst[s]) {
+          at<uint16_t>(L_GFIRST + 2 * segid[s]) = (uint16_t)rid;
+          at<uint32_t>(L_GCLI + 4 * segid[s]) = ecli[s];
+          at<uint32_t>(L_GMIN + 4 * segid[s]) = 0xffffffffu;
+        }
+      }
+      if (lane == 0) at<uint16_t>(L_GFIRST + 2 * ngroups) = (uint16_t)nranges;
+      if (__any(bad)) return DS_DECLINE;
+      __syncthreads();
+      // first appearance of each client: min over its entries' (update << 8 | position)
+#pragma unroll
+      for (uint32_t s = 0; s < EE; s++)
+        if (r0 + s < nds) atomicMin(&at<uint32_t>(L_GMIN + 4 * segid[s]), eseq[s]);
+    }
+    // merged ranges q = E*lane + s: exclusive byte prefix over range ids
+    {
+      uint32_t qb[EE], t = 0;
+#pragma unroll
+      for (uint32_t s = 0; s < EE; s++) {
+        const uint32_t q = EE * lane + s;
+        const uint32_t c0 = q < nranges ? at<uint32_t>(L_QCLK + 4 * q) : 0;
+        if constexpr (DSV2) {
+          const bool first = q < nranges && at<uint16_t>(L_GFIRST + 2 * at<uint8_t>(L_QGRP + q)) == q;
+          const uint32_t pe = q < nranges && !first ? at<uint32_t>(L_QEND + 4 * (q - 1)) : 0;
+          qb[s] = q < nranges ? vsz(c0 - pe) + vsz(at<uint32_t>(L_QEND + 4 * q) - c0 - 1) : 0;
+        } else {
+          qb[s] = q < nranges ? vsz(c0) + vsz(at<uint32_t>(L_QEND + 4 * q) - c0) : 0;
+        }
+        t += qb[s];
+      }
+      const uint32_t incl = wave_incl_add(t);
+      uint32_t run = incl - t;
+#pragma unroll
+      for (uint32_t s = 0; s < EE; s++) {
+        const uint32_t q = EE * lane + s;
+        if (q < nranges) at<uint16_t>(L_QPRE + 2 * q) = (uint16_t)run;
+        run += qb[s];
+      }
+      if (lane == 63) at<uint16_t>(L_QPRE + 2 * nranges) = (uint16_t)incl;
+    }
+    __syncthreads();
+    // groups g = lane + 64 s: bytes and rank by first appearance
+    uint32_t grk[EE], gbytes[EE];
+#pragma unroll
+    for (uint32_t s = 0; s < EE; s++) {
+      const uint32_t g = lane + 64 * s;
+      const bool v = g < ngroups;
+      const uint32_t f0 = v ? at<uint16_t>(L_GFIRST + 2 * g) : 0, f1 = v ? at<uint16_t>(L_GFIRST + 2 * g + 2) : 0;
+      gbytes[s] = v ? vsz(at<uint32_t>(L_GCLI + 4 * g)) + vsz(f1 - f0) + at<uint16_t>(L_QPRE + 2 * f1) -
+                          at<uint16_t>(L_QPRE + 2 * f0)
+                    : 0;
+      const uint32_t mine = v ? at<uint32_t>(L_GMIN + 4 * g) : 0;
+      uint32_t rk_ = 0;
+      for (uint32_t h = 0; h < ngroups; h++) rk_ += at<uint32_t>(L_GMIN + 4 * h) < mine;
+      grk[s] = rk_;
+    }
+#pragma unroll
+    for (uint32_t s = 0; s < EE; s++)
+      if (lane + 64 * s < ngroups) at<uint16_t>(L_GBYR + 2 * grk[s]) = (uint16_t)gbytes[s];
+    __syncthreads();
+    const uint32_t ds_hdr = vsz(ngroups);
+    const uint32_t dsb = hdr + struct_bytes;
+    uint32_t ds_groups_bytes;
+    {  // exclusive prefix over ranks (ranks E*lane + s)
+      uint32_t v[EE], t = 0;
+#pragma unroll
+      for (uint32_t s = 0; s < EE; s++) { const uint32_t r = EE * lane + s; v[s] = r < ngroups ? at<uint16_t>(L_GBYR + 2 * r) : 0; t += v[s]; }
+      const uint32_t incl = wave_incl_add(t);
+      ds_groups_bytes = lane_read(incl, 63);
+      uint32_t run = incl - t;
+      __syncthreads();
+#pragma unroll
+      for (uint32_t s = 0; s < EE; s++) {
+        const uint32_t r = EE * lane + s;
+        if (r < ngroups) at<uint16_t>(L_GBYR + 2 * r) = (uint16_t)run;
+        run += v[s];
+      }
+    }
+    __syncthreads();
+    // group g's output offset; its ranges' base = offset + header - prefix of its first range
+#pragma unroll
+    for (uint32_t s = 0; s < EE; s++) {
+      const uint32_t g = lane + 64 * s;
+      if (g < ngroups) {
+        const uint32_t f0 = at<uint16_t>(L_GFIRST + 2 * g), f1 = at<uint16_t>(L_GFIRST + 2 * g + 2);
+        const uint32_t off = dsb + ds_hdr + at<uint16_t>(L_GBYR + 2 * grk[s]);
+        at<uint32_t>(L_GMIN + 4 * g) = off;  // first appearance is no longer needed
+        at<uint32_t>(L_GB2 + 4 * g) = off + vsz(at<uint32_t>(L_GCLI + 4 * g)) + vsz(f1 - f0) - at<uint16_t>(L_QPRE + 2 * f0);
+      }
+    }
+    __syncthreads();
+    const uint32_t total = dsb + ds_hdr + ds_groups_bytes;
+    if (slot_al + total > slot_end) {
+      if (slot_al + total > slot + 2 * bytes + 64) return DS_DECLINE;
+      if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }
+      return DS_DONE;
+    }
+    if (STOP == 5) return DS_STOP;
+    // ---- 6. write the delete set: vu(#clients) | per client (first-appearance order): client, count, ranges
+    if (lane == 0) put_vu(dst, dsb, ngroups);
+#pragma unroll
+    for (uint32_t s = 0; s < EE; s++) {
+      const uint32_t g = lane + 64 * s;
+      if (g < ngroups)
+        put_vu(dst, put_vu(dst, at<uint32_t>(L_GMIN + 4 * g), at<uint32_t>(L_GCLI + 4 * g)),
+               at<uint16_t>(L_GFIRST + 2 * g + 2) - at<uint16_t>(L_GFIRST + 2 * g));
+      const uint32_t q = EE * lane + s;
+      if (q < nranges) {
+        const uint32_t c0 = at<uint32_t>(L_QCLK + 4 * q);
+        const uint32_t off = at<uint32_t>(L_GB2 + 4 * at<uint8_t>(L_QGRP + q)) + at<uint16_t>(L_QPRE + 2 * q);
+        if constexpr (DSV2) {
+          const bool first = at<uint16_t>(L_GFIRST + 2 * at<uint8_t>(L_QGRP + q)) == q;
+          const uint32_t pe = first ? 0 : at<uint32_t>(L_QEND + 4 * (q - 1));
+          put_vu(dst, put_vu(dst, off, c0 - pe), at<uint32_t>(L_QEND + 4 * q) - c0 - 1);
+        } else {
+          put_vu(dst, put_vu(dst, off, c0), at<uint32_t>(L_QEND + 4 * q) - c0);
+        }
+      }
+    }
+    if (lane == 0) {
+      j.out_off[d] = slot_al;
+      j.out_len[d] = total;
+      j.status[d] = ym::ST_OK;
+    }
+    return DS_DONE;
+}
+
 // DSONLY: PermanentUserData's delete-set merge (ym_ds_merge): every input is an encoded delete set (no
 // struct section); the walk is W2 only and the output is the merged delete set alone, in the DSEncoderV1
 // format, or DSEncoderV2's (DSV2: clocks delta-coded within a client, lengths minus one).
@@ -222,7 +529,7 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
       for (uint32_t v = lane; v < nvec; v += 64) at<uint4>(L_IN + 16 * v) = src[v];
     }
     for (uint32_t i = lane; i <= k; i += 64) at<uint16_t>(L_UOFF + 2 * i) = (uint16_t)(uoff_g(j, u0 + i) - b0 + base);
-    if (lane < 2) at<uint32_t>(L_MISC + 4 * lane) = 0;
+    if (lane < 3) at<uint32_t>(L_MISC + 4 * lane) = 0;
     if (lane < 16) at<uint32_t>(L_HIST + 4 * lane) = 0;
     __syncthreads();
     YM_STOP(1)
@@ -262,8 +569,43 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
       __syncthreads();
       bool ok = true;
 #pragma unroll 1
-      for (uint32_t i = lane; i < n1; i += 64) ok &= walk_sections(at<uint8_t>(L_UORD + i));
+      for (uint32_t i = lane; i < n1; i += 64) ok &= walk_skeleton(at<uint8_t>(L_UORD + i));
       if (__any(!ok)) YM_DECLINE()
+      __syncthreads();
+      // W1b: one lane per struct
+      const uint32_t nst = at<uint32_t>(L_MISC + 8), nsec0 = at<uint32_t>(L_MISC);
+#pragma unroll 1
+      for (uint32_t t = lane; t < nst; t += 64) ok &= check_struct(t);
+      if (__any(!ok)) YM_DECLINE()
+      __syncthreads();
+      // section lengths (sum of their structs'), ends, and the merge-order check inside each update
+      {
+        uint32_t first[E];
+        bool sbad = false;
+#pragma unroll
+        for (uint32_t s = 0; s < E; s++) {
+          const uint32_t q = lane + 64 * s;
+          first[s] = 1;
+          if (q < nsec0) {
+            const uint32_t w = at<uint16_t>(L_SNS + 2 * q), ns = w & 0x7fffu, t0 = at<uint16_t>(L_SE + 2 * q);
+            uint64_t len = 0;
+            for (uint32_t t = t0; t < t0 + ns; t++) len += at<uint32_t>(L_TLEN + 4 * t);
+            first[s] = w >> 15;
+            sbad |= (at<uint64_t>(L_SKEY + 8 * q) & 0xffffffffull) + len > 0xffffffffull;
+            at<uint32_t>(L_SLEN + 4 * q) = (uint32_t)len;
+            at<uint16_t>(L_SE + 2 * q) = at<uint16_t>(L_TEND + 2 * (t0 + ns - 1));
+            at<uint16_t>(L_SNS + 2 * q) = (uint16_t)ns;
+          }
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t s = 0; s < E; s++) {
+          const uint32_t q = lane + 64 * s;
+          if (q < nsec0 && !first[s])  // sections of one update in merge order: above the previous one's last unit
+            sbad |= at<uint64_t>(L_SKEY + 8 * q) < at<uint64_t>(L_SKEY + 8 * (q - 1)) + at<uint32_t>(L_SLEN + 4 * (q - 1));
+        }
+        if (__any(sbad)) YM_DECLINE()
+      }
       __syncthreads();
       YM_STOP(8)
       // W2 list: updates whose delete set has clients (first byte != 0), compacted by ballots
@@ -442,224 +784,11 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
     }
     }  // !DSONLY
     YM_STOP(7)
-    // ---- 5. delete set
     {
-      uint64_t dk[E];
-      uint32_t dl[E], dq[E], dr[E];
-#pragma unroll
-      for (uint32_t s = 0; s < E; s++) {
-        const uint32_t i = lane + 64 * s;
-        const bool v = i < nds;
-        dk[s] = v ? at<uint64_t>(L_DKEY + 8 * i) : ~0ull;
-        dl[s] = v ? at<uint32_t>(L_DLEN + 4 * i) : 0;
-        dq[s] = v ? at<uint16_t>(L_DSEQ + 2 * i) : 0;
-      }
-      rank_le(L_DKEY, nds, dk, dr);  // distinct keys: a permutation
-      __syncthreads();
-#pragma unroll
-      for (uint32_t s = 0; s < E; s++) {
-        if (lane + 64 * s < nds) {
-          const uint32_t r = dr[s];
-          at<uint64_t>(L_DKEY + 8 * r) = dk[s];
-          at<uint32_t>(L_DLEN + 4 * r) = dl[s];
-          at<uint16_t>(L_DSEQ + 2 * r) = (uint16_t)dq[s];
-        }
-      }
-      __syncthreads();
-    }
-    // sorted positions r = E*lane + s: client segments (= groups), running max end of the union,
-    // merged ranges.  Per position only its key, end, segment flag and id stay in registers.
-    uint32_t ngroups, nranges;
-    {
-      uint32_t ecl[E], ecli[E], segst[E], segid[E], eseq[E];
-      uint64_t eend[E];
-      uint32_t seg_lane = 0;
-      const uint32_t r0 = E * lane;
-      uint32_t cprev = r0 > 0 && r0 - 1 < nds ? (uint32_t)(at<uint64_t>(L_DKEY + 8 * (r0 - 1)) >> 32) : 0;
-#pragma unroll
-      for (uint32_t s = 0; s < E; s++) {
-        const uint32_t r = r0 + s;
-        const bool v = r < nds;
-        const uint64_t k = v ? at<uint64_t>(L_DKEY + 8 * r) : 0;
-        ecl[s] = (uint32_t)k >> 7;
-        ecli[s] = (uint32_t)(k >> 32);
-        eend[s] = v ? (uint64_t)ecl[s] + at<uint32_t>(L_DLEN + 4 * r) : 0;
-        eseq[s] = v ? at<uint16_t>(L_DSEQ + 2 * r) : 0xffff;
-        segst[s] = v && (r == 0 || cprev != ecli[s]);
-        seg_lane += segst[s];
-        cprev = ecli[s];
-      }
-      {
-        const uint32_t incl = wave_incl_add(seg_lane);
-        ngroups = lane_read(incl, 63);
-        uint32_t run = incl - seg_lane;
-#pragma unroll
-        for (uint32_t s = 0; s < E; s++) { run += segst[s]; segid[s] = run - 1; }
-      }
-      // running max of (segment << 33 | end): within a segment it is the max end so far
-      uint64_t m = 0, rmax[E];
-#pragma unroll
-      for (uint32_t s = 0; s < E; s++) {
-        const uint64_t x = r0 + s < nds ? ((uint64_t)segid[s] << 33) | eend[s] : 0;
-        m = x > m ? x : m;
-        rmax[s] = m;
-      }
-      const uint64_t incl = wave_incl_max64(m);
-      uint64_t ex = ((uint64_t)from_prev_lane((uint32_t)(incl >> 32)) << 32) | from_prev_lane((uint32_t)incl);
-      uint32_t newr[E], nr_lane = 0;
-#pragma unroll
-      for (uint32_t s = 0; s < E; s++) {
-        const uint64_t before = ex;  // running max through position r - 1
-        rmax[s] = rmax[s] > ex ? rmax[s] : ex;
-        ex = rmax[s];
-        newr[s] = r0 + s < nds && (segst[s] || ecl[s] > (before & 0x1ffffffffull));
-        nr_lane += newr[s];
-      }
-      const uint32_t incl_r = wave_incl_add(nr_lane);
-      nranges = lane_read(incl_r, 63);
-      uint32_t run = incl_r - nr_lane;
-      const uint32_t next_first = from_next_lane(newr[0]);  // newr of position E*(lane+1)
-      __syncthreads();  // the sorted delete ranges are in registers: the phase-5 arrays reuse R
-#pragma unroll
-      for (uint32_t s = 0; s < E; s++) {
-        const uint32_t r = r0 + s;
-        if (r >= nds) break;
-        run += newr[s];
-        const uint32_t rid = run - 1;
-        if (newr[s]) {
-          at<uint32_t>(L_QCLK + 4 * rid) = ecl[s];
-          at<uint8_t>(L_QGRP + rid) = (uint8_t)segid[s];
-        }
-        const bool nxt_new = s + 1 < E ? newr[s + 1] != 0 : next_first != 0;
-        if (r + 1 >= nds || nxt_new) {
-          const uint64_t en = rmax[s] & 0x1ffffffffull;
-          bad |= en > 0xffffffffull;
-          at<uint32_t>(L_QEND + 4 * rid) = (uint32_t)en;
-        }
-        if (segst[s]) {
-          at<uint16_t>(L_GFIRST + 2 * segid[s]) = (uint16_t)rid;
-          at<uint32_t>(L_GCLI + 4 * segid[s]) = ecli[s];
-          at<uint32_t>(L_GMIN + 4 * segid[s]) = 0xffffffffu;
-        }
-      }
-      if (lane == 0) at<uint16_t>(L_GFIRST + 2 * ngroups) = (uint16_t)nranges;
-      if (__any(bad)) YM_DECLINE()
-      __syncthreads();
-      // first appearance of each client: min over its entries' (update << 8 | position)
-#pragma unroll
-      for (uint32_t s = 0; s < E; s++)
-        if (r0 + s < nds) atomicMin(&at<uint32_t>(L_GMIN + 4 * segid[s]), eseq[s]);
-    }
-    // merged ranges q = E*lane + s: exclusive byte prefix over range ids
-    {
-      uint32_t qb[E], t = 0;
-#pragma unroll
-      for (uint32_t s = 0; s < E; s++) {
-        const uint32_t q = E * lane + s;
-        const uint32_t c0 = q < nranges ? at<uint32_t>(L_QCLK + 4 * q) : 0;
-        if constexpr (DSV2) {
-          const bool first = q < nranges && at<uint16_t>(L_GFIRST + 2 * at<uint8_t>(L_QGRP + q)) == q;
-          const uint32_t pe = q < nranges && !first ? at<uint32_t>(L_QEND + 4 * (q - 1)) : 0;
-          qb[s] = q < nranges ? vsz(c0 - pe) + vsz(at<uint32_t>(L_QEND + 4 * q) - c0 - 1) : 0;
-        } else {
-          qb[s] = q < nranges ? vsz(c0) + vsz(at<uint32_t>(L_QEND + 4 * q) - c0) : 0;
-        }
-        t += qb[s];
-      }
-      const uint32_t incl = wave_incl_add(t);
-      uint32_t run = incl - t;
-#pragma unroll
-      for (uint32_t s = 0; s < E; s++) {
-        const uint32_t q = E * lane + s;
-        if (q < nranges) at<uint16_t>(L_QPRE + 2 * q) = (uint16_t)run;
-        run += qb[s];
-      }
-      if (lane == 63) at<uint16_t>(L_QPRE + 2 * nranges) = (uint16_t)incl;
-    }
-    __syncthreads();
-    // groups g = lane + 64 s: bytes and rank by first appearance
-    uint32_t grk[E], gbytes[E];
-#pragma unroll
-    for (uint32_t s = 0; s < E; s++) {
-      const uint32_t g = lane + 64 * s;
-      const bool v = g < ngroups;
-      const uint32_t f0 = v ? at<uint16_t>(L_GFIRST + 2 * g) : 0, f1 = v ? at<uint16_t>(L_GFIRST + 2 * g + 2) : 0;
-      gbytes[s] = v ? vsz(at<uint32_t>(L_GCLI + 4 * g)) + vsz(f1 - f0) + at<uint16_t>(L_QPRE + 2 * f1) -
-                          at<uint16_t>(L_QPRE + 2 * f0)
-                    : 0;
-      const uint32_t mine = v ? at<uint32_t>(L_GMIN + 4 * g) : 0;
-      uint32_t rk_ = 0;
-      for (uint32_t h = 0; h < ngroups; h++) rk_ += at<uint32_t>(L_GMIN + 4 * h) < mine;
-      grk[s] = rk_;
-    }
-#pragma unroll
-    for (uint32_t s = 0; s < E; s++)
-      if (lane + 64 * s < ngroups) at<uint16_t>(L_GBYR + 2 * grk[s]) = (uint16_t)gbytes[s];
-    __syncthreads();
-    const uint32_t ds_hdr = vsz(ngroups);
-    const uint32_t dsb = hdr + struct_bytes;
-    uint32_t ds_groups_bytes;
-    {  // exclusive prefix over ranks (ranks E*lane + s)
-      uint32_t v[E], t = 0;
-#pragma unroll
-      for (uint32_t s = 0; s < E; s++) { const uint32_t r = E * lane + s; v[s] = r < ngroups ? at<uint16_t>(L_GBYR + 2 * r) : 0; t += v[s]; }
-      const uint32_t incl = wave_incl_add(t);
-      ds_groups_bytes = lane_read(incl, 63);
-      uint32_t run = incl - t;
-      __syncthreads();
-#pragma unroll
-      for (uint32_t s = 0; s < E; s++) {
-        const uint32_t r = E * lane + s;
-        if (r < ngroups) at<uint16_t>(L_GBYR + 2 * r) = (uint16_t)run;
-        run += v[s];
-      }
-    }
-    __syncthreads();
-    // group g's output offset; its ranges' base = offset + header - prefix of its first range
-#pragma unroll
-    for (uint32_t s = 0; s < E; s++) {
-      const uint32_t g = lane + 64 * s;
-      if (g < ngroups) {
-        const uint32_t f0 = at<uint16_t>(L_GFIRST + 2 * g), f1 = at<uint16_t>(L_GFIRST + 2 * g + 2);
-        const uint32_t off = dsb + ds_hdr + at<uint16_t>(L_GBYR + 2 * grk[s]);
-        at<uint32_t>(L_GMIN + 4 * g) = off;  // first appearance is no longer needed
-        at<uint32_t>(L_GB2 + 4 * g) = off + vsz(at<uint32_t>(L_GCLI + 4 * g)) + vsz(f1 - f0) - at<uint16_t>(L_QPRE + 2 * f0);
-      }
-    }
-    __syncthreads();
-    const uint32_t total = dsb + ds_hdr + ds_groups_bytes;
-    if (slot_al + total > slot_end) {
-      if (slot_al + total > slot + 2 * bytes + 64) YM_DECLINE()
-      if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }
-      __syncthreads();
-      continue;
-    }
-    YM_STOP(5)
-    // ---- 6. write the delete set: vu(#clients) | per client (first-appearance order): client, count, ranges
-    if (lane == 0) put_vu(dst, dsb, ngroups);
-#pragma unroll
-    for (uint32_t s = 0; s < E; s++) {
-      const uint32_t g = lane + 64 * s;
-      if (g < ngroups)
-        put_vu(dst, put_vu(dst, at<uint32_t>(L_GMIN + 4 * g), at<uint32_t>(L_GCLI + 4 * g)),
-               at<uint16_t>(L_GFIRST + 2 * g + 2) - at<uint16_t>(L_GFIRST + 2 * g));
-      const uint32_t q = E * lane + s;
-      if (q < nranges) {
-        const uint32_t c0 = at<uint32_t>(L_QCLK + 4 * q);
-        const uint32_t off = at<uint32_t>(L_GB2 + 4 * at<uint8_t>(L_QGRP + q)) + at<uint16_t>(L_QPRE + 2 * q);
-        if constexpr (DSV2) {
-          const bool first = at<uint16_t>(L_GFIRST + 2 * at<uint8_t>(L_QGRP + q)) == q;
-          const uint32_t pe = first ? 0 : at<uint32_t>(L_QEND + 4 * (q - 1));
-          put_vu(dst, put_vu(dst, off, c0 - pe), at<uint32_t>(L_QEND + 4 * q) - c0 - 1);
-        } else {
-          put_vu(dst, put_vu(dst, off, c0), at<uint32_t>(L_QEND + 4 * q) - c0);
-        }
-      }
-    }
-    if (lane == 0) {
-      j.out_off[d] = slot_al;
-      j.out_len[d] = total;
-      j.status[d] = ym::ST_OK;
+      const int r = nds <= 64 ? ds_phase<1, STOP, DSV2>(j, d, nds, hdr, struct_bytes, slot, slot_al, slot_end, bytes, dst)
+                              : ds_phase<2, STOP, DSV2>(j, d, nds, hdr, struct_bytes, slot, slot_al, slot_end, bytes, dst);
+      if (r == DS_DECLINE) YM_DECLINE()
+      if (r == DS_STOP && lane == 0) { j.status[d] = ym::ST_OK; j.out_len[d] = 0; }
     }
     __syncthreads();
   }
