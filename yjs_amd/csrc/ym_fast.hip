@@ -82,13 +82,6 @@ constexpr uint32_t L_GMIN = L_PFIRST;           // u32[DSN]  group first appeara
 static_assert(L_P5END <= L_DKEY, "phase-5 arrays must not overlap the sorted delete ranges");
 static_assert(L_GMIN + 4 * DSN <= L_END, "group array fits");
 static_assert(SEC <= UPD, "the duplicate-check array reuses the walk list");
-// W1 struct records (skeleton walk -> validation pass -> section lengths), over the delete-range arrays
-// (W2 fills those only afterwards)
-constexpr uint32_t MAXS = 192;                  // max structs per document
-constexpr uint32_t L_TOFF = L_DKEY;             // u16[MAXS] LDS offset of the struct's info byte
-constexpr uint32_t L_TEND = L_TOFF + 2 * MAXS;  // u16[MAXS] ... of its end
-constexpr uint32_t L_TLEN = L_TEND + 2 * MAXS;  // u32[MAXS] its clock length
-static_assert(L_TLEN + 4 * MAXS <= L_PFIRST, "struct records fit over the delete ranges");
 constexpr uint32_t LDS_BYTES = L_END;
 static_assert(LDS_BYTES <= 8192, "5 one-wave workgroups per SIMD (160 KB LDS per CU)");
 
@@ -104,119 +97,161 @@ __device__ __forceinline__ void put_u64(Slot o, uint32_t p, uint64_t v) {
   __builtin_amdgcn_raw_buffer_store_b64(w, o, (int)p, 0, 0);
 }
 
-// ---- W1a: skeleton walk (struct boundaries only; every field is re-read with all checks by W1b) -------
-constexpr uint32_t PLIM = IN + 8;  // skeleton positions are clamped here: 8-byte LDS reads stay in L_IN's slack
-// bytes of the varuint in window x (1..8; an unterminated window counts 8: W1b rejects it)
-__device__ __forceinline__ uint32_t vlen(uint64_t x) {
-  const uint64_t st = ~x & 0x8080808080808080ull;
-  return st ? (ctz64(st) >> 3) + 1 : 8;
-}
-// its value, clamped to 16 bits (lengths: anything larger runs past the document)
-__device__ __forceinline__ uint32_t vval16(uint64_t x, uint32_t nb) {
-  const uint32_t lo = (uint32_t)x;
-  const uint32_t v = (lo & 0x7fu) | ((lo >> 1) & 0x3f80u) | ((lo >> 2) & 0x1fc000u);
-  return nb > 2 ? (v > 0xffffu || nb > 3 ? 0xffffu : v) : v & ((1u << (7 * nb)) - 1);
-}
-__device__ __forceinline__ uint32_t skip_vu(uint32_t p) { return p + vlen(ld8(p)); }
-__device__ __forceinline__ uint32_t skip_vu2(uint32_t p) {  // an ID: two varuints, usually in one window
+// ---- short-cut Item parser (the shapes yjs writes for text, formats and map values) --------------------
+// Each helper is branch-free: a wave whose lanes sit at different Items runs one straight copy of each
+// instead of item_body's per-kind regions.  Any shape or check the short-cut does not decide clears `ok`;
+// the caller then re-parses that Item with item_body (same checks, so both agree on every Item they take).
+// An ID (client, clock): two canonical varuints < 2^32 inside one 8-byte window (ID_SKIP of skvu2)
+__device__ __forceinline__ void fast_id(uint32_t &p, bool &ok) {
   const uint64_t x = ld8(p);
   const uint64_t st = ~x & 0x8080808080808080ull, st2 = st & (st - 1);
-  return st2 ? p + (ctz64(st2) >> 3) + 1 : skip_vu(skip_vu(p));
+  const uint32_t i1 = ctz64(st) >> 3, i2r = ctz64(st2) >> 3, i2 = i2r < 7 ? i2r : 7;
+  const uint32_t b1 = (uint32_t)(x >> (8 * (i1 < 7 ? i1 : 7))) & 0xffu, b2 = (uint32_t)(x >> (8 * i2)) & 0xffu;
+  const uint32_t n1 = i1 + 1, n2 = i2r - i1;
+  ok &= (st2 != 0) & (n1 <= 5) & (n2 <= 5) & !((n1 > 1) & (b1 == 0)) & !((n2 > 1) & (b2 == 0)) &
+        !((n1 == 5) & ((b1 & 0x70u) != 0)) & !((n2 == 5) & ((b2 & 0x70u) != 0));
+  p += i2 + 1;
 }
-__device__ __forceinline__ uint32_t skip_str(uint32_t p) {  // varString / varUint8Array: length, bytes
+// a varString of at most 7 ASCII bytes with a one-byte length: its length (= UTF-16 length)
+__device__ __forceinline__ uint32_t fast_str(uint32_t &p, bool &ok) {
   const uint64_t x = ld8(p);
-  const uint32_t nb = vlen(x);
-  const uint32_t q = p + nb + vval16(x, nb);
-  return q < PLIM ? q : PLIM;
+  const uint32_t n = (uint32_t)x & 0xffu, nn = n < 7 ? n : 7;
+  const uint64_t body = (x >> 8) & ((1ull << (8 * nn)) - 1);
+  ok &= (n <= 7) & ((body & 0x8080808080808080ull) == 0);
+  p += 1 + nn;
+  return nn;
 }
-// One V1 Item (fields: UpdateDecoder.js:127-243, content refs: Item.js:665-683) skipped; kinds the fast path
-// does not take (GC, Skip, JSON, Doc, object / array / bigint / bytes `any` values, bad refs) set bad.
-__device__ __forceinline__ uint32_t skel_item(uint32_t p, uint32_t &bad) {
-  const uint32_t info = sm[p];
-  p++;
-  if (info & 0x80) p = skip_vu2(p);
-  if (info & 0x40) p = skip_vu2(p);
-  if ((info & 0xC0) == 0) {
-    p = sm[p] == 1 ? skip_str(p + 1) : skip_vu2(p + 1);  // parentInfo: ykey string / parent ID
-    if (info & 0x20) p = skip_str(p);                    // parentSub
-  }
-  switch (info & 31) {
-    case 1: p = skip_vu(p); break;                                        // ContentDeleted
-    case 3: case 4: case 5: p = skip_str(p); break;                       // Binary, String, Embed
-    case 6: p = skip_str(skip_str(p)); break;                             // Format: key, JSON value
-    case 7: {                                                             // Type: typeRef [, key]
-      const uint32_t t = sm[p];
-      p = t == 3 || t == 5 ? skip_str(p + 1) : p + 1;
-      break;
-    }
-    case 8: {                                                             // Any: count, scalar values
-      const uint64_t x = ld8(p);
-      const uint32_t nb = vlen(x), n = vval16(x, nb);
-      p += nb;
-      for (uint32_t i = 0; i < n && p < PLIM; i++) {
-        const uint32_t tag = sm[p++];
-        if (tag == 125) p = skip_vu(p);
-        else if (tag == 124) p += 4;
-        else if (tag == 123) p += 8;
-        else if (tag == 119) p = skip_str(p);
-        else if (tag < 120) { bad = 1; break; }
-      }
-      break;
-    }
-    default: bad = 1; break;
-  }
-  return p < PLIM ? p : PLIM;
+// JSON text of a format / embed: "true", "null" or "false"
+__device__ __forceinline__ void fast_json(uint32_t &p, bool &ok) {
+  const uint64_t x = ld8(p);
+  const uint32_t n = (uint32_t)x & 0xffu;
+  const uint32_t w4 = (uint32_t)(x >> 8);
+  const uint64_t w5 = (x >> 8) & 0xffffffffffull;
+  ok &= ((n == 4) & ((w4 == 0x65757274u) | (w4 == 0x6c6c756eu))) | ((n == 5) & (w5 == 0x65736c6166ull));
+  p += 1 + (n < 5 ? n : 5);
 }
-// Update u's struct section: section headers read (and checked) here, one record per client section
-// (slots for all of the update's sections at once: misc[0]; struct slots per section: misc[2]), each
-// struct's byte range recorded for W1b.  Records where the delete set starts.  Returns false to decline.
-__device__ __forceinline__ bool walk_skeleton(uint32_t u) {
+// one `any` value: undefined / null / booleans, a varInt (canonical, int32 range), a short ASCII string
+__device__ __forceinline__ void fast_any(uint32_t &p, bool &ok) {
+  const uint64_t x = ld8(p);
+  const uint32_t tag = (uint32_t)x & 0xffu;
+  const uint32_t lit = (tag == 127) | (tag == 126) | (tag == 121) | (tag == 120);
+  // varInt: sign in bit 6 of the first byte, 6 + 7k value bits, minimal, magnitude <= 2^31 - 1 when positive
+  const uint64_t v = x >> 8;
+  const uint64_t st = ~v & 0x8080808080808080ull;
+  const uint32_t i = ctz64(st) >> 3, ni = i < 4 ? i : 4;  // last byte index (<= 4: 34 bits)
+  const uint32_t lo = (uint32_t)v;
+  const uint64_t mag = (uint64_t)(lo & 0x3fu) | ((uint64_t)((lo >> 8) & 0x7fu) << 6) | ((uint64_t)((lo >> 16) & 0x7fu) << 13) |
+                       ((uint64_t)((lo >> 24) & 0x7fu) << 20) | ((uint64_t)((uint32_t)(v >> 32) & 0x7fu) << 27);
+  const uint64_t magm = mag & ((1ull << (6 + 7 * ni)) - 1);
+  const uint32_t lastb = (uint32_t)(v >> (8 * ni)) & 0xffu;
+  const bool neg = (lo & 0x40u) != 0;
+  const bool vint = (tag == 125) & (i <= 4) & !((ni > 0) & (lastb == 0)) & (neg | (magm <= 2147483647ull)) &
+                    (magm <= 0xffffffffull);
+  uint32_t q = p + 1;
+  const bool str = tag == 119;
+  bool sok = true;
+  fast_str(q, sok);
+  ok &= lit | vint | (str & sok);
+  p = str ? q : p + 1 + (tag == 125 ? ni + 1 : 0);
+}
+// value of the canonical varuint at the start of window w, nb bytes (1..5)
+__device__ __forceinline__ uint32_t vu_value(uint64_t w, uint32_t nb) {
+  const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
+  const uint32_t v = (lo & 0x7fu) | ((lo >> 1) & 0x3f80u) | ((lo >> 2) & 0x1fc000u) | ((lo >> 3) & 0xfe00000u) | (hi << 28);
+  return nb >= 5 ? v : v & ((1u << (7 * nb)) - 1);
+}
+// two varuints (lib0 readVarUint: canonical, < 2^32) read from one 8-byte window at c.p; when they do
+// not both end inside it, two rvu calls
+__device__ __forceinline__ void rvu2(Cur &c, uint32_t &a, uint32_t &b) {
+  const uint64_t x = ld8(c.p);
+  const uint64_t st = ~x & 0x8080808080808080ull, st2 = st & (st - 1);
+  if (__builtin_expect(st2 == 0, 0)) {
+    a = rvu(c);
+    b = rvu(c);
+    return;
+  }
+  const uint32_t i1 = ctz64(st) >> 3, i2 = ctz64(st2) >> 3;
+  const uint32_t b1 = (uint32_t)(x >> (8 * i1)) & 0xffu, b2 = (uint32_t)(x >> (8 * i2)) & 0xffu;
+  const uint32_t n1 = i1 + 1, n2 = i2 - i1;
+  c.bad |= (n1 > 5) | (n2 > 5) | (c.p + i2 + 1 > c.e) | ((n1 > 1) & (b1 == 0)) | ((n2 > 1) & (b2 == 0)) |
+           ((n1 == 5) & ((b1 & 0x70u) != 0)) | ((n2 == 5) & ((b2 & 0x70u) != 0));
+  a = vu_value(x, n1 < 5 ? n1 : 5);
+  b = vu_value(x >> (8 * n1), n2 < 5 ? n2 : 5);
+  c.p += i2 + 1;
+}
+// the Item after its info byte at c.p; false: not a short-cut shape (c untouched)
+__device__ __forceinline__ bool item_fast(Cur &c, uint32_t info, uint32_t &len) {
+  uint32_t p = c.p;
+  bool ok = true;
+  const uint32_t kind = info & 31;
+  if (info & 0x80) fast_id(p, ok);
+  if (info & 0x40) fast_id(p, ok);
+  if ((info & 0xC0) == 0) {  // parentInfo 1: the root type's key, then the parentSub
+    ok &= sm[p] == 1;
+    p++;
+    fast_str(p, ok);
+    if (info & 0x20) fast_str(p, ok);
+  }
+  len = 1;
+  if (kind == 4) {
+    len = fast_str(p, ok);
+    ok &= len != 0;
+  } else if (kind == 6) {
+    fast_str(p, ok);
+    fast_json(p, ok);
+  } else if (kind == 8) {
+    ok &= sm[p] == 1;  // one value
+    p++;
+    fast_any(p, ok);
+  } else {
+    ok = false;
+  }
+  ok &= p <= c.e;
+  if (ok) c.p = p;
+  return ok;
+}
+
+// Walks the struct section of update u and appends one record per client section (slot from an LDS
+// atomic counter, misc[0]); records where its delete set starts.  Item info bytes with an origin and
+// the parentSub bit get the bit cleared in place (13.5.16's lazy reader reads parentSub only without
+// origins and writes the info byte back without it, E8), so sections copy verbatim afterwards.
+// Returns false to decline.
+__device__ __forceinline__ bool walk_sections(uint32_t u) {
   Cur c = {at<uint16_t>(L_UOFF + 2 * u), at<uint16_t>(L_UOFF + 2 * u + 2), false};
   const uint32_t nclients = rvu(c);
-  uint32_t bad = c.bad | (nclients > SEC);
-  const uint32_t s0 = bad ? 0 : atomicAdd(&at<uint32_t>(L_MISC), nclients);
-  bad |= s0 + nclients > SEC;
-  for (uint32_t ci = 0; ci < nclients && !bad; ci++) {
-    const uint32_t nstructs = rvu(c);
-    const uint32_t client = rvu(c);
+  uint64_t next_min = 0;  // sections of one update in merge order: each key > the previous one's last unit
+  for (uint32_t ci = 0; ci < nclients && !c.bad; ci++) {
+    uint32_t nstructs, client;
+    rvu2(c, nstructs, client);
     const uint32_t clock = rvu(c);
-    bad |= c.bad | (nstructs == 0) | (nstructs > MAXS);
-    if (bad) break;
-    const uint32_t t0 = atomicAdd(&at<uint32_t>(L_MISC + 8), nstructs);
-    bad |= t0 + nstructs > MAXS;
-    if (bad) break;
-    const uint32_t q = s0 + ci;
-    at<uint64_t>(L_SKEY + 8 * q) = ((uint64_t)(~client) << 32) | clock;
-    at<uint16_t>(L_SNS + 2 * q) = (uint16_t)(nstructs | (ci == 0 ? 0x8000u : 0u));  // first section of its update
-    at<uint16_t>(L_SB + 2 * q) = (uint16_t)c.p;
-    at<uint16_t>(L_SE + 2 * q) = (uint16_t)t0;  // first struct slot (the section end once lengths are known)
-    uint32_t p = c.p;
-    for (uint32_t si = 0; si < nstructs; si++) {
-      at<uint16_t>(L_TOFF + 2 * (t0 + si)) = (uint16_t)p;
-      p = skel_item(p, bad);
-      at<uint16_t>(L_TEND + 2 * (t0 + si)) = (uint16_t)p;
-      if (bad | (p > c.e)) break;
+    const uint32_t b = c.p;
+    uint64_t len = 0;
+    for (uint32_t si = 0; si < nstructs && !c.bad; si++) {
+      // declines set c.bad (one exit edge per loop instead of one per check)
+      const uint32_t s0 = c.p;
+      const uint32_t info = rdb(c);
+      c.bad |= info == 10 || (info & 31) == 0;  // Skip / GC -> general path
+      uint32_t l = 1;
+      if (!c.bad && !item_fast(c, info, l)) c.bad |= !item_body(c, info, l);
+      if ((info & 0xC0) != 0 && (info & 0x20) != 0) sm[s0] = (uint8_t)(info & ~0x20u);
+      len += l;
     }
-    bad |= p > c.e;
-    c.p = p;
+    const uint64_t key = ((uint64_t)(~client) << 32) | clock;
+    c.bad |= (nstructs == 0) | ((uint64_t)clock + len > 0xffffffffull) | (key < next_min);
+    next_min = key + len;
+    if (!c.bad) {
+      const uint32_t q = atomicAdd(&at<uint32_t>(L_MISC), 1u);
+      c.bad |= q >= SEC;
+      if (q < SEC) {
+        at<uint64_t>(L_SKEY + 8 * q) = key;
+        at<uint32_t>(L_SLEN + 4 * q) = (uint32_t)len;
+        at<uint16_t>(L_SNS + 2 * q) = (uint16_t)nstructs;
+        at<uint16_t>(L_SB + 2 * q) = (uint16_t)b;
+        at<uint16_t>(L_SE + 2 * q) = (uint16_t)c.p;
+      }
+    }
   }
   at<uint16_t>(L_UDS + 2 * u) = (uint16_t)c.p;
-  return !bad;
-}
-// W1b: struct t re-read with every check (item_body: canonical varints, strict UTF-8, JSON literals,
-// canonical `any` scalars), its clock length recorded; it must end exactly where the skeleton says.  Items
-// with an origin lose the parentSub bit in place (13.5.16's lazy reader reads parentSub only without
-// origins and writes the info byte back without it, E8), so sections copy verbatim afterwards.
-__device__ __forceinline__ bool check_struct(uint32_t t) {
-  const uint32_t s0 = at<uint16_t>(L_TOFF + 2 * t);
-  Cur c = {s0, at<uint16_t>(L_TEND + 2 * t), false};
-  const uint32_t info = rdb(c);
-  c.bad |= info == 10 || (info & 31) == 0;
-  uint32_t l = 1;
-  if (!c.bad) c.bad |= !item_body(c, info, l);
-  c.bad |= c.p != c.e;
-  if ((info & 0xC0) != 0 && (info & 0x20) != 0) sm[s0] = (uint8_t)(info & ~0x20u);
-  at<uint32_t>(L_TLEN + 4 * t) = l;
   return !c.bad;
 }
 // Walks the delete set of update u (DeleteSet.js:219-256) and appends its ranges (slots from misc[1]);
@@ -229,8 +264,8 @@ __device__ __forceinline__ bool walk_ds(uint32_t u) {
   const uint32_t ndc = rvu(c);
   uint32_t pos = 0;
   for (uint32_t i = 0; i < ndc && !c.bad; i++) {
-    const uint32_t client = rvu(c);
-    const uint32_t m = rvu(c);
+    uint32_t client, m;
+    rvu2(c, client, m);
     uint64_t cur = 0;
     for (uint32_t q = 0; q < m && !c.bad; q++, pos++) {
       uint32_t clock, len;
@@ -242,8 +277,7 @@ __device__ __forceinline__ bool walk_ds(uint32_t u) {
         clock = (uint32_t)c64;
         len = (uint32_t)l64;
       } else {
-        clock = rvu(c);
-        len = rvu(c);
+        rvu2(c, clock, len);
       }
       c.bad |= (pos > 255) | (clock >= (1u << 25));
       if (!c.bad) {
@@ -276,6 +310,152 @@ __device__ __forceinline__ bool walk_ds(uint32_t u) {
     __syncthreads();                                                    \
     continue;                                                           \
   }
+
+// ---- 3/4. client sections of document d: rank sort, layout, struct section written (EE per lane) -------
+enum : int { SP_DONE = 0, SP_DECLINE = 1, SP_STOP = 2, SP_CAP = 3 };
+template <uint32_t EE, int STOP>
+__device__ __forceinline__ int sec_phase(const GeneralJob &j, uint32_t d, uint32_t nsec, uint64_t slot, uint64_t slot_al,
+                                         uint64_t slot_end, uint64_t bytes, Slot dst, uint32_t &hdr, uint32_t &struct_bytes) {
+  const uint32_t lane = threadIdx.x;
+  bool bad = false;
+    // ---- 3. section rank sort
+    uint64_t rk[EE];
+    uint32_t rl[EE], rns[EE], rb[EE], re[EE], rr[EE];
+#pragma unroll
+    for (uint32_t s = 0; s < EE; s++) {
+      const uint32_t i = lane + 64 * s;
+      const bool v = i < nsec;
+      rk[s] = v ? at<uint64_t>(L_SKEY + 8 * i) : ~0ull;
+      rl[s] = v ? at<uint32_t>(L_SLEN + 4 * i) : 0;
+      rns[s] = v ? at<uint16_t>(L_SNS + 2 * i) : 0;
+      rb[s] = v ? at<uint16_t>(L_SB + 2 * i) : 0;
+      re[s] = v ? at<uint16_t>(L_SE + 2 * i) : 0;
+    }
+    rank_le(L_SKEY, nsec, rk, rr);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t s = 0; s < EE; s++) {
+      const uint32_t i = lane + 64 * s;
+      if (i < nsec) {
+        const uint32_t r = rr[s];
+        at<uint64_t>(L_SKEY + 8 * r) = rk[s];
+        at<uint32_t>(L_SLEN + 4 * r) = rl[s];
+        at<uint16_t>(L_SNS + 2 * r) = (uint16_t)rns[s];
+        at<uint16_t>(L_SB + 2 * r) = (uint16_t)rb[s];
+        at<uint16_t>(L_SE + 2 * r) = (uint16_t)re[s];
+        at<uint8_t>(L_SSLOT + r) = (uint8_t)i;
+      }
+    }
+    __syncthreads();
+    {
+      bool dup = false;
+#pragma unroll
+      for (uint32_t s = 0; s < EE; s++) {
+        const uint32_t i = lane + 64 * s;
+        if (i < nsec) dup |= at<uint8_t>(L_SSLOT + rr[s]) != i;
+      }
+      if (__any(dup)) return SP_DECLINE;  // equal (client, clock): overlapping inputs
+    }
+    if (STOP == 3) return SP_STOP;
+    // ---- 4. layout over rank order; lane owns positions r = E*lane + s
+    uint64_t sk[EE];
+    uint32_t sl[EE], sns[EE], sb[EE], se[EE], units[EE], pstart[EE], plastf[EE], gapv[EE];
+    {
+      const uint32_t r0 = EE * lane;
+      uint64_t kp = r0 > 0 && r0 - 1 < nsec ? at<uint64_t>(L_SKEY + 8 * (r0 - 1)) : ~0ull;
+      uint32_t lp = r0 > 0 && r0 - 1 < nsec ? at<uint32_t>(L_SLEN + 4 * (r0 - 1)) : 0;
+#pragma unroll
+      for (uint32_t s = 0; s < EE; s++) {
+        const uint32_t r = r0 + s;
+        const bool v = r < nsec;
+        sk[s] = v ? at<uint64_t>(L_SKEY + 8 * r) : ~0ull;
+        sl[s] = v ? at<uint32_t>(L_SLEN + 4 * r) : 0;
+        sns[s] = v ? at<uint16_t>(L_SNS + 2 * r) : 0;
+        sb[s] = v ? at<uint16_t>(L_SB + 2 * r) : 0;
+        se[s] = v ? at<uint16_t>(L_SE + 2 * r) : 0;
+        const uint64_t kn = r + 1 < nsec ? at<uint64_t>(L_SKEY + 8 * (r + 1)) : ~0ull;
+        const bool same = v && r > 0 && (kp >> 32) == (sk[s] >> 32);
+        const uint64_t pend = (kp & 0xffffffffull) + lp;
+        const uint64_t cl = sk[s] & 0xffffffffull;
+        bad |= same && pend > cl;  // overlapping inputs: general path
+        gapv[s] = same && pend < cl ? (uint32_t)(cl - pend) : 0;
+        units[s] = v ? sns[s] + (gapv[s] != 0) : 0;
+        pstart[s] = v && !same;
+        plastf[s] = v && (r + 1 >= nsec || (kn >> 32) != (sk[s] >> 32));
+        kp = sk[s];
+        lp = sl[s];
+      }
+    }
+    if (__any(bad)) return SP_DECLINE;
+    // one scan for (parts << 16 | units)
+    uint32_t pu[EE], pu_lane = 0, nparts;
+#pragma unroll
+    for (uint32_t s = 0; s < EE; s++) pu_lane += (pstart[s] << 16) | units[s];
+    {
+      const uint32_t incl = wave_incl_add(pu_lane);
+      nparts = lane_read(incl, 63) >> 16;
+      uint32_t run = incl - pu_lane;
+#pragma unroll
+      for (uint32_t s = 0; s < EE; s++) {
+        pu[s] = run;  // exclusive (parts, units) before position r
+        run += (pstart[s] << 16) | units[s];
+        const uint32_t pid = (run >> 16) - 1;
+        if (pstart[s]) at<uint16_t>(L_PFIRST + 2 * pid) = (uint16_t)(pu[s] & 0xffff);
+        if (plastf[s]) at<uint16_t>(L_PLAST + 2 * pid) = (uint16_t)(run & 0xffff);
+      }
+    }
+    __syncthreads();
+    uint32_t runu[EE], soff[EE], sbytes_lane = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < EE; s++) {
+      runu[s] = 0;
+      uint32_t b = se[s] - sb[s];
+      if (pstart[s]) {
+        const uint32_t pid = pu[s] >> 16;
+        runu[s] = at<uint16_t>(L_PLAST + 2 * pid) - at<uint16_t>(L_PFIRST + 2 * pid);
+        b += vsz(runu[s]) + vsz(~(uint32_t)(sk[s] >> 32)) + vsz((uint32_t)sk[s]);
+      }
+      if (gapv[s]) b += 1 + vsz(gapv[s]);
+      soff[s] = b;
+      sbytes_lane += b;
+    }
+    {
+      const uint32_t incl = wave_incl_add(sbytes_lane);
+      struct_bytes = lane_read(incl, 63);
+      uint32_t run = incl - sbytes_lane;
+#pragma unroll
+      for (uint32_t s = 0; s < EE; s++) { const uint32_t b = soff[s]; soff[s] = run; run += b; }
+    }
+    hdr = vsz(nparts);
+    if (slot_al + hdr + struct_bytes > slot_end) {
+      if (slot_al + hdr + struct_bytes > slot + 2 * bytes + 64) return SP_DECLINE;
+      if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }  // caller's arena too small
+      return SP_CAP;
+    }
+    if (STOP == 4) return SP_STOP;
+    // ---- 4b. write the struct section: per section its part header, its Skip, then its bytes verbatim
+    if (lane == 0) put_vu(dst, 0, nparts);
+#pragma unroll
+    for (uint32_t s = 0; s < EE; s++) {
+      if (EE * lane + s >= nsec) break;
+      uint32_t p = hdr + soff[s];
+      if (pstart[s]) {  // part header: vu(#structs incl. skips) vu(client) vu(clock)
+        p = put_vu(dst, p, runu[s]);
+        p = put_vu(dst, p, ~(uint32_t)(sk[s] >> 32));
+        p = put_vu(dst, p, sk[s] & 0xffffffffull);
+      }
+      if (gapv[s]) {  // Skip: info 10 + varuint length (13.5.16 ui.write)
+        ob8(dst, p++, 10);
+        p = put_vu(dst, p, gapv[s]);
+      }
+      const uint32_t n = se[s] - sb[s], src = sb[s];
+      uint32_t o = 0;
+      for (; o + 8 <= n; o += 8) put_u64(dst, p + o, ld8(src + o));
+      if (o + 4 <= n) { ob32(dst, p + o, ld4(src + o)); o += 4; }
+      for (; o < n; o++) ob8(dst, p + o, sm[src + o]);
+    }
+  return SP_DONE;
+}
 
 // ---- 5/6. delete set of document d (EE delete ranges per lane: 1 when they fit one wave) --------------
 enum : int { DS_DONE = 0, DS_DECLINE = 1, DS_STOP = 2 };
@@ -529,7 +709,7 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
       for (uint32_t v = lane; v < nvec; v += 64) at<uint4>(L_IN + 16 * v) = src[v];
     }
     for (uint32_t i = lane; i <= k; i += 64) at<uint16_t>(L_UOFF + 2 * i) = (uint16_t)(uoff_g(j, u0 + i) - b0 + base);
-    if (lane < 3) at<uint32_t>(L_MISC + 4 * lane) = 0;
+    if (lane < 2) at<uint32_t>(L_MISC + 4 * lane) = 0;
     if (lane < 16) at<uint32_t>(L_HIST + 4 * lane) = 0;
     __syncthreads();
     YM_STOP(1)
@@ -569,43 +749,8 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
       __syncthreads();
       bool ok = true;
 #pragma unroll 1
-      for (uint32_t i = lane; i < n1; i += 64) ok &= walk_skeleton(at<uint8_t>(L_UORD + i));
+      for (uint32_t i = lane; i < n1; i += 64) ok &= walk_sections(at<uint8_t>(L_UORD + i));
       if (__any(!ok)) YM_DECLINE()
-      __syncthreads();
-      // W1b: one lane per struct
-      const uint32_t nst = at<uint32_t>(L_MISC + 8), nsec0 = at<uint32_t>(L_MISC);
-#pragma unroll 1
-      for (uint32_t t = lane; t < nst; t += 64) ok &= check_struct(t);
-      if (__any(!ok)) YM_DECLINE()
-      __syncthreads();
-      // section lengths (sum of their structs'), ends, and the merge-order check inside each update
-      {
-        uint32_t first[E];
-        bool sbad = false;
-#pragma unroll
-        for (uint32_t s = 0; s < E; s++) {
-          const uint32_t q = lane + 64 * s;
-          first[s] = 1;
-          if (q < nsec0) {
-            const uint32_t w = at<uint16_t>(L_SNS + 2 * q), ns = w & 0x7fffu, t0 = at<uint16_t>(L_SE + 2 * q);
-            uint64_t len = 0;
-            for (uint32_t t = t0; t < t0 + ns; t++) len += at<uint32_t>(L_TLEN + 4 * t);
-            first[s] = w >> 15;
-            sbad |= (at<uint64_t>(L_SKEY + 8 * q) & 0xffffffffull) + len > 0xffffffffull;
-            at<uint32_t>(L_SLEN + 4 * q) = (uint32_t)len;
-            at<uint16_t>(L_SE + 2 * q) = at<uint16_t>(L_TEND + 2 * (t0 + ns - 1));
-            at<uint16_t>(L_SNS + 2 * q) = (uint16_t)ns;
-          }
-        }
-        __syncthreads();
-#pragma unroll
-        for (uint32_t s = 0; s < E; s++) {
-          const uint32_t q = lane + 64 * s;
-          if (q < nsec0 && !first[s])  // sections of one update in merge order: above the previous one's last unit
-            sbad |= at<uint64_t>(L_SKEY + 8 * q) < at<uint64_t>(L_SKEY + 8 * (q - 1)) + at<uint32_t>(L_SLEN + 4 * (q - 1));
-        }
-        if (__any(sbad)) YM_DECLINE()
-      }
       __syncthreads();
       YM_STOP(8)
       // W2 list: updates whose delete set has clients (first byte != 0), compacted by ballots
@@ -643,145 +788,15 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
     if (slot_al >= slot_end) YM_DECLINE()
     const Slot dst = make_slot(j.out + slot_al, (uint32_t)(slot_end - slot_al));
     uint32_t hdr = 0, struct_bytes = 0;
-    bool bad = false;
     if constexpr (!DSONLY) {
-    // ---- 3. section rank sort
-    uint64_t rk[E];
-    uint32_t rl[E], rns[E], rb[E], re[E], rr[E];
-#pragma unroll
-    for (uint32_t s = 0; s < E; s++) {
-      const uint32_t i = lane + 64 * s;
-      const bool v = i < nsec;
-      rk[s] = v ? at<uint64_t>(L_SKEY + 8 * i) : ~0ull;
-      rl[s] = v ? at<uint32_t>(L_SLEN + 4 * i) : 0;
-      rns[s] = v ? at<uint16_t>(L_SNS + 2 * i) : 0;
-      rb[s] = v ? at<uint16_t>(L_SB + 2 * i) : 0;
-      re[s] = v ? at<uint16_t>(L_SE + 2 * i) : 0;
-    }
-    rank_le(L_SKEY, nsec, rk, rr);
-    __syncthreads();
-#pragma unroll
-    for (uint32_t s = 0; s < E; s++) {
-      const uint32_t i = lane + 64 * s;
-      if (i < nsec) {
-        const uint32_t r = rr[s];
-        at<uint64_t>(L_SKEY + 8 * r) = rk[s];
-        at<uint32_t>(L_SLEN + 4 * r) = rl[s];
-        at<uint16_t>(L_SNS + 2 * r) = (uint16_t)rns[s];
-        at<uint16_t>(L_SB + 2 * r) = (uint16_t)rb[s];
-        at<uint16_t>(L_SE + 2 * r) = (uint16_t)re[s];
-        at<uint8_t>(L_SSLOT + r) = (uint8_t)i;
+      const int r = nsec <= 64 ? sec_phase<1, STOP>(j, d, nsec, slot, slot_al, slot_end, bytes, dst, hdr, struct_bytes)
+                               : sec_phase<2, STOP>(j, d, nsec, slot, slot_al, slot_end, bytes, dst, hdr, struct_bytes);
+      if (r == SP_DECLINE) YM_DECLINE()
+      if (r == SP_STOP && lane == 0) { j.status[d] = ym::ST_OK; j.out_len[d] = 0; }
+      if (r != SP_DONE) {
+        __syncthreads();
+        continue;
       }
-    }
-    __syncthreads();
-    {
-      bool dup = false;
-#pragma unroll
-      for (uint32_t s = 0; s < E; s++) {
-        const uint32_t i = lane + 64 * s;
-        if (i < nsec) dup |= at<uint8_t>(L_SSLOT + rr[s]) != i;
-      }
-      if (__any(dup)) YM_DECLINE()  // equal (client, clock): overlapping inputs
-    }
-    YM_STOP(3)
-    // ---- 4. layout over rank order; lane owns positions r = E*lane + s
-    uint64_t sk[E];
-    uint32_t sl[E], sns[E], sb[E], se[E], units[E], pstart[E], plastf[E], gapv[E];
-    {
-      const uint32_t r0 = E * lane;
-      uint64_t kp = r0 > 0 && r0 - 1 < nsec ? at<uint64_t>(L_SKEY + 8 * (r0 - 1)) : ~0ull;
-      uint32_t lp = r0 > 0 && r0 - 1 < nsec ? at<uint32_t>(L_SLEN + 4 * (r0 - 1)) : 0;
-#pragma unroll
-      for (uint32_t s = 0; s < E; s++) {
-        const uint32_t r = r0 + s;
-        const bool v = r < nsec;
-        sk[s] = v ? at<uint64_t>(L_SKEY + 8 * r) : ~0ull;
-        sl[s] = v ? at<uint32_t>(L_SLEN + 4 * r) : 0;
-        sns[s] = v ? at<uint16_t>(L_SNS + 2 * r) : 0;
-        sb[s] = v ? at<uint16_t>(L_SB + 2 * r) : 0;
-        se[s] = v ? at<uint16_t>(L_SE + 2 * r) : 0;
-        const uint64_t kn = r + 1 < nsec ? at<uint64_t>(L_SKEY + 8 * (r + 1)) : ~0ull;
-        const bool same = v && r > 0 && (kp >> 32) == (sk[s] >> 32);
-        const uint64_t pend = (kp & 0xffffffffull) + lp;
-        const uint64_t cl = sk[s] & 0xffffffffull;
-        bad |= same && pend > cl;  // overlapping inputs: general path
-        gapv[s] = same && pend < cl ? (uint32_t)(cl - pend) : 0;
-        units[s] = v ? sns[s] + (gapv[s] != 0) : 0;
-        pstart[s] = v && !same;
-        plastf[s] = v && (r + 1 >= nsec || (kn >> 32) != (sk[s] >> 32));
-        kp = sk[s];
-        lp = sl[s];
-      }
-    }
-    if (__any(bad)) YM_DECLINE()
-    // one scan for (parts << 16 | units)
-    uint32_t pu[E], pu_lane = 0, nparts;
-#pragma unroll
-    for (uint32_t s = 0; s < E; s++) pu_lane += (pstart[s] << 16) | units[s];
-    {
-      const uint32_t incl = wave_incl_add(pu_lane);
-      nparts = lane_read(incl, 63) >> 16;
-      uint32_t run = incl - pu_lane;
-#pragma unroll
-      for (uint32_t s = 0; s < E; s++) {
-        pu[s] = run;  // exclusive (parts, units) before position r
-        run += (pstart[s] << 16) | units[s];
-        const uint32_t pid = (run >> 16) - 1;
-        if (pstart[s]) at<uint16_t>(L_PFIRST + 2 * pid) = (uint16_t)(pu[s] & 0xffff);
-        if (plastf[s]) at<uint16_t>(L_PLAST + 2 * pid) = (uint16_t)(run & 0xffff);
-      }
-    }
-    __syncthreads();
-    uint32_t runu[E], soff[E], sbytes_lane = 0;
-#pragma unroll
-    for (uint32_t s = 0; s < E; s++) {
-      runu[s] = 0;
-      uint32_t b = se[s] - sb[s];
-      if (pstart[s]) {
-        const uint32_t pid = pu[s] >> 16;
-        runu[s] = at<uint16_t>(L_PLAST + 2 * pid) - at<uint16_t>(L_PFIRST + 2 * pid);
-        b += vsz(runu[s]) + vsz(~(uint32_t)(sk[s] >> 32)) + vsz((uint32_t)sk[s]);
-      }
-      if (gapv[s]) b += 1 + vsz(gapv[s]);
-      soff[s] = b;
-      sbytes_lane += b;
-    }
-    {
-      const uint32_t incl = wave_incl_add(sbytes_lane);
-      struct_bytes = lane_read(incl, 63);
-      uint32_t run = incl - sbytes_lane;
-#pragma unroll
-      for (uint32_t s = 0; s < E; s++) { const uint32_t b = soff[s]; soff[s] = run; run += b; }
-    }
-    hdr = vsz(nparts);
-    if (slot_al + hdr + struct_bytes > slot_end) {
-      if (slot_al + hdr + struct_bytes > slot + 2 * bytes + 64) YM_DECLINE()
-      if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }  // caller's arena too small
-      __syncthreads();
-      continue;
-    }
-    YM_STOP(4)
-    // ---- 4b. write the struct section: per section its part header, its Skip, then its bytes verbatim
-    if (lane == 0) put_vu(dst, 0, nparts);
-#pragma unroll
-    for (uint32_t s = 0; s < E; s++) {
-      if (E * lane + s >= nsec) break;
-      uint32_t p = hdr + soff[s];
-      if (pstart[s]) {  // part header: vu(#structs incl. skips) vu(client) vu(clock)
-        p = put_vu(dst, p, runu[s]);
-        p = put_vu(dst, p, ~(uint32_t)(sk[s] >> 32));
-        p = put_vu(dst, p, sk[s] & 0xffffffffull);
-      }
-      if (gapv[s]) {  // Skip: info 10 + varuint length (13.5.16 ui.write)
-        ob8(dst, p++, 10);
-        p = put_vu(dst, p, gapv[s]);
-      }
-      const uint32_t n = se[s] - sb[s], src = sb[s];
-      uint32_t o = 0;
-      for (; o + 8 <= n; o += 8) put_u64(dst, p + o, ld8(src + o));
-      if (o + 4 <= n) { ob32(dst, p + o, ld4(src + o)); o += 4; }
-      for (; o < n; o++) ob8(dst, p + o, sm[src + o]);
-    }
     }  // !DSONLY
     YM_STOP(7)
     {
