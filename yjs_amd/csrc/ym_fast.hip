@@ -160,25 +160,6 @@ __device__ __forceinline__ uint32_t vu_value(uint64_t w, uint32_t nb) {
   const uint32_t v = (lo & 0x7fu) | ((lo >> 1) & 0x3f80u) | ((lo >> 2) & 0x1fc000u) | ((lo >> 3) & 0xfe00000u) | (hi << 28);
   return nb >= 5 ? v : v & ((1u << (7 * nb)) - 1);
 }
-// two varuints (lib0 readVarUint: canonical, < 2^32) read from one 8-byte window at c.p; when they do
-// not both end inside it, two rvu calls
-__device__ __forceinline__ void rvu2(Cur &c, uint32_t &a, uint32_t &b) {
-  const uint64_t x = ld8(c.p);
-  const uint64_t st = ~x & 0x8080808080808080ull, st2 = st & (st - 1);
-  if (__builtin_expect(st2 == 0, 0)) {
-    a = rvu(c);
-    b = rvu(c);
-    return;
-  }
-  const uint32_t i1 = ctz64(st) >> 3, i2 = ctz64(st2) >> 3;
-  const uint32_t b1 = (uint32_t)(x >> (8 * i1)) & 0xffu, b2 = (uint32_t)(x >> (8 * i2)) & 0xffu;
-  const uint32_t n1 = i1 + 1, n2 = i2 - i1;
-  c.bad |= (n1 > 5) | (n2 > 5) | (c.p + i2 + 1 > c.e) | ((n1 > 1) & (b1 == 0)) | ((n2 > 1) & (b2 == 0)) |
-           ((n1 == 5) & ((b1 & 0x70u) != 0)) | ((n2 == 5) & ((b2 & 0x70u) != 0));
-  a = vu_value(x, n1 < 5 ? n1 : 5);
-  b = vu_value(x >> (8 * n1), n2 < 5 ? n2 : 5);
-  c.p += i2 + 1;
-}
 // the Item after its info byte at c.p; false: not a short-cut shape (c untouched)
 __device__ __forceinline__ bool item_fast(Cur &c, uint32_t info, uint32_t &len) {
   uint32_t p = c.p;
@@ -221,8 +202,8 @@ __device__ __forceinline__ bool walk_sections(uint32_t u) {
   const uint32_t nclients = rvu(c);
   uint64_t next_min = 0;  // sections of one update in merge order: each key > the previous one's last unit
   for (uint32_t ci = 0; ci < nclients && !c.bad; ci++) {
-    uint32_t nstructs, client;
-    rvu2(c, nstructs, client);
+    const uint32_t nstructs = rvu(c);
+    const uint32_t client = rvu(c);
     const uint32_t clock = rvu(c);
     const uint32_t b = c.p;
     uint64_t len = 0;
@@ -264,8 +245,8 @@ __device__ __forceinline__ bool walk_ds(uint32_t u) {
   const uint32_t ndc = rvu(c);
   uint32_t pos = 0;
   for (uint32_t i = 0; i < ndc && !c.bad; i++) {
-    uint32_t client, m;
-    rvu2(c, client, m);
+    const uint32_t client = rvu(c);
+    const uint32_t m = rvu(c);
     uint64_t cur = 0;
     for (uint32_t q = 0; q < m && !c.bad; q++, pos++) {
       uint32_t clock, len;
@@ -277,7 +258,8 @@ __device__ __forceinline__ bool walk_ds(uint32_t u) {
         clock = (uint32_t)c64;
         len = (uint32_t)l64;
       } else {
-        rvu2(c, clock, len);
+        clock = rvu(c);
+        len = rvu(c);
       }
       c.bad |= (pos > 255) | (clock >= (1u << 25));
       if (!c.bad) {
@@ -331,7 +313,7 @@ __device__ __forceinline__ int sec_phase(const GeneralJob &j, uint32_t d, uint32
       rb[s] = v ? at<uint16_t>(L_SB + 2 * i) : 0;
       re[s] = v ? at<uint16_t>(L_SE + 2 * i) : 0;
     }
-    rank_le(L_SKEY, nsec, rk, rr);
+    rank_le4(L_SKEY, nsec, rk, rr);
     __syncthreads();
 #pragma unroll
     for (uint32_t s = 0; s < EE; s++) {
@@ -476,7 +458,7 @@ __device__ __forceinline__ int ds_phase(const GeneralJob &j, uint32_t d, uint32_
         dl[s] = v ? at<uint32_t>(L_DLEN + 4 * i) : 0;
         dq[s] = v ? at<uint16_t>(L_DSEQ + 2 * i) : 0;
       }
-      rank_le(L_DKEY, nds, dk, dr);  // distinct keys: a permutation
+      rank_le4(L_DKEY, nds, dk, dr);  // distinct keys: a permutation
       __syncthreads();
 #pragma unroll
       for (uint32_t s = 0; s < EE; s++) {
@@ -717,35 +699,60 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
     // that the lanes of one round take updates of similar shape; W2: one lane per update whose delete
     // set is not empty.  Splitting the two keeps every lane of a round busy with the same kind of work.
     {
-      uint32_t ub[UPD / 64], up[UPD / 64];
+      uint32_t ulen[UPD / 64], has[UPD / 64];
       bool empty = false;
 #pragma unroll
       for (uint32_t s = 0; s < UPD / 64; s++) {
         const uint32_t u = lane + 64 * s;
-        ub[s] = 16;
+        has[s] = 0;
+        ulen[s] = 0;
         if (u < k) {
           const uint32_t u0_ = at<uint16_t>(L_UOFF + 2 * u), len = at<uint16_t>(L_UOFF + 2 * u + 2) - u0_;
           empty |= len == 0;
+          ulen[s] = len;
           if (len > 0 && (DSONLY || sm[u0_] == 0)) {
             // no structs: the delete set follows (DSONLY: the input is the delete set)
             at<uint16_t>(L_UDS + 2 * u) = (uint16_t)(DSONLY ? u0_ : u0_ + 1);
           } else {
-            ub[s] = len >> 3 < 15 ? len >> 3 : 15;
-            up[s] = atomicAdd(&at<uint32_t>(L_HIST + 4 * ub[s]), 1u);
+            has[s] = 1;
           }
         }
       }
       if (__any(empty)) YM_DECLINE()
-      __syncthreads();
-      const uint32_t h = lane < 16 ? at<uint32_t>(L_HIST + 4 * lane) : 0;
-      const uint32_t hincl = wave_incl_add(h);
-      const uint32_t n1 = lane_read(hincl, 15);
-      __syncthreads();
-      if (lane < 16) at<uint32_t>(L_HIST + 4 * lane) = hincl - h;
-      __syncthreads();
+      uint32_t n1 = 0;
 #pragma unroll
-      for (uint32_t s = 0; s < UPD / 64; s++)
-        if (ub[s] < 16) at<uint8_t>(L_UORD + at<uint32_t>(L_HIST + 4 * ub[s]) + up[s]) = (uint8_t)(lane + 64 * s);
+      for (uint32_t s = 0; s < UPD / 64; s++) n1 += __popcll(__ballot(has[s]));
+      if (n1 <= 64) {
+        // one round: lane i walks the i-th update with structs (ballot compaction)
+        uint32_t base = 0;
+#pragma unroll
+        for (uint32_t s = 0; s < UPD / 64; s++) {
+          const uint64_t m = __ballot(has[s]);
+          if (has[s]) at<uint8_t>(L_UORD + base + __popcll(m & ((1ull << lane) - 1))) = (uint8_t)(lane + 64 * s);
+          base += __popcll(m);
+        }
+      } else {
+        // two rounds: updates ordered by length bucket, so that the lanes of a round take updates of
+        // similar shape (counting sort: bucket histogram, scan, scatter)
+        uint32_t ub[UPD / 64], up[UPD / 64];
+#pragma unroll
+        for (uint32_t s = 0; s < UPD / 64; s++) {
+          ub[s] = 16;
+          if (has[s]) {
+            ub[s] = ulen[s] >> 3 < 15 ? ulen[s] >> 3 : 15;
+            up[s] = atomicAdd(&at<uint32_t>(L_HIST + 4 * ub[s]), 1u);
+          }
+        }
+        __syncthreads();
+        const uint32_t h = lane < 16 ? at<uint32_t>(L_HIST + 4 * lane) : 0;
+        const uint32_t hincl = wave_incl_add(h);
+        __syncthreads();
+        if (lane < 16) at<uint32_t>(L_HIST + 4 * lane) = hincl - h;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t s = 0; s < UPD / 64; s++)
+          if (ub[s] < 16) at<uint8_t>(L_UORD + at<uint32_t>(L_HIST + 4 * ub[s]) + up[s]) = (uint8_t)(lane + 64 * s);
+      }
       __syncthreads();
       bool ok = true;
 #pragma unroll 1
@@ -775,9 +782,9 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
     __syncthreads();
     const uint32_t nsec = at<uint32_t>(L_MISC), nds = at<uint32_t>(L_MISC + 4);
     if ((DSONLY ? nsec != 0 : nsec == 0) || nsec > SEC || nds > DSN) YM_DECLINE()
-    if (lane == 0) {  // pad the key arrays to even length (rank loops read pairs)
-      if (nsec & 1) at<uint64_t>(L_SKEY + 8 * nsec) = ~0ull;
-      if (nds & 1) at<uint64_t>(L_DKEY + 8 * nds) = ~0ull;
+    if (lane < 3) {  // pad the key arrays to a multiple of 4 (rank loops read quads; SEC, DSN are multiples of 4)
+      if (nsec + lane < ((nsec + 3) & ~3u)) at<uint64_t>(L_SKEY + 8 * (nsec + lane)) = ~0ull;
+      if (nds + lane < ((nds + 3) & ~3u)) at<uint64_t>(L_DKEY + 8 * (nds + lane)) = ~0ull;
     }
     __syncthreads();
     YM_STOP(2)

@@ -332,6 +332,23 @@ __device__ __forceinline__ bool item_body(Cur &c, uint32_t info, uint32_t &len) 
 
 // rank of each of the lane's keys among keys[0..n): #keys <= own (own included) - 1.  Keys past n
 // are ~0 (padding) and never count.  Equal keys collide; callers detect that.
+// rank_le4: the same, four keys per iteration (two 16-B broadcast reads): keys[] padded with ~0 up to a
+// multiple of 4
+template <uint32_t E>
+__device__ __forceinline__ void rank_le4(uint32_t keys, uint32_t n, const uint64_t (&k)[E], uint32_t (&rank)[E]) {
+  uint32_t cnt[E];
+#pragma unroll
+  for (uint32_t s = 0; s < E; s++) cnt[s] = 0;
+  for (uint32_t jj = 0; jj < n; jj += 4) {
+    const uint64_t a = at<uint64_t>(keys + 8 * jj), b = at<uint64_t>(keys + 8 * jj + 8);
+    const uint64_t c = at<uint64_t>(keys + 8 * jj + 16), d = at<uint64_t>(keys + 8 * jj + 24);
+#pragma unroll
+    for (uint32_t s = 0; s < E; s++)
+      cnt[s] += (uint32_t)(a <= k[s]) + (uint32_t)(b <= k[s]) + (uint32_t)(c <= k[s]) + (uint32_t)(d <= k[s]);
+  }
+#pragma unroll
+  for (uint32_t s = 0; s < E; s++) rank[s] = cnt[s] - 1;
+}
 template <uint32_t E>
 __device__ __forceinline__ void rank_le(uint32_t keys, uint32_t n, const uint64_t (&k)[E], uint32_t (&rank)[E]) {
   uint32_t cnt[E];
