@@ -96,6 +96,7 @@ typedef struct ym_stats {
   double general_ms; /* ... of the general path (workspace sizing + both passes)           */
   uint64_t docs_large; /* documents merged by the large-document pipeline (ym_large.hip)     */
   double large_ms;   /* ... device time of that pipeline                                   */
+  uint64_t docs_chunked; /* diff / sv documents done by the chunk-parallel walk (ym_pwalk.hip) */
 } ym_stats;
 
 int ym_init(int device);           /* select the HIP device for this thread; 0 on success */

@@ -30,6 +30,21 @@ def _groups():
 
 @pytest.mark.parametrize("key", sorted(_groups().keys()), ids=lambda k: f"{k[0]}-v{k[1]}")
 def test_golden_batched_on_gpu(engine, key):
+    _check_group(engine, key)
+
+
+@pytest.mark.parametrize("key", [("diff", 1), ("sv", 1)], ids=lambda k: f"{k[0]}-v{k[1]}")
+def test_golden_through_chunked_walk(engine, key, monkeypatch):
+    """The chunk-parallel V1 walk (ym_pwalk.hip) normally takes updates of >= 32 KB only; with its
+    threshold at 1 byte every golden diff / state-vector vector goes through it (speculative chunk walk,
+    stitch, fallback to the sequential walker on a decline) and must still come out byte-identical."""
+    monkeypatch.setenv("YMERGE_PW_MIN", "1")
+    _check_group(engine, key)
+    # it accepts exactly what the sequential walker accepts (the rest: non-canonical payloads, errors)
+    assert engine.stats["docs_chunked"] == engine.stats["docs_fast"] > 0, engine.stats
+
+
+def _check_group(engine, key):
     from yjs_amd import pack_docs
     cases = _groups()[key]
     op, fmt = key

@@ -74,6 +74,8 @@ def test_c3_sv_matches_oracle(engine, fmt):
     bad = _compare(engine.run_host("sv", fmt, a2, o2, d2), outs, st)
     assert not bad, bad[:10]
     assert engine.stats["docs_fast"] == engine.stats["docs"], engine.stats
+    if fmt == 1:  # the chunk-parallel walk takes every 0.9 MB C3 update
+        assert engine.stats["docs_chunked"] == engine.stats["docs"], engine.stats
 
 
 @pytest.mark.parametrize("fmt", [1, 2])
@@ -90,6 +92,37 @@ def test_c3_diff_random_svs(engine, fmt):
     bad = _compare(engine.run_host("diff", fmt, a2, o2, d2, sva, svo), outs, st)
     assert not bad, bad[:10]
     assert engine.stats["docs_fast"] == engine.stats["docs"], engine.stats
+    if fmt == 1:
+        assert engine.stats["docs_chunked"] == engine.stats["docs"], engine.stats
+
+
+def test_c3_damaged_updates_chunked_walk(engine):
+    """Truncated and byte-flipped C3 updates through the chunk-parallel walk: wherever the damage lands
+    (struct section, a string, the delete set) the result must be the oracle's -- the same bytes or the
+    same exception -- whether the walk declines the document or not."""
+    arena, upd_off, doc_upd = load_ymb("c3_v1")
+    upd = arena.tobytes()
+    rng = np.random.default_rng(11)
+    docs, svs = [], []
+    svo_full = O.sv_from_update(upd, 1)[1]
+    full_svs = random_state_vectors(svo_full, 24, seed=5)
+    for i in range(24):
+        b = bytearray(upd)
+        if i % 3 == 0:
+            b = b[:int(rng.integers(len(b) // 2, len(b)))]
+        else:
+            for _ in range(1 + i % 4):
+                b[int(rng.integers(8, len(b)))] = int(rng.integers(0, 256))
+        docs.append(bytes(b))
+        svs.append(full_svs[i])
+    from yjs_amd import pack_docs
+    a2, o2, d2 = pack_docs([[u] for u in docs])
+    sva, svo, _ = pack_docs([[s] for s in svs])
+    for op in ("diff", "sv"):
+        extra = (sva, svo) if op == "diff" else ()
+        outs, st, _ = O.batch(op, 1, a2, o2, d2, *extra, nthreads=8)
+        bad = _compare(engine.run_host(op, 1, a2, o2, d2, *extra), outs, st)
+        assert not bad, (op, bad[:10])
 
 
 def _subset(arena, upd_off, doc_upd, docs, keep):

@@ -22,7 +22,7 @@ __global__ void k_general_ws(GeneralJob j, uint64_t *ws_size);
 __global__ void k_general(GeneralJob j, int pass);
 int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st);  // ym_fast.hip
 int fast2_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st); // ym_fast2.hip
-int big_launch(uint32_t op, const GeneralJob &j, hipStream_t st);                    // ym_big.hip
+int big_launch(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &pw);       // ym_big.hip
 int big2_launch(uint32_t op, const GeneralJob &j, hipStream_t st);                   // ym_big2.hip
 __global__ void k_fast_region(GeneralJob j, uint32_t n_upd);                         // ym_fast.hip
 }  // namespace ymk
@@ -61,6 +61,7 @@ struct DevState {
   DBuf in_arena, in_off, in_doc, in_sv, in_svoff, out_arena, out_off, out_len, status;  // host staging
   DBuf cmp_off, cmp_len, cmp_arena;  // host batches: outputs packed in document order before the D2H copy
   LargeBufs large;
+  PwBufs pw;
   hipEvent_t evl1 = nullptr;
   uint64_t *pinned = nullptr;   // host memory the finishing kernel writes into (no copy op)
   uint64_t *pinned_dev = nullptr;  // ... its device address
@@ -208,7 +209,8 @@ __global__ void k_status_flags(const uint32_t *list, uint32_t n, const int32_t *
 // the device counters for the next launch.  Stats: a few blocks, each summing 4,096 documents' status /
 // out_len with 16 independent loads per thread (one HBM round trip), partial sums by atomics, and the
 // block that finishes last writes the host words (a handful of same-address atomics, not one per doc).
-// Counters: [0] used, [2] declined (u32), [8] finished blocks (u32), [9] errors, [10] bytes out.
+// Counters: [0] used, [2] declined (u32), [8] finished blocks (u32), [9] errors, [10] bytes out,
+// [11] documents done by the chunk-parallel walk (reported in host[8]).
 // FIN_THREADS threads per block, 16 documents per thread: one 1,024-thread block up to 16 k documents (no
 // cross-block atomics), 256-thread blocks of 4,096 documents above that
 template <uint32_t FIN_THREADS>
@@ -223,10 +225,11 @@ __global__ void __launch_bounds__(FIN_THREADS) k_finish(const int32_t *status, c
   const uint32_t i0 = blockIdx.x * FIN_DOCS;
   // the host words' inputs (written by earlier kernels, never by k_finish) are loaded first, so their
   // HBM / L2 round trips overlap the stats loads instead of following the reduction one by one
-  uint64_t used = 0, in_lo = 0, in_hi = 0;
+  uint64_t used = 0, in_lo = 0, in_hi = 0, chunked = 0;
   uint32_t declined = 0;
   if (threadIdx.x == 0) {
     used = __hip_atomic_load(&c[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    chunked = __hip_atomic_load(&c[11], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     declined = __hip_atomic_load(reinterpret_cast<uint32_t *>(&c[2]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     in_lo = upd_off32 ? upd_off32[0] : upd_off[0];
     in_hi = upd_off32 ? upd_off32[n_upd] : upd_off[n_upd];
@@ -273,6 +276,8 @@ __global__ void __launch_bounds__(FIN_THREADS) k_finish(const int32_t *status, c
   host[4] = e;
   host[5] = b;
   host[6] = in_hi - in_lo;
+  host[8] = chunked;
+  c[11] = 0;
   c[0] = 0;                                     // used := 0, pend_count := 0 and the finish counters:
   reinterpret_cast<uint32_t *>(c)[4] = 0;       // the next launch starts clean (see run_op for the
   c[8] = 0;                                     // general path)
@@ -434,6 +439,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   j.counter_retry = (uint32_t *)(counters + 1);
   j.pend_count = (uint32_t *)(counters + 2);
   j.pend_list = S->list_a.as<uint32_t>();
+  j.pw_count = counters + 11;
   j.n = nd;
   const uint64_t seq = ++S->seq;
   if (op == OP_DIFF || op == OP_SV || op == OP_META) {  // per-block scratch of the streamed walkers
@@ -444,6 +450,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   if (S->dirty) HIPCHK(hipMemsetAsync(counters, 0, 1024, st));
   S->dirty = true;
   bool slots = false;  // the fast paths wrote their outputs into the slot region (merges, delete-set merges)
+  uint64_t chunked = 0;  // documents the chunk-parallel walk completed (summed over this call's round trips)
   // ends a round trip: counters and stats land in pinned host memory, then one stream sync
   auto finish = [&]() -> int {
     const bool want = stats || host;  // host batches need the bytes out (the packed size)
@@ -463,6 +470,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
     hipError_t q;
     for (int it = 0; (q = hipStreamQuery(st)) == hipErrorNotReady && it < 100000; it++) __builtin_ia32_pause();
     if (q != hipSuccess) HIPCHK(hipStreamSynchronize(st));
+    chunked += S->pinned[8];
     return 0;
   };
   if (!((op == OP_MERGE && !j.v2) || (op == OP_DSMERGE && !j.dsref)))
@@ -471,7 +479,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   // (1) fast path over every document; appends the ones it declines to list_a
   int fr = fast_launch(op, j, b->n_upd, st);     // V1 merge: LDS fast path
   if (fr == 0) fr = fast2_launch(op, j, b->n_upd, st);  // V2 merge: LDS fast path
-  if (fr == 0) fr = big_launch(op, j, st);         // V1 diff / state vector: streamed wave walker
+  if (fr == 0) fr = big_launch(op, j, st, S->pw);  // V1 diff / state vector: chunk walk + wave walker
   if (fr == 0) fr = big2_launch(op, j, st);        // V2 diff / state vector: streamed wave walker
   if (fr < 0) return fr;
   slots = op == OP_MERGE || (op == OP_DSMERGE && fr == 1);
@@ -540,6 +548,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
     stats->docs_error = S->pinned[4];
     stats->bytes_out = S->pinned[5];
     stats->bytes_in = S->pinned[6];
+    stats->docs_chunked = chunked;
   }
   if (!host) return used > out->cap ? YM_ERR_CAPACITY : 0;
   // host batch: pack the outputs in document order (out_off[d] = bytes of the outputs before d), then
@@ -607,6 +616,8 @@ static void release_state(DevState *S) {
   if (S->evl1) hipEventDestroy(S->evl1);
   for (int k = 0; k < 4; k++) if (S->large.p[k]) hipFree(S->large.p[k]);
   if (S->large.pinned) hipHostFree(S->large.pinned);
+  for (int k = 0; k < 4; k++) if (S->pw.p[k]) hipFree(S->pw.p[k]);
+  if (S->pw.pinned) hipHostFree(S->pw.pinned);
   if (S->stream) hipStreamDestroy(S->stream);
   delete S;
 }

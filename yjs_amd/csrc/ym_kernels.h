@@ -44,6 +44,8 @@ struct GeneralJob {
   uint32_t *pend_list;       // fast path: ids of the documents it declines (appended) ...
   uint32_t *pend_count;      // ... and their number
   uint8_t *bscratch;         // streamed single-update kernels: BS_BYTES per block (ym_big*.hip)
+  const uint8_t *pw_done;    // V1 diff / sv: documents the chunk-parallel walk completed (ym_pwalk.hip)
+  uint64_t *pw_count;        // ... and their number (a device counter k_finish reports and resets)
 };
 
 // Per-block HBM scratch of the streamed diff / state-vector kernels (ym_big.hip, ym_big2.hip): client
@@ -66,6 +68,16 @@ struct LargeBufs {
 // Large-document merge over `list` (n documents the fast path declined).  Documents it takes get
 // status OK; the rest keep ST_PENDING.  Returns 1 when launched, 0 when not applicable, < 0 on error.
 int large_run(const GeneralJob &j, const uint32_t *list, uint32_t n, hipStream_t st, LargeBufs &B);
+
+// device buffers of the chunk-parallel V1 walk (ym_pwalk.hip), grown on demand, cached
+struct PwBufs {
+  void *p[4] = {nullptr, nullptr, nullptr, nullptr};
+  size_t cap[4] = {0, 0, 0, 0};
+  uint32_t *pinned = nullptr;
+};
+// Chunk-parallel walk + stitch over the large single-update documents of a V1 diff / sv call; sets
+// *done (per document: 1 = completed).  Returns 1 when launched, 0 when not applicable, < 0 on error.
+int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const uint8_t **done);
 
 using ym::GeneralWsSize;
 using ym::general_ws_size;

@@ -1,0 +1,264 @@
+// ym_lane.h -- per-lane lib0 / V1 struct parser over global memory, for the chunk-parallel walk of large
+// updates (ym_pwalk.hip).  Each lane runs its own cursor (divergent across lanes, unlike the wave-uniform
+// scalar walker of ym_scalar.h); the next bytes sit in a 16-byte register window (lo, hi) refilled by one
+// unaligned 8-byte global load per ~8 consumed bytes, so a ~11-byte struct costs one or two loads.
+//
+// Same semantics and canonical-form checks as ym_scalar.h / ym_fast_common.h (lib0 0.2.42 readVarUint /
+// readVarString / readAny, UpdateDecoder.js:127-243, Item.js:665-683): a struct this parser accepts is
+// one the verbatim copy reproduces exactly; anything else is rejected.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ymk {
+namespace ln {
+
+// bytes [p, e) of the document at b; reads may run up to 15 bytes past e (the arena is padded)
+struct LCur {
+  const uint8_t *b;
+  uint32_t p, e;
+  bool bad;
+  uint64_t lo, hi;
+  uint32_t nv;
+  uint32_t cap;  // longest string / ContentAny the parse accepts (bounds a speculative parse)
+};
+__device__ __forceinline__ uint64_t ld8(const uint8_t *b, uint32_t p) {
+  uint64_t x;
+  __builtin_memcpy(&x, b + p, 8);
+  return x;
+}
+__device__ __forceinline__ uint32_t byte(const uint8_t *b, uint32_t p) { return b[p]; }
+__device__ __forceinline__ void fill(LCur &c) {  // nv >= 8 afterwards
+  if (c.nv >= 8) return;
+  const uint64_t x = ld8(c.b, c.p + c.nv);
+  if (c.nv == 0) {
+    c.lo = x;
+    c.hi = 0;
+  } else {
+    c.lo |= x << (8 * c.nv);
+    c.hi = x >> (64 - 8 * c.nv);
+  }
+  c.nv += 8;
+}
+__device__ __forceinline__ LCur make(const uint8_t *b, uint32_t p, uint32_t e, uint32_t cap = 0xffffffffu) {
+  LCur c = {b, p, e, false, 0, 0, 0, cap};
+  fill(c);
+  return c;
+}
+__device__ __forceinline__ void skip(LCur &c, uint32_t n) {
+  if (n >= c.nv) {
+    c.p += n;
+    c.nv = 0;
+  } else if (n > 0) {
+    if (n < 8) {
+      c.lo = (c.lo >> (8 * n)) | (c.hi << (64 - 8 * n));
+      c.hi >>= 8 * n;
+    } else {
+      c.lo = c.hi >> (8 * (n - 8));
+      c.hi = 0;
+    }
+    c.p += n;
+    c.nv -= n;
+  }
+  fill(c);
+}
+__device__ __forceinline__ uint64_t peek8(const LCur &c, uint32_t o) {
+  if (o == 0) return c.lo;
+  if (o + 8 <= c.nv) return o < 8 ? (c.lo >> (8 * o)) | (c.hi << (64 - 8 * o)) : c.hi >> (8 * (o - 8));
+  return ld8(c.b, c.p + o);
+}
+__device__ __forceinline__ uint32_t vu_nb(uint32_t lo, uint32_t hi) {
+  const uint32_t s_lo = ~lo & 0x80808080u;
+  const uint32_t s_hi = (~hi & 0x80u) | 0x8000u;
+  const uint32_t t = __builtin_ctzg(s_lo, 32 + __builtin_ctz(s_hi));
+  return (t >> 3) + 1;
+}
+__device__ __forceinline__ bool vu_bad(uint32_t lo, uint32_t hi, uint32_t nb, uint32_t p, uint32_t e) {
+  const uint32_t last = nb <= 4 ? (lo >> (8 * nb - 8)) & 0xffu : hi & 0xffu;
+  return (nb > 5) | (p + nb > e) | ((nb > 1) & (last == 0)) | ((nb == 5) & ((hi & 0x70u) != 0));
+}
+// lib0 readVarUint (u32, canonical encodings only)
+__device__ __forceinline__ uint32_t rvu(LCur &c) {
+  const uint32_t lo = (uint32_t)c.lo, hi = (uint32_t)(c.lo >> 32);
+  const uint32_t nb = vu_nb(lo, hi);
+  const uint32_t v = (lo & 0x7fu) | ((lo >> 1) & 0x3f80u) | ((lo >> 2) & 0x1fc000u) | ((lo >> 3) & 0xfe00000u) | (hi << 28);
+  const uint32_t m = (uint32_t)((1ull << (7 * (nb < 5 ? nb : 5))) - 1);
+  c.bad |= vu_bad(lo, hi, nb, c.p, c.e);
+  skip(c, nb < 6 ? nb : 0);
+  return v & m;
+}
+__device__ __forceinline__ void skvu(LCur &c) { (void)rvu(c); }
+__device__ __forceinline__ uint32_t rdb(LCur &c) {
+  c.bad |= c.p >= c.e;
+  const uint32_t v = (uint32_t)c.lo & 0xffu;
+  skip(c, 1);
+  return v;
+}
+__device__ __forceinline__ bool room(const LCur &c, uint32_t n) { return c.p <= c.e && n <= c.e - c.p; }
+// strict UTF-8 (lib0: decodeURIComponent(escape(..))); the UTF-16 length
+__device__ __forceinline__ uint32_t utf8_slow(const uint8_t *b, uint32_t i, uint32_t e, bool &bad) {
+  uint32_t u = 0;
+  while (i < e) {
+    const uint32_t x = byte(b, i);
+    if (x < 0x80) { u++; i++; continue; }
+    uint32_t len, cp, mn;
+    if ((x & 0xE0) == 0xC0) { len = 2; cp = x & 0x1F; mn = 0x80; }
+    else if ((x & 0xF0) == 0xE0) { len = 3; cp = x & 0x0F; mn = 0x800; }
+    else if ((x & 0xF8) == 0xF0) { len = 4; cp = x & 0x07; mn = 0x10000; }
+    else { bad = true; return 0; }
+    if (i + len > e) { bad = true; return 0; }
+    for (uint32_t q = 1; q < len; q++) {
+      const uint32_t cb = byte(b, i + q);
+      if ((cb & 0xC0) != 0x80) { bad = true; return 0; }
+      cp = (cp << 6) | (cb & 0x3F);
+    }
+    if (cp < mn || cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF)) { bad = true; return 0; }
+    u += cp >= 0x10000 ? 2 : 1;
+    i += len;
+  }
+  return u;
+}
+__device__ __forceinline__ uint64_t mask_bytes(uint64_t x, uint32_t n) { return n >= 8 ? x : x & ((1ull << (8 * n)) - 1); }
+__device__ __forceinline__ uint32_t utf16_len(LCur &c, uint32_t n) {
+  if (!room(c, n) || n > c.cap) { c.bad = true; return 0; }
+  uint64_t hi = 0;
+  for (uint32_t o = 0; o < n; o += 8) hi |= mask_bytes(peek8(c, o), n - o);
+  uint32_t u = n;
+  if (hi & 0x8080808080808080ull) u = utf8_slow(c.b, c.p, c.p + n, c.bad);
+  skip(c, n);
+  return u;
+}
+__device__ __forceinline__ uint32_t rstr(LCur &c) {
+  const uint32_t n = rvu(c);
+  return c.bad ? 0 : utf16_len(c, n);
+}
+__device__ __forceinline__ uint64_t has_byte(uint64_t x, uint64_t v) {
+  const uint64_t y = x ^ (0x0101010101010101ull * v);
+  return (y - 0x0101010101010101ull) & ~y & 0x8080808080808080ull;
+}
+__device__ __forceinline__ uint64_t has_ctl(uint64_t x) { return (x - 0x2020202020202020ull) & ~x & 0x8080808080808080ull; }
+// JSON text as yjs writes it for formats / embeds: true | false | null | "string without escapes"
+__device__ __forceinline__ void json_lit(LCur &c) {
+  const uint32_t n = rvu(c);
+  if (c.bad || !room(c, n) || n > c.cap) { c.bad = true; return; }
+  const uint64_t w = c.lo;
+  bool ok;
+  if (n == 4) ok = (uint32_t)w == 0x65757274u || (uint32_t)w == 0x6c6c756eu;
+  else if (n == 5) ok = (w & 0xffffffffffull) == 0x65736c6166ull;
+  else ok = false;
+  if (!ok && n >= 2 && (w & 0xff) == '"' && byte(c.b, c.p + n - 1) == '"') {
+    uint64_t bad = 0;
+    for (uint32_t o = 1; o + 1 < n; o += 8) {
+      const uint64_t x = mask_bytes(peek8(c, o), n - 1 - o);
+      const uint64_t pad = (n - 1 - o) >= 8 ? 0 : ~0ull << (8 * (n - 1 - o));
+      const uint64_t xs = x | (pad & 0x4040404040404040ull);
+      bad |= has_byte(xs, '"') | has_byte(xs, '\\') | (has_ctl(xs) & ~xs);
+    }
+    ok = bad == 0;
+  }
+  if (!ok) { c.bad = true; return; }
+  utf16_len(c, n);
+}
+// one scalar `any` value in the canonical form lib0 writeAny emits
+__device__ __forceinline__ void any_scalar(LCur &c) {
+  const uint32_t tag = rdb(c);
+  switch (tag) {
+    case 127: case 126: case 121: case 120: return;
+    case 125: {
+      uint32_t x = rdb(c);
+      uint64_t mag = x & 63;
+      const bool neg = x & 64;
+      int s = 6, nb = 1;
+      while ((x & 128) && !c.bad) {
+        x = rdb(c);
+        if (s > 34) { c.bad = true; return; }
+        mag |= (uint64_t)(x & 127) << s;
+        s += 7;
+        nb++;
+      }
+      if ((nb > 1 && x == 0) || (!neg && mag > 2147483647ull) || mag > 0xffffffffull) c.bad = true;
+      return;
+    }
+    case 124: {
+      if (!room(c, 4)) { c.bad = true; return; }
+      const float f = __uint_as_float(__builtin_bswap32((uint32_t)c.lo));
+      if (f != f || (truncf(f) == f && (double)f <= 2147483647.0)) c.bad = true;
+      skip(c, 4);
+      return;
+    }
+    case 123: {
+      if (!room(c, 8)) { c.bad = true; return; }
+      const double x = __longlong_as_double((long long)__builtin_bswap64(c.lo));
+      if (x == x && ((trunc(x) == x && x <= 2147483647.0) || (double)(float)x == x)) c.bad = true;
+      skip(c, 8);
+      return;
+    }
+    case 119: rstr(c); return;
+    default: c.bad = true; return;
+  }
+}
+// Item fields and content after the info byte; false for kinds the verbatim path does not verify
+// (ContentJSON, ContentDoc, bad refs) or any anomaly.  `len` = the Item's clock length.
+__device__ __forceinline__ bool item_body(LCur &c, uint32_t info, uint32_t &len) {
+  if (info & 0x80) { skvu(c); skvu(c); }
+  if (info & 0x40) { skvu(c); skvu(c); }
+  if ((info & 0xC0) == 0) {
+    const uint32_t pi = rvu(c);
+    c.bad |= pi > 1;
+    if (pi == 1) rstr(c);
+    else { skvu(c); skvu(c); }
+    if (info & 0x20) rstr(c);
+  }
+  len = 1;
+  switch (info & 31) {
+    case 1: len = rvu(c); break;
+    case 3: { const uint32_t n = rvu(c); if (!room(c, n)) c.bad = true; else skip(c, n); break; }
+    case 4: len = rstr(c); break;
+    case 5: json_lit(c); break;
+    case 6: rstr(c); json_lit(c); break;
+    case 7: {
+      const uint32_t t = rvu(c);
+      c.bad |= t > 6;
+      if (t == 3 || t == 5) rstr(c);
+      break;
+    }
+    case 8:
+      len = rvu(c);
+      c.bad |= len > c.cap;
+      for (uint32_t i = 0; i < len && !c.bad; i++) any_scalar(c);
+      break;
+    default: c.bad = true; break;
+  }
+  return !c.bad && len != 0;
+}
+
+// Record flags of one parsed struct (ym_pwalk.hip step records, bits 28-31 of the position word)
+constexpr uint32_t F_FAIL = 1u << 28;   // no struct parses here (the walk resumes one byte later)
+constexpr uint32_t F_SKIP = 1u << 29;   // a Skip (info 10)
+constexpr uint32_t F_PATCH = 1u << 30;  // the writer re-encodes the info byte differently (0x20 cleared / GC := 0)
+constexpr uint32_t POS_MASK = (1u << 28) - 1;
+
+// One V1 struct at p (GC / Skip / Item, readClientsStructRefs' cases): on success `next` is the position
+// after it, `len` its clock length and `fl` its flags.  `cap` bounds string / ContentAny lengths (the
+// speculative walk's parse of a position that may not start a struct; the stitch re-parses uncapped).
+__device__ __forceinline__ bool parse_struct(const uint8_t *b, uint32_t p, uint32_t e, uint32_t &next, uint32_t &len,
+                                             uint32_t &fl, uint32_t cap = 0xffffffffu) {
+  LCur c = make(b, p, e, cap);
+  const uint32_t info = rdb(c);
+  const bool sk = info == 10, gc = !sk && (info & 31) == 0;
+  bool ok;
+  if (sk || gc) {
+    len = rvu(c);
+    ok = !c.bad;
+  } else {
+    ok = item_body(c, info, len);
+  }
+  ok = ok && !c.bad && c.p <= c.e;
+  const uint32_t ni = sk ? info : gc ? 0 : ((info & 0xC0) ? info & ~0x20u : info);
+  fl = (sk ? F_SKIP : 0) | (ni != info ? F_PATCH : 0);
+  next = c.p;
+  return ok;
+}
+
+}  // namespace ln
+}  // namespace ymk

@@ -1,0 +1,693 @@
+// ym_pwalk.hip -- chunk-parallel V1 diffUpdate / encodeStateVectorFromUpdate over large single updates
+// (BASELINE configs[2] C3: 0.9 MB updates of ~70 k structs; configs[4] C5 diff).
+//
+// A V1 update is a byte stream of structs whose boundaries are only known by parsing from the start,
+// which made the previous design (ym_big.hip) one sequential walk per document.  Here the walk is split:
+//
+//  1. k_pw_walk -- one lane per 1 KB chunk of every document (C3: 3.6 M lanes).  Each lane parses
+//     structs *speculatively* from its chunk's first byte: a position where no struct parses is recorded
+//     as a FAIL and the walk resumes one byte later.  V1 structs re-synchronise within a few structs, so
+//     after a short garbage prefix the lane is on the document's true struct chain.  Every step is
+//     recorded (position | flags, clock length), plus the chunk's exit position (>= the chunk's end).
+//  2. k_pw_stitch -- one wave per document.  It follows the true chain chunk by chunk: at a chunk it
+//     finds its entry position among the chunk's records (a ballot over 64 records), then consumes the
+//     records 64 at a time: clocks by a wave prefix sum, the diff cut by a ballot (the segmented search of
+//     SURVEY §8a), Skips and info-byte patches by ballots.  Where the entry is not a record (the lane's
+//     speculative chain skipped it) or is a FAIL (a string / ContentAny longer than the speculative cap,
+//     or a real error), the stitch parses that one struct itself, uncapped, and goes on; an error on the
+//     true chain declines the document to the sequential walker.  Section headers and the delete set are
+//     parsed by the stitch (the delete set's varuints are validated 1 KB per wave step by a ballot over
+//     continuation bits).  The output is assembled as in ym_big.hip: part headers and the sliced first
+//     struct written by lane 0, verbatim spans copied by the wave, then the info-byte patches.
+//
+// Semantics are exactly those of ym_big.hip's k_big_v1 (yjs 13.5.16 diffUpdate / encodeStateVector-
+// FromUpdate): the same structs are accepted (ym_lane.h mirrors ym_scalar.h), the same
+// inputs are declined.  Documents this path declines (or does not take: several updates, < PW_MIN bytes)
+// go to k_big_v1, and from there to the general path.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "ym_fast_common.h"
+#include "ym_kernels.h"
+#include "ym_lane.h"
+#include "ym_scalar.h"
+
+namespace ymk {
+namespace pw {
+using namespace fastc;
+using ln::F_FAIL;
+using ln::F_PATCH;
+using ln::F_SKIP;
+using ln::POS_MASK;
+using sc::SCur;
+
+constexpr uint32_t CH = 1024;          // chunk bytes (one walking lane each)
+constexpr uint32_t CAP = CH / 2 + 8;   // records per chunk (a struct is >= 2 bytes; FAIL runs on top: overflow)
+constexpr uint32_t SPEC_CAP = 2048;    // longest string / ContentAny a speculative parse accepts
+constexpr uint64_t PW_MIN = 32768;     // smaller updates stay on k_big_v1
+constexpr uint32_t NSEC = BS_NSEC, NSV = BS_NSV, PRE = BS_PRE, SECW = BS_SECW;
+constexpr uint32_t NPATCH = 1024;
+constexpr uint32_t L_PPOS = 0;                     // u32[NPATCH] patch positions (document-relative)
+constexpr uint32_t L_PSEC = L_PPOS + 4 * NPATCH;   // u32[NPATCH] section of each patch
+constexpr uint32_t L_PVAL = L_PSEC + 4 * NPATCH;   // u8[NPATCH]  patched info bytes
+constexpr uint32_t LDS_BYTES = L_PVAL + NPATCH;
+enum { S_PRELEN = 0, S_A0, S_A1, S_B0, S_B1, S_WRITTEN, S_CLIENT, S_FCLOCK, S_OUTB };
+constexpr uint32_t NONE = 0xffffffffu;
+
+struct Scr {
+  uint32_t *sec, *svt, *dsc;
+  uint8_t *pre;
+};
+__device__ __forceinline__ Scr scratch(const GeneralJob &j) {
+  uint8_t *b = j.bscratch + (uint64_t)blockIdx.x * BS_BYTES;
+  return Scr{(uint32_t *)(b + BS_SEC), (uint32_t *)(b + BS_SVT), (uint32_t *)(b + BS_DSC), b + BS_PREB};
+}
+#define sec(ci, f) X.sec[SECW * (ci) + (f)]
+
+// ---- 0. eligibility and chunk counts ---------------------------------------------------------------
+__global__ void k_pw_prep(GeneralJob j, uint32_t *cnt, uint8_t *done, uint64_t pw_min) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d > j.n) return;
+  uint32_t c = 0;
+  if (d < j.n) {
+    done[d] = 0;
+    const uint32_t u0 = j.doc_upd[d];
+    if (j.doc_upd[d + 1] - u0 == 1) {
+      const uint64_t len = j.upd_off[u0 + 1] - j.upd_off[u0];
+      if (len >= pw_min && len > 0 && len < (1ull << 28)) c = (uint32_t)((len + CH - 1) / CH);
+    }
+  }
+  cnt[d] = c;  // cnt[n] = 0: the exclusive scan's last entry is the total
+}
+
+// ---- 1. speculative chunk walk ----------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_pw_walk(GeneralJob j, const uint32_t *cbase, uint32_t nd, uint32_t total,
+                                                 uint4 *sums, uint2 *recs) {
+  const uint32_t g = blockIdx.x * 256 + threadIdx.x;
+  if (g >= total) return;
+  uint32_t lo = 0, hi = nd - 1;  // the document: largest d with cbase[d] <= g
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (cbase[mid] <= g) lo = mid; else hi = mid - 1;
+  }
+  const uint32_t d = lo, ci = g - cbase[d];
+  const uint32_t u0 = j.doc_upd[d];
+  const uint64_t ub = j.upd_off[u0];
+  const uint32_t len = (uint32_t)(j.upd_off[u0 + 1] - ub);
+  const uint8_t *D = j.A + ub;
+  const uint32_t c0 = ci * CH, c1 = c0 + CH < len ? c0 + CH : len;
+  uint2 *R = recs + (uint64_t)g * CAP;
+  uint32_t p = c0, nrec = 0, ovf = 0;
+  bool frun = false;
+  while (p < c1) {
+    uint32_t nx, cl, fl;
+    const bool ok = ln::parse_struct(D, p, len, nx, cl, fl, SPEC_CAP);
+    if (ok || !frun) {
+      if (nrec == CAP) { ovf = 1; break; }
+      R[nrec++] = make_uint2(p | (ok ? fl : F_FAIL), ok ? cl : 0u);
+    }
+    frun = !ok;
+    p = ok ? nx : p + 1;
+  }
+  sums[g] = make_uint4(ovf ? 0u : nrec, p, ovf, 0u);  // an overflowed chunk is re-parsed by the stitch
+}
+
+// ---- 2. stitch ----------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t sv_lookup(const uint32_t *svt, uint32_t nsv, uint32_t client) {
+  int best = -1;
+  for (uint32_t i0 = 0; i0 < nsv; i0 += 64) {
+    const uint32_t i = i0 + threadIdx.x;
+    const uint64_t m = __ballot(i < nsv && svt[2 * i] == client);
+    if (m) best = (int)(i0 + 63 - __builtin_clzll(m));
+  }
+  return best >= 0 ? svt[2 * best + 1] : 0;
+}
+__device__ __forceinline__ bool seen_before(const uint32_t *dsc, uint32_t n, uint32_t client) {
+  bool hit = false;
+  for (uint32_t h0 = 0; h0 < n; h0 += 64) {
+    const uint32_t h = h0 + threadIdx.x;
+    hit |= __any(h < n && dsc[h] == client);
+  }
+  return hit;
+}
+typedef uint4 __attribute__((aligned(1))) u4u;
+__device__ __forceinline__ void copy_bytes(uint8_t *dst, const uint8_t *src, uint32_t n) {
+  const uint32_t nv = n >> 4;
+  uint32_t v = threadIdx.x;
+  for (; v + 192 < nv; v += 256) {  // four 16-byte loads in flight per lane
+    const uint4 a = reinterpret_cast<const u4u *>(src)[v], b = reinterpret_cast<const u4u *>(src)[v + 64];
+    const uint4 c = reinterpret_cast<const u4u *>(src)[v + 128], e = reinterpret_cast<const u4u *>(src)[v + 192];
+    reinterpret_cast<u4u *>(dst)[v] = a;
+    reinterpret_cast<u4u *>(dst)[v + 64] = b;
+    reinterpret_cast<u4u *>(dst)[v + 128] = c;
+    reinterpret_cast<u4u *>(dst)[v + 192] = e;
+  }
+  for (; v < nv; v += 64) reinterpret_cast<u4u *>(dst)[v] = reinterpret_cast<const u4u *>(src)[v];
+  for (uint32_t i = (nv << 4) + threadIdx.x; i < n; i += 64) dst[i] = src[i];
+}
+__device__ __forceinline__ uint32_t put_vu_g(uint8_t *o, uint32_t p, uint32_t v) {
+  while (v > 127) { o[p++] = (uint8_t)(0x80 | (v & 127)); v >>= 7; }
+  o[p++] = (uint8_t)v;
+  return p;
+}
+
+// Item.write / GC.write with offset `off` (> 0) of the struct at document position s0 (ending at s1):
+// the re-encoded head goes to `pre` (lane 0), the content tail to span [a0, a1).  False: decline (the
+// content kind cannot be sliced here, a split surrogate pair, a head longer than PRE).
+__device__ bool slice_head(sc::cu32 *B, uint32_t adj, uint32_t s0, uint32_t s1, uint32_t client, uint64_t clock,
+                           uint32_t len, uint32_t off, uint8_t *pre, uint32_t &prelen, uint32_t &a0, uint32_t &a1) {
+  const uint32_t lane = threadIdx.x;
+  const uint32_t info = sc::byte(B, s0 + adj);
+  const bool gc = (info & 31) == 0;
+  uint8_t h[PRE + 16];
+  uint32_t q = 0;
+  auto put = [&](uint32_t v) { while (v > 127) { h[q++] = (uint8_t)(0x80 | (v & 127)); v >>= 7; } h[q++] = (uint8_t)v; };
+  a0 = a1 = 0;
+  if (gc) {
+    h[q++] = 0;
+    put(len - off);
+  } else {
+    const uint32_t ref = info & 31;
+    if (ref != 1 && ref != 4 && ref != 8) return false;
+    SCur e = sc::make(B, s0 + adj + 1, s1 + adj);
+    const uint32_t ni = ref | 0x80 | (info & 0x40) | ((info & 0xC0) == 0 ? (info & 0x20) : 0);
+    if (info & 0x80) { sc::skvu(e); sc::skvu(e); }
+    uint32_t ro0 = 0, ro1 = 0;
+    if (info & 0x40) { ro0 = e.p; sc::skvu(e); sc::skvu(e); ro1 = e.p; }
+    if ((info & 0xC0) == 0) {
+      const uint32_t pi = sc::rvu(e);
+      if (pi == 1) { const uint32_t n = sc::rvu(e); sc::skip(e, n); }
+      else { sc::skvu(e); sc::skvu(e); }
+      if (info & 0x20) { const uint32_t n = sc::rvu(e); sc::skip(e, n); }
+    }
+    h[q++] = (uint8_t)ni;
+    put(client);
+    put((uint32_t)(clock + off - 1));
+    if (ro1 - ro0 > 10) return false;
+    for (uint32_t b = ro0; b < ro1; b++) h[q++] = (uint8_t)sc::byte(B, b);
+    if (ref == 1) {
+      sc::rvu(e);
+      put(len - off);
+    } else if (ref == 8) {
+      sc::rvu(e);
+      for (uint32_t i = 0; i < off; i++) sc::any_scalar(e);  // ContentAny.splice: drop `off` values
+      put(len - off);
+      a0 = e.p - adj;
+      a1 = s1;
+    } else {  // ContentString: str.slice(off) in UTF-16 units; a split surrogate pair throws in yjs
+      const uint32_t n = sc::rvu(e);
+      uint32_t bi = 0, u = 0;
+      while (u < off && bi < n) {
+        const uint32_t b = sc::byte(B, e.p + bi);
+        const uint32_t l = b < 0x80 ? 1 : b < 0xE0 ? 2 : b < 0xF0 ? 3 : 4;
+        u += l == 4 ? 2 : 1;
+        bi += l;
+      }
+      if (u != off) return false;
+      put(n - bi);
+      a0 = e.p - adj + bi;
+      a1 = e.p - adj + n;
+    }
+    if (e.bad) return false;
+  }
+  if (q > PRE) return false;
+  if (lane == 0)
+    for (uint32_t b = 0; b < q; b++) pre[b] = h[b];
+  prelen = q;
+  return true;
+}
+
+// Validates `cnt` canonical varuints (u32, lib0 readVarUint) starting at x, wave-parallel: 1 KB per
+// step, 16 bytes per lane, stop bytes counted by a wave prefix sum.  Returns the position after the
+// last one, or NONE (truncated / non-canonical).
+__device__ uint32_t skip_varuints(const uint8_t *D, uint32_t x, uint32_t e, uint64_t cnt) {
+  const uint32_t lane = threadIdx.x;
+  const uint32_t xs = x;  // the first varuint's start: bytes before it are not part of the sequence
+  while (cnt > 0) {
+    if (x >= e) return NONE;
+    const uint32_t q = x + 16 * lane;
+    uint8_t b[16];
+    if (q + 16 <= e) {
+      const uint4 v = *reinterpret_cast<const u4u *>(D + q);
+      __builtin_memcpy(b, &v, 16);
+    } else {
+      for (uint32_t k = 0; k < 16; k++) b[k] = q + k < e ? D[q + k] : 0x80;  // past the end: no stop byte
+    }
+    // continuation bytes right before q (inside [xs, q)), up to 5
+    uint32_t run = 0;
+    for (uint32_t k = 1; k <= 5 && q >= xs + k; k++) {
+      if (D[q - k] < 0x80) break;
+      run++;
+    }
+    uint32_t nstop = 0;
+    for (uint32_t k = 0; k < 16; k++) nstop += b[k] < 0x80 && q + k < e;
+    const uint32_t incl = wave_incl_add(nstop), excl = incl - nstop;
+    const uint32_t tot = lane_read(incl, 63);
+    const uint32_t need = cnt < tot ? (uint32_t)cnt : tot;  // stops consumed by this step
+    // canonical-form checks for this lane's stops of rank < need
+    bool bad = false;
+    uint32_t rank = excl, endp = 0;
+    for (uint32_t k = 0; k < 16; k++) {
+      const bool stop = b[k] < 0x80 && q + k < e;
+      if (stop && rank < need) {
+        const uint32_t nb = run + 1;
+        bad |= nb > 5 || (nb > 1 && b[k] == 0) || (nb == 5 && (b[k] & 0x70) != 0);
+        if (rank == need - 1) endp = q + k + 1;
+      }
+      rank += stop;
+      run = stop ? 0 : run + 1;
+    }
+    if (__any(bad)) return NONE;
+    if (cnt <= tot) {
+      const uint64_t m = __ballot(endp != 0);
+      return lane_read(endp, __builtin_ctzll(m));
+    }
+    // an unfinished varuint at the end of this step may not exceed 5 bytes either (checked next step
+    // through `run`)
+    cnt -= tot;
+    x += 1024;
+  }
+  return x;
+}
+
+// a declined document keeps done[d] != 1 (k_big_v1 takes it); the value says why (ym__pw_reasons)
+#define PW_DECLINE_R(r)                  \
+  {                                      \
+    if (lane == 0) done[d] = (uint8_t)(r); \
+    __syncthreads();                     \
+    continue;                            \
+  }
+#define PW_DECLINE() PW_DECLINE_R(why ? why : 2)
+
+// OP = OP_DIFF or OP_SV
+template <int OP>
+__global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *cbase, const uint4 *sums, const uint2 *recs,
+                                                  uint8_t *done) {
+  const uint32_t lane = threadIdx.x;
+  const Scr X = scratch(j);
+  for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
+    const uint32_t cb = cbase[d], nch = cbase[d + 1] - cb;
+    if (nch == 0) continue;
+    const uint32_t u0 = j.doc_upd[d];
+    const uint64_t ub = j.upd_off[u0];
+    const uint32_t len = (uint32_t)(j.upd_off[u0 + 1] - ub);
+    const uint8_t *D = j.A + ub;
+    uint32_t why = 0;  // decline reason
+    sc::cu32 *const B = sc::base_of(D);
+    const uint32_t adj = (uint32_t)(ub & 3);
+    // ---- state vector (diff): decodeStateVector, later entries win (encoding.js:536-545)
+    uint32_t nsv = 0;
+    if (OP == OP_DIFF) {
+      const uint64_t s0 = j.sv_off[d], s1 = j.sv_off[d + 1];
+      if (s1 - s0 > 16ull * NSV) PW_DECLINE_R(3)
+      bool bad;
+      {
+        SCur c = sc::make(sc::base_of(j.sv + s0), (uint32_t)(s0 & 3), (uint32_t)(s0 & 3) + (uint32_t)(s1 - s0));
+        const uint32_t n = sc::rvu(c);
+        for (uint32_t i = 0; i < n && !c.bad; i++) {
+          const uint32_t cl = sc::rvu(c), ck = sc::rvu(c);
+          if (nsv >= NSV) { c.bad = true; break; }
+          if (lane == 0) { X.svt[2 * nsv] = cl; X.svt[2 * nsv + 1] = ck; }
+          nsv++;
+        }
+        bad = c.bad;
+      }
+      __syncthreads();
+      if (bad) PW_DECLINE_R(3)
+    }
+    // ---- struct section: headers parsed here, structs from the walk's records
+    uint32_t x = 0;
+    bool declined = false;
+    uint32_t nclients;
+    {
+      ln::LCur c = ln::make(D, x, len);
+      nclients = ln::rvu(c);
+      declined = c.bad;
+      x = c.p;
+    }
+    if (declined || nclients > NSEC) PW_DECLINE_R(4)
+    uint32_t nparts = 0, npatch = 0;
+    uint32_t sv_client = 0, sv_clock = 0, sv_n = 0;
+    bool sv_stop = false, sv_any = false;
+    uint32_t prev_client = 0;
+    // chunk cursor: current chunk, its record count / exit, the next record index
+    uint32_t cc = NONE, nrec = 0, cexit = 0, s = 0;
+    const uint2 *R = nullptr;
+    for (uint32_t ci = 0; ci < nclients && !declined; ci++) {
+      uint32_t nstructs, client;
+      uint64_t clock;
+      {
+        ln::LCur c = ln::make(D, x, len);
+        nstructs = ln::rvu(c);
+        client = ln::rvu(c);
+        clock = ln::rvu(c);
+        x = c.p;
+        if (c.bad) { declined = true; why = 5; break; }
+      }
+      if (ci > 0 && client == prev_client) { declined = true; why = 6; break; }
+      prev_client = client;
+      const uint32_t k = OP == OP_DIFF ? sv_lookup(X.svt, nsv, client) : 0;
+      if (OP == OP_SV && nstructs > 0 && sv_any && client != sv_client) {
+        if (sv_clock != 0) {
+          if (sv_n >= NSV) { declined = true; why = 13; break; }
+          if (lane == 0) { X.svt[2 * sv_n] = sv_client; X.svt[2 * sv_n + 1] = sv_clock; }
+          sv_n++;
+        }
+        sv_client = client; sv_clock = 0; sv_stop = clock != 0;
+      }
+      bool copying = false;
+      uint32_t written = 0;
+      uint32_t rem = nstructs;
+      while (rem > 0) {
+        if (x >= len) { declined = true; why = 7; break; }
+        // ---- locate x among the records of its chunk
+        const uint32_t cx = x / CH;
+        if (cx != cc) {
+          cc = cx;
+          const uint4 sm4 = sums[cb + cx];
+          nrec = sm4.x;
+          cexit = sm4.y;
+          s = 0;
+          R = recs + (uint64_t)(cb + cx) * CAP;
+        }
+        bool found = false;
+        for (;;) {
+          if (s >= nrec) break;
+          const uint32_t kk = s + lane;
+          const uint32_t pw = kk < nrec ? R[kk].x : POS_MASK;
+          const uint64_t lt = __ballot(kk < nrec && (pw & POS_MASK) < x);
+          const uint32_t nlt = __popcll(lt);
+          if (nlt == 64) { s += 64; continue; }
+          s += nlt;
+          if (s < nrec) {
+            const uint32_t cand = lane_read(pw, nlt);
+            found = (cand & POS_MASK) == x && !(cand & F_FAIL);
+          }
+          break;
+        }
+        uint32_t n, pos = 0, end = 0, clen = 0, fl = 0;
+        bool valid;
+        if (found) {
+          n = nrec - s < 64 ? nrec - s : 64;
+          if (rem < n) n = rem;
+          const uint32_t kk = s + lane;
+          valid = lane < n;
+          if (valid) {
+            const uint2 r = R[kk];
+            pos = r.x & POS_MASK;
+            fl = r.x;
+            clen = r.y;
+            end = kk + 1 < nrec ? (R[kk + 1].x & POS_MASK) : cexit;
+          }
+          const uint64_t fm = __ballot(valid && (fl & F_FAIL));
+          if (fm) {  // a FAIL inside: consume up to it, the next round re-parses that struct uncapped
+            n = (uint32_t)__builtin_ctzll(fm);
+            valid = lane < n;
+          }
+          s += n;
+        } else {
+          // the walk's chain does not pass x (or failed there under its cap): parse this struct here
+          uint32_t nx, cl, f2;
+          if (!ln::parse_struct(D, x, len, nx, cl, f2)) { declined = true; why = 8; break; }
+          n = 1;
+          valid = lane == 0;
+          pos = x; end = nx; clen = cl; fl = f2;
+        }
+        // ---- consume n structs: clocks by a wave prefix sum
+        if (__any(valid && clen >= (1u << 24))) { declined = true; why = 9; break; }
+        const uint32_t cl = valid ? clen : 0;
+        const uint32_t incl = wave_incl_add(cl), excl = incl - cl;
+        const uint32_t tot = lane_read(incl, 63);
+        if (clock + tot > 0xffffffffull) { declined = true; why = 10; break; }
+        const bool skip = valid && (fl & F_SKIP);
+        const uint64_t eclk = clock + incl;  // end clock of this lane's struct
+        if (OP == OP_SV) {
+          if (!sv_any) {  // the update's first struct initialises the state
+            sv_any = true;
+            sv_client = client;
+            sv_stop = clock != 0;
+            sv_clock = sv_stop ? 0 : (uint32_t)(clock + lane_read(cl, 0));
+          }
+          const uint64_t skm = __ballot(skip);
+          const uint32_t fs = skm ? (uint32_t)__builtin_ctzll(skm) : n;  // first Skip
+          if (!sv_stop && fs > 0) sv_clock = (uint32_t)(clock + lane_read(incl, fs - 1));
+          if (skm) sv_stop = true;
+        } else {
+          uint32_t first = 0;  // first struct of this batch written verbatim (patch range start)
+          bool pend = false;
+          if (!copying) {
+            const uint64_t cm = __ballot(valid && !skip && eclk > k);
+            if (cm) {
+              const uint32_t f = (uint32_t)__builtin_ctzll(cm);
+              copying = true;
+              written = n - f;
+              const uint64_t fclk = clock + lane_read(excl, f);
+              const uint32_t off = k > fclk ? (uint32_t)(k - fclk) : 0;
+              const uint32_t fpos = lane_read(pos, f), fend = lane_read(end, f), flen = lane_read(cl, f);
+              uint32_t prelen = 0, a0 = 0, a1 = 0, b0;
+              if (off == 0) {
+                b0 = fpos;
+                first = f;
+              } else {
+                if (!slice_head(B, adj, fpos, fend, client, fclk, flen, off, X.pre + ci * PRE, prelen, a0, a1)) {
+                  declined = true;
+                  why = 11;
+                  break;
+                }
+                b0 = fend;
+                first = f + 1;
+              }
+              if (lane == 0) {
+                sec(ci, S_PRELEN) = prelen;
+                sec(ci, S_A0) = a0;
+                sec(ci, S_A1) = a1;
+                sec(ci, S_B0) = b0;
+                sec(ci, S_FCLOCK) = (uint32_t)(fclk + off);
+                sec(ci, S_CLIENT) = client;
+              }
+              pend = true;
+            }
+          } else {
+            written += n;
+            pend = true;
+          }
+          if (pend) {  // info-byte patches of the verbatim structs
+            const bool pl = valid && lane >= first && (fl & F_PATCH);
+            const uint64_t pm = __ballot(pl);
+            if (pm) {
+              const uint32_t np = __popcll(pm);
+              if (npatch + np > NPATCH) { declined = true; why = 12; break; }
+              if (pl) {
+                const uint32_t slot = npatch + __popcll(pm & ((1ull << lane) - 1));
+                const uint32_t info = D[pos];
+                const bool gc = (info & 31) == 0;
+                at<uint32_t>(L_PPOS + 4 * slot) = pos;
+                at<uint32_t>(L_PSEC + 4 * slot) = ci;
+                sm[L_PVAL + slot] = (uint8_t)(gc ? 0 : info & ~0x20u);
+              }
+              npatch += np;
+            }
+          }
+        }
+        clock += tot;
+        x = lane_read(end, n - 1);
+        rem -= n;
+      }
+      if (declined) break;
+      if (OP == OP_DIFF) {
+        if (lane == 0) {
+          sec(ci, S_B1) = copying ? x : 0;
+          sec(ci, S_WRITTEN) = written;
+          if (!copying) sec(ci, S_PRELEN) = NONE;
+        }
+        nparts += copying;
+      }
+    }
+    if (declined) PW_DECLINE()
+    __syncthreads();
+    if (OP == OP_SV) {
+      if (sv_any && sv_clock != 0) {
+        if (sv_n >= NSV) PW_DECLINE_R(13)
+        if (lane == 0) { X.svt[2 * sv_n] = sv_client; X.svt[2 * sv_n + 1] = sv_clock; }
+        sv_n++;
+      }
+      __threadfence_block();
+      __syncthreads();
+      uint32_t tl = 0;
+      for (uint32_t i = lane; i < sv_n; i += 64) tl += vsz(X.svt[2 * i]) + vsz(X.svt[2 * i + 1]);
+      const uint32_t total = vsz(sv_n) + lane_read(wave_incl_add(tl), 63);
+      uint64_t base = 0;
+      if (lane == 0) base = atomicAdd((unsigned long long *)j.used, (unsigned long long)total);
+      base = ((uint64_t)lane_read((uint32_t)(base >> 32), 0) << 32) | lane_read((uint32_t)base, 0);
+      if (lane == 0) { done[d] = 1; atomicAdd((unsigned long long *)j.pw_count, 1ull); }
+      if (base + total > j.cap) {
+        if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }
+        __syncthreads();
+        continue;
+      }
+      if (lane == 0) {
+        uint8_t *o = j.out + base;
+        uint32_t p = put_vu_g(o, 0, sv_n);
+        for (uint32_t i = 0; i < sv_n; i++) { p = put_vu_g(o, p, X.svt[2 * i]); p = put_vu_g(o, p, X.svt[2 * i + 1]); }
+        j.out_off[d] = base;
+        j.out_len[d] = total;
+        j.status[d] = ym::ST_OK;
+      }
+      __syncthreads();
+      continue;
+    }
+    // ---- delete set: validated (readDeleteSet), then copied verbatim
+    const uint32_t ds0 = x;
+    {
+      ln::LCur c = ln::make(D, x, len);
+      const uint32_t ndc = ln::rvu(c);
+      x = c.p;
+      declined = c.bad;
+      why = 17;
+      for (uint32_t i = 0; i < ndc && !declined; i++) {
+        ln::LCur h = ln::make(D, x, len);
+        const uint32_t client = ln::rvu(h);
+        const uint32_t m = ln::rvu(h);
+        x = h.p;
+        // readDeleteSet drops clients without ranges and merges a repeated client into its first
+        // occurrence: either makes the re-written set differ from the input bytes
+        if (h.bad || m == 0 || i >= BS_NDSC) { declined = true; why = 14; break; }
+        if (seen_before(X.dsc, i, client)) { declined = true; why = 15; break; }
+        if (lane == 0) X.dsc[i] = client;
+        __threadfence_block();
+        x = skip_varuints(D, x, len, 2ull * m);
+        if (x == NONE) { declined = true; why = 16; break; }
+      }
+    }
+    if (declined) PW_DECLINE()
+    why = 0;
+    const uint32_t ds1 = x;
+    __threadfence_block();
+    __syncthreads();
+    // ---- sizes, allocation
+    uint32_t tl = 0;
+    for (uint32_t ci = lane; ci < nclients; ci += 64) {
+      const uint32_t pl = sec(ci, S_PRELEN);
+      if (pl == NONE) continue;
+      tl += vsz(sec(ci, S_WRITTEN)) + vsz(sec(ci, S_CLIENT)) + vsz(sec(ci, S_FCLOCK)) + pl + (sec(ci, S_A1) - sec(ci, S_A0)) +
+            (sec(ci, S_B1) - sec(ci, S_B0));
+    }
+    const uint64_t total = vsz(nparts) + (uint64_t)(ds1 - ds0) + lane_read(wave_incl_add(tl), 63);
+    uint64_t base = 0;
+    if (lane == 0) base = atomicAdd((unsigned long long *)j.used, (unsigned long long)total);
+    base = ((uint64_t)lane_read((uint32_t)(base >> 32), 0) << 32) | lane_read((uint32_t)base, 0);
+    if (lane == 0) { done[d] = 1; atomicAdd((unsigned long long *)j.pw_count, 1ull); }
+    if (base + total > j.cap) {
+      if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }
+      __syncthreads();
+      continue;
+    }
+    // ---- write: small pieces by lane 0, spans by the wave, then the info patches
+    uint8_t *const o = j.out + base;
+    if (lane == 0) put_vu_g(o, 0, nparts);
+    uint32_t p = vsz(nparts);
+    for (uint32_t ci = 0; ci < nclients; ci++) {
+      const uint32_t pl = sec(ci, S_PRELEN);
+      if (pl == NONE) continue;
+      const uint32_t written = sec(ci, S_WRITTEN), client = sec(ci, S_CLIENT), fclock = sec(ci, S_FCLOCK);
+      if (lane == 0) {
+        uint32_t t = put_vu_g(o, p, written);
+        t = put_vu_g(o, t, client);
+        t = put_vu_g(o, t, fclock);
+        for (uint32_t b = 0; b < pl; b++) o[t + b] = X.pre[ci * PRE + b];
+      }
+      p += vsz(written) + vsz(client) + vsz(fclock) + pl;
+      const uint32_t a0 = sec(ci, S_A0), a1 = sec(ci, S_A1);
+      copy_bytes(o + p, D + a0, a1 - a0);
+      p += a1 - a0;
+      const uint32_t b0 = sec(ci, S_B0), b1 = sec(ci, S_B1);
+      copy_bytes(o + p, D + b0, b1 - b0);
+      if (lane == 0) sec(ci, S_OUTB) = p - b0;  // output position = document position + S_OUTB
+      p += b1 - b0;
+    }
+    copy_bytes(o + p, D + ds0, ds1 - ds0);
+    __threadfence();  // the patches below overwrite bytes other lanes stored
+    __syncthreads();
+    for (uint32_t i = lane; i < npatch; i += 64) {
+      const uint32_t pos = at<uint32_t>(L_PPOS + 4 * i);
+      const uint32_t ci = at<uint32_t>(L_PSEC + 4 * i);
+      o[sec(ci, S_OUTB) + pos] = sm[L_PVAL + i];
+    }
+    if (lane == 0) {
+      j.out_off[d] = base;
+      j.out_len[d] = total;
+      j.status[d] = ym::ST_OK;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace pw
+
+#define PWCHK(x)                                  \
+  do {                                            \
+    hipError_t e_ = (x);                          \
+    if (e_ != hipSuccess) return -(int)e_ - 1000; \
+  } while (0)
+
+namespace {
+int pw_ensure(PwBufs &B, int k, size_t n) {
+  if (n <= B.cap[k]) return 0;
+  if (B.p[k]) hipFree(B.p[k]);
+  B.p[k] = nullptr;
+  B.cap[k] = 0;
+  const size_t want = n + n / 8 + 4096;
+  if (hipMalloc(&B.p[k], want) != hipSuccess) return -1;
+  B.cap[k] = want;
+  return 0;
+}
+}  // namespace
+
+// Runs the chunk-parallel walk + stitch over the large single-update documents of a V1 diff / sv call.
+// Documents it completes are marked in `*done_out` (k_big_v1 skips them).  Returns 1 when launched, 0
+// when not applicable (no large document, or the record buffer could not be allocated), < 0 on error.
+const uint8_t *pw_last_done = nullptr;
+int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const uint8_t **done_out) {
+  using namespace pw;
+  *done_out = nullptr;
+  if (j.v2 || (op != OP_DIFF && op != OP_SV) || j.n == 0 || !j.pw_count || getenv("YMERGE_NO_PW")) return 0;
+  // YMERGE_PW_MIN: smallest update taken (tests push small golden cases through this path)
+  uint64_t pw_min = PW_MIN;
+  if (const char *e = getenv("YMERGE_PW_MIN")) pw_min = strtoull(e, nullptr, 10);
+  if (!B.pinned && hipHostMalloc((void **)&B.pinned, 64, hipHostMallocDefault) != hipSuccess) return -2;
+  const uint32_t n1 = j.n + 1;
+  if (pw_ensure(B, 0, 8ull * n1 + 16 + j.n)) return -2;
+  uint32_t *cnt = (uint32_t *)B.p[0], *cbase = cnt + n1;
+  uint8_t *done = (uint8_t *)(cbase + n1);
+  k_pw_prep<<<(n1 + 255) / 256, 256, 0, st>>>(j, cnt, done, pw_min);
+  size_t tmp = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cnt, cbase, n1, st);
+  if (pw_ensure(B, 1, tmp + 16)) return -2;
+  PWCHK(hipcub::DeviceScan::ExclusiveSum(B.p[1], tmp, cnt, cbase, n1, st));
+  PWCHK(hipMemcpyAsync(B.pinned, cbase + j.n, 4, hipMemcpyDeviceToHost, st));
+  PWCHK(hipStreamSynchronize(st));
+  const uint32_t total = B.pinned[0];
+  *done_out = done;  // every document is marked (0 = not taken) from here on
+  pw_last_done = done;
+  if (total == 0) return 1;
+  if (pw_ensure(B, 2, 16ull * total) || pw_ensure(B, 3, 8ull * CAP * total)) {
+    // no room for the records: leave every document to k_big_v1
+    hipMemsetAsync(done, 0, j.n, st);
+    return 1;
+  }
+  uint4 *sums = (uint4 *)B.p[2];
+  uint2 *recs = (uint2 *)B.p[3];
+  k_pw_walk<<<(total + 255) / 256, 256, 0, st>>>(j, cbase, j.n, total, sums, recs);
+  const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
+  if (op == OP_DIFF) k_pw_stitch<OP_DIFF><<<grid, 64, LDS_BYTES, st>>>(j, cbase, sums, recs, done);
+  else k_pw_stitch<OP_SV><<<grid, 64, LDS_BYTES, st>>>(j, cbase, sums, recs, done);
+  return 1;
+}
+
+}  // namespace ymk
+
+// debugging aid (not part of include/ymerge.h): the last chunk-walk call's per-document outcome on the
+// calling thread's device, 1 = completed, >= 2 = the decline reason (k_pw_stitch's `why`)
+extern "C" int ym__pw_reasons(uint8_t *host, uint32_t n) {
+  return ymk::pw_last_done ? (int)hipMemcpy(host, ymk::pw_last_done, n, hipMemcpyDeviceToHost) : -1;
+}

@@ -87,7 +87,7 @@ class _Stats(ctypes.Structure):
     _fields_ = [("docs", ctypes.c_uint64), ("docs_fast", ctypes.c_uint64), ("docs_general", ctypes.c_uint64),
                 ("docs_error", ctypes.c_uint64), ("bytes_in", ctypes.c_uint64), ("bytes_out", ctypes.c_uint64),
                 ("device_ms", ctypes.c_double), ("fast_ms", ctypes.c_double), ("general_ms", ctypes.c_double),
-                ("docs_large", ctypes.c_uint64), ("large_ms", ctypes.c_double)]
+                ("docs_large", ctypes.c_uint64), ("large_ms", ctypes.c_double), ("docs_chunked", ctypes.c_uint64)]
 
 
 EXPORTS = ("ym_init", "ym_shutdown", "ym_strerror", "ym_out_bound", "ym_merge", "ym_diff", "ym_sv", "ym_convert",
