@@ -96,6 +96,28 @@ def test_c3_diff_random_svs(engine, fmt):
         assert engine.stats["docs_chunked"] == engine.stats["docs"], engine.stats
 
 
+def test_lane_parser_short_cut_agrees(engine):
+    """The chunk walk's branch-free short cut (ym_lane.h parse_fast) decides most structs; wherever it
+    decides -- at every byte position of real V1 updates (C3, merged C2 / C5 / C4 documents) and of random
+    bytes -- it must agree with the full parser exactly (next position, clock length, flags)."""
+    import ctypes
+    from yjs_amd import pack_docs
+    bufs = [load_ymb("c3_v1")[0].tobytes()]
+    for name in ("c2_v1", "c5_v1", "c4_v1"):
+        a, o, d = load_ymb(name)
+        docs = [[a[int(o[u]):int(o[u + 1])].tobytes() for u in range(int(d[i]), int(d[i + 1]))] for i in range(2)]
+        ma, mo, ml, mst = engine.run_host("merge", 1, *pack_docs(docs))
+        bufs += [ma[int(mo[i]):int(mo[i]) + int(ml[i])].tobytes() for i in range(2)]
+    bufs.append(np.random.default_rng(1).integers(0, 256, 1 << 20, dtype=np.uint8).tobytes())
+    decided = 0
+    for b in bufs:
+        out = (ctypes.c_ulonglong * 2)()
+        assert engine.lib.ym__lane_selftest(b, ctypes.c_uint32(len(b)), out) == 0
+        assert out[1] == 0, (len(b), out[0], out[1])
+        decided += out[0]
+    assert decided > 100000
+
+
 def test_c3_damaged_updates_chunked_walk(engine):
     """Truncated and byte-flipped C3 updates through the chunk-parallel walk: wherever the damage lands
     (struct section, a string, the delete set) the result must be the oracle's -- the same bytes or the

@@ -11,3 +11,4 @@ python -c "
 import json; d=json.loads(open('gpurun_out/bench_pw.json').read().strip().splitlines()[-1])
 for k,v in d.get('secondary',{}).items(): print(k, v)
 "
+if [ -n "$PROF" ]; then TAG=${PROF} bash tools/gpu_prof_pw.sh; fi

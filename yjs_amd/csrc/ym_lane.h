@@ -212,7 +212,7 @@ __device__ __forceinline__ bool item_body(LCur &c, uint32_t info, uint32_t &len)
   len = 1;
   switch (info & 31) {
     case 1: len = rvu(c); break;
-    case 3: { const uint32_t n = rvu(c); if (!room(c, n)) c.bad = true; else skip(c, n); break; }
+    case 3: { const uint32_t n = rvu(c); if (!room(c, n) || n > c.cap) c.bad = true; else skip(c, n); break; }
     case 4: len = rstr(c); break;
     case 5: json_lit(c); break;
     case 6: rstr(c); json_lit(c); break;
@@ -238,12 +238,12 @@ constexpr uint32_t F_SKIP = 1u << 29;   // a Skip (info 10)
 constexpr uint32_t F_PATCH = 1u << 30;  // the writer re-encodes the info byte differently (0x20 cleared / GC := 0)
 constexpr uint32_t POS_MASK = (1u << 28) - 1;
 
-// One V1 struct at p (GC / Skip / Item, readClientsStructRefs' cases): on success `next` is the position
-// after it, `len` its clock length and `fl` its flags.  `cap` bounds string / ContentAny lengths (the
-// speculative walk's parse of a position that may not start a struct; the stitch re-parses uncapped).
-__device__ __forceinline__ bool parse_struct(const uint8_t *b, uint32_t p, uint32_t e, uint32_t &next, uint32_t &len,
-                                             uint32_t &fl, uint32_t cap = 0xffffffffu) {
-  LCur c = make(b, p, e, cap);
+// One V1 struct at the cursor (GC / Skip / Item, readClientsStructRefs' cases): on success the cursor
+// is after it (its register window still valid, so a walk carries it to the next struct), `len` is its
+// clock length and `fl` its flags.  The cursor's `cap` bounds string / ContentAny lengths (a speculative
+// parse of a position that may not start a struct; the stitch re-parses uncapped).
+__device__ __forceinline__ bool parse_at(LCur &c, uint32_t &len, uint32_t &fl) {
+  c.bad = false;
   const uint32_t info = rdb(c);
   const bool sk = info == 10, gc = !sk && (info & 31) == 0;
   bool ok;
@@ -256,8 +256,105 @@ __device__ __forceinline__ bool parse_struct(const uint8_t *b, uint32_t p, uint3
   ok = ok && !c.bad && c.p <= c.e;
   const uint32_t ni = sk ? info : gc ? 0 : ((info & 0xC0) ? info & ~0x20u : info);
   fl = (sk ? F_SKIP : 0) | (ni != info ? F_PATCH : 0);
+  return ok;
+}
+__device__ __forceinline__ bool parse_struct(const uint8_t *b, uint32_t p, uint32_t e, uint32_t &next, uint32_t &len,
+                                             uint32_t &fl, uint32_t cap = 0xffffffffu) {
+  LCur c = make(b, p, e, cap);
+  const bool ok = parse_at(c, len, fl);
   next = c.p;
   return ok;
+}
+
+// Branch-free short cut for the commonest structs, from one 32-byte window at p: GC / Skip, and Items with
+// an origin whose content is ContentDeleted or an ASCII ContentString (C3: ~all structs) whose varuints
+// end in the first 16 bytes and whose string ends inside the window.  Works on byte masks (bit 7 of each
+// byte of a u64): varuint ends are the stop bytes, found by clearing the lowest set bit; overlong ends
+// (a 0x00 after a continuation byte) by one SWAR mask; 5-byte varuints are left to the full parser.
+// Returns true with next / len / fl exactly as parse_at would; false = not decided here (the caller runs
+// parse_at, which also gives every rejection its exact meaning).
+__device__ __forceinline__ uint64_t lowbytes(uint32_t n) { return n >= 8 ? ~0ull : (1ull << (8 * n)) - 1; }
+__device__ __forceinline__ bool parse_fast(const uint8_t *b, uint32_t p, uint32_t e, uint32_t &next, uint32_t &len,
+                                           uint32_t &fl) {
+  if (p + 32 > e) return false;
+  typedef uint4 __attribute__((aligned(1))) u4a;
+  const uint4 A = *reinterpret_cast<const u4a *>(b + p), Bq = *reinterpret_cast<const u4a *>(b + p + 16);
+  constexpr uint64_t H = 0x8080808080808080ull, L7 = 0x7f7f7f7f7f7f7f7full;
+  const uint64_t w0 = ((uint64_t)A.y << 32) | A.x, w1 = ((uint64_t)A.w << 32) | A.z;
+  const uint64_t w2 = ((uint64_t)Bq.y << 32) | Bq.x, w3 = ((uint64_t)Bq.w << 32) | Bq.z;
+  const uint32_t info = A.x & 0xffu, ref = info & 31;
+  const bool sk = info == 10, gc = !sk && ref == 0;
+  const bool item = (info & 0xC0) != 0 && (ref == 1 || ref == 4);
+  const uint32_t V = (sk || gc) ? 1 : 1 + 2 * ((info >> 7) & 1) + 2 * ((info >> 6) & 1);
+  // stop bytes of bytes 1..15 (the info byte is not part of a varuint)
+  uint64_t s0 = ~w0 & H & ~0x80ull, s1 = ~w1 & H;
+  uint64_t E0 = 0, E1 = 0;  // the first V stop bytes
+  uint32_t ev = 0, ep = 0, prev = 0, longest = 0;
+#pragma unroll
+  for (uint32_t t = 1; t <= 5; t++) {
+    const uint64_t l0 = s0 & (0 - s0), l1 = s0 ? 0 : s1 & (0 - s1);
+    const uint32_t et = s0 ? (uint32_t)__builtin_ctzll(s0) >> 3 : s1 ? 8 + ((uint32_t)__builtin_ctzll(s1) >> 3) : 16;
+    if (t <= V) {
+      E0 |= l0;
+      E1 |= l1;
+      longest = et - prev > longest ? et - prev : longest;
+      prev = et;
+    }
+    if (t == V - 1) ep = et;
+    if (t == V) ev = et;
+    s0 ^= l0;
+    s1 ^= l1;
+  }
+  if (!(sk || gc || item) || ev >= 16 || longest >= 5) return false;
+  // overlong: a zero stop byte right after a continuation byte (the info byte does not count)
+  const uint64_t z0 = ~(((w0 & L7) + L7) | w0) & H, z1 = ~(((w1 & L7) + L7) | w1) & H;
+  const uint64_t c0 = ((w0 & ~0xffull) << 8) & H, c1 = ((w1 << 8) | (w0 >> 56)) & H;
+  if ((E0 & z0 & c0) | (E1 & z1 & c1)) return false;
+  // the last varuint's value (bytes ep+1 .. ev, at most 4)
+  const uint32_t o = ep + 1;
+  const uint64_t x = o == 0 ? w0 : o < 8 ? (w0 >> (8 * o)) | (w1 << (64 - 8 * o)) : w1 >> (8 * (o - 8));
+  const uint32_t lo = (uint32_t)x;
+  const uint32_t nb = ev - ep;
+  const uint32_t v = ((lo & 0x7fu) | ((lo >> 1) & 0x3f80u) | ((lo >> 2) & 0x1fc000u) | ((lo >> 3) & 0xfe00000u)) &
+                     ((1u << (7 * nb)) - 1);
+  uint32_t end = ev + 1;
+  if (ref == 4 && item) {  // ASCII string ending inside the window
+    if (v == 0 || ev + v >= 32) return false;
+    const uint32_t a0 = ev + 1, a1 = a0 + v;  // string bytes [a0, a1)
+    uint64_t na = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint64_t wk = k == 0 ? w0 : k == 1 ? w1 : k == 2 ? w2 : w3;
+      const uint32_t lo_b = a0 > 8 * k ? a0 - 8 * k : 0, hi_b = a1 > 8 * k ? a1 - 8 * k : 0;
+      na |= wk & H & lowbytes(hi_b) & ~lowbytes(lo_b);
+    }
+    if (na) return false;
+    end += v;
+  } else if (ref == 1 && item && v == 0) {
+    return false;
+  }
+  next = p + end;
+  len = v;
+  const uint32_t ni = sk ? info : gc ? 0 : info & ~0x20u;
+  fl = (sk ? F_SKIP : 0) | (ni != info ? F_PATCH : 0);
+  return true;
+}
+
+// First position >= q (and < lim, else lim) whose byte could start a struct parse_fast accepts: a Skip
+// (10), a GC (ref 0), or ContentDeleted / ContentString (ref 1 / 4) with an origin bit.  SWAR over 8
+// bytes per step; a byte-wise false positive only costs an extra attempt, none is missed.
+__device__ __forceinline__ uint32_t next_cand(const uint8_t *b, uint32_t q, uint32_t lim) {
+  for (uint32_t it = 0; it < 8 && q < lim; it++, q += 8) {
+    const uint64_t x = ld8(b, q);
+    const uint64_t r = x & 0x1f1f1f1f1f1f1f1full;
+    const uint64_t org = (x | (x << 1)) & 0x8080808080808080ull;  // bit 7 or bit 6 set
+    const uint64_t m = has_byte(x, 10) | has_byte(r, 0) | ((has_byte(r, 1) | has_byte(r, 4)) & org);
+    if (m) {
+      const uint32_t c = q + (__builtin_ctzll(m) >> 3);
+      return c < lim ? c : lim;
+    }
+  }
+  return q < lim ? q : lim;
 }
 
 }  // namespace ln

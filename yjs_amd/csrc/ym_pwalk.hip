@@ -43,7 +43,13 @@ using sc::SCur;
 
 constexpr uint32_t CH = 1024;          // chunk bytes (one walking lane each)
 constexpr uint32_t CAP = CH / 2 + 8;   // records per chunk (a struct is >= 2 bytes; FAIL runs on top: overflow)
-constexpr uint32_t SPEC_CAP = 2048;    // longest string / ContentAny a speculative parse accepts
+// longest string / binary / ContentAny a speculative parse accepts: a larger length read at a position
+// that does not start a struct would make the lane jump over the true chain (C3: with no cap on binaries
+// 3 % of the chunks never re-synchronised; with 64 the walk meets the true chain after 7 bytes on average,
+// 31 at p99).  Longer true contents are re-parsed uncapped by the stitch.
+constexpr uint32_t SPEC_CAP = 64;
+constexpr uint32_t NFIRST = 8;         // records per chunk descriptor (the stitch's entry lookup)
+constexpr uint32_t FAIL_RUN = 8;       // failed positions in a row before the walk only tries short-cut candidates
 constexpr uint64_t PW_MIN = 32768;     // smaller updates stay on k_big_v1
 constexpr uint32_t NSEC = BS_NSEC, NSV = BS_NSV, PRE = BS_PRE, SECW = BS_SECW;
 constexpr uint32_t NPATCH = 1024;
@@ -64,6 +70,19 @@ __device__ __forceinline__ Scr scratch(const GeneralJob &j) {
 }
 #define sec(ci, f) X.sec[SECW * (ci) + (f)]
 
+// stitch path counters (build with -DYM_PW_PROF; read with ym__pw_prof): [0] chunks consumed whole from
+// their entry, [1] entry found but the chunk not whole, [2] entry not among the first records, [3] record
+// batches, [4] structs re-parsed by the stitch, [5] record search loads
+__device__ unsigned long long pw_prof[8];
+#ifdef YM_PW_PROF
+#define PWP(i) do { if (threadIdx.x == 0) atomicAdd(&pw_prof[i], 1ull); } while (0)
+#else
+#define PWP(i) do { } while (0)
+#endif
+// Record k of chunk g.  Chunks are grouped by 64 (one walking wave) with the records interleaved, so a
+// wave's store of its lanes' k-th records is 512 contiguous bytes (whole cache lines: lane-strided 8-byte
+// stores left partial lines that cost a read-modify-write each).
+__device__ __forceinline__ uint64_t rec_idx(uint32_t g, uint32_t k) { return ((uint64_t)(g >> 6) * CAP + k) * 64 + (g & 63); }
 // ---- 0. eligibility and chunk counts ---------------------------------------------------------------
 __global__ void k_pw_prep(GeneralJob j, uint32_t *cnt, uint8_t *done, uint64_t pw_min) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
@@ -81,8 +100,13 @@ __global__ void k_pw_prep(GeneralJob j, uint32_t *cnt, uint8_t *done, uint64_t p
 }
 
 // ---- 1. speculative chunk walk ----------------------------------------------------------------------
+// Records: (position | flags, clock sum of the chunk walk's records before this one).  Chunk descriptor
+// (5 x 16 B): {nrec | lastfail << 16, lastpatch | lastskip << 16, exit, clock sum at exit}, then the
+// first NFIRST records' position words and clock sums (the stitch's entry lookup needs no record load).
+// last* = index + 1 of the last FAIL / patched / Skip record (0: none); lastfail also counts a struct of
+// >= 2^21 clocks (clock sums over the chunk could wrap): the stitch takes such records one by one.
 __global__ void __launch_bounds__(256) k_pw_walk(GeneralJob j, const uint32_t *cbase, uint32_t nd, uint32_t total,
-                                                 uint4 *sums, uint2 *recs) {
+                                                 uint4 *desc, uint2 *recs) {
   const uint32_t g = blockIdx.x * 256 + threadIdx.x;
   if (g >= total) return;
   uint32_t lo = 0, hi = nd - 1;  // the document: largest d with cbase[d] <= g
@@ -96,20 +120,51 @@ __global__ void __launch_bounds__(256) k_pw_walk(GeneralJob j, const uint32_t *c
   const uint32_t len = (uint32_t)(j.upd_off[u0 + 1] - ub);
   const uint8_t *D = j.A + ub;
   const uint32_t c0 = ci * CH, c1 = c0 + CH < len ? c0 + CH : len;
-  uint2 *R = recs + (uint64_t)g * CAP;
-  uint32_t p = c0, nrec = 0, ovf = 0;
-  bool frun = false;
+  uint32_t nrec = 0, cum = 0, lastfail = 0, lastpatch = 0, lastskip = 0, fails = 0, okrun = 0;
+  bool frun = false, ovf = false;
+  uint32_t p = c0;
   while (p < c1) {
-    uint32_t nx, cl, fl;
-    const bool ok = ln::parse_struct(D, p, len, nx, cl, fl, SPEC_CAP);
-    if (ok || !frun) {
-      if (nrec == CAP) { ovf = 1; break; }
-      R[nrec++] = make_uint2(p | (ok ? fl : F_FAIL), ok ? cl : 0u);
+    uint32_t cl, fl, nx;
+    bool ok = ln::parse_fast(D, p, len, nx, cl, fl);  // branch-free short cut (most structs)
+#ifdef YM_PW_PROF
+    atomicAdd(&pw_prof[ok ? 6 : fails < FAIL_RUN ? 7 : 5], 1ull);
+#endif
+    if (!ok && fails < FAIL_RUN) {
+      ln::LCur c = ln::make(D, p, len, SPEC_CAP);
+      ok = ln::parse_at(c, cl, fl);
+      nx = c.p;
     }
+    if (ok || !frun) {
+      if (nrec == CAP) { ovf = true; break; }  // overflow: the stitch re-parses this chunk
+      recs[rec_idx(g, nrec)] = make_uint2(p | (ok ? fl : F_FAIL), cum);
+      nrec++;
+      // a FAIL, or a struct of >= 2^21 clocks (clock sums over the chunk could wrap): the stitch takes
+      // the records from the entry up to here one by one
+      if (!ok || cl >= (1u << 21)) lastfail = nrec;
+      if (ok && (fl & F_PATCH)) lastpatch = nrec;
+      if (ok && (fl & F_SKIP)) lastskip = nrec;
+    }
+    cum += ok ? cl : 0;
+    // back to trying every position only after two structs in a row (a lone garbage GC in a delete set
+    // would otherwise restart the run of full parses)
+    okrun = ok ? okrun + 1 : 0;
+    fails = ok ? (okrun >= 2 ? 0 : fails) : fails + 1;
+    // a long run of non-struct bytes (the delete set, a long content): only positions the short cut could
+    // accept are tried from there on -- the full parser at every byte of a 100 KB delete set cost more
+    // than the whole struct section
+    p = ok ? nx : fails < FAIL_RUN ? p + 1 : ln::next_cand(D, p + 1, c1);
     frun = !ok;
-    p = ok ? nx : p + 1;
   }
-  sums[g] = make_uint4(ovf ? 0u : nrec, p, ovf, 0u);  // an overflowed chunk is re-parsed by the stitch
+  if (ovf) nrec = 0;
+  uint2 f[NFIRST];  // the first records, read back (this lane's own stores)
+#pragma unroll
+  for (uint32_t k = 0; k < NFIRST; k++) f[k] = k < nrec ? recs[rec_idx(g, k)] : make_uint2(POS_MASK, 0u);
+  uint4 *Q = desc + 5ull * g;
+  Q[0] = make_uint4(nrec | (lastfail << 16), lastpatch | (lastskip << 16), p, cum);
+  Q[1] = make_uint4(f[0].x, f[1].x, f[2].x, f[3].x);
+  Q[2] = make_uint4(f[4].x, f[5].x, f[6].x, f[7].x);
+  Q[3] = make_uint4(f[0].y, f[1].y, f[2].y, f[3].y);
+  Q[4] = make_uint4(f[4].y, f[5].y, f[6].y, f[7].y);
 }
 
 // ---- 2. stitch ----------------------------------------------------------------------------------------
@@ -217,36 +272,44 @@ __device__ bool slice_head(sc::cu32 *B, uint32_t adj, uint32_t s0, uint32_t s1, 
   return true;
 }
 
+// 16 bytes at q (bytes at or past e read as 0x80: no stop byte)
+__device__ __forceinline__ uint4 load16m(const uint8_t *D, uint32_t q, uint32_t e) {
+  if (q + 16 <= e) return *reinterpret_cast<const u4u *>(D + q);
+  uint8_t b[16];
+  for (uint32_t k = 0; k < 16; k++) b[k] = q + k < e ? D[q + k] : 0x80;
+  uint4 v;
+  __builtin_memcpy(&v, b, 16);
+  return v;
+}
 // Validates `cnt` canonical varuints (u32, lib0 readVarUint) starting at x, wave-parallel: 1 KB per
-// step, 16 bytes per lane, stop bytes counted by a wave prefix sum.  Returns the position after the
-// last one, or NONE (truncated / non-canonical).
+// step (16 bytes per lane, the next step's bytes loaded while this one is checked), stop bytes counted
+// by a wave prefix sum, the continuation run entering each lane taken from its left neighbour.  Returns
+// the position after the last one, or NONE (truncated / non-canonical).
 __device__ uint32_t skip_varuints(const uint8_t *D, uint32_t x, uint32_t e, uint64_t cnt) {
   const uint32_t lane = threadIdx.x;
-  const uint32_t xs = x;  // the first varuint's start: bytes before it are not part of the sequence
+  uint32_t carry = 0;  // continuation bytes at the end of the previous step (16 = at least 16)
+  uint4 cur = load16m(D, x + 16 * lane, e);
   while (cnt > 0) {
     if (x >= e) return NONE;
+    const uint4 nxt = x + 1024 < e ? load16m(D, x + 1024 + 16 * lane, e) : make_uint4(0, 0, 0, 0);
     const uint32_t q = x + 16 * lane;
     uint8_t b[16];
-    if (q + 16 <= e) {
-      const uint4 v = *reinterpret_cast<const u4u *>(D + q);
-      __builtin_memcpy(b, &v, 16);
-    } else {
-      for (uint32_t k = 0; k < 16; k++) b[k] = q + k < e ? D[q + k] : 0x80;  // past the end: no stop byte
+    __builtin_memcpy(b, &cur, 16);
+    uint32_t nstop = 0, tr = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++) {
+      const bool stop = b[k] < 0x80 && q + k < e;
+      nstop += stop;
+      tr = stop ? 0 : tr + 1;
     }
-    // continuation bytes right before q (inside [xs, q)), up to 5
-    uint32_t run = 0;
-    for (uint32_t k = 1; k <= 5 && q >= xs + k; k++) {
-      if (D[q - k] < 0x80) break;
-      run++;
-    }
-    uint32_t nstop = 0;
-    for (uint32_t k = 0; k < 16; k++) nstop += b[k] < 0x80 && q + k < e;
+    uint32_t run = from_prev_lane(tr);
+    if (lane == 0) run = carry;
     const uint32_t incl = wave_incl_add(nstop), excl = incl - nstop;
     const uint32_t tot = lane_read(incl, 63);
     const uint32_t need = cnt < tot ? (uint32_t)cnt : tot;  // stops consumed by this step
-    // canonical-form checks for this lane's stops of rank < need
     bool bad = false;
     uint32_t rank = excl, endp = 0;
+#pragma unroll
     for (uint32_t k = 0; k < 16; k++) {
       const bool stop = b[k] < 0x80 && q + k < e;
       if (stop && rank < need) {
@@ -262,9 +325,10 @@ __device__ uint32_t skip_varuints(const uint8_t *D, uint32_t x, uint32_t e, uint
       const uint64_t m = __ballot(endp != 0);
       return lane_read(endp, __builtin_ctzll(m));
     }
-    // an unfinished varuint at the end of this step may not exceed 5 bytes either (checked next step
-    // through `run`)
     cnt -= tot;
+    carry = lane_read(tr == 16 ? 16 + carry : tr, 63);  // a run may continue across the step boundary
+    if (carry > 16) carry = 16;
+    cur = nxt;
     x += 1024;
   }
   return x;
@@ -281,7 +345,7 @@ __device__ uint32_t skip_varuints(const uint8_t *D, uint32_t x, uint32_t e, uint
 
 // OP = OP_DIFF or OP_SV
 template <int OP>
-__global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *cbase, const uint4 *sums, const uint2 *recs,
+__global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *cbase, const uint4 *desc, const uint2 *recs,
                                                   uint8_t *done) {
   const uint32_t lane = threadIdx.x;
   const Scr X = scratch(j);
@@ -330,9 +394,9 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
     uint32_t sv_client = 0, sv_clock = 0, sv_n = 0;
     bool sv_stop = false, sv_any = false;
     uint32_t prev_client = 0;
-    // chunk cursor: current chunk, its record count / exit, the next record index
-    uint32_t cc = NONE, nrec = 0, cexit = 0, s = 0;
-    const uint2 *R = nullptr;
+    // chunk cursor: the current chunk and the next record index in it; descriptors of chunks [wb, wb + 64)
+    uint32_t cc = NONE, s = 0, wb = NONE - 64;
+    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0, q4 = q0;
     for (uint32_t ci = 0; ci < nclients && !declined; ci++) {
       uint32_t nstructs, client;
       uint64_t clock;
@@ -360,21 +424,60 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
       uint32_t rem = nstructs;
       while (rem > 0) {
         if (x >= len) { declined = true; why = 7; break; }
-        // ---- locate x among the records of its chunk
         const uint32_t cx = x / CH;
-        if (cx != cc) {
-          cc = cx;
-          const uint4 sm4 = sums[cb + cx];
-          nrec = sm4.x;
-          cexit = sm4.y;
-          s = 0;
-          R = recs + (uint64_t)(cb + cx) * CAP;
+        // ---- chunk descriptors, 64 chunks per load (one lane each)
+        if (cx < wb || cx >= wb + 64) {
+          wb = cx;
+          if (wb + lane < nch) {
+            const uint4 *Q = desc + 5ull * (cb + wb + lane);
+            q0 = Q[0]; q1 = Q[1]; q2 = Q[2]; q3 = Q[3]; q4 = Q[4];
+          }
         }
+        const int di = (int)(cx - wb);
+        const uint32_t w0 = lane_read(q0.x, di), w1 = lane_read(q0.y, di);
+        const uint32_t nrec = w0 & 0xffffu, lfe = w0 >> 16, lpe = w1 & 0xffffu, lse = w1 >> 16;
+        const uint32_t cexit = lane_read(q0.z, di), cumx = lane_read(q0.w, di);
+        if (cx != cc) { cc = cx; s = 0; }
+        const uint32_t gc = cb + cx;
+        // ---- chunk entry: x among the descriptor's first records -> the rest of the chunk in O(1)
+        if (s == 0) {
+          uint32_t fs = NONE, fcum = 0;
+#pragma unroll
+          for (int kf = NFIRST - 1; kf >= 0; kf--) {
+            const uint32_t pwk = lane_read(kf < 4 ? (&q1.x)[kf] : (&q2.x)[kf - 4], di);
+            if ((uint32_t)kf < nrec && (pwk & POS_MASK) == x && !(pwk & F_FAIL)) {
+              fs = (uint32_t)kf;
+              fcum = lane_read(kf < 4 ? (&q3.x)[kf] : (&q4.x)[kf - 4], di);
+            }
+          }
+          if (fs != NONE) {
+            const uint32_t avail = nrec - fs;
+            const uint32_t delta = cumx - fcum;  // clocks of records fs .. nrec-1 (no wrap when lfe <= fs)
+            bool whole = rem >= avail && lfe <= fs;
+            if (OP == OP_DIFF) whole = whole && (copying ? lpe <= fs : clock + delta <= k);
+            if (OP == OP_SV) whole = whole && sv_any && lse <= fs;
+            if (whole) {
+              PWP(0);
+              if (clock + delta > 0xffffffffull) { declined = true; why = 10; break; }
+              if (OP == OP_SV && !sv_stop) sv_clock = (uint32_t)(clock + delta);
+              if (OP == OP_DIFF && copying) written += avail;
+              clock += delta;
+              rem -= avail;
+              x = cexit;
+              s = nrec;
+              continue;
+            }
+            PWP(1);
+            s = fs;
+          } else PWP(2);
+        }
+        // ---- record by record: locate x among the chunk's records (a ballot over 64 per load)
         bool found = false;
         for (;;) {
           if (s >= nrec) break;
+          PWP(5);
           const uint32_t kk = s + lane;
-          const uint32_t pw = kk < nrec ? R[kk].x : POS_MASK;
+          const uint32_t pw = kk < nrec ? recs[rec_idx(gc, kk)].x : POS_MASK;
           const uint64_t lt = __ballot(kk < nrec && (pw & POS_MASK) < x);
           const uint32_t nlt = __popcll(lt);
           if (nlt == 64) { s += 64; continue; }
@@ -388,16 +491,18 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
         uint32_t n, pos = 0, end = 0, clen = 0, fl = 0;
         bool valid;
         if (found) {
+          PWP(3);
           n = nrec - s < 64 ? nrec - s : 64;
           if (rem < n) n = rem;
           const uint32_t kk = s + lane;
           valid = lane < n;
           if (valid) {
-            const uint2 r = R[kk];
+            const uint2 r = recs[rec_idx(gc, kk)];
+            const uint2 r1 = kk + 1 < nrec ? recs[rec_idx(gc, kk + 1)] : make_uint2(cexit, cumx);
             pos = r.x & POS_MASK;
             fl = r.x;
-            clen = r.y;
-            end = kk + 1 < nrec ? (R[kk + 1].x & POS_MASK) : cexit;
+            clen = r1.y - r.y;
+            end = r1.x & POS_MASK;
           }
           const uint64_t fm = __ballot(valid && (fl & F_FAIL));
           if (fm) {  // a FAIL inside: consume up to it, the next round re-parses that struct uncapped
@@ -408,6 +513,7 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
         } else {
           // the walk's chain does not pass x (or failed there under its cap): parse this struct here
           uint32_t nx, cl, f2;
+          PWP(4);
           if (!ln::parse_struct(D, x, len, nx, cl, f2)) { declined = true; why = 8; break; }
           n = 1;
           valid = lane == 0;
@@ -670,17 +776,17 @@ int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const ui
   *done_out = done;  // every document is marked (0 = not taken) from here on
   pw_last_done = done;
   if (total == 0) return 1;
-  if (pw_ensure(B, 2, 16ull * total) || pw_ensure(B, 3, 8ull * CAP * total)) {
+  if (pw_ensure(B, 2, 80ull * total) || pw_ensure(B, 3, 8ull * CAP * ((total + 63) & ~63u))) {
     // no room for the records: leave every document to k_big_v1
     hipMemsetAsync(done, 0, j.n, st);
     return 1;
   }
-  uint4 *sums = (uint4 *)B.p[2];
+  uint4 *desc = (uint4 *)B.p[2];
   uint2 *recs = (uint2 *)B.p[3];
-  k_pw_walk<<<(total + 255) / 256, 256, 0, st>>>(j, cbase, j.n, total, sums, recs);
+  k_pw_walk<<<(total + 255) / 256, 256, 0, st>>>(j, cbase, j.n, total, desc, recs);
   const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
-  if (op == OP_DIFF) k_pw_stitch<OP_DIFF><<<grid, 64, LDS_BYTES, st>>>(j, cbase, sums, recs, done);
-  else k_pw_stitch<OP_SV><<<grid, 64, LDS_BYTES, st>>>(j, cbase, sums, recs, done);
+  if (op == OP_DIFF) k_pw_stitch<OP_DIFF><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done);
+  else k_pw_stitch<OP_SV><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done);
   return 1;
 }
 
@@ -690,4 +796,38 @@ int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const ui
 // calling thread's device, 1 = completed, >= 2 = the decline reason (k_pw_stitch's `why`)
 extern "C" int ym__pw_reasons(uint8_t *host, uint32_t n) {
   return ymk::pw_last_done ? (int)hipMemcpy(host, ymk::pw_last_done, n, hipMemcpyDeviceToHost) : -1;
+}
+namespace ymk {
+namespace pw {
+// parse_fast against parse_struct (uncapped) at every byte position of a buffer: [0] positions the short
+// cut decided, [1] of them disagreeing with the full parser (next, length, flags or acceptance)
+__global__ void k_lane_selftest(const uint8_t *b, uint32_t n, unsigned long long *cnt) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  uint32_t nx, cl, fl, nx2, cl2, fl2;
+  if (!ln::parse_fast(b, p, n, nx, cl, fl)) return;
+  atomicAdd(&cnt[0], 1ull);
+  const bool ok = ln::parse_struct(b, p, n, nx2, cl2, fl2);
+  if (!ok || nx != nx2 || cl != cl2 || fl != fl2) atomicAdd(&cnt[1], 1ull);
+}
+}  // namespace pw
+}  // namespace ymk
+// test hook (not part of include/ymerge.h): runs k_lane_selftest over a host buffer on the current device
+extern "C" int ym__lane_selftest(const uint8_t *host, uint32_t n, unsigned long long *out) {
+  uint8_t *d = nullptr;
+  unsigned long long *c = nullptr;
+  if (hipMalloc(&d, n + 64) != hipSuccess || hipMalloc(&c, 16) != hipSuccess) return -1;
+  hipMemset(d, 0, n + 64);
+  hipMemcpy(d, host, n, hipMemcpyHostToDevice);
+  hipMemset(c, 0, 16);
+  ymk::pw::k_lane_selftest<<<(n + 255) / 256, 256>>>(d, n, c);
+  const int r = (int)hipMemcpy(out, c, 16, hipMemcpyDeviceToHost);
+  hipFree(d);
+  hipFree(c);
+  return r;
+}
+extern "C" int ym__pw_prof(unsigned long long *host, int reset) {
+  int r = (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ymk::pw::pw_prof), 64);
+  if (reset) { unsigned long long z[8] = {}; hipMemcpyToSymbol(HIP_SYMBOL(ymk::pw::pw_prof), z, 64); }
+  return r;
 }
