@@ -33,15 +33,18 @@ def test_golden_batched_on_gpu(engine, key):
     _check_group(engine, key)
 
 
-@pytest.mark.parametrize("key", [("diff", 1), ("sv", 1)], ids=lambda k: f"{k[0]}-v{k[1]}")
+@pytest.mark.parametrize("key", [("diff", 1), ("sv", 1), ("diff", 2), ("sv", 2)], ids=lambda k: f"{k[0]}-v{k[1]}")
 def test_golden_through_chunked_walk(engine, key, monkeypatch):
-    """The chunk-parallel V1 walk (ym_pwalk.hip) normally takes updates of >= 32 KB only; with its
-    threshold at 1 byte every golden diff / state-vector vector goes through it (speculative chunk walk,
-    stitch, fallback to the sequential walker on a decline) and must still come out byte-identical."""
+    """The chunk-parallel V1 walk (ym_pwalk.hip) and the column-parallel V2 path (ym_pv2.hip) normally
+    take updates of >= 32 KB only; with their threshold at 1 byte every golden diff / state-vector vector
+    goes through them (fallback to the sequential walkers on a decline) and must still come out
+    byte-identical."""
     monkeypatch.setenv("YMERGE_PW_MIN", "1")
     _check_group(engine, key)
-    # it accepts exactly what the sequential walker accepts (the rest: non-canonical payloads, errors)
-    assert engine.stats["docs_chunked"] == engine.stats["docs_fast"] > 0, engine.stats
+    if key[1] == 1:  # the V1 walk accepts exactly what the sequential walker accepts
+        assert engine.stats["docs_chunked"] == engine.stats["docs_fast"] > 0, engine.stats
+    else:  # the V2 path: single-section String / Deleted / GC updates
+        assert engine.stats["docs_chunked"] > 0, engine.stats
 
 
 def _check_group(engine, key):

@@ -74,8 +74,8 @@ def test_c3_sv_matches_oracle(engine, fmt):
     bad = _compare(engine.run_host("sv", fmt, a2, o2, d2), outs, st)
     assert not bad, bad[:10]
     assert engine.stats["docs_fast"] == engine.stats["docs"], engine.stats
-    if fmt == 1:  # the chunk-parallel walk takes every 0.9 MB C3 update
-        assert engine.stats["docs_chunked"] == engine.stats["docs"], engine.stats
+    # the chunk-parallel walk (V1) / column-parallel path (V2) takes every C3 update
+    assert engine.stats["docs_chunked"] == engine.stats["docs"], engine.stats
 
 
 @pytest.mark.parametrize("fmt", [1, 2])
@@ -92,8 +92,7 @@ def test_c3_diff_random_svs(engine, fmt):
     bad = _compare(engine.run_host("diff", fmt, a2, o2, d2, sva, svo), outs, st)
     assert not bad, bad[:10]
     assert engine.stats["docs_fast"] == engine.stats["docs"], engine.stats
-    if fmt == 1:
-        assert engine.stats["docs_chunked"] == engine.stats["docs"], engine.stats
+    assert engine.stats["docs_chunked"] == engine.stats["docs"], engine.stats
 
 
 def test_lane_parser_short_cut_agrees(engine):
@@ -118,15 +117,16 @@ def test_lane_parser_short_cut_agrees(engine):
     assert decided > 100000
 
 
-def test_c3_damaged_updates_chunked_walk(engine):
-    """Truncated and byte-flipped C3 updates through the chunk-parallel walk: wherever the damage lands
-    (struct section, a string, the delete set) the result must be the oracle's -- the same bytes or the
-    same exception -- whether the walk declines the document or not."""
-    arena, upd_off, doc_upd = load_ymb("c3_v1")
+@pytest.mark.parametrize("fmt", [1, 2])
+def test_c3_damaged_updates_chunked_walk(engine, fmt):
+    """Truncated and byte-flipped C3 updates through the chunk-parallel walk (V1) / column-parallel path
+    (V2): wherever the damage lands (struct section or columns, a string, the delete set) the result must
+    be the oracle's -- the same bytes or the same exception -- whether the path declines the document or not."""
+    arena, upd_off, doc_upd = load_ymb(f"c3_v{fmt}")
     upd = arena.tobytes()
-    rng = np.random.default_rng(11)
+    rng = np.random.default_rng(11 + fmt)
     docs, svs = [], []
-    svo_full = O.sv_from_update(upd, 1)[1]
+    svo_full = O.sv_from_update(upd, fmt)[1]
     full_svs = random_state_vectors(svo_full, 24, seed=5)
     for i in range(24):
         b = bytearray(upd)
@@ -142,8 +142,8 @@ def test_c3_damaged_updates_chunked_walk(engine):
     sva, svo, _ = pack_docs([[s] for s in svs])
     for op in ("diff", "sv"):
         extra = (sva, svo) if op == "diff" else ()
-        outs, st, _ = O.batch(op, 1, a2, o2, d2, *extra, nthreads=8)
-        bad = _compare(engine.run_host(op, 1, a2, o2, d2, *extra), outs, st)
+        outs, st, _ = O.batch(op, fmt, a2, o2, d2, *extra, nthreads=8)
+        bad = _compare(engine.run_host(op, fmt, a2, o2, d2, *extra), outs, st)
         assert not bad, (op, bad[:10])
 
 

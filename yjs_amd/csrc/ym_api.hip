@@ -23,7 +23,7 @@ __global__ void k_general(GeneralJob j, int pass);
 int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st);  // ym_fast.hip
 int fast2_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st); // ym_fast2.hip
 int big_launch(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &pw);       // ym_big.hip
-int big2_launch(uint32_t op, const GeneralJob &j, hipStream_t st);                   // ym_big2.hip
+int big2_launch(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &pw);      // ym_big2.hip
 __global__ void k_fast_region(GeneralJob j, uint32_t n_upd);                         // ym_fast.hip
 }  // namespace ymk
 
@@ -61,7 +61,7 @@ struct DevState {
   DBuf in_arena, in_off, in_doc, in_sv, in_svoff, out_arena, out_off, out_len, status;  // host staging
   DBuf cmp_off, cmp_len, cmp_arena;  // host batches: outputs packed in document order before the D2H copy
   LargeBufs large;
-  PwBufs pw;
+  PwBufs pw, pw2;
   hipEvent_t evl1 = nullptr;
   uint64_t *pinned = nullptr;   // host memory the finishing kernel writes into (no copy op)
   uint64_t *pinned_dev = nullptr;  // ... its device address
@@ -480,7 +480,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   int fr = fast_launch(op, j, b->n_upd, st);     // V1 merge: LDS fast path
   if (fr == 0) fr = fast2_launch(op, j, b->n_upd, st);  // V2 merge: LDS fast path
   if (fr == 0) fr = big_launch(op, j, st, S->pw);  // V1 diff / state vector: chunk walk + wave walker
-  if (fr == 0) fr = big2_launch(op, j, st);        // V2 diff / state vector: streamed wave walker
+  if (fr == 0) fr = big2_launch(op, j, st, S->pw2); // V2 diff / state vector: column path + wave walker
   if (fr < 0) return fr;
   slots = op == OP_MERGE || (op == OP_DSMERGE && fr == 1);
   HIPCHK(hipEventRecord(S->evf1, st));
@@ -616,8 +616,10 @@ static void release_state(DevState *S) {
   if (S->evl1) hipEventDestroy(S->evl1);
   for (int k = 0; k < 4; k++) if (S->large.p[k]) hipFree(S->large.p[k]);
   if (S->large.pinned) hipHostFree(S->large.pinned);
-  for (int k = 0; k < 4; k++) if (S->pw.p[k]) hipFree(S->pw.p[k]);
-  if (S->pw.pinned) hipHostFree(S->pw.pinned);
+  for (PwBufs *pb : {&S->pw, &S->pw2}) {
+    for (int k = 0; k < 4; k++) if (pb->p[k]) hipFree(pb->p[k]);
+    if (pb->pinned) hipHostFree(pb->pinned);
+  }
   if (S->stream) hipStreamDestroy(S->stream);
   delete S;
 }

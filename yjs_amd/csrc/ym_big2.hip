@@ -81,7 +81,8 @@ __device__ __forceinline__ void s_load(Doc &D, uint32_t s) {
   __syncthreads();
   const uint64_t wa = (D.b0 + pos) & ~15ull;
   const uint64_t eabs = D.b0 + end;
-  const uint32_t n = (uint32_t)(wa + W < eabs ? W : eabs - wa);
+  // (a cursor that overran its stream end after a malformed varuint loads nothing)
+  const uint32_t n = (uint32_t)(wa >= eabs ? 0 : wa + W < eabs ? W : eabs - wa);
   const uint4 *src = reinterpret_cast<const uint4 *>(D.A + wa);
   const uint32_t base = win_lds(s);
   for (uint32_t v = threadIdx.x; v < (n + 15) >> 4; v += 64) at<uint4>(base + 16 * v) = src[v];
@@ -192,7 +193,7 @@ __device__ __forceinline__ void o_vi(Doc &D, uint32_t s, bool neg, uint32_t m) {
 // copies update bytes [a, b) to the end of output stream s (all lanes)
 __device__ __forceinline__ void o_span(Doc &D, uint32_t s, uint32_t a, uint32_t b) {
   const uint32_t cur = ost(s, 1);
-  if (cur + (b - a) > ost(s, 2)) { set_bad(); return; }
+  if (b < a || (uint64_t)cur + (b - a) > ost(s, 2)) { set_bad(); return; }
   uint8_t *dst = D.O + ost(s, 0) + cur;
   const uint8_t *src = D.A + D.b0 + a;
   for (uint32_t i = threadIdx.x; i < b - a; i += 64) dst[i] = src[i];
@@ -386,6 +387,7 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
   const uint32_t lane = threadIdx.x;
   const Scr X = scratch(j);
   for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
+    if (OP != OP_META && j.pw_done && j.pw_done[d] == 1) continue;  // completed by the column-parallel path
     const uint32_t u0 = j.doc_upd[d];
     if (j.doc_upd[d + 1] - u0 != 1) YB2_DECLINE()
     Doc D;
@@ -728,10 +730,13 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
 }  // namespace big2
 
 __global__ void k_big_init(GeneralJob j);  // ym_big.hip
-int big2_launch(uint32_t op, const GeneralJob &j, hipStream_t st) {
-  if (!j.v2 || (op != OP_SV && op != OP_DIFF && op != OP_META)) return 0;
-  if (op == OP_META && j.n > 8 * BS_GRID) return 0;  // many small updates: one thread per update (general)
-  k_big_init<<<1, 64, 0, st>>>(j);
+int big2_launch(uint32_t op, const GeneralJob &j0, hipStream_t st, PwBufs &pwb) {
+  if (!j0.v2 || (op != OP_SV && op != OP_DIFF && op != OP_META)) return 0;
+  if (op == OP_META && j0.n > 8 * BS_GRID) return 0;  // many small updates: one thread per update (general)
+  k_big_init<<<1, 64, 0, st>>>(j0);
+  GeneralJob j = j0;
+  // large single-section updates: the column-parallel path first (ym_pv2.hip); k_big_v2 takes the rest
+  if (int r = pv2_run(op, j0, st, pwb, &j.pw_done); r < 0) return r;
   const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
   if (op == OP_DIFF) big2::k_big_v2<OP_DIFF><<<grid, 64, big2::LDS_BYTES, st>>>(j);
   else if (op == OP_META) big2::k_big_v2<OP_META><<<grid, 64, big2::LDS_BYTES, st>>>(j);

@@ -1,0 +1,917 @@
+// ym_pv2.hip -- column-parallel diffUpdateV2 / encodeStateVectorFromUpdateV2 over large single-section
+// V2 updates (BASELINE configs[2] C3 in V2: one client, ~70 k String / Deleted Items per 0.47 MB update).
+//
+// The V2 encoding spreads every struct over up to nine RLE columns (UpdateEncoder.js:229-408); the
+// sequential walker (ym_big2.hip) advances all of them struct by struct.  Here each column is an
+// independent stream:
+//
+//  K0 k_v2_prep   one thread per document: the header (column spans, the section header), eligibility
+//                 (one update, one client section), the scratch size.
+//  K1 k_v2_dec    one lane per (document, column), a wave = 64 documents of one column kind: the lib0
+//                 RLE decoders (RleDecoder<u8>, UintOptRleDecoder, IntDiffOptRleDecoder) run over the
+//                 whole column, every entry checked to be in the form lib0's encoder writes (canonical
+//                 varints, runs maximal, no -0 diff, diffs < 2^30, parentInfo in {0, 1}, an RLE<u8> column
+//                 ending without a count); info / parentInfo / string lengths / len values are expanded
+//                 into per-value arrays, the others only counted.
+//  K2 k_v2_struct one 256-thread block per document: per struct the values it consumes from every
+//                 column (from its info byte and parentInfo), block prefix sums over the structs give each
+//                 struct's column indices, its clock length and clock; the diff cut is the first struct
+//                 ending past sv[client]; every column must be consumed exactly (as the re-encoding would
+//                 write it).  encodeStateVectorFromUpdateV2 is answered here.
+//  K3 k_v2_splice one lane per (document, column): the cut struct's values, re-encoded (Item.write with
+//                 offset) with the rest of the column entry they share, by the lib0 encoders; the column's
+//                 following entries are then byte-identical to what the encoder would write (the input is
+//                 canonical), so they are copied.
+//  K4 k_v2_out    one wave per document: the delete set validated (readDeleteSet), the output assembled:
+//                 vu(0) | 9 x varUint8Array(column) | vu(#parts) | vu(written) vu(first clock) | delete set.
+//
+// Exactly the documents ym_big2.hip's k_big_v2 accepts among these are taken, with identical bytes;
+// everything else (several clients, Skip / Any / Type / Format / Embed / Binary content, non-ASCII string
+// columns, non-canonical columns) is left to k_big_v2 (and from there to the general path).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "ym_fast_common.h"
+#include "ym_kernels.h"
+#include "ym_lane.h"
+#include "ym_wave_ds.h"
+
+namespace ymk {
+namespace pv2 {
+using namespace fastc;
+
+constexpr uint64_t PV_MIN = 32768;  // smaller updates stay on k_big_v2
+constexpr uint32_t NONE = 0xffffffffu;
+// column kinds decoded by K1 / spliced by K3 (the V2 column index in brackets)
+enum { K_INFO = 0, K_PI, K_SL, K_LN, K_CL, K_LC, K_RC, NK };
+__host__ __device__ constexpr uint32_t col_of(uint32_t k) {  // V2 column order: kc cl lc rc in sl pi tr ln
+  return k == K_INFO ? 4 : k == K_PI ? 6 : k == K_SL ? 5 : k == K_LN ? 8 : k == K_CL ? 1 : k == K_LC ? 2 : 3;
+}
+constexpr uint32_t HB = 64;  // encoded head bytes per (document, column)
+constexpr uint32_t CKSTEP = 64;  // column entries per checkpoint (K3 starts its decode at the last one)
+
+// per-document state, in HBM
+struct Meta {
+  uint32_t ok;                // eligible (K0) and still good
+  uint32_t why;               // where a document was declined (debugging aid, ym__pv2_why)
+  uint32_t col0[9], col1[9];  // column spans (update-relative); the string column's lengths part
+  uint32_t sb0, sn;           // string body [sb0, sb0 + sn)
+  uint32_t n;                 // structs in the one section
+  uint32_t client;            // the section's client (first value of the client column)
+  uint32_t clock0;            // the section's first clock
+  uint32_t ds0;               // delete set start (rest stream, right after the section header)
+  uint64_t soff;              // scratch offset
+  uint32_t ck0[NK];           // K1 checkpoints of each column (uint4: entry position, value index, running
+                              // value) every CKSTEP entries, at the scratch's checkpoint area + ck0
+  uint32_t nck[NK];
+  // K1: values per kind; RLE<u8> kinds: values in counted entries, and whether a final (endless) entry exists
+  uint32_t nval[NK], fin[NK], finv[NK];
+  // K2: the cut and the column indices around it
+  uint32_t f;                 // cut struct (NONE: no struct ends past the state vector)
+  uint32_t off, fclock_lo;    // Item.write offset; clock of the cut struct
+  uint32_t pf[NK], pf1[NK];   // values of each kind consumed before struct f / f + 1
+  uint32_t tot[NK];           // values of each kind consumed by all structs
+  uint32_t body_f, body_fc, body_f1, body_end;  // string body offsets: before struct f, its content string, after it; consumed end
+  uint32_t info_f, pi_f, clen_f;
+  // K3
+  uint32_t hlen[NK], vstart[NK];
+  uint8_t head[NK][HB];
+};
+
+struct Job {
+  GeneralJob j;
+  Meta *meta;
+  uint8_t *scr;  // per-document value arrays
+  uint8_t *done;
+};
+// per-document value arrays at meta.soff: info u8[n], pi u8[n], sl u32[3n + 1], ln u32[n]; then the checkpoints
+__host__ __device__ inline uint64_t scr_bytes(uint32_t n) { return ((2ull * n + 3) & ~3ull) + 4ull * (4ull * n + 1) + 16; }
+__device__ __forceinline__ uint8_t *a_info(const Job &J, const Meta &M) { return J.scr + M.soff; }
+__device__ __forceinline__ uint8_t *a_pi(const Job &J, const Meta &M) { return J.scr + M.soff + M.n; }
+__device__ __forceinline__ uint32_t *a_sl(const Job &J, const Meta &M) {
+  return reinterpret_cast<uint32_t *>(J.scr + M.soff + ((2ull * M.n + 3) & ~3ull));
+}
+__device__ __forceinline__ uint32_t *a_ln(const Job &J, const Meta &M) { return a_sl(J, M) + 3ull * M.n + 1; }
+__device__ __forceinline__ uint4 *a_ck(const Job &J, const Meta &M, uint32_t kind) {
+  return reinterpret_cast<uint4 *>(J.scr + M.soff + ((scr_bytes(M.n) + 15) & ~15ull)) + M.ck0[kind];
+}
+
+// ---- K0: header ---------------------------------------------------------------------------------------
+__global__ void k_v2_prep(Job J, uint64_t pv_min, uint64_t *sizes) {
+  const GeneralJob &j = J.j;
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d > j.n) return;
+  if (d == j.n) { sizes[d] = 0; return; }
+  Meta &M = J.meta[d];
+  M.ok = 0;
+  M.why = 1;
+  J.done[d] = 0;
+  sizes[d] = 0;
+  const uint32_t u0 = j.doc_upd[d];
+  if (j.doc_upd[d + 1] - u0 != 1) return;
+  const uint64_t ub = j.upd_off[u0], len64 = j.upd_off[u0 + 1] - ub;
+  if (len64 < pv_min || len64 == 0 || len64 >= (1ull << 28)) return;
+  const uint32_t len = (uint32_t)len64;
+  const uint8_t *D = j.A + ub;
+  ln::LCur c = ln::make(D, 0, len);
+  ln::rvu(c);  // feature flag
+  for (uint32_t k = 0; k < 9; k++) {
+    const uint32_t n = ln::rvu(c);
+    M.col0[k] = c.p;
+    if (c.bad || (uint64_t)c.p + n > len) return;
+    M.col1[k] = c.p + n;
+    c = ln::make(D, c.p + n, len);
+  }
+  // typeRef / keyClock unused by the kinds taken here
+  if (M.col1[0] != M.col0[0] || M.col1[7] != M.col0[7]) return;
+  const uint32_t nclients = ln::rvu(c);
+  if (c.bad || nclients != 1) return;
+  const uint32_t nstructs = ln::rvu(c);
+  const uint32_t clock = ln::rvu(c);
+  if (c.bad || nstructs == 0 || nstructs > (1u << 26)) return;
+  M.ds0 = c.p;
+  M.n = nstructs;
+  M.clock0 = clock;
+  // string column = varString(body) | UintOptRle(lengths)
+  ln::LCur s = ln::make(D, M.col0[5], M.col1[5]);
+  const uint32_t sn = ln::rvu(s);
+  if (s.bad || (uint64_t)s.p + sn > M.col1[5]) return;
+  M.sb0 = s.p;
+  M.sn = sn;
+  M.col0[5] = s.p + sn;  // lengths part
+  M.ok = 1;
+  M.why = 0;
+  uint32_t ck = 0;  // an entry is at least one byte: a column of b bytes needs b / CKSTEP + 1 checkpoints
+  for (uint32_t k = 0; k < NK; k++) {
+    M.ck0[k] = ck;
+    ck += (M.col1[col_of(k)] - M.col0[col_of(k)]) / CKSTEP + 2;
+  }
+  sizes[d] = (scr_bytes(nstructs) + 16ull * ck + 255) & ~255ull;
+}
+
+__global__ void k_v2_meta_off(Job J, const uint64_t *offs) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d < J.j.n) J.meta[d].soff = offs[d];
+}
+
+// ---- K1: column decoders, one lane per (document, column) ----------------------------------------------
+// lib0 readVarInt as k_big_v2's s_vi: canonical, <= 5 bytes, |v| < 2^31 + (sign); returns the magnitude
+__device__ __forceinline__ uint32_t rvi(ln::LCur &c, bool &neg) {
+  const uint32_t lo = (uint32_t)c.lo, hi = (uint32_t)(c.lo >> 32);
+  const uint32_t nb = ln::vu_nb(lo, hi);
+  neg = (lo & 0x40) != 0;
+  uint32_t m = (lo & 0x3fu) | ((lo >> 2) & 0x1fc0u) | ((lo >> 3) & 0xfe000u) | ((lo >> 4) & 0x7f00000u) | ((hi & 0x7fu) << 27);
+  const uint32_t bits = 6 + 7 * (nb - 1);
+  if (nb < 5) m &= (1u << bits) - 1u;
+  const uint32_t last = nb <= 4 ? (lo >> (8 * nb - 8)) & 0xffu : hi & 0xffu;
+  c.bad |= (nb > 5) | (c.p + nb > c.e) | ((nb > 1) & (last == 0)) | ((nb == 5) & ((hi & 0x7fu) > 0x1fu));
+  ln::skip(c, nb < 6 ? nb : 0);
+  return m;
+}
+
+__global__ void __launch_bounds__(64) k_v2_dec(Job J) {
+  const GeneralJob &j = J.j;
+  const uint32_t d = blockIdx.x * 64 + threadIdx.x, kind = blockIdx.y;
+  if (d >= j.n) return;
+  Meta &M = J.meta[d];
+  if (!M.ok) return;
+  const uint8_t *D = j.A + j.upd_off[j.doc_upd[d]];
+  const uint32_t c0 = M.col0[col_of(kind)], c1 = M.col1[col_of(kind)];
+  const uint32_t n = M.n;
+  bool bad = false;
+  uint32_t nv = 0, fin = 0, finv = 0;
+  uint4 *ck = a_ck(J, M, kind);
+  uint32_t ne = 0;  // entries so far
+  if (kind == K_INFO || kind == K_PI) {  // RleDecoder<u8>: value byte, count - 1 unless it is the column's last byte
+    uint8_t *out = kind == K_INFO ? a_info(J, M) : a_pi(J, M);
+    ln::LCur c = ln::make(D, c0, c1);
+    uint32_t prev = NONE;
+    while (c.p < c1 && !bad) {
+      if ((ne & (CKSTEP - 1)) == 0) ck[ne / CKSTEP] = make_uint4(c.p, nv, 0, 0);
+      ne++;
+      const uint32_t v = ln::rdb(c);
+      bad |= v == prev || (kind == K_PI && v > 1);
+      prev = v;
+      if (c.p == c1) { fin = 1; finv = v; break; }  // the final run never ends
+      const uint32_t cnt = ln::rvu(c) + 1;
+      bad |= c.bad || cnt > n - nv || cnt == 0;
+      if (bad) break;
+      for (uint32_t i = 0; i < cnt; i++) out[nv + i] = (uint8_t)v;
+      nv += cnt;
+    }
+    if (kind == K_INFO && !bad) {  // the endless final run fills the structs left
+      if (!fin && nv != n) bad = true;
+      for (uint32_t i = nv; i < n && fin; i++) out[i] = (uint8_t)finv;
+    }
+  } else if (kind == K_SL || kind == K_LN || kind == K_CL) {  // UintOptRleDecoder
+    uint32_t *out = kind == K_SL ? a_sl(J, M) : kind == K_LN ? a_ln(J, M) : nullptr;
+    const uint32_t cap = kind == K_SL ? 3 * n : kind == K_LN ? n : 2 * n + 1;
+    ln::LCur c = ln::make(D, c0, c1);
+    uint32_t prev = NONE;
+    while (c.p < c1 && !bad) {
+      if ((ne & (CKSTEP - 1)) == 0) ck[ne / CKSTEP] = make_uint4(c.p, nv, 0, 0);
+      ne++;
+      bool neg;
+      const uint32_t v = rvi(c, neg);
+      const uint32_t cnt = neg ? ln::rvu(c) + 2 : 1;
+      bad |= c.bad || v == prev || cnt > cap - nv || cnt < (neg ? 2u : 1u);
+      if (bad) break;
+      prev = v;
+      if (kind == K_CL && nv == 0) M.client = v;  // the section header's client
+      if (out)
+        for (uint32_t i = 0; i < cnt; i++) out[nv + i] = v;
+      nv += cnt;
+    }
+  } else {  // IntDiffOptRleDecoder (left / right clocks)
+    ln::LCur c = ln::make(D, c0, c1);
+    int64_t v = 0;
+    int32_t prevdf = 0;
+    bool first = true;
+    while (c.p < c1 && !bad) {
+      if ((ne & (CKSTEP - 1)) == 0) ck[ne / CKSTEP] = make_uint4(c.p, nv, (uint32_t)v, 0);
+      ne++;
+      bool neg;
+      const uint32_t m = rvi(c, neg);
+      const int32_t t = neg ? -(int32_t)m : (int32_t)m;
+      const int32_t df = t >> 1;
+      const uint32_t cnt = (t & 1) ? ln::rvu(c) + 2 : 1;
+      // the encoder's form: no -0, diff in [-2^30, 2^30) (JS `diff << 1`), runs maximal
+      bad |= c.bad || (neg && m == 0) || df < -(1 << 30) || df >= (1 << 30) || (!first && df == prevdf) || cnt > n - nv;
+      if (bad) break;
+      v += (int64_t)df * cnt;
+      // every value stays in [0, 2^32): the run is monotone, so its ends suffice
+      const int64_t vfirst = v - (int64_t)df * (cnt - 1);
+      bad |= v < 0 || v > 0xffffffffll || vfirst < 0 || vfirst > 0xffffffffll;
+      prevdf = df;
+      first = false;
+      nv += cnt;
+    }
+  }
+  if (bad) { M.ok = 0; M.why = 10 + kind; }
+  M.nval[kind] = nv;
+  M.nck[kind] = (ne + CKSTEP - 1) / CKSTEP;
+  M.fin[kind] = fin;
+  M.finv[kind] = finv;
+}
+
+// ---- K2: struct pass ------------------------------------------------------------------------------------
+constexpr uint32_t KT = 256;       // threads
+constexpr uint32_t PER = 4;        // structs per thread per tile
+constexpr uint32_t TILE = KT * PER;
+// exclusive block scan of NS u32 sums (+ totals), KT threads
+template <uint32_t NS>
+__device__ __forceinline__ void block_scan(uint32_t (&x)[NS], uint32_t (&tot)[NS], uint32_t *sh) {
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint32_t incl[NS];
+#pragma unroll
+  for (uint32_t q = 0; q < NS; q++) incl[q] = wave_incl_add(x[q]);
+  __syncthreads();
+  if (lane == 63)
+#pragma unroll
+    for (uint32_t q = 0; q < NS; q++) sh[w * NS + q] = incl[q];
+  __syncthreads();
+#pragma unroll
+  for (uint32_t q = 0; q < NS; q++) {
+    uint32_t pre = 0, all = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < KT / 64; k++) {
+      const uint32_t s = sh[k * NS + q];
+      pre += k < w ? s : 0;
+      all += s;
+    }
+    x[q] = pre + incl[q] - x[q];
+    tot[q] = all;
+  }
+}
+
+template <int OP>
+__global__ void __launch_bounds__(KT) k_v2_struct(Job J) {
+  const GeneralJob &j = J.j;
+  const uint32_t d = blockIdx.x, t = threadIdx.x;
+  Meta &M = J.meta[d];
+  if (!M.ok) return;
+  __shared__ uint32_t sh[4 * 16];
+  __shared__ uint32_t s_bad, s_cut;
+  __shared__ uint64_t s_clock;
+  const uint8_t *D = j.A + j.upd_off[j.doc_upd[d]];
+  const uint32_t n = M.n;
+  // the state vector's clock for the client (decodeStateVector: a later entry wins)
+  uint32_t k = 0;
+  if (OP == OP_DIFF) {
+    if (t == 0) {
+      const uint64_t s0 = j.sv_off[d], s1 = j.sv_off[d + 1];
+      ln::LCur c = ln::make(j.sv + s0, 0, (uint32_t)(s1 - s0));
+      const uint32_t ns = s1 - s0 > (1u << 20) ? NONE : ln::rvu(c);
+      bool bad = ns == NONE;
+      for (uint32_t i = 0; i < ns && !bad; i++) {
+        const uint32_t cl = ln::rvu(c), ck = ln::rvu(c);
+        bad |= c.bad;
+        if (!bad && cl == M.client) k = ck;
+      }
+      s_bad = bad || c.bad;
+      s_cut = k;
+    }
+    __syncthreads();
+    if (s_bad) { if (t == 0) { M.ok = 0; M.why = 20; } return; }
+    k = s_cut;
+  }
+  // the body must be ASCII (a UTF-16 slice is then a byte slice; k_big_v2's condition)
+  {
+    bool na = false;
+    for (uint32_t i = 16 * t; i < M.sn; i += 16 * KT) {
+      uint8_t b[16];
+      const uint32_t m = M.sn - i < 16 ? M.sn - i : 16;
+      for (uint32_t q = 0; q < m; q++) b[q] = D[M.sb0 + i + q];
+      for (uint32_t q = 0; q < m; q++) na |= b[q] >= 0x80;
+    }
+    if (__syncthreads_or(na)) { if (t == 0) { M.ok = 0; M.why = 21; } return; }
+  }
+  // the section client: the client column's first value (uopt_read)
+  if (M.nval[K_CL] == 0) { if (t == 0) { M.ok = 0; M.why = 22; } return; }
+  const uint8_t *info_a = a_info(J, M), *pi_a = a_pi(J, M);
+  const uint32_t *sl_a = a_sl(J, M), *ln_a = a_ln(J, M);
+  // running column indices (carried across tiles): [K_INFO .. K_RC] + string body bytes
+  uint32_t base[NK + 1];
+#pragma unroll
+  for (uint32_t q = 0; q <= NK; q++) base[q] = 0;
+  base[K_CL] = 1;  // the section header's client
+  uint64_t clock = M.clock0;
+  uint32_t cut = NONE;
+  if (t == 0) s_bad = 0;
+  for (uint32_t t0 = 0; t0 < n; t0 += TILE) {
+    // per struct: values consumed of each kind (no Skip / Any / Type ...: only GC, Deleted, String)
+    uint32_t cons[PER][NK], info[PER], pi[PER];
+    uint32_t x[NK + 2];  // per-thread sums: kinds, body bytes, clock
+#pragma unroll
+    for (uint32_t q = 0; q < NK + 2; q++) x[q] = 0;
+    bool bad = false;
+#pragma unroll
+    for (uint32_t e = 0; e < PER; e++) {
+      const uint32_t i = t0 + t * PER + e;
+      const uint32_t v = i < n ? info_a[i] : 0;
+      info[e] = v;
+      const uint32_t ref = v & 31;
+      const bool valid = i < n;
+      const bool gc = valid && ref == 0 && v != 10;
+      const bool item = valid && !gc;
+      bad |= valid && (v == 10 || (item && ref != 1 && ref != 4));
+      const bool o = item && (v & 0x80), r = item && (v & 0x40), no = item && !(v & 0xC0);
+      cons[e][K_INFO] = valid;
+      cons[e][K_PI] = no;
+      cons[e][K_RC] = r;
+      cons[e][K_LN] = gc || (item && ref == 1);
+      pi[e] = 0;  // parentInfo value: looked up after the scan (needs the index)
+      cons[e][K_CL] = o + r;
+      cons[e][K_LC] = o;
+      cons[e][K_SL] = (item && ref == 4) + (no && (v & 0x20));
+#pragma unroll
+      for (uint32_t q = 0; q < NK; q++) x[q] += cons[e][q];
+    }
+    // parentInfo index first (the others depend on its values)
+    {
+      uint32_t xp[1] = {x[K_PI]}, tp[1];
+      block_scan<1>(xp, tp, sh);
+      uint32_t pidx = base[K_PI] + xp[0];
+#pragma unroll
+      for (uint32_t e = 0; e < PER; e++) {
+        if (cons[e][K_PI]) {
+          const uint32_t pv = pidx < M.nval[K_PI] ? pi_a[pidx] : M.finv[K_PI];
+          bad |= pidx >= M.nval[K_PI] && !M.fin[K_PI];
+          pi[e] = pv;
+          // readParentInfo: 1 -> a ykey string, else a parent ID (client, clock)
+          cons[e][K_SL] += pv == 1;
+          cons[e][K_CL] += pv != 1;
+          cons[e][K_LC] += pv != 1;
+          x[K_SL] += pv == 1;
+          x[K_CL] += pv != 1;
+          x[K_LC] += pv != 1;
+          pidx++;
+        }
+      }
+      base[K_PI] += tp[0];
+    }
+    // indices of every kind
+    uint32_t tot[NK];
+    uint32_t xs[NK];
+#pragma unroll
+    for (uint32_t q = 0; q < NK; q++) xs[q] = x[q];
+    block_scan<NK>(xs, tot, sh);
+    // string lengths -> body bytes, clock lengths
+    uint32_t sli = base[K_SL] + xs[K_SL], lni = base[K_LN] + xs[K_LN];
+    uint32_t clen[PER], bodyb[PER];
+    x[NK] = 0;
+    x[NK + 1] = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < PER; e++) {
+      uint32_t bl = 0;
+      for (uint32_t s = 0; s < cons[e][K_SL]; s++) bl += sli + s < M.nval[K_SL] ? sl_a[sli + s] : 0;
+      const uint32_t ref = info[e] & 31;
+      uint32_t cl = 0;
+      if (cons[e][K_INFO]) {
+        if (cons[e][K_LN]) cl = lni < M.nval[K_LN] ? ln_a[lni] : 0;
+        else cl = sli + cons[e][K_SL] - 1 < M.nval[K_SL] ? sl_a[sli + cons[e][K_SL] - 1] : 0;  // ContentString: last
+        bad |= (ref == 1 || ref == 4) && info[e] != 0 && cl == 0;  // Item length 0
+        bad |= cl >= (1u << 20);  // keeps the block's clock sums in u32
+      }
+      clen[e] = cl;
+      bodyb[e] = bl;
+      x[NK] += bl;
+      x[NK + 1] += cl;
+      sli += cons[e][K_SL];
+      lni += cons[e][K_LN];
+    }
+    uint32_t xb[2] = {x[NK], x[NK + 1]}, tb[2];
+    block_scan<2>(xb, tb, sh);
+    // the cut: first struct (non-Skip) whose end passes sv[client]
+    uint64_t ck = clock + xb[1];
+    uint32_t mycut = NONE;
+#pragma unroll
+    for (uint32_t e = 0; e < PER; e++) {
+      const uint32_t i = t0 + t * PER + e;
+      if (i < n && OP == OP_DIFF && mycut == NONE && cut == NONE && ck + clen[e] > k) mycut = e;
+      if (mycut == NONE) ck += clen[e];
+    }
+    if (t == 0) s_cut = NONE;
+    __syncthreads();
+    if (mycut != NONE) atomicMin(&s_cut, t0 + t * PER + mycut);
+    bad |= clock + tb[1] > 0xffffffffull;
+    if (__syncthreads_or(bad)) { if (t == 0) { M.ok = 0; M.why = 23; } return; }
+    const uint32_t tc = s_cut;
+    if (tc != NONE && cut == NONE && mycut != NONE && tc == t0 + t * PER + mycut) {  // the thread holding the cut records it
+      const uint32_t e = mycut;
+      uint32_t pre[NK], pre1[NK];
+#pragma unroll
+      for (uint32_t q = 0; q < NK; q++) {
+        pre[q] = base[q] + xs[q];
+        for (uint32_t e2 = 0; e2 < e; e2++) pre[q] += cons[e2][q];
+        pre1[q] = pre[q] + cons[e][q];
+        M.pf[q] = pre[q];
+        M.pf1[q] = pre1[q];
+      }
+      uint32_t bo = base[NK] + xb[0];
+      for (uint32_t e2 = 0; e2 < e; e2++) bo += bodyb[e2];
+      M.body_f = bo;
+      M.body_f1 = bo + bodyb[e];
+      M.body_fc = (info[e] & 31) == 4 && info[e] != 0 ? bo + bodyb[e] - clen[e] : bo + bodyb[e];
+      uint64_t cf = clock + xb[1];
+      for (uint32_t e2 = 0; e2 < e; e2++) cf += clen[e2];
+      M.f = tc;
+      M.off = k > cf ? (uint32_t)(k - cf) : 0;
+      M.fclock_lo = (uint32_t)cf;
+      M.info_f = info[e];
+      M.pi_f = pi[e];
+      M.clen_f = clen[e];
+    }
+    if (tc != NONE) cut = tc;
+#pragma unroll
+    for (uint32_t q = 0; q < NK; q++) base[q] += tot[q];
+    base[NK] += tb[0];
+    clock += tb[1];
+    __syncthreads();
+  }
+  if (t != 0) return;
+  // every column consumed exactly as the re-encoding writes it; strings inside the body
+  bool bad = false;
+#pragma unroll
+  for (uint32_t q = 0; q < NK; q++) {
+    if (q == K_INFO || q == K_PI) bad |= M.fin[q] ? base[q] < M.nval[q] + 1 : base[q] != M.nval[q];
+    else bad |= base[q] != M.nval[q];
+    M.tot[q] = base[q];
+  }
+  bad |= base[NK] > M.sn;
+  M.body_end = base[NK];
+  if (bad) { M.ok = 0; M.why = 24; return; }
+  if (cut == NONE) M.f = NONE;
+  if (OP == OP_SV) {
+    // encodeStateVectorFromUpdateV2: one section, no Skip -> (client, end) unless the section does not
+    // start at clock 0 (then nothing is known) or ends at 0
+    const uint32_t end = M.clock0 == 0 ? (uint32_t)clock : 0;
+    const uint32_t total = end ? 1 + vsz(M.client) + vsz(end) : 1;
+    const uint64_t b = atomicAdd((unsigned long long *)j.used, (unsigned long long)total);
+    J.done[d] = 1;
+    atomicAdd((unsigned long long *)j.pw_count, 1ull);
+    if (b + total > j.cap) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; return; }
+    uint8_t *o = j.out + b;
+    if (end) { o[0] = 1; uint32_t p = 1; for (uint32_t v : {M.client, end}) { while (v > 127) { o[p++] = (uint8_t)(0x80 | (v & 127)); v >>= 7; } o[p++] = (uint8_t)v; } }
+    else o[0] = 0;
+    j.out_off[d] = b;
+    j.out_len[d] = total;
+    j.status[d] = ym::ST_OK;
+  }
+}
+
+// ---- K3: splice heads ---------------------------------------------------------------------------------
+// lib0 encoders into a small byte buffer
+struct Buf {
+  uint8_t *b;
+  uint32_t n;
+  bool over;
+  __device__ void byte(uint32_t v) { if (n < HB) b[n] = (uint8_t)v; else over = true; n++; }
+  __device__ void vu(uint32_t v) { while (v > 127) { byte(0x80 | (v & 127)); v >>= 7; } byte(v); }
+  __device__ void vi(bool neg, uint32_t m) {
+    byte((m > 63 ? 0x80 : 0) | (neg ? 0x40 : 0) | (m & 63));
+    m >>= 6;
+    while (m > 0) { byte((m > 127 ? 0x80 : 0) | (m & 127)); m >>= 7; }
+  }
+};
+struct Enc {  // one encoder of kind `kind`: (s, count, diff, started)
+  uint32_t s = 0, cnt = 0, started = 0;
+  int32_t df = 0;
+  bool bad = false;
+  __device__ void put(Buf &B, uint32_t kind, uint32_t v) {
+    if (kind == K_INFO || kind == K_PI) {  // RleEncoder<u8>
+      if (started && s == v) { cnt++; return; }
+      if (cnt > 0) B.vu(cnt - 1);
+      B.byte(v);
+      s = v; cnt = 1; started = 1;
+    } else if (kind == K_LC || kind == K_RC) {  // IntDiffOptRleEncoder
+      const int64_t dd = (int64_t)v - (int64_t)s;
+      if (dd < -(1ll << 30) || dd >= (1ll << 30)) { bad = true; return; }
+      if (df == (int32_t)dd) { s = v; cnt++; return; }
+      flush(B, kind);
+      s = v; cnt = 1; df = (int32_t)dd;
+    } else {  // UintOptRleEncoder
+      if (s == v && cnt > 0) { cnt++; return; }
+      flush(B, kind);
+      s = v; cnt = 1;
+    }
+  }
+  // closes the pending run (before verbatim entries, or at the column's end: an RLE<u8> final count is
+  // not written then)
+  __device__ void flush(Buf &B, uint32_t kind, bool at_end = false) {
+    if (cnt == 0) return;
+    if (kind == K_INFO || kind == K_PI) {
+      if (!at_end) B.vu(cnt - 1);
+    } else if (kind == K_LC || kind == K_RC) {
+      const int32_t x = (int32_t)((uint32_t)df << 1) | (cnt == 1 ? 0 : 1);
+      B.vi(x < 0, x < 0 ? (uint32_t)(-(int64_t)x) : (uint32_t)x);
+      if (cnt > 1) B.vu(cnt - 2);
+    } else {
+      B.vi(cnt != 1, s);
+      if (cnt > 1) B.vu(cnt - 2);
+    }
+    cnt = 0;
+  }
+};
+
+__global__ void __launch_bounds__(64) k_v2_splice(Job J) {
+  const GeneralJob &j = J.j;
+  const uint32_t d = blockIdx.x * 64 + threadIdx.x, kind = blockIdx.y;
+  if (d >= j.n) return;
+  Meta &M = J.meta[d];
+  if (!M.ok || M.f == NONE) return;
+  const uint8_t *D = j.A + j.upd_off[j.doc_upd[d]];
+  const uint32_t c0 = M.col0[col_of(kind)], c1 = M.col1[col_of(kind)];
+  const uint32_t q0 = M.pf[kind], q1 = M.pf1[kind], tot = M.tot[kind];
+  // walk the column's entries up to the one holding value q1; collect the cut struct's values [q0, q1)
+  uint32_t fv[4] = {0, 0, 0, 0};
+  uint32_t idx = 0, p = c0, vstart = c1;
+  uint32_t rem_v = 0, rem_n = 0;  // the entry holding q1: its value (first value at q1 for diffs) and values from q1 on
+  int32_t rem_df = 0;
+  bool have_rem = false;
+  int64_t v = 0;  // IntDiff running value
+  {  // resume at K1's last checkpoint at or before value q0 (binary search)
+    const uint4 *ck = a_ck(J, M, kind);
+    uint32_t lo = 0, hi = M.nck[kind];
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (ck[mid].y <= q0) lo = mid; else hi = mid;
+    }
+    if (M.nck[kind] > 0) {
+      const uint4 c4 = ck[lo];
+      p = c4.x;
+      idx = c4.y;
+      v = c4.z;
+    }
+  }
+  while (idx < tot) {
+    uint32_t ev, cnt, entry_end;
+    int32_t df = 0;
+    if (kind == K_INFO || kind == K_PI) {
+      ev = D[p];
+      if (p + 1 >= c1) { cnt = tot - idx; entry_end = c1; }
+      else { ln::LCur c = ln::make(D, p + 1, c1); cnt = ln::rvu(c) + 1; entry_end = c.p; }
+    } else {
+      ln::LCur c = ln::make(D, p, c1);
+      bool neg;
+      const uint32_t m = rvi(c, neg);
+      if (kind == K_LC || kind == K_RC) {
+        const int32_t tt = neg ? -(int32_t)m : (int32_t)m;
+        df = tt >> 1;
+        cnt = (tt & 1) ? ln::rvu(c) + 2 : 1;
+      } else {
+        cnt = neg ? ln::rvu(c) + 2 : 1;
+      }
+      ev = m;
+      entry_end = c.p;
+    }
+    // values idx .. idx + cnt - 1 of this entry
+    for (uint32_t q = q0; q < q1; q++)
+      if (q >= idx && q < idx + cnt) {
+        const uint32_t val = (kind == K_LC || kind == K_RC) ? (uint32_t)(v + (int64_t)df * (q - idx + 1)) : ev;
+        fv[q - q0] = val;
+      }
+    if (q1 < idx + cnt && q1 >= idx) {
+      have_rem = true;
+      rem_n = idx + cnt - q1;
+      rem_df = df;
+      rem_v = (kind == K_LC || kind == K_RC) ? (uint32_t)(v + (int64_t)df * (q1 - idx + 1)) : ev;
+      vstart = entry_end;
+      if (kind == K_LC || kind == K_RC) v += (int64_t)df * cnt;
+      idx += cnt;
+      break;
+    }
+    if (kind == K_LC || kind == K_RC) v += (int64_t)df * cnt;
+    idx += cnt;
+    p = entry_end;
+  }
+  // Item.write(encoder, off) of the cut struct (v2_write), preceded for the client column by the
+  // LazyStructWriter's writeClient
+  const uint32_t info = M.info_f, off = M.off, ref = info & 31;
+  const bool gc = ref == 0 && info != 10;
+  const bool o = !gc && (info & 0x80), r = !gc && (info & 0x40), no = !gc && !(info & 0xC0);
+  const bool has_o = !gc && (off > 0 || o);
+  uint32_t hv[6], nh = 0;
+  uint32_t fi = 0;  // next of the cut struct's own values
+  if (kind == K_INFO) {
+    hv[nh++] = gc ? 0 : (ref | (has_o ? 0x80 : 0) | (info & 0x40) | (no && off == 0 ? (info & 0x20) : 0));
+  } else if (kind == K_CL) {
+    hv[nh++] = M.client;
+    if (o) { hv[nh++] = off > 0 ? M.client : fv[fi]; fi++; }
+    else if (off > 0 && !gc) hv[nh++] = M.client;
+    if (r) hv[nh++] = fv[fi++];
+    if (no && M.pi_f != 1) { if (off == 0 && !r) hv[nh++] = fv[fi]; fi++; }
+  } else if (kind == K_LC) {
+    if (o) { hv[nh++] = off > 0 ? M.fclock_lo + off - 1 : fv[fi]; fi++; }
+    else if (off > 0 && !gc) hv[nh++] = M.fclock_lo + off - 1;
+    if (no && M.pi_f != 1) { if (off == 0 && !r) hv[nh++] = fv[fi]; fi++; }
+  } else if (kind == K_RC) {
+    if (r) hv[nh++] = fv[fi++];
+  } else if (kind == K_PI) {
+    if (no && off == 0 && !r) hv[nh++] = M.pi_f == 1 ? 1 : 0;
+  } else if (kind == K_LN) {
+    if (gc || ref == 1) hv[nh++] = M.clen_f - off;
+  } else {  // K_SL: ykey / parentSub (written only with the parent info) and the content slice
+    if (no && M.pi_f == 1) { if (off == 0 && !r) hv[nh++] = fv[fi]; fi++; }
+    if (no && (info & 0x20)) { if (off == 0 && !r) hv[nh++] = fv[fi]; fi++; }
+    if (ref == 4 && !gc) hv[nh++] = fv[fi] - off;
+  }
+  uint8_t *hb = M.head[kind];
+  Buf B{hb, 0, false};
+  Enc E;
+  for (uint32_t i = 0; i < nh; i++) E.put(B, kind, hv[i]);
+  bool bad = E.bad;
+  if (have_rem) {
+    // the rest of the entry holding q1: one run in the input; the encoder sees its first value (and for
+    // diffs the second, which fixes the run's diff), every further value only extends the run
+    const bool dif = kind == K_LC || kind == K_RC;
+    E.put(B, kind, rem_v);
+    if (rem_n >= 2) {
+      if (dif) {
+        E.put(B, kind, (uint32_t)((int64_t)rem_v + rem_df));
+        E.cnt += rem_n - 2;
+        E.s = (uint32_t)((int64_t)rem_v + (int64_t)rem_df * (rem_n - 1));
+      } else {
+        E.cnt += rem_n - 1;
+      }
+    }
+    bad |= E.bad;
+    // The next input entry starts a new run (the input is canonical) -- but the re-encoded head can leave
+    // a pending run it continues (a diff equal to the entry's, or the same value): the encoder would merge
+    // them, so that entry is re-encoded too (at most twice: after a whole entry the next one differs).
+    for (int guard = 0; guard < 2 && vstart < c1 && !bad; guard++) {
+      ln::LCur c = ln::make(D, vstart, c1);
+      uint32_t nv, ncnt, nend;
+      int32_t ndf = 0;
+      if (kind == K_INFO || kind == K_PI) {
+        nv = D[vstart];
+        if (vstart + 1 >= c1) { ncnt = tot - idx; nend = c1; }
+        else { ln::LCur cc = ln::make(D, vstart + 1, c1); ncnt = ln::rvu(cc) + 1; nend = cc.p; }
+      } else {
+        bool neg;
+        const uint32_t m = rvi(c, neg);
+        nv = m;
+        if (kind == K_LC || kind == K_RC) {
+          const int32_t tt = neg ? -(int32_t)m : (int32_t)m;
+          ndf = tt >> 1;
+          ncnt = (tt & 1) ? ln::rvu(c) + 2 : 1;
+        } else {
+          ncnt = neg ? ln::rvu(c) + 2 : 1;
+        }
+        nend = c.p;
+      }
+      const bool merge = E.cnt > 0 && ((kind == K_LC || kind == K_RC) ? E.df == ndf : E.s == nv);
+      if (!merge) break;
+      E.cnt += ncnt;  // the same run, ncnt values longer
+      if (kind == K_LC || kind == K_RC) E.s = (uint32_t)((int64_t)E.s + (int64_t)ndf * ncnt);
+      idx += ncnt;
+      vstart = nend;
+    }
+    E.flush(B, kind, vstart >= c1);
+  } else {
+    E.flush(B, kind, true);
+    vstart = c1;
+  }
+  if (bad || B.over) { M.ok = 0; M.why = 30 + kind; return; }
+  M.hlen[kind] = B.n;
+  M.vstart[kind] = vstart;
+}
+
+// ---- K4: output -----------------------------------------------------------------------------------------
+using wds::u4u;
+__device__ __forceinline__ void wcopy(uint8_t *dst, const uint8_t *src, uint32_t n) {
+  const uint32_t nv = n >> 4;
+  for (uint32_t v = threadIdx.x; v < nv; v += 64) reinterpret_cast<u4u *>(dst)[v] = reinterpret_cast<const u4u *>(src)[v];
+  for (uint32_t i = (nv << 4) + threadIdx.x; i < n; i += 64) dst[i] = src[i];
+}
+
+__global__ void __launch_bounds__(64) k_v2_out(Job J) {
+  const GeneralJob &j = J.j;
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
+    Meta &M = J.meta[d];
+    if (!M.ok) continue;
+    const uint32_t u0 = j.doc_upd[d];
+    const uint64_t ub = j.upd_off[u0];
+    const uint32_t len = (uint32_t)(j.upd_off[u0 + 1] - ub);
+    const uint8_t *D = j.A + ub;
+    // delete set: readDeleteSet's reads, canonical, no repeated or empty client (then copied)
+    uint32_t x = M.ds0;
+    bool bad = false;
+    uint32_t ndc;
+    {
+      ln::LCur c = ln::make(D, x, len);
+      ndc = ln::rvu(c);
+      x = c.p;
+      bad = c.bad || ndc > 4096;
+    }
+    uint32_t *dsc = reinterpret_cast<uint32_t *>(j.bscratch + (uint64_t)blockIdx.x * BS_BYTES + BS_DSC);
+    for (uint32_t i = 0; i < ndc && !bad; i++) {
+      ln::LCur h = ln::make(D, x, len);
+      const uint32_t client = ln::rvu(h);
+      const uint32_t m = ln::rvu(h);
+      x = h.p;
+      if (h.bad || m == 0 || i >= BS_NDSC) { bad = true; break; }
+      bool hit = false;
+      for (uint32_t h0 = 0; h0 < i; h0 += 64) hit |= __any(h0 + lane < i && dsc[h0 + lane] == client);
+      if (hit) { bad = true; break; }
+      __syncthreads();
+      if (lane == 0) dsc[i] = client;
+      __threadfence_block();
+      __syncthreads();
+      x = wds::skip_varuints(D, x, len, 2ull * m);
+      if (x == NONE) bad = true;
+    }
+    if (bad) { if (lane == 0) M.why = 40; __syncthreads(); continue; }
+    const uint32_t ds1 = x;
+    // sizes
+    const bool part = M.f != NONE;
+    uint32_t cl[9];
+    for (uint32_t c = 0; c < 9; c++) cl[c] = 0;
+    uint32_t sbn = 0, sln = 0;
+    if (part) {  // spans the splice and the cut produced must lie inside their columns (else: decline)
+      bool span_bad = M.body_f > M.body_fc || M.body_fc > M.body_f1 || M.body_f1 > M.body_end || M.body_end > M.sn;
+      span_bad |= M.off != 0 && (M.info_f & 31) == 4 && M.body_fc + M.off > M.body_f1;
+      for (uint32_t kk = 0; kk < NK; kk++)
+        span_bad |= M.hlen[kk] > HB || M.vstart[kk] < M.col0[col_of(kk)] || M.vstart[kk] > M.col1[col_of(kk)];
+      if (span_bad) { if (lane == 0) M.why = 41; __syncthreads(); continue; }
+      for (uint32_t kk = 0; kk < NK; kk++) {
+        const uint32_t c = col_of(kk);
+        const uint32_t b = M.hlen[kk] + (M.col1[c] - M.vstart[kk]);
+        if (kk == K_SL) sln = b;
+        else cl[c] = b;
+      }
+      // the cut struct's strings: all of them without an offset, else only the content's tail (an offset
+      // gives the Item an origin: ykey / parentSub are not written)
+      const uint32_t hs0 = M.off == 0 ? M.body_f : (M.info_f & 31) == 4 ? M.body_fc + M.off : M.body_f1;
+      sbn = (M.body_f1 - hs0) + (M.body_end - M.body_f1);
+    }
+    cl[5] = vsz(sbn) + sbn + sln;  // the string column always holds varString(body), even an empty one
+    uint32_t total = 1;
+    for (uint32_t c = 0; c < 9; c++) total += vsz(cl[c]) + cl[c];
+    const uint32_t written = part ? M.n - M.f : 0;
+    const uint32_t fclock = part ? M.fclock_lo + M.off : 0;
+    total += vsz(part ? 1 : 0) + (part ? vsz(written) + vsz(fclock) : 0) + (ds1 - M.ds0);
+    uint64_t b = 0;
+    if (lane == 0) b = atomicAdd((unsigned long long *)j.used, (unsigned long long)total);
+    b = ((uint64_t)lane_read((uint32_t)(b >> 32), 0) << 32) | lane_read((uint32_t)b, 0);
+    if (lane == 0) { J.done[d] = 1; atomicAdd((unsigned long long *)j.pw_count, 1ull); }
+    if (b + total > j.cap) {
+      if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }
+      __syncthreads();
+      continue;
+    }
+    uint8_t *o = j.out + b;
+    auto put = [&](uint32_t p, uint32_t v) -> uint32_t {
+      const uint32_t nb = vsz(v);
+      if (lane == 0) { uint32_t q = p; while (v > 127) { o[q++] = (uint8_t)(0x80 | (v & 127)); v >>= 7; } o[q] = (uint8_t)v; }
+      return p + nb;
+    };
+    uint32_t p = put(0, 0);
+    for (uint32_t c = 0; c < 9; c++) {
+      p = put(p, cl[c]);
+      if (c == 5) p = put(p, sbn);  // string column: varString(body) | lengths
+      if (!part || cl[c] == 0) continue;
+      int kk = -1;
+      for (uint32_t q = 0; q < NK; q++) if (col_of(q) == c) kk = (int)q;
+      if (c == 5) {
+        const uint32_t hs0 = M.off == 0 ? M.body_f : (M.info_f & 31) == 4 ? M.body_fc + M.off : M.body_f1;
+        wcopy(o + p, D + M.sb0 + hs0, M.body_f1 - hs0);
+        p += M.body_f1 - hs0;
+        wcopy(o + p, D + M.sb0 + M.body_f1, M.body_end - M.body_f1);
+        p += M.body_end - M.body_f1;
+      }
+      if (kk < 0) continue;
+      if (lane == 0) for (uint32_t q = 0; q < M.hlen[kk]; q++) o[p + q] = M.head[kk][q];
+      p += M.hlen[kk];
+      wcopy(o + p, D + M.vstart[kk], M.col1[c] - M.vstart[kk]);
+      p += M.col1[c] - M.vstart[kk];
+    }
+    p = put(p, part ? 1 : 0);
+    if (part) { p = put(p, written); p = put(p, fclock); }
+    wcopy(o + p, D + M.ds0, ds1 - M.ds0);
+    if (lane == 0) {
+      j.out_off[d] = b;
+      j.out_len[d] = total;
+      j.status[d] = ym::ST_OK;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace pv2
+
+namespace {
+int pv_ensure(PwBufs &B, int k, size_t n) {
+  if (n <= B.cap[k]) return 0;
+  if (B.p[k]) hipFree(B.p[k]);
+  B.p[k] = nullptr;
+  B.cap[k] = 0;
+  const size_t want = n + n / 8 + 4096;
+  if (hipMalloc(&B.p[k], want) != hipSuccess) return -1;
+  B.cap[k] = want;
+  return 0;
+}
+}  // namespace
+
+// Column-parallel V2 diff / sv over the large single-section documents of a call; marks the documents it
+// completes in *done_out (k_big_v2 skips them).  1 = launched, 0 = not applicable, < 0 = error.
+static pv2::Meta *pv2_last_meta = nullptr;
+int pv2_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const uint8_t **done_out) {
+  using namespace pv2;
+  *done_out = nullptr;
+  if (!j.v2 || (op != OP_DIFF && op != OP_SV) || j.n == 0 || !j.pw_count || getenv("YMERGE_NO_PW")) return 0;
+  uint64_t pv_min = PV_MIN;
+  if (const char *e = getenv("YMERGE_PW_MIN")) pv_min = strtoull(e, nullptr, 10);
+  if (!B.pinned && hipHostMalloc((void **)&B.pinned, 64, hipHostMallocDefault) != hipSuccess) return -2;
+  const uint32_t n1 = j.n + 1;
+  if (pv_ensure(B, 0, sizeof(Meta) * (uint64_t)j.n + 16ull * n1 + j.n + 64)) return -2;
+  Job J;
+  J.j = j;
+  J.meta = (Meta *)B.p[0];
+  uint64_t *sizes = (uint64_t *)(J.meta + j.n), *offs = sizes + n1;
+  J.done = (uint8_t *)(offs + n1);
+  J.scr = nullptr;
+  pv2_last_meta = J.meta;
+  k_v2_prep<<<(n1 + 255) / 256, 256, 0, st>>>(J, pv_min, sizes);
+  size_t tmp = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, sizes, offs, n1, st);
+  if (pv_ensure(B, 1, tmp + 16)) return -2;
+  if (hipcub::DeviceScan::ExclusiveSum(B.p[1], tmp, sizes, offs, n1, st) != hipSuccess) return -3;
+  if (hipMemcpyAsync(B.pinned, offs + j.n, 8, hipMemcpyDeviceToHost, st) != hipSuccess) return -3;
+  if (hipStreamSynchronize(st) != hipSuccess) return -3;
+  const uint64_t total = *(uint64_t *)B.pinned;
+  *done_out = J.done;
+  if (total == 0) return 1;
+  if (pv_ensure(B, 2, total + 256)) {
+    hipMemsetAsync(J.done, 0, j.n, st);
+    return 1;
+  }
+  J.scr = (uint8_t *)B.p[2];
+  k_v2_meta_off<<<(j.n + 255) / 256, 256, 0, st>>>(J, offs);
+  const dim3 g1((j.n + 63) / 64, NK);
+  k_v2_dec<<<g1, 64, 0, st>>>(J);
+  if (op == OP_DIFF) {
+    k_v2_struct<OP_DIFF><<<j.n, KT, 0, st>>>(J);
+    k_v2_splice<<<g1, 64, 0, st>>>(J);
+    const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
+    k_v2_out<<<grid, 64, 0, st>>>(J);
+  } else {
+    k_v2_struct<OP_SV><<<j.n, KT, 0, st>>>(J);
+  }
+  return 1;
+}
+
+}  // namespace ymk
+
+// debugging aid (not part of include/ymerge.h): per document of the last V2 column-path call on this
+// device, 0 = taken, 1 = not eligible, else the stage that declined it (K1: 10 + column, K2: 20-24,
+// K3: 30 + column, K4: 40 delete set / 41 spans)
+extern "C" int ym__pv2_why(uint32_t *host, uint32_t n) {
+  using namespace ymk;
+  if (!pv2_last_meta) return -1;
+  for (uint32_t d = 0; d < n; d++)
+    if (hipMemcpy(host + d, reinterpret_cast<uint8_t *>(pv2_last_meta + d) + offsetof(pv2::Meta, why), 4,
+                  hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return 0;
+}
