@@ -140,6 +140,7 @@ def secondary(dev, eng):
     cases = [("merge_c4_v1", "merge", "c4_v1", 10000), ("merge_c2_v2", "merge", "c2_v2", 10000),
              ("merge_c4_v2", "merge", "c4_v2", 10000), ("diff_c3_v1", "diff", "c3_v1", 4096),
              ("sv_c3_v1", "sv", "c3_v1", 4096), ("diff_c3_v2", "diff", "c3_v2", 4096),
+             ("sv_c3_v2", "sv", "c3_v2", 4096),
              ("merge_c5_v1", "merge", "c5_v1", 256), ("merge_c5_v2", "merge", "c5_v2", 256),
              ("diff_c5_v1", "diff", "c5_v1", 256), ("diff_c5_v2", "diff", "c5_v2", 256),
              ("meta_c2_v1", "meta", "c2_v1", 10000), ("meta_c2_v2", "meta", "c2_v2", 10000),

@@ -169,13 +169,103 @@ __device__ __forceinline__ uint32_t rvi(ln::LCur &c, bool &neg) {
   return m;
 }
 
+// K1's column cursor: the lane's next bytes come from its own LDS slot, which the whole wave re-stages at
+// once (each lane from its own position, 32 independent 16-byte loads) whenever any lane gets within 48
+// bytes of its slot's end.  A column decode is one dependent chain per lane; read straight from HBM every
+// 8 bytes it paid a memory latency per window (C3 info column: 16 k of them); staged, it pays one per
+// ~460 bytes, and the window reads are LDS reads.
+constexpr uint32_t SW = 512, SSTRIDE = SW + 16;
+extern __shared__ __attribute__((aligned(16))) uint8_t k1_lds[];
+struct SC {
+  const uint8_t *D;
+  uint32_t p, e, nv, wbeg, wend, slot;
+  bool bad;
+  uint64_t lo, hi;
+};
+__device__ __forceinline__ uint64_t sc_ld8(const SC &c, uint32_t q) {
+  uint64_t x;
+  __builtin_memcpy(&x, k1_lds + c.slot + (q - c.wbeg), 8);
+  return x;
+}
+__device__ __forceinline__ void sc_fill(SC &c) {
+  if (c.nv >= 8) return;
+  const uint64_t x = sc_ld8(c, c.p + c.nv);
+  if (c.nv == 0) { c.lo = x; c.hi = 0; }
+  else { c.lo |= x << (8 * c.nv); c.hi = x >> (64 - 8 * c.nv); }
+  c.nv += 8;
+}
+// (re)stages the lane's slot at its read position (all lanes of the wave call it together)
+__device__ __forceinline__ void sc_stage(SC &c, uint32_t doc_end) {
+  c.wbeg = (c.p + c.nv) & ~15u;
+  typedef uint4 __attribute__((aligned(1))) u4l;
+  uint4 v[SW / 16];
+#pragma unroll
+  for (uint32_t k = 0; k < SW / 16; k++) {
+    const uint32_t q = c.wbeg + 16 * k;
+    v[k] = q < c.e && q + 16 <= doc_end ? *reinterpret_cast<const u4l *>(c.D + q) : make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < SW / 16; k++) *reinterpret_cast<uint4 *>(k1_lds + c.slot + 16 * k) = v[k];
+  c.wend = c.wbeg + SW;
+}
+__device__ __forceinline__ SC sc_make(const uint8_t *D, uint32_t p, uint32_t e, uint32_t doc_end) {
+  SC c;
+  c.D = D; c.p = p; c.e = e; c.nv = 0; c.bad = false; c.lo = c.hi = 0;
+  c.slot = threadIdx.x * SSTRIDE;
+  sc_stage(c, doc_end);
+  sc_fill(c);
+  return c;
+}
+__device__ __forceinline__ void sc_skip(SC &c, uint32_t n) {
+  if (n >= c.nv) { c.p += n; c.nv = 0; }
+  else if (n > 0) {
+    if (n < 8) { c.lo = (c.lo >> (8 * n)) | (c.hi << (64 - 8 * n)); c.hi >>= 8 * n; }
+    else { c.lo = c.hi >> (8 * (n - 8)); c.hi = 0; }
+    c.p += n;
+    c.nv -= n;
+  }
+  sc_fill(c);
+}
+__device__ __forceinline__ uint32_t sc_rdb(SC &c) {
+  c.bad |= c.p >= c.e;
+  const uint32_t v = (uint32_t)c.lo & 0xffu;
+  sc_skip(c, 1);
+  return v;
+}
+__device__ __forceinline__ uint32_t sc_rvu(SC &c) {
+  const uint32_t lo = (uint32_t)c.lo, hi = (uint32_t)(c.lo >> 32);
+  const uint32_t nb = ln::vu_nb(lo, hi);
+  const uint32_t v = (lo & 0x7fu) | ((lo >> 1) & 0x3f80u) | ((lo >> 2) & 0x1fc000u) | ((lo >> 3) & 0xfe00000u) | (hi << 28);
+  const uint32_t m = (uint32_t)((1ull << (7 * (nb < 5 ? nb : 5))) - 1);
+  c.bad |= ln::vu_bad(lo, hi, nb, c.p, c.e);
+  sc_skip(c, nb < 6 ? nb : 0);
+  return v & m;
+}
+__device__ __forceinline__ uint32_t sc_rvi(SC &c, bool &neg) {  // rvi over the staged cursor
+  const uint32_t lo = (uint32_t)c.lo, hi = (uint32_t)(c.lo >> 32);
+  const uint32_t nb = ln::vu_nb(lo, hi);
+  neg = (lo & 0x40) != 0;
+  uint32_t m = (lo & 0x3fu) | ((lo >> 2) & 0x1fc0u) | ((lo >> 3) & 0xfe000u) | ((lo >> 4) & 0x7f00000u) | ((hi & 0x7fu) << 27);
+  const uint32_t bits = 6 + 7 * (nb - 1);
+  if (nb < 5) m &= (1u << bits) - 1u;
+  const uint32_t last = nb <= 4 ? (lo >> (8 * nb - 8)) & 0xffu : hi & 0xffu;
+  c.bad |= (nb > 5) | (c.p + nb > c.e) | ((nb > 1) & (last == 0)) | ((nb == 5) & ((hi & 0x7fu) > 0x1fu));
+  sc_skip(c, nb < 6 ? nb : 0);
+  return m;
+}
+// every lane of the wave re-stages when any active lane is within 48 bytes of its slot's end
+#define SC_GUARD(c, doc_end) \
+  if (__any((c).p + 48 > (c).wend && (c).wend < (c).e + 16)) sc_stage((c), (doc_end))
+
 __global__ void __launch_bounds__(64) k_v2_dec(Job J) {
   const GeneralJob &j = J.j;
   const uint32_t d = blockIdx.x * 64 + threadIdx.x, kind = blockIdx.y;
   if (d >= j.n) return;
   Meta &M = J.meta[d];
   if (!M.ok) return;
-  const uint8_t *D = j.A + j.upd_off[j.doc_upd[d]];
+  const uint64_t ub = j.upd_off[j.doc_upd[d]];
+  const uint8_t *D = j.A + ub;
+  const uint32_t doc_end = (uint32_t)(j.upd_off[j.doc_upd[d] + 1] - ub);
   const uint32_t c0 = M.col0[col_of(kind)], c1 = M.col1[col_of(kind)];
   const uint32_t n = M.n;
   bool bad = false;
@@ -184,16 +274,17 @@ __global__ void __launch_bounds__(64) k_v2_dec(Job J) {
   uint32_t ne = 0;  // entries so far
   if (kind == K_INFO || kind == K_PI) {  // RleDecoder<u8>: value byte, count - 1 unless it is the column's last byte
     uint8_t *out = kind == K_INFO ? a_info(J, M) : a_pi(J, M);
-    ln::LCur c = ln::make(D, c0, c1);
+    SC c = sc_make(D, c0, c1, doc_end);
     uint32_t prev = NONE;
     while (c.p < c1 && !bad) {
+      SC_GUARD(c, doc_end);
       if ((ne & (CKSTEP - 1)) == 0) ck[ne / CKSTEP] = make_uint4(c.p, nv, 0, 0);
       ne++;
-      const uint32_t v = ln::rdb(c);
+      const uint32_t v = sc_rdb(c);
       bad |= v == prev || (kind == K_PI && v > 1);
       prev = v;
       if (c.p == c1) { fin = 1; finv = v; break; }  // the final run never ends
-      const uint32_t cnt = ln::rvu(c) + 1;
+      const uint32_t cnt = sc_rvu(c) + 1;
       bad |= c.bad || cnt > n - nv || cnt == 0;
       if (bad) break;
       for (uint32_t i = 0; i < cnt; i++) out[nv + i] = (uint8_t)v;
@@ -206,14 +297,15 @@ __global__ void __launch_bounds__(64) k_v2_dec(Job J) {
   } else if (kind == K_SL || kind == K_LN || kind == K_CL) {  // UintOptRleDecoder
     uint32_t *out = kind == K_SL ? a_sl(J, M) : kind == K_LN ? a_ln(J, M) : nullptr;
     const uint32_t cap = kind == K_SL ? 3 * n : kind == K_LN ? n : 2 * n + 1;
-    ln::LCur c = ln::make(D, c0, c1);
+    SC c = sc_make(D, c0, c1, doc_end);
     uint32_t prev = NONE;
     while (c.p < c1 && !bad) {
+      SC_GUARD(c, doc_end);
       if ((ne & (CKSTEP - 1)) == 0) ck[ne / CKSTEP] = make_uint4(c.p, nv, 0, 0);
       ne++;
       bool neg;
-      const uint32_t v = rvi(c, neg);
-      const uint32_t cnt = neg ? ln::rvu(c) + 2 : 1;
+      const uint32_t v = sc_rvi(c, neg);
+      const uint32_t cnt = neg ? sc_rvu(c) + 2 : 1;
       bad |= c.bad || v == prev || cnt > cap - nv || cnt < (neg ? 2u : 1u);
       if (bad) break;
       prev = v;
@@ -223,18 +315,19 @@ __global__ void __launch_bounds__(64) k_v2_dec(Job J) {
       nv += cnt;
     }
   } else {  // IntDiffOptRleDecoder (left / right clocks)
-    ln::LCur c = ln::make(D, c0, c1);
+    SC c = sc_make(D, c0, c1, doc_end);
     int64_t v = 0;
     int32_t prevdf = 0;
     bool first = true;
     while (c.p < c1 && !bad) {
+      SC_GUARD(c, doc_end);
       if ((ne & (CKSTEP - 1)) == 0) ck[ne / CKSTEP] = make_uint4(c.p, nv, (uint32_t)v, 0);
       ne++;
       bool neg;
-      const uint32_t m = rvi(c, neg);
+      const uint32_t m = sc_rvi(c, neg);
       const int32_t t = neg ? -(int32_t)m : (int32_t)m;
       const int32_t df = t >> 1;
-      const uint32_t cnt = (t & 1) ? ln::rvu(c) + 2 : 1;
+      const uint32_t cnt = (t & 1) ? sc_rvu(c) + 2 : 1;
       // the encoder's form: no -0, diff in [-2^30, 2^30) (JS `diff << 1`), runs maximal
       bad |= c.bad || (neg && m == 0) || df < -(1 << 30) || df >= (1 << 30) || (!first && df == prevdf) || cnt > n - nv;
       if (bad) break;
@@ -890,7 +983,7 @@ int pv2_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const u
   J.scr = (uint8_t *)B.p[2];
   k_v2_meta_off<<<(j.n + 255) / 256, 256, 0, st>>>(J, offs);
   const dim3 g1((j.n + 63) / 64, NK);
-  k_v2_dec<<<g1, 64, 0, st>>>(J);
+  k_v2_dec<<<g1, 64, 64 * SSTRIDE, st>>>(J);
   if (op == OP_DIFF) {
     k_v2_struct<OP_DIFF><<<j.n, KT, 0, st>>>(J);
     k_v2_splice<<<g1, 64, 0, st>>>(J);
