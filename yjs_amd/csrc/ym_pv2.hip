@@ -146,7 +146,7 @@ __global__ void k_v2_prep(Job J, uint64_t pv_min, uint64_t *sizes) {
     M.ck0[k] = ck;
     ck += (M.col1[col_of(k)] - M.col0[col_of(k)]) / CKSTEP + 2;
   }
-  sizes[d] = (scr_bytes(nstructs) + 16ull * ck + 255) & ~255ull;
+  sizes[d] = (((scr_bytes(nstructs) + 15) & ~15ull) + 16ull * ck + 255) & ~255ull;  // checkpoints start 16-aligned (a_ck)
 }
 
 __global__ void k_v2_meta_off(Job J, const uint64_t *offs) {
