@@ -121,7 +121,7 @@ __global__ void __launch_bounds__(256) k_pw_walk(GeneralJob j, const uint32_t *c
   const uint32_t len = (uint32_t)(j.upd_off[u0 + 1] - ub);
   const uint8_t *D = j.A + ub;
   const uint32_t c0 = ci * CH, c1 = c0 + CH < len ? c0 + CH : len;
-  uint32_t nrec = 0, cum = 0, lastfail = 0, lastpatch = 0, lastskip = 0, fails = 0, okrun = 0;
+  uint32_t nrec = 0, cum = 0, lastfail = 0, lastpatch = 0, lastskip = 0, fails = FAIL_RUN, okrun = 0;  // the chunk start is mid-struct: only short-cut candidates until two structs in a row
   bool frun = false, ovf = false;
   uint32_t p = c0;
   while (p < c1) {
