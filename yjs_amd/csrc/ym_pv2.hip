@@ -7,12 +7,13 @@
 //
 //  K0 k_v2_prep   one thread per document: the header (column spans, the section header), eligibility
 //                 (one update, one client section), the scratch size.
-//  K1 k_v2_dec    one lane per (document, column), a wave = 64 documents of one column kind: the lib0
-//                 RLE decoders (RleDecoder<u8>, UintOptRleDecoder, IntDiffOptRleDecoder) run over the
-//                 whole column, every entry checked to be in the form lib0's encoder writes (canonical
-//                 varints, runs maximal, no -0 diff, diffs < 2^30, parentInfo in {0, 1}, an RLE<u8> column
-//                 ending without a count); info / parentInfo / string lengths / len values are expanded
-//                 into per-value arrays, the others only counted.
+//  K1 k_v2_decw   one wave per (document, column): the lib0 RLE decoders (RleDecoder<u8>,
+//                 UintOptRleDecoder, IntDiffOptRleDecoder) parallelised by an automaton tokeniser whose
+//                 per-lane transition functions a wave prefix scan composes; every entry checked to be in
+//                 the form lib0's encoder writes (canonical varints, runs maximal, no -0 diff, diffs < 2^30,
+//                 parentInfo in {0, 1}, an RLE<u8> column ending without a count); info / parentInfo /
+//                 string lengths / len values expanded into per-value arrays, the others only counted;
+//                 a checkpoint (entry position, value index, running value) every CKSTEP entries.
 //  K2 k_v2_struct one 256-thread block per document: per struct the values it consumes from every
 //                 column (from its info byte and parentInfo), block prefix sums over the structs give each
 //                 struct's column indices, its clock length and clock; the diff cut is the first struct
@@ -169,182 +170,208 @@ __device__ __forceinline__ uint32_t rvi(ln::LCur &c, bool &neg) {
   return m;
 }
 
-// K1's column cursor: the lane's next bytes come from its own LDS slot, which the whole wave re-stages at
-// once (each lane from its own position, 32 independent 16-byte loads) whenever any lane gets within 48
-// bytes of its slot's end.  A column decode is one dependent chain per lane; read straight from HBM every
-// 8 bytes it paid a memory latency per window (C3 info column: 16 k of them); staged, it pays one per
-// ~460 bytes, and the window reads are LDS reads.
-constexpr uint32_t SW = 512, SSTRIDE = SW + 16;
-extern __shared__ __attribute__((aligned(16))) uint8_t k1_lds[];
-struct SC {
-  const uint8_t *D;
-  uint32_t p, e, nv, wbeg, wend, slot;
-  bool bad;
-  uint64_t lo, hi;
-};
-__device__ __forceinline__ uint64_t sc_ld8(const SC &c, uint32_t q) {
-  uint64_t x;
-  __builtin_memcpy(&x, k1_lds + c.slot + (q - c.wbeg), 8);
-  return x;
-}
-__device__ __forceinline__ void sc_fill(SC &c) {
-  if (c.nv >= 8) return;
-  const uint64_t x = sc_ld8(c, c.p + c.nv);
-  if (c.nv == 0) { c.lo = x; c.hi = 0; }
-  else { c.lo |= x << (8 * c.nv); c.hi = x >> (64 - 8 * c.nv); }
-  c.nv += 8;
-}
-// (re)stages the lane's slot at its read position (all lanes of the wave call it together)
-__device__ __forceinline__ void sc_stage(SC &c, uint32_t doc_end) {
-  c.wbeg = (c.p + c.nv) & ~15u;
-  typedef uint4 __attribute__((aligned(1))) u4l;
-  uint4 v[SW / 16];
+// ---- K1, wave-parallel: one wave per (document, column) ---------------------------------------------
+// A column is tokenised 1 KB per wave step (16 bytes per lane) by a finite automaton whose per-lane
+// transition functions are composed by a wave prefix scan, so every lane knows the state at its first
+// byte without a sequential pass.  RleDecoder<u8>: 0 = at a value byte, 1 = in a count varuint.
+// UintOptRle / IntDiffOptRle: 0 = at a value varint, 1 / 2 = inside one that has / has not a count
+// (the flag: the sign bit, bit 6 of the first byte, resp. bit 0 of the magnitude), 3 = in a count.
+// Entries start where the state is 0; each lane decodes the entries starting in its bytes, and wave
+// scans give their entry / value indices and (IntDiff) running values.  Checks: canonical
+// varints, maximal runs, no -0 diff, diffs < 2^30, values in [0, 2^32), parentInfo in {0, 1},
+// an RLE<u8> column ending without a count.
+constexpr uint32_t F_ID = 0xE4;  // identity on 4 states, 2 bits per state
+__device__ __forceinline__ uint32_t fcompose(uint32_t a, uint32_t b) {  // b after a
+  uint32_t c = 0;
 #pragma unroll
-  for (uint32_t k = 0; k < SW / 16; k++) {
-    const uint32_t q = c.wbeg + 16 * k;
-    v[k] = q < c.e && q + 16 <= doc_end ? *reinterpret_cast<const u4l *>(c.D + q) : make_uint4(0, 0, 0, 0);
-  }
-#pragma unroll
-  for (uint32_t k = 0; k < SW / 16; k++) *reinterpret_cast<uint4 *>(k1_lds + c.slot + 16 * k) = v[k];
-  c.wend = c.wbeg + SW;
-}
-__device__ __forceinline__ SC sc_make(const uint8_t *D, uint32_t p, uint32_t e, uint32_t doc_end) {
-  SC c;
-  c.D = D; c.p = p; c.e = e; c.nv = 0; c.bad = false; c.lo = c.hi = 0;
-  c.slot = threadIdx.x * SSTRIDE;
-  sc_stage(c, doc_end);
-  sc_fill(c);
+  for (uint32_t st = 0; st < 4; st++) c |= ((b >> (2 * ((a >> (2 * st)) & 3))) & 3) << (2 * st);
   return c;
 }
-__device__ __forceinline__ void sc_skip(SC &c, uint32_t n) {
-  if (n >= c.nv) { c.p += n; c.nv = 0; }
-  else if (n > 0) {
-    if (n < 8) { c.lo = (c.lo >> (8 * n)) | (c.hi << (64 - 8 * n)); c.hi >>= 8 * n; }
-    else { c.lo = c.hi >> (8 * (n - 8)); c.hi = 0; }
-    c.p += n;
-    c.nv -= n;
+#define CDPP(x, ctl, rm) (uint32_t) __builtin_amdgcn_update_dpp((int)F_ID, (int)(x), ctl, rm, 0xf, false)
+__device__ __forceinline__ uint32_t wave_incl_compose(uint32_t f) {
+  f = fcompose(CDPP(f, 0x111, 0xf), f);
+  f = fcompose(CDPP(f, 0x112, 0xf), f);
+  f = fcompose(CDPP(f, 0x114, 0xf), f);
+  f = fcompose(CDPP(f, 0x118, 0xf), f);
+  f = fcompose(CDPP(f, 0x142, 0xa), f);
+  f = fcompose(CDPP(f, 0x143, 0xc), f);
+  return f;
+}
+__device__ __forceinline__ uint64_t wave_incl_add64(uint64_t x) {
+#define A64(ctl, rm)                                                                                 \
+  {                                                                                                  \
+    const uint32_t rl = YM_DPP((uint32_t)x, ctl, rm), rh = YM_DPP((uint32_t)(x >> 32), ctl, rm);    \
+    x += ((uint64_t)rh << 32) | rl;                                                                  \
   }
-  sc_fill(c);
+  A64(0x111, 0xf) A64(0x112, 0xf) A64(0x114, 0xf) A64(0x118, 0xf) A64(0x142, 0xa) A64(0x143, 0xc)
+#undef A64
+  return x;
 }
-__device__ __forceinline__ uint32_t sc_rdb(SC &c) {
-  c.bad |= c.p >= c.e;
-  const uint32_t v = (uint32_t)c.lo & 0xffu;
-  sc_skip(c, 1);
-  return v;
+__device__ __forceinline__ uint32_t tstep(uint32_t st, uint32_t b, bool rle, uint32_t fb) {
+  const bool stop = b < 0x80;
+  if (rle) return st == 0 ? 1 : (stop ? 0 : 1);
+  if (st == 0) { const bool fl = (b >> fb) & 1; return stop ? (fl ? 3 : 0) : (fl ? 1 : 2); }
+  if (st == 1) return stop ? 3 : 1;
+  if (st == 2) return stop ? 0 : 2;
+  return stop ? 0 : 3;
 }
-__device__ __forceinline__ uint32_t sc_rvu(SC &c) {
-  const uint32_t lo = (uint32_t)c.lo, hi = (uint32_t)(c.lo >> 32);
-  const uint32_t nb = ln::vu_nb(lo, hi);
-  const uint32_t v = (lo & 0x7fu) | ((lo >> 1) & 0x3f80u) | ((lo >> 2) & 0x1fc000u) | ((lo >> 3) & 0xfe00000u) | (hi << 28);
-  const uint32_t m = (uint32_t)((1ull << (7 * (nb < 5 ? nb : 5))) - 1);
-  c.bad |= ln::vu_bad(lo, hi, nb, c.p, c.e);
-  sc_skip(c, nb < 6 ? nb : 0);
-  return v & m;
+struct Ent {
+  uint32_t val, cnt;
+  int32_t df;
+  bool fin, bad;
+};
+// the entry at pos: value (RLE: the byte; Opt: the varint's magnitude), count, IntDiff diff; fin = an
+// RLE<u8> value byte that ends the column (no count: the final run never ends)
+__device__ __forceinline__ Ent dec_entry(const uint8_t *D, uint32_t pos, uint32_t c1, uint32_t kind) {
+  Ent e{0, 0, 0, false, false};
+  if (kind == K_INFO || kind == K_PI) {
+    e.val = D[pos];
+    e.bad = kind == K_PI && e.val > 1;
+    if (pos + 1 >= c1) { e.fin = true; return e; }
+    ln::LCur c = ln::make(D, pos + 1, c1);
+    e.cnt = ln::rvu(c) + 1;
+    e.bad |= c.bad || e.cnt == 0;
+    return e;
+  }
+  ln::LCur c = ln::make(D, pos, c1);
+  bool neg;
+  const uint32_t m = rvi(c, neg);
+  if (kind == K_LC || kind == K_RC) {
+    const int32_t t = neg ? -(int32_t)m : (int32_t)m;
+    e.df = t >> 1;
+    e.cnt = (t & 1) ? ln::rvu(c) + 2 : 1;
+    e.bad = (neg && m == 0) || e.df < -(1 << 30) || e.df >= (1 << 30) || ((t & 1) && e.cnt < 2);
+  } else {
+    e.cnt = neg ? ln::rvu(c) + 2 : 1;
+    e.bad = neg && e.cnt < 2;
+  }
+  e.val = m;
+  e.bad |= c.bad;
+  return e;
 }
-__device__ __forceinline__ uint32_t sc_rvi(SC &c, bool &neg) {  // rvi over the staged cursor
-  const uint32_t lo = (uint32_t)c.lo, hi = (uint32_t)(c.lo >> 32);
-  const uint32_t nb = ln::vu_nb(lo, hi);
-  neg = (lo & 0x40) != 0;
-  uint32_t m = (lo & 0x3fu) | ((lo >> 2) & 0x1fc0u) | ((lo >> 3) & 0xfe000u) | ((lo >> 4) & 0x7f00000u) | ((hi & 0x7fu) << 27);
-  const uint32_t bits = 6 + 7 * (nb - 1);
-  if (nb < 5) m &= (1u << bits) - 1u;
-  const uint32_t last = nb <= 4 ? (lo >> (8 * nb - 8)) & 0xffu : hi & 0xffu;
-  c.bad |= (nb > 5) | (c.p + nb > c.e) | ((nb > 1) & (last == 0)) | ((nb == 5) & ((hi & 0x7fu) > 0x1fu));
-  sc_skip(c, nb < 6 ? nb : 0);
-  return m;
-}
-// every lane of the wave re-stages when any active lane is within 48 bytes of its slot's end
-#define SC_GUARD(c, doc_end) \
-  if (__any((c).p + 48 > (c).wend && (c).wend < (c).e + 16)) sc_stage((c), (doc_end))
 
-__global__ void __launch_bounds__(64) k_v2_dec(Job J) {
+__global__ void __launch_bounds__(64) k_v2_decw(Job J) {
   const GeneralJob &j = J.j;
-  const uint32_t d = blockIdx.x * 64 + threadIdx.x, kind = blockIdx.y;
-  if (d >= j.n) return;
+  const uint32_t d = blockIdx.x, kind = blockIdx.y, lane = threadIdx.x;
   Meta &M = J.meta[d];
   if (!M.ok) return;
-  const uint64_t ub = j.upd_off[j.doc_upd[d]];
-  const uint8_t *D = j.A + ub;
-  const uint32_t doc_end = (uint32_t)(j.upd_off[j.doc_upd[d] + 1] - ub);
+  const uint8_t *D = j.A + j.upd_off[j.doc_upd[d]];
   const uint32_t c0 = M.col0[col_of(kind)], c1 = M.col1[col_of(kind)];
   const uint32_t n = M.n;
-  bool bad = false;
-  uint32_t nv = 0, fin = 0, finv = 0;
+  const bool rle = kind == K_INFO || kind == K_PI, dif = kind == K_LC || kind == K_RC;
+  const uint32_t fb = dif ? 0 : 6;
+  const uint64_t cap = kind == K_SL ? 3ull * n : kind == K_CL ? 2ull * n + 1 : n;
+  uint8_t *o8 = kind == K_INFO ? a_info(J, M) : kind == K_PI ? a_pi(J, M) : nullptr;
+  uint32_t *o32 = kind == K_SL ? a_sl(J, M) : kind == K_LN ? a_ln(J, M) : nullptr;
   uint4 *ck = a_ck(J, M, kind);
-  uint32_t ne = 0;  // entries so far
-  if (kind == K_INFO || kind == K_PI) {  // RleDecoder<u8>: value byte, count - 1 unless it is the column's last byte
-    uint8_t *out = kind == K_INFO ? a_info(J, M) : a_pi(J, M);
-    SC c = sc_make(D, c0, c1, doc_end);
-    uint32_t prev = NONE;
-    while (c.p < c1 && !bad) {
-      SC_GUARD(c, doc_end);
-      if ((ne & (CKSTEP - 1)) == 0) ck[ne / CKSTEP] = make_uint4(c.p, nv, 0, 0);
-      ne++;
-      const uint32_t v = sc_rdb(c);
-      bad |= v == prev || (kind == K_PI && v > 1);
-      prev = v;
-      if (c.p == c1) { fin = 1; finv = v; break; }  // the final run never ends
-      const uint32_t cnt = sc_rvu(c) + 1;
-      bad |= c.bad || cnt > n - nv || cnt == 0;
-      if (bad) break;
-      for (uint32_t i = 0; i < cnt; i++) out[nv + i] = (uint8_t)v;
-      nv += cnt;
+  const uint32_t ckcap = (c1 - c0) / CKSTEP + 2;
+  uint32_t st = 0, ne = 0, fin = 0, finv = 0;  // carried across steps (wave-uniform)
+  uint64_t nv = 0;
+  int64_t vrun = 0;      // IntDiff: value before the next entry
+  uint32_t last = 0;     // the previous entry's value (Opt / RLE) or diff (IntDiff) ...
+  bool have_last = false;  // ... if any
+  bool bad = false;
+  for (uint32_t x = c0; x < c1 && !bad; x += 1024) {
+    const uint32_t q = x + 16 * lane;
+    uint8_t b[16];
+    {
+      const uint4 v4 = wds::load16m(D, q, c1);
+      __builtin_memcpy(b, &v4, 16);
     }
-    if (kind == K_INFO && !bad) {  // the endless final run fills the structs left
-      if (!fin && nv != n) bad = true;
-      for (uint32_t i = nv; i < n && fin; i++) out[i] = (uint8_t)finv;
+    uint32_t s0 = 0, s1 = 1, s2 = 2, s3 = 3;  // the lane's transition function (bytes past the column: identity)
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++) {
+      if (q + k < c1) { s0 = tstep(s0, b[k], rle, fb); s1 = tstep(s1, b[k], rle, fb); s2 = tstep(s2, b[k], rle, fb); s3 = tstep(s3, b[k], rle, fb); }
     }
-  } else if (kind == K_SL || kind == K_LN || kind == K_CL) {  // UintOptRleDecoder
-    uint32_t *out = kind == K_SL ? a_sl(J, M) : kind == K_LN ? a_ln(J, M) : nullptr;
-    const uint32_t cap = kind == K_SL ? 3 * n : kind == K_LN ? n : 2 * n + 1;
-    SC c = sc_make(D, c0, c1, doc_end);
-    uint32_t prev = NONE;
-    while (c.p < c1 && !bad) {
-      SC_GUARD(c, doc_end);
-      if ((ne & (CKSTEP - 1)) == 0) ck[ne / CKSTEP] = make_uint4(c.p, nv, 0, 0);
-      ne++;
-      bool neg;
-      const uint32_t v = sc_rvi(c, neg);
-      const uint32_t cnt = neg ? sc_rvu(c) + 2 : 1;
-      bad |= c.bad || v == prev || cnt > cap - nv || cnt < (neg ? 2u : 1u);
-      if (bad) break;
-      prev = v;
-      if (kind == K_CL && nv == 0) M.client = v;  // the section header's client
-      if (out)
-        for (uint32_t i = 0; i < cnt; i++) out[nv + i] = v;
-      nv += cnt;
+    const uint32_t f = s0 | (s1 << 2) | (s2 << 4) | (s3 << 6);
+    const uint32_t incl = wave_incl_compose(f);
+    const uint32_t excl = (uint32_t)__builtin_amdgcn_update_dpp((int)F_ID, (int)incl, 0x138, 0xf, 0xf, false);
+    uint32_t sl = (excl >> (2 * st)) & 3;  // state at the lane's first byte
+    uint32_t starts = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++) {
+      if (q + k < c1) {
+        if (sl == 0) starts |= 1u << k;
+        sl = tstep(sl, b[k], rle, fb);
+      }
     }
-  } else {  // IntDiffOptRleDecoder (left / right clocks)
-    SC c = sc_make(D, c0, c1, doc_end);
-    int64_t v = 0;
-    int32_t prevdf = 0;
-    bool first = true;
-    while (c.p < c1 && !bad) {
-      SC_GUARD(c, doc_end);
-      if ((ne & (CKSTEP - 1)) == 0) ck[ne / CKSTEP] = make_uint4(c.p, nv, (uint32_t)v, 0);
-      ne++;
-      bool neg;
-      const uint32_t m = sc_rvi(c, neg);
-      const int32_t t = neg ? -(int32_t)m : (int32_t)m;
-      const int32_t df = t >> 1;
-      const uint32_t cnt = (t & 1) ? sc_rvu(c) + 2 : 1;
-      // the encoder's form: no -0, diff in [-2^30, 2^30) (JS `diff << 1`), runs maximal
-      bad |= c.bad || (neg && m == 0) || df < -(1 << 30) || df >= (1 << 30) || (!first && df == prevdf) || cnt > n - nv;
-      if (bad) break;
-      v += (int64_t)df * cnt;
-      // every value stays in [0, 2^32): the run is monotone, so its ends suffice
-      const int64_t vfirst = v - (int64_t)df * (cnt - 1);
-      bad |= v < 0 || v > 0xffffffffll || vfirst < 0 || vfirst > 0xffffffffll;
-      prevdf = df;
-      first = false;
-      nv += cnt;
+    // pass 1: the lane's entries: counts, first / last key, diff sum, checks
+    uint32_t lne = 0, lfirst = 0, llast = 0, lfinv = 0;
+    uint64_t lnv = 0;
+    int64_t lsum = 0;
+    bool lbad = false, lfin = false;
+    for (uint32_t m = starts; m; m &= m - 1) {
+      const Ent e = dec_entry(D, q + __builtin_ctz(m), c1, kind);
+      const uint32_t key = dif ? (uint32_t)e.df : e.val;
+      lbad |= e.bad || (lne > 0 && key == llast) || e.cnt > cap;
+      if (e.fin) { lfin = true; lfinv = e.val; }
+      if (lne == 0) lfirst = key;
+      llast = key;
+      lne++;
+      lnv += e.cnt;
+      lsum += (int64_t)e.df * e.cnt;
+    }
+    // the entry before the lane's first: the nearest lower lane with entries, else the last step's
+    const uint64_t has = __ballot(lne > 0);
+    const uint64_t below = has & ((1ull << lane) - 1);
+    const int src = below ? 63 - __builtin_clzll(below) : (int)lane;
+    const uint32_t pk = (uint32_t)__shfl((int)llast, src);
+    lbad |= lne > 0 && (below ? pk == lfirst : (have_last && last == lfirst));
+    const uint32_t ne_incl = wave_incl_add(lne);
+    const uint64_t nv_incl = wave_incl_add64(lnv);
+    const uint64_t sum_incl = wave_incl_add64((uint64_t)lsum);
+    uint32_t ei = ne + ne_incl - lne;
+    uint64_t vbase = nv + nv_incl - lnv;
+    int64_t vr = vrun + (int64_t)(sum_incl - (uint64_t)lsum);
+    lbad |= vbase + lnv > cap || (lne > 0 && (ei + lne - 1) / CKSTEP >= ckcap);
+    // pass 2: checkpoints, IntDiff ranges, expansions
+    if (!__any(lbad)) {
+      for (uint32_t m = starts; m; m &= m - 1) {
+        const uint32_t pos = q + __builtin_ctz(m);
+        const Ent e = dec_entry(D, pos, c1, kind);
+        if ((ei & (CKSTEP - 1)) == 0) ck[ei / CKSTEP] = make_uint4(pos, (uint32_t)vbase, (uint32_t)vr, 0);
+        if (kind == K_CL && ei == 0) M.client = e.val;  // the section header's client
+        if (dif) {
+          const int64_t vfirst = vr + e.df, vlast = vr + (int64_t)e.df * e.cnt;
+          lbad |= vfirst < 0 || vfirst > 0xffffffffll || vlast < 0 || vlast > 0xffffffffll;
+          vr = vlast;
+        }
+        if (vbase + e.cnt <= cap) {
+          if (o8) for (uint32_t i = 0; i < e.cnt; i++) o8[vbase + i] = (uint8_t)e.val;
+          if (o32) for (uint32_t i = 0; i < e.cnt; i++) o32[vbase + i] = e.val;
+        }
+        vbase += e.cnt;
+        ei++;
+      }
+    }
+    bad |= __any(lbad);
+    const uint64_t fm = __ballot(lfin);
+    if (fm) {  // the final RLE entry ends the column
+      fin = 1;
+      finv = (uint32_t)__shfl((int)lfinv, 63 - __builtin_clzll(fm));
+    }
+    st = (lane_read(incl, 63) >> (2 * st)) & 3;
+    ne += lane_read(ne_incl, 63);
+    nv += lane_read64(nv_incl, 63);
+    vrun += (int64_t)lane_read64(sum_incl, 63);
+    if (has) {
+      last = (uint32_t)__shfl((int)llast, 63 - __builtin_clzll(has));
+      have_last = true;
     }
   }
-  if (bad) { M.ok = 0; M.why = 10 + kind; }
-  M.nval[kind] = nv;
-  M.nck[kind] = (ne + CKSTEP - 1) / CKSTEP;
-  M.fin[kind] = fin;
-  M.finv[kind] = finv;
+  if (!bad && kind == K_INFO) {  // the endless final run fills the structs left
+    if (!fin && nv != n) bad = true;
+    if (fin && nv <= n)
+      for (uint64_t i = nv + lane; i < n; i += 64) o8[i] = (uint8_t)finv;
+    else if (fin) bad = true;
+  }
+  if (lane == 0) {
+    if (bad) { M.ok = 0; M.why = 10 + kind; }
+    M.nval[kind] = (uint32_t)nv;
+    M.nck[kind] = (ne + CKSTEP - 1) / CKSTEP;
+    M.fin[kind] = fin;
+    M.finv[kind] = finv;
+  }
 }
 
 // ---- K2: struct pass ------------------------------------------------------------------------------------
@@ -677,7 +704,9 @@ __global__ void __launch_bounds__(64) k_v2_splice(Job J) {
       v = c4.z;
     }
   }
-  while (idx < tot) {
+  bool gbad = p < c0 || p > c1;  // guards: a resume point or entry outside the column declines
+  while (idx < tot && !gbad) {
+    if (p >= c1) { gbad = true; break; }
     uint32_t ev, cnt, entry_end;
     int32_t df = 0;
     if (kind == K_INFO || kind == K_PI) {
@@ -698,6 +727,7 @@ __global__ void __launch_bounds__(64) k_v2_splice(Job J) {
       ev = m;
       entry_end = c.p;
     }
+    if (cnt == 0 || entry_end <= p || entry_end > c1) { gbad = true; break; }
     // values idx .. idx + cnt - 1 of this entry
     for (uint32_t q = q0; q < q1; q++)
       if (q >= idx && q < idx + cnt) {
@@ -749,6 +779,7 @@ __global__ void __launch_bounds__(64) k_v2_splice(Job J) {
     if (no && (info & 0x20)) { if (off == 0 && !r) hv[nh++] = fv[fi]; fi++; }
     if (ref == 4 && !gc) hv[nh++] = fv[fi] - off;
   }
+  if (gbad) { M.ok = 0; M.why = 37; return; }
   uint8_t *hb = M.head[kind];
   Buf B{hb, 0, false};
   Enc E;
@@ -983,7 +1014,7 @@ int pv2_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const u
   J.scr = (uint8_t *)B.p[2];
   k_v2_meta_off<<<(j.n + 255) / 256, 256, 0, st>>>(J, offs);
   const dim3 g1((j.n + 63) / 64, NK);
-  k_v2_dec<<<g1, 64, 64 * SSTRIDE, st>>>(J);
+  k_v2_decw<<<dim3(j.n, NK), 64, 0, st>>>(J);
   if (op == OP_DIFF) {
     k_v2_struct<OP_DIFF><<<j.n, KT, 0, st>>>(J);
     k_v2_splice<<<g1, 64, 0, st>>>(J);
