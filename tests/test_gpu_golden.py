@@ -33,10 +33,11 @@ def test_golden_batched_on_gpu(engine, key):
     _check_group(engine, key)
 
 
-@pytest.mark.parametrize("key", [("diff", 1), ("sv", 1), ("diff", 2), ("sv", 2)], ids=lambda k: f"{k[0]}-v{k[1]}")
+@pytest.mark.parametrize("key", [("diff", 1), ("sv", 1), ("meta", 1), ("diff", 2), ("sv", 2), ("meta", 2)],
+                         ids=lambda k: f"{k[0]}-v{k[1]}")
 def test_golden_through_chunked_walk(engine, key, monkeypatch):
     """The chunk-parallel V1 walk (ym_pwalk.hip) and the column-parallel V2 path (ym_pv2.hip) normally
-    take updates of >= 32 KB only; with their threshold at 1 byte every golden diff / state-vector vector
+    take updates of >= 32 KB only; with their threshold at 1 byte every golden diff / state-vector / meta vector
     goes through them (fallback to the sequential walkers on a decline) and must still come out
     byte-identical."""
     monkeypatch.setenv("YMERGE_PW_MIN", "1")

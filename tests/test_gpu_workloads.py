@@ -64,14 +64,15 @@ def test_sv_and_diff_workload_matches_oracle(engine, fmt):
     assert engine.stats["docs_fast"] == engine.stats["docs"], engine.stats
 
 
+@pytest.mark.parametrize("op", ["sv", "meta"])
 @pytest.mark.parametrize("fmt", [1, 2])
-def test_c3_sv_matches_oracle(engine, fmt):
+def test_c3_sv_matches_oracle(engine, fmt, op):
     arena, upd_off, doc_upd = load_ymb(f"c3_v{fmt}")
     from yjs_amd import pack_docs
     upd = arena.tobytes()
     a2, o2, d2 = pack_docs([[upd] for _ in range(4)])
-    outs, st, _ = O.batch("sv", fmt, a2, o2, d2)
-    bad = _compare(engine.run_host("sv", fmt, a2, o2, d2), outs, st)
+    outs, st, _ = O.batch(op, fmt, a2, o2, d2)
+    bad = _compare(engine.run_host(op, fmt, a2, o2, d2), outs, st)
     assert not bad, bad[:10]
     assert engine.stats["docs_fast"] == engine.stats["docs"], engine.stats
     # the chunk-parallel walk (V1) / column-parallel path (V2) takes every C3 update

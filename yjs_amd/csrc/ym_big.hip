@@ -103,7 +103,7 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
   const uint32_t lane = threadIdx.x;
   const Scr X = scratch(j);
   for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
-    if (OP != OP_META && j.pw_done && j.pw_done[d] == 1) continue;  // completed by the chunk-parallel walk
+    if (j.pw_done && j.pw_done[d] == 1) continue;  // completed by the chunk-parallel walk
     const uint32_t u0 = j.doc_upd[d];
     if (j.doc_upd[d + 1] - u0 != 1) YB_DECLINE()
     // the update, read by scalar loads (ym_scalar.h): byte offsets from a dword-aligned base

@@ -618,6 +618,21 @@ __global__ void __launch_bounds__(KT) k_v2_struct(Job J) {
     j.out_len[d] = total;
     j.status[d] = ym::ST_OK;
   }
+  if (OP == OP_META) {
+    // parseUpdateMetaV2 of one section with structs: from = {client: first clock}, to = {client: end}
+    const uint32_t end = (uint32_t)clock;
+    const uint32_t total = 2 + 2 * vsz(M.client) + vsz(M.clock0) + vsz(end);
+    const uint64_t b = atomicAdd((unsigned long long *)j.used, (unsigned long long)total);
+    J.done[d] = 1;
+    atomicAdd((unsigned long long *)j.pw_count, 1ull);
+    if (b + total > j.cap) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; return; }
+    uint8_t *o = j.out + b;
+    uint32_t p = 0;
+    for (uint32_t v : {1u, M.client, M.clock0, 1u, M.client, end}) { while (v > 127) { o[p++] = (uint8_t)(0x80 | (v & 127)); v >>= 7; } o[p++] = (uint8_t)v; }
+    j.out_off[d] = b;
+    j.out_len[d] = total;
+    j.status[d] = ym::ST_OK;
+  }
 }
 
 // ---- K3: splice heads ---------------------------------------------------------------------------------
@@ -978,13 +993,13 @@ int pv_ensure(PwBufs &B, int k, size_t n) {
 }
 }  // namespace
 
-// Column-parallel V2 diff / sv over the large single-section documents of a call; marks the documents it
+// Column-parallel V2 diff / sv / meta over the large single-section documents of a call; marks the documents it
 // completes in *done_out (k_big_v2 skips them).  1 = launched, 0 = not applicable, < 0 = error.
 static pv2::Meta *pv2_last_meta = nullptr;
 int pv2_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const uint8_t **done_out) {
   using namespace pv2;
   *done_out = nullptr;
-  if (!j.v2 || (op != OP_DIFF && op != OP_SV) || j.n == 0 || !j.pw_count || getenv("YMERGE_NO_PW")) return 0;
+  if (!j.v2 || (op != OP_DIFF && op != OP_SV && op != OP_META) || j.n == 0 || !j.pw_count || getenv("YMERGE_NO_PW")) return 0;
   uint64_t pv_min = PV_MIN;
   if (const char *e = getenv("YMERGE_PW_MIN")) pv_min = strtoull(e, nullptr, 10);
   if (!B.pinned && hipHostMalloc((void **)&B.pinned, 64, hipHostMallocDefault) != hipSuccess) return -2;
@@ -1020,8 +1035,10 @@ int pv2_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const u
     k_v2_splice<<<g1, 64, 0, st>>>(J);
     const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
     k_v2_out<<<grid, 64, 0, st>>>(J);
-  } else {
+  } else if (op == OP_SV) {
     k_v2_struct<OP_SV><<<j.n, KT, 0, st>>>(J);
+  } else {
+    k_v2_struct<OP_META><<<j.n, KT, 0, st>>>(J);
   }
   return 1;
 }

@@ -51,6 +51,10 @@ constexpr uint32_t CAP = CH / 2 + 8;   // records per chunk (a struct is >= 2 by
 constexpr uint32_t SPEC_CAP = 64;
 constexpr uint32_t NFIRST = 8;         // records per chunk descriptor (the stitch's entry lookup)
 constexpr uint32_t FAIL_RUN = 8;       // failed positions in a row before the walk only tries short-cut candidates
+// a chunk starts mid-struct: its first START_CHEAP bytes try short-cut candidates only (C3 meets the true
+// chain there after a few bytes); a chunk still off the chain after them (structs outside the short cut,
+// C5's XML items) goes back to the full parser at every position
+constexpr uint32_t START_CHEAP = 48;
 constexpr uint64_t PW_MIN = 32768;     // smaller updates stay on k_big_v1
 constexpr uint32_t NSEC = BS_NSEC, NSV = BS_NSV, PRE = BS_PRE, SECW = BS_SECW;
 constexpr uint32_t NPATCH = 1024;
@@ -122,9 +126,13 @@ __global__ void __launch_bounds__(256) k_pw_walk(GeneralJob j, const uint32_t *c
   const uint8_t *D = j.A + ub;
   const uint32_t c0 = ci * CH, c1 = c0 + CH < len ? c0 + CH : len;
   uint32_t nrec = 0, cum = 0, lastfail = 0, lastpatch = 0, lastskip = 0, fails = FAIL_RUN, okrun = 0;  // the chunk start is mid-struct: only short-cut candidates until two structs in a row
-  bool frun = false, ovf = false;
+  bool frun = false, ovf = false, start = true;
   uint32_t p = c0;
   while (p < c1) {
+    if (start && p >= c0 + START_CHEAP) {
+      start = false;
+      if (fails >= FAIL_RUN) fails = 0;
+    }
     uint32_t cl, fl, nx;
     bool ok = ln::parse_fast(D, p, len, nx, cl, fl);  // branch-free short cut (most structs)
 #ifdef YM_PW_PROF
@@ -282,7 +290,7 @@ __device__ bool slice_head(sc::cu32 *B, uint32_t adj, uint32_t s0, uint32_t s1, 
   }
 #define PW_DECLINE() PW_DECLINE_R(why ? why : 2)
 
-// OP = OP_DIFF or OP_SV
+// OP = OP_DIFF, OP_SV or OP_META (parseUpdateMeta: from = a section's first clock, to = its end clock)
 template <int OP>
 __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *cbase, const uint4 *desc, const uint2 *recs,
                                                   uint8_t *done) {
@@ -348,6 +356,9 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
         if (c.bad) { declined = true; why = 5; break; }
       }
       if (ci > 0 && client == prev_client) { declined = true; why = 6; break; }
+      // meta: taken only when the clients descend (a repeated client would keep its first Map slot)
+      if (OP == OP_META && ci > 0 && client > prev_client) { declined = true; why = 6; break; }
+      const uint32_t first_clock = (uint32_t)clock;
       prev_client = client;
       const uint32_t k = OP == OP_DIFF ? sv_lookup(X.svt, nsv, client) : 0;
       if (OP == OP_SV && nstructs > 0 && sv_any && client != sv_client) {
@@ -477,7 +488,7 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
           const uint32_t fs = skm ? (uint32_t)__builtin_ctzll(skm) : n;  // first Skip
           if (!sv_stop && fs > 0) sv_clock = (uint32_t)(clock + lane_read(incl, fs - 1));
           if (skm) sv_stop = true;
-        } else {
+        } else if (OP == OP_DIFF) {
           uint32_t first = 0;  // first struct of this batch written verbatim (patch range start)
           bool pend = false;
           if (!copying) {
@@ -539,6 +550,11 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
         rem -= n;
       }
       if (declined) break;
+      if (OP == OP_META && nstructs > 0) {
+        if (sv_n >= NSV) { declined = true; why = 13; break; }
+        if (lane == 0) { X.svt[2 * sv_n] = client; X.svt[2 * sv_n + 1] = first_clock; X.sec[sv_n] = (uint32_t)clock; }
+        sv_n++;
+      }
       if (OP == OP_DIFF) {
         if (lane == 0) {
           sec(ci, S_B1) = copying ? x : 0;
@@ -550,6 +566,34 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
     }
     if (declined) PW_DECLINE()
     __syncthreads();
+    if (OP == OP_META) {  // from then to, each vu(n) | (client, clock)*
+      __threadfence_block();
+      __syncthreads();
+      uint32_t tl = 0;
+      for (uint32_t i = lane; i < sv_n; i += 64) tl += 2 * vsz(X.svt[2 * i]) + vsz(X.svt[2 * i + 1]) + vsz(X.sec[i]);
+      const uint32_t total = 2 * vsz(sv_n) + lane_read(wave_incl_add(tl), 63);
+      uint64_t base = 0;
+      if (lane == 0) base = atomicAdd((unsigned long long *)j.used, (unsigned long long)total);
+      base = ((uint64_t)lane_read((uint32_t)(base >> 32), 0) << 32) | lane_read((uint32_t)base, 0);
+      if (lane == 0) { done[d] = 1; atomicAdd((unsigned long long *)j.pw_count, 1ull); }
+      if (base + total > j.cap) {
+        if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }
+        __syncthreads();
+        continue;
+      }
+      if (lane == 0) {
+        uint8_t *o = j.out + base;
+        uint32_t p = put_vu_g(o, 0, sv_n);
+        for (uint32_t i = 0; i < sv_n; i++) { p = put_vu_g(o, p, X.svt[2 * i]); p = put_vu_g(o, p, X.svt[2 * i + 1]); }
+        p = put_vu_g(o, p, sv_n);
+        for (uint32_t i = 0; i < sv_n; i++) { p = put_vu_g(o, p, X.svt[2 * i]); p = put_vu_g(o, p, X.sec[i]); }
+        j.out_off[d] = base;
+        j.out_len[d] = total;
+        j.status[d] = ym::ST_OK;
+      }
+      __syncthreads();
+      continue;
+    }
     if (OP == OP_SV) {
       if (sv_any && sv_clock != 0) {
         if (sv_n >= NSV) PW_DECLINE_R(13)
@@ -695,7 +739,7 @@ const uint8_t *pw_last_done = nullptr;
 int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const uint8_t **done_out) {
   using namespace pw;
   *done_out = nullptr;
-  if (j.v2 || (op != OP_DIFF && op != OP_SV) || j.n == 0 || !j.pw_count || getenv("YMERGE_NO_PW")) return 0;
+  if (j.v2 || (op != OP_DIFF && op != OP_SV && op != OP_META) || j.n == 0 || !j.pw_count || getenv("YMERGE_NO_PW")) return 0;
   // YMERGE_PW_MIN: smallest update taken (tests push small golden cases through this path)
   uint64_t pw_min = PW_MIN;
   if (const char *e = getenv("YMERGE_PW_MIN")) pw_min = strtoull(e, nullptr, 10);
@@ -725,7 +769,8 @@ int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const ui
   k_pw_walk<<<(total + 255) / 256, 256, 0, st>>>(j, cbase, j.n, total, desc, recs);
   const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
   if (op == OP_DIFF) k_pw_stitch<OP_DIFF><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done);
-  else k_pw_stitch<OP_SV><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done);
+  else if (op == OP_SV) k_pw_stitch<OP_SV><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done);
+  else k_pw_stitch<OP_META><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done);
   return 1;
 }
 
