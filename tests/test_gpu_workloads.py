@@ -141,7 +141,7 @@ def test_c3_damaged_updates_chunked_walk(engine, fmt):
     from yjs_amd import pack_docs
     a2, o2, d2 = pack_docs([[u] for u in docs])
     sva, svo, _ = pack_docs([[s] for s in svs])
-    for op in ("diff", "sv"):
+    for op in ("diff", "sv", "meta"):
         extra = (sva, svo) if op == "diff" else ()
         outs, st, _ = O.batch(op, fmt, a2, o2, d2, *extra, nthreads=8)
         bad = _compare(engine.run_host(op, fmt, a2, o2, d2, *extra), outs, st)
@@ -448,3 +448,49 @@ def test_device_u32_offsets_mixed_paths(engine):
             bad.append(c["id"])
     assert not bad, bad[:10]
     assert engine.stats["docs_general"] > 0, engine.stats
+
+
+def _many_client_update(clients, ds):
+    """A V1 update with one two-character Y.Text insert per client (descending client order, clock 0;
+    no origin, parent ykey "t") and the delete set `ds` = [(client, [(clock, len), ...]), ...]."""
+    b = bytearray(_vu(len(clients)))
+    for c in clients:
+        b += _vu(1) + _vu(c) + _vu(0) + bytes([0x04, 1, 1, ord("t"), 2, ord("a"), ord("b")])
+    return bytes(b + _encode_ds(ds, False))
+
+
+@pytest.mark.parametrize("pw_min", ["1", None], ids=["chunked", "streamed"])
+@pytest.mark.parametrize("fmt", [1, 2])
+def test_client_map_many_clients(engine, fmt, pw_min, monkeypatch):
+    """Above 64 state-vector entries / delete-set clients the walkers look clients up in a per-block hash
+    map (ym_cmap.h) instead of scanning the list: state vectors with 65-300 entries, repeated clients
+    (decodeStateVector: the later entry wins) and absent ones; delete sets of 65-200 clients, some with a
+    client repeated (readDeleteSet merges it: the walkers must decline to the general path).  Diff, state
+    vector and meta through the chunk walk / column path (threshold 1 byte) and the streamed walkers."""
+    if pw_min:
+        monkeypatch.setenv("YMERGE_PW_MIN", pw_min)
+    from yjs_amd import pack_docs
+    rng = np.random.default_rng(31 + fmt)
+    docs, svs = [], []
+    for d in range(48):
+        nc = int(rng.integers(65, 200))
+        clients = sorted((int(c) for c in rng.choice(10**6, size=nc, replace=False)), reverse=True)
+        nd = int(rng.integers(65, 200)) if d % 3 else int(rng.integers(1, 8))
+        ds = [(int(c), [(0, 1)] if i % 2 else [(0, 1), (3, 2)]) for i, c in enumerate(rng.choice(10**6, size=nd, replace=False))]
+        if d % 4 == 1:  # a repeated delete-set client
+            ds.append((ds[int(rng.integers(0, len(ds)))][0], [(9, 1)]))
+        u = _many_client_update(clients if fmt == 1 or d % 8 else clients[:1], ds)
+        if fmt == 2:
+            u = O.convert(u, 1)[1]
+        docs.append(u)
+        sv = [(c, int(rng.integers(0, 3))) for c in rng.choice(clients, size=min(nc, int(rng.integers(60, 300))))]
+        sv += [(int(c), 5) for c in rng.integers(10**6, 2 * 10**6, size=8)]  # absent clients
+        rng.shuffle(sv)
+        svs.append(_vu(len(sv)) + b"".join(_vu(int(c)) + _vu(k) for c, k in sv))
+    a, o, dd = pack_docs([[u] for u in docs])
+    sva, svo, _ = pack_docs([[s] for s in svs])
+    for op in ("diff", "sv", "meta"):
+        extra = (sva, svo) if op == "diff" else ()
+        outs, st, _ = O.batch(op, fmt, a, o, dd, *extra, nthreads=8)
+        bad = _compare(engine.run_host(op, fmt, a, o, dd, *extra), outs, st)
+        assert not bad, (op, bad[:10])

@@ -21,6 +21,7 @@
 #include "ym_fast_common.h"
 #include "ym_kernels.h"
 #include "ym_scalar.h"
+#include "ym_cmap.h"
 
 namespace ymk {
 namespace big {
@@ -47,10 +48,11 @@ constexpr uint32_t NONE = 0xffffffffu;
 struct Scr {
   uint32_t *sec, *svt, *dsc;
   uint8_t *pre;
+  uint32_t *map;
 };
 __device__ __forceinline__ Scr scratch(const GeneralJob &j) {
   uint8_t *b = j.bscratch + (uint64_t)blockIdx.x * BS_BYTES;
-  return Scr{(uint32_t *)(b + BS_SEC), (uint32_t *)(b + BS_SVT), (uint32_t *)(b + BS_DSC), b + BS_PREB};
+  return Scr{(uint32_t *)(b + BS_SEC), (uint32_t *)(b + BS_SVT), (uint32_t *)(b + BS_DSC), b + BS_PREB, (uint32_t *)(b + BS_MAP)};
 }
 #define sec(ci, f) X.sec[SECW * (ci) + (f)]
 // sv[client] (decodeStateVector: a later entry for the same client wins), wave-parallel
@@ -132,6 +134,7 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
       }
       __syncthreads();
       if (bad) YB_DECLINE()
+      if (nsv > 64) cmap::build_sv(X.map, X.svt, nsv);
     }
     // ---- struct section (encoding.js:127-198 layout; 13.5.16 LazyStructReader)
     SCur c = sc::make(B, adj, adj + (uint32_t)len64);
@@ -154,7 +157,7 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
       if (OP == OP_META && ci > 0 && client > prev_client) { declined = true; break; }
       const uint32_t first_clock = (uint32_t)clock;
       prev_client = client;
-      const uint32_t k = OP == OP_DIFF ? sv_lookup(X.svt, nsv, client) : 0;
+      const uint32_t k = OP != OP_DIFF ? 0 : nsv > 64 ? cmap::sv_get(X.map, X.svt, client) : sv_lookup(X.svt, nsv, client);
       if (OP == OP_SV && nstructs > 0 && sv_any && client != sv_client) {  // client change (os@37724)
         if (sv_clock != 0) {
           if (sv_n >= NSV) { declined = true; break; }
@@ -364,13 +367,15 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
     const uint32_t ds0 = rel(c.p);
     {
       const uint32_t ndc = rvu(c);
+      const bool big = ndc > 64 && ndc <= BS_NDSC && !c.bad;
+      if (big) cmap::clear(X.map);
       for (uint32_t i = 0; i < ndc && !c.bad && !declined; i++) {
         const uint32_t client = rvu(c);
         const uint32_t m = rvu(c);
         // readDeleteSet drops clients without ranges and merges a repeated client into its first
         // occurrence: either makes the re-written set differ from the input bytes
         if (m == 0 || i >= BS_NDSC) { declined = true; break; }
-        if (seen_before(X.dsc, i, client)) { declined = true; break; }
+        if (big ? cmap::seen_insert(X.map, client) : seen_before(X.dsc, i, client)) { declined = true; break; }
         if (lane == 0) X.dsc[i] = client;
         __threadfence_block();
         for (uint32_t q = 0; q < m && !c.bad; q++) {

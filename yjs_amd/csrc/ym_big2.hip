@@ -17,6 +17,7 @@
 
 #include "ym_fast_common.h"
 #include "ym_kernels.h"
+#include "ym_cmap.h"
 
 namespace ymk {
 namespace big2 {
@@ -49,11 +50,11 @@ enum { M_BAD = 0, M_KEYS, M_KCLOCK, M_SPOS };
 // per-block HBM scratch (ym_kernels.h BS_*): parts (rest start, rest end, written), state vector,
 // delete-set clients
 struct Scr {
-  uint32_t *part, *svt, *dsc;
+  uint32_t *part, *svt, *dsc, *map;
 };
 __device__ __forceinline__ Scr scratch(const GeneralJob &j) {
   uint8_t *b = j.bscratch + (uint64_t)blockIdx.x * BS_BYTES;
-  return Scr{(uint32_t *)(b + BS_SEC), (uint32_t *)(b + BS_SVT), (uint32_t *)(b + BS_DSC)};
+  return Scr{(uint32_t *)(b + BS_SEC), (uint32_t *)(b + BS_SVT), (uint32_t *)(b + BS_DSC), (uint32_t *)(b + BS_MAP)};
 }
 __device__ __forceinline__ uint32_t sv_lookup(const uint32_t *svt, uint32_t nsv, uint32_t client) {
   int best = -1;  // decodeStateVector: a later entry for the same client wins
@@ -427,6 +428,7 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
       __threadfence_block();
       __syncthreads();
       if (c.bad) YB2_DECLINE()
+      if (nsv > 64) cmap::build_sv(X.map, X.svt, nsv);
     }
     // ---- header: feature flag, nine columns (UpdateDecoderV2 constructor, UpdateDecoder.js:274-293)
     ist(I_REST, 0) = 0;
@@ -504,7 +506,7 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
       if (OP == OP_META && ci > 0 && client > prev_client) { set_bad(); break; }
       prev_client = client;
       const uint32_t first_clock = (uint32_t)clock;
-      const uint32_t k = OP == OP_DIFF ? sv_lookup(X.svt, nsv, client) : 0;
+      const uint32_t k = OP != OP_DIFF ? 0 : nsv > 64 ? cmap::sv_get(X.map, X.svt, client) : sv_lookup(X.svt, nsv, client);
       if (OP == OP_SV && nstructs > 0 && sv_any && client != sv_client) {
         if (sv_clock != 0) {
           if (sv_n >= NSV) { set_bad(); break; }
@@ -626,6 +628,8 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
       ds0 = c.p - ist(I_REST, 2);
       const uint32_t ndc = rvu(c);
       s_commit(D, I_REST, c);
+      const bool big = ndc > 64 && ndc <= BS_NDSC;
+      if (big) cmap::clear(X.map);
       for (uint32_t i = 0; i < ndc && !is_bad(); i++) {
         c = s_cur(D, I_REST, MREST);
         const uint32_t client = rvu(c);
@@ -633,7 +637,8 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
         s_commit(D, I_REST, c);
         if (m == 0 || i >= BS_NDSC) { set_bad(); break; }
         bool hit = false;  // readDeleteSet merges a repeated client: the bytes would change
-        for (uint32_t h0 = 0; h0 < i; h0 += 64) hit |= __any(h0 + lane < i && X.dsc[h0 + lane] == client);
+        if (big) hit = cmap::seen_insert(X.map, client);
+        else for (uint32_t h0 = 0; h0 < i; h0 += 64) hit |= __any(h0 + lane < i && X.dsc[h0 + lane] == client);
         if (hit) set_bad();
         __syncthreads();
         if (lane == 0) X.dsc[i] = client;

@@ -56,7 +56,9 @@ constexpr uint64_t BS_SEC = 0;                                      // u32[BS_NS
 constexpr uint64_t BS_PREB = BS_SEC + 4ull * BS_NSEC * BS_SECW;     // u8[BS_NSEC][BS_PRE]
 constexpr uint64_t BS_SVT = BS_PREB + (uint64_t)BS_NSEC * BS_PRE;   // u32[BS_NSV][2]
 constexpr uint64_t BS_DSC = BS_SVT + 8ull * BS_NSV;                 // u32[BS_NDSC]
-constexpr uint64_t BS_BYTES = BS_DSC + 4ull * BS_NDSC;
+constexpr uint32_t BS_MAP_SLOTS = 4096;                             // client map (ym_cmap.h)
+constexpr uint64_t BS_MAP = BS_DSC + 4ull * BS_NDSC;                // u32[2][BS_MAP_SLOTS] keys, values
+constexpr uint64_t BS_BYTES = BS_MAP + 8ull * BS_MAP_SLOTS;
 constexpr uint32_t BS_GRID = 8192;  // up to 32 one-wave blocks per CU; scratch sized by the launch's grid
 
 // device buffers of the large-document merge pipeline (ym_large.hip), grown on demand, cached

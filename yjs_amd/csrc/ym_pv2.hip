@@ -34,6 +34,7 @@
 
 #include "ym_fast_common.h"
 #include "ym_kernels.h"
+#include "ym_cmap.h"
 #include "ym_lane.h"
 #include "ym_wave_ds.h"
 
@@ -885,6 +886,9 @@ __global__ void __launch_bounds__(64) k_v2_out(Job J) {
       bad = c.bad || ndc > 4096;
     }
     uint32_t *dsc = reinterpret_cast<uint32_t *>(j.bscratch + (uint64_t)blockIdx.x * BS_BYTES + BS_DSC);
+    uint32_t *map = reinterpret_cast<uint32_t *>(j.bscratch + (uint64_t)blockIdx.x * BS_BYTES + BS_MAP);
+    const bool big = !bad && ndc > 64 && ndc <= BS_NDSC;
+    if (big) cmap::clear(map);
     for (uint32_t i = 0; i < ndc && !bad; i++) {
       ln::LCur h = ln::make(D, x, len);
       const uint32_t client = ln::rvu(h);
@@ -892,7 +896,8 @@ __global__ void __launch_bounds__(64) k_v2_out(Job J) {
       x = h.p;
       if (h.bad || m == 0 || i >= BS_NDSC) { bad = true; break; }
       bool hit = false;
-      for (uint32_t h0 = 0; h0 < i; h0 += 64) hit |= __any(h0 + lane < i && dsc[h0 + lane] == client);
+      if (big) hit = cmap::seen_insert(map, client);
+      else for (uint32_t h0 = 0; h0 < i; h0 += 64) hit |= __any(h0 + lane < i && dsc[h0 + lane] == client);
       if (hit) { bad = true; break; }
       __syncthreads();
       if (lane == 0) dsc[i] = client;

@@ -32,6 +32,7 @@
 #include "ym_lane.h"
 #include "ym_scalar.h"
 #include "ym_wave_ds.h"
+#include "ym_cmap.h"
 
 namespace ymk {
 namespace pw {
@@ -68,10 +69,11 @@ constexpr uint32_t NONE = 0xffffffffu;
 struct Scr {
   uint32_t *sec, *svt, *dsc;
   uint8_t *pre;
+  uint32_t *map;
 };
 __device__ __forceinline__ Scr scratch(const GeneralJob &j) {
   uint8_t *b = j.bscratch + (uint64_t)blockIdx.x * BS_BYTES;
-  return Scr{(uint32_t *)(b + BS_SEC), (uint32_t *)(b + BS_SVT), (uint32_t *)(b + BS_DSC), b + BS_PREB};
+  return Scr{(uint32_t *)(b + BS_SEC), (uint32_t *)(b + BS_SVT), (uint32_t *)(b + BS_DSC), b + BS_PREB, (uint32_t *)(b + BS_MAP)};
 }
 #define sec(ci, f) X.sec[SECW * (ci) + (f)]
 
@@ -325,6 +327,7 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
       }
       __syncthreads();
       if (bad) PW_DECLINE_R(3)
+      if (nsv > 64) cmap::build_sv(X.map, X.svt, nsv);
     }
     // ---- struct section: headers parsed here, structs from the walk's records
     uint32_t x = 0;
@@ -360,7 +363,7 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
       if (OP == OP_META && ci > 0 && client > prev_client) { declined = true; why = 6; break; }
       const uint32_t first_clock = (uint32_t)clock;
       prev_client = client;
-      const uint32_t k = OP == OP_DIFF ? sv_lookup(X.svt, nsv, client) : 0;
+      const uint32_t k = OP != OP_DIFF ? 0 : nsv > 64 ? cmap::sv_get(X.map, X.svt, client) : sv_lookup(X.svt, nsv, client);
       if (OP == OP_SV && nstructs > 0 && sv_any && client != sv_client) {
         if (sv_clock != 0) {
           if (sv_n >= NSV) { declined = true; why = 13; break; }
@@ -633,6 +636,8 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
       x = c.p;
       declined = c.bad;
       why = 17;
+      const bool big = ndc > 64 && ndc <= BS_NDSC;
+      if (big) cmap::clear(X.map);
       for (uint32_t i = 0; i < ndc && !declined; i++) {
         ln::LCur h = ln::make(D, x, len);
         const uint32_t client = ln::rvu(h);
@@ -641,7 +646,7 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
         // readDeleteSet drops clients without ranges and merges a repeated client into its first
         // occurrence: either makes the re-written set differ from the input bytes
         if (h.bad || m == 0 || i >= BS_NDSC) { declined = true; why = 14; break; }
-        if (seen_before(X.dsc, i, client)) { declined = true; why = 15; break; }
+        if (big ? cmap::seen_insert(X.map, client) : seen_before(X.dsc, i, client)) { declined = true; why = 15; break; }
         if (lane == 0) X.dsc[i] = client;
         __threadfence_block();
         x = wds::skip_varuints(D, x, len, 2ull * m);
