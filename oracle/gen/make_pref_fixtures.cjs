@@ -14,6 +14,10 @@
 //   P-ref-3  merged applies to a fresh Doc with no pending structs or delete readers (StructStore.js:25-35);
 //   P-ref-sv encodeStateVectorFromUpdate(u) equals, as a map, the reference's encodeStateVector of the
 //            Doc u builds (encoding.js:587-611), when u applies completely.
+//   P-ref-diff diffUpdate(u, sv) carries, unit for unit, the structs of the reference's
+//            encodeStateAsUpdate(Doc(u), sv) (encoding.js:490-526: writeClientsStructs slices every client at
+//            sv[client], :94-116), both decoded with the reference's readClientsStructRefs; and the same
+//            delete-set coverage as the reference's (createDeleteSetFromStructStore), when u applies completely.
 // Cases the reference cannot evaluate are recorded with the reason (e.g. Skip structs -- 13.5.16 output
 // for gapped inputs, which 13.4.9 cannot decode, SURVEY.md F9).  Output: tests/pref/pref.json with, per
 // case, the golden id, the sha256 of the bytes that were checked (the golden expectation = the engine's
@@ -72,6 +76,48 @@ function units (Y, doc) {
   return JSON.stringify(out, (k, v) => typeof v === 'bigint' ? 'bigint:' + v.toString() : v)
 }
 
+// the structs of an update as units, decoded by the reference's own reader (no integration: a diff misses
+// the structs its receiver already has)
+function updateUnits (Y, bytes, v2) {
+  const UDec = v2 ? Y.UpdateDecoderV2 : Y.UpdateDecoderV1
+  const doc = new Y.Doc()
+  const refs = Y.readClientsStructRefs(new UDec(decoding.l1(bytes)), new Map(), doc)
+  const out = []
+  const idOf = id => id ? [id.client, id.clock] : null
+  const parentOf = it => {
+    const p = it.parent
+    if (p === null || p === undefined) return null
+    if (p.constructor === Y.ID) return ['id', p.client, p.clock]
+    for (const [k, v] of doc.share) if (v === p) return ['root', k]
+    return ['?']
+  }
+  for (const client of [...refs.keys()].sort((a, b) => a - b)) {
+    for (const s of refs.get(client)) {
+      if (s.constructor === Y.GC) { for (let i = 0; i < s.length; i++) out.push([client, s.id.clock + i, 'GC']); continue }
+      const ct = s.content
+      let vals = null
+      try { vals = ct.getContent() } catch (e) { vals = null }
+      for (let i = 0; i < s.length; i++) {
+        let v = vals && vals.length === s.length ? vals[i] : null
+        if (ct.constructor === Y.ContentFormat) v = [ct.key, ct.value]
+        if (ct.constructor === Y.ContentType) v = [ct.type.constructor.name, ct.type.nodeName || ct.type.hookName || null]
+        if (v && typeof v === 'object' && v.constructor && v.constructor.name !== 'Object' && v.constructor.name !== 'Array' &&
+            !(v instanceof Uint8Array)) v = v.constructor.name
+        if (v instanceof Uint8Array) v = Array.from(v)
+        if (typeof v === 'string' && v.length === 1 && (v === '\ufffd' || (v.charCodeAt(0) >= 0xd800 && v.charCodeAt(0) <= 0xdfff))) v = '<surrogate half or U+FFFD>'
+        out.push([client, s.id.clock + i, ct.constructor.name, i === 0 ? idOf(s.origin) : [client, s.id.clock + i - 1],
+          idOf(s.rightOrigin), i === 0 ? parentOf(s) : null, i === 0 ? s.parentSub : null, v === undefined ? '<undefined>' : v])
+      }
+    }
+  }
+  return JSON.stringify(out, (k, v) => typeof v === 'bigint' ? 'bigint:' + v.toString() : v)
+}
+
+function covSubset (a, b) { // every [start, end) of coverage a lies inside one of b's (both merged, sorted)
+  const m = new Map(b)
+  return a.every(([client, iv]) => iv.every(([s, e]) => (m.get(client) || []).some(([s2, e2]) => s2 <= s && e <= e2)))
+}
+
 function coverage (ds) { // DeleteSet -> {client: [[start, end], ...]} (union of the ranges)
   const out = {}
   for (const [client, items] of ds.clients) {
@@ -90,7 +136,7 @@ function coverage (ds) { // DeleteSet -> {client: [[start, end], ...]} (union of
   for (const f of fs.readdirSync(GOLDEN).filter(f => f.endsWith('.json')).sort()) {
     const g = path.basename(f, '.json')
     for (const c of JSON.parse(fs.readFileSync(path.join(GOLDEN, f))).cases) {
-      if (!c.expect || (c.op !== 'merge' && c.op !== 'sv')) continue
+      if (!c.expect || (c.op !== 'merge' && c.op !== 'sv' && c.op !== 'diff')) continue
       const id = `${g}/${c.name}/v${c.fmt}/${c.op}`
       const v2 = c.fmt === 2
       const apply = v2 ? Y.applyUpdateV2 : Y.applyUpdate
@@ -135,6 +181,27 @@ function coverage (ds) { // DeleteSet -> {client: [[start, end], ...]} (union of
             r.applicable = false
             r.reason = 'inputs of inconsistent histories (a GC and a live Item for the same ID): the Doc keeps whichever it integrates first'
           } else r.applicable = true
+        } else if (c.op === 'diff') {
+          const doc = new Y.Doc({ gc: false })
+          apply(doc, inputs[0])
+          const sv = u8(c.sv)
+          const ref = encode(doc, sv)
+          const ua = updateUnits(Y, ref, v2); const ub = updateUnits(Y, out, v2)
+          r.pref_diff = ua === ub
+          if (!r.pref_diff && process.env.PREF_DEBUG) {
+            const A = JSON.parse(ua); const B = JSON.parse(ub)
+            for (let i = 0; i < Math.max(A.length, B.length); i++) if (JSON.stringify(A[i]) !== JSON.stringify(B[i])) { console.log(id, i, JSON.stringify(A[i]), JSON.stringify(B[i])); break }
+          }
+          r.units_sha256 = sha(Buffer.from(ub))
+          const readDs = u => { const d = new UDec(decoding.l1(u)); Y.readClientsStructRefs(d, new Map(), new Y.Doc()); return Y.readDeleteSet(d) }
+          // the lazy diff keeps the input's delete set (P-ref-2 for a single input); the reference's Doc
+          // additionally marks what integration deletes (children of deleted types, overwritten map entries:
+          // Item.js:403-517), so its set must contain the engine's
+          r.ds_coverage = coverage(readDs(out))
+          r.pref_diff_ds = r.ds_coverage === coverage(readDs(inputs[0]))
+          r.pref_diff_ds_in_ref = covSubset(JSON.parse(r.ds_coverage), JSON.parse(coverage(readDs(ref))))
+          r.applicable = pending(doc) === 0
+          if (!r.applicable) r.reason = 'the update leaves pending structs or delete ranges in the reference (gaps)'
         } else {
           const doc = new Y.Doc({ gc: false })
           apply(doc, inputs[0])
@@ -151,7 +218,7 @@ function coverage (ds) { // DeleteSet -> {client: [[start, end], ...]} (union of
       }
       const key = `${g}/${c.op}/${r.applicable ? 'applicable' : 'not applicable'}`
       stats[key] = (stats[key] || 0) + 1
-      const ok = r.applicable && (c.op === 'merge' ? r.pref1 && r.pref2 && r.pref3 : r.pref_sv)
+      const ok = r.applicable && (c.op === 'merge' ? r.pref1 && r.pref2 && r.pref3 : c.op === 'diff' ? r.pref_diff && r.pref_diff_ds && r.pref_diff_ds_in_ref : r.pref_sv)
       if (r.applicable && !ok) stats[`${g}/${c.op}/FAILED`] = (stats[`${g}/${c.op}/FAILED`] || 0) + 1
       cases.push(r)
     }

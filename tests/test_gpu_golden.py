@@ -85,11 +85,12 @@ def test_pref_bytes_on_gpu(engine):
     from yjs_amd import pack_docs
     pref = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "pref", "pref.json")))
     gold = {c["id"]: c for c in CASES}  # (zero-input merges are answered by the host layer, not a kernel)
-    for op in ("merge", "sv"):
+    for op in ("merge", "sv", "diff"):
         for fmt in (1, 2):
             sel = [c for c in pref["cases"] if c["op"] == op and c["fmt"] == fmt and c.get("applicable") and c["id"] in gold]
             docs = [gold[c["id"]]["inputs"] if op == "merge" else [gold[c["id"]]["inputs"][0]] for c in sel]
-            oa, oo, ol, st = engine.run_host(op, fmt, *pack_docs(docs))
+            extra = pack_docs([[gold[c["id"]]["sv"]] for c in sel])[:2] if op == "diff" else ()
+            oa, oo, ol, st = engine.run_host(op, fmt, *pack_docs(docs), *extra)
             for i, c in enumerate(sel):
                 got = oa[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes()
                 assert st[i] == 0 and hashlib.sha256(got).hexdigest() == c["checked_sha256"], c["id"]

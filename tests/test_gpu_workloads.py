@@ -494,3 +494,97 @@ def test_client_map_many_clients(engine, fmt, pw_min, monkeypatch):
         outs, st, _ = O.batch(op, fmt, a, o, dd, *extra, nthreads=8)
         bad = _compare(engine.run_host(op, fmt, a, o, dd, *extra), outs, st)
         assert not bad, (op, bad[:10])
+
+
+def _cmap_hash(c):
+    return ((c * 0x9E3779B1) & 0xFFFFFFFF) >> 20  # ym_cmap.h hash over 4,096 slots
+
+
+def _colliding_clients(rng, n):
+    """n distinct client ids sharing one client-map slot (long probe chains)."""
+    target = _cmap_hash(12345)
+    out = []
+    while len(out) < n:
+        c = [int(x) for x in rng.integers(0, 2**32, size=1 << 16, dtype=np.uint64)]
+        out += [x for x in c if _cmap_hash(x) == target and x not in out]
+    return out[:n]
+
+
+@pytest.mark.parametrize("pw_min", ["1", None], ids=["chunked", "streamed"])
+@pytest.mark.parametrize("fmt", [1, 2])
+def test_client_map_boundary_keys(engine, fmt, pw_min, monkeypatch):
+    """The client map's boundary keys: clients 0, 0xFFFFFFFE and 0xFFFFFFFF (whose client + 1 key would
+    wrap to the empty marker) in the struct section, the state vector and the delete set (also repeated),
+    clients whose hashes all land on one slot (probe chains of ~100), and delete sets of ~2,000 clients
+    (near BS_NDSC).  Diff, state vector and meta against the oracle."""
+    if pw_min:
+        monkeypatch.setenv("YMERGE_PW_MIN", pw_min)
+    from yjs_amd import pack_docs
+    rng = np.random.default_rng(57 + fmt)
+    edge = [0, 0xFFFFFFFE, 0xFFFFFFFF]
+    coll = _colliding_clients(rng, 160)
+    docs, svs = [], []
+    for d in range(24):
+        pool = coll if d % 2 else [int(c) for c in rng.choice(10**6, size=150, replace=False)]
+        clients = sorted(set(pool[:int(rng.integers(70, 150))] + edge[:1 + d % 3]), reverse=True)
+        if d % 6 == 5:
+            nd = int(rng.integers(1900, 2040))
+            dsc = [int(c) for c in rng.choice(2**31, size=nd, replace=False)] + edge
+        else:
+            dsc = pool[::-1][:int(rng.integers(65, 140))] + edge[d % 3:]
+        ds = [(c, [(0, 1)] if i % 2 else [(0, 1), (3, 2)]) for i, c in enumerate(dsc)]
+        if d % 4 == 1:  # repeated delete-set client: 0xFFFFFFFF itself, or a colliding one
+            ds.append((0xFFFFFFFF if d % 8 == 1 else ds[int(rng.integers(0, len(ds)))][0], [(9, 1)]))
+        u = _many_client_update(clients if fmt == 1 or d % 8 else clients[:1], ds)
+        if fmt == 2:
+            u = O.convert(u, 1)[1]
+        docs.append(u)
+        sv = [(c, int(rng.integers(0, 3))) for c in rng.choice(clients, size=min(len(clients), int(rng.integers(66, 200))))]
+        sv += [(c, int(rng.integers(0, 3))) for c in edge for _ in range(1 + d % 2)]  # later entry wins
+        sv += [(int(c), 5) for c in coll[150:]]  # absent clients on the same probe chain
+        rng.shuffle(sv)
+        svs.append(_vu(len(sv)) + b"".join(_vu(int(c)) + _vu(k) for c, k in sv))
+    a, o, dd = pack_docs([[u] for u in docs])
+    sva, svo, _ = pack_docs([[s] for s in svs])
+    for op in ("diff", "sv", "meta"):
+        extra = (sva, svo) if op == "diff" else ()
+        outs, st, _ = O.batch(op, fmt, a, o, dd, *extra, nthreads=8)
+        bad = _compare(engine.run_host(op, fmt, a, o, dd, *extra), outs, st)
+        assert not bad, (op, bad[:10])
+
+
+@pytest.mark.parametrize("how", ["hash", "bytes"])
+def test_multi_device_engine_real_engine(how):
+    """MultiDeviceEngine with the real Engine on two worker threads bound to device 0 (the 1-GPU box's
+    stand-in for two GPUs): per-(thread, device) library state (ym_api.hip g_states) driven from two
+    threads at once, over a mixed batch of C2 (fast path) and C5 (large pipeline) documents, merged and
+    then diffed against random state vectors; results in docIndex order against the oracle, repeated
+    calls reuse each thread's state (device memory flat after the first call)."""
+    import torch
+    from yjs_amd import pack_docs
+    from yjs_amd.distributed import MultiDeviceEngine
+    a2, o2, d2 = load_ymb("c2_v1")
+    a5, o5, d5 = load_ymb("c5_v1")
+    upd = lambda a, o, u: a[int(o[u]):int(o[u + 1])].tobytes()
+    docs = [[upd(a2, o2, u) for u in range(int(d2[i]), int(d2[i + 1]))] for i in range(60)]
+    for i in range(4):
+        docs.insert(7 + 13 * i, [upd(a5, o5, u) for u in range(int(d5[i]), int(d5[i + 1]))])
+    a, o, d = pack_docs(docs)
+    ref, st, _ = O.batch("merge", 1, a, o, d, nthreads=8)
+    assert (st == 0).all()
+    ma, mo, md = pack_docs([[m] for m in ref])
+    svs = []
+    for i, m in enumerate(ref):
+        svs.extend(random_state_vectors(O.sv_from_update(m, 1)[1], 1, seed=i))
+    sva, svo, _ = pack_docs([[s] for s in svs])
+    dref, dst, _ = O.batch("diff", 1, ma, mo, md, sva, svo, nthreads=8)
+    dexp = [x if s == 0 else int(s) for x, s in zip(dref, dst)]
+    free = []
+    with MultiDeviceEngine([0, 0], how) as eng:
+        for it in range(3):
+            assert eng.run_host("merge", 1, a, o, d) == list(ref)
+            got = eng.run_host("diff", 1, ma, mo, md, sva, svo)
+            assert [g if isinstance(g, bytes) else g & 0xff for g in got] == dexp
+            torch.cuda.synchronize()
+            free.append(torch.cuda.mem_get_info(0)[0])
+    assert abs(free[2] - free[1]) < (64 << 20), free  # no per-call leak of streams / scratch

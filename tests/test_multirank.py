@@ -3,6 +3,7 @@ process them independently (here with the CPU oracle standing in for the device)
 collectives are the max-time / sum-of-counters reductions.  The union of the shards' outputs must equal
 a single-process run."""
 import os
+import threading
 import socket
 
 import numpy as np
@@ -98,6 +99,16 @@ def test_multi_device_engine_reassembles_doc_order():
     a, o, d = load_ymb("c2_v1")
     a, o, d = gather_docs(a, o, d, np.arange(40))
     ref, st, _ = oracle_ref.batch("merge", 1, a, o, d)
+    made = []
+
+    def runner(device):
+        made.append((device, threading.get_ident()))
+        return _OracleRunner(device)
+
     for how in ("hash", "bytes"):
-        got = MultiDeviceEngine([0, 1, 2], how, runner=_OracleRunner).run_host("merge", 1, a, o, d)
-        assert got == ref
+        made.clear()
+        with MultiDeviceEngine([0, 1, 2], how, runner=runner) as eng:
+            for _ in range(3):  # one engine per device, made once on its own long-lived worker thread
+                assert eng.run_host("merge", 1, a, o, d) == ref
+        assert sorted(m[0] for m in made) == [0, 1, 2], made
+        assert len({m[1] for m in made}) == 3 and threading.get_ident() not in {m[1] for m in made}

@@ -58,7 +58,8 @@ constexpr uint64_t BS_SVT = BS_PREB + (uint64_t)BS_NSEC * BS_PRE;   // u32[BS_NS
 constexpr uint64_t BS_DSC = BS_SVT + 8ull * BS_NSV;                 // u32[BS_NDSC]
 constexpr uint32_t BS_MAP_SLOTS = 4096;                             // client map (ym_cmap.h)
 constexpr uint64_t BS_MAP = BS_DSC + 4ull * BS_NDSC;                // u32[2][BS_MAP_SLOTS] keys, values
-constexpr uint64_t BS_BYTES = BS_MAP + 8ull * BS_MAP_SLOTS;
+                                                                    // + u32[4] (client 0xFFFFFFFF's entry)
+constexpr uint64_t BS_BYTES = BS_MAP + 8ull * BS_MAP_SLOTS + 16;
 constexpr uint32_t BS_GRID = 8192;  // up to 32 one-wave blocks per CU; scratch sized by the launch's grid
 
 // device buffers of the large-document merge pipeline (ym_large.hip), grown on demand, cached

@@ -197,6 +197,74 @@ __device__ __forceinline__ void any_scalar(LCur &c) {
     default: c.bad = true; return;
   }
 }
+// One `any` value of any shape in the form lib0 0.2.42 writeAny emits for what readAny returns, so the
+// bytes round-trip: scalars as any_scalar, Uint8Array (116), BigInt64 (122), and arrays (117) / objects
+// (118) nested up to AC_DEPTH levels.  An object's re-encoding follows Object.keys order, which equals the
+// stored order only when no key is an array index and no key repeats, and readAny's `__proto__` key
+// mutates the prototype instead of adding a key -- so keys starting with a digit, `__proto__` and
+// repeated keys (compared byte-wise against the object's earlier keys, at most AC_KEYS open keys) are
+// rejected (the general path re-encodes those exactly).
+constexpr uint32_t AC_DEPTH = 8, AC_KEYS = 32;
+__device__ __forceinline__ bool key_eq(const uint8_t *b, uint32_t p, uint32_t q, uint32_t n) {
+  for (uint32_t i = 0; i < n; i++)
+    if (b[p + i] != b[q + i]) return false;
+  return true;
+}
+__device__ __forceinline__ void any_canon(LCur &c) {
+  uint32_t rem[AC_DEPTH];   // values left in each open array / object
+  uint32_t obj[AC_DEPTH];   // 1 + first key slot of an open object, 0 for an array
+  uint32_t kp[AC_KEYS], kl[AC_KEYS];
+  uint32_t depth = 0, nk = 0;
+  for (;;) {
+    if (c.bad) return;
+    // an object expects a key before each value
+    if (depth > 0 && obj[depth - 1]) {
+      const uint32_t n = rvu(c);
+      if (c.bad || !room(c, n) || n > c.cap) { c.bad = true; return; }
+      const uint32_t p = c.p;
+      const uint32_t b0 = n > 0 ? (uint32_t)c.lo & 0xffu : 0;
+      c.bad |= n > 0 && b0 >= '0' && b0 <= '9';
+      c.bad |= n == 9 && peek8(c, 0) == 0x5f6f746f72705f5full && (uint32_t)(peek8(c, 8) & 0xff) == '_';  // "__proto__"
+      for (uint32_t k = obj[depth - 1] - 1; k < nk && !c.bad; k++) c.bad |= kl[k] == n && key_eq(c.b, kp[k], p, n);
+      utf16_len(c, n);
+      if (c.bad || nk >= AC_KEYS) { c.bad = true; return; }
+      kp[nk] = p;
+      kl[nk] = n;
+      nk++;
+    }
+    const uint32_t tag = (uint32_t)c.lo & 0xffu;
+    if (tag == 117 || tag == 118) {  // array / object: count, then the values
+      rdb(c);
+      const uint32_t n = rvu(c);
+      if (c.bad || n > c.cap || depth >= AC_DEPTH) { c.bad = true; return; }
+      if (n > 0) {
+        rem[depth] = n;
+        obj[depth] = tag == 118 ? nk + 1 : 0;
+        depth++;
+        continue;
+      }
+    } else if (tag == 116) {  // Uint8Array: varUint8Array
+      rdb(c);
+      const uint32_t n = rvu(c);
+      if (c.bad || !room(c, n) || n > c.cap) { c.bad = true; return; }
+      skip(c, n);
+    } else if (tag == 122) {  // BigInt64: 8 bytes, read and written as they are
+      rdb(c);
+      if (!room(c, 8)) { c.bad = true; return; }
+      skip(c, 8);
+    } else {
+      any_scalar(c);
+    }
+    // a value completed: close the containers it finished
+    while (depth > 0 && !c.bad) {
+      if (--rem[depth - 1] > 0) break;
+      depth--;
+      if (obj[depth]) nk = obj[depth] - 1;
+    }
+    if (depth == 0) return;
+  }
+}
+
 // Item fields and content after the info byte; false for kinds the verbatim path does not verify
 // (ContentJSON, ContentDoc, bad refs) or any anomaly.  `len` = the Item's clock length.
 __device__ __forceinline__ bool item_body(LCur &c, uint32_t info, uint32_t &len) {

@@ -32,83 +32,29 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
-#include "ym_fast_common.h"
-#include "ym_kernels.h"
+#include "ym_pv2.h"
 #include "ym_cmap.h"
-#include "ym_lane.h"
 #include "ym_wave_ds.h"
 
 namespace ymk {
 namespace pv2 {
 using namespace fastc;
 
-constexpr uint64_t PV_MIN = 32768;  // smaller updates stay on k_big_v2
-constexpr uint32_t NONE = 0xffffffffu;
-// column kinds decoded by K1 / spliced by K3 (the V2 column index in brackets)
-enum { K_INFO = 0, K_PI, K_SL, K_LN, K_CL, K_LC, K_RC, NK };
-__host__ __device__ constexpr uint32_t col_of(uint32_t k) {  // V2 column order: kc cl lc rc in sl pi tr ln
-  return k == K_INFO ? 4 : k == K_PI ? 6 : k == K_SL ? 5 : k == K_LN ? 8 : k == K_CL ? 1 : k == K_LC ? 2 : 3;
-}
-constexpr uint32_t HB = 64;  // encoded head bytes per (document, column)
-constexpr uint32_t CKSTEP = 64;  // column entries per checkpoint (K3 starts its decode at the last one)
-
-// per-document state, in HBM
-struct Meta {
-  uint32_t ok;                // eligible (K0) and still good
-  uint32_t why;               // where a document was declined (debugging aid, ym__pv2_why)
-  uint32_t col0[9], col1[9];  // column spans (update-relative); the string column's lengths part
-  uint32_t sb0, sn;           // string body [sb0, sb0 + sn)
-  uint32_t n;                 // structs in the one section
-  uint32_t client;            // the section's client (first value of the client column)
-  uint32_t clock0;            // the section's first clock
-  uint32_t ds0;               // delete set start (rest stream, right after the section header)
-  uint64_t soff;              // scratch offset
-  uint32_t ck0[NK];           // K1 checkpoints of each column (uint4: entry position, value index, running
-                              // value) every CKSTEP entries, at the scratch's checkpoint area + ck0
-  uint32_t nck[NK];
-  // K1: values per kind; RLE<u8> kinds: values in counted entries, and whether a final (endless) entry exists
-  uint32_t nval[NK], fin[NK], finv[NK];
-  // K2: the cut and the column indices around it
-  uint32_t f;                 // cut struct (NONE: no struct ends past the state vector)
-  uint32_t off, fclock_lo;    // Item.write offset; clock of the cut struct
-  uint32_t pf[NK], pf1[NK];   // values of each kind consumed before struct f / f + 1
-  uint32_t tot[NK];           // values of each kind consumed by all structs
-  uint32_t body_f, body_fc, body_f1, body_end;  // string body offsets: before struct f, its content string, after it; consumed end
-  uint32_t info_f, pi_f, clen_f;
-  // K3
-  uint32_t hlen[NK], vstart[NK];
-  uint8_t head[NK][HB];
-};
-
-struct Job {
-  GeneralJob j;
-  Meta *meta;
-  uint8_t *scr;  // per-document value arrays
-  uint8_t *done;
-};
-// per-document value arrays at meta.soff: info u8[n], pi u8[n], sl u32[3n + 1], ln u32[n]; then the checkpoints
-__host__ __device__ inline uint64_t scr_bytes(uint32_t n) { return ((2ull * n + 3) & ~3ull) + 4ull * (4ull * n + 1) + 16; }
-__device__ __forceinline__ uint8_t *a_info(const Job &J, const Meta &M) { return J.scr + M.soff; }
-__device__ __forceinline__ uint8_t *a_pi(const Job &J, const Meta &M) { return J.scr + M.soff + M.n; }
-__device__ __forceinline__ uint32_t *a_sl(const Job &J, const Meta &M) {
-  return reinterpret_cast<uint32_t *>(J.scr + M.soff + ((2ull * M.n + 3) & ~3ull));
-}
-__device__ __forceinline__ uint32_t *a_ln(const Job &J, const Meta &M) { return a_sl(J, M) + 3ull * M.n + 1; }
-__device__ __forceinline__ uint4 *a_ck(const Job &J, const Meta &M, uint32_t kind) {
-  return reinterpret_cast<uint4 *>(J.scr + M.soff + ((scr_bytes(M.n) + 15) & ~15ull)) + M.ck0[kind];
-}
-
 // ---- K0: header ---------------------------------------------------------------------------------------
-__global__ void k_v2_prep(Job J, uint64_t pv_min, uint64_t *sizes) {
+// sizes[d]: the document's value-array scratch (single section; multi-section documents get theirs after
+// the rest walk counted their structs, ms_sizes); sizes1[d]: the multi-section tables.
+__global__ void k_v2_prep(Job J, uint64_t pv_min, uint64_t *sizes, uint64_t *sizes1) {
   const GeneralJob &j = J.j;
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d > j.n) return;
-  if (d == j.n) { sizes[d] = 0; return; }
+  if (d == j.n) { sizes[d] = 0; sizes1[d] = 0; return; }
   Meta &M = J.meta[d];
   M.ok = 0;
   M.why = 1;
+  M.ms = 0;
   J.done[d] = 0;
   sizes[d] = 0;
+  sizes1[d] = 0;
   const uint32_t u0 = j.doc_upd[d];
   if (j.doc_upd[d + 1] - u0 != 1) return;
   const uint64_t ub = j.upd_off[u0], len64 = j.upd_off[u0 + 1] - ub;
@@ -124,16 +70,10 @@ __global__ void k_v2_prep(Job J, uint64_t pv_min, uint64_t *sizes) {
     M.col1[k] = c.p + n;
     c = ln::make(D, c.p + n, len);
   }
-  // typeRef / keyClock unused by the kinds taken here
-  if (M.col1[0] != M.col0[0] || M.col1[7] != M.col0[7]) return;
   const uint32_t nclients = ln::rvu(c);
-  if (c.bad || nclients != 1) return;
-  const uint32_t nstructs = ln::rvu(c);
-  const uint32_t clock = ln::rvu(c);
-  if (c.bad || nstructs == 0 || nstructs > (1u << 26)) return;
-  M.ds0 = c.p;
-  M.n = nstructs;
-  M.clock0 = clock;
+  if (c.bad || nclients == 0 || nclients > (1u << 16)) return;
+  M.nsec = nclients;
+  M.r0 = c.p;
   // string column = varString(body) | UintOptRle(lengths)
   ln::LCur s = ln::make(D, M.col0[5], M.col1[5]);
   const uint32_t sn = ln::rvu(s);
@@ -141,34 +81,34 @@ __global__ void k_v2_prep(Job J, uint64_t pv_min, uint64_t *sizes) {
   M.sb0 = s.p;
   M.sn = sn;
   M.col0[5] = s.p + sn;  // lengths part
+  if (nclients > 1) {  // several client sections: ym_pv2ms.hip (tables sized by the rest stream's bytes)
+    M.ms = 1;
+    M.n = 0;
+    M.ok = 1;
+    M.why = 0;
+    sizes1[d] = ((((uint64_t)nclients * sizeof(Sec) + 15) & ~15ull) + 4ull * (len - M.r0 + 1) + 511) & ~255ull;  // (Sec holds a u64 atomic)
+    return;
+  }
+  // typeRef / keyClock unused by the kinds the single-section path takes
+  if (M.col1[0] != M.col0[0] || M.col1[7] != M.col0[7]) return;
+  const uint32_t nstructs = ln::rvu(c);
+  const uint32_t clock = ln::rvu(c);
+  if (c.bad || nstructs == 0 || nstructs > (1u << 26)) return;
+  M.ds0 = c.p;
+  M.n = nstructs;
+  M.clock0 = clock;
   M.ok = 1;
   M.why = 0;
-  uint32_t ck = 0;  // an entry is at least one byte: a column of b bytes needs b / CKSTEP + 1 checkpoints
-  for (uint32_t k = 0; k < NK; k++) {
-    M.ck0[k] = ck;
-    ck += (M.col1[col_of(k)] - M.col0[col_of(k)]) / CKSTEP + 2;
-  }
-  sizes[d] = (((scr_bytes(nstructs) + 15) & ~15ull) + 16ull * ck + 255) & ~255ull;  // checkpoints start 16-aligned (a_ck)
+  uint32_t colb[NK];
+  for (uint32_t k = 0; k < NK; k++) colb[k] = M.col1[col_of(k)] - M.col0[col_of(k)];
+  sizes[d] = (scr_layout(M, nstructs, 1, false, colb) + 255) & ~255ull;
 }
 
-__global__ void k_v2_meta_off(Job J, const uint64_t *offs) {
+__global__ void k_v2_meta_off(Job J, const uint64_t *offs, uint32_t which) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d < J.j.n) J.meta[d].soff = offs[d];
-}
-
-// ---- K1: column decoders, one lane per (document, column) ----------------------------------------------
-// lib0 readVarInt as k_big_v2's s_vi: canonical, <= 5 bytes, |v| < 2^31 + (sign); returns the magnitude
-__device__ __forceinline__ uint32_t rvi(ln::LCur &c, bool &neg) {
-  const uint32_t lo = (uint32_t)c.lo, hi = (uint32_t)(c.lo >> 32);
-  const uint32_t nb = ln::vu_nb(lo, hi);
-  neg = (lo & 0x40) != 0;
-  uint32_t m = (lo & 0x3fu) | ((lo >> 2) & 0x1fc0u) | ((lo >> 3) & 0xfe000u) | ((lo >> 4) & 0x7f00000u) | ((hi & 0x7fu) << 27);
-  const uint32_t bits = 6 + 7 * (nb - 1);
-  if (nb < 5) m &= (1u << bits) - 1u;
-  const uint32_t last = nb <= 4 ? (lo >> (8 * nb - 8)) & 0xffu : hi & 0xffu;
-  c.bad |= (nb > 5) | (c.p + nb > c.e) | ((nb > 1) & (last == 0)) | ((nb == 5) & ((hi & 0x7fu) > 0x1fu));
-  ln::skip(c, nb < 6 ? nb : 0);
-  return m;
+  if (d >= J.j.n) return;
+  if (which) J.meta[d].soff1 = offs[d];
+  else J.meta[d].soff = offs[d];
 }
 
 // ---- K1, wave-parallel: one wave per (document, column) ---------------------------------------------
@@ -216,41 +156,6 @@ __device__ __forceinline__ uint32_t tstep(uint32_t st, uint32_t b, bool rle, uin
   if (st == 2) return stop ? 0 : 2;
   return stop ? 0 : 3;
 }
-struct Ent {
-  uint32_t val, cnt;
-  int32_t df;
-  bool fin, bad;
-};
-// the entry at pos: value (RLE: the byte; Opt: the varint's magnitude), count, IntDiff diff; fin = an
-// RLE<u8> value byte that ends the column (no count: the final run never ends)
-__device__ __forceinline__ Ent dec_entry(const uint8_t *D, uint32_t pos, uint32_t c1, uint32_t kind) {
-  Ent e{0, 0, 0, false, false};
-  if (kind == K_INFO || kind == K_PI) {
-    e.val = D[pos];
-    e.bad = kind == K_PI && e.val > 1;
-    if (pos + 1 >= c1) { e.fin = true; return e; }
-    ln::LCur c = ln::make(D, pos + 1, c1);
-    e.cnt = ln::rvu(c) + 1;
-    e.bad |= c.bad || e.cnt == 0;
-    return e;
-  }
-  ln::LCur c = ln::make(D, pos, c1);
-  bool neg;
-  const uint32_t m = rvi(c, neg);
-  if (kind == K_LC || kind == K_RC) {
-    const int32_t t = neg ? -(int32_t)m : (int32_t)m;
-    e.df = t >> 1;
-    e.cnt = (t & 1) ? ln::rvu(c) + 2 : 1;
-    e.bad = (neg && m == 0) || e.df < -(1 << 30) || e.df >= (1 << 30) || ((t & 1) && e.cnt < 2);
-  } else {
-    e.cnt = neg ? ln::rvu(c) + 2 : 1;
-    e.bad = neg && e.cnt < 2;
-  }
-  e.val = m;
-  e.bad |= c.bad;
-  return e;
-}
-
 __global__ void __launch_bounds__(64) k_v2_decw(Job J) {
   const GeneralJob &j = J.j;
   const uint32_t d = blockIdx.x, kind = blockIdx.y, lane = threadIdx.x;
@@ -259,11 +164,13 @@ __global__ void __launch_bounds__(64) k_v2_decw(Job J) {
   const uint8_t *D = j.A + j.upd_off[j.doc_upd[d]];
   const uint32_t c0 = M.col0[col_of(kind)], c1 = M.col1[col_of(kind)];
   const uint32_t n = M.n;
-  const bool rle = kind == K_INFO || kind == K_PI, dif = kind == K_LC || kind == K_RC;
+  const bool rle = k_rle(kind), dif = k_dif(kind);
   const uint32_t fb = dif ? 0 : 6;
-  const uint64_t cap = kind == K_SL ? 3ull * n : kind == K_CL ? 2ull * n + 1 : n;
-  uint8_t *o8 = kind == K_INFO ? a_info(J, M) : kind == K_PI ? a_pi(J, M) : nullptr;
-  uint32_t *o32 = kind == K_SL ? a_sl(J, M) : kind == K_LN ? a_ln(J, M) : nullptr;
+  const uint64_t cap = kind_cap(kind, n, M.nsec);
+  // expanded per-value arrays: info / parentInfo / typeRef (u8), string lengths / len (u32), and for
+  // multi-section documents the client column (each section's client)
+  uint8_t *o8 = kind == K_INFO ? a_info(J, M) : kind == K_PI ? a_pi(J, M) : kind == K_TR ? a_tr(J, M) : nullptr;
+  uint32_t *o32 = kind == K_SL ? a_sl(J, M) : kind == K_LN ? a_ln(J, M) : kind == K_CL && M.ms ? a_cl(J, M) : nullptr;
   uint4 *ck = a_ck(J, M, kind);
   const uint32_t ckcap = (c1 - c0) / CKSTEP + 2;
   uint32_t st = 0, ne = 0, fin = 0, finv = 0;  // carried across steps (wave-uniform)
@@ -304,7 +211,7 @@ __global__ void __launch_bounds__(64) k_v2_decw(Job J) {
     for (uint32_t m = starts; m; m &= m - 1) {
       const Ent e = dec_entry(D, q + __builtin_ctz(m), c1, kind);
       const uint32_t key = dif ? (uint32_t)e.df : e.val;
-      lbad |= e.bad || (lne > 0 && key == llast) || e.cnt > cap;
+      lbad |= e.bad || (lne > 0 && key == llast) || e.cnt > cap || (kind == K_TR && e.val > 6);
       if (e.fin) { lfin = true; lfinv = e.val; }
       if (lne == 0) lfirst = key;
       llast = key;
@@ -335,6 +242,9 @@ __global__ void __launch_bounds__(64) k_v2_decw(Job J) {
         if (dif) {
           const int64_t vfirst = vr + e.df, vlast = vr + (int64_t)e.df * e.cnt;
           lbad |= vfirst < 0 || vfirst > 0xffffffffll || vlast < 0 || vlast > 0xffffffffll;
+          // keyClock: readKey reads a new key string only when keyClock >= the keys read so far (value i
+          // >= i for every i; linear inside an entry, so its two ends decide)
+          if (kind == K_KC) lbad |= vfirst < (int64_t)vbase || vlast < (int64_t)(vbase + e.cnt - 1);
           vr = vlast;
         }
         if (vbase + e.cnt <= cap) {
@@ -376,41 +286,13 @@ __global__ void __launch_bounds__(64) k_v2_decw(Job J) {
 }
 
 // ---- K2: struct pass ------------------------------------------------------------------------------------
-constexpr uint32_t KT = 256;       // threads
-constexpr uint32_t PER = 4;        // structs per thread per tile
-constexpr uint32_t TILE = KT * PER;
-// exclusive block scan of NS u32 sums (+ totals), KT threads
-template <uint32_t NS>
-__device__ __forceinline__ void block_scan(uint32_t (&x)[NS], uint32_t (&tot)[NS], uint32_t *sh) {
-  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
-  uint32_t incl[NS];
-#pragma unroll
-  for (uint32_t q = 0; q < NS; q++) incl[q] = wave_incl_add(x[q]);
-  __syncthreads();
-  if (lane == 63)
-#pragma unroll
-    for (uint32_t q = 0; q < NS; q++) sh[w * NS + q] = incl[q];
-  __syncthreads();
-#pragma unroll
-  for (uint32_t q = 0; q < NS; q++) {
-    uint32_t pre = 0, all = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < KT / 64; k++) {
-      const uint32_t s = sh[k * NS + q];
-      pre += k < w ? s : 0;
-      all += s;
-    }
-    x[q] = pre + incl[q] - x[q];
-    tot[q] = all;
-  }
-}
-
+constexpr uint32_t NK1 = K_TR;     // single section: the seven kinds a GC / Deleted / String struct uses
 template <int OP>
 __global__ void __launch_bounds__(KT) k_v2_struct(Job J) {
   const GeneralJob &j = J.j;
   const uint32_t d = blockIdx.x, t = threadIdx.x;
   Meta &M = J.meta[d];
-  if (!M.ok) return;
+  if (!M.ok || M.ms) return;
   __shared__ uint32_t sh[4 * 16];
   __shared__ uint32_t s_bad, s_cut;
   __shared__ uint64_t s_clock;
@@ -452,19 +334,19 @@ __global__ void __launch_bounds__(KT) k_v2_struct(Job J) {
   const uint8_t *info_a = a_info(J, M), *pi_a = a_pi(J, M);
   const uint32_t *sl_a = a_sl(J, M), *ln_a = a_ln(J, M);
   // running column indices (carried across tiles): [K_INFO .. K_RC] + string body bytes
-  uint32_t base[NK + 1];
+  uint32_t base[NK1 + 1];
 #pragma unroll
-  for (uint32_t q = 0; q <= NK; q++) base[q] = 0;
+  for (uint32_t q = 0; q <= NK1; q++) base[q] = 0;
   base[K_CL] = 1;  // the section header's client
   uint64_t clock = M.clock0;
   uint32_t cut = NONE;
   if (t == 0) s_bad = 0;
   for (uint32_t t0 = 0; t0 < n; t0 += TILE) {
     // per struct: values consumed of each kind (no Skip / Any / Type ...: only GC, Deleted, String)
-    uint32_t cons[PER][NK], info[PER], pi[PER];
-    uint32_t x[NK + 2];  // per-thread sums: kinds, body bytes, clock
+    uint32_t cons[PER][NK1], info[PER], pi[PER];
+    uint32_t x[NK1 + 2];  // per-thread sums: kinds, body bytes, clock
 #pragma unroll
-    for (uint32_t q = 0; q < NK + 2; q++) x[q] = 0;
+    for (uint32_t q = 0; q < NK1 + 2; q++) x[q] = 0;
     bool bad = false;
 #pragma unroll
     for (uint32_t e = 0; e < PER; e++) {
@@ -476,6 +358,10 @@ __global__ void __launch_bounds__(KT) k_v2_struct(Job J) {
       const bool gc = valid && ref == 0 && v != 10;
       const bool item = valid && !gc;
       bad |= valid && (v == 10 || (item && ref != 1 && ref != 4));
+      // written back as GC.write / Item.write would (13.5.16 lazy reader: parentSub only without
+      // origins): a GC info byte with flags, or a parentSub bit next to an origin, would change
+      bad |= gc && v != 0;
+      bad |= item && (v & 0xC0) && (v & 0x20);
       const bool o = item && (v & 0x80), r = item && (v & 0x40), no = item && !(v & 0xC0);
       cons[e][K_INFO] = valid;
       cons[e][K_PI] = no;
@@ -486,7 +372,7 @@ __global__ void __launch_bounds__(KT) k_v2_struct(Job J) {
       cons[e][K_LC] = o;
       cons[e][K_SL] = (item && ref == 4) + (no && (v & 0x20));
 #pragma unroll
-      for (uint32_t q = 0; q < NK; q++) x[q] += cons[e][q];
+      for (uint32_t q = 0; q < NK1; q++) x[q] += cons[e][q];
     }
     // parentInfo index first (the others depend on its values)
     {
@@ -512,16 +398,16 @@ __global__ void __launch_bounds__(KT) k_v2_struct(Job J) {
       base[K_PI] += tp[0];
     }
     // indices of every kind
-    uint32_t tot[NK];
-    uint32_t xs[NK];
+    uint32_t tot[NK1];
+    uint32_t xs[NK1];
 #pragma unroll
-    for (uint32_t q = 0; q < NK; q++) xs[q] = x[q];
-    block_scan<NK>(xs, tot, sh);
+    for (uint32_t q = 0; q < NK1; q++) xs[q] = x[q];
+    block_scan<NK1>(xs, tot, sh);
     // string lengths -> body bytes, clock lengths
     uint32_t sli = base[K_SL] + xs[K_SL], lni = base[K_LN] + xs[K_LN];
     uint32_t clen[PER], bodyb[PER];
-    x[NK] = 0;
-    x[NK + 1] = 0;
+    x[NK1] = 0;
+    x[NK1 + 1] = 0;
 #pragma unroll
     for (uint32_t e = 0; e < PER; e++) {
       uint32_t bl = 0;
@@ -536,12 +422,12 @@ __global__ void __launch_bounds__(KT) k_v2_struct(Job J) {
       }
       clen[e] = cl;
       bodyb[e] = bl;
-      x[NK] += bl;
-      x[NK + 1] += cl;
+      x[NK1] += bl;
+      x[NK1 + 1] += cl;
       sli += cons[e][K_SL];
       lni += cons[e][K_LN];
     }
-    uint32_t xb[2] = {x[NK], x[NK + 1]}, tb[2];
+    uint32_t xb[2] = {x[NK1], x[NK1 + 1]}, tb[2];
     block_scan<2>(xb, tb, sh);
     // the cut: first struct (non-Skip) whose end passes sv[client]
     uint64_t ck = clock + xb[1];
@@ -560,16 +446,16 @@ __global__ void __launch_bounds__(KT) k_v2_struct(Job J) {
     const uint32_t tc = s_cut;
     if (tc != NONE && cut == NONE && mycut != NONE && tc == t0 + t * PER + mycut) {  // the thread holding the cut records it
       const uint32_t e = mycut;
-      uint32_t pre[NK], pre1[NK];
+      uint32_t pre[NK1], pre1[NK1];
 #pragma unroll
-      for (uint32_t q = 0; q < NK; q++) {
+      for (uint32_t q = 0; q < NK1; q++) {
         pre[q] = base[q] + xs[q];
         for (uint32_t e2 = 0; e2 < e; e2++) pre[q] += cons[e2][q];
         pre1[q] = pre[q] + cons[e][q];
         M.pf[q] = pre[q];
         M.pf1[q] = pre1[q];
       }
-      uint32_t bo = base[NK] + xb[0];
+      uint32_t bo = base[NK1] + xb[0];
       for (uint32_t e2 = 0; e2 < e; e2++) bo += bodyb[e2];
       M.body_f = bo;
       M.body_f1 = bo + bodyb[e];
@@ -585,8 +471,8 @@ __global__ void __launch_bounds__(KT) k_v2_struct(Job J) {
     }
     if (tc != NONE) cut = tc;
 #pragma unroll
-    for (uint32_t q = 0; q < NK; q++) base[q] += tot[q];
-    base[NK] += tb[0];
+    for (uint32_t q = 0; q < NK1; q++) base[q] += tot[q];
+    base[NK1] += tb[0];
     clock += tb[1];
     __syncthreads();
   }
@@ -594,13 +480,13 @@ __global__ void __launch_bounds__(KT) k_v2_struct(Job J) {
   // every column consumed exactly as the re-encoding writes it; strings inside the body
   bool bad = false;
 #pragma unroll
-  for (uint32_t q = 0; q < NK; q++) {
+  for (uint32_t q = 0; q < NK1; q++) {
     if (q == K_INFO || q == K_PI) bad |= M.fin[q] ? base[q] < M.nval[q] + 1 : base[q] != M.nval[q];
     else bad |= base[q] != M.nval[q];
     M.tot[q] = base[q];
   }
-  bad |= base[NK] > M.sn;
-  M.body_end = base[NK];
+  bad |= base[NK1] > M.sn;
+  M.body_end = base[NK1];
   if (bad) { M.ok = 0; M.why = 24; return; }
   if (cut == NONE) M.f = NONE;
   if (OP == OP_SV) {
@@ -637,65 +523,12 @@ __global__ void __launch_bounds__(KT) k_v2_struct(Job J) {
 }
 
 // ---- K3: splice heads ---------------------------------------------------------------------------------
-// lib0 encoders into a small byte buffer
-struct Buf {
-  uint8_t *b;
-  uint32_t n;
-  bool over;
-  __device__ void byte(uint32_t v) { if (n < HB) b[n] = (uint8_t)v; else over = true; n++; }
-  __device__ void vu(uint32_t v) { while (v > 127) { byte(0x80 | (v & 127)); v >>= 7; } byte(v); }
-  __device__ void vi(bool neg, uint32_t m) {
-    byte((m > 63 ? 0x80 : 0) | (neg ? 0x40 : 0) | (m & 63));
-    m >>= 6;
-    while (m > 0) { byte((m > 127 ? 0x80 : 0) | (m & 127)); m >>= 7; }
-  }
-};
-struct Enc {  // one encoder of kind `kind`: (s, count, diff, started)
-  uint32_t s = 0, cnt = 0, started = 0;
-  int32_t df = 0;
-  bool bad = false;
-  __device__ void put(Buf &B, uint32_t kind, uint32_t v) {
-    if (kind == K_INFO || kind == K_PI) {  // RleEncoder<u8>
-      if (started && s == v) { cnt++; return; }
-      if (cnt > 0) B.vu(cnt - 1);
-      B.byte(v);
-      s = v; cnt = 1; started = 1;
-    } else if (kind == K_LC || kind == K_RC) {  // IntDiffOptRleEncoder
-      const int64_t dd = (int64_t)v - (int64_t)s;
-      if (dd < -(1ll << 30) || dd >= (1ll << 30)) { bad = true; return; }
-      if (df == (int32_t)dd) { s = v; cnt++; return; }
-      flush(B, kind);
-      s = v; cnt = 1; df = (int32_t)dd;
-    } else {  // UintOptRleEncoder
-      if (s == v && cnt > 0) { cnt++; return; }
-      flush(B, kind);
-      s = v; cnt = 1;
-    }
-  }
-  // closes the pending run (before verbatim entries, or at the column's end: an RLE<u8> final count is
-  // not written then)
-  __device__ void flush(Buf &B, uint32_t kind, bool at_end = false) {
-    if (cnt == 0) return;
-    if (kind == K_INFO || kind == K_PI) {
-      if (!at_end) B.vu(cnt - 1);
-    } else if (kind == K_LC || kind == K_RC) {
-      const int32_t x = (int32_t)((uint32_t)df << 1) | (cnt == 1 ? 0 : 1);
-      B.vi(x < 0, x < 0 ? (uint32_t)(-(int64_t)x) : (uint32_t)x);
-      if (cnt > 1) B.vu(cnt - 2);
-    } else {
-      B.vi(cnt != 1, s);
-      if (cnt > 1) B.vu(cnt - 2);
-    }
-    cnt = 0;
-  }
-};
-
 __global__ void __launch_bounds__(64) k_v2_splice(Job J) {
   const GeneralJob &j = J.j;
   const uint32_t d = blockIdx.x * 64 + threadIdx.x, kind = blockIdx.y;
   if (d >= j.n) return;
   Meta &M = J.meta[d];
-  if (!M.ok || M.f == NONE) return;
+  if (!M.ok || M.ms || M.f == NONE) return;
   const uint8_t *D = j.A + j.upd_off[j.doc_upd[d]];
   const uint32_t c0 = M.col0[col_of(kind)], c1 = M.col1[col_of(kind)];
   const uint32_t q0 = M.pf[kind], q1 = M.pf1[kind], tot = M.tot[kind];
@@ -797,7 +630,7 @@ __global__ void __launch_bounds__(64) k_v2_splice(Job J) {
   }
   if (gbad) { M.ok = 0; M.why = 37; return; }
   uint8_t *hb = M.head[kind];
-  Buf B{hb, 0, false};
+  Buf B{hb, 0, HB, false};
   Enc E;
   for (uint32_t i = 0; i < nh; i++) E.put(B, kind, hv[i]);
   bool bad = E.bad;
@@ -858,19 +691,12 @@ __global__ void __launch_bounds__(64) k_v2_splice(Job J) {
 }
 
 // ---- K4: output -----------------------------------------------------------------------------------------
-using wds::u4u;
-__device__ __forceinline__ void wcopy(uint8_t *dst, const uint8_t *src, uint32_t n) {
-  const uint32_t nv = n >> 4;
-  for (uint32_t v = threadIdx.x; v < nv; v += 64) reinterpret_cast<u4u *>(dst)[v] = reinterpret_cast<const u4u *>(src)[v];
-  for (uint32_t i = (nv << 4) + threadIdx.x; i < n; i += 64) dst[i] = src[i];
-}
-
 __global__ void __launch_bounds__(64) k_v2_out(Job J) {
   const GeneralJob &j = J.j;
   const uint32_t lane = threadIdx.x;
   for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
     Meta &M = J.meta[d];
-    if (!M.ok) continue;
+    if (!M.ok || M.ms) continue;
     const uint32_t u0 = j.doc_upd[d];
     const uint64_t ub = j.upd_off[u0];
     const uint32_t len = (uint32_t)(j.upd_off[u0 + 1] - ub);
@@ -916,10 +742,10 @@ __global__ void __launch_bounds__(64) k_v2_out(Job J) {
     if (part) {  // spans the splice and the cut produced must lie inside their columns (else: decline)
       bool span_bad = M.body_f > M.body_fc || M.body_fc > M.body_f1 || M.body_f1 > M.body_end || M.body_end > M.sn;
       span_bad |= M.off != 0 && (M.info_f & 31) == 4 && M.body_fc + M.off > M.body_f1;
-      for (uint32_t kk = 0; kk < NK; kk++)
+      for (uint32_t kk = 0; kk < NK1; kk++)
         span_bad |= M.hlen[kk] > HB || M.vstart[kk] < M.col0[col_of(kk)] || M.vstart[kk] > M.col1[col_of(kk)];
       if (span_bad) { if (lane == 0) M.why = 41; __syncthreads(); continue; }
-      for (uint32_t kk = 0; kk < NK; kk++) {
+      for (uint32_t kk = 0; kk < NK1; kk++) {
         const uint32_t c = col_of(kk);
         const uint32_t b = M.hlen[kk] + (M.col1[c] - M.vstart[kk]);
         if (kk == K_SL) sln = b;
@@ -957,7 +783,7 @@ __global__ void __launch_bounds__(64) k_v2_out(Job J) {
       if (c == 5) p = put(p, sbn);  // string column: varString(body) | lengths
       if (!part || cl[c] == 0) continue;
       int kk = -1;
-      for (uint32_t q = 0; q < NK; q++) if (col_of(q) == c) kk = (int)q;
+      for (uint32_t q = 0; q < NK1; q++) if (col_of(q) == c) kk = (int)q;
       if (c == 5) {
         const uint32_t hs0 = M.off == 0 ? M.body_f : (M.info_f & 31) == 4 ? M.body_fc + M.off : M.body_f1;
         wcopy(o + p, D + M.sb0 + hs0, M.body_f1 - hs0);
@@ -998,8 +824,9 @@ int pv_ensure(PwBufs &B, int k, size_t n) {
 }
 }  // namespace
 
-// Column-parallel V2 diff / sv / meta over the large single-section documents of a call; marks the documents it
-// completes in *done_out (k_big_v2 skips them).  1 = launched, 0 = not applicable, < 0 = error.
+// Column-parallel V2 diff / sv / meta over the large documents of a call (single section: this file;
+// several sections: ym_pv2ms.hip); marks the documents it completes in *done_out (k_big_v2 skips them).
+// 1 = launched, 0 = not applicable, < 0 = error.
 static pv2::Meta *pv2_last_meta = nullptr;
 int pv2_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const uint8_t **done_out) {
   using namespace pv2;
@@ -1009,32 +836,51 @@ int pv2_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const u
   if (const char *e = getenv("YMERGE_PW_MIN")) pv_min = strtoull(e, nullptr, 10);
   if (!B.pinned && hipHostMalloc((void **)&B.pinned, 64, hipHostMallocDefault) != hipSuccess) return -2;
   const uint32_t n1 = j.n + 1;
-  if (pv_ensure(B, 0, sizeof(Meta) * (uint64_t)j.n + 16ull * n1 + j.n + 64)) return -2;
+  if (pv_ensure(B, 0, sizeof(Meta) * (uint64_t)j.n + 32ull * n1 + j.n + 64)) return -2;
   Job J;
   J.j = j;
   J.meta = (Meta *)B.p[0];
-  uint64_t *sizes = (uint64_t *)(J.meta + j.n), *offs = sizes + n1;
-  J.done = (uint8_t *)(offs + n1);
+  uint64_t *sizes = (uint64_t *)(J.meta + j.n), *offs = sizes + n1, *sizes1 = offs + n1, *offs1 = sizes1 + n1;
+  J.done = (uint8_t *)(offs1 + n1);
   J.scr = nullptr;
+  J.scr1 = nullptr;
   pv2_last_meta = J.meta;
-  k_v2_prep<<<(n1 + 255) / 256, 256, 0, st>>>(J, pv_min, sizes);
+  k_v2_prep<<<(n1 + 255) / 256, 256, 0, st>>>(J, pv_min, sizes, sizes1);
   size_t tmp = 0;
   hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, sizes, offs, n1, st);
   if (pv_ensure(B, 1, tmp + 16)) return -2;
   if (hipcub::DeviceScan::ExclusiveSum(B.p[1], tmp, sizes, offs, n1, st) != hipSuccess) return -3;
+  if (hipcub::DeviceScan::ExclusiveSum(B.p[1], tmp, sizes1, offs1, n1, st) != hipSuccess) return -3;
   if (hipMemcpyAsync(B.pinned, offs + j.n, 8, hipMemcpyDeviceToHost, st) != hipSuccess) return -3;
+  if (hipMemcpyAsync(B.pinned + 2, offs1 + j.n, 8, hipMemcpyDeviceToHost, st) != hipSuccess) return -3;
   if (hipStreamSynchronize(st) != hipSuccess) return -3;
-  const uint64_t total = *(uint64_t *)B.pinned;
+  uint64_t total = *(uint64_t *)B.pinned;
+  const uint64_t total1 = *(uint64_t *)(B.pinned + 2);
   *done_out = J.done;
+  bool ms = total1 > 0;
+  if (ms && pv_ensure(B, 3, total1 + 256)) {
+    hipMemsetAsync(J.done, 0, j.n, st);
+    return 1;
+  }
+  if (ms) {  // multi-section documents: the rest walk counts their structs, then their value arrays are sized
+    J.scr1 = (uint8_t *)B.p[3];
+    k_v2_meta_off<<<(j.n + 255) / 256, 256, 0, st>>>(J, offs1, 1);
+    ms_rest(J, st);
+    ms_sizes(J, sizes, st);
+    if (hipcub::DeviceScan::ExclusiveSum(B.p[1], tmp, sizes, offs, n1, st) != hipSuccess) return -3;
+    if (hipMemcpyAsync(B.pinned, offs + j.n, 8, hipMemcpyDeviceToHost, st) != hipSuccess) return -3;
+    if (hipStreamSynchronize(st) != hipSuccess) return -3;
+    total = *(uint64_t *)B.pinned;
+  }
   if (total == 0) return 1;
   if (pv_ensure(B, 2, total + 256)) {
     hipMemsetAsync(J.done, 0, j.n, st);
     return 1;
   }
   J.scr = (uint8_t *)B.p[2];
-  k_v2_meta_off<<<(j.n + 255) / 256, 256, 0, st>>>(J, offs);
-  const dim3 g1((j.n + 63) / 64, NK);
-  k_v2_decw<<<dim3(j.n, NK), 64, 0, st>>>(J);
+  k_v2_meta_off<<<(j.n + 255) / 256, 256, 0, st>>>(J, offs, 0);
+  const dim3 g1((j.n + 63) / 64, NK1);
+  k_v2_decw<<<dim3(j.n, ms ? NK : NK1), 64, 0, st>>>(J);
   if (op == OP_DIFF) {
     k_v2_struct<OP_DIFF><<<j.n, KT, 0, st>>>(J);
     k_v2_splice<<<g1, 64, 0, st>>>(J);
@@ -1045,6 +891,7 @@ int pv2_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const u
   } else {
     k_v2_struct<OP_META><<<j.n, KT, 0, st>>>(J);
   }
+  if (ms) ms_run(op, J, st);
   return 1;
 }
 

@@ -1,0 +1,980 @@
+// ym_pv2ms.hip -- column-parallel diffUpdateV2 / encodeStateVectorFromUpdateV2 / parseUpdateMetaV2 over
+// large V2 updates with several client sections (BASELINE configs[4] C5: ~1,000 sections per document,
+// XmlElement / XmlText types, formatted text, attributes).
+//
+// The single-section path (ym_pv2.hip) reads the one section's header from the rest stream and cuts one
+// run of every column.  Here the rest stream interleaves every section's header (vu(#structs), vu(first
+// clock)) with the payloads of its structs (Skip lengths, ContentAny / ContentFormat / ContentEmbed values,
+// ContentBinary buffers; UpdateDecoder.js:274-293, 13.5.16 LazyStructReader), and a diff keeps a suffix
+// of every section (13.5.16 diffUpdateV2 us@40707; reference writeClientsStructs encoding.js:94-116 cuts
+// each client at the state vector), so every column is rebuilt from ~1,000 kept value ranges.
+//
+//  MR  k_ms_rest    one wave per document: the rest walk -- section headers, and the payload start of every
+//                   struct that has one, found by walking the info / len columns run by run (a run of
+//                   String / Type structs costs one step) and skipping payloads with the canonical `any`
+//                   checker (ym_lane.h any_canon).  Counts the structs, so the value arrays can be sized.
+//  K1  k_v2_decw    (ym_pv2.hip) every column decoded wave-parallel, as for one section.
+//  K2  k_ms_struct  one 256-thread block per document, two passes of block prefix sums over the structs:
+//                   pass 1 gives each section's column indices, clock and body offsets, its client (the
+//                   client column's value at the section start) and, for a state vector / meta, the answer;
+//                   pass 2 finds each section's cut against sv[client] (an LDS hash map of the state vector).
+//  K3  k_ms_col     one wave per (document, column): lanes locate each kept section's value range in the
+//                   input column (K1 checkpoints) and describe it as runs -- the cut struct's re-encoded
+//                   values (Item.write with offset), the range's first two entries, its clipped last entry --
+//                   and a verbatim byte span for the entries between; then one wave-uniform lib0 encoder
+//                   folds the runs of all sections in order, so runs that continue across a section boundary
+//                   merge exactly as the encoder would merge them, and the spans are copied.
+//  K4  k_ms_out     one wave per document: the delete set validated, string body pieces and rest pieces
+//                   (vu(written) vu(first clock) payloads) per kept section, the keyClock column (writeKey
+//                   numbers keys 0, 1, 2, ...: its IntDiff encoding has a closed form), the assembly.
+//
+// Exactly the documents k_big_v2 (ym_big2.hip) would take are taken, with identical bytes, except that
+// ContentAny / Embed / Format values may be nested objects and arrays here; anything else (JSON / Doc
+// content, non-ASCII string bodies, repeated or ascending clients, a Skip right before a cut, non-canonical
+// columns) is declined to k_big_v2 and from there to the general path.
+#include <hip/hip_runtime.h>
+
+#include "ym_pv2.h"
+#include "ym_cmap.h"
+#include "ym_wave_ds.h"
+
+namespace ymk {
+namespace pv2 {
+
+// ---- MR: the rest walk ---------------------------------------------------------------------------------
+// UintOptRleDecoder over the len column: the next value / skip t values, run by run
+__device__ __forceinline__ uint32_t uopt_next(ln::LCur &c, uint32_t &v, uint32_t &rem, bool &bad) {
+  if (rem == 0) {
+    if (c.p >= c.e) { bad = true; return 0; }
+    bool neg;
+    v = rvi(c, neg);
+    rem = neg ? ln::rvu(c) + 2 : 1;
+    bad |= c.bad || rem == 0;
+  }
+  rem--;
+  return v;
+}
+__device__ __forceinline__ void uopt_skipn(ln::LCur &c, uint32_t &v, uint32_t &rem, uint32_t t, bool &bad) {
+  while (t > 0 && !bad) {
+    if (rem == 0) {
+      if (c.p >= c.e) { bad = true; return; }
+      bool neg;
+      v = rvi(c, neg);
+      rem = neg ? ln::rvu(c) + 2 : 1;
+      bad |= c.bad || rem == 0;
+    }
+    const uint32_t k = rem < t ? rem : t;
+    rem -= k;
+    t -= k;
+  }
+}
+
+__global__ void __launch_bounds__(64) k_ms_rest(Job J) {
+  const GeneralJob &j = J.j;
+  const uint32_t d = blockIdx.x;
+  Meta &M = J.meta[d];
+  if (!M.ok || !M.ms) return;
+  const uint32_t u0 = j.doc_upd[d];
+  const uint64_t ub = j.upd_off[u0];
+  const uint32_t len = (uint32_t)(j.upd_off[u0 + 1] - ub);
+  const uint8_t *D = j.A + ub;
+  Sec *S = a_sec(J, M);
+  uint32_t *ist = a_istart(J, M);
+  const uint32_t icap = len - M.r0 + 1;
+  const bool w = threadIdx.x == 0;
+  ln::LCur ci = ln::make(D, M.col0[4], M.col1[4]);  // info column (RleDecoder<u8>)
+  uint32_t iv = 0, irem = 0;                          // run value, values left (NONE: the endless final run)
+  ln::LCur cl = ln::make(D, M.col0[8], M.col1[8]);  // len column
+  uint32_t lv = 0, lrem = 0;
+  ln::LCur cr = ln::make(D, M.r0, len);              // rest stream
+  uint32_t i = 0, iord = 0;
+  bool bad = false;
+  for (uint32_t s = 0; s < M.nsec && !bad; s++) {
+    const uint32_t W = ln::rvu(cr);
+    const uint32_t clock = ln::rvu(cr);
+    bad |= cr.bad || W == 0 || W > (1u << 26);  // (an empty section still consumes a client value: declined)
+    if (w) {
+      S[s].S = i;
+      S[s].W = W;
+      S[s].clock = clock;
+      S[s].pay0 = cr.p;
+      S[s].ibase = iord;
+    }
+    uint32_t rem = bad ? 0 : W;
+    while (rem > 0 && !bad) {
+      if (irem == 0) {
+        if (ci.p >= ci.e) { bad = true; break; }
+        iv = ln::rdb(ci);
+        if (ci.p >= ci.e) irem = NONE;
+        else { irem = ln::rvu(ci) + 1; bad |= ci.bad || irem == 0; }
+      }
+      const uint32_t t = irem < rem ? irem : rem;
+      const uint32_t ref = iv & 31;
+      if (iv == 10 || ref == 3 || ref == 5 || ref == 6 || ref == 8) {  // payloads, struct by struct
+        for (uint32_t q = 0; q < t && !bad; q++) {
+          if (iord >= icap) { bad = true; break; }
+          if (w) ist[iord] = cr.p;
+          iord++;
+          if (iv == 10) {                       // Skip: vu(length)
+            bad |= ln::rvu(cr) == 0;
+          } else if (ref == 3) {                // ContentBinary: varUint8Array
+            const uint32_t nb = ln::rvu(cr);
+            if (cr.bad || !ln::room(cr, nb)) bad = true;
+            else ln::skip(cr, nb);
+          } else if (ref == 8) {                // ContentAny: len column, then that many values
+            const uint32_t cnt = uopt_next(cl, lv, lrem, bad);
+            bad |= cnt == 0;
+            for (uint32_t a = 0; a < cnt && !cr.bad && !bad; a++) ln::any_canon(cr);
+          } else {                              // ContentEmbed / ContentFormat: writeJSON = writeAny
+            ln::any_canon(cr);
+          }
+          bad |= cr.bad;
+        }
+      } else if (ref == 0) {                    // GC (info exactly 0, as GC.write writes it): len column
+        bad |= iv != 0;
+        uopt_skipn(cl, lv, lrem, t, bad);
+      } else if (ref == 1) {                    // ContentDeleted: len column
+        uopt_skipn(cl, lv, lrem, t, bad);
+      } else if (ref != 4 && ref != 7) {        // (String / Type: columns only) JSON, Doc, invalid refs
+        bad = true;
+      }
+      i += t;
+      rem -= t;
+      if (irem != NONE) irem -= t;
+      bad |= i > (1u << 26);
+    }
+    if (w) S[s].pay1 = cr.p;
+  }
+  bad |= cr.bad;
+  if (w) {
+    M.n = i;
+    M.nitem = iord;
+    M.ds0 = cr.p;
+    if (bad) { M.ok = 0; M.why = 50; }
+  }
+}
+
+__global__ void k_ms_sizes_k(Job J, uint64_t *sizes) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= J.j.n) return;
+  Meta &M = J.meta[d];
+  if (!M.ok || !M.ms) return;
+  uint32_t colb[NK];
+  for (uint32_t k = 0; k < NK; k++) colb[k] = M.col1[col_of(k)] - M.col0[col_of(k)];
+  sizes[d] = (scr_layout(M, M.n, M.nsec, true, colb) + 255) & ~255ull;
+}
+
+// ---- K2: struct passes ----------------------------------------------------------------------------------
+constexpr uint32_t SVMAX = 2048, SVSLOTS = 4096;  // state-vector entries / LDS hash slots
+__device__ __forceinline__ uint32_t sv_hash(uint32_t c) { return (c * 0x9E3779B1u) >> 20; }
+// the section holding struct i (sections are contiguous, non-empty, in struct order)
+__device__ __forceinline__ uint32_t sec_of(const Sec *S, uint32_t nsec, uint32_t i) {
+  uint32_t lo = 0, hi = nsec;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (S[mid].S <= i) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+__device__ __forceinline__ uint32_t put_vu_g(uint8_t *o, uint32_t p, uint32_t v) {
+  while (v > 127) { o[p++] = (uint8_t)(0x80 | (v & 127)); v >>= 7; }
+  o[p++] = (uint8_t)v;
+  return p;
+}
+
+// per-struct values of the scans: the nine kinds, payload-struct ordinal, key writers
+enum { X_IT = NK, X_KW, NX };
+
+template <int OP>
+__global__ void __launch_bounds__(KT) k_ms_struct(Job J) {
+  const GeneralJob &j = J.j;
+  const uint32_t d = blockIdx.x, t = threadIdx.x;
+  Meta &M = J.meta[d];
+  if (!M.ok || !M.ms) return;
+  __shared__ uint32_t sh[4 * 16];
+  __shared__ uint32_t s_bad;
+  __shared__ uint32_t mkey[OP == OP_DIFF ? SVSLOTS : 1], mval[OP == OP_DIFF ? SVSLOTS : 1];
+  __shared__ uint32_t svclk[OP == OP_DIFF ? SVMAX : 1];
+  const uint32_t u0 = j.doc_upd[d];
+  const uint64_t ub = j.upd_off[u0];
+  const uint32_t len = (uint32_t)(j.upd_off[u0 + 1] - ub);
+  const uint8_t *D = j.A + ub;
+  const uint32_t n = M.n, nsec = M.nsec;
+  Sec *S = a_sec(J, M);
+  const uint32_t *ist = a_istart(J, M);
+  const uint8_t *info_a = a_info(J, M), *pi_a = a_pi(J, M), *tr_a = a_tr(J, M);
+  const uint32_t *sl_a = a_sl(J, M), *ln_a = a_ln(J, M), *cl_a = a_cl(J, M);
+#define MS_DECLINE(code)                       \
+  {                                            \
+    if (t == 0) { M.ok = 0; M.why = (code); }  \
+    return;                                    \
+  }
+  // the string body must be ASCII (a UTF-16 slice is then a byte slice; k_big_v2's condition)
+  {
+    bool na = false;
+    for (uint32_t i = 16 * t; i < M.sn; i += 16 * KT) {
+      const uint32_t m = M.sn - i < 16 ? M.sn - i : 16;
+      for (uint32_t q = 0; q < m; q++) na |= D[M.sb0 + i + q] >= 0x80;
+    }
+    if (__syncthreads_or(na)) MS_DECLINE(21)
+  }
+  if (M.nval[K_CL] == 0) MS_DECLINE(22)
+  for (uint32_t s = t; s < nsec; s += KT) {
+    S[s].skipk = ~0ull;
+    S[s].f = NONE;
+  }
+  // decodeStateVector (encoding.js:536-545): a later entry for a client wins
+  if (OP == OP_DIFF) {
+    for (uint32_t q = t; q < SVSLOTS; q += KT) mval[q] = 0;
+    __syncthreads();
+    if (t == 0) {
+      const uint64_t s0 = j.sv_off[d], s1 = j.sv_off[d + 1];
+      ln::LCur c = ln::make(j.sv + s0, 0, (uint32_t)(s1 - s0));
+      const uint32_t ns = s1 - s0 > (1u << 20) ? NONE : ln::rvu(c);
+      bool bad = ns == NONE || ns > SVMAX;
+      for (uint32_t q = 0; q < ns && !bad; q++) {
+        const uint32_t cl = ln::rvu(c), ck = ln::rvu(c);
+        bad |= c.bad;
+        svclk[q] = ck;
+        uint32_t h = sv_hash(cl);
+        while (mval[h] != 0 && mkey[h] != cl) h = (h + 1) & (SVSLOTS - 1);
+        mkey[h] = cl;
+        mval[h] = q + 1;
+      }
+      s_bad = bad || c.bad;
+    }
+    __syncthreads();
+    if (s_bad) MS_DECLINE(20)
+  }
+  __syncthreads();
+  // running sums carried across tiles: NX kinds, body bytes; clock prefix in 64 bits
+  uint32_t base[NX + 1];
+  uint64_t clock = 0;
+  for (uint32_t pass = 1; pass <= (OP == OP_DIFF ? 2u : 1u); pass++) {
+#pragma unroll
+    for (uint32_t q = 0; q <= NX; q++) base[q] = 0;
+    clock = 0;
+    for (uint32_t t0 = 0; t0 < n; t0 += TILE) {
+      const uint32_t i0 = t0 + t * PER;
+      uint32_t s = sec_of(S, nsec, i0 < n ? i0 : n - 1);
+      uint32_t vv[PER], pv[PER], tv[PER], sec[PER];
+      bool st[PER];
+      uint32_t cons[PER][NX];
+      bool bad = false;
+      uint32_t xp[2] = {0, 0}, pi0 = 0, tr0 = 0;
+#pragma unroll
+      for (uint32_t e = 0; e < PER; e++) {
+        const uint32_t i = i0 + e;
+        const bool valid = i < n;
+        while (valid && s + 1 < nsec && S[s + 1].S <= i) s++;
+        sec[e] = s;
+        st[e] = valid && S[s].S == i;
+        const uint32_t v = valid ? info_a[i] : 0;
+        vv[e] = v;
+        const uint32_t ref = v & 31;
+        const bool sk = valid && v == 10, gc = valid && ref == 0, item = valid && !sk && !gc;
+        bad |= gc && v != 0;
+        bad |= item && (ref == 2 || ref == 9 || ref >= 10);
+        bad |= item && (v & 0xC0) && (v & 0x20);  // parentSub bit next to an origin: re-encoded without it
+        cons[e][K_PI] = item && !(v & 0xC0);
+        cons[e][K_TR] = item && ref == 7;
+        xp[0] += cons[e][K_PI];
+        xp[1] += cons[e][K_TR];
+      }
+      // parentInfo / typeRef indices first (the other kinds depend on their values)
+      {
+        uint32_t tp[2];
+        block_scan<2>(xp, tp, sh);
+        uint32_t pidx = base[K_PI] + xp[0], tidx = base[K_TR] + xp[1];
+#pragma unroll
+        for (uint32_t e = 0; e < PER; e++) {
+          pv[e] = 0;
+          tv[e] = 0;
+          if (cons[e][K_PI]) {
+            pv[e] = pidx < M.nval[K_PI] ? pi_a[pidx] : M.finv[K_PI];
+            bad |= pidx >= M.nval[K_PI] && !M.fin[K_PI];
+            pidx++;
+          }
+          if (cons[e][K_TR]) {
+            bad |= tidx >= M.nval[K_TR];
+            tv[e] = tidx < M.nval[K_TR] ? tr_a[tidx] : 0;
+            tidx++;
+          }
+        }
+        pi0 = base[K_PI] + xp[0];
+        tr0 = base[K_TR] + xp[1];
+        base[K_PI] += tp[0];
+        base[K_TR] += tp[1];
+      }
+      uint32_t xs[NX], tot[NX];
+#pragma unroll
+      for (uint32_t q = 0; q < NX; q++) xs[q] = 0;
+#pragma unroll
+      for (uint32_t e = 0; e < PER; e++) {
+        const uint32_t v = vv[e], ref = v & 31;
+        const bool valid = i0 + e < n;
+        const bool sk = valid && v == 10, gc = valid && ref == 0, item = valid && !sk && !gc;
+        const bool o = item && (v & 0x80), r = item && (v & 0x40), no = item && !(v & 0xC0);
+        const bool key = item && ref == 7 && (tv[e] == 3 || tv[e] == 5);
+        cons[e][K_INFO] = valid;
+        cons[e][K_CL] = st[e] + o + r + (no && pv[e] != 1);
+        cons[e][K_LC] = o + (no && pv[e] != 1);
+        cons[e][K_RC] = r;
+        cons[e][K_SL] = (no && pv[e] == 1) + (no && (v & 0x20)) + (item && ref == 4) + (item && ref == 6) + key;
+        cons[e][K_LN] = gc + (item && (ref == 1 || ref == 8));
+        cons[e][K_KC] = key;
+        cons[e][X_IT] = sk + (item && (ref == 3 || ref == 5 || ref == 6 || ref == 8));
+        cons[e][X_KW] = (item && ref == 6) + key;
+#pragma unroll
+        for (uint32_t q = 0; q < NX; q++)
+          if (q != K_PI && q != K_TR) xs[q] += cons[e][q];
+      }
+      block_scan<NX>(xs, tot, sh);  // (PI / TR entries are zero here: their prefixes come from above)
+      // string lengths -> body bytes; clock lengths
+      uint32_t sli = base[K_SL] + xs[K_SL], lni = base[K_LN] + xs[K_LN], iti = base[X_IT] + xs[X_IT];
+      uint32_t clen[PER], bodyb[PER];
+      uint32_t xb[2] = {0, 0};
+#pragma unroll
+      for (uint32_t e = 0; e < PER; e++) {
+        const uint32_t v = vv[e], ref = v & 31;
+        const bool valid = i0 + e < n;
+        const bool sk = valid && v == 10, gc = valid && ref == 0, item = valid && !sk && !gc;
+        uint32_t bl = 0;
+        for (uint32_t q = 0; q < cons[e][K_SL]; q++) bl += sli + q < M.nval[K_SL] ? sl_a[sli + q] : 0;
+        bad |= sli + cons[e][K_SL] > M.nval[K_SL];
+        uint32_t cl = 0;
+        if (sk) {  // Skip: vu(length) in the rest stream
+          bad |= iti >= M.nitem;
+          if (iti < M.nitem) {
+            ln::LCur c = ln::make(D, ist[iti], len);
+            cl = ln::rvu(c);
+          }
+        } else if (gc || (item && (ref == 1 || ref == 8))) {
+          bad |= lni >= M.nval[K_LN];
+          cl = lni < M.nval[K_LN] ? ln_a[lni] : 0;
+        } else if (item && ref == 4) {
+          cl = sli + cons[e][K_SL] - 1 < M.nval[K_SL] ? sl_a[sli + cons[e][K_SL] - 1] : 0;  // the content string: last
+        } else if (item) {
+          cl = 1;
+        }
+        bad |= valid && (cl == 0 || cl >= (1u << 20));  // (lengths keep the block's clock sums in u32)
+        clen[e] = cl;
+        bodyb[e] = bl;
+        xb[0] += bl;
+        xb[1] += cl;
+        sli += cons[e][K_SL];
+        lni += cons[e][K_LN];
+        iti += cons[e][X_IT];
+      }
+      uint32_t tb[2];
+      block_scan<2>(xb, tb, sh);
+      // per struct: the prefixes before it
+      uint32_t pre[NX];
+#pragma unroll
+      for (uint32_t q = 0; q < NX; q++) pre[q] = base[q] + xs[q];
+      pre[K_PI] = pi0;
+      pre[K_TR] = tr0;
+      uint32_t bo = base[NX] + xb[0];
+      uint64_t ck = clock + xb[1];
+#pragma unroll
+      for (uint32_t e = 0; e < PER; e++) {
+        const uint32_t i = i0 + e;
+        const bool valid = i < n;
+        const uint32_t v = vv[e], ref = v & 31;
+        const bool sk = valid && v == 10;
+        const uint32_t s2 = sec[e];
+        if (pass == 1 && valid) {
+          if (st[e]) {
+            Sec &X = S[s2];
+            X.C0 = (uint32_t)ck;
+            X.C1 = (uint32_t)(ck + clen[e]);
+            X.body0 = bo;
+#pragma unroll
+            for (uint32_t q = 0; q < NK; q++) X.pre[q] = pre[q];
+            X.kw0 = pre[X_KW];
+            bad |= pre[X_IT] != X.ibase;  // the rest walk and the columns agree on the payload structs
+          }
+          if (sk) atomicMin(&S[s2].skipk, ((unsigned long long)i << 32) | (uint32_t)ck);
+        }
+        if (pass == 2 && valid && !sk) {
+          const Sec &X = S[s2];
+          const uint64_t startc = (uint64_t)X.clock + ((uint32_t)ck - X.C0), end = startc + clen[e];
+          const uint64_t svs = X.sv;
+          const bool before_ok = st[e] || startc <= svs;
+          // a Skip right before a struct that ends past the state vector: the cut may lie before it
+          bad |= !st[e] && startc > svs && end > svs && info_a[i - 1] == 10;
+          if (end > svs && before_ok) {  // the cut (us@40707): the first non-Skip struct ending past sv
+            Sec &Y = S[s2];
+            Y.f = i;
+            Y.fclock = (uint32_t)startc;
+            Y.off = svs > startc ? (uint32_t)(svs - startc) : 0;
+            Y.info_f = v;
+            Y.pi_f = pv[e];
+            Y.tr_f = tv[e];
+            Y.clen_f = clen[e];
+            Y.iord_f = pre[X_IT];
+            Y.kwf = pre[X_KW];
+            Y.body_f = bo;
+            Y.body_f1 = bo + bodyb[e];
+            Y.body_fc = ref == 4 ? bo + bodyb[e] - clen[e] : bo + bodyb[e];
+#pragma unroll
+            for (uint32_t q = 0; q < NK; q++) {
+              Y.pf[q] = pre[q] + (q == K_CL && st[e] ? 1 : 0);
+              Y.pf1[q] = pre[q] + cons[e][q];
+            }
+          }
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < NX; q++) pre[q] += cons[e][q];
+        bo += bodyb[e];
+        ck += clen[e];
+      }
+      bad |= clock + tb[1] > 0xffffffffull;
+      if (__syncthreads_or(bad)) MS_DECLINE(23)
+#pragma unroll
+      for (uint32_t q = 0; q < NX; q++)
+        if (q != K_PI && q != K_TR) base[q] += tot[q];
+      base[NX] += tb[0];
+      clock += tb[1];
+      __syncthreads();
+    }
+    __threadfence_block();
+    __syncthreads();
+    if (pass == 1) {
+      // every column consumed exactly (as the re-encoding writes it); strings inside the body
+      bool bad = false;
+      uint32_t code = 24;
+      if (t == 0) {
+#pragma unroll
+        for (uint32_t q = 0; q < NK; q++) {
+          // (keyClock: only XmlElement / XmlHook types read it, while every writeKey -- formats too -- wrote
+          // one: the column is read as far as needed, and rewritten from 0)
+          const bool b = q == K_KC ? base[q] > M.nval[q]
+                         : k_rle(q) ? (M.fin[q] ? base[q] < M.nval[q] + 1 : base[q] != M.nval[q]) : base[q] != M.nval[q];
+          if (b && !bad) code = 100 + q;
+          bad |= b;
+          M.tot[q] = base[q];
+        }
+        if (!bad && base[X_IT] != M.nitem) { bad = true; code = 110; }
+        if (!bad && base[NX] > M.sn) { bad = true; code = 111; }
+        M.body_end = base[NX];
+        M.clock_tot = (uint32_t)clock;
+      }
+      // each section's client: descending (as yjs writes them), so no client repeats; its sv clock
+      for (uint32_t s = t; s < nsec && !bad; s += KT) {
+        const uint32_t ci = S[s].pre[K_CL];
+        if (ci >= M.nval[K_CL]) { bad = true; code = 25; break; }
+        const uint32_t client = cl_a[ci];
+        S[s].client = client;
+        const uint32_t cn = s + 1 < nsec ? S[s + 1].C0 : (uint32_t)clock;
+        if ((uint64_t)S[s].clock + (cn - S[s].C0) > 0xffffffffull) { bad = true; code = 26; }  // clocks stay u32
+        if (s > 0 && (S[s - 1].pre[K_CL] >= M.nval[K_CL] || cl_a[S[s - 1].pre[K_CL]] <= client)) { bad = true; code = 27; }
+        uint32_t svc = 0;
+        if (OP == OP_DIFF) {
+          uint32_t h = sv_hash(client);
+          while (mval[h] != 0) {
+            if (mkey[h] == client) { svc = svclk[mval[h] - 1]; break; }
+            h = (h + 1) & (SVSLOTS - 1);
+          }
+        }
+        S[s].sv = svc;
+      }
+      if (__syncthreads_or(bad)) {
+        if (bad) M.why = code;  // (a racy but harmless debugging aid)
+        if (t == 0) M.ok = 0;
+        return;
+      }
+      __threadfence_block();
+      __syncthreads();
+    }
+  }
+  if (OP == OP_DIFF) {
+    if (t == 0) {
+      uint32_t nk = 0, kc = 0;
+      for (uint32_t s = 0; s < nsec; s++) {
+        if (S[s].f == NONE) continue;
+        nk++;
+        kc += (s + 1 < nsec ? S[s + 1].kw0 : base[X_KW]) - S[s].kwf;
+      }
+      M.nkept = nk;
+      M.kc_out = kc;
+    }
+    return;
+  }
+  // encodeStateVectorFromUpdateV2 (os@37724) / parseUpdateMetaV2: one entry per section, written by one thread
+  if (t != 0) return;
+  const uint32_t ctot = M.clock_tot;
+  auto sec_end = [&](uint32_t s) -> uint32_t {  // the section's end clock
+    const uint32_t cn = s + 1 < nsec ? S[s + 1].C0 : ctot;
+    return S[s].clock + (cn - S[s].C0);
+  };
+  auto sv_val = [&](uint32_t s) -> uint32_t {  // what the state vector records for the section's client
+    const Sec &X = S[s];
+    if (X.clock != 0) return 0;  // stopCounting: the client must start at 0
+    if (X.skipk == ~0ull) return sec_end(s);
+    const uint32_t si = (uint32_t)(X.skipk >> 32), sc = (uint32_t)X.skipk;
+    if (si == X.S) return s == 0 ? X.clock + (X.C1 - X.C0) : 0;  // (the update's first struct is counted)
+    return X.clock + (sc - X.C0);
+  };
+  uint32_t total = 0, cnt = 0;
+  if (OP == OP_SV) {
+    for (uint32_t s = 0; s < nsec; s++) {
+      const uint32_t v = sv_val(s);
+      if (v) { cnt++; total += vsz(S[s].client) + vsz(v); }
+    }
+    total += vsz(cnt);
+  } else {
+    for (uint32_t s = 0; s < nsec; s++) total += 2 * vsz(S[s].client) + vsz(S[s].clock) + vsz(sec_end(s));
+    total += 2 * vsz(nsec);
+  }
+  const uint64_t b = atomicAdd((unsigned long long *)j.used, (unsigned long long)total);
+  J.done[d] = 1;
+  atomicAdd((unsigned long long *)j.pw_count, 1ull);
+  if (b + total > j.cap) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; return; }
+  uint8_t *o = j.out + b;
+  uint32_t p = 0;
+  if (OP == OP_SV) {
+    p = put_vu_g(o, p, cnt);
+    for (uint32_t s = 0; s < nsec; s++) {
+      const uint32_t v = sv_val(s);
+      if (v) { p = put_vu_g(o, p, S[s].client); p = put_vu_g(o, p, v); }
+    }
+  } else {
+    p = put_vu_g(o, p, nsec);
+    for (uint32_t s = 0; s < nsec; s++) { p = put_vu_g(o, p, S[s].client); p = put_vu_g(o, p, S[s].clock); }
+    p = put_vu_g(o, p, nsec);
+    for (uint32_t s = 0; s < nsec; s++) { p = put_vu_g(o, p, S[s].client); p = put_vu_g(o, p, sec_end(s)); }
+  }
+  j.out_off[d] = b;
+  j.out_len[d] = total;
+  j.status[d] = ym::ST_OK;
+#undef MS_DECLINE
+}
+
+// ---- K3: columns ----------------------------------------------------------------------------------------
+// an input entry with its value index and (IntDiff) running value before it
+struct EW {
+  uint32_t pos, end, idx, cnt, val;
+  int32_t df;
+  int64_t vr;
+  bool ok;
+};
+__device__ __forceinline__ EW ew_at(const uint8_t *D, uint32_t kind, uint32_t c1, uint32_t tot, uint32_t pos, uint32_t idx, int64_t vr) {
+  EW w{pos, c1, idx, 0, 0, 0, vr, false};
+  if (pos >= c1 || idx >= tot) return w;
+  const Ent e = dec_entry(D, pos, c1, kind);
+  if (e.bad) return w;
+  w.cnt = e.fin ? tot - idx : e.cnt;
+  w.val = e.val;
+  w.df = e.df;
+  w.end = e.end;
+  w.ok = w.cnt > 0 && w.end > pos;
+  return w;
+}
+__device__ __forceinline__ EW ew_next(const uint8_t *D, uint32_t kind, uint32_t c1, uint32_t tot, const EW &w) {
+  return ew_at(D, kind, c1, tot, w.end, w.idx + w.cnt, w.vr + (int64_t)w.df * w.cnt);
+}
+__device__ __forceinline__ uint32_t ew_value(uint32_t kind, const EW &w, uint32_t x) {
+  return k_dif(kind) ? (uint32_t)(w.vr + (int64_t)w.df * (x - w.idx + 1)) : w.val;
+}
+// the entry holding value x: K1's last checkpoint at or before it, then at most CKSTEP entries
+__device__ __forceinline__ EW locate(const Job &J, const Meta &M, const uint8_t *D, uint32_t kind, uint32_t c0, uint32_t c1,
+                                     uint32_t tot, uint32_t x) {
+  const uint4 *ck = a_ck(J, M, kind);
+  uint32_t lo = 0, hi = M.nck[kind];
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (ck[mid].y <= x) lo = mid; else hi = mid;
+  }
+  uint32_t pos = c0, idx = 0;
+  int64_t vr = 0;
+  if (M.nck[kind] > 0) {
+    const uint4 c4 = ck[lo];
+    pos = c4.x;
+    idx = c4.y;
+    vr = c4.z;
+  }
+  EW w{pos, c1, idx, 0, 0, 0, vr, false};
+  if (pos < c0 || pos > c1 || idx > x) return w;
+  w = ew_at(D, kind, c1, tot, pos, idx, vr);
+  for (uint32_t g = 0; g <= 2 * CKSTEP && w.ok && x >= w.idx + w.cnt; g++) w = ew_next(D, kind, c1, tot, w);
+  if (w.ok && (x < w.idx || x >= w.idx + w.cnt)) w.ok = false;
+  return w;
+}
+struct Run {
+  uint32_t v;
+  int32_t d;
+  uint32_t c;
+};
+__device__ __forceinline__ Run clip(uint32_t kind, const EW &w, uint32_t lo, uint32_t hi) {
+  const uint32_t a = lo > w.idx ? lo : w.idx, b = hi < w.idx + w.cnt ? hi : w.idx + w.cnt;
+  return Run{ew_value(kind, w, a), k_dif(kind) ? w.df : 0, b > a ? b - a : 0};
+}
+// a run of c values (v, v + d, ...) into the wave-uniform encoder
+__device__ __forceinline__ void feed(Enc &E, Buf &B, uint32_t kind, const Run &r) {
+  if (r.c == 0) return;
+  E.put(B, kind, r.v);
+  if (r.c == 1) return;
+  if (k_dif(kind)) {
+    const uint32_t last = (uint32_t)((int64_t)r.v + (int64_t)r.d * (r.c - 1));
+    if (E.df == r.d && E.cnt > 0) {
+      E.cnt += r.c - 1;
+    } else {
+      E.flush(B, kind);
+      E.cnt = r.c - 1;
+      E.df = r.d;
+    }
+    E.s = last;
+  } else {
+    E.cnt += r.c - 1;
+  }
+}
+// Item.write(encoder, off) / GC.write of the cut struct into column `kind` (v2_write of ym_big2.hip),
+// preceded on the client column by the LazyStructWriter's writeClient; fv = the struct's own input values
+// of the column, in reading order
+__device__ __forceinline__ uint32_t head_vals(uint32_t kind, const Sec &X, const uint32_t *fv, uint32_t nf, uint32_t *hv, bool &bad) {
+  const uint32_t info = X.info_f, off = X.off, ref = info & 31;
+  const bool gc = ref == 0, item = !gc;
+  const bool o = item && (info & 0x80), r = item && (info & 0x40), no = item && !(info & 0xC0);
+  const bool has_o = item && (off > 0 || o);
+  const bool pinfo = item && !has_o && !r;  // parent info written (implies no origins and off == 0)
+  const bool pp = no && X.pi_f != 1, py = no && X.pi_f == 1;
+  const bool key = item && ref == 7 && (X.tr_f == 3 || X.tr_f == 5);
+  uint32_t nh = 0, fi = 0;
+  switch (kind) {
+    case K_INFO:
+      fi++;
+      hv[nh++] = gc ? 0 : (ref | (has_o ? 0x80 : 0) | (info & 0x40) | (no ? (info & 0x20) : 0));
+      break;
+    case K_CL: {
+      const uint32_t oc = o ? fv[fi++] : 0, rc = r ? fv[fi++] : 0, pc = pp ? fv[fi++] : 0;
+      hv[nh++] = X.client;
+      if (item && off > 0) hv[nh++] = X.client;
+      else if (o) hv[nh++] = oc;
+      if (r) hv[nh++] = rc;
+      if (pinfo && pp) hv[nh++] = pc;
+      break;
+    }
+    case K_LC: {
+      const uint32_t ok = o ? fv[fi++] : 0, pk = pp ? fv[fi++] : 0;
+      if (item && off > 0) hv[nh++] = X.fclock + off - 1;
+      else if (o) hv[nh++] = ok;
+      if (pinfo && pp) hv[nh++] = pk;
+      break;
+    }
+    case K_RC:
+      if (r) hv[nh++] = fv[fi++];
+      break;
+    case K_PI:
+      if (no) fi++;
+      if (pinfo) hv[nh++] = X.pi_f == 1 ? 1 : 0;
+      break;
+    case K_SL: {
+      const uint32_t yk = py ? fv[fi++] : 0, ps = no && (info & 0x20) ? fv[fi++] : 0;
+      const bool hc = item && (ref == 4 || ref == 6 || key);
+      const uint32_t cs = hc ? fv[fi++] : 0;
+      if (pinfo && py) hv[nh++] = yk;
+      if (pinfo && (info & 0x20)) hv[nh++] = ps;
+      if (item && ref == 4) hv[nh++] = cs - off;
+      else if (hc) hv[nh++] = cs;
+      break;
+    }
+    case K_LN:
+      if (gc || ref == 1 || ref == 8) { fi++; hv[nh++] = X.clen_f - off; }
+      break;
+    case K_TR:
+      if (item && ref == 7) { fi++; hv[nh++] = X.tr_f; }
+      break;
+  }
+  bad |= fi != nf;
+  return nh;
+}
+
+constexpr uint32_t NKC = K_KC;  // spliced kinds (the keyClock column is regenerated)
+constexpr uint32_t RMAX = 8;    // runs before a span: <= 5 head values + the range's first two entries
+__global__ void __launch_bounds__(64) k_ms_col(Job J) {
+  const GeneralJob &j = J.j;
+  const uint32_t d = blockIdx.x, kind = blockIdx.y, lane = threadIdx.x;
+  Meta &M = J.meta[d];
+  if (!M.ok || !M.ms) return;
+  __shared__ Run sr[64][RMAX + 1];  // [RMAX]: the tail run after the span
+  __shared__ uint32_t snr[64], sm0[64], sm1[64], ssm[64], skept[64];
+  const uint8_t *D = j.A + j.upd_off[j.doc_upd[d]];
+  const uint32_t c0 = M.col0[col_of(kind)], c1 = M.col1[col_of(kind)];
+  const uint32_t tot = M.tot[kind], nsec = M.nsec;
+  const Sec *S = a_sec(J, M);
+  Buf B{a_col(J, M, kind), 0, M.ocap[kind], false};
+  B.wr = lane == 0;
+  Enc E;
+  bool bad = false;
+  for (uint32_t s0 = 0; s0 < nsec && !bad && !B.over; s0 += 64) {
+    const uint32_t s = s0 + lane;
+    // phase A (lane per section): the section's runs and span
+    uint32_t nr = 0, m0 = 0, m1 = 0, sm = 0, kept = 0;
+    Run tail{0, 0, 0};
+    bool lbad = false;
+    if (s < nsec && S[s].f != NONE) {
+      const Sec &X = S[s];
+      kept = 1;
+      const uint32_t pf = X.pf[kind], pf1 = X.pf1[kind];
+      const uint32_t pe = s + 1 < nsec ? S[s + 1].pre[kind] : tot;
+      uint32_t fv[4] = {0, 0, 0, 0};
+      const uint32_t nf = pf1 - pf;
+      lbad |= pf1 < pf || nf > 4 || pe < pf1 || pe > tot;
+      EW w{};
+      w.ok = false;
+      if (!lbad && nf > 0) {
+        w = locate(J, M, D, kind, c0, c1, tot, pf);
+        for (uint32_t q = 0; q < nf && w.ok; q++) {
+          while (w.ok && pf + q >= w.idx + w.cnt) w = ew_next(D, kind, c1, tot, w);
+          fv[q] = ew_value(kind, w, pf + q);
+        }
+        lbad |= !w.ok;
+      }
+      uint32_t hv[6];
+      const uint32_t nh = lbad ? 0 : head_vals(kind, X, fv, nf, hv, lbad);
+      for (uint32_t h = 0; h < nh; h++) sr[lane][nr++] = Run{hv[h], 0, 1};
+      if (!lbad && pf1 < pe) {
+        EW e1 = (w.ok && pf1 >= w.idx && pf1 < w.idx + w.cnt) ? w
+                : (w.ok && pf1 == w.idx + w.cnt) ? ew_next(D, kind, c1, tot, w)
+                                                 : locate(J, M, D, kind, c0, c1, tot, pf1);
+        lbad |= !e1.ok;
+        if (!lbad) {
+          sr[lane][nr++] = clip(kind, e1, pf1, pe);
+          if (e1.idx + e1.cnt < pe) {
+            const EW e2 = ew_next(D, kind, c1, tot, e1);
+            lbad |= !e2.ok;
+            if (!lbad) {
+              sr[lane][nr++] = clip(kind, e2, pf1, pe);
+              if (e2.idx + e2.cnt < pe) {
+                const EW em = locate(J, M, D, kind, c0, c1, tot, pe - 1);
+                lbad |= !em.ok || em.idx < e2.idx + e2.cnt || em.pos < e2.end;
+                if (!lbad) {
+                  m0 = e2.end;
+                  m1 = em.pos;  // the full entries strictly between: verbatim
+                  sm = (uint32_t)em.vr;
+                  tail = clip(kind, em, pf1, pe);
+                }
+              }
+            }
+          }
+        }
+      }
+    }
+    snr[lane] = nr;
+    sm0[lane] = m0;
+    sm1[lane] = m1;
+    ssm[lane] = sm;
+    skept[lane] = kept;
+    sr[lane][RMAX] = tail;
+    bad |= __any(lbad);
+    __syncthreads();
+    // phase B (wave-uniform): the encoder over the sections in order
+    const uint32_t nl = nsec - s0 < 64 ? nsec - s0 : 64;
+    for (uint32_t l = 0; l < nl && !bad; l++) {
+      if (!skept[l]) continue;
+      const uint32_t k = snr[l];
+      for (uint32_t r = 0; r < k; r++) feed(E, B, kind, sr[l][r]);
+      if (sr[l][RMAX].c > 0) {
+        const uint32_t a = sm0[l], b = sm1[l];
+        if (b > a) {  // the span: the pending run closes, the entries are copied, the tail starts a new run
+          E.flush(B, kind);
+          if ((uint64_t)B.n + (b - a) > B.cap) { B.over = true; break; }
+          wcopy(B.b + B.n, D + a, b - a);
+          B.n += b - a;
+          E.s = ssm[l];
+          E.cnt = 0;
+          E.started = 0;
+        }
+        feed(E, B, kind, sr[l][RMAX]);
+      }
+    }
+    __syncthreads();
+  }
+  E.flush(B, kind, true);
+  if (lane == 0) {
+    M.osz[kind] = B.n;
+    if (bad || B.over || E.bad) { M.ok = 0; M.why = 60 + kind; }
+  }
+}
+
+// ---- K4: output -----------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_ms_out(Job J) {
+  const GeneralJob &j = J.j;
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
+    Meta &M = J.meta[d];
+    if (!M.ok || !M.ms) continue;
+    const uint32_t u0 = j.doc_upd[d];
+    const uint64_t ub = j.upd_off[u0];
+    const uint32_t len = (uint32_t)(j.upd_off[u0 + 1] - ub);
+    const uint8_t *D = j.A + ub;
+    Sec *S = a_sec(J, M);
+    const uint32_t *ist = a_istart(J, M);
+    const uint32_t nsec = M.nsec;
+    // delete set: readDeleteSet's reads, canonical, no repeated or empty client (then copied)
+    uint32_t x = M.ds0;
+    bool bad = false;
+    uint32_t ndc;
+    {
+      ln::LCur c = ln::make(D, x, len);
+      ndc = ln::rvu(c);
+      x = c.p;
+      bad = c.bad || ndc > 4096;
+    }
+    uint32_t *dsc = reinterpret_cast<uint32_t *>(j.bscratch + (uint64_t)blockIdx.x * BS_BYTES + BS_DSC);
+    uint32_t *map = reinterpret_cast<uint32_t *>(j.bscratch + (uint64_t)blockIdx.x * BS_BYTES + BS_MAP);
+    const bool big = !bad && ndc > 64 && ndc <= BS_NDSC;
+    if (big) cmap::clear(map);
+    for (uint32_t i = 0; i < ndc && !bad; i++) {
+      ln::LCur h = ln::make(D, x, len);
+      const uint32_t client = ln::rvu(h);
+      const uint32_t m = ln::rvu(h);
+      x = h.p;
+      if (h.bad || m == 0 || i >= BS_NDSC) { bad = true; break; }
+      bool hit = false;
+      if (big) hit = cmap::seen_insert(map, client);
+      else for (uint32_t h0 = 0; h0 < i; h0 += 64) hit |= __any(h0 + lane < i && dsc[h0 + lane] == client);
+      if (hit) { bad = true; break; }
+      __syncthreads();
+      if (lane == 0) dsc[i] = client;
+      __threadfence_block();
+      __syncthreads();
+      x = wds::skip_varuints(D, x, len, 2ull * m);
+      if (x == NONE) bad = true;
+    }
+    if (bad) { if (lane == 0) { M.ok = 0; M.why = 70; } __syncthreads(); continue; }
+    const uint32_t ds1 = x;
+    // kept sections: string body piece, rest piece (after the cut struct's skipped ContentAny values)
+    uint32_t sbn = 0, rsz = 0, nk = 0;
+    for (uint32_t s0 = 0; s0 < nsec && !bad; s0 += 64) {
+      const uint32_t s = s0 + lane;
+      uint32_t bb = 0, rb = 0;
+      bool kept = false, lbad = false;
+      if (s < nsec && S[s].f != NONE) {
+        const Sec &X = S[s];
+        kept = true;
+        const uint32_t ref = X.info_f & 31;
+        const uint32_t hs0 = X.off == 0 ? X.body_f : ref == 4 ? X.body_fc + X.off : X.body_f1;
+        const uint32_t be = s + 1 < nsec ? S[s + 1].body0 : M.body_end;
+        lbad |= hs0 > be || be > M.sn || X.body_f > X.body_fc || X.body_fc > X.body_f1;
+        const uint32_t ie = s + 1 < nsec ? S[s + 1].ibase : M.nitem;
+        uint32_t rs = X.iord_f < ie ? ist[X.iord_f] : X.pay1;
+        if (ref == 8 && X.off > 0) {  // ContentAny.splice: the first `off` values are not written
+          ln::LCur c = ln::make(D, rs, X.pay1);
+          for (uint32_t a = 0; a < X.off && !c.bad; a++) ln::any_canon(c);
+          lbad |= c.bad;
+          rs = c.p;
+        }
+        lbad |= rs < X.pay0 || rs > X.pay1 || X.f < X.S || X.f - X.S >= X.W;
+        const uint32_t wr = X.W - (X.f - X.S), cw = X.fclock + X.off;
+        bb = lbad ? 0 : be - hs0;
+        rb = lbad ? 0 : vsz(wr) + vsz(cw) + (X.pay1 - rs);
+        S[s].rs = rs;
+      }
+      const uint32_t ib = wave_incl_add(bb), ir = wave_incl_add(rb);
+      if (kept) {
+        S[s].ob = sbn + ib - bb;
+        S[s].orr = rsz + ir - rb;
+      }
+      sbn += lane_read(ib, 63);
+      rsz += lane_read(ir, 63);
+      nk += (uint32_t)__builtin_popcountll(__ballot(kept));
+      bad |= __any(lbad);
+    }
+    bad |= nk != M.nkept;
+    __threadfence_block();  // the lanes' per-section offsets, read by the whole wave below
+    __syncthreads();
+    if (bad) { if (lane == 0) { M.ok = 0; M.why = 71; } __syncthreads(); continue; }
+    // column sizes: keyClock 0, 1, 2, ... = IntDiff runs (diff 0 x1)(diff 1 x K-1): 00 | 00 02 | 00 03 vu(K-3)
+    const uint32_t K = M.kc_out;
+    uint32_t cl[9];
+    cl[0] = K == 0 ? 0 : K == 1 ? 1 : K == 2 ? 2 : 2 + vsz(K - 3);
+    for (uint32_t k = 0; k < NKC; k++)
+      if (k != K_SL) cl[col_of(k)] = M.osz[k];
+    cl[5] = vsz(sbn) + sbn + M.osz[K_SL];
+    uint32_t total = 1;
+    for (uint32_t c = 0; c < 9; c++) total += vsz(cl[c]) + cl[c];
+    total += vsz(nk) + rsz + (ds1 - M.ds0);
+    uint64_t b = 0;
+    if (lane == 0) b = atomicAdd((unsigned long long *)j.used, (unsigned long long)total);
+    b = ((uint64_t)lane_read((uint32_t)(b >> 32), 0) << 32) | lane_read((uint32_t)b, 0);
+    if (lane == 0) { J.done[d] = 1; atomicAdd((unsigned long long *)j.pw_count, 1ull); }
+    if (b + total > j.cap) {
+      if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }
+      __syncthreads();
+      continue;
+    }
+    uint8_t *o = j.out + b;
+    auto put = [&](uint32_t p, uint32_t v) -> uint32_t {
+      if (lane == 0) put_vu_g(o, p, v);
+      return p + vsz(v);
+    };
+    uint32_t p = put(0, 0);
+    for (uint32_t c = 0; c < 9; c++) {
+      p = put(p, cl[c]);
+      if (c == 0) {
+        if (lane == 0 && K >= 1) o[p] = 0;
+        if (lane == 0 && K == 2) o[p + 1] = 2;
+        if (K >= 3) { if (lane == 0) o[p + 1] = 3; put(p + 2, K - 3); }
+        p += cl[0];
+        continue;
+      }
+      if (c == 5) {  // varString(body) | lengths
+        p = put(p, sbn);
+        for (uint32_t s = 0; s < nsec; s++) {
+          const Sec &X = S[s];
+          if (X.f == NONE) continue;
+          const uint32_t ref = X.info_f & 31;
+          const uint32_t hs0 = X.off == 0 ? X.body_f : ref == 4 ? X.body_fc + X.off : X.body_f1;
+          const uint32_t be = s + 1 < nsec ? S[s + 1].body0 : M.body_end;
+          wcopy(o + p + X.ob, D + M.sb0 + hs0, be - hs0);
+        }
+        p += sbn;
+        wcopy(o + p, a_col(J, M, K_SL), M.osz[K_SL]);
+        p += M.osz[K_SL];
+        continue;
+      }
+      uint32_t k = 0;
+      for (uint32_t q = 0; q < NKC; q++) if (col_of(q) == c) k = q;
+      wcopy(o + p, a_col(J, M, k), cl[c]);
+      p += cl[c];
+    }
+    p = put(p, nk);
+    for (uint32_t s = 0; s < nsec; s++) {
+      const Sec &X = S[s];
+      if (X.f == NONE) continue;
+      uint32_t q = p + X.orr;
+      q = put(q, X.W - (X.f - X.S));
+      q = put(q, X.fclock + X.off);
+      wcopy(o + q, D + X.rs, X.pay1 - X.rs);
+    }
+    p += rsz;
+    wcopy(o + p, D + M.ds0, ds1 - M.ds0);
+    if (lane == 0) {
+      j.out_off[d] = b;
+      j.out_len[d] = total;
+      j.status[d] = ym::ST_OK;
+    }
+    __syncthreads();
+  }
+}
+
+// ---- host launchers (pv2_run, ym_pv2.hip) -------------------------------------------------------------------
+void ms_rest(const Job &J, hipStream_t st) { k_ms_rest<<<J.j.n, 64, 0, st>>>(J); }
+void ms_sizes(const Job &J, uint64_t *sizes, hipStream_t st) { k_ms_sizes_k<<<(J.j.n + 255) / 256, 256, 0, st>>>(J, sizes); }
+void ms_run(uint32_t op, const Job &J, hipStream_t st) {
+  const uint32_t n = J.j.n;
+  if (op == OP_DIFF) {
+    k_ms_struct<OP_DIFF><<<n, KT, 0, st>>>(J);
+    k_ms_col<<<dim3(n, NKC), 64, 0, st>>>(J);
+    k_ms_out<<<n < BS_GRID ? n : BS_GRID, 64, 0, st>>>(J);
+  } else if (op == OP_SV) {
+    k_ms_struct<OP_SV><<<n, KT, 0, st>>>(J);
+  } else {
+    k_ms_struct<OP_META><<<n, KT, 0, st>>>(J);
+  }
+}
+
+}  // namespace pv2
+}  // namespace ymk

@@ -8,8 +8,6 @@ and never exchanges document data.  Partition:
 The only collectives are the max of the timed region and the sum of per-rank counters
 (torch.distributed: RCCL over xGMI on GPUs, gloo in the CPU tests).  Outputs return to host-side
 order by docIndex (``MultiDeviceEngine``, ``scatter_results``)."""
-import threading
-
 import numpy as np
 
 
@@ -131,11 +129,15 @@ def scatter_results(n_docs, shards, shard_results):
 
 class MultiDeviceEngine:
     """One host process driving several GPUs of a node (the library keeps one stream and workspace per
-    thread and device): a batch is partitioned over the devices, each shard runs on its own thread
-    against its own device, and the outputs come back in docIndex order.  ``runner(device)`` returns
-    an object with ``run_host`` (default: ``yjs_amd.Engine``); tests pass a stub."""
+    (thread, device)): a batch is partitioned over the devices, each shard runs on its device's own
+    long-lived worker thread, and the outputs come back in docIndex order.  The worker threads live as
+    long as the engine, so the library state they create (stream, events, pinned staging, device
+    scratch) is made once and reused by every call; ``close()`` releases it on the threads that own it
+    (``ym_shutdown``).  ``runner(device)`` returns an object with ``run_host`` (default:
+    ``yjs_amd.Engine``, created on the worker thread); tests pass a stub."""
 
     def __init__(self, devices, partition_by="hash", runner=None):
+        from concurrent.futures import ThreadPoolExecutor
         self.devices = list(devices)
         self.partition_by = partition_by
         if runner is None:
@@ -143,8 +145,10 @@ class MultiDeviceEngine:
             runner = Engine
         self._runner = runner
         self._engines = [None] * len(self.devices)
+        self._pools = [ThreadPoolExecutor(max_workers=1, thread_name_prefix=f"ym-dev{d}") for d in self.devices]
 
     def _engine(self, i):
+        # always called on worker thread i: the engine's ym_init binds that thread to device i
         if self._engines[i] is None:
             self._engines[i] = self._runner(self.devices[i])
         return self._engines[i]
@@ -152,35 +156,54 @@ class MultiDeviceEngine:
     def run_host(self, op, fmt, arena, upd_off, doc_upd, sv_arena=None, sv_off=None):
         """Like Engine.run_host, but returns per-document results in docIndex order: a list of bytes
         (status 0) or int status codes."""
+        if self._pools is None:
+            raise RuntimeError("MultiDeviceEngine is closed")
         n = len(doc_upd) - 1
         G = len(self.devices)
         shards = partition(doc_sizes(upd_off, doc_upd), G, self.partition_by)
-        results = [None] * G
-        errors = []
 
         def work(i):
-            try:
-                ids = shards[i]
-                a, o, d = gather_docs(arena, upd_off, doc_upd, ids)
-                extra = ()
-                if op == "diff":
-                    sa, so, _ = gather_docs(sv_arena, sv_off, np.arange(n + 1, dtype=np.uint32), ids)
-                    extra = (sa, so)
-                # engine state is per thread: initialise this thread's device before the call
-                eng = self._engine(i)
-                if hasattr(eng, "lib"):
-                    eng.lib.ym_init(self.devices[i])
-                oa, oo, ol, st = eng.run_host(op, fmt, a, o, d, *extra)
-                results[i] = [int(st[j]) if st[j] else oa[int(oo[j]):int(oo[j]) + int(ol[j])].tobytes()
-                              for j in range(len(ids))]
-            except Exception as e:  # re-raised on the caller's thread
-                errors.append(e)
+            ids = shards[i]
+            a, o, d = gather_docs(arena, upd_off, doc_upd, ids)
+            extra = ()
+            if op == "diff":
+                sa, so, _ = gather_docs(sv_arena, sv_off, np.arange(n + 1, dtype=np.uint32), ids)
+                extra = (sa, so)
+            eng = self._engine(i)
+            oa, oo, ol, st = eng.run_host(op, fmt, a, o, d, *extra)
+            return [int(st[j]) if st[j] else oa[int(oo[j]):int(oo[j]) + int(ol[j])].tobytes()
+                    for j in range(len(ids))]
 
-        threads = [threading.Thread(target=work, args=(i,)) for i in range(G) if len(shards[i])]
-        for t in threads:
-            t.start()
-        for t in threads:
-            t.join()
-        if errors:
-            raise errors[0]
-        return scatter_results(n, shards, [r if r is not None else [] for r in results])
+        futs = {i: self._pools[i].submit(work, i) for i in range(G) if len(shards[i])}
+        results = [[] for _ in range(G)]
+        err = None
+        for i, f in futs.items():  # wait for every shard before raising (re-raised on the caller's thread)
+            try:
+                results[i] = f.result()
+            except Exception as e:
+                err = err or e
+        if err is not None:
+            raise err
+        return scatter_results(n, shards, results)
+
+    def close(self):
+        """Releases each device's library state on the worker thread that created it, then the threads."""
+        if self._pools is None:
+            return
+
+        def release(i):
+            eng = self._engines[i]
+            if eng is not None and hasattr(eng, "lib"):
+                eng.lib.ym_shutdown()
+            self._engines[i] = None
+
+        for i, p in enumerate(self._pools):
+            p.submit(release, i).result()
+            p.shutdown(wait=True)
+        self._pools = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
