@@ -33,18 +33,24 @@ def test_golden_batched_on_gpu(engine, key):
     _check_group(engine, key)
 
 
+@pytest.mark.parametrize("ms", ["", "2"], ids=["stitch", "ms-stitch"])
 @pytest.mark.parametrize("key", [("diff", 1), ("sv", 1), ("meta", 1), ("diff", 2), ("sv", 2), ("meta", 2)],
                          ids=lambda k: f"{k[0]}-v{k[1]}")
-def test_golden_through_chunked_walk(engine, key, monkeypatch):
-    """The chunk-parallel V1 walk (ym_pwalk.hip) and the column-parallel V2 path (ym_pv2.hip) normally
-    take updates of >= 32 KB only; with their threshold at 1 byte every golden diff / state-vector / meta vector
-    goes through them (fallback to the sequential walkers on a decline) and must still come out
-    byte-identical."""
+def test_golden_through_chunked_walk(engine, key, ms, monkeypatch):
+    """The chunk-parallel V1 walk (ym_pwalk.hip) and the column-parallel V2 paths (ym_pv2.hip single section,
+    ym_pv2ms.hip several sections) normally take updates of >= 32 KB only; with their threshold at 1 byte every
+    golden diff / state-vector / meta vector goes through them (fallback to the sequential walkers on a decline)
+    and must still come out byte-identical.  ms-stitch: the V1 documents of >= 2 sections through the
+    section-parallel stitch (k_pw_ms, off by default)."""
+    if ms and key[1] == 2:
+        pytest.skip("the section-parallel stitch is V1 only")
     monkeypatch.setenv("YMERGE_PW_MIN", "1")
+    if ms:
+        monkeypatch.setenv("YMERGE_PWMS_MIN", ms)
     _check_group(engine, key)
     if key[1] == 1:  # the V1 walk accepts exactly what the sequential walker accepts
         assert engine.stats["docs_chunked"] == engine.stats["docs_fast"] > 0, engine.stats
-    else:  # the V2 path: single-section String / Deleted / GC updates
+    else:  # the V2 paths (one section: String / Deleted / GC; several: XML / format / any content too)
         assert engine.stats["docs_chunked"] > 0, engine.stats
 
 

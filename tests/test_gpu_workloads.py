@@ -225,6 +225,8 @@ def test_c5_sv_and_diff_many_clients(engine, fmt):
     bad = _compare(engine.run_host("diff", fmt, a3, o3, d3, sva, svo), outs2, st2)
     assert not bad, bad[:10]
     assert engine.stats["docs_fast"] == engine.stats["docs"], engine.stats
+    if fmt == 2:  # the multi-section column path (ym_pv2ms.hip) takes every merged C5 document
+        assert engine.stats["docs_chunked"] == engine.stats["docs"], engine.stats
 
 
 def test_state_does_not_leak_between_calls(engine):

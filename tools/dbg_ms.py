@@ -38,23 +38,29 @@ def compare(res, outs, st):
 
 
 os.environ["YMERGE_PW_MIN"] = "1"
+os.environ["YMERGE_PWMS_MIN"] = "2"
 cases = golden_io.load_cases()
-for op in ("diff", "sv", "meta"):
-    cs = [c for c in cases if c["op"] == op and c["fmt"] == 2]
+for op, fmt in [(o, f) for f in (1, 2) for o in ("diff", "sv", "meta")]:
+    cs = [c for c in cases if c["op"] == op and c["fmt"] == fmt]
     a, o, d = pack_docs([[c["inputs"][0]] for c in cs])
     extra = ()
     if op == "diff":
         sva, svo, _ = pack_docs([[c["sv"]] for c in cs])
         extra = (sva, svo)
-    res = eng.run_host(op, 2, a, o, d, *extra)
-    w = why(len(cs))
-    outs, st, _ = O.batch(op, 2, a, o, d, *extra)
+    res = eng.run_host(op, fmt, a, o, d, *extra)
+    if fmt == 2:
+        w = why(len(cs))
+    else:
+        w = np.zeros(len(cs), np.uint8)
+        eng.lib.ym__pw_reasons(w.ctypes.data_as(ctypes.c_void_p), ctypes.c_uint32(len(cs)))
+    outs, st, _ = O.batch(op, fmt, a, o, d, *extra)
     bad = compare(res, outs, st)
-    print(f"golden {op} v2: {len(cs)} cases, chunked {eng.stats['docs_chunked']}, why {dict(collections.Counter(w.tolist()))}")
+    print(f"golden {op} v{fmt}: {len(cs)} cases, chunked {eng.stats['docs_chunked']}, why {dict(collections.Counter(w.tolist()))}")
     for b in bad[:10]:
         print("   BAD", b, cs[b[0]]["id"], "why", int(w[b[0]]))
     sys.stdout.flush()
 del os.environ["YMERGE_PW_MIN"]
+del os.environ["YMERGE_PWMS_MIN"]
 
 arena, upd_off, doc_upd = load_ymb("c5_v2")
 merged, status, _ = O.batch("merge", 2, arena, upd_off, doc_upd, nthreads=8)

@@ -617,7 +617,7 @@ static void release_state(DevState *S) {
   for (int k = 0; k < 4; k++) if (S->large.p[k]) hipFree(S->large.p[k]);
   if (S->large.pinned) hipHostFree(S->large.pinned);
   for (PwBufs *pb : {&S->pw, &S->pw2}) {
-    for (int k = 0; k < 4; k++) if (pb->p[k]) hipFree(pb->p[k]);
+    for (int k = 0; k < PW_NBUF; k++) if (pb->p[k]) hipFree(pb->p[k]);
     if (pb->pinned) hipHostFree(pb->pinned);
   }
   if (S->stream) hipStreamDestroy(S->stream);

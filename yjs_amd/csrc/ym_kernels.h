@@ -73,9 +73,10 @@ struct LargeBufs {
 int large_run(const GeneralJob &j, const uint32_t *list, uint32_t n, hipStream_t st, LargeBufs &B);
 
 // device buffers of the chunk-parallel V1 walk (ym_pwalk.hip), grown on demand, cached
+constexpr int PW_NBUF = 5;
 struct PwBufs {
-  void *p[4] = {nullptr, nullptr, nullptr, nullptr};
-  size_t cap[4] = {0, 0, 0, 0};
+  void *p[PW_NBUF] = {};
+  size_t cap[PW_NBUF] = {};
   uint32_t *pinned = nullptr;
 };
 // Chunk-parallel walk + stitch over the large single-update documents of a V1 diff / sv call; sets

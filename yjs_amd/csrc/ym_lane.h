@@ -210,7 +210,13 @@ __device__ __forceinline__ bool key_eq(const uint8_t *b, uint32_t p, uint32_t q,
     if (b[p + i] != b[q + i]) return false;
   return true;
 }
+__device__ __noinline__ void any_nested(LCur &c);
 __device__ __forceinline__ void any_canon(LCur &c) {
+  const uint32_t tag = (uint32_t)c.lo & 0xffu;
+  if (tag == 116 || tag == 117 || tag == 118 || tag == 122) any_nested(c);  // (kept out of line: its key tables)
+  else any_scalar(c);
+}
+__device__ __noinline__ void any_nested(LCur &c) {
   uint32_t rem[AC_DEPTH];   // values left in each open array / object
   uint32_t obj[AC_DEPTH];   // 1 + first key slot of an open object, 0 for an array
   uint32_t kp[AC_KEYS], kl[AC_KEYS];

@@ -28,7 +28,7 @@ __host__ __device__ constexpr uint32_t col_of(uint32_t k) {  // V2 column order:
 __host__ __device__ constexpr bool k_rle(uint32_t k) { return k == K_INFO || k == K_PI; }              // RleDecoder<u8>
 __host__ __device__ constexpr bool k_dif(uint32_t k) { return k == K_LC || k == K_RC || k == K_KC; }   // IntDiffOptRle
 constexpr uint32_t HB = 64;      // encoded head bytes per (document, column)
-constexpr uint32_t CKSTEP = 64;  // column entries per checkpoint (K3 starts its decode at the last one)
+constexpr uint32_t CKSTEP = 16;  // column entries per checkpoint (K3 starts its decode at the last one)
 
 // per-document state, in HBM
 struct Meta {

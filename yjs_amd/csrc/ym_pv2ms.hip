@@ -41,6 +41,11 @@
 namespace ymk {
 namespace pv2 {
 
+// debugging aid (ym__ms_prof): [0] rest-walk ticks (100 MHz), [1] info entries, [2] len entries, [3] rest
+// items on the fast path, [4] rest items parsed by the cursor, [5] window loads, [6] global re-reads
+__device__ unsigned long long ms_prof[8];
+#define MSP(i, v) do { if (threadIdx.x == 0) atomicAdd(&ms_prof[i], (unsigned long long)(v)); } while (0)
+
 // ---- MR: the rest walk ---------------------------------------------------------------------------------
 // UintOptRleDecoder over the len column: the next value / skip t values, run by run
 __device__ __forceinline__ uint32_t uopt_next(ln::LCur &c, uint32_t &v, uint32_t &rem, bool &bad) {
@@ -69,11 +74,43 @@ __device__ __forceinline__ void uopt_skipn(ln::LCur &c, uint32_t &v, uint32_t &r
   }
 }
 
+// The walk is sequential, so its cost is the latency of each dependent read: the three streams (info
+// column, len column, rest stream) are read through LDS windows that the wave refills with 16-byte loads
+// (one refill per window, instead of one dependent HBM load per 8 bytes consumed); a value that does not
+// fit in the rest of a window is re-read from global memory.
+constexpr uint32_t WI = 1024, WL = 1024, WR = 4096, MRG = 1024;  // window bytes; rest margin per item
+struct Win {
+  uint32_t base, lim, end;  // LDS holds stream bytes [base, lim); the stream ends at end
+};
+// makes [pos, pos + need) resident (or up to the stream end); the whole wave calls it.  (The buffer is
+// passed as the __shared__ array itself, so its reads are LDS reads: generic-pointer loads would also wait
+// for the walk's outstanding global stores.)
+template <uint32_t N>
+__device__ __forceinline__ void win_at(Win &w, uint8_t (&buf)[N], const uint8_t *D, uint32_t pos, uint32_t need, uint32_t W) {
+  if (pos >= w.base && (pos + need <= w.lim || w.lim >= w.end)) return;
+  const uint32_t b = pos & ~15u;
+  const uint32_t l = b + W < w.end ? b + W : w.end;
+  MSP(5, 1);
+  __syncthreads();
+  for (uint32_t q = threadIdx.x * 16; q < l - b; q += 64 * 16) {
+    uint8_t t[16];
+    const uint4 v = wds::load16m(D, b + q, w.end);  // (bytes past the end read as 0x80)
+    __builtin_memcpy(t, &v, 16);
+    __builtin_memcpy(buf + q, t, 16);
+  }
+  __syncthreads();
+  w.base = b;
+  w.lim = l;
+}
+// a cursor over the window at pos (reads stop at the window's end: a value crossing it sets bad)
+__device__ __forceinline__ ln::LCur win_cur(const Win &w, const uint8_t *buf, uint32_t pos) { return ln::make(buf, pos - w.base, w.lim - w.base); }
+
 __global__ void __launch_bounds__(64) k_ms_rest(Job J) {
   const GeneralJob &j = J.j;
   const uint32_t d = blockIdx.x;
   Meta &M = J.meta[d];
   if (!M.ok || !M.ms) return;
+  __shared__ __attribute__((aligned(16))) uint8_t bi[WI + 32], bl[WL + 32], br[WR + 32];
   const uint32_t u0 = j.doc_upd[d];
   const uint64_t ub = j.upd_off[u0];
   const uint32_t len = (uint32_t)(j.upd_off[u0 + 1] - ub);
@@ -82,60 +119,135 @@ __global__ void __launch_bounds__(64) k_ms_rest(Job J) {
   uint32_t *ist = a_istart(J, M);
   const uint32_t icap = len - M.r0 + 1;
   const bool w = threadIdx.x == 0;
-  ln::LCur ci = ln::make(D, M.col0[4], M.col1[4]);  // info column (RleDecoder<u8>)
-  uint32_t iv = 0, irem = 0;                          // run value, values left (NONE: the endless final run)
-  ln::LCur cl = ln::make(D, M.col0[8], M.col1[8]);  // len column
-  uint32_t lv = 0, lrem = 0;
-  ln::LCur cr = ln::make(D, M.r0, len);              // rest stream
+  Win wi{1, 0, M.col1[4]}, wl{1, 0, M.col1[8]}, wr{1, 0, len};
+  uint32_t ip = M.col0[4], lp = M.col0[8], rp = M.r0;  // stream positions (update-relative)
+  uint32_t iv = 0, irem = 0;  // info run value, values left (NONE: the endless final run)
+  uint32_t lv = 0, lrem = 0;  // len run
   uint32_t i = 0, iord = 0;
   bool bad = false;
+  const uint64_t tm0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t n_ie = 0, n_le = 0, n_rf = 0, n_rs = 0, n_g = 0;
+  // the next len value (UintOptRleDecoder), or skip t of them
+  auto ln_take = [&](uint32_t t) -> uint32_t {
+    uint32_t v = 0;
+    while (t > 0 && !bad) {
+      if (lrem == 0) {
+        if (lp >= wl.end) { bad = true; break; }
+        win_at(wl, bl, D, lp, 16, WL);
+        n_le++;
+        const uint32_t b0 = bl[lp - wl.base], b1 = bl[lp - wl.base + 1];
+        if (b0 < 0x40 && lp + 1 <= wl.end) {  // one-byte value, count 1 (the common entry)
+          lv = b0;
+          lrem = 1;
+          lp += 1;
+        } else if (b0 < 0x80 && b1 < 0x80 && lp + 2 <= wl.end) {  // a run: -value (-0 too), count - 2
+          lv = b0 & 63;
+          lrem = b1 + 2;
+          lp += 2;
+        } else {
+          ln::LCur c = win_cur(wl, bl, lp);
+          bool neg;
+          lv = rvi(c, neg);
+          lrem = neg ? ln::rvu(c) + 2 : 1;
+          bad |= c.bad || lrem == 0;
+          lp = wl.base + c.p;
+        }
+      }
+      const uint32_t k = lrem < t ? lrem : t;
+      lrem -= k;
+      t -= k;
+      v = lv;
+    }
+    return v;
+  };
+  // one rest-stream item of kind k (0: section header, 1: Skip length, 2: varUint8Array, 3: one `any`) on
+  // the window, or again on global memory when it crosses the window's end; a / b: the header's values
+  uint32_t ha = 0, hb = 0;
+  auto parse = [&](ln::LCur &c, uint32_t k) {
+    if (k == 0) { ha = ln::rvu(c); hb = ln::rvu(c); }
+    else if (k == 1) c.bad |= ln::rvu(c) == 0;
+    else if (k == 2) { const uint32_t nb = ln::rvu(c); if (c.bad || !ln::room(c, nb)) c.bad = true; else ln::skip(c, nb); }
+    else ln::any_canon(c);
+  };
+  auto rest_item = [&](uint32_t k) {
+    win_at(wr, br, D, rp, MRG, WR);
+    // the common cases straight from the window: one-byte header values / lengths; `any` true / false /
+    // null / undefined and short ASCII strings (lib0 writes those canonically by construction)
+    const uint32_t qo = rp - wr.base;
+    const uint32_t t0 = br[qo], t1 = br[qo + 1];
+    if (rp + 2 <= wr.lim) {
+      if (k == 0 && t0 < 0x80 && t1 < 0x80) { ha = t0; hb = t1; rp += 2; n_rf++; return; }
+      if (k == 1 && t0 < 0x80 && t0 != 0) { rp += 1; n_rf++; return; }
+      if (k == 3 && (t0 == 120 || t0 == 121 || t0 == 126 || t0 == 127)) { rp += 1; n_rf++; return; }
+      if (k == 3 && t0 == 119 && t1 < 0x80 && rp + 2 + t1 <= wr.lim) {
+        uint32_t hi = 0;
+        for (uint32_t a = 0; a < t1; a++) hi |= br[qo + 2 + a];
+        if (hi < 0x80) { rp += 2 + t1; n_rf++; return; }
+      }
+    }
+    n_rs++;
+    ln::LCur c = win_cur(wr, br, rp);
+    parse(c, k);
+    if (!c.bad) { rp = wr.base + c.p; return; }
+    if (wr.lim >= wr.end) { bad = true; return; }
+    n_g++;
+    ln::LCur g = ln::make(D, rp, len);
+    parse(g, k);
+    bad |= g.bad;
+    rp = g.p;
+  };
   for (uint32_t s = 0; s < M.nsec && !bad; s++) {
-    const uint32_t W = ln::rvu(cr);
-    const uint32_t clock = ln::rvu(cr);
-    bad |= cr.bad || W == 0 || W > (1u << 26);  // (an empty section still consumes a client value: declined)
+    rest_item(0);
+    const uint32_t W = ha, clock = hb;
+    bad |= W == 0 || W > (1u << 26);  // (an empty section still consumes a client value: declined)
     if (w) {
       S[s].S = i;
       S[s].W = W;
       S[s].clock = clock;
-      S[s].pay0 = cr.p;
+      S[s].pay0 = rp;
       S[s].ibase = iord;
     }
     uint32_t rem = bad ? 0 : W;
     while (rem > 0 && !bad) {
       if (irem == 0) {
-        if (ci.p >= ci.e) { bad = true; break; }
-        iv = ln::rdb(ci);
-        if (ci.p >= ci.e) irem = NONE;
-        else { irem = ln::rvu(ci) + 1; bad |= ci.bad || irem == 0; }
+        if (ip >= wi.end) { bad = true; break; }
+        win_at(wi, bi, D, ip, 16, WI);
+        n_ie++;
+        const uint32_t b1 = bi[ip - wi.base + 1];
+        iv = bi[ip - wi.base];
+        if (ip + 1 >= wi.end) {  // the final run never ends
+          irem = NONE;
+          ip += 1;
+        } else if (b1 < 0x80 && ip + 2 <= wi.end) {  // one-byte count (the common entry)
+          irem = b1 + 1;
+          ip += 2;
+        } else {
+          ln::LCur c = win_cur(wi, bi, ip + 1);
+          irem = ln::rvu(c) + 1;
+          bad |= c.bad || irem == 0;
+          ip = wi.base + c.p;
+        }
       }
       const uint32_t t = irem < rem ? irem : rem;
       const uint32_t ref = iv & 31;
       if (iv == 10 || ref == 3 || ref == 5 || ref == 6 || ref == 8) {  // payloads, struct by struct
         for (uint32_t q = 0; q < t && !bad; q++) {
           if (iord >= icap) { bad = true; break; }
-          if (w) ist[iord] = cr.p;
+          if (w) ist[iord] = rp;
           iord++;
-          if (iv == 10) {                       // Skip: vu(length)
-            bad |= ln::rvu(cr) == 0;
-          } else if (ref == 3) {                // ContentBinary: varUint8Array
-            const uint32_t nb = ln::rvu(cr);
-            if (cr.bad || !ln::room(cr, nb)) bad = true;
-            else ln::skip(cr, nb);
-          } else if (ref == 8) {                // ContentAny: len column, then that many values
-            const uint32_t cnt = uopt_next(cl, lv, lrem, bad);
-            bad |= cnt == 0;
-            for (uint32_t a = 0; a < cnt && !cr.bad && !bad; a++) ln::any_canon(cr);
-          } else {                              // ContentEmbed / ContentFormat: writeJSON = writeAny
-            ln::any_canon(cr);
-          }
-          bad |= cr.bad;
+          // Skip: vu(length); ContentBinary: varUint8Array; ContentAny: len column, then that many values;
+          // ContentEmbed / ContentFormat: writeJSON = writeAny
+          const uint32_t cnt = ref == 8 ? ln_take(1) : 1;
+          bad |= cnt == 0;
+          const uint32_t k = iv == 10 ? 1 : ref == 3 ? 2 : 3;
+          for (uint32_t a = 0; a < cnt && !bad; a++) rest_item(k);
         }
-      } else if (ref == 0) {                    // GC (info exactly 0, as GC.write writes it): len column
+      } else if (ref == 0) {                      // GC (info exactly 0, as GC.write writes it): len column
         bad |= iv != 0;
-        uopt_skipn(cl, lv, lrem, t, bad);
-      } else if (ref == 1) {                    // ContentDeleted: len column
-        uopt_skipn(cl, lv, lrem, t, bad);
-      } else if (ref != 4 && ref != 7) {        // (String / Type: columns only) JSON, Doc, invalid refs
+        ln_take(t);
+      } else if (ref == 1) {                      // ContentDeleted: len column
+        ln_take(t);
+      } else if (ref != 4 && ref != 7) {          // (String / Type: columns only) JSON, Doc, invalid refs
         bad = true;
       }
       i += t;
@@ -143,15 +255,16 @@ __global__ void __launch_bounds__(64) k_ms_rest(Job J) {
       if (irem != NONE) irem -= t;
       bad |= i > (1u << 26);
     }
-    if (w) S[s].pay1 = cr.p;
+    if (w) S[s].pay1 = rp;
   }
-  bad |= cr.bad;
   if (w) {
     M.n = i;
     M.nitem = iord;
-    M.ds0 = cr.p;
+    M.ds0 = rp;
     if (bad) { M.ok = 0; M.why = 50; }
   }
+  MSP(0, __builtin_amdgcn_s_memrealtime() - tm0);
+  MSP(1, n_ie); MSP(2, n_le); MSP(3, n_rf); MSP(4, n_rs); MSP(6, n_g);
 }
 
 __global__ void k_ms_sizes_k(Job J, uint64_t *sizes) {
@@ -167,12 +280,13 @@ __global__ void k_ms_sizes_k(Job J, uint64_t *sizes) {
 // ---- K2: struct passes ----------------------------------------------------------------------------------
 constexpr uint32_t SVMAX = 2048, SVSLOTS = 4096;  // state-vector entries / LDS hash slots
 __device__ __forceinline__ uint32_t sv_hash(uint32_t c) { return (c * 0x9E3779B1u) >> 20; }
-// the section holding struct i (sections are contiguous, non-empty, in struct order)
-__device__ __forceinline__ uint32_t sec_of(const Sec *S, uint32_t nsec, uint32_t i) {
+constexpr uint32_t MSEC = 4096;  // sections a document may have on this path (their starts sit in LDS)
+// the section holding struct i (sections are contiguous, non-empty, in struct order; starts in LDS)
+__device__ __forceinline__ uint32_t sec_of(const uint32_t *secS, uint32_t nsec, uint32_t i) {
   uint32_t lo = 0, hi = nsec;
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (S[mid].S <= i) lo = mid; else hi = mid;
+    if (secS[mid] <= i) lo = mid; else hi = mid;
   }
   return lo;
 }
@@ -195,6 +309,7 @@ __global__ void __launch_bounds__(KT) k_ms_struct(Job J) {
   __shared__ uint32_t s_bad;
   __shared__ uint32_t mkey[OP == OP_DIFF ? SVSLOTS : 1], mval[OP == OP_DIFF ? SVSLOTS : 1];
   __shared__ uint32_t svclk[OP == OP_DIFF ? SVMAX : 1];
+  __shared__ uint32_t secS[MSEC + 1];  // each section's first struct (sec_of)
   const uint32_t u0 = j.doc_upd[d];
   const uint64_t ub = j.upd_off[u0];
   const uint32_t len = (uint32_t)(j.upd_off[u0 + 1] - ub);
@@ -218,11 +333,13 @@ __global__ void __launch_bounds__(KT) k_ms_struct(Job J) {
     }
     if (__syncthreads_or(na)) MS_DECLINE(21)
   }
-  if (M.nval[K_CL] == 0) MS_DECLINE(22)
+  if (M.nval[K_CL] == 0 || nsec > MSEC) MS_DECLINE(22)
   for (uint32_t s = t; s < nsec; s += KT) {
     S[s].skipk = ~0ull;
     S[s].f = NONE;
+    secS[s] = S[s].S;
   }
+  if (t == 0) secS[nsec] = NONE;
   // decodeStateVector (encoding.js:536-545): a later entry for a client wins
   if (OP == OP_DIFF) {
     for (uint32_t q = t; q < SVSLOTS; q += KT) mval[q] = 0;
@@ -256,7 +373,7 @@ __global__ void __launch_bounds__(KT) k_ms_struct(Job J) {
     clock = 0;
     for (uint32_t t0 = 0; t0 < n; t0 += TILE) {
       const uint32_t i0 = t0 + t * PER;
-      uint32_t s = sec_of(S, nsec, i0 < n ? i0 : n - 1);
+      uint32_t s = sec_of(secS, nsec, i0 < n ? i0 : n - 1);
       uint32_t vv[PER], pv[PER], tv[PER], sec[PER];
       bool st[PER];
       uint32_t cons[PER][NX];
@@ -266,9 +383,9 @@ __global__ void __launch_bounds__(KT) k_ms_struct(Job J) {
       for (uint32_t e = 0; e < PER; e++) {
         const uint32_t i = i0 + e;
         const bool valid = i < n;
-        while (valid && s + 1 < nsec && S[s + 1].S <= i) s++;
+        while (valid && secS[s + 1] <= i) s++;
         sec[e] = s;
-        st[e] = valid && S[s].S == i;
+        st[e] = valid && secS[s] == i;
         const uint32_t v = valid ? info_a[i] : 0;
         vv[e] = v;
         const uint32_t ref = v & 31;
@@ -922,13 +1039,22 @@ __global__ void __launch_bounds__(64) k_ms_out(Job J) {
       }
       if (c == 5) {  // varString(body) | lengths
         p = put(p, sbn);
-        for (uint32_t s = 0; s < nsec; s++) {
-          const Sec &X = S[s];
-          if (X.f == NONE) continue;
-          const uint32_t ref = X.info_f & 31;
-          const uint32_t hs0 = X.off == 0 ? X.body_f : ref == 4 ? X.body_fc + X.off : X.body_f1;
-          const uint32_t be = s + 1 < nsec ? S[s + 1].body0 : M.body_end;
-          wcopy(o + p + X.ob, D + M.sb0 + hs0, be - hs0);
+        for (uint32_t s0 = 0; s0 < nsec; s0 += 64) {  // each lane loads one section's piece, the wave copies them
+          const uint32_t s = s0 + lane;
+          uint32_t src = 0, dst = 0, n = 0;
+          if (s < nsec && S[s].f != NONE) {
+            const Sec &X = S[s];
+            const uint32_t ref = X.info_f & 31;
+            const uint32_t hs0 = X.off == 0 ? X.body_f : ref == 4 ? X.body_fc + X.off : X.body_f1;
+            const uint32_t be = s + 1 < nsec ? S[s + 1].body0 : M.body_end;
+            src = M.sb0 + hs0;
+            dst = X.ob;
+            n = be - hs0;
+          }
+          for (uint64_t m = __ballot(n > 0); m; m &= m - 1) {
+            const int l = __builtin_ctzll(m);
+            wcopy(o + p + lane_read(dst, l), D + lane_read(src, l), lane_read(n, l));
+          }
         }
         p += sbn;
         wcopy(o + p, a_col(J, M, K_SL), M.osz[K_SL]);
@@ -941,13 +1067,24 @@ __global__ void __launch_bounds__(64) k_ms_out(Job J) {
       p += cl[c];
     }
     p = put(p, nk);
-    for (uint32_t s = 0; s < nsec; s++) {
-      const Sec &X = S[s];
-      if (X.f == NONE) continue;
-      uint32_t q = p + X.orr;
-      q = put(q, X.W - (X.f - X.S));
-      q = put(q, X.fclock + X.off);
-      wcopy(o + q, D + X.rs, X.pay1 - X.rs);
+    for (uint32_t s0 = 0; s0 < nsec; s0 += 64) {  // each lane writes its section's header, the wave copies the payloads
+      const uint32_t s = s0 + lane;
+      uint32_t src = 0, dst = 0, n = 0;
+      bool kept = false;
+      if (s < nsec && S[s].f != NONE) {
+        const Sec &X = S[s];
+        kept = true;
+        uint32_t q = put_vu_g(o, p + X.orr, X.W - (X.f - X.S));
+        q = put_vu_g(o, q, X.fclock + X.off);
+        src = X.rs;
+        dst = q;
+        n = X.pay1 - X.rs;
+      }
+      (void)kept;
+      for (uint64_t m = __ballot(n > 0); m; m &= m - 1) {
+        const int l = __builtin_ctzll(m);
+        wcopy(o + lane_read(dst, l), D + lane_read(src, l), lane_read(n, l));
+      }
     }
     p += rsz;
     wcopy(o + p, D + M.ds0, ds1 - M.ds0);
@@ -978,3 +1115,9 @@ void ms_run(uint32_t op, const Job &J, hipStream_t st) {
 
 }  // namespace pv2
 }  // namespace ymk
+
+extern "C" int ym__ms_prof(unsigned long long *host, int reset) {
+  int r = (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ymk::pv2::ms_prof), 64);
+  if (reset) { unsigned long long z[8] = {}; hipMemcpyToSymbol(HIP_SYMBOL(ymk::pv2::ms_prof), z, 64); }
+  return r;
+}

@@ -91,19 +91,28 @@ __device__ unsigned long long pw_prof[8];
 // stores left partial lines that cost a read-modify-write each).
 __device__ __forceinline__ uint64_t rec_idx(uint32_t g, uint32_t k) { return ((uint64_t)(g >> 6) * CAP + k) * 64 + (g & 63); }
 // ---- 0. eligibility and chunk counts ---------------------------------------------------------------
-__global__ void k_pw_prep(GeneralJob j, uint32_t *cnt, uint8_t *done, uint64_t pw_min) {
+// msz[d]: the section-parallel stitch's per-document area (k_pw_ms), for documents of >= ms_min sections
+__host__ __device__ inline uint64_t ms_area(uint32_t nsec);
+__global__ void k_pw_prep(GeneralJob j, uint32_t *cnt, uint8_t *done, uint64_t pw_min, uint64_t *msz, uint32_t ms_min) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d > j.n) return;
   uint32_t c = 0;
+  uint64_t a = 0;
   if (d < j.n) {
     done[d] = 0;
     const uint32_t u0 = j.doc_upd[d];
     if (j.doc_upd[d + 1] - u0 == 1) {
       const uint64_t len = j.upd_off[u0 + 1] - j.upd_off[u0];
-      if (len >= pw_min && len > 0 && len < (1ull << 28)) c = (uint32_t)((len + CH - 1) / CH);
+      if (len >= pw_min && len > 0 && len < (1ull << 28)) {
+        c = (uint32_t)((len + CH - 1) / CH);
+        ln::LCur h = ln::make(j.A + j.upd_off[u0], 0, (uint32_t)len);
+        const uint32_t nsec = ln::rvu(h);
+        if (!h.bad && nsec >= ms_min && nsec <= (1u << 16)) a = ms_area(nsec);
+      }
     }
   }
   cnt[d] = c;  // cnt[n] = 0: the exclusive scan's last entry is the total
+  msz[d] = a;
 }
 
 // ---- 1. speculative chunk walk ----------------------------------------------------------------------
@@ -197,9 +206,9 @@ __device__ __forceinline__ bool seen_before(const uint32_t *dsc, uint32_t n, uin
   return hit;
 }
 typedef uint4 __attribute__((aligned(1))) u4u;
-__device__ __forceinline__ void copy_bytes(uint8_t *dst, const uint8_t *src, uint32_t n) {
+__device__ __forceinline__ void copy_bytes(uint8_t *dst, const uint8_t *src, uint32_t n) {  // (one wave)
   const uint32_t nv = n >> 4;
-  uint32_t v = threadIdx.x;
+  uint32_t v = threadIdx.x & 63;
   for (; v + 192 < nv; v += 256) {  // four 16-byte loads in flight per lane
     const uint4 a = reinterpret_cast<const u4u *>(src)[v], b = reinterpret_cast<const u4u *>(src)[v + 64];
     const uint4 c = reinterpret_cast<const u4u *>(src)[v + 128], e = reinterpret_cast<const u4u *>(src)[v + 192];
@@ -209,7 +218,7 @@ __device__ __forceinline__ void copy_bytes(uint8_t *dst, const uint8_t *src, uin
     reinterpret_cast<u4u *>(dst)[v + 192] = e;
   }
   for (; v < nv; v += 64) reinterpret_cast<u4u *>(dst)[v] = reinterpret_cast<const u4u *>(src)[v];
-  for (uint32_t i = (nv << 4) + threadIdx.x; i < n; i += 64) dst[i] = src[i];
+  for (uint32_t i = (nv << 4) + (threadIdx.x & 63); i < n; i += 64) dst[i] = src[i];
 }
 __device__ __forceinline__ uint32_t put_vu_g(uint8_t *o, uint32_t p, uint32_t v) {
   while (v > 127) { o[p++] = (uint8_t)(0x80 | (v & 127)); v >>= 7; }
@@ -222,7 +231,7 @@ __device__ __forceinline__ uint32_t put_vu_g(uint8_t *o, uint32_t p, uint32_t v)
 // content kind cannot be sliced here, a split surrogate pair, a head longer than PRE).
 __device__ bool slice_head(sc::cu32 *B, uint32_t adj, uint32_t s0, uint32_t s1, uint32_t client, uint64_t clock,
                            uint32_t len, uint32_t off, uint8_t *pre, uint32_t &prelen, uint32_t &a0, uint32_t &a1) {
-  const uint32_t lane = threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63;
   const uint32_t info = sc::byte(B, s0 + adj);
   const bool gc = (info & 31) == 0;
   uint8_t h[PRE + 16];
@@ -295,12 +304,12 @@ __device__ bool slice_head(sc::cu32 *B, uint32_t adj, uint32_t s0, uint32_t s1, 
 // OP = OP_DIFF, OP_SV or OP_META (parseUpdateMeta: from = a section's first clock, to = its end clock)
 template <int OP>
 __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *cbase, const uint4 *desc, const uint2 *recs,
-                                                  uint8_t *done) {
+                                                  uint8_t *done, const uint64_t *msz) {
   const uint32_t lane = threadIdx.x;
   const Scr X = scratch(j);
   for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
     const uint32_t cb = cbase[d], nch = cbase[d + 1] - cb;
-    if (nch == 0) continue;
+    if (nch == 0 || msz[d]) continue;  // (many sections: k_pw_ms)
     const uint32_t u0 = j.doc_upd[d];
     const uint64_t ub = j.upd_off[u0];
     const uint32_t len = (uint32_t)(j.upd_off[u0 + 1] - ub);
@@ -716,6 +725,561 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
   }
 }
 
+
+// ---- 3. multi-section documents, section-parallel (configs[4] C5: ~1,000 client sections) -------------
+// k_pw_stitch follows the chain one section after the other with one wave: a C5 document's ~1,000
+// sections cost ~10 dependent global loads each (header, state vector, descriptors, records, the cut),
+// ~28 ms per call although the whole chip is idle.  Here one 512-thread block per document:
+//   A  wave 0 walks only the section headers: from a section's first struct it skips its #structs
+//      along the walk's records (one descriptor lookup and one 64-record load per chunk), so each section
+//      costs ~3 dependent loads; the state vector goes into an LDS hash map meanwhile (wave 1).
+//   B  the eight waves take the sections round-robin: clocks, the cut, the sliced head, info-byte patches
+//      -- the stitch's per-section work, now eight (and across documents, 8 x 256) sections at a time.
+//   C  sizes by a block scan over the sections, then every wave writes its sections' pieces in place.
+//
+// Measured (C5 V1, 256 documents, tools/prof_c5.py): correct, but not faster than k_pw_stitch -- phase A alone
+// costs ~20 us per section (the records of one chunk are interleaved with 63 others for the walk's stores,
+// so a 64-record read touches 64 cache lines, and the first structs after a header are off the walk's chain
+// and parsed here), so the path is off by default (YMERGE_PWMS_MIN=<sections> turns it on; the golden
+// vectors run through it in tests/test_gpu_golden.py).
+constexpr uint32_t MS_WAVES = 8, MS_T = 64 * MS_WAVES;
+constexpr uint32_t MS_MIN = 0xffffffffu;  // sections from which a document takes this path (YMERGE_PWMS_MIN)
+constexpr uint32_t MSPATCH = 4096;     // info-byte patches per document
+constexpr uint32_t MSVMAX = 2048, MSVSLOTS = 4096;
+enum { M_X0 = 0, M_W, M_CLIENT, M_CLOCK, M_X1, M_PRELEN, M_A0, M_A1, M_B0, M_WRITTEN, M_FCLOCK, M_VAL, M_END, M_OUT, NMF = 16 };
+__host__ __device__ inline uint64_t ms_area(uint32_t nsec) { return (((uint64_t)nsec * (4 * NMF + PRE) + 15) & ~15ull) + 9ull * MSPATCH + 256; }
+struct MsDoc {
+  uint32_t *sec;    // [nsec][NMF]
+  uint8_t *pre;     // [nsec][PRE]
+  uint32_t *ppos, *psec;
+  uint8_t *pval;
+};
+__device__ __forceinline__ MsDoc ms_doc(uint8_t *area, uint64_t off, uint32_t nsec) {
+  uint8_t *b = area + off;
+  MsDoc m;
+  m.sec = reinterpret_cast<uint32_t *>(b);
+  m.pre = b + 4ull * NMF * nsec;
+  uint8_t *p = b + (((uint64_t)nsec * (4 * NMF + PRE) + 15) & ~15ull);
+  m.ppos = reinterpret_cast<uint32_t *>(p);
+  m.psec = m.ppos + MSPATCH;
+  m.pval = reinterpret_cast<uint8_t *>(m.psec + MSPATCH);
+  return m;
+}
+#define msec(ci, f) M.sec[NMF * (ci) + (f)]
+
+// one wave's view of the chunk descriptors: 64 chunks [wb, wb + 64) held one per lane
+struct DescWin {
+  uint32_t wb = NONE - 64;
+  uint4 q0, q1, q2, q3, q4;
+};
+__device__ __forceinline__ void desc_at(DescWin &W, const uint4 *desc, uint32_t cb, uint32_t nch, uint32_t cx) {
+  if (cx < W.wb || cx >= W.wb + 64) {
+    W.wb = cx;
+    if (W.wb + threadIdx.x % 64 < nch) {
+      const uint4 *Q = desc + 5ull * (cb + W.wb + threadIdx.x % 64);
+      W.q0 = Q[0]; W.q1 = Q[1]; W.q2 = Q[2]; W.q3 = Q[3]; W.q4 = Q[4];
+    }
+  }
+}
+// the record index of position x in chunk cx (a true struct start), or NONE: the descriptor's first
+// records, then a ballot over the records 64 at a time
+__device__ __forceinline__ uint32_t rec_entry(const DescWin &W, const uint2 *recs, uint32_t gc, uint32_t cx, uint32_t nrec, uint32_t x) {
+  const int di = (int)(cx - W.wb);
+#pragma unroll
+  for (uint32_t kf = 0; kf < NFIRST; kf++) {
+    const uint32_t pwk = lane_read(kf < 4 ? (&W.q1.x)[kf] : (&W.q2.x)[kf - 4], di);
+    if (kf < nrec && (pwk & POS_MASK) == x) return (pwk & F_FAIL) ? NONE : kf;
+  }
+  const uint32_t lane = threadIdx.x % 64;
+  for (uint32_t s = NFIRST; s < nrec; s += 64) {
+    const uint32_t kk = s + lane;
+    const uint32_t pw = kk < nrec ? recs[rec_idx(gc, kk)].x : POS_MASK;
+    const uint64_t lt = __ballot(kk < nrec && (pw & POS_MASK) < x);
+    const uint32_t nlt = __popcll(lt);
+    if (nlt == 64) continue;
+    if (s + nlt >= nrec) return NONE;
+    const uint32_t cand = lane_read(pw, nlt);
+    return (cand & POS_MASK) == x && !(cand & F_FAIL) ? s + nlt : NONE;
+  }
+  return NONE;
+}
+// phase A: the position after `w` structs from x (a true struct start), along the walk's records; a
+// struct the records do not cover (a FAIL under the speculative cap, a chain the walk missed) is parsed
+// here, uncapped.  False: a struct does not parse (the document is declined).
+__device__ bool skip_structs(DescWin &W, const uint4 *desc, const uint2 *recs, uint32_t cb, uint32_t nch, const uint8_t *D,
+                             uint32_t len, uint32_t &x, uint32_t w) {
+  const uint32_t lane = threadIdx.x % 64;
+  while (w > 0) {
+    if (x >= len) return false;
+    const uint32_t cx = x / CH;
+    desc_at(W, desc, cb, nch, cx);
+    const int di = (int)(cx - W.wb);
+    const uint32_t nrec = lane_read(W.q0.x, di) & 0xffffu, cexit = lane_read(W.q0.z, di);
+    const uint32_t gc = cb + cx;
+    const uint32_t fs = rec_entry(W, recs, gc, cx, nrec, x);
+    if (fs == NONE) {  // (after a section header the walk's chain has not resynchronised yet: parse here)
+      uint32_t nx, cl, fl;
+      if (!ln::parse_fast(D, x, len, nx, cl, fl) && !ln::parse_struct(D, x, len, nx, cl, fl)) return false;
+      x = nx;
+      w--;
+      continue;
+    }
+    // records fs .. fs + 63: up to the first FAIL (re-parsed next round) or w structs
+    const uint32_t kk = fs + lane;
+    const uint32_t pw = kk < nrec ? recs[rec_idx(gc, kk)].x : POS_MASK;
+    const uint64_t fm = __ballot(kk < nrec && (pw & F_FAIL));
+    uint32_t n = nrec - fs < 64 ? nrec - fs : 64;
+    if (fm) n = (uint32_t)__builtin_ctzll(fm);
+    if (n == 0) {  // a FAIL at x itself: (rec_entry returns NONE then; kept for safety)
+      uint32_t nx, cl, fl;
+      if (!ln::parse_struct(D, x, len, nx, cl, fl)) return false;
+      x = nx;
+      w--;
+      continue;
+    }
+    if (w < n) n = w;
+    // the position after the n-th struct: the next record's start, or the chunk's exit
+    const uint32_t nxt = lane_read(pw, n < 64 ? n : 63);
+    x = fs + n < nrec ? (n < 64 ? (nxt & POS_MASK) : (recs[rec_idx(gc, fs + n)].x & POS_MASK)) : cexit;
+    w -= n;
+  }
+  return true;
+}
+
+template <int OP>
+__global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, const uint32_t *cbase, const uint4 *desc, const uint2 *recs,
+                                                uint8_t *done, const uint64_t *msz, const uint64_t *moff, uint8_t *area) {
+  const uint32_t t = threadIdx.x, lane = t % 64, wv = t / 64;
+  __shared__ uint32_t mkey[OP == OP_DIFF ? MSVSLOTS : 1], mval[OP == OP_DIFF ? MSVSLOTS : 1], svclk[OP == OP_DIFF ? MSVMAX : 1];
+  __shared__ uint32_t s_bad, s_why, s_nsec, s_ds0, s_npatch, s_sum[MS_WAVES + 1];
+  for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
+    if (msz[d] == 0) continue;
+    const uint32_t cb = cbase[d], nch = cbase[d + 1] - cb;
+    const uint32_t u0 = j.doc_upd[d];
+    const uint64_t ub = j.upd_off[u0];
+    const uint32_t len = (uint32_t)(j.upd_off[u0 + 1] - ub);
+    const uint8_t *D = j.A + ub;
+    sc::cu32 *const B = sc::base_of(D);
+    const uint32_t adj = (uint32_t)(ub & 3);
+    if (t == 0) { s_bad = 0; s_why = 0; s_npatch = 0; }
+    if (OP == OP_DIFF)
+      for (uint32_t q = t; q < MSVSLOTS; q += MS_T) mval[q] = 0;
+    __syncthreads();
+    const uint64_t tm0 = __builtin_amdgcn_s_memrealtime();
+    // ---- A: the section headers (wave 0); the state vector (one lane of wave 1)
+    uint32_t nsec = 0;
+    {
+      ln::LCur c = ln::make(D, 0, len);
+      nsec = ln::rvu(c);
+    }
+    const MsDoc M = ms_doc(area, moff[d], nsec);
+    if (wv == 0) {
+      uint32_t x = 0, why = 0, prev = 0;
+      {
+        ln::LCur c = ln::make(D, 0, len);
+        ln::rvu(c);
+        x = c.p;
+      }
+      DescWin W;
+      for (uint32_t ci = 0; ci < nsec && !why; ci++) {
+        ln::LCur c = ln::make(D, x, len);
+        const uint32_t ns = ln::rvu(c), client = ln::rvu(c), clock = ln::rvu(c);
+        x = c.p;
+        if (c.bad) { why = 5; break; }
+        // each section a new client (the writer merges consecutive parts of one client); meta: descending
+        if (ns == 0 || (ci > 0 && client == prev) || (OP == OP_META && ci > 0 && client > prev)) { why = 6; break; }
+        prev = client;
+        if (lane == 0) { msec(ci, M_X0) = x; msec(ci, M_W) = ns; msec(ci, M_CLIENT) = client; msec(ci, M_CLOCK) = clock; }
+        if (!skip_structs(W, desc, recs, cb, nch, D, len, x, ns)) { why = 8; break; }
+        if (lane == 0) msec(ci, M_X1) = x;
+      }
+      if (lane == 0) { s_ds0 = x; if (why) { s_bad = 1; s_why = why; } }
+    } else if (OP == OP_DIFF && t == 64) {  // decodeStateVector: a later entry wins
+      const uint64_t s0 = j.sv_off[d], s1 = j.sv_off[d + 1];
+      ln::LCur c = ln::make(j.sv + s0, 0, (uint32_t)(s1 - s0));
+      const uint32_t ns = s1 - s0 > (1u << 20) ? NONE : ln::rvu(c);
+      bool bad = ns == NONE || ns > MSVMAX;
+      for (uint32_t q = 0; q < ns && !bad; q++) {
+        const uint32_t cl = ln::rvu(c), ck = ln::rvu(c);
+        bad |= c.bad;
+        svclk[q] = ck;
+        uint32_t h = (cl * 0x9E3779B1u) >> 20;
+        while (mval[h] != 0 && mkey[h] != cl) h = (h + 1) & (MSVSLOTS - 1);
+        mkey[h] = cl;
+        mval[h] = q + 1;
+      }
+      if (bad || c.bad) { s_bad = 1; s_why = 3; }
+    }
+    __threadfence_block();
+    __syncthreads();
+    if (s_bad) {
+      if (t == 0) done[d] = (uint8_t)s_why;
+      __syncthreads();
+      continue;
+    }
+    const uint64_t tm1 = __builtin_amdgcn_s_memrealtime();
+    // ---- B: sections round-robin over the waves
+    bool declined = false;
+    uint32_t why = 0;
+    DescWin W;
+    uint32_t cc = NONE, s = 0;
+    for (uint32_t ci = wv; ci < nsec && !declined; ci += MS_WAVES) {
+      cc = NONE;  // (each section looks its entry up afresh: the O(1) chunk rest needs it)
+      uint32_t x = msec(ci, M_X0);
+      const uint32_t nstructs = msec(ci, M_W), client = msec(ci, M_CLIENT);
+      uint64_t clock = msec(ci, M_CLOCK);
+      uint32_t k = 0;
+      if (OP == OP_DIFF) {
+        uint32_t h = (client * 0x9E3779B1u) >> 20;
+        while (mval[h] != 0) {
+          if (mkey[h] == client) { k = svclk[mval[h] - 1]; break; }
+          h = (h + 1) & (MSVSLOTS - 1);
+        }
+      }
+      // state vector: the first section's first struct counts even when it is a Skip (os@37724)
+      bool sv_stop = clock != 0, first = ci == 0;
+      uint32_t sv_clock = 0;
+      bool copying = false;
+      uint32_t written = 0, rem = nstructs;
+      while (rem > 0) {
+        if (x >= len) { declined = true; why = 7; break; }
+        const uint32_t cx = x / CH;
+        desc_at(W, desc, cb, nch, cx);
+        const int di = (int)(cx - W.wb);
+        const uint32_t w0 = lane_read(W.q0.x, di), w1 = lane_read(W.q0.y, di);
+        const uint32_t nrec = w0 & 0xffffu, lfe = w0 >> 16, lpe = w1 & 0xffffu, lse = w1 >> 16;
+        const uint32_t cexit = lane_read(W.q0.z, di), cumx = lane_read(W.q0.w, di);
+        if (cx != cc) { cc = cx; s = 0; }
+        const uint32_t gc = cb + cx;
+        // the rest of the chunk in O(1) when the section spans it (no FAIL / patch / Skip / cut inside)
+        if (s == 0) {
+          uint32_t fs = NONE, fcum = 0;
+#pragma unroll
+          for (int kf = NFIRST - 1; kf >= 0; kf--) {
+            const uint32_t pwk = lane_read(kf < 4 ? (&W.q1.x)[kf] : (&W.q2.x)[kf - 4], di);
+            if ((uint32_t)kf < nrec && (pwk & POS_MASK) == x && !(pwk & F_FAIL)) {
+              fs = (uint32_t)kf;
+              fcum = lane_read(kf < 4 ? (&W.q3.x)[kf] : (&W.q4.x)[kf - 4], di);
+            }
+          }
+          if (fs != NONE) {
+            const uint32_t avail = nrec - fs;
+            const uint32_t delta = cumx - fcum;
+            bool whole = rem >= avail && lfe <= fs && !first;
+            if (OP == OP_DIFF) whole = whole && (copying ? lpe <= fs : clock + delta <= k);
+            if (OP == OP_SV) whole = whole && lse <= fs;
+            if (whole) {
+              if (clock + delta > 0xffffffffull) { declined = true; why = 10; break; }
+              if (OP == OP_SV && !sv_stop) sv_clock = (uint32_t)(clock + delta);
+              if (OP == OP_DIFF && copying) written += avail;
+              clock += delta;
+              rem -= avail;
+              x = cexit;
+              s = nrec;
+              continue;
+            }
+            s = fs;
+          }
+        }
+        bool found = false;
+        for (;;) {
+          if (s >= nrec) break;
+          const uint32_t kk = s + lane;
+          const uint32_t pw = kk < nrec ? recs[rec_idx(gc, kk)].x : POS_MASK;
+          const uint64_t lt = __ballot(kk < nrec && (pw & POS_MASK) < x);
+          const uint32_t nlt = __popcll(lt);
+          if (nlt == 64) { s += 64; continue; }
+          s += nlt;
+          if (s < nrec) {
+            const uint32_t cand = lane_read(pw, nlt);
+            found = (cand & POS_MASK) == x && !(cand & F_FAIL);
+          }
+          break;
+        }
+        uint32_t n, pos = 0, end = 0, clen = 0, fl = 0;
+        bool valid;
+        if (found) {
+          n = nrec - s < 64 ? nrec - s : 64;
+          if (rem < n) n = rem;
+          const uint32_t kk = s + lane;
+          valid = lane < n;
+          if (valid) {
+            const uint2 r = recs[rec_idx(gc, kk)];
+            const uint2 r1 = kk + 1 < nrec ? recs[rec_idx(gc, kk + 1)] : make_uint2(cexit, cumx);
+            pos = r.x & POS_MASK;
+            fl = r.x;
+            clen = r1.y - r.y;
+            end = r1.x & POS_MASK;
+          }
+          const uint64_t fm = __ballot(valid && (fl & F_FAIL));
+          if (fm) {
+            n = (uint32_t)__builtin_ctzll(fm);
+            valid = lane < n;
+          }
+          s += n;
+        } else {
+          uint32_t nx, cl, f2;
+          if (!ln::parse_fast(D, x, len, nx, cl, f2) && !ln::parse_struct(D, x, len, nx, cl, f2)) { declined = true; why = 8; break; }
+          n = 1;
+          valid = lane == 0;
+          pos = x; end = nx; clen = cl; fl = f2;
+        }
+        if (n == 0) { declined = true; why = 8; break; }
+        if (__any(valid && clen >= (1u << 24))) { declined = true; why = 9; break; }
+        const uint32_t cl = valid ? clen : 0;
+        const uint32_t incl = wave_incl_add(cl), excl = incl - cl;
+        const uint32_t tot = lane_read(incl, 63);
+        if (clock + tot > 0xffffffffull) { declined = true; why = 10; break; }
+        const bool skip = valid && (fl & F_SKIP);
+        const uint64_t eclk = clock + incl;
+        if (OP == OP_SV) {
+          if (first) {  // the update's first struct initialises the state
+            first = false;
+            sv_clock = sv_stop ? 0 : (uint32_t)(clock + lane_read(cl, 0));
+          }
+          const uint64_t skm = __ballot(skip);
+          const uint32_t fs = skm ? (uint32_t)__builtin_ctzll(skm) : n;
+          if (!sv_stop && fs > 0) sv_clock = (uint32_t)(clock + lane_read(incl, fs - 1));
+          if (skm) sv_stop = true;
+        } else if (OP == OP_DIFF) {
+          first = false;
+          uint32_t firstw = 0;
+          bool pend = false;
+          if (!copying) {
+            const uint64_t cm = __ballot(valid && !skip && eclk > k);
+            if (cm) {
+              const uint32_t f = (uint32_t)__builtin_ctzll(cm);
+              copying = true;
+              written = n - f;
+              const uint64_t fclk = clock + lane_read(excl, f);
+              const uint32_t off = k > fclk ? (uint32_t)(k - fclk) : 0;
+              const uint32_t fpos = lane_read(pos, f), fend = lane_read(end, f), flen = lane_read(cl, f);
+              uint32_t prelen = 0, a0 = 0, a1 = 0, b0;
+              if (off == 0) {
+                b0 = fpos;
+                firstw = f;
+              } else {
+                if (!slice_head(B, adj, fpos, fend, client, fclk, flen, off, M.pre + (uint64_t)ci * PRE, prelen, a0, a1)) {
+                  declined = true;
+                  why = 11;
+                  break;
+                }
+                b0 = fend;
+                firstw = f + 1;
+              }
+              if (lane == 0) {
+                msec(ci, M_PRELEN) = prelen;
+                msec(ci, M_A0) = a0;
+                msec(ci, M_A1) = a1;
+                msec(ci, M_B0) = b0;
+                msec(ci, M_FCLOCK) = (uint32_t)(fclk + off);
+              }
+              pend = true;
+            }
+          } else {
+            written += n;
+            pend = true;
+          }
+          if (pend) {  // info-byte patches of the verbatim structs
+            const bool pl = valid && lane >= firstw && (fl & F_PATCH);
+            const uint64_t pm = __ballot(pl);
+            if (pm) {
+              const uint32_t np = __popcll(pm);
+              uint32_t base = 0;
+              if (lane == 0) base = atomicAdd(&s_npatch, np);
+              base = lane_read(base, 0);
+              if (base + np > MSPATCH) { declined = true; why = 12; break; }
+              if (pl) {
+                const uint32_t slot = base + __popcll(pm & ((1ull << lane) - 1));
+                const uint32_t info = D[pos];
+                M.ppos[slot] = pos;
+                M.psec[slot] = ci;
+                M.pval[slot] = (uint8_t)((info & 31) == 0 ? 0 : info & ~0x20u);
+              }
+            }
+          }
+        } else {
+          first = false;
+        }
+        clock += tot;
+        x = lane_read(end, n - 1);
+        rem -= n;
+      }
+      if (declined) break;
+      if (lane == 0) {
+        msec(ci, M_END) = (uint32_t)clock;
+        msec(ci, M_VAL) = sv_clock;
+        if (OP == OP_DIFF) {
+          msec(ci, M_WRITTEN) = copying ? written : 0;
+          if (!copying) msec(ci, M_PRELEN) = NONE;
+        }
+      }
+      if (x != msec(ci, M_X1)) { declined = true; why = 18; break; }  // (the header walk and the stitch agree)
+    }
+    if (declined && lane == 0) { s_bad = 1; s_why = why; }
+    __threadfence_block();
+    __syncthreads();
+    if (s_bad) {
+      if (t == 0) done[d] = (uint8_t)s_why;
+      __syncthreads();
+      continue;
+    }
+    const uint64_t tm2 = __builtin_amdgcn_s_memrealtime();
+    if (t == 0) { atomicAdd(&pw_prof[0], tm1 - tm0); atomicAdd(&pw_prof[1], tm2 - tm1); }
+    // ---- C
+    if (OP != OP_DIFF) {  // state vector / meta: one entry per section, written by one thread
+      if (t == 0) {
+        uint32_t total = 0, cnt = 0;
+        for (uint32_t ci = 0; ci < nsec; ci++) {
+          if (OP == OP_SV) {
+            const uint32_t v = msec(ci, M_VAL);
+            if (v) { cnt++; total += vsz(msec(ci, M_CLIENT)) + vsz(v); }
+          } else {
+            total += 2 * vsz(msec(ci, M_CLIENT)) + vsz(msec(ci, M_CLOCK)) + vsz(msec(ci, M_END));
+          }
+        }
+        total += OP == OP_SV ? vsz(cnt) : 2 * vsz(nsec);
+        const uint64_t base = atomicAdd((unsigned long long *)j.used, (unsigned long long)total);
+        done[d] = 1;
+        atomicAdd((unsigned long long *)j.pw_count, 1ull);
+        if (base + total > j.cap) {
+          j.status[d] = ym::ST_CAPACITY;
+          j.out_len[d] = 0;
+        } else {
+          uint8_t *o = j.out + base;
+          uint32_t p = put_vu_g(o, 0, OP == OP_SV ? cnt : nsec);
+          for (uint32_t ci = 0; ci < nsec; ci++) {
+            if (OP == OP_SV && !msec(ci, M_VAL)) continue;
+            p = put_vu_g(o, p, msec(ci, M_CLIENT));
+            p = put_vu_g(o, p, OP == OP_SV ? msec(ci, M_VAL) : msec(ci, M_CLOCK));
+          }
+          if (OP == OP_META) {
+            p = put_vu_g(o, p, nsec);
+            for (uint32_t ci = 0; ci < nsec; ci++) { p = put_vu_g(o, p, msec(ci, M_CLIENT)); p = put_vu_g(o, p, msec(ci, M_END)); }
+          }
+          j.out_off[d] = base;
+          j.out_len[d] = total;
+          j.status[d] = ym::ST_OK;
+        }
+      }
+      __syncthreads();
+      continue;
+    }
+    // delete set (wave 0): validated (readDeleteSet: no empty and no repeated client, checked in the LDS
+    // hash table the state vector used), then copied verbatim
+    for (uint32_t q = t; q < MSVSLOTS; q += MS_T) mval[q] = 0;
+    __syncthreads();
+    if (wv == 0) {
+      uint32_t x = s_ds0;
+      ln::LCur c = ln::make(D, x, len);
+      const uint32_t ndc = ln::rvu(c);
+      x = c.p;
+      bool bad = c.bad || ndc > MSVMAX;
+      for (uint32_t i = 0; i < ndc && !bad; i++) {
+        ln::LCur h = ln::make(D, x, len);
+        const uint32_t client = ln::rvu(h);
+        const uint32_t m = ln::rvu(h);
+        x = h.p;
+        if (h.bad || m == 0) { bad = true; break; }
+        uint32_t hit = 0;
+        if (lane == 0) {
+          uint32_t hh = (client * 0x9E3779B1u) >> 20;
+          while (mval[hh] != 0 && mkey[hh] != client) hh = (hh + 1) & (MSVSLOTS - 1);
+          hit = mval[hh] != 0;
+          mkey[hh] = client;
+          mval[hh] = 1;
+        }
+        if (lane_read(hit, 0)) { bad = true; break; }
+        x = wds::skip_varuints(D, x, len, 2ull * m);
+        if (x == NONE) { bad = true; break; }
+      }
+      if (lane == 0) { if (bad) { s_bad = 1; s_why = 17; } s_sum[MS_WAVES] = x; }
+    }
+    __syncthreads();
+    if (s_bad) {
+      if (t == 0) done[d] = (uint8_t)s_why;
+      __syncthreads();
+      continue;
+    }
+    const uint32_t ds1 = s_sum[MS_WAVES];
+    const uint32_t ds0 = s_ds0;
+    // sizes: each section's part, offsets by a block scan (sections in chunks of MS_T)
+    uint32_t acc = 0, nparts = 0;
+    for (uint32_t c0 = 0; c0 < nsec; c0 += MS_T) {
+      const uint32_t ci = c0 + t;
+      uint32_t sz = 0, kept = 0;
+      if (ci < nsec && msec(ci, M_PRELEN) != NONE) {
+        kept = 1;
+        sz = vsz(msec(ci, M_WRITTEN)) + vsz(msec(ci, M_CLIENT)) + vsz(msec(ci, M_FCLOCK)) + msec(ci, M_PRELEN) +
+             (msec(ci, M_A1) - msec(ci, M_A0)) + (msec(ci, M_X1) - msec(ci, M_B0));
+      }
+      const uint32_t wi = wave_incl_add(sz), wk = wave_incl_add(kept);
+      if (lane == 63) { s_sum[wv] = wi; }
+      __syncthreads();
+      uint32_t pre = 0, all = 0;
+      for (uint32_t q = 0; q < MS_WAVES; q++) { pre += q < wv ? s_sum[q] : 0; all += s_sum[q]; }
+      if (ci < nsec && kept) msec(ci, M_OUT) = acc + pre + wi - sz;
+      acc += all;
+      __syncthreads();
+      if (lane == 63) s_sum[wv] = wk;
+      __syncthreads();
+      for (uint32_t q = 0; q < MS_WAVES; q++) nparts += s_sum[q];
+      __syncthreads();
+    }
+    const uint64_t total = vsz(nparts) + (uint64_t)acc + (ds1 - ds0);
+    __shared__ unsigned long long s_base;
+    if (t == 0) {
+      s_base = atomicAdd((unsigned long long *)j.used, (unsigned long long)total);
+      done[d] = 1;
+      atomicAdd((unsigned long long *)j.pw_count, 1ull);
+    }
+    __threadfence_block();
+    __syncthreads();
+    const uint64_t base = s_base;
+    if (base + total > j.cap) {
+      if (t == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }
+      __syncthreads();
+      continue;
+    }
+    uint8_t *const o = j.out + base;
+    const uint32_t p0 = vsz(nparts);
+    if (t == 0) put_vu_g(o, 0, nparts);
+    for (uint32_t ci = wv; ci < nsec; ci += MS_WAVES) {
+      const uint32_t pl = msec(ci, M_PRELEN);
+      if (pl == NONE) continue;
+      const uint32_t written = msec(ci, M_WRITTEN), client = msec(ci, M_CLIENT), fclock = msec(ci, M_FCLOCK);
+      uint32_t p = p0 + msec(ci, M_OUT);
+      if (lane == 0) {
+        uint32_t q = put_vu_g(o, p, written);
+        q = put_vu_g(o, q, client);
+        q = put_vu_g(o, q, fclock);
+        for (uint32_t b = 0; b < pl; b++) o[q + b] = M.pre[(uint64_t)ci * PRE + b];
+      }
+      p += vsz(written) + vsz(client) + vsz(fclock) + pl;
+      const uint32_t a0 = msec(ci, M_A0), a1 = msec(ci, M_A1);
+      copy_bytes(o + p, D + a0, a1 - a0);
+      p += a1 - a0;
+      const uint32_t b0 = msec(ci, M_B0), b1 = msec(ci, M_X1);
+      copy_bytes(o + p, D + b0, b1 - b0);
+      if (lane == 0) msec(ci, M_OUT) = p - b0;  // output position = document position + this
+    }
+    if (wv == MS_WAVES - 1) copy_bytes(o + p0 + acc, D + ds0, ds1 - ds0);
+    __threadfence();  // the patches below overwrite bytes other waves stored
+    __syncthreads();
+    const uint32_t np = s_npatch;
+    for (uint32_t i = t; i < np; i += MS_T) o[msec(M.psec[i], M_OUT) + M.ppos[i]] = M.pval[i];
+    if (t == 0) {
+      atomicAdd(&pw_prof[2], __builtin_amdgcn_s_memrealtime() - tm2);
+      atomicAdd(&pw_prof[3], (unsigned long long)np);
+      j.out_off[d] = base;
+      j.out_len[d] = total;
+      j.status[d] = ym::ST_OK;
+    }
+    __syncthreads();
+  }
+}
+#undef msec
+
 }  // namespace pw
 
 #define PWCHK(x)                                  \
@@ -749,18 +1313,26 @@ int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const ui
   uint64_t pw_min = PW_MIN;
   if (const char *e = getenv("YMERGE_PW_MIN")) pw_min = strtoull(e, nullptr, 10);
   if (!B.pinned && hipHostMalloc((void **)&B.pinned, 64, hipHostMallocDefault) != hipSuccess) return -2;
+  uint32_t ms_min = MS_MIN;
+  if (const char *e = getenv("YMERGE_PWMS_MIN")) ms_min = (uint32_t)strtoul(e, nullptr, 10);
   const uint32_t n1 = j.n + 1;
-  if (pw_ensure(B, 0, 8ull * n1 + 16 + j.n)) return -2;
-  uint32_t *cnt = (uint32_t *)B.p[0], *cbase = cnt + n1;
+  if (pw_ensure(B, 0, 24ull * n1 + 16 + j.n)) return -2;
+  uint64_t *msz = (uint64_t *)B.p[0], *moff = msz + n1;
+  uint32_t *cnt = (uint32_t *)(moff + n1), *cbase = cnt + n1;
   uint8_t *done = (uint8_t *)(cbase + n1);
-  k_pw_prep<<<(n1 + 255) / 256, 256, 0, st>>>(j, cnt, done, pw_min);
-  size_t tmp = 0;
+  k_pw_prep<<<(n1 + 255) / 256, 256, 0, st>>>(j, cnt, done, pw_min, msz, ms_min);
+  size_t tmp = 0, tmp2 = 0;
   hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cnt, cbase, n1, st);
+  hipcub::DeviceScan::ExclusiveSum(nullptr, tmp2, msz, moff, n1, st);
+  if (tmp2 > tmp) tmp = tmp2;
   if (pw_ensure(B, 1, tmp + 16)) return -2;
   PWCHK(hipcub::DeviceScan::ExclusiveSum(B.p[1], tmp, cnt, cbase, n1, st));
+  PWCHK(hipcub::DeviceScan::ExclusiveSum(B.p[1], tmp, msz, moff, n1, st));
   PWCHK(hipMemcpyAsync(B.pinned, cbase + j.n, 4, hipMemcpyDeviceToHost, st));
+  PWCHK(hipMemcpyAsync(B.pinned + 2, moff + j.n, 8, hipMemcpyDeviceToHost, st));
   PWCHK(hipStreamSynchronize(st));
   const uint32_t total = B.pinned[0];
+  const uint64_t mtotal = *(uint64_t *)(B.pinned + 2);
   *done_out = done;  // every document is marked (0 = not taken) from here on
   pw_last_done = done;
   if (total == 0) return 1;
@@ -771,11 +1343,21 @@ int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const ui
   }
   uint4 *desc = (uint4 *)B.p[2];
   uint2 *recs = (uint2 *)B.p[3];
+  if (mtotal > 0 && pw_ensure(B, 4, mtotal + 256)) {  // no room for the section tables: the one-wave stitch takes them
+    hipMemsetAsync(msz, 0, 8ull * n1, st);
+  }
+  const bool ms = mtotal > 0 && B.p[4] != nullptr && B.cap[4] >= mtotal;
   k_pw_walk<<<(total + 255) / 256, 256, 0, st>>>(j, cbase, j.n, total, desc, recs);
   const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
-  if (op == OP_DIFF) k_pw_stitch<OP_DIFF><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done);
-  else if (op == OP_SV) k_pw_stitch<OP_SV><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done);
-  else k_pw_stitch<OP_META><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done);
+  if (op == OP_DIFF) k_pw_stitch<OP_DIFF><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done, msz);
+  else if (op == OP_SV) k_pw_stitch<OP_SV><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done, msz);
+  else k_pw_stitch<OP_META><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done, msz);
+  if (ms) {
+    uint8_t *area = (uint8_t *)B.p[4];
+    if (op == OP_DIFF) k_pw_ms<OP_DIFF><<<grid, MS_T, 0, st>>>(j, cbase, desc, recs, done, msz, moff, area);
+    else if (op == OP_SV) k_pw_ms<OP_SV><<<grid, MS_T, 0, st>>>(j, cbase, desc, recs, done, msz, moff, area);
+    else k_pw_ms<OP_META><<<grid, MS_T, 0, st>>>(j, cbase, desc, recs, done, msz, moff, area);
+  }
   return 1;
 }
 
