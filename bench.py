@@ -52,6 +52,9 @@ def parse():
                         "(auto: hash for the small-document workloads, bytes for C3 / C5)")
     p.add_argument("--cpu-stub", action="store_true",
                    help="gloo on CPU with a copy standing in for the merge (tests of the launcher only)")
+    p.add_argument("--rotate", type=int, default=12,
+                   help="distinct device copies of the batch, one per step in turn (12 x the C2 batch = "
+                        "~1 GB of inputs + outputs: above the 256 MiB on-die cache, so the roofline is HBM's)")
     p.add_argument("--no-secondary", action="store_true",
                    help="skip the secondary workload lines (C4/C2-V2/C4-V2 merges, C3 diff/sv)")
     return p.parse_args()
@@ -83,11 +86,23 @@ def cpu_baseline(arena, upd_off, doc_upd, fmt, seconds):
                   f"oracle/ymerge_oracle.c (literal yjs 13.5.16 mergeUpdates), {threads} threads",
         "errors": int((st != 0).sum()),
         # the port is faster than the JS it restates: per-thread ratios measured on identical C2 / C4
-        # documents in the build container (oracle/gen/time_js_baselines.cjs)
-        "calibration": {"port_over_yjs_13_5_16_js": {"c2": 5.25, "c4": 5.87},
-                        "port_over_reference_13_4_9_doc_roundtrip": {"c2": 11.2, "c4": 15.8},
-                        "source": "BASELINE.md section 2"},
+        # documents in the build container by tools/calibrate.py (JS cannot run on the GPU box)
+        "calibration": _calibration(),
     }
+
+
+def _calibration():
+    """The per-thread C-port / JS ratios of the last tools/calibrate.py run (profiles/calibration.json)."""
+    try:
+        c = json.load(open(os.path.join(ROOT, "profiles", "calibration.json")))
+    except (OSError, ValueError):
+        return None
+    w = c.get("workloads", {})
+    return {"port_over_yjs_13_5_16_js": {k.split("_")[0]: v["port_over_yjs_13_5_16_js"] for k, v in w.items()},
+            "port_over_reference_13_4_9_doc_roundtrip": {k.split("_")[0]: v["port_over_reference_13_4_9_doc_roundtrip"]
+                                                         for k, v in w.items()},
+            "source": f"profiles/calibration.json (tools/calibrate.py, {c.get('docs')} docs, 1 thread, "
+                      f"measured {c.get('measured_utc')})"}
 
 
 def _ds_v1_to_v2(b):
@@ -219,7 +234,9 @@ def secondary(dev, eng):
         for _ in range(steps):
             rc, _ = eng.run_device(op, fmt, ga, go, gd, oa, oo, ol, st, gsa, gso)
             assert rc == 0, rc
-            kms.append(eng.last_stats.fast_ms + eng.last_stats.large_ms)
+            # device time of the call's kernels: the specialised path, the large-document pipeline and the
+            # general path (one thread per document: parseUpdateMeta of ~1 M small updates runs there)
+            kms.append(eng.last_stats.fast_ms + eng.last_stats.large_ms + eng.last_stats.general_ms)
         torch.cuda.synchronize(dev)
         el = (time.perf_counter() - t0) / steps
         sts = eng.stats
@@ -350,25 +367,34 @@ def main():
     else:
         from yjs_amd import Engine
         eng = Engine(local)
-    g_arena = torch.from_numpy(arena).to(dev)
     # u32 offsets (YM_OFF32) when the rank's arena is below 4 GiB: half the offset bytes per update
     off32 = in_bytes < 2 ** 32
-    g_off = torch.from_numpy(upd_off.astype(np.uint32).view(np.int32) if off32 else upd_off.view(np.int64)).to(dev)
-    g_doc = torch.from_numpy(doc_upd.view(np.int32)).to(dev)
     cap = 4 * in_bytes + 128 * n_docs + 8192  # fast-path slots (2*in + 64 per doc) + general-path room
-    o_arena = torch.empty(cap, dtype=torch.uint8, device=dev)
-    o_off = torch.empty(n_docs, dtype=torch.int64, device=dev)
-    o_len = torch.empty(n_docs, dtype=torch.int64, device=dev)
-    o_st = torch.empty(n_docs, dtype=torch.int32, device=dev)
     stream = None if stub else torch.cuda.current_stream(dev)
+    # `rotate` distinct device copies of the batch (inputs and output arrays), used one per step in turn:
+    # each step reads and writes HBM lines the previous steps did not touch
+    rot = max(1, args.rotate if not stub else 1)
+    sets = []
+    for _ in range(rot):
+        g_arena = torch.from_numpy(arena).to(dev)
+        g_off = torch.from_numpy(upd_off.astype(np.uint32).view(np.int32) if off32 else upd_off.view(np.int64)).to(dev)
+        g_doc = torch.from_numpy(doc_upd.view(np.int32)).to(dev)
+        o_arena = torch.empty(cap, dtype=torch.uint8, device=dev)
+        o_off = torch.empty(n_docs, dtype=torch.int64, device=dev)
+        o_len = torch.empty(n_docs, dtype=torch.int64, device=dev)
+        o_st = torch.empty(n_docs, dtype=torch.int32, device=dev)
+        call = eng.prepare_device("merge", fmt, g_arena, g_off, g_doc, o_arena, o_off, o_len, o_st, stream=stream)
+        sets.append((call, (g_arena, g_off, g_doc, o_arena, o_off, o_len, o_st)))
+    o_len, o_st = sets[0][1][5], sets[0][1][6]
+    cur = [0]
 
     def sync():
         if not stub:
             torch.cuda.synchronize(dev)
 
-    call = eng.prepare_device("merge", fmt, g_arena, g_off, g_doc, o_arena, o_off, o_len, o_st, stream=stream)
-
     def step():
+        call = sets[cur[0] % rot][0]
+        cur[0] += 1
         rc, used = call()
         if rc != 0:
             raise RuntimeError(f"ym_merge rc={rc}")
@@ -377,6 +403,7 @@ def main():
     for _ in range(args.warmup):
         step()
     sync()
+    cur[0] = 0
     errors = int((o_st != 0).sum().item())
     st0 = dict(eng.stats)
     out_bytes = int(o_len[o_st == 0].sum().item())
@@ -445,7 +472,10 @@ def main():
             "hbm_frac_in_plus_out": round((in_all + out_all) * args.steps / elapsed / 1e9 / (HBM_PEAK_GBS * world), 5),
             "docs_fast_path": int(fast_all), "docs_general_path": int(gen_all), "doc_errors": int(err_all),
             "device_ms_per_step": round(float(np.mean(dev_ms)), 4),
+            "working_set_bytes": int((in_bytes + cap) * rot), "rotated_buffer_sets": rot,
             "roofline": {"kernel": kernel_name, "bound": "hbm", "achieved": round(achieved, 2),
+                         "limiter": "instruction issue (PMC: SQ_ACTIVE_INST_ANY per SIMD ~ the launch's duration, "
+                                    "HBM traffic ~1.2x the algorithmic bytes; DESIGN.md section 4.1)",
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "traffic_source": traffic_src, "avg_launch_ms": round(avg_fast, 5),
                          "algorithmic_bytes_per_launch": int(alg_bytes)},

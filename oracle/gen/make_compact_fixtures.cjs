@@ -1,0 +1,190 @@
+// Doc round-trip compaction fixtures (SURVEY.md §8(f) row 1), test infrastructure, container-only: the
+// reference's own compaction -- gaberogan/yjs@v0 (yjs 13.4.9, /root/reference/src via ref_yjs.cjs):
+// every update applied to a default Doc (gc: true, Doc.js:40) in order, one transaction each
+// (applyUpdate[V2], encoding.js:462-473: resumeStructIntegration :225-321 -> Item.integrate Item.js:403-517,
+// readAndApplyDeleteSet DeleteSet.js:270-323; cleanupTransactions Transaction.js:244-367: tryGcDeleteSet,
+// tryMergeDeleteSet, tryToMergeWithLeft), then encodeStateAsUpdate[V2] (encoding.js:490-526).
+// Inputs: every golden merge case the reference applies without pending structs or delete readers, and
+// per workload template set (C1, C2, C4) the first documents' update lists.  Output:
+// tests/golden/compact.json {cases: [{id, group, fmt, inputs (b64), expect (b64) | src {ymb, doc}, expect_sha256, expect_len; single_tx_same}]}
+// single_tx_same records whether applying mergeUpdates(inputs) in one transaction gives the same bytes.
+'use strict'
+const fs = require('fs')
+const path = require('path')
+const zlib = require('zlib')
+const { loadReference } = require('./ref_yjs.cjs')
+const { Y: Y13 } = require('./yjs_bundle.cjs')
+
+const GOLDEN = path.join(__dirname, '../../tests/golden')
+const u8 = b64 => new Uint8Array(Buffer.from(b64, 'base64'))
+const b64 = u => Buffer.from(u).toString('base64')
+
+function loadYmb (name) {
+  const b = zlib.gunzipSync(fs.readFileSync(path.join(__dirname, '../../bench_data', name + '.ymb.gz')))
+  const nd = b.readUInt32LE(4); const nu = b.readUInt32LE(8)
+  let o = 12
+  const docUpd = []; for (let i = 0; i <= nd; i++) { docUpd.push(b.readUInt32LE(o)); o += 4 }
+  const off = []; for (let i = 0; i <= nu; i++) { off.push(Number(b.readBigUInt64LE(o))); o += 8 }
+  const arena = b.subarray(o)
+  const docs = []
+  for (let d = 0; d < nd; d++) {
+    const ups = []
+    for (let u = docUpd[d]; u < docUpd[d + 1]; u++) ups.push(new Uint8Array(arena.subarray(off[u], off[u + 1])))
+    docs.push(ups)
+  }
+  return docs
+}
+
+;(async () => {
+  const Y = await loadReference()
+  const pending = doc => doc.store.pendingClientsStructRefs.size + doc.store.pendingStack.length + doc.store.pendingDeleteReaders.length
+  const cases = []
+  const stats = {}
+  const add = (id, group, fmt, inputs, src) => {
+    const v2 = fmt === 2
+    const apply = v2 ? Y.applyUpdateV2 : Y.applyUpdate
+    const encode = v2 ? Y.encodeStateAsUpdateV2 : Y.encodeStateAsUpdate
+    let r
+    try {
+      const doc = new Y.Doc()
+      for (const u of inputs) apply(doc, u)
+      if (pending(doc) !== 0) { stats[group + '/pending'] = (stats[group + '/pending'] || 0) + 1; return }
+      const out = encode(doc)
+      let same = null
+      try {
+        const one = new Y.Doc()
+        apply(one, inputs.length === 1 ? inputs[0] : (v2 ? Y13.mergeUpdatesV2 : Y13.mergeUpdates)(inputs))
+        same = Buffer.compare(Buffer.from(encode(one)), Buffer.from(out)) === 0
+      } catch (e) { same = null }
+      // workload documents name their bench_data source instead of repeating its bytes
+      // (and, being large, carry the SHA-256 and length of the expected bytes)
+      r = src ? { id, group, fmt, src, expect_sha256: require('crypto').createHash('sha256').update(out).digest('hex'), expect_len: out.length, single_tx_same: same } : { id, group, fmt, inputs: inputs.map(b64), expect: b64(out), single_tx_same: same }
+    } catch (e) {
+      stats[group + '/throws'] = (stats[group + '/throws'] || 0) + 1
+      return
+    }
+    cases.push(r)
+    stats[group] = (stats[group] || 0) + 1
+    if (r.single_tx_same === false) stats[group + '/single_tx_differs'] = (stats[group + '/single_tx_differs'] || 0) + 1
+  }
+  for (const f of fs.readdirSync(GOLDEN).filter(f => f.endsWith('.json') && f !== 'compact.json').sort()) {
+    const g = path.basename(f, '.json')
+    if (g === 'ties') continue  // inconsistent histories (a GC and an Item for one ID): order-dependent by design
+    for (const c of JSON.parse(fs.readFileSync(path.join(GOLDEN, f))).cases) {
+      if (c.op !== 'merge' || !c.expect || !c.inputs || c.inputs.length === 0) continue
+      add(`${g}/${c.name}/v${c.fmt}`, g, c.fmt, c.inputs.map(u8))
+    }
+  }
+  for (const [wl, n] of [['c1_v1', 1], ['c1_v2', 1], ['c2_v1', 24], ['c2_v2', 24], ['c4_v1', 12], ['c4_v2', 12]]) {
+    const docs = loadYmb(wl)
+    for (let d = 0; d < n && d < docs.length; d++) add(`wl_${wl}/doc${d}`, 'wl_' + wl.slice(0, 2), wl.endsWith('v2') ? 2 : 1, docs[d], { ymb: wl, doc: d })
+  }
+  // the workloads with formatted text (C5: nested Y.XmlText) and their bigger documents (C3)
+  for (const [wl, n] of [['c3_v1', 3], ['c3_v2', 3], ['c5_v1', 4], ['c5_v2', 4]]) {
+    const docs = loadYmb(wl)
+    for (let d = 0; d < n && d < docs.length; d++) add(`wl_${wl}/doc${d}`, 'wl_' + wl.slice(0, 2), wl.endsWith('v2') ? 2 : 1, docs[d], { ymb: wl, doc: d })
+  }
+  // randomized concurrent histories over nested Y.Text / Y.XmlText with formatting, deletes of whole nested
+  // types, map overwrites and embeds, produced by yjs 13.5.16 peers; every peer's update events are applied to
+  // the compacting Doc in a shuffled order that keeps each peer's own order (the YText observer's remote
+  // formatting cleanup, ContentType.gc and the nested cleanup transaction all run)
+  let seed = 0x5eed
+  const rnd = () => { seed = (seed + 0x6D2B79F5) | 0; let t = seed; t = Math.imul(t ^ (t >>> 15), t | 1); t ^= t + Math.imul(t ^ (t >>> 7), t | 61); return ((t ^ (t >>> 14)) >>> 0) / 4294967296 }
+  const ri = (a, b) => a + Math.floor(rnd() * (b - a + 1))
+  const pick = a => a[Math.floor(rnd() * a.length)]
+  const words = ['a', 'bc', 'def', 'gh ', 'ij\n', 'klmno', '\u00e9t\u00e9', '\ud83d\ude00x']
+  const attrsOf = () => pick([{}, { bold: true }, { italic: true }, { bold: null }, { bold: true, italic: true }, { color: 'red' }, { color: '#00f' }, { bold: false }, { size: 0 }, { link: { href: 'x' } }])
+  for (let h = 0; h < 160; h++) {
+    const npeers = ri(2, 4)
+    const peers = []
+    const msgs = []
+    for (let p = 0; p < npeers; p++) {
+      const doc = new Y13.Doc({ gc: rnd() < 0.7 })
+      doc.clientID = 1000 + h * 8 + p
+      const log = []
+      const log2 = []
+      doc.on('update', u => log.push(u))
+      doc.on('updateV2', u => log2.push(u))
+      peers.push({ doc, log, log2 })
+    }
+    const root = d => d.getMap('root')
+    // peer 0 creates the structure
+    peers[0].doc.transact(() => {
+      const m = root(peers[0].doc)
+      const t = new Y13.Text(); m.set('text', t); t.insert(0, 'hello world', { bold: true })
+      const frag = new Y13.XmlFragment(); m.set('frag', frag)
+      const el = new Y13.XmlElement('p'); frag.insert(0, [el])
+      const xt = new Y13.XmlText(); el.insert(0, [xt]); xt.insert(0, 'xml text', { italic: true })
+      const arr = new Y13.Array(); m.set('arr', arr)
+      const t2 = new Y13.Text(); arr.insert(0, [t2, 'plain']); t2.insert(0, 'inner')
+    })
+    const sync = (a, b) => Y13.applyUpdate(b.doc, Y13.encodeStateAsUpdate(a.doc, Y13.encodeStateVector(b.doc)))
+    for (let p = 1; p < npeers; p++) sync(peers[0], peers[p])
+    const texts = d => {
+      const m = root(d)
+      const out = []
+      for (const k of ['text']) if (m.get(k) instanceof Y13.Text) out.push(m.get(k))
+      const frag = m.get('frag')
+      if (frag instanceof Y13.XmlFragment) frag.toArray().forEach(el => { if (el instanceof Y13.XmlElement) el.toArray().forEach(x => { if (x instanceof Y13.XmlText) out.push(x) }) })
+      const arr = m.get('arr')
+      if (arr instanceof Y13.Array) arr.toArray().forEach(x => { if (x instanceof Y13.Text) out.push(x) })
+      return out
+    }
+    const rounds = ri(2, 6)
+    for (let r = 0; r < rounds; r++) {
+      for (const pe of peers) {
+        const ops = ri(1, 6)
+        for (let o = 0; o < ops; o++) {
+          const ts = texts(pe.doc)
+          const op = rnd()
+          if (ts.length > 0 && op < 0.75) {
+            const t = pick(ts)
+            const len = t.length
+            const k = rnd()
+            if (k < 0.35) t.insert(ri(0, len), pick(words), attrsOf())
+            else if (k < 0.6 && len > 0) { const i = ri(0, len - 1); t.format(i, ri(1, len - i), attrsOf()) }
+            else if (k < 0.8 && len > 0) { const i = ri(0, len - 1); t.delete(i, ri(1, Math.min(4, len - i))) }
+            else if (k < 0.9) t.insertEmbed(ri(0, len), { img: pick(['a', 'b']) }, attrsOf())
+            else t.insert(ri(0, len), pick(words))
+          } else if (op < 0.85) {
+            root(pe.doc).set(pick(['k1', 'k2']), pick([1, 'v', null, [1, 2], { a: 1 }]))
+          } else if (op < 0.93) {
+            const m = root(pe.doc)
+            const frag = m.get('frag')
+            if (frag instanceof Y13.XmlFragment && rnd() < 0.5) {
+              const el = new Y13.XmlElement(pick(['p', 'h1'])); frag.insert(ri(0, frag.length), [el])
+              const xt = new Y13.XmlText(); el.insert(0, [xt]); xt.insert(0, pick(words), attrsOf())
+            } else if (frag instanceof Y13.XmlFragment && frag.length > 0) frag.delete(ri(0, frag.length - 1), 1)
+          } else if (op < 0.97) {
+            const arr = root(pe.doc).get('arr')
+            if (arr instanceof Y13.Array && arr.length > 0 && rnd() < 0.5) arr.delete(ri(0, arr.length - 1), 1)
+            else if (arr instanceof Y13.Array) { const t2 = new Y13.Text(); arr.insert(ri(0, arr.length), [t2]); t2.insert(0, pick(words), attrsOf()) }
+          } else {
+            const t = new Y13.Text(); root(pe.doc).set('text', t); t.insert(0, pick(words), attrsOf())
+          }
+        }
+      }
+      // partial sync: some pairs exchange their states
+      for (let q = 0; q < npeers; q++) if (rnd() < 0.6) { const a = pick(peers), b = pick(peers); if (a !== b) sync(a, b) }
+    }
+    // every peer's own update events, interleaved in a random order that keeps each peer's order; drop the
+    // updates that only relay what another peer produced (they come from syncs) -- keep them all: a relayed
+    // update is exactly what a provider would hand the compacting Doc
+    const v2 = h % 2 === 1
+    const queues = peers.map(p => (v2 ? p.log2 : p.log).slice())
+    while (queues.some(q => q.length > 0)) {
+      const live = queues.filter(q => q.length > 0)
+      const q = pick(live)
+      const take = ri(1, Math.min(3, q.length))
+      for (let i = 0; i < take; i++) msgs.push(q.shift())
+    }
+    add(`fuzz_fmt/h${h}/v${v2 ? 2 : 1}`, 'fuzz_fmt', v2 ? 2 : 1, msgs)
+  }
+  fs.writeFileSync(path.join(GOLDEN, 'compact.json'), JSON.stringify({
+    generator: 'oracle/gen/make_compact_fixtures.cjs',
+    reference: 'gaberogan/yjs@v0 (yjs 13.4.9, /root/reference/src) under Node 12 ESM with a lib0 shim over the bundled lib0 0.2.42 (oracle/gen/ref_yjs.cjs): new Doc() (gc: true), applyUpdate[V2] per input, encodeStateAsUpdate[V2]',
+    stats,
+    cases
+  }))
+  console.log(JSON.stringify(stats, null, 1), cases.length)
+})().catch(e => { console.error(e); process.exit(1) })

@@ -2224,6 +2224,967 @@ static Buf *snap_impl(Ctx *c, const uint8_t *p, size_t n, int v2in, int v2out) {
 }
 
 /* ------------------------------------------------------------------------------------------------ */
+/* Doc round-trip compaction: gaberogan/yjs@v0 (yjs 13.4.9) itself --        */
+/* new Doc() (gc: true, Doc.js:40), applyUpdate[V2] of every input in order (one transaction each,   */
+/* encoding.js:462-473 readUpdateV2), encodeStateAsUpdate[V2] (encoding.js:490-526).                 */
+/*   readStructs            encoding.js:415-436 (readClientsStructRefs :127-198,                     */
+/*                          mergeReadStructsIntoPendingReads :354-372, resumeStructIntegration        */
+/*                          :225-321, cleanupPendingStructs :377-388, tryResumePendingDeleteReaders)  */
+/*   Item.getMissing / integrate / delete / gc / mergeWith   Item.js:355-517, 545-616                 */
+/*   splitItem Item.js:85-125, getItemCleanStart / End StructStore.js:190-231, replaceStruct :241-244  */
+/*   readAndApplyDeleteSet  DeleteSet.js:270-323, sortAndMergeDeleteSet :113-135                      */
+/*   cleanupTransactions    Transaction.js:244-367 (tryGcDeleteSet :182-204, tryMergeDeleteSet        */
+/*                          :210-227, tryToMergeWithLeft :165-176)                                    */
+/*   ContentType.delete / gc ContentType.js:101-141; ContentString.splice ContentString.js:51-66      */
+/*   writeClientsStructs / writeStructs encoding.js:71-116; createDeleteSetFromStructStore            */
+/*                          DeleteSet.js:185-210; writeDeleteSet :219-232                              */
+/* ------------------------------------------------------------------------------------------------ */
+typedef struct CType CType;
+typedef struct CIt {
+  int gc;                       /* a GC struct */
+  int64_t client, clock, len;
+  int has_origin, has_right;
+  JID origin, right;            /* origin / rightOrigin */
+  struct CIt *left, *rightp;    /* left / right */
+  CType *parent;                /* resolved parent type (NULL: none) */
+  int pkind; Str pkey; JID pid; /* parent as read: 0 none (copied from a neighbour), 1 ykey, 2 ID */
+  int has_psub; Str psub;
+  int deleted;
+  Content *ct;
+  CType *type;                  /* ContentType: its type */
+  uint32_t gen_before, gen_conf; /* Item.integrate's itemsBeforeOrigin / conflictingItems sets */
+} CIt;
+struct CType {
+  CIt *start, *item;            /* _start, _item */
+  int tref;                     /* typeRef of the ContentType (2 YText, 6 YXmlText ...); -1: a root (AbstractType) */
+  Str key;                      /* a root type's key (doc.share) */
+  Str *mk; CIt **mv; size_t mn, mcap; /* _map in insertion order */
+};
+typedef struct { int64_t client; CIt **a; size_t n, cap; } CCl;
+typedef struct { int64_t client; CIt **refs; size_t n, i; int live; } CPend;
+typedef struct {
+  Ctx *c;
+  CCl *cl; size_t ncl, capcl;        /* store.clients, Map insertion order */
+  CPend *pend; size_t npend, cappend; /* store.pendingClientsStructRefs */
+  CIt **stack; size_t nstack, capstack; /* store.pendingStack */
+  DSet *pdel; size_t npdel, cappdel; /* store.pendingDeleteReaders */
+  CType **roots; size_t nroots, caproots; /* doc.share */
+  uint32_t gen;
+  struct CTx *tx;                    /* doc._transaction */
+  int64_t *hk; size_t *hv; size_t hcap; /* client -> index into cl (open addressing) */
+} CDoc;
+typedef struct CTx {                 /* Transaction (Transaction.js:57-140) */
+  DSet ds;                           /* deleteSet */
+  CIt **ms; size_t nms, capms;       /* _mergeStructs */
+  int64_t *bc_client, *bc_clock; size_t nbc; /* beforeState */
+  CType **chg; size_t nchg, capchg;  /* changed (Map insertion order; the parentSub sets are not needed) */
+  int local;
+} CTx;
+
+#define CGROW(c, arr, n, cap, T)                                                   \
+  do {                                                                             \
+    if ((n) == (cap)) {                                                            \
+      size_t nc_ = (cap) ? (cap) * 2 : 8;                                          \
+      T *na_ = (T *)aalloc((c), nc_ * sizeof(T));                                  \
+      if (n) memcpy(na_, (arr), (n) * sizeof(T));                                  \
+      (arr) = na_; (cap) = nc_;                                                    \
+    }                                                                              \
+  } while (0)
+
+static size_t cd_hslot(const CDoc *d, int64_t client) {
+  size_t h = (size_t)((uint64_t)client * 0x9E3779B97F4A7C15ull >> 20) & (d->hcap - 1);
+  while (d->hv[h] != 0 && d->hk[h] != client) h = (h + 1) & (d->hcap - 1);
+  return h;
+}
+static CCl *cd_client(CDoc *d, int64_t client) {
+  if (d->hcap == 0) return NULL;
+  size_t h = cd_hslot(d, client);
+  return d->hv[h] ? &d->cl[d->hv[h] - 1] : NULL;
+}
+static void cd_hput(CDoc *d, int64_t client, size_t idx) {
+  if (2 * (d->ncl + 1) > d->hcap) {
+    size_t nc = d->hcap ? d->hcap * 2 : 64;
+    int64_t *ok = d->hk;
+    size_t *ov = d->hv, oc = d->hcap;
+    d->hk = (int64_t *)aalloc(d->c, nc * sizeof(int64_t));
+    d->hv = (size_t *)aalloc(d->c, nc * sizeof(size_t));
+    memset(d->hv, 0, nc * sizeof(size_t));
+    d->hcap = nc;
+    for (size_t i = 0; i < oc; i++)
+      if (ov[i]) { size_t h = cd_hslot(d, ok[i]); d->hk[h] = ok[i]; d->hv[h] = ov[i]; }
+  }
+  size_t h = cd_hslot(d, client);
+  d->hk[h] = client;
+  d->hv[h] = idx + 1;
+}
+static int64_t cl_state(const CCl *s) {
+  if (!s || s->n == 0) return 0;
+  CIt *l = s->a[s->n - 1];
+  return l->clock + l->len;
+}
+static int64_t cd_state(CDoc *d, int64_t client) { return cl_state(cd_client(d, client)); } /* getState */
+static size_t cd_find_index(CDoc *d, CCl *s, int64_t clock) { /* findIndexSS (StructStore.js:123-151) */
+  if (!s || s->n == 0) fail(d->c, YMO_ERR_UNEXPECTED);
+  size_t lo = 0, hi = s->n;
+  while (lo < hi) {
+    size_t mid = (lo + hi) / 2;
+    CIt *m = s->a[mid];
+    if (m->clock <= clock) {
+      if (clock < m->clock + m->len) return mid;
+      lo = mid + 1;
+    } else hi = mid;
+  }
+  fail(d->c, YMO_ERR_UNEXPECTED);
+}
+static CIt *cd_get(CDoc *d, JID id) { CCl *s = cd_client(d, id.client); return s->a[cd_find_index(d, s, id.clock)]; }
+static void cl_insert(CDoc *d, CCl *s, size_t at, CIt *it) {
+  CGROW(d->c, s->a, s->n, s->cap, CIt *);
+  memmove(s->a + at + 1, s->a + at, (s->n - at) * sizeof(CIt *));
+  s->a[at] = it;
+  s->n++;
+}
+static void cl_remove(CCl *s, size_t at) { memmove(s->a + at, s->a + at + 1, (s->n - at - 1) * sizeof(CIt *)); s->n--; }
+static void cd_add_struct(CDoc *d, CIt *it) { /* addStruct (StructStore.js:92-104) */
+  CCl *s = cd_client(d, it->client);
+  if (!s) {
+    cd_hput(d, it->client, d->ncl);
+    CGROW(d->c, d->cl, d->ncl, d->capcl, CCl);
+    s = &d->cl[d->ncl++];
+    memset(s, 0, sizeof(*s));
+    s->client = it->client;
+  } else {
+    CIt *l = s->a[s->n - 1];
+    if (l->clock + l->len != it->clock) fail(d->c, YMO_ERR_UNEXPECTED);
+  }
+  CGROW(d->c, s->a, s->n, s->cap, CIt *);
+  s->a[s->n++] = it;
+}
+static CType *ct_new(CDoc *d) { CType *t = (CType *)aalloc(d->c, sizeof(CType)); memset(t, 0, sizeof(*t)); t->tref = -1; return t; }
+/* beforeState.get(client) || 0: beforeState holds the store's clients in order, so the index of a client in
+   the store is its index there */
+static int64_t tx_before_at(const CTx *t, size_t idx) { return idx < t->nbc ? t->bc_clock[idx] : 0; }
+static int64_t tx_before(CDoc *d, const CTx *t, int64_t client) {
+  CCl *s = cd_client(d, client);
+  return s ? tx_before_at(t, (size_t)(s - d->cl)) : 0;
+}
+static void changed_add(CDoc *d, CType *t) { /* addChangedTypeToTransaction (Transaction.js:154-159) */
+  CTx *x = d->tx;
+  if (t->item && !(t->item->clock < tx_before(d, x, t->item->client) && !t->item->deleted)) return;
+  for (size_t i = 0; i < x->nchg; i++) if (x->chg[i] == t) return;
+  CGROW(d->c, x->chg, x->nchg, x->capchg, CType *);
+  x->chg[x->nchg++] = t;
+}
+static void changed_del(CDoc *d, CType *t) {
+  CTx *x = d->tx;
+  for (size_t i = 0; i < x->nchg; i++)
+    if (x->chg[i] == t) { memmove(x->chg + i, x->chg + i + 1, (x->nchg - i - 1) * sizeof(CType *)); x->nchg--; return; }
+}
+static CType *cd_root(CDoc *d, Str key) { /* doc.get(key): the root type, created on first use */
+  for (size_t i = 0; i < d->nroots; i++) if (str_eq(d->roots[i]->key, key)) return d->roots[i];
+  CType *t = ct_new(d);
+  t->key = key;
+  CGROW(d->c, d->roots, d->nroots, d->caproots, CType *);
+  d->roots[d->nroots++] = t;
+  return t;
+}
+static CIt *map_get(CType *t, Str k) {
+  for (size_t i = 0; i < t->mn; i++) if (str_eq(t->mk[i], k)) return t->mv[i];
+  return NULL;
+}
+static void map_set(CDoc *d, CType *t, Str k, CIt *v) {
+  for (size_t i = 0; i < t->mn; i++) if (str_eq(t->mk[i], k)) { t->mv[i] = v; return; }
+  if (t->mn == t->mcap) {
+    size_t nc = t->mcap ? t->mcap * 2 : 4;
+    Str *nk = (Str *)aalloc(d->c, nc * sizeof(Str));
+    CIt **nv = (CIt **)aalloc(d->c, nc * sizeof(CIt *));
+    if (t->mn) { memcpy(nk, t->mk, t->mn * sizeof(Str)); memcpy(nv, t->mv, t->mn * sizeof(CIt *)); }
+    t->mk = nk; t->mv = nv; t->mcap = nc;
+  }
+  t->mk[t->mn] = k; t->mv[t->mn] = v; t->mn++;
+}
+static void tds_add(CDoc *d, DSet *ds, int64_t client, int64_t clock, int64_t len) { /* addToDeleteSet */
+  dc_push(d->c, ds_get_or_add(d->c, ds, client), clock, len);
+}
+static void ms_push(CDoc *d, CIt *it) { CTx *x = d->tx; CGROW(d->c, x->ms, x->nms, x->capms, CIt *); x->ms[x->nms++] = it; }
+static JID it_last(const CIt *it) { JID r = {it->client, it->clock + it->len - 1}; return r; }
+static int jid_eq(int ha, JID a, int hb, JID b) { return ha == hb && (!ha || (a.client == b.client && a.clock == b.clock)); }
+
+/* the left part of content.splice(off) (ContentString.js:51-66 and the other contents' splice) */
+static void content_truncate(Ctx *c, Content *ct, int64_t off) {
+  switch (ct->ref) {
+    case 1: ct->dlen = off; break;
+    case 2: case 8: ct->n = (size_t)off; break;
+    case 4: {
+      Str l = str_slice(ct->str, 0, off);
+      if (off >= 1 && l.n >= (size_t)off && l.u[off - 1] >= 0xD800 && l.u[off - 1] <= 0xDBFF) {
+        uint16_t *nu = (uint16_t *)aalloc(c, (size_t)off * 2);
+        memcpy(nu, l.u, ((size_t)off - 1) * 2);
+        nu[off - 1] = 0xFFFD;
+        Str ns = {nu, (size_t)off};
+        l = ns;
+      }
+      ct->str = l;
+      break;
+    }
+    default: fail(c, YMO_ERR_METHOD);
+  }
+}
+static Content *content_copy(Ctx *c, const Content *src) {
+  Content *r = (Content *)aalloc(c, sizeof(Content));
+  *r = *src;
+  return r;
+}
+static int content_merge(Ctx *c, Content *l, const Content *r) { /* AbstractContent.mergeWith */
+  switch (l->ref) {
+    case 1: l->dlen += r->dlen; return 1;
+    case 4: {
+      uint16_t *nu = (uint16_t *)aalloc(c, (l->str.n + r->str.n + 1) * 2);
+      if (l->str.n) memcpy(nu, l->str.u, l->str.n * 2);
+      if (r->str.n) memcpy(nu + l->str.n, r->str.u, r->str.n * 2);
+      Str s = {nu, l->str.n + r->str.n};
+      l->str = s;
+      return 1;
+    }
+    case 8: {
+      Val **na = (Val **)aalloc(c, (l->n + r->n + 1) * sizeof(Val *));
+      if (l->n) memcpy(na, l->anys, l->n * sizeof(Val *));
+      if (r->n) memcpy(na + l->n, r->anys, r->n * sizeof(Val *));
+      l->anys = na; l->n += r->n;
+      return 1;
+    }
+    case 2: {
+      Str *nj = (Str *)aalloc(c, (l->n + r->n + 1) * sizeof(Str));
+      uint8_t *nu = (uint8_t *)aalloc(c, l->n + r->n + 1);
+      if (l->n) { memcpy(nj, l->jstrs, l->n * sizeof(Str)); memcpy(nu, l->jundef, l->n); }
+      if (r->n) { memcpy(nj + l->n, r->jstrs, r->n * sizeof(Str)); memcpy(nu + l->n, r->jundef, r->n); }
+      l->jstrs = nj; l->jundef = nu; l->n += r->n;
+      return 1;
+    }
+    default: return 0;
+  }
+}
+
+static CIt *split_item(CDoc *d, CIt *left, int64_t diff) { /* splitItem (Item.js:85-125) */
+  CIt *r = (CIt *)aalloc(d->c, sizeof(CIt));
+  *r = *left;
+  r->clock = left->clock + diff;
+  r->left = left;
+  r->has_origin = 1;
+  r->origin.client = left->client; r->origin.clock = left->clock + diff - 1;
+  r->rightp = left->rightp;
+  r->ct = content_splice(d->c, left->ct, diff);
+  r->len = left->len - diff;
+  r->gen_before = r->gen_conf = 0;
+  r->type = NULL;
+  Content *lc = content_copy(d->c, left->ct);
+  content_truncate(d->c, lc, diff);
+  left->ct = lc;
+  left->rightp = r;
+  if (r->rightp) r->rightp->left = r;
+  ms_push(d, r);
+  if (r->has_psub && r->rightp == NULL) map_set(d, r->parent, r->psub, r);
+  left->len = diff;
+  return r;
+}
+static CIt *get_clean_start(CDoc *d, JID id) { /* getItemCleanStart / findIndexCleanStart */
+  CCl *s = cd_client(d, id.client);
+  size_t idx = cd_find_index(d, s, id.clock);
+  CIt *st = s->a[idx];
+  if (st->clock < id.clock && !st->gc) {
+    CIt *r = split_item(d, st, id.clock - st->clock);
+    cl_insert(d, s, idx + 1, r);
+    return r;
+  }
+  return st;
+}
+static CIt *get_clean_end(CDoc *d, JID id) { /* getItemCleanEnd */
+  CCl *s = cd_client(d, id.client);
+  size_t idx = cd_find_index(d, s, id.clock);
+  CIt *st = s->a[idx];
+  if (id.clock != st->clock + st->len - 1 && !st->gc) cl_insert(d, s, idx + 1, split_item(d, st, id.clock - st->clock + 1));
+  return st;
+}
+
+static void it_delete(CDoc *d, CIt *it);
+static void ctype_delete(CDoc *d, CType *t) { /* ContentType.delete */
+  for (CIt *x = t->start; x; x = x->rightp) {
+    if (!x->deleted) it_delete(d, x);
+    else ms_push(d, x);
+  }
+  for (size_t i = 0; i < t->mn; i++) {
+    CIt *x = t->mv[i];
+    if (!x->deleted) it_delete(d, x);
+    else ms_push(d, x);
+  }
+  changed_del(d, t);
+}
+static void it_delete(CDoc *d, CIt *it) { /* Item.delete */
+  if (it->deleted) return;
+  it->deleted = 1;
+  tds_add(d, &d->tx->ds, it->client, it->clock, it->len);
+  changed_add(d, it->parent);
+  if (it->ct->ref == 7 && it->type) ctype_delete(d, it->type);
+}
+static void cd_replace(CDoc *d, CIt *old, CIt *nw) { /* replaceStruct */
+  CCl *s = cd_client(d, old->client);
+  s->a[cd_find_index(d, s, old->clock)] = nw;
+}
+static void it_gc(CDoc *d, CIt *it, int parent_gcd) { /* Item.gc */
+  if (!it->deleted) fail(d->c, YMO_ERR_UNEXPECTED);
+  if (it->ct->ref == 7 && it->type) { /* ContentType.gc */
+    CType *t = it->type;
+    for (CIt *x = t->start; x; x = x->rightp) it_gc(d, x, 1);
+    t->start = NULL;
+    for (size_t i = 0; i < t->mn; i++)
+      for (CIt *x = t->mv[i]; x; x = x->left) it_gc(d, x, 1);
+    t->mn = 0;
+  }
+  if (parent_gcd) {
+    if (it->gc) return;
+    CIt *g = (CIt *)aalloc(d->c, sizeof(CIt));
+    memset(g, 0, sizeof(*g));
+    g->gc = 1; g->client = it->client; g->clock = it->clock; g->len = it->len; g->deleted = 1;
+    cd_replace(d, it, g);
+  } else {
+    Content *cd = (Content *)aalloc(d->c, sizeof(Content));
+    memset(cd, 0, sizeof(*cd));
+    cd->ref = 1; cd->dlen = it->len;
+    it->ct = cd;
+  }
+}
+
+/* Item.getMissing: the client of a missing dependency, or -1 (and left / right / parent resolved) */
+static int64_t it_missing(CDoc *d, CIt *it) {
+  if (it->gc) return -1;
+  if (it->has_origin && it->origin.client != it->client && it->origin.clock >= cd_state(d, it->origin.client)) return it->origin.client;
+  if (it->has_right && it->right.client != it->client && it->right.clock >= cd_state(d, it->right.client)) return it->right.client;
+  if (it->pkind == 2 && it->client != it->pid.client && it->pid.clock >= cd_state(d, it->pid.client)) return it->pid.client;
+  if (it->has_origin) {
+    it->left = get_clean_end(d, it->origin);
+    it->origin = it_last(it->left);
+  }
+  if (it->has_right) {
+    it->rightp = get_clean_start(d, it->right);
+    it->right.client = it->rightp->client; it->right.clock = it->rightp->clock;
+  }
+  int par_set = it->pkind != 0;  /* `this.parent` truthy before the neighbour rules */
+  if ((it->left && it->left->gc) || (it->rightp && it->rightp->gc)) { par_set = 0; it->parent = NULL; it->pkind = 0; }
+  if (!par_set) {
+    if (it->left && !it->left->gc) { it->parent = it->left->parent; it->has_psub = it->left->has_psub; it->psub = it->left->psub; }
+    if (it->rightp && !it->rightp->gc) { it->parent = it->rightp->parent; it->has_psub = it->rightp->has_psub; it->psub = it->rightp->psub; }
+  } else if (it->pkind == 2) {
+    CIt *p = cd_get(d, it->pid);
+    it->parent = (!p->gc && p->ct->ref == 7) ? p->type : NULL;  /* a GC'd parent, or no type: GC */
+  }
+  return -1;
+}
+static void it_integrate(CDoc *d, CIt *it, int64_t off) {
+  if (it->gc) { /* GC.integrate */
+    if (off > 0) { it->clock += off; it->len -= off; }
+    cd_add_struct(d, it);
+    return;
+  }
+  if (off > 0) {
+    it->clock += off;
+    JID p = {it->client, it->clock - 1};
+    it->left = get_clean_end(d, p);
+    it->origin = it_last(it->left);
+    it->has_origin = 1;
+    it->ct = content_splice(d->c, it->ct, off);
+    it->len -= off;
+  }
+  if (!it->parent) { /* parent is not defined: integrate a GC struct instead */
+    CIt *g = (CIt *)aalloc(d->c, sizeof(CIt));
+    memset(g, 0, sizeof(*g));
+    g->gc = 1; g->client = it->client; g->clock = it->clock; g->len = it->len; g->deleted = 1;
+    cd_add_struct(d, g);
+    return;
+  }
+  CType *P = it->parent;
+  if ((!it->left && (!it->rightp || it->rightp->left != NULL)) || (it->left && it->left->rightp != it->rightp)) {
+    CIt *left = it->left, *o;
+    if (left) o = left->rightp;
+    else if (it->has_psub) { o = map_get(P, it->psub); while (o && o->left) o = o->left; }
+    else o = P->start;
+    const uint32_t gb = ++d->gen;
+    uint32_t gcf = ++d->gen;
+    while (o && o != it->rightp) {
+      o->gen_before = gb;
+      o->gen_conf = gcf;
+      if (jid_eq(it->has_origin, it->origin, o->has_origin, o->origin)) {
+        if (o->client < it->client) { left = o; gcf = ++d->gen; }
+        else if (jid_eq(it->has_right, it->right, o->has_right, o->right)) break;
+      } else if (o->has_origin) {
+        CIt *oo = cd_get(d, o->origin);
+        if (oo->gen_before == gb) {
+          if (oo->gen_conf != gcf) { left = o; gcf = ++d->gen; }
+        } else break;
+      } else break;
+      o = o->rightp;
+    }
+    it->left = left;
+  }
+  if (it->left) {
+    CIt *r = it->left->rightp;
+    it->rightp = r;
+    it->left->rightp = it;
+  } else {
+    CIt *r;
+    if (it->has_psub) { r = map_get(P, it->psub); while (r && r->left) r = r->left; }
+    else { r = P->start; P->start = it; }
+    it->rightp = r;
+  }
+  if (it->rightp) it->rightp->left = it;
+  else if (it->has_psub) {
+    map_set(d, P, it->psub, it);
+    if (it->left) it_delete(d, it->left);
+  }
+  cd_add_struct(d, it);
+  if (it->ct->ref == 7) { it->type = ct_new(d); it->type->item = it; it->type->tref = (int)it->ct->typeRef; } /* type._integrate */
+  if (it->ct->ref == 1) { /* ContentDeleted.integrate */
+    tds_add(d, &d->tx->ds, it->client, it->clock, it->ct->dlen);
+    it->deleted = 1;
+  }
+  changed_add(d, P);
+  if ((P->item && P->item->deleted) || (it->has_psub && it->rightp)) it_delete(d, it);
+}
+
+static void cd_pend_clear(CDoc *d) { d->npend = 0; }
+static CPend *cd_pend(CDoc *d, int64_t client) {
+  for (size_t i = 0; i < d->npend; i++) if (d->pend[i].live && d->pend[i].client == client) return &d->pend[i];
+  return NULL;
+}
+static void refs_sort(CIt **a, size_t n) { /* stable sort by clock (V8 TimSort is stable) */
+  for (size_t i = 1; i < n; i++) {
+    CIt *v = a[i];
+    size_t j = i;
+    while (j > 0 && a[j - 1]->clock > v->clock) { a[j] = a[j - 1]; j--; }
+    a[j] = v;
+  }
+}
+static void resume_integration(CDoc *d) { /* resumeStructIntegration (encoding.js:225-321) */
+  Ctx *c = d->c;
+  size_t nids = 0;
+  int64_t *ids = (int64_t *)aalloc(c, (d->npend + 1) * sizeof(int64_t));
+  for (size_t i = 0; i < d->npend; i++) if (d->pend[i].live) ids[nids++] = d->pend[i].client;
+  for (size_t i = 1; i < nids; i++) { int64_t v = ids[i]; size_t j = i; while (j > 0 && ids[j - 1] > v) { ids[j] = ids[j - 1]; j--; } ids[j] = v; }
+  if (nids == 0) return;
+  CPend *cur = NULL;
+  #define NEXT_TARGET()                                                      \
+    do {                                                                     \
+      cur = cd_pend(d, ids[nids - 1]);                                       \
+      while (cur->n == cur->i) {                                             \
+        nids--;                                                              \
+        if (nids > 0) cur = cd_pend(d, ids[nids - 1]);                       \
+        else { cd_pend_clear(d); cur = NULL; break; }                        \
+      }                                                                      \
+    } while (0)
+  NEXT_TARGET();
+  if (cur == NULL && d->nstack == 0) return;
+  CIt *head = d->nstack > 0 ? d->stack[--d->nstack] : cur->refs[cur->i++];
+  int64_t *sc_client = (int64_t *)aalloc(c, 64 * sizeof(int64_t)), *sc_clock = (int64_t *)aalloc(c, 64 * sizeof(int64_t));
+  size_t nsc = 0, capsc = 64;
+  for (;;) {
+    int64_t local = -1;
+    for (size_t i = 0; i < nsc; i++) if (sc_client[i] == head->client) { local = sc_clock[i]; break; }
+    if (local < 0) {
+      local = cd_state(d, head->client);
+      if (nsc == capsc) {
+        int64_t *a = (int64_t *)aalloc(c, 2 * capsc * sizeof(int64_t)), *b = (int64_t *)aalloc(c, 2 * capsc * sizeof(int64_t));
+        memcpy(a, sc_client, nsc * sizeof(int64_t)); memcpy(b, sc_clock, nsc * sizeof(int64_t));
+        sc_client = a; sc_clock = b; capsc *= 2;
+      }
+      sc_client[nsc] = head->client; sc_clock[nsc] = local; nsc++;
+    }
+    int64_t off = head->clock < local ? local - head->clock : 0;
+    if (head->clock + off != local) {
+      CPend *sr = cd_pend(d, head->client);
+      if (sr && sr->n != sr->i) {
+        CIt *r = sr->refs[sr->i];
+        if (r->clock < head->clock) {
+          sr->refs[sr->i] = head;
+          head = r;
+          CIt **rest = sr->refs + sr->i;
+          size_t rn = sr->n - sr->i;
+          CIt **na = (CIt **)aalloc(c, (rn + 1) * sizeof(CIt *));
+          memcpy(na, rest, rn * sizeof(CIt *));
+          refs_sort(na, rn);
+          sr->refs = na; sr->n = rn; sr->i = 0;
+          continue;
+        }
+      }
+      CGROW(c, d->stack, d->nstack, d->capstack, CIt *);
+      d->stack[d->nstack++] = head;
+      return;
+    }
+    int64_t missing = it_missing(d, head);
+    if (missing < 0) {
+      if (off == 0 || off < head->len) {
+        it_integrate(d, head, off);
+        for (size_t i = 0; i < nsc; i++) if (sc_client[i] == head->client) sc_clock[i] = head->clock + head->len;
+      }
+      if (d->nstack > 0) head = d->stack[--d->nstack];
+      else if (cur && cur->i < cur->n) head = cur->refs[cur->i++];
+      else {
+        NEXT_TARGET();
+        if (cur == NULL) break;
+        head = cur->refs[cur->i++];
+      }
+    } else {
+      CPend *sr = cd_pend(d, missing);
+      if (!sr || sr->n == sr->i) {
+        CGROW(c, d->stack, d->nstack, d->capstack, CIt *);
+        d->stack[d->nstack++] = head;
+        return;
+      }
+      CGROW(c, d->stack, d->nstack, d->capstack, CIt *);
+      d->stack[d->nstack++] = head;
+      head = sr->refs[sr->i++];
+    }
+  }
+  #undef NEXT_TARGET
+  cd_pend_clear(d);
+}
+
+static void cd_split_into(CDoc *d, CCl *s, size_t at, CIt *it) { cl_insert(d, s, at, it); }
+/* readAndApplyDeleteSet over a decoded delete set (DeleteSet.js:270-323); the unapplied ranges become a
+   pending delete reader */
+static void apply_ds(CDoc *d, const DSet *ds) {
+  DSet un;
+  memset(&un, 0, sizeof(un));
+  for (size_t ci = 0; ci < ds->n; ci++) {
+    int64_t client = ds->cl[ci].client;
+    CCl *s = cd_client(d, client);
+    int64_t state = cd_state(d, client);
+    for (size_t k = 0; k < ds->cl[ci].n; k++) {
+      int64_t clock = ds->cl[ci].items[k].clock, end = clock + ds->cl[ci].items[k].len;
+      if (clock < state) {
+        if (state < end) tds_add(d, &un, client, state, end - state);
+        size_t idx = cd_find_index(d, s, clock);
+        CIt *st = s->a[idx];
+        if (!st->deleted && st->clock < clock) {
+          cd_split_into(d, s, idx + 1, split_item(d, st, clock - st->clock));
+          idx++;
+        }
+        while (idx < s->n) {
+          st = s->a[idx++];
+          if (st->clock < end) {
+            if (!st->deleted) {
+              if (end < st->clock + st->len) cd_split_into(d, s, idx, split_item(d, st, end - st->clock));
+              it_delete(d, st);
+            }
+          } else break;
+        }
+      } else tds_add(d, &un, client, clock, end - clock);
+    }
+  }
+  if (un.n > 0) {
+    CGROW(d->c, d->pdel, d->npdel, d->cappdel, DSet);
+    d->pdel[d->npdel++] = un;
+  }
+}
+/* readClientsStructRefs (encoding.js:127-198): per section a ref list (a repeated client replaces the
+   earlier list: Map.set), GC for info & 31 == 0 */
+static void read_refs(CDoc *d, UDec *u, CPend **out, size_t *nout) {
+  Ctx *c = d->c;
+  uint32_t nsec = rd_vu(c, &u->rest);
+  CPend *lst = (CPend *)aalloc(c, (nsec + 1) * sizeof(CPend));
+  size_t nl = 0;
+  for (uint32_t si = 0; si < nsec; si++) {
+    uint32_t ns = rd_vu(c, &u->rest);
+    int64_t client = ud_client(c, u);
+    int64_t clock = rd_vu(c, &u->rest);
+    CIt **refs = (CIt **)aalloc(c, (ns + 1) * sizeof(CIt *));
+    for (uint32_t k = 0; k < ns; k++) {
+      int info = ud_info(c, u);
+      CIt *it = (CIt *)aalloc(c, sizeof(CIt));
+      memset(it, 0, sizeof(*it));
+      it->client = client; it->clock = clock;
+      if ((info & 31) != 0) {
+        int cant_copy = (info & 0xC0) == 0;
+        if (info & 0x80) { it->has_origin = 1; it->origin = ud_left(c, u); }
+        if (info & 0x40) { it->has_right = 1; it->right = ud_right(c, u); }
+        if (cant_copy) {
+          if (ud_parent_info(c, u)) { it->pkind = 1; it->pkey = ud_string(c, u); it->parent = cd_root(d, it->pkey); }
+          else { it->pkind = 2; it->pid = ud_left(c, u); }
+          if (info & 0x20) { it->has_psub = 1; it->psub = ud_string(c, u); }
+        }
+        if ((info & 31) == 10) fail(c, YMO_ERR_TYPE);  /* contentRefs[10] is undefined (13.4.9) */
+        it->ct = read_content(c, u, info);
+        it->len = content_len(it->ct);
+      } else {
+        it->gc = 1;
+        it->deleted = 1;
+        it->len = ud_len(c, u);
+      }
+      refs[k] = it;
+      clock += it->len;
+    }
+    size_t at = nl;
+    for (size_t q = 0; q < nl; q++) if (lst[q].client == client) at = q;
+    if (at == nl) nl++;
+    lst[at].client = client; lst[at].refs = refs; lst[at].n = ns; lst[at].i = 0; lst[at].live = 1;
+  }
+  *out = lst;
+  *nout = nl;
+}
+static void try_merge_left(CDoc *d, CCl *s, size_t pos) { /* tryToMergeWithLeft (Transaction.js:165-176) */
+  CIt *l = s->a[pos - 1], *r = s->a[pos];
+  if (l->deleted != r->deleted || l->gc != r->gc) return;
+  int ok;
+  if (l->gc) { l->len += r->len; ok = 1; }
+  else {
+    JID ll = it_last(l);
+    ok = jid_eq(r->has_origin, r->origin, 1, ll) && l->rightp == r && jid_eq(l->has_right, l->right, r->has_right, r->right) &&
+         l->client == r->client && l->clock + l->len == r->clock && l->deleted == r->deleted && l->ct->ref == r->ct->ref;
+    if (ok) {
+      Content *m = content_copy(d->c, l->ct);
+      ok = content_merge(d->c, m, r->ct);
+      if (ok) {
+        l->ct = m;
+        l->rightp = r->rightp;
+        if (l->rightp) l->rightp->left = l;
+        l->len += r->len;
+      }
+    }
+  }
+  if (ok) {
+    cl_remove(s, pos);
+    if (!r->gc && r->has_psub && r->parent && map_get(r->parent, r->psub) == r) map_set(d, r->parent, r->psub, l);
+  }
+}
+static CTx *tx_new(CDoc *d, int local) { /* new Transaction: beforeState = getStateVector(store) */
+  Ctx *c = d->c;
+  CTx *t = (CTx *)aalloc(c, sizeof(CTx));
+  memset(t, 0, sizeof(*t));
+  t->local = local;
+  t->nbc = d->ncl;
+  t->bc_client = (int64_t *)aalloc(c, (d->ncl + 1) * sizeof(int64_t));
+  t->bc_clock = (int64_t *)aalloc(c, (d->ncl + 1) * sizeof(int64_t));
+  for (size_t i = 0; i < d->ncl; i++) { t->bc_client[i] = d->cl[i].client; t->bc_clock[i] = cl_state(&d->cl[i]); }
+  return t;
+}
+
+/* ---- YText._callObserver's remote formatting cleanup (YText.js:803-856) ---- */
+typedef struct { Str *k; Val **v; size_t n, cap; } AttrMap; /* Map<string, any> of current attributes */
+static Val *am_get(const AttrMap *m, Str k) {
+  for (size_t i = 0; i < m->n; i++) if (str_eq(m->k[i], k)) return m->v[i];
+  return NULL;
+}
+static void am_set(Ctx *c, AttrMap *m, Str k, Val *v) {
+  for (size_t i = 0; i < m->n; i++) if (str_eq(m->k[i], k)) { m->v[i] = v; return; }
+  if (m->n == m->cap) {
+    size_t nc = m->cap ? m->cap * 2 : 8;
+    Str *nk = (Str *)aalloc(c, nc * sizeof(Str));
+    Val **nv = (Val **)aalloc(c, nc * sizeof(Val *));
+    if (m->n) { memcpy(nk, m->k, m->n * sizeof(Str)); memcpy(nv, m->v, m->n * sizeof(Val *)); }
+    m->k = nk; m->v = nv; m->cap = nc;
+  }
+  m->k[m->n] = k; m->v[m->n] = v; m->n++;
+}
+static void am_del(AttrMap *m, Str k) {
+  for (size_t i = 0; i < m->n; i++)
+    if (str_eq(m->k[i], k)) { m->k[i] = m->k[m->n - 1]; m->v[i] = m->v[m->n - 1]; m->n--; return; }
+}
+static AttrMap am_copy(Ctx *c, const AttrMap *m) {
+  AttrMap r = {0};
+  for (size_t i = 0; i < m->n; i++) am_set(c, &r, m->k[i], m->v[i]);
+  return r;
+}
+static void am_update(Ctx *c, AttrMap *m, const Content *f) { /* updateCurrentAttributes (YText.js:182-189) */
+  if (f->jval->t == V_NULL) am_del(m, f->key);
+  else am_set(c, m, f->key, f->jval);
+}
+/* (x || null) === v for an attribute value x (NULL: absent) and a ContentFormat value v: JS strict equality,
+   objects / arrays / typed arrays by identity */
+static int or_null_eq(const Val *x, const Val *v) {
+  if (x == NULL || !js_truthy(x)) return v->t == V_NULL;
+  if (x->t != v->t) return 0;
+  switch (x->t) {
+    case V_BOOL: return x->b == v->b;
+    case V_NUM: return x->num == v->num;
+    case V_STR: return str_eq(x->s, v->s);
+    case V_BIGINT: return memcmp(x->big, v->big, 8) == 0;
+    default: return x == v;
+  }
+}
+static int is_text_content(const CIt *it) { return it->ct->ref == 4 || it->ct->ref == 5; }
+/* cleanupFormattingGap (YText.js:348-374) */
+static int cleanup_gap(CDoc *d, CIt *start, CIt *end, const AttrMap *sa, AttrMap *ea) {
+  while (end && !is_text_content(end)) {
+    if (!end->deleted && end->ct->ref == 6) am_update(d->c, ea, end->ct);
+    end = end->rightp;
+  }
+  int n = 0;
+  while (start != end) {
+    if (!start->deleted && start->ct->ref == 6) {
+      const Content *f = start->ct;
+      if (!or_null_eq(am_get(ea, f->key), f->jval) || or_null_eq(am_get(sa, f->key), f->jval)) { it_delete(d, start); n++; }
+    }
+    start = start->rightp;
+  }
+  return n;
+}
+static void cleanup_ytext(CDoc *d, CType *t) { /* cleanupYTextFormatting (YText.js:412-437) */
+  CIt *start = t->start, *end = t->start;
+  AttrMap sa = {0}, cur = {0};
+  while (end) {
+    if (!end->deleted) {
+      if (end->ct->ref == 6) am_update(d->c, &cur, end->ct);
+      else if (is_text_content(end)) {
+        cleanup_gap(d, start, end, &sa, &cur);
+        sa = am_copy(d->c, &cur);
+        start = end;
+      }
+    }
+    end = end->rightp;
+  }
+}
+static void cleanup_contextless(CDoc *d, CIt *it) { /* cleanupContextlessFormattingGap (YText.js:380-398) */
+  while (it && it->rightp && (it->rightp->deleted || !is_text_content(it->rightp))) it = it->rightp;
+  AttrMap seen = {0};
+  while (it && (it->deleted || !is_text_content(it))) {
+    if (!it->deleted && it->ct->ref == 6) {
+      if (am_get(&seen, it->ct->key)) it_delete(d, it);
+      else am_set(d->c, &seen, it->ct->key, it->ct->jval);
+    }
+    it = it->left;
+  }
+}
+typedef struct { int kind; int found; CType *t; } ObsCb;
+static void obs_visit(CDoc *d, ObsCb *cb, CIt *st) {
+  switch (cb->kind) {
+    case 0: if (!st->deleted && st->ct->ref == 6) cb->found = 1; break; /* a new non-deleted format item */
+    case 1: if (!st->gc && !cb->found && st->parent == cb->t && st->ct->ref == 6) cb->found = 1; break;
+    case 2: if (!st->gc && st->parent == cb->t) cleanup_contextless(d, st); break;
+  }
+}
+static size_t find_clean_start(CDoc *d, CCl *s, int64_t clock) { /* findIndexCleanStart (StructStore.js:173-181) */
+  size_t idx = cd_find_index(d, s, clock);
+  CIt *st = s->a[idx];
+  if (st->clock < clock && !st->gc) {
+    cl_insert(d, s, idx + 1, split_item(d, st, clock - st->clock));
+    return idx + 1;
+  }
+  return idx;
+}
+/* iterateStructs (StructStore.js:259-273), splitting at both ends under d->tx */
+static void iterate_structs(CDoc *d, CCl *s, int64_t clock, int64_t len, ObsCb *cb) {
+  if (len == 0) return;
+  int64_t end = clock + len;
+  size_t idx = find_clean_start(d, s, clock);
+  do {
+    CIt *st = s->a[idx++];
+    if (end < st->clock + st->len) find_clean_start(d, s, end);
+    obs_visit(d, cb, st);
+  } while (idx < s->n && s->a[idx]->clock < end);
+}
+/* iterateDeletedStructs (DeleteSet.js:58-65): Map.forEach and the ranges loop both see entries appended
+   while they run */
+static void iterate_deleted(CDoc *d, DSet *ds, ObsCb *cb) {
+  for (size_t ci = 0; ci < ds->n; ci++) {
+    for (size_t k = 0; k < ds->cl[ci].n; k++) {
+      DItem di = ds->cl[ci].items[k];
+      iterate_structs(d, cd_client(d, ds->cl[ci].client), di.clock, di.len, cb);
+    }
+  }
+}
+static void ytext_observer(CDoc *d, CTx *x, CType *t, CTx **nested) {
+  ObsCb cb = {0, 0, t};
+  d->tx = x;
+  for (size_t ci = 0; ci < d->ncl && !cb.found; ci++) { /* afterState entries (store.clients order) */
+    int64_t before = tx_before_at(x, ci), after = cl_state(&d->cl[ci]);
+    if (after == before) continue;
+    iterate_structs(d, &d->cl[ci], before, after, &cb); /* (len = afterClock, as the reference passes it) */
+  }
+  if (!cb.found) { cb.kind = 1; iterate_deleted(d, &x->ds, &cb); }
+  /* transact(doc, t => ...): the first observer opens a new local transaction; it stays doc._transaction
+     (it is cleaned up after this one), so every later observer's transact joins it */
+  if (!*nested) *nested = tx_new(d, 1);
+  d->tx = *nested;
+  if (cb.found) cleanup_ytext(d, t);
+  else { ObsCb c2 = {2, 0, t}; iterate_deleted(d, &(*nested)->ds, &c2); }
+  d->tx = x;
+}
+/* cleanupTransactions (Transaction.js:244-367) for one transaction; returns the transaction the observers
+   opened (or NULL) */
+static CTx *tx_cleanup(CDoc *d, CTx *x) {
+  Ctx *c = d->c;
+  d->tx = x;
+  ds_sort_and_merge_mode(c, &x->ds, 1);
+  CTx *nested = NULL;
+  if (!x->local) { /* observers of the changed types, in Map order: only Y.Text / Y.XmlText act */
+    size_t nchg = x->nchg;
+    CType **chg = (CType **)aalloc(c, (nchg + 1) * sizeof(CType *));
+    if (nchg) memcpy(chg, x->chg, nchg * sizeof(CType *));
+    for (size_t i = 0; i < nchg; i++) {
+      CType *t = chg[i];
+      if (t->item && t->item->deleted) continue;
+      if (t->tref == 2 || t->tref == 6) ytext_observer(d, x, t, &nested);
+    }
+  }
+  d->tx = x;
+  for (size_t ci = 0; ci < x->ds.n; ci++) { /* tryGcDeleteSet (doc.gc) */
+    DClient *dc = &x->ds.cl[ci];
+    CCl *s = cd_client(d, dc->client);
+    for (size_t k = dc->n; k-- > 0;) {
+      int64_t clock = dc->items[k].clock, end = clock + dc->items[k].len;
+      for (size_t si = cd_find_index(d, s, clock); si < s->n && s->a[si]->clock < end; si++) {
+        CIt *st = s->a[si];
+        if (!st->gc && st->deleted) it_gc(d, st, 0);
+      }
+    }
+  }
+  for (size_t ci = 0; ci < x->ds.n; ci++) { /* tryMergeDeleteSet */
+    DClient *dc = &x->ds.cl[ci];
+    CCl *s = cd_client(d, dc->client);
+    for (size_t k = dc->n; k-- > 0;) {
+      int64_t clock = dc->items[k].clock, len = dc->items[k].len;
+      size_t mr = cd_find_index(d, s, clock + len - 1) + 1;
+      if (mr > s->n - 1) mr = s->n - 1;
+      for (size_t si = mr; si > 0 && s->a[si]->clock >= clock; si--) try_merge_left(d, s, si);
+    }
+  }
+  for (size_t ci = 0; ci < d->ncl; ci++) { /* the clients whose state changed (afterState) */
+    CCl *s = &d->cl[ci];
+    int64_t before = tx_before_at(x, ci);
+    if (before == cl_state(s)) continue;
+    size_t first = cd_find_index(d, s, before);
+    if (first < 1) first = 1;
+    for (size_t i = s->n - 1; i >= first && i > 0; i--) try_merge_left(d, s, i);
+  }
+  for (size_t q = 0; q < x->nms; q++) { /* _mergeStructs */
+    CIt *m = x->ms[q];
+    CCl *s = cd_client(d, m->client);
+    size_t pos = cd_find_index(d, s, m->clock);
+    if (pos + 1 < s->n) try_merge_left(d, s, pos + 1);
+    if (pos > 0) try_merge_left(d, s, pos);
+  }
+  return nested;
+}
+static void cd_transact(CDoc *d, UDec *u) { /* transact(readUpdateV2, local = false) + cleanupTransactions */
+  Ctx *c = d->c;
+  CTx *x = tx_new(d, 0);
+  d->tx = x;
+  /* readStructs */
+  CPend *refs;
+  size_t nrefs;
+  read_refs(d, u, &refs, &nrefs);
+  for (size_t q = 0; q < nrefs; q++) { /* mergeReadStructsIntoPendingReads */
+    CPend *p = cd_pend(d, refs[q].client);
+    if (!p) {
+      CGROW(c, d->pend, d->npend, d->cappend, CPend);
+      d->pend[d->npend++] = refs[q];
+    } else {
+      size_t rn = p->n - p->i;
+      CIt **na = (CIt **)aalloc(c, (rn + refs[q].n + 1) * sizeof(CIt *));
+      memcpy(na, p->refs + p->i, rn * sizeof(CIt *));
+      memcpy(na + rn, refs[q].refs, refs[q].n * sizeof(CIt *));
+      refs_sort(na, rn + refs[q].n);
+      p->refs = na; p->n = rn + refs[q].n; p->i = 0;
+    }
+  }
+  resume_integration(d);
+  { /* cleanupPendingStructs (the finished entries leave the Map; the rest keep their order) */
+    size_t w = 0;
+    for (size_t q = 0; q < d->npend; q++) {
+      CPend *p = &d->pend[q];
+      if (!p->live || p->i == p->n) continue;
+      p->refs += p->i; p->n -= p->i; p->i = 0;
+      d->pend[w++] = *p;
+    }
+    d->npend = w;
+  }
+  { /* tryResumePendingDeleteReaders */
+    DSet *pr = d->pdel;
+    size_t np = d->npdel;
+    d->pdel = NULL; d->npdel = 0; d->cappdel = 0;
+    for (size_t q = 0; q < np; q++) apply_ds(d, &pr[q]);
+  }
+  { /* readAndApplyDeleteSet: each client's ranges are applied as read (the clients are independent) */
+    uint32_t n = rd_vu(c, &u->rest);
+    for (uint32_t i = 0; i < n; i++) {
+      ud_reset_ds(u);
+      int64_t client = rd_vu(c, &u->rest);
+      uint32_t m = rd_vu(c, &u->rest);
+      DSet one;
+      memset(&one, 0, sizeof(one));
+      DClient *dc = ds_get_or_add(c, &one, client);
+      for (uint32_t j = 0; j < m; j++) {
+        int64_t clock = ud_ds_clock(c, u);
+        int64_t len = ud_ds_len(c, u);
+        dc_push(c, dc, clock, len);
+      }
+      apply_ds(d, &one);
+    }
+  }
+  /* cleanupTransactions: this one, then the one its observers opened (local: its observers do nothing) */
+  CTx *nested = tx_cleanup(d, x);
+  if (nested) tx_cleanup(d, nested);
+  d->tx = NULL;
+}
+static void cit_write(CDoc *d, UEnc *e, const CIt *it) { /* Item.write / GC.write with offset 0 */
+  Ctx *c = d->c;
+  if (it->gc) { ue_info(c, e, 0); ue_len(c, e, it->len); return; }
+  int info = (it->ct->ref & 31) | (it->has_origin ? 0x80 : 0) | (it->has_right ? 0x40 : 0) | (it->has_psub ? 0x20 : 0);
+  ue_info(c, e, info);
+  if (it->has_origin) ue_left(c, e, it->origin);
+  if (it->has_right) ue_right(c, e, it->right);
+  if (!it->has_origin && !it->has_right) {
+    CType *p = it->parent;
+    if (!p) fail(c, YMO_ERR_UNEXPECTED);
+    if (!p->item) { ue_parent_info(c, e, 1); ue_string(c, e, p->key); }
+    else { JID pid = {p->item->client, p->item->clock}; ue_parent_info(c, e, 0); ue_left(c, e, pid); }
+    if (it->has_psub) ue_string(c, e, it->psub);
+  }
+  content_write(c, e, it->ct, 0);
+}
+static Buf *compact_impl(Ctx *c, const uint8_t *const *upds, const size_t *lens, size_t n, int v2) {
+  CDoc d;
+  memset(&d, 0, sizeof(d));
+  d.c = c;
+  for (size_t k = 0; k < n; k++) {
+    UDec u;
+    udec_init(c, &u, upds[k], lens[k], v2);
+    cd_transact(&d, &u);
+  }
+  /* every input applied completely (the fixtures hold only such documents) */
+  for (size_t q = 0; q < d.npend; q++) if (d.pend[q].live) fail(c, YMO_ERR_UNSUPPORTED);
+  if (d.nstack > 0 || d.npdel > 0) fail(c, YMO_ERR_UNSUPPORTED);
+  UEnc e;
+  uenc_init(c, &e, v2);
+  /* writeClientsStructs: clients descending, every struct from clock 0 */
+  size_t *ord = (size_t *)aalloc(c, (d.ncl + 1) * sizeof(size_t));
+  for (size_t i = 0; i < d.ncl; i++) ord[i] = i;
+  for (size_t i = 1; i < d.ncl; i++) { size_t v = ord[i], j = i; while (j > 0 && d.cl[ord[j - 1]].client < d.cl[v].client) { ord[j] = ord[j - 1]; j--; } ord[j] = v; }
+  wr_vu(c, e.rest, (int64_t)d.ncl);
+  for (size_t oi = 0; oi < d.ncl; oi++) {
+    CCl *s = &d.cl[ord[oi]];
+    wr_vu(c, e.rest, (int64_t)s->n);
+    ue_client(c, &e, s->client);
+    wr_vu(c, e.rest, 0);
+    for (size_t i = 0; i < s->n; i++) cit_write(&d, &e, s->a[i]);
+  }
+  /* createDeleteSetFromStructStore (store.clients order) + writeDeleteSet */
+  DSet ds;
+  memset(&ds, 0, sizeof(ds));
+  for (size_t ci = 0; ci < d.ncl; ci++) {
+    CCl *s = &d.cl[ci];
+    DClient *dc = NULL;
+    for (size_t i = 0; i < s->n; i++) {
+      CIt *st = s->a[i];
+      if (!st->deleted) continue;
+      int64_t clock = st->clock, len = st->len;
+      while (i + 1 < s->n && s->a[i + 1]->clock == clock + len && s->a[i + 1]->deleted) len += s->a[++i]->len;
+      if (!dc) dc = ds_get_or_add(c, &ds, s->client);
+      dc_push(c, dc, clock, len);
+    }
+  }
+  ds_write(c, &e, &ds);
+  return uenc_finish(c, &e);
+}
+
+/* ------------------------------------------------------------------------------------------------ */
 /* public API                                                                                      */
 /* ------------------------------------------------------------------------------------------------ */
 static int finish_out(Ctx *c, Buf *b, uint8_t **out, size_t *out_len) {
@@ -2248,6 +3209,18 @@ int ymo_merge(const uint8_t *const *upds, const size_t *lens, size_t n, int fmt,
   int code = setjmp(c.jb);
   if (code) { ctx_free(&c); return code; }
   Buf *b = merge_impl(&c, upds, lens, n, fmt == 2);
+  int rc = finish_out(&c, b, out, out_len);
+  ctx_free(&c);
+  return rc;
+}
+
+int ymo_compact(const uint8_t *const *upds, const size_t *lens, size_t n, int fmt, uint8_t **out, size_t *out_len) {
+  *out = NULL; *out_len = 0;
+  Ctx c;
+  memset(&c, 0, sizeof(c));
+  int code = setjmp(c.jb);
+  if (code) { ctx_free(&c); return code; }
+  Buf *b = compact_impl(&c, upds, lens, n, fmt == 2);
   int rc = finish_out(&c, b, out, out_len);
   ctx_free(&c);
   return rc;

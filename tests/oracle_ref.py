@@ -74,6 +74,7 @@ def lib():
         L.ymo_convert.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t)]
         L.ymo_meta.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t)]
         L.ymo_ds_merge.argtypes = L.ymo_merge.argtypes
+        L.ymo_compact.argtypes = L.ymo_merge.argtypes
         L.ymo_snapshot.argtypes = L.ymo_convert.argtypes
         L.ymo_free.argtypes = [ctypes.c_void_p]
         vp = ctypes.c_void_p
@@ -106,6 +107,20 @@ def merge(updates, fmt=1):
     out = ctypes.POINTER(ctypes.c_uint8)()
     olen = ctypes.c_size_t()
     st = L.ymo_merge(ptrs, lens, n, fmt, ctypes.byref(out), ctypes.byref(olen))
+    return st, (_take(out, olen) if st == 0 else None)
+
+
+def compact(updates, fmt=1):
+    """Doc round trip (13.4.9, gc: true): applyUpdate[V2] of each update in order, encodeStateAsUpdate[V2]
+    -> (status, bytes)."""
+    L = lib()
+    bufs = [_buf(u) for u in updates]
+    n = len(bufs)
+    ptrs = (ctypes.POINTER(ctypes.c_uint8) * max(1, n))(*[ctypes.cast(b[0], ctypes.POINTER(ctypes.c_uint8)) for b in bufs])
+    lens = (ctypes.c_size_t * max(1, n))(*[b[1] for b in bufs])
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    olen = ctypes.c_size_t()
+    st = L.ymo_compact(ptrs, lens, n, fmt, ctypes.byref(out), ctypes.byref(olen))
     return st, (_take(out, olen) if st == 0 else None)
 
 

@@ -1,0 +1,38 @@
+"""Doc round-trip compaction: the oracle's C restatement of yjs 13.4.9's Doc engine
+(oracle/ymerge_oracle.c ymo_compact) pinned against the reference's own outputs for every fixture
+(tests/golden/compact.json: golden merge inputs, workload documents C1-C5, randomized formatted-text
+histories)."""
+import collections
+
+import pytest
+
+import compact_cases
+import oracle_ref as O
+
+
+@pytest.mark.parametrize("group", sorted({c["group"] for c in compact_cases.load()}))
+def test_oracle_compact_matches_reference(group):
+    cases = [c for c in compact_cases.load() if c["group"] == group]
+    bad = []
+    for c in cases:
+        st, out = O.compact(c["inputs"], c["fmt"])
+        if st != 0 or not compact_cases.matches(c, out):
+            bad.append((c["id"], st))
+    assert not bad, f"{len(bad)}/{len(cases)} differ: {bad[:8]}"
+
+
+def test_compact_fixture_coverage():
+    n = collections.Counter(c["group"] for c in compact_cases.load())
+    assert n["fuzz_fmt"] >= 150 and n["wl_c5"] >= 8 and n["canon"] >= 300
+
+
+def test_compact_keeps_the_state_vector():
+    """The compacted document covers exactly the inputs' clocks: its state vector equals the one of
+    mergeUpdates(inputs) (compaction garbage-collects content, never structs)."""
+    for c in compact_cases.load():
+        if c["group"] not in ("fuzz_fmt", "c5_xml", "c2_text", "canon"):
+            continue
+        st, out = O.compact(c["inputs"], c["fmt"])
+        st2, merged = O.merge(c["inputs"], c["fmt"])
+        assert st == 0 and st2 == 0, c["id"]
+        assert O.sv_from_update(out, c["fmt"]) == O.sv_from_update(merged, c["fmt"]), c["id"]
