@@ -246,13 +246,27 @@ static napi_value RunAsync(napi_env env, napi_callback_info info) {
   if (!parse(env, info, *j, argv, argc)) { delete j; return nullptr; }
   // the typed arrays stay alive (and their memory in place) until the work completes
   for (size_t i = 2; i < argc; i++) napi_create_reference(env, argv[i], 1, &j->refs[j->nrefs++]);
-  napi_value promise, name;
-  if (napi_create_promise(env, &j->deferred, &promise) != napi_ok) { delete j; return nullptr; }
+  // failure paths: release the references, the work and the Job; a created promise is rejected
+  auto release = [&](napi_value err) {
+    if (j->deferred) napi_reject_deferred(env, j->deferred, err);
+    if (j->work) napi_delete_async_work(env, j->work);
+    for (size_t i = 0; i < j->nrefs; i++) napi_delete_reference(env, j->refs[i]);
+    delete j;
+  };
+  napi_value promise, name, msg, err;
+  if (napi_create_promise(env, &j->deferred, &promise) != napi_ok) {
+    j->deferred = nullptr;
+    release(nullptr);
+    napi_throw_error(env, "YMERGE_NAPI", "could not create the promise");
+    return nullptr;
+  }
   napi_create_string_utf8(env, "ymerge", NAPI_AUTO_LENGTH, &name);
   if (napi_create_async_work(env, nullptr, name, async_execute, async_complete, j, &j->work) != napi_ok ||
       napi_queue_async_work(env, j->work) != napi_ok) {
-    napi_throw_error(env, "YMERGE_NAPI", "could not queue the async work");
-    return nullptr;
+    napi_create_string_utf8(env, "ymerge: could not queue the async work", NAPI_AUTO_LENGTH, &msg);
+    napi_create_error(env, nullptr, msg, &err);
+    release(err);  // the promise is rejected: callers awaiting it see the failure
+    return promise;
   }
   return promise;
 }
