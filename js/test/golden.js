@@ -16,7 +16,8 @@ function encodeMeta (m) {
   for (const map of [m.from, m.to]) { vu(map.size); map.forEach((clock, client) => { vu(client); vu(clock) }) }
   return Uint8Array.from(out)
 }
-for (const f of fs.readdirSync(dir).filter(f => f.endsWith('.json')).sort()) {
+// compact.json holds Doc round-trip fixtures in their own layout (tests/compact_cases.py)
+for (const f of fs.readdirSync(dir).filter(f => f.endsWith('.json') && f !== 'compact.json').sort()) {
   const cases = JSON.parse(fs.readFileSync(path.join(dir, f))).cases
   for (const c of cases) {
     const inputs = c.inputs.map(b => new Uint8Array(Buffer.from(b, 'base64')))
@@ -44,7 +45,7 @@ for (const f of fs.readdirSync(dir).filter(f => f.endsWith('.json')).sort()) {
 // the Promise-returning batch forms (napi_async_work) against the golden merges, several calls in flight
 const asyncCheck = async () => {
   const groups = { 1: [], 2: [] }
-  for (const f of fs.readdirSync(dir).filter(f => f.endsWith('.json')).sort()) {
+  for (const f of fs.readdirSync(dir).filter(f => f.endsWith('.json') && f !== 'compact.json').sort()) {
     for (const c of JSON.parse(fs.readFileSync(path.join(dir, f))).cases) {
       if (c.op === 'merge' && c.inputs.length > 1) groups[c.fmt].push(c)
     }
