@@ -162,14 +162,18 @@ def secondary(dev, eng):
              ("meta_c3_v1", "meta", "c3_v1", 4096), ("meta_c3_v2", "meta", "c3_v2", 4096),
              ("dsmerge_c4_v1", "dsmerge", "c4_v1", 10000), ("dsmerge_c4_v2", "dsmerge", "c4_v1", 10000),
              # configs[3] at its per-GPU shard: 1 M docs over 8 GPUs = 125 k docs, 4,096 distinct templates
-             ("merge_c4_v1_125k", "merge", "c4_v1", 125000)]
+             ("merge_c4_v1_125k", "merge", "c4_v1", 125000),
+             # Doc round-trip compaction (the reference's applyUpdate x N +
+             # encodeStateAsUpdate on a gc=true Doc) of the C2 / C4 documents
+             ("compact_c2_v1", "compact", "c2_v1", 10000), ("compact_c2_v2", "compact", "c2_v2", 10000),
+             ("compact_c4_v1", "compact", "c4_v1", 10000)]
     for name, op, wl, n in cases:
         if only and name not in only.split(","):
             continue
         fmt = 2 if wl.endswith("v2") else 1
         a, o, d = load_ymb(wl)
         sva = svo = None
-        if op == "merge":
+        if op in ("merge", "compact"):
             a, o, d = replicate(a, o, d, n)
         elif op == "meta":
             # parseUpdateMeta of every update of n C2 documents (~1 M single-update batch entries)

@@ -129,6 +129,15 @@ int ym_ds_merge(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
  * YM_OUT_V2 or-ed into b->format; default the input's encoding) of decodeSnapshot[V2](input): normalisation
  * (repeated clients merged in Map order) and V1 <-> V2 conversion, with decodeSnapshot's exceptions. */
 int ym_snapshot(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
+/* Doc round-trip compaction: per document, the reference's own
+ *   const doc = new Y.Doc()            (gc: true)
+ *   updates.forEach(u => Y.applyUpdate[V2](doc, u))
+ *   Y.encodeStateAsUpdate[V2](doc)
+ * (gaberogan/yjs@v0 src/utils/encoding.js:350-383 readUpdate / applyUpdate, :490-526 encodeStateAsUpdate;
+ * structs integrated by Item.integrate, deletions applied, deleted content garbage-collected and runs of
+ * structs merged by cleanupTransactions, src/utils/Transaction.js:244-367) in b->format.  Documents whose
+ * inputs leave structs or deletions pending (a missing dependency) report YM_ERR_UNSUPPORTED. */
+int ym_compact(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
 
 #ifdef __cplusplus
 }

@@ -32,7 +32,7 @@ function init () {
   }
 }
 
-const OP = { merge: 0, diff: 1, sv: 2, conv: 3, meta: 4, dsmerge: 5, snapshot: 6 }
+const OP = { merge: 0, diff: 1, sv: 2, conv: 3, meta: 4, dsmerge: 5, snapshot: 6, compact: 7 }
 const fmtOf = o => (o && (o.format === 'v2' || o.format === 2)) ? 2 : 1
 
 // status word -> the exception yjs itself throws for that input: the class from bits 0-7, the message
@@ -108,6 +108,17 @@ function convertUpdateFormatBatch (updates, opts, throwErrors = false, async = f
   const p = pack(updates.map(u => [u]))
   return call(async, [OP.conv, fmtOf(opts), p.arena, p.updOff, p.docUpd], r => unpack(r, throwErrors))
 }
+
+// Doc round-trip compaction (ym_compact): per document, encodeStateAsUpdate[V2] of a fresh gc=true Doc after
+// applyUpdate[V2] of every update in order -- the reference's own compaction (structs merged, deleted
+// content garbage-collected)
+function compactUpdatesBatch (docs, opts, throwErrors = false, async = false) {
+  const p = pack(docs)
+  return call(async, [OP.compact, fmtOf(opts), p.arena, p.updOff, p.docUpd], r => unpack(r, throwErrors))
+}
+const compactUpdates = updates => compactUpdatesBatch([updates], { format: 1 }, true)[0]
+const compactUpdatesV2 = updates => compactUpdatesBatch([updates], { format: 2 }, true)[0]
+const compactUpdatesBatchAsync = (docs, opts, throwErrors = false) => compactUpdatesBatch(docs, opts, throwErrors, true)
 
 // the engine writes parseUpdateMeta's two Maps as two encoded state vectors (from, then to)
 function decodeMeta (b) {
@@ -205,5 +216,6 @@ module.exports = {
   mergeUpdatesBatchAsync, diffUpdateBatchAsync, encodeStateVectorFromUpdateBatchAsync, convertUpdateFormatBatchAsync,
   parseUpdateMetaBatchAsync, mergeDeleteSetsBatchAsync,
   convertSnapshotBatch, convertSnapshotBatchAsync, decodeSnapshotBatch, encodeSnapshotBatch,
-  decodeSnapshot, decodeSnapshotV2, encodeSnapshot, encodeSnapshotV2
+  decodeSnapshot, decodeSnapshotV2, encodeSnapshot, encodeSnapshotV2,
+  compactUpdates, compactUpdatesV2, compactUpdatesBatch, compactUpdatesBatchAsync
 }

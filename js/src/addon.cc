@@ -151,6 +151,7 @@ static void execute(Job &j) {
            : j.op == 4 ? ym_meta(&j.b, &o, nullptr, nullptr)
            : j.op == 5 ? ym_ds_merge(&j.b, &o, nullptr, nullptr)
            : j.op == 6 ? ym_snapshot(&j.b, &o, nullptr, nullptr)
+           : j.op == 7 ? ym_compact(&j.b, &o, nullptr, nullptr)
                        : ym_sv(&j.b, &o, nullptr, nullptr);
     j.used = o.used;
     if (j.rc == YM_ERR_CAPACITY) { cap = o.used + 4096; continue; }

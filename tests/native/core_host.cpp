@@ -10,6 +10,7 @@
 //   result.out: per document: i32 status, u64 len, u8 bytes[len]
 #define YM_HD
 #include "../../yjs_amd/csrc/ym_core.h"
+#include "../../yjs_amd/csrc/ym_compact.h"
 
 #include <stdio.h>
 #include <stdlib.h>
@@ -55,6 +56,29 @@ int main(int argc, char **argv) {
     const uint8_t *svp = op == OP_DIFF ? sv.data() + sv_off[d] : nullptr;
     int st = ST_RETRY;
     std::vector<uint8_t> out;
+    if (op == 7) {  // Doc round-trip compaction (ym_compact.h compact_doc), same retry policy as the kernel
+      for (uint32_t mul = 1, round = 0; st == ST_RETRY && round < 5; mul *= 4, round++) {
+        const cpt::WsSize z = cpt::ws_size(k, bytes, mul);
+        std::vector<uint8_t> ws(z.total + 16);
+        Ctx c = {0, arena.data()};
+        cpt::Result R;
+        memset(&R, 0, sizeof(R));
+        cpt::compact_doc(c, ws.data(), z, v2, upd_off.data(), u0, k, R, nullptr);
+        st = c.err;
+        if (st) continue;
+        out.assign(R.total + 1, 0);
+        Ctx c2 = {0, arena.data()};
+        cpt::compact_doc(c2, ws.data(), z, v2, upd_off.data(), u0, k, R, out.data());
+        st = c2.err ? (c2.err == ST_RETRY ? ST_UNEXPECTED : c2.err) : 0;
+        out.resize(R.total);
+      }
+      const int32_t s32 = st;
+      const uint64_t n = st ? 0 : out.size();
+      fwrite(&s32, 4, 1, o);
+      fwrite(&n, 8, 1, o);
+      if (n) fwrite(out.data(), 1, n, o);
+      continue;
+    }
     for (uint32_t mul = 1, round = 0; st == ST_RETRY && round < 7; mul *= 8, round++) {
       const GeneralWsSize z = general_ws_size(k, bytes, mul, general_sv_bytes(op, svlen, bytes), v2);
       std::vector<uint8_t> ws(z.total + 16);

@@ -36,3 +36,21 @@ def test_compact_keeps_the_state_vector():
         st2, merged = O.merge(c["inputs"], c["fmt"])
         assert st == 0 and st2 == 0, c["id"]
         assert O.sv_from_update(out, c["fmt"]) == O.sv_from_update(merged, c["fmt"]), c["id"]
+
+
+@pytest.mark.parametrize("san", [False, True], ids=["opt", "asan_ubsan"])
+def test_device_core_compact_host_build(san):
+    """The device code itself (yjs_amd/csrc/ym_compact.h compact_doc, what k_compact runs one document per
+    lane) built for the host (tests/native/core_host.cpp op 7), optimised and under ASan + UBSan, against
+    every fixture of the reference."""
+    import core_host
+    from yjs_amd import pack_docs
+    for fmt in (1, 2):
+        cs = [c for c in compact_cases.load() if c["fmt"] == fmt]
+        if san:  # the sanitizer build on a subset: every group's first cases
+            seen = collections.Counter()
+            cs = [c for c in cs if seen.update([c["group"]]) is None and seen[c["group"]] <= 12]
+        a, o, d = pack_docs([c["inputs"] for c in cs])
+        outs, st = core_host.run("compact", fmt, a, o, d, san=san)
+        bad = [(c["id"], int(s)) for c, out, s in zip(cs, outs, st) if s != 0 or not compact_cases.matches(c, out)]
+        assert not bad, f"{len(bad)}/{len(cs)} differ: {bad[:8]}"

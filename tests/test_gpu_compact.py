@@ -1,0 +1,67 @@
+"""GPU parity of Doc round-trip compaction (ym_compact): the HIP kernel
+(ym_compact.hip, one document per lane) against the reference's own outputs (tests/golden/compact.json,
+oracle/gen/make_compact_fixtures.cjs: gaberogan/yjs@v0 applyUpdate x N + encodeStateAsUpdate on a gc=true
+Doc) and, at workload scale, against the oracle's restatement (oracle/ymerge_oracle.c compact_impl)."""
+import numpy as np
+import pytest
+
+import compact_cases
+import oracle_ref as O
+from yjs_amd.workloads import load_ymb
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from yjs_amd import Engine
+    return Engine(0)
+
+
+@pytest.mark.parametrize("lanes", ["1", "64"])
+@pytest.mark.parametrize("fmt", [1, 2])
+def test_compact_fixtures_on_gpu(engine, fmt, lanes, monkeypatch):
+    from yjs_amd import pack_docs
+    monkeypatch.setenv("YMERGE_COMPACT_LANES", lanes)
+    cs = [c for c in compact_cases.load() if c["fmt"] == fmt]
+    a, o, d = pack_docs([c["inputs"] for c in cs])
+    oa, oo, ol, st = engine.run_host("compact", fmt, a, o, d)
+    bad = []
+    for i, c in enumerate(cs):
+        got = oa[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() if st[i] == 0 else None
+        if st[i] != 0 or not compact_cases.matches(c, got):
+            bad.append((c["id"], int(st[i])))
+    assert not bad, f"{len(bad)}/{len(cs)} differ: {bad[:8]}"
+
+
+@pytest.mark.parametrize("name", ["c2_v1", "c2_v2", "c4_v1"])
+def test_compact_workload_matches_oracle(engine, name):
+    """Every template document of the C2 / C4 workloads (bench_data/) compacted on the GPU equals the
+    oracle's restatement byte for byte, and its state vector equals the merged update's."""
+    from yjs_amd import pack_docs
+    fmt = 2 if name.endswith("v2") else 1
+    arena, upd_off, doc_upd = load_ymb(name)
+    n = min(len(doc_upd) - 1, 600)
+    docs = [[arena[int(upd_off[u]):int(upd_off[u + 1])].tobytes() for u in range(int(doc_upd[i]), int(doc_upd[i + 1]))]
+            for i in range(n)]
+    a, o, d = pack_docs(docs)
+    oa, oo, ol, st = engine.run_host("compact", fmt, a, o, d)
+    assert (st == 0).all(), np.unique(st)
+    for i in range(n):
+        s, want = O.compact(docs[i], fmt)
+        assert s == 0
+        assert oa[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() == want, i
+    assert engine.stats["docs_general"] == n  # one kernel (ym_compact.hip) took every document
+
+
+def test_compact_c5_documents(engine):
+    """The large C5 documents (1,024 clients, ~16 k updates, nested XML types): workspace growth on the
+    device (ST_RETRY rounds) and the fixture hashes of the reference."""
+    from yjs_amd import pack_docs
+    cs = [c for c in compact_cases.load() if c["group"] == "wl_c5"]
+    for fmt in (1, 2):
+        sub = [c for c in cs if c["fmt"] == fmt]
+        a, o, d = pack_docs([c["inputs"] for c in sub])
+        oa, oo, ol, st = engine.run_host("compact", fmt, a, o, d)
+        for i, c in enumerate(sub):
+            assert st[i] == 0 and compact_cases.matches(c, oa[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes()), c["id"]

@@ -14,5 +14,6 @@ from .engine import (  # noqa: F401
     mergeDeleteSetsBatch, mergeEncodedDeleteSets,
     Snapshot, convertSnapshotBatch, decodeSnapshotBatch, encodeSnapshotBatch,
     decodeSnapshot, decodeSnapshotV2, encodeSnapshot, encodeSnapshotV2,
+    compactUpdates, compactUpdatesV2, compactUpdatesBatch,
     pack_docs, lib_path, status_class, status_message,
 )

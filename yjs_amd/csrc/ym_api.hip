@@ -25,6 +25,8 @@ int fast2_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t s
 int big_launch(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &pw);       // ym_big.hip
 int big2_launch(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &pw);      // ym_big2.hip
 __global__ void k_fast_region(GeneralJob j, uint32_t n_upd);                         // ym_fast.hip
+__global__ void k_compact_ws(GeneralJob j, uint64_t *ws_size);                        // ym_compact.hip
+__global__ void k_compact(GeneralJob j, uint32_t lanes);
 }  // namespace ymk
 
 using namespace ymk;
@@ -304,8 +306,52 @@ int select_docs(DevState *S, hipStream_t st, const uint32_t *list, uint32_t n, c
   return 0;
 }
 
+// Doc round-trip compaction (ym_compact.hip) over `list` (n docs, nullptr: all); documents whose workspace
+// overflowed run again with 4x the workspace.
+int run_compact(DevState *S, hipStream_t st, GeneralJob j, uint32_t *list, uint32_t n) {
+  static int lanes = -1;
+  if (lanes < 0) {  // active lanes (documents) per 64-wide wave
+    const char *e = getenv("YMERGE_COMPACT_LANES");
+    lanes = e ? atoi(e) : 1;
+    if (lanes < 1 || lanes > 64) lanes = 1;
+  }
+  uint32_t mul = 1;
+  for (int round = 0; n > 0; round++) {
+    j.list = list;
+    j.n = n;
+    j.parts_mul = mul;
+    if (S->ws_size.ensure((size_t)(n + 1) * 8) || S->ws_off.ensure((size_t)(n + 1) * 8)) return -1;
+    k_compact_ws<<<(n + 255) / 256, 256, 0, st>>>(j, S->ws_size.as<uint64_t>());
+    size_t tmp = 0;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, S->ws_size.as<uint64_t>(), S->ws_off.as<uint64_t>(), n, st);
+    if (S->scan_tmp.ensure(tmp + 16)) return -1;
+    hipcub::DeviceScan::ExclusiveSum(S->scan_tmp.p, tmp, S->ws_size.as<uint64_t>(), S->ws_off.as<uint64_t>(), n, st);
+    HIPCHK(hipMemcpyAsync(S->pinned, S->ws_off.as<uint64_t>() + (n - 1), 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(S->pinned + 1, S->ws_size.as<uint64_t>() + (n - 1), 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const uint64_t ws_total = S->pinned[0] + S->pinned[1];
+    if (S->ws.ensure(ws_total + 64)) return -2;
+    j.ws = S->ws.as<uint8_t>();
+    j.ws_off = S->ws_off.as<uint64_t>();
+    HIPCHK(hipMemsetAsync(j.counter_retry, 0, 4, st));
+    k_compact<<<(n + lanes - 1) / lanes, 64, 0, st>>>(j, (uint32_t)lanes);
+    HIPCHK(hipMemcpyAsync(S->pinned, j.counter_retry, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const uint32_t nretry = (uint32_t)(S->pinned[0] & 0xffffffffu);
+    if (nretry == 0 || round >= 5) break;
+    uint32_t *next = list == S->list_a.as<uint32_t>() ? S->list_b.as<uint32_t>() : S->list_a.as<uint32_t>();
+    uint32_t cnt = 0;
+    if (select_docs(S, st, list, n, j.status, ym::ST_RETRY, next, &cnt)) return -1;
+    list = next;
+    n = cnt;
+    mul *= 4;
+  }
+  return 0;
+}
+
 // Runs the general path over `list` (n docs); retries docs whose part table overflowed.
 int run_general(DevState *S, hipStream_t st, GeneralJob j, uint32_t *list, uint32_t n) {
+  if (j.op == OP_COMPACT) return run_compact(S, st, j, list, n);
   uint32_t parts_mul = 1;
   for (int round = 0; n > 0; round++) {
     j.list = list;
@@ -697,5 +743,6 @@ int ym_convert(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { 
 int ym_meta(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_META, b, out, stream, stats); }
 int ym_ds_merge(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_DSMERGE, b, out, stream, stats); }
 int ym_snapshot(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_SNAP, b, out, stream, stats); }
+int ym_compact(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_COMPACT, b, out, stream, stats); }
 
 }  // extern "C"

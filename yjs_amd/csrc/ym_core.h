@@ -2391,7 +2391,7 @@ YM_BIG void snap_doc(Ctx &c, DocWS &ws, uint64_t uoff, uint64_t ulen, uint32_t v
 // The general path's per-document entry (k_general in ym_general.hip; the test-only host build in
 // tests/native/core_host.cpp runs the very same function on the CPU)
 // ------------------------------------------------------------------------------------------------
-enum : uint32_t { OP_MERGE = 0, OP_DIFF = 1, OP_SV = 2, OP_CONV = 3, OP_META = 4, OP_DSMERGE = 5, OP_SNAP = 6 };
+enum : uint32_t { OP_MERGE = 0, OP_DIFF = 1, OP_SV = 2, OP_CONV = 3, OP_META = 4, OP_DSMERGE = 5, OP_SNAP = 6, OP_COMPACT = 7 };
 
 struct GeneralWsSize {
   uint64_t rs, arr, parts, ds, dsg, sv, keys, total;

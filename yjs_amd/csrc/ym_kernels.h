@@ -14,6 +14,7 @@ using ym::OP_CONV;
 using ym::OP_META;
 using ym::OP_DSMERGE;
 using ym::OP_SNAP;
+using ym::OP_COMPACT;
 
 // internal status: document not taken by the fast path, routed to the general path
 constexpr int ST_PENDING = 101;

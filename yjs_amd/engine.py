@@ -91,7 +91,7 @@ class _Stats(ctypes.Structure):
 
 
 EXPORTS = ("ym_init", "ym_shutdown", "ym_strerror", "ym_out_bound", "ym_merge", "ym_diff", "ym_sv", "ym_convert",
-           "ym_meta", "ym_ds_merge", "ym_snapshot")
+           "ym_meta", "ym_ds_merge", "ym_snapshot", "ym_compact")
 
 
 def load_library(path=None):
@@ -102,7 +102,7 @@ def load_library(path=None):
     L.ym_init.argtypes = [ctypes.c_int]
     L.ym_strerror.restype = ctypes.c_char_p
     L.ym_out_bound.restype = ctypes.c_uint64
-    for fn in (L.ym_merge, L.ym_diff, L.ym_sv, L.ym_convert, L.ym_meta, L.ym_ds_merge, L.ym_snapshot):
+    for fn in (L.ym_merge, L.ym_diff, L.ym_sv, L.ym_convert, L.ym_meta, L.ym_ds_merge, L.ym_snapshot, L.ym_compact):
         fn.argtypes = [ctypes.POINTER(_Batch), ctypes.POINTER(_Out), ctypes.c_void_p, ctypes.POINTER(_Stats)]
         fn.restype = ctypes.c_int
     return L
@@ -147,7 +147,7 @@ class Engine:
         L = self.lib
         return {"merge": L.ym_merge, "diff": L.ym_diff, "sv": L.ym_sv, "conv": L.ym_convert, "meta": L.ym_meta,
                 "dsmerge": L.ym_ds_merge, "dsmerge_ref": L.ym_ds_merge,
-                "snap_to_v1": L.ym_snapshot, "snap_to_v2": L.ym_snapshot}[op]
+                "snap_to_v1": L.ym_snapshot, "snap_to_v2": L.ym_snapshot, "compact": L.ym_compact}[op]
 
     @staticmethod
     def _format(op, fmt):
@@ -290,6 +290,22 @@ def diffUpdateBatch(updates, state_vectors, fmt=1, raise_errors=False):
 def encodeStateVectorFromUpdateBatch(updates, fmt=1, raise_errors=False):
     arena, upd_off, doc_upd = pack_docs([[u] for u in updates])
     return _unpack(*_engine().run_host("sv", fmt, arena, upd_off, doc_upd), raise_errors)
+
+
+def compactUpdatesBatch(docs, fmt=1, raise_errors=False):
+    """Doc round-trip compaction (ym_compact) over a batch: per document, encodeStateAsUpdate[V2] of a fresh
+    gc=true Doc after applyUpdate[V2] of every update in order (the reference's own compaction:
+    src/utils/encoding.js readUpdate / encodeStateAsUpdate, Transaction.js cleanupTransactions)."""
+    arena, upd_off, doc_upd = pack_docs(docs)
+    return _unpack(*_engine().run_host("compact", fmt, arena, upd_off, doc_upd), raise_errors)
+
+
+def compactUpdates(updates):
+    return compactUpdatesBatch([list(updates)], 1, True)[0]
+
+
+def compactUpdatesV2(updates):
+    return compactUpdatesBatch([list(updates)], 2, True)[0]
 
 
 def mergeUpdates(updates):
