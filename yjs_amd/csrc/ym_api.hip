@@ -310,10 +310,11 @@ int select_docs(DevState *S, hipStream_t st, const uint32_t *list, uint32_t n, c
 // overflowed run again with 4x the workspace.
 int run_compact(DevState *S, hipStream_t st, GeneralJob j, uint32_t *list, uint32_t n) {
   static int lanes = -1;
-  if (lanes < 0) {  // active lanes (documents) per 64-wide wave
+  if (lanes < 0) {  // active lanes (documents) per 64-wide wave; measured on C2 / C4 (10 k documents):
+    // 1: 209 / 268 ms, 8: 110 / 102, 16: 77 / 62, 32: 85 / 62, 64: 89 / 63 (profiles/r03c)
     const char *e = getenv("YMERGE_COMPACT_LANES");
-    lanes = e ? atoi(e) : 1;
-    if (lanes < 1 || lanes > 64) lanes = 1;
+    lanes = e ? atoi(e) : 16;
+    if (lanes < 1 || lanes > 64) lanes = 16;
   }
   uint32_t mul = 1;
   for (int round = 0; n > 0; round++) {

@@ -313,7 +313,38 @@ __device__ __forceinline__ int sec_phase(const GeneralJob &j, uint32_t d, uint32
       rb[s] = v ? at<uint16_t>(L_SB + 2 * i) : 0;
       re[s] = v ? at<uint16_t>(L_SE + 2 * i) : 0;
     }
-    rank_le4(L_SKEY, nsec, rk, rr);
+    bool ranked = false;
+    if constexpr (EE == 1) {
+      // One section per lane: rank by client groups.  A group (one client) is picked per iteration by
+      // its lowest lane; its lanes take their position within the group in lane (= walk = update) order
+      // and every lane of a larger key (smaller client) adds the group's size.  Valid when each group is
+      // clock-sorted in walk order (the updates of one client arrive in clock order: the common case),
+      // checked against the previous lane of the group; otherwise, or beyond 16 clients, rank_le4.
+      const uint64_t lt = (1ull << lane) - 1;
+      const bool v = lane < nsec;
+      const uint32_t hi = (uint32_t)(rk[0] >> 32), lo = (uint32_t)rk[0];
+      uint64_t rem = __ballot(v), grp = 0;
+      uint32_t base = 0, pos = 0;
+      for (uint32_t g = 0; rem != 0 && g < 16; g++) {
+        const uint32_t f = (uint32_t)__builtin_ctzll(rem);
+        const uint32_t h = lane_read(hi, (int)f);
+        const bool in = v && hi == h;
+        const uint64_t m = __ballot(in);
+        if (in) { pos = (uint32_t)__popcll(m & lt); grp = m; }
+        base += (v && hi > h) ? (uint32_t)__popcll(m) : 0u;
+        rem &= ~m;
+      }
+      if (rem == 0) {
+        const uint64_t pm = grp & lt;
+        const int prev = pm ? 63 - __builtin_clzll(pm) : (int)lane;
+        const uint32_t plo = (uint32_t)__shfl((int)lo, prev, 64);
+        if (__all(!v || pm == 0 || plo < lo)) {
+          rr[0] = base + pos;
+          ranked = true;
+        }
+      }
+    }
+    if (!ranked) rank_le4(L_SKEY, nsec, rk, rr);
     __syncthreads();
 #pragma unroll
     for (uint32_t s = 0; s < EE; s++) {
