@@ -166,7 +166,12 @@ def secondary(dev, eng):
              # Doc round-trip compaction (the reference's applyUpdate x N +
              # encodeStateAsUpdate on a gc=true Doc) of the C2 / C4 documents
              ("compact_c2_v1", "compact", "c2_v1", 10000), ("compact_c2_v2", "compact", "c2_v2", 10000),
-             ("compact_c4_v1", "compact", "c4_v1", 10000)]
+             ("compact_c4_v1", "compact", "c4_v1", 10000),
+             # rich content: Quill-style formats / embeds, maps of objects and arrays
+             ("merge_c2r_v1", "merge", "c2r_v1", 10000), ("merge_c2r_v2", "merge", "c2r_v2", 10000),
+             ("merge_c4r_v1", "merge", "c4r_v1", 10000), ("merge_c4r_v2", "merge", "c4r_v2", 10000),
+             ("diff_c2r_v1", "diff", "c2r_v1", 4096), ("diff_c2r_v2", "diff", "c2r_v2", 4096),
+             ("sv_c4r_v1", "sv", "c4r_v1", 4096), ("diff_c4r_v2", "diff", "c4r_v2", 4096)]
     for name, op, wl, n in cases:
         if only and name not in only.split(","):
             continue
@@ -200,8 +205,8 @@ def secondary(dev, eng):
                 fmt = 2
             docs = [[blobs[u] for u in range(int(d[t]), int(d[t + 1]))] for t in range(len(d) - 1)]
             a, o, d = replicate(*pack_docs(docs), n)
-        elif wl.startswith("c5"):
-            # the merged C5 documents (merged here by the engine), random per-client state vectors
+        elif wl.startswith("c5") or wl[:3] in ("c2r", "c4r"):
+            # the merged documents (merged here by the engine), random per-client state vectors
             ma, mo, ml, _ = eng.run_host("merge", fmt, a, o, d)
             ups = [ma[int(mo[i]):int(mo[i]) + int(ml[i])].tobytes() for i in range(len(d) - 1)]
             sa, so_, sl, _ = eng.run_host("sv", fmt, *pack_docs([[u] for u in ups]))

@@ -11,6 +11,9 @@
 //   C4  Y.Map docs, 64 clients, 128 broadcast transactions, keys k0..k7, delete p=0.6 when present;
 //       4,096 templates (SURVEY.md §8(d)).
 //   C5  Y.XmlFragment docs, 1,024 clients x 16 transactions each (V1 and V2), see genXml.
+//   C2R the C2 shape (50 transactions: documents of ~2 KB, inside the LDS fast path's budget) with rich content (Quill-style): formats {bold: true}, {header: 1..3} (a number),
+//       {link: {href}} (an object), {color: '#rrggbb'}, and image embeds {image: url} (genTextRich).
+//   C4R the C4 shape (96 transactions) whose map values are objects {x, y: [..], tag} and arrays [word, n] (genMapRich).
 // File format (.ymb, little endian): "YMB1" u32 n_docs u32 n_upd | u32 doc_upd[n_docs+1] |
 // u64 upd_off[n_upd+1] | arena bytes; gzip-compressed.
 'use strict'
@@ -169,7 +172,84 @@ function genXml (seed, nClients, nTx) {
   return { v1, v2 }
 }
 
+// C2R: genText with Quill-style rich content
+function genTextRich (seed, nClients, nTx, syncP, ids) {
+  const r = rng(seed)
+  const v1 = []; const v2 = []
+  const docs = []
+  for (let c = 0; c < nClients; c++) {
+    const d = new Y.Doc(); d.clientID = ids[c]
+    d.on('update', (u, origin) => { if (origin !== 'remote') v1.push(u) })
+    d.on('updateV2', (u, origin) => { if (origin !== 'remote') v2.push(u) })
+    docs.push(d)
+  }
+  const fmt = () => {
+    const p = r.real()
+    if (p < 0.25) return { bold: true }
+    if (p < 0.45) return { header: r.int(1, 3) }
+    if (p < 0.6) return { link: { href: 'https://e.x/' + r.word(2, 6) } }
+    if (p < 0.75) return { color: '#' + (r.u32() & 0xffffff).toString(16).padStart(6, '0') }
+    return {}
+  }
+  for (let t = 0; t < nTx; t++) {
+    const d = docs[r.u32() % docs.length]
+    const text = d.getText('text')
+    d.transact(() => {
+      const len = text.length
+      const p = r.real()
+      if (len === 0 || p < 0.5) text.insert(r.int(0, len), r.word(1, 5), fmt())
+      else if (p < 0.6) text.insertEmbed(r.int(0, len), { image: 'https://e.x/i' + r.int(0, 999) + '.png' })
+      else if (p < 0.7) { const pos = r.int(0, len - 1); text.format(pos, Math.min(r.int(1, 4), len - pos), fmt()) }
+      else { const pos = r.int(0, len - 1); text.delete(pos, Math.min(r.int(1, 3), len - pos)) }
+    })
+    if (nClients > 1 && r.real() < syncP) {
+      const a = docs[r.u32() % docs.length]; const b = docs[r.u32() % docs.length]
+      if (a !== b) Y.applyUpdate(b, Y.encodeStateAsUpdate(a, Y.encodeStateVector(b)), 'remote')
+    }
+  }
+  return { v1, v2 }
+}
+// C4R: genMapShared whose values are objects and arrays
+function genMapRich (seed, nClients, nTx, nKeys) {
+  const r = rng(seed)
+  const v1 = []; const v2 = []
+  const ids = []
+  for (let c = 0; c < nClients; c++) ids.push(500 + 31 * c)
+  const d = new Y.Doc(); d.clientID = ids[0]
+  d.on('update', u => v1.push(u))
+  d.on('updateV2', u => v2.push(u))
+  for (let t = 0; t < nTx; t++) {
+    d.clientID = ids[r.u32() % nClients]
+    const m = d.getMap('map')
+    const key = 'k' + (r.u32() % nKeys)
+    if (m.has(key) && r.real() < 0.6) m.delete(key)
+    else if (r.real() < 0.6) m.set(key, { x: r.int(0, 1000000), y: [r.int(0, 99), r.int(0, 99)], tag: r.word(1, 6) })
+    else m.set(key, [r.word(1, 6), r.int(0, 1000), r.real() < 0.5])
+  }
+  return { v1, v2 }
+}
+
 fs.mkdirSync(OUT, { recursive: true })
+if (which.includes('c2r')) {
+  const T = Number(process.env.C2_TEMPLATES || 1024)
+  const d1 = []; const d2 = []
+  for (let doc = 0; doc < T; doc++) {
+    const { v1, v2 } = genTextRich(doc + 7001, 4, 50, 0.3, [1000, 8919, 16838, 24757])
+    d1.push(v1); d2.push(v2)
+  }
+  writeYmb(path.join(OUT, 'c2r_v1.ymb.gz'), d1)
+  writeYmb(path.join(OUT, 'c2r_v2.ymb.gz'), d2)
+}
+if (which.includes('c4r')) {
+  const T = Number(process.env.C4_TEMPLATES || 1024)
+  const d1 = []; const d2 = []
+  for (let doc = 0; doc < T; doc++) {
+    const { v1, v2 } = genMapRich(doc + 9001, 64, 96, 8)
+    d1.push(v1); d2.push(v2)
+  }
+  writeYmb(path.join(OUT, 'c4r_v1.ymb.gz'), d1)
+  writeYmb(path.join(OUT, 'c4r_v2.ymb.gz'), d2)
+}
 if (which.includes('c1')) {
   const { v1, v2 } = genText(12345, 1, 1000, 10, false, 0, [7])
   writeYmb(path.join(OUT, 'c1_v1.ymb.gz'), [v1])

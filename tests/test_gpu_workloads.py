@@ -30,7 +30,7 @@ def _compare(res, outs, status):
     return bad
 
 
-@pytest.mark.parametrize("name", ["c2_v1", "c2_v2", "c4_v1", "c4_v2", "c1_v1", "c1_v2"])
+@pytest.mark.parametrize("name", ["c2_v1", "c2_v2", "c4_v1", "c4_v2", "c1_v1", "c1_v2", "c2r_v1", "c2r_v2", "c4r_v1", "c4r_v2"])
 def test_merge_workload_matches_oracle(engine, name):
     arena, upd_off, doc_upd = load_ymb(name)
     fmt = 2 if name.endswith("v2") else 1
