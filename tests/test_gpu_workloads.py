@@ -590,3 +590,33 @@ def test_multi_device_engine_real_engine(how):
             torch.cuda.synchronize()
             free.append(torch.cuda.mem_get_info(0)[0])
     assert abs(free[2] - free[1]) < (64 << 20), free  # no per-call leak of streams / scratch
+
+
+@pytest.mark.parametrize("name", ["c2r_v1", "c2r_v2", "c4r_v1", "c4r_v2"])
+def test_rich_content_stays_on_the_specialised_paths(engine, name):
+    """Rich content (number / object formats, image embeds, maps of objects and arrays: the C2R / C4R
+    templates) through the LDS merges, then the merged documents' state vectors and diffs against random
+    state vectors through the streamed walkers: equal to the oracle, and no document on the general path
+    (nested `any` values and JSON texts are checked canonical, ym_canon_chk.h, and copied)."""
+    from yjs_amd import pack_docs
+    fmt = 2 if name.endswith("v2") else 1
+    arena, upd_off, doc_upd = load_ymb(name)
+    n = 400
+    docs = [[arena[int(upd_off[u]):int(upd_off[u + 1])].tobytes() for u in range(int(doc_upd[i]), int(doc_upd[i + 1]))]
+            for i in range(n)]
+    a, o, d = pack_docs(docs)
+    outs, status, _ = O.batch("merge", fmt, a, o, d, nthreads=8)
+    bad = _compare(engine.run_host("merge", fmt, a, o, d), outs, status)
+    assert not bad, bad[:10]
+    assert engine.stats["docs_general"] == 0, engine.stats
+    a2, o2, d2 = pack_docs([[m] for m in outs])
+    svo, sst, _ = O.batch("sv", fmt, a2, o2, d2, nthreads=8)
+    bad = _compare(engine.run_host("sv", fmt, a2, o2, d2), svo, sst)
+    assert not bad, bad[:10]
+    assert engine.stats["docs_general"] == 0, engine.stats
+    svs = [random_state_vectors(svo[i], 1, seed=i)[0] for i in range(n)]
+    sva, svoff, _ = pack_docs([[s] for s in svs])
+    douts, dst, _ = O.batch("diff", fmt, a2, o2, d2, sva, svoff, nthreads=8)
+    bad = _compare(engine.run_host("diff", fmt, a2, o2, d2, sva, svoff), douts, dst)
+    assert not bad, bad[:10]
+    assert engine.stats["docs_general"] == 0, engine.stats

@@ -239,7 +239,7 @@ __global__ void __launch_bounds__(64) k_big_v1(GeneralJob j) {
                   q += vsz(len - off);
                 } else if (ref == 8) {
                   rvu(e);
-                  for (uint32_t i = 0; i < off; i++) any_scalar(e);  // ContentAny.splice: drop `off` values
+                  for (uint32_t i = 0; i < off; i++) any_canon(e);  // ContentAny.splice: drop `off` values
                   if (lane == 0) put_vu_lds(q, len - off);
                   q += vsz(len - off);
                   a0 = rel(e.p);

@@ -203,7 +203,7 @@ __device__ __forceinline__ bool walk_v2(uint32_t u) {
         case 5: case 6: {                                                  // Embed / Format (+ key)
           if ((info & 31) == 6) s2 = rstr();
           const uint32_t a = c.p;
-          any_scalar(c);
+          any_canon(c);
           sp = a | ((c.p - a) << 16);
           break;
         }
@@ -219,7 +219,7 @@ __device__ __forceinline__ bool walk_v2(uint32_t u) {
         case 8: {                                                          // ContentAny
           len = rd_uopt(ln);
           const uint32_t a = c.p;
-          for (uint32_t i = 0; i < len && !c.bad; i++) any_scalar(c);
+          for (uint32_t i = 0; i < len && !c.bad; i++) any_canon(c);
           sp = a | ((c.p - a) << 16);
           break;
         }

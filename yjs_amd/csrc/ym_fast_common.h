@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "ym_canon_chk.h"
 #include "ym_kernels.h"
 
 namespace ymk {
@@ -250,6 +251,8 @@ __device__ __forceinline__ void json_lit(Cur &c) {
     }
     ok = bad == 0;
   }
+  // numbers, objects, arrays: JSON.stringify(JSON.parse(text)) == text (ym_canon_chk.h)
+  if (!ok) ok = cchk::json_canon_ptr(sm, c.p, n);
   if (!ok) { c.bad = true; return; }
   utf16_len(c, n);
 }
@@ -294,6 +297,18 @@ __device__ __forceinline__ void any_scalar(Cur &c) {
   }
 }
 
+// one `any` value of any shape in the form writeAny emits (nested values: ym_canon_chk.h)
+__device__ __forceinline__ void any_canon(Cur &c) {
+  const uint32_t tag = c.p < c.e ? sm[c.p] : 0;
+  if (tag == 116 || tag == 117 || tag == 118 || tag == 122) {
+    uint32_t q = c.p;
+    c.bad |= !cchk::any_canon_ptr(sm, c.p, c.e, &q);
+    c.p = q;
+  } else {
+    any_scalar(c);
+  }
+}
+
 // The fields and content of one V1 Item after its info byte (UpdateDecoder.js:127-243 field readers,
 // Item.js:665-683 content refs; lazy reader of 13.5.16: parent kept raw, parentSub only without
 // origins).  Returns false (decline) for kinds this path does not verify; `len` = the Item's length.
@@ -322,7 +337,7 @@ __device__ __forceinline__ bool item_body(Cur &c, uint32_t info, uint32_t &len) 
     }
     case 8:                                                           // ContentAny
       len = rvu(c);
-      for (uint32_t i = 0; i < len && !c.bad; i++) any_scalar(c);
+      for (uint32_t i = 0; i < len && !c.bad; i++) any_canon(c);
       break;
     default: c.bad = true; break;  // ContentJSON, ContentDoc, invalid refs
   }

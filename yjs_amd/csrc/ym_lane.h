@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "ym_canon_chk.h"
+
 namespace ymk {
 namespace ln {
 
@@ -156,6 +158,8 @@ __device__ __forceinline__ void json_lit(LCur &c) {
     }
     ok = bad == 0;
   }
+  // numbers, objects, arrays: JSON.stringify(JSON.parse(text)) == text (ym_canon_chk.h)
+  if (!ok) ok = cchk::json_canon_ptr(c.b, c.p, n);
   if (!ok) { c.bad = true; return; }
   utf16_len(c, n);
 }
@@ -299,7 +303,7 @@ __device__ __forceinline__ bool item_body(LCur &c, uint32_t info, uint32_t &len)
     case 8:
       len = rvu(c);
       c.bad |= len > c.cap;
-      for (uint32_t i = 0; i < len && !c.bad; i++) any_scalar(c);
+      for (uint32_t i = 0; i < len && !c.bad; i++) any_canon(c);
       break;
     default: c.bad = true; break;
   }

@@ -295,7 +295,7 @@ __device__ bool walk_v2(const LMJob &J, uint32_t p0, uint32_t p1, uint64_t gb, c
         case 5: case 6: {                                                   // Embed / Format (+ key)
           if ((info & 31) == 6) s2 = rstr();
           const uint32_t a = c.p;
-          any_scalar(c);
+          any_canon(c);
           sp = gb + a;
           spn = c.p - a;
           break;
@@ -312,7 +312,7 @@ __device__ bool walk_v2(const LMJob &J, uint32_t p0, uint32_t p1, uint64_t gb, c
         case 8: {                                                           // ContentAny
           len = rd_uopt(ln);
           const uint32_t a = c.p;
-          for (uint32_t q = 0; q < len && !c.bad; q++) any_scalar(c);
+          for (uint32_t q = 0; q < len && !c.bad; q++) any_canon(c);
           sp = gb + a;
           spn = c.p - a;
           break;

@@ -265,7 +265,7 @@ __device__ bool slice_head(sc::cu32 *B, uint32_t adj, uint32_t s0, uint32_t s1, 
       put(len - off);
     } else if (ref == 8) {
       sc::rvu(e);
-      for (uint32_t i = 0; i < off; i++) sc::any_scalar(e);  // ContentAny.splice: drop `off` values
+      for (uint32_t i = 0; i < off; i++) sc::any_canon(e);  // ContentAny.splice: drop `off` values
       put(len - off);
       a0 = e.p - adj;
       a1 = s1;

@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "ym_canon_chk.h"
+
 namespace ymk {
 namespace sc {
 
@@ -191,8 +193,22 @@ __device__ __forceinline__ void json_lit(SCur &c) {  // true | false | null | "s
     }
     ok = bad == 0;
   }
+  // numbers, objects, arrays: JSON.stringify(JSON.parse(text)) == text (ym_canon_chk.h)
+  if (!ok) ok = cchk::json_canon_ptr((const uint8_t *)(uintptr_t)c.b, c.p, n);
   if (!ok) { c.bad = true; return; }
   utf16_len(c, n);
+}
+__device__ __forceinline__ void any_scalar(SCur &c);
+// one `any` value of any shape in the form writeAny emits (nested values: ym_canon_chk.h)
+__device__ __forceinline__ void any_canon(SCur &c) {
+  const uint32_t tag = c.p < c.e ? byte(c.b, c.p) : 0;
+  if (tag == 116 || tag == 117 || tag == 118 || tag == 122) {
+    uint32_t q = c.p;
+    if (!cchk::any_canon_ptr((const uint8_t *)(uintptr_t)c.b, c.p, c.e, &q)) { c.bad = true; return; }
+    skip(c, q - c.p);
+  } else {
+    any_scalar(c);
+  }
 }
 __device__ __forceinline__ void any_scalar(SCur &c) {
   const uint32_t tag = rdb(c);
@@ -258,7 +274,7 @@ __device__ __forceinline__ bool item_body(SCur &c, uint32_t info, uint32_t &len)
     }
     case 8:
       len = rvu(c);
-      for (uint32_t i = 0; i < len && !c.bad; i++) any_scalar(c);
+      for (uint32_t i = 0; i < len && !c.bad; i++) any_canon(c);
       break;
     default: return false;
   }
