@@ -41,7 +41,7 @@ def test_compact_workload_matches_oracle(engine, name):
     from yjs_amd import pack_docs
     fmt = 2 if name.endswith("v2") else 1
     arena, upd_off, doc_upd = load_ymb(name)
-    n = min(len(doc_upd) - 1, 600)
+    n = min(len(doc_upd) - 1, 200)
     docs = [[arena[int(upd_off[u]):int(upd_off[u + 1])].tobytes() for u in range(int(doc_upd[i]), int(doc_upd[i + 1]))]
             for i in range(n)]
     a, o, d = pack_docs(docs)

@@ -62,7 +62,8 @@ constexpr uint32_t NPATCH = 1024;
 constexpr uint32_t L_PPOS = 0;                     // u32[NPATCH] patch positions (document-relative)
 constexpr uint32_t L_PSEC = L_PPOS + 4 * NPATCH;   // u32[NPATCH] section of each patch
 constexpr uint32_t L_PVAL = L_PSEC + 4 * NPATCH;   // u8[NPATCH]  patched info bytes
-constexpr uint32_t LDS_BYTES = L_PVAL + NPATCH;
+constexpr uint32_t L_REC = L_PVAL + NPATCH;        // u32x2[CAP + 1] the records of the chunk being consumed
+constexpr uint32_t LDS_BYTES = L_REC + 8 * (CAP + 1);
 enum { S_PRELEN = 0, S_A0, S_A1, S_B0, S_B1, S_WRITTEN, S_CLIENT, S_FCLOCK, S_OUTB };
 constexpr uint32_t NONE = 0xffffffffu;
 
@@ -356,6 +357,7 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
     // chunk cursor: the current chunk and the next record index in it; descriptors of chunks [wb, wb + 64)
     uint32_t cc = NONE, s = 0, wb = NONE - 64;
     uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0, q4 = q0;
+    uint32_t staged = NONE;  // the chunk whose records (and exit sentinel) sit in LDS at L_REC
     for (uint32_t ci = 0; ci < nclients && !declined; ci++) {
       uint32_t nstructs, client;
       uint64_t clock;
@@ -433,13 +435,23 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
             s = fs;
           } else PWP(2);
         }
-        // ---- record by record: locate x among the chunk's records (a ballot over 64 per load)
+        // ---- record by record.  The chunk's records are staged into LDS first, all loads in flight at
+        // once (one memory round trip per chunk instead of one per 64-record batch, twice: the search and
+        // the consumption): C5 sections end inside chunks and cut mid-chunk, so most chunks go this way.
+        if (staged != gc && s < nrec) {
+          __syncthreads();
+          for (uint32_t k = lane; k < nrec; k += 64) at<uint2>(L_REC + 8 * k) = recs[rec_idx(gc, k)];
+          if (lane == 0) at<uint2>(L_REC + 8 * nrec) = make_uint2(cexit, cumx);
+          __syncthreads();
+          staged = gc;
+        }
+        // locate x among the chunk's records (a ballot over 64 per step)
         bool found = false;
         for (;;) {
           if (s >= nrec) break;
           PWP(5);
           const uint32_t kk = s + lane;
-          const uint32_t pw = kk < nrec ? recs[rec_idx(gc, kk)].x : POS_MASK;
+          const uint32_t pw = kk < nrec ? at<uint2>(L_REC + 8 * kk).x : POS_MASK;
           const uint64_t lt = __ballot(kk < nrec && (pw & POS_MASK) < x);
           const uint32_t nlt = __popcll(lt);
           if (nlt == 64) { s += 64; continue; }
@@ -459,8 +471,8 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
           const uint32_t kk = s + lane;
           valid = lane < n;
           if (valid) {
-            const uint2 r = recs[rec_idx(gc, kk)];
-            const uint2 r1 = kk + 1 < nrec ? recs[rec_idx(gc, kk + 1)] : make_uint2(cexit, cumx);
+            const uint2 r = at<uint2>(L_REC + 8 * kk);
+            const uint2 r1 = at<uint2>(L_REC + 8 * (kk + 1));  // (record nrec: the exit sentinel)
             pos = r.x & POS_MASK;
             fl = r.x;
             clen = r1.y - r.y;
