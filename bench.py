@@ -175,6 +175,20 @@ def secondary(dev, eng):
     for name, op, wl, n in cases:
         if only and name not in only.split(","):
             continue
+        try:
+            res[name] = _secondary_case(dev, eng, name, op, wl, n)
+        except Exception as e:  # one failing line must not take the headline line down with it
+            res[name] = {"error": f"{type(e).__name__}: {e}"}
+        torch.cuda.empty_cache()
+    return res
+
+
+def _secondary_case(dev, eng, name, op, wl, n):
+    """One secondary line (see secondary())."""
+    import torch
+    from yjs_amd import pack_docs
+    from yjs_amd.workloads import load_ymb, replicate, random_state_vectors
+    if True:
         fmt = 2 if wl.endswith("v2") else 1
         a, o, d = load_ymb(wl)
         sva = svo = None
@@ -236,7 +250,9 @@ def secondary(dev, eng):
         ol = torch.empty(nd, dtype=torch.int64, device=dev)
         st = torch.empty(nd, dtype=torch.int32, device=dev)
         steps = 5 if op in ("merge", "meta", "dsmerge") else 2
-        eng.run_device(op, fmt, ga, go, gd, oa, oo, ol, st, gsa, gso)
+        rc0, used0 = eng.run_device(op, fmt, ga, go, gd, oa, oo, ol, st, gsa, gso)
+        if rc0 != 0:
+            raise RuntimeError(f"rc {rc0} (used {used0} of cap {cap})")
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         kms = []
@@ -253,16 +269,13 @@ def secondary(dev, eng):
         kms_mean = float(np.mean(kms))
         # roofline of the call's dominant kernel(s): algorithmic bytes (inputs + outputs) / their device time
         kgbs = (len(a) + out_b) / (kms_mean * 1e-3) / 1e9 if kms_mean > 0 else 0.0
-        res[name] = {"docs": nd, "input_bytes": int(len(a)), "output_bytes": out_b,
+        return {"docs": nd, "input_bytes": int(len(a)), "output_bytes": out_b,
                      "value_gbs": round(len(a) / el / 1e9, 3),
                      "docs_per_s": round(nd / el, 1), "ms_per_step": round(el * 1e3, 3),
                      "kernel_ms": round(kms_mean, 3), "kernel_in_plus_out_gbs": round(kgbs, 2),
                      "roofline_frac": round(kgbs / HBM_PEAK_GBS, 5), "docs_fast": int(sts["docs_fast"]),
                      "docs_large": int(sts["docs_large"]), "docs_general": int(sts["docs_general"]),
                      "errors": int(sts["docs_error"]), "update_offsets": "u32" if off32 else "u64"}
-        del ga, go, gd, gsa, gso, oa, oo, ol, st
-        torch.cuda.empty_cache()
-    return res
 
 
 def _sv_of_single_client_update(upd, fmt):

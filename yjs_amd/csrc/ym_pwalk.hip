@@ -62,8 +62,8 @@ constexpr uint32_t NPATCH = 1024;
 constexpr uint32_t L_PPOS = 0;                     // u32[NPATCH] patch positions (document-relative)
 constexpr uint32_t L_PSEC = L_PPOS + 4 * NPATCH;   // u32[NPATCH] section of each patch
 constexpr uint32_t L_PVAL = L_PSEC + 4 * NPATCH;   // u8[NPATCH]  patched info bytes
-constexpr uint32_t L_REC = L_PVAL + NPATCH;        // u32x2[CAP + 1] the records of the chunk being consumed
-constexpr uint32_t LDS_BYTES = L_REC + 8 * (CAP + 1);
+constexpr uint32_t L_REC = L_PVAL + NPATCH;        // u32[CAP] the records of the chunk being consumed
+constexpr uint32_t LDS_BYTES = L_REC + 4 * CAP;
 enum { S_PRELEN = 0, S_A0, S_A1, S_B0, S_B1, S_WRITTEN, S_CLIENT, S_FCLOCK, S_OUTB };
 constexpr uint32_t NONE = 0xffffffffu;
 
@@ -91,6 +91,17 @@ __device__ unsigned long long pw_prof[8];
 // wave's store of its lanes' k-th records is 512 contiguous bytes (whole cache lines: lane-strided 8-byte
 // stores left partial lines that cost a read-modify-write each).
 __device__ __forceinline__ uint64_t rec_idx(uint32_t g, uint32_t k) { return ((uint64_t)(g >> 6) * CAP + k) * 64 + (g & 63); }
+// A record is one u32: the struct's offset in its chunk (10 bits), its flags (bits 10-12: FAIL, Skip, patch)
+// and its clock length (19 bits; a longer struct is recorded as a FAIL, so the stitch re-parses it).  Half
+// the bytes of the (position, clock sum) pair it replaced: the walk writes, and the stitch reads, 4 bytes
+// per struct.
+constexpr uint32_t REC_CLEN = 1u << 19;
+__device__ __forceinline__ uint32_t rec_make(uint32_t off, uint32_t fl, uint32_t clen) {
+  return off | ((fl >> 18) & 0x1c00u) | (clen << 13);
+}
+// the record's position word (document position | F_* flags) in chunk cx
+__device__ __forceinline__ uint32_t rec_pw(uint32_t w, uint32_t cx) { return (cx * CH + (w & 1023u)) | ((w & 0x1c00u) << 18); }
+__device__ __forceinline__ uint32_t rec_clen(uint32_t w) { return w >> 13; }
 // ---- 0. eligibility and chunk counts ---------------------------------------------------------------
 // msz[d]: the section-parallel stitch's per-document area (k_pw_ms), for documents of >= ms_min sections
 __host__ __device__ inline uint64_t ms_area(uint32_t nsec);
@@ -117,13 +128,13 @@ __global__ void k_pw_prep(GeneralJob j, uint32_t *cnt, uint8_t *done, uint64_t p
 }
 
 // ---- 1. speculative chunk walk ----------------------------------------------------------------------
-// Records: (position | flags, clock sum of the chunk walk's records before this one).  Chunk descriptor
+// Records: one u32 per step (offset in the chunk | flags | clock length, rec_make).  Chunk descriptor
 // (5 x 16 B): {nrec | lastfail << 16, lastpatch | lastskip << 16, exit, clock sum at exit}, then the
 // first NFIRST records' position words and clock sums (the stitch's entry lookup needs no record load).
-// last* = index + 1 of the last FAIL / patched / Skip record (0: none); lastfail also counts a struct of
-// >= 2^21 clocks (clock sums over the chunk could wrap): the stitch takes such records one by one.
+// last* = index + 1 of the last FAIL / patched / Skip record (0: none); a struct of >= 2^19 clocks is
+// recorded as a FAIL (its length does not fit the record): the stitch takes such records one by one.
 __global__ void __launch_bounds__(256) k_pw_walk(GeneralJob j, const uint32_t *cbase, uint32_t nd, uint32_t total,
-                                                 uint4 *desc, uint2 *recs) {
+                                                 uint4 *desc, uint32_t *recs) {
   const uint32_t g = blockIdx.x * 256 + threadIdx.x;
   if (g >= total) return;
   uint32_t lo = 0, hi = nd - 1;  // the document: largest d with cbase[d] <= g
@@ -140,6 +151,9 @@ __global__ void __launch_bounds__(256) k_pw_walk(GeneralJob j, const uint32_t *c
   uint32_t nrec = 0, cum = 0, lastfail = 0, lastpatch = 0, lastskip = 0, fails = FAIL_RUN, okrun = 0;  // the chunk start is mid-struct: only short-cut candidates until two structs in a row
   bool frun = false, ovf = false, start = true;
   uint32_t p = c0;
+  uint32_t fpw[NFIRST], fcum[NFIRST];  // the first records' position words and clock sums (the descriptor)
+#pragma unroll
+  for (uint32_t k = 0; k < NFIRST; k++) { fpw[k] = POS_MASK; fcum[k] = 0; }
   while (p < c1) {
     if (start && p >= c0 + START_CHEAP) {
       start = false;
@@ -157,11 +171,17 @@ __global__ void __launch_bounds__(256) k_pw_walk(GeneralJob j, const uint32_t *c
     }
     if (ok || !frun) {
       if (nrec == CAP) { ovf = true; break; }  // overflow: the stitch re-parses this chunk
-      recs[rec_idx(g, nrec)] = make_uint2(p | (ok ? fl : F_FAIL), cum);
+      // a struct of >= 2^19 clocks is recorded as a FAIL (its length does not fit the record; clock sums
+      // over the chunk could wrap): the stitch takes the records from the entry up to here one by one and
+      // re-parses that struct
+      const bool big = ok && cl >= REC_CLEN;
+      const uint32_t rfl = ok && !big ? fl : F_FAIL;
+      recs[rec_idx(g, nrec)] = rec_make(p - c0, rfl, ok && !big ? cl : 0);
+#pragma unroll
+      for (uint32_t k = 0; k < NFIRST; k++)
+        if (k == nrec) { fpw[k] = p | rfl; fcum[k] = cum; }
       nrec++;
-      // a FAIL, or a struct of >= 2^21 clocks (clock sums over the chunk could wrap): the stitch takes
-      // the records from the entry up to here one by one
-      if (!ok || cl >= (1u << 21)) lastfail = nrec;
+      if (!ok || big) lastfail = nrec;
       if (ok && (fl & F_PATCH)) lastpatch = nrec;
       if (ok && (fl & F_SKIP)) lastskip = nrec;
     }
@@ -177,15 +197,12 @@ __global__ void __launch_bounds__(256) k_pw_walk(GeneralJob j, const uint32_t *c
     frun = !ok;
   }
   if (ovf) nrec = 0;
-  uint2 f[NFIRST];  // the first records, read back (this lane's own stores)
-#pragma unroll
-  for (uint32_t k = 0; k < NFIRST; k++) f[k] = k < nrec ? recs[rec_idx(g, k)] : make_uint2(POS_MASK, 0u);
   uint4 *Q = desc + 5ull * g;
   Q[0] = make_uint4(nrec | (lastfail << 16), lastpatch | (lastskip << 16), p, cum);
-  Q[1] = make_uint4(f[0].x, f[1].x, f[2].x, f[3].x);
-  Q[2] = make_uint4(f[4].x, f[5].x, f[6].x, f[7].x);
-  Q[3] = make_uint4(f[0].y, f[1].y, f[2].y, f[3].y);
-  Q[4] = make_uint4(f[4].y, f[5].y, f[6].y, f[7].y);
+  Q[1] = make_uint4(fpw[0], fpw[1], fpw[2], fpw[3]);
+  Q[2] = make_uint4(fpw[4], fpw[5], fpw[6], fpw[7]);
+  Q[3] = make_uint4(fcum[0], fcum[1], fcum[2], fcum[3]);
+  Q[4] = make_uint4(fcum[4], fcum[5], fcum[6], fcum[7]);
 }
 
 // ---- 2. stitch ----------------------------------------------------------------------------------------
@@ -304,7 +321,7 @@ __device__ bool slice_head(sc::cu32 *B, uint32_t adj, uint32_t s0, uint32_t s1, 
 
 // OP = OP_DIFF, OP_SV or OP_META (parseUpdateMeta: from = a section's first clock, to = its end clock)
 template <int OP>
-__global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *cbase, const uint4 *desc, const uint2 *recs,
+__global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *cbase, const uint4 *desc, const uint32_t *recs,
                                                   uint8_t *done, const uint64_t *msz) {
   const uint32_t lane = threadIdx.x;
   const Scr X = scratch(j);
@@ -440,8 +457,7 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
         // the consumption): C5 sections end inside chunks and cut mid-chunk, so most chunks go this way.
         if (staged != gc && s < nrec) {
           __syncthreads();
-          for (uint32_t k = lane; k < nrec; k += 64) at<uint2>(L_REC + 8 * k) = recs[rec_idx(gc, k)];
-          if (lane == 0) at<uint2>(L_REC + 8 * nrec) = make_uint2(cexit, cumx);
+          for (uint32_t k = lane; k < nrec; k += 64) at<uint32_t>(L_REC + 4 * k) = recs[rec_idx(gc, k)];
           __syncthreads();
           staged = gc;
         }
@@ -451,7 +467,7 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
           if (s >= nrec) break;
           PWP(5);
           const uint32_t kk = s + lane;
-          const uint32_t pw = kk < nrec ? at<uint2>(L_REC + 8 * kk).x : POS_MASK;
+          const uint32_t pw = kk < nrec ? rec_pw(at<uint32_t>(L_REC + 4 * kk), cx) : POS_MASK;
           const uint64_t lt = __ballot(kk < nrec && (pw & POS_MASK) < x);
           const uint32_t nlt = __popcll(lt);
           if (nlt == 64) { s += 64; continue; }
@@ -471,12 +487,12 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
           const uint32_t kk = s + lane;
           valid = lane < n;
           if (valid) {
-            const uint2 r = at<uint2>(L_REC + 8 * kk);
-            const uint2 r1 = at<uint2>(L_REC + 8 * (kk + 1));  // (record nrec: the exit sentinel)
-            pos = r.x & POS_MASK;
-            fl = r.x;
-            clen = r1.y - r.y;
-            end = r1.x & POS_MASK;
+            const uint32_t w = at<uint32_t>(L_REC + 4 * kk);
+            fl = rec_pw(w, cx);
+            pos = fl & POS_MASK;
+            clen = rec_clen(w);
+            // a struct ends where the next record starts (the chunk's last one at the walk's exit)
+            end = kk + 1 < nrec ? rec_pw(at<uint32_t>(L_REC + 4 * (kk + 1)), cx) & POS_MASK : cexit;
           }
           const uint64_t fm = __ballot(valid && (fl & F_FAIL));
           if (fm) {  // a FAIL inside: consume up to it, the next round re-parses that struct uncapped
@@ -795,7 +811,7 @@ __device__ __forceinline__ void desc_at(DescWin &W, const uint4 *desc, uint32_t 
 }
 // the record index of position x in chunk cx (a true struct start), or NONE: the descriptor's first
 // records, then a ballot over the records 64 at a time
-__device__ __forceinline__ uint32_t rec_entry(const DescWin &W, const uint2 *recs, uint32_t gc, uint32_t cx, uint32_t nrec, uint32_t x) {
+__device__ __forceinline__ uint32_t rec_entry(const DescWin &W, const uint32_t *recs, uint32_t gc, uint32_t cx, uint32_t nrec, uint32_t x) {
   const int di = (int)(cx - W.wb);
 #pragma unroll
   for (uint32_t kf = 0; kf < NFIRST; kf++) {
@@ -805,7 +821,7 @@ __device__ __forceinline__ uint32_t rec_entry(const DescWin &W, const uint2 *rec
   const uint32_t lane = threadIdx.x % 64;
   for (uint32_t s = NFIRST; s < nrec; s += 64) {
     const uint32_t kk = s + lane;
-    const uint32_t pw = kk < nrec ? recs[rec_idx(gc, kk)].x : POS_MASK;
+    const uint32_t pw = kk < nrec ? rec_pw(recs[rec_idx(gc, kk)], cx) : POS_MASK;
     const uint64_t lt = __ballot(kk < nrec && (pw & POS_MASK) < x);
     const uint32_t nlt = __popcll(lt);
     if (nlt == 64) continue;
@@ -818,7 +834,7 @@ __device__ __forceinline__ uint32_t rec_entry(const DescWin &W, const uint2 *rec
 // phase A: the position after `w` structs from x (a true struct start), along the walk's records; a
 // struct the records do not cover (a FAIL under the speculative cap, a chain the walk missed) is parsed
 // here, uncapped.  False: a struct does not parse (the document is declined).
-__device__ bool skip_structs(DescWin &W, const uint4 *desc, const uint2 *recs, uint32_t cb, uint32_t nch, const uint8_t *D,
+__device__ bool skip_structs(DescWin &W, const uint4 *desc, const uint32_t *recs, uint32_t cb, uint32_t nch, const uint8_t *D,
                              uint32_t len, uint32_t &x, uint32_t w) {
   const uint32_t lane = threadIdx.x % 64;
   while (w > 0) {
@@ -838,7 +854,7 @@ __device__ bool skip_structs(DescWin &W, const uint4 *desc, const uint2 *recs, u
     }
     // records fs .. fs + 63: up to the first FAIL (re-parsed next round) or w structs
     const uint32_t kk = fs + lane;
-    const uint32_t pw = kk < nrec ? recs[rec_idx(gc, kk)].x : POS_MASK;
+    const uint32_t pw = kk < nrec ? rec_pw(recs[rec_idx(gc, kk)], cx) : POS_MASK;
     const uint64_t fm = __ballot(kk < nrec && (pw & F_FAIL));
     uint32_t n = nrec - fs < 64 ? nrec - fs : 64;
     if (fm) n = (uint32_t)__builtin_ctzll(fm);
@@ -852,14 +868,14 @@ __device__ bool skip_structs(DescWin &W, const uint4 *desc, const uint2 *recs, u
     if (w < n) n = w;
     // the position after the n-th struct: the next record's start, or the chunk's exit
     const uint32_t nxt = lane_read(pw, n < 64 ? n : 63);
-    x = fs + n < nrec ? (n < 64 ? (nxt & POS_MASK) : (recs[rec_idx(gc, fs + n)].x & POS_MASK)) : cexit;
+    x = fs + n < nrec ? (n < 64 ? (nxt & POS_MASK) : (rec_pw(recs[rec_idx(gc, fs + n)], cx) & POS_MASK)) : cexit;
     w -= n;
   }
   return true;
 }
 
 template <int OP>
-__global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, const uint32_t *cbase, const uint4 *desc, const uint2 *recs,
+__global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, const uint32_t *cbase, const uint4 *desc, const uint32_t *recs,
                                                 uint8_t *done, const uint64_t *msz, const uint64_t *moff, uint8_t *area) {
   const uint32_t t = threadIdx.x, lane = t % 64, wv = t / 64;
   __shared__ uint32_t mkey[OP == OP_DIFF ? MSVSLOTS : 1], mval[OP == OP_DIFF ? MSVSLOTS : 1], svclk[OP == OP_DIFF ? MSVMAX : 1];
@@ -997,7 +1013,7 @@ __global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, const uint32_t *cb
         for (;;) {
           if (s >= nrec) break;
           const uint32_t kk = s + lane;
-          const uint32_t pw = kk < nrec ? recs[rec_idx(gc, kk)].x : POS_MASK;
+          const uint32_t pw = kk < nrec ? rec_pw(recs[rec_idx(gc, kk)], cx) : POS_MASK;
           const uint64_t lt = __ballot(kk < nrec && (pw & POS_MASK) < x);
           const uint32_t nlt = __popcll(lt);
           if (nlt == 64) { s += 64; continue; }
@@ -1016,12 +1032,11 @@ __global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, const uint32_t *cb
           const uint32_t kk = s + lane;
           valid = lane < n;
           if (valid) {
-            const uint2 r = recs[rec_idx(gc, kk)];
-            const uint2 r1 = kk + 1 < nrec ? recs[rec_idx(gc, kk + 1)] : make_uint2(cexit, cumx);
-            pos = r.x & POS_MASK;
-            fl = r.x;
-            clen = r1.y - r.y;
-            end = r1.x & POS_MASK;
+            const uint32_t w = recs[rec_idx(gc, kk)];
+            fl = rec_pw(w, cx);
+            pos = fl & POS_MASK;
+            clen = rec_clen(w);
+            end = kk + 1 < nrec ? rec_pw(recs[rec_idx(gc, kk + 1)], cx) & POS_MASK : cexit;
           }
           const uint64_t fm = __ballot(valid && (fl & F_FAIL));
           if (fm) {
@@ -1348,13 +1363,13 @@ int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const ui
   *done_out = done;  // every document is marked (0 = not taken) from here on
   pw_last_done = done;
   if (total == 0) return 1;
-  if (pw_ensure(B, 2, 80ull * total) || pw_ensure(B, 3, 8ull * CAP * ((total + 63) & ~63u))) {
+  if (pw_ensure(B, 2, 80ull * total) || pw_ensure(B, 3, 4ull * CAP * ((total + 63) & ~63u))) {
     // no room for the records: leave every document to k_big_v1
     hipMemsetAsync(done, 0, j.n, st);
     return 1;
   }
   uint4 *desc = (uint4 *)B.p[2];
-  uint2 *recs = (uint2 *)B.p[3];
+  uint32_t *recs = (uint32_t *)B.p[3];
   if (mtotal > 0 && pw_ensure(B, 4, mtotal + 256)) {  // no room for the section tables: the one-wave stitch takes them
     hipMemsetAsync(msz, 0, 8ull * n1, st);
   }
