@@ -292,7 +292,7 @@ __device__ __forceinline__ bool v2_read(Doc &D, uint32_t info, uint32_t sn, Rec 
       if ((info & 31) == 6) rstr(D, sn, r.ka, r.kn);
       Cur c = s_cur(D, I_REST, MREST);
       r.r0 = c.p - ist(I_REST, 2);
-      any_canon(c);
+      any_canon<true>(c);
       s_commit(D, I_REST, c);
       r.r1 = ist(I_REST, 0);
       break;
@@ -311,7 +311,7 @@ __device__ __forceinline__ bool v2_read(Doc &D, uint32_t info, uint32_t sn, Rec 
       r.len = uopt_read(D, I_LN);
       Cur c = s_cur(D, I_REST, MREST);
       r.r0 = c.p - ist(I_REST, 2);
-      for (uint32_t i = 0; i < r.len && !c.bad; i++) any_canon(c);
+      for (uint32_t i = 0; i < r.len && !c.bad; i++) any_canon<true>(c);
       s_commit(D, I_REST, c);
       r.r1 = ist(I_REST, 0);
       break;
@@ -363,7 +363,7 @@ __device__ __forceinline__ void v2_write(Doc &D, const Rec &r, uint32_t off, uin
         const uint32_t wd = ist(I_REST, 2);
         if (r.r0 + wd < L_WREST || r.r1 + wd > L_WREST + WREST) { set_bad(); return; }
         Cur c = {r.r0 + wd, r.r1 + wd, false};
-        for (uint32_t i = 0; i < off; i++) any_canon(c);
+        for (uint32_t i = 0; i < off; i++) any_canon<true>(c);
         if (c.bad) { set_bad(); return; }
         a = c.p - wd;
       }

@@ -230,7 +230,10 @@ __device__ __forceinline__ uint64_t has_byte(uint64_t x, uint64_t b) {
 __device__ __forceinline__ uint64_t has_ctl(uint64_t x) {
   return (x - 0x2020202020202020ull) & ~x & 0x8080808080808080ull;
 }
-// JSON text as yjs writes it for formats / embeds: true | false | null | "string without escapes"
+// JSON text as yjs writes it for formats / embeds: true | false | null | "string without escapes"; with
+// NESTED also integers, arrays and objects (ym_canon_chk.h, an out-of-line call: only the kernels off the
+// headline path instantiate it, the call's stack and registers would cost the LDS merge kernel occupancy)
+template <bool NESTED = false>
 __device__ __forceinline__ void json_lit(Cur &c) {
   const uint32_t n = rvu(c);
   if (c.bad || !room(c, n)) { c.bad = true; return; }
@@ -252,7 +255,7 @@ __device__ __forceinline__ void json_lit(Cur &c) {
     ok = bad == 0;
   }
   // numbers, objects, arrays: JSON.stringify(JSON.parse(text)) == text (ym_canon_chk.h)
-  if (!ok) ok = cchk::json_canon_ptr(sm, c.p, n);
+  if (NESTED && !ok) ok = cchk::json_canon_ptr(sm, c.p, n);
   if (!ok) { c.bad = true; return; }
   utf16_len(c, n);
 }
@@ -297,10 +300,11 @@ __device__ __forceinline__ void any_scalar(Cur &c) {
   }
 }
 
-// one `any` value of any shape in the form writeAny emits (nested values: ym_canon_chk.h)
+// one `any` value in the form writeAny emits: scalars; with NESTED also nested values (ym_canon_chk.h)
+template <bool NESTED = false>
 __device__ __forceinline__ void any_canon(Cur &c) {
   const uint32_t tag = c.p < c.e ? sm[c.p] : 0;
-  if (tag == 116 || tag == 117 || tag == 118 || tag == 122) {
+  if (NESTED && (tag == 116 || tag == 117 || tag == 118 || tag == 122)) {
     uint32_t q = c.p;
     c.bad |= !cchk::any_canon_ptr(sm, c.p, c.e, &q);
     c.p = q;
@@ -312,6 +316,7 @@ __device__ __forceinline__ void any_canon(Cur &c) {
 // The fields and content of one V1 Item after its info byte (UpdateDecoder.js:127-243 field readers,
 // Item.js:665-683 content refs; lazy reader of 13.5.16: parent kept raw, parentSub only without
 // origins).  Returns false (decline) for kinds this path does not verify; `len` = the Item's length.
+template <bool NESTED = false>
 __device__ __forceinline__ bool item_body(Cur &c, uint32_t info, uint32_t &len) {
   if (info & 0x80) skvu2(c);
   if (info & 0x40) skvu2(c);
@@ -327,8 +332,8 @@ __device__ __forceinline__ bool item_body(Cur &c, uint32_t info, uint32_t &len) 
     case 1: len = rvu(c); break;                                      // ContentDeleted
     case 3: { const uint32_t n = rvu(c); if (!room(c, n)) c.bad = true; else c.p += n; break; }  // Binary
     case 4: len = rstr(c); break;                                     // ContentString
-    case 5: json_lit(c); break;                                       // ContentEmbed
-    case 6: rstr(c); json_lit(c); break;                              // ContentFormat
+    case 5: json_lit<NESTED>(c); break;                               // ContentEmbed
+    case 6: rstr(c); json_lit<NESTED>(c); break;                      // ContentFormat
     case 7: {                                                         // ContentType
       const uint32_t t = rvu(c);
       c.bad |= t > 6;
@@ -337,7 +342,7 @@ __device__ __forceinline__ bool item_body(Cur &c, uint32_t info, uint32_t &len) 
     }
     case 8:                                                           // ContentAny
       len = rvu(c);
-      for (uint32_t i = 0; i < len && !c.bad; i++) any_canon(c);
+      for (uint32_t i = 0; i < len && !c.bad; i++) any_canon<NESTED>(c);
       break;
     default: c.bad = true; break;  // ContentJSON, ContentDoc, invalid refs
   }

@@ -140,6 +140,7 @@ __device__ __forceinline__ uint64_t has_byte(uint64_t x, uint64_t v) {
 }
 __device__ __forceinline__ uint64_t has_ctl(uint64_t x) { return (x - 0x2020202020202020ull) & ~x & 0x8080808080808080ull; }
 // JSON text as yjs writes it for formats / embeds: true | false | null | "string without escapes"
+template <bool NESTED = false>
 __device__ __forceinline__ void json_lit(LCur &c) {
   const uint32_t n = rvu(c);
   if (c.bad || !room(c, n) || n > c.cap) { c.bad = true; return; }
@@ -159,7 +160,7 @@ __device__ __forceinline__ void json_lit(LCur &c) {
     ok = bad == 0;
   }
   // numbers, objects, arrays: JSON.stringify(JSON.parse(text)) == text (ym_canon_chk.h)
-  if (!ok) ok = cchk::json_canon_ptr(c.b, c.p, n);
+  if (NESTED && !ok) ok = cchk::json_canon_ptr(c.b, c.p, n);
   if (!ok) { c.bad = true; return; }
   utf16_len(c, n);
 }
@@ -277,6 +278,10 @@ __device__ __noinline__ void any_nested(LCur &c) {
 
 // Item fields and content after the info byte; false for kinds the verbatim path does not verify
 // (ContentJSON, ContentDoc, bad refs) or any anomaly.  `len` = the Item's clock length.
+// NESTED: nested `any` values and JSON texts through ym_canon_chk.h's out-of-line checks.  The chunk walk and
+// its stitch do without (their call stack and registers would halve the walk's occupancy): a nested value
+// fails there, and the document goes to the streamed walker, which checks it.
+template <bool NESTED = false>
 __device__ __forceinline__ bool item_body(LCur &c, uint32_t info, uint32_t &len) {
   if (info & 0x80) { skvu(c); skvu(c); }
   if (info & 0x40) { skvu(c); skvu(c); }
@@ -292,8 +297,8 @@ __device__ __forceinline__ bool item_body(LCur &c, uint32_t info, uint32_t &len)
     case 1: len = rvu(c); break;
     case 3: { const uint32_t n = rvu(c); if (!room(c, n) || n > c.cap) c.bad = true; else skip(c, n); break; }
     case 4: len = rstr(c); break;
-    case 5: json_lit(c); break;
-    case 6: rstr(c); json_lit(c); break;
+    case 5: json_lit<NESTED>(c); break;
+    case 6: rstr(c); json_lit<NESTED>(c); break;
     case 7: {
       const uint32_t t = rvu(c);
       c.bad |= t > 6;
@@ -303,7 +308,10 @@ __device__ __forceinline__ bool item_body(LCur &c, uint32_t info, uint32_t &len)
     case 8:
       len = rvu(c);
       c.bad |= len > c.cap;
-      for (uint32_t i = 0; i < len && !c.bad; i++) any_canon(c);
+      for (uint32_t i = 0; i < len && !c.bad; i++) {
+        if (NESTED) any_canon(c);
+        else any_scalar(c);
+      }
       break;
     default: c.bad = true; break;
   }

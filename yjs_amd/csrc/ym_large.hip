@@ -116,7 +116,7 @@ __device__ bool walk_v1(const LMJob &J, uint32_t p0, uint32_t p1, uint64_t gb, c
       const uint32_t info = rdb(c);
       if (info == 10 || (info & 31) == 0) return false;  // Skip / GC inputs: general path
       uint32_t len;
-      if (!item_body(c, info, len)) return false;
+      if (!item_body<true>(c, info, len)) return false;
       if ((uint64_t)clock + len > 0xffffffffull) return false;
       const uint64_t key = ((uint64_t)(~client) << 32) | clock;
       if (have_prev && key <= prev) return false;  // each update must already be in merge order
@@ -295,7 +295,7 @@ __device__ bool walk_v2(const LMJob &J, uint32_t p0, uint32_t p1, uint64_t gb, c
         case 5: case 6: {                                                   // Embed / Format (+ key)
           if ((info & 31) == 6) s2 = rstr();
           const uint32_t a = c.p;
-          any_canon(c);
+          any_canon<true>(c);
           sp = gb + a;
           spn = c.p - a;
           break;
@@ -312,7 +312,7 @@ __device__ bool walk_v2(const LMJob &J, uint32_t p0, uint32_t p1, uint64_t gb, c
         case 8: {                                                           // ContentAny
           len = rd_uopt(ln);
           const uint32_t a = c.p;
-          for (uint32_t q = 0; q < len && !c.bad; q++) any_canon(c);
+          for (uint32_t q = 0; q < len && !c.bad; q++) any_canon<true>(c);
           sp = gb + a;
           spn = c.p - a;
           break;

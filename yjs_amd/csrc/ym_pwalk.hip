@@ -151,9 +151,11 @@ __global__ void __launch_bounds__(256) k_pw_walk(GeneralJob j, const uint32_t *c
   uint32_t nrec = 0, cum = 0, lastfail = 0, lastpatch = 0, lastskip = 0, fails = FAIL_RUN, okrun = 0;  // the chunk start is mid-struct: only short-cut candidates until two structs in a row
   bool frun = false, ovf = false, start = true;
   uint32_t p = c0;
-  uint32_t fpw[NFIRST], fcum[NFIRST];  // the first records' position words and clock sums (the descriptor)
-#pragma unroll
-  for (uint32_t k = 0; k < NFIRST; k++) { fpw[k] = POS_MASK; fcum[k] = 0; }
+  // the descriptor's first-record words (position | flags, clock sum) are stored as the records come
+  uint4 *Q = desc + 5ull * g;
+  uint32_t *fpw = reinterpret_cast<uint32_t *>(Q + 1), *fcum = reinterpret_cast<uint32_t *>(Q + 3);
+  Q[1] = Q[2] = make_uint4(POS_MASK, POS_MASK, POS_MASK, POS_MASK);
+  Q[3] = Q[4] = make_uint4(0, 0, 0, 0);
   while (p < c1) {
     if (start && p >= c0 + START_CHEAP) {
       start = false;
@@ -177,9 +179,7 @@ __global__ void __launch_bounds__(256) k_pw_walk(GeneralJob j, const uint32_t *c
       const bool big = ok && cl >= REC_CLEN;
       const uint32_t rfl = ok && !big ? fl : F_FAIL;
       recs[rec_idx(g, nrec)] = rec_make(p - c0, rfl, ok && !big ? cl : 0);
-#pragma unroll
-      for (uint32_t k = 0; k < NFIRST; k++)
-        if (k == nrec) { fpw[k] = p | rfl; fcum[k] = cum; }
+      if (nrec < NFIRST) { fpw[nrec] = p | rfl; fcum[nrec] = cum; }
       nrec++;
       if (!ok || big) lastfail = nrec;
       if (ok && (fl & F_PATCH)) lastpatch = nrec;
@@ -197,12 +197,7 @@ __global__ void __launch_bounds__(256) k_pw_walk(GeneralJob j, const uint32_t *c
     frun = !ok;
   }
   if (ovf) nrec = 0;
-  uint4 *Q = desc + 5ull * g;
   Q[0] = make_uint4(nrec | (lastfail << 16), lastpatch | (lastskip << 16), p, cum);
-  Q[1] = make_uint4(fpw[0], fpw[1], fpw[2], fpw[3]);
-  Q[2] = make_uint4(fpw[4], fpw[5], fpw[6], fpw[7]);
-  Q[3] = make_uint4(fcum[0], fcum[1], fcum[2], fcum[3]);
-  Q[4] = make_uint4(fcum[4], fcum[5], fcum[6], fcum[7]);
 }
 
 // ---- 2. stitch ----------------------------------------------------------------------------------------
@@ -283,7 +278,7 @@ __device__ bool slice_head(sc::cu32 *B, uint32_t adj, uint32_t s0, uint32_t s1, 
       put(len - off);
     } else if (ref == 8) {
       sc::rvu(e);
-      for (uint32_t i = 0; i < off; i++) sc::any_canon(e);  // ContentAny.splice: drop `off` values
+      for (uint32_t i = 0; i < off; i++) sc::any_scalar(e);  // ContentAny.splice: drop `off` values
       put(len - off);
       a0 = e.p - adj;
       a1 = s1;
