@@ -48,8 +48,9 @@ def test_golden_through_chunked_walk(engine, key, ms, monkeypatch):
     if ms:
         monkeypatch.setenv("YMERGE_PWMS_MIN", ms)
     _check_group(engine, key)
-    if key[1] == 1:  # the V1 walk accepts exactly what the sequential walker accepts
-        assert engine.stats["docs_chunked"] == engine.stats["docs_fast"] > 0, engine.stats
+    if key[1] == 1:  # the V1 walk accepts what the sequential walker accepts, except nested payloads (objects /
+        # arrays in ContentAny, integer / object JSON formats: checked out of line by the sequential walker only)
+        assert 0 < engine.stats["docs_chunked"] <= engine.stats["docs_fast"], engine.stats
     else:  # the V2 paths (one section: String / Deleted / GC; several: XML / format / any content too)
         assert engine.stats["docs_chunked"] > 0, engine.stats
 
