@@ -251,9 +251,11 @@ def _secondary_case(dev, eng, name, op, wl, n):
         st = torch.empty(nd, dtype=torch.int32, device=dev)
         steps = 5 if op in ("merge", "meta", "dsmerge") else 2
         rc0, used0 = eng.run_device(op, fmt, ga, go, gd, oa, oo, ol, st, gsa, gso)
-        if rc0 == 9:  # YM_ERR_CAPACITY: the call reports what it needs (the streamed V2 diff walker uses the
-            # output arena as scratch, ~2 KB per client section); a caller grows the arena once
-            cap = used0 + 65536
+        for _ in range(3):  # YM_ERR_CAPACITY: the call reports what it needed so far (the streamed V2 diff
+            # walker uses the output arena as scratch, ~2 KB per client section); a caller grows the arena
+            if rc0 != 9:
+                break
+            cap = 2 * used0 + 65536
             oa = torch.empty(cap, dtype=torch.uint8, device=dev)
             rc0, used0 = eng.run_device(op, fmt, ga, go, gd, oa, oo, ol, st, gsa, gso)
         if rc0 != 0:
