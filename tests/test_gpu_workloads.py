@@ -609,6 +609,9 @@ def test_rich_content_stays_on_the_specialised_paths(engine, name):
     bad = _compare(engine.run_host("merge", fmt, a, o, d), outs, status)
     assert not bad, bad[:10]
     assert engine.stats["docs_general"] == 0, engine.stats
+    # the LDS merge kernels' retry pass with nested payload checks takes most of them (the rest: inputs
+    # over the kernels' staging size, to the large-document pipeline)
+    assert engine.stats["docs_fast"] >= 0.6 * n, engine.stats
     a2, o2, d2 = pack_docs([[m] for m in outs])
     svo, sst, _ = O.batch("sv", fmt, a2, o2, d2, nthreads=8)
     bad = _compare(engine.run_host("sv", fmt, a2, o2, d2), svo, sst)

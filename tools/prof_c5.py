@@ -15,7 +15,7 @@ import oracle_ref as O  # noqa: E402
 from yjs_amd import Engine, pack_docs  # noqa: E402
 from yjs_amd.workloads import load_ymb, random_state_vectors  # noqa: E402
 
-eng = Engine(0)
+eng = Engine(0, path=os.environ["YMLIB"]) if os.environ.get("YMLIB") else Engine(0)  # YMLIB: e.g. the prof build
 dev = torch.device("cuda", 0)
 reps = int(os.environ.get("REPS", "32"))  # documents = 8 templates x reps (bench: 256)
 for fmt in [int(x) for x in os.environ.get("FMTS", "2,1").split(",")]:
@@ -55,7 +55,15 @@ for fmt in [int(x) for x in os.environ.get("FMTS", "2,1").split(",")]:
         import ctypes
         pr = (ctypes.c_ulonglong * 8)()
         eng.lib.ym__pw_prof(pr, 1)
-        print("   k_pw_ms phase ticks (100 MHz, summed over docs and calls) A %d B %d C %d patches %d" % (pr[0], pr[1], pr[2], pr[3]))
+        print("   pw_prof: k_pw_ms phase ticks A %d B %d C %d patches %d | stitch counters: whole %d, entry not whole %d, "
+              "entry not in first %d, record batches %d, re-parsed structs %d, search loads %d" % (tuple(pr[:4]) + tuple(pr[:6])))
+        if hasattr(eng.lib, "ym__pw_ticks"):
+            tk = (ctypes.c_ulonglong * 16)()
+            eng.lib.ym__pw_ticks(tk, 1)
+            if any(tk):
+                names = "sv hdr desc stage search consume cut ds alloc write patch".split()
+                per = 1e-2 / (len(docs) * 6)  # us per document per call (6 calls incl. the checked one)
+                print("   k_pw_stitch us/doc: " + " ".join("%s %.0f" % (n, tk[i] * per) for i, n in enumerate(names)), flush=True)
         eng.lib.ym__ms_prof(pr, 1)
         print("   k_ms_rest: ticks %d info entries %d len entries %d rest fast %d rest cursor %d window loads %d global %d" % tuple(pr[:7]))
         for i in bad[:2]:

@@ -196,7 +196,9 @@ __device__ __forceinline__ bool item_fast(Cur &c, uint32_t info, uint32_t &len) 
 // atomic counter, misc[0]); records where its delete set starts.  Item info bytes with an origin and
 // the parentSub bit get the bit cleared in place (13.5.16's lazy reader reads parentSub only without
 // origins and writes the info byte back without it, E8), so sections copy verbatim afterwards.
-// Returns false to decline.
+// Returns false to decline.  NESTED: nested payloads (any objects / arrays, JSON texts) are checked too
+// (the retry pass over the documents the hot kernel declined; ym_canon_chk.h).
+template <bool NESTED = false>
 __device__ __forceinline__ bool walk_sections(uint32_t u) {
   Cur c = {at<uint16_t>(L_UOFF + 2 * u), at<uint16_t>(L_UOFF + 2 * u + 2), false};
   const uint32_t nclients = rvu(c);
@@ -213,7 +215,7 @@ __device__ __forceinline__ bool walk_sections(uint32_t u) {
       const uint32_t info = rdb(c);
       c.bad |= info == 10 || (info & 31) == 0;  // Skip / GC -> general path
       uint32_t l = 1;
-      if (!c.bad && !item_fast(c, info, l)) c.bad |= !item_body(c, info, l);
+      if (!c.bad && !item_fast(c, info, l)) c.bad |= !item_body<NESTED>(c, info, l);
       if ((info & 0xC0) != 0 && (info & 0x20) != 0) sm[s0] = (uint8_t)(info & ~0x20u);
       len += l;
     }
@@ -702,12 +704,15 @@ __device__ __forceinline__ int ds_phase(const GeneralJob &j, uint32_t d, uint32_
 // struct section); the walk is W2 only and the output is the merged delete set alone, in the DSEncoderV1
 // format, or DSEncoderV2's (DSV2: clocks delta-coded within a client, lengths minus one).
 // Grid: a multiple of 8 blocks; block b takes documents (b % 8) * G/8 + b / 8 + k * G.
-template <int STOP, int OCC, bool DSONLY = false, bool DSV2 = false>
-__global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
+// NESTED: the retry pass over the `nd` documents listed in j.list (those the first pass declined), with
+// nested payload checks; its declines go to j.pend_list as before.
+template <int STOP, int OCC, bool DSONLY = false, bool DSV2 = false, bool NESTED = false>
+__global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j, uint32_t nd) {
   const uint32_t lane = threadIdx.x;
   const uint64_t arena0 = uoff_g(j, 0);
   const uint32_t d0 = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-  for (uint32_t d = d0; d < j.n; d += gridDim.x) {
+  for (uint32_t di = d0; di < nd; di += gridDim.x) {
+    const uint32_t d = NESTED ? j.list[di] : di;
     const uint32_t u0 = j.doc_upd[d], k = j.doc_upd[d + 1] - u0;
     const uint64_t b0 = uoff_g(j, u0), bytes = uoff_g(j, u0 + k) - b0;
     if ((DSONLY ? k == 0 : k <= 1) || k > UPD || bytes > IN) {
@@ -787,7 +792,7 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j) {
       __syncthreads();
       bool ok = true;
 #pragma unroll 1
-      for (uint32_t i = lane; i < n1; i += 64) ok &= walk_sections(at<uint8_t>(L_UORD + i));
+      for (uint32_t i = lane; i < n1; i += 64) ok &= walk_sections<NESTED>(at<uint8_t>(L_UORD + i));
       if (__any(!ok)) YM_DECLINE()
       __syncthreads();
       YM_STOP(8)
@@ -863,8 +868,8 @@ int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st
   if (op == OP_DSMERGE) {  // delete-set merges: the same kernel, delete sets only
     if (j.dsref) return 0;  // the reference's adjacency-only coalescing: general path
     const uint32_t grid = fast_grid(j.n);
-    if (j.v2) k_fast_merge_v1<0, 5, true, true><<<grid, 64, fastv1::LDS_BYTES, st>>>(j);
-    else k_fast_merge_v1<0, 5, true, false><<<grid, 64, fastv1::LDS_BYTES, st>>>(j);
+    if (j.v2) k_fast_merge_v1<0, 5, true, true><<<grid, 64, fastv1::LDS_BYTES, st>>>(j, j.n);
+    else k_fast_merge_v1<0, 5, true, false><<<grid, 64, fastv1::LDS_BYTES, st>>>(j, j.n);
     return 1;
   }
   if (op != OP_MERGE || j.v2) return 0;  // fast path: V1 merges (the C2/C4 headline configs)
@@ -880,7 +885,7 @@ int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st
   const uint32_t LDS_BYTES = fastv1::LDS_BYTES + pad;
   static int occ = -1;
   if (occ < 0) { const char *e = getenv("YMERGE_FAST_OCC"); occ = e ? atoi(e) : 5; }
-#define YM_LAUNCH(S, O) k_fast_merge_v1<S, O><<<grid, 64, LDS_BYTES, st>>>(j)
+#define YM_LAUNCH(S, O) k_fast_merge_v1<S, O><<<grid, 64, LDS_BYTES, st>>>(j, j.n)
   if (occ == 4) {
     YM_LAUNCH(0, 4);
   } else if (occ == 6) {
@@ -898,6 +903,19 @@ int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st
     }
   }
 #undef YM_LAUNCH
+  return 1;
+}
+
+// The retry pass: V1 merges the hot kernel declined (j.list, n documents), now with nested payload checks
+// (rich content: any objects / arrays, JSON texts); what this pass declines goes on to the large-document
+// pipeline / general path through j.pend_list.
+int fast_nested_launch(const GeneralJob &j, uint32_t n, hipStream_t st) {
+  using namespace fastv1;
+  if (j.op != OP_MERGE || j.v2 || !j.list || n == 0) return 0;
+  static int off = -1;
+  if (off < 0) { const char *e = getenv("YMERGE_FAST_NESTED"); off = e && atoi(e) == 0 ? 1 : 0; }
+  if (off) return 0;
+  k_fast_merge_v1<0, 5, false, false, true><<<fast_grid(n), 64, fastv1::LDS_BYTES, st>>>(j, n);
   return 1;
 }
 

@@ -128,7 +128,9 @@ __device__ __forceinline__ void decline(const GeneralJob &j, uint32_t d) {
   j.pend_list[atomicAdd(j.pend_count, 1u)] = d;
 }
 
-// Walks one V2 update (lane-private decoders) and appends struct records and delete ranges.
+// Walks one V2 update (lane-private decoders) and appends struct records and delete ranges.  NESTED:
+// nested any values (objects, arrays) are checked canonical too (the retry pass, ym_canon_chk.h).
+template <bool NESTED = false>
 __device__ __forceinline__ bool walk_v2(uint32_t u) {
   const uint32_t p0 = at<uint16_t>(L_UOFF + 2 * u), p1 = at<uint16_t>(L_UOFF + 2 * u + 2);
   Cur h = {p0, p1, false};
@@ -203,7 +205,7 @@ __device__ __forceinline__ bool walk_v2(uint32_t u) {
         case 5: case 6: {                                                  // Embed / Format (+ key)
           if ((info & 31) == 6) s2 = rstr();
           const uint32_t a = c.p;
-          any_canon(c);
+          any_canon<NESTED>(c);
           sp = a | ((c.p - a) << 16);
           break;
         }
@@ -219,7 +221,7 @@ __device__ __forceinline__ bool walk_v2(uint32_t u) {
         case 8: {                                                          // ContentAny
           len = rd_uopt(ln);
           const uint32_t a = c.p;
-          for (uint32_t i = 0; i < len && !c.bad; i++) any_canon(c);
+          for (uint32_t i = 0; i < len && !c.bad; i++) any_canon<NESTED>(c);
           sp = a | ((c.p - a) << 16);
           break;
         }
@@ -410,11 +412,13 @@ __device__ __forceinline__ uint32_t col_encode(Get get, uint32_t n, bool wr, O o
     __syncthreads();                                                    \
     continue;                                                           \
   }
-template <int STOP, int OCC = 1>
-__global__ void __launch_bounds__(64, OCC) k_fast_merge_v2(GeneralJob j) {
+// NESTED: the retry pass over the `nd` documents listed in j.list (those the first pass declined).
+template <int STOP, int OCC = 1, bool NESTED = false>
+__global__ void __launch_bounds__(64, OCC) k_fast_merge_v2(GeneralJob j, uint32_t nd) {
   const uint32_t lane = threadIdx.x;
   const uint64_t arena0 = j.upd_off[0];
-  for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
+  for (uint32_t di = blockIdx.x; di < nd; di += gridDim.x) {
+    const uint32_t d = NESTED ? j.list[di] : di;
     const uint32_t u0 = j.doc_upd[d], k = j.doc_upd[d + 1] - u0;
     const uint64_t b0 = j.upd_off[u0], bytes = j.upd_off[u0 + k] - b0;
     if (k <= 1 || k > UPD || bytes > IN) {
@@ -435,7 +439,7 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v2(GeneralJob j) {
     // ---- 2. walk
     bool ok = true;
 #pragma unroll 1
-    for (uint32_t u = lane; u < k; u += 64) ok &= walk_v2(u);
+    for (uint32_t u = lane; u < k; u += 64) ok &= walk_v2<NESTED>(u);
     if (__any(!ok)) YM2_DECLINE()
     __syncthreads();
     const uint32_t nrec = at<uint32_t>(L_MISC), nds = at<uint32_t>(L_MISC + 4);
@@ -948,17 +952,27 @@ int fast2_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t s
   if (stop < 0) { const char *e = getenv("YMERGE_FAST_STOP"); stop = e ? atoi(e) : 0; }
   if (occ < 0) { const char *e = getenv("YMERGE_FAST2_OCC"); occ = e ? atoi(e) : 3; }  // min waves / SIMD (3: 168 VGPRs, no spills)
   if (stop == 0 && occ >= 2) {
-    if (occ == 2) fastv2::k_fast_merge_v2<0, 2><<<grid, 64, fastv2::LDS_BYTES, st>>>(j);
-    else if (occ == 3) fastv2::k_fast_merge_v2<0, 3><<<grid, 64, fastv2::LDS_BYTES, st>>>(j);
-    else fastv2::k_fast_merge_v2<0, 4><<<grid, 64, fastv2::LDS_BYTES, st>>>(j);
+    if (occ == 2) fastv2::k_fast_merge_v2<0, 2><<<grid, 64, fastv2::LDS_BYTES, st>>>(j, j.n);
+    else if (occ == 3) fastv2::k_fast_merge_v2<0, 3><<<grid, 64, fastv2::LDS_BYTES, st>>>(j, j.n);
+    else fastv2::k_fast_merge_v2<0, 4><<<grid, 64, fastv2::LDS_BYTES, st>>>(j, j.n);
     return 1;
   }
   switch (stop) {
-#define YM2_L(S) case S: fastv2::k_fast_merge_v2<S><<<grid, 64, fastv2::LDS_BYTES, st>>>(j); break;
+#define YM2_L(S) case S: fastv2::k_fast_merge_v2<S><<<grid, 64, fastv2::LDS_BYTES, st>>>(j, j.n); break;
     YM2_L(1) YM2_L(2) YM2_L(3) YM2_L(4) YM2_L(5) YM2_L(6) YM2_L(7)
-    default: fastv2::k_fast_merge_v2<0><<<grid, 64, fastv2::LDS_BYTES, st>>>(j); break;
+    default: fastv2::k_fast_merge_v2<0><<<grid, 64, fastv2::LDS_BYTES, st>>>(j, j.n); break;
 #undef YM2_L
   }
+  return 1;
+}
+
+// The V2 retry pass with nested payload checks (see fast_nested_launch, ym_fast.hip).
+int fast2_nested_launch(const GeneralJob &j, uint32_t n, hipStream_t st) {
+  if (j.op != OP_MERGE || !j.v2 || !j.list || n == 0) return 0;
+  static int off = -1;
+  if (off < 0) { const char *e = getenv("YMERGE_FAST_NESTED"); off = e && atoi(e) == 0 ? 1 : 0; }
+  if (off) return 0;
+  fastv2::k_fast_merge_v2<0, 3, true><<<n < 131072 ? n : 131072, 64, fastv2::LDS_BYTES, st>>>(j, n);
   return 1;
 }
 

@@ -87,6 +87,20 @@ __device__ unsigned long long pw_prof[8];
 #else
 #define PWP(i) do { } while (0)
 #endif
+// stitch phase time (same build; ym__pw_ticks, 100 MHz ticks summed over documents): PT(i) charges the
+// time since the previous PT to phase i -- [0] state vector, [1] section headers + SV lookup, [2] chunk
+// descriptors + O(1) entry, [3] record staging, [4] record search, [5] consumption, [6] the cut + sliced
+// head, [7] delete set, [8] sizes + allocation, [9] write, [10] patches
+__device__ unsigned long long pw_ticks[16];
+#ifdef YM_PW_PROF
+#define PT_DECL uint64_t pt_t = __builtin_amdgcn_s_memrealtime(), pt_acc[11] = {};
+#define PT(i) do { const uint64_t t_ = __builtin_amdgcn_s_memrealtime(); pt_acc[i] += t_ - pt_t; pt_t = t_; } while (0)
+#define PT_FLUSH() do { if (threadIdx.x == 0) for (int i_ = 0; i_ < 11; i_++) atomicAdd(&pw_ticks[i_], pt_acc[i_]); } while (0)
+#else
+#define PT_DECL
+#define PT(i) do { } while (0)
+#define PT_FLUSH() do { } while (0)
+#endif
 // Record k of chunk g.  Chunks are grouped by 64 (one walking wave) with the records interleaved, so a
 // wave's store of its lanes' k-th records is 512 contiguous bytes (whole cache lines: lane-strided 8-byte
 // stores left partial lines that cost a read-modify-write each).
@@ -320,6 +334,7 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
                                                   uint8_t *done, const uint64_t *msz) {
   const uint32_t lane = threadIdx.x;
   const Scr X = scratch(j);
+  PT_DECL
   for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
     const uint32_t cb = cbase[d], nch = cbase[d + 1] - cb;
     if (nch == 0 || msz[d]) continue;  // (many sections: k_pw_ms)
@@ -351,6 +366,7 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
       if (bad) PW_DECLINE_R(3)
       if (nsv > 64) cmap::build_sv(X.map, X.svt, nsv);
     }
+    PT(0);
     // ---- struct section: headers parsed here, structs from the walk's records
     uint32_t x = 0;
     bool declined = false;
@@ -398,6 +414,7 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
       bool copying = false;
       uint32_t written = 0;
       uint32_t rem = nstructs;
+      PT(1);
       while (rem > 0) {
         if (x >= len) { declined = true; why = 7; break; }
         const uint32_t cx = x / CH;
@@ -415,6 +432,7 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
         const uint32_t cexit = lane_read(q0.z, di), cumx = lane_read(q0.w, di);
         if (cx != cc) { cc = cx; s = 0; }
         const uint32_t gc = cb + cx;
+        PT(2);
         // ---- chunk entry: x among the descriptor's first records -> the rest of the chunk in O(1)
         if (s == 0) {
           uint32_t fs = NONE, fcum = 0;
@@ -441,6 +459,7 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
               rem -= avail;
               x = cexit;
               s = nrec;
+              PT(5);
               continue;
             }
             PWP(1);
@@ -456,6 +475,7 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
           __syncthreads();
           staged = gc;
         }
+        PT(3);
         // locate x among the chunk's records (a ballot over 64 per step)
         bool found = false;
         for (;;) {
@@ -473,6 +493,7 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
           }
           break;
         }
+        PT(4);
         uint32_t n, pos = 0, end = 0, clen = 0, fl = 0;
         bool valid;
         if (found) {
@@ -524,6 +545,7 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
           if (!sv_stop && fs > 0) sv_clock = (uint32_t)(clock + lane_read(incl, fs - 1));
           if (skm) sv_stop = true;
         } else if (OP == OP_DIFF) {
+          PT(5);
           uint32_t first = 0;  // first struct of this batch written verbatim (patch range start)
           bool pend = false;
           if (!copying) {
@@ -583,6 +605,7 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
         clock += tot;
         x = lane_read(end, n - 1);
         rem -= n;
+        PT(OP == OP_DIFF ? 6 : 5);
       }
       if (declined) break;
       if (OP == OP_META && nstructs > 0) {
@@ -688,6 +711,7 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
     if (declined) PW_DECLINE()
     why = 0;
     const uint32_t ds1 = x;
+    PT(7);
     __threadfence_block();
     __syncthreads();
     // ---- sizes, allocation
@@ -708,32 +732,48 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
       __syncthreads();
       continue;
     }
-    // ---- write: small pieces by lane 0, spans by the wave, then the info patches
+    PT(8);
+    // ---- write: 64 sections per round, one per lane for the section table reads, the header and the
+    // sliced head (placed by a wave prefix sum of the section sizes), then the wave copies the spans
+    // section by section -- a C5 document's ~1,000 sections no longer cost ~5 dependent loads each
     uint8_t *const o = j.out + base;
     if (lane == 0) put_vu_g(o, 0, nparts);
     uint32_t p = vsz(nparts);
-    for (uint32_t ci = 0; ci < nclients; ci++) {
-      const uint32_t pl = sec(ci, S_PRELEN);
-      if (pl == NONE) continue;
-      const uint32_t written = sec(ci, S_WRITTEN), client = sec(ci, S_CLIENT), fclock = sec(ci, S_FCLOCK);
-      if (lane == 0) {
-        uint32_t t = put_vu_g(o, p, written);
+    for (uint32_t c0 = 0; c0 < nclients; c0 += 64) {
+      const uint32_t ci = c0 + lane;
+      const uint32_t pl = ci < nclients ? sec(ci, S_PRELEN) : NONE;
+      uint32_t a0 = 0, a1 = 0, b0 = 0, b1 = 0, hb = 0, written = 0, client = 0, fclock = 0;
+      if (pl != NONE) {
+        written = sec(ci, S_WRITTEN);
+        client = sec(ci, S_CLIENT);
+        fclock = sec(ci, S_FCLOCK);
+        a0 = sec(ci, S_A0);
+        a1 = sec(ci, S_A1);
+        b0 = sec(ci, S_B0);
+        b1 = sec(ci, S_B1);
+        hb = vsz(written) + vsz(client) + vsz(fclock) + pl;
+      }
+      const uint32_t sz = hb + (a1 - a0) + (b1 - b0);
+      const uint32_t incl = wave_incl_add(sz), q = p + incl - sz + hb;  // q: the section's first span byte
+      if (pl != NONE) {
+        uint32_t t = put_vu_g(o, q - hb, written);
         t = put_vu_g(o, t, client);
         t = put_vu_g(o, t, fclock);
         for (uint32_t b = 0; b < pl; b++) o[t + b] = X.pre[ci * PRE + b];
+        sec(ci, S_OUTB) = q + (a1 - a0) - b0;  // output position = document position + S_OUTB
       }
-      p += vsz(written) + vsz(client) + vsz(fclock) + pl;
-      const uint32_t a0 = sec(ci, S_A0), a1 = sec(ci, S_A1);
-      copy_bytes(o + p, D + a0, a1 - a0);
-      p += a1 - a0;
-      const uint32_t b0 = sec(ci, S_B0), b1 = sec(ci, S_B1);
-      copy_bytes(o + p, D + b0, b1 - b0);
-      if (lane == 0) sec(ci, S_OUTB) = p - b0;  // output position = document position + S_OUTB
-      p += b1 - b0;
+      for (uint64_t live = __ballot(sz > hb); live; live &= live - 1) {
+        const uint32_t k = (uint32_t)__builtin_ctzll(live);
+        const uint32_t kq = lane_read(q, k), ka0 = lane_read(a0, k), kna = lane_read(a1 - a0, k);
+        copy_bytes(o + kq, D + ka0, kna);
+        copy_bytes(o + kq + kna, D + lane_read(b0, k), lane_read(b1 - b0, k));
+      }
+      p += lane_read(incl, 63);
     }
     copy_bytes(o + p, D + ds0, ds1 - ds0);
     __threadfence();  // the patches below overwrite bytes other lanes stored
     __syncthreads();
+    PT(9);
     for (uint32_t i = lane; i < npatch; i += 64) {
       const uint32_t pos = at<uint32_t>(L_PPOS + 4 * i);
       const uint32_t ci = at<uint32_t>(L_PSEC + 4 * i);
@@ -745,7 +785,9 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
       j.status[d] = ym::ST_OK;
     }
     __syncthreads();
+    PT(10);
   }
+  PT_FLUSH();
 }
 
 
@@ -1417,6 +1459,11 @@ extern "C" int ym__lane_selftest(const uint8_t *host, uint32_t n, unsigned long 
   const int r = (int)hipMemcpy(out, c, 16, hipMemcpyDeviceToHost);
   hipFree(d);
   hipFree(c);
+  return r;
+}
+extern "C" int ym__pw_ticks(unsigned long long *host, int reset) {  // 16 words
+  int r = (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ymk::pw::pw_ticks), 128);
+  if (reset) { unsigned long long z[16] = {}; hipMemcpyToSymbol(HIP_SYMBOL(ymk::pw::pw_ticks), z, 128); }
   return r;
 }
 extern "C" int ym__pw_prof(unsigned long long *host, int reset) {
