@@ -565,7 +565,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   uint32_t nlarge = 0;
   bool large = false;
   if (ngen > 0 && list && op == OP_MERGE) {
-    int lr = large_run(j, list, ngen, st, S->large);
+    int lr = large_run(j, list, ngen, b->n_upd, st, S->large);
     if (lr < 0) return lr;
     if (lr == 1) {
       large = true;

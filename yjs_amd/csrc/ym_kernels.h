@@ -71,7 +71,7 @@ struct LargeBufs {
 };
 // Large-document merge over `list` (n documents the fast path declined).  Documents it takes get
 // status OK; the rest keep ST_PENDING.  Returns 1 when launched, 0 when not applicable, < 0 on error.
-int large_run(const GeneralJob &j, const uint32_t *list, uint32_t n, hipStream_t st, LargeBufs &B);
+int large_run(const GeneralJob &j, const uint32_t *list, uint32_t n, uint32_t n_upd, hipStream_t st, LargeBufs &B);
 
 // device buffers of the chunk-parallel V1 walk (ym_pwalk.hip), grown on demand, cached
 constexpr int PW_NBUF = 5;

@@ -1073,7 +1073,7 @@ int ensure(LargeBufs &B, int k, size_t n) {
     if (e_ != hipSuccess) return -(int)e_ - 1000; \
   } while (0)
 
-int large_run(const GeneralJob &j, const uint32_t *list, uint32_t nb, hipStream_t st, LargeBufs &B) {
+int large_run(const GeneralJob &j, const uint32_t *list, uint32_t nb, uint32_t n_upd, hipStream_t st, LargeBufs &B) {
   using namespace lm;
   if (j.op != OP_MERGE || nb == 0) return 0;
   if (!B.pinned && hipHostMalloc((void **)&B.pinned, 64, hipHostMallocDefault) != hipSuccess) return -2;
@@ -1111,9 +1111,9 @@ int large_run(const GeneralJob &j, const uint32_t *list, uint32_t nb, hipStream_
   hipcub::DeviceScan::ExclusiveSum(B.p[3], tmp, ccnt, J.ch_off, n1, st);
   LMCHK(hipMemcpyAsync(tot, J.bu_off + nb, 4, hipMemcpyDeviceToDevice, st));
   LMCHK(hipMemcpyAsync(tot + 1, J.ch_off + nb, 4, hipMemcpyDeviceToDevice, st));
-  LMCHK(hipMemcpyAsync(B.pinned, tot, 8, hipMemcpyDeviceToHost, st));
-  LMCHK(hipStreamSynchronize(st));
-  const uint32_t nbu = ((uint32_t *)B.pinned)[0], nch = ((uint32_t *)B.pinned)[1];
+  // no host round trip for the update / chunk totals: the per-update count arrays are sized by the
+  // batch's update count and the walk's grid by the chunk bound (the walk reads the true total, tot[1])
+  const uint32_t nbu = n_upd, nch = (uint32_t)((n_upd + 63ull * nb) / 64);  // >= sum over listed docs of ceil(k / 64)
   if (nch == 0) return 0;
   J.stride = nbu + 1;
   if (ensure(B, 1, 2 * csize<uint32_t>(3ull * J.stride))) return -2;
@@ -1128,7 +1128,9 @@ int large_run(const GeneralJob &j, const uint32_t *list, uint32_t nb, hipStream_
   if (ensure(B, 3, t2 + 256)) return -2;
   for (int k = 0; k < 3; k++) hipcub::DeviceScan::ExclusiveSum(B.p[3], t2, J.u_cnt + k * J.stride, J.u_off + k * J.stride, J.stride, st);
   for (int k = 0; k < 3; k++) LMCHK(hipMemcpyAsync((uint32_t *)B.pinned + k, J.u_off + k * J.stride + nbu, 4, hipMemcpyDeviceToHost, st));
+  LMCHK(hipMemcpyAsync((uint32_t *)B.pinned + 3, tot + 1, 4, hipMemcpyDeviceToHost, st));
   LMCHK(hipStreamSynchronize(st));
+  if (((uint32_t *)B.pinned)[3] == 0) return 0;  // no listed document has a chunk: all stay pending
   const uint64_t NS = ((uint32_t *)B.pinned)[0] + 1ull, NR = ((uint32_t *)B.pinned)[1] + 1ull, ND = ((uint32_t *)B.pinned)[2] + 1ull;
   const bool v2 = J.v2;
   uint64_t need = csize<uint64_t>(NS) * 2 + csize<uint32_t>(NS) * 3 + (v2 ? csize<uint4>(NS) + csize<uint64_t>(3 * NS) : 0) +
