@@ -66,6 +66,14 @@ int main(int argc, char **argv) {
         cpt::compact_doc(c, ws.data(), z, v2, upd_off.data(), u0, k, R, nullptr);
         st = c.err;
         if (st) continue;
+        if (getenv("YM_CPT_STATS")) {  // workspace use (sizing experiments): used / reserved per region
+          const cpt::Doc *dp = (const cpt::Doc *)ws.data();
+          const cpt::Arena *ap = (const cpt::Arena *)(ws.data() + ym::al16(sizeof(cpt::Doc)));
+          fprintf(stderr, "CPT %u %llu it %u %u pc %u %u el %u %u src %u %u ty %u %u gen %llu %llu total %llu szit %zu szpc %zu szel %zu szsrc %zu szty %zu\n", k,
+                  (unsigned long long)bytes, dp->nit, dp->capit, dp->npc, dp->cappc, dp->nel, dp->capel, dp->nsrc, dp->capsrc, dp->nty,
+                  dp->capty, (unsigned long long)ap->used, (unsigned long long)ap->cap, (unsigned long long)z.total, sizeof(cpt::Item),
+                  sizeof(cpt::Piece), sizeof(cpt::Elem), sizeof(cpt::Src), sizeof(cpt::Type));
+        }
         out.assign(R.total + 1, 0);
         Ctx c2 = {0, arena.data()};
         cpt::compact_doc(c2, ws.data(), z, v2, upd_off.data(), u0, k, R, out.data());

@@ -41,6 +41,13 @@ template <class T> YM_INL bool vgrow(Ctx &c, Arena &a, Vec<T> &v, uint32_t need)
   if (need <= v.cap) return true;
   uint32_t nc = v.cap ? 2 * v.cap : 8;
   while (nc < need) nc *= 2;
+  // the arena's last allocation grows in place (a vector pushed to in a loop no longer leaves its
+  // outgrown copies behind)
+  if (v.p && (uint8_t *)(v.p + v.cap) == a.base + a.used && a.used + (uint64_t)(nc - v.cap) * sizeof(T) <= a.cap) {
+    a.used += (uint64_t)(nc - v.cap) * sizeof(T);
+    v.cap = nc;
+    return true;
+  }
   T *np = (T *)aalloc(c, a, (uint64_t)nc * sizeof(T));
   if (!np) return false;
   for (uint32_t i = 0; i < v.n; i++) np[i] = v.p[i];
@@ -96,7 +103,7 @@ struct Cl { int64_t client; Vec<int32_t> a; };
 struct Pend { int64_t client; int32_t *refs; uint32_t n, i; uint8_t live; };
 struct DIt { int64_t clock, len; };
 struct DCl { int64_t client; Vec<DIt> it; };
-struct DSet { Vec<DCl> cl; };
+struct DSet { Vec<DCl> cl; Arena *ar; };  // ar: the arena its vectors grow in (nullptr: the document's)
 struct Tx {
   DSet ds;
   Vec<int32_t> ms;   // _mergeStructs
@@ -115,7 +122,8 @@ struct Src { Span a, b; int64_t cnt; FVal fv; uint8_t nca, ncb, keyundef, ref, f
 
 struct Doc {
   Ctx *c;
-  Arena *a;
+  Arena *a;   // persistent: the store's vectors, pending structs / deletes, types
+  Arena *ta;  // transient: one update's reader and transaction (released after each update)
   uint32_t v2;
   Item *it; uint32_t nit, capit;
   Piece *pc; uint32_t npc, cappc;
@@ -272,14 +280,14 @@ YM_INL int32_t ds_get_or_add(Doc &d, DSet &ds, int64_t client) {
   DCl z;
   __builtin_memset(&z, 0, sizeof(DCl));
   z.client = client;
-  if (!vpush(*d.c, *d.a, ds.cl, z)) return NIL;
+  if (!vpush(*d.c, ds.ar ? *ds.ar : *d.a, ds.cl, z)) return NIL;
   return (int32_t)(ds.cl.n - 1);
 }
 YM_INL void tds_add(Doc &d, DSet &ds, int64_t client, int64_t clock, int64_t len) {  // addToDeleteSet
   const int32_t k = ds_get_or_add(d, ds, client);
   if (k == NIL) return;
   DIt e = {clock, len};
-  vpush(*d.c, *d.a, ds.cl.p[k].it, e);
+  vpush(*d.c, ds.ar ? *ds.ar : *d.a, ds.cl.p[k].it, e);
 }
 // sortAndMergeDeleteSet, the reference's own (DeleteSet.js:113-135): stable sort by clock, exactly
 // adjacent ranges coalesce
@@ -420,7 +428,7 @@ YM_BIG void content_split(Doc &d, int32_t l, int32_t r, int64_t diff) {
 }
 
 // ---- items -------------------------------------------------------------------------------------------
-YM_INL void ms_push(Doc &d, int32_t i) { vpush(*d.c, *d.a, d.tx->ms, i); }
+YM_INL void ms_push(Doc &d, int32_t i) { vpush(*d.c, *d.ta, d.tx->ms, i); }
 YM_INL int64_t tx_before_at(const Tx &t, uint32_t idx) { return idx < t.nbc ? t.bc[idx] : 0; }
 YM_INL int64_t tx_before(Doc &d, const Tx &t, int64_t client) {
   const int32_t s = cd_client(d, client);
@@ -433,7 +441,7 @@ YM_INL void changed_add(Doc &d, int32_t t) {  // addChangedTypeToTransaction (Tr
   if (ti != NIL && !(d.it[ti].clock < tx_before(d, x, d.it[ti].client) && !d.it[ti].deleted)) return;
   for (uint32_t i = 0; i < x.chg.n; i++)
     if (x.chg.p[i] == t) return;
-  vpush(*d.c, *d.a, x.chg, t);
+  vpush(*d.c, *d.ta, x.chg, t);
 }
 YM_INL void changed_del(Doc &d, int32_t t) {
   Tx &x = *d.tx;
@@ -967,7 +975,7 @@ YM_BIG void read_refs(Doc &d, Reader &r, Vec<Pend> &out) {
     const int64_t client = r.v2 ? (int64_t)uopt_read(c, r.cl) : (int64_t)rd_vu(c, r.rest);
     int64_t clock = rd_vu(c, r.rest);
     if (c.err) return;
-    int32_t *refs = (int32_t *)aalloc(c, *d.a, 4ull * (ns + 1));
+    int32_t *refs = (int32_t *)aalloc(c, *d.ta, 4ull * (ns + 1));  // (what stays pending moves to *d.a)
     if (!refs) return;
     for (uint32_t k = 0; k < ns && !c.err; k++) {
       const int info = r.v2 ? rle_read(c, r.in) : rbyte(c, r.rest);
@@ -1007,7 +1015,7 @@ YM_BIG void read_refs(Doc &d, Reader &r, Vec<Pend> &out) {
     for (uint32_t q = 0; q < out.n; q++)
       if (out.p[q].client == client) at = q;
     Pend p = {client, refs, ns, 0, 1};
-    if (at == out.n) vpush(c, *d.a, out, p);
+    if (at == out.n) vpush(c, *d.ta, out, p);
     else out.p[at] = p;
   }
 }
@@ -1015,12 +1023,13 @@ YM_BIG void read_refs(Doc &d, Reader &r, Vec<Pend> &out) {
 // ---- transactions ------------------------------------------------------------------------------------
 YM_INL Tx *tx_new(Doc &d, uint8_t local) {  // new Transaction: beforeState = getStateVector(store)
   Ctx &c = *d.c;
-  Tx *t = (Tx *)aalloc(c, *d.a, sizeof(Tx));
+  Tx *t = (Tx *)aalloc(c, *d.ta, sizeof(Tx));
   if (!t) return nullptr;
   __builtin_memset(t, 0, sizeof(Tx));
+  t->ds.ar = d.ta;
   t->local = local;
   t->nbc = d.cl.n;
-  t->bc = (int64_t *)aalloc(c, *d.a, 8ull * (d.cl.n + 1));
+  t->bc = (int64_t *)aalloc(c, *d.ta, 8ull * (d.cl.n + 1));
   if (!t->bc) return nullptr;
   for (uint32_t i = 0; i < d.cl.n; i++) t->bc[i] = cl_state(d, (int32_t)i);
   return t;
@@ -1297,7 +1306,7 @@ YM_BIG Tx *tx_cleanup(Doc &d, Tx *x) {
   Tx *nested = nullptr;
   if (!x->local) {  // observers of the changed types, in Map order: only Y.Text / Y.XmlText act
     const uint32_t nchg = x->chg.n;
-    int32_t *chg = (int32_t *)aalloc(c, *d.a, 4ull * (nchg + 1));
+    int32_t *chg = (int32_t *)aalloc(c, *d.ta, 4ull * (nchg + 1));
     if (!chg) return nullptr;
     for (uint32_t i = 0; i < nchg; i++) chg[i] = x->chg.p[i];
     for (uint32_t i = 0; i < nchg && !c.err; i++) {
@@ -1376,6 +1385,12 @@ YM_BIG void cd_transact(Doc &d, Reader &r) {
       Pend p = d.pend.p[q];
       if (!p.live || p.i == p.n) continue;
       p.refs += p.i; p.n -= p.i; p.i = 0;
+      if ((const uint8_t *)p.refs >= d.ta->base && (const uint8_t *)p.refs < d.ta->base + d.ta->cap) {
+        int32_t *na = (int32_t *)aalloc(c, *d.a, 4ull * (p.n + 1));  // this update's refs outlive it
+        if (!na) return;
+        for (uint32_t k = 0; k < p.n; k++) na[k] = p.refs[k];
+        p.refs = na;
+      }
       d.pend.p[w++] = p;
     }
     d.pend.n = w;
@@ -1391,7 +1406,7 @@ YM_BIG void cd_transact(Doc &d, Reader &r) {
       r.dsCurr = 0;
       const int64_t client = rd_vu(c, r.rest);
       const uint32_t m = rd_vu(c, r.rest);
-      DSet one = {{nullptr, 0, 0}};
+      DSet one = {{nullptr, 0, 0}, d.ta};  // read, applied, dropped
       const int32_t k = ds_get_or_add(d, one, client);
       if (k == NIL) return;
       for (uint32_t j = 0; j < m && !c.err; j++) {
@@ -1406,7 +1421,7 @@ YM_BIG void cd_transact(Doc &d, Reader &r) {
           len = rd_vu(c, r.rest);
         }
         DIt e = {clock, len};
-        vpush(c, *d.a, one.cl.p[k].it, e);
+        vpush(c, *d.ta, one.cl.p[k].it, e);
       }
       if (!c.err) apply_ds(d, one);
     }
@@ -1566,7 +1581,7 @@ inline void cpt_debug_check(Doc &d, uint32_t u) {
 #endif
 // ---- one document ------------------------------------------------------------------------------------
 // workspace of a document of `bytes` input bytes in k updates; mul grows it on ST_RETRY
-struct WsSize { uint64_t it, pc, el, src, ty, gen, total; };
+struct WsSize { uint64_t it, pc, el, src, ty, gen, gent, total; };
 YM_INL WsSize ws_size(uint32_t k, uint64_t bytes, uint32_t mul) {
   WsSize z;
   const uint64_t base = bytes + 16ull * k + 64;
@@ -1576,8 +1591,10 @@ YM_INL WsSize ws_size(uint32_t k, uint64_t bytes, uint32_t mul) {
   z.src = (base / 8 + 16) * mul;
   z.ty = (base / 16 + 16) * mul;
   z.gen = (16 * base + 16384) * mul;
+  z.gent = (4 * base + 4096) * mul;
   z.total = al16(z.it * sizeof(Item)) + al16(z.pc * sizeof(Piece)) + al16(z.el * sizeof(Elem)) +
-            al16(z.src * sizeof(Src)) + al16(z.ty * sizeof(Type)) + z.gen + al16(sizeof(Doc)) + al16(sizeof(Arena)) + 64;
+            al16(z.src * sizeof(Src)) + al16(z.ty * sizeof(Type)) + al16(z.gen) + z.gent + al16(sizeof(Doc)) +
+            2 * al16(sizeof(Arena)) + 64;
   return z;
 }
 // Applies the k updates of a document (offsets upd_off[u0 .. u0 + k]) to a fresh Doc and sizes / writes
@@ -1588,12 +1605,14 @@ YM_BIG void compact_doc(Ctx &c, uint8_t *ws, const WsSize &z, uint32_t v2, const
                         Result &R, uint8_t *out) {
   Doc *dp = (Doc *)ws;  // the document's state heads its workspace
   Arena *ap = (Arena *)(ws + al16(sizeof(Doc)));
-  uint8_t *p = ws + al16(sizeof(Doc)) + al16(sizeof(Arena));
+  Arena *tp = (Arena *)(ws + al16(sizeof(Doc)) + al16(sizeof(Arena)));
+  uint8_t *p = ws + al16(sizeof(Doc)) + 2 * al16(sizeof(Arena));
   Doc &d = *dp;
   if (!out) {
     __builtin_memset(&d, 0, sizeof(Doc));
     d.c = &c;
     d.a = ap;
+    d.ta = tp;
     d.v2 = v2;
     d.it = (Item *)p; d.capit = (uint32_t)z.it; p += al16(z.it * sizeof(Item));
     d.pc = (Piece *)p; d.cappc = (uint32_t)z.pc; p += al16(z.pc * sizeof(Piece));
@@ -1603,16 +1622,20 @@ YM_BIG void compact_doc(Ctx &c, uint8_t *ws, const WsSize &z, uint32_t v2, const
     ap->base = p;
     ap->cap = z.gen;
     ap->used = 0;
+    tp->base = p + al16(z.gen);
+    tp->cap = z.gent;
+    tp->used = 0;
     for (uint32_t u = 0; u < k && !c.err; u++) {
       Reader r;
       reader_open(c, r, upd_off[u0 + u], upd_off[u0 + u + 1] - upd_off[u0 + u], v2);
       if (c.err) return;
       if (v2) {
         r.keys_cap = (uint32_t)(upd_off[u0 + u + 1] - upd_off[u0 + u]) + 16;
-        r.keys = (Span *)aalloc(c, *ap, sizeof(Span) * (uint64_t)r.keys_cap);
+        r.keys = (Span *)aalloc(c, *tp, sizeof(Span) * (uint64_t)r.keys_cap);
         if (c.err) return;
       }
       cd_transact(d, r);
+      tp->used = 0;  // the update's reader and transactions are gone
 #ifdef YM_CPT_DEBUG
       cpt_debug_check(d, u);
 #endif
