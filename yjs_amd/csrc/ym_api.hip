@@ -28,7 +28,7 @@ int big_launch(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &pw);   
 int big2_launch(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &pw);      // ym_big2.hip
 __global__ void k_fast_region(GeneralJob j, uint32_t n_upd);                         // ym_fast.hip
 __global__ void k_compact_ws(GeneralJob j, uint64_t *ws_size);                        // ym_compact.hip
-__global__ void k_compact(GeneralJob j, uint32_t lanes);
+template <int OCC> __global__ void k_compact(GeneralJob j, uint32_t lanes);
 }  // namespace ymk
 
 using namespace ymk;
@@ -320,6 +320,8 @@ int run_compact(DevState *S, hipStream_t st, GeneralJob j, uint32_t *list, uint3
     lanes = e ? atoi(e) : 16;
     if (lanes < 1 || lanes > 64) lanes = 16;
   }
+  static int occ = -1;
+  if (occ < 0) { const char *e = getenv("YMERGE_COMPACT_OCC"); occ = e && atoi(e) == 2 ? 2 : 1; }
   uint32_t mul = 1;
   for (int round = 0; n > 0; round++) {
     j.list = list;
@@ -339,7 +341,8 @@ int run_compact(DevState *S, hipStream_t st, GeneralJob j, uint32_t *list, uint3
     j.ws = S->ws.as<uint8_t>();
     j.ws_off = S->ws_off.as<uint64_t>();
     HIPCHK(hipMemsetAsync(j.counter_retry, 0, 4, st));
-    k_compact<<<(n + lanes - 1) / lanes, 64, 0, st>>>(j, (uint32_t)lanes);
+    if (occ == 2) k_compact<2><<<(n + lanes - 1) / lanes, 64, 0, st>>>(j, (uint32_t)lanes);
+    else k_compact<1><<<(n + lanes - 1) / lanes, 64, 0, st>>>(j, (uint32_t)lanes);
     HIPCHK(hipMemcpyAsync(S->pinned, j.counter_retry, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     const uint32_t nretry = (uint32_t)(S->pinned[0] & 0xffffffffu);

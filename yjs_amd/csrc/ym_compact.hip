@@ -25,7 +25,10 @@ __global__ void k_compact_ws(GeneralJob j, uint64_t *ws_size) {
   ws_size[i] = cpt::ws_size(k, bytes, j.parts_mul).total;
 }
 
-__global__ void __launch_bounds__(64) k_compact(GeneralJob j, uint32_t lanes) {
+// OCC: waves per SIMD the register allocation targets (1: 256 VGPRs + 98 AGPRs, no spills; 2: 256 registers,
+// a few spills -- twice the waves in flight to hide the workspace's memory latency)
+template <int OCC>
+__global__ void __launch_bounds__(64, OCC) k_compact(GeneralJob j, uint32_t lanes) {
   const uint32_t lane = threadIdx.x;
   if (lane >= lanes) return;
   const uint32_t i = blockIdx.x * lanes + lane;
@@ -56,5 +59,8 @@ __global__ void __launch_bounds__(64) k_compact(GeneralJob j, uint32_t lanes) {
   j.out_off[d] = off;
   j.out_len[d] = c2.err ? 0 : R.total;
 }
+
+template __global__ void k_compact<1>(GeneralJob, uint32_t);
+template __global__ void k_compact<2>(GeneralJob, uint32_t);
 
 }  // namespace ymk
