@@ -24,6 +24,13 @@
 #include "ym_core.h"
 
 namespace ym {
+// small routines called per struct / per write: inlined into the kernel (an out-of-line call saves and
+// restores the caller's live registers through scratch, which dominated the kernel's time)
+#ifdef __HIP_DEVICE_COMPILE__
+#define YM_HOT YM_HD inline __attribute__((always_inline))
+#else
+#define YM_HOT YM_HD inline
+#endif
 namespace cpt {
 
 constexpr int32_t NIL = -1;
@@ -187,7 +194,7 @@ YM_INL int32_t cd_client(Doc &d, int64_t client) {
   const uint32_t h = cl_hslot(d, client);
   return d.hv[h] ? (int32_t)(d.hv[h] - 1) : NIL;
 }
-YM_BIG void cl_hput(Doc &d, int64_t client, uint32_t idx) {
+YM_HOT void cl_hput(Doc &d, int64_t client, uint32_t idx) {
   Ctx &c = *d.c;
   if (2 * (d.cl.n + 1) > d.hcap) {
     const uint32_t nc = d.hcap ? 2 * d.hcap : 64;
@@ -234,7 +241,7 @@ YM_INL int32_t cd_get(Doc &d, int64_t client, int64_t clock) {  // getItem
   const uint32_t i = find_index(d, s, clock);
   return d.c->err ? NIL : d.cl.p[s].a.p[i];
 }
-YM_BIG void add_struct(Doc &d, int32_t i) {  // addStruct (StructStore.js:92-104)
+YM_HOT void add_struct(Doc &d, int32_t i) {  // addStruct (StructStore.js:92-104)
   Ctx &c = *d.c;
   const Item &x = d.it[i];
   int32_t s = cd_client(d, x.client);
@@ -291,7 +298,7 @@ YM_INL void tds_add(Doc &d, DSet &ds, int64_t client, int64_t clock, int64_t len
 }
 // sortAndMergeDeleteSet, the reference's own (DeleteSet.js:113-135): stable sort by clock, exactly
 // adjacent ranges coalesce
-YM_BIG void ds_sort_merge(DSet &ds) {
+YM_HOT void ds_sort_merge(DSet &ds) {
   for (uint32_t ci = 0; ci < ds.cl.n; ci++) {
     Vec<DIt> &v = ds.cl.p[ci].it;
     for (uint32_t i = 1; i < v.n; i++) {  // insertion sort: stable
@@ -315,7 +322,7 @@ YM_BIG void ds_sort_merge(DSet &ds) {
 // units of a string piece's UTF-8 body
 YM_INL uint32_t body16(const Piece &p) { return p.n16 - p.fffd - p.lo - p.hi - p.tfffd; }
 // splits piece q at unit k (0 < k < n16): q keeps [0, k), the new piece (returned, linked after q) [k, n16)
-YM_BIG int32_t piece_cut_str(Doc &d, int32_t q, uint32_t k) {
+YM_HOT int32_t piece_cut_str(Doc &d, int32_t q, uint32_t k) {
   const int32_t r = new_piece(d);
   if (r == NIL) return NIL;
   Piece P = d.pc[q];
@@ -394,7 +401,7 @@ YM_INL void piece_drop_first(Doc &d, int32_t q) {
 }
 // content.splice(diff) of item l into the new item r (ContentString.js:51-66, ContentAny / ContentJSON
 // slicing, ContentDeleted length); other contents cannot be split
-YM_BIG void content_split(Doc &d, int32_t l, int32_t r, int64_t diff) {
+YM_HOT void content_split(Doc &d, int32_t l, int32_t r, int64_t diff) {
   Item &L = d.it[l];
   const uint8_t ref = L.ref;
   if (ref == 1) return;
@@ -449,7 +456,7 @@ YM_INL void changed_del(Doc &d, int32_t t) {
     if (x.chg.p[i] == t) { vremove(x.chg, i); return; }
 }
 // splitItem (Item.js:85-125)
-YM_BIG int32_t split_item(Doc &d, int32_t l, int64_t diff) {
+YM_HOT int32_t split_item(Doc &d, int32_t l, int64_t diff) {
   const int32_t r = new_item(d);
   if (r == NIL) return NIL;
   Item &L = d.it[l];
@@ -583,7 +590,7 @@ YM_BIG void it_gc(Doc &d, int32_t root) {
 }
 
 // Item.getMissing: the client of a missing dependency, or -1 (and left / right / parent resolved)
-YM_BIG int64_t it_missing(Doc &d, int32_t i) {
+YM_HOT int64_t it_missing(Doc &d, int32_t i) {
   Item &x = d.it[i];
   if (x.gc) return -1;
   if (x.has_origin && x.oc != x.client && x.ok >= cd_state(d, x.oc)) return x.oc;
@@ -886,7 +893,7 @@ YM_BIG void apply_ds(Doc &d, const DSet &ds) {
 // ---- reading -----------------------------------------------------------------------------------------
 // one struct's content into item i (readItemContent, Item.js:665-683): strings as a piece, Any / JSON as
 // element ranges, the single-valued contents as a source record
-YM_BIG void read_item_content(Doc &d, Reader &r, int32_t i, int info) {
+YM_HOT void read_item_content(Doc &d, Reader &r, int32_t i, int info) {
   Ctx &c = *d.c;
   SStruct s;
   __builtin_memset(&s, 0, sizeof(SStruct));
@@ -1035,7 +1042,7 @@ YM_INL Tx *tx_new(Doc &d, uint8_t local) {  // new Transaction: beforeState = ge
   return t;
 }
 // tryToMergeWithLeft (Transaction.js:165-176) with Item.mergeWith / AbstractContent.mergeWith
-YM_BIG void try_merge_left(Doc &d, int32_t s, uint32_t pos) {
+YM_HOT void try_merge_left(Doc &d, int32_t s, uint32_t pos) {
   const int32_t l = d.cl.p[s].a.p[pos - 1], r = d.cl.p[s].a.p[pos];
   Item &L = d.it[l];
   const Item &R = d.it[r];
@@ -1262,7 +1269,7 @@ YM_INL uint32_t find_clean_start(Doc &d, int32_t s, int64_t clock) {  // findInd
   return idx;
 }
 // iterateStructs (StructStore.js:259-273), splitting at both ends under d.tx
-YM_BIG void iterate_structs(Doc &d, int32_t s, int64_t clock, int64_t len, ObsCb &cb) {
+YM_HOT void iterate_structs(Doc &d, int32_t s, int64_t clock, int64_t len, ObsCb &cb) {
   if (len == 0 || s == NIL) return;
   const int64_t end = clock + len;
   uint32_t idx = find_clean_start(d, s, clock);
@@ -1436,7 +1443,7 @@ YM_BIG void cd_transact(Doc &d, Reader &r) {
 // ---- writing -----------------------------------------------------------------------------------------
 // ContentString.write of a piece list: V2 through the column's StringEncoder (lone halves pair up across
 // strings), V1 writeVarString (a lone surrogate throws URIError)
-YM_BIG void write_str(Ctx &c, Enc &e, const Doc &d, int32_t head) {
+YM_HOT void write_str(Ctx &c, Enc &e, const Doc &d, int32_t head) {
   if (e.v2) {
     uint32_t n16 = 0;
     for (int32_t q = head; q != NIL && !c.err; q = d.pc[q].next) {
@@ -1479,7 +1486,7 @@ YM_BIG void write_str(Ctx &c, Enc &e, const Doc &d, int32_t head) {
   }
 }
 // Item.write / GC.write with offset 0 (Item.js:625-658, GC.js:45-48)
-YM_BIG void item_write(Ctx &c, Enc &e, const Doc &d, int32_t i) {
+YM_HOT void item_write(Ctx &c, Enc &e, const Doc &d, int32_t i) {
   const Item &x = d.it[i];
   if (x.gc) { e_info(e, 0); e_len(e, x.len); return; }
   const int info = (x.ref & 31) | (x.has_origin ? 0x80 : 0) | (x.has_right ? 0x40 : 0) | (x.has_psub ? 0x20 : 0);
