@@ -517,7 +517,7 @@ YM_INL void mark_deleted(Doc &d, int32_t i) {
 // Item.delete (Item.js) with ContentType.delete's walk over the type's children (ContentType.js:101-125),
 // depth-first in the reference's order on an explicit stack
 struct DelFrame { int32_t t, cur; uint32_t mi; uint32_t phase; };
-YM_BIG void it_delete(Doc &d, int32_t root) {
+YM_HOT void it_delete(Doc &d, int32_t root) {
   Ctx &c = *d.c;
   if (d.it[root].deleted) return;
   mark_deleted(d, root);
@@ -629,7 +629,7 @@ YM_INL bool id_eq(uint8_t ha, int64_t ac, int64_t ak, uint8_t hb, int64_t bc, in
   return ha == hb && (!ha || (ac == bc && ak == bk));
 }
 // Item.integrate (Item.js:403-517) / GC.integrate
-YM_BIG void it_integrate(Doc &d, int32_t i, int64_t off) {
+YM_HOT void it_integrate(Doc &d, int32_t i, int64_t off) {
   Ctx &c = *d.c;
   if (d.it[i].gc) {
     if (off > 0) { d.it[i].clock += off; d.it[i].len -= off; }
@@ -754,7 +754,7 @@ YM_INL void refs_sort(Doc &d, int32_t *a, uint32_t n) {  // stable sort by clock
   }
 }
 // resumeStructIntegration (encoding.js:225-321)
-YM_BIG void resume_integration(Doc &d) {
+YM_HOT void resume_integration(Doc &d) {
   Ctx &c = *d.c;
   Arena &A = *d.a;
   uint32_t nids = 0;
@@ -847,7 +847,7 @@ YM_BIG void resume_integration(Doc &d) {
 
 // readAndApplyDeleteSet over decoded ranges (DeleteSet.js:270-323); unapplied ranges become a pending
 // delete reader
-YM_BIG void apply_ds(Doc &d, const DSet &ds) {
+YM_HOT void apply_ds(Doc &d, const DSet &ds) {
   Ctx &c = *d.c;
   DSet un = {{nullptr, 0, 0}};
   for (uint32_t ci = 0; ci < ds.cl.n && !c.err; ci++) {
@@ -974,7 +974,7 @@ YM_HOT void read_item_content(Doc &d, Reader &r, int32_t i, int info) {
 }
 // readClientsStructRefs (encoding.js:127-198): per section a ref list; a repeated client replaces the
 // earlier list (Map.set); info & 31 == 0 is a GC
-YM_BIG void read_refs(Doc &d, Reader &r, Vec<Pend> &out) {
+YM_HOT void read_refs(Doc &d, Reader &r, Vec<Pend> &out) {
   Ctx &c = *d.c;
   const uint32_t nsec = rd_vu(c, r.rest);
   for (uint32_t si = 0; si < nsec && !c.err; si++) {
@@ -1306,7 +1306,7 @@ YM_BIG void ytext_observer(Doc &d, Tx *x, int32_t t, Tx **nested) {
   d.tx = x;
 }
 // cleanupTransactions (Transaction.js:244-367) for one transaction; returns the one its observers opened
-YM_BIG Tx *tx_cleanup(Doc &d, Tx *x) {
+YM_HOT Tx *tx_cleanup(Doc &d, Tx *x) {
   Ctx &c = *d.c;
   d.tx = x;
   ds_sort_merge(x->ds);
@@ -1363,7 +1363,7 @@ YM_BIG Tx *tx_cleanup(Doc &d, Tx *x) {
   return nested;
 }
 // transact(readUpdateV2, local = false) + cleanupTransactions (encoding.js readUpdateV2)
-YM_BIG void cd_transact(Doc &d, Reader &r) {
+YM_HOT void cd_transact(Doc &d, Reader &r) {
   Ctx &c = *d.c;
   Tx *x = tx_new(d, 0);
   if (!x) return;
