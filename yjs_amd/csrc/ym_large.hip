@@ -520,8 +520,44 @@ __device__ __forceinline__ uint32_t gput_vi(uint8_t *o, uint32_t p, bool neg, ui
   while (m > 0) { o[p++] = (uint8_t)((m > 127 ? 0x80 : 0) | (m & 127)); m >>= 7; }
   return p;
 }
+// One thread's copy of a struct's bytes (unaligned on both sides).  All loads of a piece are issued
+// before its stores, 16 / 8 / 4 / 1 bytes wide: a byte loop waited for every load (a C5 document's
+// ~16 k structs of ~30 bytes made k_lm_doc2 a chain of byte round trips).
+typedef uint4 __attribute__((aligned(1))) lm_u4u;
+typedef uint64_t __attribute__((aligned(1))) lm_u8u;
+typedef uint32_t __attribute__((aligned(1))) lm_u32u;
 __device__ __forceinline__ void copy_bytes(uint8_t *dst, const uint8_t *src, uint32_t n) {
-  for (uint32_t b = 0; b < n; b++) dst[b] = src[b];
+  uint32_t b = 0;
+  for (; b + 64 <= n; b += 64) {
+    const uint4 v0 = *reinterpret_cast<const lm_u4u *>(src + b), v1 = *reinterpret_cast<const lm_u4u *>(src + b + 16);
+    const uint4 v2 = *reinterpret_cast<const lm_u4u *>(src + b + 32), v3 = *reinterpret_cast<const lm_u4u *>(src + b + 48);
+    *reinterpret_cast<lm_u4u *>(dst + b) = v0;
+    *reinterpret_cast<lm_u4u *>(dst + b + 16) = v1;
+    *reinterpret_cast<lm_u4u *>(dst + b + 32) = v2;
+    *reinterpret_cast<lm_u4u *>(dst + b + 48) = v3;
+  }
+  // the rest (< 64 bytes): up to three 16-byte pieces, then 8, 4 and single bytes, loads first
+  const uint32_t k = (n - b) >> 4;
+  uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0, v2 = v0;
+  if (k > 0) v0 = *reinterpret_cast<const lm_u4u *>(src + b);
+  if (k > 1) v1 = *reinterpret_cast<const lm_u4u *>(src + b + 16);
+  if (k > 2) v2 = *reinterpret_cast<const lm_u4u *>(src + b + 32);
+  const uint32_t t8 = b + 16 * k;
+  const bool h8 = t8 + 8 <= n;
+  const uint64_t w8 = h8 ? *reinterpret_cast<const lm_u8u *>(src + t8) : 0;
+  const uint32_t t4 = t8 + (h8 ? 8 : 0);
+  const bool h4 = t4 + 4 <= n;
+  const uint32_t w4 = h4 ? *reinterpret_cast<const lm_u32u *>(src + t4) : 0;
+  const uint32_t t1 = t4 + (h4 ? 4 : 0);
+  const uint8_t c0 = t1 < n ? src[t1] : 0, c1 = t1 + 1 < n ? src[t1 + 1] : 0, c2 = t1 + 2 < n ? src[t1 + 2] : 0;
+  if (k > 0) *reinterpret_cast<lm_u4u *>(dst + b) = v0;
+  if (k > 1) *reinterpret_cast<lm_u4u *>(dst + b + 16) = v1;
+  if (k > 2) *reinterpret_cast<lm_u4u *>(dst + b + 32) = v2;
+  if (h8) *reinterpret_cast<lm_u8u *>(dst + t8) = w8;
+  if (h4) *reinterpret_cast<lm_u32u *>(dst + t4) = w4;
+  if (t1 < n) dst[t1] = c0;
+  if (t1 + 1 < n) dst[t1 + 1] = c1;
+  if (t1 + 2 < n) dst[t1 + 2] = c2;
 }
 
 enum { K_UOPT = 0, K_IDIF = 1, K_RLE = 2 };
