@@ -368,16 +368,23 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # YMERGE_BENCH_DEVICE pins every rank to one device (the multi-rank path rehearsed on a one-GPU box,
+    # tests/test_gpu_workloads.py); YMERGE_BENCH_BACKEND picks the reduce's backend (default: RCCL on GPUs)
+    if os.environ.get("YMERGE_BENCH_DEVICE"):
+        local = int(os.environ["YMERGE_BENCH_DEVICE"])
+    backend = os.environ.get("YMERGE_BENCH_BACKEND", "gloo" if args.cpu_stub else "nccl")
     stub = args.cpu_stub
     if stub:
         dev = torch.device("cpu")
-        if world > 1:
-            dist.init_process_group("gloo")
     else:
         dev = torch.device("cuda", local)
         torch.cuda.set_device(dev)
-        if world > 1:
+    if world > 1:
+        if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    red_dev = dev if backend == "nccl" else torch.device("cpu")  # where the reduce's tensors live
 
     from yjs_amd.distributed import weak_scaling_shard
     from yjs_amd.workloads import load_ymb
@@ -456,7 +463,7 @@ def main():
     from yjs_amd.distributed import reduce_run
     elapsed, (in_all, out_all, docs_all, err_all, fast_all, gen_all, upd_all) = reduce_run(
         dist if world > 1 else None, elapsed,
-        [in_bytes, out_bytes, n_docs, errors, st0["docs_fast"], st0["docs_general"], int(doc_upd[-1])], device=dev)
+        [in_bytes, out_bytes, n_docs, errors, st0["docs_fast"], st0["docs_general"], int(doc_upd[-1])], device=red_dev)
 
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
@@ -496,7 +503,8 @@ def main():
                        "output_bytes_total": int(out_all), "format": f"v{fmt}",
                        "update_offsets": "u32 (YM_OFF32)" if off32 else "u64",
                        "parallelism": f"docs {how}-partitioned over {world} GPU(s) (one process each), "
-                                      "no collective in the hot path; max-time / sum-counters all-reduce"},
+                                      "no collective in the hot path; max-time / sum-counters all-reduce",
+                       "reduce_backend": backend if world > 1 else None},
             "docs_per_s": round(docs_s, 1),
             "hbm_frac_in_plus_out": round((in_all + out_all) * args.steps / elapsed / 1e9 / (HBM_PEAK_GBS * world), 5),
             "docs_fast_path": int(fast_all), "docs_general_path": int(gen_all), "doc_errors": int(err_all),

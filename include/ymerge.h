@@ -135,8 +135,13 @@ int ym_snapshot(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
  *   Y.encodeStateAsUpdate[V2](doc)
  * (gaberogan/yjs@v0 src/utils/encoding.js:350-383 readUpdate / applyUpdate, :490-526 encodeStateAsUpdate;
  * structs integrated by Item.integrate, deletions applied, deleted content garbage-collected and runs of
- * structs merged by cleanupTransactions, src/utils/Transaction.js:244-367) in b->format.  Documents whose
- * inputs leave structs or deletions pending (a missing dependency) report YM_ERR_UNSUPPORTED. */
+ * structs merged by cleanupTransactions, src/utils/Transaction.js:244-367) in b->format.  Structs whose
+ * dependencies never arrive stay pending (pendingStack / pendingClientsStructRefs, encoding.js:225-321) and
+ * so do deletions of unseen clocks (pendingDeleteReaders, DeleteSet.js:270-323): like the reference, the
+ * output is the integrated store and its delete set only (encoding.js:490-493).  An input on which the
+ * reference throws reports that exception (class and message, ym_strerror).  A document whose workspace
+ * does not fit the device-memory budget (YMERGE_COMPACT_WS_GB, default 16 GiB per launch) reports
+ * YM_ERR_CAPACITY; large batches run in budget-sized chunks. */
 int ym_compact(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
 
 #ifdef __cplusplus

@@ -4,10 +4,15 @@
 // (applyUpdate[V2], encoding.js:462-473: resumeStructIntegration :225-321 -> Item.integrate Item.js:403-517,
 // readAndApplyDeleteSet DeleteSet.js:270-323; cleanupTransactions Transaction.js:244-367: tryGcDeleteSet,
 // tryMergeDeleteSet, tryToMergeWithLeft), then encodeStateAsUpdate[V2] (encoding.js:490-526).
-// Inputs: every golden merge case the reference applies without pending structs or delete readers, and
-// per workload template set (C1, C2, C4) the first documents' update lists.  Output:
-// tests/golden/compact.json {cases: [{id, group, fmt, inputs (b64), expect (b64) | src {ymb, doc}, expect_sha256, expect_len; single_tx_same}]}
-// single_tx_same records whether applying mergeUpdates(inputs) in one transaction gives the same bytes.
+// Inputs: every golden merge case, per workload template set (C1-C5) the first documents' update lists,
+// randomized formatted-text histories, and gapped histories (updates dropped: the reference keeps what
+// they would have enabled in pendingStack / pendingClientsStructRefs / pendingDeleteReaders and
+// encodeStateAsUpdate writes only the integrated store, encoding.js:490-493).  Output:
+// tests/golden/compact.json {cases: [{id, group, fmt, inputs (b64), expect (b64) | src {ymb, doc, drop?},
+// expect_sha256, expect_len | error {name, message}; pending [structRefs, stack, deleteReaders];
+// single_tx_same}]}.  A case whose applyUpdate / encodeStateAsUpdate throws records the exception's class
+// and message instead of bytes.  single_tx_same records whether applying mergeUpdates(inputs) in one
+// transaction gives the same bytes.
 'use strict'
 const fs = require('fs')
 const path = require('path')
@@ -37,31 +42,39 @@ function loadYmb (name) {
 
 ;(async () => {
   const Y = await loadReference()
-  const pending = doc => doc.store.pendingClientsStructRefs.size + doc.store.pendingStack.length + doc.store.pendingDeleteReaders.length
+  const pending = doc => [doc.store.pendingClientsStructRefs.size, doc.store.pendingStack.length, doc.store.pendingDeleteReaders.length]
   const cases = []
   const stats = {}
   const add = (id, group, fmt, inputs, src) => {
-    const v2 = fmt === 2
+    const v2 = +fmt === 2
     const apply = v2 ? Y.applyUpdateV2 : Y.applyUpdate
     const encode = v2 ? Y.encodeStateAsUpdateV2 : Y.encodeStateAsUpdate
-    let r
+    const r = src ? { id, group, fmt: v2 ? 2 : 1, src } : { id, group, fmt: v2 ? 2 : 1, inputs: inputs.map(b64) }
     try {
       const doc = new Y.Doc()
       for (const u of inputs) apply(doc, u)
-      if (pending(doc) !== 0) { stats[group + '/pending'] = (stats[group + '/pending'] || 0) + 1; return }
+      const pend = pending(doc)
       const out = encode(doc)
+      if (pend[0] + pend[1] + pend[2] !== 0) {
+        r.pending = pend
+        stats[group + '/pending'] = (stats[group + '/pending'] || 0) + 1
+      }
       let same = null
-      try {
-        const one = new Y.Doc()
-        apply(one, inputs.length === 1 ? inputs[0] : (v2 ? Y13.mergeUpdatesV2 : Y13.mergeUpdates)(inputs))
-        same = Buffer.compare(Buffer.from(encode(one)), Buffer.from(out)) === 0
-      } catch (e) { same = null }
+      if (!r.pending) {
+        try {
+          const one = new Y.Doc()
+          apply(one, inputs.length === 1 ? inputs[0] : (v2 ? Y13.mergeUpdatesV2 : Y13.mergeUpdates)(inputs))
+          same = Buffer.compare(Buffer.from(encode(one)), Buffer.from(out)) === 0
+        } catch (e) { same = null }
+      }
       // workload documents name their bench_data source instead of repeating its bytes
       // (and, being large, carry the SHA-256 and length of the expected bytes)
-      r = src ? { id, group, fmt, src, expect_sha256: require('crypto').createHash('sha256').update(out).digest('hex'), expect_len: out.length, single_tx_same: same } : { id, group, fmt, inputs: inputs.map(b64), expect: b64(out), single_tx_same: same }
+      if (src) { r.expect_sha256 = require('crypto').createHash('sha256').update(out).digest('hex'); r.expect_len = out.length } else r.expect = b64(out)
+      r.single_tx_same = same
     } catch (e) {
+      // the reference's exception (applyUpdate's transaction still runs its cleanup in `finally`)
+      r.error = { name: e.constructor.name, message: e.message }
       stats[group + '/throws'] = (stats[group + '/throws'] || 0) + 1
-      return
     }
     cases.push(r)
     stats[group] = (stats[group] || 0) + 1
@@ -84,6 +97,13 @@ function loadYmb (name) {
     const docs = loadYmb(wl)
     for (let d = 0; d < n && d < docs.length; d++) add(`wl_${wl}/doc${d}`, 'wl_' + wl.slice(0, 2), wl.endsWith('v2') ? 2 : 1, docs[d], { ymb: wl, doc: d })
   }
+  // gapped histories: every 5th update of the workload documents dropped (the lost messages of a provider);
+  // what depends on them stays pending in the reference's store
+  for (const [wl, n] of [['c2_v1', 24], ['c2_v2', 24], ['c4_v1', 8], ['c4_v2', 8], ['c5_v1', 2], ['c5_v2', 2]]) {
+    const docs = loadYmb(wl)
+    for (let d = 0; d < n && d < docs.length; d++) add(`gap_${wl}/doc${d}`, 'gap_' + wl.slice(0, 2), wl.endsWith('v2') ? 2 : 1, docs[d].filter((u, i) => i % 5 !== 4), { ymb: wl, doc: d, drop: 5 })
+  }
+  const histories = []
   // randomized concurrent histories over nested Y.Text / Y.XmlText with formatting, deletes of whole nested
   // types, map overwrites and embeds, produced by yjs 13.5.16 peers; every peer's update events are applied to
   // the compacting Doc in a shuffled order that keeps each peer's own order (the YText observer's remote
@@ -179,6 +199,25 @@ function loadYmb (name) {
       for (let i = 0; i < take; i++) msgs.push(q.shift())
     }
     add(`fuzz_fmt/h${h}/v${v2 ? 2 : 1}`, 'fuzz_fmt', v2 ? 2 : 1, msgs)
+    histories.push([v2, msgs])
+  }
+  // the same histories with messages lost (each dropped with p = 0.15) and some delivered twice or late:
+  // pending structs wait on the stack, deletes of unknown clocks wait as pending delete readers, and a
+  // late message resumes them
+  seed = 0x9a7
+  for (let h = 0; h < histories.length; h++) {
+    const [v2, msgs] = histories[h]
+    const out = []
+    const late = []
+    for (const m of msgs) {
+      const x = rnd()
+      if (x < 0.15) continue
+      if (x < 0.25) { late.push(m); continue }
+      out.push(m)
+      if (x > 0.95) out.push(m)
+    }
+    for (const m of late) if (rnd() < 0.5) out.push(m)
+    add(`fuzz_gap/h${h}/v${v2 ? 2 : 1}`, 'fuzz_gap', v2 ? 2 : 1, out)
   }
   fs.writeFileSync(path.join(GOLDEN, 'compact.json'), JSON.stringify({
     generator: 'oracle/gen/make_compact_fixtures.cjs',

@@ -2601,6 +2601,8 @@ static void it_integrate(CDoc *d, CIt *it, int64_t off) {
     return;
   }
   CType *P = it->parent;
+  /* 13.4.9 Item.js:413-450: a GC on the left has no `right`, so the conflict scan reads undefined.origin */
+  if (it->left && it->left->gc) fail(d->c, YMO_ERR_TYPE);
   if ((!it->left && (!it->rightp || it->rightp->left != NULL)) || (it->left && it->left->rightp != it->rightp)) {
     CIt *left = it->left, *o;
     if (left) o = left->rightp;
@@ -2662,12 +2664,13 @@ static void refs_sort(CIt **a, size_t n) { /* stable sort by clock (V8 TimSort i
     a[j] = v;
   }
 }
+static int cmp_i64(const void *a, const void *b) { int64_t x = *(const int64_t *)a, y = *(const int64_t *)b; return x < y ? -1 : x > y; }
 static void resume_integration(CDoc *d) { /* resumeStructIntegration (encoding.js:225-321) */
   Ctx *c = d->c;
   size_t nids = 0;
   int64_t *ids = (int64_t *)aalloc(c, (d->npend + 1) * sizeof(int64_t));
   for (size_t i = 0; i < d->npend; i++) if (d->pend[i].live) ids[nids++] = d->pend[i].client;
-  for (size_t i = 1; i < nids; i++) { int64_t v = ids[i]; size_t j = i; while (j > 0 && ids[j - 1] > v) { ids[j] = ids[j - 1]; j--; } ids[j] = v; }
+  qsort(ids, nids, sizeof(int64_t), cmp_i64); /* Array.from(keys).sort((a, b) => a - b): distinct keys */
   if (nids == 0) return;
   CPend *cur = NULL;
   #define NEXT_TARGET()                                                      \
@@ -2682,20 +2685,10 @@ static void resume_integration(CDoc *d) { /* resumeStructIntegration (encoding.j
   NEXT_TARGET();
   if (cur == NULL && d->nstack == 0) return;
   CIt *head = d->nstack > 0 ? d->stack[--d->nstack] : cur->refs[cur->i++];
-  int64_t *sc_client = (int64_t *)aalloc(c, 64 * sizeof(int64_t)), *sc_clock = (int64_t *)aalloc(c, 64 * sizeof(int64_t));
-  size_t nsc = 0, capsc = 64;
-  for (;;) {
-    int64_t local = -1;
-    for (size_t i = 0; i < nsc; i++) if (sc_client[i] == head->client) { local = sc_clock[i]; break; }
-    if (local < 0) {
-      local = cd_state(d, head->client);
-      if (nsc == capsc) {
-        int64_t *a = (int64_t *)aalloc(c, 2 * capsc * sizeof(int64_t)), *b = (int64_t *)aalloc(c, 2 * capsc * sizeof(int64_t));
-        memcpy(a, sc_client, nsc * sizeof(int64_t)); memcpy(b, sc_clock, nsc * sizeof(int64_t));
-        sc_client = a; sc_clock = b; capsc *= 2;
-      }
-      sc_client[nsc] = head->client; sc_clock[nsc] = local; nsc++;
-    }
+  /* the reference's state cache (encoding.js:257-260, 289) always equals getState: a client's state only
+     changes when one of its structs integrates, and that updates the cache to the same value */
+  while (1) {
+    int64_t local = cd_state(d, head->client);
     int64_t off = head->clock < local ? local - head->clock : 0;
     if (head->clock + off != local) {
       CPend *sr = cd_pend(d, head->client);
@@ -2721,7 +2714,6 @@ static void resume_integration(CDoc *d) { /* resumeStructIntegration (encoding.j
     if (missing < 0) {
       if (off == 0 || off < head->len) {
         it_integrate(d, head, off);
-        for (size_t i = 0; i < nsc; i++) if (sc_client[i] == head->client) sc_clock[i] = head->clock + head->len;
       }
       if (d->nstack > 0) head = d->stack[--d->nstack];
       else if (cur && cur->i < cur->n) head = cur->refs[cur->i++];
@@ -2749,9 +2741,22 @@ static void resume_integration(CDoc *d) { /* resumeStructIntegration (encoding.j
 static void cd_split_into(CDoc *d, CCl *s, size_t at, CIt *it) { cl_insert(d, s, at, it); }
 /* readAndApplyDeleteSet over a decoded delete set (DeleteSet.js:270-323); the unapplied ranges become a
    pending delete reader */
-static void apply_ds(CDoc *d, const DSet *ds) {
+static void apply_ds(CDoc *d, const DSet *ds, int kept) {
   DSet un;
   memset(&un, 0, sizeof(un));
+  if (kept) { /* a pending reader none of whose ranges applies comes back unchanged (it went through the
+                 round trip below once already) */
+    int any = 0;
+    for (size_t ci = 0; ci < ds->n && !any; ci++) {
+      int64_t state = cd_state(d, ds->cl[ci].client);
+      for (size_t k = 0; k < ds->cl[ci].n && !any; k++) any = ds->cl[ci].items[k].clock < state;
+    }
+    if (!any) {
+      CGROW(d->c, d->pdel, d->npdel, d->cappdel, DSet);
+      d->pdel[d->npdel++] = *ds;
+      return;
+    }
+  }
   for (size_t ci = 0; ci < ds->n; ci++) {
     int64_t client = ds->cl[ci].client;
     CCl *s = cd_client(d, client);
@@ -2779,6 +2784,20 @@ static void apply_ds(CDoc *d, const DSet *ds) {
     }
   }
   if (un.n > 0) {
+    /* the pending reader is a DSDecoderV2 over writeDeleteSet(DSEncoderV2, unappliedDS) (:317-321): clock
+       deltas to the previous range's end and len - 1 through writeVarUint (a negative value: its low 7 bits) */
+    for (size_t ci = 0; ci < un.n; ci++) {
+      int64_t enc = 0, dec = 0;
+      for (size_t k = 0; k < un.cl[ci].n; k++) {
+        DItem *r = &un.cl[ci].items[k];
+        int64_t dc = r->clock - enc, dl = r->len - 1;
+        enc = r->clock + r->len;
+        dec += dc > 127 ? dc : (dc & 127);
+        r->clock = dec;
+        r->len = (dl > 127 ? dl : (dl & 127)) + 1;
+        dec += r->len;
+      }
+    }
     CGROW(d->c, d->pdel, d->npdel, d->cappdel, DSet);
     d->pdel[d->npdel++] = un;
   }
@@ -3099,7 +3118,7 @@ static void cd_transact(CDoc *d, UDec *u) { /* transact(readUpdateV2, local = fa
     DSet *pr = d->pdel;
     size_t np = d->npdel;
     d->pdel = NULL; d->npdel = 0; d->cappdel = 0;
-    for (size_t q = 0; q < np; q++) apply_ds(d, &pr[q]);
+    for (size_t q = 0; q < np; q++) apply_ds(d, &pr[q], 1);
   }
   { /* readAndApplyDeleteSet: each client's ranges are applied as read (the clients are independent) */
     uint32_t n = rd_vu(c, &u->rest);
@@ -3115,7 +3134,7 @@ static void cd_transact(CDoc *d, UDec *u) { /* transact(readUpdateV2, local = fa
         int64_t len = ud_ds_len(c, u);
         dc_push(c, dc, clock, len);
       }
-      apply_ds(d, &one);
+      apply_ds(d, &one, 0);
     }
   }
   /* cleanupTransactions: this one, then the one its observers opened (local: its observers do nothing) */
@@ -3148,9 +3167,8 @@ static Buf *compact_impl(Ctx *c, const uint8_t *const *upds, const size_t *lens,
     udec_init(c, &u, upds[k], lens[k], v2);
     cd_transact(&d, &u);
   }
-  /* every input applied completely (the fixtures hold only such documents) */
-  for (size_t q = 0; q < d.npend; q++) if (d.pend[q].live) fail(c, YMO_ERR_UNSUPPORTED);
-  if (d.nstack > 0 || d.npdel > 0) fail(c, YMO_ERR_UNSUPPORTED);
+  /* what is still pending (structs on the stack / in the pending refs, delete readers) is not written:
+     encodeStateAsUpdate = the integrated store + its delete set (encoding.js:490-493) */
   UEnc e;
   uenc_init(c, &e, v2);
   /* writeClientsStructs: clients descending, every struct from clock 0 */

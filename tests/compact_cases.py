@@ -1,7 +1,10 @@
 """Doc round-trip compaction fixtures (tests/golden/compact.json, oracle/gen/make_compact_fixtures.cjs):
 gaberogan/yjs@v0 (yjs 13.4.9) new Doc() (gc: true), applyUpdate[V2] of every input in order,
-encodeStateAsUpdate[V2].  Workload documents name their bench_data source and carry the expected output's
-SHA-256 instead of its bytes."""
+encodeStateAsUpdate[V2].  Workload documents name their bench_data source (`drop`: every drop-th update
+left out, a gapped history) and carry the expected output's SHA-256 instead of its bytes.  Cases on which the
+reference throws carry the exception (`error`: class and message) instead of bytes; `pending` records what the
+reference's store still held pending after the last input (such documents compact to the integrated store
+only)."""
 import base64
 import functools
 import hashlib
@@ -28,18 +31,41 @@ def load():
             arena, upd_off, doc_upd = _ymb(c["src"]["ymb"])
             k = c["src"]["doc"]
             ins = [arena[int(upd_off[u]):int(upd_off[u + 1])].tobytes() for u in range(int(doc_upd[k]), int(doc_upd[k + 1]))]
+            drop = c["src"].get("drop")
+            if drop:
+                ins = [u for i, u in enumerate(ins) if i % drop != drop - 1]
             exp = None
         else:
             ins = [base64.b64decode(x) for x in c["inputs"]]
-            exp = base64.b64decode(c["expect"])
+            exp = base64.b64decode(c["expect"]) if "expect" in c else None
         out.append(dict(id=c["id"], group=c["group"], fmt=c["fmt"], inputs=ins, expect=exp,
-                        sha=c.get("expect_sha256"), elen=c.get("expect_len")))
+                        sha=c.get("expect_sha256"), elen=c.get("expect_len"), error=c.get("error"),
+                        pending=c.get("pending")))
     return out
 
 
 def matches(case, got):
-    if got is None:
+    if got is None or case["error"]:
         return False
     if case["expect"] is not None:
         return got == case["expect"]
     return len(got) == case["elen"] and hashlib.sha256(got).hexdigest() == case["sha"]
+
+
+def mismatch(case, status, got, message=True):
+    """None if (status, bytes) is the reference's result for `case`, else the reason.  Error cases: the
+    status word's class is the exception's class and (message=True: the engine, whose status word carries
+    which message) ym_strerror's text is the exception's message."""
+    import oracle_ref
+    st = int(status)
+    if case["error"]:
+        e = case["error"]
+        if st == 0:
+            return "no error, reference threw " + e["name"]
+        if message:
+            return oracle_ref.js_error_mismatch(st, e["name"], e["message"])
+        want = oracle_ref.js_error_status(e["name"], e["message"])
+        return None if st & 0xff == want else f"class {st & 0xff} != {want}"
+    if st != 0:
+        return f"status {st:#x}"
+    return None if matches(case, got) else "bytes differ"

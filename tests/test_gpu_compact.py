@@ -18,20 +18,26 @@ def engine():
     return Engine(0)
 
 
-@pytest.mark.parametrize("lanes", ["1", "64"])
+@pytest.mark.parametrize("lanes", ["1", "16", "64"])
 @pytest.mark.parametrize("fmt", [1, 2])
 def test_compact_fixtures_on_gpu(engine, fmt, lanes, monkeypatch):
+    """Every fixture of the reference, including the histories it leaves pending (gapped workload documents,
+    lost / late messages: only the integrated store is written) and the inputs on which it throws (class and
+    message), at 1, 16 (the default) and 64 documents per wave (the library reads YMERGE_COMPACT_LANES on
+    every call)."""
     from yjs_amd import pack_docs
     monkeypatch.setenv("YMERGE_COMPACT_LANES", lanes)
-    cs = [c for c in compact_cases.load() if c["fmt"] == fmt]
+    cs = [c for c in compact_cases.load() if c["fmt"] == fmt and c["group"] != "gap_c5"]
     a, o, d = pack_docs([c["inputs"] for c in cs])
     oa, oo, ol, st = engine.run_host("compact", fmt, a, o, d)
     bad = []
     for i, c in enumerate(cs):
         got = oa[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() if st[i] == 0 else None
-        if st[i] != 0 or not compact_cases.matches(c, got):
-            bad.append((c["id"], int(st[i])))
+        why = compact_cases.mismatch(c, st[i], got)
+        if why:
+            bad.append((c["id"], why))
     assert not bad, f"{len(bad)}/{len(cs)} differ: {bad[:8]}"
+    assert sum(1 for c in cs if c["pending"]) > 60 and sum(1 for c in cs if c["error"]) > 0
 
 
 @pytest.mark.parametrize("name", ["c2_v1", "c2_v2", "c4_v1"])
@@ -55,13 +61,40 @@ def test_compact_workload_matches_oracle(engine, name):
 
 
 def test_compact_c5_documents(engine):
-    """The large C5 documents (1,024 clients, ~16 k updates, nested XML types): workspace growth on the
-    device (ST_RETRY rounds) and the fixture hashes of the reference."""
+    """The large C5 documents (1,024 clients, ~16 k updates, nested XML types), complete and with every 5th
+    update dropped (thousands of structs left pending): workspace growth on the device (ST_RETRY rounds) and
+    the fixture hashes of the reference."""
     from yjs_amd import pack_docs
-    cs = [c for c in compact_cases.load() if c["group"] == "wl_c5"]
+    cs = [c for c in compact_cases.load() if c["group"] in ("wl_c5", "gap_c5")]
     for fmt in (1, 2):
         sub = [c for c in cs if c["fmt"] == fmt]
         a, o, d = pack_docs([c["inputs"] for c in sub])
         oa, oo, ol, st = engine.run_host("compact", fmt, a, o, d)
         for i, c in enumerate(sub):
-            assert st[i] == 0 and compact_cases.matches(c, oa[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes()), c["id"]
+            assert compact_cases.mismatch(c, st[i], oa[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes()) is None, c["id"]
+
+
+def test_compact_workspace_budget_chunks(engine, monkeypatch):
+    """A batch whose workspaces exceed the device-memory budget runs in chunks (YMERGE_COMPACT_WS_GB, read
+    on every call) with the same bytes as one launch; a document whose workspace alone exceeds the budget
+    reports YM_ERR_CAPACITY without affecting the others."""
+    from yjs_amd import pack_docs
+    arena, upd_off, doc_upd = load_ymb("c2_v1")
+    n = 300
+    docs = [[arena[int(upd_off[u]):int(upd_off[u + 1])].tobytes() for u in range(int(doc_upd[i]), int(doc_upd[i + 1]))]
+            for i in range(n)]
+    a, o, d = pack_docs(docs)
+    oa, oo, ol, st = engine.run_host("compact", 1, a, o, d)
+    assert (st == 0).all()
+    want = [oa[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() for i in range(n)]
+    monkeypatch.setenv("YMERGE_COMPACT_WS_GB", "0.01")  # ~10 MB: ~27 documents per chunk
+    oa, oo, ol, st = engine.run_host("compact", 1, a, o, d)
+    assert (st == 0).all()
+    assert [oa[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() for i in range(n)] == want
+    # one C5 document (0.7 MB of updates: a workspace of tens of MB) between small ones
+    big = [c for c in compact_cases.load() if c["group"] == "wl_c5" and c["fmt"] == 1][0]
+    a, o, d = pack_docs([docs[0], big["inputs"], docs[1]])
+    oa, oo, ol, st = engine.run_host("compact", 1, a, o, d)
+    assert int(st[1]) == 9 and int(st[0]) == 0 and int(st[2]) == 0  # YM_ERR_CAPACITY
+    assert oa[int(oo[0]):int(oo[0]) + int(ol[0])].tobytes() == want[0]
+    assert oa[int(oo[2]):int(oo[2]) + int(ol[2])].tobytes() == want[1]

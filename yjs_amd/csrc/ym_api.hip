@@ -311,23 +311,39 @@ int select_docs(DevState *S, hipStream_t st, const uint32_t *list, uint32_t n, c
 }
 
 // Doc round-trip compaction (ym_compact.hip) over `list` (n docs, nullptr: all); documents whose workspace
-// overflowed run again with 4x the workspace.
+// overflowed run again with 4x the workspace.  The workspaces of one launch are bounded by a device-memory
+// budget (YMERGE_COMPACT_WS_GB, default 16 GiB): a list whose workspaces exceed it runs in chunks cut at the
+// exclusive scan of the per-document sizes; a document that alone exceeds it, or whose workspace cannot be
+// allocated, or that still overflows after the last growth round, reports ST_CAPACITY (the others are not
+// affected).
+__global__ void k_iota(uint32_t *dst, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = i;
+}
+__global__ void k_set_status(const uint32_t *list, uint32_t n, int32_t *status, uint64_t *out_len, int from, int to) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t d = list ? list[i] : i;
+  if (from < 0 || status[d] == from) { status[d] = to; out_len[d] = 0; }
+}
 int run_compact(DevState *S, hipStream_t st, GeneralJob j, uint32_t *list, uint32_t n) {
-  static int lanes = -1;
-  if (lanes < 0) {  // active lanes (documents) per 64-wide wave; measured on C2 / C4 (10 k documents):
-    // 1: 209 / 268 ms, 8: 110 / 102, 16: 77 / 62, 32: 85 / 62, 64: 89 / 63 (profiles/r03c)
-    const char *e = getenv("YMERGE_COMPACT_LANES");
-    lanes = e ? atoi(e) : 16;
-    if (lanes < 1 || lanes > 64) lanes = 16;
-  }
-  static int occ = -1;
-  if (occ < 0) { const char *e = getenv("YMERGE_COMPACT_OCC"); occ = e && atoi(e) == 2 ? 2 : 1; }
+  // read on every call (a process may change them between calls): active lanes (documents) per 64-wide
+  // wave -- measured on C2 / C4 (10 k documents): 1: 209 / 268 ms, 8: 110 / 102, 16: 77 / 62, 32: 85 / 62,
+  // 64: 89 / 63 (profiles/r03c) -- and the register-occupancy variant
+  const char *el = getenv("YMERGE_COMPACT_LANES");
+  int lanes = el ? atoi(el) : 16;
+  if (lanes < 1 || lanes > 64) lanes = 16;
+  const char *eo = getenv("YMERGE_COMPACT_OCC");
+  const int occ = eo && atoi(eo) == 2 ? 2 : 1;
+  const char *eb = getenv("YMERGE_COMPACT_WS_GB");
+  const double gb = eb ? atof(eb) : 16.0;
+  const uint64_t budget = gb > 0 ? (uint64_t)(gb * (double)(1ull << 30)) : (16ull << 30);
   uint32_t mul = 1;
   for (int round = 0; n > 0; round++) {
-    j.list = list;
-    j.n = n;
     j.parts_mul = mul;
     if (S->ws_size.ensure((size_t)(n + 1) * 8) || S->ws_off.ensure((size_t)(n + 1) * 8)) return -1;
+    j.list = list;
+    j.n = n;
     k_compact_ws<<<(n + 255) / 256, 256, 0, st>>>(j, S->ws_size.as<uint64_t>());
     size_t tmp = 0;
     hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, S->ws_size.as<uint64_t>(), S->ws_off.as<uint64_t>(), n, st);
@@ -337,16 +353,59 @@ int run_compact(DevState *S, hipStream_t st, GeneralJob j, uint32_t *list, uint3
     HIPCHK(hipMemcpyAsync(S->pinned + 1, S->ws_size.as<uint64_t>() + (n - 1), 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     const uint64_t ws_total = S->pinned[0] + S->pinned[1];
-    if (S->ws.ensure(ws_total + 64)) return -2;
-    j.ws = S->ws.as<uint8_t>();
-    j.ws_off = S->ws_off.as<uint64_t>();
+    // chunks [cut[k], cut[k + 1]) of the list, each within the budget (one chunk in the common case)
+    std::vector<uint32_t> cut = {0, n};
+    std::vector<uint64_t> off;
+    if (ws_total > budget) {
+      if (!list) {  // chunks are sub-ranges of a list: the identity list of all documents
+        if (S->list_a.ensure((size_t)(n + 1) * 4)) return -2;
+        list = S->list_a.as<uint32_t>();
+        k_iota<<<(n + 255) / 256, 256, 0, st>>>(list, n);
+      }
+      off.resize((size_t)n + 1);
+      HIPCHK(hipMemcpyAsync(off.data(), S->ws_off.as<uint64_t>(), (size_t)n * 8, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      off[n] = ws_total;
+      cut.assign(1, 0);
+      for (uint32_t a = 0; a < n;) {
+        uint32_t b = a + 1;
+        while (b < n && off[b + 1] - off[a] <= budget) b++;
+        cut.push_back(b);
+        a = b;
+      }
+    }
+    // one allocation serves every chunk (they run one after the other on the stream)
+    uint64_t maxb = 0;
+    for (size_t k = 0; k + 1 < cut.size(); k++) {
+      const uint64_t bytes = off.empty() ? ws_total : off[cut[k + 1]] - off[cut[k]];
+      if (bytes <= budget || cut[k + 1] - cut[k] > 1) maxb = bytes > maxb ? bytes : maxb;
+    }
+    if (maxb && S->ws.ensure(maxb + 64)) return -2;
     HIPCHK(hipMemsetAsync(j.counter_retry, 0, 4, st));
-    if (occ == 2) k_compact<2><<<(n + lanes - 1) / lanes, 64, 0, st>>>(j, (uint32_t)lanes);
-    else k_compact<1><<<(n + lanes - 1) / lanes, 64, 0, st>>>(j, (uint32_t)lanes);
+    for (size_t k = 0; k + 1 < cut.size(); k++) {
+      const uint32_t a = cut[k], cnt = cut[k + 1] - a;
+      const uint64_t base = off.empty() ? 0 : off[a];
+      const uint64_t bytes = off.empty() ? ws_total : off[a + cnt] - base;
+      GeneralJob jc = j;
+      jc.list = list ? list + a : nullptr;
+      jc.n = cnt;
+      jc.ws_off = S->ws_off.as<uint64_t>() + a;
+      if (bytes > maxb) {  // one document whose workspace alone exceeds the budget
+        k_set_status<<<1, 64, 0, st>>>(jc.list, cnt, j.status, j.out_len, -1, ym::ST_CAPACITY);
+        continue;
+      }
+      jc.ws = S->ws.as<uint8_t>() - base;  // ws + ws_off[i] lands in this chunk's allocation
+      if (occ == 2) k_compact<2><<<(cnt + lanes - 1) / lanes, 64, 0, st>>>(jc, (uint32_t)lanes);
+      else k_compact<1><<<(cnt + lanes - 1) / lanes, 64, 0, st>>>(jc, (uint32_t)lanes);
+    }
     HIPCHK(hipMemcpyAsync(S->pinned, j.counter_retry, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     const uint32_t nretry = (uint32_t)(S->pinned[0] & 0xffffffffu);
-    if (nretry == 0 || round >= 5) break;
+    if (nretry == 0) break;
+    if (round >= 5) {  // still overflowing at 1024x: a public status, not the internal retry code
+      k_set_status<<<(n + 255) / 256, 256, 0, st>>>(list, n, j.status, j.out_len, ym::ST_RETRY, ym::ST_CAPACITY);
+      break;
+    }
     uint32_t *next = list == S->list_a.as<uint32_t>() ? S->list_b.as<uint32_t>() : S->list_a.as<uint32_t>();
     uint32_t cnt = 0;
     if (select_docs(S, st, list, n, j.status, ym::ST_RETRY, next, &cnt)) return -1;
@@ -726,6 +785,7 @@ const char *ym_strerror(int code) {
       case 8: return "Cannot read property 'length' of undefined";
       case 9: return "Invalid code point NaN";
       case 10: return "Offset is outside the bounds of the DataView";
+      case 12: return "Cannot read property 'origin' of undefined";
       case 11:
         if (arg == 0x7fff) return "Invalid typed array length";
         snprintf(buf, sizeof buf, "Invalid typed array length: %d", arg);

@@ -663,6 +663,10 @@ YM_HOT void it_integrate(Doc &d, int32_t i, int64_t off) {
     return;
   }
   const int32_t P = d.it[i].parent;
+  // 13.4.9 with a GC on the left (getClean* on a GC id; a parent from the right neighbour, Item.js:375-387,
+  // or the own-client predecessor of an offset): a GC has no `right`, undefined !== this.right, so the
+  // conflict scan starts at o = undefined and reads o.origin (Item.js:413, 425, 450)
+  if (d.it[i].left != NIL && d.it[d.it[i].left].gc) { seterr(c, st_d(ST_TYPE, D_ORIGIN_UNDEF)); return; }
   {
     Item &x = d.it[i];
     if ((x.left == NIL && (x.right == NIL || d.it[x.right].left != NIL)) || (x.left != NIL && d.it[x.left].right != x.right)) {
@@ -686,7 +690,7 @@ YM_HOT void it_integrate(Doc &d, int32_t i, int64_t off) {
           else if (id_eq(xi.has_right, xi.rc, xi.rk, ob.has_right, ob.rc, ob.rk)) break;
         } else if (ob.has_origin) {
           const int32_t oo = cd_get(d, ob.oc, ob.ok);
-          if (oo == NIL) return;
+          if (oo == NIL) { seterr(c, ST_UNEXPECTED); return; }  // (unreachable: an integrated origin is stored)
           if (d.it[oo].gen_before == gb) {
             if (d.it[oo].gen_conf != gcf) { left = o; gcf = ++d.gen; }
           } else {
@@ -757,8 +761,9 @@ YM_INL void refs_sort(Doc &d, int32_t *a, uint32_t n) {  // stable sort by clock
 YM_HOT void resume_integration(Doc &d) {
   Ctx &c = *d.c;
   Arena &A = *d.a;
+  Arena &T = *d.ta;  // the sorted ids and the state cache live for this call only
   uint32_t nids = 0;
-  int64_t *ids = (int64_t *)aalloc(c, A, 8ull * (d.pend.n + 1));
+  int64_t *ids = (int64_t *)aalloc(c, T, 8ull * (d.pend.n + 1));
   if (!ids) return;
   for (uint32_t i = 0; i < d.pend.n; i++)
     if (d.pend.p[i].live) ids[nids++] = d.pend.p[i].client;
@@ -791,8 +796,8 @@ YM_HOT void resume_integration(Doc &d) {
       if (scc.p[i] == hc) { local = sck.p[i]; break; }
     if (local < 0) {
       local = cd_state(d, hc);
-      vpush(c, A, scc, hc);
-      vpush(c, A, sck, local);
+      vpush(c, T, scc, hc);
+      vpush(c, T, sck, local);
     }
     const int64_t off = d.it[head].clock < local ? local - d.it[head].clock : 0;
     if (d.it[head].clock + off != local) {
@@ -846,10 +851,21 @@ YM_HOT void resume_integration(Doc &d) {
 }
 
 // readAndApplyDeleteSet over decoded ranges (DeleteSet.js:270-323); unapplied ranges become a pending
-// delete reader
-YM_HOT void apply_ds(Doc &d, const DSet &ds) {
+// delete reader.  `kept`: ds is a pending reader already in the persistent arena -- when none of its ranges
+// applies, the new reader equals it range for range and is kept as it is (a history that leaves deletes
+// pending re-reads every pending reader on every update; copying them each time grew the arena
+// quadratically)
+YM_HOT void apply_ds(Doc &d, const DSet &ds, bool kept = false) {
   Ctx &c = *d.c;
-  DSet un = {{nullptr, 0, 0}};
+  if (kept) {
+    bool any = false;
+    for (uint32_t ci = 0; ci < ds.cl.n && !any; ci++) {
+      const int64_t state = cd_state(d, ds.cl.p[ci].client);
+      for (uint32_t k = 0; k < ds.cl.p[ci].it.n && !any; k++) any = ds.cl.p[ci].it.p[k].clock < state;
+    }
+    if (!any) { vpush(c, *d.a, d.pdel, ds); return; }
+  }
+  DSet un = {{nullptr, 0, 0}, d.ta};
   for (uint32_t ci = 0; ci < ds.cl.n && !c.err; ci++) {
     const int64_t client = ds.cl.p[ci].client;
     const int32_t s = cd_client(d, client);
@@ -887,7 +903,31 @@ YM_HOT void apply_ds(Doc &d, const DSet &ds) {
       }
     }
   }
-  if (un.cl.n > 0) vpush(c, *d.a, d.pdel, un);
+  if (c.err || un.cl.n == 0) return;
+  // the reader pushed is a DSDecoderV2 over writeDeleteSet(DSEncoderV2, unappliedDS) (DeleteSet.js:317-321):
+  // per client the clock is written as a delta to the previous range's end and the length as len - 1, both
+  // by writeVarUint, which writes a negative value as its low 7 bits.  Ranges sorted, disjoint and non-empty
+  // (what yjs writes) come back unchanged; the others come back as that round trip makes them.  The
+  // transient reader moves to the persistent arena.
+  DSet keep = {{nullptr, 0, 0}, nullptr};
+  if (!vgrow(c, *d.a, keep.cl, un.cl.n)) return;
+  for (uint32_t k = 0; k < un.cl.n; k++) {
+    DCl z = {un.cl.p[k].client, {nullptr, 0, 0}};
+    if (!vgrow(c, *d.a, z.it, un.cl.p[k].it.n)) return;
+    int64_t enc = 0, dec = 0;
+    for (uint32_t q = 0; q < un.cl.p[k].it.n; q++) {
+      const DIt r = un.cl.p[k].it.p[q];
+      const int64_t dc = r.clock - enc, dl = r.len - 1;
+      enc = r.clock + r.len;
+      dec += dc > 127 ? dc : (dc & 127);
+      const int64_t len = (dl > 127 ? dl : (dl & 127)) + 1;
+      z.it.p[q] = {dec, len};
+      dec += len;
+    }
+    z.it.n = un.cl.p[k].it.n;
+    keep.cl.p[keep.cl.n++] = z;
+  }
+  vpush(c, *d.a, d.pdel, keep);
 }
 
 // ---- reading -----------------------------------------------------------------------------------------
@@ -1402,10 +1442,14 @@ YM_HOT void cd_transact(Doc &d, Reader &r) {
     }
     d.pend.n = w;
   }
-  {  // tryResumePendingDeleteReaders
+  {  // tryResumePendingDeleteReaders: the readers are re-read in order and the ones still pending written
+     // back in place (reader q's successor lands at an index <= q, after reader q was read)
     const Vec<DSet> pr = d.pdel;
-    d.pdel.p = nullptr; d.pdel.n = 0; d.pdel.cap = 0;
-    for (uint32_t q = 0; q < pr.n && !c.err; q++) apply_ds(d, pr.p[q]);
+    d.pdel.n = 0;
+    for (uint32_t q = 0; q < pr.n && !c.err; q++) {
+      const DSet one = pr.p[q];
+      apply_ds(d, one, true);
+    }
   }
   {  // readAndApplyDeleteSet: each client's ranges are applied as read (the clients are independent)
     const uint32_t n = rd_vu(c, r.rest);
@@ -1648,10 +1692,9 @@ YM_BIG void compact_doc(Ctx &c, uint8_t *ws, const WsSize &z, uint32_t v2, const
 #endif
     }
     if (c.err) return;
-    // every input applied completely (pending structs or deletes: not expressible as one update here)
-    for (uint32_t q = 0; q < d.pend.n; q++)
-      if (d.pend.p[q].live) { seterr(c, ST_UNSUPPORTED); return; }
-    if (d.stack.n > 0 || d.pdel.n > 0) { seterr(c, ST_UNSUPPORTED); return; }
+    // structs still waiting for a missing dependency (pending refs, the pending stack) and deletes of
+    // clocks not yet seen (pending delete readers) stay out of the output: encodeStateAsUpdate writes the
+    // integrated store and its delete set only (encoding.js:490-493)
   }
   d.c = &c;
   if (!out) {

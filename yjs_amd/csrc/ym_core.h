@@ -51,6 +51,7 @@ enum : int {
   D_CODEPOINT_NAN = 9,  // RangeError Invalid code point NaN                                  (lib0 readVarString, short)
   D_DATAVIEW = 10,      // RangeError Offset is outside the bounds of the DataView            (readFloat32/64, readBigInt64)
   D_TA_LENGTH = 11,     // RangeError Invalid typed array length: <arg>                       (lib0 readUint8Array)
+  D_ORIGIN_UNDEF = 12,  // TypeError  Cannot read property 'origin' of undefined              (13.4.9 Item.integrate, Item.js:450: left is a GC)
 };
 YM_INL int st_d(int cls, int detail, uint64_t arg = 0) {
   return cls | (detail << 8) | (int)((arg < 0x7fff ? arg : 0x7fff) << 16);

@@ -132,10 +132,27 @@ def pack_docs(docs):
     return arena, upd_off, np.array(doc_upd, np.uint32)
 
 
+def _torch_first():
+    """torch's wheel bundles its own HIP runtime.  When libymerge.so's runtime initialises the device first,
+    torch's first CUDA call in the same process reports "No HIP GPUs are available"; in the other order both
+    work.  So the engine lets torch initialise first whenever torch is importable (it is the plumbing for
+    device tensors, the multi-GPU launcher and the benchmark)."""
+    try:
+        import torch
+    except ImportError:
+        return
+    try:
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except RuntimeError as e:  # torch cannot see a device the HIP runtime may still see: say which
+        raise RuntimeError(f"torch could not initialise the GPU before libymerge.so ({e})") from e
+
+
 class Engine:
     """One engine per process/GPU (the library keeps one HIP stream and workspace per thread)."""
 
     def __init__(self, device=0, path=None):
+        _torch_first()
         self.lib = load_library(path)
         rc = self.lib.ym_init(device)
         if rc != 0:
