@@ -60,16 +60,17 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(arena, upd_off, doc_upd, fmt, seconds):
-    """The oracle (CPU port of yjs 13.5.16 mergeUpdates) over the same documents, all host threads of
-    this process's CPU share, repeated until `seconds` of wall time."""
+def cpu_baseline(arena, upd_off, doc_upd, fmt, seconds, op="merge"):
+    """The oracle (CPU port of yjs 13.5.16 mergeUpdates; op="compact": of the reference's Doc round trip)
+    over the same documents, all host threads of this process's CPU share, repeated until `seconds` of wall
+    time."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ref  # test infrastructure: only the cpu_baseline leg may load it
     threads = host_cores()
     n_docs = len(doc_upd) - 1
     reps, t0 = 0, time.perf_counter()
     while True:
-        _, st, out_len = oracle_ref.batch("merge", fmt, arena, upd_off, doc_upd, nthreads=threads, want_output=False)
+        _, st, out_len = oracle_ref.batch(op, fmt, arena, upd_off, doc_upd, nthreads=threads, want_output=False)
         reps += 1
         el = time.perf_counter() - t0
         if el >= seconds:
@@ -83,11 +84,16 @@ def cpu_baseline(arena, upd_off, doc_upd, fmt, seconds):
         "host_cpu_count": os.cpu_count(),
         "kind": "port",
         "sample": f"{reps} x {n_docs} docs ({bytes_in / reps / 1e6:.1f} MB input each) in {el:.1f} s, "
-                  f"oracle/ymerge_oracle.c (literal yjs 13.5.16 mergeUpdates), {threads} threads",
+                  + ("oracle/ymerge_oracle.c compact_impl (the reference's 13.4.9 Doc round trip restated)"
+                     if op == "compact" else "oracle/ymerge_oracle.c (literal yjs 13.5.16 mergeUpdates)")
+                  + f", {threads} threads",
         "errors": int((st != 0).sum()),
         # the port is faster than the JS it restates: per-thread ratios measured on identical C2 / C4
         # documents in the build container by tools/calibrate.py (JS cannot run on the GPU box)
-        "calibration": _calibration(),
+        "calibration": _calibration() if op == "merge" else None,
+        # the whole machine's cores at the measured per-thread rate (what a host-side deployment could reach)
+        "all_host_cores_estimate": {"cores": os.cpu_count(),
+                                    "docs_per_s": round(n_docs * reps / el / threads * (os.cpu_count() or 1), 1)},
     }
 
 
@@ -274,6 +280,11 @@ def _secondary_case(dev, eng, name, op, wl, n):
         sts = eng.stats
         out_b = int(ol[st == 0].sum().item())
         kms_mean = float(np.mean(kms))
+        cpu = None
+        if op == "compact" and not os.environ.get("YM_NO_CPU_BASELINE"):
+            # the host baseline of the same documents (a bounded sample: 2,000 of them, ~2 s per pass)
+            k = min(nd, 2000)
+            cpu = cpu_baseline(a[:int(o[d[k]])], o[:int(d[k]) + 1], d[:k + 1], fmt, 2.0, op="compact")
         # roofline of the call's dominant kernel(s): algorithmic bytes (inputs + outputs) / their device time
         kgbs = (len(a) + out_b) / (kms_mean * 1e-3) / 1e9 if kms_mean > 0 else 0.0
         return {"docs": nd, "input_bytes": int(len(a)), "output_bytes": out_b,
@@ -282,7 +293,8 @@ def _secondary_case(dev, eng, name, op, wl, n):
                      "kernel_ms": round(kms_mean, 3), "kernel_in_plus_out_gbs": round(kgbs, 2),
                      "roofline_frac": round(kgbs / HBM_PEAK_GBS, 5), "docs_fast": int(sts["docs_fast"]),
                      "docs_large": int(sts["docs_large"]), "docs_general": int(sts["docs_general"]),
-                     "errors": int(sts["docs_error"]), "update_offsets": "u32" if off32 else "u64"}
+                     "errors": int(sts["docs_error"]), "update_offsets": "u32" if off32 else "u64",
+                     **({"cpu_baseline": cpu} if cpu else {})}
 
 
 def _sv_of_single_client_update(upd, fmt):

@@ -3367,6 +3367,8 @@ static void *batch_worker(void *arg) {
       st = ymo_ds_merge(ptrs, lens, n, j->fmt, &out, &olen);
     } else if (j->op == 6) {
       st = n == 1 ? ymo_snapshot(ptrs[0], lens[0], j->fmt, &out, &olen) : YMO_ERR_UNEXPECTED;
+    } else if (j->op == 7) {
+      st = ymo_compact(ptrs, lens, n, j->fmt, &out, &olen);
     } else st = n >= 1 ? ymo_sv_from_update(ptrs[0], lens[0], j->fmt, &out, &olen) : YMO_ERR_UNEXPECTED;
     if (st == YMO_OK && j->out_arena) {
       uint64_t cap = j->out_cap_off[d + 1] - j->out_cap_off[d];

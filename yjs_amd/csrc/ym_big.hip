@@ -469,13 +469,12 @@ __global__ void k_big_init(GeneralJob j) {
 
 int big_launch(uint32_t op, const GeneralJob &j0, hipStream_t st, PwBufs &pwb) {
   if (j0.v2 || (op != OP_DIFF && op != OP_SV && op != OP_META)) return 0;
-  // meta over many small updates (e.g. every update of a batch): one thread per update on the general
-  // path beats a grid of BS_GRID waves walking hundreds of tiny updates each (1 M C2 updates: 2.5 vs 12 ms)
-  if (op == OP_META && j0.n > 8 * BS_GRID) return 0;
   k_big_init<<<1, 64, 0, st>>>(j0);
   GeneralJob j = j0;
-  // large single updates: the chunk-parallel walk first (ym_pwalk.hip); k_big_v1 takes the rest
+  // large single updates: the chunk-parallel walk first (ym_pwalk.hip); small ones one per lane
+  // (ym_small.hip); k_big_v1 takes the rest (it skips what those completed)
   if (int r = pw_run(op, j0, st, pwb, &j.pw_done); r < 0) return r;
+  small_launch(op, j, const_cast<uint8_t *>(j.pw_done), st);
   const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
   if (op == OP_DIFF) big::k_big_v1<OP_DIFF><<<grid, 64, big::LDS_BYTES, st>>>(j);
   else if (op == OP_META) big::k_big_v1<OP_META><<<grid, 64, big::LDS_BYTES, st>>>(j);

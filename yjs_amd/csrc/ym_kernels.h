@@ -83,6 +83,8 @@ struct PwBufs {
 // Chunk-parallel walk + stitch over the large single-update documents of a V1 diff / sv call; sets
 // *done (per document: 1 = completed).  Returns 1 when launched, 0 when not applicable, < 0 on error.
 int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const uint8_t **done);
+// Small single updates of a V1 diff / sv / meta call, one document per lane (ym_small.hip); marks done[d].
+int small_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t st);
 // The same for V2 (ym_pv2.hip): column-parallel diff / sv over large single-section documents.
 int pv2_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const uint8_t **done);
 

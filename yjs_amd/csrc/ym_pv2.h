@@ -112,6 +112,18 @@ __device__ __forceinline__ Sec *a_sec(const Job &J, const Meta &M) { return rein
 __device__ __forceinline__ uint32_t *a_istart(const Job &J, const Meta &M) {
   return reinterpret_cast<uint32_t *>(J.scr1 + M.soff1 + (((uint64_t)M.nsec * sizeof(Sec) + 15) & ~15ull));
 }
+// multi-section rest walk (MR): the payload structs in struct order -- struct index, and kind | count / len
+// ordinal -- and the len column's entries (first value ordinal, value); icap = rest bytes + 1 bounds both
+// the payload structs and the payload starts
+__host__ __device__ inline uint32_t ms_icap(uint32_t len, uint32_t r0) { return len - r0 + 1; }
+__host__ __device__ inline uint64_t ms_scr1_bytes(uint32_t nsec, uint32_t len, uint32_t r0, uint32_t lncol) {
+  return ((((uint64_t)nsec * sizeof(Sec) + 15) & ~15ull) + 12ull * ms_icap(len, r0) + 8ull * (lncol + 2) + 511) & ~255ull;
+}
+__device__ __forceinline__ uint32_t *a_pidx(const Job &J, const Meta &M, uint32_t len) { return a_istart(J, M) + ms_icap(len, M.r0); }
+__device__ __forceinline__ uint32_t *a_pkl(const Job &J, const Meta &M, uint32_t len) { return a_istart(J, M) + 2ull * ms_icap(len, M.r0); }
+__device__ __forceinline__ uint2 *a_lent(const Job &J, const Meta &M, uint32_t len) {  // (16-aligned: the slack of ms_scr1_bytes)
+  return reinterpret_cast<uint2 *>((reinterpret_cast<uintptr_t>(a_istart(J, M) + 3ull * ms_icap(len, M.r0)) + 15) & ~(uintptr_t)15);
+}
 // value capacity of kind k's expanded / counted values
 __host__ __device__ inline uint64_t kind_cap(uint32_t k, uint32_t n, uint32_t nsec) {
   return k == K_SL ? 3ull * n + 1 : k == K_CL ? 2ull * n + nsec + 1 : n;
@@ -160,6 +172,43 @@ __device__ __forceinline__ uint32_t rvi(ln::LCur &c, bool &neg) {
   c.bad |= (nb > 5) | (c.p + nb > c.e) | ((nb > 1) & (last == 0)) | ((nb == 5) & ((hi & 0x7fu) > 0x1fu));
   ln::skip(c, nb < 6 ? nb : 0);
   return m;
+}
+
+// ---- the column automaton (K1; the multi-section rest walk's column passes) ----------------------
+constexpr uint32_t F_ID = 0xE4;  // identity on 4 states, 2 bits per state
+__device__ __forceinline__ uint32_t fcompose(uint32_t a, uint32_t b) {  // b after a
+  uint32_t c = 0;
+#pragma unroll
+  for (uint32_t st = 0; st < 4; st++) c |= ((b >> (2 * ((a >> (2 * st)) & 3))) & 3) << (2 * st);
+  return c;
+}
+#define CDPP(x, ctl, rm) (uint32_t) __builtin_amdgcn_update_dpp((int)F_ID, (int)(x), ctl, rm, 0xf, false)
+__device__ __forceinline__ uint32_t wave_incl_compose(uint32_t f) {
+  f = fcompose(CDPP(f, 0x111, 0xf), f);
+  f = fcompose(CDPP(f, 0x112, 0xf), f);
+  f = fcompose(CDPP(f, 0x114, 0xf), f);
+  f = fcompose(CDPP(f, 0x118, 0xf), f);
+  f = fcompose(CDPP(f, 0x142, 0xa), f);
+  f = fcompose(CDPP(f, 0x143, 0xc), f);
+  return f;
+}
+__device__ __forceinline__ uint64_t wave_incl_add64(uint64_t x) {
+#define A64(ctl, rm)                                                                                 \
+  {                                                                                                  \
+    const uint32_t rl = YM_DPP((uint32_t)x, ctl, rm), rh = YM_DPP((uint32_t)(x >> 32), ctl, rm);    \
+    x += ((uint64_t)rh << 32) | rl;                                                                  \
+  }
+  A64(0x111, 0xf) A64(0x112, 0xf) A64(0x114, 0xf) A64(0x118, 0xf) A64(0x142, 0xa) A64(0x143, 0xc)
+#undef A64
+  return x;
+}
+__device__ __forceinline__ uint32_t tstep(uint32_t st, uint32_t b, bool rle, uint32_t fb) {
+  const bool stop = b < 0x80;
+  if (rle) return st == 0 ? 1 : (stop ? 0 : 1);
+  if (st == 0) { const bool fl = (b >> fb) & 1; return stop ? (fl ? 3 : 0) : (fl ? 1 : 2); }
+  if (st == 1) return stop ? 3 : 1;
+  if (st == 2) return stop ? 0 : 2;
+  return stop ? 0 : 3;
 }
 
 struct Ent {

@@ -86,7 +86,7 @@ __global__ void k_v2_prep(Job J, uint64_t pv_min, uint64_t *sizes, uint64_t *siz
     M.n = 0;
     M.ok = 1;
     M.why = 0;
-    sizes1[d] = ((((uint64_t)nclients * sizeof(Sec) + 15) & ~15ull) + 4ull * (len - M.r0 + 1) + 511) & ~255ull;  // (Sec holds a u64 atomic)
+    sizes1[d] = ms_scr1_bytes(nclients, len, M.r0, M.col1[8] - M.col0[8]);  // (Sec holds a u64 atomic)
     return;
   }
   // typeRef / keyClock unused by the kinds the single-section path takes
@@ -121,41 +121,6 @@ __global__ void k_v2_meta_off(Job J, const uint64_t *offs, uint32_t which) {
 // scans give their entry / value indices and (IntDiff) running values.  Checks: canonical
 // varints, maximal runs, no -0 diff, diffs < 2^30, values in [0, 2^32), parentInfo in {0, 1},
 // an RLE<u8> column ending without a count.
-constexpr uint32_t F_ID = 0xE4;  // identity on 4 states, 2 bits per state
-__device__ __forceinline__ uint32_t fcompose(uint32_t a, uint32_t b) {  // b after a
-  uint32_t c = 0;
-#pragma unroll
-  for (uint32_t st = 0; st < 4; st++) c |= ((b >> (2 * ((a >> (2 * st)) & 3))) & 3) << (2 * st);
-  return c;
-}
-#define CDPP(x, ctl, rm) (uint32_t) __builtin_amdgcn_update_dpp((int)F_ID, (int)(x), ctl, rm, 0xf, false)
-__device__ __forceinline__ uint32_t wave_incl_compose(uint32_t f) {
-  f = fcompose(CDPP(f, 0x111, 0xf), f);
-  f = fcompose(CDPP(f, 0x112, 0xf), f);
-  f = fcompose(CDPP(f, 0x114, 0xf), f);
-  f = fcompose(CDPP(f, 0x118, 0xf), f);
-  f = fcompose(CDPP(f, 0x142, 0xa), f);
-  f = fcompose(CDPP(f, 0x143, 0xc), f);
-  return f;
-}
-__device__ __forceinline__ uint64_t wave_incl_add64(uint64_t x) {
-#define A64(ctl, rm)                                                                                 \
-  {                                                                                                  \
-    const uint32_t rl = YM_DPP((uint32_t)x, ctl, rm), rh = YM_DPP((uint32_t)(x >> 32), ctl, rm);    \
-    x += ((uint64_t)rh << 32) | rl;                                                                  \
-  }
-  A64(0x111, 0xf) A64(0x112, 0xf) A64(0x114, 0xf) A64(0x118, 0xf) A64(0x142, 0xa) A64(0x143, 0xc)
-#undef A64
-  return x;
-}
-__device__ __forceinline__ uint32_t tstep(uint32_t st, uint32_t b, bool rle, uint32_t fb) {
-  const bool stop = b < 0x80;
-  if (rle) return st == 0 ? 1 : (stop ? 0 : 1);
-  if (st == 0) { const bool fl = (b >> fb) & 1; return stop ? (fl ? 3 : 0) : (fl ? 1 : 2); }
-  if (st == 1) return stop ? 3 : 1;
-  if (st == 2) return stop ? 0 : 2;
-  return stop ? 0 : 3;
-}
 __global__ void __launch_bounds__(64) k_v2_decw(Job J) {
   const GeneralJob &j = J.j;
   const uint32_t d = blockIdx.x, kind = blockIdx.y, lane = threadIdx.x;

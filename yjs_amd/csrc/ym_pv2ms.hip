@@ -267,6 +267,388 @@ __global__ void __launch_bounds__(64) k_ms_rest(Job J) {
   MSP(1, n_ie); MSP(2, n_le); MSP(3, n_rf); MSP(4, n_rs); MSP(6, n_g);
 }
 
+// ---- MR, block-parallel (k_ms_rest2): the walk's sequential chain reduced to the rest stream's tokens ----
+// The serial walk above spends most of its steps on the info column (C5: ~55 k run entries per document,
+// 0.6 us each on one wave) although only the rest stream is sequential.  Here one 256-thread block per
+// document:
+//  A  tokenises the info column 4 KB per block step (the RLE<u8> automaton of K1, composed across the
+//     block) and writes the PAYLOAD LIST: every struct that has rest tokens (Skip: a varuint, Binary: a
+//     varUint8Array, Embed / Format: one `any`, Any: `len` of them), in struct order, with its struct
+//     index and kind (Any: its ordinal among the len column's consumers: GC, Deleted, Any);
+//  B  tokenises the len column (UintOptRle) into its entries (first value ordinal, value) and resolves
+//     every Any's value count by a binary search;
+//  C  walks the rest stream with one thread, 4 KB window by window: the whole block first computes, for
+//     every byte offset of the window, the length of the token a varuint / varUint8Array / scalar `any`
+//     would have there (0: not decidable from the window, or invalid -- the walker then parses that token
+//     itself), so each step of the chain is a table lookup: a section header (two varuints, parsed), then
+//     the tokens of the payload structs up to the section's end (payload list, staged into LDS per window).
+// Outputs are those of k_ms_rest: the section table (first struct, structs, clock, payload span, payload
+// ordinal), every payload struct's rest position, the struct and payload counts, the delete set's start.
+constexpr uint32_t MR_T = 256, MR_W = 4096, MR_MARG = 256, MR_PC = 1024;
+// per-thread 16-byte slice transition of the RLE<u8> / UintOptRle automaton (K1's tstep), packed 2 bits per state
+__device__ __forceinline__ uint32_t mr_slice_f(const uint8_t (&b)[16], uint32_t q, uint32_t c1, bool rle, uint32_t fb) {
+  uint32_t s0 = 0, s1 = 1, s2 = 2, s3 = 3;
+#pragma unroll
+  for (uint32_t k = 0; k < 16; k++)
+    if (q + k < c1) { s0 = tstep(s0, b[k], rle, fb); s1 = tstep(s1, b[k], rle, fb); s2 = tstep(s2, b[k], rle, fb); s3 = tstep(s3, b[k], rle, fb); }
+  return s0 | (s1 << 2) | (s2 << 4) | (s3 << 6);
+}
+// block-wide: the transition before this thread's slice (composed over lower threads) and the block's total
+__device__ __forceinline__ uint32_t mr_block_compose(uint32_t f, uint32_t *sh, uint32_t &total) {
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint32_t incl = wave_incl_compose(f);
+  const uint32_t excl = (uint32_t)__builtin_amdgcn_update_dpp((int)F_ID, (int)incl, 0x138, 0xf, 0xf, false);
+  __syncthreads();
+  if (lane == 63) sh[w] = incl;
+  __syncthreads();
+  uint32_t pre = F_ID;
+  for (uint32_t k = 0; k < w; k++) pre = fcompose(pre, sh[k]);
+  total = F_ID;
+  for (uint32_t k = 0; k < MR_T / 64; k++) total = fcompose(total, sh[k]);
+  return fcompose(pre, excl);
+}
+// block-wide exclusive sums of a u64 and three u32 values (+ the block's totals)
+__device__ __forceinline__ void mr_block_scan(uint64_t &a, uint32_t &b, uint32_t &c, uint32_t &e, uint64_t *sh64, uint32_t *sh,
+                                              uint64_t &ta, uint32_t &tb, uint32_t &tc, uint32_t &te) {
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint64_t ia = wave_incl_add64(a);
+  const uint32_t ib = wave_incl_add(b), ic = wave_incl_add(c), ie = wave_incl_add(e);
+  __syncthreads();
+  if (lane == 63) { sh64[w] = ia; sh[3 * w] = ib; sh[3 * w + 1] = ic; sh[3 * w + 2] = ie; }
+  __syncthreads();
+  uint64_t pa = 0;
+  uint32_t pb = 0, pc = 0, pe = 0;
+  ta = 0; tb = 0; tc = 0; te = 0;
+  for (uint32_t k = 0; k < MR_T / 64; k++) {
+    if (k < w) { pa += sh64[k]; pb += sh[3 * k]; pc += sh[3 * k + 1]; pe += sh[3 * k + 2]; }
+    ta += sh64[k]; tb += sh[3 * k]; tc += sh[3 * k + 1]; te += sh[3 * k + 2];
+  }
+  a = pa + ia - a; b = pb + ib - b; c = pc + ic - c; e = pe + ie - e;
+}
+// payload kinds (the low 3 bits of a payload-list entry)
+enum : uint32_t { PK_NONE = 0, PK_SKIP = 1, PK_BIN = 2, PK_ONE = 3, PK_ANY = 4 };
+// an info byte's rest payload kind and whether it consumes a len value; false: a kind this path declines
+__device__ __forceinline__ bool mr_kind(uint32_t v, uint32_t &pk, bool &lenc) {
+  pk = PK_NONE;
+  lenc = false;
+  if (v == 10) { pk = PK_SKIP; return true; }
+  const uint32_t ref = v & 31;
+  switch (ref) {
+    case 0: lenc = true; return v == 0;  // GC (GC.write writes info 0)
+    case 1: lenc = true; return true;    // ContentDeleted
+    case 3: pk = PK_BIN; return true;
+    case 5: case 6: pk = PK_ONE; return true;
+    case 8: pk = PK_ANY; lenc = true; return true;
+    case 4: case 7: return true;         // String / Type: columns only
+    default: return false;               // JSON, Doc, invalid refs
+  }
+}
+// the token of kind k at o of the window buffer (bytes [0, lim)): its length, 0 when not decidable here
+__device__ __forceinline__ uint32_t mr_tok_len(const uint8_t *w, uint32_t o, uint32_t lim, uint32_t k) {
+  ln::LCur c = ln::make(w, o, lim, lim);
+  if (k == PK_SKIP) {
+    const uint32_t v = ln::rvu(c);
+    return c.bad || v == 0 ? 0 : c.p - o;
+  }
+  if (k == PK_BIN) {
+    const uint32_t n = ln::rvu(c);
+    if (c.bad || !ln::room(c, n)) return 0;
+    return c.p + n - o;
+  }
+  const uint32_t tag = (uint32_t)c.lo & 0xffu;
+  if (tag == 116 || tag == 117 || tag == 118 || tag == 122) return 0;  // nested: the walker's own parse
+  ln::any_scalar(c);
+  return c.bad ? 0 : c.p - o;
+}
+// the token of kind k at p, parsed from the document (the walker's slow path); NONE: invalid
+__device__ __noinline__ uint32_t mr_tok_slow(const uint8_t *D, uint32_t p, uint32_t len, uint32_t k) {
+  ln::LCur c = ln::make(D, p, len);
+  if (k == PK_SKIP) c.bad |= ln::rvu(c) == 0;
+  else if (k == PK_BIN) { const uint32_t nb = ln::rvu(c); if (c.bad || !ln::room(c, nb)) c.bad = true; else ln::skip(c, nb); }
+  else ln::any_canon(c);
+  return c.bad ? NONE : c.p;
+}
+// the len column's value at ordinal o (entries: first ordinal, value); NONE past its end
+__device__ __forceinline__ uint32_t mr_len_at(const uint2 *le, uint32_t nle, uint32_t ltot, uint32_t o) {
+  if (o >= ltot || nle == 0) return NONE;
+  uint32_t lo = 0, hi = nle;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (le[mid].x <= o) lo = mid; else hi = mid;
+  }
+  return le[lo].y;
+}
+
+__global__ void __launch_bounds__(MR_T) k_ms_rest2(Job J) {
+  const GeneralJob &j = J.j;
+  const uint32_t d = blockIdx.x, t = threadIdx.x;
+  Meta &M = J.meta[d];
+  if (!M.ok || !M.ms) return;
+  __shared__ __attribute__((aligned(16))) uint8_t win[MR_W + MR_MARG + 16];
+  __shared__ uint16_t tV[MR_W], tB[MR_W], tA[MR_W];
+  __shared__ uint32_t sidx[MR_PC], skl[MR_PC];
+  __shared__ uint32_t shf[MR_T / 64], shs[3 * (MR_T / 64)];
+  __shared__ uint64_t sh64[MR_T / 64];
+  __shared__ uint32_t s_bad;
+  // walker state (thread 0 writes, the block reads at window boundaries)
+  __shared__ uint32_t w_p, w_s, w_k, w_i, w_send, w_insec, w_rt, w_kind, w_done;
+  const uint32_t u0 = j.doc_upd[d];
+  const uint64_t ub = j.upd_off[u0];
+  const uint32_t len = (uint32_t)(j.upd_off[u0 + 1] - ub);
+  const uint8_t *D = j.A + ub;
+  Sec *S = a_sec(J, M);
+  uint32_t *ist = a_istart(J, M), *pidx = a_pidx(J, M, len), *pkl = a_pkl(J, M, len);
+  uint2 *lent = a_lent(J, M, len);
+  const uint32_t icap = ms_icap(len, M.r0);
+  if (t == 0) s_bad = 0;
+  __syncthreads();
+  // ---- A: info column -> payload list
+  uint64_t nstr = 0;        // structs of the counted entries
+  uint32_t npay = 0, nlc = 0, fin = 0, finv = 0, fin_k = 0, fin_l = 0;
+  uint64_t fin_i = 0;
+  {
+    const uint32_t c0 = M.col0[4], c1 = M.col1[4];
+    uint32_t st = 0;
+    for (uint32_t x = c0; x < c1; x += 16 * MR_T) {
+      const uint32_t q = x + 16 * t;
+      uint8_t b[16];
+      { const uint4 v4 = wds::load16m(D, q, c1); __builtin_memcpy(b, &v4, 16); }
+      uint32_t tot;
+      const uint32_t ex = mr_block_compose(mr_slice_f(b, q, c1, true, 0), shf, tot);
+      uint32_t sl = (ex >> (2 * st)) & 3, starts = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 16; k++)
+        if (q + k < c1) { if (sl == 0) starts |= 1u << k; sl = tstep(sl, b[k], true, 0); }
+      uint64_t ns = 0;
+      uint32_t np = 0, nl = 0, nf = 0, fv = 0;
+      bool bad = false;
+      for (uint32_t m = starts; m; m &= m - 1) {
+        const Ent e = dec_entry(D, q + __builtin_ctz(m), c1, K_INFO);
+        uint32_t pk;
+        bool lc;
+        bad |= e.bad || !mr_kind(e.val, pk, lc) || e.cnt > (1u << 26);
+        if (e.fin) { nf = 1; fv = e.val; continue; }
+        ns += e.cnt;
+        np += pk != PK_NONE ? e.cnt : 0;
+        nl += lc ? e.cnt : 0;
+      }
+      uint64_t a = ns;
+      uint32_t bb = np, cc = nl, ee = nf, tb, tc, te;
+      uint64_t tta;
+      mr_block_scan(a, bb, cc, ee, sh64, shs, tta, tb, tc, te);
+      // emission: the thread's entries' payload structs
+      uint64_t si = nstr + a;
+      uint32_t pi = npay + bb, li = nlc + cc;
+      bad |= nstr + tta > (1ull << 26) || npay + tb > icap;
+      if (!bad)
+        for (uint32_t m = starts; m; m &= m - 1) {
+          const Ent e = dec_entry(D, q + __builtin_ctz(m), c1, K_INFO);
+          uint32_t pk;
+          bool lc;
+          mr_kind(e.val, pk, lc);
+          if (e.fin) {  // the endless final run: its structs start after every counted one
+            fin_i = nstr + tta; fin_k = npay + tb; fin_l = nlc + tc;
+            continue;
+          }
+          if (pk != PK_NONE)
+            for (uint32_t r = 0; r < e.cnt; r++) {
+              pidx[pi + r] = (uint32_t)(si + r);
+              pkl[pi + r] = pk == PK_ANY ? ((li + r) << 3) | PK_ANY : pk;
+            }
+          si += e.cnt;
+          pi += pk != PK_NONE ? e.cnt : 0;
+          li += lc ? e.cnt : 0;
+        }
+      if (bad) s_bad = 1;
+      if (nf) { fin = 1; finv = fv; }
+      // (the final entry is the column's last byte: one thread of the last step has it)
+      st = (tot >> (2 * st)) & 3;
+      nstr += tta; npay += tb; nlc += tc;
+      __syncthreads();
+      if (s_bad) break;
+    }
+  }
+  // the final entry's values to every thread
+  __shared__ uint32_t s_fin2[5];
+  __shared__ uint64_t s_fini2;
+  if (t == 0) { s_fin2[0] = 0; }
+  __syncthreads();
+  if (fin) { s_fin2[0] = 1; s_fin2[1] = finv; s_fin2[2] = fin_k; s_fin2[3] = fin_l; s_fini2 = fin_i; }
+  __syncthreads();
+  fin = s_fin2[0];
+  if (fin) { finv = s_fin2[1]; fin_k = s_fin2[2]; fin_l = s_fin2[3]; fin_i = s_fini2; }
+  uint32_t fin_pk = PK_NONE;
+  {
+    bool lc;
+    if (fin) mr_kind(finv, fin_pk, lc);
+  }
+  // ---- B: len column entries; the Any structs' value counts
+  uint32_t nle = 0, ltot = 0;
+  if (!s_bad) {
+    const uint32_t c0 = M.col0[8], c1 = M.col1[8];
+    uint32_t st = 0;
+    uint64_t lsum = 0;
+    for (uint32_t x = c0; x < c1; x += 16 * MR_T) {
+      const uint32_t q = x + 16 * t;
+      uint8_t b[16];
+      { const uint4 v4 = wds::load16m(D, q, c1); __builtin_memcpy(b, &v4, 16); }
+      uint32_t tot;
+      const uint32_t ex = mr_block_compose(mr_slice_f(b, q, c1, false, 6), shf, tot);
+      uint32_t sl = (ex >> (2 * st)) & 3, starts = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 16; k++)
+        if (q + k < c1) { if (sl == 0) starts |= 1u << k; sl = tstep(sl, b[k], false, 6); }
+      uint64_t nv = 0;
+      uint32_t ne = 0;
+      bool bad = false;
+      for (uint32_t m = starts; m; m &= m - 1) {
+        const Ent e = dec_entry(D, q + __builtin_ctz(m), c1, K_LN);
+        bad |= e.bad;
+        nv += e.cnt;
+        ne++;
+      }
+      uint64_t a = nv;
+      uint32_t bb = ne, cc = 0, ee = 0, tb, tc, te;
+      uint64_t tta;
+      mr_block_scan(a, bb, cc, ee, sh64, shs, tta, tb, tc, te);
+      bad |= lsum + tta > 0xffffffffull;
+      if (!bad) {
+        uint64_t o = lsum + a;
+        uint32_t ei = nle + bb;
+        for (uint32_t m = starts; m; m &= m - 1) {
+          const Ent e = dec_entry(D, q + __builtin_ctz(m), c1, K_LN);
+          lent[ei++] = make_uint2((uint32_t)o, e.val);
+          o += e.cnt;
+        }
+      }
+      if (bad) s_bad = 1;
+      st = (tot >> (2 * st)) & 3;
+      lsum += tta;
+      nle += tb;
+      __syncthreads();
+      if (s_bad) break;
+    }
+    ltot = (uint32_t)lsum;
+  }
+  __syncthreads();
+  if (!s_bad) {  // Any: the count of values (the len value at its ordinal)
+    bool bad = false;
+    for (uint32_t k = t; k < npay; k += MR_T) {
+      const uint32_t kl = pkl[k];
+      if ((kl & 7) != PK_ANY) continue;
+      const uint32_t v = mr_len_at(lent, nle, ltot, kl >> 3);
+      bad |= v == NONE || v == 0 || v >= (1u << 28);
+      pkl[k] = (v << 3) | PK_ANY;
+    }
+    if (bad) s_bad = 1;
+  }
+  if (t == 0) { w_p = M.r0; w_s = 0; w_k = 0; w_i = 0; w_send = 0; w_insec = 0; w_rt = 0; w_kind = 0; w_done = 0; }
+  __syncthreads();
+  // ---- C: the walk, window by window
+  const uint32_t nsec = M.nsec;
+  while (!s_bad && !w_done) {
+    const uint32_t p0 = w_p, k0 = w_k;
+    const uint32_t wb = p0 & ~15u;
+    const uint32_t wl = wb + MR_W + MR_MARG < len ? wb + MR_W + MR_MARG : len;  // window bytes [wb, wl)
+    const uint32_t lim = wl - wb;
+    for (uint32_t q = 16 * t; q < lim; q += 16 * MR_T) {
+      const uint4 v = wds::load16m(D, wb + q, len);
+      uint8_t tb16[16];
+      __builtin_memcpy(tb16, &v, 16);
+      __builtin_memcpy(win + q, tb16, 16);
+    }
+    for (uint32_t k = t; k < MR_PC; k += MR_T)
+      if (k0 + k < npay) { sidx[k] = pidx[k0 + k]; skl[k] = pkl[k0 + k]; }
+    __syncthreads();
+    // token lengths at every offset the walk may start a token at (first MR_W bytes of the window)
+    const uint32_t wn = lim < MR_W ? lim : MR_W;
+    for (uint32_t o = t; o < wn; o += MR_T) {
+      const uint32_t lv = mr_tok_len(win, o, lim, PK_SKIP), lb = mr_tok_len(win, o, lim, PK_BIN), la = mr_tok_len(win, o, lim, PK_ONE);
+      tV[o] = (uint16_t)(lv < 65536 ? lv : 0);
+      tB[o] = (uint16_t)(lb < 65536 ? lb : 0);
+      tA[o] = (uint16_t)(la < 65536 ? la : 0);
+    }
+    __syncthreads();
+    if (t == 0) {
+      uint32_t p = p0, s = w_s, k = w_k, i = w_i, send = w_send, insec = w_insec, rt = w_rt, kind = w_kind;
+      bool bad = false, done = false;
+      const uint32_t wend = wb + wn;  // tokens starting before here use the tables
+      while (!bad) {
+        if (rt > 0) {  // inside a payload struct: its next token
+          if (p >= wend) { bad = wend >= len; break; }  // (next window; past the document's end: truncated)
+          const uint32_t o = p - wb;
+          uint32_t L = kind == PK_SKIP ? tV[o] : kind == PK_BIN ? tB[o] : tA[o];
+          if (L == 0) {
+            const uint32_t e = mr_tok_slow(D, p, len, kind == PK_ANY ? PK_ONE : kind);
+            if (e == NONE) { bad = true; break; }
+            L = e - p;
+          }
+          p += L;
+          rt--;
+          continue;
+        }
+        if (!insec) {  // a section header: vu(#structs) vu(first clock)
+          if (s == nsec) { done = true; break; }
+          if (p >= wend) { bad = wend >= len; break; }
+          ln::LCur c = p + 16 <= wl ? ln::make(win, p - wb, lim) : ln::make(D, p, len);
+          const uint32_t W = ln::rvu(c), clock = ln::rvu(c);
+          const uint32_t pe = (p + 16 <= wl ? wb : 0) + c.p;
+          bad |= c.bad || W == 0 || W > (1u << 26);
+          if (bad) break;
+          S[s].S = i;
+          S[s].W = W;
+          S[s].clock = clock;
+          S[s].pay0 = pe;
+          S[s].ibase = k;
+          p = pe;
+          send = i + W;
+          bad |= send > (1u << 26);
+          insec = 1;
+          continue;
+        }
+        // the next payload struct, if it belongs to this section
+        uint32_t nidx, nkl;
+        if (k < npay) {
+          if (k - k0 >= MR_PC) break;  // the staged payload list is used up: next window
+          nidx = sidx[k - k0];
+          nkl = skl[k - k0];
+        } else if (fin && fin_pk != PK_NONE) {  // the endless final run
+          const uint64_t x = fin_i + (k - fin_k);
+          nidx = x < 0xffffffffull ? (uint32_t)x : NONE;
+          nkl = fin_pk;
+          if (fin_pk == PK_ANY) {
+            const uint32_t v = mr_len_at(lent, nle, ltot, fin_l + (k - fin_k));
+            if (v == NONE || v == 0 || v >= (1u << 28)) { if (nidx < send) { bad = true; break; } }
+            nkl = (v << 3) | PK_ANY;
+          }
+        } else {
+          nidx = NONE;
+          nkl = 0;
+        }
+        if (nidx >= send) {  // the section is complete
+          S[s].pay1 = p;
+          i = send;
+          s++;
+          insec = 0;
+          continue;
+        }
+        if (k >= icap) { bad = true; break; }
+        ist[k] = p;
+        k++;
+        kind = nkl & 7;
+        rt = kind == PK_ANY ? nkl >> 3 : 1;
+      }
+      if (done && !fin && (uint64_t)i > nstr) bad = true;  // the info column has fewer structs than the sections
+      w_p = p; w_s = s; w_k = k; w_i = i; w_send = send; w_insec = insec; w_rt = rt; w_kind = kind;
+      w_done = done;
+      if (bad) s_bad = 1;
+      if (done) { M.n = i; M.nitem = k; M.ds0 = p; }
+    }
+    __syncthreads();
+  }
+  if (t == 0 && s_bad) { M.ok = 0; M.why = 50; }
+}
+
 __global__ void k_ms_sizes_k(Job J, uint64_t *sizes) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= J.j.n) return;
@@ -1098,7 +1480,12 @@ __global__ void __launch_bounds__(64) k_ms_out(Job J) {
 }
 
 // ---- host launchers (pv2_run, ym_pv2.hip) -------------------------------------------------------------------
-void ms_rest(const Job &J, hipStream_t st) { k_ms_rest<<<J.j.n, 64, 0, st>>>(J); }
+void ms_rest(const Job &J, hipStream_t st) {
+  static int old = -1;
+  if (old < 0) { const char *e = getenv("YMERGE_MS_REST_SERIAL"); old = e && atoi(e) == 1; }
+  if (old) k_ms_rest<<<J.j.n, 64, 0, st>>>(J);
+  else k_ms_rest2<<<J.j.n, MR_T, 0, st>>>(J);
+}
 void ms_sizes(const Job &J, uint64_t *sizes, hipStream_t st) { k_ms_sizes_k<<<(J.j.n + 255) / 256, 256, 0, st>>>(J, sizes); }
 void ms_run(uint32_t op, const Job &J, hipStream_t st) {
   const uint32_t n = J.j.n;
