@@ -177,7 +177,11 @@ def secondary(dev, eng):
              ("merge_c2r_v1", "merge", "c2r_v1", 10000), ("merge_c2r_v2", "merge", "c2r_v2", 10000),
              ("merge_c4r_v1", "merge", "c4r_v1", 10000), ("merge_c4r_v2", "merge", "c4r_v2", 10000),
              ("diff_c2r_v1", "diff", "c2r_v1", 4096), ("diff_c2r_v2", "diff", "c2r_v2", 4096),
-             ("sv_c4r_v1", "sv", "c4r_v1", 4096), ("diff_c4r_v2", "diff", "c4r_v2", 4096)]
+             ("sv_c4r_v1", "sv", "c4r_v1", 4096), ("diff_c4r_v2", "diff", "c4r_v2", 4096),
+             # the sync server's SyncStep1 -> SyncStep2 load: diffUpdate / state vector of
+             # the merged C2 documents (~1 KB each) against random state vectors
+             ("diff_c2_v1", "diff", "c2_v1", 10000), ("sv_c2_v1", "sv", "c2_v1", 10000),
+             ("diff_c2_v2", "diff", "c2_v2", 10000), ("sv_c2_v2", "sv", "c2_v2", 10000)]
     for name, op, wl, n in cases:
         if only and name not in only.split(","):
             continue
@@ -225,7 +229,7 @@ def _secondary_case(dev, eng, name, op, wl, n):
                 fmt = 2
             docs = [[blobs[u] for u in range(int(d[t]), int(d[t + 1]))] for t in range(len(d) - 1)]
             a, o, d = replicate(*pack_docs(docs), n)
-        elif wl.startswith("c5") or wl[:3] in ("c2r", "c4r"):
+        elif wl.startswith("c5") or wl[:3] in ("c2r", "c4r") or (op in ("diff", "sv") and wl[:2] in ("c2", "c4")):
             # the merged documents (merged here by the engine), random per-client state vectors
             ma, mo, ml, _ = eng.run_host("merge", fmt, a, o, d)
             ups = [ma[int(mo[i]):int(mo[i]) + int(ml[i])].tobytes() for i in range(len(d) - 1)]

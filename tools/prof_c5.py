@@ -64,8 +64,11 @@ for fmt in [int(x) for x in os.environ.get("FMTS", "2,1").split(",")]:
                 names = "sv hdr desc stage search consume cut ds alloc write patch".split()
                 per = 1e-2 / (len(docs) * 6)  # us per document per call (6 calls incl. the checked one)
                 print("   k_pw_stitch us/doc: " + " ".join("%s %.0f" % (n, tk[i] * per) for i, n in enumerate(names)), flush=True)
-        eng.lib.ym__ms_prof(pr, 1)
-        print("   k_ms_rest: ticks %d info entries %d len entries %d rest fast %d rest cursor %d window loads %d global %d" % tuple(pr[:7]))
+        pm = (ctypes.c_ulonglong * 16)()
+        eng.lib.ym__ms_prof(pm, 1)
+        print("   k_ms_rest/k_ms_walk (ticks of 10 ns, summed over documents and calls): columns %d, walk kernel %d (serial %d, "
+              "tables %d), windows %d, tokens %d (walker-parsed %d), headers %d (global %d), final-run structs %d, len cursor "
+              "moves %d" % (pm[0], pm[1], pm[2], pm[7], pm[3], pm[4], pm[5], pm[6], pm[9], pm[8], pm[10]))
         for i in bad[:2]:
             got = res[0][int(res[1][i]):int(res[1][i]) + int(res[2][i])].tobytes()
             want = outs[i]

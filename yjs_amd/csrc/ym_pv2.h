@@ -44,6 +44,10 @@ struct Meta {
   uint32_t clock0;            // single section: the section's first clock
   uint32_t ds0;               // delete set start (rest stream)
   uint32_t nitem;             // multi-section: structs with rest payloads (Skip / Binary / Embed / Format / Any)
+  // multi-section rest walk, column passes -> walk: payload list length, counted structs, token kinds present,
+  // the info column's endless final entry (value, payload kind, first struct / payload / len ordinal), len entries
+  uint32_t mr_npay, mr_kinds, mr_fin, mr_finpk, mr_fink, mr_finl, mr_nle, mr_ltot;
+  uint64_t mr_nstr, mr_fini;
   uint64_t soff;              // scratch offset (value arrays, checkpoints, column outputs)
   uint64_t soff1;             // multi-section: section table + payload starts
   uint64_t o_tr, o_sl, o_ln, o_cl, o_ck, o_col[NK];  // scratch layout (relative to soff)

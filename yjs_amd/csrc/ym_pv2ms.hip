@@ -9,10 +9,10 @@
 // of every section (13.5.16 diffUpdateV2 us@40707; reference writeClientsStructs encoding.js:94-116 cuts
 // each client at the state vector), so every column is rebuilt from ~1,000 kept value ranges.
 //
-//  MR  k_ms_rest    one wave per document: the rest walk -- section headers, and the payload start of every
-//                   struct that has one, found by walking the info / len columns run by run (a run of
-//                   String / Type structs costs one step) and skipping payloads with the canonical `any`
-//                   checker (ym_lane.h any_canon).  Counts the structs, so the value arrays can be sized.
+//  MR  k_ms_rest    one block per document: the rest walk -- section headers, and the payload start of every
+//                   struct that has one: the info / len columns are tokenised block-parallel into the list of
+//                   payload structs, then one thread follows the rest stream's tokens through per-window
+//                   token-length tables.  Counts the structs, so the value arrays can be sized.
 //  K1  k_v2_decw    (ym_pv2.hip) every column decoded wave-parallel, as for one section.
 //  K2  k_ms_struct  one 256-thread block per document, two passes of block prefix sums over the structs:
 //                   pass 1 gives each section's column indices, clock and body offsets, its client (the
@@ -41,235 +41,17 @@
 namespace ymk {
 namespace pv2 {
 
-// debugging aid (ym__ms_prof): [0] rest-walk ticks (100 MHz), [1] info entries, [2] len entries, [3] rest
-// items on the fast path, [4] rest items parsed by the cursor, [5] window loads, [6] global re-reads
-__device__ unsigned long long ms_prof[8];
+// debugging aid (ym__ms_prof), the rest walk (ticks of the 100 MHz s_memrealtime, summed over documents):
+// [0] column passes A + B, [1] phase C, [2] C's serial walk, [3] windows, [4] tokens from the tables,
+// [5] tokens parsed by the walker itself, [6] section headers, [7] C's table computation
+__device__ unsigned long long ms_prof[16];
 #define MSP(i, v) do { if (threadIdx.x == 0) atomicAdd(&ms_prof[i], (unsigned long long)(v)); } while (0)
 
 // ---- MR: the rest walk ---------------------------------------------------------------------------------
-// UintOptRleDecoder over the len column: the next value / skip t values, run by run
-__device__ __forceinline__ uint32_t uopt_next(ln::LCur &c, uint32_t &v, uint32_t &rem, bool &bad) {
-  if (rem == 0) {
-    if (c.p >= c.e) { bad = true; return 0; }
-    bool neg;
-    v = rvi(c, neg);
-    rem = neg ? ln::rvu(c) + 2 : 1;
-    bad |= c.bad || rem == 0;
-  }
-  rem--;
-  return v;
-}
-__device__ __forceinline__ void uopt_skipn(ln::LCur &c, uint32_t &v, uint32_t &rem, uint32_t t, bool &bad) {
-  while (t > 0 && !bad) {
-    if (rem == 0) {
-      if (c.p >= c.e) { bad = true; return; }
-      bool neg;
-      v = rvi(c, neg);
-      rem = neg ? ln::rvu(c) + 2 : 1;
-      bad |= c.bad || rem == 0;
-    }
-    const uint32_t k = rem < t ? rem : t;
-    rem -= k;
-    t -= k;
-  }
-}
-
-// The walk is sequential, so its cost is the latency of each dependent read: the three streams (info
-// column, len column, rest stream) are read through LDS windows that the wave refills with 16-byte loads
-// (one refill per window, instead of one dependent HBM load per 8 bytes consumed); a value that does not
-// fit in the rest of a window is re-read from global memory.
-constexpr uint32_t WI = 1024, WL = 1024, WR = 4096, MRG = 1024;  // window bytes; rest margin per item
-struct Win {
-  uint32_t base, lim, end;  // LDS holds stream bytes [base, lim); the stream ends at end
-};
-// makes [pos, pos + need) resident (or up to the stream end); the whole wave calls it.  (The buffer is
-// passed as the __shared__ array itself, so its reads are LDS reads: generic-pointer loads would also wait
-// for the walk's outstanding global stores.)
-template <uint32_t N>
-__device__ __forceinline__ void win_at(Win &w, uint8_t (&buf)[N], const uint8_t *D, uint32_t pos, uint32_t need, uint32_t W) {
-  if (pos >= w.base && (pos + need <= w.lim || w.lim >= w.end)) return;
-  const uint32_t b = pos & ~15u;
-  const uint32_t l = b + W < w.end ? b + W : w.end;
-  MSP(5, 1);
-  __syncthreads();
-  for (uint32_t q = threadIdx.x * 16; q < l - b; q += 64 * 16) {
-    uint8_t t[16];
-    const uint4 v = wds::load16m(D, b + q, w.end);  // (bytes past the end read as 0x80)
-    __builtin_memcpy(t, &v, 16);
-    __builtin_memcpy(buf + q, t, 16);
-  }
-  __syncthreads();
-  w.base = b;
-  w.lim = l;
-}
-// a cursor over the window at pos (reads stop at the window's end: a value crossing it sets bad)
-__device__ __forceinline__ ln::LCur win_cur(const Win &w, const uint8_t *buf, uint32_t pos) { return ln::make(buf, pos - w.base, w.lim - w.base); }
-
-__global__ void __launch_bounds__(64) k_ms_rest(Job J) {
-  const GeneralJob &j = J.j;
-  const uint32_t d = blockIdx.x;
-  Meta &M = J.meta[d];
-  if (!M.ok || !M.ms) return;
-  __shared__ __attribute__((aligned(16))) uint8_t bi[WI + 32], bl[WL + 32], br[WR + 32];
-  const uint32_t u0 = j.doc_upd[d];
-  const uint64_t ub = j.upd_off[u0];
-  const uint32_t len = (uint32_t)(j.upd_off[u0 + 1] - ub);
-  const uint8_t *D = j.A + ub;
-  Sec *S = a_sec(J, M);
-  uint32_t *ist = a_istart(J, M);
-  const uint32_t icap = len - M.r0 + 1;
-  const bool w = threadIdx.x == 0;
-  Win wi{1, 0, M.col1[4]}, wl{1, 0, M.col1[8]}, wr{1, 0, len};
-  uint32_t ip = M.col0[4], lp = M.col0[8], rp = M.r0;  // stream positions (update-relative)
-  uint32_t iv = 0, irem = 0;  // info run value, values left (NONE: the endless final run)
-  uint32_t lv = 0, lrem = 0;  // len run
-  uint32_t i = 0, iord = 0;
-  bool bad = false;
-  const uint64_t tm0 = __builtin_amdgcn_s_memrealtime();
-  uint32_t n_ie = 0, n_le = 0, n_rf = 0, n_rs = 0, n_g = 0;
-  // the next len value (UintOptRleDecoder), or skip t of them
-  auto ln_take = [&](uint32_t t) -> uint32_t {
-    uint32_t v = 0;
-    while (t > 0 && !bad) {
-      if (lrem == 0) {
-        if (lp >= wl.end) { bad = true; break; }
-        win_at(wl, bl, D, lp, 16, WL);
-        n_le++;
-        const uint32_t b0 = bl[lp - wl.base], b1 = bl[lp - wl.base + 1];
-        if (b0 < 0x40 && lp + 1 <= wl.end) {  // one-byte value, count 1 (the common entry)
-          lv = b0;
-          lrem = 1;
-          lp += 1;
-        } else if (b0 < 0x80 && b1 < 0x80 && lp + 2 <= wl.end) {  // a run: -value (-0 too), count - 2
-          lv = b0 & 63;
-          lrem = b1 + 2;
-          lp += 2;
-        } else {
-          ln::LCur c = win_cur(wl, bl, lp);
-          bool neg;
-          lv = rvi(c, neg);
-          lrem = neg ? ln::rvu(c) + 2 : 1;
-          bad |= c.bad || lrem == 0;
-          lp = wl.base + c.p;
-        }
-      }
-      const uint32_t k = lrem < t ? lrem : t;
-      lrem -= k;
-      t -= k;
-      v = lv;
-    }
-    return v;
-  };
-  // one rest-stream item of kind k (0: section header, 1: Skip length, 2: varUint8Array, 3: one `any`) on
-  // the window, or again on global memory when it crosses the window's end; a / b: the header's values
-  uint32_t ha = 0, hb = 0;
-  auto parse = [&](ln::LCur &c, uint32_t k) {
-    if (k == 0) { ha = ln::rvu(c); hb = ln::rvu(c); }
-    else if (k == 1) c.bad |= ln::rvu(c) == 0;
-    else if (k == 2) { const uint32_t nb = ln::rvu(c); if (c.bad || !ln::room(c, nb)) c.bad = true; else ln::skip(c, nb); }
-    else ln::any_canon(c);
-  };
-  auto rest_item = [&](uint32_t k) {
-    win_at(wr, br, D, rp, MRG, WR);
-    // the common cases straight from the window: one-byte header values / lengths; `any` true / false /
-    // null / undefined and short ASCII strings (lib0 writes those canonically by construction)
-    const uint32_t qo = rp - wr.base;
-    const uint32_t t0 = br[qo], t1 = br[qo + 1];
-    if (rp + 2 <= wr.lim) {
-      if (k == 0 && t0 < 0x80 && t1 < 0x80) { ha = t0; hb = t1; rp += 2; n_rf++; return; }
-      if (k == 1 && t0 < 0x80 && t0 != 0) { rp += 1; n_rf++; return; }
-      if (k == 3 && (t0 == 120 || t0 == 121 || t0 == 126 || t0 == 127)) { rp += 1; n_rf++; return; }
-      if (k == 3 && t0 == 119 && t1 < 0x80 && rp + 2 + t1 <= wr.lim) {
-        uint32_t hi = 0;
-        for (uint32_t a = 0; a < t1; a++) hi |= br[qo + 2 + a];
-        if (hi < 0x80) { rp += 2 + t1; n_rf++; return; }
-      }
-    }
-    n_rs++;
-    ln::LCur c = win_cur(wr, br, rp);
-    parse(c, k);
-    if (!c.bad) { rp = wr.base + c.p; return; }
-    if (wr.lim >= wr.end) { bad = true; return; }
-    n_g++;
-    ln::LCur g = ln::make(D, rp, len);
-    parse(g, k);
-    bad |= g.bad;
-    rp = g.p;
-  };
-  for (uint32_t s = 0; s < M.nsec && !bad; s++) {
-    rest_item(0);
-    const uint32_t W = ha, clock = hb;
-    bad |= W == 0 || W > (1u << 26);  // (an empty section still consumes a client value: declined)
-    if (w) {
-      S[s].S = i;
-      S[s].W = W;
-      S[s].clock = clock;
-      S[s].pay0 = rp;
-      S[s].ibase = iord;
-    }
-    uint32_t rem = bad ? 0 : W;
-    while (rem > 0 && !bad) {
-      if (irem == 0) {
-        if (ip >= wi.end) { bad = true; break; }
-        win_at(wi, bi, D, ip, 16, WI);
-        n_ie++;
-        const uint32_t b1 = bi[ip - wi.base + 1];
-        iv = bi[ip - wi.base];
-        if (ip + 1 >= wi.end) {  // the final run never ends
-          irem = NONE;
-          ip += 1;
-        } else if (b1 < 0x80 && ip + 2 <= wi.end) {  // one-byte count (the common entry)
-          irem = b1 + 1;
-          ip += 2;
-        } else {
-          ln::LCur c = win_cur(wi, bi, ip + 1);
-          irem = ln::rvu(c) + 1;
-          bad |= c.bad || irem == 0;
-          ip = wi.base + c.p;
-        }
-      }
-      const uint32_t t = irem < rem ? irem : rem;
-      const uint32_t ref = iv & 31;
-      if (iv == 10 || ref == 3 || ref == 5 || ref == 6 || ref == 8) {  // payloads, struct by struct
-        for (uint32_t q = 0; q < t && !bad; q++) {
-          if (iord >= icap) { bad = true; break; }
-          if (w) ist[iord] = rp;
-          iord++;
-          // Skip: vu(length); ContentBinary: varUint8Array; ContentAny: len column, then that many values;
-          // ContentEmbed / ContentFormat: writeJSON = writeAny
-          const uint32_t cnt = ref == 8 ? ln_take(1) : 1;
-          bad |= cnt == 0;
-          const uint32_t k = iv == 10 ? 1 : ref == 3 ? 2 : 3;
-          for (uint32_t a = 0; a < cnt && !bad; a++) rest_item(k);
-        }
-      } else if (ref == 0) {                      // GC (info exactly 0, as GC.write writes it): len column
-        bad |= iv != 0;
-        ln_take(t);
-      } else if (ref == 1) {                      // ContentDeleted: len column
-        ln_take(t);
-      } else if (ref != 4 && ref != 7) {          // (String / Type: columns only) JSON, Doc, invalid refs
-        bad = true;
-      }
-      i += t;
-      rem -= t;
-      if (irem != NONE) irem -= t;
-      bad |= i > (1u << 26);
-    }
-    if (w) S[s].pay1 = rp;
-  }
-  if (w) {
-    M.n = i;
-    M.nitem = iord;
-    M.ds0 = rp;
-    if (bad) { M.ok = 0; M.why = 50; }
-  }
-  MSP(0, __builtin_amdgcn_s_memrealtime() - tm0);
-  MSP(1, n_ie); MSP(2, n_le); MSP(3, n_rf); MSP(4, n_rs); MSP(6, n_g);
-}
-
-// ---- MR, block-parallel (k_ms_rest2): the walk's sequential chain reduced to the rest stream's tokens ----
-// The serial walk above spends most of its steps on the info column (C5: ~55 k run entries per document,
-// 0.6 us each on one wave) although only the rest stream is sequential.  Here one 256-thread block per
+// ---- MR: the rest walk, block-parallel where it can be ---------------------------------------------------
+// A walk of the rest stream alone is sequential (each section header's position depends on every payload
+// before it), but most of what a struct-by-struct walk does is not: round 3's one-wave walk spent its steps
+// on the info column (C5: ~55 k run entries per document, 0.6 us each).  Here one 256-thread block per
 // document:
 //  A  tokenises the info column 4 KB per block step (the RLE<u8> automaton of K1, composed across the
 //     block) and writes the PAYLOAD LIST: every struct that has rest tokens (Skip: a varuint, Binary: a
@@ -282,9 +64,14 @@ __global__ void __launch_bounds__(64) k_ms_rest(Job J) {
 //     would have there (0: not decidable from the window, or invalid -- the walker then parses that token
 //     itself), so each step of the chain is a table lookup: a section header (two varuints, parsed), then
 //     the tokens of the payload structs up to the section's end (payload list, staged into LDS per window).
-// Outputs are those of k_ms_rest: the section table (first struct, structs, clock, payload span, payload
+// Outputs: the section table (first struct, structs, clock, payload span, payload
 // ordinal), every payload struct's rest position, the struct and payload counts, the delete set's start.
 constexpr uint32_t MR_T = 256, MR_W = 4096, MR_MARG = 256, MR_PC = 1024;
+// a store to global memory through an address-space-1 pointer: the walker's stores through generic pointers
+// (flat stores) counted against the LDS counter too, so each next table read waited for the previous
+// store's round trip to HBM (~0.9 us per token)
+template <class T>
+__device__ __forceinline__ void gst(T *p, T v) { *(__attribute__((address_space(1))) T *)p = v; }
 // per-thread 16-byte slice transition of the RLE<u8> / UintOptRle automaton (K1's tstep), packed 2 bits per state
 __device__ __forceinline__ uint32_t mr_slice_f(const uint8_t (&b)[16], uint32_t q, uint32_t c1, bool rle, uint32_t fb) {
   uint32_t s0 = 0, s1 = 1, s2 = 2, s3 = 3;
@@ -360,6 +147,19 @@ __device__ __forceinline__ uint32_t mr_tok_len(const uint8_t *w, uint32_t o, uin
   ln::any_scalar(c);
   return c.bad ? 0 : c.p - o;
 }
+// lib0 readVarUint (canonical, u32) at o of the LDS window w (bytes [0, lim)), advancing o
+template <uint32_t N>
+__device__ __forceinline__ uint32_t mr_vu(const uint8_t (&w)[N], uint32_t &o, uint32_t lim, bool &bad) {
+  uint32_t v = 0, nb = 0, x = 0x80;
+  while ((x & 0x80) && nb < 5) {
+    x = o + nb < lim ? w[o + nb] : 0x80;
+    v |= (x & 0x7f) << (7 * nb);
+    nb++;
+  }
+  bad |= (x & 0x80) || (nb > 1 && x == 0) || (nb == 5 && (x & 0x70) != 0);
+  o += nb;
+  return v;
+}
 // the token of kind k at p, parsed from the document (the walker's slow path); NONE: invalid
 __device__ __noinline__ uint32_t mr_tok_slow(const uint8_t *D, uint32_t p, uint32_t len, uint32_t k) {
   ln::LCur c = ln::make(D, p, len);
@@ -379,19 +179,14 @@ __device__ __forceinline__ uint32_t mr_len_at(const uint2 *le, uint32_t nle, uin
   return le[lo].y;
 }
 
-__global__ void __launch_bounds__(MR_T) k_ms_rest2(Job J) {
+__global__ void __launch_bounds__(MR_T) k_ms_rest(Job J) {
   const GeneralJob &j = J.j;
   const uint32_t d = blockIdx.x, t = threadIdx.x;
   Meta &M = J.meta[d];
-  if (!M.ok || !M.ms) return;
-  __shared__ __attribute__((aligned(16))) uint8_t win[MR_W + MR_MARG + 16];
-  __shared__ uint16_t tV[MR_W], tB[MR_W], tA[MR_W];
-  __shared__ uint32_t sidx[MR_PC], skl[MR_PC];
+  if (__builtin_amdgcn_readfirstlane((int)M.ok) == 0 || __builtin_amdgcn_readfirstlane((int)M.ms) == 0) return;
   __shared__ uint32_t shf[MR_T / 64], shs[3 * (MR_T / 64)];
   __shared__ uint64_t sh64[MR_T / 64];
   __shared__ uint32_t s_bad;
-  // walker state (thread 0 writes, the block reads at window boundaries)
-  __shared__ uint32_t w_p, w_s, w_k, w_i, w_send, w_insec, w_rt, w_kind, w_done;
   const uint32_t u0 = j.doc_upd[d];
   const uint64_t ub = j.upd_off[u0];
   const uint32_t len = (uint32_t)(j.upd_off[u0 + 1] - ub);
@@ -401,6 +196,7 @@ __global__ void __launch_bounds__(MR_T) k_ms_rest2(Job J) {
   uint2 *lent = a_lent(J, M, len);
   const uint32_t icap = ms_icap(len, M.r0);
   if (t == 0) s_bad = 0;
+  const uint64_t tm0 = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
   // ---- A: info column -> payload list
   uint64_t nstr = 0;        // structs of the counted entries
@@ -465,7 +261,7 @@ __global__ void __launch_bounds__(MR_T) k_ms_rest2(Job J) {
       st = (tot >> (2 * st)) & 3;
       nstr += tta; npay += tb; nlc += tc;
       __syncthreads();
-      if (s_bad) break;
+      if (__builtin_amdgcn_readfirstlane((int)s_bad)) break;
     }
   }
   // the final entry's values to every thread
@@ -484,7 +280,7 @@ __global__ void __launch_bounds__(MR_T) k_ms_rest2(Job J) {
   }
   // ---- B: len column entries; the Any structs' value counts
   uint32_t nle = 0, ltot = 0;
-  if (!s_bad) {
+  if (!__builtin_amdgcn_readfirstlane((int)s_bad)) {
     const uint32_t c0 = M.col0[8], c1 = M.col1[8];
     uint32_t st = 0;
     uint64_t lsum = 0;
@@ -526,12 +322,12 @@ __global__ void __launch_bounds__(MR_T) k_ms_rest2(Job J) {
       lsum += tta;
       nle += tb;
       __syncthreads();
-      if (s_bad) break;
+      if (__builtin_amdgcn_readfirstlane((int)s_bad)) break;
     }
     ltot = (uint32_t)lsum;
   }
   __syncthreads();
-  if (!s_bad) {  // Any: the count of values (the len value at its ordinal)
+  if (!__builtin_amdgcn_readfirstlane((int)s_bad)) {  // Any: the count of values (the len value at its ordinal)
     bool bad = false;
     for (uint32_t k = t; k < npay; k += MR_T) {
       const uint32_t kl = pkl[k];
@@ -542,111 +338,209 @@ __global__ void __launch_bounds__(MR_T) k_ms_rest2(Job J) {
     }
     if (bad) s_bad = 1;
   }
-  if (t == 0) { w_p = M.r0; w_s = 0; w_k = 0; w_i = 0; w_send = 0; w_insec = 0; w_rt = 0; w_kind = 0; w_done = 0; }
   __syncthreads();
-  // ---- C: the walk, window by window
-  const uint32_t nsec = M.nsec;
-  while (!s_bad && !w_done) {
-    const uint32_t p0 = w_p, k0 = w_k;
-    const uint32_t wb = p0 & ~15u;
+  // which token kinds the document has (tables are computed for those only): Skip / Binary / any
+  __shared__ uint32_t s_kinds;
+  if (t == 0) s_kinds = fin ? 1u << fin_pk : 0;
+  __syncthreads();
+  {
+    uint32_t m = 0;
+    for (uint32_t k = t; k < npay; k += MR_T) m |= 1u << (pkl[k] & 7);
+    if (m) atomicOr(&s_kinds, m);
+  }
+  __syncthreads();
+  if (t == 0) {
+    if (s_bad) { M.ok = 0; M.why = 50; }
+    M.mr_npay = npay; M.mr_kinds = s_kinds; M.mr_fin = fin; M.mr_finpk = fin_pk; M.mr_fink = fin_k; M.mr_finl = fin_l;
+    M.mr_nle = nle; M.mr_ltot = ltot; M.mr_nstr = nstr; M.mr_fini = fin_i;
+  }
+  MSP(0, __builtin_amdgcn_s_memrealtime() - tm0);
+}
+
+// ---- MR, the walk: one wave per document, in lockstep -----------------------------------------------------
+// Every lane computes the same values (LDS reads made uniform by readfirstlane), so the chain's state stays in
+// scalar registers and its branches are uniform; the wave computes each window's token-length tables
+// (64 offsets per lane), then follows the chain: a section header (two varuints), then the tokens of the
+// payload structs up to the section's end, each one table lookup.
+__global__ void __launch_bounds__(64) k_ms_walk(Job J) {
+  const GeneralJob &j = J.j;
+  const uint32_t d = blockIdx.x, t = threadIdx.x;
+  Meta &M = J.meta[d];
+  auto U = [](uint32_t x) -> uint32_t { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
+  if (U(M.ok) == 0 || U(M.ms) == 0) return;
+  __shared__ __attribute__((aligned(16))) uint8_t win[MR_W + MR_MARG + 16];
+  __shared__ uint16_t tV[MR_W], tB[MR_W], tA[MR_W];
+  __shared__ uint2 spay[MR_PC];     // the window's payload structs (index, kind | token count << 3)
+  __shared__ uint32_t sist[MR_PC];  // their first tokens' offsets (flushed to ist at the window's end)
+  const uint32_t u0 = j.doc_upd[d];
+  const uint64_t ub = j.upd_off[u0];
+  const uint32_t len = U((uint32_t)(j.upd_off[u0 + 1] - ub));
+  const uint8_t *D = j.A + ub;
+  Sec *S = a_sec(J, M);
+  uint32_t *ist = a_istart(J, M), *pidx = a_pidx(J, M, len), *pkl = a_pkl(J, M, len);
+  const uint2 *lent = a_lent(J, M, len);
+  const uint32_t icap = ms_icap(len, U(M.r0));
+  const uint32_t npay = U(M.mr_npay), kinds = U(M.mr_kinds), fin = U(M.mr_fin), fin_pk = U(M.mr_finpk);
+  const uint32_t fin_k = U(M.mr_fink), fin_l = U(M.mr_finl), nle = U(M.mr_nle), ltot = U(M.mr_ltot);
+  const uint64_t nstr = M.mr_nstr, fin_i = M.mr_fini;
+  const uint32_t nsec = U(M.nsec);
+  const bool need_v = kinds & (1u << PK_SKIP), need_b = kinds & (1u << PK_BIN);
+  const uint64_t tm0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t t_walk = 0, t_tab = 0;
+  uint32_t n_win = 0, n_tok = 0, n_slow = 0, n_hdr = 0, n_fin = 0, n_ghdr = 0, n_lc = 0;
+  // the len column's cursor for the endless final run: entry lc_e - 1 holds ordinals [lc_lo, lc_hi), value lc_v
+  uint32_t lc_e = 0, lc_lo = 1, lc_hi = 0, lc_v = NONE;
+  // the chain's state (uniform)
+  uint32_t p = U(M.r0), s = 0, k = 0, i = 0, send = 0, insec = 0, rt = 0, kind = 0;
+  bool bad = false, done = false;
+  uint32_t tab_wb = NONE;
+  uint32_t tab_wn = 0;
+  while (!bad && !done) {
+    // the window: the current one while p is inside its tables, else one starting at p
+    const uint32_t k0 = k, wb = tab_wb != NONE && p >= tab_wb && p < tab_wb + tab_wn ? tab_wb : p & ~15u;
     const uint32_t wl = wb + MR_W + MR_MARG < len ? wb + MR_W + MR_MARG : len;  // window bytes [wb, wl)
-    const uint32_t lim = wl - wb;
-    for (uint32_t q = 16 * t; q < lim; q += 16 * MR_T) {
-      const uint4 v = wds::load16m(D, wb + q, len);
-      uint8_t tb16[16];
-      __builtin_memcpy(tb16, &v, 16);
-      __builtin_memcpy(win + q, tb16, 16);
-    }
-    for (uint32_t k = t; k < MR_PC; k += MR_T)
-      if (k0 + k < npay) { sidx[k] = pidx[k0 + k]; skl[k] = pkl[k0 + k]; }
+    const uint32_t lim = wl - wb, wn = lim < MR_W ? lim : MR_W;
+    const bool fresh = wb != tab_wb;
+    const uint64_t tt0 = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
-    // token lengths at every offset the walk may start a token at (first MR_W bytes of the window)
-    const uint32_t wn = lim < MR_W ? lim : MR_W;
-    for (uint32_t o = t; o < wn; o += MR_T) {
-      const uint32_t lv = mr_tok_len(win, o, lim, PK_SKIP), lb = mr_tok_len(win, o, lim, PK_BIN), la = mr_tok_len(win, o, lim, PK_ONE);
-      tV[o] = (uint16_t)(lv < 65536 ? lv : 0);
-      tB[o] = (uint16_t)(lb < 65536 ? lb : 0);
-      tA[o] = (uint16_t)(la < 65536 ? la : 0);
+    if (fresh)
+      for (uint32_t q = 16 * t; q < lim; q += 16 * 64) {
+        const uint4 v = wds::load16m(D, wb + q, len);
+        uint8_t tb16[16];
+        __builtin_memcpy(tb16, &v, 16);
+        __builtin_memcpy(win + q, tb16, 16);
+      }
+    for (uint32_t q = t; q < MR_PC; q += 64)
+      if (k0 + q < npay) spay[q] = make_uint2(pidx[k0 + q], pkl[k0 + q]);
+    __syncthreads();
+    if (fresh) {
+      for (uint32_t o = t; o < wn; o += 64) {
+        const uint32_t la = mr_tok_len(win, o, lim, PK_ONE);
+        tA[o] = (uint16_t)(la < 65536 ? la : 0);
+        if (need_v) { const uint32_t lv = mr_tok_len(win, o, lim, PK_SKIP); tV[o] = (uint16_t)(lv < 65536 ? lv : 0); }
+        if (need_b) { const uint32_t lb = mr_tok_len(win, o, lim, PK_BIN); tB[o] = (uint16_t)(lb < 65536 ? lb : 0); }
+      }
+      tab_wb = wb;
+      tab_wn = wn;
     }
     __syncthreads();
-    if (t == 0) {
-      uint32_t p = p0, s = w_s, k = w_k, i = w_i, send = w_send, insec = w_insec, rt = w_rt, kind = w_kind;
-      bool bad = false, done = false;
-      const uint32_t wend = wb + wn;  // tokens starting before here use the tables
-      while (!bad) {
-        if (rt > 0) {  // inside a payload struct: its next token
-          if (p >= wend) { bad = wend >= len; break; }  // (next window; past the document's end: truncated)
-          const uint32_t o = p - wb;
-          uint32_t L = kind == PK_SKIP ? tV[o] : kind == PK_BIN ? tB[o] : tA[o];
-          if (L == 0) {
-            const uint32_t e = mr_tok_slow(D, p, len, kind == PK_ANY ? PK_ONE : kind);
-            if (e == NONE) { bad = true; break; }
-            L = e - p;
-          }
+    const uint64_t tt1 = __builtin_amdgcn_s_memrealtime();
+    t_tab += tt1 - tt0;
+    n_win++;
+    const uint32_t wend = wb + wn;  // tokens starting before here use the tables
+    for (;;) {
+      if (rt > 0) {  // inside a payload struct: its tokens
+        const uint16_t *tab = kind == PK_SKIP ? tV : kind == PK_BIN ? tB : tA;
+        const uint32_t rt0 = rt;
+        while (rt > 0 && p < wend) {
+          const uint32_t L = U(tab[p - wb]);
+          if (L == 0) break;
           p += L;
           rt--;
-          continue;
         }
-        if (!insec) {  // a section header: vu(#structs) vu(first clock)
-          if (s == nsec) { done = true; break; }
-          if (p >= wend) { bad = wend >= len; break; }
-          ln::LCur c = p + 16 <= wl ? ln::make(win, p - wb, lim) : ln::make(D, p, len);
-          const uint32_t W = ln::rvu(c), clock = ln::rvu(c);
-          const uint32_t pe = (p + 16 <= wl ? wb : 0) + c.p;
-          bad |= c.bad || W == 0 || W > (1u << 26);
-          if (bad) break;
-          S[s].S = i;
-          S[s].W = W;
-          S[s].clock = clock;
-          S[s].pay0 = pe;
-          S[s].ibase = k;
-          p = pe;
-          send = i + W;
-          bad |= send > (1u << 26);
-          insec = 1;
-          continue;
-        }
-        // the next payload struct, if it belongs to this section
-        uint32_t nidx, nkl;
-        if (k < npay) {
-          if (k - k0 >= MR_PC) break;  // the staged payload list is used up: next window
-          nidx = sidx[k - k0];
-          nkl = skl[k - k0];
-        } else if (fin && fin_pk != PK_NONE) {  // the endless final run
-          const uint64_t x = fin_i + (k - fin_k);
-          nidx = x < 0xffffffffull ? (uint32_t)x : NONE;
-          nkl = fin_pk;
-          if (fin_pk == PK_ANY) {
-            const uint32_t v = mr_len_at(lent, nle, ltot, fin_l + (k - fin_k));
-            if (v == NONE || v == 0 || v >= (1u << 28)) { if (nidx < send) { bad = true; break; } }
-            nkl = (v << 3) | PK_ANY;
-          }
-        } else {
-          nidx = NONE;
-          nkl = 0;
-        }
-        if (nidx >= send) {  // the section is complete
-          S[s].pay1 = p;
-          i = send;
-          s++;
-          insec = 0;
-          continue;
-        }
-        if (k >= icap) { bad = true; break; }
-        ist[k] = p;
-        k++;
-        kind = nkl & 7;
-        rt = kind == PK_ANY ? nkl >> 3 : 1;
+        n_tok += rt0 - rt;
+        if (rt == 0) continue;
+        if (p >= wend) { bad = wend >= len; break; }  // (next window; past the document's end: truncated)
+        const uint32_t e = U(mr_tok_slow(D, p, len, kind == PK_ANY ? PK_ONE : kind));  // (a token the table lacks)
+        if (e == NONE) { bad = true; break; }
+        n_slow++;
+        n_tok++;
+        p = e;
+        rt--;
+        continue;
       }
-      if (done && !fin && (uint64_t)i > nstr) bad = true;  // the info column has fewer structs than the sections
-      w_p = p; w_s = s; w_k = k; w_i = i; w_send = send; w_insec = insec; w_rt = rt; w_kind = kind;
-      w_done = done;
-      if (bad) s_bad = 1;
-      if (done) { M.n = i; M.nitem = k; M.ds0 = p; }
+      if (!insec) {  // a section header: vu(#structs) vu(first clock)
+        if (s == nsec) { done = true; break; }
+        if (p >= wend) { bad = wend >= len; break; }
+        n_hdr++;
+        uint32_t W, clock, pe;
+        bool hb = false;
+        if (p + 16 <= wl) {
+          uint32_t o = p - wb;
+          W = U(mr_vu(win, o, lim, hb));
+          clock = U(mr_vu(win, o, lim, hb));
+          pe = wb + U(o);
+        } else {
+          n_ghdr++;
+          ln::LCur c = ln::make(D, p, len);
+          W = U(ln::rvu(c));
+          clock = U(ln::rvu(c));
+          pe = U(c.p);
+          hb = c.bad;
+        }
+        if (U(hb ? 1u : 0u) != 0 || W == 0 || W > (1u << 26)) { bad = true; break; }
+        if (t == 0) {
+          gst(&S[s].S, i);
+          gst(&S[s].W, W);
+          gst(&S[s].clock, clock);
+          gst(&S[s].pay0, pe);
+          gst(&S[s].ibase, k);
+        }
+        p = pe;
+        send = i + W;
+        if (send > (1u << 26)) { bad = true; break; }
+        insec = 1;
+        continue;
+      }
+      // the next payload struct, if it belongs to this section
+      uint32_t nidx, nkl;
+      if (k - k0 >= MR_PC) break;  // the staged payload list (or the offsets' buffer) is used up: next window
+      if (k < npay) {
+        const uint2 e = spay[k - k0];
+        nidx = U(e.x);
+        nkl = U(e.y);
+      } else if (fin && fin_pk != PK_NONE) {  // the endless final run
+        const uint64_t x = fin_i + (k - fin_k);
+        nidx = x < 0xffffffffull ? (uint32_t)x : NONE;
+        nkl = fin_pk;
+        n_fin++;
+        if (fin_pk == PK_ANY) {  // (consecutive ordinals: the cursor moves to the next entry, else a search)
+          const uint32_t o = fin_l + (k - fin_k);
+          if (o < lc_lo || o >= lc_hi) {
+            n_lc++;
+            lc_v = NONE; lc_lo = 1; lc_hi = 0;
+            if (o < ltot && nle != 0) {
+              uint32_t e = lc_e;
+              if (!(e < nle && U(lent[e].x) <= o && (e + 1 == nle || U(lent[e + 1].x) > o))) {
+                uint32_t lo = 0, hi = nle;
+                while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (U(lent[mid].x) <= o) lo = mid; else hi = mid; }
+                e = lo;
+              }
+              lc_lo = U(lent[e].x); lc_v = U(lent[e].y); lc_hi = e + 1 < nle ? U(lent[e + 1].x) : ltot; lc_e = e + 1;
+            }
+          }
+          const uint32_t v = lc_v;
+          if (v == NONE || v == 0 || v >= (1u << 28)) { if (nidx < send) { bad = true; break; } }
+          nkl = (v << 3) | PK_ANY;
+        }
+      } else {
+        nidx = NONE;
+        nkl = 0;
+      }
+      if (nidx >= send) {  // the section is complete
+        if (t == 0) gst(&S[s].pay1, p);
+        i = send;
+        s++;
+        insec = 0;
+        continue;
+      }
+      if (k >= icap) { bad = true; break; }
+      if (t == 0) sist[k - k0] = p;
+      k++;
+      kind = nkl & 7;
+      rt = kind == PK_ANY ? nkl >> 3 : 1;
     }
+    t_walk += __builtin_amdgcn_s_memrealtime() - tt1;
     __syncthreads();
+    for (uint32_t q = t; q < k - k0; q += 64) ist[k0 + q] = sist[q];
   }
-  if (t == 0 && s_bad) { M.ok = 0; M.why = 50; }
+  if (done && !fin && (uint64_t)i > nstr) bad = true;  // the info column has fewer structs than the sections
+  if (t == 0) {
+    if (bad) { M.ok = 0; M.why = 50; }
+    else { M.n = i; M.nitem = k; M.ds0 = p; }
+  }
+  MSP(1, __builtin_amdgcn_s_memrealtime() - tm0); MSP(2, t_walk); MSP(3, n_win);
+  MSP(4, n_tok); MSP(5, n_slow); MSP(6, n_hdr); MSP(7, t_tab); MSP(8, n_fin); MSP(9, n_ghdr); MSP(10, n_lc);
 }
 
 __global__ void k_ms_sizes_k(Job J, uint64_t *sizes) {
@@ -1301,6 +1195,7 @@ __global__ void __launch_bounds__(64) k_ms_col(Job J) {
 __global__ void __launch_bounds__(64) k_ms_out(Job J) {
   const GeneralJob &j = J.j;
   const uint32_t lane = threadIdx.x;
+  __shared__ wds::DsLds dsl;
   for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
     Meta &M = J.meta[d];
     if (!M.ok || !M.ms) continue;
@@ -1311,11 +1206,13 @@ __global__ void __launch_bounds__(64) k_ms_out(Job J) {
     Sec *S = a_sec(J, M);
     const uint32_t *ist = a_istart(J, M);
     const uint32_t nsec = M.nsec;
-    // delete set: readDeleteSet's reads, canonical, no repeated or empty client (then copied)
-    uint32_t x = M.ds0;
-    bool bad = false;
-    uint32_t ndc;
-    {
+    // delete set: readDeleteSet's reads, canonical, no repeated or empty client (then copied); through the
+    // LDS token tables, or client by client when those cannot decide
+    uint32_t x = wds::ds_validate_lds(D, M.ds0, len, dsl);
+    bool bad = x == NONE;
+    uint32_t ndc = 0;
+    if (x == wds::DS_BIG) {
+      x = M.ds0;
       ln::LCur c = ln::make(D, x, len);
       ndc = ln::rvu(c);
       x = c.p;
@@ -1481,10 +1378,8 @@ __global__ void __launch_bounds__(64) k_ms_out(Job J) {
 
 // ---- host launchers (pv2_run, ym_pv2.hip) -------------------------------------------------------------------
 void ms_rest(const Job &J, hipStream_t st) {
-  static int old = -1;
-  if (old < 0) { const char *e = getenv("YMERGE_MS_REST_SERIAL"); old = e && atoi(e) == 1; }
-  if (old) k_ms_rest<<<J.j.n, 64, 0, st>>>(J);
-  else k_ms_rest2<<<J.j.n, MR_T, 0, st>>>(J);
+  k_ms_rest<<<J.j.n, MR_T, 0, st>>>(J);
+  k_ms_walk<<<J.j.n, 64, 0, st>>>(J);
 }
 void ms_sizes(const Job &J, uint64_t *sizes, hipStream_t st) { k_ms_sizes_k<<<(J.j.n + 255) / 256, 256, 0, st>>>(J, sizes); }
 void ms_run(uint32_t op, const Job &J, hipStream_t st) {
@@ -1504,7 +1399,7 @@ void ms_run(uint32_t op, const Job &J, hipStream_t st) {
 }  // namespace ymk
 
 extern "C" int ym__ms_prof(unsigned long long *host, int reset) {
-  int r = (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ymk::pv2::ms_prof), 64);
-  if (reset) { unsigned long long z[8] = {}; hipMemcpyToSymbol(HIP_SYMBOL(ymk::pv2::ms_prof), z, 64); }
+  int r = (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ymk::pv2::ms_prof), 128);
+  if (reset) { unsigned long long z[16] = {}; hipMemcpyToSymbol(HIP_SYMBOL(ymk::pv2::ms_prof), z, 128); }
   return r;
 }

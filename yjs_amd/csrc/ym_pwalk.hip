@@ -135,7 +135,7 @@ __global__ void k_pw_prep(GeneralJob j, uint32_t *cnt, uint8_t *done, uint64_t p
         c = (uint32_t)((len + CH - 1) / CH);
         ln::LCur h = ln::make(j.A + j.upd_off[u0], 0, (uint32_t)len);
         const uint32_t nsec = ln::rvu(h);
-        if (!h.bad && nsec >= ms_min && nsec <= (1u << 16)) a = ms_area(nsec);
+        if (!h.bad && nsec >= ms_min && nsec <= (1u << 16)) { a = ms_area(nsec); c = 0; }  // (the table walk: no chunks)
       }
     }
   }
@@ -800,24 +800,21 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
 }
 
 
-// ---- 3. multi-section documents, section-parallel (configs[4] C5: ~1,000 client sections) -------------
-// k_pw_stitch follows the chain one section after the other with one wave: a C5 document's ~1,000
-// sections cost ~10 dependent global loads each (header, state vector, descriptors, records, the cut),
-// ~28 ms per call although the whole chip is idle.  Here one 512-thread block per document:
-//   A  wave 0 walks only the section headers: from a section's first struct it skips its #structs
-//      along the walk's records (one descriptor lookup and one 64-record load per chunk), so each section
-//      costs ~3 dependent loads; the state vector goes into an LDS hash map meanwhile (wave 1).
-//   B  the eight waves take the sections round-robin: clocks, the cut, the sliced head, info-byte patches
-//      -- the stitch's per-section work, now eight (and across documents, 8 x 256) sections at a time.
-//   C  sizes by a block scan over the sections, then every wave writes its sections' pieces in place.
-//
-// Measured (C5 V1, 256 documents, tools/prof_c5.py): correct, but not faster than k_pw_stitch -- phase A alone
-// costs ~20 us per section (the records of one chunk are interleaved with 63 others for the walk's stores,
-// so a 64-record read touches 64 cache lines, and the first structs after a header are off the walk's chain
-// and parsed here), so the path is off by default (YMERGE_PWMS_MIN=<sections> turns it on; the golden
-// vectors run through it in tests/test_gpu_golden.py).
+// ---- 3. multi-section documents (configs[4] C5: ~1,000 client sections, ~30 k structs) -------------------
+// k_pw_stitch follows the chain one section after the other: a C5 section costs ~10 dependent global loads
+// (header, state vector, descriptors, records, the cut) plus ~5 structs re-parsed after its header, where
+// the walk's speculative chain lost step (round 3: ~25 us per section, 28 ms per call).  Here one 512-thread
+// block per document and no chunk walk:
+//   A+B  the chain through LDS windows of 4 KB: the block parses a struct at EVERY byte offset of the window
+//        (next position, clock length, Skip / patch flags: tables), then thread 0 follows the true chain --
+//        section headers parsed, each struct one table lookup -- and does the stitch's per-section work on
+//        the way: clocks, the state-vector entry, the cut and its sliced head, the info-byte patches.
+//   C    the delete set validated through LDS token tables (ym_wave_ds.h), sizes by a block scan over the
+//        sections, then every wave writes its sections' pieces in place.
+// The same documents are accepted, with the same bytes, as k_pw_stitch / k_big_v1 would (the golden vectors
+// run through this path with YMERGE_PWMS_MIN=2, tests/test_gpu_golden.py).
 constexpr uint32_t MS_WAVES = 8, MS_T = 64 * MS_WAVES;
-constexpr uint32_t MS_MIN = 0xffffffffu;  // sections from which a document takes this path (YMERGE_PWMS_MIN)
+constexpr uint32_t MS_MIN = 16;  // sections from which a document takes this path (YMERGE_PWMS_MIN)
 constexpr uint32_t MSPATCH = 4096;     // info-byte patches per document
 constexpr uint32_t MSVMAX = 2048, MSVSLOTS = 4096;
 enum { M_X0 = 0, M_W, M_CLIENT, M_CLOCK, M_X1, M_PRELEN, M_A0, M_A1, M_B0, M_WRITTEN, M_FCLOCK, M_VAL, M_END, M_OUT, NMF = 16 };
@@ -841,148 +838,238 @@ __device__ __forceinline__ MsDoc ms_doc(uint8_t *area, uint64_t off, uint32_t ns
 }
 #define msec(ci, f) M.sec[NMF * (ci) + (f)]
 
-// one wave's view of the chunk descriptors: 64 chunks [wb, wb + 64) held one per lane
-struct DescWin {
-  uint32_t wb = NONE - 64;
-  uint4 q0, q1, q2, q3, q4;
+// the walk's tables over one LDS window: per byte offset the struct a parse there would give (next
+// position, clock length, flags; TV: decided), computed by the whole block
+constexpr uint32_t TW = 4096, TMARG = 256;
+constexpr uint32_t TV = 0x80;
+struct TabLds {
+  uint8_t b[TW + TMARG + 16];
+  uint16_t nx[TW];
+  uint32_t len[TW];
+  uint8_t fl[TW];
 };
-__device__ __forceinline__ void desc_at(DescWin &W, const uint4 *desc, uint32_t cb, uint32_t nch, uint32_t cx) {
-  if (cx < W.wb || cx >= W.wb + 64) {
-    W.wb = cx;
-    if (W.wb + threadIdx.x % 64 < nch) {
-      const uint4 *Q = desc + 5ull * (cb + W.wb + threadIdx.x % 64);
-      W.q0 = Q[0]; W.q1 = Q[1]; W.q2 = Q[2]; W.q3 = Q[3]; W.q4 = Q[4];
-    }
+union MsLds {
+  TabLds tab;
+  wds::DsLds ds;
+};
+// lib0 readVarUint (canonical, u32) at o of the LDS bytes b (valid [0, lim)), advancing o
+__device__ __forceinline__ uint32_t tab_vu(const uint8_t *b, uint32_t &o, uint32_t lim, bool &bad) {
+  uint32_t v = 0, nb = 0, x = 0x80;
+  while ((x & 0x80) && nb < 5) {
+    x = o + nb < lim ? b[o + nb] : 0x80;
+    v |= (x & 0x7f) << (7 * nb);
+    nb++;
   }
-}
-// the record index of position x in chunk cx (a true struct start), or NONE: the descriptor's first
-// records, then a ballot over the records 64 at a time
-__device__ __forceinline__ uint32_t rec_entry(const DescWin &W, const uint32_t *recs, uint32_t gc, uint32_t cx, uint32_t nrec, uint32_t x) {
-  const int di = (int)(cx - W.wb);
-#pragma unroll
-  for (uint32_t kf = 0; kf < NFIRST; kf++) {
-    const uint32_t pwk = lane_read(kf < 4 ? (&W.q1.x)[kf] : (&W.q2.x)[kf - 4], di);
-    if (kf < nrec && (pwk & POS_MASK) == x) return (pwk & F_FAIL) ? NONE : kf;
-  }
-  const uint32_t lane = threadIdx.x % 64;
-  for (uint32_t s = NFIRST; s < nrec; s += 64) {
-    const uint32_t kk = s + lane;
-    const uint32_t pw = kk < nrec ? rec_pw(recs[rec_idx(gc, kk)], cx) : POS_MASK;
-    const uint64_t lt = __ballot(kk < nrec && (pw & POS_MASK) < x);
-    const uint32_t nlt = __popcll(lt);
-    if (nlt == 64) continue;
-    if (s + nlt >= nrec) return NONE;
-    const uint32_t cand = lane_read(pw, nlt);
-    return (cand & POS_MASK) == x && !(cand & F_FAIL) ? s + nlt : NONE;
-  }
-  return NONE;
-}
-// phase A: the position after `w` structs from x (a true struct start), along the walk's records; a
-// struct the records do not cover (a FAIL under the speculative cap, a chain the walk missed) is parsed
-// here, uncapped.  False: a struct does not parse (the document is declined).
-__device__ bool skip_structs(DescWin &W, const uint4 *desc, const uint32_t *recs, uint32_t cb, uint32_t nch, const uint8_t *D,
-                             uint32_t len, uint32_t &x, uint32_t w) {
-  const uint32_t lane = threadIdx.x % 64;
-  while (w > 0) {
-    if (x >= len) return false;
-    const uint32_t cx = x / CH;
-    desc_at(W, desc, cb, nch, cx);
-    const int di = (int)(cx - W.wb);
-    const uint32_t nrec = lane_read(W.q0.x, di) & 0xffffu, cexit = lane_read(W.q0.z, di);
-    const uint32_t gc = cb + cx;
-    const uint32_t fs = rec_entry(W, recs, gc, cx, nrec, x);
-    if (fs == NONE) {  // (after a section header the walk's chain has not resynchronised yet: parse here)
-      uint32_t nx, cl, fl;
-      if (!ln::parse_fast(D, x, len, nx, cl, fl) && !ln::parse_struct(D, x, len, nx, cl, fl)) return false;
-      x = nx;
-      w--;
-      continue;
-    }
-    // records fs .. fs + 63: up to the first FAIL (re-parsed next round) or w structs
-    const uint32_t kk = fs + lane;
-    const uint32_t pw = kk < nrec ? rec_pw(recs[rec_idx(gc, kk)], cx) : POS_MASK;
-    const uint64_t fm = __ballot(kk < nrec && (pw & F_FAIL));
-    uint32_t n = nrec - fs < 64 ? nrec - fs : 64;
-    if (fm) n = (uint32_t)__builtin_ctzll(fm);
-    if (n == 0) {  // a FAIL at x itself: (rec_entry returns NONE then; kept for safety)
-      uint32_t nx, cl, fl;
-      if (!ln::parse_struct(D, x, len, nx, cl, fl)) return false;
-      x = nx;
-      w--;
-      continue;
-    }
-    if (w < n) n = w;
-    // the position after the n-th struct: the next record's start, or the chunk's exit
-    const uint32_t nxt = lane_read(pw, n < 64 ? n : 63);
-    x = fs + n < nrec ? (n < 64 ? (nxt & POS_MASK) : (rec_pw(recs[rec_idx(gc, fs + n)], cx) & POS_MASK)) : cexit;
-    w -= n;
-  }
-  return true;
+  bad |= (x & 0x80) || (nb > 1 && x == 0) || (nb == 5 && (x & 0x70) != 0);
+  o += nb;
+  return v;
 }
 
 template <int OP>
-__global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, const uint32_t *cbase, const uint4 *desc, const uint32_t *recs,
-                                                uint8_t *done, const uint64_t *msz, const uint64_t *moff, uint8_t *area) {
+__global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, uint8_t *done, const uint64_t *msz, const uint64_t *moff,
+                                                uint8_t *area) {
   const uint32_t t = threadIdx.x, lane = t % 64, wv = t / 64;
   __shared__ uint32_t mkey[OP == OP_DIFF ? MSVSLOTS : 1], mval[OP == OP_DIFF ? MSVSLOTS : 1], svclk[OP == OP_DIFF ? MSVMAX : 1];
   __shared__ uint32_t s_bad, s_why, s_nsec, s_ds0, s_npatch, s_sum[MS_WAVES + 1];
+  __shared__ uint32_t s_p, s_done;
+  __shared__ MsLds U;
+  TabLds &T = U.tab;
   for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
     if (msz[d] == 0) continue;
-    const uint32_t cb = cbase[d], nch = cbase[d + 1] - cb;
     const uint32_t u0 = j.doc_upd[d];
     const uint64_t ub = j.upd_off[u0];
     const uint32_t len = (uint32_t)(j.upd_off[u0 + 1] - ub);
     const uint8_t *D = j.A + ub;
     sc::cu32 *const B = sc::base_of(D);
     const uint32_t adj = (uint32_t)(ub & 3);
-    if (t == 0) { s_bad = 0; s_why = 0; s_npatch = 0; }
+    if (t == 0) { s_bad = 0; s_why = 0; s_npatch = 0; s_done = 0; }
     if (OP == OP_DIFF)
       for (uint32_t q = t; q < MSVSLOTS; q += MS_T) mval[q] = 0;
     __syncthreads();
     const uint64_t tm0 = __builtin_amdgcn_s_memrealtime();
-    // ---- A: the section headers (wave 0); the state vector (one lane of wave 1)
+    // ---- the state vector (diff): its bytes staged into LDS, decodeStateVector by thread 0 into the hash
+    // map (a later entry wins)
+    if (OP == OP_DIFF) {
+      const uint64_t s0 = j.sv_off[d], s1 = j.sv_off[d + 1];
+      const uint32_t sl = s1 - s0 > TW + TMARG ? NONE : (uint32_t)(s1 - s0);
+      if (sl != NONE)
+        for (uint32_t q = t; q < sl; q += MS_T) T.b[q] = j.sv[s0 + q];
+      __syncthreads();
+      if (t == 0) {
+        bool bad = sl == NONE;
+        uint32_t o = 0;
+        const uint32_t ns = bad ? 0 : tab_vu(T.b, o, sl, bad);
+        bad |= ns > MSVMAX;
+        for (uint32_t q = 0; q < ns && !bad; q++) {
+          const uint32_t cl = tab_vu(T.b, o, sl, bad), ck = tab_vu(T.b, o, sl, bad);
+          svclk[q] = ck;
+          uint32_t h = (cl * 0x9E3779B1u) >> 20;
+          while (mval[h] != 0 && mkey[h] != cl) h = (h + 1) & (MSVSLOTS - 1);
+          mkey[h] = cl;
+          mval[h] = q + 1;
+        }
+        if (bad) { s_bad = 1; s_why = 3; }
+      }
+    }
     uint32_t nsec = 0;
     {
       ln::LCur c = ln::make(D, 0, len);
       nsec = ln::rvu(c);
+      if (t == 0) s_p = c.p;
     }
     const MsDoc M = ms_doc(area, moff[d], nsec);
-    if (wv == 0) {
-      uint32_t x = 0, why = 0, prev = 0;
-      {
-        ln::LCur c = ln::make(D, 0, len);
-        ln::rvu(c);
-        x = c.p;
+    // ---- A + B: the struct chain, window by window: the block computes the tables, thread 0 follows the
+    // chain (section headers parsed, each struct a table lookup; a struct the window cannot decide -- one
+    // that runs past it, a string longer than the margin -- parsed by thread 0 from the document)
+    // thread 0's walk state, carried across windows
+    uint32_t ci = 0, rem = 0, client = 0, k = 0, prev = 0, written = 0, sv_clock = 0, npatch = 0;
+    uint64_t clock = 0;
+    bool insec = false, copying = false, sv_stop = false, first = false;
+    __syncthreads();
+    while (!s_bad && !s_done) {
+      const uint32_t wb = s_p & ~15u;
+      const uint32_t wl = wb + TW + TMARG < len ? wb + TW + TMARG : len;
+      const uint32_t lim = wl - wb, wn = lim < TW ? lim : TW;
+      __syncthreads();
+      for (uint32_t q = 16 * t; q < lim; q += 16 * MS_T) {
+        const uint4 v = wds::load16m(D, wb + q, len);
+        __builtin_memcpy(T.b + q, &v, 16);
       }
-      DescWin W;
-      for (uint32_t ci = 0; ci < nsec && !why; ci++) {
-        ln::LCur c = ln::make(D, x, len);
-        const uint32_t ns = ln::rvu(c), client = ln::rvu(c), clock = ln::rvu(c);
-        x = c.p;
-        if (c.bad) { why = 5; break; }
-        // each section a new client (the writer merges consecutive parts of one client); meta: descending
-        if (ns == 0 || (ci > 0 && client == prev) || (OP == OP_META && ci > 0 && client > prev)) { why = 6; break; }
-        prev = client;
-        if (lane == 0) { msec(ci, M_X0) = x; msec(ci, M_W) = ns; msec(ci, M_CLIENT) = client; msec(ci, M_CLOCK) = clock; }
-        if (!skip_structs(W, desc, recs, cb, nch, D, len, x, ns)) { why = 8; break; }
-        if (lane == 0) msec(ci, M_X1) = x;
+      __syncthreads();
+      for (uint32_t o = t; o < wn; o += MS_T) {
+        uint32_t nx, cl, fl;
+        const bool ok = ln::parse_fast(T.b, o, lim, nx, cl, fl) || ln::parse_struct(T.b, o, lim, nx, cl, fl, lim);
+        T.nx[o] = (uint16_t)(ok ? nx - o : 0);
+        T.len[o] = cl;
+        T.fl[o] = (uint8_t)(ok ? TV | ((fl & F_SKIP) ? 1 : 0) | ((fl & F_PATCH) ? 2 : 0) : 0);
       }
-      if (lane == 0) { s_ds0 = x; if (why) { s_bad = 1; s_why = why; } }
-    } else if (OP == OP_DIFF && t == 64) {  // decodeStateVector: a later entry wins
-      const uint64_t s0 = j.sv_off[d], s1 = j.sv_off[d + 1];
-      ln::LCur c = ln::make(j.sv + s0, 0, (uint32_t)(s1 - s0));
-      const uint32_t ns = s1 - s0 > (1u << 20) ? NONE : ln::rvu(c);
-      bool bad = ns == NONE || ns > MSVMAX;
-      for (uint32_t q = 0; q < ns && !bad; q++) {
-        const uint32_t cl = ln::rvu(c), ck = ln::rvu(c);
-        bad |= c.bad;
-        svclk[q] = ck;
-        uint32_t h = (cl * 0x9E3779B1u) >> 20;
-        while (mval[h] != 0 && mkey[h] != cl) h = (h + 1) & (MSVSLOTS - 1);
-        mkey[h] = cl;
-        mval[h] = q + 1;
+      __syncthreads();
+      if (t == 0) {
+        uint32_t p = s_p, why = 0;
+        const uint32_t wend = wb + wn;
+        for (;;) {
+          if (!insec) {  // a section header: vu(#structs) vu(client) vu(clock)
+            if (ci == nsec) { s_done = 1; break; }
+            if (p >= wend) { if (wend >= len) why = 7; break; }
+            bool bad = false;
+            uint32_t ns, first_clock;
+            if (p + 16 <= wl) {
+              uint32_t o = p - wb;
+              ns = tab_vu(T.b, o, lim, bad);
+              client = tab_vu(T.b, o, lim, bad);
+              first_clock = tab_vu(T.b, o, lim, bad);
+              p = wb + o;
+            } else {
+              ln::LCur c = ln::make(D, p, len);
+              ns = ln::rvu(c);
+              client = ln::rvu(c);
+              first_clock = ln::rvu(c);
+              p = c.p;
+              bad = c.bad;
+            }
+            if (bad) { why = 5; break; }
+            // each section a new client (the writer merges consecutive parts of one client); meta: descending
+            if (ns == 0 || (ci > 0 && client == prev) || (OP == OP_META && ci > 0 && client > prev)) { why = 6; break; }
+            prev = client;
+            msec(ci, M_X0) = p; msec(ci, M_W) = ns; msec(ci, M_CLIENT) = client; msec(ci, M_CLOCK) = first_clock;
+            k = 0;
+            if (OP == OP_DIFF) {
+              uint32_t h = (client * 0x9E3779B1u) >> 20;
+              while (mval[h] != 0) {
+                if (mkey[h] == client) { k = svclk[mval[h] - 1]; break; }
+                h = (h + 1) & (MSVSLOTS - 1);
+              }
+            }
+            clock = first_clock;
+            sv_stop = clock != 0;
+            first = ci == 0;  // the state vector: the first section's first struct counts even as a Skip (os@37724)
+            sv_clock = 0;
+            copying = false;
+            written = 0;
+            rem = ns;
+            insec = true;
+            continue;
+          }
+          if (rem == 0) {  // the section's end
+            msec(ci, M_END) = (uint32_t)clock;
+            msec(ci, M_VAL) = sv_clock;
+            if (OP == OP_DIFF) {
+              msec(ci, M_WRITTEN) = copying ? written : 0;
+              if (!copying) msec(ci, M_PRELEN) = NONE;
+            }
+            msec(ci, M_X1) = p;
+            ci++;
+            insec = false;
+            continue;
+          }
+          // one struct
+          if (p >= wend) { if (wend >= len) why = 7; break; }
+          const uint32_t o = p - wb;
+          uint32_t fl = T.fl[o], nx, cl;
+          if (fl & TV) {
+            nx = p + T.nx[o];
+            cl = T.len[o];
+          } else {
+            uint32_t f2;
+            if (!ln::parse_fast(D, p, len, nx, cl, f2) && !ln::parse_struct(D, p, len, nx, cl, f2)) { why = 8; break; }
+            fl = TV | ((f2 & F_SKIP) ? 1 : 0) | ((f2 & F_PATCH) ? 2 : 0);
+          }
+          if (cl >= (1u << 24)) { why = 9; break; }
+          if (clock + cl > 0xffffffffull) { why = 10; break; }
+          const bool skip = fl & 1;
+          const uint64_t end = clock + cl;
+          if (OP == OP_SV) {
+            if (first) {
+              first = false;
+              if (!sv_stop) sv_clock = (uint32_t)end;
+              if (skip) sv_stop = true;
+            } else if (!sv_stop) {
+              if (skip) sv_stop = true;
+              else sv_clock = (uint32_t)end;
+            }
+          } else if (OP == OP_DIFF) {
+            bool patch = false;
+            if (!copying) {
+              if (!skip && end > k) {  // the cut: the first struct that ends past sv[client]
+                copying = true;
+                written = 1;
+                const uint32_t off = k > clock ? (uint32_t)(k - clock) : 0;
+                uint32_t prelen = 0, a0 = 0, a1 = 0, b0;
+                if (off == 0) {
+                  b0 = p;
+                  patch = true;
+                } else {
+                  if (!slice_head(B, adj, p, nx, client, clock, cl, off, M.pre + (uint64_t)ci * PRE, prelen, a0, a1)) { why = 11; break; }
+                  b0 = nx;
+                }
+                msec(ci, M_PRELEN) = prelen;
+                msec(ci, M_A0) = a0;
+                msec(ci, M_A1) = a1;
+                msec(ci, M_B0) = b0;
+                msec(ci, M_FCLOCK) = (uint32_t)(clock + off);
+              }
+            } else {
+              written++;
+              patch = true;
+            }
+            if (patch && (fl & 2)) {  // the info byte re-encoded: 0x20 cleared with an origin, GC := 0
+              if (npatch >= MSPATCH) { why = 12; break; }
+              const uint32_t info = o < lim ? T.b[o] : D[p];
+              M.ppos[npatch] = p;
+              M.psec[npatch] = ci;
+              M.pval[npatch] = (uint8_t)((info & 31) == 0 ? 0 : info & ~0x20u);
+              npatch++;
+            }
+          }
+          clock = end;
+          p = nx;
+          rem--;
+        }
+        s_p = p;
+        if (why) { s_bad = 1; s_why = why; }
+        if (s_done) { s_ds0 = p; s_npatch = npatch; }
       }
-      if (bad || c.bad) { s_bad = 1; s_why = 3; }
+      __syncthreads();
     }
     __threadfence_block();
     __syncthreads();
@@ -992,213 +1079,8 @@ __global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, const uint32_t *cb
       continue;
     }
     const uint64_t tm1 = __builtin_amdgcn_s_memrealtime();
-    // ---- B: sections round-robin over the waves
-    bool declined = false;
-    uint32_t why = 0;
-    DescWin W;
-    uint32_t cc = NONE, s = 0;
-    for (uint32_t ci = wv; ci < nsec && !declined; ci += MS_WAVES) {
-      cc = NONE;  // (each section looks its entry up afresh: the O(1) chunk rest needs it)
-      uint32_t x = msec(ci, M_X0);
-      const uint32_t nstructs = msec(ci, M_W), client = msec(ci, M_CLIENT);
-      uint64_t clock = msec(ci, M_CLOCK);
-      uint32_t k = 0;
-      if (OP == OP_DIFF) {
-        uint32_t h = (client * 0x9E3779B1u) >> 20;
-        while (mval[h] != 0) {
-          if (mkey[h] == client) { k = svclk[mval[h] - 1]; break; }
-          h = (h + 1) & (MSVSLOTS - 1);
-        }
-      }
-      // state vector: the first section's first struct counts even when it is a Skip (os@37724)
-      bool sv_stop = clock != 0, first = ci == 0;
-      uint32_t sv_clock = 0;
-      bool copying = false;
-      uint32_t written = 0, rem = nstructs;
-      while (rem > 0) {
-        if (x >= len) { declined = true; why = 7; break; }
-        const uint32_t cx = x / CH;
-        desc_at(W, desc, cb, nch, cx);
-        const int di = (int)(cx - W.wb);
-        const uint32_t w0 = lane_read(W.q0.x, di), w1 = lane_read(W.q0.y, di);
-        const uint32_t nrec = w0 & 0xffffu, lfe = w0 >> 16, lpe = w1 & 0xffffu, lse = w1 >> 16;
-        const uint32_t cexit = lane_read(W.q0.z, di), cumx = lane_read(W.q0.w, di);
-        if (cx != cc) { cc = cx; s = 0; }
-        const uint32_t gc = cb + cx;
-        // the rest of the chunk in O(1) when the section spans it (no FAIL / patch / Skip / cut inside)
-        if (s == 0) {
-          uint32_t fs = NONE, fcum = 0;
-#pragma unroll
-          for (int kf = NFIRST - 1; kf >= 0; kf--) {
-            const uint32_t pwk = lane_read(kf < 4 ? (&W.q1.x)[kf] : (&W.q2.x)[kf - 4], di);
-            if ((uint32_t)kf < nrec && (pwk & POS_MASK) == x && !(pwk & F_FAIL)) {
-              fs = (uint32_t)kf;
-              fcum = lane_read(kf < 4 ? (&W.q3.x)[kf] : (&W.q4.x)[kf - 4], di);
-            }
-          }
-          if (fs != NONE) {
-            const uint32_t avail = nrec - fs;
-            const uint32_t delta = cumx - fcum;
-            bool whole = rem >= avail && lfe <= fs && !first;
-            if (OP == OP_DIFF) whole = whole && (copying ? lpe <= fs : clock + delta <= k);
-            if (OP == OP_SV) whole = whole && lse <= fs;
-            if (whole) {
-              if (clock + delta > 0xffffffffull) { declined = true; why = 10; break; }
-              if (OP == OP_SV && !sv_stop) sv_clock = (uint32_t)(clock + delta);
-              if (OP == OP_DIFF && copying) written += avail;
-              clock += delta;
-              rem -= avail;
-              x = cexit;
-              s = nrec;
-              continue;
-            }
-            s = fs;
-          }
-        }
-        bool found = false;
-        for (;;) {
-          if (s >= nrec) break;
-          const uint32_t kk = s + lane;
-          const uint32_t pw = kk < nrec ? rec_pw(recs[rec_idx(gc, kk)], cx) : POS_MASK;
-          const uint64_t lt = __ballot(kk < nrec && (pw & POS_MASK) < x);
-          const uint32_t nlt = __popcll(lt);
-          if (nlt == 64) { s += 64; continue; }
-          s += nlt;
-          if (s < nrec) {
-            const uint32_t cand = lane_read(pw, nlt);
-            found = (cand & POS_MASK) == x && !(cand & F_FAIL);
-          }
-          break;
-        }
-        uint32_t n, pos = 0, end = 0, clen = 0, fl = 0;
-        bool valid;
-        if (found) {
-          n = nrec - s < 64 ? nrec - s : 64;
-          if (rem < n) n = rem;
-          const uint32_t kk = s + lane;
-          valid = lane < n;
-          if (valid) {
-            const uint32_t w = recs[rec_idx(gc, kk)];
-            fl = rec_pw(w, cx);
-            pos = fl & POS_MASK;
-            clen = rec_clen(w);
-            end = kk + 1 < nrec ? rec_pw(recs[rec_idx(gc, kk + 1)], cx) & POS_MASK : cexit;
-          }
-          const uint64_t fm = __ballot(valid && (fl & F_FAIL));
-          if (fm) {
-            n = (uint32_t)__builtin_ctzll(fm);
-            valid = lane < n;
-          }
-          s += n;
-        } else {
-          uint32_t nx, cl, f2;
-          if (!ln::parse_fast(D, x, len, nx, cl, f2) && !ln::parse_struct(D, x, len, nx, cl, f2)) { declined = true; why = 8; break; }
-          n = 1;
-          valid = lane == 0;
-          pos = x; end = nx; clen = cl; fl = f2;
-        }
-        if (n == 0) { declined = true; why = 8; break; }
-        if (__any(valid && clen >= (1u << 24))) { declined = true; why = 9; break; }
-        const uint32_t cl = valid ? clen : 0;
-        const uint32_t incl = wave_incl_add(cl), excl = incl - cl;
-        const uint32_t tot = lane_read(incl, 63);
-        if (clock + tot > 0xffffffffull) { declined = true; why = 10; break; }
-        const bool skip = valid && (fl & F_SKIP);
-        const uint64_t eclk = clock + incl;
-        if (OP == OP_SV) {
-          if (first) {  // the update's first struct initialises the state
-            first = false;
-            sv_clock = sv_stop ? 0 : (uint32_t)(clock + lane_read(cl, 0));
-          }
-          const uint64_t skm = __ballot(skip);
-          const uint32_t fs = skm ? (uint32_t)__builtin_ctzll(skm) : n;
-          if (!sv_stop && fs > 0) sv_clock = (uint32_t)(clock + lane_read(incl, fs - 1));
-          if (skm) sv_stop = true;
-        } else if (OP == OP_DIFF) {
-          first = false;
-          uint32_t firstw = 0;
-          bool pend = false;
-          if (!copying) {
-            const uint64_t cm = __ballot(valid && !skip && eclk > k);
-            if (cm) {
-              const uint32_t f = (uint32_t)__builtin_ctzll(cm);
-              copying = true;
-              written = n - f;
-              const uint64_t fclk = clock + lane_read(excl, f);
-              const uint32_t off = k > fclk ? (uint32_t)(k - fclk) : 0;
-              const uint32_t fpos = lane_read(pos, f), fend = lane_read(end, f), flen = lane_read(cl, f);
-              uint32_t prelen = 0, a0 = 0, a1 = 0, b0;
-              if (off == 0) {
-                b0 = fpos;
-                firstw = f;
-              } else {
-                if (!slice_head(B, adj, fpos, fend, client, fclk, flen, off, M.pre + (uint64_t)ci * PRE, prelen, a0, a1)) {
-                  declined = true;
-                  why = 11;
-                  break;
-                }
-                b0 = fend;
-                firstw = f + 1;
-              }
-              if (lane == 0) {
-                msec(ci, M_PRELEN) = prelen;
-                msec(ci, M_A0) = a0;
-                msec(ci, M_A1) = a1;
-                msec(ci, M_B0) = b0;
-                msec(ci, M_FCLOCK) = (uint32_t)(fclk + off);
-              }
-              pend = true;
-            }
-          } else {
-            written += n;
-            pend = true;
-          }
-          if (pend) {  // info-byte patches of the verbatim structs
-            const bool pl = valid && lane >= firstw && (fl & F_PATCH);
-            const uint64_t pm = __ballot(pl);
-            if (pm) {
-              const uint32_t np = __popcll(pm);
-              uint32_t base = 0;
-              if (lane == 0) base = atomicAdd(&s_npatch, np);
-              base = lane_read(base, 0);
-              if (base + np > MSPATCH) { declined = true; why = 12; break; }
-              if (pl) {
-                const uint32_t slot = base + __popcll(pm & ((1ull << lane) - 1));
-                const uint32_t info = D[pos];
-                M.ppos[slot] = pos;
-                M.psec[slot] = ci;
-                M.pval[slot] = (uint8_t)((info & 31) == 0 ? 0 : info & ~0x20u);
-              }
-            }
-          }
-        } else {
-          first = false;
-        }
-        clock += tot;
-        x = lane_read(end, n - 1);
-        rem -= n;
-      }
-      if (declined) break;
-      if (lane == 0) {
-        msec(ci, M_END) = (uint32_t)clock;
-        msec(ci, M_VAL) = sv_clock;
-        if (OP == OP_DIFF) {
-          msec(ci, M_WRITTEN) = copying ? written : 0;
-          if (!copying) msec(ci, M_PRELEN) = NONE;
-        }
-      }
-      if (x != msec(ci, M_X1)) { declined = true; why = 18; break; }  // (the header walk and the stitch agree)
-    }
-    if (declined && lane == 0) { s_bad = 1; s_why = why; }
-    __threadfence_block();
-    __syncthreads();
-    if (s_bad) {
-      if (t == 0) done[d] = (uint8_t)s_why;
-      __syncthreads();
-      continue;
-    }
-    const uint64_t tm2 = __builtin_amdgcn_s_memrealtime();
-    if (t == 0) { atomicAdd(&pw_prof[0], tm1 - tm0); atomicAdd(&pw_prof[1], tm2 - tm1); }
+    const uint64_t tm2 = tm1;
+    if (t == 0) { atomicAdd(&pw_prof[0], tm1 - tm0); }
     // ---- C
     if (OP != OP_DIFF) {  // state vector / meta: one entry per section, written by one thread
       if (t == 0) {
@@ -1238,35 +1120,14 @@ __global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, const uint32_t *cb
       __syncthreads();
       continue;
     }
-    // delete set (wave 0): validated (readDeleteSet: no empty and no repeated client, checked in the LDS
-    // hash table the state vector used), then copied verbatim
-    for (uint32_t q = t; q < MSVSLOTS; q += MS_T) mval[q] = 0;
-    __syncthreads();
-    if (wv == 0) {
-      uint32_t x = s_ds0;
-      ln::LCur c = ln::make(D, x, len);
-      const uint32_t ndc = ln::rvu(c);
-      x = c.p;
-      bool bad = c.bad || ndc > MSVMAX;
-      for (uint32_t i = 0; i < ndc && !bad; i++) {
-        ln::LCur h = ln::make(D, x, len);
-        const uint32_t client = ln::rvu(h);
-        const uint32_t m = ln::rvu(h);
-        x = h.p;
-        if (h.bad || m == 0) { bad = true; break; }
-        uint32_t hit = 0;
-        if (lane == 0) {
-          uint32_t hh = (client * 0x9E3779B1u) >> 20;
-          while (mval[hh] != 0 && mkey[hh] != client) hh = (hh + 1) & (MSVSLOTS - 1);
-          hit = mval[hh] != 0;
-          mkey[hh] = client;
-          mval[hh] = 1;
-        }
-        if (lane_read(hit, 0)) { bad = true; break; }
-        x = wds::skip_varuints(D, x, len, 2ull * m);
-        if (x == NONE) { bad = true; break; }
+    // delete set: validated (readDeleteSet: no empty and no repeated client) through the LDS token tables
+    // (ym_wave_ds.h), then copied verbatim
+    {
+      const uint32_t x = wds::ds_validate_lds(D, s_ds0, len, U.ds);
+      if (t == 0) {
+        if (x == NONE || x == wds::DS_BIG) { s_bad = 1; s_why = 17; }
+        s_sum[MS_WAVES] = x;
       }
-      if (lane == 0) { if (bad) { s_bad = 1; s_why = 17; } s_sum[MS_WAVES] = x; }
     }
     __syncthreads();
     if (s_bad) {
@@ -1408,29 +1269,29 @@ int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const ui
   const uint64_t mtotal = *(uint64_t *)(B.pinned + 2);
   *done_out = done;  // every document is marked (0 = not taken) from here on
   pw_last_done = done;
+  const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
+  // many-section documents: the table walk (no chunk records)
+  if (mtotal > 0) {
+    if (pw_ensure(B, 4, mtotal + 256)) {  // no room for the section tables: k_big_v1 takes those documents
+      hipMemsetAsync(msz, 0, 8ull * n1, st);
+    } else {
+      uint8_t *area = (uint8_t *)B.p[4];
+      if (op == OP_DIFF) k_pw_ms<OP_DIFF><<<grid, MS_T, 0, st>>>(j, done, msz, moff, area);
+      else if (op == OP_SV) k_pw_ms<OP_SV><<<grid, MS_T, 0, st>>>(j, done, msz, moff, area);
+      else k_pw_ms<OP_META><<<grid, MS_T, 0, st>>>(j, done, msz, moff, area);
+    }
+  }
   if (total == 0) return 1;
   if (pw_ensure(B, 2, 80ull * total) || pw_ensure(B, 3, 4ull * CAP * ((total + 63) & ~63u))) {
-    // no room for the records: leave every document to k_big_v1
-    hipMemsetAsync(done, 0, j.n, st);
+    // no room for the records: the chunk-walked documents go to k_big_v1 (the table-walked ones are done)
     return 1;
   }
   uint4 *desc = (uint4 *)B.p[2];
   uint32_t *recs = (uint32_t *)B.p[3];
-  if (mtotal > 0 && pw_ensure(B, 4, mtotal + 256)) {  // no room for the section tables: the one-wave stitch takes them
-    hipMemsetAsync(msz, 0, 8ull * n1, st);
-  }
-  const bool ms = mtotal > 0 && B.p[4] != nullptr && B.cap[4] >= mtotal;
   k_pw_walk<<<(total + 255) / 256, 256, 0, st>>>(j, cbase, j.n, total, desc, recs);
-  const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
   if (op == OP_DIFF) k_pw_stitch<OP_DIFF><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done, msz);
   else if (op == OP_SV) k_pw_stitch<OP_SV><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done, msz);
   else k_pw_stitch<OP_META><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done, msz);
-  if (ms) {
-    uint8_t *area = (uint8_t *)B.p[4];
-    if (op == OP_DIFF) k_pw_ms<OP_DIFF><<<grid, MS_T, 0, st>>>(j, cbase, desc, recs, done, msz, moff, area);
-    else if (op == OP_SV) k_pw_ms<OP_SV><<<grid, MS_T, 0, st>>>(j, cbase, desc, recs, done, msz, moff, area);
-    else k_pw_ms<OP_META><<<grid, MS_T, 0, st>>>(j, cbase, desc, recs, done, msz, moff, area);
-  }
   return 1;
 }
 

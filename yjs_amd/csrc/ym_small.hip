@@ -40,29 +40,30 @@ struct Lay {
   static constexpr uint32_t BYTES = SV + ND * NSVE * 8;
 };
 
-// writeVarUint into global memory; returns the position after it
-__device__ __forceinline__ uint32_t gput(uint8_t *o, uint32_t p, uint32_t v) {
-  while (v > 127) { o[p++] = (uint8_t)(0x80 | (v & 127)); v >>= 7; }
-  o[p++] = (uint8_t)v;
-  return p;
+// Output stores go through a buffer resource (the document's output range, ym_fast_common.h Slot): vector
+// memory stores at byte offsets.  (A generic pointer's store would also count against the LDS counter, so
+// every later LDS read of the lane's walk would wait for that store's round trip to HBM.)
+__device__ __forceinline__ void put_u64s(Slot o, uint32_t p, uint64_t v) {
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 w = {(unsigned int)v, (unsigned int)(v >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b64(w, o, (int)p, 0, 0);
 }
-// n bytes from the LDS document (generic pointer) to global memory
-__device__ __forceinline__ void gcopy(uint8_t *o, const uint8_t *s, uint32_t n) {
+__device__ __forceinline__ uint32_t gput(Slot o, uint32_t p, uint32_t v) { return put_vu(o, p, v); }
+// n bytes from LDS offset s to output offset p
+__device__ __forceinline__ void gcopy(Slot o, uint32_t p, uint32_t s, uint32_t n) {
   uint32_t i = 0;
-  for (; i + 8 <= n; i += 8) { uint64_t x; __builtin_memcpy(&x, s + i, 8); __builtin_memcpy(o + i, &x, 8); }
-  for (; i < n; i++) o[i] = s[i];
+  for (; i + 8 <= n; i += 8) put_u64s(o, p + i, ld8(s + i));
+  for (; i < n; i++) ob8(o, p + i, sm[s + i]);
 }
-// one struct at p (doc bytes b, end e): next position, clock length, info byte; false: k_big_v1's decline
-__device__ __forceinline__ bool one(const uint8_t *b, uint32_t p, uint32_t e, uint32_t &nx, uint32_t &len, uint32_t &info) {
-  uint32_t fl;
-  info = b[p];
-  if (ln::parse_fast(b, p, e, nx, len, fl)) return true;
-  ln::LCur c = ln::make(b, p, e);
-  const uint32_t inf = ln::rdb(c);
-  const bool skip = inf == 10, gc = !skip && (inf & 31) == 0;
+// one struct at LDS offset p (document end e): next position, clock length, info byte; false: k_big_v1's
+// decline.  The parsers of the LDS merge kernels (ym_fast_common.h), nested payloads included.
+__device__ __forceinline__ bool one(uint32_t p, uint32_t e, uint32_t &nx, uint32_t &len, uint32_t &info) {
+  info = sm[p];
+  Cur c = {p + 1, e, false};
+  const bool skip = info == 10, gc = !skip && (info & 31) == 0;
   if (skip || gc) {
-    len = ln::rvu(c);
-  } else if (!ln::item_body(c, inf, len)) {
+    len = rvu(c);
+  } else if (!item_body<true>(c, info, len)) {
     return false;
   }
   nx = c.p;
@@ -72,60 +73,60 @@ __device__ __forceinline__ uint32_t norm_info(uint32_t info) {
   const bool skip = info == 10, gc = !skip && (info & 31) == 0;
   return skip ? info : gc ? 0 : ((info & 0xC0) ? info & ~0x20u : info);
 }
-// Item.write / GC.write with offset off (> 0) of the struct [s0, s1) (info byte at s0) of client `client`
-// at `clock`: writes the head to o (when o != nullptr) and returns its bytes, with the content tail [a0, a1)
-// of the input that follows it; NONE: k_big_v1 declines (a kind it does not slice, a cut inside a surrogate
-// pair: the general path raises yjs's error)
-__device__ __forceinline__ uint32_t head(const uint8_t *b, uint32_t s0, uint32_t s1, uint32_t info, uint32_t client,
-                                         uint32_t clock, uint32_t len, uint32_t off, uint8_t *o, uint32_t &a0, uint32_t &a1) {
+// Item.write / GC.write with offset off (> 0) of the struct [s0, s1) (LDS offsets, info byte at s0) of client
+// `client` at `clock`: writes the head to o (when o != nullptr) and returns its bytes, with the content tail
+// [a0, a1) of the input that follows it; NONE: k_big_v1 declines (a kind it does not slice, a cut inside a
+// surrogate pair: the general path raises yjs's error)
+__device__ __forceinline__ uint32_t head(uint32_t s0, uint32_t s1, uint32_t info, uint32_t client, uint32_t clock,
+                                         uint32_t len, uint32_t off, bool wr, Slot o, uint32_t p, uint32_t &a0, uint32_t &a1) {
   a0 = a1 = 0;
   const bool gc = info != 10 && (info & 31) == 0;
   if (gc) {
-    if (o) { o[0] = 0; gput(o, 1, len - off); }
+    if (wr) { ob8(o, p, 0); gput(o, p + 1, len - off); }
     return 1 + vsz(len - off);
   }
   const uint32_t ref = info & 31;
   if (ref != 1 && ref != 4 && ref != 8) return NONE;
-  ln::LCur e = ln::make(b, s0 + 1, s1);
+  Cur e = {s0 + 1, s1, false};
   const uint32_t ni = ref | 0x80 | (info & 0x40) | ((info & 0xC0) == 0 ? (info & 0x20) : 0);
-  if (info & 0x80) { ln::skvu(e); ln::skvu(e); }
+  if (info & 0x80) { skvu(e); skvu(e); }
   uint32_t ro0 = 0, ro1 = 0;
-  if (info & 0x40) { ro0 = e.p; ln::skvu(e); ln::skvu(e); ro1 = e.p; }
+  if (info & 0x40) { ro0 = e.p; skvu(e); skvu(e); ro1 = e.p; }
   if ((info & 0xC0) == 0) {
-    const uint32_t pi = ln::rvu(e);
-    if (pi == 1) { const uint32_t n = ln::rvu(e); ln::skip(e, n); }
-    else { ln::skvu(e); ln::skvu(e); }
-    if (info & 0x20) { const uint32_t n = ln::rvu(e); ln::skip(e, n); }
+    const uint32_t pi = rvu(e);
+    if (pi == 1) { const uint32_t n = rvu(e); e.p += n; }
+    else { skvu(e); skvu(e); }
+    if (info & 0x20) { const uint32_t n = rvu(e); e.p += n; }
   }
   uint32_t q = 1 + vsz(client) + vsz(clock + off - 1) + (ro1 - ro0);
-  if (o) {
-    o[0] = (uint8_t)ni;
-    uint32_t t = gput(o, 1, client);
+  if (wr) {
+    ob8(o, p, ni);
+    uint32_t t = gput(o, p + 1, client);
     t = gput(o, t, clock + off - 1);
-    for (uint32_t x = ro0; x < ro1; x++) o[t++] = b[x];
+    for (uint32_t x = ro0; x < ro1; x++) ob8(o, t++, sm[x]);
   }
   if (ref == 1) {
-    ln::rvu(e);
-    if (o) gput(o, q, len - off);
+    rvu(e);
+    if (wr) gput(o, p + q, len - off);
     q += vsz(len - off);
   } else if (ref == 8) {
-    ln::rvu(e);
-    for (uint32_t i = 0; i < off; i++) ln::any_canon(e);  // ContentAny.splice: drop `off` values
-    if (o) gput(o, q, len - off);
+    rvu(e);
+    for (uint32_t i = 0; i < off; i++) any_canon<true>(e);  // ContentAny.splice: drop `off` values
+    if (wr) gput(o, p + q, len - off);
     q += vsz(len - off);
     a0 = e.p;
     a1 = s1;
   } else {  // ContentString: str.slice(off) in UTF-16 units
-    const uint32_t n = ln::rvu(e);
+    const uint32_t n = rvu(e);
     uint32_t bi = 0, u = 0;
     while (u < off && bi < n) {
-      const uint32_t x = b[e.p + bi];
+      const uint32_t x = sm[e.p + bi];
       const uint32_t l = x < 0x80 ? 1 : x < 0xE0 ? 2 : x < 0xF0 ? 3 : 4;
       u += l == 4 ? 2 : 1;
       bi += l;
     }
     if (u != off) return NONE;
-    if (o) gput(o, q, n - bi);
+    if (wr) gput(o, p + q, n - bi);
     q += vsz(n - bi);
     a0 = e.p + bi;
     a1 = e.p + n;
@@ -164,9 +165,11 @@ __global__ void __launch_bounds__(64) k_small_v1(GeneralJob j, uint8_t *done) {
   const uint64_t ub = j.upd_off[u0], len64 = j.upd_off[u0 + 1] - ub;
   if (len64 == 0 || len64 + 48 > SLOT) return;
   const uint32_t len = (uint32_t)len64;
-  const uint8_t *b = &sm[lane * SLOT + (uint32_t)(ub & 15)];  // update byte 0
-  uint32_t *rec = &at<uint32_t>(L::REC + lane * NSEC * 20);   // [NSEC][5]
-  uint32_t *svt = &at<uint32_t>(L::SV + lane * NSVE * 8);     // [NSVE][2]
+  const uint32_t B = lane * SLOT + (uint32_t)(ub & 15), E = B + len;  // the update's bytes: LDS [B, E)
+  const uint32_t REC = L::REC + lane * NSEC * 20;                      // u32[NSEC][5]
+  const uint32_t SVT = L::SV + lane * NSVE * 8;                        // u32[NSVE][2]
+  auto rec = [&](uint32_t i) -> uint32_t & { return at<uint32_t>(REC + 4 * i); };
+  auto svt = [&](uint32_t i) -> uint32_t & { return at<uint32_t>(SVT + 4 * i); };
   // ---- the state vector (diff): decodeStateVector, a later entry for a client wins
   uint32_t nsv = 0;
   if (OP == OP_DIFF) {
@@ -176,8 +179,9 @@ __global__ void __launch_bounds__(64) k_small_v1(GeneralJob j, uint8_t *done) {
     const uint32_t n = ln::rvu(c);
     if (c.bad || n > NSVE) return;
     for (uint32_t i = 0; i < n; i++) {
-      svt[2 * i] = ln::rvu(c);
-      svt[2 * i + 1] = ln::rvu(c);
+      const uint32_t cl = ln::rvu(c), ck = ln::rvu(c);
+      svt(2 * i) = cl;
+      svt(2 * i + 1) = ck;
     }
     if (c.bad) return;
     nsv = n;
@@ -185,24 +189,24 @@ __global__ void __launch_bounds__(64) k_small_v1(GeneralJob j, uint8_t *done) {
   auto sv_get = [&](uint32_t client) -> uint32_t {
     uint32_t k = 0;
     for (uint32_t i = 0; i < nsv; i++)
-      if (svt[2 * i] == client) k = svt[2 * i + 1];
+      if (svt(2 * i) == client) k = svt(2 * i + 1);
     return k;
   };
   // ---- pass 1: the struct section
-  ln::LCur c = ln::make(b, 0, len);
-  const uint32_t nclients = ln::rvu(c);
+  Cur c = {B, E, false};
+  const uint32_t nclients = rvu(c);
   if (c.bad || nclients > NSEC) return;
   uint32_t p = c.p;
   uint32_t nparts = 0, body = 0;  // diff: kept sections, their bytes (headers included)
   uint32_t sv_client = 0, sv_clock = 0, sv_n = 0, prev_client = 0;
   bool sv_stop = false, sv_any = false;
   for (uint32_t ci = 0; ci < nclients; ci++) {
-    ln::LCur h = ln::make(b, p, len);
-    const uint32_t nstructs = ln::rvu(h), client = ln::rvu(h);
-    uint64_t clock = ln::rvu(h);
+    Cur h = {p, E, false};
+    const uint32_t nstructs = rvu(h), client = rvu(h);
+    uint64_t clock = rvu(h);
     if (h.bad) return;
     p = h.p;
-    if (ci > 0 && client == prev_client) return;            // the writer would not start a part
+    if (ci > 0 && client == prev_client) return;                  // the writer would not start a part
     if (OP == OP_META && ci > 0 && client > prev_client) return;  // a repeated client keeps its first position
     const uint32_t first_clock = (uint32_t)clock;
     prev_client = client;
@@ -210,8 +214,8 @@ __global__ void __launch_bounds__(64) k_small_v1(GeneralJob j, uint8_t *done) {
     if (OP == OP_SV && nstructs > 0 && sv_any && client != sv_client) {  // client change (os@37724)
       if (sv_clock != 0) {
         if (sv_n >= NSEC) return;
-        rec[2 * sv_n] = sv_client;
-        rec[2 * sv_n + 1] = sv_clock;
+        rec(2 * sv_n) = sv_client;
+        rec(2 * sv_n + 1) = sv_clock;
         sv_n++;
       }
       sv_client = client; sv_clock = 0; sv_stop = clock != 0;
@@ -220,7 +224,7 @@ __global__ void __launch_bounds__(64) k_small_v1(GeneralJob j, uint8_t *done) {
     uint32_t written = 0, sbytes = 0;
     for (uint32_t si = 0; si < nstructs; si++) {
       uint32_t nx, l, info;
-      if (p >= len || !one(b, p, len, nx, l, info)) return;
+      if (p >= E || !one(p, E, nx, l, info)) return;
       const bool skip = info == 10;
       if (clock + l > 0xffffffffull) return;
       if (OP == OP_SV) {
@@ -242,12 +246,14 @@ __global__ void __launch_bounds__(64) k_small_v1(GeneralJob j, uint8_t *done) {
             uint32_t hb = nx - p;
             if (off > 0) {
               uint32_t a0, a1;
-              hb = head(b, p, nx, info, client, (uint32_t)clock, l, off, nullptr, a0, a1);
+              hb = head(p, nx, info, client, (uint32_t)clock, l, off, false, make_slot(j.out, 0), 0, a0, a1);
               if (hb == NONE) return;
               hb += a1 - a0;
             }
-            uint32_t *r = rec + 5 * nparts;
-            r[0] = p; r[1] = off; r[3] = (uint32_t)(clock + off); r[4] = client;
+            rec(5 * nparts) = p;
+            rec(5 * nparts + 1) = off;
+            rec(5 * nparts + 3) = (uint32_t)(clock + off);
+            rec(5 * nparts + 4) = client;
             sbytes = hb;
           }
         } else {
@@ -260,54 +266,53 @@ __global__ void __launch_bounds__(64) k_small_v1(GeneralJob j, uint8_t *done) {
     }
     if (OP == OP_META && nstructs > 0) {
       if (sv_n >= NSEC) return;
-      rec[3 * sv_n] = client;
-      rec[3 * sv_n + 1] = first_clock;
-      rec[3 * sv_n + 2] = (uint32_t)clock;
+      rec(3 * sv_n) = client;
+      rec(3 * sv_n + 1) = first_clock;
+      rec(3 * sv_n + 2) = (uint32_t)clock;
       sv_n++;
     }
     if (OP == OP_DIFF && copying) {
-      rec[5 * nparts + 2] = written;
-      body += vsz(written) + vsz(client) + vsz(rec[5 * nparts + 3]) + sbytes;
+      rec(5 * nparts + 2) = written;
+      body += vsz(written) + vsz(client) + vsz(rec(5 * nparts + 3)) + sbytes;
       nparts++;
     }
   }
-  uint8_t *o = nullptr;
   uint32_t total = 0;
   if (OP == OP_META) {
     uint32_t tl = 2 * vsz(sv_n);
-    for (uint32_t i = 0; i < sv_n; i++) tl += 2 * vsz(rec[3 * i]) + vsz(rec[3 * i + 1]) + vsz(rec[3 * i + 2]);
+    for (uint32_t i = 0; i < sv_n; i++) tl += 2 * vsz(rec(3 * i)) + vsz(rec(3 * i + 1)) + vsz(rec(3 * i + 2));
     total = tl;
   } else if (OP == OP_SV) {
     if (sv_any && sv_clock != 0) {
       if (sv_n >= NSEC) return;
-      rec[2 * sv_n] = sv_client;
-      rec[2 * sv_n + 1] = sv_clock;
+      rec(2 * sv_n) = sv_client;
+      rec(2 * sv_n + 1) = sv_clock;
       sv_n++;
     }
     uint32_t tl = vsz(sv_n);
-    for (uint32_t i = 0; i < sv_n; i++) tl += vsz(rec[2 * i]) + vsz(rec[2 * i + 1]);
+    for (uint32_t i = 0; i < sv_n; i++) tl += vsz(rec(2 * i)) + vsz(rec(2 * i + 1));
     total = tl;
   }
   // ---- delete set (diff): validated, copied verbatim (readDeleteSet + writeDeleteSet round trip)
   const uint32_t ds0 = p;
   if (OP == OP_DIFF) {
-    ln::LCur e = ln::make(b, p, len);
-    const uint32_t ndc = ln::rvu(e);
-    if (e.bad || ndc > NSVE) return;
+    Cur e = {p, E, false};
+    const uint32_t ndc = rvu(e);
+    if (e.bad || ndc > 2 * NSVE) return;
     // repeated clients: checked against the clients seen so far (the sv table's space is free now)
     for (uint32_t i = 0; i < ndc; i++) {
-      const uint32_t client = ln::rvu(e), m = ln::rvu(e);
+      const uint32_t client = rvu(e), m = rvu(e);
       if (e.bad || m == 0) return;
       for (uint32_t h = 0; h < i; h++)
-        if (svt[h] == client) return;
-      svt[i] = client;
-      for (uint32_t q = 0; q < m && !e.bad; q++) { ln::rvu(e); ln::rvu(e); }
+        if (svt(h) == client) return;
+      svt(i) = client;
+      for (uint32_t q = 0; q < m && !e.bad; q++) { skvu(e); skvu(e); }
     }
     if (e.bad) return;
     p = e.p;
     total = vsz(nparts) + body + (p - ds0);
   }
-  // ---- allocation, then the output
+  // ---- allocation, then the output (buffer stores into the document's output range)
   const uint64_t base = atomicAdd((unsigned long long *)j.used, (unsigned long long)total);
   done[d] = 1;
   if (base + total > j.cap) {
@@ -315,43 +320,41 @@ __global__ void __launch_bounds__(64) k_small_v1(GeneralJob j, uint8_t *done) {
     j.out_len[d] = 0;
     return;
   }
-  o = j.out + base;
+  const Slot o = make_slot(j.out + base, total);
   if (OP == OP_META) {  // from then to: vu(n) | (client, clock)*
     uint32_t q = gput(o, 0, sv_n);
-    for (uint32_t i = 0; i < sv_n; i++) { q = gput(o, q, rec[3 * i]); q = gput(o, q, rec[3 * i + 1]); }
+    for (uint32_t i = 0; i < sv_n; i++) { q = gput(o, q, rec(3 * i)); q = gput(o, q, rec(3 * i + 1)); }
     q = gput(o, q, sv_n);
-    for (uint32_t i = 0; i < sv_n; i++) { q = gput(o, q, rec[3 * i]); q = gput(o, q, rec[3 * i + 2]); }
+    for (uint32_t i = 0; i < sv_n; i++) { q = gput(o, q, rec(3 * i)); q = gput(o, q, rec(3 * i + 2)); }
   } else if (OP == OP_SV) {
     uint32_t q = gput(o, 0, sv_n);
-    for (uint32_t i = 0; i < sv_n; i++) { q = gput(o, q, rec[2 * i]); q = gput(o, q, rec[2 * i + 1]); }
+    for (uint32_t i = 0; i < sv_n; i++) { q = gput(o, q, rec(2 * i)); q = gput(o, q, rec(2 * i + 1)); }
   } else {
     // ---- pass 2 (diff): each kept section from its cut struct
     uint32_t q = gput(o, 0, nparts);
     for (uint32_t s = 0; s < nparts; s++) {
-      const uint32_t *r = rec + 5 * s;
-      const uint32_t written = r[2], off = r[1], client = r[4];
+      const uint32_t written = rec(5 * s + 2), off = rec(5 * s + 1), fclock = rec(5 * s + 3), client = rec(5 * s + 4);
       q = gput(o, q, written);
       q = gput(o, q, client);
-      q = gput(o, q, r[3]);
-      uint32_t x = r[0];
+      q = gput(o, q, fclock);
+      uint32_t x = rec(5 * s);
       for (uint32_t w = 0; w < written; w++) {
         uint32_t nx, l, info;
-        one(b, x, len, nx, l, info);  // (parsed in pass 1)
+        one(x, E, nx, l, info);  // (parsed in pass 1)
         if (w == 0 && off > 0) {
           uint32_t a0, a1;
-          const uint32_t hb = head(b, x, nx, info, client, r[3] - off, l, off, o + q, a0, a1);
-          q += hb;
-          gcopy(o + q, b + a0, a1 - a0);
+          q += head(x, nx, info, client, fclock - off, l, off, true, o, q, a0, a1);
+          gcopy(o, q, a0, a1 - a0);
           q += a1 - a0;
         } else {
-          o[q] = (uint8_t)norm_info(info);
-          gcopy(o + q + 1, b + x + 1, nx - x - 1);
+          ob8(o, q, norm_info(info));
+          gcopy(o, q + 1, x + 1, nx - x - 1);
           q += nx - x;
         }
         x = nx;
       }
     }
-    gcopy(o + q, b + ds0, p - ds0);
+    gcopy(o, q, ds0, p - ds0);
   }
   j.out_off[d] = base;
   j.out_len[d] = total;
