@@ -526,9 +526,10 @@ def main():
             "docs_fast_path": int(fast_all), "docs_general_path": int(gen_all), "doc_errors": int(err_all),
             "device_ms_per_step": round(float(np.mean(dev_ms)), 4),
             "working_set_bytes": int((in_bytes + cap) * rot), "rotated_buffer_sets": rot,
-            "roofline": {"kernel": kernel_name, "bound": "hbm", "achieved": round(achieved, 2),
+            "roofline": {"kernel": kernel_name, "bound": "issue", "roof": "hbm", "achieved": round(achieved, 2),
                          "limiter": "instruction issue (PMC: SQ_ACTIVE_INST_ANY per SIMD ~ the launch's duration, "
-                                    "HBM traffic ~1.2x the algorithmic bytes; DESIGN.md section 4.1)",
+                                    "HBM traffic ~1.2x the algorithmic bytes; DESIGN.md section 4.1); frac is "
+                                    "against the HBM roof",
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic, "traffic_source": traffic_src, "avg_launch_ms": round(avg_fast, 5),
                          "algorithmic_bytes_per_launch": int(alg_bytes)},

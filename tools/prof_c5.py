@@ -53,8 +53,10 @@ for fmt in [int(x) for x in os.environ.get("FMTS", "2,1").split(",")]:
         print(f"c5 v{fmt} {op}: {len(docs)} docs, rc {rc}, ms {['%.2f' % x for x in ts]}, chunked {eng.stats['docs_chunked']}, "
               f"fast {eng.stats['docs_fast']}, bad(first 8) {bad}", flush=True)
         import ctypes
-        pr = (ctypes.c_ulonglong * 8)()
+        pr = (ctypes.c_ulonglong * 16)()
         eng.lib.ym__pw_prof(pr, 1)
+        if pr[10]:
+            print("   k_pw_ms (ticks of 10 ns, summed): tables %d, serial walk %d, windows %d, structs %d" % (pr[8], pr[9], pr[10], pr[11]))
         print("   pw_prof: k_pw_ms phase ticks A %d B %d C %d patches %d | stitch counters: whole %d, entry not whole %d, "
               "entry not in first %d, record batches %d, re-parsed structs %d, search loads %d" % (tuple(pr[:4]) + tuple(pr[:6])))
         if hasattr(eng.lib, "ym__pw_ticks"):

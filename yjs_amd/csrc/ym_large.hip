@@ -12,7 +12,7 @@
 //      into an LDS window per wave; struct records, client runs (the structs of one client inside one
 //      update: contiguous clocks) and delete ranges go to SoA arrays at offsets from exclusive scans
 //      of the per-update counts (hipcub::DeviceScan).
-//   2. segmented radix sorts (hipcub::DeviceSegmentedRadixSort, one segment per document): runs by
+//   2. segmented radix sorts (ym_segsort.hip, one workgroup per document): runs by
 //      (~client << 32 | clock), delete ranges by (client << 32 | clock); the ranges' values are their
 //      emission index = first-appearance order.
 //   3. one 1024-thread workgroup per document, tile loops with carried block scans:
@@ -1169,7 +1169,8 @@ int large_run(const GeneralJob &j, const uint32_t *list, uint32_t nb, uint32_t n
   if (((uint32_t *)B.pinned)[3] == 0) return 0;  // no listed document has a chunk: all stay pending
   const uint64_t NS = ((uint32_t *)B.pinned)[0] + 1ull, NR = ((uint32_t *)B.pinned)[1] + 1ull, ND = ((uint32_t *)B.pinned)[2] + 1ull;
   const bool v2 = J.v2;
-  uint64_t need = csize<uint64_t>(NS) * 2 + csize<uint32_t>(NS) * 3 + (v2 ? csize<uint4>(NS) + csize<uint64_t>(3 * NS) : 0) +
+  const uint64_t NT = NR > ND ? NR : ND;  // the sorts' scratch pair
+  uint64_t need = csize<uint64_t>(NT) + csize<uint32_t>(NT) + csize<uint64_t>(NS) * 2 + csize<uint32_t>(NS) * 3 + (v2 ? csize<uint4>(NS) + csize<uint64_t>(3 * NS) : 0) +
                   csize<uint64_t>(NR) * 2 + csize<uint32_t>(NR) * 10 + csize<uint32_t>(NS) * 4 +
                   csize<uint64_t>(ND) * 2 + csize<uint32_t>(ND) * 12 +
                   (v2 ? csize<uint32_t>(3 * NS) * 2 + csize<uint32_t>(NS) * 3 + csize<uint8_t>(2 * NS) + csize<uint8_t>(NS) * 2 +
@@ -1226,23 +1227,16 @@ int large_run(const GeneralJob &j, const uint32_t *list, uint32_t nb, uint32_t n
     J.c_tr = carve<uint8_t>(p, NS);
     J.c_st = carve<uint64_t>(p, 3 * NS);
   }
+  uint64_t *skt = carve<uint64_t>(p, NT);
+  uint32_t *svt = carve<uint32_t>(p, NT);
   if ((uint64_t)(p - (uint8_t *)B.p[2]) > B.cap[2]) return -3;
   if (J.v2) k_lm_walk<true, true><<<grid, 64, WALK_LDS, st>>>(J, tot);
   else k_lm_walk<true, false><<<grid, 64, WALK_LDS, st>>>(J, tot);
   k_lm_segs<<<(nb + 255) / 256, 256, 0, st>>>(J, seg);
-  // segmented radix sorts: runs by (~client << 32 | clock), delete ranges by (client << 32 | clock)
-  size_t s1 = 0, s2 = 0;
-  hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, s1, J.runkey, J.srunkey, J.runidx, J.srunidx, (int)(NR - 1), (int)nb,
-                                              seg, seg + nb, 0, 64, st);
-  hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, s2, J.dkey, J.sdkey, J.didx, J.sdidx, (int)(ND - 1), (int)nb,
-                                              seg + 2 * nb, seg + 3 * nb, 0, 64, st);
-  if (ensure(B, 3, (s1 > s2 ? s1 : s2) + 256)) return -2;
-  if (NR > 1)
-    hipcub::DeviceSegmentedRadixSort::SortPairs(B.p[3], s1, J.runkey, J.srunkey, J.runidx, J.srunidx, (int)(NR - 1), (int)nb,
-                                                seg, seg + nb, 0, 64, st);
-  if (ND > 1)
-    hipcub::DeviceSegmentedRadixSort::SortPairs(B.p[3], s2, J.dkey, J.sdkey, J.didx, J.sdidx, (int)(ND - 1), (int)nb,
-                                                seg + 2 * nb, seg + 3 * nb, 0, 64, st);
+  // segmented radix sorts (ym_segsort.hip, one workgroup per document): runs by (~client << 32 | clock),
+  // delete ranges by (client << 32 | clock)
+  if (NR > 1 && segsort_pairs(J.runkey, J.runidx, J.srunkey, J.srunidx, skt, svt, seg, seg + nb, nb, st)) return -3;
+  if (ND > 1 && segsort_pairs(J.dkey, J.didx, J.sdkey, J.sdidx, skt, svt, seg + 2 * nb, seg + 3 * nb, nb, st)) return -3;
   if (J.v2) {
     k_lm_doc1<true><<<nb, BT, 0, st>>>(J);
     k_lm_col<false><<<dim3(nb, 9), BT, 0, st>>>(J);

@@ -81,7 +81,7 @@ __device__ __forceinline__ Scr scratch(const GeneralJob &j) {
 // stitch path counters (build with -DYM_PW_PROF; read with ym__pw_prof): [0] chunks consumed whole from
 // their entry, [1] entry found but the chunk not whole, [2] entry not among the first records, [3] record
 // batches, [4] structs re-parsed by the stitch, [5] record search loads
-__device__ unsigned long long pw_prof[8];
+__device__ unsigned long long pw_prof[16];
 #ifdef YM_PW_PROF
 #define PWP(i) do { if (threadIdx.x == 0) atomicAdd(&pw_prof[i], 1ull); } while (0)
 #else
@@ -852,6 +852,8 @@ union MsLds {
   TabLds tab;
   wds::DsLds ds;
 };
+// lane 0's value to the whole wave, as a scalar
+__device__ __forceinline__ uint32_t RF(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 // lib0 readVarUint (canonical, u32) at o of the LDS bytes b (valid [0, lim)), advancing o
 __device__ __forceinline__ uint32_t tab_vu(const uint8_t *b, uint32_t &o, uint32_t lim, bool &bad) {
   uint32_t v = 0, nb = 0, x = 0x80;
@@ -925,8 +927,10 @@ __global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, uint8_t *done, con
     uint32_t ci = 0, rem = 0, client = 0, k = 0, prev = 0, written = 0, sv_clock = 0, npatch = 0;
     uint64_t clock = 0;
     bool insec = false, copying = false, sv_stop = false, first = false;
+    uint64_t t_tab = 0, t_walk = 0, n_win = 0, n_str = 0;
     __syncthreads();
     while (!s_bad && !s_done) {
+      const uint64_t tw0 = __builtin_amdgcn_s_memrealtime();
       const uint32_t wb = s_p & ~15u;
       const uint32_t wl = wb + TW + TMARG < len ? wb + TW + TMARG : len;
       const uint32_t lim = wl - wb, wn = lim < TW ? lim : TW;
@@ -944,39 +948,44 @@ __global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, uint8_t *done, con
         T.fl[o] = (uint8_t)(ok ? TV | ((fl & F_SKIP) ? 1 : 0) | ((fl & F_PATCH) ? 2 : 0) : 0);
       }
       __syncthreads();
-      if (t == 0) {
-        uint32_t p = s_p, why = 0;
+      const uint64_t tw1 = __builtin_amdgcn_s_memrealtime();
+      t_tab += tw1 - tw0;
+      n_win++;
+      if (wv == 0) {  // wave 0 in lockstep: every lane the same values (LDS reads made uniform), state in SGPRs
+        uint32_t p = RF(s_p), why = 0;
+        bool fin = false;
         const uint32_t wend = wb + wn;
         for (;;) {
           if (!insec) {  // a section header: vu(#structs) vu(client) vu(clock)
-            if (ci == nsec) { s_done = 1; break; }
+            if (ci == nsec) { fin = true; break; }
             if (p >= wend) { if (wend >= len) why = 7; break; }
             bool bad = false;
             uint32_t ns, first_clock;
             if (p + 16 <= wl) {
               uint32_t o = p - wb;
-              ns = tab_vu(T.b, o, lim, bad);
-              client = tab_vu(T.b, o, lim, bad);
-              first_clock = tab_vu(T.b, o, lim, bad);
-              p = wb + o;
+              ns = RF(tab_vu(T.b, o, lim, bad));
+              client = RF(tab_vu(T.b, o, lim, bad));
+              first_clock = RF(tab_vu(T.b, o, lim, bad));
+              p = wb + RF(o);
+              bad = RF(bad ? 1u : 0u) != 0;
             } else {
               ln::LCur c = ln::make(D, p, len);
-              ns = ln::rvu(c);
-              client = ln::rvu(c);
-              first_clock = ln::rvu(c);
-              p = c.p;
-              bad = c.bad;
+              ns = RF(ln::rvu(c));
+              client = RF(ln::rvu(c));
+              first_clock = RF(ln::rvu(c));
+              p = RF(c.p);
+              bad = RF(c.bad ? 1u : 0u) != 0;
             }
             if (bad) { why = 5; break; }
             // each section a new client (the writer merges consecutive parts of one client); meta: descending
             if (ns == 0 || (ci > 0 && client == prev) || (OP == OP_META && ci > 0 && client > prev)) { why = 6; break; }
             prev = client;
-            msec(ci, M_X0) = p; msec(ci, M_W) = ns; msec(ci, M_CLIENT) = client; msec(ci, M_CLOCK) = first_clock;
+            if (lane == 0) { msec(ci, M_X0) = p; msec(ci, M_W) = ns; msec(ci, M_CLIENT) = client; msec(ci, M_CLOCK) = first_clock; }
             k = 0;
             if (OP == OP_DIFF) {
               uint32_t h = (client * 0x9E3779B1u) >> 20;
-              while (mval[h] != 0) {
-                if (mkey[h] == client) { k = svclk[mval[h] - 1]; break; }
+              while (RF(mval[h]) != 0) {
+                if (RF(mkey[h]) == client) { k = RF(svclk[RF(mval[h]) - 1]); break; }
                 h = (h + 1) & (MSVSLOTS - 1);
               }
             }
@@ -991,13 +1000,15 @@ __global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, uint8_t *done, con
             continue;
           }
           if (rem == 0) {  // the section's end
-            msec(ci, M_END) = (uint32_t)clock;
-            msec(ci, M_VAL) = sv_clock;
-            if (OP == OP_DIFF) {
-              msec(ci, M_WRITTEN) = copying ? written : 0;
-              if (!copying) msec(ci, M_PRELEN) = NONE;
+            if (lane == 0) {
+              msec(ci, M_END) = (uint32_t)clock;
+              msec(ci, M_VAL) = sv_clock;
+              if (OP == OP_DIFF) {
+                msec(ci, M_WRITTEN) = copying ? written : 0;
+                if (!copying) msec(ci, M_PRELEN) = NONE;
+              }
+              msec(ci, M_X1) = p;
             }
-            msec(ci, M_X1) = p;
             ci++;
             insec = false;
             continue;
@@ -1005,13 +1016,16 @@ __global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, uint8_t *done, con
           // one struct
           if (p >= wend) { if (wend >= len) why = 7; break; }
           const uint32_t o = p - wb;
-          uint32_t fl = T.fl[o], nx, cl;
+          uint32_t fl = RF(T.fl[o]), nx, cl;
           if (fl & TV) {
-            nx = p + T.nx[o];
-            cl = T.len[o];
+            nx = p + RF(T.nx[o]);
+            cl = RF(T.len[o]);
           } else {
             uint32_t f2;
-            if (!ln::parse_fast(D, p, len, nx, cl, f2) && !ln::parse_struct(D, p, len, nx, cl, f2)) { why = 8; break; }
+            if (RF(ln::parse_fast(D, p, len, nx, cl, f2) || ln::parse_struct(D, p, len, nx, cl, f2) ? 1u : 0u) == 0) { why = 8; break; }
+            nx = RF(nx);
+            cl = RF(cl);
+            f2 = RF(f2);
             fl = TV | ((f2 & F_SKIP) ? 1 : 0) | ((f2 & F_PATCH) ? 2 : 0);
           }
           if (cl >= (1u << 24)) { why = 9; break; }
@@ -1039,14 +1053,18 @@ __global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, uint8_t *done, con
                   b0 = p;
                   patch = true;
                 } else {
-                  if (!slice_head(B, adj, p, nx, client, clock, cl, off, M.pre + (uint64_t)ci * PRE, prelen, a0, a1)) { why = 11; break; }
+                  // (every lane computes the head; the lanes store the same bytes)
+                  if (RF(slice_head(B, adj, p, nx, client, clock, cl, off, M.pre + (uint64_t)ci * PRE, prelen, a0, a1) ? 1u : 0u) == 0) { why = 11; break; }
+                  prelen = RF(prelen); a0 = RF(a0); a1 = RF(a1);
                   b0 = nx;
                 }
-                msec(ci, M_PRELEN) = prelen;
-                msec(ci, M_A0) = a0;
-                msec(ci, M_A1) = a1;
-                msec(ci, M_B0) = b0;
-                msec(ci, M_FCLOCK) = (uint32_t)(clock + off);
+                if (lane == 0) {
+                  msec(ci, M_PRELEN) = prelen;
+                  msec(ci, M_A0) = a0;
+                  msec(ci, M_A1) = a1;
+                  msec(ci, M_B0) = b0;
+                  msec(ci, M_FCLOCK) = (uint32_t)(clock + off);
+                }
               }
             } else {
               written++;
@@ -1054,20 +1072,26 @@ __global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, uint8_t *done, con
             }
             if (patch && (fl & 2)) {  // the info byte re-encoded: 0x20 cleared with an origin, GC := 0
               if (npatch >= MSPATCH) { why = 12; break; }
-              const uint32_t info = o < lim ? T.b[o] : D[p];
-              M.ppos[npatch] = p;
-              M.psec[npatch] = ci;
-              M.pval[npatch] = (uint8_t)((info & 31) == 0 ? 0 : info & ~0x20u);
+              const uint32_t info = RF(o < lim ? T.b[o] : D[p]);
+              if (lane == 0) {
+                M.ppos[npatch] = p;
+                M.psec[npatch] = ci;
+                M.pval[npatch] = (uint8_t)((info & 31) == 0 ? 0 : info & ~0x20u);
+              }
               npatch++;
             }
           }
           clock = end;
           p = nx;
           rem--;
+          n_str++;
         }
-        s_p = p;
-        if (why) { s_bad = 1; s_why = why; }
-        if (s_done) { s_ds0 = p; s_npatch = npatch; }
+        t_walk += __builtin_amdgcn_s_memrealtime() - tw1;
+        if (lane == 0) {
+          s_p = p;
+          if (why) { s_bad = 1; s_why = why; }
+          if (fin) { s_done = 1; s_ds0 = p; s_npatch = npatch; }
+        }
       }
       __syncthreads();
     }
@@ -1080,7 +1104,10 @@ __global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, uint8_t *done, con
     }
     const uint64_t tm1 = __builtin_amdgcn_s_memrealtime();
     const uint64_t tm2 = tm1;
-    if (t == 0) { atomicAdd(&pw_prof[0], tm1 - tm0); }
+    if (t == 0) {
+      atomicAdd(&pw_prof[0], tm1 - tm0);
+      atomicAdd(&pw_prof[8], t_tab); atomicAdd(&pw_prof[9], t_walk); atomicAdd(&pw_prof[10], n_win); atomicAdd(&pw_prof[11], n_str);
+    }
     // ---- C
     if (OP != OP_DIFF) {  // state vector / meta: one entry per section, written by one thread
       if (t == 0) {
@@ -1337,7 +1364,7 @@ extern "C" int ym__pw_ticks(unsigned long long *host, int reset) {  // 16 words
   return r;
 }
 extern "C" int ym__pw_prof(unsigned long long *host, int reset) {
-  int r = (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ymk::pw::pw_prof), 64);
-  if (reset) { unsigned long long z[8] = {}; hipMemcpyToSymbol(HIP_SYMBOL(ymk::pw::pw_prof), z, 64); }
+  int r = (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ymk::pw::pw_prof), 128);
+  if (reset) { unsigned long long z[16] = {}; hipMemcpyToSymbol(HIP_SYMBOL(ymk::pw::pw_prof), z, 128); }
   return r;
 }
