@@ -1241,6 +1241,337 @@ __global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, uint8_t *done, con
 }
 #undef msec
 
+// ---- 4. small documents: one wave per document, the whole update in one LDS window ---------------------
+// The sync server's SyncStep1 -> SyncStep2 load: diffUpdate / encodeStateVectorFromUpdate / parseUpdateMeta
+// over merged C2-size documents (~1-2 KB, a few to tens of client sections, ~100 structs).  k_pw_ms's table
+// walk at one wave: the wave stages the update (<= SW_MAX bytes) and parses a struct at every byte offset
+// (one packed word per offset: next delta, Skip / patch flags, clock length); the wave then follows the
+// chain in lockstep (every lane the same values, LDS reads made uniform: the chain's state in SGPRs), one
+// table lookup per struct, doing the per-section work on the way (state-vector rules, the diff's cut and
+// sliced head, info-byte patches) into LDS section records; the delete set is validated by the same
+// lockstep walk (canonical varuints, no empty or repeated client); then lane ci sizes / writes section ci
+// (wave prefix sums place them) and the wave copies the spans.  Same acceptance and bytes as k_pw_ms /
+// k_big_v1 (a document this declines keeps done[d] == 0: the lane-per-document kernels and k_big_v1 follow).
+constexpr uint32_t SW_MIN = 80, SW_MAX = 2048, SW_NSEC = 64, SW_NSV = 128, SW_SVS = 256, SW_NPATCH = 512, SW_DHS = 256;
+constexpr uint32_t SW_TV = 1u << 13, SW_CLEN = 1u << 18;  // table word: delta (11 bits) | skip << 11 | patch << 12 | TV | clen << 14
+enum { Q_W = 0, Q_CLIENT, Q_CLOCK, Q_X1, Q_PRELEN, Q_A0, Q_A1, Q_B0, Q_WRITTEN, Q_FCLOCK, Q_VAL, Q_END, Q_OUT, NQ = 13 };
+struct SwLds {
+  uint8_t b[SW_MAX + 48];
+  uint32_t tab[SW_MAX];
+  uint32_t sec[SW_NSEC][NQ];
+  uint8_t pre[SW_NSEC][PRE];
+  uint16_t ppos[SW_NPATCH];
+  uint8_t psec[SW_NPATCH], pval[SW_NPATCH];
+  uint32_t mkey[SW_SVS], mval[SW_SVS], svclk[SW_NSV];
+  uint32_t dhs[SW_DHS];
+};
+// lockstep lib0 readVarUint over the LDS bytes (uniform o): canonical, u32
+__device__ __forceinline__ uint32_t sw_vu(const uint8_t *b, uint32_t &o, uint32_t lim, bool &bad) {
+  uint32_t v = 0, nb = 0, x = 0x80;
+  while ((x & 0x80) && nb < 5) {
+    x = o + nb < lim ? RF(b[o + nb]) : 0x80;
+    v |= (x & 0x7f) << (7 * nb);
+    nb++;
+  }
+  bad |= (x & 0x80) || (nb > 1 && x == 0) || (nb == 5 && (x & 0x70) != 0);
+  o += nb;
+  return v;
+}
+
+template <int OP>
+__global__ void __launch_bounds__(64) k_pw_small(GeneralJob j, uint8_t *done) {
+  __shared__ SwLds L;
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
+    const uint32_t u0 = j.doc_upd[d];
+    if (j.doc_upd[d + 1] - u0 != 1 || done[d]) continue;
+    const uint64_t ub = j.upd_off[u0];
+    const uint64_t len64 = j.upd_off[u0 + 1] - ub;
+    if (len64 <= SW_MIN || len64 > SW_MAX) continue;  // (tiny updates: the lane-per-document kernel)
+    const uint32_t len = (uint32_t)len64;
+    const uint8_t *D = j.A + ub;
+    sc::cu32 *const B = sc::base_of(D);
+    const uint32_t adj = (uint32_t)(ub & 3);
+    __syncthreads();
+    for (uint32_t q = 16 * lane; q < len + 48; q += 16 * 64) {
+      const uint4 v = wds::load16m(D, q, len);
+      __builtin_memcpy(L.b + q, &v, 16);
+    }
+    uint32_t why = 0;
+    bool bad = false;
+    // the state vector (diff): decodeStateVector into the LDS hash map (a later entry wins), in lockstep
+    if (OP == OP_DIFF) {
+      for (uint32_t q = lane; q < SW_SVS; q += 64) L.mval[q] = 0;
+      const uint64_t s0 = j.sv_off[d], s1 = j.sv_off[d + 1];
+      __syncthreads();
+      if (s1 - s0 > (1u << 20)) {
+        why = 3;
+      } else {
+        ln::LCur sv = ln::make(j.sv + s0, 0, (uint32_t)(s1 - s0));
+        const uint32_t ns = RF(ln::rvu(sv));
+        if (RF(sv.bad ? 1u : 0u) || ns > SW_NSV) why = 3;
+        for (uint32_t q = 0; q < ns && !why; q++) {
+          const uint32_t cl = RF(ln::rvu(sv)), ck = RF(ln::rvu(sv));
+          if (RF(sv.bad ? 1u : 0u)) { why = 3; break; }
+          if (lane == 0) L.svclk[q] = ck;
+          uint32_t h = (cl * 0x9E3779B1u) >> 24;
+          while (RF(L.mval[h]) != 0 && RF(L.mkey[h]) != cl) h = (h + 1) & (SW_SVS - 1);
+          if (lane == 0) { L.mkey[h] = cl; L.mval[h] = q + 1; }
+          __syncthreads();
+        }
+      }
+      if (why) PW_DECLINE()
+    }
+    __syncthreads();
+    // the tables: a struct parsed at every offset
+    for (uint32_t o = lane; o < len; o += 64) {
+      uint32_t nx, cl, fl;
+      const bool ok = ln::parse_fast(L.b, o, len, nx, cl, fl) || ln::parse_struct(L.b, o, len, nx, cl, fl, len);
+      L.tab[o] = ok && cl < SW_CLEN ? (nx - o) | ((fl & F_SKIP) ? 1u << 11 : 0) | ((fl & F_PATCH) ? 1u << 12 : 0) | SW_TV | (cl << 14) : 0;
+    }
+    __syncthreads();
+    // the chain, in lockstep
+    uint32_t o = 0;
+    const uint32_t nsec = sw_vu(L.b, o, len, bad);
+    uint32_t p = o, npatch = 0, prev = 0;
+    if (bad || nsec > SW_NSEC) PW_DECLINE_R(2)
+    for (uint32_t ci = 0; ci < nsec && !why; ci++) {
+      uint32_t q = p;
+      const uint32_t ns = sw_vu(L.b, q, len, bad), client = sw_vu(L.b, q, len, bad), first_clock = sw_vu(L.b, q, len, bad);
+      p = q;
+      if (bad) { why = 5; break; }
+      if (ns == 0 || (ci > 0 && client == prev) || (OP == OP_META && ci > 0 && client > prev)) { why = 6; break; }
+      prev = client;
+      uint32_t k = 0;
+      if (OP == OP_DIFF) {
+        uint32_t h = (client * 0x9E3779B1u) >> 24;
+        while (RF(L.mval[h]) != 0) {
+          if (RF(L.mkey[h]) == client) { k = RF(L.svclk[RF(L.mval[h]) - 1]); break; }
+          h = (h + 1) & (SW_SVS - 1);
+        }
+      }
+      uint64_t clock = first_clock;
+      bool sv_stop = clock != 0, first = ci == 0, copying = false;
+      uint32_t sv_clock = 0, written = 0;
+      for (uint32_t r = 0; r < ns; r++) {
+        if (p >= len) { why = 7; break; }
+        const uint32_t w = RF(L.tab[p]);
+        uint32_t nx, cl, fl;
+        if (w & SW_TV) {
+          nx = p + (w & 2047u);
+          cl = w >> 14;
+          fl = (w >> 11) & 3;
+        } else {
+          uint32_t f2;
+          if (RF(ln::parse_struct(L.b, p, len, nx, cl, f2, len) ? 1u : 0u) == 0) { why = 8; break; }
+          nx = RF(nx);
+          cl = RF(cl);
+          f2 = RF(f2);
+          fl = ((f2 & F_SKIP) ? 1 : 0) | ((f2 & F_PATCH) ? 2 : 0);
+        }
+        if (cl >= (1u << 24)) { why = 9; break; }
+        if (clock + cl > 0xffffffffull) { why = 10; break; }
+        const bool skip = fl & 1;
+        const uint64_t end = clock + cl;
+        if (OP == OP_SV) {
+          if (first) {
+            first = false;
+            if (!sv_stop) sv_clock = (uint32_t)end;
+            if (skip) sv_stop = true;
+          } else if (!sv_stop) {
+            if (skip) sv_stop = true;
+            else sv_clock = (uint32_t)end;
+          }
+        } else if (OP == OP_DIFF) {
+          bool patch = false;
+          if (!copying) {
+            if (!skip && end > k) {  // the cut: the first struct that ends past sv[client]
+              copying = true;
+              written = 1;
+              const uint32_t off = k > clock ? (uint32_t)(k - clock) : 0;
+              uint32_t prelen = 0, a0 = 0, a1 = 0, b0;
+              if (off == 0) {
+                b0 = p;
+                patch = true;
+              } else {
+                if (RF(slice_head(B, adj, p, nx, client, clock, cl, off, L.pre[ci], prelen, a0, a1) ? 1u : 0u) == 0) { why = 11; break; }
+                prelen = RF(prelen); a0 = RF(a0); a1 = RF(a1);
+                b0 = nx;
+              }
+              if (lane == 0) {
+                L.sec[ci][Q_PRELEN] = prelen;
+                L.sec[ci][Q_A0] = a0;
+                L.sec[ci][Q_A1] = a1;
+                L.sec[ci][Q_B0] = b0;
+                L.sec[ci][Q_FCLOCK] = (uint32_t)(clock + off);
+              }
+            }
+          } else {
+            written++;
+            patch = true;
+          }
+          if (patch && (fl & 2)) {  // the info byte re-encoded: 0x20 cleared with an origin, GC := 0
+            if (npatch >= SW_NPATCH) { why = 12; break; }
+            const uint32_t info = RF(L.b[p]);
+            if (lane == 0) {
+              L.ppos[npatch] = (uint16_t)p;
+              L.psec[npatch] = (uint8_t)ci;
+              L.pval[npatch] = (uint8_t)((info & 31) == 0 ? 0 : info & ~0x20u);
+            }
+            npatch++;
+          }
+        }
+        clock = end;
+        p = nx;
+      }
+      if (why) break;
+      if (lane == 0) {
+        L.sec[ci][Q_W] = ns;
+        L.sec[ci][Q_CLIENT] = client;
+        L.sec[ci][Q_CLOCK] = first_clock;
+        L.sec[ci][Q_END] = (uint32_t)clock;
+        L.sec[ci][Q_VAL] = sv_clock;
+        L.sec[ci][Q_X1] = p;
+        if (OP == OP_DIFF) {
+          L.sec[ci][Q_WRITTEN] = copying ? written : 0;
+          if (!copying) L.sec[ci][Q_PRELEN] = NONE;
+        }
+      }
+    }
+    if (why) PW_DECLINE()
+    const uint32_t ds0 = p;
+    uint32_t ds1 = 0;
+    if (OP == OP_DIFF) {  // the delete set: readDeleteSet's varuints canonical, no empty and no repeated client
+      for (uint32_t q = lane; q < SW_DHS; q += 64) L.dhs[q] = NONE;
+      __syncthreads();
+      uint32_t q = p;
+      const uint32_t ndc = sw_vu(L.b, q, len, bad);
+      bool seen_max = false;
+      if (bad || ndc > SW_DHS / 2) why = 17;
+      for (uint32_t c = 0; c < ndc && !why; c++) {
+        const uint32_t client = sw_vu(L.b, q, len, bad), m = sw_vu(L.b, q, len, bad);
+        if (bad || m == 0) { why = 17; break; }
+        if (client == NONE) {
+          if (seen_max) { why = 17; break; }
+          seen_max = true;
+        } else {
+          uint32_t h = (client * 0x9E3779B1u) >> 24;
+          for (;;) {
+            const uint32_t x = RF(L.dhs[h]);
+            if (x == client) { why = 17; break; }
+            if (x == NONE) break;
+            h = (h + 1) & (SW_DHS - 1);
+          }
+          if (why) break;
+          if (lane == 0) L.dhs[h] = client;
+          __syncthreads();
+        }
+        for (uint32_t r = 0; r < 2 * m && !bad; r++) sw_vu(L.b, q, len, bad);
+        if (bad) { why = 17; break; }
+      }
+      ds1 = q;
+      if (why) PW_DECLINE()
+    }
+    __syncthreads();
+    // outputs
+    const uint32_t ci = lane;
+    const bool live = ci < nsec;
+    if (OP != OP_DIFF) {
+      // state vector: vu(#entries) | per section with a value: client, value; meta: vu(nsec) | client, first
+      // clock ... | vu(nsec) | client, end ...
+      uint32_t sz = 0, sz2 = 0, cnt = 0;
+      if (live) {
+        if (OP == OP_SV) {
+          const uint32_t v = L.sec[ci][Q_VAL];
+          cnt = v != 0;
+          sz = v ? vsz(L.sec[ci][Q_CLIENT]) + vsz(v) : 0;
+        } else {
+          sz = vsz(L.sec[ci][Q_CLIENT]) + vsz(L.sec[ci][Q_CLOCK]);
+          sz2 = vsz(L.sec[ci][Q_CLIENT]) + vsz(L.sec[ci][Q_END]);
+        }
+      }
+      const uint32_t i1 = wave_incl_add(sz), i2 = wave_incl_add(sz2), ic = wave_incl_add(cnt);
+      const uint32_t t1 = lane_read(i1, 63), t2 = lane_read(i2, 63), tc = lane_read(ic, 63);
+      const uint32_t h1 = vsz(OP == OP_SV ? tc : nsec), h2 = OP == OP_META ? vsz(nsec) : 0;
+      const uint32_t total = h1 + t1 + h2 + t2;
+      uint64_t base = 0;
+      if (lane == 0) base = atomicAdd((unsigned long long *)j.used, (unsigned long long)total);
+      base = ((uint64_t)RF((uint32_t)(base >> 32)) << 32) | RF((uint32_t)base);
+      if (lane == 0) { done[d] = 1; atomicAdd((unsigned long long *)j.pw_count, 1ull); }
+      if (base + total > j.cap) {
+        if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }
+        continue;
+      }
+      uint8_t *o = j.out + base;
+      if (lane == 0) put_vu_g(o, 0, OP == OP_SV ? tc : nsec);
+      if (live && sz) {
+        const uint32_t q = put_vu_g(o, h1 + i1 - sz, L.sec[ci][Q_CLIENT]);
+        put_vu_g(o, q, OP == OP_SV ? L.sec[ci][Q_VAL] : L.sec[ci][Q_CLOCK]);
+      }
+      if (OP == OP_META) {
+        if (lane == 0) put_vu_g(o, h1 + t1, nsec);
+        if (live) put_vu_g(o, put_vu_g(o, h1 + t1 + h2 + i2 - sz2, L.sec[ci][Q_CLIENT]), L.sec[ci][Q_END]);
+      }
+      if (lane == 0) {
+        j.out_off[d] = base;
+        j.out_len[d] = total;
+        j.status[d] = ym::ST_OK;
+      }
+      continue;
+    }
+    // diff: kept sections' parts (header, sliced head, spans), then the delete set verbatim
+    uint32_t sz = 0, kept = 0;
+    if (live && L.sec[ci][Q_PRELEN] != NONE) {
+      kept = 1;
+      sz = vsz(L.sec[ci][Q_WRITTEN]) + vsz(L.sec[ci][Q_CLIENT]) + vsz(L.sec[ci][Q_FCLOCK]) + L.sec[ci][Q_PRELEN] +
+           (L.sec[ci][Q_A1] - L.sec[ci][Q_A0]) + (L.sec[ci][Q_X1] - L.sec[ci][Q_B0]);
+    }
+    const uint32_t wi = wave_incl_add(sz), wk = wave_incl_add(kept);
+    const uint32_t acc = lane_read(wi, 63), nparts = lane_read(wk, 63);
+    const uint32_t p0 = vsz(nparts);
+    const uint64_t total = p0 + (uint64_t)acc + (ds1 - ds0);
+    uint64_t base = 0;
+    if (lane == 0) base = atomicAdd((unsigned long long *)j.used, (unsigned long long)total);
+    base = ((uint64_t)RF((uint32_t)(base >> 32)) << 32) | RF((uint32_t)base);
+    if (lane == 0) { done[d] = 1; atomicAdd((unsigned long long *)j.pw_count, 1ull); }
+    if (base + total > j.cap) {
+      if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }
+      continue;
+    }
+    uint8_t *const out = j.out + base;
+    if (lane == 0) put_vu_g(out, 0, nparts);
+    if (kept) {  // header and sliced head; the section's span placement for the patches
+      const uint32_t pl = L.sec[ci][Q_PRELEN];
+      uint32_t q = put_vu_g(out, p0 + wi - sz, L.sec[ci][Q_WRITTEN]);
+      q = put_vu_g(out, q, L.sec[ci][Q_CLIENT]);
+      q = put_vu_g(out, q, L.sec[ci][Q_FCLOCK]);
+      for (uint32_t x = 0; x < pl; x++) out[q + x] = L.pre[ci][x];
+      q += pl;
+      L.sec[ci][Q_OUT] = q;
+    }
+    __syncthreads();
+    // the spans, section by section, 64 bytes per step from LDS
+    for (uint32_t c = 0; c < nsec; c++) {
+      const uint32_t pl = RF(L.sec[c][Q_PRELEN]);
+      if (pl == NONE) continue;
+      uint32_t q = RF(L.sec[c][Q_OUT]);
+      const uint32_t a0 = RF(L.sec[c][Q_A0]), a1 = RF(L.sec[c][Q_A1]), b0 = RF(L.sec[c][Q_B0]), x1 = RF(L.sec[c][Q_X1]);
+      for (uint32_t x = lane; x < a1 - a0; x += 64) out[q + x] = L.b[a0 + x];
+      q += a1 - a0;
+      for (uint32_t x = lane; x < x1 - b0; x += 64) out[q + x] = L.b[b0 + x];
+      if (lane == 0) L.sec[c][Q_OUT] = q - b0;  // output position = document position + this
+    }
+    for (uint32_t x = lane; x < ds1 - ds0; x += 64) out[p0 + acc + x] = L.b[ds0 + x];
+    __syncthreads();
+    for (uint32_t i = lane; i < npatch; i += 64) out[L.sec[L.psec[i]][Q_OUT] + L.ppos[i]] = L.pval[i];
+    if (lane == 0) {
+      j.out_off[d] = base;
+      j.out_len[d] = total;
+      j.status[d] = ym::ST_OK;
+    }
+  }
+}
+
 }  // namespace pw
 
 #define PWCHK(x)                                  \
@@ -1297,6 +1628,14 @@ int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const ui
   *done_out = done;  // every document is marked (0 = not taken) from here on
   pw_last_done = done;
   const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
+  // small single updates: one wave per document (YMERGE_NO_PWSMALL: off)
+  static const bool no_small = getenv("YMERGE_NO_PWSMALL") != nullptr;
+  if (!no_small) {
+    const uint32_t gs = j.n < 65536 ? j.n : 65536;
+    if (op == OP_DIFF) k_pw_small<OP_DIFF><<<gs, 64, 0, st>>>(j, done);
+    else if (op == OP_SV) k_pw_small<OP_SV><<<gs, 64, 0, st>>>(j, done);
+    else k_pw_small<OP_META><<<gs, 64, 0, st>>>(j, done);
+  }
   // many-section documents: the table walk (no chunk records)
   if (mtotal > 0) {
     if (pw_ensure(B, 4, mtotal + 256)) {  // no room for the section tables: k_big_v1 takes those documents
