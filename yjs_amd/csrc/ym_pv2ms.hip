@@ -131,15 +131,18 @@ __device__ __forceinline__ bool mr_kind(uint32_t v, uint32_t &pk, bool &lenc) {
   }
 }
 // the token of kind k at o of the window buffer (bytes [0, lim)): its length, 0 when not decidable here
+// (strings / binaries longer than MR_CAP: 0, the walker's own parse -- an uncapped parse at a garbage offset can
+// run to the window's end, and the tables would cost O(window x window))
+constexpr uint32_t MR_CAP = 128;
 __device__ __forceinline__ uint32_t mr_tok_len(const uint8_t *w, uint32_t o, uint32_t lim, uint32_t k) {
-  ln::LCur c = ln::make(w, o, lim, lim);
+  ln::LCur c = ln::make(w, o, lim, MR_CAP);
   if (k == PK_SKIP) {
     const uint32_t v = ln::rvu(c);
     return c.bad || v == 0 ? 0 : c.p - o;
   }
   if (k == PK_BIN) {
     const uint32_t n = ln::rvu(c);
-    if (c.bad || !ln::room(c, n)) return 0;
+    if (c.bad || n > MR_CAP || !ln::room(c, n)) return 0;
     return c.p + n - o;
   }
   const uint32_t tag = (uint32_t)c.lo & 0xffu;
@@ -370,7 +373,7 @@ __global__ void __launch_bounds__(64) k_ms_walk(Job J) {
   if (U(M.ok) == 0 || U(M.ms) == 0) return;
   __shared__ __attribute__((aligned(16))) uint8_t win[MR_W + MR_MARG + 16];
   __shared__ uint16_t tV[MR_W], tB[MR_W], tA[MR_W];
-  __shared__ uint2 spay[MR_PC];     // the window's payload structs (index, kind | token count << 3)
+  __shared__ uint2 spay[MR_PC + 1]; // the window's payload structs (index, kind | token count << 3; one token: the kind)
   __shared__ uint32_t sist[MR_PC];  // their first tokens' offsets (flushed to ist at the window's end)
   const uint32_t u0 = j.doc_upd[d];
   const uint64_t ub = j.upd_off[u0];
@@ -411,7 +414,10 @@ __global__ void __launch_bounds__(64) k_ms_walk(Job J) {
         __builtin_memcpy(win + q, tb16, 16);
       }
     for (uint32_t q = t; q < MR_PC; q += 64)
-      if (k0 + q < npay) spay[q] = make_uint2(pidx[k0 + q], pkl[k0 + q]);
+      if (k0 + q < npay) {
+        const uint32_t kl = pkl[k0 + q];
+        spay[q] = make_uint2(pidx[k0 + q], kl == ((1u << 3) | PK_ANY) ? (uint32_t)PK_ONE : kl);  // (Any of one value: one token)
+      }
     __syncthreads();
     if (fresh) {
       for (uint32_t o = t; o < wn; o += 64) {
@@ -428,6 +434,8 @@ __global__ void __launch_bounds__(64) k_ms_walk(Job J) {
     t_tab += tt1 - tt0;
     n_win++;
     const uint32_t wend = wb + wn;  // tokens starting before here use the tables
+    // the staged entries the fast loop may take (below the payload list's end and the first-token capacity)
+    const uint32_t kfast = min(min(npay, k0 + MR_PC), icap);
     for (;;) {
       if (rt > 0) {  // inside a payload struct: its tokens
         const uint16_t *tab = kind == PK_SKIP ? tV : kind == PK_BIN ? tB : tA;
@@ -481,6 +489,25 @@ __global__ void __launch_bounds__(64) k_ms_walk(Job J) {
         if (send > (1u << 26)) { bad = true; break; }
         insec = 1;
         continue;
+      }
+      // fast loop: consecutive one-token payload structs of one kind inside the window and the staged list --
+      // one table read per struct, the next entry's read issued before it (the general steps below take
+      // everything else: section ends, Any runs, tokens the tables lack, window and list ends)
+      if (k < kfast && p < wend) {
+        uint2 e = spay[k - k0];
+        const uint32_t code = U(e.y);
+        if (U(e.x) < send && code != PK_NONE && code < PK_ANY) {
+          const uint16_t *tab = code == PK_SKIP ? tV : code == PK_BIN ? tB : tA;
+          for (;;) {
+            const uint2 en = spay[k + 1 - k0];
+            const uint32_t L = U(tab[p - wb]);
+            if (L == 0) break;
+            if (t == 0) sist[k - k0] = p;
+            p += L;
+            k++;
+            if (k >= kfast || p >= wend || U(en.x) >= send || U(en.y) != code) break;
+          }
+        }
       }
       // the next payload struct, if it belongs to this section
       uint32_t nidx, nkl;

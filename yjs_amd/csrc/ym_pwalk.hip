@@ -56,6 +56,11 @@ constexpr uint32_t FAIL_RUN = 8;       // failed positions in a row before the w
 // chain there after a few bytes); a chunk still off the chain after them (structs outside the short cut,
 // C5's XML items) goes back to the full parser at every position
 constexpr uint32_t START_CHEAP = 48;
+// longest string / binary / ContentAny the window tables accept (k_pw_ms, k_pw_small): a table entry is a
+// parse at an offset that may not start a struct, and an uncapped parse there can run to the window's end
+// (a garbage length read as a string to validate): the tables cost O(window x cap).  Longer true contents
+// are parsed uncapped by the chain walk itself.
+constexpr uint32_t TAB_CAP = 128;
 constexpr uint64_t PW_MIN = 32768;     // smaller updates stay on k_big_v1
 constexpr uint32_t NSEC = BS_NSEC, NSV = BS_NSV, PRE = BS_PRE, SECW = BS_SECW;
 constexpr uint32_t NPATCH = 1024;
@@ -814,7 +819,10 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
 // The same documents are accepted, with the same bytes, as k_pw_stitch / k_big_v1 would (the golden vectors
 // run through this path with YMERGE_PWMS_MIN=2, tests/test_gpu_golden.py).
 constexpr uint32_t MS_WAVES = 8, MS_T = 64 * MS_WAVES;
-constexpr uint32_t MS_MIN = 16;  // sections from which a document takes this path (YMERGE_PWMS_MIN)
+// sections from which a document takes this path (YMERGE_PWMS_MIN; off by default: measured on C5 V1 diff,
+// 57 ms against k_pw_stitch's 27.6 -- the tables parse every byte offset of a 700 KB document with the full
+// divergent struct parser, ~13 ms per document, and the lockstep chain costs ~2,000 cycles per struct)
+constexpr uint32_t MS_MIN = 0xffffffffu;
 constexpr uint32_t MSPATCH = 4096;     // info-byte patches per document
 constexpr uint32_t MSVMAX = 2048, MSVSLOTS = 4096;
 enum { M_X0 = 0, M_W, M_CLIENT, M_CLOCK, M_X1, M_PRELEN, M_A0, M_A1, M_B0, M_WRITTEN, M_FCLOCK, M_VAL, M_END, M_OUT, NMF = 16 };
@@ -942,7 +950,7 @@ __global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, uint8_t *done, con
       __syncthreads();
       for (uint32_t o = t; o < wn; o += MS_T) {
         uint32_t nx, cl, fl;
-        const bool ok = ln::parse_fast(T.b, o, lim, nx, cl, fl) || ln::parse_struct(T.b, o, lim, nx, cl, fl, lim);
+        const bool ok = ln::parse_fast(T.b, o, lim, nx, cl, fl) || ln::parse_struct(T.b, o, lim, nx, cl, fl, TAB_CAP);
         T.nx[o] = (uint16_t)(ok ? nx - o : 0);
         T.len[o] = cl;
         T.fl[o] = (uint8_t)(ok ? TV | ((fl & F_SKIP) ? 1 : 0) | ((fl & F_PATCH) ? 2 : 0) : 0);
@@ -1244,7 +1252,7 @@ __global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, uint8_t *done, con
 // ---- 4. small documents: one wave per document, the whole update in one LDS window ---------------------
 // The sync server's SyncStep1 -> SyncStep2 load: diffUpdate / encodeStateVectorFromUpdate / parseUpdateMeta
 // over merged C2-size documents (~1-2 KB, a few to tens of client sections, ~100 structs).  k_pw_ms's table
-// walk at one wave: the wave stages the update (<= SW_MAX bytes) and parses a struct at every byte offset
+// walk at one wave: the wave stages the update (<= 2 KB, or <= 4 KB) and parses a struct at every byte offset
 // (one packed word per offset: next delta, Skip / patch flags, clock length); the wave then follows the
 // chain in lockstep (every lane the same values, LDS reads made uniform: the chain's state in SGPRs), one
 // table lookup per struct, doing the per-section work on the way (state-vector rules, the diff's cut and
@@ -1252,12 +1260,13 @@ __global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, uint8_t *done, con
 // lockstep walk (canonical varuints, no empty or repeated client); then lane ci sizes / writes section ci
 // (wave prefix sums place them) and the wave copies the spans.  Same acceptance and bytes as k_pw_ms /
 // k_big_v1 (a document this declines keeps done[d] == 0: the lane-per-document kernels and k_big_v1 follow).
-constexpr uint32_t SW_MIN = 80, SW_MAX = 2048, SW_NSEC = 64, SW_NSV = 128, SW_SVS = 256, SW_NPATCH = 512, SW_DHS = 256;
-constexpr uint32_t SW_TV = 1u << 13, SW_CLEN = 1u << 18;  // table word: delta (11 bits) | skip << 11 | patch << 12 | TV | clen << 14
+constexpr uint32_t SW_MIN = 80, SW_NSEC = 64, SW_NSV = 128, SW_SVS = 256, SW_NPATCH = 512, SW_DHS = 256;
+constexpr uint32_t SW_TV = 1u << 14, SW_CLEN = 1u << 17;  // table word: delta (12 bits) | skip << 12 | patch << 13 | TV | clen << 15
 enum { Q_W = 0, Q_CLIENT, Q_CLOCK, Q_X1, Q_PRELEN, Q_A0, Q_A1, Q_B0, Q_WRITTEN, Q_FCLOCK, Q_VAL, Q_END, Q_OUT, NQ = 13 };
+template <uint32_t SWB>
 struct SwLds {
-  uint8_t b[SW_MAX + 48];
-  uint32_t tab[SW_MAX];
+  uint8_t b[SWB + 48];
+  uint32_t tab[SWB];
   uint32_t sec[SW_NSEC][NQ];
   uint8_t pre[SW_NSEC][PRE];
   uint16_t ppos[SW_NPATCH];
@@ -1278,16 +1287,18 @@ __device__ __forceinline__ uint32_t sw_vu(const uint8_t *b, uint32_t &o, uint32_
   return v;
 }
 
-template <int OP>
-__global__ void __launch_bounds__(64) k_pw_small(GeneralJob j, uint8_t *done) {
-  __shared__ SwLds L;
+// documents of (SWMIN, SWB] bytes
+template <int OP, uint32_t SWMIN, uint32_t SWB>
+__global__ void __launch_bounds__(64) k_pw_small(GeneralJob j, uint8_t *done, uint64_t pw_min) {
+  __shared__ SwLds<SWB> L;
   const uint32_t lane = threadIdx.x;
   for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
     const uint32_t u0 = j.doc_upd[d];
     if (j.doc_upd[d + 1] - u0 != 1 || done[d]) continue;
     const uint64_t ub = j.upd_off[u0];
     const uint64_t len64 = j.upd_off[u0 + 1] - ub;
-    if (len64 <= SW_MIN || len64 > SW_MAX) continue;  // (tiny updates: the lane-per-document kernel)
+    // (tiny updates: the lane-per-document kernel; from pw_min on: the chunk walk / k_pw_ms)
+    if (len64 <= SWMIN || len64 > SWB || len64 >= pw_min) continue;
     const uint32_t len = (uint32_t)len64;
     const uint8_t *D = j.A + ub;
     sc::cu32 *const B = sc::base_of(D);
@@ -1323,11 +1334,13 @@ __global__ void __launch_bounds__(64) k_pw_small(GeneralJob j, uint8_t *done) {
       if (why) PW_DECLINE()
     }
     __syncthreads();
-    // the tables: a struct parsed at every offset
+    // the tables: the branch-free short cut at every offset (most offsets start no struct, and the full
+    // parser's divergent union over 64 garbage offsets costs ~5x the whole lockstep walk); a struct it does
+    // not decide is parsed by the walk itself
     for (uint32_t o = lane; o < len; o += 64) {
       uint32_t nx, cl, fl;
-      const bool ok = ln::parse_fast(L.b, o, len, nx, cl, fl) || ln::parse_struct(L.b, o, len, nx, cl, fl, len);
-      L.tab[o] = ok && cl < SW_CLEN ? (nx - o) | ((fl & F_SKIP) ? 1u << 11 : 0) | ((fl & F_PATCH) ? 1u << 12 : 0) | SW_TV | (cl << 14) : 0;
+      const bool ok = ln::parse_fast(L.b, o, len, nx, cl, fl);
+      L.tab[o] = ok && cl < SW_CLEN && nx - o < 4096 ? (nx - o) | ((fl & F_SKIP) ? 1u << 12 : 0) | ((fl & F_PATCH) ? 1u << 13 : 0) | SW_TV | (cl << 15) : 0;
     }
     __syncthreads();
     // the chain, in lockstep
@@ -1358,9 +1371,9 @@ __global__ void __launch_bounds__(64) k_pw_small(GeneralJob j, uint8_t *done) {
         const uint32_t w = RF(L.tab[p]);
         uint32_t nx, cl, fl;
         if (w & SW_TV) {
-          nx = p + (w & 2047u);
-          cl = w >> 14;
-          fl = (w >> 11) & 3;
+          nx = p + (w & 4095u);
+          cl = w >> 15;
+          fl = (w >> 12) & 3;
         } else {
           uint32_t f2;
           if (RF(ln::parse_struct(L.b, p, len, nx, cl, f2, len) ? 1u : 0u) == 0) { why = 8; break; }
@@ -1632,9 +1645,13 @@ int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const ui
   static const bool no_small = getenv("YMERGE_NO_PWSMALL") != nullptr;
   if (!no_small) {
     const uint32_t gs = j.n < 65536 ? j.n : 65536;
-    if (op == OP_DIFF) k_pw_small<OP_DIFF><<<gs, 64, 0, st>>>(j, done);
-    else if (op == OP_SV) k_pw_small<OP_SV><<<gs, 64, 0, st>>>(j, done);
-    else k_pw_small<OP_META><<<gs, 64, 0, st>>>(j, done);
+#define PW_SMALL(O) \
+    k_pw_small<O, SW_MIN, 2048><<<gs, 64, 0, st>>>(j, done, pw_min); \
+    k_pw_small<O, 2048, 4096><<<gs, 64, 0, st>>>(j, done, pw_min);
+    if (op == OP_DIFF) { PW_SMALL(OP_DIFF) }
+    else if (op == OP_SV) { PW_SMALL(OP_SV) }
+    else { PW_SMALL(OP_META) }
+#undef PW_SMALL
   }
   // many-section documents: the table walk (no chunk records)
   if (mtotal > 0) {
