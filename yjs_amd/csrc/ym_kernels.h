@@ -85,6 +85,8 @@ struct PwBufs {
 int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const uint8_t **done);
 // Small single updates of a V1 diff / sv / meta call, one document per lane (ym_small.hip); marks done[d].
 int small_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t st);
+// ... and what those left of 80 B - 4 KB: one wave per document (ym_pwalk.hip k_pw_small).
+int pw_small_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t st);
 // ym_segsort.hip: segments [seg_b[s], seg_e[s]) of (ki, vi) stably sorted by key into (ko, vo); (kt, vt) scratch
 int segsort_pairs(const uint64_t *ki, const uint32_t *vi, uint64_t *ko, uint32_t *vo, uint64_t *kt, uint32_t *vt,
                   const uint32_t *seg_b, const uint32_t *seg_e, uint32_t nseg, hipStream_t st);

@@ -1641,18 +1641,6 @@ int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const ui
   *done_out = done;  // every document is marked (0 = not taken) from here on
   pw_last_done = done;
   const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
-  // small single updates: one wave per document (YMERGE_NO_PWSMALL: off)
-  static const bool no_small = getenv("YMERGE_NO_PWSMALL") != nullptr;
-  if (!no_small) {
-    const uint32_t gs = j.n < 65536 ? j.n : 65536;
-#define PW_SMALL(O) \
-    k_pw_small<O, SW_MIN, 2048><<<gs, 64, 0, st>>>(j, done, pw_min); \
-    k_pw_small<O, 2048, 4096><<<gs, 64, 0, st>>>(j, done, pw_min);
-    if (op == OP_DIFF) { PW_SMALL(OP_DIFF) }
-    else if (op == OP_SV) { PW_SMALL(OP_SV) }
-    else { PW_SMALL(OP_META) }
-#undef PW_SMALL
-  }
   // many-section documents: the table walk (no chunk records)
   if (mtotal > 0) {
     if (pw_ensure(B, 4, mtotal + 256)) {  // no room for the section tables: k_big_v1 takes those documents
@@ -1678,6 +1666,27 @@ int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const ui
   return 1;
 }
 
+}  // namespace ymk
+
+// Small single updates of a V1 diff / sv / meta call that the lane-per-document kernels (ym_small.hip) left:
+// one wave per document (k_pw_small; YMERGE_NO_PWSMALL: off).  After pw_run (done marked), before k_big_v1.
+namespace ymk {
+int pw_small_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t st) {
+  using namespace pw;
+  static const bool no_small = getenv("YMERGE_NO_PWSMALL") != nullptr;
+  if (!done || no_small || j.v2 || (op != OP_DIFF && op != OP_SV && op != OP_META) || j.n == 0) return 0;
+  uint64_t pw_min = PW_MIN;
+  if (const char *e = getenv("YMERGE_PW_MIN")) pw_min = strtoull(e, nullptr, 10);
+  const uint32_t gs = j.n < 65536 ? j.n : 65536;
+#define PW_SMALL(O)                                                  \
+  k_pw_small<O, SW_MIN, 2048><<<gs, 64, 0, st>>>(j, done, pw_min); \
+  k_pw_small<O, 2048, 4096><<<gs, 64, 0, st>>>(j, done, pw_min);
+  if (op == OP_DIFF) { PW_SMALL(OP_DIFF) }
+  else if (op == OP_SV) { PW_SMALL(OP_SV) }
+  else { PW_SMALL(OP_META) }
+#undef PW_SMALL
+  return 1;
+}
 }  // namespace ymk
 
 // debugging aid (not part of include/ymerge.h): the last chunk-walk call's per-document outcome on the

@@ -59,6 +59,10 @@ __device__ __forceinline__ void gcopy(Slot o, uint32_t p, uint32_t s, uint32_t n
 // decline.  The parsers of the LDS merge kernels (ym_fast_common.h), nested payloads included.
 __device__ __forceinline__ bool one(uint32_t p, uint32_t e, uint32_t &nx, uint32_t &len, uint32_t &info) {
   info = sm[p];
+  // the branch-free short cut first (ym_lane.h: GC / Skip, Items with an origin and ContentDeleted or an
+  // ASCII string -- the lanes of a wave stay converged on the structs of text documents), else the parsers
+  uint32_t fl;
+  if (ln::parse_fast(sm, p, e, nx, len, fl)) return true;
   Cur c = {p + 1, e, false};
   const bool skip = info == 10, gc = !skip && (info & 31) == 0;
   if (skip || gc) {
@@ -370,10 +374,13 @@ int small_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t st
   using namespace smallv1;
   if (!done || j.v2 || getenv("YMERGE_NO_SMALL")) return 0;
   const uint32_t g64 = (j.n + 63) / 64, g16 = (j.n + 15) / 16;
-  // tiny: 64 documents of <= 80 bytes (2 sections, 16 state-vector entries); small: 16 of <= 2 KB (64 each)
+  // tiny: 64 documents of <= 80 bytes (2 sections, 16 state-vector entries); small: 16 of <= 2 KB (32 each;
+  // more: k_pw_small)
+  // (the 2 KB shape for meta only: measured on C2 / C2r / C4r merged documents, diff and state vector run
+  // faster as one wave per document, k_pw_small -- a rich document's lanes diverge in the parsers)
 #define YS_LAUNCH(O)                                                                                         \
   k_small_v1<O, 64, 128, 8, 16><<<g64, 64, Lay<64, 128, 8, 16>::BYTES, st>>>(j, done);                    \
-  k_small_v1<O, 16, 2112, 64, 64><<<g16, 64, Lay<16, 2112, 64, 64>::BYTES, st>>>(j, done);
+  if (O == OP_META) k_small_v1<O, 16, 2112, 32, 32><<<g16, 64, Lay<16, 2112, 32, 32>::BYTES, st>>>(j, done);
   if (op == OP_DIFF) { YS_LAUNCH(OP_DIFF) }
   else if (op == OP_SV) { YS_LAUNCH(OP_SV) }
   else if (op == OP_META) { YS_LAUNCH(OP_META) }
