@@ -97,7 +97,7 @@ __device__ unsigned long long pw_prof[16];
 // descriptors + O(1) entry, [3] record staging, [4] record search, [5] consumption, [6] the cut + sliced
 // head, [7] delete set, [8] sizes + allocation, [9] write, [10] patches
 __device__ unsigned long long pw_ticks[16];
-#ifdef YM_PW_PROF
+#if defined(YM_PW_PROF) || defined(YM_PW_TICKS)
 #define PT_DECL uint64_t pt_t = __builtin_amdgcn_s_memrealtime(), pt_acc[11] = {};
 #define PT(i) do { const uint64_t t_ = __builtin_amdgcn_s_memrealtime(); pt_acc[i] += t_ - pt_t; pt_t = t_; } while (0)
 #define PT_FLUSH() do { if (threadIdx.x == 0) for (int i_ = 0; i_ < 11; i_++) atomicAdd(&pw_ticks[i_], pt_acc[i_]); } while (0)
@@ -531,13 +531,28 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
           }
           s += n;
         } else {
-          // the walk's chain does not pass x (or failed there under its cap): parse this struct here
-          uint32_t nx, cl, f2;
-          PWP(4);
-          if (!ln::parse_struct(D, x, len, nx, cl, f2)) { declined = true; why = 8; break; }
-          n = 1;
-          valid = lane == 0;
-          pos = x; end = nx; clen = cl; fl = f2;
+          // the walk's chain does not pass x (or failed there under its cap): the structs are parsed here, in
+          // lockstep, one batch up to the first that starts at a usable record of the chain (C5: ~5 after each
+          // section header), the section's or the chunk's end, or 64 -- one consumption round for them all
+          uint32_t y = x, t = 0, sp = s;
+          bool bad = false;
+          for (;;) {
+            uint32_t nx, cl, f2;
+            PWP(4);
+            if (!ln::parse_struct(D, y, len, nx, cl, f2)) { bad = t == 0; break; }  // (t > 0: the next round declines)
+            if (lane == t) { pos = y; end = nx; clen = cl; fl = f2; }
+            t++;
+            y = nx;
+            if (t >= rem || t >= 64 || y / CH != cx) break;
+            if (staged == gc) {  // does the chain's record list pass y?
+              uint32_t rp = NONE;
+              while (sp < nrec && ((rp = rec_pw(at<uint32_t>(L_REC + 4 * sp), cx)) & POS_MASK) < y) sp++;
+              if (sp < nrec && (rp & POS_MASK) == y && !(rp & F_FAIL)) break;
+            }
+          }
+          if (bad) { declined = true; why = 8; break; }
+          n = t;
+          valid = lane < n;
         }
         // ---- consume n structs: clocks by a wave prefix sum
         if (__any(valid && clen >= (1u << 24))) { declined = true; why = 9; break; }
