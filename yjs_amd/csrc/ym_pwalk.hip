@@ -69,6 +69,7 @@ constexpr uint32_t L_PSEC = L_PPOS + 4 * NPATCH;   // u32[NPATCH] section of eac
 constexpr uint32_t L_PVAL = L_PSEC + 4 * NPATCH;   // u8[NPATCH]  patched info bytes
 constexpr uint32_t L_REC = L_PVAL + NPATCH;        // u32[CAP] the records of the chunk being consumed
 constexpr uint32_t LDS_BYTES = L_REC + 4 * CAP;
+constexpr uint32_t L_DSL = (LDS_BYTES + 15) & ~15u;  // diff: wds::DsLds (the delete set's token tables)
 enum { S_PRELEN = 0, S_A0, S_A1, S_B0, S_B1, S_WRITTEN, S_CLIENT, S_FCLOCK, S_OUTB };
 constexpr uint32_t NONE = 0xffffffffu;
 
@@ -712,9 +713,15 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
       __syncthreads();
       continue;
     }
-    // ---- delete set: validated (readDeleteSet), then copied verbatim
+    // ---- delete set: validated (readDeleteSet), then copied verbatim -- through the LDS token tables
+    // (ym_wave_ds.h; C5: ~1,000 clients, each a few dependent loads on the walk below), or the walk below
+    // when those cannot decide (a client's ranges beyond a window, too many clients)
     const uint32_t ds0 = x;
-    {
+    const uint32_t xds = wds::ds_validate_lds(D, x, len, *reinterpret_cast<wds::DsLds *>(sm + L_DSL));
+    if (xds == NONE) { why = 17; PW_DECLINE() }
+    if (xds != wds::DS_BIG) {
+      x = xds;
+    } else {
       ln::LCur c = ln::make(D, x, len);
       const uint32_t ndc = ln::rvu(c);
       x = c.p;
@@ -1675,7 +1682,7 @@ int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const ui
   uint4 *desc = (uint4 *)B.p[2];
   uint32_t *recs = (uint32_t *)B.p[3];
   k_pw_walk<<<(total + 255) / 256, 256, 0, st>>>(j, cbase, j.n, total, desc, recs);
-  if (op == OP_DIFF) k_pw_stitch<OP_DIFF><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done, msz);
+  if (op == OP_DIFF) k_pw_stitch<OP_DIFF><<<grid, 64, L_DSL + sizeof(wds::DsLds), st>>>(j, cbase, desc, recs, done, msz);
   else if (op == OP_SV) k_pw_stitch<OP_SV><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done, msz);
   else k_pw_stitch<OP_META><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done, msz);
   return 1;
