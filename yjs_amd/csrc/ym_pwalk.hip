@@ -69,7 +69,8 @@ constexpr uint32_t L_PSEC = L_PPOS + 4 * NPATCH;   // u32[NPATCH] section of eac
 constexpr uint32_t L_PVAL = L_PSEC + 4 * NPATCH;   // u8[NPATCH]  patched info bytes
 constexpr uint32_t L_REC = L_PVAL + NPATCH;        // u32[CAP] the records of the chunk being consumed
 constexpr uint32_t LDS_BYTES = L_REC + 4 * CAP;
-constexpr uint32_t L_DSL = (LDS_BYTES + 15) & ~15u;  // diff: wds::DsLds (the delete set's token tables)
+constexpr uint32_t L_DSL = (LDS_BYTES + 15) & ~15u;  // diff: wds::DsLdsS (the delete set's token tables, 1 KB windows:
+                                                    // the 4 KB ones cost the stitch its occupancy -- C3 V1 diff 14 -> 24 ms)
 enum { S_PRELEN = 0, S_A0, S_A1, S_B0, S_B1, S_WRITTEN, S_CLIENT, S_FCLOCK, S_OUTB };
 constexpr uint32_t NONE = 0xffffffffu;
 
@@ -127,7 +128,10 @@ __device__ __forceinline__ uint32_t rec_clen(uint32_t w) { return w >> 13; }
 // ---- 0. eligibility and chunk counts ---------------------------------------------------------------
 // msz[d]: the section-parallel stitch's per-document area (k_pw_ms), for documents of >= ms_min sections
 __host__ __device__ inline uint64_t ms_area(uint32_t nsec);
-__global__ void k_pw_prep(GeneralJob j, uint32_t *cnt, uint8_t *done, uint64_t pw_min, uint64_t *msz, uint32_t ms_min) {
+// *many: set when a chunk-walked document has > 64 client sections (the stitch then validates delete sets through
+// LDS token tables; C5: ~1,000 clients)
+__global__ void k_pw_prep(GeneralJob j, uint32_t *cnt, uint8_t *done, uint64_t pw_min, uint64_t *msz, uint32_t ms_min,
+                          uint32_t *many) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d > j.n) return;
   uint32_t c = 0;
@@ -142,6 +146,7 @@ __global__ void k_pw_prep(GeneralJob j, uint32_t *cnt, uint8_t *done, uint64_t p
         ln::LCur h = ln::make(j.A + j.upd_off[u0], 0, (uint32_t)len);
         const uint32_t nsec = ln::rvu(h);
         if (!h.bad && nsec >= ms_min && nsec <= (1u << 16)) { a = ms_area(nsec); c = 0; }  // (the table walk: no chunks)
+        if (c && !h.bad && nsec > 64) atomicOr(many, 1u);
       }
     }
   }
@@ -344,7 +349,9 @@ __device__ bool slice_head(sc::cu32 *B, uint32_t adj, uint32_t s0, uint32_t s1, 
 #define PW_DECLINE() PW_DECLINE_R(why ? why : 2)
 
 // OP = OP_DIFF, OP_SV or OP_META (parseUpdateMeta: from = a section's first clock, to = its end clock)
-template <int OP>
+// DSL: the delete set validated through LDS token tables (ym_wave_ds.h) first -- batches with many-client
+// documents only: the tables' 17 KB of LDS cost the stitch occupancy (C3 V1 diff 14.3 -> 17.5 ms)
+template <int OP, bool DSL = false>
 __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *cbase, const uint4 *desc, const uint32_t *recs,
                                                   uint8_t *done, const uint64_t *msz) {
   const uint32_t lane = threadIdx.x;
@@ -717,7 +724,7 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
     // (ym_wave_ds.h; C5: ~1,000 clients, each a few dependent loads on the walk below), or the walk below
     // when those cannot decide (a client's ranges beyond a window, too many clients)
     const uint32_t ds0 = x;
-    const uint32_t xds = wds::ds_validate_lds(D, x, len, *reinterpret_cast<wds::DsLds *>(sm + L_DSL));
+    const uint32_t xds = DSL ? wds::ds_validate_lds(D, x, len, *reinterpret_cast<wds::DsLdsS *>(sm + L_DSL)) : wds::DS_BIG;
     if (xds == NONE) { why = 17; PW_DECLINE() }
     if (xds != wds::DS_BIG) {
       x = xds;
@@ -1643,11 +1650,13 @@ int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const ui
   uint32_t ms_min = MS_MIN;
   if (const char *e = getenv("YMERGE_PWMS_MIN")) ms_min = (uint32_t)strtoul(e, nullptr, 10);
   const uint32_t n1 = j.n + 1;
-  if (pw_ensure(B, 0, 24ull * n1 + 16 + j.n)) return -2;
+  if (pw_ensure(B, 0, 24ull * n1 + 32 + j.n)) return -2;
   uint64_t *msz = (uint64_t *)B.p[0], *moff = msz + n1;
   uint32_t *cnt = (uint32_t *)(moff + n1), *cbase = cnt + n1;
   uint8_t *done = (uint8_t *)(cbase + n1);
-  k_pw_prep<<<(n1 + 255) / 256, 256, 0, st>>>(j, cnt, done, pw_min, msz, ms_min);
+  uint32_t *many = (uint32_t *)(((uintptr_t)(done + j.n) + 15) & ~(uintptr_t)15);
+  PWCHK(hipMemsetAsync(many, 0, 4, st));
+  k_pw_prep<<<(n1 + 255) / 256, 256, 0, st>>>(j, cnt, done, pw_min, msz, ms_min, many);
   size_t tmp = 0, tmp2 = 0;
   hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cnt, cbase, n1, st);
   hipcub::DeviceScan::ExclusiveSum(nullptr, tmp2, msz, moff, n1, st);
@@ -1657,7 +1666,9 @@ int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const ui
   PWCHK(hipcub::DeviceScan::ExclusiveSum(B.p[1], tmp, msz, moff, n1, st));
   PWCHK(hipMemcpyAsync(B.pinned, cbase + j.n, 4, hipMemcpyDeviceToHost, st));
   PWCHK(hipMemcpyAsync(B.pinned + 2, moff + j.n, 8, hipMemcpyDeviceToHost, st));
+  PWCHK(hipMemcpyAsync(B.pinned + 4, many, 4, hipMemcpyDeviceToHost, st));
   PWCHK(hipStreamSynchronize(st));
+  const bool dsl = B.pinned[4] != 0;
   const uint32_t total = B.pinned[0];
   const uint64_t mtotal = *(uint64_t *)(B.pinned + 2);
   *done_out = done;  // every document is marked (0 = not taken) from here on
@@ -1682,7 +1693,8 @@ int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const ui
   uint4 *desc = (uint4 *)B.p[2];
   uint32_t *recs = (uint32_t *)B.p[3];
   k_pw_walk<<<(total + 255) / 256, 256, 0, st>>>(j, cbase, j.n, total, desc, recs);
-  if (op == OP_DIFF) k_pw_stitch<OP_DIFF><<<grid, 64, L_DSL + sizeof(wds::DsLds), st>>>(j, cbase, desc, recs, done, msz);
+  if (op == OP_DIFF && dsl) k_pw_stitch<OP_DIFF, true><<<grid, 64, L_DSL + sizeof(wds::DsLdsS), st>>>(j, cbase, desc, recs, done, msz);
+  else if (op == OP_DIFF) k_pw_stitch<OP_DIFF><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done, msz);
   else if (op == OP_SV) k_pw_stitch<OP_SV><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done, msz);
   else k_pw_stitch<OP_META><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done, msz);
   return 1;

@@ -83,10 +83,11 @@ __device__ __forceinline__ uint32_t skip_varuints(const uint8_t *D, uint32_t x, 
 // each varuint its index, the lane holding its last byte decodes and checks it) into value / end / bad-prefix
 // tables, then lane 0 steps client by client in O(1): client = val[t], m = val[t + 1], the 2m range tokens are
 // good iff the bad prefix does not change, t += 2 + 2m.  Repeated clients: an LDS hash set.
-constexpr uint32_t DW = 4096;     // window bytes
 constexpr uint32_t DHS = 2048;    // hash-set slots (at most DHS * 3 / 4 clients; more: the caller's own walk)
 constexpr uint32_t DS_BIG = 0xfffffffeu;  // not decided here (a client's ranges beyond a window, too many clients)
-struct DsLds {
+// DW: window bytes (a multiple of 64: each lane tokenises DW / 64 of them)
+template <uint32_t DW>
+struct DsLdsT {
   uint8_t b[DW + 16];
   uint32_t val[DW];
   uint16_t end[DW];       // position after token t (window-relative)
@@ -94,8 +95,12 @@ struct DsLds {
   uint32_t hs[DHS];
   uint32_t ntok, wtot, lastc, hmax;
 };
+using DsLds = DsLdsT<4096>;   // ~45 KB
+using DsLdsS = DsLdsT<1024>;  // ~17 KB (kernels that keep their occupancy)
 // (Called by every thread of the block; wave 0 tokenises, thread 0 walks.)
-__device__ __forceinline__ uint32_t ds_validate_lds(const uint8_t *D, uint32_t x, uint32_t e, DsLds &L) {
+template <uint32_t DW>
+__device__ __forceinline__ uint32_t ds_validate_lds(const uint8_t *D, uint32_t x, uint32_t e, DsLdsT<DW> &L) {
+  constexpr uint32_t PB = DW / 64;  // bytes per lane
   const uint32_t t = threadIdx.x, nt = blockDim.x, lane = t & 63;
   for (uint32_t i = t; i < DHS; i += nt) L.hs[i] = NONE;
   if (t == 0) { L.lastc = 0; L.hmax = 0; }
@@ -111,11 +116,11 @@ __device__ __forceinline__ uint32_t ds_validate_lds(const uint8_t *D, uint32_t x
     }
     __syncthreads();
     if (t < 64) {
-    // tokenise: lane l owns bytes [64 l, 64 l + 64)
-    const uint32_t b0 = 64 * lane;
+    // tokenise: lane l owns bytes [PB l, PB l + PB)
+    const uint32_t b0 = PB * lane;
     uint64_t stops = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < 64; k++) stops |= (uint64_t)((b0 + k < wl) && L.b[b0 + k] < 0x80) << k;
+    for (uint32_t k = 0; k < PB; k++) stops |= (uint64_t)((b0 + k < wl) && L.b[b0 + k] < 0x80) << k;
     const uint32_t nst = (uint32_t)__popcll(stops);
     const uint32_t tincl = wave_incl_add(nst), tbase = tincl - nst, ntok = lane_read(tincl, 63);
     // the last stop before this lane's bytes (the previous token's end): a max scan of each lane's last stop
