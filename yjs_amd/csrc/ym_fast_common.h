@@ -86,15 +86,20 @@ __device__ __forceinline__ uint32_t put_vu(O o, uint32_t p, uint64_t v) {
   ob8(o, p++, (uint32_t)v);
   return p;
 }
-// Lane-serial LDS -> LDS byte copy (regions do not overlap): eight loads in flight per wait instead of one.
+// Lane-serial LDS -> LDS copy (regions do not overlap): 8-byte unaligned LDS reads and writes (gfx950's LDS
+// takes unaligned b64 accesses), then the tail byte-wise.
 __device__ __forceinline__ void lds_copy(uint32_t dst, uint32_t src, uint32_t n) {
   uint32_t b = 0;
   for (; b + 8 <= n; b += 8) {
-    uint8_t t[8];
-#pragma unroll
-    for (uint32_t k = 0; k < 8; k++) t[k] = sm[src + b + k];
-#pragma unroll
-    for (uint32_t k = 0; k < 8; k++) sm[dst + b + k] = t[k];
+    uint64_t x;
+    __builtin_memcpy(&x, sm + src + b, 8);
+    __builtin_memcpy(sm + dst + b, &x, 8);
+  }
+  if (b + 4 <= n) {
+    uint32_t x;
+    __builtin_memcpy(&x, sm + src + b, 4);
+    __builtin_memcpy(sm + dst + b, &x, 4);
+    b += 4;
   }
   for (; b < n; b++) sm[dst + b] = sm[src + b];
 }
