@@ -45,7 +45,13 @@ namespace pv2 {
 // [0] column passes A + B, [1] phase C, [2] C's serial walk, [3] windows, [4] tokens from the tables,
 // [5] tokens parsed by the walker itself, [6] section headers, [7] C's table computation
 __device__ unsigned long long ms_prof[16];
+#ifdef YM_PW_TICKS
 #define MSP(i, v) do { if (threadIdx.x == 0) atomicAdd(&ms_prof[i], (unsigned long long)(v)); } while (0)
+#define MSC(x) x
+#else  // (the walk's counters and timers cost it scalar registers: diagnostics builds only)
+#define MSP(i, v) do { } while (0)
+#define MSC(x) do { } while (0)
+#endif
 
 // ---- MR: the rest walk ---------------------------------------------------------------------------------
 // ---- MR: the rest walk, block-parallel where it can be ---------------------------------------------------
@@ -375,6 +381,7 @@ __global__ void __launch_bounds__(64) k_ms_walk(Job J) {
   __shared__ uint16_t tV[MR_W], tB[MR_W], tA[MR_W];
   __shared__ uint2 spay[MR_PC + 1]; // the window's payload structs (index, kind | token count << 3; one token: the kind)
   __shared__ uint32_t sist[MR_PC];  // their first tokens' offsets (flushed to ist at the window's end)
+  __shared__ uint32_t sdum[64];     // (the fast loop's other lanes' stores)
   const uint32_t u0 = j.doc_upd[d];
   const uint64_t ub = j.upd_off[u0];
   const uint32_t len = U((uint32_t)(j.upd_off[u0 + 1] - ub));
@@ -431,8 +438,8 @@ __global__ void __launch_bounds__(64) k_ms_walk(Job J) {
     }
     __syncthreads();
     const uint64_t tt1 = __builtin_amdgcn_s_memrealtime();
-    t_tab += tt1 - tt0;
-    n_win++;
+    MSC(t_tab += tt1 - tt0);
+    MSC(n_win++);
     const uint32_t wend = wb + wn;  // tokens starting before here use the tables
     // the staged entries the fast loop may take (below the payload list's end and the first-token capacity)
     const uint32_t kfast = min(min(npay, k0 + MR_PC), icap);
@@ -446,13 +453,14 @@ __global__ void __launch_bounds__(64) k_ms_walk(Job J) {
           p += L;
           rt--;
         }
-        n_tok += rt0 - rt;
+        MSC(n_tok += rt0 - rt);
+        (void)rt0;
         if (rt == 0) continue;
         if (p >= wend) { bad = wend >= len; break; }  // (next window; past the document's end: truncated)
         const uint32_t e = U(mr_tok_slow(D, p, len, kind == PK_ANY ? PK_ONE : kind));  // (a token the table lacks)
         if (e == NONE) { bad = true; break; }
-        n_slow++;
-        n_tok++;
+        MSC(n_slow++);
+        MSC(n_tok++);
         p = e;
         rt--;
         continue;
@@ -460,7 +468,7 @@ __global__ void __launch_bounds__(64) k_ms_walk(Job J) {
       if (!insec) {  // a section header: vu(#structs) vu(first clock)
         if (s == nsec) { done = true; break; }
         if (p >= wend) { bad = wend >= len; break; }
-        n_hdr++;
+        MSC(n_hdr++);
         uint32_t W, clock, pe;
         bool hb = false;
         if (p + 16 <= wl) {
@@ -469,7 +477,7 @@ __global__ void __launch_bounds__(64) k_ms_walk(Job J) {
           clock = U(mr_vu(win, o, lim, hb));
           pe = wb + U(o);
         } else {
-          n_ghdr++;
+          MSC(n_ghdr++);
           ln::LCur c = ln::make(D, p, len);
           W = U(ln::rvu(c));
           clock = U(ln::rvu(c));
@@ -499,10 +507,15 @@ __global__ void __launch_bounds__(64) k_ms_walk(Job J) {
         if (U(e.x) < send && code != PK_NONE && code < PK_ANY) {
           const uint16_t *tab = code == PK_SKIP ? tV : code == PK_BIN ? tB : tA;
           for (;;) {
+            // both LDS reads in flight together (the barrier keeps the compiler from sinking the entry's read
+            // below the table read's wait); lane 0 records the first-token offset, the other lanes write a
+            // slot of their own (no exec-mask branch, no bank conflict)
             const uint2 en = spay[k + 1 - k0];
-            const uint32_t L = U(tab[p - wb]);
+            const uint32_t tv = tab[p - wb];
+            asm volatile("" ::: "memory");
+            const uint32_t L = U(tv);
             if (L == 0) break;
-            if (t == 0) sist[k - k0] = p;
+            *(t == 0 ? &sist[k - k0] : &sdum[t]) = p;
             p += L;
             k++;
             if (k >= kfast || p >= wend || U(en.x) >= send || U(en.y) != code) break;
@@ -520,11 +533,11 @@ __global__ void __launch_bounds__(64) k_ms_walk(Job J) {
         const uint64_t x = fin_i + (k - fin_k);
         nidx = x < 0xffffffffull ? (uint32_t)x : NONE;
         nkl = fin_pk;
-        n_fin++;
+        MSC(n_fin++);
         if (fin_pk == PK_ANY) {  // (consecutive ordinals: the cursor moves to the next entry, else a search)
           const uint32_t o = fin_l + (k - fin_k);
           if (o < lc_lo || o >= lc_hi) {
-            n_lc++;
+            MSC(n_lc++);
             lc_v = NONE; lc_lo = 1; lc_hi = 0;
             if (o < ltot && nle != 0) {
               uint32_t e = lc_e;
@@ -557,7 +570,7 @@ __global__ void __launch_bounds__(64) k_ms_walk(Job J) {
       kind = nkl & 7;
       rt = kind == PK_ANY ? nkl >> 3 : 1;
     }
-    t_walk += __builtin_amdgcn_s_memrealtime() - tt1;
+    MSC(t_walk += __builtin_amdgcn_s_memrealtime() - tt1);
     __syncthreads();
     for (uint32_t q = t; q < k - k0; q += 64) ist[k0 + q] = sist[q];
   }
