@@ -175,6 +175,12 @@ __global__ void __launch_bounds__(256) k_pw_walk(GeneralJob j, const uint32_t *c
   const uint32_t len = (uint32_t)(j.upd_off[u0 + 1] - ub);
   const uint8_t *D = j.A + ub;
   const uint32_t c0 = ci * CH, c1 = c0 + CH < len ? c0 + CH : len;
+  // documents of many client sections (C5) try a section header where the chain falls off (below)
+  bool many = false;
+  {
+    ln::LCur h = ln::make(D, 0, len);
+    many = ln::rvu(h) > 16 && !h.bad;
+  }
   uint32_t nrec = 0, cum = 0, lastfail = 0, lastpatch = 0, lastskip = 0, fails = FAIL_RUN, okrun = 0;  // the chunk start is mid-struct: only short-cut candidates until two structs in a row
   bool frun = false, ovf = false, start = true;
   uint32_t p = c0;
@@ -198,6 +204,26 @@ __global__ void __launch_bounds__(256) k_pw_walk(GeneralJob j, const uint32_t *c
       ln::LCur c = ln::make(D, p, len, SPEC_CAP);
       ok = ln::parse_at(c, cl, fl);
       nx = c.p;
+    }
+    // The chain just fell off at p after a struct: most often a section header (C5: ~1,000 per document).
+    // Three varuints (#structs > 0, client, clock) followed by a struct that parses: the chain goes on past
+    // the header (the FAIL recorded at p ends the previous section's last struct there), so the stitch finds
+    // the section's first struct among the records instead of re-parsing until the chain meets it again.
+    uint32_t hjump = 0;
+    if (many && !ok && okrun >= 2 && p > c0) {  // (after >= 2 structs in a row: not inside a delete set's varuints)
+      ln::LCur h = ln::make(D, p, len);
+      const uint32_t ns = ln::rvu(h);
+      ln::rvu(h);
+      ln::rvu(h);
+      if (!h.bad && ns > 0 && h.p < len) {
+        uint32_t cl2, fl2, nx2;
+        bool ok2 = ln::parse_fast(D, h.p, len, nx2, cl2, fl2);
+        if (!ok2) {
+          ln::LCur c2 = ln::make(D, h.p, len, SPEC_CAP);
+          ok2 = ln::parse_at(c2, cl2, fl2);
+        }
+        if (ok2) hjump = h.p;
+      }
     }
     if (ok || !frun) {
       if (nrec == CAP) { ovf = true; break; }  // overflow: the stitch re-parses this chunk
@@ -226,8 +252,8 @@ __global__ void __launch_bounds__(256) k_pw_walk(GeneralJob j, const uint32_t *c
     // a long run of non-struct bytes (the delete set, a long content): only positions the short cut could
     // accept are tried from there on -- the full parser at every byte of a 100 KB delete set cost more
     // than the whole struct section
-    p = ok ? nx : fails < FAIL_RUN ? p + 1 : ln::next_cand(D, p + 1, c1);
-    frun = !ok;
+    p = ok ? nx : hjump ? hjump : fails < FAIL_RUN ? p + 1 : ln::next_cand(D, p + 1, c1);
+    frun = !ok && !hjump;
   }
   if (ovf) nrec = 0;
   if (nrec & 3) *reinterpret_cast<uint4 *>(recs + rec_idx(g, nrec & ~3u)) = rq;  // the last group (its tail: don't-care)
