@@ -65,6 +65,9 @@ enum { YM_DS_REF = 0x100 };
 enum { YM_OFF32 = 0x200 };
 /* ym_snapshot only, or-ed into ym_batch.format: the output encoding (default: the input's) */
 enum { YM_OUT_V1 = 0x1000, YM_OUT_V2 = 0x2000 };
+/* ym_compact only, or-ed into ym_batch.format: the document is new Y.Doc({ gc: false }) (deleted content
+ * is kept and written; Doc.js:40-43, Transaction.js:302-304) */
+enum { YM_NO_GC = 0x4000 };
 
 typedef struct ym_batch {
   const uint8_t *arena;    /* concatenated update bytes                                   */
@@ -130,7 +133,7 @@ int ym_ds_merge(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
  * (repeated clients merged in Map order) and V1 <-> V2 conversion, with decodeSnapshot's exceptions. */
 int ym_snapshot(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
 /* Doc round-trip compaction: per document, the reference's own
- *   const doc = new Y.Doc()            (gc: true)
+ *   const doc = new Y.Doc()            (gc: true; with YM_NO_GC in b->format, { gc: false })
  *   updates.forEach(u => Y.applyUpdate[V2](doc, u))
  *   Y.encodeStateAsUpdate[V2](doc)
  * (gaberogan/yjs@v0 src/utils/encoding.js:350-383 readUpdate / applyUpdate, :490-526 encodeStateAsUpdate;

@@ -14,6 +14,8 @@ import os
 from yjs_amd.workloads import load_ymb
 
 PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "compact.json")
+# new Y.Doc({ gc: false }) over the same inputs (oracle/gen/make_compact_nogc_fixtures.cjs; ym_compact with YM_NO_GC)
+PATH_NOGC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "compact_nogc.json")
 
 
 @functools.lru_cache(maxsize=None)
@@ -21,9 +23,9 @@ def _ymb(name):
     return load_ymb(name)
 
 
-@functools.lru_cache(maxsize=1)
-def load():
-    with open(PATH) as f:
+@functools.lru_cache(maxsize=2)
+def load(nogc=False):
+    with open(PATH_NOGC if nogc else PATH) as f:
         d = json.load(f)
     out = []
     for c in d["cases"]:
@@ -40,7 +42,7 @@ def load():
             exp = base64.b64decode(c["expect"]) if "expect" in c else None
         out.append(dict(id=c["id"], group=c["group"], fmt=c["fmt"], inputs=ins, expect=exp,
                         sha=c.get("expect_sha256"), elen=c.get("expect_len"), error=c.get("error"),
-                        pending=c.get("pending")))
+                        pending=c.get("pending"), differs=c.get("differs_from_gc")))
     return out
 
 

@@ -31,6 +31,8 @@ def run(op, fmt, arena, upd_off, doc_upd, sv_arena=None, sv_off=None, san=False)
     sv_off = np.ascontiguousarray(sv_off, np.uint64)
     if op == "dsmerge_ref":  # ym_ds_merge with YM_DS_REF: the reference's adjacency-only coalescing
         op, fmt = "dsmerge", fmt | 0x100
+    if op == "compact_nogc":  # ym_compact with YM_NO_GC: new Y.Doc({ gc: false })
+        op, fmt = "compact", fmt | 0x4000
     if op in ("snap_to_v1", "snap_to_v2"):  # ym_snapshot with YM_OUT_V1 / YM_OUT_V2
         op, fmt = "snap", fmt | (0x2000 if op == "snap_to_v2" else 0x1000)
     exe = binary(san)

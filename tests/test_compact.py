@@ -45,6 +45,33 @@ def test_compact_keeps_the_state_vector():
         assert O.sv_from_update(out, c["fmt"]) == O.sv_from_update(merged, c["fmt"]), c["id"]
 
 
+def test_compact_nogc_fixture_coverage():
+    """gc: false fixtures (the same inputs on new Y.Doc({ gc: false })): most documents with deletions keep
+    their deleted content, so their bytes differ from the gc: true ones."""
+    cs = compact_cases.load(nogc=True)
+    assert len(cs) >= 1000
+    assert sum(1 for c in cs if c["differs"]) >= 500
+    assert sum(1 for c in cs if c["pending"]) >= 100 and sum(1 for c in cs if c["error"]) >= 5
+
+
+@pytest.mark.parametrize("san", [False, True], ids=["opt", "asan_ubsan"])
+def test_device_core_compact_nogc_host_build(san):
+    """YM_NO_GC (new Y.Doc({ gc: false })): the device code built for the host against every gc: false
+    fixture of the reference (the oracle's C restatement models gc: true only; these are pinned by the
+    reference's bytes)."""
+    import core_host
+    from yjs_amd import pack_docs
+    for fmt in (1, 2):
+        cs = [c for c in compact_cases.load(nogc=True) if c["fmt"] == fmt]
+        if san:
+            seen = collections.Counter()
+            cs = [c for c in cs if seen.update([c["group"]]) is None and seen[c["group"]] <= 12]
+        a, o, d = pack_docs([c["inputs"] for c in cs])
+        outs, st = core_host.run("compact_nogc", fmt, a, o, d, san=san)
+        bad = [(c["id"], why) for c, out, s in zip(cs, outs, st) if (why := compact_cases.mismatch(c, s, out))]
+        assert not bad, f"{len(bad)}/{len(cs)} differ: {bad[:8]}"
+
+
 @pytest.mark.parametrize("san", [False, True], ids=["opt", "asan_ubsan"])
 def test_device_core_compact_host_build(san):
     """The device code itself (yjs_amd/csrc/ym_compact.h compact_doc, what k_compact runs one document per

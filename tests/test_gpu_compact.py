@@ -40,6 +40,23 @@ def test_compact_fixtures_on_gpu(engine, fmt, lanes, monkeypatch):
     assert sum(1 for c in cs if c["pending"]) > 60 and sum(1 for c in cs if c["error"]) > 0
 
 
+@pytest.mark.parametrize("fmt", [1, 2])
+def test_compact_nogc_fixtures_on_gpu(engine, fmt):
+    """YM_NO_GC: every gc: false fixture of the reference (new Y.Doc({ gc: false }), deleted content kept)."""
+    from yjs_amd import pack_docs
+    cs = [c for c in compact_cases.load(nogc=True) if c["fmt"] == fmt]
+    a, o, d = pack_docs([c["inputs"] for c in cs])
+    oa, oo, ol, st = engine.run_host("compact_nogc", fmt, a, o, d)
+    bad = []
+    for i, c in enumerate(cs):
+        got = oa[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() if st[i] == 0 else None
+        why = compact_cases.mismatch(c, st[i], got)
+        if why:
+            bad.append((c["id"], why))
+    assert not bad, f"{len(bad)}/{len(cs)} differ: {bad[:8]}"
+    assert sum(1 for c in cs if c["differs"]) > 200
+
+
 @pytest.mark.parametrize("name", ["c2_v1", "c2_v2", "c4_v1"])
 def test_compact_workload_matches_oracle(engine, name):
     """Every template document of the C2 / C4 workloads (bench_data/) compacted on the GPU equals the

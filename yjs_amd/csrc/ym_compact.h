@@ -132,6 +132,7 @@ struct Doc {
   Arena *a;   // persistent: the store's vectors, pending structs / deletes, types
   Arena *ta;  // transient: one update's reader and transaction (released after each update)
   uint32_t v2;
+  uint32_t nogc;       // Doc({ gc: false }): deleted content is kept (no tryGcDeleteSet), Doc.js:40-43
   Item *it; uint32_t nit, capit;
   Piece *pc; uint32_t npc, cappc;
   Elem *el; uint32_t nel, capel;
@@ -1364,7 +1365,7 @@ YM_HOT Tx *tx_cleanup(Doc &d, Tx *x) {
     }
   }
   d.tx = x;
-  for (uint32_t ci = 0; ci < x->ds.cl.n && !c.err; ci++) {  // tryGcDeleteSet (doc.gc)
+  for (uint32_t ci = 0; ci < x->ds.cl.n && !c.err && !d.nogc; ci++) {  // tryGcDeleteSet (doc.gc, Transaction.js:302-304)
     const int32_t s = cd_client(d, x->ds.cl.p[ci].client);
     for (uint32_t k = x->ds.cl.p[ci].it.n; k-- > 0 && !c.err;) {
       const int64_t clock = x->ds.cl.p[ci].it.p[k].clock, end = clock + x->ds.cl.p[ci].it.p[k].len;
@@ -1652,8 +1653,10 @@ YM_INL WsSize ws_size(uint32_t k, uint64_t bytes, uint32_t mul) {
 // its encodeStateAsUpdate[V2].  out == nullptr: sizing only (L.total); else the bytes are written there.
 // The engine state stays in the workspace between the two calls of one document (pass 2 only writes).
 struct Result { uint64_t col[C_N]; uint64_t rest, total; };
-YM_BIG void compact_doc(Ctx &c, uint8_t *ws, const WsSize &z, uint32_t v2, const uint64_t *upd_off, uint32_t u0, uint32_t k,
+// flags: bit 0 V2, bit 1 Doc({ gc: false })
+YM_BIG void compact_doc(Ctx &c, uint8_t *ws, const WsSize &z, uint32_t flags, const uint64_t *upd_off, uint32_t u0, uint32_t k,
                         Result &R, uint8_t *out) {
+  const uint32_t v2 = flags & 1;
   Doc *dp = (Doc *)ws;  // the document's state heads its workspace
   Arena *ap = (Arena *)(ws + al16(sizeof(Doc)));
   Arena *tp = (Arena *)(ws + al16(sizeof(Doc)) + al16(sizeof(Arena)));
@@ -1665,6 +1668,7 @@ YM_BIG void compact_doc(Ctx &c, uint8_t *ws, const WsSize &z, uint32_t v2, const
     d.a = ap;
     d.ta = tp;
     d.v2 = v2;
+    d.nogc = (flags >> 1) & 1;
     d.it = (Item *)p; d.capit = (uint32_t)z.it; p += al16(z.it * sizeof(Item));
     d.pc = (Piece *)p; d.cappc = (uint32_t)z.pc; p += al16(z.pc * sizeof(Piece));
     d.el = (Elem *)p; d.capel = (uint32_t)z.el; p += al16(z.el * sizeof(Elem));

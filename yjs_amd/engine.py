@@ -45,6 +45,7 @@ class UnsupportedInput(YjsError):
 YM_DS_REF = 0x100  # ym_ds_merge: the reference's adjacency-only coalescing (include/ymerge.h)
 YM_OFF32 = 0x200   # upd_off holds uint32_t offsets (include/ymerge.h)
 YM_OUT_V1, YM_OUT_V2 = 0x1000, 0x2000  # ym_snapshot: output encoding
+YM_NO_GC = 0x4000  # ym_compact: new Y.Doc({ gc: false })
 
 
 def _off_flag(upd_off):
@@ -164,11 +165,12 @@ class Engine:
         L = self.lib
         return {"merge": L.ym_merge, "diff": L.ym_diff, "sv": L.ym_sv, "conv": L.ym_convert, "meta": L.ym_meta,
                 "dsmerge": L.ym_ds_merge, "dsmerge_ref": L.ym_ds_merge,
-                "snap_to_v1": L.ym_snapshot, "snap_to_v2": L.ym_snapshot, "compact": L.ym_compact}[op]
+                "snap_to_v1": L.ym_snapshot, "snap_to_v2": L.ym_snapshot, "compact": L.ym_compact,
+                "compact_nogc": L.ym_compact}[op]
 
     @staticmethod
     def _format(op, fmt):
-        extra = {"dsmerge_ref": YM_DS_REF, "snap_to_v1": YM_OUT_V1, "snap_to_v2": YM_OUT_V2}
+        extra = {"dsmerge_ref": YM_DS_REF, "snap_to_v1": YM_OUT_V1, "snap_to_v2": YM_OUT_V2, "compact_nogc": YM_NO_GC}
         return fmt | extra.get(op, 0)
 
     # ---- host-memory batches ------------------------------------------------------------------
@@ -309,12 +311,12 @@ def encodeStateVectorFromUpdateBatch(updates, fmt=1, raise_errors=False):
     return _unpack(*_engine().run_host("sv", fmt, arena, upd_off, doc_upd), raise_errors)
 
 
-def compactUpdatesBatch(docs, fmt=1, raise_errors=False):
+def compactUpdatesBatch(docs, fmt=1, raise_errors=False, gc=True):
     """Doc round-trip compaction (ym_compact) over a batch: per document, encodeStateAsUpdate[V2] of a fresh
-    gc=true Doc after applyUpdate[V2] of every update in order (the reference's own compaction:
+    Doc({ gc }) after applyUpdate[V2] of every update in order (the reference's own compaction:
     src/utils/encoding.js readUpdate / encodeStateAsUpdate, Transaction.js cleanupTransactions)."""
     arena, upd_off, doc_upd = pack_docs(docs)
-    return _unpack(*_engine().run_host("compact", fmt, arena, upd_off, doc_upd), raise_errors)
+    return _unpack(*_engine().run_host("compact" if gc else "compact_nogc", fmt, arena, upd_off, doc_upd), raise_errors)
 
 
 def compactUpdates(updates):
