@@ -77,8 +77,9 @@ typedef struct ym_batch {
   uint32_t n_upd;
   int32_t format;          /* YM_V1 | YM_V2                                               */
   int32_t mem;             /* YM_MEM_HOST | YM_MEM_DEVICE (applies to every array here)   */
-  const uint8_t *sv_arena; /* ym_diff only: concatenated encoded state vectors            */
-  const uint64_t *sv_off;  /* ym_diff only: n_docs + 1                                    */
+  const uint8_t *sv_arena; /* ym_diff: concatenated encoded state vectors; ym_compact:     */
+                           /* target state vectors (NULL: none); other ops: ignored       */
+  const uint64_t *sv_off;  /* n_docs + 1 (with sv_arena)                                  */
 } ym_batch;
 
 typedef struct ym_out {
@@ -135,7 +136,9 @@ int ym_snapshot(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
 /* Doc round-trip compaction: per document, the reference's own
  *   const doc = new Y.Doc()            (gc: true; with YM_NO_GC in b->format, { gc: false })
  *   updates.forEach(u => Y.applyUpdate[V2](doc, u))
- *   Y.encodeStateAsUpdate[V2](doc)
+ *   Y.encodeStateAsUpdate[V2](doc)      (with b->sv_arena: Y.encodeStateAsUpdate[V2](doc, sv), doc d's
+ *                                        target state vector sv_arena[sv_off[d] .. sv_off[d+1]) -- only the
+ *                                        structs the target lacks, the whole delete set; encoding.js:71-116)
  * (gaberogan/yjs@v0 src/utils/encoding.js:350-383 readUpdate / applyUpdate, :490-526 encodeStateAsUpdate;
  * structs integrated by Item.integrate, deletions applied, deleted content garbage-collected and runs of
  * structs merged by cleanupTransactions, src/utils/Transaction.js:244-367) in b->format.  Structs whose

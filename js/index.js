@@ -109,15 +109,24 @@ function convertUpdateFormatBatch (updates, opts, throwErrors = false, async = f
   return call(async, [OP.conv, fmtOf(opts), p.arena, p.updOff, p.docUpd], r => unpack(r, throwErrors))
 }
 
-// Doc round-trip compaction (ym_compact): per document, encodeStateAsUpdate[V2] of a fresh gc=true Doc after
+// Doc round-trip compaction (ym_compact): per document, encodeStateAsUpdate[V2] of a fresh Doc after
 // applyUpdate[V2] of every update in order -- the reference's own compaction (structs merged, deleted
-// content garbage-collected)
+// content garbage-collected).  opts.gc === false: new Y.Doc({ gc: false }) (YM_NO_GC);
+// opts.targetStateVectors: one encoded state vector per document, encodeStateAsUpdate[V2](doc, sv)
+const YM_NO_GC = 0x4000
 function compactUpdatesBatch (docs, opts, throwErrors = false, async = false) {
   const p = pack(docs)
-  return call(async, [OP.compact, fmtOf(opts), p.arena, p.updOff, p.docUpd], r => unpack(r, throwErrors))
+  const fmt = fmtOf(opts) | (opts && opts.gc === false ? YM_NO_GC : 0)
+  const args = [OP.compact, fmt, p.arena, p.updOff, p.docUpd]
+  if (opts && opts.targetStateVectors) {
+    if (opts.targetStateVectors.length !== docs.length) throw new RangeError('one target state vector per document')
+    const s = pack(opts.targetStateVectors.map(x => [x]))
+    args.push(s.arena, s.updOff)
+  }
+  return call(async, args, r => unpack(r, throwErrors))
 }
-const compactUpdates = updates => compactUpdatesBatch([updates], { format: 1 }, true)[0]
-const compactUpdatesV2 = updates => compactUpdatesBatch([updates], { format: 2 }, true)[0]
+const compactUpdates = (updates, sv) => compactUpdatesBatch([updates], { format: 1, targetStateVectors: sv ? [sv] : null }, true)[0]
+const compactUpdatesV2 = (updates, sv) => compactUpdatesBatch([updates], { format: 2, targetStateVectors: sv ? [sv] : null }, true)[0]
 const compactUpdatesBatchAsync = (docs, opts, throwErrors = false) => compactUpdatesBatch(docs, opts, throwErrors, true)
 
 // the engine writes parseUpdateMeta's two Maps as two encoded state vectors (from, then to)

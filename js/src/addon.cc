@@ -115,11 +115,17 @@ static bool parse(napi_env env, napi_callback_info info, Job &j, napi_value *arg
     napi_throw_range_error(env, nullptr, "updOff / docUpd exceed the arena");
     return false;
   }
-  if (j.op == 1 && (argc < 7 || !get_u8(env, argv[5], &sva, &svlen) || !get_u64(env, argv[6], &sv_off, &nsv1, j.sv_conv) ||
-                    nsv1 != ndocs1 || sv_off[nsv1 - 1] > svlen)) {
-    napi_throw_type_error(env, nullptr, "diff needs svArena (Uint8Array) and svOff (one more entry than documents)");
+  // state vectors: ym_diff's (required), ym_compact's target vectors (optional)
+  napi_valuetype t5 = napi_undefined;
+  if (argc >= 7) napi_typeof(env, argv[5], &t5);
+  const bool want_sv = j.op == 1 || (j.op == 7 && t5 != napi_undefined && t5 != napi_null);
+  if (want_sv && (argc < 7 || !get_u8(env, argv[5], &sva, &svlen) || !get_u64(env, argv[6], &sv_off, &nsv1, j.sv_conv) ||
+                  nsv1 != ndocs1 || sv_off[nsv1 - 1] > svlen)) {
+    napi_throw_type_error(env, nullptr, "diff / compact need svArena (Uint8Array) and svOff (one more entry than documents)");
     return false;
   }
+  static const uint8_t no_bytes[1] = {0};
+  if (want_sv && !sva) sva = no_bytes;  // every vector empty: still a batch with targets (NULL: none)
   memset(&j.b, 0, sizeof(j.b));
   j.b.arena = arena;
   j.b.upd_off = upd_off;
@@ -128,8 +134,8 @@ static bool parse(napi_env env, napi_callback_info info, Job &j, napi_value *arg
   j.b.n_upd = (uint32_t)(nupd1 - 1);
   j.b.format = fmt;
   j.b.mem = YM_MEM_HOST;
-  j.b.sv_arena = sva;
-  j.b.sv_off = j.op == 1 ? sv_off : nullptr;
+  j.b.sv_arena = want_sv ? sva : nullptr;
+  j.b.sv_off = want_sv ? sv_off : nullptr;
   return true;
 }
 

@@ -16,8 +16,9 @@ function encodeMeta (m) {
   for (const map of [m.from, m.to]) { vu(map.size); map.forEach((clock, client) => { vu(client); vu(clock) }) }
   return Uint8Array.from(out)
 }
-// compact.json holds Doc round-trip fixtures in their own layout (tests/compact_cases.py)
-for (const f of fs.readdirSync(dir).filter(f => f.endsWith('.json') && f !== 'compact.json').sort()) {
+// compact*.json hold Doc round-trip fixtures in their own layout (tests/compact_cases.py): checked below
+const opFiles = () => fs.readdirSync(dir).filter(f => f.endsWith('.json') && !f.startsWith('compact')).sort()
+for (const f of opFiles()) {
   const cases = JSON.parse(fs.readFileSync(path.join(dir, f))).cases
   for (const c of cases) {
     const inputs = c.inputs.map(b => new Uint8Array(Buffer.from(b, 'base64')))
@@ -45,7 +46,7 @@ for (const f of fs.readdirSync(dir).filter(f => f.endsWith('.json') && f !== 'co
 // the Promise-returning batch forms (napi_async_work) against the golden merges, several calls in flight
 const asyncCheck = async () => {
   const groups = { 1: [], 2: [] }
-  for (const f of fs.readdirSync(dir).filter(f => f.endsWith('.json') && f !== 'compact.json').sort()) {
+  for (const f of opFiles()) {
     for (const c of JSON.parse(fs.readFileSync(path.join(dir, f))).cases) {
       if (c.op === 'merge' && c.inputs.length > 1) groups[c.fmt].push(c)
     }
@@ -60,7 +61,27 @@ const asyncCheck = async () => {
   await Promise.all(runs)
   return n
 }
+// Doc round-trip compaction through the JS API: the inline gc: false fixtures (opts.gc === false) and the
+// target-state-vector slice documents (opts.targetStateVectors), errors by class and message
+let compactOk = 0
+{
+  const b = x => new Uint8Array(Buffer.from(x, 'base64'))
+  const check = (id, r, c) => {
+    const good = c.error ? r instanceof Error && r.constructor.name === c.error.name && r.message === c.error.message
+      : !(r instanceof Error) && Buffer.compare(Buffer.from(r), Buffer.from(c.expect, 'base64')) === 0
+    if (good) compactOk++; else bad.push([id, 'compact', r instanceof Error ? r.message : r.length])
+  }
+  for (const fmt of [1, 2]) {
+    const nogc = JSON.parse(fs.readFileSync(path.join(dir, 'compact_nogc.json'))).cases.filter(c => c.inputs && c.fmt === fmt)
+    Y.compactUpdatesBatch(nogc.map(c => c.inputs.map(b)), { format: fmt, gc: false }).forEach((r, i) => check(nogc[i].id, r, nogc[i]))
+    for (const c of JSON.parse(fs.readFileSync(path.join(dir, 'compact_sv.json'))).cases.filter(c => c.group === 'slice' && c.fmt === fmt)) {
+      const ins = c.inputs.map(b)
+      Y.compactUpdatesBatch(c.targets.map(() => ins), { format: fmt, gc: c.gc, targetStateVectors: c.targets.map(t => b(t.sv)) })
+        .forEach((r, i) => check(c.id + '/' + i, r, c.targets[i]))
+    }
+  }
+}
 asyncCheck().then(asyncOk => {
-  console.log(JSON.stringify({ ok, bad: bad.length, unsupported, async_ok: asyncOk, first: bad.slice(0, 10) }))
+  console.log(JSON.stringify({ ok, bad: bad.length, unsupported, async_ok: asyncOk, compact_ok: compactOk, first: bad.slice(0, 10) }))
   process.exit(bad.length ? 1 : 0)
 }, e => { console.error(e); process.exit(1) })

@@ -18,6 +18,11 @@ PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "compa
 PATH_NOGC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "compact_nogc.json")
 
 
+# encodeStateAsUpdate[V2](doc, targetStateVector) (oracle/gen/make_compact_sv_fixtures.cjs; ym_compact with
+# ym_batch.sv_arena)
+PATH_SV = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "compact_sv.json")
+
+
 @functools.lru_cache(maxsize=None)
 def _ymb(name):
     return load_ymb(name)
@@ -71,3 +76,28 @@ def mismatch(case, status, got, message=True):
     if st != 0:
         return f"status {st:#x}"
     return None if matches(case, got) else "bytes differ"
+
+
+@functools.lru_cache(maxsize=1)
+def load_sv():
+    """Target-state-vector fixtures, one entry per (document, target): the document's inputs (an inline
+    case of compact.json named by `ref`, a workload document, or the generator's own "slice" documents),
+    gc, the encoded target state vector and the reference's output (bytes or SHA-256) or exception."""
+    base = {c["id"]: c for c in load()}
+    with open(PATH_SV) as f:
+        d = json.load(f)
+    out = []
+    for c in d["cases"]:
+        if "ref" in c:
+            ins = base[c["ref"]]["inputs"]
+            cid = c["ref"]
+        else:
+            ins = [base64.b64decode(x) for x in c["inputs"]]
+            cid = c["id"]
+        for i, t in enumerate(c["targets"]):
+            out.append(dict(id=f"{cid}/{t['kind']}{i}", group=c["group"], fmt=c["fmt"], gc=c["gc"], inputs=ins,
+                            sv=base64.b64decode(t["sv"]), kind=t["kind"],
+                            expect=base64.b64decode(t["expect"]) if "expect" in t else None,
+                            sha=t.get("expect_sha256"), elen=t.get("expect_len"), error=t.get("error"),
+                            pending=None, differs=None))
+    return out

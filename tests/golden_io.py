@@ -5,8 +5,8 @@ import json
 import os
 
 GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-# fixture files with their own case layout and loader (compact.json: tests/compact_cases.py)
-OTHER_FORMATS = {"compact"}
+# fixture files with their own case layout and loader (compact*.json: tests/compact_cases.py)
+OTHER_FORMATS = {"compact", "compact_nogc", "compact_sv"}
 
 
 def load_cases(groups=None):

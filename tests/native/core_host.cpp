@@ -57,13 +57,16 @@ int main(int argc, char **argv) {
     int st = ST_RETRY;
     std::vector<uint8_t> out;
     if (op == 7) {  // Doc round-trip compaction (ym_compact.h compact_doc), same retry policy as the kernel
+      // fmt bit 15 (test-only): the batch carries target state vectors (ym_batch.sv_arena != NULL)
+      const uint8_t *tsv = (fmt & 0x8000) ? sv.data() + sv_off[d] : nullptr;
+      const uint64_t tsvlen = (fmt & 0x8000) ? sv_off[d + 1] - sv_off[d] : 0;
       for (uint32_t mul = 1, round = 0; st == ST_RETRY && round < 5; mul *= 4, round++) {
         const cpt::WsSize z = cpt::ws_size(k, bytes, mul);
         std::vector<uint8_t> ws(z.total + 16);
         Ctx c = {0, arena.data()};
         cpt::Result R;
         memset(&R, 0, sizeof(R));
-        cpt::compact_doc(c, ws.data(), z, v2 | ((fmt & 0x4000) ? 2u : 0u), upd_off.data(), u0, k, R, nullptr);
+        cpt::compact_doc(c, ws.data(), z, v2 | ((fmt & 0x4000) ? 2u : 0u), upd_off.data(), u0, k, tsv, tsvlen, R, nullptr);
         st = c.err;
         if (st) continue;
         if (getenv("YM_CPT_STATS")) {  // workspace use (sizing experiments): used / reserved per region
@@ -76,7 +79,7 @@ int main(int argc, char **argv) {
         }
         out.assign(R.total + 1, 0);
         Ctx c2 = {0, arena.data()};
-        cpt::compact_doc(c2, ws.data(), z, v2 | ((fmt & 0x4000) ? 2u : 0u), upd_off.data(), u0, k, R, out.data());
+        cpt::compact_doc(c2, ws.data(), z, v2 | ((fmt & 0x4000) ? 2u : 0u), upd_off.data(), u0, k, tsv, tsvlen, R, out.data());
         st = c2.err ? (c2.err == ST_RETRY ? ST_UNEXPECTED : c2.err) : 0;
         out.resize(R.total);
       }

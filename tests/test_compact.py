@@ -88,3 +88,36 @@ def test_device_core_compact_host_build(san):
         outs, st = core_host.run("compact", fmt, a, o, d, san=san)
         bad = [(c["id"], why) for c, out, s in zip(cs, outs, st) if (why := compact_cases.mismatch(c, s, out))]
         assert not bad, f"{len(bad)}/{len(cs)} differ: {bad[:8]}"
+
+
+def test_compact_sv_fixture_coverage():
+    """encodeStateAsUpdate(doc, sv) fixtures: every target kind, gc: false documents, the slice group's every
+    clock (a surrogate pair cut by str.slice: V1 throws URIError), malformed vectors."""
+    cs = compact_cases.load_sv()
+    n = collections.Counter(c["kind"] for c in cs)
+    assert all(n[k] >= 900 for k in ("empty", "full", "prefix", "repeat", "past")) and n["random"] >= 1800
+    assert n["clock"] >= 300 and n["zero_length"] >= 10 and n["truncated"] >= 10
+    assert sum(1 for c in cs if not c["gc"]) >= 1000
+    err = collections.Counter(c["error"]["name"] for c in cs if c["error"])
+    assert err["URIError"] >= 20 and sum(err.values()) >= 60
+    # a target with the document's own state vector receives no structs, only the delete set
+    assert all(c["error"] is None for c in cs if c["kind"] == "full")
+
+
+@pytest.mark.parametrize("san", [False, True], ids=["opt", "asan_ubsan"])
+def test_device_core_compact_target_sv_host_build(san):
+    """ym_compact with target state vectors (encodeStateAsUpdate[V2](doc, sv)): the device code built for the
+    host against every target fixture of the reference (gc: true and false documents)."""
+    import core_host
+    from yjs_amd import pack_docs
+    for fmt in (1, 2):
+        for gc in (True, False):
+            cs = [c for c in compact_cases.load_sv() if c["fmt"] == fmt and c["gc"] == gc]
+            if san:
+                seen = collections.Counter()
+                cs = [c for c in cs if seen.update([c["group"] + c["kind"]]) is None and seen[c["group"] + c["kind"]] <= 6]
+            a, o, d = pack_docs([c["inputs"] for c in cs])
+            sa, so, _ = pack_docs([[c["sv"]] for c in cs])
+            outs, st = core_host.run("compact" if gc else "compact_nogc", fmt, a, o, d, sa, so, san=san)
+            bad = [(c["id"], why) for c, out, s in zip(cs, outs, st) if (why := compact_cases.mismatch(c, s, out))]
+            assert not bad, f"fmt {fmt} gc {gc}: {len(bad)}/{len(cs)} differ: {bad[:8]}"

@@ -57,6 +57,29 @@ def test_compact_nogc_fixtures_on_gpu(engine, fmt):
     assert sum(1 for c in cs if c["differs"]) > 200
 
 
+@pytest.mark.parametrize("gc", [True, False], ids=["gc", "nogc"])
+@pytest.mark.parametrize("fmt", [1, 2])
+def test_compact_target_sv_fixtures_on_gpu(engine, fmt, gc):
+    """ym_compact with a target state vector per document (encodeStateAsUpdate[V2](doc, sv)): every target
+    fixture of the reference -- empty / full / prefix / random / repeated / past-the-state vectors, each
+    clock of the slice documents (surrogate pairs cut by str.slice), malformed vectors.  (The C5 workload
+    document's targets, one lane each at HBM latency, are pinned through the host build of the same device
+    code, tests/test_compact.py.)"""
+    from yjs_amd import pack_docs
+    cs = [c for c in compact_cases.load_sv() if c["fmt"] == fmt and c["gc"] == gc and c["group"] != "wl_c5"]
+    a, o, d = pack_docs([c["inputs"] for c in cs])
+    sa, so, _ = pack_docs([[c["sv"]] for c in cs])
+    oa, oo, ol, st = engine.run_host("compact" if gc else "compact_nogc", fmt, a, o, d, sa, so)
+    bad = []
+    for i, c in enumerate(cs):
+        got = oa[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() if st[i] == 0 else None
+        why = compact_cases.mismatch(c, st[i], got)
+        if why:
+            bad.append((c["id"], why))
+    assert not bad, f"{len(bad)}/{len(cs)} differ: {bad[:8]}"
+    assert len(cs) > 400
+
+
 @pytest.mark.parametrize("name", ["c2_v1", "c2_v2", "c4_v1"])
 def test_compact_workload_matches_oracle(engine, name):
     """Every template document of the C2 / C4 workloads (bench_data/) compacted on the GPU equals the

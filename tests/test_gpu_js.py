@@ -20,6 +20,7 @@ def test_js_api_golden():
     assert r.returncode == 0 and res["bad"] == 0, res
     assert res["ok"] >= 990 and res["unsupported"] == 0, res
     assert res["async_ok"] >= 800, res  # mergeUpdatesBatchAsync (napi_async_work) over the golden merges
+    assert res["compact_ok"] >= 1000, res  # compactUpdatesBatch with gc: false and target state vectors
 
 
 @pytest.mark.skipif(shutil.which("node") is None, reason="node not installed on this box")

@@ -487,7 +487,9 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   uint64_t dev_cap = out->cap;
   if (host) {  // stage inputs
     uint64_t abytes = upd_off[b->n_upd];
-    const uint64_t svb = op == OP_DIFF ? sv_off[nd] : 0;
+    // ym_diff's state vectors; ym_compact's optional target state vectors
+    const bool stage_sv = op == OP_DIFF || (op == OP_COMPACT && svp);
+    const uint64_t svb = stage_sv ? sv_off[nd] : 0;
     const uint64_t bound = 4 * abytes + 2 * svb + 128ull * nd + 8192;
     dev_cap = out->cap > bound ? out->cap : bound;
     if (S->min_stage_cap > dev_cap) dev_cap = S->min_stage_cap;
@@ -498,7 +500,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
     A = S->in_arena.as<uint8_t>();
     upd_off = S->in_off.as<uint64_t>();
     doc_upd = S->in_doc.as<uint32_t>();
-    if (op == OP_DIFF) {
+    if (stage_sv) {
       uint64_t sb = sv_off[nd];
       if (S->in_sv.ensure(sb + 16) || S->in_svoff.ensure((nd + 1) * 8ull)) return -2;
       HIPCHK(hipMemcpyAsync(S->in_sv.p, svp, sb, hipMemcpyHostToDevice, st));
@@ -535,8 +537,8 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
     return 0;
   };
   j.doc_upd = doc_upd;
-  j.sv = svp;
-  j.sv_off = sv_off;
+  j.sv = op == OP_DIFF || op == OP_COMPACT ? svp : nullptr;
+  j.sv_off = j.sv ? sv_off : nullptr;
   j.op = op;
   j.v2 = (b->format & 0xff) == YM_V2;
   j.dsref = op == OP_DSMERGE && (b->format & YM_DS_REF) != 0;

@@ -147,6 +147,7 @@ struct Doc {
   uint32_t gen;
   Tx *tx;
   uint32_t *ord;       // output order of the store's clients (descending)
+  int64_t *svst;       // target state vector: per client the first clock written, -1: none (doc_write)
 };
 
 YM_INL Item &IT(Doc &d, int32_t i) { return d.it[i]; }
@@ -322,12 +323,11 @@ YM_HOT void ds_sort_merge(DSet &ds) {
 // ---- content splice / merge ------------------------------------------------------------------------
 // units of a string piece's UTF-8 body
 YM_INL uint32_t body16(const Piece &p) { return p.n16 - p.fffd - p.lo - p.hi - p.tfffd; }
-// splits piece q at unit k (0 < k < n16): q keeps [0, k), the new piece (returned, linked after q) [k, n16)
-YM_HOT int32_t piece_cut_str(Doc &d, int32_t q, uint32_t k) {
-  const int32_t r = new_piece(d);
-  if (r == NIL) return NIL;
-  Piece P = d.pc[q];
-  Piece L = P, R = P;
+// the two parts of string piece P split at unit k (0 < k < n16): str.slice(0, k) and str.slice(k) of the
+// piece's units, a surrogate pair cut in two leaving a lone high half in L and a lone low half in R
+YM_INL void piece_split_str(const Ctx &c, const Piece &P, uint32_t k, Piece &L, Piece &R) {
+  L = P;
+  R = P;
   L.tfffd = 0; L.hi = 0;
   R.fffd = 0; R.lo = 0;
   uint32_t u = k;
@@ -348,7 +348,7 @@ YM_HOT int32_t piece_cut_str(Doc &d, int32_t q, uint32_t k) {
     const uint32_t nb = body16(P);
     if (u <= nb) {
       int split = 0;
-      const uint64_t b = utf8_unit_offset(*d.c, P.off, P.n, u, &split);
+      const uint64_t b = utf8_unit_offset(c, P.off, P.n, u, &split);
       L.n = (uint32_t)b;
       L.hi = split ? 1 : 0;
       L.n16 = k;
@@ -367,7 +367,14 @@ YM_HOT int32_t piece_cut_str(Doc &d, int32_t q, uint32_t k) {
       (void)u;
     }
   }
-  R.next = P.next;
+}
+// splits piece q at unit k (0 < k < n16): q keeps [0, k), the new piece (returned, linked after q) [k, n16)
+YM_HOT int32_t piece_cut_str(Doc &d, int32_t q, uint32_t k) {
+  const int32_t r = new_piece(d);
+  if (r == NIL) return NIL;
+  Piece L, R;
+  piece_split_str(*d.c, d.pc[q], k, L, R);
+  R.next = d.pc[q].next;
   L.next = r;
   d.pc[q] = L;
   d.pc[r] = R;
@@ -1488,11 +1495,13 @@ YM_HOT void cd_transact(Doc &d, Reader &r) {
 // ---- writing -----------------------------------------------------------------------------------------
 // ContentString.write of a piece list: V2 through the column's StringEncoder (lone halves pair up across
 // strings), V1 writeVarString (a lone surrogate throws URIError)
-YM_HOT void write_str(Ctx &c, Enc &e, const Doc &d, int32_t head) {
+// (first: the chain's first piece, possibly a local one linked into the document's list; nullptr: empty)
+YM_INL const Piece *pnext(const Doc &d, const Piece *p) { return p->next == NIL ? nullptr : &d.pc[p->next]; }
+YM_HOT void write_str(Ctx &c, Enc &e, const Doc &d, const Piece *first) {
   if (e.v2) {
     uint32_t n16 = 0;
-    for (int32_t q = head; q != NIL && !c.err; q = d.pc[q].next) {
-      const Piece &p = d.pc[q];
+    for (const Piece *pp = first; pp && !c.err; pp = pnext(d, pp)) {
+      const Piece &p = *pp;
       const Span s = {p.off, p.n, 0, p.fffd, p.lo, p.hi, 0};
       e_str_bytes(e, c, s);
       if (p.tfffd) {
@@ -1506,8 +1515,8 @@ YM_HOT void write_str(Ctx &c, Enc &e, const Doc &d, int32_t head) {
   }
   uint64_t bytes = 0;
   bool pend = false;
-  for (int32_t q = head; q != NIL; q = d.pc[q].next) {
-    const Piece &p = d.pc[q];
+  for (const Piece *pp = first; pp; pp = pnext(d, pp)) {
+    const Piece &p = *pp;
     if (p.fffd) { if (pend) { seterr(c, ST_URI); return; } bytes += 3; }
     if (p.lo) { if (!pend) { seterr(c, ST_URI); return; } bytes += 4; pend = false; }
     if (pend && (p.n || p.hi || p.tfffd)) { seterr(c, ST_URI); return; }
@@ -1518,8 +1527,8 @@ YM_HOT void write_str(Ctx &c, Enc &e, const Doc &d, int32_t head) {
   if (pend) { seterr(c, ST_URI); return; }
   ovu(e.rest, (int64_t)bytes);
   uint32_t hi = 0;
-  for (int32_t q = head; q != NIL; q = d.pc[q].next) {
-    const Piece &p = d.pc[q];
+  for (const Piece *pp = first; pp; pp = pnext(d, pp)) {
+    const Piece &p = *pp;
     if (p.fffd) { o8(e.rest, 0xEF); o8(e.rest, 0xBF); o8(e.rest, 0xBD); }
     if (p.lo) {
       const uint32_t cp = 0x10000 + ((hi - 0xD800) << 10) + (sur_lo(c, p.off - 4) - 0xDC00);
@@ -1530,15 +1539,20 @@ YM_HOT void write_str(Ctx &c, Enc &e, const Doc &d, int32_t head) {
     if (p.tfffd) { o8(e.rest, 0xEF); o8(e.rest, 0xBF); o8(e.rest, 0xBD); }
   }
 }
-// Item.write / GC.write with offset 0 (Item.js:625-658, GC.js:45-48)
-YM_HOT void item_write(Ctx &c, Enc &e, const Doc &d, int32_t i) {
+// Item.write / GC.write (Item.js:625-658, GC.js:45-48).  off > 0 (the first struct of a client written from
+// a target state vector's clock, encoding.js:71-84): the origin becomes (client, clock + off - 1) and the
+// content is written from unit off (ContentString str.slice(off), ContentAny / ContentJSON elements
+// from off, ContentDeleted / GC len - off; other contents have length 1, so off is 0)
+YM_HOT void item_write(Ctx &c, Enc &e, const Doc &d, int32_t i, int64_t off = 0) {
   const Item &x = d.it[i];
-  if (x.gc) { e_info(e, 0); e_len(e, x.len); return; }
-  const int info = (x.ref & 31) | (x.has_origin ? 0x80 : 0) | (x.has_right ? 0x40 : 0) | (x.has_psub ? 0x20 : 0);
+  if (x.gc) { e_info(e, 0); e_len(e, x.len - off); return; }
+  const bool org = x.has_origin || off > 0;
+  const int info = (x.ref & 31) | (org ? 0x80 : 0) | (x.has_right ? 0x40 : 0) | (x.has_psub ? 0x20 : 0);
   e_info(e, info);
-  if (x.has_origin) e_left(e, x.oc, x.ok);
+  if (off > 0) e_left(e, x.client, x.clock + off - 1);
+  else if (x.has_origin) e_left(e, x.oc, x.ok);
   if (x.has_right) e_right(e, x.rc, x.rk);
-  if (!x.has_origin && !x.has_right) {
+  if (!org && !x.has_right) {
     if (x.parent == NIL) { seterr(c, ST_UNEXPECTED); return; }
     const Type &P = d.ty[x.parent];
     if (P.item == NIL) { e_parent_info(e, 1); e_string(e, c, P.key); }
@@ -1546,12 +1560,28 @@ YM_HOT void item_write(Ctx &c, Enc &e, const Doc &d, int32_t i) {
     if (x.has_psub) e_string(e, c, x.psub);
   }
   switch (x.ref) {
-    case 1: e_len(e, x.len); break;
-    case 4: write_str(c, e, d, x.chead); break;
+    case 1: e_len(e, x.len - off); break;
+    case 4: {
+      const Piece *first = x.chead == NIL ? nullptr : &d.pc[x.chead];
+      Piece L, R;
+      if (off > 0) {  // the piece holding unit off, cut there (the document's pieces stay as they are)
+        uint32_t skip = (uint32_t)off;
+        while (first && skip >= first->n16) { skip -= first->n16; first = pnext(d, first); }
+        if (first && skip > 0) {
+          piece_split_str(c, *first, skip, L, R);
+          R.next = first->next;
+          first = &R;
+        }
+      }
+      write_str(c, e, d, first);
+      break;
+    }
     case 2: case 8: {
-      e_len(e, x.len);
+      e_len(e, x.len - off);
+      uint64_t g = 0;  // element index within the content
       for (int32_t q = x.chead; q != NIL && !c.err; q = d.pc[q].next)
-        for (uint32_t k = 0; k < d.pc[q].n && !c.err; k++) {
+        for (uint32_t k = 0; k < d.pc[q].n && !c.err; k++, g++) {
+          if ((int64_t)g < off) continue;
           const Elem &el = d.el[d.pc[q].off + k];
           if (x.ref == 8) {
             if (el.nc) canon_out(c, e.rest, c.A, el.off, el.off + el.n, G_ANY, T_ANY);
@@ -1575,16 +1605,30 @@ YM_HOT void item_write(Ctx &c, Enc &e, const Doc &d, int32_t i) {
     }
   }
 }
-// encodeStateAsUpdate[V2](doc): writeClientsStructs (clients descending, every struct from clock 0) then
-// writeDeleteSet(createDeleteSetFromStructStore(store)) (store order, adjacent deleted structs joined)
+// encodeStateAsUpdate[V2](doc, targetStateVector): writeClientsStructs (encoding.js:94-116: clients
+// descending, each from its clock in the target state vector -- 0 when absent; a client the target already
+// has up to its state is left out) then writeDeleteSet(createDeleteSetFromStructStore(store)) (store
+// order, adjacent deleted structs joined; the whole delete set, whatever the target).  d.svst: per client
+// the first clock to write, -1 to leave the client out (nullptr: every client from 0)
 YM_BIG void doc_write(Ctx &c, Enc &e, Doc &d, uint32_t *ord) {
-  ovu(e.rest, (int64_t)d.cl.n);
+  uint32_t nw = d.cl.n;
+  if (d.svst) {
+    nw = 0;
+    for (uint32_t ci = 0; ci < d.cl.n; ci++) nw += d.svst[ci] >= 0;
+  }
+  ovu(e.rest, (int64_t)nw);
   for (uint32_t oi = 0; oi < d.cl.n && !c.err; oi++) {
     const Cl &s = d.cl.p[ord[oi]];
-    ovu(e.rest, (int64_t)s.a.n);
+    const int64_t clock = d.svst ? d.svst[ord[oi]] : 0;
+    if (clock < 0) continue;
+    if (s.a.n == 0) { ovu(e.rest, 0); e_client(e, s.client); ovu(e.rest, 0); continue; }
+    const uint32_t i0 = clock == 0 ? 0 : find_index(d, (int32_t)ord[oi], clock);  // writeStructs, :71-84
+    if (c.err) return;
+    ovu(e.rest, (int64_t)(s.a.n - i0));
     e_client(e, s.client);
-    ovu(e.rest, 0);
-    for (uint32_t i = 0; i < s.a.n && !c.err; i++) item_write(c, e, d, s.a.p[i]);
+    ovu(e.rest, clock);
+    item_write(c, e, d, s.a.p[i0], clock - d.it[s.a.p[i0]].clock);
+    for (uint32_t i = i0 + 1; i < s.a.n && !c.err; i++) item_write(c, e, d, s.a.p[i]);
   }
   uint32_t ndc = 0;
   for (uint32_t ci = 0; ci < d.cl.n; ci++) {
@@ -1653,9 +1697,10 @@ YM_INL WsSize ws_size(uint32_t k, uint64_t bytes, uint32_t mul) {
 // its encodeStateAsUpdate[V2].  out == nullptr: sizing only (L.total); else the bytes are written there.
 // The engine state stays in the workspace between the two calls of one document (pass 2 only writes).
 struct Result { uint64_t col[C_N]; uint64_t rest, total; };
-// flags: bit 0 V2, bit 1 Doc({ gc: false })
+// flags: bit 0 V2, bit 1 Doc({ gc: false }).  svp / svlen: the encoded target state vector of
+// encodeStateAsUpdate[V2](doc, sv) (svp == nullptr: none, every struct is written)
 YM_BIG void compact_doc(Ctx &c, uint8_t *ws, const WsSize &z, uint32_t flags, const uint64_t *upd_off, uint32_t u0, uint32_t k,
-                        Result &R, uint8_t *out) {
+                        const uint8_t *svp, uint64_t svlen, Result &R, uint8_t *out) {
   const uint32_t v2 = flags & 1;
   Doc *dp = (Doc *)ws;  // the document's state heads its workspace
   Arena *ap = (Arena *)(ws + al16(sizeof(Doc)));
@@ -1711,6 +1756,25 @@ YM_BIG void compact_doc(Ctx &c, uint8_t *ws, const WsSize &z, uint32_t flags, co
       uint32_t j = i;
       while (j > 0 && d.cl.p[ord[j - 1]].client < d.cl.p[v].client) { ord[j] = ord[j - 1]; j--; }
       ord[j] = v;
+    }
+    d.svst = nullptr;
+    if (svp) {  // decodeStateVector (encoding.js:536-565, DSDecoderV1 for both formats; later entries win)
+      int64_t *st = (int64_t *)aalloc(c, *ap, 8ull * (d.cl.n + 1));
+      if (c.err) return;
+      for (uint32_t i = 0; i < d.cl.n; i++) st[i] = 0;  // absent from the target: from clock 0
+      Ctx cs = {0, svp};
+      Rd sd = {0, svlen, 0};
+      const uint32_t ns = rd_vu(cs, sd);
+      for (uint32_t i = 0; i < ns && !cs.err; i++) {
+        const int64_t client = rd_vu(cs, sd);
+        const int64_t clock = rd_vu(cs, sd);
+        if (cs.err) break;
+        const int32_t ci = cd_client(d, client);
+        // a client the target has up to (or past) its state is left out (encoding.js:97-102)
+        if (ci != NIL) st[ci] = cl_state(d, ci) > clock ? clock : -1;
+      }
+      if (cs.err) { seterr(c, cs.err); return; }
+      d.svst = st;
     }
   }
   uint32_t *ord = d.ord;

@@ -191,11 +191,12 @@ class Engine:
         b.n_upd = n_upd
         b.format = self._format(op, fmt)
         b.mem = 0
-        if op == "diff":
-            sv_arena = np.ascontiguousarray(sv_arena, np.uint8)
+        if op == "diff" or sv_arena is not None:  # ym_diff's state vectors / ym_compact's target vectors
+            # (a non-null arena even when every vector is empty: for ym_compact NULL means "no target")
+            sv_arena = np.concatenate([np.ascontiguousarray(sv_arena, np.uint8), np.zeros(1, np.uint8)])
             sv_off = np.ascontiguousarray(sv_off, np.uint64)
             keep += [sv_arena, sv_off]
-            b.sv_arena = sv_arena.ctypes.data if sv_arena.size else None
+            b.sv_arena = sv_arena.ctypes.data
             b.sv_off = sv_off.ctypes.data
         cap = int(self.lib.ym_out_bound(ctypes.byref(b)))
         fn = self._fn(op)
@@ -229,7 +230,7 @@ class Engine:
         b.n_upd = upd_off.numel() - 1
         b.format = self._format(op, fmt) | _off_flag(upd_off)
         b.mem = 1
-        if op == "diff":
+        if op == "diff" or sv_arena is not None:
             b.sv_arena = sv_arena.data_ptr()
             b.sv_off = sv_off.data_ptr()
         o = _Out(out_arena.data_ptr(), out_arena.numel(), out_off.data_ptr(), out_len.data_ptr(), status.data_ptr(), 0)
@@ -250,7 +251,7 @@ class Engine:
         b.n_upd = upd_off.numel() - 1
         b.format = self._format(op, fmt) | _off_flag(upd_off)
         b.mem = 1
-        if op == "diff":
+        if op == "diff" or sv_arena is not None:
             b.sv_arena = sv_arena.data_ptr()
             b.sv_off = sv_off.data_ptr()
         o = _Out(out_arena.data_ptr(), out_arena.numel(), out_off.data_ptr(), out_len.data_ptr(), status.data_ptr(), 0)
@@ -311,20 +312,29 @@ def encodeStateVectorFromUpdateBatch(updates, fmt=1, raise_errors=False):
     return _unpack(*_engine().run_host("sv", fmt, arena, upd_off, doc_upd), raise_errors)
 
 
-def compactUpdatesBatch(docs, fmt=1, raise_errors=False, gc=True):
+def compactUpdatesBatch(docs, fmt=1, raise_errors=False, gc=True, target_state_vectors=None):
     """Doc round-trip compaction (ym_compact) over a batch: per document, encodeStateAsUpdate[V2] of a fresh
     Doc({ gc }) after applyUpdate[V2] of every update in order (the reference's own compaction:
-    src/utils/encoding.js readUpdate / encodeStateAsUpdate, Transaction.js cleanupTransactions)."""
+    src/utils/encoding.js readUpdate / encodeStateAsUpdate, Transaction.js cleanupTransactions).
+    target_state_vectors: one encoded state vector per document -- encodeStateAsUpdate[V2](doc, sv), only
+    what the target is missing (encoding.js:94-116; the sync protocol's step-2 answer)."""
     arena, upd_off, doc_upd = pack_docs(docs)
-    return _unpack(*_engine().run_host("compact" if gc else "compact_nogc", fmt, arena, upd_off, doc_upd), raise_errors)
+    sva = svo = None
+    if target_state_vectors is not None:
+        assert len(target_state_vectors) == len(docs)
+        sva, svo, _ = pack_docs([[s] for s in target_state_vectors])
+    return _unpack(*_engine().run_host("compact" if gc else "compact_nogc", fmt, arena, upd_off, doc_upd, sva, svo),
+                   raise_errors)
 
 
-def compactUpdates(updates):
-    return compactUpdatesBatch([list(updates)], 1, True)[0]
+def compactUpdates(updates, target_state_vector=None):
+    t = None if target_state_vector is None else [target_state_vector]
+    return compactUpdatesBatch([list(updates)], 1, True, target_state_vectors=t)[0]
 
 
-def compactUpdatesV2(updates):
-    return compactUpdatesBatch([list(updates)], 2, True)[0]
+def compactUpdatesV2(updates, target_state_vector=None):
+    t = None if target_state_vector is None else [target_state_vector]
+    return compactUpdatesBatch([list(updates)], 2, True, target_state_vectors=t)[0]
 
 
 def mergeUpdates(updates):
