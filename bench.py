@@ -55,6 +55,11 @@ def parse():
     p.add_argument("--rotate", type=int, default=12,
                    help="distinct device copies of the batch, one per step in turn (12 x the C2 batch = "
                         "~1 GB of inputs + outputs: above the 256 MiB on-die cache, so the roofline is HBM's)")
+    p.add_argument("--submit", default="auto", choices=["auto", "async", "sync"],
+                   help="async: each step is one ym_merge_async call (the LDS fast path enqueued on the "
+                        "stream, no host round trip; the serving loop's form), verified in the warmup to "
+                        "complete every document with the bytes of ym_merge; sync: one ym_merge call per "
+                        "step (host waits for each); auto: async when the verification passes")
     p.add_argument("--no-secondary", action="store_true",
                    help="skip the secondary workload lines (C4/C2-V2/C4-V2 merges, C3 diff/sv)")
     return p.parse_args()
@@ -422,7 +427,9 @@ def main():
     # u32 offsets (YM_OFF32) when the rank's arena is below 4 GiB: half the offset bytes per update
     off32 = in_bytes < 2 ** 32
     cap = 4 * in_bytes + 128 * n_docs + 8192  # fast-path slots (2*in + 64 per doc) + general-path room
-    stream = None if stub else torch.cuda.current_stream(dev)
+    # a stream of its own (torch's default stream handle is NULL, which the library reads as "its own
+    # stream"): the library's kernels and the bench's HIP events are then on the same stream
+    stream = None if stub else torch.cuda.Stream(device=dev)
     # `rotate` distinct device copies of the batch (inputs and output arrays), used one per step in turn:
     # each step reads and writes HBM lines the previous steps did not touch
     rot = max(1, args.rotate if not stub else 1)
@@ -460,20 +467,91 @@ def main():
     st0 = dict(eng.stats)
     out_bytes = int(o_len[o_st == 0].sum().item())
 
+    # asynchronous submission (ym_merge_async): used for the timed steps when, on every buffer set, it
+    # completes every document (no YM_PENDING) with exactly ym_merge's bytes, lengths and statuses
+    submit, async_calls, pending = "sync", None, None
+    if not stub and args.submit != "sync":
+        import torch as _t
+        pending = _t.zeros(1, dtype=_t.int32, device=dev)
+        async_calls = [eng.prepare_merge_async(fmt, *bufs[:3], *bufs[3:], pending=pending, stream=stream)
+                       for _, bufs in sets]
+        ok = True
+        for (call, bufs), acall in zip(sets, async_calls):
+            if not ok:
+                break
+            _, _, _, o_arena_k, o_off_k, o_len_k, o_st_k = bufs
+            if call()[0] != 0:
+                ok = False
+                break
+            sync()
+            ref = (o_arena_k.clone(), o_off_k.clone(), o_len_k.clone(), o_st_k.clone())
+            o_arena_k.fill_(0xA5)
+            o_len_k.fill_(-1)
+            o_st_k.fill_(-1)
+            sync()  # (torch's fills run on its default stream, the library on `stream`)
+            rc = acall()
+            sync()
+            why = [k for k, bad in (("rc", rc != 0), ("pending", int(pending.item()) != 0),
+                                    ("status", not bool((o_st_k == ref[3]).all().item())),
+                                    ("len", not bool((o_len_k == ref[2]).all().item())),
+                                    ("off", not bool((o_off_k == ref[1]).all().item()))) if bad]
+            ok = not why
+            if why:
+                print(f"bench: ym_merge_async verification failed ({', '.join(why)}); sync submission",
+                      file=sys.stderr)
+            if ok:  # every output's bytes: the ranges [off, off + len) of the documents that succeeded
+                m = ref[3] == 0
+                off_t, len_t = ref[1][m], ref[2][m]
+                if off_t.numel():
+                    end = int((off_t + len_t).max().item())
+                    mark = _t.zeros(end + 1, dtype=_t.int32, device=dev)
+                    mark.index_add_(0, off_t, _t.ones_like(off_t, dtype=_t.int32))
+                    mark.index_add_(0, off_t + len_t, -_t.ones_like(off_t, dtype=_t.int32))
+                    inside = mark.cumsum(0)[:end] > 0
+                    ok = bool((o_arena_k[:end][inside] == ref[0][:end][inside]).all().item())
+        if ok:
+            submit = "async"
+        elif args.submit == "async":
+            raise RuntimeError("ym_merge_async did not reproduce ym_merge on this batch")
+        pending.zero_()
+
     if world > 1:
         dist.barrier()
     sync()
     fast_ms, dev_ms = [], []
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        s = eng.last_stats
-        fast_ms.append(s.fast_ms + s.large_ms)  # LDS fast path, or the large-document pipeline (C5)
-        dev_ms.append(s.device_ms)
-    sync()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    if submit == "async":
+        import torch as _t
+        # one HIP event pair on the kernels' stream around the K back-to-back launches (an event pair per
+        # launch would put two markers between consecutive kernels): their span / K is the average launch
+        # duration, inter-kernel gaps included (an upper bound; the rocprofv3 kernel average is the check)
+        ev0, ev1 = _t.cuda.Event(enable_timing=True), _t.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for i in range(args.steps):
+            rc = async_calls[i % rot]()
+            if rc != 0:
+                raise RuntimeError(f"ym_merge_async rc={rc}")
+        ev1.record(stream)
+        sync()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        # every document of every timed step completed on the fast path (else the line is invalid)
+        if int(pending.item()) != 0:
+            raise RuntimeError("ym_merge_async declined documents in the timed steps")
+        fast_ms = [ev0.elapsed_time(ev1) / args.steps]  # the kernel's launches, HIP events on its stream
+        dev_ms = fast_ms
+    else:
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+            s = eng.last_stats
+            fast_ms.append(s.fast_ms + s.large_ms)  # LDS fast path, or the large-document pipeline (C5)
+            dev_ms.append(s.device_ms)
+        sync()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
 
     # the only collectives: max of the timed region, sum of per-rank counters (RCCL over xGMI)
     from yjs_amd.distributed import reduce_run
@@ -526,6 +604,10 @@ def main():
             "docs_fast_path": int(fast_all), "docs_general_path": int(gen_all), "doc_errors": int(err_all),
             "device_ms_per_step": round(float(np.mean(dev_ms)), 4),
             "working_set_bytes": int((in_bytes + cap) * rot), "rotated_buffer_sets": rot,
+            "submission": ("async: one ym_merge_async per step, enqueued back to back on the stream (no host "
+                           "round trip per step), verified in the warmup to give ym_merge's bytes for every "
+                           "document of every buffer set; 0 documents declined in the timed steps"
+                           if submit == "async" else "sync: one ym_merge call per step (the host waits for each)"),
             "roofline": {"kernel": kernel_name, "bound": "issue", "roof": "hbm", "achieved": round(achieved, 2),
                          "limiter": "instruction issue (PMC: SQ_ACTIVE_INST_ANY per SIMD ~ the launch's duration, "
                                     "HBM traffic ~1.2x the algorithmic bytes; DESIGN.md section 4.1); frac is "

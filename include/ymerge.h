@@ -49,6 +49,7 @@ enum {
   YM_ERR_UNSUPPORTED = 7, /* valid input needing a canonicalisation the engine does not implement */
   YM_ERR_METHOD = 8,      /* Error('Method unimplemented')                                       */
   YM_ERR_CAPACITY = 9,    /* output arena too small: call again with a larger cap                */
+  YM_PENDING = 101,       /* ym_merge_async only: declined by the fast path, pass it to ym_merge  */
 };
 
 #define YM_STATUS_CLASS(s) ((s) & 0xff)
@@ -113,6 +114,15 @@ uint64_t ym_out_bound(const ym_batch *b); /* a capacity that is normally suffici
 /* stream: a hipStream_t (NULL = the library's stream for the device).  Return value: 0, or
  * YM_ERR_CAPACITY when out->used > out->cap (nothing useful was written), or a negative HIP error. */
 int ym_merge(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
+/* Asynchronous ym_merge for device batches (the serving loop: calls queue back to back on `stream` and
+ * the host never waits).  Runs the LDS fast path only (small documents: <= 128 updates, <= 2.5 KB V1;
+ * the C2 / C4 shapes) and returns once the kernel is enqueued; the results are valid when the stream has
+ * drained.  Each output lands in the slot region [0, 2 * input bytes + 64 * n_docs + 64) of out->arena
+ * (out->cap below that: YM_ERR_CAPACITY for the documents that do not fit); out->used is not written.
+ * A document the fast path declines (larger, rich nested content, invalid input) gets status YM_PENDING
+ * and increments *pending (a uint32_t in device memory, or NULL): run those through ym_merge.
+ * Return value: 0, or a negative error (not a device batch, HIP launch failure). */
+int ym_merge_async(const ym_batch *b, ym_out *out, void *stream, uint32_t *pending);
 int ym_diff(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
 int ym_sv(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
 /* convertUpdateFormatV1ToV2 (b->format = YM_V1) / convertUpdateFormatV2ToV1 (b->format = YM_V2): one

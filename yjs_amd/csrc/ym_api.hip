@@ -830,6 +830,51 @@ uint64_t ym_out_bound(const ym_batch *b) {
 }
 
 int ym_merge(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_MERGE, b, out, stream, stats); }
+
+// Asynchronous submission (include/ymerge.h): the LDS fast path alone, enqueued on the stream; no host
+// round trip, no finishing kernel.  Declined documents keep status ST_PENDING (YM_PENDING) and are counted
+// into *pending (device memory); the per-document capacity check of the fast kernels reports YM_ERR_CAPACITY.
+int ym_merge_async(const ym_batch *b, ym_out *out, void *stream, uint32_t *pending) {
+  if (!b || !out || b->mem != YM_MEM_DEVICE) return -1;
+  DevState *S = state();
+  {
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || cur != S->device) HIPCHK(hipSetDevice(S->device));
+  }
+  hipStream_t st = stream ? (hipStream_t)stream : S->stream;
+  const uint32_t nd = b->n_docs;
+  if (nd == 0) return 0;
+  if (S->counters.ensure(1024)) return -2;
+  GeneralJob j;
+  memset(&j, 0, sizeof(j));
+  j.A = b->arena;
+  const bool off32 = (b->format & YM_OFF32) != 0;
+  j.v2 = (b->format & 0xff) == YM_V2;
+  if (off32) {
+    j.upd_off32 = reinterpret_cast<const uint32_t *>(b->upd_off);
+    if (j.v2) {  // the V2 kernel reads u64 offsets: widened into the library's buffer (stream-ordered)
+      if (S->in_off.ensure((b->n_upd + 1) * 8ull)) return -2;
+      k_widen<<<(b->n_upd + 256) / 256, 256, 0, st>>>(j.upd_off32, S->in_off.as<uint64_t>(), b->n_upd + 1);
+      j.upd_off = S->in_off.as<uint64_t>();
+    }
+  } else {
+    j.upd_off = b->upd_off;
+  }
+  j.doc_upd = b->doc_upd;
+  j.op = OP_MERGE;
+  j.status = out->status;
+  j.out = out->arena;
+  j.cap = out->cap;
+  j.out_off = out->out_off;
+  j.out_len = out->out_len;
+  j.n = nd;
+  j.pend_list = nullptr;  // declines are only counted
+  j.pend_count = pending ? pending : reinterpret_cast<uint32_t *>(S->counters.as<uint64_t>() + 15);
+  int fr = fast_launch(OP_MERGE, j, b->n_upd, st);
+  if (fr == 0) fr = fast2_launch(OP_MERGE, j, b->n_upd, st);
+  if (fr < 0) return fr;
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
 int ym_diff(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_DIFF, b, out, stream, stats); }
 int ym_sv(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_SV, b, out, stream, stats); }
 int ym_convert(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_CONV, b, out, stream, stats); }

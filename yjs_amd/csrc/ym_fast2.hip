@@ -125,7 +125,8 @@ __device__ __forceinline__ uint32_t rd_idif(IdifD &r) {
 
 __device__ __forceinline__ void decline(const GeneralJob &j, uint32_t d) {
   j.status[d] = ST_PENDING;
-  j.pend_list[atomicAdd(j.pend_count, 1u)] = d;
+  const uint32_t q = atomicAdd(j.pend_count, 1u);
+  if (j.pend_list) j.pend_list[q] = d;  // (ym_merge_async: declines are only counted)
 }
 
 // Walks one V2 update (lane-private decoders) and appends struct records and delete ranges.  NESTED:

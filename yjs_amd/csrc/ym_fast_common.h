@@ -405,7 +405,8 @@ __device__ __forceinline__ void rank_exact(uint32_t keys, uint32_t n, const uint
 // a declined document is appended to the general path's work list
 __device__ __forceinline__ void decline(const GeneralJob &j, uint32_t d) {
   j.status[d] = ST_PENDING;
-  j.pend_list[atomicAdd(j.pend_count, 1u)] = d;
+  const uint32_t q = atomicAdd(j.pend_count, 1u);
+  if (j.pend_list) j.pend_list[q] = d;  // (ym_merge_async: declines are only counted)
 }
 }  // namespace fastc
 }  // namespace ymk

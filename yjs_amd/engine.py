@@ -92,7 +92,8 @@ class _Stats(ctypes.Structure):
 
 
 EXPORTS = ("ym_init", "ym_shutdown", "ym_strerror", "ym_out_bound", "ym_merge", "ym_diff", "ym_sv", "ym_convert",
-           "ym_meta", "ym_ds_merge", "ym_snapshot", "ym_compact")
+           "ym_meta", "ym_ds_merge", "ym_snapshot", "ym_compact", "ym_merge_async")
+YM_PENDING = 101  # ym_merge_async: declined by the fast path (pass the document to ym_merge)
 
 
 def load_library(path=None):
@@ -106,6 +107,8 @@ def load_library(path=None):
     for fn in (L.ym_merge, L.ym_diff, L.ym_sv, L.ym_convert, L.ym_meta, L.ym_ds_merge, L.ym_snapshot, L.ym_compact):
         fn.argtypes = [ctypes.POINTER(_Batch), ctypes.POINTER(_Out), ctypes.c_void_p, ctypes.POINTER(_Stats)]
         fn.restype = ctypes.c_int
+    L.ym_merge_async.argtypes = [ctypes.POINTER(_Batch), ctypes.POINTER(_Out), ctypes.c_void_p, ctypes.c_void_p]
+    L.ym_merge_async.restype = ctypes.c_int
     return L
 
 
@@ -264,6 +267,30 @@ class Engine:
             rc = fn(pb, po, s, ps)
             return rc, o.used
         call.keep = keep
+        return call
+
+    def prepare_merge_async(self, fmt, arena, upd_off, doc_upd, out_arena, out_off, out_len, status, pending=None,
+                            stream=None):
+        """ym_merge_async over fixed device buffers: a zero-argument callable that enqueues one merge of the
+        batch on `stream` (the LDS fast path only) and returns its rc without waiting.  Declined documents
+        get status YM_PENDING and are counted into `pending` (a 1-element int32 CUDA tensor, or None)."""
+        b = _Batch()
+        b.arena = arena.data_ptr()
+        b.upd_off = upd_off.data_ptr()
+        b.doc_upd = doc_upd.data_ptr()
+        b.n_docs = doc_upd.numel() - 1
+        b.n_upd = upd_off.numel() - 1
+        b.format = int(fmt) | _off_flag(upd_off)
+        b.mem = 1
+        o = _Out(out_arena.data_ptr(), out_arena.numel(), out_off.data_ptr(), out_len.data_ptr(), status.data_ptr(), 0)
+        s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+        pend = ctypes.c_void_p(pending.data_ptr()) if pending is not None else None
+        fn = self.lib.ym_merge_async
+        pb, po = ctypes.byref(b), ctypes.byref(o)
+
+        def call():
+            return fn(pb, po, s, pend)
+        call.keep = (b, o)
         return call
 
     @property
