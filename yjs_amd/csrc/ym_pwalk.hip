@@ -1317,17 +1317,22 @@ __global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, uint8_t *done, con
 // k_big_v1 (a document this declines keeps done[d] == 0: the lane-per-document kernels and k_big_v1 follow).
 constexpr uint32_t SW_MIN = 80, SW_NSEC = 64, SW_NSV = 128, SW_SVS = 256, SW_NPATCH = 512, SW_DHS = 256;
 constexpr uint32_t SW_TV = 1u << 14, SW_CLEN = 1u << 17;  // table word: delta (12 bits) | skip << 12 | patch << 13 | TV | clen << 15
-enum { Q_W = 0, Q_CLIENT, Q_CLOCK, Q_X1, Q_PRELEN, Q_A0, Q_A1, Q_B0, Q_WRITTEN, Q_FCLOCK, Q_VAL, Q_END, Q_OUT, NQ = 13 };
-template <uint32_t SWB>
+// section record fields: the first NQ_SV are what the state vector / meta walks keep, the rest the diff's
+enum { Q_W = 0, Q_CLIENT, Q_CLOCK, Q_X1, Q_VAL, Q_END, NQ_SV, Q_PRELEN = NQ_SV, Q_A0, Q_A1, Q_B0, Q_WRITTEN, Q_FCLOCK, Q_OUT, NQ };
+// DF: the diff's arrays (sliced heads, info-byte patches, the target state vector's hash, the delete set's
+// client set) and section fields; the state vector / meta walks leave them out: 11.9 KB instead of 22.3 KB
+// per wave at the 2 KB window, 13 waves per CU instead of 7 (their 58 VGPRs allow more; the diff's 173 do not)
+template <uint32_t SWB, bool DF>
 struct SwLds {
+  static constexpr uint32_t NP = DF ? SW_NPATCH : 1, NS = DF ? SW_NSEC : 1, NH = DF ? SW_SVS : 1;
   uint8_t b[SWB + 48];
   uint32_t tab[SWB];
-  uint32_t sec[SW_NSEC][NQ];
-  uint8_t pre[SW_NSEC][PRE];
-  uint16_t ppos[SW_NPATCH];
-  uint8_t psec[SW_NPATCH], pval[SW_NPATCH];
-  uint32_t mkey[SW_SVS], mval[SW_SVS], svclk[SW_NSV];
-  uint32_t dhs[SW_DHS];
+  uint32_t sec[SW_NSEC][DF ? NQ : NQ_SV];
+  uint8_t pre[NS][PRE];
+  uint16_t ppos[NP];
+  uint8_t psec[NP], pval[NP];
+  uint32_t mkey[NH], mval[NH], svclk[DF ? SW_NSV : 1];
+  uint32_t dhs[DF ? SW_DHS : 1];
 };
 // lockstep lib0 readVarUint over the LDS bytes (uniform o): canonical, u32
 __device__ __forceinline__ uint32_t sw_vu(const uint8_t *b, uint32_t &o, uint32_t lim, bool &bad) {
@@ -1345,7 +1350,7 @@ __device__ __forceinline__ uint32_t sw_vu(const uint8_t *b, uint32_t &o, uint32_
 // documents of (SWMIN, SWB] bytes
 template <int OP, uint32_t SWMIN, uint32_t SWB>
 __global__ void __launch_bounds__(64) k_pw_small(GeneralJob j, uint8_t *done, uint64_t pw_min) {
-  __shared__ SwLds<SWB> L;
+  __shared__ SwLds<SWB, OP == OP_DIFF> L;
   const uint32_t lane = threadIdx.x;
   for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
     const uint32_t u0 = j.doc_upd[d];
