@@ -102,16 +102,14 @@ def test_compact_workload_matches_oracle(engine, name):
     assert engine.stats["docs_general"] == n  # one kernel (ym_compact.hip) took every document
 
 
-def test_compact_c5_documents(engine, monkeypatch):
+def test_compact_c5_documents(engine):
     """The large C5 documents (1,024 clients, ~16 k updates, nested XML types): workspace growth on the device
     (ST_RETRY rounds) and the fixture hashes of the reference.  (The gapped C5 documents, every 5th update
     dropped, leave ~1,000 clients' structs and deletes pending; the reference re-examines every pending reader
     on every update, which one lane per document cannot do at HBM latency in a test's time: they are pinned
     through the host build of the same device code, tests/test_compact.py.)"""
     from yjs_amd import pack_docs
-    # one document per wave: the four documents of a format run side by side instead of as divergent lanes
-    # of one wave (one after the other)
-    monkeypatch.setenv("YMERGE_COMPACT_LANES", "1")
+    # (documents above YMERGE_COMPACT_BIG input bytes get a wave each: the four run side by side)
     cs = [c for c in compact_cases.load() if c["group"] == "wl_c5"]
     for fmt in (1, 2):
         sub = [c for c in cs if c["fmt"] == fmt]

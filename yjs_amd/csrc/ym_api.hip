@@ -28,7 +28,7 @@ int big_launch(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &pw);   
 int big2_launch(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &pw);      // ym_big2.hip
 __global__ void k_fast_region(GeneralJob j, uint32_t n_upd);                         // ym_fast.hip
 __global__ void k_compact_ws(GeneralJob j, uint64_t *ws_size);                        // ym_compact.hip
-template <int OCC> __global__ void k_compact(GeneralJob j, uint32_t lanes);
+template <int OCC> __global__ void k_compact(GeneralJob j, uint32_t lanes, uint64_t big, int part);
 }  // namespace ymk
 
 using namespace ymk;
@@ -335,6 +335,9 @@ int run_compact(DevState *S, hipStream_t st, GeneralJob j, uint32_t *list, uint3
   if (lanes < 1 || lanes > 64) lanes = 16;
   const char *eo = getenv("YMERGE_COMPACT_OCC");
   const int occ = eo && atoi(eo) == 2 ? 2 : 1;
+  // input bytes above which a document gets a wave of its own
+  const char *eg = getenv("YMERGE_COMPACT_BIG");
+  const uint64_t big = eg ? strtoull(eg, nullptr, 10) : 65536;
   const char *eb = getenv("YMERGE_COMPACT_WS_GB");
   const double gb = eb ? atof(eb) : 16.0;
   const uint64_t budget = gb > 0 ? (uint64_t)(gb * (double)(1ull << 30)) : (16ull << 30);
@@ -395,8 +398,13 @@ int run_compact(DevState *S, hipStream_t st, GeneralJob j, uint32_t *list, uint3
         continue;
       }
       jc.ws = S->ws.as<uint8_t>() - base;  // ws + ws_off[i] lands in this chunk's allocation
-      if (occ == 2) k_compact<2><<<(cnt + lanes - 1) / lanes, 64, 0, st>>>(jc, (uint32_t)lanes);
-      else k_compact<1><<<(cnt + lanes - 1) / lanes, 64, 0, st>>>(jc, (uint32_t)lanes);
+      // documents above `big` input bytes first, one per wave; then the rest, `lanes` per wave
+      const bool split = lanes > 1;
+      for (int part = split ? 1 : 0; part <= (split ? 2 : 0); part++) {
+        const uint32_t ln = part == 1 ? 1u : (uint32_t)lanes;
+        if (occ == 2) k_compact<2><<<(cnt + ln - 1) / ln, 64, 0, st>>>(jc, ln, big, part);
+        else k_compact<1><<<(cnt + ln - 1) / ln, 64, 0, st>>>(jc, ln, big, part);
+      }
     }
     HIPCHK(hipMemcpyAsync(S->pinned, j.counter_retry, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));

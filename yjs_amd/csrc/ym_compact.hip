@@ -27,8 +27,11 @@ __global__ void k_compact_ws(GeneralJob j, uint64_t *ws_size) {
 
 // OCC: waves per SIMD the register allocation targets (1: 256 VGPRs + 98 AGPRs, no spills; 2: 256 registers,
 // a few spills -- twice the waves in flight to hide the workspace's memory latency)
+// big: documents of more input bytes run in a launch of their own, one per wave (a wave's lanes run their
+// documents' divergent code one after the other: a few large documents sharing a wave serialise).
+// part 0: every document; 1: only those above `big`; 2: only those up to `big`
 template <int OCC>
-__global__ void __launch_bounds__(64, OCC) k_compact(GeneralJob j, uint32_t lanes) {
+__global__ void __launch_bounds__(64, OCC) k_compact(GeneralJob j, uint32_t lanes, uint64_t big, int part) {
   const uint32_t lane = threadIdx.x;
   if (lane >= lanes) return;
   const uint32_t i = blockIdx.x * lanes + lane;
@@ -36,6 +39,7 @@ __global__ void __launch_bounds__(64, OCC) k_compact(GeneralJob j, uint32_t lane
   const uint32_t d = cpt_doc(j, i);
   const uint32_t u0 = j.doc_upd[d], k = j.doc_upd[d + 1] - u0;
   const uint64_t bytes = j.upd_off[u0 + k] - j.upd_off[u0];
+  if ((part == 1 && bytes <= big) || (part == 2 && bytes > big)) return;
   const cpt::WsSize z = cpt::ws_size(k, bytes, j.parts_mul);
   uint8_t *ws = j.ws + j.ws_off[i];
   Ctx c = {0, j.A};
@@ -63,7 +67,7 @@ __global__ void __launch_bounds__(64, OCC) k_compact(GeneralJob j, uint32_t lane
   j.out_len[d] = c2.err ? 0 : R.total;
 }
 
-template __global__ void k_compact<1>(GeneralJob, uint32_t);
-template __global__ void k_compact<2>(GeneralJob, uint32_t);
+template __global__ void k_compact<1>(GeneralJob, uint32_t, uint64_t, int);
+template __global__ void k_compact<2>(GeneralJob, uint32_t, uint64_t, int);
 
 }  // namespace ymk
