@@ -17,7 +17,7 @@ def engine():
 
 
 def _dev(torch, arena, upd_off, doc_upd, cap, off32):
-    g = dict(arena=torch.from_numpy(arena).cuda(),
+    g = dict(arena=torch.from_numpy(np.array(arena, np.uint8)).cuda(),
              off=torch.from_numpy(upd_off.astype(np.uint32).view(np.int32) if off32 else upd_off.view(np.int64)).cuda(),
              doc=torch.from_numpy(doc_upd.view(np.int32)).cuda())
     nd = len(doc_upd) - 1
