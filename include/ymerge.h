@@ -121,6 +121,8 @@ int ym_merge(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
  * (out->cap below that: YM_ERR_CAPACITY for the documents that do not fit); out->used is not written.
  * A document the fast path declines (larger, rich nested content, invalid input) gets status YM_PENDING
  * and increments *pending (a uint32_t in device memory, or NULL): run those through ym_merge.
+ * V2 batches with YM_OFF32 widen their offsets into one buffer of the library's device state: calls of
+ * that kind on different streams must not overlap (on one stream they are ordered).
  * Return value: 0, or a negative error (not a device batch, HIP launch failure). */
 int ym_merge_async(const ym_batch *b, ym_out *out, void *stream, uint32_t *pending);
 int ym_diff(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
