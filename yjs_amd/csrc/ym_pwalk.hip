@@ -1315,7 +1315,10 @@ __global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, uint8_t *done, con
 // lockstep walk (canonical varuints, no empty or repeated client); then lane ci sizes / writes section ci
 // (wave prefix sums place them) and the wave copies the spans.  Same acceptance and bytes as k_pw_ms /
 // k_big_v1 (a document this declines keeps done[d] == 0: the lane-per-document kernels and k_big_v1 follow).
-constexpr uint32_t SW_MIN = 80, SW_NSEC = 64, SW_NSV = 128, SW_SVS = 256, SW_NPATCH = 512, SW_DHS = 256;
+// SW_NPRE: sliced first structs (one per section the diff cuts inside a struct) a document may have; more
+// and the document goes to the streamed walker (the pool instead of one per section: 20.0 KB of LDS per
+// diff wave instead of 22.3, 8 waves per CU instead of 7)
+constexpr uint32_t SW_MIN = 80, SW_NSEC = 64, SW_NSV = 128, SW_SVS = 256, SW_NPATCH = 512, SW_DHS = 256, SW_NPRE = 16;
 constexpr uint32_t SW_TV = 1u << 14, SW_CLEN = 1u << 17;  // table word: delta (12 bits) | skip << 12 | patch << 13 | TV | clen << 15
 // section record fields: the first NQ_SV are what the state vector / meta walks keep, the rest the diff's
 enum { Q_W = 0, Q_CLIENT, Q_CLOCK, Q_X1, Q_VAL, Q_END, NQ_SV, Q_PRELEN = NQ_SV, Q_A0, Q_A1, Q_B0, Q_WRITTEN, Q_FCLOCK, Q_OUT, NQ };
@@ -1324,7 +1327,7 @@ enum { Q_W = 0, Q_CLIENT, Q_CLOCK, Q_X1, Q_VAL, Q_END, NQ_SV, Q_PRELEN = NQ_SV, 
 // per wave at the 2 KB window, 13 waves per CU instead of 7 (their 58 VGPRs allow more; the diff's 173 do not)
 template <uint32_t SWB, bool DF>
 struct SwLds {
-  static constexpr uint32_t NP = DF ? SW_NPATCH : 1, NS = DF ? SW_NSEC : 1, NH = DF ? SW_SVS : 1;
+  static constexpr uint32_t NP = DF ? SW_NPATCH : 1, NS = DF ? SW_NPRE : 1, NH = DF ? SW_SVS : 1;
   uint8_t b[SWB + 48];
   uint32_t tab[SWB];
   uint32_t sec[SW_NSEC][DF ? NQ : NQ_SV];
@@ -1408,6 +1411,7 @@ __global__ void __launch_bounds__(64) k_pw_small(GeneralJob j, uint8_t *done, ui
     const uint32_t nsec = sw_vu(L.b, o, len, bad);
     uint32_t p = o, npatch = 0, prev = 0;
     if (bad || nsec > SW_NSEC) PW_DECLINE_R(2)
+    uint32_t npre = 0;  // sliced heads in the pool (diff)
     for (uint32_t ci = 0; ci < nsec && !why; ci++) {
       uint32_t q = p;
       const uint32_t ns = sw_vu(L.b, q, len, bad), client = sw_vu(L.b, q, len, bad), first_clock = sw_vu(L.b, q, len, bad);
@@ -1462,17 +1466,19 @@ __global__ void __launch_bounds__(64) k_pw_small(GeneralJob j, uint8_t *done, ui
               copying = true;
               written = 1;
               const uint32_t off = k > clock ? (uint32_t)(k - clock) : 0;
-              uint32_t prelen = 0, a0 = 0, a1 = 0, b0;
+              uint32_t prelen = 0, a0 = 0, a1 = 0, b0, slot = 0;
               if (off == 0) {
                 b0 = p;
                 patch = true;
               } else {
-                if (RF(slice_head(B, adj, p, nx, client, clock, cl, off, L.pre[ci], prelen, a0, a1) ? 1u : 0u) == 0) { why = 11; break; }
+                if (npre >= SW_NPRE) { why = 12; break; }
+                slot = npre++;
+                if (RF(slice_head(B, adj, p, nx, client, clock, cl, off, L.pre[slot], prelen, a0, a1) ? 1u : 0u) == 0) { why = 11; break; }
                 prelen = RF(prelen); a0 = RF(a0); a1 = RF(a1);
                 b0 = nx;
               }
               if (lane == 0) {
-                L.sec[ci][Q_PRELEN] = prelen;
+                L.sec[ci][Q_PRELEN] = prelen | slot << 8;  // (prelen <= PRE < 256)
                 L.sec[ci][Q_A0] = a0;
                 L.sec[ci][Q_A1] = a1;
                 L.sec[ci][Q_B0] = b0;
@@ -1596,7 +1602,7 @@ __global__ void __launch_bounds__(64) k_pw_small(GeneralJob j, uint8_t *done, ui
     uint32_t sz = 0, kept = 0;
     if (live && L.sec[ci][Q_PRELEN] != NONE) {
       kept = 1;
-      sz = vsz(L.sec[ci][Q_WRITTEN]) + vsz(L.sec[ci][Q_CLIENT]) + vsz(L.sec[ci][Q_FCLOCK]) + L.sec[ci][Q_PRELEN] +
+      sz = vsz(L.sec[ci][Q_WRITTEN]) + vsz(L.sec[ci][Q_CLIENT]) + vsz(L.sec[ci][Q_FCLOCK]) + (L.sec[ci][Q_PRELEN] & 0xffu) +
            (L.sec[ci][Q_A1] - L.sec[ci][Q_A0]) + (L.sec[ci][Q_X1] - L.sec[ci][Q_B0]);
     }
     const uint32_t wi = wave_incl_add(sz), wk = wave_incl_add(kept);
@@ -1614,11 +1620,11 @@ __global__ void __launch_bounds__(64) k_pw_small(GeneralJob j, uint8_t *done, ui
     uint8_t *const out = j.out + base;
     if (lane == 0) put_vu_g(out, 0, nparts);
     if (kept) {  // header and sliced head; the section's span placement for the patches
-      const uint32_t pl = L.sec[ci][Q_PRELEN];
+      const uint32_t pl = L.sec[ci][Q_PRELEN] & 0xffu, slot = L.sec[ci][Q_PRELEN] >> 8;
       uint32_t q = put_vu_g(out, p0 + wi - sz, L.sec[ci][Q_WRITTEN]);
       q = put_vu_g(out, q, L.sec[ci][Q_CLIENT]);
       q = put_vu_g(out, q, L.sec[ci][Q_FCLOCK]);
-      for (uint32_t x = 0; x < pl; x++) out[q + x] = L.pre[ci][x];
+      for (uint32_t x = 0; x < pl; x++) out[q + x] = L.pre[slot][x];
       q += pl;
       L.sec[ci][Q_OUT] = q;
     }
