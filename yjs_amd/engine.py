@@ -15,7 +15,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def lib_path():
-    return os.path.join(_HERE, "libymerge.so")
+    # YMERGE_LIB: another build of the library (diagnostics / A-B builds: libymerge_prof.so, ...)
+    return os.environ.get("YMERGE_LIB") or os.path.join(_HERE, "libymerge.so")
 
 
 class YjsError(Exception):
