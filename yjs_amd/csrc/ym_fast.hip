@@ -46,14 +46,18 @@ constexpr uint32_t SEC = 64 * E; // max client sections per document
 constexpr uint32_t DSN = 64 * E; // max delete ranges per document (before the union)
 
 // ---- LDS map (byte offsets; every array 16-aligned) ----------------------------------------------
+// 5,664 B per one-wave workgroup: 28 workgroups per CU = 7 waves per SIMD (the VGPR budget allows 8).  The
+// delete set is walked after the struct section is written, so its ranges reuse the section records' region
+// and its merge arrays the (then dead) document bytes.
 constexpr uint32_t L_IN = 0;                    // u8[IN + 16]   document bytes (+ slack for 8-B reads)
 constexpr uint32_t L_UOFF = IN + 16;            // u16[UPD + 1]  update start (absolute LDS offsets)
 constexpr uint32_t L_MISC = L_UOFF + 272;       // u32[16]       counters
 constexpr uint32_t L_HIST = L_MISC + 64;        // u32[16]       update-length histogram -> bucket offsets
 constexpr uint32_t L_UORD = L_HIST + 64;        // u8[UPD]       struct walk list (updates with structs, by length)
-constexpr uint32_t L_UORD2 = L_UORD + UPD;      // u8[UPD]       delete-set walk list (updates with deletes)
-constexpr uint32_t L_UDS = L_UORD2 + UPD;       // u16[UPD]      LDS offset of each update's delete set
-constexpr uint32_t L_SSLOT = L_UORD;            // u8[SEC]       rank -> walk slot (duplicate check; walk lists are dead)
+constexpr uint32_t L_SSLOT = L_UORD;            // u8[SEC]       rank -> walk slot (duplicate check; the walk list is dead)
+constexpr uint32_t L_UORD2 = L_UORD;            // u8[UPD]       delete-set walk list (updates with deletes; built after
+                                                //               the section phase)
+constexpr uint32_t L_UDS = L_UORD + UPD;        // u16[UPD]      LDS offset of each update's delete set
 constexpr uint32_t R = L_UDS + 2 * UPD;         // phase region
 // phase 2-4: client sections (walk order, then rank order in place)
 constexpr uint32_t L_SKEY = R;                  // u64[SEC]  (~client << 32 | clock)
@@ -61,15 +65,17 @@ constexpr uint32_t L_SLEN = L_SKEY + 8 * SEC;   // u32[SEC]  clock length of the
 constexpr uint32_t L_SNS = L_SLEN + 4 * SEC;    // u16[SEC]  structs in the section
 constexpr uint32_t L_SB = L_SNS + 2 * SEC;      // u16[SEC]  LDS offset of its first struct
 constexpr uint32_t L_SE = L_SB + 2 * SEC;       // u16[SEC]  ... and of its end
-// phase 2, 5: delete ranges
-constexpr uint32_t L_DKEY = L_SE + 2 * SEC;     // u64[DSN]  (client << 32 | clock << 7 | slot)
+constexpr uint32_t L_END = L_SE + 2 * SEC;
+// phase 4 (the layout holds the rank-ordered records in registers): parts over the clock lengths
+constexpr uint32_t L_PFIRST = L_SLEN;           // u16[SEC]  part -> units before it
+constexpr uint32_t L_PLAST = L_SLEN + 2 * SEC;  // u16[SEC]  part -> units through it
+// phase 5/6 (after the struct section is written): delete ranges over the section records
+constexpr uint32_t L_DKEY = R;                  // u64[DSN]  (client << 32 | clock << 7 | slot)
 constexpr uint32_t L_DLEN = L_DKEY + 8 * DSN;   // u32[DSN]
 constexpr uint32_t L_DSEQ = L_DLEN + 4 * DSN;   // u16[DSN]  update << 8 | position (first appearance)
-constexpr uint32_t L_PFIRST = L_DSEQ + 2 * DSN; // u16[SEC]  part -> units before it
-constexpr uint32_t L_PLAST = L_PFIRST + 2 * SEC;// u16[SEC]  part -> units through it
-constexpr uint32_t L_END = L_PLAST + 2 * SEC;
-// phase 5 (after the struct section is written): merged ranges and groups, over R
-constexpr uint32_t L_QCLK = R;                  // u32[DSN]  merged range start
+constexpr uint32_t L_GMIN = L_DSEQ + 2 * DSN;   // u32[DSN]  group first appearance, then group base
+// ... merged ranges and groups over the document bytes (dead once the delete sets are walked)
+constexpr uint32_t L_QCLK = L_IN;               // u32[DSN]  merged range start
 constexpr uint32_t L_QEND = L_QCLK + 4 * DSN;   // u32[DSN]  merged range end
 constexpr uint32_t L_QGRP = L_QEND + 4 * DSN;   // u8[DSN]   merged range -> group
 constexpr uint32_t L_QPRE = L_QGRP + DSN;       // u16[DSN + 1] exclusive byte prefix over ranges
@@ -78,12 +84,13 @@ constexpr uint32_t L_GCLI = L_GFIRST + 272;     // u32[DSN]  group client
 constexpr uint32_t L_P5END = L_GCLI + 4 * DSN;
 constexpr uint32_t L_GBYR = L_DKEY;             // u16[DSN]  bytes by rank, then offsets by rank (sorted keys are dead)
 constexpr uint32_t L_GB2 = L_DKEY + 512;        // u32[DSN]  group -> base offset of its ranges
-constexpr uint32_t L_GMIN = L_PFIRST;           // u32[DSN]  group first appearance, then group base (parts are dead)
-static_assert(L_P5END <= L_DKEY, "phase-5 arrays must not overlap the sorted delete ranges");
-static_assert(L_GMIN + 4 * DSN <= L_END, "group array fits");
+static_assert(L_P5END <= L_UOFF, "phase-5 arrays fit in the document bytes");
+static_assert(L_GMIN + 4 * DSN <= L_END, "delete ranges and groups fit in the section region");
+static_assert(L_GB2 + 4 * DSN <= L_DSEQ + 2 * DSN && L_GB2 >= L_GBYR + 2 * DSN, "rank arrays fit over the sorted keys");
+static_assert(L_PLAST + 2 * SEC <= L_SNS, "part arrays fit over the clock lengths");
 static_assert(SEC <= UPD, "the duplicate-check array reuses the walk list");
 constexpr uint32_t LDS_BYTES = L_END;
-static_assert(LDS_BYTES <= 8192, "5 one-wave workgroups per SIMD (160 KB LDS per CU)");
+static_assert(LDS_BYTES * 28 <= 160 * 1024, "7 one-wave workgroups per SIMD (160 KB LDS per CU)");
 
 using namespace fastc;
 
@@ -284,7 +291,7 @@ __device__ __forceinline__ bool walk_ds(uint32_t u) {
   {                                                  \
     if (lane == 0) decline(j, d);                    \
     __syncthreads();                                 \
-    continue;                                        \
+    return;                                          \
   }
 // STOP > 0 builds a timing-only variant that ends every document after phase STOP (profiling the
 // phases by ablation); outputs of such builds are not meaningful.
@@ -292,7 +299,7 @@ __device__ __forceinline__ bool walk_ds(uint32_t u) {
   if (STOP == (n)) {                                                    \
     if (lane == 0) { j.status[d] = ym::ST_OK; j.out_len[d] = 0; }       \
     __syncthreads();                                                    \
-    continue;                                                           \
+    return;                                                             \
   }
 
 // ---- 3/4. client sections of document d: rank sort, layout, struct section written (EE per lane) -------
@@ -556,7 +563,7 @@ __device__ __forceinline__ int ds_phase(const GeneralJob &j, uint32_t d, uint32_
       nranges = lane_read(incl_r, 63);
       uint32_t run = incl_r - nr_lane;
       const uint32_t next_first = from_next_lane(newr[0]);  // newr of position E*(lane+1)
-      __syncthreads();  // the sorted delete ranges are in registers: the phase-5 arrays reuse R
+      __syncthreads();  // the sorted delete ranges are in registers (the phase-5 arrays overlay the document bytes)
 #pragma unroll
       for (uint32_t s = 0; s < EE; s++) {
         const uint32_t r = r0 + s;
@@ -706,18 +713,16 @@ __device__ __forceinline__ int ds_phase(const GeneralJob &j, uint32_t d, uint32_
 // Grid: a multiple of 8 blocks; block b takes documents (b % 8) * G/8 + b / 8 + k * G.
 // NESTED: the retry pass over the `nd` documents listed in j.list (those the first pass declined), with
 // nested payload checks; its declines go to j.pend_list as before.
-template <int STOP, int OCC, bool DSONLY = false, bool DSV2 = false, bool NESTED = false>
-__global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j, uint32_t nd) {
+template <int STOP, bool DSONLY, bool DSV2, bool NESTED>
+__device__ __forceinline__ void merge_doc_v1(const GeneralJob &j, uint32_t di) {
   const uint32_t lane = threadIdx.x;
-  const uint64_t arena0 = uoff_g(j, 0);
-  const uint32_t d0 = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-  for (uint32_t di = d0; di < nd; di += gridDim.x) {
+  {
     const uint32_t d = NESTED ? j.list[di] : di;
     const uint32_t u0 = j.doc_upd[d], k = j.doc_upd[d + 1] - u0;
     const uint64_t b0 = uoff_g(j, u0), bytes = uoff_g(j, u0 + k) - b0;
     if ((DSONLY ? k == 0 : k <= 1) || k > UPD || bytes > IN) {
       if (lane == 0) decline(j, d);
-      continue;
+      return;
     }
     // ---- 1. stage with 16-B loads covering [b0, b0 + bytes); byte b0 lands at LDS offset `base`
     const uint32_t base = (uint32_t)(b0 & 15);
@@ -794,9 +799,36 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j, uint32_
 #pragma unroll 1
       for (uint32_t i = lane; i < n1; i += 64) ok &= walk_sections<NESTED>(at<uint8_t>(L_UORD + i));
       if (__any(!ok)) YM_DECLINE()
-      __syncthreads();
-      YM_STOP(8)
-      // W2 list: updates whose delete set has clients (first byte != 0), compacted by ballots
+    }
+    __syncthreads();
+    YM_STOP(8)
+    const uint32_t nsec = at<uint32_t>(L_MISC);
+    if ((DSONLY ? nsec != 0 : nsec == 0) || nsec > SEC) YM_DECLINE()
+    // pad the key array to a multiple of 4 (rank loops read quads; SEC is a multiple of 4)
+    if (lane < 3 && nsec + lane < ((nsec + 3) & ~3u)) at<uint64_t>(L_SKEY + 8 * (nsec + lane)) = ~0ull;
+    __syncthreads();
+    // output slot: 64-aligned inside the bound 2 * in + 64 per doc (no global atomics)
+    const uint64_t slot = 2 * (b0 - uoff_g(j, 0)) + 64ull * d;
+    const uint64_t slot_al = (slot + 63) & ~63ull;
+    const uint64_t slot_end = slot + 2 * bytes + 64 < j.cap ? slot + 2 * bytes + 64 : j.cap;
+    if (slot_al >= slot_end) YM_DECLINE()
+    const Slot dst = make_slot(j.out + slot_al, (uint32_t)(slot_end - slot_al));
+    uint32_t hdr = 0, struct_bytes = 0;
+    if constexpr (!DSONLY) {
+      const int r = nsec <= 64 ? sec_phase<1, STOP>(j, d, nsec, slot, slot_al, slot_end, bytes, dst, hdr, struct_bytes)
+                               : sec_phase<2, STOP>(j, d, nsec, slot, slot_al, slot_end, bytes, dst, hdr, struct_bytes);
+      if (r == SP_DECLINE) YM_DECLINE()
+      if (r == SP_STOP && lane == 0) { j.status[d] = ym::ST_OK; j.out_len[d] = 0; }
+      if (r != SP_DONE) {
+        __syncthreads();
+        return;
+      }
+    }  // !DSONLY
+    __syncthreads();
+    YM_STOP(7)
+    // ---- W2 (after the struct section is written: the ranges reuse the section records' LDS): one lane per
+    // update whose delete set has clients (first byte != 0), compacted by ballots
+    {
       uint32_t n2 = 0;
 #pragma unroll
       for (uint32_t s = 0; s < UPD / 64; s++) {
@@ -811,37 +843,17 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j, uint32_
         n2 += __popcll(m);
       }
       __syncthreads();
+      bool ok = true;
 #pragma unroll 1
       for (uint32_t i = lane; i < n2; i += 64) ok &= walk_ds<DSV2>(at<uint8_t>(L_UORD2 + i));
       if (__any(!ok)) YM_DECLINE()
     }
     __syncthreads();
-    const uint32_t nsec = at<uint32_t>(L_MISC), nds = at<uint32_t>(L_MISC + 4);
-    if ((DSONLY ? nsec != 0 : nsec == 0) || nsec > SEC || nds > DSN) YM_DECLINE()
-    if (lane < 3) {  // pad the key arrays to a multiple of 4 (rank loops read quads; SEC, DSN are multiples of 4)
-      if (nsec + lane < ((nsec + 3) & ~3u)) at<uint64_t>(L_SKEY + 8 * (nsec + lane)) = ~0ull;
-      if (nds + lane < ((nds + 3) & ~3u)) at<uint64_t>(L_DKEY + 8 * (nds + lane)) = ~0ull;
-    }
+    const uint32_t nds = at<uint32_t>(L_MISC + 4);
+    if (nds > DSN) YM_DECLINE()
+    if (lane < 3 && nds + lane < ((nds + 3) & ~3u)) at<uint64_t>(L_DKEY + 8 * (nds + lane)) = ~0ull;
     __syncthreads();
     YM_STOP(2)
-    // output slot: 64-aligned inside the bound 2 * in + 64 per doc (no global atomics)
-    const uint64_t slot = 2 * (b0 - arena0) + 64ull * d;
-    const uint64_t slot_al = (slot + 63) & ~63ull;
-    const uint64_t slot_end = slot + 2 * bytes + 64 < j.cap ? slot + 2 * bytes + 64 : j.cap;
-    if (slot_al >= slot_end) YM_DECLINE()
-    const Slot dst = make_slot(j.out + slot_al, (uint32_t)(slot_end - slot_al));
-    uint32_t hdr = 0, struct_bytes = 0;
-    if constexpr (!DSONLY) {
-      const int r = nsec <= 64 ? sec_phase<1, STOP>(j, d, nsec, slot, slot_al, slot_end, bytes, dst, hdr, struct_bytes)
-                               : sec_phase<2, STOP>(j, d, nsec, slot, slot_al, slot_end, bytes, dst, hdr, struct_bytes);
-      if (r == SP_DECLINE) YM_DECLINE()
-      if (r == SP_STOP && lane == 0) { j.status[d] = ym::ST_OK; j.out_len[d] = 0; }
-      if (r != SP_DONE) {
-        __syncthreads();
-        continue;
-      }
-    }  // !DSONLY
-    YM_STOP(7)
     {
       const int r = nds <= 64 ? ds_phase<1, STOP, DSV2>(j, d, nds, hdr, struct_bytes, slot, slot_al, slot_end, bytes, dst)
                               : ds_phase<2, STOP, DSV2>(j, d, nds, hdr, struct_bytes, slot, slot_al, slot_end, bytes, dst);
@@ -849,6 +861,18 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j, uint32_
       if (r == DS_STOP && lane == 0) { j.status[d] = ym::ST_OK; j.out_len[d] = 0; }
     }
     __syncthreads();
+  }
+}
+// ONE: the grid covers every document (one per block, no loop: nothing is hoisted across documents, so
+// the per-document values are not kept live -- and spilled -- for the whole kernel); otherwise a
+// grid-stride loop.  Grid: a multiple of 8 blocks; block b takes documents (b % 8) * G/8 + b / 8 + k * G.
+template <int STOP, int OCC, bool DSONLY = false, bool DSV2 = false, bool NESTED = false, bool ONE = true>
+__global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j, uint32_t nd) {
+  const uint32_t d0 = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  if constexpr (ONE) {
+    if (d0 < nd) merge_doc_v1<STOP, DSONLY, DSV2, NESTED>(j, d0);
+  } else {
+    for (uint32_t di = d0; di < nd; di += gridDim.x) merge_doc_v1<STOP, DSONLY, DSV2, NESTED>(j, di);
   }
 }
 
@@ -860,16 +884,24 @@ __global__ void k_fast_region(GeneralJob j, uint32_t n_upd) {
   if (threadIdx.x == 0 && blockIdx.x == 0) *j.used = 2 * (j.upd_off[n_upd] - j.upd_off[0]) + 64ull * j.n + 64;
 }
 
-// grid: a multiple of 8 one-wave blocks (the kernel's XCD-contiguous document mapping)
-static uint32_t fast_grid(uint32_t n) { return ((n < 131072 ? n : 131072) + 7) & ~7u; }
+// grid: a multiple of 8 one-wave blocks (the kernel's XCD-contiguous document mapping); one block per
+// document up to FAST_ONE_MAX documents (the ONE form), a grid-stride loop above
+constexpr uint32_t FAST_ONE_MAX = 1u << 24;
+static uint32_t fast_grid(uint32_t n) { return ((n < FAST_ONE_MAX ? n : FAST_ONE_MAX) + 7) & ~7u; }
 
 int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st) {
   using namespace fastv1;
   if (op == OP_DSMERGE) {  // delete-set merges: the same kernel, delete sets only
     if (j.dsref) return 0;  // the reference's adjacency-only coalescing: general path
     const uint32_t grid = fast_grid(j.n);
-    if (j.v2) k_fast_merge_v1<0, 5, true, true><<<grid, 64, fastv1::LDS_BYTES, st>>>(j, j.n);
-    else k_fast_merge_v1<0, 5, true, false><<<grid, 64, fastv1::LDS_BYTES, st>>>(j, j.n);
+    const bool one = j.n <= FAST_ONE_MAX;
+    if (j.v2) {
+      if (one) k_fast_merge_v1<0, 5, true, true><<<grid, 64, fastv1::LDS_BYTES, st>>>(j, j.n);
+      else k_fast_merge_v1<0, 5, true, true, false, false><<<grid, 64, fastv1::LDS_BYTES, st>>>(j, j.n);
+    } else {
+      if (one) k_fast_merge_v1<0, 5, true, false><<<grid, 64, fastv1::LDS_BYTES, st>>>(j, j.n);
+      else k_fast_merge_v1<0, 5, true, false, false, false><<<grid, 64, fastv1::LDS_BYTES, st>>>(j, j.n);
+    }
     return 1;
   }
   if (op != OP_MERGE || j.v2) return 0;  // fast path: V1 merges (the C2/C4 headline configs)
@@ -884,12 +916,14 @@ int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st
   }
   const uint32_t LDS_BYTES = fastv1::LDS_BYTES + pad;
   static int occ = -1;
+  // (the launch bound only steers register allocation: 5 leaves the kernel at <= 64 VGPRs, 8 waves per SIMD
+  // by registers; the LDS map sets 7)
   if (occ < 0) { const char *e = getenv("YMERGE_FAST_OCC"); occ = e ? atoi(e) : 5; }
 #define YM_LAUNCH(S, O) k_fast_merge_v1<S, O><<<grid, 64, LDS_BYTES, st>>>(j, j.n)
-  if (occ == 4) {
-    YM_LAUNCH(0, 4);
-  } else if (occ == 6) {
-    YM_LAUNCH(0, 6);
+  if (j.n > FAST_ONE_MAX) {
+    k_fast_merge_v1<0, 5, false, false, false, false><<<grid, 64, LDS_BYTES, st>>>(j, j.n);
+  } else if (occ == 8) {
+    YM_LAUNCH(0, 8);
   } else {
     switch (stop) {
       case 1: YM_LAUNCH(1, 5); break;
@@ -915,7 +949,8 @@ int fast_nested_launch(const GeneralJob &j, uint32_t n, hipStream_t st) {
   static int off = -1;
   if (off < 0) { const char *e = getenv("YMERGE_FAST_NESTED"); off = e && atoi(e) == 0 ? 1 : 0; }
   if (off) return 0;
-  k_fast_merge_v1<0, 5, false, false, true><<<fast_grid(n), 64, fastv1::LDS_BYTES, st>>>(j, n);
+  if (n <= FAST_ONE_MAX) k_fast_merge_v1<0, 5, false, false, true><<<fast_grid(n), 64, fastv1::LDS_BYTES, st>>>(j, n);
+  else k_fast_merge_v1<0, 5, false, false, true, false><<<fast_grid(n), 64, fastv1::LDS_BYTES, st>>>(j, n);
   return 1;
 }
 
