@@ -39,58 +39,67 @@
 namespace ymk {
 namespace fastv1 {
 
-constexpr uint32_t IN = 2560;    // max document bytes
 constexpr uint32_t UPD = 128;    // max updates per document
 constexpr uint32_t E = 2;        // records per lane
 constexpr uint32_t SEC = 64 * E; // max client sections per document
 constexpr uint32_t DSN = 64 * E; // max delete ranges per document (before the union)
+constexpr uint32_t IN_HOT = 2432;     // max document bytes, hot pass (C2 / C4 documents: <= 2.2 KB)
+constexpr uint32_t IN_NESTED = 3328;  // ... retry pass over rich content (C2R documents: <= 3.2 KB)
 
 // ---- LDS map (byte offsets; every array 16-aligned) ----------------------------------------------
-// 5,664 B per one-wave workgroup: 28 workgroups per CU = 7 waves per SIMD (the VGPR budget allows 8).  The
-// delete set is walked after the struct section is written, so its ranges reuse the section records' region
-// and its merge arrays the (then dead) document bytes.
-constexpr uint32_t L_IN = 0;                    // u8[IN + 16]   document bytes (+ slack for 8-B reads)
-constexpr uint32_t L_UOFF = IN + 16;            // u16[UPD + 1]  update start (absolute LDS offsets)
-constexpr uint32_t L_MISC = L_UOFF + 272;       // u32[16]       counters
-constexpr uint32_t L_HIST = L_MISC + 64;        // u32[16]       update-length histogram -> bucket offsets
-constexpr uint32_t L_UORD = L_HIST + 64;        // u8[UPD]       struct walk list (updates with structs, by length)
-constexpr uint32_t L_SSLOT = L_UORD;            // u8[SEC]       rank -> walk slot (duplicate check; the walk list is dead)
-constexpr uint32_t L_UORD2 = L_UORD;            // u8[UPD]       delete-set walk list (updates with deletes; built after
-                                                //               the section phase)
-constexpr uint32_t L_UDS = L_UORD + UPD;        // u16[UPD]      LDS offset of each update's delete set
-constexpr uint32_t R = L_UDS + 2 * UPD;         // phase region
-// phase 2-4: client sections (walk order, then rank order in place)
-constexpr uint32_t L_SKEY = R;                  // u64[SEC]  (~client << 32 | clock)
-constexpr uint32_t L_SLEN = L_SKEY + 8 * SEC;   // u32[SEC]  clock length of the section
-constexpr uint32_t L_SNS = L_SLEN + 4 * SEC;    // u16[SEC]  structs in the section
-constexpr uint32_t L_SB = L_SNS + 2 * SEC;      // u16[SEC]  LDS offset of its first struct
-constexpr uint32_t L_SE = L_SB + 2 * SEC;       // u16[SEC]  ... and of its end
-constexpr uint32_t L_END = L_SE + 2 * SEC;
-// phase 4 (the layout holds the rank-ordered records in registers): parts over the clock lengths
-constexpr uint32_t L_PFIRST = L_SLEN;           // u16[SEC]  part -> units before it
-constexpr uint32_t L_PLAST = L_SLEN + 2 * SEC;  // u16[SEC]  part -> units through it
-// phase 5/6 (after the struct section is written): delete ranges over the section records
-constexpr uint32_t L_DKEY = R;                  // u64[DSN]  (client << 32 | clock << 7 | slot)
-constexpr uint32_t L_DLEN = L_DKEY + 8 * DSN;   // u32[DSN]
-constexpr uint32_t L_DSEQ = L_DLEN + 4 * DSN;   // u16[DSN]  update << 8 | position (first appearance)
-constexpr uint32_t L_GMIN = L_DSEQ + 2 * DSN;   // u32[DSN]  group first appearance, then group base
-// ... merged ranges and groups over the document bytes (dead once the delete sets are walked)
-constexpr uint32_t L_QCLK = L_IN;               // u32[DSN]  merged range start
-constexpr uint32_t L_QEND = L_QCLK + 4 * DSN;   // u32[DSN]  merged range end
-constexpr uint32_t L_QGRP = L_QEND + 4 * DSN;   // u8[DSN]   merged range -> group
-constexpr uint32_t L_QPRE = L_QGRP + DSN;       // u16[DSN + 1] exclusive byte prefix over ranges
-constexpr uint32_t L_GFIRST = L_QPRE + 272;     // u16[DSN + 1] group -> first range
-constexpr uint32_t L_GCLI = L_GFIRST + 272;     // u32[DSN]  group client
-constexpr uint32_t L_P5END = L_GCLI + 4 * DSN;
-constexpr uint32_t L_GBYR = L_DKEY;             // u16[DSN]  bytes by rank, then offsets by rank (sorted keys are dead)
-constexpr uint32_t L_GB2 = L_DKEY + 512;        // u32[DSN]  group -> base offset of its ranges
-static_assert(L_P5END <= L_UOFF, "phase-5 arrays fit in the document bytes");
-static_assert(L_GMIN + 4 * DSN <= L_END, "delete ranges and groups fit in the section region");
-static_assert(L_GB2 + 4 * DSN <= L_DSEQ + 2 * DSN && L_GB2 >= L_GBYR + 2 * DSN, "rank arrays fit over the sorted keys");
-static_assert(L_PLAST + 2 * SEC <= L_SNS, "part arrays fit over the clock lengths");
-static_assert(SEC <= UPD, "the duplicate-check array reuses the walk list");
-constexpr uint32_t LDS_BYTES = L_END;
-static_assert(LDS_BYTES * 28 <= 160 * 1024, "7 one-wave workgroups per SIMD (160 KB LDS per CU)");
+// IN_ + 2,688 B per one-wave workgroup: 5,120 B for the hot pass = 32 workgroups per CU, 8 waves per SIMD.
+// The delete set is walked after the struct section is written, so its ranges reuse the section records'
+// region and its merge arrays the (then dead) document bytes; the walk lists are read into registers before
+// their walks and live in the record region too.
+template <uint32_t IN_>
+struct Map {
+  static constexpr uint32_t IN = IN_;
+  static constexpr uint32_t L_IN = 0;                    // u8[IN + 16]   document bytes (+ slack for 8-B reads)
+  static constexpr uint32_t L_UOFF = IN + 16;            // u16[UPD + 1]  update start (absolute LDS offsets)
+  static constexpr uint32_t L_MISC = L_UOFF + 272;       // u32[4]        counters: sections, delete ranges
+  static constexpr uint32_t L_DUP = L_MISC + 16;         // u32[4]        section ranks seen (duplicate check)
+  static constexpr uint32_t L_HIST = L_DUP + 16;         // u32[16]       update-length histogram -> bucket offsets
+  static constexpr uint32_t L_UDS = L_HIST + 64;         // u16[UPD]      LDS offset of each update's delete set
+  static constexpr uint32_t R = L_UDS + 2 * UPD;         // record region
+  // client sections (walk order, then rank order in place)
+  static constexpr uint32_t L_SKEY = R;                  // u64[SEC]  (~client << 32 | clock)
+  static constexpr uint32_t L_SLN = L_SKEY + 8 * SEC;    // u32[SEC]  clock length (21 bits) | structs << 21
+  static constexpr uint32_t L_SB = L_SLN + 4 * SEC;      // u16[SEC]  LDS offset of its first struct
+  static constexpr uint32_t L_SE = L_SB + 2 * SEC;       // u16[SEC]  ... and of its end
+  static constexpr uint32_t L_END = L_SE + 2 * SEC;
+  static constexpr uint32_t L_UORD = L_SE;               // u8[UPD]   struct walk list (updates with structs, by
+                                                         //           length), in registers before the walk
+  static constexpr uint32_t L_UORD2 = L_SE;              // u8[UPD]   delete-set walk list (after the section phase)
+  // the layout holds the rank-ordered records in registers: parts over the clock lengths
+  static constexpr uint32_t L_PFIRST = L_SLN;            // u16[SEC]  part -> units before it
+  static constexpr uint32_t L_PLAST = L_SLN + 2 * SEC;   // u16[SEC]  part -> units through it
+  // after the struct section is written: delete ranges over the section records
+  static constexpr uint32_t L_DKEY = R;                  // u64[DSN]  (client << 32 | clock << 7 | slot)
+  static constexpr uint32_t L_DLEN = L_DKEY + 8 * DSN;   // u32[DSN]
+  static constexpr uint32_t L_DSEQ = L_DLEN + 4 * DSN;   // u16[DSN]  update << 8 | position (first appearance)
+  // ... merged ranges and groups over the document bytes and the walk tables (dead once the delete sets are
+  // walked)
+  static constexpr uint32_t L_QCLK = L_IN;               // u32[DSN]  merged range start
+  static constexpr uint32_t L_QEND = L_QCLK + 4 * DSN;   // u32[DSN]  merged range end
+  static constexpr uint32_t L_QGRP = L_QEND + 4 * DSN;   // u8[DSN]   merged range -> group
+  static constexpr uint32_t L_QPRE = L_QGRP + DSN;       // u16[DSN + 1] exclusive byte prefix over ranges
+  static constexpr uint32_t L_GFIRST = L_QPRE + 272;     // u16[DSN + 1] group -> first range
+  static constexpr uint32_t L_GCLI = L_GFIRST + 272;     // u32[DSN]  group client
+  static constexpr uint32_t L_GMIN = L_GCLI + 4 * DSN;   // u32[DSN]  group first appearance, then group base
+  static constexpr uint32_t L_GBYR = L_DKEY;             // u16[DSN]  bytes by rank, then offsets by rank (sorted keys
+                                                         //           are dead)
+  static constexpr uint32_t L_GB2 = L_DKEY + 512;        // u32[DSN]  group -> base offset of its ranges
+  static constexpr uint32_t LDS_BYTES = L_END;
+  static_assert(IN % 16 == 0, "16-B staging");
+  static_assert(L_GMIN + 4 * DSN <= R, "phase-5 arrays fit below the record region");
+  static_assert(L_DSEQ + 2 * DSN <= L_END, "delete ranges fit in the section region");
+  static_assert(L_GB2 + 4 * DSN <= L_DSEQ + 2 * DSN && L_GB2 >= L_GBYR + 2 * DSN, "rank arrays fit over the sorted keys");
+  static_assert(L_PLAST + 2 * SEC <= L_SB, "part arrays fit over the clock lengths");
+  static_assert(L_UORD + UPD <= L_END, "walk lists fit in the record region");
+};
+using MapHot = Map<IN_HOT>;
+using MapNested = Map<IN_NESTED>;
+static_assert(MapHot::LDS_BYTES * 32 <= 160 * 1024, "8 one-wave workgroups per SIMD (160 KB LDS per CU)");
 
 using namespace fastc;
 
@@ -205,9 +214,9 @@ __device__ __forceinline__ bool item_fast(Cur &c, uint32_t info, uint32_t &len) 
 // origins and writes the info byte back without it, E8), so sections copy verbatim afterwards.
 // Returns false to decline.  NESTED: nested payloads (any objects / arrays, JSON texts) are checked too
 // (the retry pass over the documents the hot kernel declined; ym_canon_chk.h).
-template <bool NESTED = false>
+template <class M, bool NESTED = false>
 __device__ __forceinline__ bool walk_sections(uint32_t u) {
-  Cur c = {at<uint16_t>(L_UOFF + 2 * u), at<uint16_t>(L_UOFF + 2 * u + 2), false};
+  Cur c = {at<uint16_t>(M::L_UOFF + 2 * u), at<uint16_t>(M::L_UOFF + 2 * u + 2), false};
   const uint32_t nclients = rvu(c);
   uint64_t next_min = 0;  // sections of one update in merge order: each key > the previous one's last unit
   for (uint32_t ci = 0; ci < nclients && !c.bad; ci++) {
@@ -227,30 +236,29 @@ __device__ __forceinline__ bool walk_sections(uint32_t u) {
       len += l;
     }
     const uint64_t key = ((uint64_t)(~client) << 32) | clock;
-    c.bad |= (nstructs == 0) | ((uint64_t)clock + len > 0xffffffffull) | (key < next_min);
+    c.bad |= (nstructs == 0) | (nstructs >= (1u << 11)) | (len >= (1u << 21)) | (key < next_min);
     next_min = key + len;
     if (!c.bad) {
-      const uint32_t q = atomicAdd(&at<uint32_t>(L_MISC), 1u);
+      const uint32_t q = atomicAdd(&at<uint32_t>(M::L_MISC), 1u);
       c.bad |= q >= SEC;
       if (q < SEC) {
-        at<uint64_t>(L_SKEY + 8 * q) = key;
-        at<uint32_t>(L_SLEN + 4 * q) = (uint32_t)len;
-        at<uint16_t>(L_SNS + 2 * q) = (uint16_t)nstructs;
-        at<uint16_t>(L_SB + 2 * q) = (uint16_t)b;
-        at<uint16_t>(L_SE + 2 * q) = (uint16_t)c.p;
+        at<uint64_t>(M::L_SKEY + 8 * q) = key;
+        at<uint32_t>(M::L_SLN + 4 * q) = (uint32_t)len | (nstructs << 21);
+        at<uint16_t>(M::L_SB + 2 * q) = (uint16_t)b;
+        at<uint16_t>(M::L_SE + 2 * q) = (uint16_t)c.p;
       }
     }
   }
-  at<uint16_t>(L_UDS + 2 * u) = (uint16_t)c.p;
+  at<uint16_t>(M::L_UDS + 2 * u) = (uint16_t)c.p;
   return !c.bad;
 }
 // Walks the delete set of update u (DeleteSet.js:219-256) and appends its ranges (slots from misc[1]);
 // a range's payload (u << 8 | position) keeps yjs's first-appearance order.
 // V2: DSDecoderV2 (UpdateDecoder.js:258-267): clock delta-coded against the running value, which each
 // client resets; length stored as len - 1.
-template <bool V2 = false>
+template <class M, bool V2 = false>
 __device__ __forceinline__ bool walk_ds(uint32_t u) {
-  Cur c = {at<uint16_t>(L_UDS + 2 * u), at<uint16_t>(L_UOFF + 2 * u + 2), false};
+  Cur c = {at<uint16_t>(M::L_UDS + 2 * u), at<uint16_t>(M::L_UOFF + 2 * u + 2), false};
   const uint32_t ndc = rvu(c);
   uint32_t pos = 0;
   for (uint32_t i = 0; i < ndc && !c.bad; i++) {
@@ -272,14 +280,14 @@ __device__ __forceinline__ bool walk_ds(uint32_t u) {
       }
       c.bad |= (pos > 255) | (clock >= (1u << 25));
       if (!c.bad) {
-        const uint32_t x = atomicAdd(&at<uint32_t>(L_MISC + 4), 1u);
+        const uint32_t x = atomicAdd(&at<uint32_t>(M::L_MISC + 4), 1u);
         c.bad |= x >= DSN;
         // the slot in the low bits makes every key distinct (ranks are a permutation without a
         // tie-break pass: equal (client, clock) ranges from several inputs are the common case)
         if (x < DSN) {
-          at<uint64_t>(L_DKEY + 8 * x) = ((uint64_t)client << 32) | (clock << 7) | x;
-          at<uint32_t>(L_DLEN + 4 * x) = len;
-          at<uint16_t>(L_DSEQ + 2 * x) = (uint16_t)((u << 8) | pos);
+          at<uint64_t>(M::L_DKEY + 8 * x) = ((uint64_t)client << 32) | (clock << 7) | x;
+          at<uint32_t>(M::L_DLEN + 4 * x) = len;
+          at<uint16_t>(M::L_DSEQ + 2 * x) = (uint16_t)((u << 8) | pos);
         }
       }
     }
@@ -304,23 +312,22 @@ __device__ __forceinline__ bool walk_ds(uint32_t u) {
 
 // ---- 3/4. client sections of document d: rank sort, layout, struct section written (EE per lane) -------
 enum : int { SP_DONE = 0, SP_DECLINE = 1, SP_STOP = 2, SP_CAP = 3 };
-template <uint32_t EE, int STOP>
+template <class M, uint32_t EE, int STOP>
 __device__ __forceinline__ int sec_phase(const GeneralJob &j, uint32_t d, uint32_t nsec, uint64_t slot, uint64_t slot_al,
                                          uint64_t slot_end, uint64_t bytes, Slot dst, uint32_t &hdr, uint32_t &struct_bytes) {
   const uint32_t lane = threadIdx.x;
   bool bad = false;
     // ---- 3. section rank sort
     uint64_t rk[EE];
-    uint32_t rl[EE], rns[EE], rb[EE], re[EE], rr[EE];
+    uint32_t rl[EE], rb[EE], re[EE], rr[EE];
 #pragma unroll
     for (uint32_t s = 0; s < EE; s++) {
       const uint32_t i = lane + 64 * s;
       const bool v = i < nsec;
-      rk[s] = v ? at<uint64_t>(L_SKEY + 8 * i) : ~0ull;
-      rl[s] = v ? at<uint32_t>(L_SLEN + 4 * i) : 0;
-      rns[s] = v ? at<uint16_t>(L_SNS + 2 * i) : 0;
-      rb[s] = v ? at<uint16_t>(L_SB + 2 * i) : 0;
-      re[s] = v ? at<uint16_t>(L_SE + 2 * i) : 0;
+      rk[s] = v ? at<uint64_t>(M::L_SKEY + 8 * i) : ~0ull;
+      rl[s] = v ? at<uint32_t>(M::L_SLN + 4 * i) : 0;
+      rb[s] = v ? at<uint16_t>(M::L_SB + 2 * i) : 0;
+      re[s] = v ? at<uint16_t>(M::L_SE + 2 * i) : 0;
     }
     bool ranked = false;
     if constexpr (EE == 1) {
@@ -353,30 +360,28 @@ __device__ __forceinline__ int sec_phase(const GeneralJob &j, uint32_t d, uint32
         }
       }
     }
-    if (!ranked) rank_le4(L_SKEY, nsec, rk, rr);
+    if (!ranked) rank_le4(M::L_SKEY, nsec, rk, rr);
     __syncthreads();
 #pragma unroll
     for (uint32_t s = 0; s < EE; s++) {
       const uint32_t i = lane + 64 * s;
       if (i < nsec) {
         const uint32_t r = rr[s];
-        at<uint64_t>(L_SKEY + 8 * r) = rk[s];
-        at<uint32_t>(L_SLEN + 4 * r) = rl[s];
-        at<uint16_t>(L_SNS + 2 * r) = (uint16_t)rns[s];
-        at<uint16_t>(L_SB + 2 * r) = (uint16_t)rb[s];
-        at<uint16_t>(L_SE + 2 * r) = (uint16_t)re[s];
-        at<uint8_t>(L_SSLOT + r) = (uint8_t)i;
+        at<uint64_t>(M::L_SKEY + 8 * r) = rk[s];
+        at<uint32_t>(M::L_SLN + 4 * r) = rl[s];
+        at<uint16_t>(M::L_SB + 2 * r) = (uint16_t)rb[s];
+        at<uint16_t>(M::L_SE + 2 * r) = (uint16_t)re[s];
+        atomicOr(&at<uint32_t>(M::L_DUP + 4 * (r >> 5)), 1u << (r & 31));
       }
     }
     __syncthreads();
     {
-      bool dup = false;
-#pragma unroll
-      for (uint32_t s = 0; s < EE; s++) {
-        const uint32_t i = lane + 64 * s;
-        if (i < nsec) dup |= at<uint8_t>(L_SSLOT + rr[s]) != i;
-      }
-      if (__any(dup)) return SP_DECLINE;  // equal (client, clock): overlapping inputs
+      // equal (client, clock) keys share a rank: the ranks seen must be all nsec of them (else overlapping
+      // inputs)
+      const uint4 w = at<uint4>(M::L_DUP);
+      const uint32_t seen = __popc(__builtin_amdgcn_readfirstlane(w.x)) + __popc(__builtin_amdgcn_readfirstlane(w.y)) +
+                            __popc(__builtin_amdgcn_readfirstlane(w.z)) + __popc(__builtin_amdgcn_readfirstlane(w.w));
+      if (seen != nsec) return SP_DECLINE;
     }
     if (STOP == 3) return SP_STOP;
     // ---- 4. layout over rank order; lane owns positions r = E*lane + s
@@ -384,18 +389,19 @@ __device__ __forceinline__ int sec_phase(const GeneralJob &j, uint32_t d, uint32
     uint32_t sl[EE], sns[EE], sb[EE], se[EE], units[EE], pstart[EE], plastf[EE], gapv[EE];
     {
       const uint32_t r0 = EE * lane;
-      uint64_t kp = r0 > 0 && r0 - 1 < nsec ? at<uint64_t>(L_SKEY + 8 * (r0 - 1)) : ~0ull;
-      uint32_t lp = r0 > 0 && r0 - 1 < nsec ? at<uint32_t>(L_SLEN + 4 * (r0 - 1)) : 0;
+      uint64_t kp = r0 > 0 && r0 - 1 < nsec ? at<uint64_t>(M::L_SKEY + 8 * (r0 - 1)) : ~0ull;
+      uint32_t lp = r0 > 0 && r0 - 1 < nsec ? at<uint32_t>(M::L_SLN + 4 * (r0 - 1)) & 0x1fffffu : 0;
 #pragma unroll
       for (uint32_t s = 0; s < EE; s++) {
         const uint32_t r = r0 + s;
         const bool v = r < nsec;
-        sk[s] = v ? at<uint64_t>(L_SKEY + 8 * r) : ~0ull;
-        sl[s] = v ? at<uint32_t>(L_SLEN + 4 * r) : 0;
-        sns[s] = v ? at<uint16_t>(L_SNS + 2 * r) : 0;
-        sb[s] = v ? at<uint16_t>(L_SB + 2 * r) : 0;
-        se[s] = v ? at<uint16_t>(L_SE + 2 * r) : 0;
-        const uint64_t kn = r + 1 < nsec ? at<uint64_t>(L_SKEY + 8 * (r + 1)) : ~0ull;
+        sk[s] = v ? at<uint64_t>(M::L_SKEY + 8 * r) : ~0ull;
+        const uint32_t ln = v ? at<uint32_t>(M::L_SLN + 4 * r) : 0;
+        sl[s] = ln & 0x1fffffu;
+        sns[s] = ln >> 21;
+        sb[s] = v ? at<uint16_t>(M::L_SB + 2 * r) : 0;
+        se[s] = v ? at<uint16_t>(M::L_SE + 2 * r) : 0;
+        const uint64_t kn = r + 1 < nsec ? at<uint64_t>(M::L_SKEY + 8 * (r + 1)) : ~0ull;
         const bool same = v && r > 0 && (kp >> 32) == (sk[s] >> 32);
         const uint64_t pend = (kp & 0xffffffffull) + lp;
         const uint64_t cl = sk[s] & 0xffffffffull;
@@ -422,8 +428,8 @@ __device__ __forceinline__ int sec_phase(const GeneralJob &j, uint32_t d, uint32
         pu[s] = run;  // exclusive (parts, units) before position r
         run += (pstart[s] << 16) | units[s];
         const uint32_t pid = (run >> 16) - 1;
-        if (pstart[s]) at<uint16_t>(L_PFIRST + 2 * pid) = (uint16_t)(pu[s] & 0xffff);
-        if (plastf[s]) at<uint16_t>(L_PLAST + 2 * pid) = (uint16_t)(run & 0xffff);
+        if (pstart[s]) at<uint16_t>(M::L_PFIRST + 2 * pid) = (uint16_t)(pu[s] & 0xffff);
+        if (plastf[s]) at<uint16_t>(M::L_PLAST + 2 * pid) = (uint16_t)(run & 0xffff);
       }
     }
     __syncthreads();
@@ -434,7 +440,7 @@ __device__ __forceinline__ int sec_phase(const GeneralJob &j, uint32_t d, uint32
       uint32_t b = se[s] - sb[s];
       if (pstart[s]) {
         const uint32_t pid = pu[s] >> 16;
-        runu[s] = at<uint16_t>(L_PLAST + 2 * pid) - at<uint16_t>(L_PFIRST + 2 * pid);
+        runu[s] = at<uint16_t>(M::L_PLAST + 2 * pid) - at<uint16_t>(M::L_PFIRST + 2 * pid);
         b += vsz(runu[s]) + vsz(~(uint32_t)(sk[s] >> 32)) + vsz((uint32_t)sk[s]);
       }
       if (gapv[s]) b += 1 + vsz(gapv[s]);
@@ -481,7 +487,7 @@ __device__ __forceinline__ int sec_phase(const GeneralJob &j, uint32_t d, uint32
 
 // ---- 5/6. delete set of document d (EE delete ranges per lane: 1 when they fit one wave) --------------
 enum : int { DS_DONE = 0, DS_DECLINE = 1, DS_STOP = 2 };
-template <uint32_t EE, int STOP, bool DSV2>
+template <class M, uint32_t EE, int STOP, bool DSV2>
 __device__ __forceinline__ int ds_phase(const GeneralJob &j, uint32_t d, uint32_t nds, uint32_t hdr, uint32_t struct_bytes,
                                         uint64_t slot, uint64_t slot_al, uint64_t slot_end, uint64_t bytes, Slot dst) {
   const uint32_t lane = threadIdx.x;
@@ -494,19 +500,19 @@ __device__ __forceinline__ int ds_phase(const GeneralJob &j, uint32_t d, uint32_
       for (uint32_t s = 0; s < EE; s++) {
         const uint32_t i = lane + 64 * s;
         const bool v = i < nds;
-        dk[s] = v ? at<uint64_t>(L_DKEY + 8 * i) : ~0ull;
-        dl[s] = v ? at<uint32_t>(L_DLEN + 4 * i) : 0;
-        dq[s] = v ? at<uint16_t>(L_DSEQ + 2 * i) : 0;
+        dk[s] = v ? at<uint64_t>(M::L_DKEY + 8 * i) : ~0ull;
+        dl[s] = v ? at<uint32_t>(M::L_DLEN + 4 * i) : 0;
+        dq[s] = v ? at<uint16_t>(M::L_DSEQ + 2 * i) : 0;
       }
-      rank_le4(L_DKEY, nds, dk, dr);  // distinct keys: a permutation
+      rank_le4(M::L_DKEY, nds, dk, dr);  // distinct keys: a permutation
       __syncthreads();
 #pragma unroll
       for (uint32_t s = 0; s < EE; s++) {
         if (lane + 64 * s < nds) {
           const uint32_t r = dr[s];
-          at<uint64_t>(L_DKEY + 8 * r) = dk[s];
-          at<uint32_t>(L_DLEN + 4 * r) = dl[s];
-          at<uint16_t>(L_DSEQ + 2 * r) = (uint16_t)dq[s];
+          at<uint64_t>(M::L_DKEY + 8 * r) = dk[s];
+          at<uint32_t>(M::L_DLEN + 4 * r) = dl[s];
+          at<uint16_t>(M::L_DSEQ + 2 * r) = (uint16_t)dq[s];
         }
       }
       __syncthreads();
@@ -519,16 +525,16 @@ __device__ __forceinline__ int ds_phase(const GeneralJob &j, uint32_t d, uint32_
       uint64_t eend[EE];
       uint32_t seg_lane = 0;
       const uint32_t r0 = EE * lane;
-      uint32_t cprev = r0 > 0 && r0 - 1 < nds ? (uint32_t)(at<uint64_t>(L_DKEY + 8 * (r0 - 1)) >> 32) : 0;
+      uint32_t cprev = r0 > 0 && r0 - 1 < nds ? (uint32_t)(at<uint64_t>(M::L_DKEY + 8 * (r0 - 1)) >> 32) : 0;
 #pragma unroll
       for (uint32_t s = 0; s < EE; s++) {
         const uint32_t r = r0 + s;
         const bool v = r < nds;
-        const uint64_t k = v ? at<uint64_t>(L_DKEY + 8 * r) : 0;
+        const uint64_t k = v ? at<uint64_t>(M::L_DKEY + 8 * r) : 0;
         ecl[s] = (uint32_t)k >> 7;
         ecli[s] = (uint32_t)(k >> 32);
-        eend[s] = v ? (uint64_t)ecl[s] + at<uint32_t>(L_DLEN + 4 * r) : 0;
-        eseq[s] = v ? at<uint16_t>(L_DSEQ + 2 * r) : 0xffff;
+        eend[s] = v ? (uint64_t)ecl[s] + at<uint32_t>(M::L_DLEN + 4 * r) : 0;
+        eseq[s] = v ? at<uint16_t>(M::L_DSEQ + 2 * r) : 0xffff;
         segst[s] = v && (r == 0 || cprev != ecli[s]);
         seg_lane += segst[s];
         cprev = ecli[s];
@@ -571,28 +577,28 @@ __device__ __forceinline__ int ds_phase(const GeneralJob &j, uint32_t d, uint32_
         run += newr[s];
         const uint32_t rid = run - 1;
         if (newr[s]) {
-          at<uint32_t>(L_QCLK + 4 * rid) = ecl[s];
-          at<uint8_t>(L_QGRP + rid) = (uint8_t)segid[s];
+          at<uint32_t>(M::L_QCLK + 4 * rid) = ecl[s];
+          at<uint8_t>(M::L_QGRP + rid) = (uint8_t)segid[s];
         }
         const bool nxt_new = s + 1 < EE ? newr[s + 1] != 0 : next_first != 0;
         if (r + 1 >= nds || nxt_new) {
           const uint64_t en = rmax[s] & 0x1ffffffffull;
           bad |= en > 0xffffffffull;
-          at<uint32_t>(L_QEND + 4 * rid) = (uint32_t)en;
+          at<uint32_t>(M::L_QEND + 4 * rid) = (uint32_t)en;
         }
         if (segst[s]) {
-          at<uint16_t>(L_GFIRST + 2 * segid[s]) = (uint16_t)rid;
-          at<uint32_t>(L_GCLI + 4 * segid[s]) = ecli[s];
-          at<uint32_t>(L_GMIN + 4 * segid[s]) = 0xffffffffu;
+          at<uint16_t>(M::L_GFIRST + 2 * segid[s]) = (uint16_t)rid;
+          at<uint32_t>(M::L_GCLI + 4 * segid[s]) = ecli[s];
+          at<uint32_t>(M::L_GMIN + 4 * segid[s]) = 0xffffffffu;
         }
       }
-      if (lane == 0) at<uint16_t>(L_GFIRST + 2 * ngroups) = (uint16_t)nranges;
+      if (lane == 0) at<uint16_t>(M::L_GFIRST + 2 * ngroups) = (uint16_t)nranges;
       if (__any(bad)) return DS_DECLINE;
       __syncthreads();
       // first appearance of each client: min over its entries' (update << 8 | position)
 #pragma unroll
       for (uint32_t s = 0; s < EE; s++)
-        if (r0 + s < nds) atomicMin(&at<uint32_t>(L_GMIN + 4 * segid[s]), eseq[s]);
+        if (r0 + s < nds) atomicMin(&at<uint32_t>(M::L_GMIN + 4 * segid[s]), eseq[s]);
     }
     // merged ranges q = E*lane + s: exclusive byte prefix over range ids
     {
@@ -600,13 +606,13 @@ __device__ __forceinline__ int ds_phase(const GeneralJob &j, uint32_t d, uint32_
 #pragma unroll
       for (uint32_t s = 0; s < EE; s++) {
         const uint32_t q = EE * lane + s;
-        const uint32_t c0 = q < nranges ? at<uint32_t>(L_QCLK + 4 * q) : 0;
+        const uint32_t c0 = q < nranges ? at<uint32_t>(M::L_QCLK + 4 * q) : 0;
         if constexpr (DSV2) {
-          const bool first = q < nranges && at<uint16_t>(L_GFIRST + 2 * at<uint8_t>(L_QGRP + q)) == q;
-          const uint32_t pe = q < nranges && !first ? at<uint32_t>(L_QEND + 4 * (q - 1)) : 0;
-          qb[s] = q < nranges ? vsz(c0 - pe) + vsz(at<uint32_t>(L_QEND + 4 * q) - c0 - 1) : 0;
+          const bool first = q < nranges && at<uint16_t>(M::L_GFIRST + 2 * at<uint8_t>(M::L_QGRP + q)) == q;
+          const uint32_t pe = q < nranges && !first ? at<uint32_t>(M::L_QEND + 4 * (q - 1)) : 0;
+          qb[s] = q < nranges ? vsz(c0 - pe) + vsz(at<uint32_t>(M::L_QEND + 4 * q) - c0 - 1) : 0;
         } else {
-          qb[s] = q < nranges ? vsz(c0) + vsz(at<uint32_t>(L_QEND + 4 * q) - c0) : 0;
+          qb[s] = q < nranges ? vsz(c0) + vsz(at<uint32_t>(M::L_QEND + 4 * q) - c0) : 0;
         }
         t += qb[s];
       }
@@ -615,10 +621,10 @@ __device__ __forceinline__ int ds_phase(const GeneralJob &j, uint32_t d, uint32_
 #pragma unroll
       for (uint32_t s = 0; s < EE; s++) {
         const uint32_t q = EE * lane + s;
-        if (q < nranges) at<uint16_t>(L_QPRE + 2 * q) = (uint16_t)run;
+        if (q < nranges) at<uint16_t>(M::L_QPRE + 2 * q) = (uint16_t)run;
         run += qb[s];
       }
-      if (lane == 63) at<uint16_t>(L_QPRE + 2 * nranges) = (uint16_t)incl;
+      if (lane == 63) at<uint16_t>(M::L_QPRE + 2 * nranges) = (uint16_t)incl;
     }
     __syncthreads();
     // groups g = lane + 64 s: bytes and rank by first appearance
@@ -627,18 +633,18 @@ __device__ __forceinline__ int ds_phase(const GeneralJob &j, uint32_t d, uint32_
     for (uint32_t s = 0; s < EE; s++) {
       const uint32_t g = lane + 64 * s;
       const bool v = g < ngroups;
-      const uint32_t f0 = v ? at<uint16_t>(L_GFIRST + 2 * g) : 0, f1 = v ? at<uint16_t>(L_GFIRST + 2 * g + 2) : 0;
-      gbytes[s] = v ? vsz(at<uint32_t>(L_GCLI + 4 * g)) + vsz(f1 - f0) + at<uint16_t>(L_QPRE + 2 * f1) -
-                          at<uint16_t>(L_QPRE + 2 * f0)
+      const uint32_t f0 = v ? at<uint16_t>(M::L_GFIRST + 2 * g) : 0, f1 = v ? at<uint16_t>(M::L_GFIRST + 2 * g + 2) : 0;
+      gbytes[s] = v ? vsz(at<uint32_t>(M::L_GCLI + 4 * g)) + vsz(f1 - f0) + at<uint16_t>(M::L_QPRE + 2 * f1) -
+                          at<uint16_t>(M::L_QPRE + 2 * f0)
                     : 0;
-      const uint32_t mine = v ? at<uint32_t>(L_GMIN + 4 * g) : 0;
+      const uint32_t mine = v ? at<uint32_t>(M::L_GMIN + 4 * g) : 0;
       uint32_t rk_ = 0;
-      for (uint32_t h = 0; h < ngroups; h++) rk_ += at<uint32_t>(L_GMIN + 4 * h) < mine;
+      for (uint32_t h = 0; h < ngroups; h++) rk_ += at<uint32_t>(M::L_GMIN + 4 * h) < mine;
       grk[s] = rk_;
     }
 #pragma unroll
     for (uint32_t s = 0; s < EE; s++)
-      if (lane + 64 * s < ngroups) at<uint16_t>(L_GBYR + 2 * grk[s]) = (uint16_t)gbytes[s];
+      if (lane + 64 * s < ngroups) at<uint16_t>(M::L_GBYR + 2 * grk[s]) = (uint16_t)gbytes[s];
     __syncthreads();
     const uint32_t ds_hdr = vsz(ngroups);
     const uint32_t dsb = hdr + struct_bytes;
@@ -646,7 +652,7 @@ __device__ __forceinline__ int ds_phase(const GeneralJob &j, uint32_t d, uint32_
     {  // exclusive prefix over ranks (ranks E*lane + s)
       uint32_t v[EE], t = 0;
 #pragma unroll
-      for (uint32_t s = 0; s < EE; s++) { const uint32_t r = EE * lane + s; v[s] = r < ngroups ? at<uint16_t>(L_GBYR + 2 * r) : 0; t += v[s]; }
+      for (uint32_t s = 0; s < EE; s++) { const uint32_t r = EE * lane + s; v[s] = r < ngroups ? at<uint16_t>(M::L_GBYR + 2 * r) : 0; t += v[s]; }
       const uint32_t incl = wave_incl_add(t);
       ds_groups_bytes = lane_read(incl, 63);
       uint32_t run = incl - t;
@@ -654,7 +660,7 @@ __device__ __forceinline__ int ds_phase(const GeneralJob &j, uint32_t d, uint32_
 #pragma unroll
       for (uint32_t s = 0; s < EE; s++) {
         const uint32_t r = EE * lane + s;
-        if (r < ngroups) at<uint16_t>(L_GBYR + 2 * r) = (uint16_t)run;
+        if (r < ngroups) at<uint16_t>(M::L_GBYR + 2 * r) = (uint16_t)run;
         run += v[s];
       }
     }
@@ -664,10 +670,10 @@ __device__ __forceinline__ int ds_phase(const GeneralJob &j, uint32_t d, uint32_
     for (uint32_t s = 0; s < EE; s++) {
       const uint32_t g = lane + 64 * s;
       if (g < ngroups) {
-        const uint32_t f0 = at<uint16_t>(L_GFIRST + 2 * g), f1 = at<uint16_t>(L_GFIRST + 2 * g + 2);
-        const uint32_t off = dsb + ds_hdr + at<uint16_t>(L_GBYR + 2 * grk[s]);
-        at<uint32_t>(L_GMIN + 4 * g) = off;  // first appearance is no longer needed
-        at<uint32_t>(L_GB2 + 4 * g) = off + vsz(at<uint32_t>(L_GCLI + 4 * g)) + vsz(f1 - f0) - at<uint16_t>(L_QPRE + 2 * f0);
+        const uint32_t f0 = at<uint16_t>(M::L_GFIRST + 2 * g), f1 = at<uint16_t>(M::L_GFIRST + 2 * g + 2);
+        const uint32_t off = dsb + ds_hdr + at<uint16_t>(M::L_GBYR + 2 * grk[s]);
+        at<uint32_t>(M::L_GMIN + 4 * g) = off;  // first appearance is no longer needed
+        at<uint32_t>(M::L_GB2 + 4 * g) = off + vsz(at<uint32_t>(M::L_GCLI + 4 * g)) + vsz(f1 - f0) - at<uint16_t>(M::L_QPRE + 2 * f0);
       }
     }
     __syncthreads();
@@ -684,18 +690,18 @@ __device__ __forceinline__ int ds_phase(const GeneralJob &j, uint32_t d, uint32_
     for (uint32_t s = 0; s < EE; s++) {
       const uint32_t g = lane + 64 * s;
       if (g < ngroups)
-        put_vu(dst, put_vu(dst, at<uint32_t>(L_GMIN + 4 * g), at<uint32_t>(L_GCLI + 4 * g)),
-               at<uint16_t>(L_GFIRST + 2 * g + 2) - at<uint16_t>(L_GFIRST + 2 * g));
+        put_vu(dst, put_vu(dst, at<uint32_t>(M::L_GMIN + 4 * g), at<uint32_t>(M::L_GCLI + 4 * g)),
+               at<uint16_t>(M::L_GFIRST + 2 * g + 2) - at<uint16_t>(M::L_GFIRST + 2 * g));
       const uint32_t q = EE * lane + s;
       if (q < nranges) {
-        const uint32_t c0 = at<uint32_t>(L_QCLK + 4 * q);
-        const uint32_t off = at<uint32_t>(L_GB2 + 4 * at<uint8_t>(L_QGRP + q)) + at<uint16_t>(L_QPRE + 2 * q);
+        const uint32_t c0 = at<uint32_t>(M::L_QCLK + 4 * q);
+        const uint32_t off = at<uint32_t>(M::L_GB2 + 4 * at<uint8_t>(M::L_QGRP + q)) + at<uint16_t>(M::L_QPRE + 2 * q);
         if constexpr (DSV2) {
-          const bool first = at<uint16_t>(L_GFIRST + 2 * at<uint8_t>(L_QGRP + q)) == q;
-          const uint32_t pe = first ? 0 : at<uint32_t>(L_QEND + 4 * (q - 1));
-          put_vu(dst, put_vu(dst, off, c0 - pe), at<uint32_t>(L_QEND + 4 * q) - c0 - 1);
+          const bool first = at<uint16_t>(M::L_GFIRST + 2 * at<uint8_t>(M::L_QGRP + q)) == q;
+          const uint32_t pe = first ? 0 : at<uint32_t>(M::L_QEND + 4 * (q - 1));
+          put_vu(dst, put_vu(dst, off, c0 - pe), at<uint32_t>(M::L_QEND + 4 * q) - c0 - 1);
         } else {
-          put_vu(dst, put_vu(dst, off, c0), at<uint32_t>(L_QEND + 4 * q) - c0);
+          put_vu(dst, put_vu(dst, off, c0), at<uint32_t>(M::L_QEND + 4 * q) - c0);
         }
       }
     }
@@ -713,14 +719,14 @@ __device__ __forceinline__ int ds_phase(const GeneralJob &j, uint32_t d, uint32_
 // Grid: a multiple of 8 blocks; block b takes documents (b % 8) * G/8 + b / 8 + k * G.
 // NESTED: the retry pass over the `nd` documents listed in j.list (those the first pass declined), with
 // nested payload checks; its declines go to j.pend_list as before.
-template <int STOP, bool DSONLY, bool DSV2, bool NESTED>
+template <class M, int STOP, bool DSONLY, bool DSV2, bool NESTED>
 __device__ __forceinline__ void merge_doc_v1(const GeneralJob &j, uint32_t di) {
   const uint32_t lane = threadIdx.x;
   {
     const uint32_t d = NESTED ? j.list[di] : di;
     const uint32_t u0 = j.doc_upd[d], k = j.doc_upd[d + 1] - u0;
     const uint64_t b0 = uoff_g(j, u0), bytes = uoff_g(j, u0 + k) - b0;
-    if ((DSONLY ? k == 0 : k <= 1) || k > UPD || bytes > IN) {
+    if ((DSONLY ? k == 0 : k <= 1) || k > UPD || bytes > M::IN) {
       if (lane == 0) decline(j, d);
       return;
     }
@@ -729,11 +735,11 @@ __device__ __forceinline__ void merge_doc_v1(const GeneralJob &j, uint32_t di) {
     {
       const uint4 *src = reinterpret_cast<const uint4 *>(j.A + (b0 - base));
       const uint32_t nvec = (uint32_t)((base + bytes + 15) >> 4);
-      for (uint32_t v = lane; v < nvec; v += 64) at<uint4>(L_IN + 16 * v) = src[v];
+      for (uint32_t v = lane; v < nvec; v += 64) at<uint4>(M::L_IN + 16 * v) = src[v];
     }
-    for (uint32_t i = lane; i <= k; i += 64) at<uint16_t>(L_UOFF + 2 * i) = (uint16_t)(uoff_g(j, u0 + i) - b0 + base);
-    if (lane < 2) at<uint32_t>(L_MISC + 4 * lane) = 0;
-    if (lane < 16) at<uint32_t>(L_HIST + 4 * lane) = 0;
+    for (uint32_t i = lane; i <= k; i += 64) at<uint16_t>(M::L_UOFF + 2 * i) = (uint16_t)(uoff_g(j, u0 + i) - b0 + base);
+    if (lane < 8) at<uint32_t>(M::L_MISC + 4 * lane) = 0;  // counters, duplicate-check bitmap
+    if (lane < 16) at<uint32_t>(M::L_HIST + 4 * lane) = 0;
     __syncthreads();
     YM_STOP(1)
     // ---- 2. walk.  W1: one lane per update that has structs, updates ordered by length bucket so
@@ -748,12 +754,12 @@ __device__ __forceinline__ void merge_doc_v1(const GeneralJob &j, uint32_t di) {
         has[s] = 0;
         ulen[s] = 0;
         if (u < k) {
-          const uint32_t u0_ = at<uint16_t>(L_UOFF + 2 * u), len = at<uint16_t>(L_UOFF + 2 * u + 2) - u0_;
+          const uint32_t u0_ = at<uint16_t>(M::L_UOFF + 2 * u), len = at<uint16_t>(M::L_UOFF + 2 * u + 2) - u0_;
           empty |= len == 0;
           ulen[s] = len;
           if (len > 0 && (DSONLY || sm[u0_] == 0)) {
             // no structs: the delete set follows (DSONLY: the input is the delete set)
-            at<uint16_t>(L_UDS + 2 * u) = (uint16_t)(DSONLY ? u0_ : u0_ + 1);
+            at<uint16_t>(M::L_UDS + 2 * u) = (uint16_t)(DSONLY ? u0_ : u0_ + 1);
           } else {
             has[s] = 1;
           }
@@ -769,7 +775,7 @@ __device__ __forceinline__ void merge_doc_v1(const GeneralJob &j, uint32_t di) {
 #pragma unroll
         for (uint32_t s = 0; s < UPD / 64; s++) {
           const uint64_t m = __ballot(has[s]);
-          if (has[s]) at<uint8_t>(L_UORD + base + __popcll(m & ((1ull << lane) - 1))) = (uint8_t)(lane + 64 * s);
+          if (has[s]) at<uint8_t>(M::L_UORD + base + __popcll(m & ((1ull << lane) - 1))) = (uint8_t)(lane + 64 * s);
           base += __popcll(m);
         }
       } else {
@@ -781,31 +787,34 @@ __device__ __forceinline__ void merge_doc_v1(const GeneralJob &j, uint32_t di) {
           ub[s] = 16;
           if (has[s]) {
             ub[s] = ulen[s] >> 3 < 15 ? ulen[s] >> 3 : 15;
-            up[s] = atomicAdd(&at<uint32_t>(L_HIST + 4 * ub[s]), 1u);
+            up[s] = atomicAdd(&at<uint32_t>(M::L_HIST + 4 * ub[s]), 1u);
           }
         }
         __syncthreads();
-        const uint32_t h = lane < 16 ? at<uint32_t>(L_HIST + 4 * lane) : 0;
+        const uint32_t h = lane < 16 ? at<uint32_t>(M::L_HIST + 4 * lane) : 0;
         const uint32_t hincl = wave_incl_add(h);
         __syncthreads();
-        if (lane < 16) at<uint32_t>(L_HIST + 4 * lane) = hincl - h;
+        if (lane < 16) at<uint32_t>(M::L_HIST + 4 * lane) = hincl - h;
         __syncthreads();
 #pragma unroll
         for (uint32_t s = 0; s < UPD / 64; s++)
-          if (ub[s] < 16) at<uint8_t>(L_UORD + at<uint32_t>(L_HIST + 4 * ub[s]) + up[s]) = (uint8_t)(lane + 64 * s);
+          if (ub[s] < 16) at<uint8_t>(M::L_UORD + at<uint32_t>(M::L_HIST + 4 * ub[s]) + up[s]) = (uint8_t)(lane + 64 * s);
       }
+      __syncthreads();
+      // the list lives in the record region: read into registers before the walk appends records
+      const uint32_t w0 = at<uint8_t>(M::L_UORD + lane), w1 = at<uint8_t>(M::L_UORD + 64 + lane);
       __syncthreads();
       bool ok = true;
 #pragma unroll 1
-      for (uint32_t i = lane; i < n1; i += 64) ok &= walk_sections<NESTED>(at<uint8_t>(L_UORD + i));
+      for (uint32_t i = lane, w = w0; i < n1; i += 64, w = w1) ok &= walk_sections<M, NESTED>(w);
       if (__any(!ok)) YM_DECLINE()
     }
     __syncthreads();
     YM_STOP(8)
-    const uint32_t nsec = at<uint32_t>(L_MISC);
+    const uint32_t nsec = at<uint32_t>(M::L_MISC);
     if ((DSONLY ? nsec != 0 : nsec == 0) || nsec > SEC) YM_DECLINE()
     // pad the key array to a multiple of 4 (rank loops read quads; SEC is a multiple of 4)
-    if (lane < 3 && nsec + lane < ((nsec + 3) & ~3u)) at<uint64_t>(L_SKEY + 8 * (nsec + lane)) = ~0ull;
+    if (lane < 3 && nsec + lane < ((nsec + 3) & ~3u)) at<uint64_t>(M::L_SKEY + 8 * (nsec + lane)) = ~0ull;
     __syncthreads();
     // output slot: 64-aligned inside the bound 2 * in + 64 per doc (no global atomics)
     const uint64_t slot = 2 * (b0 - uoff_g(j, 0)) + 64ull * d;
@@ -815,8 +824,8 @@ __device__ __forceinline__ void merge_doc_v1(const GeneralJob &j, uint32_t di) {
     const Slot dst = make_slot(j.out + slot_al, (uint32_t)(slot_end - slot_al));
     uint32_t hdr = 0, struct_bytes = 0;
     if constexpr (!DSONLY) {
-      const int r = nsec <= 64 ? sec_phase<1, STOP>(j, d, nsec, slot, slot_al, slot_end, bytes, dst, hdr, struct_bytes)
-                               : sec_phase<2, STOP>(j, d, nsec, slot, slot_al, slot_end, bytes, dst, hdr, struct_bytes);
+      const int r = nsec <= 64 ? sec_phase<M, 1, STOP>(j, d, nsec, slot, slot_al, slot_end, bytes, dst, hdr, struct_bytes)
+                               : sec_phase<M, 2, STOP>(j, d, nsec, slot, slot_al, slot_end, bytes, dst, hdr, struct_bytes);
       if (r == SP_DECLINE) YM_DECLINE()
       if (r == SP_STOP && lane == 0) { j.status[d] = ym::ST_OK; j.out_len[d] = 0; }
       if (r != SP_DONE) {
@@ -835,28 +844,30 @@ __device__ __forceinline__ void merge_doc_v1(const GeneralJob &j, uint32_t di) {
         const uint32_t u = lane + 64 * s;
         bool has = false;
         if (u < k) {
-          const uint32_t p = at<uint16_t>(L_UDS + 2 * u);
-          has = p >= at<uint16_t>(L_UOFF + 2 * u + 2) || sm[p] != 0;  // (a missing delete set: W2 declines)
+          const uint32_t p = at<uint16_t>(M::L_UDS + 2 * u);
+          has = p >= at<uint16_t>(M::L_UOFF + 2 * u + 2) || sm[p] != 0;  // (a missing delete set: W2 declines)
         }
         const uint64_t m = __ballot(has);
-        if (has) at<uint8_t>(L_UORD2 + n2 + __popcll(m & ((1ull << lane) - 1))) = (uint8_t)u;
+        if (has) at<uint8_t>(M::L_UORD2 + n2 + __popcll(m & ((1ull << lane) - 1))) = (uint8_t)u;
         n2 += __popcll(m);
       }
       __syncthreads();
+      const uint32_t w0 = at<uint8_t>(M::L_UORD2 + lane), w1 = at<uint8_t>(M::L_UORD2 + 64 + lane);
+      __syncthreads();
       bool ok = true;
 #pragma unroll 1
-      for (uint32_t i = lane; i < n2; i += 64) ok &= walk_ds<DSV2>(at<uint8_t>(L_UORD2 + i));
+      for (uint32_t i = lane, w = w0; i < n2; i += 64, w = w1) ok &= walk_ds<M, DSV2>(w);
       if (__any(!ok)) YM_DECLINE()
     }
     __syncthreads();
-    const uint32_t nds = at<uint32_t>(L_MISC + 4);
+    const uint32_t nds = at<uint32_t>(M::L_MISC + 4);
     if (nds > DSN) YM_DECLINE()
-    if (lane < 3 && nds + lane < ((nds + 3) & ~3u)) at<uint64_t>(L_DKEY + 8 * (nds + lane)) = ~0ull;
+    if (lane < 3 && nds + lane < ((nds + 3) & ~3u)) at<uint64_t>(M::L_DKEY + 8 * (nds + lane)) = ~0ull;
     __syncthreads();
     YM_STOP(2)
     {
-      const int r = nds <= 64 ? ds_phase<1, STOP, DSV2>(j, d, nds, hdr, struct_bytes, slot, slot_al, slot_end, bytes, dst)
-                              : ds_phase<2, STOP, DSV2>(j, d, nds, hdr, struct_bytes, slot, slot_al, slot_end, bytes, dst);
+      const int r = nds <= 64 ? ds_phase<M, 1, STOP, DSV2>(j, d, nds, hdr, struct_bytes, slot, slot_al, slot_end, bytes, dst)
+                              : ds_phase<M, 2, STOP, DSV2>(j, d, nds, hdr, struct_bytes, slot, slot_al, slot_end, bytes, dst);
       if (r == DS_DECLINE) YM_DECLINE()
       if (r == DS_STOP && lane == 0) { j.status[d] = ym::ST_OK; j.out_len[d] = 0; }
     }
@@ -870,9 +881,9 @@ template <int STOP, int OCC, bool DSONLY = false, bool DSV2 = false, bool NESTED
 __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j, uint32_t nd) {
   const uint32_t d0 = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
   if constexpr (ONE) {
-    if (d0 < nd) merge_doc_v1<STOP, DSONLY, DSV2, NESTED>(j, d0);
+    if (d0 < nd) merge_doc_v1<Map<NESTED ? IN_NESTED : IN_HOT>, STOP, DSONLY, DSV2, NESTED>(j, d0);
   } else {
-    for (uint32_t di = d0; di < nd; di += gridDim.x) merge_doc_v1<STOP, DSONLY, DSV2, NESTED>(j, di);
+    for (uint32_t di = d0; di < nd; di += gridDim.x) merge_doc_v1<Map<NESTED ? IN_NESTED : IN_HOT>, STOP, DSONLY, DSV2, NESTED>(j, di);
   }
 }
 
@@ -896,11 +907,11 @@ int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st
     const uint32_t grid = fast_grid(j.n);
     const bool one = j.n <= FAST_ONE_MAX;
     if (j.v2) {
-      if (one) k_fast_merge_v1<0, 5, true, true><<<grid, 64, fastv1::LDS_BYTES, st>>>(j, j.n);
-      else k_fast_merge_v1<0, 5, true, true, false, false><<<grid, 64, fastv1::LDS_BYTES, st>>>(j, j.n);
+      if (one) k_fast_merge_v1<0, 8, true, true><<<grid, 64, MapHot::LDS_BYTES, st>>>(j, j.n);
+      else k_fast_merge_v1<0, 5, true, true, false, false><<<grid, 64, MapHot::LDS_BYTES, st>>>(j, j.n);
     } else {
-      if (one) k_fast_merge_v1<0, 5, true, false><<<grid, 64, fastv1::LDS_BYTES, st>>>(j, j.n);
-      else k_fast_merge_v1<0, 5, true, false, false, false><<<grid, 64, fastv1::LDS_BYTES, st>>>(j, j.n);
+      if (one) k_fast_merge_v1<0, 8, true, false><<<grid, 64, MapHot::LDS_BYTES, st>>>(j, j.n);
+      else k_fast_merge_v1<0, 5, true, false, false, false><<<grid, 64, MapHot::LDS_BYTES, st>>>(j, j.n);
     }
     return 1;
   }
@@ -914,26 +925,26 @@ int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st
     e = getenv("YMERGE_FAST_LDS_PAD");  // occupancy experiments: extra dynamic LDS per wave
     pad = e ? atoi(e) : 0;
   }
-  const uint32_t LDS_BYTES = fastv1::LDS_BYTES + pad;
+  const uint32_t LDS_BYTES = MapHot::LDS_BYTES + pad;
   static int occ = -1;
-  // (the launch bound only steers register allocation: 5 leaves the kernel at <= 64 VGPRs, 8 waves per SIMD
-  // by registers; the LDS map sets 7)
-  if (occ < 0) { const char *e = getenv("YMERGE_FAST_OCC"); occ = e ? atoi(e) : 5; }
+  // (the launch bound steers register allocation: 8 keeps the kernel within 8 waves' SGPRs and VGPRs per SIMD,
+  // what the 5 KB LDS map allows; 5 lets it use more registers, 7 waves by SGPRs)
+  if (occ < 0) { const char *e = getenv("YMERGE_FAST_OCC"); occ = e ? atoi(e) : 8; }
 #define YM_LAUNCH(S, O) k_fast_merge_v1<S, O><<<grid, 64, LDS_BYTES, st>>>(j, j.n)
   if (j.n > FAST_ONE_MAX) {
     k_fast_merge_v1<0, 5, false, false, false, false><<<grid, 64, LDS_BYTES, st>>>(j, j.n);
-  } else if (occ == 8) {
-    YM_LAUNCH(0, 8);
+  } else if (occ == 5) {
+    YM_LAUNCH(0, 5);
   } else {
     switch (stop) {
-      case 1: YM_LAUNCH(1, 5); break;
-      case 2: YM_LAUNCH(2, 5); break;
-      case 3: YM_LAUNCH(3, 5); break;
-      case 4: YM_LAUNCH(4, 5); break;
-      case 5: YM_LAUNCH(5, 5); break;
-      case 7: YM_LAUNCH(7, 5); break;
-      case 8: YM_LAUNCH(8, 5); break;
-      default: YM_LAUNCH(0, 5); break;
+      case 1: YM_LAUNCH(1, 8); break;
+      case 2: YM_LAUNCH(2, 8); break;
+      case 3: YM_LAUNCH(3, 8); break;
+      case 4: YM_LAUNCH(4, 8); break;
+      case 5: YM_LAUNCH(5, 8); break;
+      case 7: YM_LAUNCH(7, 8); break;
+      case 8: YM_LAUNCH(8, 8); break;
+      default: YM_LAUNCH(0, 8); break;
     }
   }
 #undef YM_LAUNCH
@@ -949,8 +960,8 @@ int fast_nested_launch(const GeneralJob &j, uint32_t n, hipStream_t st) {
   static int off = -1;
   if (off < 0) { const char *e = getenv("YMERGE_FAST_NESTED"); off = e && atoi(e) == 0 ? 1 : 0; }
   if (off) return 0;
-  if (n <= FAST_ONE_MAX) k_fast_merge_v1<0, 5, false, false, true><<<fast_grid(n), 64, fastv1::LDS_BYTES, st>>>(j, n);
-  else k_fast_merge_v1<0, 5, false, false, true, false><<<fast_grid(n), 64, fastv1::LDS_BYTES, st>>>(j, n);
+  if (n <= FAST_ONE_MAX) k_fast_merge_v1<0, 6, false, false, true><<<fast_grid(n), 64, MapNested::LDS_BYTES, st>>>(j, n);
+  else k_fast_merge_v1<0, 5, false, false, true, false><<<fast_grid(n), 64, MapNested::LDS_BYTES, st>>>(j, n);
   return 1;
 }
 
