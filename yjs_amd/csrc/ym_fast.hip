@@ -295,6 +295,13 @@ __device__ __forceinline__ bool walk_ds(uint32_t u) {
   return !c.bad;
 }
 
+#ifdef YM_FAST_TIMELINE
+__device__ unsigned g_fast_ph[131072][8];  // per block: s_memrealtime (low 32 bits) after each phase
+#define YM_TS(i) \
+  if (threadIdx.x == 0 && blockIdx.x < 131072) g_fast_ph[blockIdx.x][i] = (unsigned)__builtin_amdgcn_s_memrealtime();
+#else
+#define YM_TS(i)
+#endif
 #define YM_DECLINE()                                 \
   {                                                  \
     if (lane == 0) decline(j, d);                    \
@@ -383,6 +390,7 @@ __device__ __forceinline__ int sec_phase(const GeneralJob &j, uint32_t d, uint32
                             __popc(__builtin_amdgcn_readfirstlane(w.z)) + __popc(__builtin_amdgcn_readfirstlane(w.w));
       if (seen != nsec) return SP_DECLINE;
     }
+    YM_TS(2)
     if (STOP == 3) return SP_STOP;
     // ---- 4. layout over rank order; lane owns positions r = E*lane + s
     uint64_t sk[EE];
@@ -460,6 +468,7 @@ __device__ __forceinline__ int sec_phase(const GeneralJob &j, uint32_t d, uint32
       if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }  // caller's arena too small
       return SP_CAP;
     }
+    YM_TS(3)
     if (STOP == 4) return SP_STOP;
     // ---- 4b. write the struct section: per section its part header, its Skip, then its bytes verbatim
     if (lane == 0) put_vu(dst, 0, nparts);
@@ -683,6 +692,7 @@ __device__ __forceinline__ int ds_phase(const GeneralJob &j, uint32_t d, uint32_
       if (lane == 0) { j.status[d] = ym::ST_CAPACITY; j.out_len[d] = 0; }
       return DS_DONE;
     }
+    YM_TS(6)
     if (STOP == 5) return DS_STOP;
     // ---- 6. write the delete set: vu(#clients) | per client (first-appearance order): client, count, ranges
     if (lane == 0) put_vu(dst, dsb, ngroups);
@@ -741,6 +751,7 @@ __device__ __forceinline__ void merge_doc_v1(const GeneralJob &j, uint32_t di) {
     if (lane < 8) at<uint32_t>(M::L_MISC + 4 * lane) = 0;  // counters, duplicate-check bitmap
     if (lane < 16) at<uint32_t>(M::L_HIST + 4 * lane) = 0;
     __syncthreads();
+    YM_TS(0)
     YM_STOP(1)
     // ---- 2. walk.  W1: one lane per update that has structs, updates ordered by length bucket so
     // that the lanes of one round take updates of similar shape; W2: one lane per update whose delete
@@ -810,6 +821,7 @@ __device__ __forceinline__ void merge_doc_v1(const GeneralJob &j, uint32_t di) {
       if (__any(!ok)) YM_DECLINE()
     }
     __syncthreads();
+    YM_TS(1)
     YM_STOP(8)
     const uint32_t nsec = at<uint32_t>(M::L_MISC);
     if ((DSONLY ? nsec != 0 : nsec == 0) || nsec > SEC) YM_DECLINE()
@@ -834,6 +846,7 @@ __device__ __forceinline__ void merge_doc_v1(const GeneralJob &j, uint32_t di) {
       }
     }  // !DSONLY
     __syncthreads();
+    YM_TS(4)
     YM_STOP(7)
     // ---- W2 (after the struct section is written: the ranges reuse the section records' LDS): one lane per
     // update whose delete set has clients (first byte != 0), compacted by ballots
@@ -864,6 +877,7 @@ __device__ __forceinline__ void merge_doc_v1(const GeneralJob &j, uint32_t di) {
     if (nds > DSN) YM_DECLINE()
     if (lane < 3 && nds + lane < ((nds + 3) & ~3u)) at<uint64_t>(M::L_DKEY + 8 * (nds + lane)) = ~0ull;
     __syncthreads();
+    YM_TS(5)
     YM_STOP(2)
     {
       const int r = nds <= 64 ? ds_phase<M, 1, STOP, DSV2>(j, d, nds, hdr, struct_bytes, slot, slot_al, slot_end, bytes, dst)
@@ -877,11 +891,29 @@ __device__ __forceinline__ void merge_doc_v1(const GeneralJob &j, uint32_t di) {
 // ONE: the grid covers every document (one per block, no loop: nothing is hoisted across documents, so
 // the per-document values are not kept live -- and spilled -- for the whole kernel); otherwise a
 // grid-stride loop.  Grid: a multiple of 8 blocks; block b takes documents (b % 8) * G/8 + b / 8 + k * G.
+#ifdef YM_FAST_TIMELINE
+// diagnostics build: per block of the last launch, its start / end (s_memrealtime, 100 MHz), the hardware ids
+// (HW_ID: wave, SIMD, CU, SE; XCC_ID) and its document (read with ym__fast_timeline)
+__device__ unsigned long long g_fast_tl[131072][4];
+#endif
 template <int STOP, int OCC, bool DSONLY = false, bool DSV2 = false, bool NESTED = false, bool ONE = true>
 __global__ void __launch_bounds__(64, OCC) k_fast_merge_v1(GeneralJob j, uint32_t nd) {
   const uint32_t d0 = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
   if constexpr (ONE) {
+#ifdef YM_FAST_TIMELINE
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+#endif
     if (d0 < nd) merge_doc_v1<Map<NESTED ? IN_NESTED : IN_HOT>, STOP, DSONLY, DSV2, NESTED>(j, d0);
+#ifdef YM_FAST_TIMELINE
+    __syncthreads();
+    if (threadIdx.x == 0 && blockIdx.x < 131072) {
+      g_fast_tl[blockIdx.x][0] = t0;
+      g_fast_tl[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+      g_fast_tl[blockIdx.x][2] = ((unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11)) << 32) |
+                                 (unsigned)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+      g_fast_tl[blockIdx.x][3] = d0;
+    }
+#endif
   } else {
     for (uint32_t di = d0; di < nd; di += gridDim.x) merge_doc_v1<Map<NESTED ? IN_NESTED : IN_HOT>, STOP, DSONLY, DSV2, NESTED>(j, di);
   }
@@ -966,3 +998,12 @@ int fast_nested_launch(const GeneralJob &j, uint32_t n, hipStream_t st) {
 }
 
 }  // namespace ymk
+
+#ifdef YM_FAST_TIMELINE
+extern "C" int ym__fast_timeline(unsigned long long *host, int n) {  // n blocks x 4 words
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ymk::fastv1::g_fast_tl), (size_t)n * 32);
+}
+extern "C" int ym__fast_phases(unsigned *host, int n) {  // n blocks x 8 words
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ymk::fastv1::g_fast_ph), (size_t)n * 32);
+}
+#endif
