@@ -115,14 +115,15 @@ uint64_t ym_out_bound(const ym_batch *b); /* a capacity that is normally suffici
  * YM_ERR_CAPACITY when out->used > out->cap (nothing useful was written), or a negative HIP error. */
 int ym_merge(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
 /* Asynchronous ym_merge for device batches (the serving loop: calls queue back to back on `stream` and
- * the host never waits).  Runs the LDS fast path only (small documents: <= 128 updates, <= 2.5 KB V1;
+ * the host never waits).  Runs the LDS fast path only (small documents: <= 128 updates, <= 2,432 B V1;
  * the C2 / C4 shapes) and returns once the kernel is enqueued; the results are valid when the stream has
  * drained.  Each output lands in the slot region [0, 2 * input bytes + 64 * n_docs + 64) of out->arena
  * (out->cap below that: YM_ERR_CAPACITY for the documents that do not fit); out->used is not written.
  * A document the fast path declines (larger, rich nested content, invalid input) gets status YM_PENDING
  * and increments *pending (a uint32_t in device memory, or NULL): run those through ym_merge.
- * V2 batches with YM_OFF32 widen their offsets into one buffer of the library's device state: calls of
- * that kind on different streams must not overlap (on one stream they are ordered).
+ * V2 batches with YM_OFF32 widen their offsets into a device buffer of the async path's own (the synchronous
+ * entry points never touch it, so they may run on other streams at the same time); an async call of that kind
+ * waits on the device for the previous one to finish reading it, whatever stream either runs on.
  * Return value: 0, or a negative error (not a device batch, HIP launch failure). */
 int ym_merge_async(const ym_batch *b, ym_out *out, void *stream, uint32_t *pending);
 int ym_diff(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);

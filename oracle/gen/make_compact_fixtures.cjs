@@ -219,6 +219,31 @@ function loadYmb (name) {
     for (const m of late) if (rnd() < 0.5) out.push(m)
     add(`fuzz_gap/h${h}/v${v2 ? 2 : 1}`, 'fuzz_gap', v2 ? 2 : 1, out)
   }
+  // V1 delete sets with zero-length ranges (readDsLen is a plain varuint in V1): one past the client's state
+  // goes to the unapplied set, whose writeDeleteSet(DSEncoderV2) throws at it (UpdateEncoder.js:255-258); one
+  // below the state only splits the item there; an error while reading a later client comes first
+  {
+    const vu = v => { const o = []; while (v > 127) { o.push(0x80 | (v & 127)); v = Math.floor(v / 128) } o.push(v); return o }
+    const dsOnly = clients => { const o = [0, ...vu(clients.length)]; for (const [c, rs] of clients) { o.push(...vu(c), ...vu(rs.length)); for (const [k, l] of rs) o.push(...vu(k), ...vu(l)) } return new Uint8Array(o) }
+    const src = new Y13.Doc()
+    src.clientID = 1
+    const log = []
+    src.on('update', u => log.push(u))
+    src.getText('t').insert(0, 'abcd')
+    src.getText('t').insert(4, 'ef')
+    const cs = [
+      ['past_state', [...log, dsOnly([[1, [[9, 0]]]])]],
+      ['unknown_client', [dsOnly([[77, [[0, 0]]]])]],
+      ['below_state', [...log, dsOnly([[1, [[2, 0]]]])]],
+      ['below_then_past', [...log, dsOnly([[1, [[1, 0], [7, 0]]]])]],
+      ['mixed_ranges', [...log, dsOnly([[1, [[1, 2], [8, 0], [10, 3]]]])]],
+      ['two_clients', [...log, dsOnly([[2, [[0, 0]]], [1, [[0, 2]]]])]],
+      ['then_truncated', [...log, new Uint8Array([0, 2, 1, 1, 9, 0, 2, 1])]],
+      ['pending_then_zero', [log[1], log[0], dsOnly([[1, [[3, 0]]]])]],
+      ['zero_after_resume', [dsOnly([[1, [[5, 1]]]]), ...log, dsOnly([[1, [[1, 0]]]])]]
+    ]
+    for (const [name, inputs] of cs) add(`ds_zero/${name}/v1`, 'ds_zero', 1, inputs)
+  }
   fs.writeFileSync(path.join(GOLDEN, 'compact.json'), JSON.stringify({
     generator: 'oracle/gen/make_compact_fixtures.cjs',
     reference: 'gaberogan/yjs@v0 (yjs 13.4.9, /root/reference/src) under Node 12 ESM with a lib0 shim over the bundled lib0 0.2.42 (oracle/gen/ref_yjs.cjs): new Doc() (gc: true), applyUpdate[V2] per input, encodeStateAsUpdate[V2]',

@@ -2740,8 +2740,10 @@ static void resume_integration(CDoc *d) { /* resumeStructIntegration (encoding.j
 
 static void cd_split_into(CDoc *d, CCl *s, size_t at, CIt *it) { cl_insert(d, s, at, it); }
 /* readAndApplyDeleteSet over a decoded delete set (DeleteSet.js:270-323); the unapplied ranges become a
-   pending delete reader */
-static void apply_ds(CDoc *d, const DSet *ds, int kept) {
+   pending delete reader.  An unapplied range of length 0 (a V1 delete set may hold one) sets *zero: the
+   reference's writeDeleteSet of the unapplied set throws at it (DSEncoderV2.writeDsLen, UpdateEncoder.js:
+   255-258), after every client of the update's delete set has been read and applied */
+static void apply_ds(CDoc *d, const DSet *ds, int kept, int *zero) {
   DSet un;
   memset(&un, 0, sizeof(un));
   if (kept) { /* a pending reader none of whose ranges applies comes back unchanged (it went through the
@@ -2790,6 +2792,7 @@ static void apply_ds(CDoc *d, const DSet *ds, int kept) {
       int64_t enc = 0, dec = 0;
       for (size_t k = 0; k < un.cl[ci].n; k++) {
         DItem *r = &un.cl[ci].items[k];
+        if (r->len == 0 && zero) *zero = 1;
         int64_t dc = r->clock - enc, dl = r->len - 1;
         enc = r->clock + r->len;
         dec += dc > 127 ? dc : (dc & 127);
@@ -3118,10 +3121,11 @@ static void cd_transact(CDoc *d, UDec *u) { /* transact(readUpdateV2, local = fa
     DSet *pr = d->pdel;
     size_t np = d->npdel;
     d->pdel = NULL; d->npdel = 0; d->cappdel = 0;
-    for (size_t q = 0; q < np; q++) apply_ds(d, &pr[q], 1);
+    for (size_t q = 0; q < np; q++) apply_ds(d, &pr[q], 1, NULL);
   }
   { /* readAndApplyDeleteSet: each client's ranges are applied as read (the clients are independent) */
     uint32_t n = rd_vu(c, &u->rest);
+    int zero = 0;
     for (uint32_t i = 0; i < n; i++) {
       ud_reset_ds(u);
       int64_t client = rd_vu(c, &u->rest);
@@ -3134,8 +3138,9 @@ static void cd_transact(CDoc *d, UDec *u) { /* transact(readUpdateV2, local = fa
         int64_t len = ud_ds_len(c, u);
         dc_push(c, dc, clock, len);
       }
-      apply_ds(d, &one, 0);
+      apply_ds(d, &one, 0, &zero);
     }
+    if (zero) fail(c, YMO_ERR_UNEXPECTED);
   }
   /* cleanupTransactions: this one, then the one its observers opened (local: its observers do nothing) */
   CTx *nested = tx_cleanup(d, x);

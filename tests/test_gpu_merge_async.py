@@ -85,3 +85,36 @@ def test_async_declines_and_capacity(engine):
     got = _outputs(g2)
     assert got[0] == want[0]
     assert all(x in (9, YM_PENDING) for x in got[1:]), got
+
+
+def test_async_v2_off32_overlaps_host_merges(engine):
+    """V2 + YM_OFF32 async calls widen their offsets into their own buffer, so synchronous host-batch
+    merges issued while they run (on the library's stream, writing its staging offsets) cannot change what
+    the async kernels read."""
+    import torch
+    from yjs_amd.engine import _unpack
+    arena, upd_off, doc_upd = load_ymb("c2_v2")
+    n = min(len(doc_upd) - 1, 2000)
+    doc_upd = doc_upd[:n + 1].copy()
+    upd_off = upd_off[:int(doc_upd[-1]) + 1].copy()
+    arena = arena[:int(upd_off[-1])].copy()
+    want = _unpack(*engine.run_host("merge", 2, arena, upd_off, doc_upd), False)
+    a1, o1, d1 = load_ymb("c4_v2")  # the host batches: other documents, other offsets
+    m = 500
+    d1 = d1[:m + 1].copy()
+    o1 = o1[:int(d1[-1]) + 1].copy()
+    a1 = a1[:int(o1[-1])].copy()
+    want1 = _unpack(*engine.run_host("merge", 2, a1, o1, d1), False)
+    cap = 2 * int(upd_off[-1]) + 64 * n + 64
+    g = _dev(torch, arena, upd_off, doc_upd, cap, True)
+    s1 = torch.cuda.Stream()
+    pend = torch.zeros(1, dtype=torch.int32, device="cuda")
+    call = engine.prepare_merge_async(2, g["arena"], g["off"], g["doc"], g["out"], g["oo"], g["ol"], g["st"], pending=pend,
+                                      stream=s1)
+    for _ in range(3):
+        for _ in range(4):
+            assert call() == 0
+        assert _unpack(*engine.run_host("merge", 2, a1, o1, d1), False) == want1
+    torch.cuda.synchronize()
+    assert int(pend.item()) == 0
+    assert _outputs(g) == want

@@ -64,6 +64,8 @@ struct DevState {
   DBuf ws, ws_size, ws_off, layout, counters, scan_tmp, list_a, list_b, flags, bscratch;
   DBuf in_arena, in_off, in_doc, in_sv, in_svoff, out_arena, out_off, out_len, status;  // host staging
   DBuf cmp_off, cmp_len, cmp_arena;  // host batches: outputs packed in document order before the D2H copy
+  DBuf async_off;                    // ym_merge_async: its own widened offsets (not in_off: the synchronous
+  hipEvent_t ev_async = nullptr;     // calls write that one on their streams), guarded by this event
   LargeBufs large;
   PwBufs pw, pw2;
   hipEvent_t evl1 = nullptr, evn0 = nullptr, evn1 = nullptr;
@@ -397,7 +399,8 @@ int run_compact(DevState *S, hipStream_t st, GeneralJob j, uint32_t *list, uint3
         k_set_status<<<1, 64, 0, st>>>(jc.list, cnt, j.status, j.out_len, -1, ym::ST_CAPACITY);
         continue;
       }
-      jc.ws = S->ws.as<uint8_t>() - base;  // ws + ws_off[i] lands in this chunk's allocation
+      jc.ws = S->ws.as<uint8_t>();  // ws + (ws_off[i] - ws_base) lands in this chunk's allocation
+      jc.ws_base = base;
       // documents above `big` input bytes first, one per wave; then the rest, `lanes` per wave
       const bool split = lanes > 1;
       for (int part = split ? 1 : 0; part <= (split ? 2 : 0); part++) {
@@ -749,8 +752,9 @@ static void release_state(DevState *S) {
   if (S->stream) hipStreamSynchronize(S->stream);
   DBuf *bufs[] = {&S->ws, &S->ws_size, &S->ws_off, &S->layout, &S->counters, &S->scan_tmp, &S->list_a, &S->list_b,
                   &S->flags, &S->bscratch, &S->in_arena, &S->in_off, &S->in_doc, &S->in_sv, &S->in_svoff, &S->out_arena,
-                  &S->out_off, &S->out_len, &S->status, &S->cmp_off, &S->cmp_len, &S->cmp_arena};
+                  &S->out_off, &S->out_len, &S->status, &S->cmp_off, &S->cmp_len, &S->cmp_arena, &S->async_off};
   for (DBuf *b : bufs) if (b->p) hipFree(b->p);
+  if (S->ev_async) hipEventDestroy(S->ev_async);
   if (S->pinned) hipHostFree(S->pinned);
   if (S->ev0) hipEventDestroy(S->ev0);
   if (S->ev1) hipEventDestroy(S->ev1);
@@ -860,10 +864,15 @@ int ym_merge_async(const ym_batch *b, ym_out *out, void *stream, uint32_t *pendi
   j.v2 = (b->format & 0xff) == YM_V2;
   if (off32) {
     j.upd_off32 = reinterpret_cast<const uint32_t *>(b->upd_off);
-    if (j.v2) {  // the V2 kernel reads u64 offsets: widened into the library's buffer (stream-ordered)
-      if (S->in_off.ensure((b->n_upd + 1) * 8ull)) return -2;
-      k_widen<<<(b->n_upd + 256) / 256, 256, 0, st>>>(j.upd_off32, S->in_off.as<uint64_t>(), b->n_upd + 1);
-      j.upd_off = S->in_off.as<uint64_t>();
+    if (j.v2) {
+      // the V2 kernel reads u64 offsets: widened into the async path's own buffer.  The widening waits (on the
+      // device, stream-ordered) for the previous async call that read the buffer, on whatever stream it ran;
+      // the synchronous entry points use other buffers, so interleaving them with async calls is safe.
+      if (!S->ev_async) HIPCHK(hipEventCreateWithFlags(&S->ev_async, hipEventDisableTiming));
+      if (S->async_off.ensure((b->n_upd + 1) * 8ull)) return -2;
+      HIPCHK(hipStreamWaitEvent(st, S->ev_async, 0));
+      k_widen<<<(b->n_upd + 256) / 256, 256, 0, st>>>(j.upd_off32, S->async_off.as<uint64_t>(), b->n_upd + 1);
+      j.upd_off = S->async_off.as<uint64_t>();
     }
   } else {
     j.upd_off = b->upd_off;
@@ -881,6 +890,7 @@ int ym_merge_async(const ym_batch *b, ym_out *out, void *stream, uint32_t *pendi
   int fr = fast_launch(OP_MERGE, j, b->n_upd, st);
   if (fr == 0) fr = fast2_launch(OP_MERGE, j, b->n_upd, st);
   if (fr < 0) return fr;
+  if (off32 && j.v2) HIPCHK(hipEventRecord(S->ev_async, st));
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 int ym_diff(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_DIFF, b, out, stream, stats); }

@@ -862,8 +862,10 @@ YM_HOT void resume_integration(Doc &d) {
 // delete reader.  `kept`: ds is a pending reader already in the persistent arena -- when none of its ranges
 // applies, the new reader equals it range for range and is kept as it is (a history that leaves deletes
 // pending re-reads every pending reader on every update; copying them each time grew the arena
-// quadratically)
-YM_HOT void apply_ds(Doc &d, const DSet &ds, bool kept = false) {
+// quadratically).  An unapplied range of length 0 (a V1 delete set may hold one) sets *zero: the reference's
+// writeDeleteSet of the unapplied set throws at it (DSEncoderV2.writeDsLen, UpdateEncoder.js:255-258), after
+// every client of the update's delete set has been read and applied.
+YM_HOT void apply_ds(Doc &d, const DSet &ds, bool kept = false, bool *zero = nullptr) {
   Ctx &c = *d.c;
   if (kept) {
     bool any = false;
@@ -925,6 +927,7 @@ YM_HOT void apply_ds(Doc &d, const DSet &ds, bool kept = false) {
     int64_t enc = 0, dec = 0;
     for (uint32_t q = 0; q < un.cl.p[k].it.n; q++) {
       const DIt r = un.cl.p[k].it.p[q];
+      if (r.len == 0 && zero) *zero = true;
       const int64_t dc = r.clock - enc, dl = r.len - 1;
       enc = r.clock + r.len;
       dec += dc > 127 ? dc : (dc & 127);
@@ -1461,6 +1464,7 @@ YM_HOT void cd_transact(Doc &d, Reader &r) {
   }
   {  // readAndApplyDeleteSet: each client's ranges are applied as read (the clients are independent)
     const uint32_t n = rd_vu(c, r.rest);
+    bool zero = false;
     for (uint32_t i = 0; i < n && !c.err; i++) {
       r.dsCurr = 0;
       const int64_t client = rd_vu(c, r.rest);
@@ -1482,8 +1486,9 @@ YM_HOT void cd_transact(Doc &d, Reader &r) {
         DIt e = {clock, len};
         vpush(c, *d.ta, one.cl.p[k].it, e);
       }
-      if (!c.err) apply_ds(d, one);
+      if (!c.err) apply_ds(d, one, false, &zero);
     }
+    if (zero && !c.err) seterr(c, ST_UNEXPECTED);
   }
   if (c.err) return;
   // cleanupTransactions: this one, then the one its observers opened (local: its observers do nothing)

@@ -41,7 +41,7 @@ __global__ void __launch_bounds__(64, OCC) k_compact(GeneralJob j, uint32_t lane
   const uint64_t bytes = j.upd_off[u0 + k] - j.upd_off[u0];
   if ((part == 1 && bytes <= big) || (part == 2 && bytes > big)) return;
   const cpt::WsSize z = cpt::ws_size(k, bytes, j.parts_mul);
-  uint8_t *ws = j.ws + j.ws_off[i];
+  uint8_t *ws = j.ws + (j.ws_off[i] - j.ws_base);
   Ctx c = {0, j.A};
   cpt::Result R;
   // ym_compact with sv_arena: doc d's target state vector (encodeStateAsUpdate(doc, sv))

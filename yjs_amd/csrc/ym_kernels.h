@@ -36,6 +36,7 @@ struct GeneralJob {
   uint32_t parts_mul;        // part-table capacity multiplier (grown on ST_RETRY)
   uint8_t *ws;               // workspace
   const uint64_t *ws_off;    // per listed slot
+  uint64_t ws_base;          // ws_off value at ws (ym_compact's chunked launches; 0 elsewhere)
   ym::Layout *layout;        // per doc
   int32_t *status;           // per doc
   uint8_t *out;              // output arena

@@ -328,6 +328,7 @@ constexpr uint32_t POS_MASK = (1u << 28) - 1;
 // is after it (its register window still valid, so a walk carries it to the next struct), `len` is its
 // clock length and `fl` its flags.  The cursor's `cap` bounds string / ContentAny lengths (a speculative
 // parse of a position that may not start a struct; the stitch re-parses uncapped).
+template <bool NESTED = false>
 __device__ __forceinline__ bool parse_at(LCur &c, uint32_t &len, uint32_t &fl) {
   c.bad = false;
   const uint32_t info = rdb(c);
@@ -337,17 +338,18 @@ __device__ __forceinline__ bool parse_at(LCur &c, uint32_t &len, uint32_t &fl) {
     len = rvu(c);
     ok = !c.bad;
   } else {
-    ok = item_body(c, info, len);
+    ok = item_body<NESTED>(c, info, len);
   }
   ok = ok && !c.bad && c.p <= c.e;
   const uint32_t ni = sk ? info : gc ? 0 : ((info & 0xC0) ? info & ~0x20u : info);
   fl = (sk ? F_SKIP : 0) | (ni != info ? F_PATCH : 0);
   return ok;
 }
+template <bool NESTED = false>
 __device__ __forceinline__ bool parse_struct(const uint8_t *b, uint32_t p, uint32_t e, uint32_t &next, uint32_t &len,
                                              uint32_t &fl, uint32_t cap = 0xffffffffu) {
   LCur c = make(b, p, e, cap);
-  const bool ok = parse_at(c, len, fl);
+  const bool ok = parse_at<NESTED>(c, len, fl);
   next = c.p;
   return ok;
 }

@@ -1350,14 +1350,29 @@ __device__ __forceinline__ uint32_t sw_vu(const uint8_t *b, uint32_t &o, uint32_
   return v;
 }
 
-// documents of (SWMIN, SWB] bytes
+#define SW_DECLINE_R(r)                                    \
+  {                                                        \
+    if (lane == 0) { done[d] = (uint8_t)(r); atomicAdd(tally, 1u); } \
+    __syncthreads();                                       \
+    continue;                                              \
+  }
+// documents of (SWMIN, SWB] bytes.  tally[0]: documents this kernel's launches of the call declined so far
+// (completions: j.pw_count, with the chunk walk's).  Rich content (nested `any` values, JSON objects / numbers: C2R / C4R) is declined to
+// k_big_v1 after the table pass and part of the walk; once a batch has shown mostly such documents (more than
+// 256 declines, 8 per completion), the blocks that start later leave their documents to k_big_v1 untried
+// (the results are the same either way: only the wasted work goes).
 template <int OP, uint32_t SWMIN, uint32_t SWB>
-__global__ void __launch_bounds__(64) k_pw_small(GeneralJob j, uint8_t *done, uint64_t pw_min) {
+__global__ void __launch_bounds__(64) k_pw_small(GeneralJob j, uint8_t *done, uint64_t pw_min, uint32_t *tally) {
   __shared__ SwLds<SWB, OP == OP_DIFF> L;
   const uint32_t lane = threadIdx.x;
   for (uint32_t d = blockIdx.x; d < j.n; d += gridDim.x) {
     const uint32_t u0 = j.doc_upd[d];
     if (j.doc_upd[d + 1] - u0 != 1 || done[d]) continue;
+    {
+      const uint32_t dec = __builtin_nontemporal_load(tally);
+      const uint64_t acc = __builtin_nontemporal_load(j.pw_count);
+      if (dec > 256 && dec > 8 * acc) continue;
+    }
     const uint64_t ub = j.upd_off[u0];
     const uint64_t len64 = j.upd_off[u0 + 1] - ub;
     // (tiny updates: the lane-per-document kernel; from pw_min on: the chunk walk / k_pw_ms)
@@ -1394,7 +1409,7 @@ __global__ void __launch_bounds__(64) k_pw_small(GeneralJob j, uint8_t *done, ui
           __syncthreads();
         }
       }
-      if (why) PW_DECLINE()
+      if (why) SW_DECLINE_R(why ? why : 2)
     }
     __syncthreads();
     // the tables: the branch-free short cut at every offset (most offsets start no struct, and the full
@@ -1410,7 +1425,7 @@ __global__ void __launch_bounds__(64) k_pw_small(GeneralJob j, uint8_t *done, ui
     uint32_t o = 0;
     const uint32_t nsec = sw_vu(L.b, o, len, bad);
     uint32_t p = o, npatch = 0, prev = 0;
-    if (bad || nsec > SW_NSEC) PW_DECLINE_R(2)
+    if (bad || nsec > SW_NSEC) SW_DECLINE_R(2)
     uint32_t npre = 0;  // sliced heads in the pool (diff)
     for (uint32_t ci = 0; ci < nsec && !why; ci++) {
       uint32_t q = p;
@@ -1517,7 +1532,7 @@ __global__ void __launch_bounds__(64) k_pw_small(GeneralJob j, uint8_t *done, ui
         }
       }
     }
-    if (why) PW_DECLINE()
+    if (why) SW_DECLINE_R(why ? why : 2)
     const uint32_t ds0 = p;
     uint32_t ds1 = 0;
     if (OP == OP_DIFF) {  // the delete set: readDeleteSet's varuints canonical, no empty and no repeated client
@@ -1549,7 +1564,7 @@ __global__ void __launch_bounds__(64) k_pw_small(GeneralJob j, uint8_t *done, ui
         if (bad) { why = 17; break; }
       }
       ds1 = q;
-      if (why) PW_DECLINE()
+      if (why) SW_DECLINE_R(why ? why : 2)
     }
     __syncthreads();
     // outputs
@@ -1692,7 +1707,7 @@ int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const ui
   uint32_t *cnt = (uint32_t *)(moff + n1), *cbase = cnt + n1;
   uint8_t *done = (uint8_t *)(cbase + n1);
   uint32_t *many = (uint32_t *)(((uintptr_t)(done + j.n) + 15) & ~(uintptr_t)15);
-  PWCHK(hipMemsetAsync(many, 0, 4, st));
+  PWCHK(hipMemsetAsync(many, 0, 12, st));  // (many[1..2]: k_pw_small's tally of declines / completions)
   k_pw_prep<<<(n1 + 255) / 256, 256, 0, st>>>(j, cnt, done, pw_min, msz, ms_min, many);
   size_t tmp = 0, tmp2 = 0;
   hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cnt, cbase, n1, st);
@@ -1749,9 +1764,10 @@ int pw_small_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t
   uint64_t pw_min = PW_MIN;
   if (const char *e = getenv("YMERGE_PW_MIN")) pw_min = strtoull(e, nullptr, 10);
   const uint32_t gs = j.n < 65536 ? j.n : 65536;
-#define PW_SMALL(O)                                                  \
-  k_pw_small<O, SW_MIN, 2048><<<gs, 64, 0, st>>>(j, done, pw_min); \
-  k_pw_small<O, 2048, 4096><<<gs, 64, 0, st>>>(j, done, pw_min);
+  uint32_t *tally = (uint32_t *)(((uintptr_t)(done + j.n) + 15) & ~(uintptr_t)15) + 1;  // (pw_run's `many` + 1)
+#define PW_SMALL(O)                                                          \
+  k_pw_small<O, SW_MIN, 2048><<<gs, 64, 0, st>>>(j, done, pw_min, tally); \
+  k_pw_small<O, 2048, 4096><<<gs, 64, 0, st>>>(j, done, pw_min, tally);
   if (op == OP_DIFF) { PW_SMALL(OP_DIFF) }
   else if (op == OP_SV) { PW_SMALL(OP_SV) }
   else { PW_SMALL(OP_META) }

@@ -140,8 +140,9 @@ def pack_docs(docs):
 def _torch_first():
     """torch's wheel bundles its own HIP runtime.  When libymerge.so's runtime initialises the device first,
     torch's first CUDA call in the same process reports "No HIP GPUs are available"; in the other order both
-    work.  So the engine lets torch initialise first whenever torch is importable (it is the plumbing for
-    device tensors, the multi-GPU launcher and the benchmark)."""
+    work.  So by default the engine lets torch initialise first when torch is importable (it is the plumbing
+    for device tensors, the multi-GPU launcher and the benchmark).  A failure there is a warning, not an
+    error: the library may still see the device (host batches need no torch)."""
     try:
         import torch
     except ImportError:
@@ -150,14 +151,19 @@ def _torch_first():
         if torch.cuda.is_available():
             torch.cuda.init()
     except RuntimeError as e:  # torch cannot see a device the HIP runtime may still see: say which
-        raise RuntimeError(f"torch could not initialise the GPU before libymerge.so ({e})") from e
+        import warnings
+        warnings.warn(f"torch could not initialise the GPU before libymerge.so ({e}); device tensors of this "
+                      "process may not work", RuntimeWarning)
 
 
 class Engine:
-    """One engine per process/GPU (the library keeps one HIP stream and workspace per thread)."""
+    """One engine per process/GPU (the library keeps one HIP stream and workspace per thread).
+    torch_first=False skips importing and initialising torch (host batches only: run_host and the batch
+    functions; torch used later in the same process would then not see the GPU)."""
 
-    def __init__(self, device=0, path=None):
-        _torch_first()
+    def __init__(self, device=0, path=None, torch_first=True):
+        if torch_first:
+            _torch_first()
         self.lib = load_library(path)
         rc = self.lib.ym_init(device)
         if rc != 0:
