@@ -69,6 +69,11 @@ enum { YM_OUT_V1 = 0x1000, YM_OUT_V2 = 0x2000 };
 /* ym_compact only, or-ed into ym_batch.format: the document is new Y.Doc({ gc: false }) (deleted content
  * is kept and written; Doc.js:40-43, Transaction.js:302-304) */
 enum { YM_NO_GC = 0x4000 };
+/* ym_compact only, or-ed into ym_batch.format: each output is the compacted Doc's encodeStateVector(doc)
+ * (reference src/utils/encoding.js:572-611; clients in StructStore insertion order, StructStore.js:49-56 --
+ * the SyncStep1 a server that keeps Docs sends) immediately followed by the update; the state vector is
+ * self-delimiting (vu(n) then n (client, clock) varuint pairs) */
+enum { YM_SV_FIRST = 0x10000 };
 
 typedef struct ym_batch {
   const uint8_t *arena;    /* concatenated update bytes                                   */

@@ -112,18 +112,29 @@ function convertUpdateFormatBatch (updates, opts, throwErrors = false, async = f
 // Doc round-trip compaction (ym_compact): per document, encodeStateAsUpdate[V2] of a fresh Doc after
 // applyUpdate[V2] of every update in order -- the reference's own compaction (structs merged, deleted
 // content garbage-collected).  opts.gc === false: new Y.Doc({ gc: false }) (YM_NO_GC);
-// opts.targetStateVectors: one encoded state vector per document, encodeStateAsUpdate[V2](doc, sv)
+// opts.targetStateVectors: one encoded state vector per document, encodeStateAsUpdate[V2](doc, sv);
+// opts.withStateVector: per document { stateVector: encodeStateVector(doc), update } (YM_SV_FIRST: the Doc's
+// own state vector, clients in StructStore insertion order -- what a server keeping Docs sends as SyncStep1)
 const YM_NO_GC = 0x4000
+const YM_SV_FIRST = 0x10000
+function splitStateVector (b) {
+  let pos = 0
+  const vu = () => { let v = 0; let m = 1; let x; do { x = b[pos++]; v += (x & 127) * m; m *= 128 } while (x & 128); return v }
+  const n = vu()
+  for (let i = 0; i < 2 * n; i++) vu()
+  return { stateVector: b.subarray(0, pos), update: b.subarray(pos) }
+}
 function compactUpdatesBatch (docs, opts, throwErrors = false, async = false) {
   const p = pack(docs)
-  const fmt = fmtOf(opts) | (opts && opts.gc === false ? YM_NO_GC : 0)
+  const withSv = !!(opts && opts.withStateVector)
+  const fmt = fmtOf(opts) | (opts && opts.gc === false ? YM_NO_GC : 0) | (withSv ? YM_SV_FIRST : 0)
   const args = [OP.compact, fmt, p.arena, p.updOff, p.docUpd]
   if (opts && opts.targetStateVectors) {
     if (opts.targetStateVectors.length !== docs.length) throw new RangeError('one target state vector per document')
     const s = pack(opts.targetStateVectors.map(x => [x]))
     args.push(s.arena, s.updOff)
   }
-  return call(async, args, r => unpack(r, throwErrors))
+  return call(async, args, r => unpack(r, throwErrors).map(x => withSv && x instanceof Uint8Array ? splitStateVector(x) : x))
 }
 const compactUpdates = (updates, sv) => compactUpdatesBatch([updates], { format: 1, targetStateVectors: sv ? [sv] : null }, true)[0]
 const compactUpdatesV2 = (updates, sv) => compactUpdatesBatch([updates], { format: 2, targetStateVectors: sv ? [sv] : null }, true)[0]

@@ -74,6 +74,13 @@ let compactOk = 0
   for (const fmt of [1, 2]) {
     const nogc = JSON.parse(fs.readFileSync(path.join(dir, 'compact_nogc.json'))).cases.filter(c => c.inputs && c.fmt === fmt)
     Y.compactUpdatesBatch(nogc.map(c => c.inputs.map(b)), { format: fmt, gc: false }).forEach((r, i) => check(nogc[i].id, r, nogc[i]))
+    // opts.withStateVector: { stateVector: encodeStateVector(doc), update } per document
+    Y.compactUpdatesBatch(nogc.map(c => c.inputs.map(b)), { format: fmt, gc: false, withStateVector: true }).forEach((r, i) => {
+      const c = nogc[i]
+      if (r instanceof Error || c.error) { check(c.id + '/sv', r, c); return }
+      check(c.id + '/sv', r.update, c)
+      if (Buffer.compare(Buffer.from(r.stateVector), Buffer.from(c.sv, 'base64')) !== 0) bad.push([c.id, 'compact doc sv', r.stateVector.length])
+    })
     for (const c of JSON.parse(fs.readFileSync(path.join(dir, 'compact_sv.json'))).cases.filter(c => c.group === 'slice' && c.fmt === fmt)) {
       const ins = c.inputs.map(b)
       Y.compactUpdatesBatch(c.targets.map(() => ins), { format: fmt, gc: c.gc, targetStateVectors: c.targets.map(t => b(t.sv)) })

@@ -10,7 +10,7 @@
 // encodeStateAsUpdate writes only the integrated store, encoding.js:490-493).  Output:
 // tests/golden/compact.json {cases: [{id, group, fmt, inputs (b64), expect (b64) | src {ymb, doc, drop?},
 // expect_sha256, expect_len | error {name, message}; pending [structRefs, stack, deleteReaders];
-// single_tx_same}]}.  A case whose applyUpdate / encodeStateAsUpdate throws records the exception's class
+// single_tx_same, sv (encodeStateVector(doc))}]}.  A case whose applyUpdate / encodeStateAsUpdate throws records the exception's class
 // and message instead of bytes.  single_tx_same records whether applying mergeUpdates(inputs) in one
 // transaction gives the same bytes.
 'use strict'
@@ -70,6 +70,8 @@ function loadYmb (name) {
       // workload documents name their bench_data source instead of repeating its bytes
       // (and, being large, carry the SHA-256 and length of the expected bytes)
       if (src) { r.expect_sha256 = require('crypto').createHash('sha256').update(out).digest('hex'); r.expect_len = out.length } else r.expect = b64(out)
+      // the Doc's own state vector (encoding.js:572-611: clients in StructStore insertion order)
+      r.sv = b64(Y.encodeStateVector(doc))
       r.single_tx_same = same
     } catch (e) {
       // the reference's exception (applyUpdate's transaction still runs its cleanup in `finally`)

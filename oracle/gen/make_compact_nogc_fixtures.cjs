@@ -57,6 +57,7 @@ function loadYmb (name) {
       if (p[0] + p[1] + p[2] !== 0) r.pending = p
       const out = (v2 ? Y.encodeStateAsUpdateV2 : Y.encodeStateAsUpdate)(doc)
       if (c.src) { r.expect_sha256 = crypto.createHash('sha256').update(out).digest('hex'); r.expect_len = out.length } else r.expect = b64(out)
+      r.sv = b64(Y.encodeStateVector(doc))  // the Doc's own state vector (encoding.js:572-611)
       // does gc: false change the bytes for this input? (a document without deletions is the same either way)
       r.differs_from_gc = c.error ? null : (c.expect !== undefined ? c.expect !== r.expect : c.expect_sha256 !== r.expect_sha256)
     } catch (e) {

@@ -47,7 +47,8 @@ def load(nogc=False):
             exp = base64.b64decode(c["expect"]) if "expect" in c else None
         out.append(dict(id=c["id"], group=c["group"], fmt=c["fmt"], inputs=ins, expect=exp,
                         sha=c.get("expect_sha256"), elen=c.get("expect_len"), error=c.get("error"),
-                        pending=c.get("pending"), differs=c.get("differs_from_gc")))
+                        pending=c.get("pending"), differs=c.get("differs_from_gc"),
+                        docsv=base64.b64decode(c["sv"]) if "sv" in c else None))
     return out
 
 
@@ -57,6 +58,17 @@ def matches(case, got):
     if case["expect"] is not None:
         return got == case["expect"]
     return len(got) == case["elen"] and hashlib.sha256(got).hexdigest() == case["sha"]
+
+
+def mismatch_sv_first(case, status, got):
+    """mismatch() of a YM_SV_FIRST output: the reference's encodeStateVector(doc), then its update bytes."""
+    if case["error"] or int(status) != 0 or got is None:
+        return mismatch(case, status, got)
+    from yjs_amd.engine import split_state_vector
+    sv, rest = split_state_vector(got)
+    if sv != case["docsv"]:
+        return "state vector differs"
+    return mismatch(case, status, rest)
 
 
 def mismatch(case, status, got, message=True):

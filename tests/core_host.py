@@ -24,6 +24,8 @@ def run(op, fmt, arena, upd_off, doc_upd, sv_arena=None, sv_off=None, san=False)
     upd_off = np.ascontiguousarray(upd_off, np.uint64)
     doc_upd = np.ascontiguousarray(doc_upd, np.uint32)
     nd = len(doc_upd) - 1
+    if op in ("compact_sv", "compact_nogc_sv"):  # YM_SV_FIRST: encodeStateVector(doc), then the update
+        op, fmt = op[:-3], fmt | 0x10000
     if op in ("compact", "compact_nogc") and sv_arena is not None:
         fmt |= 0x8000  # core_host.cpp: the batch carries target state vectors (ym_batch.sv_arena != NULL)
     if sv_arena is None:

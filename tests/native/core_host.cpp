@@ -66,7 +66,8 @@ int main(int argc, char **argv) {
         Ctx c = {0, arena.data()};
         cpt::Result R;
         memset(&R, 0, sizeof(R));
-        cpt::compact_doc(c, ws.data(), z, v2 | ((fmt & 0x4000) ? 2u : 0u), upd_off.data(), u0, k, tsv, tsvlen, R, nullptr);
+        const uint32_t cflags = v2 | ((fmt & 0x4000) ? 2u : 0u) | ((fmt & 0x10000) ? 4u : 0u);
+        cpt::compact_doc(c, ws.data(), z, cflags, upd_off.data(), u0, k, tsv, tsvlen, R, nullptr);
         st = c.err;
         if (st) continue;
         if (getenv("YM_CPT_STATS")) {  // workspace use (sizing experiments): used / reserved per region
@@ -79,7 +80,7 @@ int main(int argc, char **argv) {
         }
         out.assign(R.total + 1, 0);
         Ctx c2 = {0, arena.data()};
-        cpt::compact_doc(c2, ws.data(), z, v2 | ((fmt & 0x4000) ? 2u : 0u), upd_off.data(), u0, k, tsv, tsvlen, R, out.data());
+        cpt::compact_doc(c2, ws.data(), z, cflags, upd_off.data(), u0, k, tsv, tsvlen, R, out.data());
         st = c2.err ? (c2.err == ST_RETRY ? ST_UNEXPECTED : c2.err) : 0;
         out.resize(R.total);
       }

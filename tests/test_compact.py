@@ -121,3 +121,22 @@ def test_device_core_compact_target_sv_host_build(san):
             outs, st = core_host.run("compact" if gc else "compact_nogc", fmt, a, o, d, sa, so, san=san)
             bad = [(c["id"], why) for c, out, s in zip(cs, outs, st) if (why := compact_cases.mismatch(c, s, out))]
             assert not bad, f"fmt {fmt} gc {gc}: {len(bad)}/{len(cs)} differ: {bad[:8]}"
+
+
+@pytest.mark.parametrize("san", [False, True], ids=["opt", "asan_ubsan"])
+def test_device_core_compact_doc_state_vector_host_build(san):
+    """YM_SV_FIRST: encodeStateVector(doc) of the compacted Doc (clients in StructStore insertion order, not the
+    descending order of the update) then the update, against the reference's own bytes (the `sv` of
+    compact.json / compact_nogc.json), through the host build of the device core."""
+    import core_host
+    from yjs_amd import pack_docs
+    for nogc in (False, True):
+        for fmt in (1, 2):
+            cs = [c for c in compact_cases.load(nogc=nogc) if c["fmt"] == fmt and c["expect"] is not None or
+                  (c["fmt"] == fmt and c["error"])]
+            if san:
+                cs = cs[::4]
+            a, o, d = pack_docs([c["inputs"] for c in cs])
+            outs, st = core_host.run("compact_nogc_sv" if nogc else "compact_sv", fmt, a, o, d, san=san)
+            bad = [(c["id"], w) for c, s_, g in zip(cs, st, outs) if (w := compact_cases.mismatch_sv_first(c, s_, g))]
+            assert not bad, f"{len(bad)}/{len(cs)}: {bad[:5]}"

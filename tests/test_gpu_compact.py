@@ -143,3 +143,21 @@ def test_compact_workspace_budget_chunks(engine, monkeypatch):
     assert int(st[1]) == 9 and int(st[0]) == 0 and int(st[2]) == 0  # YM_ERR_CAPACITY
     assert oa[int(oo[0]):int(oo[0]) + int(ol[0])].tobytes() == want[0]
     assert oa[int(oo[2]):int(oo[2]) + int(ol[2])].tobytes() == want[1]
+
+
+@pytest.mark.parametrize("gc", [True, False], ids=["gc", "nogc"])
+@pytest.mark.parametrize("fmt", [1, 2])
+def test_compact_doc_state_vector_on_gpu(engine, fmt, gc):
+    """YM_SV_FIRST on the GPU: the compacted Doc's encodeStateVector (StructStore insertion order) before the
+    update, against the reference's bytes for every fixture of compact.json / compact_nogc.json."""
+    from yjs_amd import pack_docs
+    cs = [c for c in compact_cases.load(nogc=not gc) if c["fmt"] == fmt and c["group"] not in ("gap_c5", "wl_c5")]
+    a, o, d = pack_docs([c["inputs"] for c in cs])
+    oa, oo, ol, st = engine.run_host("compact_sv" if gc else "compact_nogc_sv", fmt, a, o, d)
+    bad = []
+    for i, c in enumerate(cs):
+        got = oa[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() if st[i] == 0 else None
+        why = compact_cases.mismatch_sv_first(c, st[i], got)
+        if why:
+            bad.append((c["id"], why))
+    assert not bad, f"{len(bad)}/{len(cs)} differ: {bad[:8]}"

@@ -554,6 +554,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   j.v2 = (b->format & 0xff) == YM_V2;
   j.dsref = op == OP_DSMERGE && (b->format & YM_DS_REF) != 0;
   j.nogc = op == OP_COMPACT && (b->format & YM_NO_GC) != 0;
+  j.svfirst = op == OP_COMPACT && (b->format & YM_SV_FIRST) != 0;
   // ym_snapshot: the output encoding (YM_OUT_V1 / YM_OUT_V2; default: the input's)
   j.v2out = op == OP_SNAP && ((b->format & YM_OUT_V2) != 0 || (j.v2 && (b->format & YM_OUT_V1) == 0));
   j.layout = S->layout.as<ym::Layout>();

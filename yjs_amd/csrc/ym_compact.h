@@ -1701,8 +1701,22 @@ YM_INL WsSize ws_size(uint32_t k, uint64_t bytes, uint32_t mul) {
 // Applies the k updates of a document (offsets upd_off[u0 .. u0 + k]) to a fresh Doc and sizes / writes
 // its encodeStateAsUpdate[V2].  out == nullptr: sizing only (L.total); else the bytes are written there.
 // The engine state stays in the workspace between the two calls of one document (pass 2 only writes).
-struct Result { uint64_t col[C_N]; uint64_t rest, total; };
-// flags: bit 0 V2, bit 1 Doc({ gc: false }).  svp / svlen: the encoded target state vector of
+struct Result { uint64_t col[C_N]; uint64_t rest, total, sv; };
+// encodeStateVector(doc) (encoding.js:572-611: writeStateVector over getStateVector, StructStore.js:49-56):
+// vu(#clients) | (client, state)* with the clients in StructStore insertion order (d.cl: add_struct appends),
+// state = the last struct's clock + length; the same bytes through DSEncoderV1 and DSEncoderV2
+YM_INL uint64_t doc_sv(const Doc &d, uint8_t *out) {
+  Out o = {out, 0};  // out == nullptr: size only
+  ovu(o, (int64_t)d.cl.n);
+  for (uint32_t ci = 0; ci < d.cl.n; ci++) {
+    const Cl &s = d.cl.p[ci];
+    const Item &l = d.it[s.a.p[s.a.n - 1]];
+    ovu(o, s.client);
+    ovu(o, l.clock + l.len);
+  }
+  return o.n;
+}
+// flags: bit 0 V2, bit 1 Doc({ gc: false }), bit 2 the Doc's encodeStateVector written first (YM_SV_FIRST).  svp / svlen: the encoded target state vector of
 // encodeStateAsUpdate[V2](doc, sv) (svp == nullptr: none, every struct is written)
 YM_BIG void compact_doc(Ctx &c, uint8_t *ws, const WsSize &z, uint32_t flags, const uint64_t *upd_off, uint32_t u0, uint32_t k,
                         const uint8_t *svp, uint64_t svlen, Result &R, uint8_t *out) {
@@ -1801,7 +1815,13 @@ YM_BIG void compact_doc(Ctx &c, uint8_t *ws, const WsSize &z, uint32_t flags, co
       h += vu_size(sc) + sc;
     }
     R.total = h + R.rest;
+    R.sv = (flags & 4) ? doc_sv(d, nullptr) : 0;
+    R.total += R.sv;
     return;
+  }
+  if (R.sv) {  // encodeStateVector(doc), then the update after it
+    doc_sv(d, out);
+    out += R.sv;
   }
   // writing: every stream at its final place (UpdateEncoderV2.toUint8Array layout, ym_core.h Layout)
   Out hdr = {out, 0};

@@ -47,7 +47,8 @@ __global__ void __launch_bounds__(64, OCC) k_compact(GeneralJob j, uint32_t lane
   // ym_compact with sv_arena: doc d's target state vector (encodeStateAsUpdate(doc, sv))
   const uint8_t *svp = j.sv ? j.sv + j.sv_off[d] : nullptr;
   const uint64_t svlen = j.sv ? j.sv_off[d + 1] - j.sv_off[d] : 0;
-  cpt::compact_doc(c, ws, z, j.v2 | (j.nogc << 1), j.upd_off, u0, k, svp, svlen, R, nullptr);
+  const uint32_t flags = j.v2 | (j.nogc << 1) | (j.svfirst << 2);
+  cpt::compact_doc(c, ws, z, flags, j.upd_off, u0, k, svp, svlen, R, nullptr);
   if (c.err) {
     j.status[d] = c.err;
     j.out_len[d] = 0;
@@ -61,7 +62,7 @@ __global__ void __launch_bounds__(64, OCC) k_compact(GeneralJob j, uint32_t lane
     return;
   }
   Ctx c2 = {0, j.A};
-  cpt::compact_doc(c2, ws, z, j.v2 | (j.nogc << 1), j.upd_off, u0, k, svp, svlen, R, j.out + off);
+  cpt::compact_doc(c2, ws, z, flags, j.upd_off, u0, k, svp, svlen, R, j.out + off);
   j.status[d] = c2.err ? (c2.err == ST_RETRY ? ST_UNEXPECTED : c2.err) : ST_OK;
   j.out_off[d] = off;
   j.out_len[d] = c2.err ? 0 : R.total;

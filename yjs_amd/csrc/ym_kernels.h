@@ -33,6 +33,7 @@ struct GeneralJob {
   uint32_t dsref;            // ym_ds_merge: the reference's adjacency-only coalescing (YM_DS_REF)
   uint32_t v2out;            // ym_snapshot: V2 output encoding
   uint32_t nogc;             // ym_compact: Doc({ gc: false }) (YM_NO_GC)
+  uint32_t svfirst;          // ym_compact: the Doc's encodeStateVector before the update (YM_SV_FIRST)
   uint32_t parts_mul;        // part-table capacity multiplier (grown on ST_RETRY)
   uint8_t *ws;               // workspace
   const uint64_t *ws_off;    // per listed slot

@@ -47,6 +47,7 @@ YM_DS_REF = 0x100  # ym_ds_merge: the reference's adjacency-only coalescing (inc
 YM_OFF32 = 0x200   # upd_off holds uint32_t offsets (include/ymerge.h)
 YM_OUT_V1, YM_OUT_V2 = 0x1000, 0x2000  # ym_snapshot: output encoding
 YM_NO_GC = 0x4000  # ym_compact: new Y.Doc({ gc: false })
+YM_SV_FIRST = 0x10000  # ym_compact: the Doc's encodeStateVector, then the update
 
 
 def _off_flag(upd_off):
@@ -176,11 +177,12 @@ class Engine:
         return {"merge": L.ym_merge, "diff": L.ym_diff, "sv": L.ym_sv, "conv": L.ym_convert, "meta": L.ym_meta,
                 "dsmerge": L.ym_ds_merge, "dsmerge_ref": L.ym_ds_merge,
                 "snap_to_v1": L.ym_snapshot, "snap_to_v2": L.ym_snapshot, "compact": L.ym_compact,
-                "compact_nogc": L.ym_compact}[op]
+                "compact_nogc": L.ym_compact, "compact_sv": L.ym_compact, "compact_nogc_sv": L.ym_compact}[op]
 
     @staticmethod
     def _format(op, fmt):
-        extra = {"dsmerge_ref": YM_DS_REF, "snap_to_v1": YM_OUT_V1, "snap_to_v2": YM_OUT_V2, "compact_nogc": YM_NO_GC}
+        extra = {"dsmerge_ref": YM_DS_REF, "snap_to_v1": YM_OUT_V1, "snap_to_v2": YM_OUT_V2, "compact_nogc": YM_NO_GC,
+                 "compact_sv": YM_SV_FIRST, "compact_nogc_sv": YM_NO_GC | YM_SV_FIRST}
         return fmt | extra.get(op, 0)
 
     # ---- host-memory batches ------------------------------------------------------------------
@@ -346,19 +348,31 @@ def encodeStateVectorFromUpdateBatch(updates, fmt=1, raise_errors=False):
     return _unpack(*_engine().run_host("sv", fmt, arena, upd_off, doc_upd), raise_errors)
 
 
-def compactUpdatesBatch(docs, fmt=1, raise_errors=False, gc=True, target_state_vectors=None):
+def split_state_vector(buf):
+    """(encoded state vector, rest) of a YM_SV_FIRST output: the vector is vu(n) then n varuint pairs."""
+    pos = 0
+    n, pos = _read_vu(buf, pos)
+    for _ in range(2 * n):
+        _, pos = _read_vu(buf, pos)
+    return bytes(buf[:pos]), bytes(buf[pos:])
+
+
+def compactUpdatesBatch(docs, fmt=1, raise_errors=False, gc=True, target_state_vectors=None, with_state_vector=False):
     """Doc round-trip compaction (ym_compact) over a batch: per document, encodeStateAsUpdate[V2] of a fresh
     Doc({ gc }) after applyUpdate[V2] of every update in order (the reference's own compaction:
     src/utils/encoding.js readUpdate / encodeStateAsUpdate, Transaction.js cleanupTransactions).
     target_state_vectors: one encoded state vector per document -- encodeStateAsUpdate[V2](doc, sv), only
-    what the target is missing (encoding.js:94-116; the sync protocol's step-2 answer)."""
+    what the target is missing (encoding.js:94-116; the sync protocol's step-2 answer).
+    with_state_vector: per document (encodeStateVector(doc), update) instead -- the Doc's own state vector,
+    clients in StructStore insertion order (encoding.js:572-611, StructStore.js:49-56; YM_SV_FIRST)."""
     arena, upd_off, doc_upd = pack_docs(docs)
     sva = svo = None
     if target_state_vectors is not None:
         assert len(target_state_vectors) == len(docs)
         sva, svo, _ = pack_docs([[s] for s in target_state_vectors])
-    return _unpack(*_engine().run_host("compact" if gc else "compact_nogc", fmt, arena, upd_off, doc_upd, sva, svo),
-                   raise_errors)
+    op = ("compact" if gc else "compact_nogc") + ("_sv" if with_state_vector else "")
+    res = _unpack(*_engine().run_host(op, fmt, arena, upd_off, doc_upd, sva, svo), raise_errors)
+    return [split_state_vector(r) if with_state_vector and isinstance(r, bytes) else r for r in res]
 
 
 def compactUpdates(updates, target_state_vector=None):
