@@ -770,6 +770,7 @@ static void release_state(DevState *S) {
   for (PwBufs *pb : {&S->pw, &S->pw2}) {
     for (int k = 0; k < PW_NBUF; k++) if (pb->p[k]) hipFree(pb->p[k]);
     if (pb->pinned) hipHostFree(pb->pinned);
+    if (pb->ev) hipEventDestroy(pb->ev);
   }
   if (S->stream) hipStreamDestroy(S->stream);
   delete S;

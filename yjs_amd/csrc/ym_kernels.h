@@ -82,10 +82,18 @@ struct PwBufs {
   void *p[PW_NBUF] = {};
   size_t cap[PW_NBUF] = {};
   uint32_t *pinned = nullptr;
+  uint32_t *pinned_dev = nullptr;  // (its device address: a kernel writes the totals there, no copy op)
+  hipEvent_t ev = nullptr;   // pw_prepare's totals have reached `pinned`
+  bool pending = false;      // pw_prepare ran, pw_finish not yet
+  uint32_t op = 0;
 };
-// Chunk-parallel walk + stitch over the large single-update documents of a V1 diff / sv call; sets
-// *done (per document: 1 = completed).  Returns 1 when launched, 0 when not applicable, < 0 on error.
-int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const uint8_t **done);
+// Chunk-parallel walk + stitch over the large single-update documents of a V1 diff / sv call, in two steps:
+// pw_prepare marks every document not done (*done) and sends the large documents' chunk / table totals to
+// the host without waiting for them; the kernels of the small documents are enqueued next (their work hides
+// that round trip); pw_finish then waits for the totals, sizes the record buffers and launches the walk and
+// stitch (documents completed get done[d] = 1).  Return 1 when launched, 0 when not applicable, < 0 on error.
+int pw_prepare(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const uint8_t **done);
+int pw_finish(const GeneralJob &j, hipStream_t st, PwBufs &B);
 // Small single updates of a V1 diff / sv / meta call, one document per lane (ym_small.hip); marks done[d].
 int small_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t st);
 // ... and what those left of 80 B - 4 KB: one wave per document (ym_pwalk.hip k_pw_small).

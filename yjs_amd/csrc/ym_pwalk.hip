@@ -152,6 +152,14 @@ __global__ void k_pw_prep(GeneralJob j, uint32_t *cnt, uint8_t *done, uint64_t p
   }
   cnt[d] = c;  // cnt[n] = 0: the exclusive scan's last entry is the total
   msz[d] = a;
+  // the totals the host sizes the record buffers by (only large documents add: no contention otherwise)
+  if (c) atomicAdd(many + 2, c);
+  if (a) atomicAdd((unsigned long long *)(many + 4), (unsigned long long)a);
+}
+
+// the prep's totals (six words) straight into the coherent pinned host words pw_finish reads
+__global__ void k_pw_totals(const uint32_t *many, uint32_t *host) {
+  if (threadIdx.x < 6) host[threadIdx.x] = many[threadIdx.x];
 }
 
 // ---- 1. speculative chunk walk ----------------------------------------------------------------------
@@ -1687,44 +1695,68 @@ int pw_ensure(PwBufs &B, int k, size_t n) {
 }
 }  // namespace
 
-// Runs the chunk-parallel walk + stitch over the large single-update documents of a V1 diff / sv call.
-// Documents it completes are marked in `*done_out` (k_big_v1 skips them).  Returns 1 when launched, 0
-// when not applicable (no large document, or the record buffer could not be allocated), < 0 on error.
+// The chunk-parallel walk + stitch over the large single-update documents of a V1 diff / sv call (ym_kernels.h
+// pw_prepare / pw_finish).  Documents it completes are marked in `*done_out` (k_big_v1 skips them).
 const uint8_t *pw_last_done = nullptr;
-int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const uint8_t **done_out) {
+namespace {
+// the prep kernel's outputs after `done`: many[0] (a chunk-walked document of > 64 sections), many[1]
+// (k_pw_small's tally), many[2] (chunks in all), many[4..5] (u64: bytes of the table-walked documents' areas)
+uint32_t *pw_many(const GeneralJob &j, uint8_t *done) { return (uint32_t *)(((uintptr_t)(done + j.n) + 15) & ~(uintptr_t)15); }
+}  // namespace
+int pw_prepare(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const uint8_t **done_out) {
   using namespace pw;
   *done_out = nullptr;
+  B.pending = false;
   if (j.v2 || (op != OP_DIFF && op != OP_SV && op != OP_META) || j.n == 0 || !j.pw_count || getenv("YMERGE_NO_PW")) return 0;
   // YMERGE_PW_MIN: smallest update taken (tests push small golden cases through this path)
   uint64_t pw_min = PW_MIN;
   if (const char *e = getenv("YMERGE_PW_MIN")) pw_min = strtoull(e, nullptr, 10);
-  if (!B.pinned && hipHostMalloc((void **)&B.pinned, 64, hipHostMallocDefault) != hipSuccess) return -2;
+  if (!B.pinned_dev) {
+    if (B.pinned) hipHostFree(B.pinned);
+    B.pinned = nullptr;
+    if (hipHostMalloc((void **)&B.pinned, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return -2;
+    if (hipHostGetDevicePointer((void **)&B.pinned_dev, B.pinned, 0) != hipSuccess) return -2;
+  }
+  if (!B.ev && hipEventCreateWithFlags(&B.ev, hipEventDisableTiming) != hipSuccess) return -2;
   uint32_t ms_min = MS_MIN;
   if (const char *e = getenv("YMERGE_PWMS_MIN")) ms_min = (uint32_t)strtoul(e, nullptr, 10);
   const uint32_t n1 = j.n + 1;
-  if (pw_ensure(B, 0, 24ull * n1 + 32 + j.n)) return -2;
-  uint64_t *msz = (uint64_t *)B.p[0], *moff = msz + n1;
-  uint32_t *cnt = (uint32_t *)(moff + n1), *cbase = cnt + n1;
-  uint8_t *done = (uint8_t *)(cbase + n1);
-  uint32_t *many = (uint32_t *)(((uintptr_t)(done + j.n) + 15) & ~(uintptr_t)15);
-  PWCHK(hipMemsetAsync(many, 0, 12, st));  // (many[1..2]: k_pw_small's tally of declines / completions)
+  if (pw_ensure(B, 0, 24ull * n1 + 64 + j.n)) return -2;
+  uint64_t *msz = (uint64_t *)B.p[0];
+  uint32_t *cnt = (uint32_t *)(msz + 2 * n1);
+  uint8_t *done = (uint8_t *)(cnt + 2 * n1);
+  uint32_t *many = pw_many(j, done);
+  PWCHK(hipMemsetAsync(many, 0, 24, st));
   k_pw_prep<<<(n1 + 255) / 256, 256, 0, st>>>(j, cnt, done, pw_min, msz, ms_min, many);
-  size_t tmp = 0, tmp2 = 0;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cnt, cbase, n1, st);
-  hipcub::DeviceScan::ExclusiveSum(nullptr, tmp2, msz, moff, n1, st);
-  if (tmp2 > tmp) tmp = tmp2;
-  if (pw_ensure(B, 1, tmp + 16)) return -2;
-  PWCHK(hipcub::DeviceScan::ExclusiveSum(B.p[1], tmp, cnt, cbase, n1, st));
-  PWCHK(hipcub::DeviceScan::ExclusiveSum(B.p[1], tmp, msz, moff, n1, st));
-  PWCHK(hipMemcpyAsync(B.pinned, cbase + j.n, 4, hipMemcpyDeviceToHost, st));
-  PWCHK(hipMemcpyAsync(B.pinned + 2, moff + j.n, 8, hipMemcpyDeviceToHost, st));
-  PWCHK(hipMemcpyAsync(B.pinned + 4, many, 4, hipMemcpyDeviceToHost, st));
-  PWCHK(hipStreamSynchronize(st));
-  const bool dsl = B.pinned[4] != 0;
-  const uint32_t total = B.pinned[0];
-  const uint64_t mtotal = *(uint64_t *)(B.pinned + 2);
+  k_pw_totals<<<1, 64, 0, st>>>(many, B.pinned_dev);  // (a copy op would hold the stream ~25 us)
+  PWCHK(hipEventRecord(B.ev, st));
   *done_out = done;  // every document is marked (0 = not taken) from here on
   pw_last_done = done;
+  B.pending = true;
+  B.op = op;
+  return 1;
+}
+int pw_finish(const GeneralJob &j, hipStream_t st, PwBufs &B) {
+  using namespace pw;
+  if (!B.pending) return 0;
+  B.pending = false;
+  const uint32_t op = B.op, n1 = j.n + 1;
+  uint64_t *msz = (uint64_t *)B.p[0], *moff = msz + n1;
+  uint32_t *cnt = (uint32_t *)(msz + 2 * n1), *cbase = cnt + n1;
+  uint8_t *done = (uint8_t *)(cnt + 2 * n1);
+  PWCHK(hipEventSynchronize(B.ev));  // (the small documents' kernels keep the device busy meanwhile)
+  const bool dsl = B.pinned[0] != 0;
+  const uint32_t total = B.pinned[2];
+  uint64_t mtotal;
+  __builtin_memcpy(&mtotal, B.pinned + 4, 8);
+  if (total == 0 && mtotal == 0) return 1;
+  size_t tmp = 0, tmp2 = 0;
+  if (total) hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cnt, cbase, n1, st);
+  if (mtotal) hipcub::DeviceScan::ExclusiveSum(nullptr, tmp2, msz, moff, n1, st);
+  if (tmp2 > tmp) tmp = tmp2;
+  if (pw_ensure(B, 1, tmp + 16)) return -2;
+  if (total) PWCHK(hipcub::DeviceScan::ExclusiveSum(B.p[1], tmp, cnt, cbase, n1, st));
+  if (mtotal) PWCHK(hipcub::DeviceScan::ExclusiveSum(B.p[1], tmp, msz, moff, n1, st));
   const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
   // many-section documents: the table walk (no chunk records)
   if (mtotal > 0) {
@@ -1755,7 +1787,7 @@ int pw_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const ui
 }  // namespace ymk
 
 // Small single updates of a V1 diff / sv / meta call that the lane-per-document kernels (ym_small.hip) left:
-// one wave per document (k_pw_small; YMERGE_NO_PWSMALL: off).  After pw_run (done marked), before k_big_v1.
+// one wave per document (k_pw_small; YMERGE_NO_PWSMALL: off).  After pw_prepare (done marked), before pw_finish.
 namespace ymk {
 int pw_small_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t st) {
   using namespace pw;
@@ -1764,7 +1796,7 @@ int pw_small_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t
   uint64_t pw_min = PW_MIN;
   if (const char *e = getenv("YMERGE_PW_MIN")) pw_min = strtoull(e, nullptr, 10);
   const uint32_t gs = j.n < 65536 ? j.n : 65536;
-  uint32_t *tally = (uint32_t *)(((uintptr_t)(done + j.n) + 15) & ~(uintptr_t)15) + 1;  // (pw_run's `many` + 1)
+  uint32_t *tally = (uint32_t *)(((uintptr_t)(done + j.n) + 15) & ~(uintptr_t)15) + 1;  // (pw_prepare's `many` + 1)
 #define PW_SMALL(O)                                                          \
   k_pw_small<O, SW_MIN, 2048><<<gs, 64, 0, st>>>(j, done, pw_min, tally); \
   k_pw_small<O, 2048, 4096><<<gs, 64, 0, st>>>(j, done, pw_min, tally);
