@@ -5,7 +5,7 @@
 // path (ym_general.hip) with an HBM workspace sized by an exclusive scan; (3) outputs are bump-
 // allocated in the caller's arena.  Host-memory batches are staged through device buffers.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include "ym_scan.h"
 
 #include <atomic>
 #include <mutex>
@@ -301,11 +301,9 @@ int select_docs(DevState *S, hipStream_t st, const uint32_t *list, uint32_t n, c
   k_status_flags<<<(n + 255) / 256, 256, 0, st>>>(list, n, status, want, S->flags.as<uint8_t>());
   uint32_t *d_num = S->counters.as<uint32_t>() + 8;
   size_t tmp = 0;
-  if (list) hipcub::DeviceSelect::Flagged(nullptr, tmp, list, S->flags.as<uint8_t>(), dst, d_num, n, st);
-  else hipcub::DeviceSelect::Flagged(nullptr, tmp, hipcub::CountingInputIterator<uint32_t>(0), S->flags.as<uint8_t>(), dst, d_num, n, st);
+  select_flagged(nullptr, tmp, list, S->flags.as<uint8_t>(), dst, d_num, n, st);
   if (S->scan_tmp.ensure(tmp + 16)) return -1;
-  if (list) hipcub::DeviceSelect::Flagged(S->scan_tmp.p, tmp, list, S->flags.as<uint8_t>(), dst, d_num, n, st);
-  else hipcub::DeviceSelect::Flagged(S->scan_tmp.p, tmp, hipcub::CountingInputIterator<uint32_t>(0), S->flags.as<uint8_t>(), dst, d_num, n, st);
+  if (select_flagged(S->scan_tmp.p, tmp, list, S->flags.as<uint8_t>(), dst, d_num, n, st)) return -1;
   HIPCHK(hipMemcpyAsync(S->pinned, d_num, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   *count_out = (uint32_t)(S->pinned[0] & 0xffffffffu);
@@ -351,9 +349,9 @@ int run_compact(DevState *S, hipStream_t st, GeneralJob j, uint32_t *list, uint3
     j.n = n;
     k_compact_ws<<<(n + 255) / 256, 256, 0, st>>>(j, S->ws_size.as<uint64_t>());
     size_t tmp = 0;
-    hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, S->ws_size.as<uint64_t>(), S->ws_off.as<uint64_t>(), n, st);
+    scan_excl<uint64_t>(nullptr, tmp, S->ws_size.as<uint64_t>(), S->ws_off.as<uint64_t>(), n, st);
     if (S->scan_tmp.ensure(tmp + 16)) return -1;
-    hipcub::DeviceScan::ExclusiveSum(S->scan_tmp.p, tmp, S->ws_size.as<uint64_t>(), S->ws_off.as<uint64_t>(), n, st);
+    if (scan_excl<uint64_t>(S->scan_tmp.p, tmp, S->ws_size.as<uint64_t>(), S->ws_off.as<uint64_t>(), n, st)) return -1;
     HIPCHK(hipMemcpyAsync(S->pinned, S->ws_off.as<uint64_t>() + (n - 1), 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(S->pinned + 1, S->ws_size.as<uint64_t>() + (n - 1), 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -438,9 +436,9 @@ int run_general(DevState *S, hipStream_t st, GeneralJob j, uint32_t *list, uint3
     if (S->ws_size.ensure((size_t)(n + 1) * 8) || S->ws_off.ensure((size_t)(n + 1) * 8)) return -1;
     k_general_ws<<<(n + 255) / 256, 256, 0, st>>>(j, S->ws_size.as<uint64_t>());
     size_t tmp = 0;
-    hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, S->ws_size.as<uint64_t>(), S->ws_off.as<uint64_t>(), n, st);
+    scan_excl<uint64_t>(nullptr, tmp, S->ws_size.as<uint64_t>(), S->ws_off.as<uint64_t>(), n, st);
     if (S->scan_tmp.ensure(tmp + 16)) return -1;
-    hipcub::DeviceScan::ExclusiveSum(S->scan_tmp.p, tmp, S->ws_size.as<uint64_t>(), S->ws_off.as<uint64_t>(), n, st);
+    if (scan_excl<uint64_t>(S->scan_tmp.p, tmp, S->ws_size.as<uint64_t>(), S->ws_off.as<uint64_t>(), n, st)) return -1;
     HIPCHK(hipMemcpyAsync(S->pinned, S->ws_off.as<uint64_t>() + (n - 1), 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(S->pinned + 1, S->ws_size.as<uint64_t>() + (n - 1), 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -715,9 +713,9 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
     if (S->cmp_off.ensure(nd * 8ull + 8) || S->cmp_len.ensure(nd * 8ull + 8) || S->cmp_arena.ensure(total + 16)) return -2;
     uint64_t *mlen = S->cmp_len.as<uint64_t>();
     k_mask_len<<<(nd + 255) / 256, 256, 0, st>>>(o_status, o_len, mlen, nd);
-    hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, mlen, (uint64_t *)nullptr, nd, st);
+    scan_excl<uint64_t>(nullptr, tmp, mlen, (uint64_t *)nullptr, nd, st);
     if (S->scan_tmp.ensure(tmp + 16)) return -2;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(S->scan_tmp.p, tmp, mlen, S->cmp_off.as<uint64_t>(), nd, st));
+    if (scan_excl<uint64_t>(S->scan_tmp.p, tmp, mlen, S->cmp_off.as<uint64_t>(), nd, st)) return -3;
     if (total) {
       const uint64_t chunks = (total + PACK_CHUNK - 1) / PACK_CHUNK;
       const uint32_t grid = chunks < 65536 ? (uint32_t)chunks : 65536;

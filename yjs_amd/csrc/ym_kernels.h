@@ -71,6 +71,7 @@ struct LargeBufs {
   void *p[4] = {nullptr, nullptr, nullptr, nullptr};
   size_t cap[4] = {0, 0, 0, 0};
   uint64_t *pinned = nullptr;
+  uint64_t *pinned_dev = nullptr;  // (its device address: k_lm_totals writes the record totals there)
 };
 // Large-document merge over `list` (n documents the fast path declined).  Documents it takes get
 // status OK; the rest keep ST_PENDING.  Returns 1 when launched, 0 when not applicable, < 0 on error.

@@ -11,7 +11,7 @@
 //   1. walk (count, then emit): one lane per update, 64 consecutive updates of a document staged
 //      into an LDS window per wave; struct records, client runs (the structs of one client inside one
 //      update: contiguous clocks) and delete ranges go to SoA arrays at offsets from exclusive scans
-//      of the per-update counts (hipcub::DeviceScan).
+//      of the per-update counts (ym_scan.h: the listed documents' updates only, counted on the device).
 //   2. segmented radix sorts (ym_segsort.hip, one workgroup per document): runs by
 //      (~client << 32 | clock), delete ranges by (client << 32 | clock); the ranges' values are their
 //      emission index = first-appearance order.
@@ -23,7 +23,9 @@
 //      start positions);  E  delete set: carried segmented running-max scan = union, groups ranked by
 //      their first appearance;  F  placement in the document's output slot;  G/H  writes.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <string.h>
+
+#include "ym_scan.h"
 
 #include "ym_fast_common.h"
 #include "ym_kernels.h"
@@ -92,6 +94,25 @@ __global__ void k_lm_prep(LMJob J, const uint32_t *list, uint32_t *kcnt, uint32_
   J.bad[i] = !ok;
   kcnt[i] = ok ? k : 0;
   ccnt[i] = ok ? (k + 63) / 64 : 0;
+}
+
+// the per-update count arrays zeroed over the listed documents' updates (tot[0] + 1 entries each)
+__global__ void k_lm_zero(LMJob J, const uint32_t *tot) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > tot[0] || i >= J.stride) return;
+  J.u_cnt[i] = 0;
+  J.u_cnt[J.stride + i] = 0;
+  J.u_cnt[2 * J.stride + i] = 0;
+}
+// the record totals (structs, runs, delete ranges) and the chunk total into the coherent pinned host words
+__global__ void k_lm_totals(LMJob J, const uint32_t *tot, uint32_t *host) {
+  if (threadIdx.x == 0) {
+    const uint32_t nu = tot[0];
+    host[0] = J.u_off[nu];
+    host[1] = J.u_off[J.stride + nu];
+    host[2] = J.u_off[2 * J.stride + nu];
+    host[3] = tot[1];
+  }
 }
 
 // ---- 1. walkers (one lane per update; LDS bytes at [p0, p1), arena offset of LDS byte 0 = gb) ------
@@ -1112,7 +1133,12 @@ int ensure(LargeBufs &B, int k, size_t n) {
 int large_run(const GeneralJob &j, const uint32_t *list, uint32_t nb, uint32_t n_upd, hipStream_t st, LargeBufs &B) {
   using namespace lm;
   if (j.op != OP_MERGE || nb == 0) return 0;
-  if (!B.pinned && hipHostMalloc((void **)&B.pinned, 64, hipHostMallocDefault) != hipSuccess) return -2;
+  if (!B.pinned_dev) {
+    if (B.pinned) hipHostFree(B.pinned);
+    B.pinned = nullptr;
+    if (hipHostMalloc((void **)&B.pinned, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return -2;
+    if (hipHostGetDevicePointer((void **)&B.pinned_dev, B.pinned, 0) != hipSuccess) return -2;
+  }
   LMJob J;
   memset(&J, 0, sizeof(J));
   J.A = j.A;
@@ -1141,10 +1167,9 @@ int large_run(const GeneralJob &j, const uint32_t *list, uint32_t nb, uint32_t n
   J.dinfo = carve<uint32_t>(p, (uint64_t)DI_N * nb);
   k_lm_prep<<<(nb + 256) / 256, 256, 0, st>>>(J, list, kcnt, ccnt);
   size_t tmp = 0, t2 = 0;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, kcnt, J.bu_off, n1, st);
+  scan_excl<uint32_t>(nullptr, tmp, kcnt, J.bu_off, n1, st);
   if (ensure(B, 3, tmp + 256)) return -2;
-  hipcub::DeviceScan::ExclusiveSum(B.p[3], tmp, kcnt, J.bu_off, n1, st);
-  hipcub::DeviceScan::ExclusiveSum(B.p[3], tmp, ccnt, J.ch_off, n1, st);
+  if (scan_excl<uint32_t>(B.p[3], tmp, kcnt, J.bu_off, n1, st) || scan_excl<uint32_t>(B.p[3], tmp, ccnt, J.ch_off, n1, st)) return -3;
   LMCHK(hipMemcpyAsync(tot, J.bu_off + nb, 4, hipMemcpyDeviceToDevice, st));
   LMCHK(hipMemcpyAsync(tot + 1, J.ch_off + nb, 4, hipMemcpyDeviceToDevice, st));
   // no host round trip for the update / chunk totals: the per-update count arrays are sized by the
@@ -1156,15 +1181,16 @@ int large_run(const GeneralJob &j, const uint32_t *list, uint32_t nb, uint32_t n
   p = (uint8_t *)B.p[1];
   J.u_cnt = carve<uint32_t>(p, 3ull * J.stride);
   J.u_off = carve<uint32_t>(p, 3ull * J.stride);
-  LMCHK(hipMemsetAsync(J.u_cnt, 0, 12ull * J.stride, st));
+  // the listed documents' updates only (tot[0] of them; J.stride, the batch's update count + 1, bounds it)
+  k_lm_zero<<<(J.stride + 255) / 256, 256, 0, st>>>(J, tot);
   const uint32_t grid = nch < 65536 ? nch : 65536;
   if (J.v2) k_lm_walk<false, true><<<grid, 64, WALK_LDS, st>>>(J, tot);
   else k_lm_walk<false, false><<<grid, 64, WALK_LDS, st>>>(J, tot);
-  hipcub::DeviceScan::ExclusiveSum(nullptr, t2, J.u_cnt, J.u_off, J.stride, st);
+  scan_excl<uint32_t>(nullptr, t2, J.u_cnt, J.u_off, J.stride, st, tot, 1);
   if (ensure(B, 3, t2 + 256)) return -2;
-  for (int k = 0; k < 3; k++) hipcub::DeviceScan::ExclusiveSum(B.p[3], t2, J.u_cnt + k * J.stride, J.u_off + k * J.stride, J.stride, st);
-  for (int k = 0; k < 3; k++) LMCHK(hipMemcpyAsync((uint32_t *)B.pinned + k, J.u_off + k * J.stride + nbu, 4, hipMemcpyDeviceToHost, st));
-  LMCHK(hipMemcpyAsync((uint32_t *)B.pinned + 3, tot + 1, 4, hipMemcpyDeviceToHost, st));
+  for (int k = 0; k < 3; k++)
+    if (scan_excl<uint32_t>(B.p[3], t2, J.u_cnt + k * J.stride, J.u_off + k * J.stride, J.stride, st, tot, 1)) return -3;
+  k_lm_totals<<<1, 64, 0, st>>>(J, tot, (uint32_t *)B.pinned_dev);
   LMCHK(hipStreamSynchronize(st));
   if (((uint32_t *)B.pinned)[3] == 0) return 0;  // no listed document has a chunk: all stay pending
   const uint64_t NS = ((uint32_t *)B.pinned)[0] + 1ull, NR = ((uint32_t *)B.pinned)[1] + 1ull, ND = ((uint32_t *)B.pinned)[2] + 1ull;

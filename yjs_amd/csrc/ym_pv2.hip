@@ -30,7 +30,7 @@
 // everything else (several clients, Skip / Any / Type / Format / Embed / Binary content, non-ASCII string
 // columns, non-canonical columns) is left to k_big_v2 (and from there to the general path).
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include "ym_scan.h"
 
 #include "ym_pv2.h"
 #include "ym_cmap.h"
@@ -812,10 +812,10 @@ int pv2_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const u
   pv2_last_meta = J.meta;
   k_v2_prep<<<(n1 + 255) / 256, 256, 0, st>>>(J, pv_min, sizes, sizes1);
   size_t tmp = 0;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, sizes, offs, n1, st);
+  scan_excl<uint64_t>(nullptr, tmp, sizes, offs, n1, st);
   if (pv_ensure(B, 1, tmp + 16)) return -2;
-  if (hipcub::DeviceScan::ExclusiveSum(B.p[1], tmp, sizes, offs, n1, st) != hipSuccess) return -3;
-  if (hipcub::DeviceScan::ExclusiveSum(B.p[1], tmp, sizes1, offs1, n1, st) != hipSuccess) return -3;
+  if (scan_excl<uint64_t>(B.p[1], tmp, sizes, offs, n1, st)) return -3;
+  if (scan_excl<uint64_t>(B.p[1], tmp, sizes1, offs1, n1, st)) return -3;
   if (hipMemcpyAsync(B.pinned, offs + j.n, 8, hipMemcpyDeviceToHost, st) != hipSuccess) return -3;
   if (hipMemcpyAsync(B.pinned + 2, offs1 + j.n, 8, hipMemcpyDeviceToHost, st) != hipSuccess) return -3;
   if (hipStreamSynchronize(st) != hipSuccess) return -3;
@@ -832,7 +832,7 @@ int pv2_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const u
     k_v2_meta_off<<<(j.n + 255) / 256, 256, 0, st>>>(J, offs1, 1);
     ms_rest(J, st);
     ms_sizes(J, sizes, st);
-    if (hipcub::DeviceScan::ExclusiveSum(B.p[1], tmp, sizes, offs, n1, st) != hipSuccess) return -3;
+    if (scan_excl<uint64_t>(B.p[1], tmp, sizes, offs, n1, st)) return -3;
     if (hipMemcpyAsync(B.pinned, offs + j.n, 8, hipMemcpyDeviceToHost, st) != hipSuccess) return -3;
     if (hipStreamSynchronize(st) != hipSuccess) return -3;
     total = *(uint64_t *)B.pinned;

@@ -25,7 +25,7 @@
 // inputs are declined.  Documents this path declines (or does not take: several updates, < PW_MIN bytes)
 // go to k_big_v1, and from there to the general path.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include "ym_scan.h"
 
 #include "ym_fast_common.h"
 #include "ym_kernels.h"
@@ -1751,12 +1751,12 @@ int pw_finish(const GeneralJob &j, hipStream_t st, PwBufs &B) {
   __builtin_memcpy(&mtotal, B.pinned + 4, 8);
   if (total == 0 && mtotal == 0) return 1;
   size_t tmp = 0, tmp2 = 0;
-  if (total) hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cnt, cbase, n1, st);
-  if (mtotal) hipcub::DeviceScan::ExclusiveSum(nullptr, tmp2, msz, moff, n1, st);
+  if (total) scan_excl<uint32_t>(nullptr, tmp, cnt, cbase, n1, st);
+  if (mtotal) scan_excl<uint64_t>(nullptr, tmp2, msz, moff, n1, st);
   if (tmp2 > tmp) tmp = tmp2;
   if (pw_ensure(B, 1, tmp + 16)) return -2;
-  if (total) PWCHK(hipcub::DeviceScan::ExclusiveSum(B.p[1], tmp, cnt, cbase, n1, st));
-  if (mtotal) PWCHK(hipcub::DeviceScan::ExclusiveSum(B.p[1], tmp, msz, moff, n1, st));
+  if (total && scan_excl<uint32_t>(B.p[1], tmp, cnt, cbase, n1, st)) return -3;
+  if (mtotal && scan_excl<uint64_t>(B.p[1], tmp, msz, moff, n1, st)) return -3;
   const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
   // many-section documents: the table walk (no chunk records)
   if (mtotal > 0) {
