@@ -101,3 +101,29 @@ def test_pref_bytes_on_gpu(engine):
             for i, c in enumerate(sel):
                 got = oa[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes()
                 assert st[i] == 0 and hashlib.sha256(got).hexdigest() == c["checked_sha256"], c["id"]
+
+
+@pytest.mark.parametrize("fmt", [1, 2])
+def test_golden_meta_update_log_shape(engine, fmt):
+    """parseUpdateMeta[V2] of an update log (> 65,536 single-update documents: the lane-per-update kernels,
+    ym_small.hip / ym_fast2.hip k_meta_v2, with their declines on the general path): every golden meta
+    vector, repeated to that batch size, byte-identical (or the same error) in every copy."""
+    from yjs_amd import pack_docs
+    cases = _groups()[("meta", fmt)]
+    reps = 65536 // len(cases) + 2
+    arena, upd_off, doc_upd = pack_docs([[c["inputs"][0]] for c in cases] * reps)
+    out_arena, out_off, out_len, status = engine.run_host("meta", fmt, arena, upd_off, doc_upd)
+    bad = []
+    for i in range(len(status)):
+        c = cases[i % len(cases)]
+        st = int(status[i])
+        if "error" in c:
+            why = O.js_error_mismatch(st, c["error"], c["message"])
+            if why:
+                bad.append((i, c["id"], why))
+            continue
+        got = out_arena[int(out_off[i]):int(out_off[i]) + int(out_len[i])].tobytes() if st == 0 else None
+        if st != 0 or got != c["expect"]:
+            bad.append((i, c["id"], st))
+    assert not bad, bad[:20]
+    assert engine.stats["docs_fast"] > 0, engine.stats

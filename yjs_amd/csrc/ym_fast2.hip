@@ -942,8 +942,189 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v2(GeneralJob j, uint32_
   }
 }
 
+// ---- parseUpdateMetaV2 over small updates: one update per LANE --------------------------------------
+// 13.5.16 parseUpdateMetaV2 (LazyStructReader over UpdateDecoderV2; the delete set is not read): per client
+// section with structs its client, its first clock (from) and the end of its last struct (to).  A block takes
+// 64 consecutive single-update documents: the wave stages their (contiguous) bytes into one LDS window with
+// 16-byte loads, then lane l walks document l with the per-lane column decoders of the merge walk (walk_v2:
+// the same acceptance -- canonical columns, ASCII string bodies, no Skip / GC, no ContentJSON / Doc, keys never
+// read from the cache) and k_big_v2's meta rules (clients strictly descending); the wave sizes the outputs by a
+// prefix sum and bump-allocates them with one atomic.  A lane that declines, or a document outside the window,
+// leaves the document to k_big_v2 (done[d] stays 0) or, without a done array, to the general path (declined).
+constexpr uint32_t MW_WIN = 4096, MW_NSEC = 8;
+constexpr uint32_t MW_TAB = MW_WIN + 48;                   // u32[64][MW_NSEC][3]: client, from, to
+constexpr uint32_t MW_LDS = MW_TAB + 64 * MW_NSEC * 12;
+// the lane's update at LDS [p0, p1): its sections into the table at `tab`; the count, or -1 to decline
+__device__ __forceinline__ int meta_walk_v2(uint32_t p0, uint32_t p1, uint32_t tab) {
+  Cur h = {p0, p1, false};
+  rvu(h);  // feature flag
+  Cur col[9];
+#pragma unroll
+  for (uint32_t k = 0; k < 9; k++) {
+    const uint32_t n = rvu(h);
+    if (!room(h, n)) return -1;
+    col[k] = Cur{h.p, h.p + n, false};
+    h.p += n;
+  }
+  if (h.bad) return -1;
+  const uint32_t sn = rvu(col[5]);
+  if (col[5].bad || !room(col[5], sn)) return -1;
+  const uint32_t sb = col[5].p;
+  {
+    uint64_t hi = 0;
+    for (uint32_t o = 0; o < sn; o += 8) hi |= mask_bytes(ld8(sb + o), sn - o);
+    if (hi & 0x8080808080808080ull) return -1;  // (the StringDecoder decodes the body eagerly: non-ASCII -> general)
+  }
+  col[5].p += sn;
+  IdifD kc = {col[0], 0, 0, 0};
+  UoptD cl = {col[1], 0, 0};
+  IdifD lc = {col[2], 0, 0, 0}, rc = {col[3], 0, 0, 0};
+  RleD in = {col[4], 0, 0};
+  UoptD sl = {col[5], 0, 0};
+  RleD pi_ = {col[6], 0, 0};
+  UoptD tr = {col[7], 0, 0}, ln = {col[8], 0, 0};
+  uint32_t spos = 0, keys = 0;
+  Cur c = h;  // rest stream
+  bool bad = false;
+  auto rstr = [&]() -> uint32_t {  // StringDecoder.read(): its UTF-16 length (= bytes: ASCII)
+    const uint32_t n = rd_uopt(sl);
+    bad |= spos + n > sn;
+    spos += n;
+    return n;
+  };
+  const uint32_t nclients = rvu(c);
+  uint32_t prev_client = 0, nsec = 0;
+  for (uint32_t ci = 0; ci < nclients && !c.bad && !bad; ci++) {
+    const uint32_t nstructs = rvu(c);
+    const uint32_t client = rd_uopt(cl);
+    uint64_t clock = rvu(c);
+    bad |= ci > 0 && client >= prev_client;  // a repeated or ascending client: k_big_v2 declines (Map order)
+    prev_client = client;
+    const uint32_t first = (uint32_t)clock;
+    for (uint32_t si = 0; si < nstructs && !c.bad && !bad; si++) {
+      const uint32_t info = rd_rle(in);
+      bad |= info == 10 || (info & 31) == 0 || info > 255;  // Skip / GC: the streamed walker
+      if (info & 0x80) { rd_uopt(cl); rd_idif(lc); }
+      if (info & 0x40) { rd_uopt(cl); rd_idif(rc); }
+      if ((info & 0xC0) == 0) {
+        if (rd_rle(pi_) == 1) rstr();
+        else { rd_uopt(cl); rd_idif(lc); }
+        if (info & 0x20) rstr();
+      }
+      uint32_t len = 1;
+      switch (info & 31) {
+        case 1: len = rd_uopt(ln); break;  // ContentDeleted
+        case 3: {                          // ContentBinary (rest)
+          const uint32_t n = rvu(c);
+          if (!room(c, n)) bad = true;
+          else c.p += n;
+          break;
+        }
+        case 4: len = rstr(); break;  // ContentString
+        case 5: case 6:               // Embed / Format (+ key)
+          if ((info & 31) == 6) rstr();
+          any_canon<false>(c);
+          break;
+        case 7: {  // ContentType
+          const uint32_t t = rd_uopt(tr);
+          bad |= t > 6;
+          if (t == 3 || t == 5) {
+            bad |= rd_idif(kc) < keys;
+            keys++;
+            rstr();
+          }
+          break;
+        }
+        case 8:  // ContentAny
+          len = rd_uopt(ln);
+          for (uint32_t i = 0; i < len && !c.bad; i++) any_canon<false>(c);
+          break;
+        default: bad = true; break;  // ContentJSON, ContentDoc, invalid refs
+      }
+      bad |= c.bad | (len == 0) | ((uint64_t)clock + len > 0xffffffffull);
+      clock += len;
+    }
+    if (nstructs > 0 && !bad) {
+      bad |= nsec >= MW_NSEC;
+      if (!bad) {
+        at<uint32_t>(tab + 12 * nsec) = client;
+        at<uint32_t>(tab + 12 * nsec + 4) = first;
+        at<uint32_t>(tab + 12 * nsec + 8) = (uint32_t)clock;
+        nsec++;
+      }
+    }
+  }
+  bad |= c.bad | cl.c.bad | lc.c.bad | rc.c.bad | in.c.bad | sl.c.bad | pi_.c.bad | tr.c.bad | ln.c.bad | kc.c.bad;
+  return bad ? -1 : (int)nsec;
+}
+__global__ void __launch_bounds__(64) k_meta_v2(GeneralJob j, uint8_t *done) {
+  const uint32_t lane = threadIdx.x;
+  const uint32_t d0 = blockIdx.x * 64, d = d0 + lane;
+  if (d0 >= j.n) return;
+  const uint32_t dn = j.n - d0 < 64 ? j.n - d0 : 64;
+  // the window: the bytes of document d0 onwards (the 64 documents' updates are contiguous in a packed batch)
+  const uint64_t w0 = j.upd_off[j.doc_upd[d0]] & ~15ull;
+  const uint64_t wend = j.upd_off[j.doc_upd[d0 + dn]];
+  const uint32_t wbytes = (uint32_t)((wend - w0 < MW_WIN ? wend - w0 : MW_WIN) + 15) & ~15u;
+  {
+    const uint4 *src = reinterpret_cast<const uint4 *>(j.A + w0);
+    for (uint32_t v = lane; v < wbytes / 16; v += 64) at<uint4>(16 * v) = src[v];
+  }
+  __syncthreads();
+  int ns = -1;
+  uint32_t u0 = 0;
+  bool mine = false;
+  if (lane < dn) {
+    u0 = j.doc_upd[d];
+    mine = j.doc_upd[d + 1] - u0 == 1 && !(done && done[d]);
+    if (mine) {
+      const uint64_t a = j.upd_off[u0], b = j.upd_off[u0 + 1];
+      if (a >= w0 && b <= w0 + wbytes && b > a) ns = meta_walk_v2((uint32_t)(a - w0), (uint32_t)(b - w0), MW_TAB + 12 * MW_NSEC * lane);
+    }
+  }
+  // sizes: vu(n) | (client, from)* | vu(n) | (client, to)*
+  uint32_t sz = 0;
+  const uint32_t tab = MW_TAB + 12 * MW_NSEC * lane;
+  if (ns >= 0) {
+    sz = 2 * vsz((uint32_t)ns);
+    for (int k = 0; k < ns; k++) sz += 2 * vsz(at<uint32_t>(tab + 12 * k)) + vsz(at<uint32_t>(tab + 12 * k + 4)) + vsz(at<uint32_t>(tab + 12 * k + 8));
+  }
+  const uint32_t incl = wave_incl_add(sz), total = lane_read(incl, 63);
+  uint64_t base = 0;
+  if (lane == 0 && total) base = atomicAdd((unsigned long long *)j.used, (unsigned long long)total);
+  base = ((uint64_t)lane_read((uint32_t)(base >> 32), 0) << 32) | lane_read((uint32_t)base, 0);
+  if (ns >= 0) {
+    const uint64_t off = base + incl - sz;
+    if (off + sz > j.cap) {
+      j.status[d] = ym::ST_CAPACITY;
+      j.out_len[d] = 0;
+    } else {
+      const Slot o = make_slot(j.out + off, sz);
+      uint32_t p = put_vu(o, 0, (uint32_t)ns);
+      for (int k = 0; k < ns; k++) p = put_vu(o, put_vu(o, p, at<uint32_t>(tab + 12 * k)), at<uint32_t>(tab + 12 * k + 4));
+      p = put_vu(o, p, (uint32_t)ns);
+      for (int k = 0; k < ns; k++) p = put_vu(o, put_vu(o, p, at<uint32_t>(tab + 12 * k)), at<uint32_t>(tab + 12 * k + 8));
+      j.out_off[d] = off;
+      j.out_len[d] = sz;
+      j.status[d] = ym::ST_OK;
+    }
+    if (done) done[d] = 1;
+  } else if (lane < dn && !done) {
+    decline(j, d);  // no streamed walker after this kernel: the general path
+  }
+}
+
 }  // namespace fastv2
 
+
+// parseUpdateMetaV2 over small single updates, one per lane (k_meta_v2); done: the streamed walker's
+// done array (nullptr: the kernel is the call's only specialised pass, its declines go to the general path)
+int meta_v2_launch(const GeneralJob &j, uint8_t *done, hipStream_t st) {
+  static const bool off = getenv("YMERGE_NO_META_V2") != nullptr;
+  if (off || j.op != OP_META || !j.v2 || j.n == 0) return 0;
+  fastv2::k_meta_v2<<<(j.n + 63) / 64, 64, fastv2::MW_LDS, st>>>(j, done);
+  return 1;
+}
 
 int fast2_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st) {
   if (op != OP_MERGE || !j.v2) return 0;
