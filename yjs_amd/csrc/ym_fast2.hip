@@ -942,20 +942,25 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v2(GeneralJob j, uint32_
   }
 }
 
-// ---- parseUpdateMetaV2 over small updates: one update per LANE --------------------------------------
-// 13.5.16 parseUpdateMetaV2 (LazyStructReader over UpdateDecoderV2; the delete set is not read): per client
-// section with structs its client, its first clock (from) and the end of its last struct (to).  A block takes
-// 64 consecutive single-update documents: the wave stages their (contiguous) bytes into one LDS window with
-// 16-byte loads, then lane l walks document l with the per-lane column decoders of the merge walk (walk_v2:
-// the same acceptance -- canonical columns, ASCII string bodies, no Skip / GC, no ContentJSON / Doc, keys never
-// read from the cache) and k_big_v2's meta rules (clients strictly descending); the wave sizes the outputs by a
-// prefix sum and bump-allocates them with one atomic.  A lane that declines, or a document outside the window,
-// leaves the document to k_big_v2 (done[d] stays 0) or, without a done array, to the general path (declined).
-constexpr uint32_t MW_WIN = 4096, MW_NSEC = 8;
-constexpr uint32_t MW_TAB = MW_WIN + 48;                   // u32[64][MW_NSEC][3]: client, from, to
-constexpr uint32_t MW_LDS = MW_TAB + 64 * MW_NSEC * 12;
-// the lane's update at LDS [p0, p1): its sections into the table at `tab`; the count, or -1 to decline
-__device__ __forceinline__ int meta_walk_v2(uint32_t p0, uint32_t p1, uint32_t tab) {
+// ---- parseUpdateMetaV2 / encodeStateVectorFromUpdateV2 over small updates: one update per LANE -------------
+// 13.5.16 parseUpdateMetaV2 / encodeStateVectorFromUpdateV2 (LazyStructReader over UpdateDecoderV2; the delete
+// set is not read): per client section with structs its client, its first clock and the end of its last
+// struct; meta writes (client, first)* then (client, end)*, the state vector (client, end) for the sections
+// that start at clock 0 (os@37724: a section from a later clock counts nothing; no Skip reaches here).  A block
+// takes ND consecutive single-update documents: the wave stages their (contiguous) bytes into one LDS window
+// of WIN bytes with 16-byte loads, then lane l walks document l with the per-lane column decoders of the merge
+// walk (walk_v2: the same acceptance -- canonical columns, ASCII string bodies, no Skip / GC, no ContentJSON /
+// Doc, keys never read from the cache) and k_big_v2's rules (clients strictly descending); the wave sizes the
+// outputs by a prefix sum and bump-allocates them with one atomic.  A lane that declines, or a document outside
+// the window, leaves the document to k_big_v2 (done[d] stays 0) or, without a done array, to the general path.
+template <uint32_t ND, uint32_t WIN, uint32_t NSEC>
+struct Sv2Lay {
+  static constexpr uint32_t TAB = WIN + 48;                // u32[ND][NSEC][3]: client, first, end
+  static constexpr uint32_t BYTES = TAB + ND * NSEC * 12;
+};
+// the lane's update at LDS [p0, p1): its sections into the table at `tab` (<= nsec_max); the count, or -1 to
+// decline
+__device__ __forceinline__ int meta_walk_v2(uint32_t p0, uint32_t p1, uint32_t tab, uint32_t nsec_max) {
   Cur h = {p0, p1, false};
   rvu(h);  // feature flag
   Cur col[9];
@@ -1045,7 +1050,7 @@ __device__ __forceinline__ int meta_walk_v2(uint32_t p0, uint32_t p1, uint32_t t
       clock += len;
     }
     if (nstructs > 0 && !bad) {
-      bad |= nsec >= MW_NSEC;
+      bad |= nsec >= nsec_max;
       if (!bad) {
         at<uint32_t>(tab + 12 * nsec) = client;
         at<uint32_t>(tab + 12 * nsec + 4) = first;
@@ -1057,37 +1062,41 @@ __device__ __forceinline__ int meta_walk_v2(uint32_t p0, uint32_t p1, uint32_t t
   bad |= c.bad | cl.c.bad | lc.c.bad | rc.c.bad | in.c.bad | sl.c.bad | pi_.c.bad | tr.c.bad | ln.c.bad | kc.c.bad;
   return bad ? -1 : (int)nsec;
 }
-__global__ void __launch_bounds__(64) k_meta_v2(GeneralJob j, uint8_t *done) {
+template <int OP, uint32_t ND, uint32_t WIN, uint32_t NSEC>
+__global__ void __launch_bounds__(64) k_small_v2(GeneralJob j, uint8_t *done) {
+  using L = Sv2Lay<ND, WIN, NSEC>;
   const uint32_t lane = threadIdx.x;
-  const uint32_t d0 = blockIdx.x * 64, d = d0 + lane;
+  const uint32_t d0 = blockIdx.x * ND, d = d0 + lane;
   if (d0 >= j.n) return;
-  const uint32_t dn = j.n - d0 < 64 ? j.n - d0 : 64;
-  // the window: the bytes of document d0 onwards (the 64 documents' updates are contiguous in a packed batch)
+  const uint32_t dn = j.n - d0 < ND ? j.n - d0 : ND;
+  // the window: the bytes of document d0 onwards (the ND documents' updates are contiguous in a packed batch)
   const uint64_t w0 = j.upd_off[j.doc_upd[d0]] & ~15ull;
   const uint64_t wend = j.upd_off[j.doc_upd[d0 + dn]];
-  const uint32_t wbytes = (uint32_t)((wend - w0 < MW_WIN ? wend - w0 : MW_WIN) + 15) & ~15u;
+  const uint32_t wbytes = (uint32_t)((wend - w0 < WIN ? wend - w0 : WIN) + 15) & ~15u;
   {
     const uint4 *src = reinterpret_cast<const uint4 *>(j.A + w0);
     for (uint32_t v = lane; v < wbytes / 16; v += 64) at<uint4>(16 * v) = src[v];
   }
   __syncthreads();
   int ns = -1;
-  uint32_t u0 = 0;
-  bool mine = false;
+  const uint32_t tab = L::TAB + 12 * NSEC * (lane < ND ? lane : 0);
   if (lane < dn) {
-    u0 = j.doc_upd[d];
-    mine = j.doc_upd[d + 1] - u0 == 1 && !(done && done[d]);
-    if (mine) {
+    const uint32_t u0 = j.doc_upd[d];
+    if (j.doc_upd[d + 1] - u0 == 1 && !(done && done[d])) {
       const uint64_t a = j.upd_off[u0], b = j.upd_off[u0 + 1];
-      if (a >= w0 && b <= w0 + wbytes && b > a) ns = meta_walk_v2((uint32_t)(a - w0), (uint32_t)(b - w0), MW_TAB + 12 * MW_NSEC * lane);
+      if (a >= w0 && b <= w0 + wbytes && b > a) ns = meta_walk_v2((uint32_t)(a - w0), (uint32_t)(b - w0), tab, NSEC);
     }
   }
-  // sizes: vu(n) | (client, from)* | vu(n) | (client, to)*
-  uint32_t sz = 0;
-  const uint32_t tab = MW_TAB + 12 * MW_NSEC * lane;
+  // meta: vu(n) | (client, first)* | vu(n) | (client, end)*;  sv: vu(m) | (client, end)* over the m sections
+  // that start at 0
+  uint32_t sz = 0, m = 0;
   if (ns >= 0) {
-    sz = 2 * vsz((uint32_t)ns);
-    for (int k = 0; k < ns; k++) sz += 2 * vsz(at<uint32_t>(tab + 12 * k)) + vsz(at<uint32_t>(tab + 12 * k + 4)) + vsz(at<uint32_t>(tab + 12 * k + 8));
+    for (int k = 0; k < ns; k++) {
+      const uint32_t cl = at<uint32_t>(tab + 12 * k), f = at<uint32_t>(tab + 12 * k + 4), e = at<uint32_t>(tab + 12 * k + 8);
+      if (OP == OP_META) sz += 2 * vsz(cl) + vsz(f) + vsz(e);
+      else if (f == 0) { sz += vsz(cl) + vsz(e); m++; }
+    }
+    sz += OP == OP_META ? 2 * vsz((uint32_t)ns) : vsz(m);
   }
   const uint32_t incl = wave_incl_add(sz), total = lane_read(incl, 63);
   uint64_t base = 0;
@@ -1100,10 +1109,16 @@ __global__ void __launch_bounds__(64) k_meta_v2(GeneralJob j, uint8_t *done) {
       j.out_len[d] = 0;
     } else {
       const Slot o = make_slot(j.out + off, sz);
-      uint32_t p = put_vu(o, 0, (uint32_t)ns);
-      for (int k = 0; k < ns; k++) p = put_vu(o, put_vu(o, p, at<uint32_t>(tab + 12 * k)), at<uint32_t>(tab + 12 * k + 4));
-      p = put_vu(o, p, (uint32_t)ns);
-      for (int k = 0; k < ns; k++) p = put_vu(o, put_vu(o, p, at<uint32_t>(tab + 12 * k)), at<uint32_t>(tab + 12 * k + 8));
+      if (OP == OP_META) {
+        uint32_t p = put_vu(o, 0, (uint32_t)ns);
+        for (int k = 0; k < ns; k++) p = put_vu(o, put_vu(o, p, at<uint32_t>(tab + 12 * k)), at<uint32_t>(tab + 12 * k + 4));
+        p = put_vu(o, p, (uint32_t)ns);
+        for (int k = 0; k < ns; k++) p = put_vu(o, put_vu(o, p, at<uint32_t>(tab + 12 * k)), at<uint32_t>(tab + 12 * k + 8));
+      } else {
+        uint32_t p = put_vu(o, 0, m);
+        for (int k = 0; k < ns; k++)
+          if (at<uint32_t>(tab + 12 * k + 4) == 0) p = put_vu(o, put_vu(o, p, at<uint32_t>(tab + 12 * k)), at<uint32_t>(tab + 12 * k + 8));
+      }
       j.out_off[d] = off;
       j.out_len[d] = sz;
       j.status[d] = ym::ST_OK;
@@ -1116,13 +1131,21 @@ __global__ void __launch_bounds__(64) k_meta_v2(GeneralJob j, uint8_t *done) {
 
 }  // namespace fastv2
 
-
-// parseUpdateMetaV2 over small single updates, one per lane (k_meta_v2); done: the streamed walker's
-// done array (nullptr: the kernel is the call's only specialised pass, its declines go to the general path)
-int meta_v2_launch(const GeneralJob &j, uint8_t *done, hipStream_t st) {
-  static const bool off = getenv("YMERGE_NO_META_V2") != nullptr;
-  if (off || j.op != OP_META || !j.v2 || j.n == 0) return 0;
-  fastv2::k_meta_v2<<<(j.n + 63) / 64, 64, fastv2::MW_LDS, st>>>(j, done);
+// parseUpdateMetaV2 / encodeStateVectorFromUpdateV2 over small single updates, one per lane (k_small_v2);
+// done: the streamed walker's done array (nullptr: the kernel is the call's only specialised pass, its
+// declines go to the general path).  Meta: 64 updates of an update log per wave (4 KB window); state
+// vectors: 16 merged documents per wave (~1 KB each: a 24 KB window, 32 sections each).
+int small_v2_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t st) {
+  static const bool off = getenv("YMERGE_NO_SMALL_V2") != nullptr;
+  if (off || !j.v2 || j.n == 0) return 0;
+  using namespace fastv2;
+  if (op == OP_META) {
+    k_small_v2<OP_META, 64, 4096, 8><<<(j.n + 63) / 64, 64, Sv2Lay<64, 4096, 8>::BYTES, st>>>(j, done);
+  } else if (op == OP_SV) {
+    k_small_v2<OP_SV, 16, 24576, 32><<<(j.n + 15) / 16, 64, Sv2Lay<16, 24576, 32>::BYTES, st>>>(j, done);
+  } else {
+    return 0;
+  }
   return 1;
 }
 
