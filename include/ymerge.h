@@ -49,7 +49,7 @@ enum {
   YM_ERR_UNSUPPORTED = 7, /* valid input needing a canonicalisation the engine does not implement */
   YM_ERR_METHOD = 8,      /* Error('Method unimplemented')                                       */
   YM_ERR_CAPACITY = 9,    /* output arena too small: call again with a larger cap                */
-  YM_PENDING = 101,       /* ym_merge_async only: declined by the fast path, pass it to ym_merge  */
+  YM_PENDING = 101,       /* ym_*_async only: declined by the async kernels, pass it to ym_merge etc. */
 };
 
 #define YM_STATUS_CLASS(s) ((s) & 0xff)
@@ -133,6 +133,21 @@ int ym_merge(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
 int ym_merge_async(const ym_batch *b, ym_out *out, void *stream, uint32_t *pending);
 int ym_diff(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
 int ym_sv(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);
+/* Asynchronous ym_diff / ym_sv for device batches (a sync server answering SyncStep1 messages back to back
+ * on `stream`): the single-update walkers only (small documents one per lane or per wave, the rest one wave
+ * per document), enqueued without a host round trip; the results are valid when the stream has drained.
+ * Outputs are bump-allocated from the start of out->arena (out->used is not written); a document that does
+ * not fit gets YM_ERR_CAPACITY.  A V2 diff's walker re-encodes the columns in scratch taken from the same
+ * arena: 8 x the input bytes + 2 x the state-vector bytes + (1 KB + 384 B per client section) per document
+ * always suffices.  A document the walkers decline (several updates, more than 2,048 client
+ * sections or state-vector entries, non-canonical or invalid input) gets YM_PENDING and increments *pending
+ * (a uint32_t in device memory, or NULL): run those through ym_diff / ym_sv, which also report their
+ * exceptions.  Large single updates run on the one-wave walker here (the chunk- and column-parallel passes
+ * of the synchronous calls size their records on the host).  The async calls share device scratch: each
+ * waits on the device for the previous one, whatever stream either runs on (the synchronous entry points
+ * and ym_merge_async use other buffers).  Return value: 0, or a negative error. */
+int ym_diff_async(const ym_batch *b, ym_out *out, void *stream, uint32_t *pending);
+int ym_sv_async(const ym_batch *b, ym_out *out, void *stream, uint32_t *pending);
 /* convertUpdateFormatV1ToV2 (b->format = YM_V1) / convertUpdateFormatV2ToV1 (b->format = YM_V2): one
  * update per document, re-encoded in the other format (yjs 13.5.x convertUpdateFormat, bundle ms@41803) */
 int ym_convert(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats);

@@ -26,6 +26,8 @@ int fast2_nested_launch(const GeneralJob &j, uint32_t n, hipStream_t st);  // ym
 int fast2_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st); // ym_fast2.hip
 int big_launch(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &pw);       // ym_big.hip
 int big2_launch(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &pw);      // ym_big2.hip
+int big_async_launch(uint32_t op, const GeneralJob &j, uint8_t *done, uint32_t grid_max, hipStream_t st);   // ym_big.hip
+int big2_async_launch(uint32_t op, const GeneralJob &j, uint8_t *done, uint32_t grid_max, hipStream_t st);  // ym_big2.hip
 __global__ void k_fast_region(GeneralJob j, uint32_t n_upd);                         // ym_fast.hip
 __global__ void k_compact_ws(GeneralJob j, uint64_t *ws_size);                        // ym_compact.hip
 template <int OCC> __global__ void k_compact(GeneralJob j, uint32_t lanes, uint64_t big, int part);
@@ -66,6 +68,10 @@ struct DevState {
   DBuf cmp_off, cmp_len, cmp_arena;  // host batches: outputs packed in document order before the D2H copy
   DBuf async_off;                    // ym_merge_async: its own widened offsets (not in_off: the synchronous
   hipEvent_t ev_async = nullptr;     // calls write that one on their streams), guarded by this event
+  // ym_diff_async / ym_sv_async: counters + done flags, per-block walker scratch, widened offsets, guarded
+  // by ev_async2 (each such call waits on the device for the previous one)
+  DBuf async2_ws, async2_bs, async2_off;
+  hipEvent_t ev_async2 = nullptr;
   LargeBufs large;
   PwBufs pw, pw2;
   hipEvent_t evl1 = nullptr, evn0 = nullptr, evn1 = nullptr;
@@ -751,9 +757,11 @@ static void release_state(DevState *S) {
   if (S->stream) hipStreamSynchronize(S->stream);
   DBuf *bufs[] = {&S->ws, &S->ws_size, &S->ws_off, &S->layout, &S->counters, &S->scan_tmp, &S->list_a, &S->list_b,
                   &S->flags, &S->bscratch, &S->in_arena, &S->in_off, &S->in_doc, &S->in_sv, &S->in_svoff, &S->out_arena,
-                  &S->out_off, &S->out_len, &S->status, &S->cmp_off, &S->cmp_len, &S->cmp_arena, &S->async_off};
+                  &S->out_off, &S->out_len, &S->status, &S->cmp_off, &S->cmp_len, &S->cmp_arena, &S->async_off,
+                  &S->async2_ws, &S->async2_bs, &S->async2_off};
   for (DBuf *b : bufs) if (b->p) hipFree(b->p);
   if (S->ev_async) hipEventDestroy(S->ev_async);
+  if (S->ev_async2) hipEventDestroy(S->ev_async2);
   if (S->pinned) hipHostFree(S->pinned);
   if (S->ev0) hipEventDestroy(S->ev0);
   if (S->ev1) hipEventDestroy(S->ev1);
@@ -894,6 +902,71 @@ int ym_merge_async(const ym_batch *b, ym_out *out, void *stream, uint32_t *pendi
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 int ym_diff(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_DIFF, b, out, stream, stats); }
+
+// Asynchronous diff / state vector (include/ymerge.h): the streamed single-update kernels enqueued without a
+// host round trip -- small documents one per lane or per wave, k_big_v1 / k_big_v2 the rest; no chunk- or
+// column-parallel pass (those size their records on the host) and no general path.  The call's counters,
+// done flags and walker scratch are the async path's own: each call waits (on the device) for the previous one.
+static int run_async(uint32_t op, const ym_batch *b, ym_out *out, void *stream, uint32_t *pending) {
+  if (!b || !out || b->mem != YM_MEM_DEVICE) return -1;
+  if (op == OP_DIFF && (!b->sv_arena || !b->sv_off)) return -1;
+  DevState *S = state();
+  {
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || cur != S->device) HIPCHK(hipSetDevice(S->device));
+  }
+  hipStream_t st = stream ? (hipStream_t)stream : S->stream;
+  const uint32_t nd = b->n_docs;
+  if (nd == 0) return 0;
+  constexpr uint32_t GRID = 2048;  // k_big_*'s blocks (BS_BYTES of scratch each)
+  const uint32_t grid = nd < GRID ? nd : GRID;
+  const bool off32 = (b->format & YM_OFF32) != 0;
+  const uint64_t ws_bytes = 64 + ((nd + 15ull) & ~15ull) + 64;
+  if (!S->ev_async2) HIPCHK(hipEventCreateWithFlags(&S->ev_async2, hipEventDisableTiming));
+  // growing a buffer frees it: let the previous async call finish reading it first
+  if (S->async2_ws.cap < ws_bytes || S->async2_bs.cap < grid * BS_BYTES || (off32 && S->async2_off.cap < (b->n_upd + 1) * 8ull))
+    HIPCHK(hipEventSynchronize(S->ev_async2));
+  if (S->async2_ws.ensure(ws_bytes) || S->async2_bs.ensure(grid * BS_BYTES) ||
+      (off32 && S->async2_off.ensure((b->n_upd + 1) * 8ull)))
+    return -2;
+  HIPCHK(hipStreamWaitEvent(st, S->ev_async2, 0));
+  uint64_t *ctr = S->async2_ws.as<uint64_t>();  // [0] used (bump allocator), [1] declined (u32), [2] completions
+  uint8_t *done = S->async2_ws.as<uint8_t>() + 64;
+  HIPCHK(hipMemsetAsync(ctr, 0, ws_bytes, st));
+  GeneralJob j;
+  memset(&j, 0, sizeof(j));
+  j.A = b->arena;
+  j.v2 = (b->format & 0xff) == YM_V2;
+  if (off32) {
+    j.upd_off32 = reinterpret_cast<const uint32_t *>(b->upd_off);
+    k_widen<<<(b->n_upd + 256) / 256, 256, 0, st>>>(j.upd_off32, S->async2_off.as<uint64_t>(), b->n_upd + 1);
+    j.upd_off = S->async2_off.as<uint64_t>();
+  } else {
+    j.upd_off = b->upd_off;
+  }
+  j.doc_upd = b->doc_upd;
+  j.sv = op == OP_DIFF ? b->sv_arena : nullptr;
+  j.sv_off = op == OP_DIFF ? b->sv_off : nullptr;
+  j.op = op;
+  j.status = out->status;
+  j.out = out->arena;
+  j.cap = out->cap;
+  j.out_off = out->out_off;
+  j.out_len = out->out_len;
+  j.used = ctr;
+  j.pend_list = nullptr;  // declines are only counted
+  j.pend_count = pending ? pending : reinterpret_cast<uint32_t *>(ctr + 1);
+  j.pw_count = ctr + 2;
+  j.n = nd;
+  j.bscratch = S->async2_bs.as<uint8_t>();
+  int fr = big_async_launch(op, j, done, grid, st);
+  if (fr == 0) fr = big2_async_launch(op, j, done, grid, st);
+  if (fr <= 0) return fr < 0 ? fr : -1;
+  HIPCHK(hipEventRecord(S->ev_async2, st));
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+int ym_diff_async(const ym_batch *b, ym_out *out, void *stream, uint32_t *pending) { return run_async(OP_DIFF, b, out, stream, pending); }
+int ym_sv_async(const ym_batch *b, ym_out *out, void *stream, uint32_t *pending) { return run_async(OP_SV, b, out, stream, pending); }
 int ym_sv(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_SV, b, out, stream, stats); }
 int ym_convert(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_CONV, b, out, stream, stats); }
 int ym_meta(const ym_batch *b, ym_out *out, void *stream, ym_stats *stats) { return run_op(OP_META, b, out, stream, stats); }

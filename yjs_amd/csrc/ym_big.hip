@@ -92,7 +92,8 @@ __device__ __forceinline__ uint32_t put_vu_lds(uint32_t p, uint32_t v) {
   {                                                         \
     if (threadIdx.x == 0) {                                 \
       j.status[d] = ST_PENDING;                             \
-      j.pend_list[atomicAdd(j.pend_count, 1u)] = d;         \
+      const uint32_t q_ = atomicAdd(j.pend_count, 1u);      \
+      if (j.pend_list) j.pend_list[q_] = d;                 \
     }                                                       \
     __syncthreads();                                        \
     continue;                                               \
@@ -480,6 +481,22 @@ int big_launch(uint32_t op, const GeneralJob &j0, hipStream_t st, PwBufs &pwb) {
   const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
   if (op == OP_DIFF) big::k_big_v1<OP_DIFF><<<grid, 64, big::LDS_BYTES, st>>>(j);
   else if (op == OP_META) big::k_big_v1<OP_META><<<grid, 64, big::LDS_BYTES, st>>>(j);
+  else big::k_big_v1<OP_SV><<<grid, 64, big::LDS_BYTES, st>>>(j);
+  return 1;
+}
+
+// The asynchronous form (ym_diff_async / ym_sv_async): the same kernels without the chunk-parallel walk
+// (it sizes its records on the host) -- small documents one per lane, up to 4 KB one per wave, k_big_v1 the
+// rest over a grid of at most grid_max blocks.  done: n zeroed bytes, followed at the next 16-byte boundary
+// by 32 zeroed bytes (k_pw_small's tally).
+int big_async_launch(uint32_t op, const GeneralJob &j0, uint8_t *done, uint32_t grid_max, hipStream_t st) {
+  if (j0.v2 || (op != OP_DIFF && op != OP_SV)) return 0;
+  GeneralJob j = j0;
+  j.pw_done = done;
+  small_launch(op, j, done, st);
+  pw_small_launch(op, j, done, st);
+  const uint32_t grid = j.n < grid_max ? j.n : grid_max;
+  if (op == OP_DIFF) big::k_big_v1<OP_DIFF><<<grid, 64, big::LDS_BYTES, st>>>(j);
   else big::k_big_v1<OP_SV><<<grid, 64, big::LDS_BYTES, st>>>(j);
   return 1;
 }

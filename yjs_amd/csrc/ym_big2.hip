@@ -377,7 +377,8 @@ __device__ __forceinline__ void v2_write(Doc &D, const Rec &r, uint32_t off, uin
   {                                                         \
     if (threadIdx.x == 0) {                                 \
       j.status[d] = ST_PENDING;                             \
-      j.pend_list[atomicAdd(j.pend_count, 1u)] = d;         \
+      const uint32_t q_ = atomicAdd(j.pend_count, 1u);      \
+      if (j.pend_list) j.pend_list[q_] = d;                 \
     }                                                       \
     __syncthreads();                                        \
     continue;                                               \
@@ -749,6 +750,19 @@ int big2_launch(uint32_t op, const GeneralJob &j0, hipStream_t st, PwBufs &pwb) 
   const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
   if (op == OP_DIFF) big2::k_big_v2<OP_DIFF><<<grid, 64, big2::LDS_BYTES, st>>>(j);
   else if (op == OP_META) big2::k_big_v2<OP_META><<<grid, 64, big2::LDS_BYTES, st>>>(j);
+  else big2::k_big_v2<OP_SV><<<grid, 64, big2::LDS_BYTES, st>>>(j);
+  return 1;
+}
+
+// The asynchronous form (ym_diff_async / ym_sv_async): no column-parallel pass (it sizes its records on the
+// host); small state vectors one per lane, k_big_v2 the rest over at most grid_max blocks.  done: n zeroed bytes.
+int big2_async_launch(uint32_t op, const GeneralJob &j0, uint8_t *done, uint32_t grid_max, hipStream_t st) {
+  if (!j0.v2 || (op != OP_DIFF && op != OP_SV)) return 0;
+  GeneralJob j = j0;
+  j.pw_done = done;
+  small_v2_launch(op, j, done, st);
+  const uint32_t grid = j.n < grid_max ? j.n : grid_max;
+  if (op == OP_DIFF) big2::k_big_v2<OP_DIFF><<<grid, 64, big2::LDS_BYTES, st>>>(j);
   else big2::k_big_v2<OP_SV><<<grid, 64, big2::LDS_BYTES, st>>>(j);
   return 1;
 }

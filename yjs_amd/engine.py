@@ -94,8 +94,8 @@ class _Stats(ctypes.Structure):
 
 
 EXPORTS = ("ym_init", "ym_shutdown", "ym_strerror", "ym_out_bound", "ym_merge", "ym_diff", "ym_sv", "ym_convert",
-           "ym_meta", "ym_ds_merge", "ym_snapshot", "ym_compact", "ym_merge_async")
-YM_PENDING = 101  # ym_merge_async: declined by the fast path (pass the document to ym_merge)
+           "ym_meta", "ym_ds_merge", "ym_snapshot", "ym_compact", "ym_merge_async", "ym_diff_async", "ym_sv_async")
+YM_PENDING = 101  # ym_*_async: declined by the async kernels (pass the document to ym_merge / ym_diff / ym_sv)
 
 
 def load_library(path=None):
@@ -109,8 +109,9 @@ def load_library(path=None):
     for fn in (L.ym_merge, L.ym_diff, L.ym_sv, L.ym_convert, L.ym_meta, L.ym_ds_merge, L.ym_snapshot, L.ym_compact):
         fn.argtypes = [ctypes.POINTER(_Batch), ctypes.POINTER(_Out), ctypes.c_void_p, ctypes.POINTER(_Stats)]
         fn.restype = ctypes.c_int
-    L.ym_merge_async.argtypes = [ctypes.POINTER(_Batch), ctypes.POINTER(_Out), ctypes.c_void_p, ctypes.c_void_p]
-    L.ym_merge_async.restype = ctypes.c_int
+    for fn in (L.ym_merge_async, L.ym_diff_async, L.ym_sv_async):
+        fn.argtypes = [ctypes.POINTER(_Batch), ctypes.POINTER(_Out), ctypes.c_void_p, ctypes.c_void_p]
+        fn.restype = ctypes.c_int
     return L
 
 
@@ -283,6 +284,15 @@ class Engine:
         """ym_merge_async over fixed device buffers: a zero-argument callable that enqueues one merge of the
         batch on `stream` (the LDS fast path only) and returns its rc without waiting.  Declined documents
         get status YM_PENDING and are counted into `pending` (a 1-element int32 CUDA tensor, or None)."""
+        return self.prepare_async("merge", fmt, arena, upd_off, doc_upd, out_arena, out_off, out_len, status,
+                                  pending=pending, stream=stream)
+
+    def prepare_async(self, op, fmt, arena, upd_off, doc_upd, out_arena, out_off, out_len, status, sv_arena=None,
+                      sv_off=None, pending=None, stream=None):
+        """ym_merge_async / ym_diff_async / ym_sv_async (op "merge" / "diff" / "sv") over fixed device buffers:
+        a zero-argument callable that enqueues the call on `stream` and returns its rc without waiting.
+        Declined documents get status YM_PENDING and are counted into `pending` (a 1-element int32 CUDA tensor,
+        or None); diff takes each document's state vector from sv_arena / sv_off (int64 offsets)."""
         b = _Batch()
         b.arena = arena.data_ptr()
         b.upd_off = upd_off.data_ptr()
@@ -293,8 +303,11 @@ class Engine:
         b.mem = 1
         o = _Out(out_arena.data_ptr(), out_arena.numel(), out_off.data_ptr(), out_len.data_ptr(), status.data_ptr(), 0)
         s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+        if op == "diff":
+            b.sv_arena = sv_arena.data_ptr()
+            b.sv_off = sv_off.data_ptr()
         pend = ctypes.c_void_p(pending.data_ptr()) if pending is not None else None
-        fn = self.lib.ym_merge_async
+        fn = {"merge": self.lib.ym_merge_async, "diff": self.lib.ym_diff_async, "sv": self.lib.ym_sv_async}[op]
         pb, po = ctypes.byref(b), ctypes.byref(o)
 
         def call():
