@@ -5,6 +5,7 @@ vector must come out byte-identical (or with the same error), including the payl
 tests/golden/canon.json."""
 import collections
 
+import numpy as np
 import pytest
 
 import golden_io
@@ -53,6 +54,20 @@ def test_golden_through_chunked_walk(engine, key, ms, monkeypatch):
         assert 0 < engine.stats["docs_chunked"] <= engine.stats["docs_fast"], engine.stats
     else:  # the V2 paths (one section: String / Deleted / GC; several: XML / format / any content too)
         assert engine.stats["docs_chunked"] > 0, engine.stats
+
+
+def test_golden_v2_diff_through_lane_kernel(engine, monkeypatch):
+    """k_diff_small_v2 (one update per lane, ym_fast2.hip) runs on batches of more than 8,192 documents only;
+    with YMERGE_DF2_MIN=0 every golden V2 diff goes through it first (declines fall back to k_big_v2) and must
+    come out byte-identical.  (Many vectors are outside its acceptance on purpose: non-ASCII strings, Skip / GC /
+    JSON content, repeated clients; those decline and take the walker.)"""
+    import ctypes
+    monkeypatch.setenv("YMERGE_DF2_MIN", "0")
+    _check_group(engine, ("diff", 2))
+    n = len(_groups()[("diff", 2)])
+    done = np.zeros(n, np.uint8)
+    assert engine.lib.ym__pv2_done(done.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), ctypes.c_uint32(n)) == 0
+    assert (done == 1).sum() >= n // 8, np.unique(done, return_counts=True)
 
 
 def _check_group(engine, key):

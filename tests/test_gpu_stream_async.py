@@ -70,9 +70,10 @@ def _inputs(engine, docs, fmt, seed=0):
 @pytest.mark.parametrize("op", ["diff", "sv"])
 @pytest.mark.parametrize("name,off32", [("c2_v1", True), ("c2_v1", False), ("c4_v1", True), ("c2r_v1", False),
                                         ("c2_v2", True), ("c4_v2", False), ("c2r_v2", True)])
-def test_async_equals_sync(engine, name, off32, op):
+def test_async_equals_sync(engine, name, off32, op, monkeypatch):
     import torch
     from yjs_amd.engine import _unpack
+    monkeypatch.setenv("YMERGE_DF2_MIN", "0")  # (V2 diffs through k_diff_small_v2 at this batch size too)
     fmt, merged = _merged(engine, name, 2000)
     a, o, d, sva, svo = _inputs(engine, [[m] for m in merged], fmt)
     want = _unpack(*engine.run_host(op, fmt, a, o, d, *((sva, svo) if op == "diff" else ())), False)

@@ -1129,13 +1129,531 @@ __global__ void __launch_bounds__(64) k_small_v2(GeneralJob j, uint8_t *done) {
   }
 }
 
+// ---- diffUpdateV2 over small updates: one update per LANE --------------------------------------------------
+// 13.5.16 diffUpdateV2 (us@40707): the structs of each client section from the first one ending past the state
+// vector's clock on (that one sliced by `off`), re-encoded with the lib0 column encoders -- Item.write(encoder,
+// off) as k_big_v2's v2_write -- into per-lane output streams in LDS, then vu(0) | 9 x varUint8Array(column) |
+// vu(#parts) | parts (vu(written) | first clock | payloads) | delete set (copied: a canonical V2 delete set
+// round-trips byte for byte).  A block takes ND consecutive single-update documents and their state vectors:
+// both windows are staged into LDS with 16-byte loads, each lane decodes its state vector into a table, sizes
+// its eleven output streams from its input columns (a wave prefix sum carves them out of one LDS pool), walks
+// its update with the per-lane column decoders of the merge walk and writes the streams; the wave sizes the
+// outputs by a prefix sum, bump-allocates them with one atomic and each lane copies its document out.  Anything
+// outside this path's acceptance (Skip / GC / JSON / Doc inputs, cached keys, non-ASCII strings, clients not
+// strictly descending, a stream or table overflow, documents outside the windows) leaves done[d] = 0: k_big_v2.
+template <uint32_t ND, uint32_t WIN, uint32_t POOL>
+struct Df2Lay {
+  static constexpr uint32_t SVW = ND == 1 ? 1024 : 64 * ND, NSV = ND == 1 ? 128 : 32, NPART = ND == 1 ? 128 : 32;
+  static constexpr uint32_t SV = WIN + 48;               // u8[SVW + 16]: the state vectors
+  static constexpr uint32_t SVT = SV + SVW + 16;         // u32[ND][NSV][2]: client, clock (then the ds clients)
+  static constexpr uint32_t PT = SVT + ND * NSV * 8;     // u32[ND][NPART][4]: rest start, rest end, written
+  static constexpr uint32_t OUT = PT + ND * NPART * 16;  // u8[POOL]: the lanes' output streams
+  static constexpr uint32_t BYTES = OUT + POOL + 16;
+};
+namespace df2 {
+struct OS { uint32_t a, n, cap; };  // an output stream in LDS: start, bytes written (may pass cap), capacity
+__device__ __forceinline__ void ob(OS &s, uint32_t v) {
+  if (s.n < s.cap) at<uint8_t>(s.a + s.n) = (uint8_t)v;
+  s.n++;
+}
+__device__ __forceinline__ void ovu(OS &s, uint32_t v) {
+  while (v > 127) { ob(s, 0x80 | (v & 127)); v >>= 7; }
+  ob(s, v);
+}
+__device__ __forceinline__ void ovi(OS &s, bool neg, uint32_t m) {  // lib0 writeVarInt (sign in the first byte)
+  ob(s, (m > 63 ? 0x80 : 0) | (neg ? 0x40 : 0) | (m & 63));
+  m >>= 6;
+  while (m > 0) { ob(s, (m > 127 ? 0x80 : 0) | (m & 127)); m >>= 7; }
+}
+__device__ __forceinline__ void ospan(OS &s, uint32_t a, uint32_t n) {  // LDS bytes [a, a + n)
+  if (s.n + n <= s.cap) lds_copy(s.a + s.n, a, n);
+  s.n += n;
+}
+// LDS bytes [src, src + n) to dst <= src (ascending 8-byte chunks: safe when the regions overlap)
+__device__ __forceinline__ void lds_move_down(uint32_t dst, uint32_t src, uint32_t n) {
+  if (dst == src) return;
+  lds_copy(dst, src, n);
+}
+struct UE { uint32_t s, n; };             // UintOptRleEncoder
+struct IE { uint32_t s, n; int32_t d; };  // IntDiffOptRleEncoder
+struct RE { uint32_t s, n; };             // RleEncoder<u8> (n == 0: nothing written yet)
+__device__ __forceinline__ void ue_flush(OS &o, const UE &e) {
+  if (e.n > 0) {
+    ovi(o, e.n != 1, e.s);  // count == 1 ? s : -s (-0 for 0)
+    if (e.n > 1) ovu(o, e.n - 2);
+  }
+}
+__device__ __forceinline__ void ue_w(OS &o, UE &e, uint32_t v) {
+  if (e.s == v) { e.n++; return; }
+  ue_flush(o, e);
+  e.s = v;
+  e.n = 1;
+}
+__device__ __forceinline__ void ie_flush(OS &o, const IE &e) {
+  if (e.n > 0) {
+    const int32_t x = (int32_t)((uint32_t)e.d << 1) | (e.n == 1 ? 0 : 1);
+    ovi(o, x < 0, x < 0 ? (uint32_t)(-(int64_t)x) : (uint32_t)x);
+    if (e.n > 1) ovu(o, e.n - 2);
+  }
+}
+__device__ __forceinline__ void ie_w(OS &o, IE &e, uint32_t v, bool &bad) {
+  const int64_t d = (int64_t)v - (int64_t)e.s;
+  bad |= d < -(1ll << 30) || d >= (1ll << 30);  // JS `diff << 1` wraps beyond
+  if (e.d == (int32_t)d) { e.s = v; e.n++; return; }
+  ie_flush(o, e);
+  e.s = v;
+  e.n = 1;
+  e.d = (int32_t)d;
+}
+__device__ __forceinline__ void re_w(OS &o, RE &e, uint32_t v) {
+  if (e.n > 0 && e.s == v) { e.n++; return; }
+  if (e.n > 0) ovu(o, e.n - 1);
+  ob(o, v);
+  e.s = v;
+  e.n = 1;
+}
+// output streams: the nine columns (the string column as body + lengths) and the rest stream of the parts
+enum { S_KC = 0, S_CL, S_LC, S_RC, S_IN, S_SB, S_SL, S_PI, S_TR, S_LN, S_RE, NS };
+
+// Column cursors with their next 8 bytes already in registers: the refill load is issued as soon as a value
+// is consumed and waited for only at the column's next read (usually a struct later), so a struct's chain of
+// column reads does not wait on one LDS round trip per field.
+struct PC { uint32_t p, e; bool bad; uint64_t w; };
+__device__ __forceinline__ PC pc_make(const Cur &c) { return PC{c.p, c.e, c.bad, ld8(c.p)}; }
+__device__ __forceinline__ void pc_adv(PC &c, uint32_t nb) { c.p += nb; c.w = ld8(c.p); }
+__device__ __forceinline__ uint32_t pc_vu(PC &c) {  // rvu
+  const uint32_t lo = (uint32_t)c.w, hi = (uint32_t)(c.w >> 32);
+  if (__all((lo & 0x80u) == 0)) {
+    c.bad |= c.p >= c.e;
+    pc_adv(c, 1);
+    return lo & 0x7fu;
+  }
+  const uint32_t nb = vu_nb(lo, hi);
+  const uint32_t v = (lo & 0x7fu) | ((lo >> 1) & 0x3f80u) | ((lo >> 2) & 0x1fc000u) | ((lo >> 3) & 0xfe00000u) | (hi << 28);
+  const uint32_t m = (uint32_t)((1ull << (7 * (nb < 5 ? nb : 5))) - 1);
+  c.bad |= vu_bad(lo, hi, nb, c.p, c.e);
+  pc_adv(c, nb < 6 ? nb : 0);
+  return v & m;
+}
+__device__ __forceinline__ uint32_t pc_vi(PC &c, bool &neg) {  // rvi
+  const uint32_t lo = (uint32_t)c.w, hi = (uint32_t)(c.w >> 32);
+  neg = (lo & 0x40) != 0;
+  if (__all((lo & 0x80u) == 0)) {
+    c.bad |= c.p >= c.e;
+    pc_adv(c, 1);
+    return lo & 0x3fu;
+  }
+  const uint32_t nb = vu_nb(lo, hi);
+  uint32_t m = (lo & 0x3fu) | ((lo >> 2) & 0x1fc0u) | ((lo >> 3) & 0xfe000u) | ((lo >> 4) & 0x7f00000u) | ((hi & 0x7fu) << 27);
+  const uint32_t bits = 6 + 7 * (nb - 1);
+  if (nb < 5) m &= (1u << bits) - 1u;
+  c.bad |= (nb > 5) | (c.p + nb > c.e) | ((nb == 5) & ((hi & 0x7fu) > 0x1fu));
+  pc_adv(c, nb < 6 ? nb : 0);
+  return m;
+}
+__device__ __forceinline__ uint32_t pc_b(PC &c) {  // rdb
+  c.bad |= c.p >= c.e;
+  const uint32_t v = (uint32_t)c.w & 0xffu;
+  pc_adv(c, 1);
+  return v;
+}
+struct PRle { PC c; uint32_t s, n; };
+struct PUopt { PC c; uint32_t s, n; };
+struct PIdif { PC c; uint32_t s, n; int32_t d; };
+__device__ __forceinline__ uint32_t pd_rle(PRle &r) {  // rd_rle
+  if (r.n == 0) {
+    r.s = pc_b(r.c);
+    r.n = r.c.p < r.c.e ? pc_vu(r.c) + 1 : 0xffffffffu;  // the final run never ends
+  }
+  if (r.n != 0xffffffffu) r.n--;
+  return r.s;
+}
+__device__ __forceinline__ uint32_t pd_uopt(PUopt &r) {  // rd_uopt
+  if (r.n == 0) {
+    bool neg;
+    r.s = pc_vi(r.c, neg);
+    r.n = neg ? pc_vu(r.c) + 2 : 1;
+  }
+  r.n--;
+  return r.s;
+}
+__device__ __forceinline__ uint32_t pd_idif(PIdif &r) {  // rd_idif
+  if (r.n == 0) {
+    bool neg;
+    const uint32_t m = pc_vi(r.c, neg);
+    const int32_t t = (int32_t)(neg ? 0u - m : m);
+    r.d = t >> 1;
+    r.n = (t & 1) ? pc_vu(r.c) + 2 : 1;
+  }
+  const int64_t v = (int64_t)r.s + r.d;
+  r.c.bad |= v < 0 || v > 0xffffffffll;
+  r.s = (uint32_t)v;
+  r.n--;
+  return r.s;
+}
+}  // namespace df2
+
+template <uint32_t ND, uint32_t WIN, uint32_t POOL, int OCC>
+__global__ void __launch_bounds__(64, OCC) k_diff_small_v2(GeneralJob j, uint8_t *done) {
+  using namespace df2;
+  using L = Df2Lay<ND, WIN, POOL>;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t d0 = blockIdx.x * ND, d = d0 + lane;
+  if (d0 >= j.n) return;
+  const uint32_t dn = j.n - d0 < ND ? j.n - d0 : ND;
+  // the windows: the ND updates and their state vectors (each contiguous in a packed batch)
+  const uint64_t w0 = j.upd_off[j.doc_upd[d0]] & ~15ull, wend = j.upd_off[j.doc_upd[d0 + dn]];
+  const uint32_t wbytes = (uint32_t)((wend - w0 < WIN ? wend - w0 : WIN) + 15) & ~15u;
+  const uint64_t v0 = j.sv_off[d0] & ~15ull, vend = j.sv_off[d0 + dn];
+  const uint32_t vbytes = (uint32_t)((vend - v0 < L::SVW ? vend - v0 : L::SVW) + 15) & ~15u;
+  {
+    const uint4 *src = reinterpret_cast<const uint4 *>(j.A + w0);
+    for (uint32_t v = lane; v < wbytes / 16; v += 64) at<uint4>(16 * v) = src[v];
+    const uint4 *svs = reinterpret_cast<const uint4 *>(j.sv + v0);
+    for (uint32_t v = lane; v < vbytes / 16; v += 64) at<uint4>(L::SV + 16 * v) = svs[v];
+  }
+  __syncthreads();
+  bool ok = false;
+  uint32_t p0 = 0, p1 = 0, s0 = 0, s1 = 0;
+  if (lane < dn) {
+    const uint32_t u0 = j.doc_upd[d];
+    if (j.doc_upd[d + 1] - u0 == 1 && !done[d]) {
+      const uint64_t a = j.upd_off[u0], b = j.upd_off[u0 + 1], sa = j.sv_off[d], sb = j.sv_off[d + 1];
+      ok = a >= w0 && b <= w0 + wbytes && b > a && sa >= v0 && sb <= v0 + vbytes && sb >= sa;
+      p0 = (uint32_t)(a - w0); p1 = (uint32_t)(b - w0);
+      s0 = L::SV + (uint32_t)(sa - v0); s1 = L::SV + (uint32_t)(sb - v0);
+    }
+  }
+  // decline reasons (done[d], read by ym__pv2_done): 2 not in the windows / several updates, 3 state vector,
+  // 4 header, 5 output pool, 6 walk, 7 delete set, 8 stream overflow, 9 in-place assembly
+  uint32_t why = ok ? 0 : 2;
+  const uint32_t svt = L::SVT + 8 * L::NSV * (lane < ND ? lane : 0);
+  const uint32_t pt = L::PT + 16 * L::NPART * (lane < ND ? lane : 0);
+  // decodeStateVector into the lane's table (a later entry for a client wins: the lookup scans backwards)
+  uint32_t nsv = 0;
+  if (ok) {
+    Cur c = {s0, s1, false};
+    const uint32_t n = rvu(c);
+    ok = !c.bad && n <= L::NSV;
+    for (uint32_t i = 0; ok && i < n; i++) {
+      const uint32_t cl = rvu(c), ck = rvu(c);
+      at<uint2>(svt + 8 * i) = make_uint2(cl, ck);
+    }
+    ok &= !c.bad;
+    nsv = n;
+    if (!ok && !why) why = 3;
+  }
+  // header: the nine column spans, the ASCII string body, the rest stream's client count
+  Cur col[9], c = {0, 0, false};
+  uint32_t sn = 0, sb = 0, nclients = 0, need = 0;
+  uint32_t in_sz[NS];
+  if (ok) {
+    Cur h = {p0, p1, false};
+    rvu(h);  // feature flag
+#pragma unroll
+    for (uint32_t k = 0; k < 9; k++) {
+      const uint32_t n = rvu(h);
+      ok &= room(h, n);
+      col[k] = Cur{h.p, h.p + n, false};
+      h.p += ok ? n : 0;
+    }
+    ok &= !h.bad;
+    sn = rvu(col[5]);
+    ok &= !col[5].bad && room(col[5], sn);
+    sb = col[5].p;
+    if (ok) {
+      uint64_t hi = 0;
+      for (uint32_t o = 0; o < sn; o += 8) hi |= mask_bytes(ld8(sb + o), sn - o);
+      ok &= (hi & 0x8080808080808080ull) == 0;
+      col[5].p += sn;
+    }
+    c = h;  // rest stream
+    nclients = rvu(c);
+    ok &= !c.bad && nclients <= L::NPART;
+    const uint32_t slack = 8 + 16 * nclients;
+    in_sz[S_KC] = col[0].e - col[0].p; in_sz[S_CL] = col[1].e - col[1].p; in_sz[S_LC] = col[2].e - col[2].p;
+    in_sz[S_RC] = col[3].e - col[3].p; in_sz[S_IN] = col[4].e - col[4].p; in_sz[S_SB] = sn;
+    in_sz[S_SL] = col[5].e - col[5].p; in_sz[S_PI] = col[6].e - col[6].p; in_sz[S_TR] = col[7].e - col[7].p;
+    in_sz[S_LN] = col[8].e - col[8].p; in_sz[S_RE] = p1 - c.p;
+#pragma unroll
+    for (uint32_t k = 0; k < NS; k++) { in_sz[k] += (in_sz[k] >> 3) + slack; need += in_sz[k]; }
+    need = (need + 16 + 15) & ~15u;  // (16 bytes ahead of the streams: the output is assembled in place)
+    if (!ok && !why) why = 4;
+  }
+  // the lanes' output streams out of the pool
+  const uint32_t incl = wave_incl_add(ok ? need : 0);
+  ok &= incl <= POOL;
+  if (!ok && !why) why = 5;
+  OS os[NS];
+  {
+    uint32_t a = L::OUT + incl - (ok ? need : 0) + 16;
+#pragma unroll
+    for (uint32_t k = 0; k < NS; k++) { os[k] = OS{a, 0, ok ? in_sz[k] : 0}; a += ok ? in_sz[k] : 0; }
+  }
+  PIdif kc = {pc_make(col[0]), 0, 0, 0};
+  PUopt cl = {pc_make(col[1]), 0, 0};
+  PIdif lc = {pc_make(col[2]), 0, 0, 0}, rc = {pc_make(col[3]), 0, 0, 0};
+  PRle in = {pc_make(col[4]), 0, 0};
+  PUopt sl = {pc_make(col[5]), 0, 0};
+  PRle pi_ = {pc_make(col[6]), 0, 0};
+  PUopt tr = {pc_make(col[7]), 0, 0}, ln = {pc_make(col[8]), 0, 0};
+  UE e_cl = {0, 0}, e_sl = {0, 0}, e_tr = {0, 0}, e_ln = {0, 0};
+  IE e_kc = {0, 0, 0}, e_lc = {0, 0, 0}, e_rc = {0, 0, 0};
+  RE e_in = {0, 0}, e_pi = {0, 0};
+  uint32_t spos = 0, keys = 0, kclock = 0, nparts = 0, prev_client = 0;
+  bool bad = !ok;
+  auto rstr = [&](uint32_t &a, uint32_t &n) {  // StringDecoder.read(): an ASCII byte slice of the body
+    n = pd_uopt(sl);
+    bad |= spos + n > sn;
+    a = sb + spos;
+    spos += n;
+  };
+  auto wstr = [&](uint32_t a, uint32_t n) {  // StringEncoder.write
+    ospan(os[S_SB], a, n);
+    ue_w(os[S_SL], e_sl, n);
+  };
+  auto wkey = [&]() {  // writeKey: keyClock++ (never cached, E9)
+    ie_w(os[S_KC], e_kc, kclock, bad);
+    kclock++;
+  };
+  for (uint32_t ci = 0; ci < nclients && !bad; ci++) {
+    const uint32_t nstructs = rvu(c);
+    const uint32_t client = pd_uopt(cl);
+    uint32_t clock = rvu(c);
+    bad |= ci > 0 && client >= prev_client;  // a repeated or ascending client: k_big_v2
+    prev_client = client;
+    uint32_t k = 0;  // state.get(client) || 0
+    for (uint32_t i = nsv; i-- > 0;) {
+      const uint2 e = at<uint2>(svt + 8 * i);
+      if (e.x == client) { k = e.y; break; }
+    }
+    bool copying = false;
+    uint32_t written = 0, prest0 = 0;
+    for (uint32_t si = 0; si < nstructs && !bad; si++) {
+      const uint32_t info = pd_rle(in);
+      bad |= info == 10 || (info & 31) == 0 || info > 255;  // Skip / GC inputs: k_big_v2
+      // the struct (LazyStructReader): what Item.write needs to re-encode it
+      uint32_t oc = 0, ok_ = 0, rcl = 0, rk = 0, pi = 0, ya = 0, yn = 0, pc = 0, pk = 0, pa = 0, pn = 0;
+      uint32_t ca = 0, cn = 0, ka = 0, kn = 0, t = 0, r0 = 0, r1 = 0, len = 1;
+      if (info & 0x80) { oc = pd_uopt(cl); ok_ = pd_idif(lc); }
+      if (info & 0x40) { rcl = pd_uopt(cl); rk = pd_idif(rc); }
+      if ((info & 0xC0) == 0) {
+        pi = pd_rle(pi_) == 1 ? 1 : 0;
+        if (pi) rstr(ya, yn);
+        else { pc = pd_uopt(cl); pk = pd_idif(lc); }
+        if (info & 0x20) rstr(pa, pn);
+      }
+      switch (info & 31) {
+        case 1: len = pd_uopt(ln); break;  // ContentDeleted
+        case 3: {                          // ContentBinary: rest varUint8Array
+          r0 = c.p;
+          const uint32_t n = rvu(c);
+          if (!room(c, n)) bad = true;
+          else c.p += n;
+          r1 = c.p;
+          break;
+        }
+        case 4: rstr(ca, cn); len = cn; break;  // ContentString
+        case 5: case 6:                         // Embed / Format: rest any (Format reads its key as a string)
+          if ((info & 31) == 6) rstr(ka, kn);
+          r0 = c.p;
+          any_canon<true>(c);
+          r1 = c.p;
+          break;
+        case 7:  // ContentType
+          t = pd_uopt(tr);
+          bad |= t > 6;
+          if (t == 3 || t == 5) {  // readKey: a cached key (keyClock < keys read) reads no string
+            bad |= pd_idif(kc) < keys;
+            keys++;
+            rstr(ka, kn);
+          }
+          break;
+        case 8:  // ContentAny: len column + rest values
+          len = pd_uopt(ln);
+          r0 = c.p;
+          for (uint32_t i = 0; i < len && !c.bad; i++) any_canon<true>(c);
+          r1 = c.p;
+          break;
+        default: bad = true; break;  // ContentJSON, ContentDoc, invalid refs
+      }
+      bad |= c.bad | (len == 0) | ((uint64_t)clock + len > 0xffffffffull);
+      if (bad) break;
+      uint32_t off = 0;
+      bool wr = copying;
+      if (!copying && clock + len > k) {  // the cut (us@40707): LazyStructWriter starts a part
+        copying = true;
+        wr = true;
+        written = 0;
+        off = k > clock ? k - clock : 0;
+        ue_w(os[S_CL], e_cl, client);
+        prest0 = os[S_RE].n;
+        ovu(os[S_RE], clock + off);
+      }
+      if (wr) {  // Item.write(encoder, off) (k_big_v2 v2_write)
+        written++;
+        const uint32_t ref = info & 31;
+        const bool noorig = (info & 0xC0) == 0;
+        bad |= off > 0 && ref != 1 && ref != 4 && ref != 8;
+        const bool has_o = off > 0 || (info & 0x80);
+        re_w(os[S_IN], e_in, ref | (has_o ? 0x80 : 0) | (info & 0x40) | (noorig ? (info & 0x20) : 0));
+        if (off > 0) { ue_w(os[S_CL], e_cl, client); ie_w(os[S_LC], e_lc, clock + off - 1, bad); }
+        else if (info & 0x80) { ue_w(os[S_CL], e_cl, oc); ie_w(os[S_LC], e_lc, ok_, bad); }
+        if (info & 0x40) { ue_w(os[S_CL], e_cl, rcl); ie_w(os[S_RC], e_rc, rk, bad); }
+        if (!has_o && !(info & 0x40)) {
+          re_w(os[S_PI], e_pi, pi);
+          if (pi) wstr(ya, yn);
+          else { ue_w(os[S_CL], e_cl, pc); ie_w(os[S_LC], e_lc, pk, bad); }
+          if (info & 0x20) wstr(pa, pn);
+        }
+        switch (ref) {
+          case 1: ue_w(os[S_LN], e_ln, len - off); break;
+          case 3: case 5: ospan(os[S_RE], r0, r1 - r0); break;
+          case 4: wstr(ca + off, cn - off); break;
+          case 6: wkey(); wstr(ka, kn); ospan(os[S_RE], r0, r1 - r0); break;
+          case 7:
+            ue_w(os[S_TR], e_tr, t);
+            if (t == 3 || t == 5) { wkey(); wstr(ka, kn); }
+            break;
+          case 8: {
+            ue_w(os[S_LN], e_ln, len - off);
+            Cur v = {r0, r1, false};  // ContentAny.splice: drop `off` values
+            for (uint32_t i = 0; i < off; i++) any_canon<true>(v);
+            bad |= v.bad;
+            ospan(os[S_RE], v.p, r1 - v.p);
+            break;
+          }
+        }
+      }
+      clock += len;
+    }
+    if (copying && !bad) {
+      bad |= nparts >= L::NPART;
+      if (!bad) at<uint4>(pt + 16 * nparts) = make_uint4(prest0, os[S_RE].n, written, 0);
+      nparts++;
+    }
+  }
+  bad |= c.bad | cl.c.bad | lc.c.bad | rc.c.bad | in.c.bad | sl.c.bad | pi_.c.bad | tr.c.bad | ln.c.bad | kc.c.bad;
+  if (bad && !why) why = 6;
+  // the delete set (rest stream): validated, then copied (readDeleteSet / writeDeleteSet round-trip it)
+  const uint32_t ds0 = c.p;
+  if (!bad) {
+    const uint32_t ndc = rvu(c);
+    bad |= ndc > L::NSV;
+    for (uint32_t i = 0; i < ndc && !bad && !c.bad; i++) {
+      const uint32_t client = rvu(c), m = rvu(c);
+      bad |= m == 0;  // readDeleteSet drops a client without ranges: the bytes would change
+      for (uint32_t q = 0; q < i; q++) bad |= at<uint32_t>(svt + 4 * q) == client;  // a repeated client merges
+      at<uint32_t>(svt + 4 * i) = client;
+      for (uint32_t q = 0; q < m && !c.bad; q++) { rvu(c); rvu(c); }
+    }
+    bad |= c.bad;
+    if (bad && !why) why = 7;
+  }
+  const uint32_t ds1 = c.p;
+  // lib0 toUint8Array: Uint / IntDiff runs flushed, the Rle<u8> final counts omitted
+  ie_flush(os[S_KC], e_kc);
+  ue_flush(os[S_CL], e_cl);
+  ie_flush(os[S_LC], e_lc);
+  ie_flush(os[S_RC], e_rc);
+  ue_flush(os[S_SL], e_sl);
+  ue_flush(os[S_TR], e_tr);
+  ue_flush(os[S_LN], e_ln);
+#pragma unroll
+  for (uint32_t k = 0; k < NS; k++) bad |= os[k].n > os[k].cap;
+  if (bad && !why) why = 8;
+  // the output: vu(0) | 9 x (vu(n) column) | vu(#parts) parts | delete set
+  uint32_t coln[9];
+  coln[0] = os[S_KC].n; coln[1] = os[S_CL].n; coln[2] = os[S_LC].n; coln[3] = os[S_RC].n; coln[4] = os[S_IN].n;
+  coln[5] = vsz(os[S_SB].n) + os[S_SB].n + os[S_SL].n; coln[6] = os[S_PI].n; coln[7] = os[S_TR].n; coln[8] = os[S_LN].n;
+  uint32_t total = 0;
+  if (!bad) {
+    total = 1 + vsz(nparts) + (ds1 - ds0);
+#pragma unroll
+    for (uint32_t q = 0; q < 9; q++) total += vsz(coln[q]) + coln[q];
+    for (uint32_t q = 0; q < nparts; q++) {
+      const uint4 e = at<uint4>(pt + 16 * q);
+      total += vsz(e.z) + e.y - e.x;
+    }
+  }
+  // assemble the output in place: each piece moves down to the end of what precedes it (the 16 bytes
+  // ahead of the streams and every stream's slack hold the varuint headers); the delete set comes from the
+  // input window
+  const uint32_t area = os[S_KC].a - 16;
+  if (!bad) {
+    bad |= total + 16 > os[S_RE].a + os[S_RE].cap - area;  // (cannot happen: the slack covers the headers)
+  }
+  if (!bad) {
+    uint32_t p = area;
+    auto put = [&](uint32_t v) { while (v > 127) { at<uint8_t>(p++) = (uint8_t)(0x80 | (v & 127)); v >>= 7; } at<uint8_t>(p++) = (uint8_t)v; };
+    // a piece moves only downwards; a header that reached into a piece not yet moved declines the document
+    // (k_big_v2 reads the input from HBM, so the half-assembled area is simply dropped)
+    auto mv = [&](uint32_t src, uint32_t n) {
+      bad |= p > src;
+      if (!bad) lds_move_down(p, src, n);
+      p += n;
+    };
+    put(0);
+#pragma unroll
+    for (uint32_t q = 0; q < 9; q++) {
+      put(coln[q]);
+      if (q == 5) {
+        put(os[S_SB].n);
+        mv(os[S_SB].a, os[S_SB].n);
+        mv(os[S_SL].a, os[S_SL].n);
+      } else {
+        const uint32_t k = q == 0 ? S_KC : q == 1 ? S_CL : q == 2 ? S_LC : q == 3 ? S_RC : q == 4 ? S_IN : q == 6 ? S_PI : q == 7 ? S_TR : S_LN;
+        mv(os[k].a, os[k].n);
+      }
+    }
+    put(nparts);
+    for (uint32_t q = 0; q < nparts; q++) {
+      const uint4 e = at<uint4>(pt + 16 * q);
+      put(e.z);
+      mv(os[S_RE].a + e.x, e.y - e.x);
+    }
+    if (!bad) lds_copy(p, ds0, ds1 - ds0);
+    if (bad && !why) why = 9;
+  }
+  // sizes: one bump allocation per wave; every output starts 16-byte aligned (the cooperative copy's stores)
+  const uint32_t total16 = bad ? 0 : (total + 15) & ~15u;
+  const uint32_t oincl = wave_incl_add(total16), otot = lane_read(oincl, 63);
+  uint64_t base = 0;
+  if (lane == 0 && otot) base = atomicAdd((unsigned long long *)j.used, (unsigned long long)otot + 15);
+  base = ((uint64_t)lane_read((uint32_t)(base >> 32), 0) << 32) | lane_read((uint32_t)base, 0);
+  base = (base + 15) & ~15ull;
+  const uint64_t off = base + oincl - total16;
+  const bool fits = off + total16 <= j.cap;
+  if (bad && lane < dn && why) done[d] = (uint8_t)why;
+  if (!bad) {
+    done[d] = 1;
+    if (fits) {
+      j.out_off[d] = off;
+      j.out_len[d] = total;
+      j.status[d] = ym::ST_OK;
+    } else {
+      j.status[d] = ym::ST_CAPACITY;
+      j.out_len[d] = 0;
+    }
+  }
+  // the wave copies each completed output out of LDS with 16-byte accesses
+  for (uint32_t q = 0; q < dn; q++) {
+    const uint32_t n = lane_read(bad || !fits ? 0 : total16, q);
+    if (n == 0) continue;
+    const uint32_t src = lane_read(area, q);
+    const uint64_t dst = ((uint64_t)lane_read((uint32_t)(off >> 32), q) << 32) | lane_read((uint32_t)off, q);
+    for (uint32_t k = lane; k < n / 16; k += 64)
+      *reinterpret_cast<uint4 *>(j.out + dst + 16 * k) = at<uint4>(src + 16 * k);
+  }
+}
+
 }  // namespace fastv2
 
 // parseUpdateMetaV2 / encodeStateVectorFromUpdateV2 over small single updates, one per lane (k_small_v2);
 // done: the streamed walker's done array (nullptr: the kernel is the call's only specialised pass, its
 // declines go to the general path).  Meta: 64 updates of an update log per wave (4 KB window); state
 // vectors: 16 merged documents per wave (~1 KB each: a 24 KB window, 32 sections each).
-int small_v2_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t st) {
+int small_v2_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t st, uint32_t diff_min) {
   static const bool off = getenv("YMERGE_NO_SMALL_V2") != nullptr;
   if (off || !j.v2 || j.n == 0) return 0;
   using namespace fastv2;
@@ -1143,6 +1661,14 @@ int small_v2_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t
     k_small_v2<OP_META, 64, 4096, 8><<<(j.n + 63) / 64, 64, Sv2Lay<64, 4096, 8>::BYTES, st>>>(j, done);
   } else if (op == OP_SV) {
     k_small_v2<OP_SV, 16, 24576, 32><<<(j.n + 15) / 16, 64, Sv2Lay<16, 24576, 32>::BYTES, st>>>(j, done);
+  } else if (op == OP_DIFF && done && j.sv) {
+    // 4 documents per wave (measured on C2: 0.93 ms per 10 k documents; 8 per wave 1.08, 2 per wave 0.96, 1 per
+    // wave 1.48; a 128-VGPR build spills and loses).  Below `diff_min` documents the one-wave walker's single
+    // generation is the faster engine (C2R / C4R, 4 k documents: 1.2 / 1.8 ms against 2.2 / 2.5 ms with this
+    // kernel in front of it), so the kernel runs only for larger batches.
+    if (const char *e = getenv("YMERGE_DF2_MIN")) diff_min = (uint32_t)strtoul(e, nullptr, 10);  // (tests: 0)
+    if (j.n < diff_min || getenv("YMERGE_NO_DF2")) return 0;
+    k_diff_small_v2<4, 6144, 8192, 1><<<(j.n + 3) / 4, 64, Df2Lay<4, 6144, 8192>::BYTES, st>>>(j, done);
   } else {
     return 0;
   }

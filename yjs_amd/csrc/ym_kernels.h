@@ -103,7 +103,8 @@ int pw_small_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t
 int segsort_pairs(const uint64_t *ki, const uint32_t *vi, uint64_t *ko, uint32_t *vo, uint64_t *kt, uint32_t *vt,
                   const uint32_t *seg_b, const uint32_t *seg_e, uint32_t nseg, hipStream_t st);
 // The same for V2 (ym_pv2.hip): column-parallel diff / sv over large single-section documents.
-int pv2_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const uint8_t **done);
+int pv2_prepare(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const uint8_t **done);
+int pv2_finish(const GeneralJob &j, hipStream_t st, PwBufs &B);
 
 using ym::GeneralWsSize;
 using ym::general_ws_size;

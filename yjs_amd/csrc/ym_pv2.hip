@@ -793,13 +793,31 @@ int pv_ensure(PwBufs &B, int k, size_t n) {
 // several sections: ym_pv2ms.hip); marks the documents it completes in *done_out (k_big_v2 skips them).
 // 1 = launched, 0 = not applicable, < 0 = error.
 static pv2::Meta *pv2_last_meta = nullptr;
-int pv2_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const uint8_t **done_out) {
+static const uint8_t *pv2_last_done = nullptr;
+namespace pv2 {
+// the scanned totals (scratch bytes of the single- and multi-section documents) straight into the coherent
+// pinned host words pv2_finish reads (a copy op would hold the stream ~25 us)
+__global__ void k_v2_totals(const uint64_t *t0, const uint64_t *t1, uint64_t *host) {
+  if (threadIdx.x == 0) { host[0] = *t0; host[1] = *t1; }
+}
+}  // namespace pv2
+// Step 1: the per-document prep and the scans of its scratch sizes; every document is marked not done
+// (*done_out) and the totals start towards the host.  The small documents' kernels are enqueued next (their
+// work hides that round trip; the column path only takes documents of >= PV_MIN bytes, beyond their windows).
+int pv2_prepare(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const uint8_t **done_out) {
   using namespace pv2;
   *done_out = nullptr;
+  B.pending = false;
   if (!j.v2 || (op != OP_DIFF && op != OP_SV && op != OP_META) || j.n == 0 || !j.pw_count || getenv("YMERGE_NO_PW")) return 0;
   uint64_t pv_min = PV_MIN;
   if (const char *e = getenv("YMERGE_PW_MIN")) pv_min = strtoull(e, nullptr, 10);
-  if (!B.pinned && hipHostMalloc((void **)&B.pinned, 64, hipHostMallocDefault) != hipSuccess) return -2;
+  if (!B.pinned_dev) {
+    if (B.pinned) hipHostFree(B.pinned);
+    B.pinned = nullptr;
+    if (hipHostMalloc((void **)&B.pinned, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return -2;
+    if (hipHostGetDevicePointer((void **)&B.pinned_dev, B.pinned, 0) != hipSuccess) return -2;
+  }
+  if (!B.ev && hipEventCreateWithFlags(&B.ev, hipEventDisableTiming) != hipSuccess) return -2;
   const uint32_t n1 = j.n + 1;
   if (pv_ensure(B, 0, sizeof(Meta) * (uint64_t)j.n + 32ull * n1 + j.n + 64)) return -2;
   Job J;
@@ -807,41 +825,55 @@ int pv2_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const u
   J.meta = (Meta *)B.p[0];
   uint64_t *sizes = (uint64_t *)(J.meta + j.n), *offs = sizes + n1, *sizes1 = offs + n1, *offs1 = sizes1 + n1;
   J.done = (uint8_t *)(offs1 + n1);
-  J.scr = nullptr;
-  J.scr1 = nullptr;
   pv2_last_meta = J.meta;
+  pv2_last_done = J.done;
   k_v2_prep<<<(n1 + 255) / 256, 256, 0, st>>>(J, pv_min, sizes, sizes1);
   size_t tmp = 0;
   scan_excl<uint64_t>(nullptr, tmp, sizes, offs, n1, st);
   if (pv_ensure(B, 1, tmp + 16)) return -2;
   if (scan_excl<uint64_t>(B.p[1], tmp, sizes, offs, n1, st)) return -3;
   if (scan_excl<uint64_t>(B.p[1], tmp, sizes1, offs1, n1, st)) return -3;
-  if (hipMemcpyAsync(B.pinned, offs + j.n, 8, hipMemcpyDeviceToHost, st) != hipSuccess) return -3;
-  if (hipMemcpyAsync(B.pinned + 2, offs1 + j.n, 8, hipMemcpyDeviceToHost, st) != hipSuccess) return -3;
-  if (hipStreamSynchronize(st) != hipSuccess) return -3;
-  uint64_t total = *(uint64_t *)B.pinned;
-  const uint64_t total1 = *(uint64_t *)(B.pinned + 2);
+  k_v2_totals<<<1, 64, 0, st>>>(offs + j.n, offs1 + j.n, (uint64_t *)B.pinned_dev);
+  if (hipEventRecord(B.ev, st) != hipSuccess) return -3;
   *done_out = J.done;
+  B.pending = true;
+  B.op = op;
+  return 1;
+}
+// Step 2: waits for the totals, then the column path over the large documents (documents it completes get
+// done[d] = 1; what it leaves stays 0 for k_big_v2).
+int pv2_finish(const GeneralJob &j, hipStream_t st, PwBufs &B) {
+  using namespace pv2;
+  if (!B.pending) return 0;
+  B.pending = false;
+  const uint32_t op = B.op, n1 = j.n + 1;
+  Job J;
+  J.j = j;
+  J.meta = (Meta *)B.p[0];
+  uint64_t *sizes = (uint64_t *)(J.meta + j.n), *offs = sizes + n1, *sizes1 = offs + n1, *offs1 = sizes1 + n1;
+  J.done = (uint8_t *)(offs1 + n1);
+  J.scr = nullptr;
+  J.scr1 = nullptr;
+  size_t tmp = 0;
+  scan_excl<uint64_t>(nullptr, tmp, sizes, offs, n1, st);
+  if (hipEventSynchronize(B.ev) != hipSuccess) return -3;  // (the small documents' kernels run meanwhile)
+  uint64_t total, total1;
+  __builtin_memcpy(&total, B.pinned, 8);
+  __builtin_memcpy(&total1, B.pinned + 2, 8);
   bool ms = total1 > 0;
-  if (ms && pv_ensure(B, 3, total1 + 256)) {
-    hipMemsetAsync(J.done, 0, j.n, st);
-    return 1;
-  }
+  if (ms && pv_ensure(B, 3, total1 + 256)) return 1;  // no room: k_big_v2 takes the large documents
   if (ms) {  // multi-section documents: the rest walk counts their structs, then their value arrays are sized
     J.scr1 = (uint8_t *)B.p[3];
     k_v2_meta_off<<<(j.n + 255) / 256, 256, 0, st>>>(J, offs1, 1);
     ms_rest(J, st);
     ms_sizes(J, sizes, st);
     if (scan_excl<uint64_t>(B.p[1], tmp, sizes, offs, n1, st)) return -3;
-    if (hipMemcpyAsync(B.pinned, offs + j.n, 8, hipMemcpyDeviceToHost, st) != hipSuccess) return -3;
+    k_v2_totals<<<1, 64, 0, st>>>(offs + j.n, offs1 + j.n, (uint64_t *)B.pinned_dev);
     if (hipStreamSynchronize(st) != hipSuccess) return -3;
-    total = *(uint64_t *)B.pinned;
+    __builtin_memcpy(&total, B.pinned, 8);
   }
   if (total == 0) return 1;
-  if (pv_ensure(B, 2, total + 256)) {
-    hipMemsetAsync(J.done, 0, j.n, st);
-    return 1;
-  }
+  if (pv_ensure(B, 2, total + 256)) return 1;  // no room: k_big_v2 takes them (done stays 0)
   J.scr = (uint8_t *)B.p[2];
   k_v2_meta_off<<<(j.n + 255) / 256, 256, 0, st>>>(J, offs, 0);
   const dim3 g1((j.n + 63) / 64, NK1);
@@ -865,6 +897,11 @@ int pv2_run(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const u
 // debugging aid (not part of include/ymerge.h): per document of the last V2 column-path call on this
 // device, 0 = taken, 1 = not eligible, else the stage that declined it (K1: 10 + column, K2: 20-24,
 // K3: 30 + column, K4: 40 delete set / 41 spans)
+// ... and its done array (1 = completed by a specialised kernel, >= 2 = the small-document kernel's decline
+// reason, k_diff_small_v2)
+extern "C" int ym__pv2_done(uint8_t *host, uint32_t n) {
+  return ymk::pv2_last_done ? (int)hipMemcpy(host, ymk::pv2_last_done, n, hipMemcpyDeviceToHost) : -1;
+}
 extern "C" int ym__pv2_why(uint32_t *host, uint32_t n) {
   using namespace ymk;
   if (!pv2_last_meta) return -1;
