@@ -18,7 +18,21 @@
 namespace ymk {
 namespace cchk {
 
-constexpr uint32_t DEPTH = 8, KEYS = 32;
+// Nesting depth and open-object keys: the containers' state lives in registers (every array index below is a
+// select over the unrolled entries, so nothing is placed in scratch memory); deeper or wider payloads decline.
+constexpr uint32_t DEPTH = 4, KEYS = 8;
+template <uint32_t N>
+__device__ __forceinline__ uint32_t rsel(const uint32_t (&a)[N], uint32_t i) {
+  uint32_t v = a[0];
+#pragma unroll
+  for (uint32_t k = 1; k < N; k++) v = i == k ? a[k] : v;
+  return v;
+}
+template <uint32_t N>
+__device__ __forceinline__ void wsel(uint32_t (&a)[N], uint32_t i, uint32_t v) {
+#pragma unroll
+  for (uint32_t k = 0; k < N; k++) a[k] = i == k ? v : a[k];
+}
 
 __device__ __forceinline__ bool bytes_eq(const uint8_t *b, uint32_t p, uint32_t q, uint32_t n) {
   for (uint32_t i = 0; i < n; i++)
@@ -59,28 +73,31 @@ __device__ __forceinline__ bool utf8_ok(const uint8_t *b, uint32_t p, uint32_t n
   return true;
 }
 // an object key (bytes [p, p + n)) acceptable for a verbatim copy, and not among the open object's keys
-__device__ __forceinline__ bool key_ok(const uint8_t *b, uint32_t p, uint32_t n, const uint32_t *kp, const uint32_t *kl,
-                                       uint32_t k0, uint32_t nk) {
+// (entries k0 .. nk - 1 of kp / kl)
+__device__ __forceinline__ bool key_ok(const uint8_t *b, uint32_t p, uint32_t n, const uint32_t (&kp)[KEYS],
+                                       const uint32_t (&kl)[KEYS], uint32_t k0, uint32_t nk) {
   if (n > 0 && b[p] >= '0' && b[p] <= '9') return false;
   if (n == 9 && b[p] == '_' && b[p + 1] == '_' && b[p + 2] == 'p' && b[p + 3] == 'r' &&
       b[p + 4] == 'o' && b[p + 5] == 't' && b[p + 6] == 'o' && b[p + 7] == '_' && b[p + 8] == '_')
     return false;
-  for (uint32_t k = k0; k < nk; k++)
-    if (kl[k] == n && bytes_eq(b, kp[k], p, n)) return false;
-  return true;
+  bool dup = false;
+#pragma unroll
+  for (uint32_t k = 0; k < KEYS; k++)
+    if (k >= k0 && k < nk && kl[k] == n) dup |= bytes_eq(b, kp[k], p, n);
+  return !dup;
 }
 
 // One `any` value at p (< e): true and *end = its end when the bytes are what writeAny emits for it.
-__device__ __noinline__ bool any_canon_ptr(const uint8_t *b, uint32_t p, uint32_t e, uint32_t *end) {
-  uint32_t rem[DEPTH], obj[DEPTH], kp[KEYS], kl[KEYS];
+__device__ __forceinline__ bool any_canon_ptr(const uint8_t *b, uint32_t p, uint32_t e, uint32_t *end) {
+  uint32_t rem[DEPTH] = {}, obj[DEPTH] = {}, kp[KEYS] = {}, kl[KEYS] = {};
   uint32_t depth = 0, nk = 0;
   for (;;) {
-    if (depth > 0 && obj[depth - 1]) {  // an object: a key before each value
+    if (depth > 0 && rsel(obj, depth - 1)) {  // an object: a key before each value
       uint32_t n;
       if (!vu(b, p, e, n) || n > e - p) return false;
-      if (!key_ok(b, p, n, kp, kl, obj[depth - 1] - 1, nk) || !utf8_ok(b, p, n) || nk >= KEYS) return false;
-      kp[nk] = p;
-      kl[nk] = n;
+      if (nk >= KEYS || !key_ok(b, p, n, kp, kl, rsel(obj, depth - 1) - 1, nk) || !utf8_ok(b, p, n)) return false;
+      wsel(kp, nk, p);
+      wsel(kl, nk, n);
       nk++;
       p += n;
     }
@@ -141,8 +158,8 @@ __device__ __noinline__ bool any_canon_ptr(const uint8_t *b, uint32_t p, uint32_
         uint32_t n;
         if (!vu(b, p, e, n) || n > e - p || depth >= DEPTH) return false;
         if (n > 0) {
-          rem[depth] = n;
-          obj[depth] = tag == 118 ? nk + 1 : 0;
+          wsel(rem, depth, n);
+          wsel(obj, depth, tag == 118 ? nk + 1 : 0);
           depth++;
           continue;
         }
@@ -151,9 +168,12 @@ __device__ __noinline__ bool any_canon_ptr(const uint8_t *b, uint32_t p, uint32_
       default: return false;
     }
     while (depth > 0) {  // a value completed: close the containers it finished
-      if (--rem[depth - 1] > 0) break;
+      const uint32_t r = rsel(rem, depth - 1) - 1;
+      wsel(rem, depth - 1, r);
+      if (r > 0) break;
       depth--;
-      if (obj[depth]) nk = obj[depth] - 1;
+      const uint32_t o = rsel(obj, depth);
+      if (o) nk = o - 1;
     }
     if (depth == 0) { *end = p; return true; }
   }
@@ -170,18 +190,18 @@ __device__ __forceinline__ bool jstr(const uint8_t *b, uint32_t p, uint32_t e, u
   return false;
 }
 // The V1 JSON text [p, p + n) (already UTF-8-validated by the caller) in the form JSON.stringify gives.
-__device__ __noinline__ bool json_canon_ptr(const uint8_t *b, uint32_t p, uint32_t n) {
+__device__ __forceinline__ bool json_canon_ptr(const uint8_t *b, uint32_t p, uint32_t n) {
   const uint32_t e = p + n;
-  uint32_t obj[DEPTH], kp[KEYS], kl[KEYS];
+  uint32_t obj[DEPTH] = {}, kp[KEYS] = {}, kl[KEYS] = {};
   uint32_t depth = 0, nk = 0;
   for (;;) {
-    if (depth > 0 && obj[depth - 1]) {  // key ':'
+    if (depth > 0 && rsel(obj, depth - 1)) {  // key ':'
       uint32_t q;
       if (!jstr(b, p, e, q) || q >= e || b[q] != ':') return false;
       const uint32_t kn = q - p - 2;
-      if (!key_ok(b, p + 1, kn, kp, kl, obj[depth - 1] - 1, nk) || nk >= KEYS) return false;
-      kp[nk] = p + 1;
-      kl[nk] = kn;
+      if (nk >= KEYS || !key_ok(b, p + 1, kn, kp, kl, rsel(obj, depth - 1) - 1, nk)) return false;
+      wsel(kp, nk, p + 1);
+      wsel(kl, nk, kn);
       nk++;
       p = q + 1;
     }
@@ -218,7 +238,7 @@ __device__ __noinline__ bool json_canon_ptr(const uint8_t *b, uint32_t p, uint32
       if (b[p + 1] == (x == '[' ? ']' : '}')) {
         p += 2;  // an empty container
       } else {
-        obj[depth] = x == '{' ? nk + 1 : 0;
+        wsel(obj, depth, x == '{' ? nk + 1 : 0);
         depth++;
         p++;
         continue;
@@ -230,10 +250,11 @@ __device__ __noinline__ bool json_canon_ptr(const uint8_t *b, uint32_t p, uint32
       if (depth == 0) return p == e;
       if (p >= e) return false;
       if (b[p] == ',') { p++; break; }
-      if (b[p] != (obj[depth - 1] ? '}' : ']')) return false;
+      if (b[p] != (rsel(obj, depth - 1) ? '}' : ']')) return false;
       p++;
       depth--;
-      if (obj[depth]) nk = obj[depth] - 1;
+      const uint32_t o = rsel(obj, depth);
+      if (o) nk = o - 1;
     }
   }
 }

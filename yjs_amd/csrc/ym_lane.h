@@ -208,39 +208,43 @@ __device__ __forceinline__ void any_scalar(LCur &c) {
 // stored order only when no key is an array index and no key repeats, and readAny's `__proto__` key
 // mutates the prototype instead of adding a key -- so keys starting with a digit, `__proto__` and
 // repeated keys (compared byte-wise against the object's earlier keys, at most AC_KEYS open keys) are
-// rejected (the general path re-encodes those exactly).
-constexpr uint32_t AC_DEPTH = 8, AC_KEYS = 32;
+// rejected (the general path re-encodes those exactly).  The containers' state is register-resident
+// (cchk::rsel / wsel selects over unrolled entries: no scratch memory); deeper or wider values decline.
+constexpr uint32_t AC_DEPTH = cchk::DEPTH, AC_KEYS = cchk::KEYS;
 __device__ __forceinline__ bool key_eq(const uint8_t *b, uint32_t p, uint32_t q, uint32_t n) {
   for (uint32_t i = 0; i < n; i++)
     if (b[p + i] != b[q + i]) return false;
   return true;
 }
-__device__ __noinline__ void any_nested(LCur &c);
+__device__ __forceinline__ void any_nested(LCur &c);
 __device__ __forceinline__ void any_canon(LCur &c) {
   const uint32_t tag = (uint32_t)c.lo & 0xffu;
-  if (tag == 116 || tag == 117 || tag == 118 || tag == 122) any_nested(c);  // (kept out of line: its key tables)
+  if (tag == 116 || tag == 117 || tag == 118 || tag == 122) any_nested(c);
   else any_scalar(c);
 }
-__device__ __noinline__ void any_nested(LCur &c) {
-  uint32_t rem[AC_DEPTH];   // values left in each open array / object
-  uint32_t obj[AC_DEPTH];   // 1 + first key slot of an open object, 0 for an array
-  uint32_t kp[AC_KEYS], kl[AC_KEYS];
+__device__ __forceinline__ void any_nested(LCur &c) {
+  uint32_t rem[AC_DEPTH] = {};   // values left in each open array / object
+  uint32_t obj[AC_DEPTH] = {};   // 1 + first key slot of an open object, 0 for an array
+  uint32_t kp[AC_KEYS] = {}, kl[AC_KEYS] = {};
   uint32_t depth = 0, nk = 0;
   for (;;) {
     if (c.bad) return;
     // an object expects a key before each value
-    if (depth > 0 && obj[depth - 1]) {
+    if (depth > 0 && cchk::rsel(obj, depth - 1)) {
       const uint32_t n = rvu(c);
       if (c.bad || !room(c, n) || n > c.cap) { c.bad = true; return; }
       const uint32_t p = c.p;
       const uint32_t b0 = n > 0 ? (uint32_t)c.lo & 0xffu : 0;
       c.bad |= n > 0 && b0 >= '0' && b0 <= '9';
       c.bad |= n == 9 && peek8(c, 0) == 0x5f6f746f72705f5full && (uint32_t)(peek8(c, 8) & 0xff) == '_';  // "__proto__"
-      for (uint32_t k = obj[depth - 1] - 1; k < nk && !c.bad; k++) c.bad |= kl[k] == n && key_eq(c.b, kp[k], p, n);
+      const uint32_t k0 = cchk::rsel(obj, depth - 1) - 1;
+#pragma unroll
+      for (uint32_t k = 0; k < AC_KEYS; k++)
+        if (k >= k0 && k < nk && kl[k] == n && !c.bad) c.bad |= key_eq(c.b, kp[k], p, n);
       utf16_len(c, n);
       if (c.bad || nk >= AC_KEYS) { c.bad = true; return; }
-      kp[nk] = p;
-      kl[nk] = n;
+      cchk::wsel(kp, nk, p);
+      cchk::wsel(kl, nk, n);
       nk++;
     }
     const uint32_t tag = (uint32_t)c.lo & 0xffu;
@@ -249,8 +253,8 @@ __device__ __noinline__ void any_nested(LCur &c) {
       const uint32_t n = rvu(c);
       if (c.bad || n > c.cap || depth >= AC_DEPTH) { c.bad = true; return; }
       if (n > 0) {
-        rem[depth] = n;
-        obj[depth] = tag == 118 ? nk + 1 : 0;
+        cchk::wsel(rem, depth, n);
+        cchk::wsel(obj, depth, tag == 118 ? nk + 1 : 0);
         depth++;
         continue;
       }
@@ -268,9 +272,12 @@ __device__ __noinline__ void any_nested(LCur &c) {
     }
     // a value completed: close the containers it finished
     while (depth > 0 && !c.bad) {
-      if (--rem[depth - 1] > 0) break;
+      const uint32_t r = cchk::rsel(rem, depth - 1) - 1;
+      cchk::wsel(rem, depth - 1, r);
+      if (r > 0) break;
       depth--;
-      if (obj[depth]) nk = obj[depth] - 1;
+      const uint32_t o = cchk::rsel(obj, depth);
+      if (o) nk = o - 1;
     }
     if (depth == 0) return;
   }
