@@ -475,8 +475,12 @@ int big_launch(uint32_t op, const GeneralJob &j0, hipStream_t st, PwBufs &pwb) {
   // large single updates: the chunk-parallel walk first (ym_pwalk.hip); small ones one per lane
   // (ym_small.hip); k_big_v1 takes the rest (it skips what those completed)
   if (int r = pw_prepare(op, j0, st, pwb, &j.pw_done); r < 0) return r;
-  small_launch(op, j, const_cast<uint8_t *>(j.pw_done), st);
-  pw_small_launch(op, j, const_cast<uint8_t *>(j.pw_done), st);
+  // an update log (parseUpdateMeta over > 65,536 single updates, nearly all <= 80 B): the tiny lane-per-update
+  // shape alone; the 2 KB shape and k_pw_small would each spend ~0.15-0.28 ms stepping over a million
+  // documents to find none of theirs, so the rare larger update goes to k_big_v1
+  const bool log = op == OP_META && j0.n > 8 * BS_GRID;
+  small_launch(op, j, const_cast<uint8_t *>(j.pw_done), st, log);
+  if (!log) pw_small_launch(op, j, const_cast<uint8_t *>(j.pw_done), st);
   if (int r = pw_finish(j0, st, pwb); r < 0) return r;  // (waits for the prep's totals: the kernels above run)
   const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
   if (op == OP_DIFF) big::k_big_v1<OP_DIFF><<<grid, 64, big::LDS_BYTES, st>>>(j);

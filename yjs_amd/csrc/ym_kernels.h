@@ -96,7 +96,7 @@ struct PwBufs {
 int pw_prepare(uint32_t op, const GeneralJob &j, hipStream_t st, PwBufs &B, const uint8_t **done);
 int pw_finish(const GeneralJob &j, hipStream_t st, PwBufs &B);
 // Small single updates of a V1 diff / sv / meta call, one document per lane (ym_small.hip); marks done[d].
-int small_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t st);
+int small_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t st, bool tiny_only = false);
 // ... and what those left of 80 B - 4 KB: one wave per document (ym_pwalk.hip k_pw_small).
 int pw_small_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t st);
 // ym_segsort.hip: segments [seg_b[s], seg_e[s]) of (ki, vi) stably sorted by key into (ko, vo); (kt, vt) scratch

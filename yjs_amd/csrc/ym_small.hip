@@ -370,7 +370,7 @@ __global__ void __launch_bounds__(64) k_small_v1(GeneralJob j, uint8_t *done) {
 // The lane-per-document pass over the small single-update documents of a V1 diff / sv / meta call (after the
 // chunk walk, before k_big_v1, which skips what this marks done).  Two shapes: tiny updates (<= 80 bytes:
 // 64 per block, e.g. parseUpdateMeta over an update log) and small documents (<= 2 KB: 16 per block).
-int small_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t st) {
+int small_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t st, bool tiny_only) {
   using namespace smallv1;
   if (!done || j.v2 || getenv("YMERGE_NO_SMALL")) return 0;
   const uint32_t g64 = (j.n + 63) / 64, g16 = (j.n + 15) / 16;
@@ -380,7 +380,7 @@ int small_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t st
   // faster as one wave per document, k_pw_small -- a rich document's lanes diverge in the parsers)
 #define YS_LAUNCH(O)                                                                                         \
   k_small_v1<O, 64, 128, 8, 16><<<g64, 64, Lay<64, 128, 8, 16>::BYTES, st>>>(j, done);                    \
-  if (O == OP_META) k_small_v1<O, 16, 2112, 32, 32><<<g16, 64, Lay<16, 2112, 32, 32>::BYTES, st>>>(j, done);
+  if (O == OP_META && !tiny_only) k_small_v1<O, 16, 2112, 32, 32><<<g16, 64, Lay<16, 2112, 32, 32>::BYTES, st>>>(j, done);
   if (op == OP_DIFF) { YS_LAUNCH(OP_DIFF) }
   else if (op == OP_SV) { YS_LAUNCH(OP_SV) }
   else if (op == OP_META) { YS_LAUNCH(OP_META) }
