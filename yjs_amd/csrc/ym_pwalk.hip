@@ -1327,6 +1327,7 @@ __global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, uint8_t *done, con
 // and the document goes to the streamed walker (the pool instead of one per section: 20.0 KB of LDS per
 // diff wave instead of 22.3, 8 waves per CU instead of 7)
 constexpr uint32_t SW_MIN = 80, SW_NSEC = 64, SW_NSV = 128, SW_SVS = 256, SW_NPATCH = 512, SW_DHS = 256, SW_NPRE = 16;
+constexpr uint32_t SW_PROBE = 4;  // structs of the first section parsed before the tables (rich content declines; sv / meta: 2)
 constexpr uint32_t SW_TV = 1u << 14, SW_CLEN = 1u << 17;  // table word: delta (12 bits) | skip << 12 | patch << 13 | TV | clen << 15
 // section record fields: the first NQ_SV are what the state vector / meta walks keep, the rest the diff's
 enum { Q_W = 0, Q_CLIENT, Q_CLOCK, Q_X1, Q_VAL, Q_END, NQ_SV, Q_PRELEN = NQ_SV, Q_A0, Q_A1, Q_B0, Q_WRITTEN, Q_FCLOCK, Q_OUT, NQ };
@@ -1420,6 +1421,23 @@ __global__ void __launch_bounds__(64) k_pw_small(GeneralJob j, uint8_t *done, ui
       if (why) SW_DECLINE_R(why ? why : 2)
     }
     __syncthreads();
+    // probe: the chain's first structs with the full (non-nested) parser, in lockstep.  Rich content (nested
+    // `any` values, JSON objects / numbers) usually shows there, and declines before the table pass that
+    // makes up most of a document's cost here (C2R diff / C4R sv: every document declines to k_big_v1).
+    {
+      uint32_t q = 0;
+      bool pb = false;
+      const uint32_t nsec0 = sw_vu(L.b, q, len, pb);
+      const uint32_t ns0 = nsec0 ? sw_vu(L.b, q, len, pb) : 0;
+      sw_vu(L.b, q, len, pb);  // client
+      sw_vu(L.b, q, len, pb);  // first clock
+      for (uint32_t r = 0; r < ns0 && r < (OP == OP_DIFF ? SW_PROBE : 2u) && !pb; r++) {
+        uint32_t nx, cl, f2;
+        if (RF(ln::parse_struct(L.b, q, len, nx, cl, f2, len) ? 1u : 0u) == 0) { why = 8; break; }
+        q = RF(nx);
+      }
+    }
+    if (why) SW_DECLINE_R(why)
     // the tables: the branch-free short cut at every offset (most offsets start no struct, and the full
     // parser's divergent union over 64 garbage offsets costs ~5x the whole lockstep walk); a struct it does
     // not decide is parsed by the walk itself
