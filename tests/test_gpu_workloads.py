@@ -623,3 +623,34 @@ def test_rich_content_stays_on_the_specialised_paths(engine, name):
     bad = _compare(engine.run_host("diff", fmt, a2, o2, d2, sva, svoff), douts, dst)
     assert not bad, bad[:10]
     assert engine.stats["docs_general"] == 0, engine.stats
+
+
+@pytest.mark.parametrize("name", ["c2r_v2", "c4r_v2", "c4_v2"])
+def test_v2_small_kernels_rich_and_wide_match_oracle(engine, name, monkeypatch):
+    """The V2 lane-per-document kernels (k_diff_small_v2 forced at this batch size with YMERGE_DF2_MIN=0;
+    k_small_v2 for state vectors) over merged rich (Quill formats / embeds, maps of objects and arrays) and
+    wide (64-client) documents against random state vectors: every document byte-identical to the oracle,
+    whichever kernel completes it (the lane kernels or, for what they decline, k_big_v2)."""
+    import ctypes
+    from yjs_amd import pack_docs
+    monkeypatch.setenv("YMERGE_DF2_MIN", "0")
+    arena, upd_off, doc_upd = load_ymb(name)
+    n = min(len(doc_upd) - 1, 600)
+    doc_upd = doc_upd[:n + 1].copy()
+    merged, status, _ = O.batch("merge", 2, arena, upd_off, doc_upd, nthreads=8)
+    assert (status == 0).all()
+    a2, o2, d2 = pack_docs([[m] for m in merged])
+    outs, st, _ = O.batch("sv", 2, a2, o2, d2, nthreads=8)
+    bad = _compare(engine.run_host("sv", 2, a2, o2, d2), outs, st)
+    assert not bad, bad[:10]
+    svs = []
+    for i in range(n):
+        svs.extend(random_state_vectors(outs[i], 1, seed=100 + i))
+    sva, svo, _ = pack_docs([[s] for s in svs])
+    outs2, st2, _ = O.batch("diff", 2, a2, o2, d2, sva, svo, nthreads=8)
+    bad = _compare(engine.run_host("diff", 2, a2, o2, d2, sva, svo), outs2, st2)
+    assert not bad, bad[:10]
+    done = np.zeros(n, np.uint8)
+    assert engine.lib.ym__pv2_done(done.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), ctypes.c_uint32(n)) == 0
+    if name == "c2r_v2":  # most rich text documents are within the lane kernel's acceptance
+        assert (done == 1).sum() > n // 2, np.unique(done, return_counts=True)
