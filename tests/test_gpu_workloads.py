@@ -654,3 +654,22 @@ def test_v2_small_kernels_rich_and_wide_match_oracle(engine, name, monkeypatch):
     assert engine.lib.ym__pv2_done(done.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), ctypes.c_uint32(n)) == 0
     if name == "c2r_v2":  # most rich text documents are within the lane kernel's acceptance
         assert (done == 1).sum() > n // 2, np.unique(done, return_counts=True)
+
+
+@pytest.mark.parametrize("fmt", [1, 2])
+def test_merge_nested_first_adapts(engine, fmt):
+    """Merge batches of mostly rich documents make the next calls start with the nested LDS pass (per format,
+    re-probed with the hot pass every 16 calls); a plain batch after them, and every call in between, must
+    still give the oracle's bytes."""
+    rich = load_ymb(f"c2r_v{fmt}")
+    plain = load_ymb(f"c2_v{fmt}")
+    want = {}
+    for name, (arena, upd_off, doc_upd) in (("rich", rich), ("plain", plain)):
+        n = min(len(doc_upd) - 1, 300)
+        d = doc_upd[:n + 1].copy()
+        want[name] = (arena, upd_off, d) + O.batch("merge", fmt, arena, upd_off, d, nthreads=8)[:2]
+    seq = ["rich"] * 18 + ["plain", "plain", "rich", "plain"]
+    for i, name in enumerate(seq):
+        arena, upd_off, d, outs, status = want[name]
+        bad = _compare(engine.run_host("merge", fmt, arena, upd_off, d), outs, status)
+        assert not bad, (i, name, bad[:5])

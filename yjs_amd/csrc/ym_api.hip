@@ -80,6 +80,10 @@ struct DevState {
   bool dirty = true;            // device counters not known to be reset (first call, failed call)
   uint64_t seq = 0;             // call sequence number: the fast paths' completion flag (pinned[7])
   uint64_t min_stage_cap = 0;   // host batches: staging capacity learnt from an overflowing call
+  // merges (per format): the last calls' batches were mostly rich content (nested payloads), so the next one
+  // starts with the nested LDS pass instead of a hot pass that would decline most documents; re-probed with
+  // the hot pass every NESTED_PROBE calls
+  uint32_t nested_first[2] = {0, 0};
 };
 
 // Device state is per (thread, device): a thread may drive several devices in turn (ym_init switches
@@ -470,6 +474,7 @@ int run_general(DevState *S, hipStream_t st, GeneralJob j, uint32_t *list, uint3
   return 0;
 }
 
+constexpr uint32_t NESTED_PROBE = 16;
 int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *stats, int depth = 0) {
   if (!b || !out) return -1;
   DevState *S = state();
@@ -608,8 +613,14 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   if (!((op == OP_MERGE && !j.v2) || (op == OP_DSMERGE && !j.dsref)))
     if (int r = widen()) return r;
   HIPCHK(hipEventRecord(S->ev0, st));
-  // (1) fast path over every document; appends the ones it declines to list_a
-  int fr = fast_launch(op, j, b->n_upd, st);     // V1 merge: LDS fast path
+  // (1) fast path over every document; appends the ones it declines to list_a.  A merge batch of mostly rich
+  // documents (as the previous calls saw) starts with the nested pass over every document instead
+  const uint32_t fi = j.v2 ? 1 : 0;
+  const bool nested_first = op == OP_MERGE && S->nested_first[fi] > 0 && S->nested_first[fi] % NESTED_PROBE != 0 &&
+                            !getenv("YMERGE_NO_NESTED_FIRST");
+  int fr = 0;
+  if (nested_first) fr = j.v2 ? fast2_nested_launch(j, nd, st) : fast_nested_launch(j, nd, st);
+  if (fr == 0) fr = fast_launch(op, j, b->n_upd, st);     // V1 merge: LDS fast path
   if (fr == 0) fr = fast2_launch(op, j, b->n_upd, st);  // V2 merge: LDS fast path
   if (fr == 0) fr = big_launch(op, j, st, S->pw);  // V1 diff / state vector: chunk walk + wave walker
   if (fr == 0) fr = big2_launch(op, j, st, S->pw2); // V2 diff / state vector: column path + wave walker
@@ -624,12 +635,18 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
     ngen = (uint32_t)(S->pinned[2] & 0xffffffffu);
     list = S->list_a.as<uint32_t>();
   }
+  if (op == OP_MERGE && fr == 1) {
+    // the hot pass declined most documents: start the next calls with the nested pass; the nested pass
+    // (first) took most of them: keep doing so, with a hot-pass probe every NESTED_PROBE calls
+    const bool rich = nested_first ? ngen < nd / 2 : ngen > nd / 2;
+    S->nested_first[fi] = rich ? S->nested_first[fi] + 1 : 0;
+  }
   if (ngen > 0)
     if (int r = widen()) return r;
   // (1b) merges: the declined documents once more through the LDS kernel with nested payload checks
   // (rich content); it re-declines the rest into list_b
   bool nested = false;
-  if (ngen > 0 && list && op == OP_MERGE) {
+  if (ngen > 0 && list && op == OP_MERGE && !nested_first) {
     GeneralJob jn = j;
     jn.list = list;
     jn.pend_list = S->list_b.as<uint32_t>();

@@ -733,7 +733,7 @@ template <class M, int STOP, bool DSONLY, bool DSV2, bool NESTED>
 __device__ __forceinline__ void merge_doc_v1(const GeneralJob &j, uint32_t di) {
   const uint32_t lane = threadIdx.x;
   {
-    const uint32_t d = NESTED ? j.list[di] : di;
+    const uint32_t d = NESTED && j.list ? j.list[di] : di;  // (NESTED without a list: every document)
     const uint32_t u0 = j.doc_upd[d], k = j.doc_upd[d + 1] - u0;
     const uint64_t b0 = uoff_g(j, u0), bytes = uoff_g(j, u0 + k) - b0;
     if ((DSONLY ? k == 0 : k <= 1) || k > UPD || bytes > M::IN) {
@@ -988,7 +988,7 @@ int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st
 // pipeline / general path through j.pend_list.
 int fast_nested_launch(const GeneralJob &j, uint32_t n, hipStream_t st) {
   using namespace fastv1;
-  if (j.op != OP_MERGE || j.v2 || !j.list || n == 0) return 0;
+  if (j.op != OP_MERGE || j.v2 || n == 0) return 0;
   static int off = -1;
   if (off < 0) { const char *e = getenv("YMERGE_FAST_NESTED"); off = e && atoi(e) == 0 ? 1 : 0; }
   if (off) return 0;

@@ -419,7 +419,7 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v2(GeneralJob j, uint32_
   const uint32_t lane = threadIdx.x;
   const uint64_t arena0 = j.upd_off[0];
   for (uint32_t di = blockIdx.x; di < nd; di += gridDim.x) {
-    const uint32_t d = NESTED ? j.list[di] : di;
+    const uint32_t d = NESTED && j.list ? j.list[di] : di;  // (NESTED without a list: every document)
     const uint32_t u0 = j.doc_upd[d], k = j.doc_upd[d + 1] - u0;
     const uint64_t b0 = j.upd_off[u0], bytes = j.upd_off[u0 + k] - b0;
     if (k <= 1 || k > UPD || bytes > IN) {
@@ -1699,7 +1699,7 @@ int fast2_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t s
 
 // The V2 retry pass with nested payload checks (see fast_nested_launch, ym_fast.hip).
 int fast2_nested_launch(const GeneralJob &j, uint32_t n, hipStream_t st) {
-  if (j.op != OP_MERGE || !j.v2 || !j.list || n == 0) return 0;
+  if (j.op != OP_MERGE || !j.v2 || n == 0) return 0;
   static int off = -1;
   if (off < 0) { const char *e = getenv("YMERGE_FAST_NESTED"); off = e && atoi(e) == 0 ? 1 : 0; }
   if (off) return 0;
