@@ -746,7 +746,7 @@ int big2_launch(uint32_t op, const GeneralJob &j0, hipStream_t st, PwBufs &pwb) 
   // large single-section updates: the column-parallel path first (ym_pv2.hip); small ones one per lane
   // (parseUpdateMeta); k_big_v2 takes the rest
   if (int r = pv2_prepare(op, j0, st, pwb, &j.pw_done); r < 0) return r;
-  if (j.pw_done) small_v2_launch(op, j, const_cast<uint8_t *>(j.pw_done), st, BS_GRID);
+  if (j.pw_done) small_v2_launch(op, j, const_cast<uint8_t *>(j.pw_done), st, 4096);
   if (int r = pv2_finish(j0, st, pwb); r < 0) return r;  // (waits for the prep's totals: the kernels above run)
   const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
   if (op == OP_DIFF) big2::k_big_v2<OP_DIFF><<<grid, 64, big2::LDS_BYTES, st>>>(j);

@@ -1143,7 +1143,9 @@ __global__ void __launch_bounds__(64) k_small_v2(GeneralJob j, uint8_t *done) {
 // strictly descending, a stream or table overflow, documents outside the windows) leaves done[d] = 0: k_big_v2.
 template <uint32_t ND, uint32_t WIN, uint32_t POOL>
 struct Df2Lay {
-  static constexpr uint32_t SVW = ND == 1 ? 1024 : 64 * ND, NSV = ND == 1 ? 128 : 32, NPART = ND == 1 ? 128 : 32;
+  // (several documents per wave: at most 32 client sections / state-vector entries each -- a wider document,
+  // C4's 64 clients, declines at its header and takes k_big_v2's single generation, which is faster for it)
+  static constexpr uint32_t SVW = ND == 1 ? 1024 : 128 * ND, NSV = ND == 1 ? 128 : 32, NPART = NSV;
   static constexpr uint32_t SV = WIN + 48;               // u8[SVW + 16]: the state vectors
   static constexpr uint32_t SVT = SV + SVW + 16;         // u32[ND][NSV][2]: client, clock (then the ds clients)
   static constexpr uint32_t PT = SVT + ND * NSV * 8;     // u32[ND][NPART][4]: rest start, rest end, written
@@ -1370,13 +1372,21 @@ __global__ void __launch_bounds__(64, OCC) k_diff_small_v2(GeneralJob j, uint8_t
     c = h;  // rest stream
     nclients = rvu(c);
     ok &= !c.bad && nclients <= L::NPART;
-    const uint32_t slack = 8 + 16 * nclients;
     in_sz[S_KC] = col[0].e - col[0].p; in_sz[S_CL] = col[1].e - col[1].p; in_sz[S_LC] = col[2].e - col[2].p;
     in_sz[S_RC] = col[3].e - col[3].p; in_sz[S_IN] = col[4].e - col[4].p; in_sz[S_SB] = sn;
     in_sz[S_SL] = col[5].e - col[5].p; in_sz[S_PI] = col[6].e - col[6].p; in_sz[S_TR] = col[7].e - col[7].p;
     in_sz[S_LN] = col[8].e - col[8].p; in_sz[S_RE] = p1 - c.p;
+    // room per stream: what the written structs can add over their input bytes -- run splits at every part
+    // (one per client section at most), the cut struct's new origin (client + left clock) and sliced length,
+    // the part headers in the rest stream; the string body only shrinks.  A stream that still overflows
+    // declines the document (k_big_v2).
+    const uint32_t nc = nclients;
+    const uint32_t room[NS] = {8, 8 + 16 * nc, 8 + 16 * nc, 8 + 8 * nc, 8 + 4 * nc, 0, 8 + 4 * nc, 8 + 2 * nc, 8, 8 + 8 * nc, 8 + 8 * nc};
 #pragma unroll
-    for (uint32_t k = 0; k < NS; k++) { in_sz[k] += (in_sz[k] >> 3) + slack; need += in_sz[k]; }
+    for (uint32_t k = 0; k < NS; k++) {
+      in_sz[k] += (k == S_SB || k == S_KC || k == S_TR || k == S_PI || k == S_LN ? 0 : in_sz[k] >> 3) + room[k];
+      need += in_sz[k];
+    }
     need = (need + 16 + 15) & ~15u;  // (16 bytes ahead of the streams: the output is assembled in place)
     if (!ok && !why) why = 4;
   }
@@ -1662,13 +1672,21 @@ int small_v2_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t
   } else if (op == OP_SV) {
     k_small_v2<OP_SV, 16, 24576, 32><<<(j.n + 15) / 16, 64, Sv2Lay<16, 24576, 32>::BYTES, st>>>(j, done);
   } else if (op == OP_DIFF && done && j.sv) {
-    // 4 documents per wave (measured on C2: 0.93 ms per 10 k documents; 8 per wave 1.08, 2 per wave 0.96, 1 per
-    // wave 1.48; a 128-VGPR build spills and loses).  Below `diff_min` documents the one-wave walker's single
-    // generation is the faster engine (C2R / C4R, 4 k documents: 1.2 / 1.8 ms against 2.2 / 2.5 ms with this
-    // kernel in front of it), so the kernel runs only for larger batches.
-    if (const char *e = getenv("YMERGE_DF2_MIN")) diff_min = (uint32_t)strtoul(e, nullptr, 10);  // (tests: 0)
-    if (j.n < diff_min || getenv("YMERGE_NO_DF2")) return 0;
-    k_diff_small_v2<4, 6144, 8192, 1><<<(j.n + 3) / 4, 64, Df2Lay<4, 6144, 8192>::BYTES, st>>>(j, done);
+    // documents per wave so that the batch is one generation of waves (2 per SIMD: 2,048 on the chip; a
+    // second generation doubles the call: C2, 10 k documents, 4 per wave 0.93 ms against 5 per wave 0.56),
+    // each wave with a 7.5 KB window and 7.5 KB of output streams (its documents share both)
+    // Batches that fit one generation of k_big_v2's one-document waves (<= 4,096 documents here) stay on it:
+    // per document the lane walk is faster only for narrow documents (C2R 4 k: 0.87 against 1.25 ms), and
+    // slower for wide rich ones (C4R 4 k, 64 clients with object values: 2.7 against 1.9 ms), which a batch
+    // does not announce (YMERGE_DF2_MIN lowers the threshold: tests)
+    if (getenv("YMERGE_NO_DF2")) return 0;
+    if (const char *e = getenv("YMERGE_DF2_MIN")) diff_min = (uint32_t)strtoul(e, nullptr, 10);
+    if (j.n <= diff_min) return 0;
+    const uint32_t nd = j.n <= 2048 ? 1 : j.n <= 4096 ? 2 : j.n <= 6144 ? 3 : j.n <= 8192 ? 4 : 5;
+#define DF2(N) \
+  if (nd == N) k_diff_small_v2<N, 7680, 7680, 1><<<(j.n + N - 1) / N, 64, Df2Lay<N, 7680, 7680>::BYTES, st>>>(j, done);
+    DF2(1) DF2(2) DF2(3) DF2(4) DF2(5)
+#undef DF2
   } else {
     return 0;
   }
