@@ -635,11 +635,11 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
     ngen = (uint32_t)(S->pinned[2] & 0xffffffffu);
     list = S->list_a.as<uint32_t>();
   }
-  if (op == OP_MERGE && fr == 1) {
-    // the hot pass declined most documents: start the next calls with the nested pass; the nested pass
-    // (first) took most of them: keep doing so, with a hot-pass probe every NESTED_PROBE calls
-    const bool rich = nested_first ? ngen < nd / 2 : ngen > nd / 2;
-    S->nested_first[fi] = rich ? S->nested_first[fi] + 1 : 0;
+  const uint32_t ngen_hot = ngen;
+  if (op == OP_MERGE && fr == 1 && (nested_first || ngen <= nd / 2)) {
+    // the nested pass (first) took most documents: keep it first, with a hot-pass probe every NESTED_PROBE
+    // calls; or the hot pass declined at most half of them: the batch is not rich
+    S->nested_first[fi] = nested_first && ngen < nd / 2 ? S->nested_first[fi] + 1 : 0;
   }
   if (ngen > 0)
     if (int r = widen()) return r;
@@ -659,6 +659,10 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
       list = S->list_b.as<uint32_t>();
     }
   }
+  // the hot pass declined most documents and the nested pass took most of the batch (rich content, not
+  // documents too large for the LDS kernels): start the next calls with the nested pass
+  if (op == OP_MERGE && fr == 1 && !nested_first && ngen_hot > nd / 2)
+    S->nested_first[fi] = nested && ngen_hot - ngen > nd / 2 ? S->nested_first[fi] + 1 : 0;
   // (2) large-document merges (ym_large.hip) over the declined list; what it declines stays pending
   uint32_t nlarge = 0;
   bool large = false;
