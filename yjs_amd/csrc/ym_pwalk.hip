@@ -1815,9 +1815,12 @@ int pw_small_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t
   if (const char *e = getenv("YMERGE_PW_MIN")) pw_min = strtoull(e, nullptr, 10);
   const uint32_t gs = j.n < 65536 ? j.n : 65536;
   uint32_t *tally = (uint32_t *)(((uintptr_t)(done + j.n) + 15) & ~(uintptr_t)15) + 1;  // (pw_prepare's `many` + 1)
+// (the first window at 1,536 B: merged C2 documents, ~1 KB, fit it, and its 2.6 KB less LDS than a 2 KB window
+// let more waves in -- diff_c2_v1 0.76 -> 0.71 ms, sv_c2_v1 0.49 -> 0.46; 1,280 B sends too many to the 4 KB
+// launch: 0.95 / 0.56)
 #define PW_SMALL(O)                                                          \
-  k_pw_small<O, SW_MIN, 2048><<<gs, 64, 0, st>>>(j, done, pw_min, tally); \
-  k_pw_small<O, 2048, 4096><<<gs, 64, 0, st>>>(j, done, pw_min, tally);
+  k_pw_small<O, SW_MIN, 1536><<<gs, 64, 0, st>>>(j, done, pw_min, tally);    \
+  k_pw_small<O, 1536, 4096><<<gs, 64, 0, st>>>(j, done, pw_min, tally);
   if (op == OP_DIFF) { PW_SMALL(OP_DIFF) }
   else if (op == OP_SV) { PW_SMALL(OP_SV) }
   else { PW_SMALL(OP_META) }
