@@ -1662,7 +1662,7 @@ __global__ void __launch_bounds__(64, OCC) k_diff_small_v2(GeneralJob j, uint8_t
 // parseUpdateMetaV2 / encodeStateVectorFromUpdateV2 over small single updates, one per lane (k_small_v2);
 // done: the streamed walker's done array (nullptr: the kernel is the call's only specialised pass, its
 // declines go to the general path).  Meta: 64 updates of an update log per wave (4 KB window); state
-// vectors: 16 merged documents per wave (~1 KB each: a 24 KB window, 32 sections each).
+// vectors: 4 merged documents per wave (~1 KB each: an 8 KB window, 32 sections each).
 int small_v2_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t st, uint32_t diff_min) {
   static const bool off = getenv("YMERGE_NO_SMALL_V2") != nullptr;
   if (off || !j.v2 || j.n == 0) return 0;
@@ -1670,7 +1670,9 @@ int small_v2_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t
   if (op == OP_META) {
     k_small_v2<OP_META, 64, 4096, 8><<<(j.n + 63) / 64, 64, Sv2Lay<64, 4096, 8>::BYTES, st>>>(j, done);
   } else if (op == OP_SV) {
-    k_small_v2<OP_SV, 16, 24576, 32><<<(j.n + 15) / 16, 64, Sv2Lay<16, 24576, 32>::BYTES, st>>>(j, done);
+    // 4 documents per wave with an 8 KB window: one generation of short waves (C2, 10 k documents: 0.41 ms at
+    // 16 per wave, 0.42 at 8, 0.31 at 4 and 0.32 at 2)
+    k_small_v2<OP_SV, 4, 8192, 32><<<(j.n + 3) / 4, 64, Sv2Lay<4, 8192, 32>::BYTES, st>>>(j, done);
   } else if (op == OP_DIFF && done && j.sv) {
     // documents per wave so that the batch is one generation of waves (2 per SIMD: 2,048 on the chip; a
     // second generation doubles the call: C2, 10 k documents, 4 per wave 0.93 ms against 5 per wave 0.56),
