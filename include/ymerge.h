@@ -115,6 +115,13 @@ int ym_shutdown(void);
  * carries (Node 12 / V8 7.x wording; thread-local buffer, valid until the thread's next call) */
 const char *ym_strerror(int code);
 uint64_t ym_out_bound(const ym_batch *b); /* a capacity that is normally sufficient for ym_* */
+/* Page-locked host memory from the library's pool (power-of-two size classes, recycled by ym_host_free):
+ * host batches whose arrays live there are copied by the DMA engines directly (no staging copy, no first-touch
+ * page faults on the outputs).  Host merges of >= 4,096 documents with YM_OFF32 offsets run pipelined: the
+ * batch is cut into chunks of ~3 MiB of input, and chunk c + 1 is copied in while chunk c is merged and its
+ * packed outputs copied out.  Any pointer works as before; these just make the copies faster. */
+void *ym_host_alloc(size_t bytes);
+void ym_host_free(void *p);
 
 /* stream: a hipStream_t (NULL = the library's stream for the device).  Return value: 0, or
  * YM_ERR_CAPACITY when out->used > out->cap (nothing useful was written), or a negative HIP error. */

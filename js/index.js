@@ -53,12 +53,21 @@ const YM_DS_REF = 0x100 // mergeDeleteSets with the reference's adjacency-only c
 const YM_OUT_V1 = 0x1000 // ym_snapshot output encodings
 const YM_OUT_V2 = 0x2000
 
+// a large batch is packed into page-locked memory from the library's pool (addon.hostBuffer: DMA copies to the
+// GPU, no per-call page pinning); small ones, or without a HIP runtime, into ordinary memory
+const HOST_MIN = 1 << 20
+function hostBytes (n, big) {
+  const b = big ? addon.hostBuffer(n) : undefined
+  return b || new Uint8Array(n)
+}
 function pack (docs) {
   let n = 0; let bytes = 0
   for (const d of docs) { n += d.length; for (const u of d) bytes += u.length }
-  const arena = new Uint8Array(bytes)
-  const updOff = new Float64Array(n + 1)
-  const docUpd = new Uint32Array(docs.length + 1)
+  const big = bytes >= HOST_MIN
+  const arena = hostBytes(bytes, big)
+  // u32 offsets below 4 GiB (YM_OFF32 in the addon: half the offset bytes to copy, pipelined host merges)
+  const updOff = bytes < 4294967296 ? new Uint32Array(hostBytes(4 * (n + 1), big).buffer, 0, n + 1) : new Float64Array(n + 1)
+  const docUpd = new Uint32Array(hostBytes(4 * (docs.length + 1), big).buffer, 0, docs.length + 1)
   let o = 0; let u = 0
   docs.forEach((d, i) => {
     docUpd[i] = u

@@ -6,8 +6,9 @@
 //   runAsync(op, format, arena, updOff, docUpd[, svArena, svOff])  -> Promise (napi_async_work: the
 //        library call runs on a libuv worker thread; the inputs are pinned by references until it ends)
 //   strerror(status)                                              ym_strerror (yjs's exception text)
-// The output arena is allocated uninitialised (the library writes every byte it reports) and handed to
-// JS as an external ArrayBuffer: no zero-fill, no second copy.
+// The output arena comes uninitialised from the library's page-locked pool (ym_host_alloc: the device-to-host
+// copies land in it directly; the library writes every byte it reports) and is handed to JS as an external
+// ArrayBuffer whose finalizer returns it to the pool: no zero-fill, no second copy.
 #include <node_api.h>
 
 #include <stdint.h>
@@ -41,6 +42,7 @@ static bool get_u8(napi_env env, napi_value v, const uint8_t **p, size_t *n) {
 }
 
 // u64 offsets from a BigUint64Array (used in place), a Float64Array (exact below 2^53) or a Uint32Array
+// (converted; update offsets in a Uint32Array are passed as they are instead, with YM_OFF32: see parse)
 static bool get_u64(napi_env env, napi_value v, const uint64_t **p, size_t *n, std::vector<uint64_t> &conv) {
   bool is_ta = false;
   if (napi_is_typedarray(env, v, &is_ta) != napi_ok || !is_ta) return false;
@@ -79,17 +81,24 @@ struct Job {
   int32_t op = 0;
   ym_batch b;
   std::vector<uint64_t> upd_conv, sv_conv;
-  uint8_t *arena = nullptr;  // malloc'ed, uninitialised
+  uint8_t *arena = nullptr;  // from the library's page-locked pool (ym_host_alloc), uninitialised
   uint64_t used = 0;
-  std::vector<uint64_t> out_off, out_len;
-  std::vector<int32_t> status;
+  // per-document results, also from the pool: with every output array page-locked the library's packing
+  // kernels write them straight into host memory (no copy op)
+  uint64_t *out_off = nullptr, *out_len = nullptr;
+  int32_t *status = nullptr;
   int rc = 0;
   // async only
   napi_ref refs[7] = {};
   size_t nrefs = 0;
   napi_deferred deferred = nullptr;
   napi_async_work work = nullptr;
-  ~Job() { free(arena); }
+  ~Job() {
+    ym_host_free(arena);
+    ym_host_free(out_off);
+    ym_host_free(out_len);
+    ym_host_free(status);
+  }
 };
 
 // parses run()'s arguments into job (throws and returns false on a bad argument)
@@ -105,13 +114,17 @@ static bool parse(napi_env env, napi_callback_info info, Job &j, napi_value *arg
   const uint8_t *arena = nullptr, *sva = nullptr;
   const uint64_t *upd_off = nullptr, *sv_off = nullptr;
   size_t alen = 0, svlen = 0, ndocs1 = 0, nupd1 = 0, nsv1 = 0;
-  const uint32_t *doc_upd = nullptr;
-  if (!get_u8(env, argv[2], &arena, &alen) || !get_u64(env, argv[3], &upd_off, &nupd1, j.upd_conv) ||
+  const uint32_t *doc_upd = nullptr, *upd_off32 = nullptr;
+  // update offsets: a Uint32Array goes to the library as it is (YM_OFF32: half the bytes to copy in, and host
+  // merges of many documents run pipelined); BigUint64Array / Float64Array as u64
+  const bool off32 = get_u32(env, argv[3], &upd_off32, &nupd1);
+  if (!get_u8(env, argv[2], &arena, &alen) || (!off32 && !get_u64(env, argv[3], &upd_off, &nupd1, j.upd_conv)) ||
       !get_u32(env, argv[4], &doc_upd, &ndocs1) || nupd1 == 0 || ndocs1 == 0) {
-    napi_throw_type_error(env, nullptr, "arena must be a Uint8Array, updOff a BigUint64Array/Float64Array, docUpd a Uint32Array");
+    napi_throw_type_error(env, nullptr, "arena must be a Uint8Array, updOff a Uint32Array/BigUint64Array/Float64Array, docUpd a Uint32Array");
     return false;
   }
-  if (upd_off[nupd1 - 1] > alen || doc_upd[ndocs1 - 1] > nupd1 - 1) {
+  const uint64_t off_end = off32 ? upd_off32[nupd1 - 1] : upd_off[nupd1 - 1];
+  if (off_end > alen || doc_upd[ndocs1 - 1] > nupd1 - 1) {
     napi_throw_range_error(env, nullptr, "updOff / docUpd exceed the arena");
     return false;
   }
@@ -128,11 +141,11 @@ static bool parse(napi_env env, napi_callback_info info, Job &j, napi_value *arg
   if (want_sv && !sva) sva = no_bytes;  // every vector empty: still a batch with targets (NULL: none)
   memset(&j.b, 0, sizeof(j.b));
   j.b.arena = arena;
-  j.b.upd_off = upd_off;
+  j.b.upd_off = off32 ? reinterpret_cast<const uint64_t *>(upd_off32) : upd_off;
   j.b.doc_upd = doc_upd;
   j.b.n_docs = (uint32_t)(ndocs1 - 1);
   j.b.n_upd = (uint32_t)(nupd1 - 1);
-  j.b.format = fmt;
+  j.b.format = fmt | (off32 ? YM_OFF32 : 0);
   j.b.mem = YM_MEM_HOST;
   j.b.sv_arena = want_sv ? sva : nullptr;
   j.b.sv_off = want_sv ? sv_off : nullptr;
@@ -142,15 +155,16 @@ static bool parse(napi_env env, napi_callback_info info, Job &j, napi_value *arg
 // the library call (no N-API use: runs on the main thread or a worker)
 static void execute(Job &j) {
   const size_t nd = j.b.n_docs ? j.b.n_docs : 1;
-  j.out_off.resize(nd);
-  j.out_len.resize(nd);
-  j.status.resize(nd);
+  j.out_off = (uint64_t *)ym_host_alloc(nd * 8);
+  j.out_len = (uint64_t *)ym_host_alloc(nd * 8);
+  j.status = (int32_t *)ym_host_alloc(nd * 4);
+  if (!j.out_off || !j.out_len || !j.status) { j.rc = YM_ERR_CAPACITY; return; }
   uint64_t cap = ym_out_bound(&j.b);
   for (int attempt = 0; attempt < 4; attempt++) {
-    free(j.arena);
-    j.arena = (uint8_t *)malloc(cap ? cap : 1);
+    ym_host_free(j.arena);
+    j.arena = (uint8_t *)ym_host_alloc(cap ? cap : 1);
     if (!j.arena) { j.rc = YM_ERR_CAPACITY; return; }
-    ym_out o = {j.arena, cap, j.out_off.data(), j.out_len.data(), j.status.data(), 0};
+    ym_out o = {j.arena, cap, j.out_off, j.out_len, j.status, 0};
     j.rc = j.op == 0   ? ym_merge(&j.b, &o, nullptr, nullptr)
            : j.op == 1 ? ym_diff(&j.b, &o, nullptr, nullptr)
            : j.op == 3 ? ym_convert(&j.b, &o, nullptr, nullptr)
@@ -165,7 +179,7 @@ static void execute(Job &j) {
   }
 }
 
-static void free_arena(napi_env, void *data, void *) { free(data); }
+static void free_arena(napi_env, void *data, void *) { ym_host_free(data); }  // back to the pool
 
 static napi_value make_f64(napi_env env, const uint64_t *src, size_t n) {
   void *data = nullptr;
@@ -206,9 +220,9 @@ static napi_value result(napi_env env, Job &j, napi_value *err) {
   if (napi_create_typedarray(env, napi_uint8_array, n, ab, 0, &ta) != napi_ok) return nullptr;
   if (napi_create_object(env, &res) != napi_ok) return nullptr;
   napi_set_named_property(env, res, "arena", ta);
-  napi_set_named_property(env, res, "offsets", make_f64(env, j.out_off.data(), j.b.n_docs));
-  napi_set_named_property(env, res, "lengths", make_f64(env, j.out_len.data(), j.b.n_docs));
-  napi_set_named_property(env, res, "status", make_i32(env, j.status.data(), j.b.n_docs));
+  napi_set_named_property(env, res, "offsets", make_f64(env, j.out_off, j.b.n_docs));
+  napi_set_named_property(env, res, "lengths", make_f64(env, j.out_len, j.b.n_docs));
+  napi_set_named_property(env, res, "status", make_i32(env, j.status, j.b.n_docs));
   return res;
 }
 
@@ -278,6 +292,32 @@ static napi_value RunAsync(napi_env env, napi_callback_info info) {
   return promise;
 }
 
+// hostBuffer(n) -> Uint8Array over n bytes of page-locked memory from the library's pool (ym_host_alloc), given
+// back to the pool when the buffer is garbage collected; undefined when none can be had (no HIP runtime).  The
+// JS module packs large batches into it, so the library's copies to the GPU are DMA transfers of that memory.
+static napi_value HostBuffer(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  double n = 0;
+  if (argc < 1 || napi_get_value_double(env, argv[0], &n) != napi_ok || !(n >= 0) || n > 9007199254740991.0) {
+    napi_throw_type_error(env, nullptr, "hostBuffer(bytes)");
+    return nullptr;
+  }
+  napi_value undef;
+  napi_get_undefined(env, &undef);
+  const size_t bytes = (size_t)n;
+  void *p = ym_host_alloc(bytes ? bytes : 1);
+  if (!p) return undef;
+  napi_value ab, ta;
+  if (napi_create_external_arraybuffer(env, p, bytes, free_arena, nullptr, &ab) != napi_ok) {
+    ym_host_free(p);
+    return undef;
+  }
+  NAPI_CALL(env, napi_create_typedarray(env, napi_uint8_array, bytes, ab, 0, &ta));
+  return ta;
+}
+
 static napi_value StrError(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1];
@@ -293,7 +333,7 @@ static napi_value Init(napi_env env, napi_value exports) {
   int32_t dev = 0;
   const char *e = getenv("YMERGE_DEVICE");
   if (e) dev = atoi(e);
-  struct { const char *name; napi_callback cb; } fns[] = {{"run", Run}, {"runAsync", RunAsync}, {"strerror", StrError}};
+  struct { const char *name; napi_callback cb; } fns[] = {{"run", Run}, {"runAsync", RunAsync}, {"strerror", StrError}, {"hostBuffer", HostBuffer}};
   for (auto &f : fns) {
     napi_value fn;
     if (napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &fn) != napi_ok) return nullptr;

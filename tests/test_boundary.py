@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def header_symbols():
     src = open(os.path.join(ROOT, "include", "ymerge.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char \*|uint64_t)\s*\*?\s*(ym_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|const char \*|uint64_t|void \*|void)\s*\*?\s*(ym_\w+)\s*\(", src, re.M)))
 
 
 def test_header_declares_the_batched_yjs_functions():

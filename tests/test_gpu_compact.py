@@ -149,7 +149,10 @@ def test_compact_workspace_budget_chunks(engine, monkeypatch):
 @pytest.mark.parametrize("fmt", [1, 2])
 def test_compact_doc_state_vector_on_gpu(engine, fmt, gc):
     """YM_SV_FIRST on the GPU: the compacted Doc's encodeStateVector (StructStore insertion order) before the
-    update, against the reference's bytes for every fixture of compact.json / compact_nogc.json."""
+    update, against the reference's bytes for every fixture of compact.json / compact_nogc.json except the
+    gap_c5 / wl_c5 groups: those C5 documents (~13 k updates, ~1,500 pending readers) take minutes per format
+    on k_compact's one-lane-per-document integration, so their doc-side state vectors are checked through the
+    host build of the same device code only (tests/test_compact.py)."""
     from yjs_amd import pack_docs
     cs = [c for c in compact_cases.load(nogc=not gc) if c["fmt"] == fmt and c["group"] not in ("gap_c5", "wl_c5")]
     a, o, d = pack_docs([c["inputs"] for c in cs])

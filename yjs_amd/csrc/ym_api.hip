@@ -12,6 +12,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <vector>
 
 #include "../../include/ymerge.h"
@@ -84,6 +85,13 @@ struct DevState {
   // starts with the nested LDS pass instead of a hot pass that would decline most documents; re-probed with
   // the hot pass every NESTED_PROBE calls
   uint32_t nested_first[2] = {0, 0};
+  // pipelined host merges (run_host_pipe): copy streams, per-chunk events, the u32 offsets' staging buffer and
+  // the mapped host words the per-chunk scan kernels write (chunk output ranges, declined count)
+  hipStream_t s_h2d = nullptr, s_h2d2 = nullptr, s_d2h = nullptr;
+  hipEvent_t pev_h[16] = {}, pev_h2[16] = {}, pev_k[16] = {}, pev_p[16] = {};
+  DBuf in_off32;
+  uint64_t *pipe_host = nullptr, *pipe_host_dev = nullptr;
+  bool pipe_skip = false;  // the pipelined call's own fallback runs the unpipelined flow
 };
 
 // Device state is per (thread, device): a thread may drive several devices in turn (ym_init switches
@@ -127,24 +135,9 @@ DevState *state() {
 }
 
 // host batches: document d's output moves to the packed offset cmp_off[d] (exclusive scan of the masked
-// lengths), so the device-to-host copy carries the outputs only, not the fast paths' sparse slot region.
-// The grid walks the PACKED output in 16 KB chunks (a large document gets many blocks, a chunk may hold
-// many small documents): each thread writes one aligned 16-byte word of the destination, assembled
-// from two aligned 16-byte source loads and a byte funnel shift (the source slot of a document is at
-// an arbitrary offset relative to its packed position); the one word per document boundary that spans
-// two documents is assembled byte by byte.  Reads may touch <= 15 bytes past a document's output
-// (inside the arena's 16-byte padding).
-constexpr uint32_t PACK_THREADS = 256, PACK_WORDS = 4, PACK_CHUNK = PACK_THREADS * PACK_WORDS * 16;
-
-__device__ inline uint32_t pack_doc_of(const uint64_t *cmp_off, uint32_t lo, uint32_t hi, uint64_t p) {
-  // largest d in [lo, hi] with cmp_off[d] <= p
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi + 1) >> 1;
-    if (cmp_off[mid] <= p) lo = mid; else hi = mid - 1;
-  }
-  return lo;
-}
-
+// lengths), so the device-to-host copy carries the outputs only, not the fast paths' sparse slot region
+// (k_pack_docs, one wave per document).  pack_load16: 16 bytes at any source offset from two aligned 16-byte
+// loads and a byte funnel shift (reads <= 31 bytes past s, inside the arena's padding).
 __device__ inline uint4 pack_load16(const uint8_t *src, uint64_t s) {
   const uint64_t a = s & ~15ull;
   const uint32_t sh = (uint32_t)(s & 15);
@@ -167,40 +160,87 @@ __device__ inline uint4 pack_load16(const uint8_t *src, uint64_t s) {
   return make_uint4(r[0], r[1], r[2], r[3]);
 }
 
-__global__ void __launch_bounds__(PACK_THREADS) k_pack(const uint8_t *src, const uint64_t *off, const uint64_t *mlen,
-                                                       const uint64_t *cmp_off, uint8_t *dst, uint32_t n, uint64_t total) {
-  __shared__ uint32_t s_rng[2];
-  for (uint64_t c0 = (uint64_t)blockIdx.x * PACK_CHUNK; c0 < total; c0 += (uint64_t)gridDim.x * PACK_CHUNK) {
-    __syncthreads();
-    if (threadIdx.x < 2) {
-      const uint64_t p = threadIdx.x == 0 ? c0 : (c0 + PACK_CHUNK < total ? c0 + PACK_CHUNK : total) - 1;
-      s_rng[threadIdx.x] = pack_doc_of(cmp_off, 0, n - 1, p);
-    }
-    __syncthreads();
-    const uint32_t lo = s_rng[0], hi = s_rng[1];
+// ---- pipelined host merges (run_host_pipe) ----------------------------------------------------------
+// One block per chunk: the exclusive scan of the chunk's masked output lengths, placed after the outputs of
+// the chunks before it (`running` carries the packed total from chunk to chunk in stream order).  The chunk's
+// packed range goes to mapped host memory (hw[2c], hw[2c + 1]) so the host can start its device-to-host copy
+// while later chunks are still being copied in or merged; the last chunk also reports the declined count
+// (hw[62]) and the documents that are not YM_OK (hw[61]).
+__device__ inline uint64_t blk_excl64(uint64_t x, uint64_t *s_w, uint64_t &total) {
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, nw = blockDim.x >> 6;
+  uint64_t incl = x;
 #pragma unroll
-    for (uint32_t it = 0; it < PACK_WORDS; it++) {
-      const uint64_t p = c0 + (uint64_t)(it * PACK_THREADS + threadIdx.x) * 16;
-      if (p >= total) break;
-      uint32_t d = pack_doc_of(cmp_off, lo, hi, p);
-      uint64_t e = cmp_off[d] + mlen[d];
-      const uint64_t pe = p + 16 < total ? p + 16 : total;
-      if (pe <= e) {  // one document
-        const uint4 v = pack_load16(src, off[d] - cmp_off[d] + p);
-        if (pe - p == 16) {
-          *reinterpret_cast<uint4 *>(dst + p) = v;
-        } else {
-          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-          for (uint64_t q = p; q < pe; q++) dst[q] = (uint8_t)(w[(q - p) >> 2] >> (8 * ((q - p) & 3)));
-        }
-        continue;
-      }
-      for (uint64_t q = p; q < pe; q++) {  // spans a document boundary (empty documents are skipped)
-        while (q >= e) { d++; e = cmp_off[d] + mlen[d]; }
-        dst[q] = src[off[d] + (q - cmp_off[d])];
-      }
-    }
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(incl, o, 64);
+    if (lane >= (uint32_t)o) incl += y;
   }
+  if (lane == 63) s_w[w] = incl;
+  __syncthreads();
+  uint64_t before = 0;
+  total = 0;
+  for (uint32_t k = 0; k < nw; k++) {
+    const uint64_t v = s_w[k];
+    before += k < w ? v : 0;
+    total += v;
+  }
+  __syncthreads();
+  return before + incl - x;
+}
+__global__ void __launch_bounds__(1024) k_chunk_scan(const int32_t *status, const uint64_t *len, uint32_t n, uint64_t *cmp_off,
+                                                     uint64_t *cmp_len, uint64_t *running, volatile uint64_t *hw, uint32_t c,
+                                                     const uint32_t *pend, int last, uint64_t *h_off, uint64_t *h_len,
+                                                     int32_t *h_st) {
+  __shared__ uint64_t s_w[16];
+  __shared__ uint32_t s_bad;
+  const uint32_t t = threadIdx.x;
+  if (t == 0) s_bad = 0;
+  __syncthreads();
+  const uint64_t base = running[0];
+  uint64_t carry = 0;
+  uint32_t bad = 0;
+  for (uint32_t t0 = 0; t0 < n; t0 += blockDim.x) {
+    const uint32_t i = t0 + t;
+    const int32_t sv = i < n ? status[i] : 0;
+    const uint64_t x = i < n && sv == 0 ? len[i] : 0;
+    bad += i < n && sv != 0;
+    uint64_t tot;
+    const uint64_t ex = blk_excl64(x, s_w, tot);
+    if (i < n) {
+      cmp_off[i] = base + carry + ex;
+      cmp_len[i] = x;
+      if (h_off) { h_off[i] = base + carry + ex; h_len[i] = x; h_st[i] = sv; }  // host memory, over PCIe
+    }
+    carry += tot;
+  }
+  if (bad) atomicAdd(&s_bad, bad);
+  __syncthreads();
+  if (t == 0) {
+    running[0] = base + carry;
+    running[1] += s_bad;
+    hw[2 * c] = base;
+    hw[2 * c + 1] = base + carry;
+    if (last) { hw[61] = running[1]; hw[62] = *pend; }
+    __threadfence_system();
+  }
+}
+// one wave per document: its output from the fast path's slot to its packed place (16-byte stores)
+// (dst may be page-locked host memory: the stores then cross PCIe as 16-byte writes; a document past `cap` is
+// not written, the host reports YM_ERR_CAPACITY)
+__global__ void __launch_bounds__(256) k_pack_docs(const uint8_t *src, const uint64_t *src_off, const uint64_t *dst_off,
+                                                   const uint64_t *len, uint32_t n, uint8_t *dst, uint64_t cap) {
+  const uint32_t d = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (d >= n) return;
+  const uint64_t L = len[d];
+  if (L == 0) return;
+  const uint64_t so = src_off[d], dof = dst_off[d];
+  if (dof + L > cap) return;
+  const uint32_t head0 = (uint32_t)((16 - (dof & 15)) & 15);
+  const uint64_t h = head0 < L ? head0 : L;
+  if (lane < h) dst[dof + lane] = src[so + lane];
+  const uint64_t body = (L - h) & ~15ull;
+  for (uint64_t k = (uint64_t)lane * 16; k < body; k += 64 * 16)
+    *reinterpret_cast<uint4 *>(dst + dof + h + k) = pack_load16(src, so + h + k);
+  for (uint64_t i = h + body + lane; i < L; i += 64) dst[dof + i] = src[so + i];
 }
 
 // YM_OFF32 offsets widened to u64 for the kernels that read u64 offsets
@@ -474,8 +514,248 @@ int run_general(DevState *S, hipStream_t st, GeneralJob j, uint32_t *list, uint3
   return 0;
 }
 
+// ---- pipelined host merges ---------------------------------------------------------------------------
+// A host batch of merges (u32 offsets, YM_OFF32) in document chunks of ~equal bytes, three streams deep:
+//   copy stream   H2D of chunk c's bytes, offsets and doc_upd entries           -> event h[c]
+//   compute       (waits h[c]) the LDS fast kernel over chunk c, its packing:   -> event k[c]
+//                 k_chunk_scan (placed after the previous chunks) + k_pack_docs
+//   copy stream 2 (host waits k[c], reads the chunk's packed range from mapped memory) D2H of chunk c
+// so the PCIe link carries chunk c + 1 in while chunk c's outputs go out (full duplex) and the kernels run
+// under the copies.  Optimistic: the fast kernels must take every document; if any is declined (or not OK)
+// the call runs again through the general flow (run_op, unpipelined), which handles everything exactly.
+// ---- the page-locked host pool's bookkeeping (ym_host_alloc / ym_host_free, below) ----
+std::mutex g_pool_mu;
+std::vector<void *> g_pool_free[64];
+std::vector<std::pair<void *, int>> g_pool_live;  // (pointer, class) of every buffer handed out
+int pool_class(size_t n) {
+  int k = 16;
+  while (k < 63 && (1ull << k) < n) k++;
+  return k;
+}
+// [p, p + bytes) lies inside one live pool buffer: the device may read it directly (and a little past it)
+bool pool_holds(const void *p, size_t bytes) {
+  std::lock_guard<std::mutex> g(g_pool_mu);
+  const uint8_t *q = (const uint8_t *)p;
+  for (const auto &e : g_pool_live) {
+    const uint8_t *b = (const uint8_t *)e.first;
+    if (q >= b && q + bytes <= b + (1ull << e.second)) return true;
+  }
+  return false;
+}
+
+// the device address of host memory the device can reach (page-locked: hipHostMalloc / hipHostRegister), or
+// nullptr (pageable memory)
+uint8_t *host_dev_ptr(const void *p) {
+  hipPointerAttribute_t a;
+  if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // (pageable memory: not an error of the call)
+    return nullptr;
+  }
+  if (a.type != hipMemoryTypeHost || !a.devicePointer) return nullptr;
+  const uint8_t *hp = a.hostPointer ? (const uint8_t *)a.hostPointer : (const uint8_t *)p;
+  return (uint8_t *)a.devicePointer + ((const uint8_t *)p - hp);
+}
+constexpr uint32_t PIPE_MIN_DOCS = 4096, PIPE_MAX = 16;
+constexpr uint64_t PIPE_CHUNK_BYTES = 3ull << 20;
+int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *stats, int depth = 0);
+int run_host_pipe(DevState *S, const ym_batch *b, ym_out *out, hipStream_t st, ym_stats *stats) {
+  const uint32_t nd = b->n_docs, nu = b->n_upd;
+  const uint32_t *o32 = reinterpret_cast<const uint32_t *>(b->upd_off);
+  const uint32_t *du = b->doc_upd;
+  const uint64_t A_lo = o32[0], A_hi = o32[nu], abytes = A_hi;  // arena positions are absolute
+  const bool v2 = (b->format & 0xff) == YM_V2;
+  if (!S->s_h2d) {
+    HIPCHK(hipStreamCreateWithFlags(&S->s_h2d, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&S->s_h2d2, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&S->s_d2h, hipStreamNonBlocking));
+    for (uint32_t c = 0; c < PIPE_MAX; c++) {
+      HIPCHK(hipEventCreateWithFlags(&S->pev_h[c], hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&S->pev_h2[c], hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&S->pev_k[c], hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&S->pev_p[c], hipEventDisableTiming));
+    }
+    HIPCHK(hipHostMalloc((void **)&S->pipe_host, 64 * sizeof(uint64_t), hipHostMallocCoherent | hipHostMallocMapped));
+    HIPCHK(hipHostGetDevicePointer((void **)&S->pipe_host_dev, S->pipe_host, 0));
+  }
+  // chunk boundaries: documents, cut at ~equal input bytes
+  uint32_t nc = (uint32_t)((A_hi - A_lo + PIPE_CHUNK_BYTES - 1) / PIPE_CHUNK_BYTES);
+  nc = nc < 2 ? 2 : nc > PIPE_MAX ? PIPE_MAX : nc;
+  uint32_t cut[PIPE_MAX + 1];
+  cut[0] = 0;
+  for (uint32_t c = 1; c < nc; c++) {
+    const uint64_t target = A_lo + (A_hi - A_lo) * c / nc;
+    uint32_t lo = cut[c - 1], hi = nd;  // first document starting at or after target
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (o32[du[mid]] < target) lo = mid + 1; else hi = mid;
+    }
+    cut[c] = lo;
+  }
+  cut[nc] = nd;
+  // device buffers
+  const uint64_t bound = 4 * abytes + 128ull * nd + 8192;
+  uint64_t dev_cap = out->cap > bound ? out->cap : bound;
+  if (S->min_stage_cap > dev_cap) dev_cap = S->min_stage_cap;
+  if (S->in_arena.ensure(abytes + 16) || S->in_off32.ensure((nu + 1) * 4ull) || S->in_doc.ensure((nd + 1) * 4ull) ||
+      S->out_arena.ensure(dev_cap + 16) || S->out_off.ensure(nd * 8ull) || S->out_len.ensure(nd * 8ull) ||
+      S->status.ensure(nd * 4ull) || S->cmp_off.ensure(nd * 8ull + 8) || S->cmp_len.ensure(nd * 8ull + 8) ||
+      S->cmp_arena.ensure(dev_cap + 16) || S->counters.ensure(1024) || S->list_a.ensure((nd + 1) * 4ull) ||
+      S->layout.ensure(nd * sizeof(ym::Layout) + 16) || (v2 && S->in_off.ensure((nu + 1) * 8ull)))
+    return -2;
+  uint8_t *dA = S->in_arena.as<uint8_t>();
+  uint32_t *dO = S->in_off32.as<uint32_t>(), *dD = S->in_doc.as<uint32_t>();
+  uint64_t *counters = S->counters.as<uint64_t>();
+  GeneralJob j;
+  memset(&j, 0, sizeof(j));
+  j.A = dA;
+  j.upd_off32 = v2 ? nullptr : dO;
+  j.upd_off = v2 ? S->in_off.as<uint64_t>() : nullptr;
+  j.op = OP_MERGE;
+  j.v2 = v2;
+  j.layout = S->layout.as<ym::Layout>();
+  j.out = S->out_arena.as<uint8_t>();
+  j.cap = dev_cap;
+  j.used = counters + 0;
+  j.counter_retry = (uint32_t *)(counters + 1);
+  j.pend_count = (uint32_t *)(counters + 2);
+  j.pend_list = S->list_a.as<uint32_t>();
+  j.pw_count = counters + 11;
+  // counters (declines, the running packed total [20], non-OK documents [21]) start at zero; the
+  // compute stream's previous work (an earlier call) is ordered before
+  HIPCHK(hipMemsetAsync(counters, 0, 1024, st));
+  S->dirty = true;  // k_finish does not run here: the next unpipelined call resets the counters
+  HIPCHK(hipEventRecord(S->ev0, st));
+  HIPCHK(hipStreamWaitEvent(S->s_h2d, S->ev0, 0));  // staging buffers: free once the earlier work is done
+  HIPCHK(hipStreamWaitEvent(S->s_h2d2, S->ev0, 0));
+  volatile uint64_t *hw = S->pipe_host;
+  for (uint32_t c = 0; c < nc; c++) hw[2 * c] = hw[2 * c + 1] = ~0ull;
+  // outputs in page-locked memory the device can address (ym_host_alloc, hipHostMalloc / hipHostRegister):
+  // the packing kernels write the outputs, offsets, lengths and statuses straight into it over PCIe (no copy
+  // op at all); otherwise the packed chunks are copied out as each completes
+  uint8_t *h_arena = host_dev_ptr(out->arena);
+  uint64_t *h_off = (uint64_t *)host_dev_ptr(out->out_off), *h_len = (uint64_t *)host_dev_ptr(out->out_len);
+  int32_t *h_st = (int32_t *)host_dev_ptr(out->status);
+  const bool direct = h_arena && h_off && h_len && h_st && !getenv("YMERGE_PIPE_COPY");
+  // inputs in the library's pool (the Node addon packs there): the merge kernels read them over PCIe themselves
+  // (zero-copy: no DMA copy op, whose per-copy setup left the link idle between chunks); the pool's size
+  // classes leave room for the 16-byte staging loads' over-read past the end
+  const uint8_t *z_arena = pool_holds(b->arena, A_hi + 64) ? host_dev_ptr(b->arena) : nullptr;
+  const uint32_t *z_off = pool_holds(o32, (nu + 1) * 4ull + 64) ? (const uint32_t *)host_dev_ptr(o32) : nullptr;
+  const uint32_t *z_doc = pool_holds(du, (nd + 1) * 4ull + 64) ? (const uint32_t *)host_dev_ptr(du) : nullptr;
+  const bool zin = z_arena && z_off && z_doc && !getenv("YMERGE_PIPE_NOZC");
+  if (zin) {
+    j.A = z_arena;
+    if (!v2) j.upd_off32 = z_off;
+    dO = const_cast<uint32_t *>(z_off);
+    dD = const_cast<uint32_t *>(z_doc);
+  }
+  // (1) every copy in, up front: the two DMA queues run back to back without waiting for the host
+  if (!zin) HIPCHK(hipMemcpyAsync(dD, du, (nd + 1) * 4ull, hipMemcpyHostToDevice, S->s_h2d2));  // doc_upd: one copy
+  for (uint32_t c = 0; c < nc && !zin; c++) {
+    const uint32_t d0 = cut[c], d1 = cut[c + 1];
+    if (d1 == d0) continue;
+    const uint32_t u0 = du[d0], u1 = du[d1];
+    // the chunk's bytes on one copy queue and its offsets on another (two DMA engines: their per-copy setup
+    // overlaps), both cut at 64-byte boundaries (an unaligned end costs a blit kernel; the few bytes a cut
+    // shares with the neighbouring chunk are copied twice, the same values, in stream order)
+    const uint64_t a0 = c == 0 ? 0 : o32[u0] & ~63ull, a1e = c + 1 == nc ? A_hi : (o32[u1] + 63) & ~63ull;
+    const uint64_t a1 = a1e < A_hi ? a1e : A_hi;
+    if (a1 > a0) HIPCHK(hipMemcpyAsync(dA + a0, b->arena + a0, a1 - a0, hipMemcpyHostToDevice, S->s_h2d));
+    const uint32_t o0 = c == 0 ? 0 : u0 & ~15u, o1e = c + 1 == nc ? nu + 1 : ((u1 + 1 + 15) & ~15u);
+    const uint32_t o1 = o1e < nu + 1 ? o1e : nu + 1;
+    HIPCHK(hipMemcpyAsync(dO + o0, o32 + o0, (o1 - o0) * 4ull, hipMemcpyHostToDevice, S->s_h2d2));
+    HIPCHK(hipEventRecord(S->pev_h[c], S->s_h2d));
+    HIPCHK(hipEventRecord(S->pev_h2[c], S->s_h2d2));
+  }
+  // (2) per chunk: the merge kernel and the placement scan on the compute stream, the packing on the output
+  // stream (it overlaps the next chunk's merge)
+  for (uint32_t c = 0; c < nc; c++) {
+    const uint32_t d0 = cut[c], d1 = cut[c + 1];
+    if (d1 == d0) continue;
+    const uint32_t u0 = du[d0], u1 = du[d1];
+    if (!zin) {
+      HIPCHK(hipStreamWaitEvent(st, S->pev_h[c], 0));
+      HIPCHK(hipStreamWaitEvent(st, S->pev_h2[c], 0));
+    }
+    const uint32_t o0 = c == 0 ? 0 : u0 & ~15u;
+    if (v2) k_widen<<<(u1 - o0 + 256) / 256, 256, 0, st>>>(dO + o0, S->in_off.as<uint64_t>() + o0, u1 - o0 + 1);
+    GeneralJob jc = j;
+    jc.doc_upd = dD + d0;
+    jc.n = d1 - d0;
+    jc.doc_base = d0;
+    jc.status = S->status.as<int32_t>() + d0;
+    jc.out_off = S->out_off.as<uint64_t>() + d0;
+    jc.out_len = S->out_len.as<uint64_t>() + d0;
+    const int fr = v2 ? fast2_launch(OP_MERGE, jc, nu, st) : fast_launch(OP_MERGE, jc, nu, st);
+    if (fr != 1) return -3;
+    k_chunk_scan<<<1, 1024, 0, st>>>(jc.status, jc.out_len, jc.n, S->cmp_off.as<uint64_t>() + d0, S->cmp_len.as<uint64_t>() + d0,
+                                      counters + 20, S->pipe_host_dev, c, j.pend_count, c + 1 == nc,
+                                      direct ? h_off + d0 : nullptr, direct ? h_len + d0 : nullptr,
+                                      direct ? h_st + d0 : nullptr);
+    HIPCHK(hipEventRecord(S->pev_k[c], st));
+    HIPCHK(hipStreamWaitEvent(S->s_d2h, S->pev_k[c], 0));
+    k_pack_docs<<<(jc.n + 3) / 4, 256, 0, S->s_d2h>>>(j.out, jc.out_off, S->cmp_off.as<uint64_t>() + d0,
+                                                      S->cmp_len.as<uint64_t>() + d0, jc.n,
+                                                      direct ? h_arena : S->cmp_arena.as<uint8_t>(), direct ? out->cap : ~0ull);
+    if (!direct) HIPCHK(hipEventRecord(S->pev_p[c], S->s_d2h));
+  }
+  if (stats) HIPCHK(hipEventRecord(S->ev1, st));
+  // (3) copy mode: each chunk's packed range as soon as it is packed
+  uint64_t total = 0;
+  bool over = false;
+  for (uint32_t c = 0; c < nc && !direct; c++) {
+    if (cut[c + 1] == cut[c]) continue;
+    hipError_t q = hipEventQuery(S->pev_p[c]);
+    for (uint64_t it = 0; q == hipErrorNotReady && it < (1ull << 28); it++) {
+      __builtin_ia32_pause();
+      q = hipEventQuery(S->pev_p[c]);
+    }
+    if (q != hipSuccess) HIPCHK(hipEventSynchronize(S->pev_p[c]));
+    const uint64_t lo = hw[2 * c], hi = hw[2 * c + 1];
+    if (lo == ~0ull || hi < lo) return -4;
+    if (hi > out->cap) over = true;
+    if (over) continue;
+    // the range widened to 64-byte boundaries (an unaligned copy runs as a blit kernel): the bytes past hi
+    // belong to the next chunk and are copied again, correctly, by its own copy later on this stream; past the
+    // last chunk they are unused capacity
+    const uint64_t alo = lo & ~63ull, ahe = (hi + 63) & ~63ull, ahi = ahe < out->cap ? ahe : out->cap;
+    if (ahi > alo)
+      HIPCHK(hipMemcpyAsync(out->arena + alo, S->cmp_arena.as<uint8_t>() + alo, ahi - alo, hipMemcpyDeviceToHost, S->s_d2h));
+    const uint32_t d0 = cut[c], n = cut[c + 1] - cut[c];  // the chunk's offsets, lengths and statuses
+    HIPCHK(hipMemcpyAsync(out->out_off + d0, S->cmp_off.as<uint64_t>() + d0, n * 8ull, hipMemcpyDeviceToHost, S->s_d2h));
+    HIPCHK(hipMemcpyAsync(out->out_len + d0, S->cmp_len.as<uint64_t>() + d0, n * 8ull, hipMemcpyDeviceToHost, S->s_d2h));
+    HIPCHK(hipMemcpyAsync(out->status + d0, S->status.as<int32_t>() + d0, n * 4ull, hipMemcpyDeviceToHost, S->s_d2h));
+  }
+  HIPCHK(hipStreamSynchronize(S->s_d2h));
+  {
+    uint32_t c = nc;
+    while (c > 0 && cut[c] == cut[c - 1]) c--;
+    total = c > 0 ? hw[2 * (c - 1) + 1] : 0;
+    if (total > out->cap) over = true;
+  }
+  const uint64_t nbad = hw[61];
+  if (nbad != 0) {  // a declined (or capacity) document: the whole call through the exact flow
+    S->pipe_skip = true;
+    const int r = run_op(OP_MERGE, b, out, st, stats);
+    S->pipe_skip = false;
+    return r;
+  }
+  out->used = total;
+  if (over) return YM_ERR_CAPACITY;
+  if (stats) {
+    memset(stats, 0, sizeof(*stats));
+    float ms = 0;
+    hipEventElapsedTime(&ms, S->ev0, S->ev1);
+    stats->device_ms = ms;
+    stats->docs = stats->docs_fast = nd;
+    stats->bytes_in = A_hi - A_lo;
+    stats->bytes_out = total;
+  }
+  return 0;
+}
+
 constexpr uint32_t NESTED_PROBE = 16;
-int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *stats, int depth = 0) {
+int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *stats, int depth) {
   if (!b || !out) return -1;
   DevState *S = state();
   {  // the caller (e.g. torch) may have switched this thread's device
@@ -486,15 +766,14 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   uint32_t nd = b->n_docs;
   if (stats) memset(stats, 0, sizeof(*stats));
   if (nd == 0) { out->used = 0; return 0; }
-  const uint8_t *A = b->arena;
   const bool off32 = (b->format & YM_OFF32) != 0;
+  // host merges of many documents with u32 offsets: the pipelined path (depth 8 = its own fallback)
+  if (op == OP_MERGE && off32 && b->mem == YM_MEM_HOST && depth == 0 && !S->pipe_skip && nd >= PIPE_MIN_DOCS &&
+      !getenv("YMERGE_NO_PIPE"))
+    return run_host_pipe(S, b, out, st, stats);
+  const uint8_t *A = b->arena;
   const uint64_t *upd_off = off32 ? nullptr : b->upd_off;
-  std::vector<uint64_t> host_off;
-  if (off32 && b->mem == YM_MEM_HOST) {  // host batches: widened here, staged as u64
-    const uint32_t *o32 = reinterpret_cast<const uint32_t *>(b->upd_off);
-    host_off.assign(o32, o32 + b->n_upd + 1);
-    upd_off = host_off.data();
-  }
+  const uint32_t *upd_off32 = off32 ? reinterpret_cast<const uint32_t *>(b->upd_off) : nullptr;  // (host or device)
   const uint32_t *doc_upd = b->doc_upd;
   const uint8_t *svp = b->sv_arena;
   const uint64_t *sv_off = b->sv_off;
@@ -505,20 +784,27 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   // device output capacity: the caller's (device batches); for host batches the library's own staging,
   // at least the internal bound (the caller's buffer only receives the packed outputs)
   uint64_t dev_cap = out->cap;
-  if (host) {  // stage inputs
-    uint64_t abytes = upd_off[b->n_upd];
+  if (host) {  // stage inputs (u32 offsets as they are: widened on the device where a kernel reads u64)
+    uint64_t abytes = off32 ? upd_off32[b->n_upd] : upd_off[b->n_upd];
     // ym_diff's state vectors; ym_compact's optional target state vectors
     const bool stage_sv = op == OP_DIFF || (op == OP_COMPACT && svp);
     const uint64_t svb = stage_sv ? sv_off[nd] : 0;
     const uint64_t bound = 4 * abytes + 2 * svb + 128ull * nd + 8192;
     dev_cap = out->cap > bound ? out->cap : bound;
     if (S->min_stage_cap > dev_cap) dev_cap = S->min_stage_cap;
-    if (S->in_arena.ensure(abytes + 16) || S->in_off.ensure((b->n_upd + 1) * 8ull) || S->in_doc.ensure((nd + 1) * 4ull)) return -2;
+    if (S->in_arena.ensure(abytes + 16) || S->in_doc.ensure((nd + 1) * 4ull)) return -2;
     HIPCHK(hipMemcpyAsync(S->in_arena.p, A, abytes, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(S->in_off.p, upd_off, (b->n_upd + 1) * 8ull, hipMemcpyHostToDevice, st));
+    if (off32) {
+      if (S->in_off32.ensure((b->n_upd + 1) * 4ull)) return -2;
+      HIPCHK(hipMemcpyAsync(S->in_off32.p, upd_off32, (b->n_upd + 1) * 4ull, hipMemcpyHostToDevice, st));
+      upd_off32 = S->in_off32.as<uint32_t>();
+    } else {
+      if (S->in_off.ensure((b->n_upd + 1) * 8ull)) return -2;
+      HIPCHK(hipMemcpyAsync(S->in_off.p, upd_off, (b->n_upd + 1) * 8ull, hipMemcpyHostToDevice, st));
+      upd_off = S->in_off.as<uint64_t>();
+    }
     HIPCHK(hipMemcpyAsync(S->in_doc.p, doc_upd, (nd + 1) * 4ull, hipMemcpyHostToDevice, st));
     A = S->in_arena.as<uint8_t>();
-    upd_off = S->in_off.as<uint64_t>();
     doc_upd = S->in_doc.as<uint32_t>();
     if (stage_sv) {
       uint64_t sb = sv_off[nd];
@@ -546,7 +832,7 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
   memset(&j, 0, sizeof(j));
   j.A = A;
   j.upd_off = upd_off;
-  if (off32 && !host) j.upd_off32 = reinterpret_cast<const uint32_t *>(b->upd_off);
+  if (off32) j.upd_off32 = upd_off32;
   // device u32 offsets: the V1 fast kernel reads them as they are; every other kernel reads u64
   // offsets, widened here on first need
   auto widen = [&]() -> int {
@@ -743,12 +1029,8 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
     scan_excl<uint64_t>(nullptr, tmp, mlen, (uint64_t *)nullptr, nd, st);
     if (S->scan_tmp.ensure(tmp + 16)) return -2;
     if (scan_excl<uint64_t>(S->scan_tmp.p, tmp, mlen, S->cmp_off.as<uint64_t>(), nd, st)) return -3;
-    if (total) {
-      const uint64_t chunks = (total + PACK_CHUNK - 1) / PACK_CHUNK;
-      const uint32_t grid = chunks < 65536 ? (uint32_t)chunks : 65536;
-      k_pack<<<grid, PACK_THREADS, 0, st>>>(o_arena, o_off, mlen, S->cmp_off.as<uint64_t>(), S->cmp_arena.as<uint8_t>(),
-                                            nd, total);
-    }
+    // one wave per document (round 6; k_pack, a search per 16 output bytes, took 38 us for 10.6 MB)
+    if (total) k_pack_docs<<<(nd + 3) / 4, 256, 0, st>>>(o_arena, o_off, S->cmp_off.as<uint64_t>(), mlen, nd, S->cmp_arena.as<uint8_t>(), ~0ull);
   }
   if (total) HIPCHK(hipMemcpyAsync(out->arena, S->cmp_arena.p, total, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(out->out_off, S->cmp_off.p, nd * 8ull, hipMemcpyDeviceToHost, st));
@@ -779,8 +1061,16 @@ static void release_state(DevState *S) {
   DBuf *bufs[] = {&S->ws, &S->ws_size, &S->ws_off, &S->layout, &S->counters, &S->scan_tmp, &S->list_a, &S->list_b,
                   &S->flags, &S->bscratch, &S->in_arena, &S->in_off, &S->in_doc, &S->in_sv, &S->in_svoff, &S->out_arena,
                   &S->out_off, &S->out_len, &S->status, &S->cmp_off, &S->cmp_len, &S->cmp_arena, &S->async_off,
-                  &S->async2_ws, &S->async2_bs, &S->async2_off};
+                  &S->async2_ws, &S->async2_bs, &S->async2_off, &S->in_off32};
   for (DBuf *b : bufs) if (b->p) hipFree(b->p);
+  for (hipStream_t x : {S->s_h2d, S->s_h2d2, S->s_d2h}) if (x) { hipStreamSynchronize(x); hipStreamDestroy(x); }
+  for (int c = 0; c < 16; c++) {
+    if (S->pev_h[c]) hipEventDestroy(S->pev_h[c]);
+    if (S->pev_h2[c]) hipEventDestroy(S->pev_h2[c]);
+    if (S->pev_k[c]) hipEventDestroy(S->pev_k[c]);
+    if (S->pev_p[c]) hipEventDestroy(S->pev_p[c]);
+  }
+  if (S->pipe_host) hipHostFree(S->pipe_host);
   if (S->ev_async) hipEventDestroy(S->ev_async);
   if (S->ev_async2) hipEventDestroy(S->ev_async2);
   if (S->pinned) hipHostFree(S->pinned);
@@ -853,6 +1143,36 @@ const char *ym_strerror(int code) {
   }
 }
 
+// ---- pinned host memory pool (ym_host_alloc / ym_host_free) -----------------------------------------------
+// Page-locked buffers in power-of-two size classes (>= 64 KiB), kept on per-class free lists when released:
+// a serving loop that hands every call a fresh output arena (the Node addon's external ArrayBuffers) gets
+// memory the DMA engines write directly, without first-touch page faults or the runtime's staging copy.
+void *ym_host_alloc(size_t bytes) {
+  const int k = pool_class(bytes ? bytes : 1);
+  std::lock_guard<std::mutex> g(g_pool_mu);
+  void *p = nullptr;
+  if (!g_pool_free[k].empty()) {
+    p = g_pool_free[k].back();
+    g_pool_free[k].pop_back();
+  } else if (hipHostMalloc(&p, 1ull << k, hipHostMallocPortable) != hipSuccess) {
+    return nullptr;
+  }
+  g_pool_live.emplace_back(p, k);
+  return p;
+}
+
+void ym_host_free(void *p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> g(g_pool_mu);
+  for (size_t i = 0; i < g_pool_live.size(); i++) {
+    if (g_pool_live[i].first != p) continue;
+    g_pool_free[g_pool_live[i].second].push_back(p);
+    g_pool_live[i] = g_pool_live.back();
+    g_pool_live.pop_back();
+    return;
+  }
+}
+
 uint64_t ym_out_bound(const ym_batch *b) {
   // device batches: the fast-path slot region (2 * in + 64 per doc) followed by room for general-path
   // outputs; host batches: the packed outputs only (the library stages the slot region itself)
@@ -898,6 +1218,9 @@ int ym_merge_async(const ym_batch *b, ym_out *out, void *stream, uint32_t *pendi
       // device, stream-ordered) for the previous async call that read the buffer, on whatever stream it ran;
       // the synchronous entry points use other buffers, so interleaving them with async calls is safe.
       if (!S->ev_async) HIPCHK(hipEventCreateWithFlags(&S->ev_async, hipEventDisableTiming));
+      // growing the buffer frees the old one, which the previous async call (any stream) may still read: wait
+      // for it on the host first, as run_async does for its buffers
+      if ((b->n_upd + 1) * 8ull > S->async_off.cap) HIPCHK(hipEventSynchronize(S->ev_async));
       if (S->async_off.ensure((b->n_upd + 1) * 8ull)) return -2;
       HIPCHK(hipStreamWaitEvent(st, S->ev_async, 0));
       k_widen<<<(b->n_upd + 256) / 256, 256, 0, st>>>(j.upd_off32, S->async_off.as<uint64_t>(), b->n_upd + 1);

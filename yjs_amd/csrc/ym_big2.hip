@@ -18,6 +18,7 @@
 #include "ym_fast_common.h"
 #include "ym_kernels.h"
 #include "ym_cmap.h"
+#include "ym_pv2.h"
 
 namespace ymk {
 namespace big2 {
@@ -736,17 +737,24 @@ __global__ void __launch_bounds__(64) k_big_v2(GeneralJob j) {
 }  // namespace big2
 
 __global__ void k_big_init(GeneralJob j);  // ym_big.hip
-int small_v2_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t st, uint32_t diff_min);  // ym_fast2.hip
+int small_v2_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t st, uint32_t diff_min,
+                    uint64_t pv_min);  // ym_fast2.hip
+// batches of at most this many documents keep the V2 diff on k_big_v2 (one generation of one-document waves,
+// faster for wide rich documents than the lane walk: C4R 4 k 1.9 against 2.7 ms); the sync and async paths
+// share it (YMERGE_DF2_MIN overrides it, tests)
+constexpr uint32_t DF2_MIN_DOCS = 4096;
 int big2_launch(uint32_t op, const GeneralJob &j0, hipStream_t st, PwBufs &pwb) {
   if (!j0.v2 || (op != OP_SV && op != OP_DIFF && op != OP_META)) return 0;
   // many small updates (an update log): one update per lane (k_meta_v2), what it declines to the general path
-  if (op == OP_META && j0.n > 8 * BS_GRID) return small_v2_launch(op, j0, nullptr, st, 0);
+  if (op == OP_META && j0.n > 8 * BS_GRID) return small_v2_launch(op, j0, nullptr, st, 0, ~0ull);
   k_big_init<<<1, 64, 0, st>>>(j0);
   GeneralJob j = j0;
   // large single-section updates: the column-parallel path first (ym_pv2.hip); small ones one per lane
   // (parseUpdateMeta); k_big_v2 takes the rest
   if (int r = pv2_prepare(op, j0, st, pwb, &j.pw_done); r < 0) return r;
-  if (j.pw_done) small_v2_launch(op, j, const_cast<uint8_t *>(j.pw_done), st, 4096);
+  uint64_t pv_min = pv2::PV_MIN;  // (as pv2_prepare: the column path's documents are not the small kernels')
+  if (const char *e = getenv("YMERGE_PW_MIN")) pv_min = strtoull(e, nullptr, 10);
+  if (j.pw_done) small_v2_launch(op, j, const_cast<uint8_t *>(j.pw_done), st, DF2_MIN_DOCS, pv_min);
   if (int r = pv2_finish(j0, st, pwb); r < 0) return r;  // (waits for the prep's totals: the kernels above run)
   const uint32_t grid = j.n < BS_GRID ? j.n : BS_GRID;
   if (op == OP_DIFF) big2::k_big_v2<OP_DIFF><<<grid, 64, big2::LDS_BYTES, st>>>(j);
@@ -761,7 +769,7 @@ int big2_async_launch(uint32_t op, const GeneralJob &j0, uint8_t *done, uint32_t
   if (!j0.v2 || (op != OP_DIFF && op != OP_SV)) return 0;
   GeneralJob j = j0;
   j.pw_done = done;
-  small_v2_launch(op, j, done, st, grid_max);
+  small_v2_launch(op, j, done, st, DF2_MIN_DOCS, ~0ull);
   const uint32_t grid = j.n < grid_max ? j.n : grid_max;
   if (op == OP_DIFF) big2::k_big_v2<OP_DIFF><<<grid, 64, big2::LDS_BYTES, st>>>(j);
   else big2::k_big_v2<OP_SV><<<grid, 64, big2::LDS_BYTES, st>>>(j);

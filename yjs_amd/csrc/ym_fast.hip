@@ -829,7 +829,7 @@ __device__ __forceinline__ void merge_doc_v1(const GeneralJob &j, uint32_t di) {
     if (lane < 3 && nsec + lane < ((nsec + 3) & ~3u)) at<uint64_t>(M::L_SKEY + 8 * (nsec + lane)) = ~0ull;
     __syncthreads();
     // output slot: 64-aligned inside the bound 2 * in + 64 per doc (no global atomics)
-    const uint64_t slot = 2 * (b0 - uoff_g(j, 0)) + 64ull * d;
+    const uint64_t slot = 2 * (b0 - uoff_g(j, 0)) + 64ull * (d + j.doc_base);
     const uint64_t slot_al = (slot + 63) & ~63ull;
     const uint64_t slot_end = slot + 2 * bytes + 64 < j.cap ? slot + 2 * bytes + 64 : j.cap;
     if (slot_al >= slot_end) YM_DECLINE()

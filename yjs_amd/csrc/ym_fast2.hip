@@ -669,7 +669,7 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v2(GeneralJob j, uint32_
     }
     const uint32_t rest_base = colbytes + vsz(nparts);
     // output slot (as the V1 fast path): 16-aligned inside 2 * in + 64 per doc
-    const uint64_t slot = 2 * (b0 - arena0) + 64ull * d;
+    const uint64_t slot = 2 * (b0 - arena0) + 64ull * (d + j.doc_base);
     const uint64_t slot_al = (slot + 15) & ~15ull;
     const uint64_t slot_end = slot + 2 * bytes + 64 < j.cap ? slot + 2 * bytes + 64 : j.cap;
     if (slot_al + rest_base + rest_bytes > slot_end) {
@@ -1063,7 +1063,7 @@ __device__ __forceinline__ int meta_walk_v2(uint32_t p0, uint32_t p1, uint32_t t
   return bad ? -1 : (int)nsec;
 }
 template <int OP, uint32_t ND, uint32_t WIN, uint32_t NSEC>
-__global__ void __launch_bounds__(64) k_small_v2(GeneralJob j, uint8_t *done) {
+__global__ void __launch_bounds__(64) k_small_v2(GeneralJob j, uint8_t *done, uint64_t pv_min) {
   using L = Sv2Lay<ND, WIN, NSEC>;
   const uint32_t lane = threadIdx.x;
   const uint32_t d0 = blockIdx.x * ND, d = d0 + lane;
@@ -1084,7 +1084,8 @@ __global__ void __launch_bounds__(64) k_small_v2(GeneralJob j, uint8_t *done) {
     const uint32_t u0 = j.doc_upd[d];
     if (j.doc_upd[d + 1] - u0 == 1 && !(done && done[d])) {
       const uint64_t a = j.upd_off[u0], b = j.upd_off[u0 + 1];
-      if (a >= w0 && b <= w0 + wbytes && b > a) ns = meta_walk_v2((uint32_t)(a - w0), (uint32_t)(b - w0), tab, NSEC);
+      // (from pv_min on, a document is the column path's: the two sets stay disjoint)
+      if (a >= w0 && b <= w0 + wbytes && b > a && b - a < pv_min) ns = meta_walk_v2((uint32_t)(a - w0), (uint32_t)(b - w0), tab, NSEC);
     }
   }
   // meta: vu(n) | (client, first)* | vu(n) | (client, end)*;  sv: vu(m) | (client, end)* over the m sections
@@ -1296,7 +1297,7 @@ __device__ __forceinline__ uint32_t pd_idif(PIdif &r) {  // rd_idif
 }  // namespace df2
 
 template <uint32_t ND, uint32_t WIN, uint32_t POOL, int OCC>
-__global__ void __launch_bounds__(64, OCC) k_diff_small_v2(GeneralJob j, uint8_t *done) {
+__global__ void __launch_bounds__(64, OCC) k_diff_small_v2(GeneralJob j, uint8_t *done, uint64_t pv_min) {
   using namespace df2;
   using L = Df2Lay<ND, WIN, POOL>;
   const uint32_t lane = threadIdx.x;
@@ -1321,7 +1322,7 @@ __global__ void __launch_bounds__(64, OCC) k_diff_small_v2(GeneralJob j, uint8_t
     const uint32_t u0 = j.doc_upd[d];
     if (j.doc_upd[d + 1] - u0 == 1 && !done[d]) {
       const uint64_t a = j.upd_off[u0], b = j.upd_off[u0 + 1], sa = j.sv_off[d], sb = j.sv_off[d + 1];
-      ok = a >= w0 && b <= w0 + wbytes && b > a && sa >= v0 && sb <= v0 + vbytes && sb >= sa;
+      ok = a >= w0 && b <= w0 + wbytes && b > a && b - a < pv_min && sa >= v0 && sb <= v0 + vbytes && sb >= sa;
       p0 = (uint32_t)(a - w0); p1 = (uint32_t)(b - w0);
       s0 = L::SV + (uint32_t)(sa - v0); s1 = L::SV + (uint32_t)(sb - v0);
     }
@@ -1663,16 +1664,17 @@ __global__ void __launch_bounds__(64, OCC) k_diff_small_v2(GeneralJob j, uint8_t
 // done: the streamed walker's done array (nullptr: the kernel is the call's only specialised pass, its
 // declines go to the general path).  Meta: 64 updates of an update log per wave (4 KB window); state
 // vectors: 4 merged documents per wave (~1 KB each: an 8 KB window, 32 sections each).
-int small_v2_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t st, uint32_t diff_min) {
+// pv_min: the column path's smallest update in this call (its documents are not taken here); ~0: no column path
+int small_v2_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t st, uint32_t diff_min, uint64_t pv_min) {
   static const bool off = getenv("YMERGE_NO_SMALL_V2") != nullptr;
   if (off || !j.v2 || j.n == 0) return 0;
   using namespace fastv2;
   if (op == OP_META) {
-    k_small_v2<OP_META, 64, 4096, 8><<<(j.n + 63) / 64, 64, Sv2Lay<64, 4096, 8>::BYTES, st>>>(j, done);
+    k_small_v2<OP_META, 64, 4096, 8><<<(j.n + 63) / 64, 64, Sv2Lay<64, 4096, 8>::BYTES, st>>>(j, done, pv_min);
   } else if (op == OP_SV) {
     // 4 documents per wave with an 8 KB window: one generation of short waves (C2, 10 k documents: 0.41 ms at
     // 16 per wave, 0.42 at 8, 0.31 at 4 and 0.32 at 2)
-    k_small_v2<OP_SV, 4, 8192, 32><<<(j.n + 3) / 4, 64, Sv2Lay<4, 8192, 32>::BYTES, st>>>(j, done);
+    k_small_v2<OP_SV, 4, 8192, 32><<<(j.n + 3) / 4, 64, Sv2Lay<4, 8192, 32>::BYTES, st>>>(j, done, pv_min);
   } else if (op == OP_DIFF && done && j.sv) {
     // documents per wave so that the batch is one generation of waves (2 per SIMD: 2,048 on the chip; a
     // second generation doubles the call: C2, 10 k documents, 4 per wave 0.93 ms against 5 per wave 0.56),
@@ -1686,7 +1688,7 @@ int small_v2_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t
     if (j.n <= diff_min) return 0;
     const uint32_t nd = j.n <= 2048 ? 1 : j.n <= 4096 ? 2 : j.n <= 6144 ? 3 : j.n <= 8192 ? 4 : 5;
 #define DF2(N) \
-  if (nd == N) k_diff_small_v2<N, 7680, 7680, 1><<<(j.n + N - 1) / N, 64, Df2Lay<N, 7680, 7680>::BYTES, st>>>(j, done);
+  if (nd == N) k_diff_small_v2<N, 7680, 7680, 1><<<(j.n + N - 1) / N, 64, Df2Lay<N, 7680, 7680>::BYTES, st>>>(j, done, pv_min);
     DF2(1) DF2(2) DF2(3) DF2(4) DF2(5)
 #undef DF2
   } else {

@@ -15,7 +15,22 @@ extern __shared__ __attribute__((aligned(16))) uint8_t sm[];
 template <class T>
 __device__ __forceinline__ T &at(uint32_t off) { return *reinterpret_cast<T *>(sm + off); }
 // unaligned LDS accesses (gfx950 runs them in hardware: tools/probe/lds_unaligned.hip)
+#ifdef YM_LD8_ALIGNED
+// 8 bytes at any offset from two 8-aligned LDS reads (one ds_read2_b64) and byte funnel shifts: unaligned
+// ds_read_b64s stall the CU's LDS pipeline (SQ_LDS_UNALIGNED_STALL) for every wave on it.  Reads up to 15
+// bytes past p.
+__device__ __forceinline__ uint64_t ld8(uint32_t p) {
+  const uint32_t a = p & ~7u;
+  const uint64_t q0 = *reinterpret_cast<const uint64_t *>(sm + a), q1 = *reinterpret_cast<const uint64_t *>(sm + a + 8);
+  const uint32_t d0 = (uint32_t)q0, d1 = (uint32_t)(q0 >> 32), d2 = (uint32_t)q1, d3 = (uint32_t)(q1 >> 32);
+  const bool k = (p & 4u) != 0;
+  const uint32_t x0 = k ? d1 : d0, x1 = k ? d2 : d1, x2 = k ? d3 : d2, s = p & 3u;
+  const uint32_t lo = __builtin_amdgcn_alignbyte(x1, x0, s), hi = __builtin_amdgcn_alignbyte(x2, x1, s);
+  return ((uint64_t)hi << 32) | lo;
+}
+#else
 __device__ __forceinline__ uint64_t ld8(uint32_t p) { uint64_t x; __builtin_memcpy(&x, sm + p, 8); return x; }
+#endif
 __device__ __forceinline__ uint32_t ld4(uint32_t p) { uint32_t x; __builtin_memcpy(&x, sm + p, 4); return x; }
 __device__ __forceinline__ void st4(uint32_t p, uint32_t x) { __builtin_memcpy(sm + p, &x, 4); }
 
@@ -406,7 +421,7 @@ __device__ __forceinline__ void rank_exact(uint32_t keys, uint32_t n, const uint
 __device__ __forceinline__ void decline(const GeneralJob &j, uint32_t d) {
   j.status[d] = ST_PENDING;
   const uint32_t q = atomicAdd(j.pend_count, 1u);
-  if (j.pend_list) j.pend_list[q] = d;  // (ym_merge_async: declines are only counted)
+  if (j.pend_list) j.pend_list[q] = d + j.doc_base;  // (ym_merge_async: declines are only counted)
 }
 }  // namespace fastc
 }  // namespace ymk

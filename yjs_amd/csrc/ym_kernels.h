@@ -50,6 +50,9 @@ struct GeneralJob {
   uint8_t *bscratch;         // streamed single-update kernels: BS_BYTES per block (ym_big*.hip)
   const uint8_t *pw_done;    // V1 diff / sv: documents the chunk-parallel walk completed (ym_pwalk.hip)
   uint64_t *pw_count;        // ... and their number (a device counter k_finish reports and resets)
+  uint32_t doc_base;         // merge fast paths over one chunk of a pipelined host batch (ym_api.hip run_host_pipe):
+                             // doc_upd / status / out_off / out_len start at document doc_base of the batch, whose
+                             // id this adds to the slot position and the declined list (0 elsewhere)
 };
 
 // Per-block HBM scratch of the streamed diff / state-vector kernels (ym_big.hip, ym_big2.hip): client

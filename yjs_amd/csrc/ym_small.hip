@@ -141,7 +141,7 @@ __device__ __forceinline__ uint32_t head(uint32_t s0, uint32_t s1, uint32_t info
 
 // OP_DIFF / OP_SV / OP_META over documents [blockIdx.x * ND, + ND) that are one update of <= SLOT - 48 bytes
 template <int OP, uint32_t ND, uint32_t SLOT, uint32_t NSEC, uint32_t NSVE>
-__global__ void __launch_bounds__(64) k_small_v1(GeneralJob j, uint8_t *done) {
+__global__ void __launch_bounds__(64) k_small_v1(GeneralJob j, uint8_t *done, uint64_t pw_min) {
   using L = Lay<ND, SLOT, NSEC, NSVE>;
   const uint32_t lane = threadIdx.x;
   const uint32_t d0 = blockIdx.x * ND;
@@ -153,7 +153,7 @@ __global__ void __launch_bounds__(64) k_small_v1(GeneralJob j, uint8_t *done) {
     const uint32_t u0 = j.doc_upd[d];
     if (j.doc_upd[d + 1] - u0 != 1 || done[d]) return;
     const uint64_t b0 = j.upd_off[u0], len = j.upd_off[u0 + 1] - b0;
-    if (len == 0 || len + 48 > SLOT) return;
+    if (len == 0 || len + 48 > SLOT || len >= pw_min) return;
     const uint4 *src = reinterpret_cast<const uint4 *>(j.A + (b0 & ~15ull));
     const uint32_t nvec = (uint32_t)(((b0 & 15) + len + 15) >> 4);
     for (uint32_t v = v0; v < nvec; v += dv) at<uint4>(l * SLOT + 16 * v) = src[v];
@@ -167,7 +167,8 @@ __global__ void __launch_bounds__(64) k_small_v1(GeneralJob j, uint8_t *done) {
   const uint32_t u0 = j.doc_upd[d];
   if (j.doc_upd[d + 1] - u0 != 1 || done[d]) return;
   const uint64_t ub = j.upd_off[u0], len64 = j.upd_off[u0 + 1] - ub;
-  if (len64 == 0 || len64 + 48 > SLOT) return;
+  // (from pw_min on the document is the chunk walk's: the two sets stay disjoint, as k_pw_small's)
+  if (len64 == 0 || len64 + 48 > SLOT || len64 >= pw_min) return;
   const uint32_t len = (uint32_t)len64;
   const uint32_t B = lane * SLOT + (uint32_t)(ub & 15), E = B + len;  // the update's bytes: LDS [B, E)
   const uint32_t REC = L::REC + lane * NSEC * 20;                      // u32[NSEC][5]
@@ -374,13 +375,15 @@ int small_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t st
   using namespace smallv1;
   if (!done || j.v2 || getenv("YMERGE_NO_SMALL")) return 0;
   const uint32_t g64 = (j.n + 63) / 64, g16 = (j.n + 15) / 16;
+  uint64_t pw_min = 32768;  // ym_pwalk.hip PW_MIN: the chunk walk's documents (YMERGE_PW_MIN, as pw_prepare)
+  if (const char *e = getenv("YMERGE_PW_MIN")) pw_min = strtoull(e, nullptr, 10);
   // tiny: 64 documents of <= 80 bytes (2 sections, 16 state-vector entries); small: 16 of <= 2 KB (32 each;
   // more: k_pw_small)
   // (the 2 KB shape for meta only: measured on C2 / C2r / C4r merged documents, diff and state vector run
   // faster as one wave per document, k_pw_small -- a rich document's lanes diverge in the parsers)
 #define YS_LAUNCH(O)                                                                                         \
-  k_small_v1<O, 64, 128, 8, 16><<<g64, 64, Lay<64, 128, 8, 16>::BYTES, st>>>(j, done);                    \
-  if (O == OP_META && !tiny_only) k_small_v1<O, 16, 2112, 32, 32><<<g16, 64, Lay<16, 2112, 32, 32>::BYTES, st>>>(j, done);
+  k_small_v1<O, 64, 128, 8, 16><<<g64, 64, Lay<64, 128, 8, 16>::BYTES, st>>>(j, done, pw_min);                    \
+  if (O == OP_META && !tiny_only) k_small_v1<O, 16, 2112, 32, 32><<<g16, 64, Lay<16, 2112, 32, 32>::BYTES, st>>>(j, done, pw_min);
   if (op == OP_DIFF) { YS_LAUNCH(OP_DIFF) }
   else if (op == OP_SV) { YS_LAUNCH(OP_SV) }
   else if (op == OP_META) { YS_LAUNCH(OP_META) }

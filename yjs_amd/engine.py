@@ -94,7 +94,8 @@ class _Stats(ctypes.Structure):
 
 
 EXPORTS = ("ym_init", "ym_shutdown", "ym_strerror", "ym_out_bound", "ym_merge", "ym_diff", "ym_sv", "ym_convert",
-           "ym_meta", "ym_ds_merge", "ym_snapshot", "ym_compact", "ym_merge_async", "ym_diff_async", "ym_sv_async")
+           "ym_meta", "ym_ds_merge", "ym_snapshot", "ym_compact", "ym_merge_async", "ym_diff_async", "ym_sv_async",
+           "ym_host_alloc", "ym_host_free")
 YM_PENDING = 101  # ym_*_async: declined by the async kernels (pass the document to ym_merge / ym_diff / ym_sv)
 
 
@@ -109,6 +110,10 @@ def load_library(path=None):
     for fn in (L.ym_merge, L.ym_diff, L.ym_sv, L.ym_convert, L.ym_meta, L.ym_ds_merge, L.ym_snapshot, L.ym_compact):
         fn.argtypes = [ctypes.POINTER(_Batch), ctypes.POINTER(_Out), ctypes.c_void_p, ctypes.POINTER(_Stats)]
         fn.restype = ctypes.c_int
+    L.ym_host_alloc.argtypes = [ctypes.c_size_t]
+    L.ym_host_alloc.restype = ctypes.c_void_p
+    L.ym_host_free.argtypes = [ctypes.c_void_p]
+    L.ym_host_free.restype = None
     for fn in (L.ym_merge_async, L.ym_diff_async, L.ym_sv_async):
         fn.argtypes = [ctypes.POINTER(_Batch), ctypes.POINTER(_Out), ctypes.c_void_p, ctypes.c_void_p]
         fn.restype = ctypes.c_int
@@ -158,6 +163,45 @@ def _torch_first():
                       "process may not work", RuntimeWarning)
 
 
+class HostOut:
+    """Reusable page-locked output arrays for run_host (ym_host_alloc): the device-to-host copies land in them
+    directly.  The arrays run_host returns with out=... are views into these buffers, valid until the next call
+    that uses them; close() (or garbage collection) gives the memory back to the library's pool."""
+
+    def __init__(self, engine, n_docs, cap):
+        L = engine.lib
+        self._lib = L
+        n = max(int(n_docs), 1)
+        self.cap = int(cap)
+        self._ptrs = []
+
+        def alloc(count, dtype):
+            nbytes = max(count * np.dtype(dtype).itemsize, 1)
+            p = L.ym_host_alloc(nbytes)
+            if not p:
+                raise MemoryError("ym_host_alloc failed")
+            self._ptrs.append(p)
+            buf = (ctypes.c_uint8 * nbytes).from_address(p)
+            return np.frombuffer(buf, dtype=dtype, count=count)
+
+        self.arena = alloc(max(self.cap, 1), np.uint8)
+        self.out_off = alloc(n, np.uint64)
+        self.out_len = alloc(n, np.uint64)
+        self.status = alloc(n, np.int32)
+        self.n_docs = n
+
+    def close(self):
+        for p in self._ptrs:
+            self._lib.ym_host_free(p)
+        self._ptrs = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
+
+
 class Engine:
     """One engine per process/GPU (the library keeps one HIP stream and workspace per thread).
     torch_first=False skips importing and initialising torch (host batches only: run_host and the batch
@@ -187,11 +231,32 @@ class Engine:
         return fmt | extra.get(op, 0)
 
     # ---- host-memory batches ------------------------------------------------------------------
-    def run_host(self, op, fmt, arena, upd_off, doc_upd, sv_arena=None, sv_off=None):
+    def host_array(self, count, dtype=np.uint8):
+        """A numpy array in page-locked memory from the library's pool (ym_host_alloc): host batches packed
+        into such arrays are copied in by the DMA engines directly (no per-call page pinning).  The memory goes
+        back to the pool when the array (and every view of it) is garbage collected."""
+        import weakref
+        nbytes = max(int(count) * np.dtype(dtype).itemsize, 1)
+        p = self.lib.ym_host_alloc(nbytes)
+        if not p:
+            raise MemoryError("ym_host_alloc failed")
+        buf = (ctypes.c_uint8 * nbytes).from_address(p)
+        weakref.finalize(buf, self.lib.ym_host_free, p)
+        return np.frombuffer(buf, dtype=dtype, count=int(count))
+
+    def host_out(self, n_docs, cap):
+        """Page-locked output arrays for run_host(..., out=...) (see HostOut)."""
+        return HostOut(self, n_docs, cap)
+
+    def run_host(self, op, fmt, arena, upd_off, doc_upd, sv_arena=None, sv_off=None, out=None):
         """Runs op ('merge'|'diff'|'sv'|'conv'|'meta'|'dsmerge') over a packed host batch.
+        upd_off: u64 offsets, or u32 (an arena below 4 GiB: passed as YM_OFF32, half the bytes to copy; host
+        merges of >= 4,096 documents then run pipelined, include/ymerge.h).  out: a HostOut to write into
+        (its arrays are returned, as views); by default fresh arrays.
         Returns (out_arena u8, out_off u64, out_len u64, status i32)."""
         arena = np.ascontiguousarray(arena, np.uint8)
-        upd_off = np.ascontiguousarray(upd_off, np.uint64)
+        off32 = isinstance(upd_off, np.ndarray) and upd_off.dtype == np.uint32
+        upd_off = np.ascontiguousarray(upd_off, np.uint32 if off32 else np.uint64)
         doc_upd = np.ascontiguousarray(doc_upd, np.uint32)
         n_docs = len(doc_upd) - 1
         n_upd = len(upd_off) - 1
@@ -202,7 +267,7 @@ class Engine:
         b.doc_upd = doc_upd.ctypes.data
         b.n_docs = n_docs
         b.n_upd = n_upd
-        b.format = self._format(op, fmt)
+        b.format = self._format(op, fmt) | (YM_OFF32 if off32 else 0)
         b.mem = 0
         if op == "diff" or sv_arena is not None:  # ym_diff's state vectors / ym_compact's target vectors
             # (a non-null arena even when every vector is empty: for ym_compact NULL means "no target")
@@ -213,6 +278,16 @@ class Engine:
             b.sv_off = sv_off.ctypes.data
         cap = int(self.lib.ym_out_bound(ctypes.byref(b)))
         fn = self._fn(op)
+        if out is not None and out.n_docs >= n_docs:
+            o = _Out(out.arena.ctypes.data, out.cap, out.out_off.ctypes.data, out.out_len.ctypes.data,
+                     out.status.ctypes.data, 0)
+            rc = fn(ctypes.byref(b), ctypes.byref(o), None, ctypes.byref(self.last_stats))
+            if rc == 0:
+                del keep
+                return out.arena[:int(o.used)], out.out_off[:n_docs], out.out_len[:n_docs], out.status[:n_docs]
+            if rc != 9:
+                raise RuntimeError(f"libymerge call failed: {rc} ({self.lib.ym_strerror(rc).decode()})")
+            cap = int(o.used) + 4096  # too small: fresh arrays below
         for _ in range(4):
             out_arena = np.zeros(max(cap, 1), np.uint8)
             out_off = np.zeros(max(n_docs, 1), np.uint64)
