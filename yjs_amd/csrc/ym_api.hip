@@ -243,6 +243,43 @@ __global__ void __launch_bounds__(256) k_pack_docs(const uint8_t *src, const uin
   for (uint64_t i = h + body + lane; i < L; i += 64) dst[dof + i] = src[so + i];
 }
 
+// Host -> HBM copy kernel (pipelined host merges with the batch in page-locked pool memory): up to three
+// 16-byte-granular segments, 16-byte loads of the host memory, four in flight per thread.  On the box it moves
+// 50-56 GB/s, as an SDMA copy does (tools/probe/h2d_kernel.hip), without the DMA queue's per-copy setup gaps
+// and its occasional multi-millisecond stalls.
+struct H2dSeg {
+  const uint4 *src;
+  uint4 *dst;
+  uint64_t n;  // 16-byte words
+};
+__global__ void __launch_bounds__(256) k_h2d_copy(H2dSeg s0, H2dSeg s1, H2dSeg s2) {
+  const uint64_t n01 = s0.n + s1.n, total = n01 + s2.n;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  auto at = [&](uint64_t i, const uint4 *&src, uint4 *&dst) {
+    if (i < s0.n) { src = s0.src + i; dst = s0.dst + i; }
+    else if (i < n01) { src = s1.src + (i - s0.n); dst = s1.dst + (i - s0.n); }
+    else { src = s2.src + (i - n01); dst = s2.dst + (i - n01); }
+  };
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < total; i += 4 * stride) {
+    const uint4 *sp[4];
+    uint4 *dp[4];
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) at(i + u * stride, sp[u], dp[u]);
+#pragma unroll
+    for (int u = 0; u < 4; u++) v[u] = *sp[u];
+#pragma unroll
+    for (int u = 0; u < 4; u++) *dp[u] = v[u];
+  }
+  for (; i < total; i += stride) {
+    const uint4 *sp;
+    uint4 *dp;
+    at(i, sp, dp);
+    *dp = *sp;
+  }
+}
+
 // YM_OFF32 offsets widened to u64 for the kernels that read u64 offsets
 __global__ void k_widen(const uint32_t *src, uint64_t *dst, uint32_t n) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -515,14 +552,20 @@ int run_general(DevState *S, hipStream_t st, GeneralJob j, uint32_t *list, uint3
 }
 
 // ---- pipelined host merges ---------------------------------------------------------------------------
-// A host batch of merges (u32 offsets, YM_OFF32) in document chunks of ~equal bytes, three streams deep:
-//   copy stream   H2D of chunk c's bytes, offsets and doc_upd entries           -> event h[c]
-//   compute       (waits h[c]) the LDS fast kernel over chunk c, its packing:   -> event k[c]
-//                 k_chunk_scan (placed after the previous chunks) + k_pack_docs
-//   copy stream 2 (host waits k[c], reads the chunk's packed range from mapped memory) D2H of chunk c
-// so the PCIe link carries chunk c + 1 in while chunk c's outputs go out (full duplex) and the kernels run
-// under the copies.  Optimistic: the fast kernels must take every document; if any is declined (or not OK)
-// the call runs again through the general flow (run_op, unpipelined), which handles everything exactly.
+// A host batch of merges (u32 offsets, YM_OFF32) in document chunks of ~6 MiB of input, three streams deep:
+//   copy stream   chunk c's bytes + offsets (+ the document ranges once): a copy kernel when the batch lives in
+//                 the library's page-locked pool (how the Node addon packs it), else DMA copies  -> event h[c]
+//   compute       (waits h[c]) the LDS fast kernel over chunk c, then k_chunk_scan (its documents' packed
+//                 offsets after the previous chunks', in stream order)                            -> event k[c]
+//   output        (waits k[c]) k_pack_docs: with every output array page-locked it writes the outputs,
+//                 offsets, lengths and statuses straight into host memory over PCIe; else into an HBM staging
+//                 arena that the host copies out chunk by chunk
+// so the link carries chunk c + 1 in while chunk c's outputs go out (full duplex) and the kernels run under
+// the copies.  Measured on the box (tools/pipe_sweep.sh, C2 V1 10 k documents, 17.4 MB in / 10.6 MB out): 0.79
+// ms per call with the batch in pool memory (copy kernels), 0.65 ms with DMA copies but with 7-8 ms stalls in
+// about one call in six (the DMA queue), 1.9 ms unpipelined.  Optimistic: the fast kernels must take every
+// document; if any is declined (or not OK) the call runs again through the general flow (run_op,
+// unpipelined), which handles everything exactly.
 // ---- the page-locked host pool's bookkeeping (ym_host_alloc / ym_host_free, below) ----
 std::mutex g_pool_mu;
 std::vector<void *> g_pool_free[64];
@@ -556,7 +599,7 @@ uint8_t *host_dev_ptr(const void *p) {
   return (uint8_t *)a.devicePointer + ((const uint8_t *)p - hp);
 }
 constexpr uint32_t PIPE_MIN_DOCS = 4096, PIPE_MAX = 16;
-constexpr uint64_t PIPE_CHUNK_BYTES = 3ull << 20;
+constexpr uint64_t PIPE_CHUNK_BYTES = 6ull << 20;
 int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *stats, int depth = 0);
 int run_host_pipe(DevState *S, const ym_batch *b, ym_out *out, hipStream_t st, ym_stats *stats) {
   const uint32_t nd = b->n_docs, nu = b->n_upd;
@@ -565,7 +608,11 @@ int run_host_pipe(DevState *S, const ym_batch *b, ym_out *out, hipStream_t st, y
   const uint64_t A_lo = o32[0], A_hi = o32[nu], abytes = A_hi;  // arena positions are absolute
   const bool v2 = (b->format & 0xff) == YM_V2;
   if (!S->s_h2d) {
-    HIPCHK(hipStreamCreateWithFlags(&S->s_h2d, hipStreamNonBlocking));
+    {  // the copy-in queue at the highest priority: its copy kernels are dispatched ahead of the merges
+      int lo = 0, hi = 0;
+      if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
+      HIPCHK(hipStreamCreateWithPriority(&S->s_h2d, hipStreamNonBlocking, getenv("YMERGE_PIPE_NOPRIO") ? 0 : hi));
+    }
     HIPCHK(hipStreamCreateWithFlags(&S->s_h2d2, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&S->s_d2h, hipStreamNonBlocking));
     for (uint32_t c = 0; c < PIPE_MAX; c++) {
@@ -578,7 +625,10 @@ int run_host_pipe(DevState *S, const ym_batch *b, ym_out *out, hipStream_t st, y
     HIPCHK(hipHostGetDevicePointer((void **)&S->pipe_host_dev, S->pipe_host, 0));
   }
   // chunk boundaries: documents, cut at ~equal input bytes
-  uint32_t nc = (uint32_t)((A_hi - A_lo + PIPE_CHUNK_BYTES - 1) / PIPE_CHUNK_BYTES);
+  static const uint64_t chunk_bytes = getenv("YMERGE_PIPE_CHUNK_KB") ? strtoull(getenv("YMERGE_PIPE_CHUNK_KB"), nullptr, 10) << 10
+                                                                     : PIPE_CHUNK_BYTES;
+  static const int alt = getenv("YMERGE_PIPE_ALT") ? atoi(getenv("YMERGE_PIPE_ALT")) : 0;
+  uint32_t nc = (uint32_t)((A_hi - A_lo + chunk_bytes - 1) / chunk_bytes);
   nc = nc < 2 ? 2 : nc > PIPE_MAX ? PIPE_MAX : nc;
   uint32_t cut[PIPE_MAX + 1];
   cut[0] = 0;
@@ -596,7 +646,7 @@ int run_host_pipe(DevState *S, const ym_batch *b, ym_out *out, hipStream_t st, y
   const uint64_t bound = 4 * abytes + 128ull * nd + 8192;
   uint64_t dev_cap = out->cap > bound ? out->cap : bound;
   if (S->min_stage_cap > dev_cap) dev_cap = S->min_stage_cap;
-  if (S->in_arena.ensure(abytes + 16) || S->in_off32.ensure((nu + 1) * 4ull) || S->in_doc.ensure((nd + 1) * 4ull) ||
+  if (S->in_arena.ensure(abytes + 64) || S->in_off32.ensure((nu + 1) * 4ull + 64) || S->in_doc.ensure((nd + 1) * 4ull + 64) ||
       S->out_arena.ensure(dev_cap + 16) || S->out_off.ensure(nd * 8ull) || S->out_len.ensure(nd * 8ull) ||
       S->status.ensure(nd * 4ull) || S->cmp_off.ensure(nd * 8ull + 8) || S->cmp_len.ensure(nd * 8ull + 8) ||
       S->cmp_arena.ensure(dev_cap + 16) || S->counters.ensure(1024) || S->list_a.ensure((nd + 1) * 4ull) ||
@@ -643,13 +693,23 @@ int run_host_pipe(DevState *S, const ym_batch *b, ym_out *out, hipStream_t st, y
   const uint32_t *z_off = pool_holds(o32, (nu + 1) * 4ull + 64) ? (const uint32_t *)host_dev_ptr(o32) : nullptr;
   const uint32_t *z_doc = pool_holds(du, (nd + 1) * 4ull + 64) ? (const uint32_t *)host_dev_ptr(du) : nullptr;
   const bool zin = z_arena && z_off && z_doc && !getenv("YMERGE_PIPE_NOZC");
-  if (zin) {
-    j.A = z_arena;
-    if (!v2) j.upd_off32 = z_off;
-    dO = const_cast<uint32_t *>(z_off);
-    dD = const_cast<uint32_t *>(z_doc);
+  // (1) every copy in, up front: pool-resident batches by a copy kernel per chunk on the copy stream (its
+  // bytes, its offsets, and with the first chunk the document ranges); otherwise DMA copies on two queues
+  // running back to back without waiting for the host
+  for (uint32_t c = 0; c < nc && zin; c++) {
+    const uint32_t d0 = cut[c], d1 = cut[c + 1];
+    if (d1 == d0) continue;
+    const uint32_t u0 = du[d0], u1 = du[d1];
+    const uint64_t a0 = c == 0 ? 0 : o32[u0] & ~63ull, a1e = c + 1 == nc ? A_hi : (o32[u1] + 63) & ~63ull;
+    const uint64_t a1 = ((a1e < A_hi ? a1e : A_hi) + 15) & ~15ull;
+    const uint32_t o0 = c == 0 ? 0 : u0 & ~15u, o1e = c + 1 == nc ? nu + 1 : ((u1 + 1 + 15) & ~15u);
+    const uint32_t o1 = ((o1e < nu + 1 ? o1e : nu + 1) + 3) & ~3u;
+    const H2dSeg sa = {(const uint4 *)(z_arena + a0), (uint4 *)(dA + a0), (a1 - a0) / 16};
+    const H2dSeg so = {(const uint4 *)(z_off + o0), (uint4 *)(dO + o0), (o1 - o0) / 4ull};
+    const H2dSeg sd = {(const uint4 *)z_doc, (uint4 *)dD, c == 0 ? (nd + 1 + 3) / 4ull : 0};
+    k_h2d_copy<<<512, 256, 0, S->s_h2d>>>(sa, so, sd);
+    HIPCHK(hipEventRecord(S->pev_h[c], S->s_h2d));
   }
-  // (1) every copy in, up front: the two DMA queues run back to back without waiting for the host
   if (!zin) HIPCHK(hipMemcpyAsync(dD, du, (nd + 1) * 4ull, hipMemcpyHostToDevice, S->s_h2d2));  // doc_upd: one copy
   for (uint32_t c = 0; c < nc && !zin; c++) {
     const uint32_t d0 = cut[c], d1 = cut[c + 1];
@@ -660,12 +720,15 @@ int run_host_pipe(DevState *S, const ym_batch *b, ym_out *out, hipStream_t st, y
     // shares with the neighbouring chunk are copied twice, the same values, in stream order)
     const uint64_t a0 = c == 0 ? 0 : o32[u0] & ~63ull, a1e = c + 1 == nc ? A_hi : (o32[u1] + 63) & ~63ull;
     const uint64_t a1 = a1e < A_hi ? a1e : A_hi;
-    if (a1 > a0) HIPCHK(hipMemcpyAsync(dA + a0, b->arena + a0, a1 - a0, hipMemcpyHostToDevice, S->s_h2d));
+    // (alt: chunk c's bytes and offsets both on queue c & 1, so one queue's per-copy setup overlaps the other's
+    // transfer; otherwise bytes on one queue, offsets on the other)
+    hipStream_t qa = alt && (c & 1) ? S->s_h2d2 : S->s_h2d, qo = alt ? qa : S->s_h2d2;
+    if (a1 > a0) HIPCHK(hipMemcpyAsync(dA + a0, b->arena + a0, a1 - a0, hipMemcpyHostToDevice, qa));
     const uint32_t o0 = c == 0 ? 0 : u0 & ~15u, o1e = c + 1 == nc ? nu + 1 : ((u1 + 1 + 15) & ~15u);
     const uint32_t o1 = o1e < nu + 1 ? o1e : nu + 1;
-    HIPCHK(hipMemcpyAsync(dO + o0, o32 + o0, (o1 - o0) * 4ull, hipMemcpyHostToDevice, S->s_h2d2));
-    HIPCHK(hipEventRecord(S->pev_h[c], S->s_h2d));
-    HIPCHK(hipEventRecord(S->pev_h2[c], S->s_h2d2));
+    HIPCHK(hipMemcpyAsync(dO + o0, o32 + o0, (o1 - o0) * 4ull, hipMemcpyHostToDevice, qo));
+    HIPCHK(hipEventRecord(S->pev_h[c], qa));
+    HIPCHK(hipEventRecord(S->pev_h2[c], qo));
   }
   // (2) per chunk: the merge kernel and the placement scan on the compute stream, the packing on the output
   // stream (it overlaps the next chunk's merge)
@@ -673,10 +736,8 @@ int run_host_pipe(DevState *S, const ym_batch *b, ym_out *out, hipStream_t st, y
     const uint32_t d0 = cut[c], d1 = cut[c + 1];
     if (d1 == d0) continue;
     const uint32_t u0 = du[d0], u1 = du[d1];
-    if (!zin) {
-      HIPCHK(hipStreamWaitEvent(st, S->pev_h[c], 0));
-      HIPCHK(hipStreamWaitEvent(st, S->pev_h2[c], 0));
-    }
+    HIPCHK(hipStreamWaitEvent(st, S->pev_h[c], 0));
+    if (!zin) HIPCHK(hipStreamWaitEvent(st, S->pev_h2[c], 0));
     const uint32_t o0 = c == 0 ? 0 : u0 & ~15u;
     if (v2) k_widen<<<(u1 - o0 + 256) / 256, 256, 0, st>>>(dO + o0, S->in_off.as<uint64_t>() + o0, u1 - o0 + 1);
     GeneralJob jc = j;
@@ -1154,7 +1215,8 @@ void *ym_host_alloc(size_t bytes) {
   if (!g_pool_free[k].empty()) {
     p = g_pool_free[k].back();
     g_pool_free[k].pop_back();
-  } else if (hipHostMalloc(&p, 1ull << k, hipHostMallocPortable) != hipSuccess) {
+  } else if (hipHostMalloc(&p, 1ull << k, hipHostMallocPortable) != hipSuccess) {  // (coherent: kernels read it at
+                                                                                   // 50-56 GB/s, non-coherent 43)
     return nullptr;
   }
   g_pool_live.emplace_back(p, k);
