@@ -186,7 +186,11 @@ def secondary(dev, eng):
              # the sync server's SyncStep1 -> SyncStep2 load: diffUpdate / state vector of
              # the merged C2 documents (~1 KB each) against random state vectors
              ("diff_c2_v1", "diff", "c2_v1", 10000), ("sv_c2_v1", "sv", "c2_v1", 10000),
-             ("diff_c2_v2", "diff", "c2_v2", 10000), ("sv_c2_v2", "sv", "c2_v2", 10000)]
+             ("diff_c2_v2", "diff", "c2_v2", 10000), ("sv_c2_v2", "sv", "c2_v2", 10000),
+             # realistic text: C2U, the C2 shape with CJK / emoji / accented words and pastes
+             ("merge_c2u_v1", "merge", "c2u_v1", 10000), ("merge_c2u_v2", "merge", "c2u_v2", 10000),
+             ("diff_c2u_v1", "diff", "c2u_v1", 10000), ("sv_c2u_v1", "sv", "c2u_v1", 10000),
+             ("diff_c2u_v2", "diff", "c2u_v2", 10000), ("sv_c2u_v2", "sv", "c2u_v2", 10000)]
     for name, op, wl, n in cases:
         if only and name not in only.split(","):
             continue

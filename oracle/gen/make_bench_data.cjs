@@ -229,7 +229,71 @@ function genMapRich (seed, nClients, nTx, nKeys) {
   return { v1, v2 }
 }
 
+// C2U: the C2 shape (50 transactions, as C2R: documents of ~2 KB) with realistic text: ~30% of the short
+// inserts are CJK words, emoji (surrogate pairs) or accented Latin, 10% of the inserts are pastes of 20-200
+// characters of mixed text; 20% bold.  Inserts and deletes never fall inside a surrogate pair (an editor
+// moves by code points).
+function genTextUnicode (seed, nClients, nTx, syncP, ids) {
+  const r = rng(seed)
+  const v1 = []; const v2 = []
+  const docs = []
+  for (let c = 0; c < nClients; c++) {
+    const d = new Y.Doc(); d.clientID = ids[c]
+    d.on('update', (u, origin) => { if (origin !== 'remote') v1.push(u) })
+    d.on('updateV2', (u, origin) => { if (origin !== 'remote') v2.push(u) })
+    docs.push(d)
+  }
+  const cjk = n => { let w = ''; for (let i = 0; i < n; i++) w += String.fromCodePoint(0x4e00 + r.u32() % 0x51a0); return w }
+  const emoji = n => { let w = ''; for (let i = 0; i < n; i++) w += String.fromCodePoint(0x1f600 + r.u32() % 0x50); return w }
+  const accent = n => { const a = 'éèêëàâäôöûüçñß'; let w = ''; for (let i = 0; i < n; i++) w += r.real() < 0.4 ? a[r.u32() % a.length] : String.fromCharCode(97 + r.u32() % 26); return w }
+  const word = () => {
+    const p = r.real()
+    if (p < 0.7) return r.word(1, 5)
+    if (p < 0.82) return cjk(r.int(1, 4))
+    if (p < 0.91) return emoji(r.int(1, 3))
+    return accent(r.int(2, 7))
+  }
+  const paste = () => {
+    const n = r.int(20, 200); let s = ''
+    while ([...s].length < n) s += (s ? ' ' : '') + word()
+    return [...s].slice(0, n).join('')
+  }
+  // a UTF-16 position at a code point boundary of s (pos <= s.length)
+  const cpPos = (s, pos) => (pos > 0 && pos < s.length && s.charCodeAt(pos) >= 0xdc00 && s.charCodeAt(pos) <= 0xdfff) ? pos - 1 : pos
+  for (let t = 0; t < nTx; t++) {
+    const d = docs[r.u32() % docs.length]
+    const text = d.getText('text')
+    d.transact(() => {
+      const s = text.toString()
+      const len = s.length
+      if (len === 0 || r.real() < 0.6) {
+        const pos = cpPos(s, r.int(0, len)); const w = r.real() < 0.1 ? paste() : word()
+        if (r.real() < 0.2) text.insert(pos, w, { bold: true }); else text.insert(pos, w)
+      } else {
+        const pos = cpPos(s, r.int(0, len - 1))
+        const end = cpPos(s, Math.min(pos + r.int(1, 3), len))
+        if (end > pos) text.delete(pos, end - pos)
+      }
+    })
+    if (nClients > 1 && r.real() < syncP) {
+      const a = docs[r.u32() % docs.length]; const b = docs[r.u32() % docs.length]
+      if (a !== b) Y.applyUpdate(b, Y.encodeStateAsUpdate(a, Y.encodeStateVector(b)), 'remote')
+    }
+  }
+  return { v1, v2 }
+}
+
 fs.mkdirSync(OUT, { recursive: true })
+if (which.includes('c2u')) {
+  const T = Number(process.env.C2_TEMPLATES || 1024)
+  const d1 = []; const d2 = []
+  for (let doc = 0; doc < T; doc++) {
+    const { v1, v2 } = genTextUnicode(doc + 11001, 4, 50, 0.3, [1000, 8919, 16838, 24757])
+    d1.push(v1); d2.push(v2)
+  }
+  writeYmb(path.join(OUT, 'c2u_v1.ymb.gz'), d1)
+  writeYmb(path.join(OUT, 'c2u_v2.ymb.gz'), d2)
+}
 if (which.includes('c2r')) {
   const T = Number(process.env.C2_TEMPLATES || 1024)
   const d1 = []; const d2 = []

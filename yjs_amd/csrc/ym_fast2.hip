@@ -36,7 +36,7 @@ constexpr uint32_t L_RKEY = R;                     // u64 (~client << 32 | clock
 constexpr uint32_t L_RLEN = L_RKEY + 8 * REC;      // u32
 constexpr uint32_t L_RAUX = L_RLEN + 4 * REC;      // u32 info | pi << 8 | typeRef << 16
 constexpr uint32_t L_RF = L_RAUX + 4 * REC;        // u32[4]: origin (or parent id) client, clock; right origin client, clock
-constexpr uint32_t L_RS = L_RF + 16 * REC;         // u32[3]: strings (LDS offset | n << 16): ykey, parentSub, content/key/name
+constexpr uint32_t L_RS = L_RF + 16 * REC;         // u32[3]: strings (se_make): ykey, parentSub, content/key/name
 constexpr uint32_t L_RSP = L_RS + 12 * REC;        // u32 rest span (LDS offset | n << 16)
 constexpr uint32_t L_RSLOT = L_RSP + 4 * REC;      // u8
 constexpr uint32_t L_RCEND = L_RSLOT + REC;
@@ -57,7 +57,7 @@ constexpr uint32_t V_CL = R;                       // u32[3 * REC]
 constexpr uint32_t V_LC = V_CL + 12 * REC;         // u32[REC]
 constexpr uint32_t V_RC = V_LC + 4 * REC;          // u32[REC]
 constexpr uint32_t V_LN = V_RC + 4 * REC;          // u32[REC]
-constexpr uint32_t V_ST = V_LN + 4 * REC;          // u32[3 * REC] (offset | n << 16)
+constexpr uint32_t V_ST = V_LN + 4 * REC;          // u32[3 * REC] (se_make)
 constexpr uint32_t V_TR = V_ST + 12 * REC;         // u8[REC]
 constexpr uint32_t V_IN = V_TR + REC;              // u8[2 * REC]
 constexpr uint32_t V_PI = V_IN + 2 * REC;          // u8[REC]
@@ -68,6 +68,13 @@ constexpr uint32_t L_QCLK = R, L_QEND = L_QCLK + 4 * DSN, L_QGRP = L_QEND + 4 * 
 constexpr uint32_t L_GFIRST = L_QPRE + 272, L_GCLI = L_GFIRST + 272, L_GB2 = L_GCLI + 4 * DSN, L_GBYR = L_GB2 + 4 * DSN;
 constexpr uint32_t L_GMIN = L_PFIRST;
 static_assert(L_GBYR + 2 * DSN <= L_RCEND, "delete-set arrays fit the record region");
+
+// a string of the document's string columns: its LDS offset (12 bits), UTF-8 bytes and UTF-16 units (10 bits each)
+static_assert(IN + 16 <= 4096, "string offsets fit 12 bits");
+__device__ __forceinline__ uint32_t se_make(uint32_t off, uint32_t bytes, uint32_t units) { return off | (bytes << 12) | (units << 22); }
+__device__ __forceinline__ uint32_t se_off(uint32_t e) { return e & 0xfffu; }
+__device__ __forceinline__ uint32_t se_bytes(uint32_t e) { return (e >> 12) & 0x3ffu; }
+__device__ __forceinline__ uint32_t se_units(uint32_t e) { return e >> 22; }
 
 // ---- per-lane lib0 decoders over LDS (canonical inputs only; anything else declines) -------------
 // readVarInt: sign (incl. -0) + u32 magnitude, at most 5 bytes
@@ -126,7 +133,7 @@ __device__ __forceinline__ uint32_t rd_idif(IdifD &r) {
 __device__ __forceinline__ void decline(const GeneralJob &j, uint32_t d) {
   j.status[d] = ST_PENDING;
   const uint32_t q = atomicAdd(j.pend_count, 1u);
-  if (j.pend_list) j.pend_list[q] = d;  // (ym_merge_async: declines are only counted)
+  if (j.pend_list) j.pend_list[q] = d + j.doc_base;  // (ym_merge_async: declines are only counted)
 }
 
 // Walks one V2 update (lane-private decoders) and appends struct records and delete ranges.  NESTED:
@@ -145,14 +152,23 @@ __device__ __forceinline__ bool walk_v2(uint32_t u) {
     h.p += n;
   }
   if (h.bad) return false;
-  // StringDecoder: varString(body) then the UintOptRle of UTF-16 lengths; ASCII bodies only
+  // StringDecoder: varString(body) then the UintOptRle of UTF-16 lengths.  The body must be valid UTF-8 (the
+  // decoder's replacement characters would re-encode differently); each string is then sliced by its UTF-16
+  // length: bytes = units for an ASCII body, else a walk over the lead bytes (round 6; ASCII only before)
   const uint32_t sn = rvu(col[5]);
   if (col[5].bad || !room(col[5], sn)) return false;
   const uint32_t sb = col[5].p;
+  bool sascii;
+  uint32_t sunits = sn;
   {
     uint64_t hi = 0;
     for (uint32_t o = 0; o < sn; o += 8) hi |= mask_bytes(ld8(sb + o), sn - o);
-    if (hi & 0x8080808080808080ull) return false;
+    sascii = (hi & 0x8080808080808080ull) == 0;
+    if (!sascii) {
+      bool ub = false;
+      sunits = utf8_slow(sb, sb + sn, ub);
+      if (ub) return false;
+    }
   }
   col[5].p += sn;
   IdifD kc = {col[0], 0, 0, 0};
@@ -162,14 +178,17 @@ __device__ __forceinline__ bool walk_v2(uint32_t u) {
   UoptD sl = {col[5], 0, 0};
   RleD pi_ = {col[6], 0, 0};
   UoptD tr = {col[7], 0, 0}, ln = {col[8], 0, 0};
-  uint32_t spos = 0, keys = 0;
+  uint32_t spos = 0, supos = 0, keys = 0;
   Cur c = h;  // rest stream
   bool bad = false;
-  auto rstr = [&]() -> uint32_t {  // StringDecoder.read(): (LDS offset | n << 16)
+  auto rstr = [&]() -> uint32_t {  // StringDecoder.read(): LDS offset | bytes << 12 | UTF-16 units << 22 (SE_*)
     const uint32_t n = rd_uopt(sl);
-    bad |= spos + n > sn || n > 0xffff;
-    const uint32_t v = (sb + spos) | (n << 16);
-    spos += n;
+    uint32_t nb = n;
+    if (!sascii) nb = utf8_span(sb + spos, sb + sn, n, bad);
+    bad |= spos + nb > sn || supos + n > sunits || n > 1023 || nb > 1023;
+    const uint32_t v = se_make(sb + spos, nb, n);
+    spos += nb;
+    supos += n;
     return v;
   };
   const uint32_t nclients = rvu(c);
@@ -202,7 +221,7 @@ __device__ __forceinline__ bool walk_v2(uint32_t u) {
           sp = a | ((c.p - a) << 16);
           break;
         }
-        case 4: s2 = rstr(); len = s2 >> 16; break;                        // ContentString
+        case 4: s2 = rstr(); len = se_units(s2); break;                    // ContentString
         case 5: case 6: {                                                  // Embed / Format (+ key)
           if ((info & 31) == 6) s2 = rstr();
           const uint32_t a = c.p;
@@ -616,7 +635,7 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v2(GeneralJob j, uint32_
     auto g_in = [](uint32_t i) { return (uint32_t)at<uint8_t>(V_IN + i); };
     auto g_pi = [](uint32_t i) { return (uint32_t)at<uint8_t>(V_PI + i); };
     auto g_kc = [](uint32_t i) { return i; };
-    auto g_sl = [](uint32_t i) { return at<uint32_t>(V_ST + 4 * i) >> 16; };
+    auto g_sl = [](uint32_t i) { return se_units(at<uint32_t>(V_ST + 4 * i)); };
     // string body bytes and per-entry offsets
     uint32_t sbody, sboff[CPL];
     {
@@ -625,7 +644,7 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v2(GeneralJob j, uint32_
       for (uint32_t q = 0; q < CPL; q++) {
         const uint32_t i = lane * CPL + q;
         sboff[q] = t;
-        t += i < nst ? at<uint32_t>(V_ST + 4 * i) >> 16 : 0;
+        t += i < nst ? se_bytes(at<uint32_t>(V_ST + 4 * i)) : 0;
       }
       const uint32_t incl = wave_incl_add(t);
       sbody = lane_read(incl, 63);
@@ -704,7 +723,7 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v2(GeneralJob j, uint32_
       for (uint32_t q = 0; q < CPL; q++) {  // string bodies: copied from the update's string column
         const uint32_t i = lane * CPL + q;
         if (i >= nst) break;
-        const uint32_t e = at<uint32_t>(V_ST + 4 * i), a = e & 0xffff, n = e >> 16;
+        const uint32_t e = at<uint32_t>(V_ST + 4 * i), a = se_off(e), n = se_bytes(e);
         lds_copy(dst.b + sbase + sboff[q], a, n);
       }
       col_encode<K_UOPT>(g_sl, nst, true, dst, sbase + sbody, cbad);
@@ -975,10 +994,15 @@ __device__ __forceinline__ int meta_walk_v2(uint32_t p0, uint32_t p1, uint32_t t
   const uint32_t sn = rvu(col[5]);
   if (col[5].bad || !room(col[5], sn)) return -1;
   const uint32_t sb = col[5].p;
+  uint32_t sunits = sn;  // the body's UTF-16 units: only lengths matter here (strings are not sliced or copied)
   {
     uint64_t hi = 0;
     for (uint32_t o = 0; o < sn; o += 8) hi |= mask_bytes(ld8(sb + o), sn - o);
-    if (hi & 0x8080808080808080ull) return -1;  // (the StringDecoder decodes the body eagerly: non-ASCII -> general)
+    if (hi & 0x8080808080808080ull) {  // (valid UTF-8 only: the decoder's replacements would change lengths)
+      bool ub = false;
+      sunits = utf8_slow(sb, sb + sn, ub);
+      if (ub) return -1;
+    }
   }
   col[5].p += sn;
   IdifD kc = {col[0], 0, 0, 0};
@@ -991,9 +1015,9 @@ __device__ __forceinline__ int meta_walk_v2(uint32_t p0, uint32_t p1, uint32_t t
   uint32_t spos = 0, keys = 0;
   Cur c = h;  // rest stream
   bool bad = false;
-  auto rstr = [&]() -> uint32_t {  // StringDecoder.read(): its UTF-16 length (= bytes: ASCII)
+  auto rstr = [&]() -> uint32_t {  // StringDecoder.read(): its UTF-16 length (str.slice within the body's units)
     const uint32_t n = rd_uopt(sl);
-    bad |= spos + n > sn;
+    bad |= spos + n > sunits;
     spos += n;
     return n;
   };
@@ -1348,7 +1372,8 @@ __global__ void __launch_bounds__(64, OCC) k_diff_small_v2(GeneralJob j, uint8_t
   }
   // header: the nine column spans, the ASCII string body, the rest stream's client count
   Cur col[9], c = {0, 0, false};
-  uint32_t sn = 0, sb = 0, nclients = 0, need = 0;
+  uint32_t sn = 0, sb = 0, sunits = 0, nclients = 0, need = 0;
+  bool sascii = true;
   uint32_t in_sz[NS];
   if (ok) {
     Cur h = {p0, p1, false};
@@ -1367,7 +1392,14 @@ __global__ void __launch_bounds__(64, OCC) k_diff_small_v2(GeneralJob j, uint8_t
     if (ok) {
       uint64_t hi = 0;
       for (uint32_t o = 0; o < sn; o += 8) hi |= mask_bytes(ld8(sb + o), sn - o);
-      ok &= (hi & 0x8080808080808080ull) == 0;
+      sascii = (hi & 0x8080808080808080ull) == 0;
+      if (!sascii) {  // valid UTF-8 only (round 6; ASCII only before): strings are sliced by UTF-16 units
+        bool ub = false;
+        sunits = utf8_slow(sb, sb + sn, ub);
+        ok &= !ub;
+      } else {
+        sunits = sn;
+      }
       col[5].p += sn;
     }
     c = h;  // rest stream
@@ -1411,17 +1443,21 @@ __global__ void __launch_bounds__(64, OCC) k_diff_small_v2(GeneralJob j, uint8_t
   UE e_cl = {0, 0}, e_sl = {0, 0}, e_tr = {0, 0}, e_ln = {0, 0};
   IE e_kc = {0, 0, 0}, e_lc = {0, 0, 0}, e_rc = {0, 0, 0};
   RE e_in = {0, 0}, e_pi = {0, 0};
-  uint32_t spos = 0, keys = 0, kclock = 0, nparts = 0, prev_client = 0;
-  bool bad = !ok;
-  auto rstr = [&](uint32_t &a, uint32_t &n) {  // StringDecoder.read(): an ASCII byte slice of the body
-    n = pd_uopt(sl);
-    bad |= spos + n > sn;
+  uint32_t spos = 0, supos = 0, keys = 0, kclock = 0, nparts = 0, prev_client = 0;
+  bool bad = !ok, uri = false;
+  // a string: its body offset a and n = bytes | UTF-16 units << 16
+  auto rstr = [&](uint32_t &a, uint32_t &n) {  // StringDecoder.read(): str.slice(spos, spos + units)
+    const uint32_t u = pd_uopt(sl);
+    const uint32_t nb = sascii ? u : utf8_span(sb + spos, sb + sn, u, bad);
+    bad |= spos + nb > sn || supos + u > sunits || u > 0xffff;
     a = sb + spos;
-    spos += n;
+    n = nb | (u << 16);
+    spos += nb;
+    supos += u;
   };
   auto wstr = [&](uint32_t a, uint32_t n) {  // StringEncoder.write
-    ospan(os[S_SB], a, n);
-    ue_w(os[S_SL], e_sl, n);
+    ospan(os[S_SB], a, n & 0xffff);
+    ue_w(os[S_SL], e_sl, n >> 16);
   };
   auto wkey = [&]() {  // writeKey: keyClock++ (never cached, E9)
     ie_w(os[S_KC], e_kc, kclock, bad);
@@ -1464,7 +1500,7 @@ __global__ void __launch_bounds__(64, OCC) k_diff_small_v2(GeneralJob j, uint8_t
           r1 = c.p;
           break;
         }
-        case 4: rstr(ca, cn); len = cn; break;  // ContentString
+        case 4: rstr(ca, cn); len = cn >> 16; break;  // ContentString
         case 5: case 6:                         // Embed / Format: rest any (Format reads its key as a string)
           if ((info & 31) == 6) rstr(ka, kn);
           r0 = c.p;
@@ -1520,7 +1556,14 @@ __global__ void __launch_bounds__(64, OCC) k_diff_small_v2(GeneralJob j, uint8_t
         switch (ref) {
           case 1: ue_w(os[S_LN], e_ln, len - off); break;
           case 3: case 5: ospan(os[S_RE], r0, r1 - r0); break;
-          case 4: wstr(ca + off, cn - off); break;
+          case 4: {  // str.slice(off): a cut inside a surrogate pair leaves a lone low surrogate, which the
+                     // column's writeVarString rejects (URIError, toUint8Array: after everything is read)
+            bool split = false;
+            const uint32_t ob = sascii ? off : utf8_span(ca, ca + (cn & 0xffff), off, split);
+            uri |= split;
+            if (!split) wstr(ca + ob, ((cn & 0xffff) - ob) | (((cn >> 16) - off) << 16));
+            break;
+          }
           case 6: wkey(); wstr(ka, kn); ospan(os[S_RE], r0, r1 - r0); break;
           case 7:
             ue_w(os[S_TR], e_tr, t);
@@ -1626,6 +1669,9 @@ __global__ void __launch_bounds__(64, OCC) k_diff_small_v2(GeneralJob j, uint8_t
     if (!bad) lds_copy(p, ds0, ds1 - ds0);
     if (bad && !why) why = 9;
   }
+  // a valid document whose result is yjs's URIError (a string cut inside a surrogate pair): no output
+  const bool uerr = !bad && uri;
+  if (uerr) bad = true;
   // sizes: one bump allocation per wave; every output starts 16-byte aligned (the cooperative copy's stores)
   const uint32_t total16 = bad ? 0 : (total + 15) & ~15u;
   const uint32_t oincl = wave_incl_add(total16), otot = lane_read(oincl, 63);
@@ -1636,6 +1682,12 @@ __global__ void __launch_bounds__(64, OCC) k_diff_small_v2(GeneralJob j, uint8_t
   const uint64_t off = base + oincl - total16;
   const bool fits = off + total16 <= j.cap;
   if (bad && lane < dn && why) done[d] = (uint8_t)why;
+  if (uerr) {
+    done[d] = 1;
+    j.status[d] = ym::ST_URI;
+    j.out_len[d] = 0;
+    j.out_off[d] = 0;
+  }
   if (!bad) {
     done[d] = 1;
     if (fits) {

@@ -229,6 +229,23 @@ __device__ __forceinline__ uint32_t utf8_slow(uint32_t i, uint32_t e, bool &bad)
   return u;
 }
 __device__ __forceinline__ uint64_t mask_bytes(uint64_t x, uint32_t n) { return n >= 8 ? x : x & ((1ull << (8 * n)) - 1); }
+// The bytes of the next n UTF-16 units of valid UTF-8 at LDS [p, e) (a StringDecoder slice of a V2 string
+// column body, validated by utf8_slow beforehand); `bad` when the slice ends inside a surrogate pair (a 4-byte
+// character split between two strings: the halves re-encode by context, the fast paths decline it) or runs
+// past e.  ASCII runs go 8 bytes per step.
+__device__ __forceinline__ uint32_t utf8_span(uint32_t p, uint32_t e, uint32_t n, bool &bad) {
+  uint32_t q = p, u = 0;
+  while (u < n && q < e) {
+    if (n - u >= 8 && e - q >= 8 && (ld8(q) & 0x8080808080808080ull) == 0) { q += 8; u += 8; continue; }
+    const uint32_t b = sm[q];
+    const uint32_t len = b < 0x80 ? 1 : b < 0xE0 ? 2 : b < 0xF0 ? 3 : 4, cu = len == 4 ? 2 : 1;
+    if (u + cu > n) { bad = true; return 0; }
+    u += cu;
+    q += len;
+  }
+  if (u < n || q > e) bad = true;
+  return q - p;
+}
 __device__ __forceinline__ uint32_t utf16_len(Cur &c, uint32_t n) {
   if (!room(c, n)) { c.bad = true; return 0; }
   uint64_t hi = 0;

@@ -308,10 +308,14 @@ __device__ __forceinline__ uint32_t put_vu_g(uint8_t *o, uint32_t p, uint32_t v)
 }
 
 // Item.write / GC.write with offset `off` (> 0) of the struct at document position s0 (ending at s1):
-// the re-encoded head goes to `pre` (lane 0), the content tail to span [a0, a1).  False: decline (the
-// content kind cannot be sliced here, a split surrogate pair, a head longer than PRE).
-__device__ bool slice_head(sc::cu32 *B, uint32_t adj, uint32_t s0, uint32_t s1, uint32_t client, uint64_t clock,
-                           uint32_t len, uint32_t off, uint8_t *pre, uint32_t &prelen, uint32_t &a0, uint32_t &a1) {
+// the re-encoded head goes to `pre` (lane 0), the content tail to span [a0, a1).  Returns SH_OK; SH_DECLINE
+// (the content kind cannot be sliced here, a head longer than PRE); SH_URI when `off` splits a surrogate pair
+// of a ContentString: ContentString.write(encoder, off) writes str.slice(off), which starts with a lone low
+// surrogate, and V1 writeVarString (encodeURIComponent) throws URIError there -- yjs's diffUpdate throws it
+// as it writes that struct, before reading anything after it (the lazy reader).
+enum : uint32_t { SH_DECLINE = 0, SH_OK = 1, SH_URI = 2 };
+__device__ uint32_t slice_head(sc::cu32 *B, uint32_t adj, uint32_t s0, uint32_t s1, uint32_t client, uint64_t clock,
+                               uint32_t len, uint32_t off, uint8_t *pre, uint32_t &prelen, uint32_t &a0, uint32_t &a1) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t info = sc::byte(B, s0 + adj);
   const bool gc = (info & 31) == 0;
@@ -324,7 +328,7 @@ __device__ bool slice_head(sc::cu32 *B, uint32_t adj, uint32_t s0, uint32_t s1, 
     put(len - off);
   } else {
     const uint32_t ref = info & 31;
-    if (ref != 1 && ref != 4 && ref != 8) return false;
+    if (ref != 1 && ref != 4 && ref != 8) return SH_DECLINE;
     SCur e = sc::make(B, s0 + adj + 1, s1 + adj);
     const uint32_t ni = ref | 0x80 | (info & 0x40) | ((info & 0xC0) == 0 ? (info & 0x20) : 0);
     if (info & 0x80) { sc::skvu(e); sc::skvu(e); }
@@ -339,7 +343,7 @@ __device__ bool slice_head(sc::cu32 *B, uint32_t adj, uint32_t s0, uint32_t s1, 
     h[q++] = (uint8_t)ni;
     put(client);
     put((uint32_t)(clock + off - 1));
-    if (ro1 - ro0 > 10) return false;
+    if (ro1 - ro0 > 10) return SH_DECLINE;
     for (uint32_t b = ro0; b < ro1; b++) h[q++] = (uint8_t)sc::byte(B, b);
     if (ref == 1) {
       sc::rvu(e);
@@ -359,18 +363,20 @@ __device__ bool slice_head(sc::cu32 *B, uint32_t adj, uint32_t s0, uint32_t s1, 
         u += l == 4 ? 2 : 1;
         bi += l;
       }
-      if (u != off) return false;
+      if (e.bad || n > e.e - e.p) return SH_DECLINE;
+      if (u == off + 1) return SH_URI;  // a 4-byte character split (the struct's bytes were validated)
+      if (u != off) return SH_DECLINE;
       put(n - bi);
       a0 = e.p - adj + bi;
       a1 = e.p - adj + n;
     }
-    if (e.bad) return false;
+    if (e.bad) return SH_DECLINE;
   }
-  if (q > PRE) return false;
+  if (q > PRE) return SH_DECLINE;
   if (lane == 0)
     for (uint32_t b = 0; b < q; b++) pre[b] = h[b];
   prelen = q;
-  return true;
+  return SH_OK;
 }
 
 // a declined document keeps done[d] != 1 (k_big_v1 takes it); the value says why (ym__pw_reasons)
@@ -381,6 +387,20 @@ __device__ bool slice_head(sc::cu32 *B, uint32_t adj, uint32_t s0, uint32_t s1, 
     continue;                            \
   }
 #define PW_DECLINE() PW_DECLINE_R(why ? why : 2)
+// the document's result is yjs's URIError (slice_head SH_URI): completed here with that status
+constexpr uint32_t WHY_URI = 99;
+#define PW_URIERR()                                                                  \
+  {                                                                                  \
+    if (lane == 0) {                                                                 \
+      j.status[d] = ym::ST_URI;                                                      \
+      j.out_len[d] = 0;                                                              \
+      j.out_off[d] = 0;                                                              \
+      done[d] = 1;                                                                   \
+      atomicAdd((unsigned long long *)j.pw_count, 1ull);                             \
+    }                                                                                \
+    __syncthreads();                                                                 \
+    continue;                                                                        \
+  }
 
 // OP = OP_DIFF, OP_SV or OP_META (parseUpdateMeta: from = a section's first clock, to = its end clock)
 // DSL: the delete set validated through LDS token tables (ym_wave_ds.h) first -- batches with many-client
@@ -633,9 +653,10 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
                 b0 = fpos;
                 first = f;
               } else {
-                if (!slice_head(B, adj, fpos, fend, client, fclk, flen, off, X.pre + ci * PRE, prelen, a0, a1)) {
+                const uint32_t sh = slice_head(B, adj, fpos, fend, client, fclk, flen, off, X.pre + ci * PRE, prelen, a0, a1);
+                if (sh != SH_OK) {
                   declined = true;
-                  why = 11;
+                  why = sh == SH_URI ? WHY_URI : 11;
                   break;
                 }
                 b0 = fend;
@@ -693,6 +714,7 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
         nparts += copying;
       }
     }
+    if (declined && why == WHY_URI) PW_URIERR()
     if (declined) PW_DECLINE()
     __syncthreads();
     if (OP == OP_META) {  // from then to, each vu(n) | (client, clock)*
@@ -1365,6 +1387,7 @@ __device__ __forceinline__ uint32_t sw_vu(const uint8_t *b, uint32_t &o, uint32_
     __syncthreads();                                       \
     continue;                                              \
   }
+#define SW_URIERR() PW_URIERR()  // (the same completion: URIError status, done, counted)
 // documents of (SWMIN, SWB] bytes.  tally[0]: documents this kernel's launches of the call declined so far
 // (completions: j.pw_count, with the chunk walk's).  Rich content (nested `any` values, JSON objects / numbers: C2R / C4R) is declined to
 // k_big_v1 after the table pass and part of the walk; once a batch has shown mostly such documents (more than
@@ -1514,7 +1537,8 @@ __global__ void __launch_bounds__(64) k_pw_small(GeneralJob j, uint8_t *done, ui
               } else {
                 if (npre >= SW_NPRE) { why = 12; break; }
                 slot = npre++;
-                if (RF(slice_head(B, adj, p, nx, client, clock, cl, off, L.pre[slot], prelen, a0, a1) ? 1u : 0u) == 0) { why = 11; break; }
+                const uint32_t sh = RF(slice_head(B, adj, p, nx, client, clock, cl, off, L.pre[slot], prelen, a0, a1));
+                if (sh != SH_OK) { why = sh == SH_URI ? WHY_URI : 11; break; }
                 prelen = RF(prelen); a0 = RF(a0); a1 = RF(a1);
                 b0 = nx;
               }
@@ -1558,6 +1582,7 @@ __global__ void __launch_bounds__(64) k_pw_small(GeneralJob j, uint8_t *done, ui
         }
       }
     }
+    if (why == WHY_URI) SW_URIERR()
     if (why) SW_DECLINE_R(why ? why : 2)
     const uint32_t ds0 = p;
     uint32_t ds1 = 0;
