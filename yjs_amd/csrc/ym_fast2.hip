@@ -1321,12 +1321,13 @@ __device__ __forceinline__ uint32_t pd_idif(PIdif &r) {  // rd_idif
 }  // namespace df2
 
 template <uint32_t ND, uint32_t WIN, uint32_t POOL, int OCC>
-__global__ void __launch_bounds__(64, OCC) k_diff_small_v2(GeneralJob j, uint8_t *done, uint64_t pv_min) {
+__global__ void __launch_bounds__(64, OCC) k_diff_small_v2(GeneralJob j, uint8_t *done, uint64_t pv_min, uint32_t retry) {
   using namespace df2;
   using L = Df2Lay<ND, WIN, POOL>;
   const uint32_t lane = threadIdx.x;
   const uint32_t d0 = blockIdx.x * ND, d = d0 + lane;
   if (d0 >= j.n) return;
+  if (retry && ND == 1 && done[d0] != 2 && done[d0] != 5) return;  // (retry launches: most blocks have nothing to do)
   const uint32_t dn = j.n - d0 < ND ? j.n - d0 : ND;
   // the windows: the ND updates and their state vectors (each contiguous in a packed batch)
   const uint64_t w0 = j.upd_off[j.doc_upd[d0]] & ~15ull, wend = j.upd_off[j.doc_upd[d0 + dn]];
@@ -1340,11 +1341,14 @@ __global__ void __launch_bounds__(64, OCC) k_diff_small_v2(GeneralJob j, uint8_t
     for (uint32_t v = lane; v < vbytes / 16; v += 64) at<uint4>(L::SV + 16 * v) = svs[v];
   }
   __syncthreads();
-  bool ok = false;
+  bool ok = false, sel = false;
   uint32_t p0 = 0, p1 = 0, s0 = 0, s1 = 0;
   if (lane < dn) {
     const uint32_t u0 = j.doc_upd[d];
-    if (j.doc_upd[d + 1] - u0 == 1 && !done[d]) {
+    // retry: only the documents a previous launch left outside its windows or its shared output pool (done 2
+    // or 5; one document per wave)
+    sel = retry ? done[d] == 2 || done[d] == 5 : !done[d];
+    if (j.doc_upd[d + 1] - u0 == 1 && sel) {
       const uint64_t a = j.upd_off[u0], b = j.upd_off[u0 + 1], sa = j.sv_off[d], sb = j.sv_off[d + 1];
       ok = a >= w0 && b <= w0 + wbytes && b > a && b - a < pv_min && sa >= v0 && sb <= v0 + vbytes && sb >= sa;
       p0 = (uint32_t)(a - w0); p1 = (uint32_t)(b - w0);
@@ -1353,7 +1357,7 @@ __global__ void __launch_bounds__(64, OCC) k_diff_small_v2(GeneralJob j, uint8_t
   }
   // decline reasons (done[d], read by ym__pv2_done): 2 not in the windows / several updates, 3 state vector,
   // 4 header, 5 output pool, 6 walk, 7 delete set, 8 stream overflow, 9 in-place assembly
-  uint32_t why = ok ? 0 : 2;
+  uint32_t why = ok || !sel ? 0 : 2;  // (a document this launch does not select keeps its done value)
   const uint32_t svt = L::SVT + 8 * L::NSV * (lane < ND ? lane : 0);
   const uint32_t pt = L::PT + 16 * L::NPART * (lane < ND ? lane : 0);
   // decodeStateVector into the lane's table (a later entry for a client wins: the lookup scans backwards)
@@ -1740,9 +1744,12 @@ int small_v2_launch(uint32_t op, const GeneralJob &j, uint8_t *done, hipStream_t
     if (j.n <= diff_min) return 0;
     const uint32_t nd = j.n <= 2048 ? 1 : j.n <= 4096 ? 2 : j.n <= 6144 ? 3 : j.n <= 8192 ? 4 : 5;
 #define DF2(N) \
-  if (nd == N) k_diff_small_v2<N, 7680, 7680, 1><<<(j.n + N - 1) / N, 64, Df2Lay<N, 7680, 7680>::BYTES, st>>>(j, done, pv_min);
+  if (nd == N) k_diff_small_v2<N, 7680, 7680, 1><<<(j.n + N - 1) / N, 64, Df2Lay<N, 7680, 7680>::BYTES, st>>>(j, done, pv_min, 0);
     DF2(1) DF2(2) DF2(3) DF2(4) DF2(5)
 #undef DF2
+    // documents larger than their share of a shared window or output pool (done 2 / 5: e.g. merged C2U documents,
+    // five to a 7.5 KB window) once more one per wave before k_big_v2, whose walker takes ASCII string columns only
+    if (nd > 1) k_diff_small_v2<1, 7680, 7680, 1><<<j.n, 64, Df2Lay<1, 7680, 7680>::BYTES, st>>>(j, done, pv_min, 1);
   } else {
     return 0;
   }

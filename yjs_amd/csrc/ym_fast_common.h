@@ -209,6 +209,7 @@ __device__ __forceinline__ bool room(const Cur &c, uint32_t n) { return c.p <= c
 __device__ __forceinline__ uint32_t utf8_slow(uint32_t i, uint32_t e, bool &bad) {
   uint32_t u = 0;
   while (i < e) {
+    if (e - i >= 8 && (ld8(i) & 0x8080808080808080ull) == 0) { u += 8; i += 8; continue; }  // an ASCII run
     const uint32_t b = sm[i];
     if (b < 0x80) { u++; i++; continue; }
     uint32_t len, cp, mn;

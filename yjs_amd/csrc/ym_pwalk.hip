@@ -1147,7 +1147,8 @@ __global__ void __launch_bounds__(MS_T) k_pw_ms(GeneralJob j, uint8_t *done, con
                   patch = true;
                 } else {
                   // (every lane computes the head; the lanes store the same bytes)
-                  if (RF(slice_head(B, adj, p, nx, client, clock, cl, off, M.pre + (uint64_t)ci * PRE, prelen, a0, a1) ? 1u : 0u) == 0) { why = 11; break; }
+                  // (a split surrogate pair, SH_URI, declines here: the streamed walker / general path report it)
+                  if (RF(slice_head(B, adj, p, nx, client, clock, cl, off, M.pre + (uint64_t)ci * PRE, prelen, a0, a1)) != SH_OK) { why = 11; break; }
                   prelen = RF(prelen); a0 = RF(a0); a1 = RF(a1);
                   b0 = nx;
                 }
