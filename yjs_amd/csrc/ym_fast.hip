@@ -723,6 +723,55 @@ __device__ __forceinline__ int ds_phase(const GeneralJob &j, uint32_t d, uint32_
     return DS_DONE;
 }
 
+// ---- 1. stage: every load of document d in flight at once (round 6: the loops issued one 16-byte load per
+// lane, waited for it, stored it, then issued the next): its update offsets (<= 129: three per lane) with the
+// offsets of its first and last byte, then its 16-byte vectors covering [b0, b0 + bytes) (byte b0 lands at LDS
+// offset b0 & 15), then the LDS stores.  False: the document is outside this kernel's shape (declined).
+template <class M, bool DSONLY, class T>
+__device__ __forceinline__ bool stage_doc(const GeneralJob &j, const T *off, uint32_t u0, uint32_t k, uint64_t &b0,
+                                          uint64_t &bytes) {
+  const uint32_t lane = threadIdx.x;
+  constexpr uint32_t NO = (UPD + 1 + 63) / 64, NV = (M::IN + 31) / 16 / 64 + 1;
+  // (the loads are unconditional, at clamped indices: exec-masked loads made the compiler wait for each one)
+  const uint32_t kc = k <= UPD ? k : 0;
+  uint64_t ov[NO];
+#pragma unroll
+  for (uint32_t t = 0; t < NO; t++) ov[t] = off[u0 + (lane + 64 * t < kc ? lane + 64 * t : kc)];
+#ifdef YM_STAGE_SCALAR_B0
+  b0 = off[u0];
+  bytes = (uint64_t)off[u0 + k] - b0;
+#else
+  // the document's first and last offsets from those loads (lane 0 / the lane holding index kc): one memory
+  // round trip for all of them instead of a scalar one first
+  {
+    uint64_t ve = ov[0];
+#pragma unroll
+    for (uint32_t t = 1; t < NO; t++) ve = (kc >> 6) == t ? ov[t] : ve;
+    b0 = lane_read64(ov[0], 0);
+    bytes = lane_read64(ve, (int)(kc & 63)) - b0;
+  }
+#endif
+  if ((DSONLY ? k == 0 : k <= 1) || k > UPD || bytes > M::IN) return false;
+  const uint32_t base = (uint32_t)(b0 & 15);
+  const uint4 *src = reinterpret_cast<const uint4 *>(j.A + (b0 - base));
+  const uint32_t nvec = (uint32_t)((base + bytes + 15) >> 4);
+  // (stores at the same clamped indices, unconditionally: a lane past the end writes the last vector / offset
+  // again, the same bytes; a conditional store let the compiler sink each load into its branch and wait there)
+  uint32_t vi[NV];
+  uint4 vv[NV];
+#pragma unroll
+  for (uint32_t t = 0; t < NV; t++) {
+    vi[t] = lane + 64 * t < nvec ? lane + 64 * t : nvec - 1;
+    vv[t] = src[vi[t]];
+  }
+#pragma unroll
+  for (uint32_t t = 0; t < NV; t++) at<uint4>(M::L_IN + 16 * vi[t]) = vv[t];
+#pragma unroll
+  for (uint32_t t = 0; t < NO; t++)
+    at<uint16_t>(M::L_UOFF + 2 * (lane + 64 * t < kc ? lane + 64 * t : kc)) = (uint16_t)(ov[t] - b0 + base);
+  return true;
+}
+
 // DSONLY: PermanentUserData's delete-set merge (ym_ds_merge): every input is an encoded delete set (no
 // struct section); the walk is W2 only and the output is the merged delete set alone, in the DSEncoderV1
 // format, or DSEncoderV2's (DSV2: clocks delta-coded within a client, lengths minus one).
@@ -735,19 +784,14 @@ __device__ __forceinline__ void merge_doc_v1(const GeneralJob &j, uint32_t di) {
   {
     const uint32_t d = NESTED && j.list ? j.list[di] : di;  // (NESTED without a list: every document)
     const uint32_t u0 = j.doc_upd[d], k = j.doc_upd[d + 1] - u0;
-    const uint64_t b0 = uoff_g(j, u0), bytes = uoff_g(j, u0 + k) - b0;
-    if ((DSONLY ? k == 0 : k <= 1) || k > UPD || bytes > M::IN) {
+    // ---- 1. stage (stage_doc): the offsets' width is a wave-uniform branch here, not one per load
+    uint64_t b0 = 0, bytes = 0;
+    const bool staged = j.upd_off32 ? stage_doc<M, DSONLY>(j, j.upd_off32, u0, k, b0, bytes)
+                                    : stage_doc<M, DSONLY>(j, j.upd_off, u0, k, b0, bytes);
+    if (!staged) {
       if (lane == 0) decline(j, d);
       return;
     }
-    // ---- 1. stage with 16-B loads covering [b0, b0 + bytes); byte b0 lands at LDS offset `base`
-    const uint32_t base = (uint32_t)(b0 & 15);
-    {
-      const uint4 *src = reinterpret_cast<const uint4 *>(j.A + (b0 - base));
-      const uint32_t nvec = (uint32_t)((base + bytes + 15) >> 4);
-      for (uint32_t v = lane; v < nvec; v += 64) at<uint4>(M::L_IN + 16 * v) = src[v];
-    }
-    for (uint32_t i = lane; i <= k; i += 64) at<uint16_t>(M::L_UOFF + 2 * i) = (uint16_t)(uoff_g(j, u0 + i) - b0 + base);
     if (lane < 8) at<uint32_t>(M::L_MISC + 4 * lane) = 0;  // counters, duplicate-check bitmap
     if (lane < 16) at<uint32_t>(M::L_HIST + 4 * lane) = 0;
     __syncthreads();
