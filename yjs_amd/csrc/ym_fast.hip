@@ -729,8 +729,9 @@ __device__ __forceinline__ int ds_phase(const GeneralJob &j, uint32_t d, uint32_
 // offset b0 & 15), then the LDS stores.  False: the document is outside this kernel's shape (declined).
 template <class M, bool DSONLY, class T>
 __device__ __forceinline__ bool stage_doc(const GeneralJob &j, const T *off, uint32_t u0, uint32_t k, uint64_t &b0,
-                                          uint64_t &bytes) {
+                                          uint64_t &bytes, uint64_t &arena0) {
   const uint32_t lane = threadIdx.x;
+  arena0 = off[0];  // (the slot's origin, needed after the walk: loaded with the rest, not in the middle of the wave)
   constexpr uint32_t NO = (UPD + 1 + 63) / 64, NV = (M::IN + 31) / 16 / 64 + 1;
   // (the loads are unconditional, at clamped indices: exec-masked loads made the compiler wait for each one)
   const uint32_t kc = k <= UPD ? k : 0;
@@ -785,9 +786,9 @@ __device__ __forceinline__ void merge_doc_v1(const GeneralJob &j, uint32_t di) {
     const uint32_t d = NESTED && j.list ? j.list[di] : di;  // (NESTED without a list: every document)
     const uint32_t u0 = j.doc_upd[d], k = j.doc_upd[d + 1] - u0;
     // ---- 1. stage (stage_doc): the offsets' width is a wave-uniform branch here, not one per load
-    uint64_t b0 = 0, bytes = 0;
-    const bool staged = j.upd_off32 ? stage_doc<M, DSONLY>(j, j.upd_off32, u0, k, b0, bytes)
-                                    : stage_doc<M, DSONLY>(j, j.upd_off, u0, k, b0, bytes);
+    uint64_t b0 = 0, bytes = 0, arena0 = 0;
+    const bool staged = j.upd_off32 ? stage_doc<M, DSONLY>(j, j.upd_off32, u0, k, b0, bytes, arena0)
+                                    : stage_doc<M, DSONLY>(j, j.upd_off, u0, k, b0, bytes, arena0);
     if (!staged) {
       if (lane == 0) decline(j, d);
       return;
@@ -873,7 +874,7 @@ __device__ __forceinline__ void merge_doc_v1(const GeneralJob &j, uint32_t di) {
     if (lane < 3 && nsec + lane < ((nsec + 3) & ~3u)) at<uint64_t>(M::L_SKEY + 8 * (nsec + lane)) = ~0ull;
     __syncthreads();
     // output slot: 64-aligned inside the bound 2 * in + 64 per doc (no global atomics)
-    const uint64_t slot = 2 * (b0 - uoff_g(j, 0)) + 64ull * (d + j.doc_base);
+    const uint64_t slot = 2 * (b0 - arena0) + 64ull * (d + j.doc_base);
     const uint64_t slot_al = (slot + 63) & ~63ull;
     const uint64_t slot_end = slot + 2 * bytes + 64 < j.cap ? slot + 2 * bytes + 64 : j.cap;
     if (slot_al >= slot_end) YM_DECLINE()
