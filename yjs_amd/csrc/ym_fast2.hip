@@ -447,12 +447,16 @@ __global__ void __launch_bounds__(64, OCC) k_fast_merge_v2(GeneralJob j, uint32_
     }
     // ---- 1. stage
     const uint32_t base = (uint32_t)(b0 & 15);
-    {
-      const uint4 *src = reinterpret_cast<const uint4 *>(j.A + (b0 - base));
-      const uint32_t nvec = (uint32_t)((base + bytes + 15) >> 4);
-      for (uint32_t v = lane; v < nvec; v += 64) at<uint4>(L_IN + 16 * v) = src[v];
+    {  // (offsets loaded before the vectors' stores: all of the stage's loads in flight together)
+      uint64_t ov[(UPD + 64) / 64];
+#pragma unroll
+      for (uint32_t t = 0; t < (UPD + 64) / 64; t++) ov[t] = j.upd_off[u0 + (lane + 64 * t < k ? lane + 64 * t : k)];
+      stage16<(IN + 31) / 16 / 64 + 1>(L_IN, reinterpret_cast<const uint4 *>(j.A + (b0 - base)),
+                                        (uint32_t)((base + bytes + 15) >> 4));
+#pragma unroll
+      for (uint32_t t = 0; t < (UPD + 64) / 64; t++)
+        at<uint16_t>(L_UOFF + 2 * (lane + 64 * t < k ? lane + 64 * t : k)) = (uint16_t)(ov[t] - b0 + base);
     }
-    for (uint32_t i = lane; i <= k; i += 64) at<uint16_t>(L_UOFF + 2 * i) = (uint16_t)(j.upd_off[u0 + i] - b0 + base);
     if (lane < 2) at<uint32_t>(L_MISC + 4 * lane) = 0;
     __syncthreads();
     YM2_STOP(1)
@@ -1097,10 +1101,7 @@ __global__ void __launch_bounds__(64) k_small_v2(GeneralJob j, uint8_t *done, ui
   const uint64_t w0 = j.upd_off[j.doc_upd[d0]] & ~15ull;
   const uint64_t wend = j.upd_off[j.doc_upd[d0 + dn]];
   const uint32_t wbytes = (uint32_t)((wend - w0 < WIN ? wend - w0 : WIN) + 15) & ~15u;
-  {
-    const uint4 *src = reinterpret_cast<const uint4 *>(j.A + w0);
-    for (uint32_t v = lane; v < wbytes / 16; v += 64) at<uint4>(16 * v) = src[v];
-  }
+  if (wbytes) stage16<(WIN + 15) / 16 / 64 + 1>(0, reinterpret_cast<const uint4 *>(j.A + w0), wbytes / 16);
   __syncthreads();
   int ns = -1;
   const uint32_t tab = L::TAB + 12 * NSEC * (lane < ND ? lane : 0);
@@ -1334,12 +1335,8 @@ __global__ void __launch_bounds__(64, OCC) k_diff_small_v2(GeneralJob j, uint8_t
   const uint32_t wbytes = (uint32_t)((wend - w0 < WIN ? wend - w0 : WIN) + 15) & ~15u;
   const uint64_t v0 = j.sv_off[d0] & ~15ull, vend = j.sv_off[d0 + dn];
   const uint32_t vbytes = (uint32_t)((vend - v0 < L::SVW ? vend - v0 : L::SVW) + 15) & ~15u;
-  {
-    const uint4 *src = reinterpret_cast<const uint4 *>(j.A + w0);
-    for (uint32_t v = lane; v < wbytes / 16; v += 64) at<uint4>(16 * v) = src[v];
-    const uint4 *svs = reinterpret_cast<const uint4 *>(j.sv + v0);
-    for (uint32_t v = lane; v < vbytes / 16; v += 64) at<uint4>(L::SV + 16 * v) = svs[v];
-  }
+  if (wbytes) stage16<(WIN + 15) / 16 / 64 + 1>(0, reinterpret_cast<const uint4 *>(j.A + w0), wbytes / 16);
+  if (vbytes) stage16<(L::SVW + 15) / 16 / 64 + 1>(L::SV, reinterpret_cast<const uint4 *>(j.sv + v0), vbytes / 16);
   __syncthreads();
   bool ok = false, sel = false;
   uint32_t p0 = 0, p1 = 0, s0 = 0, s1 = 0;

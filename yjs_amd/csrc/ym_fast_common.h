@@ -128,6 +128,28 @@ __device__ __forceinline__ void copy_out(uint8_t *g, uint32_t src, uint32_t n, u
   for (uint32_t i = 16 * n16 + lane; i < n; i += 64) g[i] = sm[src + i];
 }
 
+// Staging (one wave): nvec 16-byte vectors from global `src` to LDS byte offset `dst`, MAXV vectors per lane per
+// pass with every load of the pass in flight before its stores (round 6: a `for (v = lane; v < n; v += 64)` loop
+// waits for each load before the next -- one memory round trip per 1 KB, the head of every wave's latency).
+// Lanes past the end re-load and re-store the last vector (the same bytes): no branch the compiler could sink
+// the loads into.
+template <uint32_t MAXV>
+__device__ __forceinline__ void stage16(uint32_t dst, const uint4 *src, uint32_t nvec) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t v0 = 0; v0 < nvec; v0 += 64 * MAXV) {
+    uint32_t ix[MAXV];
+    uint4 x[MAXV];
+#pragma unroll
+    for (uint32_t t = 0; t < MAXV; t++) {
+      const uint32_t i = v0 + lane + 64 * t;
+      ix[t] = i < nvec ? i : nvec - 1;
+      x[t] = src[ix[t]];
+    }
+#pragma unroll
+    for (uint32_t t = 0; t < MAXV; t++) at<uint4>(dst + 16 * ix[t]) = x[t];
+  }
+}
+
 // ---- V1 walker over LDS bytes ---------------------------------------------------------------------
 // Any anomaly (truncation, non-canonical varint, invalid UTF-8, a payload kind this path does not
 // verify) sets `bad`; the general path then reproduces yjs's exact result or error.

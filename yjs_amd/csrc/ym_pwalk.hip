@@ -1415,9 +1415,20 @@ __global__ void __launch_bounds__(64) k_pw_small(GeneralJob j, uint8_t *done, ui
     sc::cu32 *const B = sc::base_of(D);
     const uint32_t adj = (uint32_t)(ub & 3);
     __syncthreads();
-    for (uint32_t q = 16 * lane; q < len + 48; q += 16 * 64) {
-      const uint4 v = wds::load16m(D, q, len);
-      __builtin_memcpy(L.b + q, &v, 16);
+    {  // the bytes (all loads in flight before the stores; the vector crossing the end re-loads the last 16
+       // bytes) and 48 bytes of 0x80 past them (no stop byte)
+      constexpr uint32_t NQ = (SWB + 1023) / 1024;
+      uint32_t qs[NQ];
+      uint4 xv[NQ];
+#pragma unroll
+      for (uint32_t t = 0; t < NQ; t++) {
+        const uint32_t q = 16 * lane + 1024 * t;
+        qs[t] = q + 16 <= len ? q : len - 16;
+        xv[t] = *reinterpret_cast<const wds::u4u *>(D + qs[t]);
+      }
+#pragma unroll
+      for (uint32_t t = 0; t < NQ; t++) __builtin_memcpy(L.b + qs[t], &xv[t], 16);
+      if (lane < 48) L.b[len + lane] = 0x80;
     }
     uint32_t why = 0;
     bool bad = false;

@@ -156,6 +156,15 @@ __global__ void __launch_bounds__(64) k_small_v1(GeneralJob j, uint8_t *done, ui
     if (len == 0 || len + 48 > SLOT || len >= pw_min) return;
     const uint4 *src = reinterpret_cast<const uint4 *>(j.A + (b0 & ~15ull));
     const uint32_t nvec = (uint32_t)(((b0 & 15) + len + 15) >> 4);
+    if (ND == 64) {  // a lane's own document: every load in flight before the first store
+      constexpr uint32_t MV = (SLOT - 48 + 30) / 16;
+      uint4 x[MV];
+#pragma unroll
+      for (uint32_t t = 0; t < MV; t++) x[t] = src[t < nvec ? t : nvec - 1];
+#pragma unroll
+      for (uint32_t t = 0; t < MV; t++) at<uint4>(l * SLOT + 16 * (t < nvec ? t : nvec - 1)) = x[t];
+      return;
+    }
     for (uint32_t v = v0; v < nvec; v += dv) at<uint4>(l * SLOT + 16 * v) = src[v];
   };
   if (ND == 64) stage(lane, 0, 1);
