@@ -7,6 +7,7 @@
 
 #include "ym_canon_chk.h"
 #include "ym_kernels.h"
+#include "ym_utf8.h"
 
 namespace ymk {
 namespace fastc {
@@ -227,29 +228,18 @@ __device__ __forceinline__ uint32_t rdb(Cur &c) {
   return sm[c.p++];
 }
 __device__ __forceinline__ bool room(const Cur &c, uint32_t n) { return c.p <= c.e && n <= c.e - c.p; }
-// strict UTF-8 (lib0: decodeURIComponent(escape(..))) over the next n bytes; returns the UTF-16 length
+// strict UTF-8 (lib0: decodeURIComponent(escape(..))) over LDS [i, e); returns the UTF-16 length (ym_utf8.h,
+// 4 bytes per step; reads up to 3 bytes past e)
+// Out of line: only non-ASCII strings get here, and inlined its registers cost the one-wave kernels occupancy.
+__device__ __attribute__((noinline)) uint32_t utf8_lds(uint32_t i, uint32_t e) {
+  bool bad = false;
+  const uint32_t u = utf8::units<uint32_t>([](uint32_t p) { return ld4(p); }, i, e, bad);
+  return bad ? 0xffffffffu : u;
+}
 __device__ __forceinline__ uint32_t utf8_slow(uint32_t i, uint32_t e, bool &bad) {
-  uint32_t u = 0;
-  while (i < e) {
-    if (e - i >= 8 && (ld8(i) & 0x8080808080808080ull) == 0) { u += 8; i += 8; continue; }  // an ASCII run
-    const uint32_t b = sm[i];
-    if (b < 0x80) { u++; i++; continue; }
-    uint32_t len, cp, mn;
-    if ((b & 0xE0) == 0xC0) { len = 2; cp = b & 0x1F; mn = 0x80; }
-    else if ((b & 0xF0) == 0xE0) { len = 3; cp = b & 0x0F; mn = 0x800; }
-    else if ((b & 0xF8) == 0xF0) { len = 4; cp = b & 0x07; mn = 0x10000; }
-    else { bad = true; return 0; }
-    if (i + len > e) { bad = true; return 0; }
-    for (uint32_t q = 1; q < len; q++) {
-      const uint32_t cb = sm[i + q];
-      if ((cb & 0xC0) != 0x80) { bad = true; return 0; }
-      cp = (cp << 6) | (cb & 0x3F);
-    }
-    if (cp < mn || cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF)) { bad = true; return 0; }
-    u += cp >= 0x10000 ? 2 : 1;
-    i += len;
-  }
-  return u;
+  const uint32_t u = utf8_lds(i, e);
+  bad |= u == 0xffffffffu;
+  return u == 0xffffffffu ? 0 : u;
 }
 __device__ __forceinline__ uint64_t mask_bytes(uint64_t x, uint32_t n) { return n >= 8 ? x : x & ((1ull << (8 * n)) - 1); }
 // The bytes of the next n UTF-16 units of valid UTF-8 at LDS [p, e) (a StringDecoder slice of a V2 string

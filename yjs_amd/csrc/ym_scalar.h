@@ -12,6 +12,7 @@
 #include <stdint.h>
 
 #include "ym_canon_chk.h"
+#include "ym_utf8.h"
 
 namespace ymk {
 namespace sc {
@@ -133,26 +134,7 @@ __device__ __forceinline__ uint32_t rdb(SCur &c) {
 }
 __device__ __forceinline__ bool room(const SCur &c, uint32_t n) { return c.p <= c.e && n <= c.e - c.p; }
 __device__ __forceinline__ uint32_t utf8_slow(cu32 *b, uint32_t i, uint32_t e, bool &bad) {
-  uint32_t u = 0;
-  while (i < e) {
-    const uint32_t x = byte(b, i);
-    if (x < 0x80) { u++; i++; continue; }
-    uint32_t len, cp, mn;
-    if ((x & 0xE0) == 0xC0) { len = 2; cp = x & 0x1F; mn = 0x80; }
-    else if ((x & 0xF0) == 0xE0) { len = 3; cp = x & 0x0F; mn = 0x800; }
-    else if ((x & 0xF8) == 0xF0) { len = 4; cp = x & 0x07; mn = 0x10000; }
-    else { bad = true; return 0; }
-    if (i + len > e) { bad = true; return 0; }
-    for (uint32_t q = 1; q < len; q++) {
-      const uint32_t cb = byte(b, i + q);
-      if ((cb & 0xC0) != 0x80) { bad = true; return 0; }
-      cp = (cp << 6) | (cb & 0x3F);
-    }
-    if (cp < mn || cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF)) { bad = true; return 0; }
-    u += cp >= 0x10000 ? 2 : 1;
-    i += len;
-  }
-  return u;
+  return utf8::units<uint32_t>([b](uint32_t p) { return (uint32_t)ld8(b, p); }, i, e, bad);  // (ym_utf8.h: 4 bytes per step)
 }
 __device__ __forceinline__ uint64_t mask_bytes(uint64_t x, uint32_t n) { return n >= 8 ? x : x & ((1ull << (8 * n)) - 1); }
 __device__ __forceinline__ uint32_t utf16_len(SCur &c, uint32_t n) {
