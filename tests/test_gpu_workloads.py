@@ -702,3 +702,57 @@ def test_c2u_realistic_text_matches_oracle(engine, fmt):
     assert not _compare(engine.run_host("diff", fmt, a2, o2, d2, sva, svo), douts, dst)
     assert engine.stats["docs_general"] == 0, engine.stats
     assert (dst == 3).sum() > 0  # some cuts split an emoji: URIError, reported by the diff kernels themselves
+
+
+def _text_update(client, s):
+    """A V1 update inserting the raw bytes `s` as one ContentString (client, clock 0, no origin, parent ykey
+    "t"); the string's UTF-16 length is not encoded in V1, so any bytes fit."""
+    return _vu(1) + _vu(1) + _vu(client) + _vu(0) + bytes([0x04, 1, 1, ord("t")]) + _vu(len(s)) + s + _vu(0)
+
+
+def _utf8_text(rng, nbytes):
+    """Valid UTF-8 of about nbytes: ASCII, 2-byte (accents), 3-byte (CJK, Hangul near the surrogates) and
+    4-byte (emoji, U+10FFFF) characters."""
+    out = bytearray()
+    pool = [0x61, 0xe9, 0x7ff, 0x800, 0x4e2d, 0xd7ff, 0xe000, 0xfffd, 0x1f600, 0x10000, 0x10ffff]
+    while len(out) < nbytes:
+        k = int(rng.integers(0, 4))
+        cp = int(rng.choice(pool)) if rng.random() < 0.3 else [0x20 + int(rng.integers(0, 90)), 0xc0 + int(rng.integers(0, 0x700)),
+                                                                  0x4e00 + int(rng.integers(0, 0x5000)), 0x1f300 + int(rng.integers(0, 0x300))][k]
+        out += chr(cp).encode("utf-8")
+    return bytes(out)
+
+
+def test_long_non_ascii_strings_deferred_validation(engine):
+    """ContentStrings of >= 32 non-ASCII bytes in the LDS merge kernel are counted by their lane and validated
+    by the whole wave after the walk (ym_fast_common.h rstr_defer / deferred_ok: 4 bytes per lane, carries
+    between lanes and 256-byte steps).  Valid texts of 30-700 bytes, and the same with each kind of invalid
+    sequence (stray continuation, overlong C0 / E0 / F0, surrogate ED A0, above U+10FFFF, F5-FF, a sequence cut
+    by the string's end) placed at random and at the 4-byte / 256-byte step boundaries, 1-20 long strings per
+    document: merged bytes and statuses (yjs's URIError) equal the oracle's."""
+    from yjs_amd import pack_docs
+    rng = np.random.default_rng(2026)
+    bad_seqs = [b"\x80", b"\xc0\x80", b"\xc1\xbf", b"\xe0\x80\x80", b"\xe0\x9f\xbf", b"\xed\xa0\x80", b"\xed\xbf\xbf",
+                b"\xf0\x80\x80\x80", b"\xf0\x8f\xbf\xbf", b"\xf4\x90\x80\x80", b"\xf5\x80\x80\x80", b"\xff", b"\xe4\xb8",
+                b"\xf0\x9f\x98"]
+    docs = []
+    for d in range(3000):
+        nstr = 1 if d % 5 else int(rng.integers(2, 21))
+        ups = []
+        for u in range(nstr + 1):
+            n = int(rng.choice([30, 31, 32, 33, 63, 64, 255, 256, 257, 300, 511, 512, 513, 700])) if u < nstr else 5
+            s = _utf8_text(rng, n)
+            kind = d % 4
+            if u < nstr and kind == 1:  # an invalid sequence somewhere
+                b = bad_seqs[int(rng.integers(0, len(bad_seqs)))]
+                at = int(rng.choice([0, 3, 4, 5, 252, 253, 254, 255, 256, 257, len(s) // 2, len(s)]))
+                at = min(at, len(s))
+                s = s[:at] + b + s[at:]
+            elif u < nstr and kind == 2:  # a cut multi-byte sequence at the end, or a step-boundary end
+                s = s[:-1] if s[-1] >= 0x80 else s + b"\xe4"
+            ups.append(_text_update(1000 + 7 * (nstr - u), s))
+        docs.append(ups)
+    a, o, dd = pack_docs(docs)
+    outs, st, _ = O.batch("merge", 1, a, o, dd, nthreads=8)
+    assert (st != 0).sum() > 100 and (st == 0).sum() > 1000
+    assert not _compare(engine.run_host("merge", 1, a, o, dd), outs, st)

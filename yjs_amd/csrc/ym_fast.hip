@@ -137,6 +137,29 @@ __device__ __forceinline__ uint32_t fast_str(uint32_t &p, bool &ok) {
   p += 1 + nn;
   return nn;
 }
+// UTF-16 length of the strict UTF-8 in the low n (1..7) bytes of w, or ~0 (out of line: inlined, its registers
+// spill in the hot kernel)
+__device__ __attribute__((noinline)) uint32_t utf8_short(uint64_t w, uint32_t n) {
+  utf8::State s;
+  utf8::word<uint32_t>(s, (uint32_t)w, n < 4 ? n : 4);
+  if (n > 4) utf8::word<uint32_t>(s, (uint32_t)(w >> 32), n - 4);
+  return s.bad || s.owe != 0 ? 0xffffffffu : s.units;
+}
+// ContentString: a varString of at most 7 bytes with a one-byte length, any strict UTF-8 (CJK / emoji / accented
+// text, checked by ym_utf8.h on the window's two halves): its UTF-16 length
+__device__ __forceinline__ uint32_t fast_ustr(uint32_t &p, bool &ok) {
+  const uint64_t x = ld8(p);
+  const uint32_t n = (uint32_t)x & 0xffu, nn = n < 7 ? n : 7;
+  const uint64_t body = (x >> 8) & ((1ull << (8 * nn)) - 1);
+  uint32_t units = nn;
+  ok &= n <= 7;
+  if (body & 0x8080808080808080ull) {
+    units = utf8_short(body, nn);
+    ok &= units != 0xffffffffu;
+  }
+  p += 1 + nn;
+  return units;
+}
 // JSON text of a format / embed: "true", "null" or "false"
 __device__ __forceinline__ void fast_json(uint32_t &p, bool &ok) {
   const uint64_t x = ld8(p);
@@ -191,7 +214,7 @@ __device__ __forceinline__ bool item_fast(Cur &c, uint32_t info, uint32_t &len) 
   }
   len = 1;
   if (kind == 4) {
-    len = fast_str(p, ok);
+    len = fast_ustr(p, ok);
     ok &= len != 0;
   } else if (kind == 6) {
     fast_str(p, ok);
@@ -231,7 +254,7 @@ __device__ __forceinline__ bool walk_sections(uint32_t u) {
       const uint32_t info = rdb(c);
       c.bad |= info == 10 || (info & 31) == 0;  // Skip / GC -> general path
       uint32_t l = 1;
-      if (!c.bad && !item_fast(c, info, l)) c.bad |= !item_body<NESTED>(c, info, l);
+      if (!c.bad && !item_fast(c, info, l)) c.bad |= !item_body<NESTED, M::L_HIST, M::L_MISC + 8>(c, info, l);
       if ((info & 0xC0) != 0 && (info & 0x20) != 0) sm[s0] = (uint8_t)(info & ~0x20u);
       len += l;
     }
@@ -866,6 +889,8 @@ __device__ __forceinline__ void merge_doc_v1(const GeneralJob &j, uint32_t di) {
       if (__any(!ok)) YM_DECLINE()
     }
     __syncthreads();
+    // long non-ASCII strings the walk listed (L_HIST is free during the walk): validated by the whole wave
+    if (!deferred_ok<M::L_HIST, M::L_MISC + 8>()) YM_DECLINE()
     YM_TS(1)
     YM_STOP(8)
     const uint32_t nsec = at<uint32_t>(M::L_MISC);

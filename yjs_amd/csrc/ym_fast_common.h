@@ -272,6 +272,68 @@ __device__ __forceinline__ uint32_t rstr(Cur &c) {
   const uint32_t n = rvu(c);
   return c.bad ? 0 : utf16_len(c, n);
 }
+// Long non-ASCII ContentStrings in the LDS merge kernel (round 6; pasted CJK / emoji text): the lane only counts
+// the UTF-16 units (bytes that are not continuation bytes + 4-byte leaders, 8 bytes per step) and lists the
+// string (u32 at DL: LDS offset | bytes << 16; the count at DC) for the wave to validate together after the walk
+// (deferred_ok: 4 bytes per lane, 256 bytes per step).  A lane walking a 500-byte paste byte-serially held its
+// whole wave for ~10 k instructions.  The count is the UTF-16 length of any valid string; an invalid one makes
+// deferred_ok decline the document.  More than DEFER_MAX strings in a document: declined too.
+constexpr uint32_t DEFER_MIN = 32, DEFER_MAX = 16;
+template <uint32_t DL, uint32_t DC>
+__device__ __forceinline__ uint32_t rstr_defer(Cur &c) {
+  const uint32_t n = rvu(c);
+  if (c.bad) return 0;
+  if (n < DEFER_MIN) return utf16_len(c, n);
+  if (!room(c, n)) { c.bad = true; return 0; }
+  uint64_t any = 0;
+  uint32_t u = 0;
+  for (uint32_t o = 0; o < n; o += 8) {
+    const uint32_t k = n - o < 8 ? n - o : 8;
+    const uint64_t x = mask_bytes(ld8(c.p + o), k);
+    const uint64_t hi = x & 0x8080808080808080ull, x1 = x << 1;
+    any |= hi;
+    u += k - (uint32_t)__popcll(hi & ~x1) + (uint32_t)__popcll(hi & x1 & (x << 2) & (x << 3));
+  }
+  if (any) {
+    const uint32_t q = atomicAdd(&at<uint32_t>(DC), 1u);
+    if (q < DEFER_MAX) at<uint32_t>(DL + 4 * q) = c.p | (n << 16);
+    else c.bad = true;
+  }
+  c.p += n;
+  return u;
+}
+// The wave validates the listed strings (after a barrier; wave-uniform result).  Lane l takes bytes [4l, 4l + 4)
+// of each 256-byte step; the continuation bytes and second-byte checks a word owes its successor come from the
+// previous lane (DPP), across steps from lane 63.
+template <uint32_t DL, uint32_t DC>
+__device__ __forceinline__ bool deferred_ok() {
+  const uint32_t nd = at<uint32_t>(DC);
+  if (nd == 0) return true;
+  if (nd > DEFER_MAX) return false;
+  const uint32_t lane = threadIdx.x & 63;
+  bool bad = false;
+  for (uint32_t i = 0; i < nd; i++) {
+    const uint32_t ent = at<uint32_t>(DL + 4 * i), p = ent & 0xffffu, n = ent >> 16;
+    uint32_t co = 0, cc = 0;
+    for (uint32_t o = 0; o < n; o += 256) {
+      const uint32_t q = o + 4 * lane;
+      const uint32_t k = q < n ? (n - q < 4 ? n - q : 4) : 0;
+      const uint32_t x = ld4(p + (q < n ? q : 0));
+      utf8::State own;
+      utf8::word<uint32_t>(own, x, k);  // (its carries out depend on its own bytes only)
+      const uint32_t po = from_prev_lane(own.owe), pc = from_prev_lane(own.chk);
+      utf8::State s;
+      s.owe = lane == 0 ? co : po;
+      s.chk = lane == 0 ? cc : pc;
+      utf8::word<uint32_t>(s, x, k);
+      bad |= s.bad;
+      co = lane_read(own.owe, 63);
+      cc = lane_read(own.chk, 63);
+    }
+    bad |= co != 0;  // (a sequence cut by the string's end at a step boundary)
+  }
+  return !__any(bad);
+}
 // SWAR: bytes of x equal to b / below 0x20 (exact per byte for the masked-in bytes)
 __device__ __forceinline__ uint64_t has_byte(uint64_t x, uint64_t b) {
   const uint64_t y = x ^ (0x0101010101010101ull * b);
@@ -366,7 +428,8 @@ __device__ __forceinline__ void any_canon(Cur &c) {
 // The fields and content of one V1 Item after its info byte (UpdateDecoder.js:127-243 field readers,
 // Item.js:665-683 content refs; lazy reader of 13.5.16: parent kept raw, parentSub only without
 // origins).  Returns false (decline) for kinds this path does not verify; `len` = the Item's length.
-template <bool NESTED = false>
+// DL / DC (the LDS merge kernel's walk): long non-ASCII ContentStrings deferred (rstr_defer).
+template <bool NESTED = false, uint32_t DL = 0, uint32_t DC = 0>
 __device__ __forceinline__ bool item_body(Cur &c, uint32_t info, uint32_t &len) {
   if (info & 0x80) skvu2(c);
   if (info & 0x40) skvu2(c);
@@ -381,7 +444,7 @@ __device__ __forceinline__ bool item_body(Cur &c, uint32_t info, uint32_t &len) 
   switch (info & 31) {
     case 1: len = rvu(c); break;                                      // ContentDeleted
     case 3: { const uint32_t n = rvu(c); if (!room(c, n)) c.bad = true; else c.p += n; break; }  // Binary
-    case 4: len = rstr(c); break;                                     // ContentString
+    case 4: len = DL ? rstr_defer<DL, DC>(c) : rstr(c); break;         // ContentString
     case 5: json_lit<NESTED>(c); break;                               // ContentEmbed
     case 6: rstr(c); json_lit<NESTED>(c); break;                      // ContentFormat
     case 7: {                                                         // ContentType
