@@ -111,6 +111,8 @@ struct Pend { int64_t client; int32_t *refs; uint32_t n, i; uint8_t live; };
 struct DIt { int64_t clock, len; };
 struct DCl { int64_t client; Vec<DIt> it; };
 struct DSet { Vec<DCl> cl; Arena *ar; };  // ar: the arena its vectors grow in (nullptr: the document's)
+struct Wt { int64_t thresh; uint32_t pos; };  // pending delete reader `pos` waits for state(client) > thresh
+struct WL { int64_t client; Vec<Wt> w; };
 struct Tx {
   DSet ds;
   Vec<int32_t> ms;   // _mergeStructs
@@ -140,9 +142,17 @@ struct Doc {
   Type *ty; uint32_t nty, capty;
   Vec<Cl> cl;
   int64_t *hk; uint32_t *hv; uint32_t hcap;  // client -> store index + 1 (open addressing)
-  Vec<Pend> pend;      // store.pendingClientsStructRefs
+  Vec<Pend> pend;      // store.pendingClientsStructRefs, sorted by client (cd_pend)
   Vec<int32_t> stack;  // store.pendingStack
-  Vec<DSet> pdel;      // store.pendingDeleteReaders
+  // store.pendingDeleteReaders, append-only: a re-read reader's remainder takes its place, a reader applied in
+  // full leaves a hole (cl.n == 0), so positions keep the reference's order.  tryResumePendingDeleteReaders
+  // re-reads every reader on every update, but a reader none of whose ranges starts below its client's state
+  // leaves the store as it was: only the readers some client's state has passed since (`awake`, found by the
+  // per-client watch lists add_struct consults) are re-read (pdel_watch / pdel_wake).
+  Vec<DSet> pdel;
+  int64_t *wk; uint32_t *wv; uint32_t wcap;  // client -> watch list index + 1 (open addressing)
+  Vec<WL> wl;
+  Vec<uint32_t> awake;
   Vec<int32_t> roots;  // doc.share
   uint32_t gen;
   Tx *tx;
@@ -220,6 +230,77 @@ YM_INL int64_t cl_state(Doc &d, int32_t s) {
   return l.clock + l.len;
 }
 YM_INL int64_t cd_state(Doc &d, int64_t client) { return cl_state(d, cd_client(d, client)); }  // getState
+// ---- watch lists of the pending delete readers (Doc.pdel) ----
+YM_INL uint32_t wl_hslot(const Doc &d, int64_t client) {
+  uint32_t h = (uint32_t)(((uint64_t)client * 0x9E3779B97F4A7C15ull) >> 40) & (d.wcap - 1);
+  while (d.wv[h] != 0 && d.wk[h] != client) h = (h + 1) & (d.wcap - 1);
+  return h;
+}
+// the watch list of `client` (created when `add`), or NIL
+YM_HOT int32_t wl_get(Doc &d, int64_t client, bool add) {
+  Ctx &c = *d.c;
+  if (d.wcap) {
+    const uint32_t h = wl_hslot(d, client);
+    if (d.wv[h]) return (int32_t)(d.wv[h] - 1);
+  }
+  if (!add) return NIL;
+  if (2 * (d.wl.n + 1) > d.wcap) {
+    const uint32_t nc = d.wcap ? 2 * d.wcap : 64;
+    int64_t *ok = d.wk;
+    uint32_t *ov = d.wv, oc = d.wcap;
+    d.wk = (int64_t *)aalloc(c, *d.a, 8ull * nc);
+    d.wv = (uint32_t *)aalloc(c, *d.a, 4ull * nc);
+    if (c.err) return NIL;
+    for (uint32_t i = 0; i < nc; i++) d.wv[i] = 0;
+    d.wcap = nc;
+    for (uint32_t i = 0; i < oc; i++)
+      if (ov[i]) { const uint32_t h = wl_hslot(d, ok[i]); d.wk[h] = ok[i]; d.wv[h] = ov[i]; }
+  }
+  WL z;
+  __builtin_memset(&z, 0, sizeof(WL));
+  z.client = client;
+  if (!vpush(c, *d.a, d.wl, z)) return NIL;
+  const uint32_t h = wl_hslot(d, client);
+  d.wk[h] = client;
+  d.wv[h] = d.wl.n;
+  return (int32_t)(d.wl.n - 1);
+}
+// reader d.pdel[pos] (just written): per client, woken once that client's state passes its first clock; a
+// reader one of whose ranges already starts below the state (possible after writeDeleteSet's round trip of an
+// unsorted or empty range) is awake at once
+YM_HOT void pdel_watch(Doc &d, uint32_t pos) {
+  Ctx &c = *d.c;
+  const DSet &ds = d.pdel.p[pos];
+  bool now = false;
+  for (uint32_t ci = 0; ci < ds.cl.n && !c.err; ci++) {
+    const DCl &z = ds.cl.p[ci];
+    if (z.it.n == 0) continue;
+    int64_t th = z.it.p[0].clock;
+    for (uint32_t k = 1; k < z.it.n; k++) th = z.it.p[k].clock < th ? z.it.p[k].clock : th;
+    if (th < cd_state(d, z.client)) { now = true; continue; }
+    const int32_t w = wl_get(d, z.client, true);
+    if (w == NIL) return;
+    const Wt e = {th, pos};
+    vpush(c, *d.a, d.wl.p[w].w, e);
+  }
+  if (now) vpush(c, *d.a, d.awake, pos);
+}
+// client's state is now `state` (add_struct): the readers waiting on it are awake (a watcher of a reader since
+// replaced wakes its position for nothing: the re-read finds no range to apply)
+YM_HOT void pdel_wake(Doc &d, int64_t client, int64_t state) {
+  if (d.wcap == 0) return;
+  const int32_t w = wl_get(d, client, false);
+  if (w == NIL) return;
+  Vec<Wt> &v = d.wl.p[w].w;
+  for (uint32_t k = 0; k < v.n;) {
+    if (v.p[k].thresh < state) {
+      if (!vpush(*d.c, *d.a, d.awake, v.p[k].pos)) return;
+      v.p[k] = v.p[--v.n];
+    } else {
+      k++;
+    }
+  }
+}
 // findIndexSS (StructStore.js:123-151); an absent clock is an unexpected case (returns 0)
 YM_INL uint32_t find_index(Doc &d, int32_t s, int64_t clock) {
   if (s == NIL || d.cl.p[s].a.n == 0) { seterr(*d.c, ST_UNEXPECTED); return 0; }
@@ -258,7 +339,7 @@ YM_HOT void add_struct(Doc &d, int32_t i) {  // addStruct (StructStore.js:92-104
     const Item &l = d.it[d.cl.p[s].a.p[d.cl.p[s].a.n - 1]];
     if (l.clock + l.len != x.clock) { seterr(c, ST_UNEXPECTED); return; }
   }
-  vpush(c, *d.a, d.cl.p[s].a, i);
+  if (vpush(c, *d.a, d.cl.p[s].a, i)) pdel_wake(d, x.client, x.clock + x.len);
 }
 YM_INL int32_t cd_root(Doc &d, const Span &key) {  // doc.get(key): created on first use
   for (uint32_t i = 0; i < d.roots.n; i++)
@@ -752,10 +833,20 @@ YM_HOT void it_integrate(Doc &d, int32_t i, int64_t off) {
 }
 
 // ---- pending structs ---------------------------------------------------------------------------------
+// d.pend is kept sorted by client (one entry per client): the reference's Map is only ever read in that
+// order (resumeStructIntegration sorts its keys), so lookups are a binary search and the sort is free
+YM_INL uint32_t pend_lb(const Doc &d, int64_t client) {
+  uint32_t lo = 0, hi = d.pend.n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (d.pend.p[mid].client < client) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
 YM_INL int32_t cd_pend(Doc &d, int64_t client) {
-  for (uint32_t i = 0; i < d.pend.n; i++)
-    if (d.pend.p[i].live && d.pend.p[i].client == client) return (int32_t)i;
-  return NIL;
+  const uint32_t i = pend_lb(d, client);
+  return i < d.pend.n && d.pend.p[i].live && d.pend.p[i].client == client ? (int32_t)i : NIL;
 }
 YM_INL void refs_sort(Doc &d, int32_t *a, uint32_t n) {  // stable sort by clock (V8's sort is stable)
   for (uint32_t i = 1; i < n; i++) {
@@ -769,25 +860,17 @@ YM_INL void refs_sort(Doc &d, int32_t *a, uint32_t n) {  // stable sort by clock
 YM_HOT void resume_integration(Doc &d) {
   Ctx &c = *d.c;
   Arena &A = *d.a;
-  Arena &T = *d.ta;  // the sorted ids and the state cache live for this call only
-  uint32_t nids = 0;
-  int64_t *ids = (int64_t *)aalloc(c, T, 8ull * (d.pend.n + 1));
-  if (!ids) return;
-  for (uint32_t i = 0; i < d.pend.n; i++)
-    if (d.pend.p[i].live) ids[nids++] = d.pend.p[i].client;
-  for (uint32_t i = 1; i < nids; i++) {
-    const int64_t v = ids[i];
-    uint32_t j = i;
-    while (j > 0 && ids[j - 1] > v) { ids[j] = ids[j - 1]; j--; }
-    ids[j] = v;
-  }
+  Arena &T = *d.ta;  // the state cache lives for this call only
+  // the pending clients in ascending order are d.pend itself (sorted by client, every entry live, not
+  // reordered here): the target is the last entry not yet exhausted
+  uint32_t nids = d.pend.n;
   if (nids == 0) return;
   int32_t cur = NIL;
   auto next_target = [&]() {
-    cur = cd_pend(d, ids[nids - 1]);
+    cur = (int32_t)(nids - 1);
     while (cur != NIL && d.pend.p[cur].n == d.pend.p[cur].i) {
       nids--;
-      if (nids > 0) cur = cd_pend(d, ids[nids - 1]);
+      if (nids > 0) cur = (int32_t)(nids - 1);
       else { d.pend.n = 0; cur = NIL; break; }
     }
   };
@@ -859,22 +942,14 @@ YM_HOT void resume_integration(Doc &d) {
 }
 
 // readAndApplyDeleteSet over decoded ranges (DeleteSet.js:270-323); unapplied ranges become a pending
-// delete reader.  `kept`: ds is a pending reader already in the persistent arena -- when none of its ranges
-// applies, the new reader equals it range for range and is kept as it is (a history that leaves deletes
-// pending re-reads every pending reader on every update; copying them each time grew the arena
-// quadratically).  An unapplied range of length 0 (a V1 delete set may hold one) sets *zero: the reference's
-// writeDeleteSet of the unapplied set throws at it (DSEncoderV2.writeDsLen, UpdateEncoder.js:255-258), after
-// every client of the update's delete set has been read and applied.
-YM_HOT void apply_ds(Doc &d, const DSet &ds, bool kept = false, bool *zero = nullptr) {
+// delete reader, appended to d.pdel, or written at `slot` (the re-read reader's own position, a hole before).
+// A pending reader none of whose ranges starts below its client's state would come back range for range (its
+// ranges have made writeDeleteSet's round trip once already), so the caller re-reads only readers with such a
+// range (tryResumePendingDeleteReaders, cd_transact).  An unapplied range of length 0 (a V1 delete set may hold
+// one) sets *zero: the reference's writeDeleteSet of the unapplied set throws at it (DSEncoderV2.writeDsLen,
+// UpdateEncoder.js:255-258), after every client of the update's delete set has been read and applied.
+YM_HOT void apply_ds(Doc &d, const DSet &ds, bool *zero = nullptr, uint32_t slot = 0xffffffffu) {
   Ctx &c = *d.c;
-  if (kept) {
-    bool any = false;
-    for (uint32_t ci = 0; ci < ds.cl.n && !any; ci++) {
-      const int64_t state = cd_state(d, ds.cl.p[ci].client);
-      for (uint32_t k = 0; k < ds.cl.p[ci].it.n && !any; k++) any = ds.cl.p[ci].it.p[k].clock < state;
-    }
-    if (!any) { vpush(c, *d.a, d.pdel, ds); return; }
-  }
   DSet un = {{nullptr, 0, 0}, d.ta};
   for (uint32_t ci = 0; ci < ds.cl.n && !c.err; ci++) {
     const int64_t client = ds.cl.p[ci].client;
@@ -938,7 +1013,13 @@ YM_HOT void apply_ds(Doc &d, const DSet &ds, bool kept = false, bool *zero = nul
     z.it.n = un.cl.p[k].it.n;
     keep.cl.p[keep.cl.n++] = z;
   }
-  vpush(c, *d.a, d.pdel, keep);
+  if (slot == 0xffffffffu) {
+    slot = d.pdel.n;
+    if (!vpush(c, *d.a, d.pdel, keep)) return;
+  } else {
+    d.pdel.p[slot] = keep;
+  }
+  pdel_watch(d, slot);
 }
 
 // ---- reading -----------------------------------------------------------------------------------------
@@ -1424,7 +1505,7 @@ YM_HOT void cd_transact(Doc &d, Reader &r) {
   for (uint32_t q = 0; q < refs.n && !c.err; q++) {  // mergeReadStructsIntoPendingReads
     const int32_t p = cd_pend(d, refs.p[q].client);
     if (p == NIL) {
-      vpush(c, *d.a, d.pend, refs.p[q]);
+      vinsert(c, *d.a, d.pend, pend_lb(d, refs.p[q].client), refs.p[q]);
     } else {
       const uint32_t rn = d.pend.p[p].n - d.pend.p[p].i, m = refs.p[q].n;
       int32_t *na = (int32_t *)aalloc(c, *d.a, 4ull * (rn + m + 1));
@@ -1453,13 +1534,30 @@ YM_HOT void cd_transact(Doc &d, Reader &r) {
     }
     d.pend.n = w;
   }
-  {  // tryResumePendingDeleteReaders: the readers are re-read in order and the ones still pending written
-     // back in place (reader q's successor lands at an index <= q, after reader q was read)
-    const Vec<DSet> pr = d.pdel;
-    d.pdel.n = 0;
-    for (uint32_t q = 0; q < pr.n && !c.err; q++) {
-      const DSet one = pr.p[q];
-      apply_ds(d, one, true);
+  if (d.awake.n) {  // tryResumePendingDeleteReaders: the awake readers re-read in order, each remainder in its
+                    // reader's place (what a reader pushes now is re-read on the next update, as in the reference)
+    const uint32_t n = d.awake.n;
+    uint32_t *aw = (uint32_t *)aalloc(c, *d.ta, 4ull * n);
+    if (!aw) return;
+    for (uint32_t k = 0; k < n; k++) {  // insertion sort (a few positions per update)
+      const uint32_t v = d.awake.p[k];
+      uint32_t j = k;
+      while (j > 0 && aw[j - 1] > v) { aw[j] = aw[j - 1]; j--; }
+      aw[j] = v;
+    }
+    d.awake.n = 0;
+    for (uint32_t k = 0; k < n && !c.err; k++) {
+      const uint32_t q = aw[k];
+      if (k > 0 && aw[k - 1] == q) continue;
+      const DSet one = d.pdel.p[q];
+      bool any = false;
+      for (uint32_t ci = 0; ci < one.cl.n && !any; ci++) {
+        const int64_t state = cd_state(d, one.cl.p[ci].client);
+        for (uint32_t i = 0; i < one.cl.p[ci].it.n && !any; i++) any = one.cl.p[ci].it.p[i].clock < state;
+      }
+      if (!any) continue;  // (a hole, or a watcher of a replaced reader: nothing to apply)
+      d.pdel.p[q].cl.n = 0;
+      apply_ds(d, one, nullptr, q);
     }
   }
   {  // readAndApplyDeleteSet: each client's ranges are applied as read (the clients are independent)
@@ -1486,7 +1584,7 @@ YM_HOT void cd_transact(Doc &d, Reader &r) {
         DIt e = {clock, len};
         vpush(c, *d.ta, one.cl.p[k].it, e);
       }
-      if (!c.err) apply_ds(d, one, false, &zero);
+      if (!c.err) apply_ds(d, one, &zero);
     }
     if (zero && !c.err) seterr(c, ST_UNEXPECTED);
   }
