@@ -12,6 +12,7 @@
 #include <node_api.h>
 
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -82,6 +83,7 @@ struct Job {
   ym_batch b;
   std::vector<uint64_t> upd_conv, sv_conv;
   uint8_t *arena = nullptr;  // from the library's page-locked pool (ym_host_alloc), uninitialised
+  uint64_t cap = 0;          // ... the bytes asked for it
   uint64_t used = 0;
   // per-document results, also from the pool: with every output array page-locked the library's packing
   // kernels write them straight into host memory (no copy op)
@@ -163,7 +165,12 @@ static void execute(Job &j) {
   for (int attempt = 0; attempt < 4; attempt++) {
     ym_host_free(j.arena);
     j.arena = (uint8_t *)ym_host_alloc(cap ? cap : 1);
-    if (!j.arena) { j.rc = YM_ERR_CAPACITY; return; }
+    j.cap = cap;
+    if (!j.arena) {
+      if (getenv("YMERGE_TRACE_CAP")) fprintf(stderr, "addon: no pool buffer of %llu bytes\n", (unsigned long long)cap);
+      j.rc = YM_ERR_CAPACITY;
+      return;
+    }
     ym_out o = {j.arena, cap, j.out_off, j.out_len, j.status, 0};
     j.rc = j.op == 0   ? ym_merge(&j.b, &o, nullptr, nullptr)
            : j.op == 1 ? ym_diff(&j.b, &o, nullptr, nullptr)
@@ -174,12 +181,34 @@ static void execute(Job &j) {
            : j.op == 7 ? ym_compact(&j.b, &o, nullptr, nullptr)
                        : ym_sv(&j.b, &o, nullptr, nullptr);
     j.used = o.used;
+    if (getenv("YMERGE_TRACE_CAP")) fprintf(stderr, "addon op %d attempt %d cap %llu rc %d used %llu\n", j.op, attempt, (unsigned long long)cap, j.rc, (unsigned long long)o.used);
     if (j.rc == YM_ERR_CAPACITY) { cap = o.used + 4096; continue; }
     break;
   }
 }
 
-static void free_arena(napi_env, void *data, void *) { ym_host_free(data); }  // back to the pool
+// A pool buffer handed to JS is reported to V8 as external memory (its whole page-locked size class, >= 64 KiB),
+// so the collector runs as such buffers pile up: unreported, a few thousand small results (each a 64 KiB pinned
+// buffer) waited for a collection V8 saw no reason to start, and the pool's hipHostMalloc failed.
+static size_t pool_bytes(size_t n) {
+  size_t c = 1ull << 16;  // ym_host_alloc's smallest class
+  while (c < n) c <<= 1;
+  return c;
+}
+static void free_arena(napi_env env, void *data, void *hint) {  // back to the pool
+  ym_host_free(data);
+  int64_t now = 0;
+  napi_adjust_external_memory(env, -(int64_t)(uintptr_t)hint, &now);
+}
+// data (from ym_host_alloc, `bytes` asked for) as an external ArrayBuffer
+static napi_status pool_arraybuffer(napi_env env, void *data, size_t n, size_t bytes, napi_value *ab) {
+  const size_t c = pool_bytes(bytes ? bytes : 1);
+  napi_status s = napi_create_external_arraybuffer(env, data, n, free_arena, (void *)(uintptr_t)c, ab);
+  if (s != napi_ok) return s;
+  int64_t now = 0;
+  napi_adjust_external_memory(env, (int64_t)c, &now);
+  return napi_ok;
+}
 
 static napi_value make_f64(napi_env env, const uint64_t *src, size_t n) {
   void *data = nullptr;
@@ -212,7 +241,7 @@ static napi_value result(napi_env env, Job &j, napi_value *err) {
   const uint64_t n = j.used;
   napi_value ab, ta, res;
   if (n > 0) {
-    if (napi_create_external_arraybuffer(env, j.arena, n, free_arena, nullptr, &ab) != napi_ok) return nullptr;
+    if (pool_arraybuffer(env, j.arena, n, j.cap, &ab) != napi_ok) return nullptr;
     j.arena = nullptr;  // owned by the ArrayBuffer now
   } else if (napi_create_arraybuffer(env, 0, nullptr, &ab) != napi_ok) {
     return nullptr;
@@ -310,7 +339,7 @@ static napi_value HostBuffer(napi_env env, napi_callback_info info) {
   void *p = ym_host_alloc(bytes ? bytes : 1);
   if (!p) return undef;
   napi_value ab, ta;
-  if (napi_create_external_arraybuffer(env, p, bytes, free_arena, nullptr, &ab) != napi_ok) {
+  if (pool_arraybuffer(env, p, bytes, bytes, &ab) != napi_ok) {
     ym_host_free(p);
     return undef;
   }

@@ -142,3 +142,31 @@ def test_golden_meta_update_log_shape(engine, fmt):
             bad.append((i, c["id"], st))
     assert not bad, bad[:20]
     assert engine.stats["docs_fast"] > 0, engine.stats
+
+
+def test_tiny_inputs_one_document_per_call(engine):
+    """Every golden merge / delete-set merge with at most 16 input bytes as a call of its own (the Node API's
+    shape: each document alone, its bytes at offset 0 of the arena), with u64 and u32 offsets.  A document of no
+    bytes at all (one empty delete set, empty updates) once made k_fast_merge_v1's staging load a vector at index
+    2^32 - 1 (an illegal address that ended the process's GPU context)."""
+    from yjs_amd import pack_docs
+    cases = [c for c in CASES if c["op"] in ("merge", "dsmerge", "dsmerge_ref") and len(c["inputs"]) > 0
+             and sum(len(x) for x in c["inputs"]) <= 16]
+    assert any(sum(len(x) for x in c["inputs"]) == 0 for c in cases)
+    bad = []
+    for c in cases:
+        for off32 in (False, True):
+            arena, upd_off, doc_upd = pack_docs([c["inputs"]])
+            if off32:
+                upd_off = upd_off.astype(np.uint32)
+            out_arena, out_off, out_len, status = engine.run_host(c["op"], c["fmt"], arena, upd_off, doc_upd)
+            st = int(status[0])
+            if "error" in c:
+                why = O.js_error_mismatch(st, c["error"], c["message"])
+                if why:
+                    bad.append((c["id"], off32, why))
+                continue
+            got = out_arena[int(out_off[0]):int(out_off[0]) + int(out_len[0])].tobytes() if st == 0 else None
+            if got != c["expect"]:
+                bad.append((c["id"], off32, st))
+    assert not bad, bad[:20]

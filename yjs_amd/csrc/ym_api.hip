@@ -1070,6 +1070,11 @@ int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *
     stats->bytes_in = S->pinned[6];
     stats->docs_chunked = chunked;
   }
+  static const bool trace = getenv("YMERGE_TRACE_CAP") != nullptr;  // diagnostics: why a call reports capacity
+  if (trace)
+    fprintf(stderr, "ym trace op %u depth %d nd %u used %llu dev_cap %llu out_cap %llu bytes_out %llu ngen %u\n", op, depth, nd,
+            (unsigned long long)used, (unsigned long long)dev_cap, (unsigned long long)out->cap,
+            (unsigned long long)S->pinned[5], ngen);
   if (!host) return used > out->cap ? YM_ERR_CAPACITY : 0;
   // host batch: pack the outputs in document order (out_off[d] = bytes of the outputs before d), then
   // copy only them back.  The staging arena is the library's own: an overflow grows it and runs the

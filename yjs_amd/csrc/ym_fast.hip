@@ -781,15 +781,19 @@ __device__ __forceinline__ bool stage_doc(const GeneralJob &j, const T *off, uin
   const uint32_t nvec = (uint32_t)((base + bytes + 15) >> 4);
   // (stores at the same clamped indices, unconditionally: a lane past the end writes the last vector / offset
   // again, the same bytes; a conditional store let the compiler sink each load into its branch and wait there)
-  uint32_t vi[NV];
-  uint4 vv[NV];
+  // (no bytes at all -- empty inputs: a delete-set merge of one empty set, a merge of empty updates -- loads
+  // nothing: the clamped index nvec - 1 would wrap to 2^32 - 1)
+  if (nvec != 0) {
+    uint32_t vi[NV];
+    uint4 vv[NV];
 #pragma unroll
-  for (uint32_t t = 0; t < NV; t++) {
-    vi[t] = lane + 64 * t < nvec ? lane + 64 * t : nvec - 1;
-    vv[t] = src[vi[t]];
+    for (uint32_t t = 0; t < NV; t++) {
+      vi[t] = lane + 64 * t < nvec ? lane + 64 * t : nvec - 1;
+      vv[t] = src[vi[t]];
+    }
+#pragma unroll
+    for (uint32_t t = 0; t < NV; t++) at<uint4>(M::L_IN + 16 * vi[t]) = vv[t];
   }
-#pragma unroll
-  for (uint32_t t = 0; t < NV; t++) at<uint4>(M::L_IN + 16 * vi[t]) = vv[t];
 #pragma unroll
   for (uint32_t t = 0; t < NO; t++)
     at<uint16_t>(M::L_UOFF + 2 * (lane + 64 * t < kc ? lane + 64 * t : kc)) = (uint16_t)(ov[t] - b0 + base);
