@@ -56,6 +56,7 @@ constexpr uint32_t FAIL_RUN = 8;       // failed positions in a row before the w
 // chain there after a few bytes); a chunk still off the chain after them (structs outside the short cut,
 // C5's XML items) goes back to the full parser at every position
 constexpr uint32_t START_CHEAP = 48;
+constexpr uint32_t PRE_ONE = 0, PRE_MANY = 512;  // k_pw_walk's pre-roll (bytes before the chunk, no records)
 // longest string / binary / ContentAny the window tables accept (k_pw_ms, k_pw_small): a table entry is a
 // parse at an offset that may not start a struct, and an uncapped parse there can run to the window's end
 // (a garbage length read as a string to validate): the tables cost O(window x cap).  Longer true contents
@@ -168,8 +169,11 @@ __global__ void k_pw_totals(const uint32_t *many, uint32_t *host) {
 // first NFIRST records' position words and clock sums (the stitch's entry lookup needs no record load).
 // last* = index + 1 of the last FAIL / patched / Skip record (0: none); a struct of >= 2^19 clocks is
 // recorded as a FAIL (its length does not fit the record): the stitch takes such records one by one.
+// pre_one / pre_many: bytes walked before the chunk's first byte, without records (documents of <= 16 / > 16
+// client sections), so that the chain is met before the chunk starts: the stitch then finds its entry among
+// the chunk's first records instead of re-parsing structs in lockstep until the chain meets it (round 6)
 __global__ void __launch_bounds__(256) k_pw_walk(GeneralJob j, const uint32_t *cbase, uint32_t nd, uint32_t total,
-                                                 uint4 *desc, uint32_t *recs) {
+                                                 uint4 *desc, uint32_t *recs, uint32_t pre_one, uint32_t pre_many) {
   const uint32_t g = blockIdx.x * 256 + threadIdx.x;
   if (g >= total) return;
   uint32_t lo = 0, hi = nd - 1;  // the document: largest d with cbase[d] <= g
@@ -191,7 +195,9 @@ __global__ void __launch_bounds__(256) k_pw_walk(GeneralJob j, const uint32_t *c
   }
   uint32_t nrec = 0, cum = 0, lastfail = 0, lastpatch = 0, lastskip = 0, fails = FAIL_RUN, okrun = 0;  // the chunk start is mid-struct: only short-cut candidates until two structs in a row
   bool frun = false, ovf = false, start = true;
-  uint32_t p = c0;
+  const uint32_t pre = many ? pre_many : pre_one;
+  const uint32_t w0 = c0 > pre ? c0 - pre : 0;  // the walk's start (records from c0 on)
+  uint32_t p = w0;
   // the descriptor's first-record words (position | flags, clock sum) are stored as the records come
   uint4 *Q = desc + 5ull * g;
   uint4 rq = make_uint4(0, 0, 0, 0);  // the records of the current group of four
@@ -199,7 +205,7 @@ __global__ void __launch_bounds__(256) k_pw_walk(GeneralJob j, const uint32_t *c
   Q[1] = Q[2] = make_uint4(POS_MASK, POS_MASK, POS_MASK, POS_MASK);
   Q[3] = Q[4] = make_uint4(0, 0, 0, 0);
   while (p < c1) {
-    if (start && p >= c0 + START_CHEAP) {
+    if (start && p >= w0 + START_CHEAP) {
       start = false;
       if (fails >= FAIL_RUN) fails = 0;
     }
@@ -218,7 +224,7 @@ __global__ void __launch_bounds__(256) k_pw_walk(GeneralJob j, const uint32_t *c
     // the header (the FAIL recorded at p ends the previous section's last struct there), so the stitch finds
     // the section's first struct among the records instead of re-parsing until the chain meets it again.
     uint32_t hjump = 0;
-    if (many && !ok && okrun >= 2 && p > c0) {  // (after >= 2 structs in a row: not inside a delete set's varuints)
+    if (many && !ok && okrun >= 2 && p > w0) {  // (after >= 2 structs in a row: not inside a delete set's varuints)
       ln::LCur h = ln::make(D, p, len);
       const uint32_t ns = ln::rvu(h);
       ln::rvu(h);
@@ -233,7 +239,8 @@ __global__ void __launch_bounds__(256) k_pw_walk(GeneralJob j, const uint32_t *c
         if (ok2) hjump = h.p;
       }
     }
-    if (ok || !frun) {
+    const bool rec = p >= c0;  // (the pre-roll records nothing)
+    if (rec && (ok || !frun)) {
       if (nrec == CAP) { ovf = true; break; }  // overflow: the stitch re-parses this chunk
       // a struct of >= 2^19 clocks is recorded as a FAIL (its length does not fit the record; clock sums
       // over the chunk could wrap): the stitch takes the records from the entry up to here one by one and
@@ -252,7 +259,7 @@ __global__ void __launch_bounds__(256) k_pw_walk(GeneralJob j, const uint32_t *c
       if (ok && (fl & F_PATCH)) lastpatch = nrec;
       if (ok && (fl & F_SKIP)) lastskip = nrec;
     }
-    cum += ok ? cl : 0;
+    cum += ok && rec ? cl : 0;
     // back to trying every position only after two structs in a row (a lone garbage GC in a delete set
     // would otherwise restart the run of full parses)
     okrun = ok ? okrun + 1 : 0;
@@ -1831,7 +1838,13 @@ int pw_finish(const GeneralJob &j, hipStream_t st, PwBufs &B) {
   }
   uint4 *desc = (uint4 *)B.p[2];
   uint32_t *recs = (uint32_t *)B.p[3];
-  k_pw_walk<<<(total + 255) / 256, 256, 0, st>>>(j, cbase, j.n, total, desc, recs);
+  static int pre_one = -1, pre_many = -1;
+  if (pre_one < 0) {  // (YMERGE_PW_PRE: both; YMERGE_PW_PRE_MANY: many-section documents only)
+    const char *e = getenv("YMERGE_PW_PRE"), *em = getenv("YMERGE_PW_PRE_MANY");
+    pre_one = e ? atoi(e) : (int)PRE_ONE;
+    pre_many = em ? atoi(em) : e ? atoi(e) : (int)PRE_MANY;
+  }
+  k_pw_walk<<<(total + 255) / 256, 256, 0, st>>>(j, cbase, j.n, total, desc, recs, (uint32_t)pre_one, (uint32_t)pre_many);
   if (op == OP_DIFF && dsl) k_pw_stitch<OP_DIFF, true><<<grid, 64, L_DSL + sizeof(wds::DsLdsS), st>>>(j, cbase, desc, recs, done, msz);
   else if (op == OP_DIFF) k_pw_stitch<OP_DIFF><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done, msz);
   else if (op == OP_SV) k_pw_stitch<OP_SV><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done, msz);
