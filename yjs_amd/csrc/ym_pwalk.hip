@@ -72,6 +72,7 @@ constexpr uint32_t L_REC = L_PVAL + NPATCH;        // u32[CAP] the records of th
 constexpr uint32_t LDS_BYTES = L_REC + 4 * CAP;
 constexpr uint32_t L_DSL = (LDS_BYTES + 15) & ~15u;  // diff: wds::DsLdsS (the delete set's token tables, 1 KB windows:
                                                     // the 4 KB ones cost the stitch its occupancy -- C3 V1 diff 14 -> 24 ms)
+constexpr uint32_t L_SVM = (L_DSL + (uint32_t)sizeof(wds::DsLdsS) + 15) & ~15u;  // diff, DSL: lsv's map (32 KB)
 enum { S_PRELEN = 0, S_A0, S_A1, S_B0, S_B1, S_WRITTEN, S_CLIENT, S_FCLOCK, S_OUTB };
 constexpr uint32_t NONE = 0xffffffffu;
 
@@ -395,6 +396,98 @@ __device__ uint32_t slice_head(sc::cu32 *B, uint32_t adj, uint32_t s0, uint32_t 
   }
 #define PW_DECLINE() PW_DECLINE_R(why ? why : 2)
 // the document's result is yjs's URIError (slice_head SH_URI): completed here with that status
+// ---- LDS state-vector map of the DSL variant (many-section documents: C5's ~1,000-entry state vectors): sv[client]
+// from one probe round of LDS reads instead of cmap's three dependent device-scope loads per section (round 6).
+// Keys client + 1 (0 = empty) over 4,096 slots (load factor <= 1/2 at BS_NSV entries); a slot's value is first the
+// largest entry index mapped to it (decodeStateVector: a later entry for a client wins, encoding.js:536-545), then
+// that entry's clock.  Client 0xFFFFFFFF (whose key would be 0) keeps its index / clock in the two words after.
+namespace lsv {
+constexpr uint32_t SLOTS = 4096, MASK = SLOTS - 1, BYTES = 8 * SLOTS + 16;
+static_assert(SLOTS == BS_MAP_SLOTS && SLOTS >= 2 * NSV, "cmap::hash; load factor <= 1/2");
+__device__ __forceinline__ void build(uint32_t base, const uint32_t *svt, uint32_t nsv) {
+  const uint32_t lane = threadIdx.x;
+  uint32_t *K = reinterpret_cast<uint32_t *>(sm + base), *V = K + SLOTS;
+  for (uint32_t i = lane; i < (2 * SLOTS + 4) / 4; i += 64) reinterpret_cast<uint4 *>(K)[i] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  for (uint32_t i = lane; i < nsv; i += 64) {
+    const uint32_t c = svt[2 * i];
+    if (c == cmap::XCLIENT) {
+      atomicMax(&K[2 * SLOTS], i + 1);
+      continue;
+    }
+    uint32_t sl = cmap::hash(c);
+    for (uint32_t probe = 0; probe < SLOTS; probe++, sl = (sl + 1) & MASK) {
+      const uint32_t old = atomicCAS(&K[sl], 0u, c + 1);
+      if (old == 0 || old == c + 1) {
+        atomicMax(&V[sl], i + 1);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t sl = lane; sl < SLOTS; sl += 64) {
+    const uint32_t v = V[sl];
+    if (v) V[sl] = svt[2 * (v - 1) + 1];
+  }
+  if (lane == 0 && K[2 * SLOTS]) K[2 * SLOTS + 1] = svt[2 * (K[2 * SLOTS] - 1) + 1];
+  __syncthreads();
+}
+// sv[client] (0 when absent), wave-uniform client
+__device__ __forceinline__ uint32_t get(uint32_t base, uint32_t client) {
+  const uint32_t *K = reinterpret_cast<const uint32_t *>(sm + base), *V = K + SLOTS;
+  if (client == cmap::XCLIENT) return K[2 * SLOTS] ? K[2 * SLOTS + 1] : 0;
+  const uint32_t key = client + 1, s0 = cmap::hash(client);
+  for (uint32_t b = 0; b < SLOTS; b += 64) {
+    const uint32_t sl = (s0 + b + threadIdx.x) & MASK;
+    const uint32_t kv = K[sl];
+    const uint64_t hit = __ballot(kv == key), emp = __ballot(kv == 0);
+    if (hit | emp) {
+      const uint32_t fh = hit ? (uint32_t)__builtin_ctzll(hit) : 64, fe = emp ? (uint32_t)__builtin_ctzll(emp) : 64;
+      if (fh > fe) return 0;
+      return V[(s0 + b + fh) & MASK];
+    }
+  }
+  return 0;
+}
+}  // namespace lsv
+
+// A section header (#structs, client, clock: three lib0 varuints, <= 15 bytes) from one 24-byte window whose
+// three loads are issued together.  ln::rvu refills its cursor after each varint: three dependent global loads
+// per section, ~2 of the stitch's ~8 ms per C5 document (~1,000 sections).  Same checks as ln::rvu.
+__device__ __forceinline__ uint64_t win8(uint64_t a, uint64_t b, uint64_t c, uint32_t o) {  // bytes [o, o + 8), o < 16
+  const uint64_t lo = o < 8 ? a : b, hi = o < 8 ? b : c;
+  const uint32_t sh = 8 * (o & 7);
+  return sh == 0 ? lo : (lo >> sh) | (hi << (64 - sh));
+}
+__device__ __forceinline__ bool hdr3(const uint8_t *D, uint32_t &x, uint32_t len, uint32_t &v0, uint32_t &v1, uint64_t &v2) {
+  if (x + 24 > len) {
+    ln::LCur c = ln::make(D, x, len);
+    v0 = ln::rvu(c);
+    v1 = ln::rvu(c);
+    v2 = ln::rvu(c);
+    x = c.p;
+    return !c.bad;
+  }
+  const uint64_t a = ln::ld8(D, x), b = ln::ld8(D, x + 8), c = ln::ld8(D, x + 16);
+  uint32_t o = 0, v[3];
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const uint64_t w = win8(a, b, c, o);
+    const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
+    const uint32_t nb = ln::vu_nb(lo, hi);
+    const uint32_t val = (lo & 0x7fu) | ((lo >> 1) & 0x3f80u) | ((lo >> 2) & 0x1fc000u) | ((lo >> 3) & 0xfe00000u) | (hi << 28);
+    bad |= ln::vu_bad(lo, hi, nb, x + o, len);
+    v[k] = val & (uint32_t)((1ull << (7 * (nb < 5 ? nb : 5))) - 1);
+    o += nb < 6 ? nb : 0;
+  }
+  v0 = v[0];
+  v1 = v[1];
+  v2 = v[2];
+  x += o;
+  return !bad;
+}
+
 constexpr uint32_t WHY_URI = 99;
 #define PW_URIERR()                                                                  \
   {                                                                                  \
@@ -447,7 +540,10 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
       }
       __syncthreads();
       if (bad) PW_DECLINE_R(3)
-      if (nsv > 64) cmap::build_sv(X.map, X.svt, nsv);
+      if (nsv > 64) {
+        if constexpr (DSL) lsv::build(L_SVM, X.svt, nsv);
+        else cmap::build_sv(X.map, X.svt, nsv);
+      }
     }
     PT(0);
     // ---- struct section: headers parsed here, structs from the walk's records
@@ -472,20 +568,15 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
     for (uint32_t ci = 0; ci < nclients && !declined; ci++) {
       uint32_t nstructs, client;
       uint64_t clock;
-      {
-        ln::LCur c = ln::make(D, x, len);
-        nstructs = ln::rvu(c);
-        client = ln::rvu(c);
-        clock = ln::rvu(c);
-        x = c.p;
-        if (c.bad) { declined = true; why = 5; break; }
-      }
+      if (!hdr3(D, x, len, nstructs, client, clock)) { declined = true; why = 5; break; }
       if (ci > 0 && client == prev_client) { declined = true; why = 6; break; }
       // meta: taken only when the clients descend (a repeated client would keep its first Map slot)
       if (OP == OP_META && ci > 0 && client > prev_client) { declined = true; why = 6; break; }
       const uint32_t first_clock = (uint32_t)clock;
       prev_client = client;
-      const uint32_t k = OP != OP_DIFF ? 0 : nsv > 64 ? cmap::sv_get(X.map, X.svt, client) : sv_lookup(X.svt, nsv, client);
+      const uint32_t k = OP != OP_DIFF ? 0
+                         : nsv > 64 ? (DSL ? lsv::get(L_SVM, client) : cmap::sv_get(X.map, X.svt, client))
+                                    : sv_lookup(X.svt, nsv, client);
       if (OP == OP_SV && nstructs > 0 && sv_any && client != sv_client) {
         if (sv_clock != 0) {
           if (sv_n >= NSV) { declined = true; why = 13; break; }
@@ -1845,7 +1936,7 @@ int pw_finish(const GeneralJob &j, hipStream_t st, PwBufs &B) {
     pre_many = em ? atoi(em) : e ? atoi(e) : (int)PRE_MANY;
   }
   k_pw_walk<<<(total + 255) / 256, 256, 0, st>>>(j, cbase, j.n, total, desc, recs, (uint32_t)pre_one, (uint32_t)pre_many);
-  if (op == OP_DIFF && dsl) k_pw_stitch<OP_DIFF, true><<<grid, 64, L_DSL + sizeof(wds::DsLdsS), st>>>(j, cbase, desc, recs, done, msz);
+  if (op == OP_DIFF && dsl) k_pw_stitch<OP_DIFF, true><<<grid, 64, L_SVM + lsv::BYTES, st>>>(j, cbase, desc, recs, done, msz);
   else if (op == OP_DIFF) k_pw_stitch<OP_DIFF><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done, msz);
   else if (op == OP_SV) k_pw_stitch<OP_SV><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done, msz);
   else k_pw_stitch<OP_META><<<grid, 64, LDS_BYTES, st>>>(j, cbase, desc, recs, done, msz);
