@@ -1041,6 +1041,10 @@ int fast_launch(uint32_t op, const GeneralJob &j, uint32_t n_upd, hipStream_t st
     k_fast_merge_v1<0, 5, false, false, false, false><<<grid, 64, LDS_BYTES, st>>>(j, j.n);
   } else if (occ == 5) {
     YM_LAUNCH(0, 5);
+  } else if (occ == 6) {
+    YM_LAUNCH(0, 6);
+  } else if (occ == 7) {
+    YM_LAUNCH(0, 7);
   } else {
     switch (stop) {
       case 1: YM_LAUNCH(1, 8); break;
