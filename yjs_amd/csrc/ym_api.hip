@@ -226,11 +226,21 @@ __global__ void __launch_bounds__(1024) k_chunk_scan(const int32_t *status, cons
 // one wave per document: its output from the fast path's slot to its packed place (16-byte stores)
 // (dst may be page-locked host memory: the stores then cross PCIe as 16-byte writes; a document past `cap` is
 // not written, the host reports YM_ERR_CAPACITY)
+// h_off / h_len / h_st (pipelined host merges with page-locked result arrays, else nullptr): document d's packed
+// offset, length and status go to host memory here, one lane each, on the output stream -- written by the
+// placement scan instead, these ~20 B PCIe stores per document held the compute stream ~50 us per chunk
 __global__ void __launch_bounds__(256) k_pack_docs(const uint8_t *src, const uint64_t *src_off, const uint64_t *dst_off,
-                                                   const uint64_t *len, uint32_t n, uint8_t *dst, uint64_t cap) {
+                                                   const uint64_t *len, uint32_t n, uint8_t *dst, uint64_t cap,
+                                                   const int32_t *st = nullptr, uint64_t *h_off = nullptr,
+                                                   uint64_t *h_len = nullptr, int32_t *h_st = nullptr) {
   const uint32_t d = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (d >= n) return;
   const uint64_t L = len[d];
+  if (h_off) {
+    if (lane == 0) h_off[d] = dst_off[d];
+    else if (lane == 1) h_len[d] = L;
+    else if (lane == 2) h_st[d] = st[d];
+  }
   if (L == 0) return;
   const uint64_t so = src_off[d], dof = dst_off[d];
   if (dof + L > cap) return;
@@ -750,14 +760,14 @@ int run_host_pipe(DevState *S, const ym_batch *b, ym_out *out, hipStream_t st, y
     const int fr = v2 ? fast2_launch(OP_MERGE, jc, nu, st) : fast_launch(OP_MERGE, jc, nu, st);
     if (fr != 1) return -3;
     k_chunk_scan<<<1, 1024, 0, st>>>(jc.status, jc.out_len, jc.n, S->cmp_off.as<uint64_t>() + d0, S->cmp_len.as<uint64_t>() + d0,
-                                      counters + 20, S->pipe_host_dev, c, j.pend_count, c + 1 == nc,
-                                      direct ? h_off + d0 : nullptr, direct ? h_len + d0 : nullptr,
-                                      direct ? h_st + d0 : nullptr);
+                                      counters + 20, S->pipe_host_dev, c, j.pend_count, c + 1 == nc, nullptr, nullptr, nullptr);
     HIPCHK(hipEventRecord(S->pev_k[c], st));
     HIPCHK(hipStreamWaitEvent(S->s_d2h, S->pev_k[c], 0));
     k_pack_docs<<<(jc.n + 3) / 4, 256, 0, S->s_d2h>>>(j.out, jc.out_off, S->cmp_off.as<uint64_t>() + d0,
                                                       S->cmp_len.as<uint64_t>() + d0, jc.n,
-                                                      direct ? h_arena : S->cmp_arena.as<uint8_t>(), direct ? out->cap : ~0ull);
+                                                      direct ? h_arena : S->cmp_arena.as<uint8_t>(), direct ? out->cap : ~0ull,
+                                                      jc.status, direct ? h_off + d0 : nullptr, direct ? h_len + d0 : nullptr,
+                                                      direct ? h_st + d0 : nullptr);
     if (!direct) HIPCHK(hipEventRecord(S->pev_p[c], S->s_d2h));
   }
   if (stats) HIPCHK(hipEventRecord(S->ev1, st));
