@@ -640,11 +640,13 @@ def main():
             got = eng.run_host("merge", fmt, pa, po, pd, out=hout)
             same = (np.array_equal(ref[1], got[1]) and np.array_equal(ref[2], got[2]) and
                     np.array_equal(ref[3], got[3]) and np.array_equal(ref[0][:len(got[0])], got[0]))
-            reps = 10
-            th = time.perf_counter()
+            reps = 16
+            ths = []
             for _ in range(reps):
+                t1 = time.perf_counter()
                 eng.run_host("merge", fmt, pa, po, pd, out=hout)
-            th = (time.perf_counter() - th) / reps
+                ths.append(time.perf_counter() - t1)
+            th = float(np.median(ths))  # (median: a call now and then waits several ms for the host / driver)
             tq = time.perf_counter()
             for _ in range(reps):  # the same from pageable input arrays
                 eng.run_host("merge", fmt, arena, upd_off.astype(np.uint32), doc_upd, out=hout)
@@ -655,6 +657,8 @@ def main():
             tp = (time.perf_counter() - tp) / 3
             line["pcie_inclusive"] = {"value": round(in_bytes / th / 1e9, 3), "unit": "GB/s",
                                       "ms_per_call": round(th * 1e3, 3), "bytes_match_unpipelined": bool(same),
+                                      "ms_per_call_each": [round(x * 1e3, 3) for x in ths],
+                                      "mean_ms_per_call": round(float(np.mean(ths)) * 1e3, 3),
                                       "source": "batch and outputs in page-locked pool memory (ym_host_alloc: the "
                                                 "Node addon packs into it, include/ymerge.h), u32 offsets, "
                                                 "pipelined chunks",
