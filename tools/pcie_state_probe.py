@@ -13,7 +13,11 @@ sys.path.insert(0, ROOT)
 from yjs_amd import Engine  # noqa: E402
 from yjs_amd.workloads import load_ymb, replicate  # noqa: E402
 
-a, o, d = replicate(*load_ymb("c2_v1"), 10000)
+if os.environ.get("BENCH_DATA"):  # the bench's own batch (distinct copies, hash-partitioned over one rank)
+    from yjs_amd.distributed import weak_scaling_shard
+    a, o, d, _ = weak_scaling_shard(*load_ymb("c2_v1"), 10000, 1, 0, "hash")
+else:
+    a, o, d = replicate(*load_ymb("c2_v1"), 10000)
 e = Engine(0)
 o32 = o.astype(np.uint32)
 pa = e.host_array(len(a)); pa[:] = a
