@@ -233,24 +233,27 @@ __global__ void __launch_bounds__(256) k_pack_docs(const uint8_t *src, const uin
                                                    const uint64_t *len, uint32_t n, uint8_t *dst, uint64_t cap,
                                                    const int32_t *st = nullptr, uint64_t *h_off = nullptr,
                                                    uint64_t *h_len = nullptr, int32_t *h_st = nullptr) {
-  const uint32_t d = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (d >= n) return;
-  const uint64_t L = len[d];
-  if (h_off) {
-    if (lane == 0) h_off[d] = dst_off[d];
-    else if (lane == 1) h_len[d] = L;
-    else if (lane == 2) h_st[d] = st[d];
+  const uint32_t lane = threadIdx.x & 63;
+  // (a grid smaller than n / 4 blocks loops: the pipelined path keeps its packing waves few, so the next
+  // chunk's merge kernel, running beside them, keeps its wave slots)
+  for (uint32_t d = blockIdx.x * 4 + (threadIdx.x >> 6); d < n; d += gridDim.x * 4) {
+    const uint64_t L = len[d];
+    if (h_off) {
+      if (lane == 0) h_off[d] = dst_off[d];
+      else if (lane == 1) h_len[d] = L;
+      else if (lane == 2) h_st[d] = st[d];
+    }
+    if (L == 0) continue;
+    const uint64_t so = src_off[d], dof = dst_off[d];
+    if (dof + L > cap) continue;
+    const uint32_t head0 = (uint32_t)((16 - (dof & 15)) & 15);
+    const uint64_t h = head0 < L ? head0 : L;
+    if (lane < h) dst[dof + lane] = src[so + lane];
+    const uint64_t body = (L - h) & ~15ull;
+    for (uint64_t k = (uint64_t)lane * 16; k < body; k += 64 * 16)
+      *reinterpret_cast<uint4 *>(dst + dof + h + k) = pack_load16(src, so + h + k);
+    for (uint64_t i = h + body + lane; i < L; i += 64) dst[dof + i] = src[so + i];
   }
-  if (L == 0) return;
-  const uint64_t so = src_off[d], dof = dst_off[d];
-  if (dof + L > cap) return;
-  const uint32_t head0 = (uint32_t)((16 - (dof & 15)) & 15);
-  const uint64_t h = head0 < L ? head0 : L;
-  if (lane < h) dst[dof + lane] = src[so + lane];
-  const uint64_t body = (L - h) & ~15ull;
-  for (uint64_t k = (uint64_t)lane * 16; k < body; k += 64 * 16)
-    *reinterpret_cast<uint4 *>(dst + dof + h + k) = pack_load16(src, so + h + k);
-  for (uint64_t i = h + body + lane; i < L; i += 64) dst[dof + i] = src[so + i];
 }
 
 // Host -> HBM copy kernel (pipelined host merges with the batch in page-locked pool memory): up to three
@@ -609,6 +612,7 @@ uint8_t *host_dev_ptr(const void *p) {
   return (uint8_t *)a.devicePointer + ((const uint8_t *)p - hp);
 }
 constexpr uint32_t PIPE_MIN_DOCS = 4096, PIPE_MAX = 16;
+constexpr uint32_t PIPE_PACK_GRID = 0;  // k_pack_docs blocks per chunk in the pipelined path (0: one per 4 documents)
 constexpr uint64_t PIPE_CHUNK_BYTES = 6ull << 20;
 int run_op(uint32_t op, const ym_batch *b, ym_out *out, void *stream, ym_stats *stats, int depth = 0);
 int run_host_pipe(DevState *S, const ym_batch *b, ym_out *out, hipStream_t st, ym_stats *stats) {
@@ -763,7 +767,9 @@ int run_host_pipe(DevState *S, const ym_batch *b, ym_out *out, hipStream_t st, y
                                       counters + 20, S->pipe_host_dev, c, j.pend_count, c + 1 == nc, nullptr, nullptr, nullptr);
     HIPCHK(hipEventRecord(S->pev_k[c], st));
     HIPCHK(hipStreamWaitEvent(S->s_d2h, S->pev_k[c], 0));
-    k_pack_docs<<<(jc.n + 3) / 4, 256, 0, S->s_d2h>>>(j.out, jc.out_off, S->cmp_off.as<uint64_t>() + d0,
+    static const uint32_t pack_grid = getenv("YMERGE_PACK_GRID") ? (uint32_t)atoi(getenv("YMERGE_PACK_GRID")) : PIPE_PACK_GRID;
+    const uint32_t pg = (jc.n + 3) / 4 < pack_grid || pack_grid == 0 ? (jc.n + 3) / 4 : pack_grid;
+    k_pack_docs<<<pg, 256, 0, S->s_d2h>>>(j.out, jc.out_off, S->cmp_off.as<uint64_t>() + d0,
                                                       S->cmp_len.as<uint64_t>() + d0, jc.n,
                                                       direct ? h_arena : S->cmp_arena.as<uint8_t>(), direct ? out->cap : ~0ull,
                                                       jc.status, direct ? h_off + d0 : nullptr, direct ? h_len + d0 : nullptr,
