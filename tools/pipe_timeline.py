@@ -6,10 +6,8 @@ import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if "k_h2d_copy" in r["Kernel_Name"]]
-first = idx[-1]
-while first > 0 and "k_h2d_copy" in rows[first - 1]["Kernel_Name"]:
-    first -= 1
+first = idx[-3]  # the last call's first copy kernel (three chunks per C2 call)
 t0 = int(rows[first]["Start_Timestamp"])
-for r in rows[first - 2:first + 14]:
+for r in rows[first - 1:first + 14]:
     s, e = (int(r["Start_Timestamp"]) - t0) / 1e3, (int(r["End_Timestamp"]) - t0) / 1e3
     print(f"{s:8.1f} {e:8.1f} {e - s:7.1f} q{r['Queue_Id']} grid {r['Grid_Size_X']:>7} {r['Kernel_Name'][:70]}")
