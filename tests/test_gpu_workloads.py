@@ -149,6 +149,35 @@ def test_c3_damaged_updates_chunked_walk(engine, fmt):
         assert not bad, (op, bad[:10])
 
 
+@pytest.mark.parametrize("fmt", [1, 2])
+def test_c5_damaged_updates_chunked_walk(engine, fmt):
+    """Truncated and byte-flipped merged C5 updates (~1,000 client sections each: V1 through the chunk walk's
+    pre-roll and the stitch's LDS state-vector map, V2 through the multi-section column path): the oracle's
+    bytes or exception for every document, whether the path takes it or declines it."""
+    from yjs_amd import pack_docs
+    arena, upd_off, doc_upd = load_ymb(f"c5_v{fmt}")
+    merged, status, _ = O.batch("merge", fmt, arena, upd_off, doc_upd, nthreads=8)
+    assert (status == 0).all()
+    rng = np.random.default_rng(23 + fmt)
+    docs, svs = [], []
+    for i in range(16):
+        b = bytearray(merged[i % len(merged)])
+        if i % 4 == 0:
+            b = b[:int(rng.integers(len(b) // 2, len(b)))]
+        elif i % 4 != 3:  # (every 4th document undamaged)
+            for _ in range(1 + i % 3):
+                b[int(rng.integers(8, len(b)))] = int(rng.integers(0, 256))
+        docs.append(bytes(b))
+        svs.append(random_state_vectors(O.sv_from_update(merged[i % len(merged)], fmt)[1], 1, seed=40 + i)[0])
+    a2, o2, d2 = pack_docs([[u] for u in docs])
+    sva, svo, _ = pack_docs([[s] for s in svs])
+    for op in ("diff", "sv", "meta"):
+        extra = (sva, svo) if op == "diff" else ()
+        outs, st, _ = O.batch(op, fmt, a2, o2, d2, *extra, nthreads=8)
+        bad = _compare(engine.run_host(op, fmt, a2, o2, d2, *extra), outs, st)
+        assert not bad, (op, bad[:10])
+
+
 def _subset(arena, upd_off, doc_upd, docs, keep):
     """Documents `docs` of a template file, each restricted to the updates u (local index) with keep(u)."""
     from yjs_amd import pack_docs
