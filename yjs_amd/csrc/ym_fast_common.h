@@ -287,12 +287,21 @@ __device__ __forceinline__ uint32_t rstr_defer(Cur &c) {
   if (!room(c, n)) { c.bad = true; return 0; }
   uint64_t any = 0;
   uint32_t u = 0;
-  for (uint32_t o = 0; o < n; o += 8) {
-    const uint32_t k = n - o < 8 ? n - o : 8;
-    const uint64_t x = mask_bytes(ld8(c.p + o), k);
+  // 16 bytes per step (two independent 8-byte LDS reads in flight; a 600-byte paste is 38 steps of its lane)
+  auto cnt = [&](uint64_t x, uint32_t k) {
     const uint64_t hi = x & 0x8080808080808080ull, x1 = x << 1;
     any |= hi;
     u += k - (uint32_t)__popcll(hi & ~x1) + (uint32_t)__popcll(hi & x1 & (x << 2) & (x << 3));
+  };
+  uint32_t o = 0;
+  for (; o + 16 <= n; o += 16) {
+    const uint64_t x0 = ld8(c.p + o), x1 = ld8(c.p + o + 8);
+    cnt(x0, 8);
+    cnt(x1, 8);
+  }
+  for (; o < n; o += 8) {
+    const uint32_t k = n - o < 8 ? n - o : 8;
+    cnt(mask_bytes(ld8(c.p + o), k), k);
   }
   if (any) {
     const uint32_t q = atomicAdd(&at<uint32_t>(DC), 1u);
