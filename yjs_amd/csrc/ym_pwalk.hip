@@ -322,8 +322,9 @@ __device__ __forceinline__ uint32_t put_vu_g(uint8_t *o, uint32_t p, uint32_t v)
 // surrogate, and V1 writeVarString (encodeURIComponent) throws URIError there -- yjs's diffUpdate throws it
 // as it writes that struct, before reading anything after it (the lazy reader).
 enum : uint32_t { SH_DECLINE = 0, SH_OK = 1, SH_URI = 2 };
-__device__ uint32_t slice_head(sc::cu32 *B, uint32_t adj, uint32_t s0, uint32_t s1, uint32_t client, uint64_t clock,
-                               uint32_t len, uint32_t off, uint8_t *pre, uint32_t &prelen, uint32_t &a0, uint32_t &a1) {
+__device__ __forceinline__ uint32_t slice_head_body(sc::cu32 *B, uint32_t adj, uint32_t s0, uint32_t s1, uint32_t client,
+                                                   uint64_t clock, uint32_t len, uint32_t off, uint8_t *pre, uint32_t &prelen,
+                                                   uint32_t &a0, uint32_t &a1) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t info = sc::byte(B, s0 + adj);
   const bool gc = (info & 31) == 0;
@@ -385,6 +386,13 @@ __device__ uint32_t slice_head(sc::cu32 *B, uint32_t adj, uint32_t s0, uint32_t 
     for (uint32_t b = 0; b < q; b++) pre[b] = h[b];
   prelen = q;
   return SH_OK;
+}
+// out of line (k_pw_small, k_pw_ms, the many-section stitch: inlined, its registers cost them occupancy -- diff_c2_v1
+// 0.70 -> 0.78 ms); the single-section stitch inlines slice_head_body (C3 V1 diff 14.9 -> 14.1 ms: the call saved
+// and restored the stitch's live registers through scratch)
+__device__ __noinline__ uint32_t slice_head(sc::cu32 *B, uint32_t adj, uint32_t s0, uint32_t s1, uint32_t client, uint64_t clock,
+                                           uint32_t len, uint32_t off, uint8_t *pre, uint32_t &prelen, uint32_t &a0, uint32_t &a1) {
+  return slice_head_body(B, adj, s0, s1, client, clock, len, off, pre, prelen, a0, a1);
 }
 
 // a declined document keeps done[d] != 1 (k_big_v1 takes it); the value says why (ym__pw_reasons)
@@ -751,7 +759,8 @@ __global__ void __launch_bounds__(64) k_pw_stitch(GeneralJob j, const uint32_t *
                 b0 = fpos;
                 first = f;
               } else {
-                const uint32_t sh = slice_head(B, adj, fpos, fend, client, fclk, flen, off, X.pre + ci * PRE, prelen, a0, a1);
+                const uint32_t sh = DSL ? slice_head(B, adj, fpos, fend, client, fclk, flen, off, X.pre + ci * PRE, prelen, a0, a1)
+                                        : slice_head_body(B, adj, fpos, fend, client, fclk, flen, off, X.pre + ci * PRE, prelen, a0, a1);
                 if (sh != SH_OK) {
                   declined = true;
                   why = sh == SH_URI ? WHY_URI : 11;
